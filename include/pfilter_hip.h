@@ -1,0 +1,133 @@
+/* pfilter_hip — C ABI of the MI355X-native PFilter/FLOAM odometry hot path.
+ *
+ * One handle = one HIP stream = one caller thread (the reference classes are used by exactly one
+ * worker thread each: src/odomEstimationNode copy.cpp:54-148, src/laserProcessingNode.cpp:53-106).
+ * Handles on different devices are independent; that is the per-sequence multi-GPU model.
+ * Every entry point returns a status code and never throws across the ABI.
+ *
+ * Reference interfaces replaced (the C++ drop-in shims in pfilter-noetic_amd/shim/ map 1:1):
+ *   pf_fe_create/pf_fe_extract     LaserProcessingClass::init / featureExtraction
+ *                                  (include/laserProcessingClass.h:36-37, src/laserProcessingClass.cpp:10-96)
+ *   pf_odom_create                 Odom_ES_EstimationClass::init (include/odomEstimationClass.h:146,
+ *                                  src/odomEstimationClass.cpp:182-208)
+ *   pf_odom_init_map               Odom_ES_EstimationClass::initMapWithPoints (.h:148, .cpp:217-222)
+ *   pf_odom_update                 Odom_ES_EstimationClass::updatePointsToMap (.h:149, .cpp:229-282)
+ *   pf_odom_get_pose               public member `odom` as read by the node (copy.cpp:105-107)
+ *   pf_odom_get_map                public members laserCloudCornerMap / laserCloudSurfMap (.h:151-152)
+ *                                  and getMap (.h:147, .cpp:210-215)
+ */
+#ifndef PFILTER_HIP_H
+#define PFILTER_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes: 0 ok, > 0 warnings (execution continued, as the reference prints and continues),
+ * < 0 errors */
+#define PF_OK 0
+#define PF_W_MAP_TOO_SMALL 1     /* "not enough points in map to associate" (.cpp:274-277) */
+#define PF_W_FEW_CORRESPONDENCES 2 /* "not enough correct points" (.cpp:428-431, 574-577) */
+#define PF_EINVAL (-1)           /* bad argument, e.g. weight_type not in {0,1,2,12} (reference: UB) */
+#define PF_EHIP (-2)             /* HIP runtime error */
+#define PF_ENOMEM (-3)           /* device allocation failed */
+#define PF_ECAPACITY (-4)        /* input or map larger than the handle's capacity */
+#define PF_EUNSUPPORTED (-5)     /* configuration outside the implemented path */
+
+typedef struct {                 /* lidar::Lidar fields read on the path (include/lidar.h:9-30) */
+    int num_lines;               /* 16, 32 or 64 (others: every point in ring 0, as the reference) */
+    double min_dist;
+    double max_dist;
+    double scan_period;
+} pf_lidar_params;
+
+typedef struct {                 /* Odom_ES_EstimationClass::init arguments */
+    double map_res;              /* map_resolution (edge leaf; surf leaf = 2x) */
+    int k_new;
+    float theta_p;
+    int theta_max;
+    int weight_type;             /* 0 none, 1 observe, 2 sparsity, 12 both */
+} pf_odom_params;
+
+typedef struct {
+    int64_t n_edge_in, n_surf_in;        /* E, S */
+    int64_t n_edge_ds, n_surf_ds;        /* E', S' after VoxelGrid */
+    int64_t n_edge_map, n_surf_map;      /* map sizes after the update */
+    int64_t n_edge_res, n_surf_res;      /* residual blocks in the last outer iteration */
+    int64_t n_edge_valid, n_surf_valid;  /* gated + fitted associations, last outer iteration */
+    int32_t outer_iterations;
+    int32_t lm_iterations;               /* summed over outer iterations */
+    int32_t map_too_small;
+    int32_t status;
+} pf_odom_stats;
+
+/* ---------------- feature extraction (LaserProcessingClass) ---------------- */
+typedef struct pf_fe pf_fe;
+int pf_fe_create(const pf_lidar_params* lidar, int device, size_t max_points, pf_fe** out);
+int pf_fe_destroy(pf_fe* h);
+/* xyzi: n points, x,y,z at byte offsets 0,4,8 and intensity at 16 (PCL PointXYZI) or 12 (packed)
+ * selected by stride_bytes (32 = PCL layout, 16 = packed float4). Outputs are packed float4
+ * (x, y, z, intensity), bit-identical copies of input points in reference order
+ * (ring -> sector -> edges by descending curvature / surfs ascending). `cap` is the capacity of
+ * each output in points. */
+int pf_fe_extract(pf_fe* h, const float* xyzi, size_t n, size_t stride_bytes, float* edge_out,
+                  size_t* n_edge, float* surf_out, size_t* n_surf, size_t cap);
+
+/* ---------------- odometry (Odom_ES_EstimationClass) ---------------- */
+typedef struct pf_odom pf_odom;
+/* max_points: largest raw scan / edge / surf input; map_capacity: largest local map (per map). */
+int pf_odom_create(const pf_lidar_params* lidar, const pf_odom_params* params, int device,
+                   size_t max_points, size_t map_capacity, pf_odom** out);
+int pf_odom_destroy(pf_odom* h);
+/* edge/surf: points with x,y,z at offsets 0,4,8 and the given stride (16 packed, 32 PCL). */
+int pf_odom_init_map(pf_odom* h, const float* edge, size_t ne, size_t edge_stride, const float* surf,
+                     size_t ns, size_t surf_stride);
+int pf_odom_update(pf_odom* h, const float* edge, size_t ne, size_t edge_stride, const float* surf,
+                   size_t ns, size_t surf_stride, double pose_out[7]);
+/* pose = {qx, qy, qz, qw, tx, ty, tz} of `odom` (q = Quaterniond(odom.rotation())) */
+int pf_odom_get_pose(pf_odom* h, double pose[7]);
+/* which: 0 = edge (corner) map, 1 = surf map. xyz 3 floats/pt, rg 2 bytes/pt (r=age, g=p-index).
+ * Either output may be NULL; with cap too small *n is set and PF_ECAPACITY returned. */
+int pf_odom_get_map(pf_odom* h, int which, float* xyz, uint8_t* rg, size_t cap, size_t* n);
+int pf_odom_set_map(pf_odom* h, int which, const float* xyz, const uint8_t* rg, size_t n);
+int pf_odom_get_stats(pf_odom* h, pf_odom_stats* s);
+
+/* ---------------- whole-frame device pipeline (featureExtraction -> odometry) ----------------
+ * d_xyzi: device pointer to n packed float4 points (HBM-resident scan). The first frame seeds the
+ * map (initMapWithPoints), later frames run updatePointsToMap. The pose of every frame is kept on
+ * the device (pf_odom_poses). pose_out may be NULL, in which case the call only enqueues work on
+ * the handle's stream and returns without waiting. */
+int pf_odom_frame_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]);
+int pf_odom_frame_host(pf_odom* h, const float* xyzi, size_t n, size_t stride_bytes, double pose_out[7]);
+int pf_odom_sync(pf_odom* h);
+/* poses of frames processed so far, 7 doubles each */
+int pf_odom_poses(pf_odom* h, double* poses, size_t cap, size_t* n);
+/* enable/disable hipGraph replay of the steady-state frame (default on) */
+int pf_odom_set_graph(pf_odom* h, int enable);
+
+/* ---------------- device memory helpers (scan staging without a framework) ---------------- */
+int pf_device_count(int* n);
+int pf_dev_malloc(int device, size_t bytes, void** d);
+int pf_dev_free(int device, void* d);
+int pf_memcpy_h2d(int device, void* dst, const void* src, size_t bytes);
+int pf_memcpy_d2h(int device, void* dst, const void* src, size_t bytes);
+
+/* ---------------- exact radius-gated 5-NN (the roofline kernel) ----------------
+ * Exact 5 nearest map points with squared distance < 1 (f32, accumulated x->y->z), ties by map
+ * index: the search of KdTreeFLANN::nearestKSearch(k=5) restricted to what the reference consumes
+ * (src/odomEstimationClass.cpp:299-300, 447-451). Unfound slots get idx = -1, d2 = +inf. */
+typedef struct pf_knn pf_knn;
+int pf_knn_create(int device, size_t map_capacity, size_t query_capacity, pf_knn** out);
+int pf_knn_destroy(pf_knn* h);
+int pf_knn_set_map(pf_knn* h, const float* xyz4, size_t m);            /* host, 4 floats/pt */
+int pf_knn_query(pf_knn* h, const float* q4, size_t nq, int32_t* idx, float* d2);
+/* time `iters` launches of the query kernel on the resident map/queries with HIP events.
+ * Returns the average kernel ms and the algorithmic bytes per launch. */
+int pf_knn_bench(pf_knn* h, int iters, double* avg_ms, double* alg_bytes_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

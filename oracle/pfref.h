@@ -1,0 +1,125 @@
+/* pfref — CPU restatement of the PFilter/FLOAM ES odometry hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. This library is the parity oracle and the reported
+ * single-core CPU baseline. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it; the product (pfilter-noetic_amd/) never links it.
+ *
+ * It restates, in plain C++17 with no third-party dependencies:
+ *   - LaserProcessingClass::featureExtraction(+FromSector)   src/laserProcessingClass.cpp:10-209
+ *   - Odom_ES_EstimationClass init/initMapWithPoints/updatePointsToMap/addEdgeCostFactor/
+ *     addSurfCostFactor/addPointsToMap                       src/odomEstimationClass.cpp:182-647
+ *   - OdomBaseClass rgbds/extractstablepoint/observeMean/pointAssociateToMap
+ *                                                            src/odomEstimationClass.cpp:7-174
+ *   - pointSparsityMean                                      include/odomEstimationClass.h:111-126
+ *   - Edge/SurfNormAnalyticCostFunction, PoseSE3Parameterization, getTransformFromSe3
+ *                                                            src/lidarOptimization.cpp:12-155
+ * and the third-party semantics those call: PCL 1.10 VoxelGrid,
+ * CropBox, ExtractIndices, KdTreeFLANN (FLANN 1.9.1 single kd-tree, leaf 15), Eigen 3.3
+ * quaternion/isometry formulas, a 3x3 symmetric eigensolver, column-pivoting Householder
+ * least squares, and the Ceres 1.14 Levenberg-Marquardt trust-region loop with
+ * HuberLoss(0.1), Jacobi scaling and DENSE_QR.
+ *
+ * PARITY STATUS: the reference ships no tests, golden vectors or fixtures and
+ * its dependencies (ROS, PCL, FLANN, Eigen, Ceres) are absent here, so it cannot be run.
+ * Arithmetic owned by the reference's own files is restated operation-for-operation
+ * (float vs double exactly as the C++ source evaluates it). Arithmetic inside PCL/Eigen/
+ * FLANN/Ceres is "parity unpinned": restated from their published algorithms, with the
+ * ambiguous choices exposed as option bits below so their pose sensitivity can be bounded.
+ */
+#ifndef PFREF_H
+#define PFREF_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {            /* lidar::Lidar fields read on the path (include/lidar.h:9-30) */
+    int num_lines;
+    double min_distance;
+    double max_distance;
+    double scan_period;
+} pfref_lidar;
+
+typedef struct {            /* Odom_ES_EstimationClass::init arguments (include/odomEstimationClass.h:146) */
+    double map_resolution;
+    int k_new;
+    float theta_p;
+    int theta_max;
+    double weight_type;     /* 0, 1, 2 or 12 */
+} pfref_odom_params;
+
+/* Option bits (0 = reference-faithful choice). */
+enum {
+    PFREF_FE_STABLE_TIES = 1,   /* sector sort by (curvature, id) instead of libstdc++ std::sort  */
+    PFREF_FE_SQRT_DOUBLE = 2,   /* ring-binning range as sqrt((double)(x*x+y*y)) not sqrtf       */
+    PFREF_VG_STABLE      = 4,   /* VoxelGrid/rgbds ties kept in input order (stable sort)        */
+    PFREF_KNN_BRUTE      = 8,   /* brute-force kNN instead of the FLANN-style kd-tree            */
+    PFREF_LM_NORMAL_EQ   = 16,  /* LM step by 6x6 normal equations instead of dense Householder QR */
+    PFREF_GPU_EQUIV      = 1 | 4 | 16
+};
+
+typedef struct {
+    int64_t n_edge_in, n_surf_in;        /* E, S */
+    int64_t n_edge_ds, n_surf_ds;        /* E', S' */
+    int64_t n_edge_map, n_surf_map;      /* map sizes after the update */
+    int64_t n_edge_res, n_surf_res;      /* residuals in the last outer iteration */
+    int64_t n_edge_valid, n_surf_valid;  /* associations passing the gate + fit test (last outer it.) */
+    int32_t outer_iterations;            /* optimization_count used */
+    int32_t lm_iterations;               /* summed over outer iterations */
+    int32_t map_too_small;               /* 1 when the solve was skipped (odomEstimationClass.cpp:274-277) */
+    int32_t status;
+    double t_downsample, t_tree, t_assoc, t_solve, t_mapupdate;  /* seconds */
+} pfref_stats;
+
+/* --- feature extraction: LaserProcessingClass::featureExtraction --------------------- */
+/* xyzi: 4 floats per point (x, y, z, intensity). Outputs are XYZI copies of input points
+ * in reference order (ring -> sector -> edge by descending curvature / surf ascending).
+ * Returns 0, or -1 when cap is exceeded. */
+int pfref_feature_extraction(const pfref_lidar* lidar, int opts, const float* xyzi, size_t n,
+                             float* edge_out, size_t* n_edge, float* surf_out, size_t* n_surf,
+                             size_t cap);
+
+/* --- third-party semantics, exposed for unit tests ---------------------------------- */
+/* PCL VoxelGrid<PointXYZRGB> (B.1): pts = 4 floats (x,y,z, rgb packed as uint32 bits r<<16|g<<8|b). */
+int pfref_voxel_grid(const float* pts, size_t n, float leaf, int opts, float* out, size_t* n_out);
+/* OdomBaseClass::rgbds (a15): same point layout. */
+int pfref_rgbds(const float* pts, size_t n, float leaf, int opts, float* out, size_t* n_out);
+/* exact kNN (d^2 in float accumulated x->y->z), ties by index. map/queries 4 floats/pt. */
+int pfref_knn(const float* map, size_t m, const float* queries, size_t q, int k, int opts,
+              int32_t* idx_out, float* d2_out);
+/* 3x3 symmetric eigen (ascending). a = {a00,a01,a02,a11,a12,a22}. */
+void pfref_eigen_sym3(const double a[6], double evals[3], double evecs[9] /* column-major */);
+/* 5x3 column-pivoting Householder least squares of A n = -1 (A row-major 5x3). */
+void pfref_plane_fit(const double A[15], double n_out[3]);
+/* PoseSE3Parameterization::Plus */
+void pfref_se3_plus(const double x[7], const double delta[6], double out[7]);
+/* Edge/SurfNormAnalyticCostFunction::Evaluate: returns residual, J[7] */
+double pfref_edge_eval(const double x[7], const double cur[3], const double a[3], const double b[3],
+                       double weight, double J[7]);
+double pfref_surf_eval(const double x[7], const double cur[3], const double n[3], double d,
+                       double weight, double J[7]);
+
+/* --- odometry: Odom_ES_EstimationClass ------------------------------------------------ */
+typedef struct pfref_odom pfref_odom;
+pfref_odom* pfref_odom_create(const pfref_lidar* lidar, const pfref_odom_params* params, int opts);
+void pfref_odom_destroy(pfref_odom* h);
+/* edge/surf: 4 floats per point (x, y, z, intensity); r = g = 0 as after copyPointCloud */
+int pfref_odom_init_map(pfref_odom* h, const float* edge, size_t ne, const float* surf, size_t ns);
+int pfref_odom_update(pfref_odom* h, const float* edge, size_t ne, const float* surf, size_t ns,
+                      double pose_out[7]);
+/* pose = {qx,qy,qz,qw,tx,ty,tz} of odom (rotation via Quaterniond(odom.rotation())) */
+void pfref_odom_get_pose(const pfref_odom* h, double pose[7]);
+/* which: 0 edge (corner) map, 1 surf map. xyz: 3 floats/pt, rg: 2 bytes/pt (r, g). */
+int pfref_odom_get_map(const pfref_odom* h, int which, float* xyz, uint8_t* rg, size_t cap, size_t* n);
+int pfref_odom_set_map(pfref_odom* h, int which, const float* xyz, const uint8_t* rg, size_t n);
+void pfref_odom_get_stats(const pfref_odom* h, pfref_stats* s);
+
+/* --- whole frame: featureExtraction then initMapWithPoints (first call) / updatePointsToMap */
+int pfref_odom_frame(pfref_odom* h, const pfref_lidar* lidar, const float* xyzi, size_t n,
+                     double pose_out[7]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,251 @@
+"""ctypes binding of the pfref CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+See oracle/pfref.h for what is restated from the reference and where parity is unpinned.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "build", "libpfref.so")
+
+FE_STABLE_TIES = 1
+FE_SQRT_DOUBLE = 2
+VG_STABLE = 4
+KNN_BRUTE = 8
+LM_NORMAL_EQ = 16
+GPU_EQUIV = FE_STABLE_TIES | VG_STABLE | LM_NORMAL_EQ
+
+
+def build(force=False):
+    srcs = [os.path.join(_HERE, f) for f in ("pfref_fe.cpp", "pfref_odom.cpp", "pfref.h", "pfref_internal.h",
+                                              "pfref_math.h")]
+    newest = max(os.path.getmtime(s) for s in srcs)
+    if force or not os.path.exists(_LIB) or os.path.getmtime(_LIB) < newest:
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB
+
+
+class Lidar(ctypes.Structure):
+    _fields_ = [("num_lines", ctypes.c_int), ("min_distance", ctypes.c_double),
+                ("max_distance", ctypes.c_double), ("scan_period", ctypes.c_double)]
+
+
+class OdomParams(ctypes.Structure):
+    _fields_ = [("map_resolution", ctypes.c_double), ("k_new", ctypes.c_int), ("theta_p", ctypes.c_float),
+                ("theta_max", ctypes.c_int), ("weight_type", ctypes.c_double)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in ("n_edge_in", "n_surf_in", "n_edge_ds", "n_surf_ds", "n_edge_map",
+                                              "n_surf_map", "n_edge_res", "n_surf_res", "n_edge_valid",
+                                              "n_surf_valid")] + \
+               [(n, ctypes.c_int32) for n in ("outer_iterations", "lm_iterations", "map_too_small", "status")] + \
+               [(n, ctypes.c_double) for n in ("t_downsample", "t_tree", "t_assoc", "t_solve", "t_mapupdate")]
+
+    def as_dict(self):
+        return {f[0]: getattr(self, f[0]) for f in self._fields_}
+
+
+_lib = None
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL(build())
+        L = _lib
+        L.pfref_feature_extraction.argtypes = [ctypes.POINTER(Lidar), ctypes.c_int, _vp, _sz, _vp,
+                                               ctypes.POINTER(_sz), _vp, ctypes.POINTER(_sz), _sz]
+        L.pfref_voxel_grid.argtypes = [_vp, _sz, ctypes.c_float, ctypes.c_int, _vp, ctypes.POINTER(_sz)]
+        L.pfref_rgbds.argtypes = [_vp, _sz, ctypes.c_float, ctypes.c_int, _vp, ctypes.POINTER(_sz)]
+        L.pfref_knn.argtypes = [_vp, _sz, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp, _vp]
+        L.pfref_eigen_sym3.argtypes = [_vp, _vp, _vp]
+        L.pfref_plane_fit.argtypes = [_vp, _vp]
+        L.pfref_se3_plus.argtypes = [_vp, _vp, _vp]
+        L.pfref_edge_eval.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_double, _vp]
+        L.pfref_edge_eval.restype = ctypes.c_double
+        L.pfref_surf_eval.argtypes = [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _vp]
+        L.pfref_surf_eval.restype = ctypes.c_double
+        L.pfref_odom_create.argtypes = [ctypes.POINTER(Lidar), ctypes.POINTER(OdomParams), ctypes.c_int]
+        L.pfref_odom_create.restype = _vp
+        L.pfref_odom_destroy.argtypes = [_vp]
+        L.pfref_odom_init_map.argtypes = [_vp, _vp, _sz, _vp, _sz]
+        L.pfref_odom_update.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp]
+        L.pfref_odom_get_pose.argtypes = [_vp, _vp]
+        L.pfref_odom_get_map.argtypes = [_vp, ctypes.c_int, _vp, _vp, _sz, ctypes.POINTER(_sz)]
+        L.pfref_odom_set_map.argtypes = [_vp, ctypes.c_int, _vp, _vp, _sz]
+        L.pfref_odom_get_stats.argtypes = [_vp, ctypes.POINTER(Stats)]
+        L.pfref_odom_frame.argtypes = [_vp, ctypes.POINTER(Lidar), _vp, _sz, _vp]
+    return _lib
+
+
+def _f32(a, cols=4):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    assert a.ndim == 2 and a.shape[1] == cols
+    return a
+
+
+def make_lidar(num_lines=64, min_distance=3.0, max_distance=90.0, scan_period=0.1):
+    return Lidar(int(num_lines), float(min_distance), float(max_distance), float(scan_period))
+
+
+def feature_extraction(xyzi, lidar, opts=0):
+    x = _f32(xyzi)
+    n = x.shape[0]
+    edge = np.empty((max(n, 1), 4), np.float32)
+    surf = np.empty((max(n, 1), 4), np.float32)
+    ne, ns = _sz(), _sz()
+    rc = lib().pfref_feature_extraction(ctypes.byref(lidar), int(opts), x.ctypes.data, n, edge.ctypes.data,
+                                        ctypes.byref(ne), surf.ctypes.data, ctypes.byref(ns), max(n, 1))
+    if rc != 0:
+        raise RuntimeError("pfref_feature_extraction failed")
+    return edge[:ne.value].copy(), surf[:ns.value].copy()
+
+
+def pack_rgb(xyz, r=None, g=None, b=None):
+    n = xyz.shape[0]
+    out = np.zeros((n, 4), np.float32)
+    out[:, :3] = xyz[:, :3]
+    r = np.zeros(n, np.uint32) if r is None else np.asarray(r, np.uint32)
+    g = np.zeros(n, np.uint32) if g is None else np.asarray(g, np.uint32)
+    b = np.zeros(n, np.uint32) if b is None else np.asarray(b, np.uint32)
+    out[:, 3] = ((r << 16) | (g << 8) | b).view(np.float32)
+    return out
+
+
+def unpack_rgb(pts):
+    rgb = np.ascontiguousarray(pts[:, 3]).view(np.uint32)
+    return pts[:, :3].copy(), ((rgb >> 16) & 255).astype(np.uint8), ((rgb >> 8) & 255).astype(np.uint8)
+
+
+def voxel_grid(pts, leaf, opts=0):
+    p = _f32(pts)
+    out = np.empty_like(p) if p.shape[0] else np.empty((1, 4), np.float32)
+    n = _sz()
+    lib().pfref_voxel_grid(p.ctypes.data, p.shape[0], float(leaf), int(opts), out.ctypes.data, ctypes.byref(n))
+    return out[:n.value].copy()
+
+
+def rgbds(pts, leaf, opts=0):
+    p = _f32(pts)
+    out = np.empty_like(p) if p.shape[0] else np.empty((1, 4), np.float32)
+    n = _sz()
+    lib().pfref_rgbds(p.ctypes.data, p.shape[0], float(leaf), int(opts), out.ctypes.data, ctypes.byref(n))
+    return out[:n.value].copy()
+
+
+def knn(map_pts, queries, k=5, opts=0):
+    m = _f32(map_pts)
+    q = _f32(queries)
+    idx = np.empty((q.shape[0], k), np.int32)
+    d2 = np.empty((q.shape[0], k), np.float32)
+    rc = lib().pfref_knn(m.ctypes.data, m.shape[0], q.ctypes.data, q.shape[0], int(k), int(opts),
+                         idx.ctypes.data, d2.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("pfref_knn failed")
+    return idx, d2
+
+
+def eigen_sym3(a6):
+    a = np.ascontiguousarray(a6, np.float64)
+    ev = np.empty(3)
+    vec = np.empty(9)
+    lib().pfref_eigen_sym3(a.ctypes.data, ev.ctypes.data, vec.ctypes.data)
+    return ev, vec.reshape(3, 3).T  # columns are eigenvectors
+
+
+def plane_fit(A):
+    A = np.ascontiguousarray(A, np.float64).reshape(5, 3)
+    n = np.empty(3)
+    lib().pfref_plane_fit(A.ctypes.data, n.ctypes.data)
+    return n
+
+
+def se3_plus(x, delta):
+    x = np.ascontiguousarray(x, np.float64)
+    d = np.ascontiguousarray(delta, np.float64)
+    out = np.empty(7)
+    lib().pfref_se3_plus(x.ctypes.data, d.ctypes.data, out.ctypes.data)
+    return out
+
+
+def edge_eval(x, cur, a, b, w=0.0):
+    J = np.empty(7)
+    arr = [np.ascontiguousarray(v, np.float64) for v in (x, cur, a, b)]
+    r = lib().pfref_edge_eval(*(v.ctypes.data for v in arr), float(w), J.ctypes.data)
+    return r, J
+
+
+def surf_eval(x, cur, n, d, w=0.0):
+    J = np.empty(7)
+    arr = [np.ascontiguousarray(v, np.float64) for v in (x, cur, n)]
+    r = lib().pfref_surf_eval(*(v.ctypes.data for v in arr), float(d), float(w), J.ctypes.data)
+    return r, J
+
+
+class Odom:
+    """Odom_ES_EstimationClass restated on the CPU."""
+
+    def __init__(self, lidar=None, map_resolution=0.4, k_new=0, theta_p=0.4, theta_max=75, weight_type=0,
+                 opts=0):
+        self.lidar = lidar if lidar is not None else make_lidar()
+        self.params = OdomParams(float(map_resolution), int(k_new), float(theta_p), int(theta_max),
+                                 float(weight_type))
+        self._h = lib().pfref_odom_create(ctypes.byref(self.lidar), ctypes.byref(self.params), int(opts))
+        if not self._h:
+            raise ValueError("invalid odometry parameters")
+        self.inited = False
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().pfref_odom_destroy(self._h)
+            self._h = None
+
+    def init_map(self, edge, surf):
+        e, s = _f32(edge), _f32(surf)
+        lib().pfref_odom_init_map(self._h, e.ctypes.data, e.shape[0], s.ctypes.data, s.shape[0])
+        self.inited = True
+
+    def update(self, edge, surf):
+        e, s = _f32(edge), _f32(surf)
+        pose = np.empty(7)
+        lib().pfref_odom_update(self._h, e.ctypes.data, e.shape[0], s.ctypes.data, s.shape[0], pose.ctypes.data)
+        return pose
+
+    def frame(self, xyzi):
+        x = _f32(xyzi)
+        pose = np.empty(7)
+        rc = lib().pfref_odom_frame(self._h, ctypes.byref(self.lidar), x.ctypes.data, x.shape[0], pose.ctypes.data)
+        if rc != 0:
+            raise RuntimeError("pfref_odom_frame failed")
+        self.inited = True
+        return pose
+
+    def pose(self):
+        p = np.empty(7)
+        lib().pfref_odom_get_pose(self._h, p.ctypes.data)
+        return p
+
+    def get_map(self, which):
+        n = _sz()
+        lib().pfref_odom_get_map(self._h, int(which), None, None, 0, ctypes.byref(n))
+        xyz = np.empty((max(n.value, 1), 3), np.float32)
+        rg = np.empty((max(n.value, 1), 2), np.uint8)
+        lib().pfref_odom_get_map(self._h, int(which), xyz.ctypes.data, rg.ctypes.data, n.value, ctypes.byref(n))
+        return xyz[:n.value].copy(), rg[:n.value].copy()
+
+    def set_map(self, which, xyz, rg):
+        xyz = np.ascontiguousarray(xyz, np.float32)
+        rg = np.ascontiguousarray(rg, np.uint8)
+        lib().pfref_odom_set_map(self._h, int(which), xyz.ctypes.data, rg.ctypes.data, xyz.shape[0])
+
+    def stats(self):
+        s = Stats()
+        lib().pfref_odom_get_stats(self._h, ctypes.byref(s))
+        return s.as_dict()

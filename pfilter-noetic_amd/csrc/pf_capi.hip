@@ -1,0 +1,399 @@
+// C ABI (include/pfilter_hip.h) over the device pipeline. Host code here only stages inputs,
+// enqueues work on the handle's stream and copies results back; all arithmetic is on the device.
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "pf_fe.h"
+#include "pf_odom.h"
+
+using namespace pf;
+
+namespace {
+
+__global__ void k_set_int(int* p, int v) {
+    if (threadIdx.x == 0) *p = v;
+}
+
+// repack points with x,y,z at offsets 0,4,8 (+ intensity at 16 for a 32-byte PCL stride, at 12 for
+// 16-byte packing) into packed float4
+void repack(const float* src, size_t n, size_t stride, std::vector<float4>& out) {
+    out.resize(n);
+    const char* b = reinterpret_cast<const char*>(src);
+    for (size_t i = 0; i < n; ++i) {
+        const float* p = reinterpret_cast<const float*>(b + i * stride);
+        float inten = 0.f;
+        if (stride >= 20) inten = p[4];
+        else if (stride >= 16) inten = p[3];
+        out[i] = make_float4(p[0], p[1], p[2], inten);
+    }
+}
+
+bool valid_stride(size_t s) { return s == 16 || s == 32 || s >= 12; }
+
+}  // namespace
+
+struct pf_fe {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    FeGPU fe;
+    float4* d_edge = nullptr;
+    float4* d_surf = nullptr;
+    int* d_cnt = nullptr;   // [0] n, [1] ne, [2] ns
+    int* h_cnt = nullptr;   // pinned
+    std::vector<float4> host;
+};
+
+struct pf_odom {
+    OdomGPU o;
+    std::vector<float4> host_e, host_s;
+};
+
+extern "C" {
+
+// ------------------------------------------------------------------------------------------------
+int pf_fe_create(const pf_lidar_params* lidar, int device, size_t max_points, pf_fe** out) {
+    if (!lidar || !out || max_points == 0) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(device));
+    pf_fe* h = new (std::nothrow) pf_fe();
+    if (!h) return PF_ENOMEM;
+    h->device = device;
+    int rc = fe_alloc(h->fe, *lidar, max_points);
+    const size_t ecap = (size_t)h->fe.rings * 6 * kEdgePerSector;
+    if (rc == PF_OK && hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) rc = PF_EHIP;
+    if (rc == PF_OK && hipMalloc(&h->d_edge, sizeof(float4) * ecap) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMalloc(&h->d_surf, sizeof(float4) * max_points) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMalloc(&h->d_cnt, sizeof(int) * 4) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipHostMalloc(&h->h_cnt, sizeof(int) * 4) != hipSuccess) rc = PF_ENOMEM;
+    if (rc != PF_OK) {
+        pf_fe_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return PF_OK;
+}
+
+int pf_fe_destroy(pf_fe* h) {
+    if (!h) return PF_OK;
+    (void)hipSetDevice(h->device);
+    fe_free(h->fe);
+    (void)hipFree(h->d_edge);
+    (void)hipFree(h->d_surf);
+    (void)hipFree(h->d_cnt);
+    if (h->h_cnt) (void)hipHostFree(h->h_cnt);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return PF_OK;
+}
+
+int pf_fe_extract(pf_fe* h, const float* xyzi, size_t n, size_t stride_bytes, float* edge_out, size_t* n_edge,
+                  float* surf_out, size_t* n_surf, size_t cap) {
+    if (!h || (!xyzi && n) || !n_edge || !n_surf || !valid_stride(stride_bytes)) return PF_EINVAL;
+    if (n > h->fe.cap) return PF_ECAPACITY;
+    PF_HIP_TRY(hipSetDevice(h->device));
+    repack(xyzi, n, stride_bytes, h->host);
+    if (n) PF_HIP_TRY(hipMemcpyAsync(h->fe.d_in_stage, h->host.data(), sizeof(float4) * n, hipMemcpyHostToDevice,
+                                     h->stream));
+    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, h->stream, h->d_cnt, (int)n);
+    fe_enqueue(h->fe, h->fe.d_in_stage, h->d_cnt, h->d_edge, h->d_cnt + 1, h->d_surf, h->d_cnt + 2, h->stream);
+    PF_HIP_TRY(hipMemcpyAsync(h->h_cnt, h->d_cnt, sizeof(int) * 3, hipMemcpyDeviceToHost, h->stream));
+    int ferr = 0;
+    PF_HIP_TRY(hipMemcpyAsync(&ferr, h->fe.err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    PF_HIP_TRY(hipStreamSynchronize(h->stream));
+    PF_HIP_TRY(hipGetLastError());
+    if (ferr) {
+        (void)hipMemsetAsync(h->fe.err, 0, sizeof(int), h->stream);
+        return PF_EUNSUPPORTED;
+    }
+    const size_t ne = (size_t)h->h_cnt[1], ns = (size_t)h->h_cnt[2];
+    *n_edge = ne;
+    *n_surf = ns;
+    if (ne > cap || ns > cap) return PF_ECAPACITY;
+    if (ne && edge_out)
+        PF_HIP_TRY(hipMemcpyAsync(edge_out, h->d_edge, sizeof(float4) * ne, hipMemcpyDeviceToHost, h->stream));
+    if (ns && surf_out)
+        PF_HIP_TRY(hipMemcpyAsync(surf_out, h->d_surf, sizeof(float4) * ns, hipMemcpyDeviceToHost, h->stream));
+    PF_HIP_TRY(hipStreamSynchronize(h->stream));
+    return PF_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+int pf_odom_create(const pf_lidar_params* lidar, const pf_odom_params* params, int device, size_t max_points,
+                   size_t map_capacity, pf_odom** out) {
+    if (!lidar || !params || !out) return PF_EINVAL;
+    const int wt = params->weight_type;
+    if (!(wt == 0 || wt == 1 || wt == 2 || wt == 12)) return PF_EINVAL;   // reference: ROS_ERROR + UB
+    if (!(params->map_res > 0)) return PF_EINVAL;
+    if (max_points == 0) max_points = 300000;
+    if (map_capacity == 0) map_capacity = (size_t)1 << 22;
+    PF_HIP_TRY(hipSetDevice(device));
+    pf_odom* h = new (std::nothrow) pf_odom();
+    if (!h) return PF_ENOMEM;
+    int rc = odom_create(h->o, *lidar, *params, device, max_points, map_capacity);
+    if (rc != PF_OK) {
+        pf_odom_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return PF_OK;
+}
+
+int pf_odom_destroy(pf_odom* h) {
+    if (!h) return PF_OK;
+    (void)hipSetDevice(h->o.device);
+    (void)hipStreamSynchronize(h->o.stream);
+    odom_destroy(h->o);
+    delete h;
+    return PF_OK;
+}
+
+static int stage_inputs(pf_odom* h, const float* edge, size_t ne, size_t es, const float* surf, size_t ns,
+                        size_t ss) {
+    OdomGPU& o = h->o;
+    if ((!edge && ne) || (!surf && ns) || !valid_stride(es) || !valid_stride(ss)) return PF_EINVAL;
+    if (ne > o.in_cap || ns > o.in_cap) return PF_ECAPACITY;
+    repack(edge, ne, es, h->host_e);
+    repack(surf, ns, ss, h->host_s);
+    if (ne) PF_HIP_TRY(hipMemcpyAsync(o.in_edge, h->host_e.data(), sizeof(float4) * ne, hipMemcpyHostToDevice, o.stream));
+    if (ns) PF_HIP_TRY(hipMemcpyAsync(o.in_surf, h->host_s.data(), sizeof(float4) * ns, hipMemcpyHostToDevice, o.stream));
+    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_EIN, (int)ne);
+    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_SIN, (int)ns);
+    return PF_OK;
+}
+
+static int read_pose(pf_odom* h, double pose[7]) {
+    OdomGPU& o = h->o;
+    if (o.frames == 0) {
+        const double id[7] = {0, 0, 0, 1, 0, 0, 0};
+        std::memcpy(pose, id, sizeof(id));
+        return PF_OK;
+    }
+    const size_t slot = (size_t)(o.frames - 1) % o.pose_cap;
+    PF_HIP_TRY(hipMemcpyAsync(o.h_pose, o.poses + 7 * slot, sizeof(double) * 7, hipMemcpyDeviceToHost, o.stream));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    std::memcpy(pose, o.h_pose, sizeof(double) * 7);
+    return PF_OK;
+}
+
+static int frame_status(pf_odom* h) {
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipMemcpyAsync(o.h_cnt, o.cnt, sizeof(int) * C_COUNT, hipMemcpyDeviceToHost, o.stream));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    PF_HIP_TRY(hipGetLastError());
+    if (!o.h_cnt[C_GATE]) return PF_W_MAP_TOO_SMALL;
+    if (o.h_cnt[C_EDGE_KEPT] < 20 || o.h_cnt[C_SURF_KEPT] < 20) return PF_W_FEW_CORRESPONDENCES;
+    return PF_OK;
+}
+
+int pf_odom_init_map(pf_odom* h, const float* edge, size_t ne, size_t edge_stride, const float* surf, size_t ns,
+                     size_t surf_stride) {
+    if (!h) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    int rc = stage_inputs(h, edge, ne, edge_stride, surf, ns, surf_stride);
+    if (rc) return rc;
+    odom_enqueue_init(h->o, h->o.stream);
+    h->o.frames++;
+    PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
+    PF_HIP_TRY(hipGetLastError());
+    return PF_OK;
+}
+
+int pf_odom_update(pf_odom* h, const float* edge, size_t ne, size_t edge_stride, const float* surf, size_t ns,
+                   size_t surf_stride, double pose_out[7]) {
+    if (!h) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    int rc = stage_inputs(h, edge, ne, edge_stride, surf, ns, surf_stride);
+    if (rc) return rc;
+    odom_enqueue_update(h->o, h->o.stream);
+    h->o.frames++;
+    if (pose_out) {
+        rc = read_pose(h, pose_out);
+        if (rc) return rc;
+    }
+    return frame_status(h);
+}
+
+int pf_odom_get_pose(pf_odom* h, double pose[7]) {
+    if (!h || !pose) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    return read_pose(h, pose);
+}
+
+int pf_odom_get_map(pf_odom* h, int which, float* xyz, uint8_t* rg, size_t cap, size_t* n) {
+    if (!h || !n || (which != 0 && which != 1)) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipMemcpyAsync(o.h_cnt, o.cnt, sizeof(int) * C_COUNT, hipMemcpyDeviceToHost, o.stream));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    const size_t m = (size_t)o.h_cnt[which == 0 ? C_ME : C_MS];
+    *n = m;
+    if (!xyz && !rg) return PF_OK;
+    if (m > cap) return PF_ECAPACITY;
+    std::vector<float4> tmp(m);
+    if (m) PF_HIP_TRY(hipMemcpy(tmp.data(), which == 0 ? o.map_e : o.map_s, sizeof(float4) * m, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < m; ++i) {
+        if (xyz) { xyz[3 * i] = tmp[i].x; xyz[3 * i + 1] = tmp[i].y; xyz[3 * i + 2] = tmp[i].z; }
+        if (rg) {
+            uint32_t w;
+            std::memcpy(&w, &tmp[i].w, 4);
+            rg[2 * i] = (uint8_t)(w & 255u);
+            rg[2 * i + 1] = (uint8_t)((w >> 8) & 255u);
+        }
+    }
+    return PF_OK;
+}
+
+int pf_odom_set_map(pf_odom* h, int which, const float* xyz, const uint8_t* rg, size_t n) {
+    if (!h || (which != 0 && which != 1) || (!xyz && n)) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    if (n > o.map_cap) return PF_ECAPACITY;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    std::vector<float4> tmp(n);
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t w = rg ? pack_rg(rg[2 * i], rg[2 * i + 1]) : 0u;
+        float wf;
+        std::memcpy(&wf, &w, 4);
+        tmp[i] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], wf);
+    }
+    if (n) PF_HIP_TRY(hipMemcpyAsync(which == 0 ? o.map_e : o.map_s, tmp.data(), sizeof(float4) * n,
+                                     hipMemcpyHostToDevice, o.stream));
+    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + (which == 0 ? C_ME : C_MS), (int)n);
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    return PF_OK;
+}
+
+int pf_odom_get_stats(pf_odom* h, pf_odom_stats* s) {
+    if (!h || !s) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipMemcpyAsync(o.h_cnt, o.cnt, sizeof(int) * C_COUNT, hipMemcpyDeviceToHost, o.stream));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    const int* c = o.h_cnt;
+    std::memset(s, 0, sizeof(*s));
+    s->n_edge_in = c[C_EIN];
+    s->n_surf_in = c[C_SIN];
+    s->n_edge_ds = c[C_EDS];
+    s->n_surf_ds = c[C_SDS];
+    s->n_edge_map = c[C_ME];
+    s->n_surf_map = c[C_MS];
+    s->n_edge_res = c[C_EDGE_KEPT];
+    s->n_surf_res = c[C_SURF_KEPT];
+    s->n_edge_valid = c[C_EDGE_VALID];
+    s->n_surf_valid = c[C_SURF_VALID];
+    s->outer_iterations = c[C_OUTER];
+    s->lm_iterations = c[C_LM_ITERS];
+    s->map_too_small = c[C_GATE] ? 0 : 1;
+    return PF_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// whole frame on the device. Steady-state frames (optimization_count == 2) replay one captured
+// hipGraph of the ~130-launch frame; the scan is first copied into the handle's fixed staging buffer.
+static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n) {
+    OdomGPU& o = h->o;
+    if (n > o.in_cap) return PF_ECAPACITY;
+    const bool steady = o.inited && o.opt_count_host <= 2;
+    if (steady && o.graph_enabled) {
+        if (n) PF_HIP_TRY(hipMemcpyAsync(o.stage, d_in, sizeof(float4) * n, hipMemcpyDeviceToDevice, o.stream));
+        hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_NIN, (int)n);
+        if (!o.graph) {
+            hipGraph_t g;
+            PF_HIP_TRY(hipStreamBeginCapture(o.stream, hipStreamCaptureModeThreadLocal));
+            odom_enqueue_frame(o, o.stage, o.stream);
+            PF_HIP_TRY(hipStreamEndCapture(o.stream, &g));
+            PF_HIP_TRY(hipGraphInstantiate(&o.graph, g, nullptr, nullptr, 0));
+            (void)hipGraphDestroy(g);
+        }
+        PF_HIP_TRY(hipGraphLaunch(o.graph, o.stream));
+    } else {
+        hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_NIN, (int)n);
+        odom_enqueue_frame(o, d_in, o.stream);
+    }
+    o.frames++;
+    return PF_OK;
+}
+
+int pf_odom_frame_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]) {
+    if (!h || (!d_xyzi && n)) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    int rc = enqueue_frame(h, reinterpret_cast<const float4*>(d_xyzi), n);
+    if (rc) return rc;
+    if (pose_out) return read_pose(h, pose_out);
+    return PF_OK;
+}
+
+int pf_odom_frame_host(pf_odom* h, const float* xyzi, size_t n, size_t stride_bytes, double pose_out[7]) {
+    if (!h || (!xyzi && n) || !valid_stride(stride_bytes)) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    if (n > o.in_cap) return PF_ECAPACITY;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    repack(xyzi, n, stride_bytes, h->host_e);
+    if (n) PF_HIP_TRY(hipMemcpyAsync(o.fe.d_in_stage, h->host_e.data(), sizeof(float4) * n, hipMemcpyHostToDevice,
+                                     o.stream));
+    int rc = enqueue_frame(h, o.fe.d_in_stage, n);
+    if (rc) return rc;
+    if (pose_out) return read_pose(h, pose_out);
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));   // host staging buffer is reused by the next call
+    return PF_OK;
+}
+
+int pf_odom_sync(pf_odom* h) {
+    if (!h) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
+    PF_HIP_TRY(hipGetLastError());
+    return PF_OK;
+}
+
+int pf_odom_poses(pf_odom* h, double* poses, size_t cap, size_t* n) {
+    if (!h || !n) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    const size_t f = (size_t)o.frames;
+    *n = f;
+    if (!poses) return PF_OK;
+    if (f > cap || f > o.pose_cap) return PF_ECAPACITY;
+    if (f) PF_HIP_TRY(hipMemcpy(poses, o.poses, sizeof(double) * 7 * f, hipMemcpyDeviceToHost));
+    return PF_OK;
+}
+
+int pf_odom_set_graph(pf_odom* h, int enable) {
+    if (!h) return PF_EINVAL;
+    h->o.graph_enabled = enable != 0;
+    return PF_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+int pf_device_count(int* n) {
+    if (!n) return PF_EINVAL;
+    PF_HIP_TRY(hipGetDeviceCount(n));
+    return PF_OK;
+}
+
+int pf_dev_malloc(int device, size_t bytes, void** d) {
+    if (!d) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(device));
+    if (hipMalloc(d, bytes) != hipSuccess) return PF_ENOMEM;
+    return PF_OK;
+}
+
+int pf_dev_free(int device, void* d) {
+    PF_HIP_TRY(hipSetDevice(device));
+    PF_HIP_TRY(hipFree(d));
+    return PF_OK;
+}
+
+int pf_memcpy_h2d(int device, void* dst, const void* src, size_t bytes) {
+    PF_HIP_TRY(hipSetDevice(device));
+    PF_HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return PF_OK;
+}
+
+int pf_memcpy_d2h(int device, void* dst, const void* src, size_t bytes) {
+    PF_HIP_TRY(hipSetDevice(device));
+    PF_HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return PF_OK;
+}
+
+}  // extern "C"

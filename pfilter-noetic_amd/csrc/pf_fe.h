@@ -1,0 +1,38 @@
+// Feature extraction on the device: LaserProcessingClass::featureExtraction
+// (src/laserProcessingClass.cpp:10-209) as six launches with device-resident counts.
+#pragma once
+#include "pf_common.h"
+
+namespace pf {
+
+constexpr int kMaxRings = 128;
+constexpr int kSecCap = 4096;      // max curvature entries per sector (KITTI-64: ~330)
+constexpr int kEdgePerSector = 20; // src/laserProcessingClass.cpp:121
+
+struct FeGPU {
+    pf_lidar_params lidar{};
+    int sqrt_double = 0;         // 0: sqrtf overload (default), 1: double sqrt
+    size_t cap = 0;              // max input points
+    int nblk_cap = 0;            // ceil(cap / 256)
+    int rings = 0;               // number of ring lists (num_lines)
+    // buffers
+    int* ring = nullptr;         // [cap]  ring id or -1
+    u32* blkhist = nullptr;      // [rings * nblk_cap]
+    int* ring_start = nullptr;   // [kMaxRings + 1]
+    float4* rp = nullptr;        // [cap] ring-ordered points
+    int* sec_edge_ids = nullptr; // [rings*6*20]
+    int* sec_surf_ids = nullptr; // [rings*6*kSecCap]
+    int* sec_cnt = nullptr;      // [rings*6*2]  edge, surf counts
+    int* sec_off = nullptr;      // [rings*6*2]  output offsets
+    int* err = nullptr;          // [1] sector overflow flag
+    float4* d_in_stage = nullptr;// [cap] staging for host inputs
+};
+
+int fe_alloc(FeGPU& f, const pf_lidar_params& lidar, size_t cap);
+void fe_free(FeGPU& f);
+// Enqueue feature extraction of *d_n device points (count read on the device). Outputs: edge/surf
+// float4 arrays with device counts d_ne / d_ns (capacity: edge >= rings*120, surf >= n).
+void fe_enqueue(FeGPU& f, const float4* d_in, const int* d_n, float4* edge, int* d_ne, float4* surf, int* d_ns,
+                hipStream_t s);
+
+}  // namespace pf

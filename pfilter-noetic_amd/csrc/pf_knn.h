@@ -1,0 +1,91 @@
+// Exact radius-gated 5-NN on a dense 1 m cell grid.
+//
+// The reference takes the 5 nearest map points from KdTreeFLANN::nearestKSearch and uses them only
+// when the 5th squared distance is < 1 (src/odomEstimationClass.cpp:299-300, 447-451). Every point
+// with d^2 < 1 of a query lies in the 3x3x3 block of 1 m cells around the query's cell (float
+// subtraction is monotone, so |fl(px - qx)| < 1 implies |px - qx| < 1), hence scanning those 27
+// cells with the same float distance (x, then y, then z, no FMA) gives bit-identical neighbours and
+// distances for every query the reference keeps. Ties are broken by map index.
+#pragma once
+#include "pf_common.h"
+#include "pf_prims.h"
+
+namespace pf {
+
+struct GridGPU {
+    int* bounds = nullptr;      // [2][6]   min cell x,y,z / max cell x,y,z per map (atomics)
+    int* dims = nullptr;        // [2][8]   minx,miny,minz, dx,dy,dz, base, valid
+    int* d_ncells = nullptr;    // [1]      total cells + 1 (scan length)
+    int* err = nullptr;         // [1]      cell capacity exceeded
+    u32* cell_count = nullptr;  // [cell_cap + 1]
+    u32* cell_start = nullptr;  // [cell_cap + 1]
+    u32* slot = nullptr;        // [pts_cap]
+    float4* cpts = nullptr;     // [pts_cap] cell-ordered (x, y, z, bits(map index))
+    size_t pts_cap = 0;
+    size_t cell_cap = 0;
+};
+
+int grid_alloc(GridGPU& g, size_t pts_cap, size_t cell_cap);
+void grid_free(GridGPU& g);
+// Build the grids of up to two maps (map1 may be null). Counts are device-resident.
+void grid_build(GridGPU& g, const float4* map0, const int* d_m0, const float4* map1, const int* d_m1, PrimWork& w,
+                hipStream_t s);
+
+struct GridView {
+    const int* dims;
+    const u32* cell_start;
+    const float4* cpts;
+};
+
+__device__ __forceinline__ bool knn_lt(float da, int ia, float db, int ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+// 5 nearest neighbours with d2 < 1 of query q in map m. Returns the count found (0..5); d/id sorted.
+__device__ __forceinline__ int knn5(const GridView& gv, int m, float qx, float qy, float qz, float (&d)[5],
+                                    int (&id)[5]) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { d[k] = 1.0f; id[k] = 0x7fffffff; }
+    const int* dm = gv.dims + 8 * m;
+    if (!dm[7]) return 0;
+    const int cx = (int)floorf(qx), cy = (int)floorf(qy), cz = (int)floorf(qz);
+    const int minx = dm[0], miny = dm[1], minz = dm[2], dx = dm[3], dy = dm[4], dz = dm[5], base = dm[6];
+    for (int oz = -1; oz <= 1; ++oz) {
+        const int z = cz + oz - minz;
+        if (z < 0 || z >= dz) continue;
+        for (int oy = -1; oy <= 1; ++oy) {
+            const int y = cy + oy - miny;
+            if (y < 0 || y >= dy) continue;
+            for (int ox = -1; ox <= 1; ++ox) {
+                const int x = cx + ox - minx;
+                if (x < 0 || x >= dx) continue;
+                const int cid = base + (z * dy + y) * dx + x;
+                const u32 b0 = gv.cell_start[cid], b1 = gv.cell_start[cid + 1];
+                for (u32 k = b0; k < b1; ++k) {
+                    const float4 p = gv.cpts[k];
+                    float r = 0.0f;
+                    float t = qx - p.x; r += t * t;
+                    t = qy - p.y; r += t * t;
+                    t = qz - p.z; r += t * t;
+                    if (!(r < 1.0f)) continue;
+                    const int idx = __float_as_int(p.w);
+                    if (!knn_lt(r, idx, d[4], id[4])) continue;
+                    d[4] = r; id[4] = idx;
+#pragma unroll
+                    for (int q = 4; q > 0; --q) {
+                        if (knn_lt(d[q], id[q], d[q - 1], id[q - 1])) {
+                            float td = d[q]; d[q] = d[q - 1]; d[q - 1] = td;
+                            int ti = id[q]; id[q] = id[q - 1]; id[q - 1] = ti;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    int found = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) found += (id[k] != 0x7fffffff) ? 1 : 0;
+    return found;
+}
+
+}  // namespace pf

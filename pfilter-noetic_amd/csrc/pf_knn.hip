@@ -1,0 +1,333 @@
+// Dense 1 m cell grid build (counting sort) and the standalone exact 5-NN query API.
+#include "pf_knn.h"
+
+#include <climits>
+#include <vector>
+
+namespace pf {
+namespace {
+
+__global__ void k_grid_reset(int* __restrict__ bounds) {
+    const int t = threadIdx.x;
+    if (t < 12) bounds[t] = ((t % 6) < 3) ? INT_MAX : INT_MIN;
+}
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// per-map min/max cell coordinates; one atomic per wave and coordinate
+__global__ void __launch_bounds__(256) k_grid_bounds(const float4* __restrict__ m0, const int* __restrict__ d_m0,
+                                                      const float4* __restrict__ m1, const int* __restrict__ d_m1,
+                                                      int* __restrict__ bounds) {
+    const int n0 = *d_m0, n1 = m1 ? *d_m1 : 0;
+    const int l = lane_id();
+    for (int mi = 0; mi < 2; ++mi) {
+        const float4* mp = mi == 0 ? m0 : m1;
+        const int n = mi == 0 ? n0 : n1;
+        int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+            const float4 p = mp[i];
+            const int c[3] = {(int)floorf(p.x), (int)floorf(p.y), (int)floorf(p.z)};
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { mn[k] = min(mn[k], c[k]); mx[k] = max(mx[k], c[k]); }
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int a = wave_min_i(mn[k]), b = wave_max_i(mx[k]);
+            if (l == 0 && a != INT_MAX) {
+                atomicMin(&bounds[mi * 6 + k], a);
+                atomicMax(&bounds[mi * 6 + 3 + k], b);
+            }
+        }
+    }
+}
+
+__global__ void k_grid_dims(const int* __restrict__ bounds, const int* __restrict__ d_m0, const int* __restrict__ d_m1,
+                            int* __restrict__ dims, int* __restrict__ d_ncells, long long cell_cap, int* __restrict__ err) {
+    if (threadIdx.x != 0) return;
+    long long base = 0;
+    for (int mi = 0; mi < 2; ++mi) {
+        const int n = mi == 0 ? *d_m0 : (d_m1 ? *d_m1 : 0);
+        int* dm = dims + 8 * mi;
+        if (n <= 0) {
+            for (int k = 0; k < 8; ++k) dm[k] = 0;
+            dm[6] = (int)base;
+            continue;
+        }
+        const int* b = bounds + 6 * mi;
+        const long long dx = (long long)b[3] - b[0] + 1, dy = (long long)b[4] - b[1] + 1, dz = (long long)b[5] - b[2] + 1;
+        const long long nc = dx * dy * dz;
+        if (base + nc > cell_cap) {           // grid too large for the handle: mark invalid
+            for (int k = 0; k < 8; ++k) dm[k] = 0;
+            dm[6] = (int)base;
+            atomicOr(err, 1);
+            continue;
+        }
+        dm[0] = b[0]; dm[1] = b[1]; dm[2] = b[2];
+        dm[3] = (int)dx; dm[4] = (int)dy; dm[5] = (int)dz;
+        dm[6] = (int)base;
+        dm[7] = 1;
+        base += nc;
+    }
+    *d_ncells = (int)(base + 1);
+}
+
+__global__ void __launch_bounds__(256) k_grid_clear(u32* __restrict__ cnt, const int* __restrict__ d_ncells) {
+    const int n = *d_ncells;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) cnt[i] = 0;
+}
+
+__device__ __forceinline__ int cell_of(const int* dm, float4 p) {
+    const int x = (int)floorf(p.x) - dm[0], y = (int)floorf(p.y) - dm[1], z = (int)floorf(p.z) - dm[2];
+    return dm[6] + (z * dm[4] + y) * dm[3] + x;
+}
+
+__global__ void __launch_bounds__(256) k_grid_count(const float4* __restrict__ m0, const int* __restrict__ d_m0,
+                                                     const float4* __restrict__ m1, const int* __restrict__ d_m1,
+                                                     const int* __restrict__ dims, u32* __restrict__ cnt,
+                                                     u32* __restrict__ slot) {
+    const int n0 = *d_m0, n1 = m1 ? *d_m1 : 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
+        const int mi = i < n0 ? 0 : 1;
+        const int* dm = dims + 8 * mi;
+        if (!dm[7]) continue;
+        const float4 p = mi == 0 ? m0[i] : m1[i - n0];
+        slot[i] = atomicAdd(&cnt[cell_of(dm, p)], 1u);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_grid_scatter(const float4* __restrict__ m0, const int* __restrict__ d_m0,
+                                                       const float4* __restrict__ m1, const int* __restrict__ d_m1,
+                                                       const int* __restrict__ dims, const u32* __restrict__ start,
+                                                       const u32* __restrict__ slot, float4* __restrict__ cpts) {
+    const int n0 = *d_m0, n1 = m1 ? *d_m1 : 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
+        const int mi = i < n0 ? 0 : 1;
+        const int* dm = dims + 8 * mi;
+        if (!dm[7]) continue;
+        const int li = mi == 0 ? i : i - n0;
+        const float4 p = mi == 0 ? m0[li] : m1[li];
+        cpts[start[cell_of(dm, p)] + slot[i]] = make_float4(p.x, p.y, p.z, __int_as_float(li));
+    }
+}
+
+// standalone query: queries in map 0
+__global__ void __launch_bounds__(256) k_knn_query(GridView gv, const float4* __restrict__ q, int nq,
+                                                    int* __restrict__ idx, float* __restrict__ d2) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const float4 p = q[i];
+    float d[5];
+    int id[5];
+    knn5(gv, 0, p.x, p.y, p.z, d, id);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const bool f = id[k] != 0x7fffffff;
+        idx[5 * i + k] = f ? id[k] : -1;
+        d2[5 * i + k] = f ? d[k] : __int_as_float(0x7f800000);
+    }
+}
+
+// |C(q)|: points in the 27 cells around each query (algorithmic byte count)
+__global__ void __launch_bounds__(256) k_knn_cellpop(GridView gv, const float4* __restrict__ q, int nq,
+                                                      unsigned long long* __restrict__ total) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long c = 0;
+    if (i < nq) {
+        const float4 p = q[i];
+        const int* dm = gv.dims;
+        if (dm[7]) {
+            const int cx = (int)floorf(p.x), cy = (int)floorf(p.y), cz = (int)floorf(p.z);
+            for (int oz = -1; oz <= 1; ++oz)
+                for (int oy = -1; oy <= 1; ++oy)
+                    for (int ox = -1; ox <= 1; ++ox) {
+                        const int x = cx + ox - dm[0], y = cy + oy - dm[1], z = cz + oz - dm[2];
+                        if (x < 0 || y < 0 || z < 0 || x >= dm[3] || y >= dm[4] || z >= dm[5]) continue;
+                        const int cid = dm[6] + (z * dm[4] + y) * dm[3] + x;
+                        c += gv.cell_start[cid + 1] - gv.cell_start[cid];
+                    }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane_id() == 0 && c) atomicAdd(total, c);
+}
+
+}  // namespace
+
+int grid_alloc(GridGPU& g, size_t pts_cap, size_t cell_cap) {
+    g.pts_cap = pts_cap;
+    g.cell_cap = cell_cap;
+    if (hipMalloc(&g.bounds, sizeof(int) * 12) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&g.dims, sizeof(int) * 16) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&g.d_ncells, sizeof(int)) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&g.err, sizeof(int)) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&g.cell_count, sizeof(u32) * (cell_cap + 1)) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&g.cell_start, sizeof(u32) * (cell_cap + 1)) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&g.slot, sizeof(u32) * pts_cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&g.cpts, sizeof(float4) * pts_cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMemset(g.err, 0, sizeof(int)) != hipSuccess) return PF_EHIP;
+    return PF_OK;
+}
+
+void grid_free(GridGPU& g) {
+    (void)hipFree(g.bounds);
+    (void)hipFree(g.dims);
+    (void)hipFree(g.d_ncells);
+    (void)hipFree(g.err);
+    (void)hipFree(g.cell_count);
+    (void)hipFree(g.cell_start);
+    (void)hipFree(g.slot);
+    (void)hipFree(g.cpts);
+    g = GridGPU{};
+}
+
+void grid_build(GridGPU& g, const float4* map0, const int* d_m0, const float4* map1, const int* d_m1, PrimWork& w,
+                hipStream_t s) {
+    const int nb = 512;
+    hipLaunchKernelGGL(k_grid_reset, dim3(1), dim3(64), 0, s, g.bounds);
+    hipLaunchKernelGGL(k_grid_bounds, dim3(nb), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.bounds);
+    hipLaunchKernelGGL(k_grid_dims, dim3(1), dim3(64), 0, s, g.bounds, d_m0, d_m1, g.dims, g.d_ncells,
+                       (long long)g.cell_cap, g.err);
+    hipLaunchKernelGGL(k_grid_clear, dim3(1024), dim3(256), 0, s, g.cell_count, g.d_ncells);
+    hipLaunchKernelGGL(k_grid_count, dim3(nb), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.dims, g.cell_count, g.slot);
+    scan_exclusive(g.cell_count, g.cell_start, g.d_ncells, nullptr, w, s);
+    hipLaunchKernelGGL(k_grid_scatter, dim3(nb), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.dims, g.cell_start,
+                       g.slot, g.cpts);
+}
+
+}  // namespace pf
+
+// ==================================================================================================
+// standalone kNN C ABI
+// ==================================================================================================
+using namespace pf;
+
+struct pf_knn {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    GridGPU grid;
+    PrimWork prim;
+    float4* d_map = nullptr;
+    int* d_m = nullptr;
+    float4* d_q = nullptr;
+    int* d_idx = nullptr;
+    float* d_d2 = nullptr;
+    unsigned long long* d_pop = nullptr;
+    size_t map_cap = 0, q_cap = 0;
+    int nq = 0;
+};
+
+extern "C" {
+
+int pf_knn_create(int device, size_t map_capacity, size_t query_capacity, pf_knn** out) {
+    if (!out || map_capacity == 0 || query_capacity == 0) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(device));
+    pf_knn* h = new pf_knn();
+    h->device = device;
+    h->map_cap = map_capacity;
+    h->q_cap = query_capacity;
+    int rc = PF_OK;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) rc = PF_EHIP;
+    // cells: a 1 m grid over the map bounding box; 64M cells covers e.g. a 400 x 400 x 400 m block
+    if (rc == PF_OK) rc = grid_alloc(h->grid, map_capacity, (size_t)1 << 26);
+    if (rc == PF_OK) rc = prim_alloc(h->prim, 1);  // scans only: no sort scratch
+    if (rc == PF_OK && hipMalloc(&h->d_map, sizeof(float4) * map_capacity) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMalloc(&h->d_m, sizeof(int) * 2) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMalloc(&h->d_q, sizeof(float4) * query_capacity) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMalloc(&h->d_idx, sizeof(int) * 5 * query_capacity) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMalloc(&h->d_d2, sizeof(float) * 5 * query_capacity) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMalloc(&h->d_pop, sizeof(unsigned long long)) != hipSuccess) rc = PF_ENOMEM;
+    if (rc != PF_OK) {
+        pf_knn_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return PF_OK;
+}
+
+int pf_knn_destroy(pf_knn* h) {
+    if (!h) return PF_OK;
+    (void)hipSetDevice(h->device);
+    grid_free(h->grid);
+    prim_free(h->prim);
+    (void)hipFree(h->d_map);
+    (void)hipFree(h->d_m);
+    (void)hipFree(h->d_q);
+    (void)hipFree(h->d_idx);
+    (void)hipFree(h->d_d2);
+    (void)hipFree(h->d_pop);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return PF_OK;
+}
+
+int pf_knn_set_map(pf_knn* h, const float* xyz4, size_t m) {
+    if (!h || (!xyz4 && m)) return PF_EINVAL;
+    if (m > h->map_cap) return PF_ECAPACITY;
+    PF_HIP_TRY(hipSetDevice(h->device));
+    const int mm[2] = {(int)m, 0};
+    if (m) PF_HIP_TRY(hipMemcpyAsync(h->d_map, xyz4, sizeof(float4) * m, hipMemcpyHostToDevice, h->stream));
+    PF_HIP_TRY(hipMemcpyAsync(h->d_m, mm, sizeof(mm), hipMemcpyHostToDevice, h->stream));
+    grid_build(h->grid, h->d_map, h->d_m, nullptr, nullptr, h->prim, h->stream);
+    int err = 0;
+    PF_HIP_TRY(hipMemcpyAsync(&err, h->grid.err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    PF_HIP_TRY(hipStreamSynchronize(h->stream));
+    PF_HIP_TRY(hipGetLastError());
+    return err ? PF_ECAPACITY : PF_OK;
+}
+
+int pf_knn_query(pf_knn* h, const float* q4, size_t nq, int32_t* idx, float* d2) {
+    if (!h || (!q4 && nq)) return PF_EINVAL;
+    if (nq > h->q_cap) return PF_ECAPACITY;
+    PF_HIP_TRY(hipSetDevice(h->device));
+    h->nq = (int)nq;
+    if (nq == 0) return PF_OK;
+    PF_HIP_TRY(hipMemcpyAsync(h->d_q, q4, sizeof(float4) * nq, hipMemcpyHostToDevice, h->stream));
+    GridView gv{h->grid.dims, h->grid.cell_start, h->grid.cpts};
+    hipLaunchKernelGGL(k_knn_query, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, h->stream, gv, h->d_q, (int)nq,
+                       h->d_idx, h->d_d2);
+    if (idx) PF_HIP_TRY(hipMemcpyAsync(idx, h->d_idx, sizeof(int) * 5 * nq, hipMemcpyDeviceToHost, h->stream));
+    if (d2) PF_HIP_TRY(hipMemcpyAsync(d2, h->d_d2, sizeof(float) * 5 * nq, hipMemcpyDeviceToHost, h->stream));
+    PF_HIP_TRY(hipStreamSynchronize(h->stream));
+    PF_HIP_TRY(hipGetLastError());
+    return PF_OK;
+}
+
+int pf_knn_bench(pf_knn* h, int iters, double* avg_ms, double* alg_bytes) {
+    if (!h || iters <= 0 || h->nq <= 0) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->device));
+    GridView gv{h->grid.dims, h->grid.cell_start, h->grid.cpts};
+    const dim3 grid((unsigned)((h->nq + 255) / 256));
+    PF_HIP_TRY(hipMemsetAsync(h->d_pop, 0, sizeof(unsigned long long), h->stream));
+    hipLaunchKernelGGL(k_knn_cellpop, grid, dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_pop);
+    unsigned long long pop = 0;
+    PF_HIP_TRY(hipMemcpyAsync(&pop, h->d_pop, sizeof(pop), hipMemcpyDeviceToHost, h->stream));
+    hipLaunchKernelGGL(k_knn_query, grid, dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2);  // warm
+    hipEvent_t e0, e1;
+    PF_HIP_TRY(hipEventCreate(&e0));
+    PF_HIP_TRY(hipEventCreate(&e1));
+    PF_HIP_TRY(hipEventRecord(e0, h->stream));
+    for (int it = 0; it < iters; ++it)
+        hipLaunchKernelGGL(k_knn_query, grid, dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2);
+    PF_HIP_TRY(hipEventRecord(e1, h->stream));
+    PF_HIP_TRY(hipEventSynchronize(e1));
+    float ms = 0;
+    PF_HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    PF_HIP_TRY(hipGetLastError());
+    if (avg_ms) *avg_ms = ms / iters;
+    if (alg_bytes) *alg_bytes = (double)h->nq * (16.0 + 40.0 + 27.0 * 8.0) + 16.0 * (double)pop;
+    return PF_OK;
+}
+
+}  // extern "C"

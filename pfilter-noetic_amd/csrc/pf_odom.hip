@@ -1,0 +1,1098 @@
+// Device-resident odometry: Odom_ES_EstimationClass::updatePointsToMap / initMapWithPoints
+// (src/odomEstimationClass.cpp:217-282) as a fixed sequence of launches with every count kept on
+// the device, so a frame is enqueued without any host round trip (and can be replayed as a graph).
+//
+//   k_predict        constant-velocity prediction, optimization_count schedule, map-size gate (:232-247)
+//   VoxelGrid        k_vg_minmax / k_vg_keys / radix sort / segments / k_vg_reduce: PCL 1.10 VoxelGrid
+//                    (edge leaf 0.4, surf 0.8, :242-245) for both clouds in one batched pass
+//   grid_build       1 m cell grids of the edge and surf maps (the kd-trees of :249-250)
+//   per outer iteration (:252-272)
+//     k_assoc        pointAssociateToMap + exact 5-NN + line fit (eigen, :299-331) / plane fit (QR,
+//                    :447-476) + round / sparsity
+//     p-index        (neighbour, query) pairs radix-sorted by neighbour: c_i(n) = earlier valid queries
+//                    sharing neighbour n reproduces the in-order increments of :345-346 / :493-496
+//     k_observe      observe/round skip test (:348-356, :497-505), kept flags, weight statistics
+//     LM             k_lm_init + 5 x (k_lm_eval, k_lm_step): Ceres 1.14 LM (Huber 0.1, Jacobi scaling,
+//                    radius 1e4, <= 4 iterations) on the 6x6 normal equations
+//   k_finalize       odom from the solved pose (:278-280), pose output (node: copy.cpp:105-107)
+//   addPointsToMap   transform/append, CropBox +-100 m, rgbds (centroid + max r/g), extractstablepoint,
+//                    ageing (:589-647): batched keys / radix sort / segments / reduce / compaction
+#include "pf_odom.h"
+#include "pf_geom.h"
+
+#include <climits>
+#include <cstring>
+
+namespace pf {
+namespace {
+
+constexpr u32 kSentinel = 0xFFFFFFFFu;
+constexpr int kGrid = 512;   // grid-stride workgroups for per-point kernels
+
+__device__ __forceinline__ float wave_minf(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ u32 w_r(const float4& p) { return __float_as_uint(p.w) & 255u; }
+__device__ __forceinline__ u32 w_g(const float4& p) { return (__float_as_uint(p.w) >> 8) & 255u; }
+
+__device__ __forceinline__ iso load_iso(const double* R, const double* t) {
+    iso a;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) a.R.m[i][j] = R[3 * i + j];
+    a.t = d3{t[0], t[1], t[2]};
+    return a;
+}
+__device__ __forceinline__ void store_iso(const iso& a, double* R, double* t) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[3 * i + j] = a.R.m[i][j];
+    t[0] = a.t.x; t[1] = a.t.y; t[2] = a.t.z;
+}
+
+// pointAssociateToMap (:162-174): double transform, float result
+__device__ __forceinline__ float4 associate(const double* prm, float4 p) {
+    const qd q{prm[0], prm[1], prm[2], prm[3]};
+    const d3 w = add3(qrot(q, d3{(double)p.x, (double)p.y, (double)p.z}), d3{prm[4], prm[5], prm[6]});
+    return make_float4((float)w.x, (float)w.y, (float)w.z, p.w);
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ void k_predict(DevState* __restrict__ st, int* __restrict__ cnt, u32* __restrict__ acc) {
+    const int t = threadIdx.x;
+    if (t < 12) acc[A_VG + t] = ((t % 6) < 3) ? 0xFFFFFFFFu : 0u;
+    if (t != 0) return;
+    if (st->optimization_count > 2) st->optimization_count--;                 // :232-233
+    const iso odom = load_iso(st->odomR, st->odomt);
+    const iso last = load_iso(st->lastR, st->lastt);
+    const iso pred = iso_mul(odom, iso_mul(iso_inv(last), odom));             // :235
+    store_iso(odom, st->lastR, st->lastt);
+    store_iso(pred, st->odomR, st->odomt);
+    const qd q = m2q(pred.R);                                                  // :239 (rotation() = linear())
+    st->params[0] = q.x; st->params[1] = q.y; st->params[2] = q.z; st->params[3] = q.w;
+    st->params[4] = pred.t.x; st->params[5] = pred.t.y; st->params[6] = pred.t.z;
+    const int gate = (cnt[C_ME] > 10 && cnt[C_MS] > 50) ? 1 : 0;              // :247
+    st->gate = gate;
+    cnt[C_GATE] = gate;
+    cnt[C_OUTER] = gate ? st->optimization_count : 0;
+    cnt[C_LM_ITERS] = 0;
+    cnt[C_EDGE_KEPT] = cnt[C_SURF_KEPT] = cnt[C_EDGE_VALID] = cnt[C_SURF_VALID] = 0;
+    cnt[C_VGN] = cnt[C_EIN] + cnt[C_SIN];
+}
+
+// ----------------------------------- VoxelGrid (B.1) ------------------------------------------
+__global__ void __launch_bounds__(256) k_vg_minmax(const float4* __restrict__ e, const float4* __restrict__ s,
+                                                    const int* __restrict__ cnt, u32* __restrict__ acc) {
+    __shared__ float red[4][12];
+    const int n0 = cnt[C_EIN], n1 = cnt[C_SIN];
+    float v[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) v[k] = ((k % 6) < 3) ? FLT_MAX : -FLT_MAX;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
+        const int c = i < n0 ? 0 : 1;
+        const float4 p = c == 0 ? e[i] : s[i - n0];
+        const float xyz[3] = {p.x, p.y, p.z};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (c == 0) { v[k] = fminf(v[k], xyz[k]); v[3 + k] = fmaxf(v[3 + k], xyz[k]); }
+            else { v[6 + k] = fminf(v[6 + k], xyz[k]); v[9 + k] = fmaxf(v[9 + k], xyz[k]); }
+        }
+    }
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const float r = ((k % 6) < 3) ? wave_minf(v[k]) : wave_maxf(v[k]);
+        if (lane_id() == 0) red[w][k] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        const int k = threadIdx.x;
+        float r = red[0][k];
+        for (int ww = 1; ww < 4; ++ww) r = ((k % 6) < 3) ? fminf(r, red[ww][k]) : fmaxf(r, red[ww][k]);
+        const bool any = ((k % 6) < 3) ? (r != FLT_MAX) : (r != -FLT_MAX);
+        if (any) {
+            if ((k % 6) < 3) atomicMin(&acc[A_VG + k], f2ord(r));
+            else atomicMax(&acc[A_VG + k], f2ord(r));
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_vg_keys(const float4* __restrict__ e, const float4* __restrict__ s,
+                                                  const int* __restrict__ cnt, const u32* __restrict__ acc,
+                                                  float leaf0, float leaf1, u32* __restrict__ keys,
+                                                  u32* __restrict__ vals) {
+    const int n0 = cnt[C_EIN], n1 = cnt[C_SIN];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
+        const int c = i < n0 ? 0 : 1;
+        const float4 p = c == 0 ? e[i] : s[i - n0];
+        const float inv = 1.0f / (c == 0 ? leaf0 : leaf1);     // inverse_leaf_size_
+        const u32* a = acc + A_VG + 6 * c;
+        const float mn[3] = {ord2f(a[0]), ord2f(a[1]), ord2f(a[2])};
+        const float mx[3] = {ord2f(a[3]), ord2f(a[4]), ord2f(a[5])};
+        const long long dx = (long long)((mx[0] - mn[0]) * inv) + 1;
+        const long long dy = (long long)((mx[1] - mn[1]) * inv) + 1;
+        const long long dz = (long long)((mx[2] - mn[2]) * inv) + 1;
+        u32 key;
+        if (dx * dy * dz > (long long)INT_MAX) {
+            key = (u32)(i - (c == 0 ? 0 : n0));   // "leaf too small": output = input, order kept
+        } else {
+            int minb[3], div[3];
+            for (int k = 0; k < 3; ++k) {
+                minb[k] = (int)floorf(mn[k] * inv);
+                div[k] = (int)floorf(mx[k] * inv) - minb[k] + 1;
+            }
+            const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
+            const int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
+            const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
+            key = (u32)(i0 + i1 * div[0] + i2 * (div[0] * div[1]));
+        }
+        keys[i] = key | ((u32)c << 31);
+        vals[i] = (u32)i;
+    }
+}
+
+// segment heads of a sorted key array; sentinel keys never start a segment
+__global__ void __launch_bounds__(256) k_seg_heads(const u32* __restrict__ keys, const int* __restrict__ d_n,
+                                                    u32* __restrict__ flags) {
+    const int n = *d_n;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const u32 k = keys[i];
+        flags[i] = (k != kSentinel && (i == 0 || keys[i - 1] != k)) ? 1u : 0u;
+    }
+}
+
+// segment starts; count of cloud-0 segments and of non-sentinel entries
+__global__ void __launch_bounds__(256) k_seg_starts(const u32* __restrict__ keys, const int* __restrict__ d_n,
+                                                     const u32* __restrict__ flags, const u32* __restrict__ segid,
+                                                     u32* __restrict__ segstart, int* __restrict__ cnt) {
+    const int n = *d_n;
+    const int nseg = cnt[C_NSEG];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (n == 0) { cnt[C_NSEG_E] = 0; cnt[C_NRG_VALID] = 0; }
+        else {
+            if (keys[0] == kSentinel) cnt[C_NRG_VALID] = 0;
+            if ((keys[0] >> 31) != 0) cnt[C_NSEG_E] = 0;
+            const u32 kl = keys[n - 1];
+            if (kl != kSentinel) cnt[C_NRG_VALID] = n;
+            if ((kl >> 31) == 0) cnt[C_NSEG_E] = nseg;
+        }
+    }
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (flags[i]) segstart[segid[i]] = (u32)i;
+        if (i > 0) {
+            const u32 k = keys[i], kp = keys[i - 1];
+            if ((kp >> 31) == 0 && (k >> 31) == 1) cnt[C_NSEG_E] = (int)segid[i];
+            if (kp != kSentinel && k == kSentinel) cnt[C_NRG_VALID] = i;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_vg_reduce(const float4* __restrict__ e, const float4* __restrict__ s,
+                                                    const u32* __restrict__ keys, const u32* __restrict__ vals,
+                                                    const u32* __restrict__ segstart, int* __restrict__ cnt,
+                                                    float4* __restrict__ ds_e, float4* __restrict__ ds_s) {
+    const int n0 = cnt[C_EIN];
+    const int n = cnt[C_VGN];
+    const int nseg = cnt[C_NSEG], nse = cnt[C_NSEG_E];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        cnt[C_EDS] = nse;
+        cnt[C_SDS] = nseg - nse;
+        cnt[C_NQ] = nseg;
+    }
+    for (int sg = blockIdx.x * blockDim.x + threadIdx.x; sg < nseg; sg += gridDim.x * blockDim.x) {
+        const u32 b0 = segstart[sg], b1 = (sg + 1 < nseg) ? segstart[sg + 1] : (u32)n;
+        const int c = (int)(keys[b0] >> 31);
+        float sx = 0.f, sy = 0.f, sz = 0.f;
+        for (u32 k = b0; k < b1; ++k) {      // AccumulatorXYZ, sorted (stable) order
+            const u32 i = vals[k];
+            const float4 p = (int)i < n0 ? e[i] : s[i - n0];
+            sx += p.x; sy += p.y; sz += p.z;
+        }
+        const float nn = (float)(b1 - b0);
+        // rgb of inputs is 0 (copyPointCloud XYZI -> XYZRGB): averages stay 0
+        const float4 o = make_float4(sx / nn, sy / nn, sz / nn, __uint_as_float(0u));
+        if (c == 0) ds_e[sg] = o;
+        else ds_s[sg - nse] = o;
+    }
+}
+
+// ---------------------------------- association ---------------------------------------------
+struct AssocArgs {
+    const DevState* st;
+    int* cnt;
+    u32* acc;
+    GridView gv;
+    const float4* ds_e;
+    const float4* ds_s;
+    const float4* map_e;
+    const float4* map_s;
+    int* nbr;
+    int* qflag;
+    double* geo;
+    float* spars;
+    float* roundv;
+    u32* keys;
+    u32* vals;
+    u32 map_cap;
+};
+
+__global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
+    const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
+    const int gate = a.st->gate;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.cnt[C_NPAIR] = gate ? 5 * nq : 0;
+        a.cnt[C_EDGE_KEPT] = a.cnt[C_SURF_KEPT] = a.cnt[C_EDGE_VALID] = a.cnt[C_SURF_VALID] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 8) a.acc[A_W + threadIdx.x] = (threadIdx.x & 1) ? 0u : 0xFFFFFFFFu;
+    if (!gate) return;
+    double prm[7];
+    for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+        const int c = q < ne ? 0 : 1;
+        const float4 p = c == 0 ? a.ds_e[q] : a.ds_s[q - ne];
+        const float4 pw = associate(prm, p);
+        float d[5];
+        int id[5];
+        const int found = knn5(a.gv, c, pw.x, pw.y, pw.z, d, id);
+        bool valid = false;
+        const float4* mp = c == 0 ? a.map_e : a.map_s;
+        if (found == 5) {
+            double px[5], py[5], pz[5];
+            u32 rsum = 0;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const float4 m = mp[id[j]];
+                px[j] = m.x; py[j] = m.y; pz[j] = m.z;
+                rsum += w_r(m);
+            }
+            double* G = a.geo + 8 * (size_t)q;
+            if (c == 0) {                                            // :302-331
+                d3 center{0, 0, 0};
+                for (int j = 0; j < 5; ++j) center = add3(center, d3{px[j], py[j], pz[j]});
+                center = d3{center.x / 5.0, center.y / 5.0, center.z / 5.0};
+                double cov[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+                for (int j = 0; j < 5; ++j) {
+                    const double tv[3] = {px[j] - center.x, py[j] - center.y, pz[j] - center.z};
+                    for (int r = 0; r < 3; ++r)
+                        for (int cc = 0; cc < 3; ++cc) cov[r][cc] = cov[r][cc] + tv[r] * tv[cc];
+                }
+                double ev[3], V[3][3];
+                eig3(cov, ev, V);
+                if (ev[2] > 3 * ev[1]) {
+                    valid = true;
+                    const d3 dir{V[0][2], V[1][2], V[2][2]};
+                    G[0] = 0.1 * dir.x + center.x; G[1] = 0.1 * dir.y + center.y; G[2] = 0.1 * dir.z + center.z;
+                    G[3] = -0.1 * dir.x + center.x; G[4] = -0.1 * dir.y + center.y; G[5] = -0.1 * dir.z + center.z;
+                }
+            } else {                                                 // :449-476
+                double A[5][3];
+                for (int j = 0; j < 5; ++j) { A[j][0] = px[j]; A[j][1] = py[j]; A[j][2] = pz[j]; }
+                d3 n = plane5(A);
+                const double nd = 1 / nrm3(n);
+                const double z = n.x * n.x + n.y * n.y + n.z * n.z;
+                if (z > 0.0) {
+                    const double sq = sqrt(z);
+                    n = d3{n.x / sq, n.y / sq, n.z / sq};
+                }
+                valid = true;
+                for (int j = 0; j < 5; ++j)
+                    if (fabs(n.x * px[j] + n.y * py[j] + n.z * pz[j] + nd) > 0.2) { valid = false; break; }
+                if (valid) {
+                    G[0] = n.x; G[1] = n.y; G[2] = n.z;
+                    G[3] = (double)(float)nd;                        // surfInfo::negative_OA_dot_norm is float (A.7)
+                }
+            }
+            if (valid) {
+                a.roundv[q] = (float)(rsum / 5.0);                   // :339-344 (r constant within a frame)
+                d3 cn{0, 0, 0};                                      // sparsity, :367-385
+                for (int j = 0; j < 5; ++j) cn = add3(cn, d3{px[j], py[j], pz[j]});
+                cn = d3{cn.x / 5, cn.y / 5, cn.z / 5};
+                float sum = 0;
+                for (int j = 0; j < 5; ++j) sum += nrm3(sub3(cn, d3{px[j], py[j], pz[j]}));
+                sum /= 5.0;
+                a.spars[q] = sum;
+            }
+        }
+        a.qflag[q] = valid ? 1 : 0;
+        const u32 off = c == 0 ? 0u : a.map_cap;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            a.nbr[5 * q + j] = found == 5 ? id[j] : -1;
+            a.keys[5 * q + j] = valid ? off + (u32)id[j] : kSentinel;
+            a.vals[5 * q + j] = (u32)(5 * q + j);
+        }
+    }
+}
+
+// c_i(n): earlier valid queries sharing neighbour n (pairs sorted stably by neighbour)
+__global__ void __launch_bounds__(256) k_pidx_count(const u32* __restrict__ keys, const u32* __restrict__ vals,
+                                                     const int* __restrict__ cnt, u32* __restrict__ pcnt,
+                                                     u32* __restrict__ tailinc) {
+    const int n = cnt[C_NPAIR];
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+        const u32 k = keys[p];
+        if (k == kSentinel) { tailinc[p] = 0; continue; }
+        int c = 0;
+        while (p - c - 1 >= 0 && keys[p - c - 1] == k) ++c;
+        pcnt[vals[p]] = (u32)c;
+        const bool tail = (p == n - 1) || keys[p + 1] != k;
+        tailinc[p] = tail ? (u32)(c + 1) : 0u;
+    }
+}
+
+struct ObsArgs {
+    int* cnt;
+    u32* acc;
+    const float4* map_e;
+    const float4* map_s;
+    float4* ds_e;
+    float4* ds_s;
+    const int* nbr;
+    int* qflag;
+    const u32* pcnt;
+    const float* roundv;
+    const float* spars;
+    float* observe;
+    int k_new;
+    float theta_p;
+    int theta_max;
+};
+
+__global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
+    const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
+    const int t = threadIdx.x;
+    float mn[2][2] = {{FLT_MAX, FLT_MAX}, {FLT_MAX, FLT_MAX}}, mx[2][2] = {{-FLT_MAX, -FLT_MAX}, {-FLT_MAX, -FLT_MAX}};
+    int nvalid[2] = {0, 0}, nkept[2] = {0, 0};
+    for (int q = blockIdx.x * blockDim.x + t; q < nq; q += gridDim.x * blockDim.x) {
+        int f = a.qflag[q];
+        if (!(f & 1)) continue;
+        const int c = q < ne ? 0 : 1;
+        const float4* mp = c == 0 ? a.map_e : a.map_s;
+        int gs = 0;
+        for (int j = 0; j < 5; ++j) {
+            const u32 g0 = w_g(mp[a.nbr[5 * q + j]]);
+            gs += min(255u, g0 + a.pcnt[5 * q + j]);
+        }
+        float observe = gs / 5.0 + 1;                        // :332-338 / :480-486
+        const float round = a.roundv[q];
+        ++nvalid[c];
+        if (observe / round > 5) observe = 255;              // :348-349
+        if (observe < round * a.theta_p && round > a.k_new && observe < a.theta_max) continue;   // :350-353
+        ++nkept[c];
+        a.qflag[q] = f | 2;
+        a.observe[q] = observe;
+        const u32 rq = (u32)min(255, int(round)), gq = (u32)min(255, int(observe));   // :354-355
+        if (c == 0) a.ds_e[q].w = __uint_as_float(pack_rg(rq, gq));
+        else a.ds_s[q - ne].w = __uint_as_float(pack_rg(rq, gq));
+        const float sp = a.spars[q];
+        mn[c][0] = fminf(mn[c][0], observe); mx[c][0] = fmaxf(mx[c][0], observe);
+        mn[c][1] = fminf(mn[c][1], sp); mx[c][1] = fmaxf(mx[c][1], sp);
+    }
+    for (int c = 0; c < 2; ++c) {
+        const int v = wave_sum_i(nvalid[c]), k = wave_sum_i(nkept[c]);
+        if (lane_id() == 0) {
+            if (v) atomicAdd(&a.cnt[c == 0 ? C_EDGE_VALID : C_SURF_VALID], v);
+            if (k) atomicAdd(&a.cnt[c == 0 ? C_EDGE_KEPT : C_SURF_KEPT], k);
+        }
+        for (int w = 0; w < 2; ++w) {
+            const float lo = wave_minf(mn[c][w]), hi = wave_maxf(mx[c][w]);
+            if (lane_id() == 0 && lo != FLT_MAX) {
+                atomicMin(&a.acc[A_W + 4 * c + 2 * w], f2ord(lo));
+                atomicMax(&a.acc[A_W + 4 * c + 2 * w + 1], f2ord(hi));
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pidx_apply(const u32* __restrict__ keys, const u32* __restrict__ tailinc,
+                                                     const int* __restrict__ cnt, float4* __restrict__ map_e,
+                                                     float4* __restrict__ map_s, u32 map_cap) {
+    const int n = cnt[C_NPAIR];
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+        const u32 inc = tailinc[p];
+        if (!inc) continue;
+        const u32 k = keys[p];
+        float4* mp = k >= map_cap ? map_s : map_e;
+        const u32 idx = k >= map_cap ? k - map_cap : k;
+        const float4 m = mp[idx];
+        const u32 g = min(255u, w_g(m) + inc);                       // g = min(255, g + 1), c times
+        mp[idx].w = __uint_as_float(pack_rg(w_r(m), g));
+    }
+}
+
+// ------------------------------------ LM (B.6) ----------------------------------------------
+__global__ void k_lm_init(const DevState* __restrict__ st, const int* __restrict__ cnt, const u32* __restrict__ acc,
+                          LMState* __restrict__ lm) {
+    if (threadIdx.x != 0) return;
+    const int nres = cnt[C_EDGE_KEPT] + cnt[C_SURF_KEPT];
+    double xn = 0;
+    for (int k = 0; k < 7; ++k) {
+        lm->x[k] = lm->cand[k] = lm->best[k] = st->params[k];
+        xn += lm->x[k] * lm->x[k];
+    }
+    lm->x_norm = sqrt(xn);
+    lm->radius = 1e4;
+    lm->decrease = 2.0;
+    lm->iteration = 0;
+    lm->invalid = 0;
+    lm->reuse = 0;
+    lm->phase = 0;
+    lm->n_res = nres;
+    lm->done = (!st->gate || nres == 0) ? 1 : 0;   // no residual blocks: parameter block untouched
+    for (int c = 0; c < 2; ++c)
+        for (int w = 0; w < 2; ++w) {
+            lm->wmin[c][w] = (double)ord2f(acc[A_W + 4 * c + 2 * w]);
+            lm->wmax[c][w] = (double)ord2f(acc[A_W + 4 * c + 2 * w + 1]);
+        }
+}
+
+// observeMean (:136-160) / pointSparsityMean (.h:111-126) of one element, given min/max
+__device__ __forceinline__ double norm_weight(double e, double mn, double mx, bool clamp) {
+    const double length = mx - mn;
+    if (length == 0) return e;
+    e = (e - mn) / length;
+    e -= 1.0;
+    e = fabs(e);
+    e *= 2.0;
+    if (clamp) e = fmax(0.1, e);
+    return e;
+}
+
+struct EvalArgs {
+    const LMState* lm;
+    const int* cnt;
+    const int* qflag;
+    const float4* ds_e;
+    const float4* ds_s;
+    const double* geo;
+    const float* observe;
+    const float* spars;
+    double* part;
+    int weight_type;
+};
+
+__global__ void __launch_bounds__(256) k_lm_eval(EvalArgs a) {
+    if (a.lm->done) return;
+    __shared__ double red[4][kLmParts];
+    const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
+    double x[7];
+    for (int k = 0; k < 7; ++k) x[k] = a.lm->cand[k];
+    double acc[kLmParts];
+#pragma unroll
+    for (int k = 0; k < kLmParts; ++k) acc[k] = 0.0;
+    const int wt = a.weight_type;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+        if (!(a.qflag[q] & 2)) continue;
+        const int c = q < ne ? 0 : 1;
+        const float4 p = c == 0 ? a.ds_e[q] : a.ds_s[q - ne];
+        const d3 cur{(double)p.x, (double)p.y, (double)p.z};
+        double w = 0.0;
+        if (wt != 0) {
+            const double wo = norm_weight((double)a.observe[q], a.lm->wmin[c][0], a.lm->wmax[c][0], true);
+            const double ws = norm_weight((double)a.spars[q], a.lm->wmin[c][1], a.lm->wmax[c][1], false);
+            if (wt == 1) w = wo;
+            else if (wt == 2) w = ws;
+            else w = c == 0 ? (ws + wo) / 2 : (wo + ws) / 2;
+        }
+        const double* G = a.geo + 8 * (size_t)q;
+        double J[6];
+        double r = c == 0 ? edge_eval(x, cur, d3{G[0], G[1], G[2]}, d3{G[3], G[4], G[5]}, w, J)
+                          : surf_eval(x, cur, d3{G[0], G[1], G[2]}, G[3], w, J);
+        bool jbad = false;
+        for (int k = 0; k < 6; ++k) jbad |= !isfinite(J[k]);
+        if (!isfinite(r)) { acc[28] += 1.0; continue; }
+        if (jbad) acc[29] += 1.0;
+        const double s = r * r;                                    // HuberLoss(0.1) + Corrector
+        double rho0, rho1;
+        if (s > 0.1 * 0.1) {
+            const double rr = sqrt(s);
+            rho0 = 2.0 * 0.1 * rr - 0.1 * 0.1;
+            rho1 = fmax(DBL_MIN, 0.1 / rr);
+        } else {
+            rho0 = s;
+            rho1 = 1.0;
+        }
+        acc[0] += 0.5 * rho0;
+        const double sr = sqrt(rho1);
+        r *= sr;
+        for (int k = 0; k < 6; ++k) J[k] *= sr;
+        for (int k = 0; k < 6; ++k) acc[1 + k] += J[k] * r;
+        int h = 7;
+        for (int i = 0; i < 6; ++i)
+            for (int j = i; j < 6; ++j) acc[h++] += J[i] * J[j];
+    }
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < kLmParts; ++k) {
+        const double v = wave_sum(acc[k]);
+        if (lane_id() == 0) red[w][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kLmParts) {
+        const int k = threadIdx.x;
+        a.part[blockIdx.x * 32 + k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+    }
+}
+
+__device__ bool chol6(const double* H, const double* g, double* y) {
+    double L[36];
+    for (int i = 0; i < 36; ++i) L[i] = 0.0;
+    for (int i = 0; i < 6; ++i) {
+        for (int j = 0; j <= i; ++j) {
+            double s = H[i * 6 + j];
+            for (int k = 0; k < j; ++k) s -= L[i * 6 + k] * L[j * 6 + k];
+            if (i == j) {
+                if (!(s > 0.0)) return false;
+                L[i * 6 + i] = sqrt(s);
+            } else {
+                L[i * 6 + j] = s / L[j * 6 + j];
+            }
+        }
+    }
+    double z[6];
+    for (int i = 0; i < 6; ++i) {
+        double s = g[i];
+        for (int k = 0; k < i; ++k) s -= L[i * 6 + k] * z[k];
+        z[i] = s / L[i * 6 + i];
+    }
+    for (int i = 5; i >= 0; --i) {
+        double s = z[i];
+        for (int k = i + 1; k < 6; ++k) s -= L[k * 6 + i] * y[k];
+        y[i] = s / L[i * 6 + i];
+    }
+    return true;
+}
+
+__device__ double grad_max_norm(const double* x, const double* g) {
+    double ng[6], xp[7];
+    for (int j = 0; j < 6; ++j) ng[j] = -g[j];
+    se3_plus(x, ng, xp);
+    double m = 0.0;
+    for (int j = 0; j < 7; ++j) m = fmax(m, fabs(x[j] - xp[j]));
+    return m;
+}
+
+__device__ __forceinline__ void full_h(const double* h21, double* H) {
+    int h = 0;
+    for (int i = 0; i < 6; ++i)
+        for (int j = i; j < 6; ++j) { H[i * 6 + j] = h21[h]; H[j * 6 + i] = h21[h]; ++h; }
+}
+
+// TrustRegionMinimizer + LevenbergMarquardtStrategy state machine (one lane)
+__device__ void lm_next_step(LMState* lm, int* cnt) {
+    const int kMaxIter = 4;
+    double H[36];
+    full_h(lm->H, H);
+    for (;;) {
+        lm->iteration++;
+        double Hs[36], gs[6];
+        for (int i = 0; i < 6; ++i) {
+            gs[i] = lm->scale[i] * lm->g[i];
+            for (int j = 0; j < 6; ++j) Hs[i * 6 + j] = lm->scale[i] * H[i * 6 + j] * lm->scale[j];
+        }
+        if (!lm->reuse)
+            for (int j = 0; j < 6; ++j) lm->D[j] = fmin(fmax(Hs[j * 6 + j], 1e-6), 1e32);
+        double A[36], y[6];
+        for (int i = 0; i < 36; ++i) A[i] = Hs[i];
+        for (int j = 0; j < 6; ++j) {
+            const double ld = sqrt(lm->D[j] / lm->radius);
+            A[j * 6 + j] += ld * ld;
+        }
+        bool ok = chol6(A, gs, y);
+        for (int j = 0; j < 6; ++j) ok = ok && isfinite(y[j]);
+        lm->reuse = 1;
+        double step[6], mcc = 0.0;
+        if (ok) {
+            for (int j = 0; j < 6; ++j) step[j] = -y[j];
+            double sg = 0.0, sHs = 0.0;
+            for (int i = 0; i < 6; ++i) {
+                sg += step[i] * gs[i];
+                double hi = 0.0;
+                for (int j = 0; j < 6; ++j) hi += Hs[i * 6 + j] * step[j];
+                sHs += step[i] * hi;
+            }
+            mcc = -(sg + 0.5 * sHs);
+        }
+        if (!ok || !(mcc > 0.0)) {                       // invalid step (HandleInvalidStep)
+            if (++lm->invalid >= 5) { lm->done = 1; return; }
+            lm->radius = lm->radius / lm->decrease;
+            lm->decrease *= 2.0;
+            if (lm->iteration >= kMaxIter || lm->radius <= 1e-32) { lm->done = 1; return; }
+            continue;
+        }
+        lm->invalid = 0;
+        double delta[6];
+        for (int j = 0; j < 6; ++j) delta[j] = step[j] * lm->scale[j];
+        se3_plus(lm->x, delta, lm->cand);
+        lm->mcc = mcc;
+        lm->phase = 1;
+        return;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_lm_step(LMState* __restrict__ lm, const double* __restrict__ part,
+                                                  DevState* __restrict__ st, int* __restrict__ cnt) {
+    __shared__ double sub[kLmParts][8];
+    __shared__ double tot[kLmParts];
+    if (lm->done) return;
+    const int t = threadIdx.x;
+    if (t < kLmParts * 8) {
+        const int k = t >> 3, s = t & 7;
+        double v = 0.0;
+        for (int b = s * (kLmBlocks / 8); b < (s + 1) * (kLmBlocks / 8); ++b) v += part[b * 32 + k];
+        sub[k][s] = v;
+    }
+    __syncthreads();
+    if (t < kLmParts) {
+        double v = 0.0;
+        for (int s = 0; s < 8; ++s) v += sub[t][s];
+        tot[t] = v;
+    }
+    __syncthreads();
+    if (t != 0) return;
+    const double cost_c = tot[0];
+    const bool bad_r = tot[28] > 0.0, bad_j = tot[29] > 0.0;
+    const int kMaxIter = 4;
+    if (lm->phase == 0) {                                        // IterationZero
+        if (bad_r || bad_j) {
+            lm->done = 1;
+        } else {
+            lm->cost = cost_c;
+            for (int k = 0; k < 6; ++k) lm->g[k] = tot[1 + k];
+            for (int k = 0; k < 21; ++k) lm->H[k] = tot[7 + k];
+            int d = 0;
+            for (int i = 0; i < 6; ++i) {
+                lm->scale[i] = 1.0 / (1.0 + sqrt(lm->H[d]));     // Jacobi scaling, computed once
+                d += 6 - i;
+            }
+            lm->min_cost = lm->cost;
+            for (int k = 0; k < 7; ++k) lm->best[k] = lm->x[k];
+            if (grad_max_norm(lm->x, lm->g) <= 1e-10) lm->done = 1;
+            else lm_next_step(lm, cnt);
+        }
+    } else {                                                     // candidate evaluated
+        const double cand_cost = bad_r ? DBL_MAX : cost_c;
+        double sn = 0.0;
+        for (int j = 0; j < 7; ++j) sn += (lm->x[j] - lm->cand[j]) * (lm->x[j] - lm->cand[j]);
+        sn = sqrt(sn);
+        if (sn <= 1e-8 * (lm->x_norm + 1e-8)) {
+            lm->done = 1;                                        // parameter tolerance
+        } else if (fabs(lm->cost - cand_cost) <= 1e-6 * lm->cost) {
+            lm->done = 1;                                        // function tolerance
+        } else {
+            const double rel = (lm->cost - cand_cost) / lm->mcc;
+            bool step_ok = false;
+            if (rel > 1e-3) {
+                double xn = 0;
+                for (int j = 0; j < 7; ++j) { lm->x[j] = lm->cand[j]; xn += lm->x[j] * lm->x[j]; }
+                lm->x_norm = sqrt(xn);
+                if (bad_j) {
+                    lm->done = 1;                                // Jacobian evaluation failed
+                } else {
+                    lm->cost = cand_cost;
+                    for (int k = 0; k < 6; ++k) lm->g[k] = tot[1 + k];
+                    for (int k = 0; k < 21; ++k) lm->H[k] = tot[7 + k];
+                    const double f = 1.0 - pow(2.0 * rel - 1.0, 3.0);
+                    lm->radius = lm->radius / fmax(1.0 / 3.0, f);
+                    lm->radius = fmin(1e16, lm->radius);
+                    lm->decrease = 2.0;
+                    lm->reuse = 0;
+                    step_ok = true;
+                    if (lm->cost < lm->min_cost) {
+                        lm->min_cost = lm->cost;
+                        for (int k = 0; k < 7; ++k) lm->best[k] = lm->x[k];
+                    }
+                }
+            } else {
+                lm->radius = lm->radius / lm->decrease;
+                lm->decrease *= 2.0;
+                lm->reuse = 1;
+            }
+            if (!lm->done) {
+                if (lm->iteration >= kMaxIter) lm->done = 1;
+                else if (step_ok && grad_max_norm(lm->x, lm->g) <= 1e-10) lm->done = 1;
+                else if (lm->radius <= 1e-32) lm->done = 1;
+                else lm_next_step(lm, cnt);
+            }
+        }
+    }
+    for (int k = 0; k < 7; ++k) st->params[k] = lm->best[k];
+    if (lm->done) atomicAdd(&cnt[C_LM_ITERS], lm->iteration);
+}
+
+// ---------------------------------- pose / map update ---------------------------------------
+// mode 1: odom = (q2m(q), t) from the solved pose (:278-280); mode 0: keep odom. Writes the pose
+// {m2q(odom.rotation()), odom.translation()} of the node (copy.cpp:105-107).
+__global__ void k_finalize(DevState* __restrict__ st, double* __restrict__ poses, int pose_cap, int mode,
+                           u32* __restrict__ acc) {
+    const int t = threadIdx.x;
+    if (t < 12) acc[A_RG + t] = ((t % 6) < 3) ? 0xFFFFFFFFu : 0u;
+    if (t != 0) return;
+    if (mode == 1) {
+        const qd q{st->params[0], st->params[1], st->params[2], st->params[3]};
+        iso o;
+        o.R = q2m(q);
+        o.t = d3{st->params[4], st->params[5], st->params[6]};
+        store_iso(o, st->odomR, st->odomt);
+    }
+    const iso o = load_iso(st->odomR, st->odomt);
+    const qd q = m2q(o.R);
+    double* P = poses + 7 * (size_t)(st->frame % pose_cap);
+    P[0] = q.x; P[1] = q.y; P[2] = q.z; P[3] = q.w;
+    P[4] = o.t.x; P[5] = o.t.y; P[6] = o.t.z;
+    st->frame++;
+}
+
+__global__ void __launch_bounds__(256) k_map_append(const DevState* __restrict__ st, const int* __restrict__ cnt,
+                                                     const float4* __restrict__ ds_e, const float4* __restrict__ ds_s,
+                                                     float4* __restrict__ app_e, float4* __restrict__ app_s) {
+    const int ne = cnt[C_EDS], ns = cnt[C_SDS];
+    double prm[7];
+    for (int k = 0; k < 7; ++k) prm[k] = st->params[k];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ne + ns; i += gridDim.x * blockDim.x) {
+        if (i < ne) app_e[i] = associate(prm, ds_e[i]);           // :592-597 (r, g carried)
+        else app_s[i - ne] = associate(prm, ds_s[i - ne]);        // :599-604
+    }
+}
+
+struct RgView {
+    const float4 *map_e, *app_e, *map_s, *app_s;
+    int me, ne, ms, ns;
+    __device__ __forceinline__ int total() const { return me + ne + ms + ns; }
+    __device__ __forceinline__ float4 at(int v, int& c) const {
+        if (v < me) { c = 0; return map_e[v]; }
+        v -= me;
+        if (v < ne) { c = 0; return app_e[v]; }
+        v -= ne;
+        if (v < ms) { c = 1; return map_s[v]; }
+        c = 1;
+        return app_s[v - ms];
+    }
+};
+
+__device__ __forceinline__ RgView rg_view(const int* cnt, const float4* map_e, const float4* app_e,
+                                          const float4* map_s, const float4* app_s) {
+    return RgView{map_e, app_e, map_s, app_s, cnt[C_ME], cnt[C_EDS], cnt[C_MS], cnt[C_SDS]};
+}
+
+// CropBox bounds t +- 100 as float, inclusive (:606-615, B.2)
+__device__ __forceinline__ bool in_crop(const DevState* st, float4 p) {
+    const float lox = (float)(st->odomt[0] - 100), loy = (float)(st->odomt[1] - 100), loz = (float)(st->odomt[2] - 100);
+    const float hix = (float)(st->odomt[0] + 100), hiy = (float)(st->odomt[1] + 100), hiz = (float)(st->odomt[2] + 100);
+    return !((p.x < lox || p.y < loy || p.z < loz) || (p.x > hix || p.y > hiy || p.z > hiz));
+}
+
+__global__ void __launch_bounds__(256) k_rg_minmax(const DevState* __restrict__ st, int* __restrict__ cnt,
+                                                    u32* __restrict__ acc, const float4* map_e, const float4* app_e,
+                                                    const float4* map_s, const float4* app_s) {
+    __shared__ float red[4][12];
+    const RgView V = rg_view(cnt, map_e, app_e, map_s, app_s);
+    const int n = V.total();
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[C_NRG] = n;
+    float v[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) v[k] = ((k % 6) < 3) ? FLT_MAX : -FLT_MAX;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        int c;
+        const float4 p = V.at(i, c);
+        if (!in_crop(st, p)) continue;
+        const float xyz[3] = {p.x, p.y, p.z};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (c == 0) { v[k] = fminf(v[k], xyz[k]); v[3 + k] = fmaxf(v[3 + k], xyz[k]); }
+            else { v[6 + k] = fminf(v[6 + k], xyz[k]); v[9 + k] = fmaxf(v[9 + k], xyz[k]); }
+        }
+    }
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const float r = ((k % 6) < 3) ? wave_minf(v[k]) : wave_maxf(v[k]);
+        if (lane_id() == 0) red[w][k] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        const int k = threadIdx.x;
+        float r = red[0][k];
+        for (int ww = 1; ww < 4; ++ww) r = ((k % 6) < 3) ? fminf(r, red[ww][k]) : fmaxf(r, red[ww][k]);
+        const bool any = ((k % 6) < 3) ? (r != FLT_MAX) : (r != -FLT_MAX);
+        if (any) {
+            if ((k % 6) < 3) atomicMin(&acc[A_RG + k], f2ord(r));
+            else atomicMax(&acc[A_RG + k], f2ord(r));
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st, const int* __restrict__ cnt,
+                                                  const u32* __restrict__ acc, const float4* map_e,
+                                                  const float4* app_e, const float4* map_s, const float4* app_s,
+                                                  float leaf0, float leaf1, u32* __restrict__ keys,
+                                                  u32* __restrict__ vals) {
+    const RgView V = rg_view(cnt, map_e, app_e, map_s, app_s);
+    const int n = V.total();
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        int c;
+        const float4 p = V.at(i, c);
+        vals[i] = (u32)i;
+        if (!in_crop(st, p)) { keys[i] = kSentinel; continue; }
+        const float leaf = c == 0 ? leaf0 : leaf1;
+        const u32* a = acc + A_RG + 6 * c;
+        int minb[3], div[3];
+        for (int k = 0; k < 3; ++k) {                                // :46-56 (f32 division)
+            minb[k] = (int)floorf(ord2f(a[k]) / leaf);
+            div[k] = (int)floorf(ord2f(a[3 + k]) / leaf) - minb[k] + 1;
+        }
+        const int i0 = (int)(floorf(p.x / leaf) - (float)minb[0]);  // :63-65
+        const int i1 = (int)(floorf(p.y / leaf) - (float)minb[1]);
+        const int i2 = (int)(floorf(p.z / leaf) - (float)minb[2]);
+        const int idx = i0 * 1 + i1 * div[0] + i2 * (div[0] * div[1]);
+        keys[i] = ((u32)idx & 0x7fffffffu) | ((u32)c << 31);
+    }
+}
+
+struct RgReduceArgs {
+    const int* cnt;
+    const float4 *map_e, *app_e, *map_s, *app_s;
+    const u32* keys;
+    const u32* vals;
+    const u32* segstart;
+    float4* seg_out;
+    u32* keep;
+    int k_new;
+    float theta_p;
+    int theta_max;
+};
+
+__global__ void __launch_bounds__(256) k_rg_reduce(RgReduceArgs a) {
+    const RgView V = rg_view(a.cnt, a.map_e, a.app_e, a.map_s, a.app_s);
+    const int nseg = a.cnt[C_NSEG], nvalid = a.cnt[C_NRG_VALID];
+    for (int sg = blockIdx.x * blockDim.x + threadIdx.x; sg < nseg; sg += gridDim.x * blockDim.x) {
+        const u32 b0 = a.segstart[sg], b1 = (sg + 1 < nseg) ? a.segstart[sg + 1] : (u32)nvalid;
+        float cx = 0.f, cy = 0.f, cz = 0.f;                            // Vector4f centroid (:108-125)
+        int r_max = -1;
+        float g_max = -1;
+        for (u32 k = b0; k < b1; ++k) {
+            int c;
+            const float4 p = V.at((int)a.vals[k], c);
+            cx += p.x; cy += p.y; cz += p.z;
+            const int r = (int)w_r(p);
+            const float g = (float)w_g(p);
+            if (r > r_max) r_max = r;
+            if (g > g_max) g_max = g;
+        }
+        const float nn = (float)(b1 - b0);
+        const u32 r = (u32)r_max & 255u, g = (u32)g_max & 255u;         // stored into uint8 r, g
+        // extractstablepoint (:12-14) on the voxel's uint8 r, g
+        const bool drop = ((float)g < (float)r * a.theta_p) && ((int)r > a.k_new) && ((int)g < a.theta_max + 1);
+        const u32 aged = r > 250 ? 255u : r + 2u;                       // :634-646
+        a.seg_out[sg] = make_float4(cx / nn, cy / nn, cz / nn, __uint_as_float(pack_rg(aged, g)));
+        a.keep[sg] = drop ? 0u : 1u;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const float4* __restrict__ seg_out,
+                                                   const u32* __restrict__ keep, const u32* __restrict__ pos,
+                                                   float4* __restrict__ map_e, float4* __restrict__ map_s) {
+    const int nseg = cnt[C_NSEG], nse = cnt[C_NSEG_E], total = cnt[C_KEEP_TOTAL];
+    const int kept_e = nse < nseg ? (int)pos[nse] : total;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        cnt[C_PAD0] = kept_e;
+        cnt[C_PAD1] = total - kept_e;
+    }
+    for (int sg = blockIdx.x * blockDim.x + threadIdx.x; sg < nseg; sg += gridDim.x * blockDim.x) {
+        if (!keep[sg]) continue;
+        const u32 p = pos[sg];
+        if (sg < nse) map_e[p] = seg_out[sg];
+        else map_s[p - kept_e] = seg_out[sg];
+    }
+}
+
+__global__ void k_map_counts(int* __restrict__ cnt) {
+    if (threadIdx.x == 0) {
+        cnt[C_ME] = cnt[C_PAD0];
+        cnt[C_MS] = cnt[C_PAD1];
+    }
+}
+
+// initMapWithPoints (:217-222): append raw clouds (r = g = 0)
+__global__ void __launch_bounds__(256) k_init_map(const int* __restrict__ cnt, const float4* __restrict__ e,
+                                                   const float4* __restrict__ s, float4* __restrict__ map_e,
+                                                   float4* __restrict__ map_s) {
+    const int n0 = cnt[C_EIN], n1 = cnt[C_SIN], b0 = cnt[C_ME], b1 = cnt[C_MS];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
+        if (i < n0) { const float4 p = e[i]; map_e[b0 + i] = make_float4(p.x, p.y, p.z, __uint_as_float(0u)); }
+        else { const float4 p = s[i - n0]; map_s[b1 + i - n0] = make_float4(p.x, p.y, p.z, __uint_as_float(0u)); }
+    }
+}
+
+__global__ void k_init_counts(int* __restrict__ cnt, DevState* __restrict__ st) {
+    if (threadIdx.x != 0) return;
+    cnt[C_ME] += cnt[C_EIN];
+    cnt[C_MS] += cnt[C_SIN];
+    st->optimization_count = 12;
+}
+
+}  // namespace
+
+// ==============================================================================================
+int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& prm, int device, size_t in_cap,
+                size_t map_cap) {
+    o.lidar = lidar;
+    o.prm = prm;
+    o.device = device;
+    o.in_cap = in_cap;
+    o.map_cap = map_cap;
+    o.sort_cap = 2 * map_cap + 2 * in_cap;
+    if (o.sort_cap < 10 * in_cap) o.sort_cap = 10 * in_cap;
+    o.pose_cap = (size_t)1 << 20;
+    o.leaf_vg[0] = (float)prm.map_res;
+    o.leaf_vg[1] = (float)(prm.map_res * 2);
+    o.leaf_rg[0] = (float)prm.map_res;
+    o.leaf_rg[1] = (float)prm.map_res * 2;
+    if (hipStreamCreateWithFlags(&o.stream, hipStreamNonBlocking) != hipSuccess) return PF_EHIP;
+    int rc = fe_alloc(o.fe, lidar, in_cap);
+    if (rc) return rc;
+    // 1 m cells over both maps' bounding boxes: 2 x (201 m)^2 x 400 m covers the +-100 m crop box
+    rc = grid_alloc(o.grid, 2 * map_cap, (size_t)1 << 25);
+    if (rc) return rc;
+    rc = prim_alloc(o.prim, o.sort_cap > ((size_t)1 << 25) + 2 ? o.sort_cap : ((size_t)1 << 25) + 2);
+    if (rc) return rc;
+    const size_t nq = 2 * in_cap;
+#define PF_ALLOC(ptr, bytes) \
+    if (hipMalloc(&(ptr), (bytes)) != hipSuccess) return PF_ENOMEM;
+    PF_ALLOC(o.st, sizeof(DevState));
+    PF_ALLOC(o.lm, sizeof(LMState));
+    PF_ALLOC(o.cnt, sizeof(int) * C_COUNT);
+    PF_ALLOC(o.acc, sizeof(u32) * A_COUNT);
+    PF_ALLOC(o.in_edge, sizeof(float4) * in_cap);
+    PF_ALLOC(o.in_surf, sizeof(float4) * in_cap);
+    PF_ALLOC(o.ds_edge, sizeof(float4) * in_cap);
+    PF_ALLOC(o.ds_surf, sizeof(float4) * in_cap);
+    PF_ALLOC(o.map_e, sizeof(float4) * map_cap);
+    PF_ALLOC(o.map_s, sizeof(float4) * map_cap);
+    PF_ALLOC(o.app_e, sizeof(float4) * in_cap);
+    PF_ALLOC(o.app_s, sizeof(float4) * in_cap);
+    PF_ALLOC(o.seg_out, sizeof(float4) * o.sort_cap);
+    PF_ALLOC(o.keys, sizeof(u32) * (o.sort_cap + 1));
+    PF_ALLOC(o.vals, sizeof(u32) * (o.sort_cap + 1));
+    PF_ALLOC(o.flags, sizeof(u32) * (o.sort_cap + 1));
+    PF_ALLOC(o.scan_out, sizeof(u32) * (o.sort_cap + 1));
+    PF_ALLOC(o.segstart, sizeof(u32) * (o.sort_cap + 1));
+    PF_ALLOC(o.nbr, sizeof(int) * 5 * nq);
+    PF_ALLOC(o.qflag, sizeof(int) * nq);
+    PF_ALLOC(o.geo, sizeof(double) * 8 * nq);
+    PF_ALLOC(o.spars, sizeof(float) * nq);
+    PF_ALLOC(o.roundv, sizeof(float) * nq);
+    PF_ALLOC(o.observe, sizeof(float) * nq);
+    PF_ALLOC(o.pcnt, sizeof(u32) * 5 * nq);
+    PF_ALLOC(o.tailinc, sizeof(u32) * (o.sort_cap + 1));
+    PF_ALLOC(o.lm_part, sizeof(double) * kLmBlocks * 32);
+    PF_ALLOC(o.poses, sizeof(double) * 7 * o.pose_cap);
+    PF_ALLOC(o.stage, sizeof(float4) * 2 * in_cap);
+#undef PF_ALLOC
+    if (hipHostMalloc(&o.h_cnt, sizeof(int) * C_COUNT) != hipSuccess) return PF_ENOMEM;
+    if (hipHostMalloc(&o.h_pose, sizeof(double) * 8) != hipSuccess) return PF_ENOMEM;
+    // init (:182-208): identity odom / last_odom, parameters {0,0,0,1,0,0,0}, optimization_count 2
+    DevState h{};
+    h.params[3] = 1.0;
+    for (int i = 0; i < 3; ++i) h.odomR[4 * i] = h.lastR[4 * i] = 1.0;
+    h.optimization_count = 2;
+    if (hipMemcpy(o.st, &h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) return PF_EHIP;
+    if (hipMemset(o.cnt, 0, sizeof(int) * C_COUNT) != hipSuccess) return PF_EHIP;
+    if (hipMemset(o.acc, 0, sizeof(u32) * A_COUNT) != hipSuccess) return PF_EHIP;
+    if (hipMemset(o.lm, 0, sizeof(LMState)) != hipSuccess) return PF_EHIP;
+    o.opt_count_host = 2;
+    return PF_OK;
+}
+
+void odom_destroy(OdomGPU& o) {
+    if (o.graph) (void)hipGraphExecDestroy(o.graph);
+    fe_free(o.fe);
+    grid_free(o.grid);
+    prim_free(o.prim);
+    void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.in_edge, o.in_surf, o.ds_edge, o.ds_surf, o.map_e, o.map_s,
+                    o.app_e, o.app_s, o.seg_out, o.keys, o.vals, o.flags, o.scan_out, o.segstart, o.nbr,
+                    o.qflag, o.geo, o.spars, o.roundv, o.observe, o.pcnt, o.tailinc, o.lm_part, o.poses, o.stage};
+    for (void* p : ptrs) (void)hipFree(p);
+    if (o.h_cnt) (void)hipHostFree(o.h_cnt);
+    if (o.h_pose) (void)hipHostFree(o.h_pose);
+    if (o.stream) (void)hipStreamDestroy(o.stream);
+    o = OdomGPU{};
+}
+
+void odom_enqueue_init(OdomGPU& o, hipStream_t s) {
+    hipLaunchKernelGGL(k_init_map, dim3(kGrid), dim3(256), 0, s, o.cnt, o.in_edge, o.in_surf, o.map_e, o.map_s);
+    hipLaunchKernelGGL(k_init_counts, dim3(1), dim3(64), 0, s, o.cnt, o.st);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, o.st, o.poses, (int)o.pose_cap, 0, o.acc);
+    o.opt_count_host = 12;
+    o.inited = true;
+}
+
+void odom_enqueue_update(OdomGPU& o, hipStream_t s) {
+    if (o.opt_count_host > 2) o.opt_count_host--;
+    int* cnt = o.cnt;
+    hipLaunchKernelGGL(k_predict, dim3(1), dim3(64), 0, s, o.st, cnt, o.acc);
+    // VoxelGrid of both inputs (:242-245)
+    hipLaunchKernelGGL(k_vg_minmax, dim3(128), dim3(256), 0, s, o.in_edge, o.in_surf, cnt, o.acc);
+    hipLaunchKernelGGL(k_vg_keys, dim3(kGrid), dim3(256), 0, s, o.in_edge, o.in_surf, cnt, o.acc, o.leaf_vg[0],
+                       o.leaf_vg[1], o.keys, o.vals);
+    radix_sort_pairs(o.keys, o.vals, cnt + C_VGN, 32, o.prim, s);
+    hipLaunchKernelGGL(k_seg_heads, dim3(kGrid), dim3(256), 0, s, o.keys, cnt + C_VGN, o.flags);
+    scan_exclusive(o.flags, o.scan_out, cnt + C_VGN, (u32*)(cnt + C_NSEG), o.prim, s);
+    hipLaunchKernelGGL(k_seg_starts, dim3(kGrid), dim3(256), 0, s, o.keys, cnt + C_VGN, o.flags, o.scan_out,
+                       o.segstart, cnt);
+    hipLaunchKernelGGL(k_vg_reduce, dim3(kGrid), dim3(256), 0, s, o.in_edge, o.in_surf, o.keys, o.vals, o.segstart,
+                       cnt, o.ds_edge, o.ds_surf);
+    // grids of the edge / surf maps (kd-tree build, :249-250)
+    grid_build(o.grid, o.map_e, cnt + C_ME, o.map_s, cnt + C_MS, o.prim, s);
+    const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
+    for (int it = 0; it < o.opt_count_host; ++it) {
+        AssocArgs aa{o.st, cnt, o.acc, gv, o.ds_edge, o.ds_surf, o.map_e, o.map_s, o.nbr, o.qflag, o.geo, o.spars,
+                     o.roundv, o.keys, o.vals, (u32)o.map_cap};
+        hipLaunchKernelGGL(k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
+        radix_sort_pairs(o.keys, o.vals, cnt + C_NPAIR, 32, o.prim, s);
+        hipLaunchKernelGGL(k_pidx_count, dim3(kGrid), dim3(256), 0, s, o.keys, o.vals, cnt, o.pcnt, o.tailinc);
+        ObsArgs oa{cnt, o.acc, o.map_e, o.map_s, o.ds_edge, o.ds_surf, o.nbr, o.qflag, o.pcnt, o.roundv, o.spars,
+                   o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
+        hipLaunchKernelGGL(k_observe, dim3(kGrid), dim3(256), 0, s, oa);
+        hipLaunchKernelGGL(k_pidx_apply, dim3(kGrid), dim3(256), 0, s, o.keys, o.tailinc, cnt, o.map_e, o.map_s,
+                           (u32)o.map_cap);
+        hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, s, o.st, cnt, o.acc, o.lm);
+        EvalArgs ea{o.lm, cnt, o.qflag, o.ds_edge, o.ds_surf, o.geo, o.observe, o.spars, o.lm_part,
+                    o.prm.weight_type};
+        for (int e = 0; e < 5; ++e) {
+            hipLaunchKernelGGL(k_lm_eval, dim3(kLmBlocks), dim3(256), 0, s, ea);
+            hipLaunchKernelGGL(k_lm_step, dim3(1), dim3(256), 0, s, o.lm, o.lm_part, o.st, cnt);
+        }
+    }
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, o.st, o.poses, (int)o.pose_cap, 1, o.acc);
+    // addPointsToMap (:589-647)
+    hipLaunchKernelGGL(k_map_append, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.ds_edge, o.ds_surf, o.app_e, o.app_s);
+    hipLaunchKernelGGL(k_rg_minmax, dim3(128), dim3(256), 0, s, o.st, cnt, o.acc, o.map_e, o.app_e, o.map_s, o.app_s);
+    hipLaunchKernelGGL(k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, o.map_e, o.app_e, o.map_s, o.app_s,
+                       o.leaf_rg[0], o.leaf_rg[1], o.keys, o.vals);
+    radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s);
+    hipLaunchKernelGGL(k_seg_heads, dim3(kGrid), dim3(256), 0, s, o.keys, cnt + C_NRG, o.flags);
+    scan_exclusive(o.flags, o.scan_out, cnt + C_NRG, (u32*)(cnt + C_NSEG), o.prim, s);
+    hipLaunchKernelGGL(k_seg_starts, dim3(kGrid), dim3(256), 0, s, o.keys, cnt + C_NRG, o.flags, o.scan_out,
+                       o.segstart, cnt);
+    RgReduceArgs ra{cnt, o.map_e, o.app_e, o.map_s, o.app_s, o.keys, o.vals, o.segstart, o.seg_out, o.flags,
+                    o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
+    hipLaunchKernelGGL(k_rg_reduce, dim3(kGrid), dim3(256), 0, s, ra);
+    scan_exclusive(o.flags, o.scan_out, cnt + C_NSEG, (u32*)(cnt + C_KEEP_TOTAL), o.prim, s);
+    hipLaunchKernelGGL(k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, o.flags, o.scan_out, o.map_e,
+                       o.map_s);
+    hipLaunchKernelGGL(k_map_counts, dim3(1), dim3(64), 0, s, cnt);
+}
+
+void odom_enqueue_frame(OdomGPU& o, const float4* d_in, hipStream_t s) {
+    fe_enqueue(o.fe, d_in, o.cnt + C_NIN, o.in_edge, o.cnt + C_EIN, o.in_surf, o.cnt + C_SIN, s);
+    if (!o.inited) odom_enqueue_init(o, s);
+    else odom_enqueue_update(o, s);
+}
+
+}  // namespace pf

@@ -1,0 +1,333 @@
+"""ctypes binding of libpfilter_hip.so (include/pfilter_hip.h) for tests and bench.py.
+
+Mirrors the reference classes used on the hot path, same method names and argument meaning:
+  LaserProcessingClass.init / featureExtraction          include/laserProcessingClass.h:36-37
+  Odom_ES_EstimationClass.init / initMapWithPoints /
+      updatePointsToMap / getMap, members odom,
+      laserCloudCornerMap, laserCloudSurfMap              include/odomEstimationClass.h:140-152
+Point clouds are numpy float32 arrays [n, 4] (x, y, z, intensity).
+
+There is no CPU fallback: if the HIP library is missing or fails to load, this module raises.
+If PyTorch is also used in the process, import torch BEFORE this module so that one HIP runtime
+(torch's, same SONAME) serves both.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpfilter_hip.so")
+
+PF_OK = 0
+PF_W_MAP_TOO_SMALL = 1
+PF_W_FEW_CORRESPONDENCES = 2
+PF_EINVAL = -1
+PF_EHIP = -2
+PF_ENOMEM = -3
+PF_ECAPACITY = -4
+PF_EUNSUPPORTED = -5
+
+
+class PFError(RuntimeError):
+    def __init__(self, fn, code):
+        super().__init__("%s failed with status %d" % (fn, code))
+        self.code = code
+
+
+def build():
+    """Compile libpfilter_hip.so for gfx950 (hipcc cross-compiles without a GPU)."""
+    subprocess.check_call(["make", "-s", "-j8", "-C", _HERE])
+    return LIB_PATH
+
+
+class LidarParams(ctypes.Structure):
+    _fields_ = [("num_lines", ctypes.c_int), ("min_dist", ctypes.c_double), ("max_dist", ctypes.c_double),
+                ("scan_period", ctypes.c_double)]
+
+
+class OdomParams(ctypes.Structure):
+    _fields_ = [("map_res", ctypes.c_double), ("k_new", ctypes.c_int), ("theta_p", ctypes.c_float),
+                ("theta_max", ctypes.c_int), ("weight_type", ctypes.c_int)]
+
+
+class OdomStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in ("n_edge_in", "n_surf_in", "n_edge_ds", "n_surf_ds", "n_edge_map",
+                                              "n_surf_map", "n_edge_res", "n_surf_res", "n_edge_valid",
+                                              "n_surf_valid")] + \
+               [(n, ctypes.c_int32) for n in ("outer_iterations", "lm_iterations", "map_too_small", "status")]
+
+    def as_dict(self):
+        return {f[0]: getattr(self, f[0]) for f in self._fields_}
+
+
+EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "pf_odom_destroy",
+           "pf_odom_init_map", "pf_odom_update", "pf_odom_get_pose", "pf_odom_get_map", "pf_odom_set_map",
+           "pf_odom_get_stats", "pf_odom_frame_device", "pf_odom_frame_host", "pf_odom_sync", "pf_odom_poses",
+           "pf_odom_set_graph", "pf_device_count", "pf_dev_malloc", "pf_dev_free", "pf_memcpy_h2d",
+           "pf_memcpy_d2h", "pf_knn_create", "pf_knn_destroy", "pf_knn_set_map", "pf_knn_query", "pf_knn_bench"]
+
+_lib = None
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_i = ctypes.c_int
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError("libpfilter_hip.so not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    L.pf_fe_create.argtypes = [ctypes.POINTER(LidarParams), _i, _sz, ctypes.POINTER(_vp)]
+    L.pf_fe_destroy.argtypes = [_vp]
+    L.pf_fe_extract.argtypes = [_vp, _vp, _sz, _sz, _vp, ctypes.POINTER(_sz), _vp, ctypes.POINTER(_sz), _sz]
+    L.pf_odom_create.argtypes = [ctypes.POINTER(LidarParams), ctypes.POINTER(OdomParams), _i, _sz, _sz,
+                                 ctypes.POINTER(_vp)]
+    L.pf_odom_destroy.argtypes = [_vp]
+    L.pf_odom_init_map.argtypes = [_vp, _vp, _sz, _sz, _vp, _sz, _sz]
+    L.pf_odom_update.argtypes = [_vp, _vp, _sz, _sz, _vp, _sz, _sz, _vp]
+    L.pf_odom_get_pose.argtypes = [_vp, _vp]
+    L.pf_odom_get_map.argtypes = [_vp, _i, _vp, _vp, _sz, ctypes.POINTER(_sz)]
+    L.pf_odom_set_map.argtypes = [_vp, _i, _vp, _vp, _sz]
+    L.pf_odom_get_stats.argtypes = [_vp, ctypes.POINTER(OdomStats)]
+    L.pf_odom_frame_device.argtypes = [_vp, _vp, _sz, _vp]
+    L.pf_odom_frame_host.argtypes = [_vp, _vp, _sz, _sz, _vp]
+    L.pf_odom_sync.argtypes = [_vp]
+    L.pf_odom_poses.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
+    L.pf_odom_set_graph.argtypes = [_vp, _i]
+    L.pf_device_count.argtypes = [ctypes.POINTER(_i)]
+    L.pf_dev_malloc.argtypes = [_i, _sz, ctypes.POINTER(_vp)]
+    L.pf_dev_free.argtypes = [_i, _vp]
+    L.pf_memcpy_h2d.argtypes = [_i, _vp, _vp, _sz]
+    L.pf_memcpy_d2h.argtypes = [_i, _vp, _vp, _sz]
+    L.pf_knn_create.argtypes = [_i, _sz, _sz, ctypes.POINTER(_vp)]
+    L.pf_knn_destroy.argtypes = [_vp]
+    L.pf_knn_set_map.argtypes = [_vp, _vp, _sz]
+    L.pf_knn_query.argtypes = [_vp, _vp, _sz, _vp, _vp]
+    L.pf_knn_bench.argtypes = [_vp, _i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    _lib = L
+    return L
+
+
+def _check(fn, rc, allow_warn=True):
+    if rc < 0 or (rc > 0 and not allow_warn):
+        raise PFError(fn, rc)
+    return rc
+
+
+def _f32x4(a):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if a.ndim != 2 or a.shape[1] != 4:
+        raise ValueError("expected an [n, 4] float32 array")
+    return a
+
+
+def make_lidar(num_lines=64, min_dist=3.0, max_dist=90.0, scan_period=0.1):
+    return LidarParams(int(num_lines), float(min_dist), float(max_dist), float(scan_period))
+
+
+def device_count():
+    n = _i()
+    _check("pf_device_count", lib().pf_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class DeviceBuffer:
+    """Raw HBM allocation (scans staged once, read by the device pipeline)."""
+
+    def __init__(self, nbytes, device=0):
+        self.device, self.nbytes = device, int(nbytes)
+        p = _vp()
+        _check("pf_dev_malloc", lib().pf_dev_malloc(device, self.nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+
+    def upload(self, arr, offset=0):
+        a = np.ascontiguousarray(arr)
+        assert offset + a.nbytes <= self.nbytes
+        _check("pf_memcpy_h2d", lib().pf_memcpy_h2d(self.device, self.ptr + offset, a.ctypes.data, a.nbytes))
+
+    def download(self, arr, offset=0):
+        _check("pf_memcpy_d2h", lib().pf_memcpy_d2h(self.device, arr.ctypes.data, self.ptr + offset, arr.nbytes))
+        return arr
+
+    def free(self):
+        if self.ptr:
+            lib().pf_dev_free(self.device, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class LaserProcessingClass:
+    """Drop-in for LaserProcessingClass (featureExtraction on the GPU)."""
+
+    def __init__(self, device=0, max_points=300000):
+        self.device, self.max_points = device, max_points
+        self._h = None
+
+    def init(self, lidar_param):
+        h = _vp()
+        _check("pf_fe_create", lib().pf_fe_create(ctypes.byref(lidar_param), self.device, self.max_points,
+                                                  ctypes.byref(h)))
+        self._h = h.value
+        self._rings = lidar_param.num_lines
+
+    def featureExtraction(self, pc_in):
+        x = _f32x4(pc_in)
+        n = x.shape[0]
+        cap = max(n, 1)
+        edge = np.empty((cap, 4), np.float32)
+        surf = np.empty((cap, 4), np.float32)
+        ne, ns = _sz(), _sz()
+        _check("pf_fe_extract", lib().pf_fe_extract(self._h, x.ctypes.data, n, 16, edge.ctypes.data,
+                                                    ctypes.byref(ne), surf.ctypes.data, ctypes.byref(ns), cap))
+        return edge[:ne.value].copy(), surf[:ns.value].copy()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().pf_fe_destroy(self._h)
+            self._h = None
+
+
+class Odom_ES_EstimationClass:
+    """Drop-in for Odom_ES_EstimationClass (the whole update on the GPU)."""
+
+    def __init__(self, device=0, max_points=300000, map_capacity=1 << 22):
+        self.device, self.max_points, self.map_capacity = device, max_points, map_capacity
+        self._h = None
+        self.last_status = PF_OK
+
+    def init(self, lidar_param, map_resolution, k_new, theta_p, theta_max, weightType):
+        self.lidar = lidar_param
+        prm = OdomParams(float(map_resolution), int(k_new), float(theta_p), int(theta_max), int(weightType))
+        h = _vp()
+        _check("pf_odom_create", lib().pf_odom_create(ctypes.byref(lidar_param), ctypes.byref(prm), self.device,
+                                                      self.max_points, self.map_capacity, ctypes.byref(h)))
+        self._h = h.value
+
+    def initMapWithPoints(self, edge_in, surf_in):
+        e, s = _f32x4(edge_in), _f32x4(surf_in)
+        _check("pf_odom_init_map", lib().pf_odom_init_map(self._h, e.ctypes.data, e.shape[0], 16, s.ctypes.data,
+                                                          s.shape[0], 16))
+
+    def updatePointsToMap(self, edge_in, surf_in):
+        e, s = _f32x4(edge_in), _f32x4(surf_in)
+        pose = np.empty(7)
+        self.last_status = _check("pf_odom_update", lib().pf_odom_update(
+            self._h, e.ctypes.data, e.shape[0], 16, s.ctypes.data, s.shape[0], 16, pose.ctypes.data))
+        return pose
+
+    @property
+    def odom(self):
+        """pose {qx, qy, qz, qw, tx, ty, tz} of the member `odom`"""
+        p = np.empty(7)
+        _check("pf_odom_get_pose", lib().pf_odom_get_pose(self._h, p.ctypes.data))
+        return p
+
+    def _map(self, which):
+        n = _sz()
+        _check("pf_odom_get_map", lib().pf_odom_get_map(self._h, which, None, None, 0, ctypes.byref(n)))
+        xyz = np.empty((max(n.value, 1), 3), np.float32)
+        rg = np.empty((max(n.value, 1), 2), np.uint8)
+        _check("pf_odom_get_map", lib().pf_odom_get_map(self._h, which, xyz.ctypes.data, rg.ctypes.data, n.value,
+                                                        ctypes.byref(n)))
+        return xyz[:n.value].copy(), rg[:n.value].copy()
+
+    @property
+    def laserCloudCornerMap(self):
+        return self._map(0)
+
+    @property
+    def laserCloudSurfMap(self):
+        return self._map(1)
+
+    def getMap(self):
+        """surf map then corner map, appended (src/odomEstimationClass.cpp:210-215)"""
+        s, c = self._map(1), self._map(0)
+        return np.concatenate([s[0], c[0]]), np.concatenate([s[1], c[1]])
+
+    def set_map(self, which, xyz, rg):
+        xyz = np.ascontiguousarray(xyz, np.float32)
+        rg = np.ascontiguousarray(rg, np.uint8)
+        _check("pf_odom_set_map", lib().pf_odom_set_map(self._h, which, xyz.ctypes.data, rg.ctypes.data,
+                                                        xyz.shape[0]))
+
+    def stats(self):
+        s = OdomStats()
+        _check("pf_odom_get_stats", lib().pf_odom_get_stats(self._h, ctypes.byref(s)))
+        return s.as_dict()
+
+    # ---- whole-frame pipeline (featureExtraction -> init / update, all on the device) ----
+    def frame_host(self, xyzi, want_pose=True):
+        x = _f32x4(xyzi)
+        pose = np.empty(7)
+        _check("pf_odom_frame_host", lib().pf_odom_frame_host(self._h, x.ctypes.data, x.shape[0], 16,
+                                                              pose.ctypes.data if want_pose else None))
+        return pose if want_pose else None
+
+    def frame_device(self, dptr, n, want_pose=False):
+        pose = np.empty(7)
+        _check("pf_odom_frame_device", lib().pf_odom_frame_device(self._h, dptr, int(n),
+                                                                  pose.ctypes.data if want_pose else None))
+        return pose if want_pose else None
+
+    def sync(self):
+        _check("pf_odom_sync", lib().pf_odom_sync(self._h))
+
+    def poses(self):
+        n = _sz()
+        _check("pf_odom_poses", lib().pf_odom_poses(self._h, None, 0, ctypes.byref(n)))
+        out = np.empty((max(n.value, 1), 7))
+        _check("pf_odom_poses", lib().pf_odom_poses(self._h, out.ctypes.data, n.value, ctypes.byref(n)))
+        return out[:n.value].copy()
+
+    def set_graph(self, enable):
+        _check("pf_odom_set_graph", lib().pf_odom_set_graph(self._h, int(bool(enable))))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().pf_odom_destroy(self._h)
+            self._h = None
+
+
+# the node-facing alias named by the north star
+OdomEstimationClass = Odom_ES_EstimationClass
+
+
+class Knn:
+    """Exact radius-gated 5-NN (the roofline kernel) on a resident map."""
+
+    def __init__(self, map_capacity, query_capacity, device=0):
+        h = _vp()
+        _check("pf_knn_create", lib().pf_knn_create(device, int(map_capacity), int(query_capacity),
+                                                    ctypes.byref(h)))
+        self._h = h.value
+
+    def set_map(self, xyz4):
+        m = _f32x4(xyz4)
+        _check("pf_knn_set_map", lib().pf_knn_set_map(self._h, m.ctypes.data, m.shape[0]), allow_warn=False)
+
+    def query(self, q4):
+        q = _f32x4(q4)
+        idx = np.empty((q.shape[0], 5), np.int32)
+        d2 = np.empty((q.shape[0], 5), np.float32)
+        _check("pf_knn_query", lib().pf_knn_query(self._h, q.ctypes.data, q.shape[0], idx.ctypes.data,
+                                                  d2.ctypes.data))
+        return idx, d2
+
+    def bench(self, iters=20):
+        ms, b = ctypes.c_double(), ctypes.c_double()
+        _check("pf_knn_bench", lib().pf_knn_bench(self._h, int(iters), ctypes.byref(ms), ctypes.byref(b)))
+        return ms.value, b.value
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().pf_knn_destroy(self._h)
+            self._h = None
