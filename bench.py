@@ -1,0 +1,247 @@
+"""Benchmark: LiDAR frames/sec (scan -> pose) on a KITTI-00-like 64-line sequence, MI355X.
+
+A "step" is one frame of the hot path: featureExtraction + updatePointsToMap (the reference's timed
+boundary, src/laserProcessingNode.cpp:71-78 + src/odomEstimationNode copy.cpp:92-100). Workload =
+BASELINE.json configs[1]: 64 lines, min_dis 3 / max_dis 90, k_new=0 theta_p=0.4 theta_max=75,
+weightType 0, map_resolution 0.4, on the synthetic S64 sequence (ray-cast urban scene, KITTI-00
+length 4541 frames; no network for KITTI itself, real .bin scans are used when PF_KITTI_ROOT is set).
+All scans are resident in HBM before the timed region. Per-frame poses stay on the device.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+N > 1: one process per GPU (torch.distributed.run), one independent sequence per rank (weak
+scaling); RCCL all-gather of the per-rank pose arrays after the timed region.
+
+Extra legs (rank 0, N=1 only, outside the timed region):
+  roofline     exact 5-NN kernel on config 5 (2M-point map, 200k queries) timed with HIP events on
+               its own stream; achieved = algorithmic bytes / avg kernel time
+  cpu_baseline the pfref oracle (single thread, reference-faithful options) on a bounded sample of
+               the same frames
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "pfilter-noetic_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, os.path.join(PKG, "synth"))
+
+METRIC = "LiDAR frames/sec (scan→pose) on KITTI-00 64-line; kNN HBM GB/s vs roofline"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+KITTI00_FRAMES = 4541
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=KITTI00_FRAMES - 20)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-roofline", action="store_true", help="skip the kNN roofline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-graph", action="store_true")
+    return ap.parse_args()
+
+
+def lidar_cfg():
+    import pfilter_amd as pa
+    return pa.make_lidar(64, 3.0, 90.0, 0.1)
+
+
+ODOM_CFG = dict(map_resolution=0.4, k_new=0, theta_p=0.4, theta_max=75, weightType=0)
+
+
+def load_frames(rank, total, threads):
+    """Yields (frame_index, [nf,cap,4] chunk, counts) for the rank's sequence."""
+    import pfsynth
+    kroot = os.environ.get("PF_KITTI_ROOT")
+    if kroot:
+        seqdir = os.path.join(kroot, "sequences", "%02d" % rank, "velodyne")
+        files = sorted(f for f in os.listdir(seqdir) if f.endswith(".bin"))[:total]
+        frames = [np.fromfile(os.path.join(seqdir, f), np.float32).reshape(-1, 4) for f in files]
+        cap = max(f.shape[0] for f in frames)
+        buf = np.zeros((len(frames), cap, 4), np.float32)
+        counts = np.zeros(len(frames), np.int64)
+        for i, f in enumerate(frames):
+            buf[i, :f.shape[0]] = f
+            counts[i] = f.shape[0]
+        yield 0, buf, counts, "kitti-%02d" % rank
+        return
+    seq = pfsynth.Sequence("S64", n_frames=total, seed=rank)
+    chunk = 256
+    for f0 in range(0, total, chunk):
+        nf = min(chunk, total - f0)
+        buf, counts = seq.frames(f0, nf, threads=threads)
+        yield f0, buf, counts, "synthetic S64 seed %d" % rank
+
+
+def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier):
+    import pfilter_amd as pa
+    total = warmup + steps
+    lid = lidar_cfg()
+    od = pa.Odom_ES_EstimationClass(device=local_rank, max_points=300000, map_capacity=1 << 22)
+    od.init(lid, **ODOM_CFG)
+    od.set_graph(use_graph)
+    # stage every scan in HBM (untimed)
+    bufs, ptrs = [], []
+    data_desc = None
+    npts = []
+    for f0, buf, counts, desc in load_frames(rank, total, threads):
+        data_desc = desc
+        db = pa.DeviceBuffer(buf.nbytes, device=local_rank)
+        db.upload(buf)
+        stride = buf.shape[1] * 16
+        for i in range(buf.shape[0]):
+            ptrs.append((db.ptr + i * stride, int(counts[i])))
+            npts.append(int(counts[i]))
+        bufs.append(db)
+    for k in range(min(warmup, len(ptrs))):
+        od.frame_device(*ptrs[k])
+    od.sync()
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(warmup, len(ptrs)):
+        od.frame_device(*ptrs[k])
+    od.sync()
+    barrier()
+    t1 = time.perf_counter()
+    poses = od.poses()
+    stats = od.stats()
+    nframes = len(ptrs) - warmup
+    return dict(elapsed=t1 - t0, frames=nframes, poses=poses, stats=stats, data=data_desc,
+                mean_points=float(np.mean(npts)) if npts else 0.0, od=od, bufs=bufs, ptrs=ptrs)
+
+
+def knn_roofline(device=0, nmap=2_000_000, nq=200_000, iters=50):
+    """Config 5: exact 5-NN of 200k jittered queries against a 2M-point dense map."""
+    import pfilter_amd as pa
+    import pfsynth
+    mp = pfsynth.dense_map(nmap, seed=5)
+    q = pfsynth.dense_queries(mp, nq, sigma=0.3, seed=6)
+    kn = pa.Knn(nmap, nq, device=device)
+    kn.set_map(mp)
+    idx, d2 = kn.query(q)
+    ms, alg = kn.bench(iters)
+    achieved = alg / (ms * 1e-3) / 1e9
+    found = int((idx[:, 4] >= 0).sum())
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "knn_pmc_r01.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "k_knn_query (exact radius-gated 5-NN, 1 m cell grid)",
+            "workload": "config 5: map %d pts, %d queries, %d with 5 neighbours" % (nmap, nq, found),
+            "alg_bytes_per_launch": alg, "avg_kernel_ms": round(ms, 5)}
+
+
+def cpu_baseline(budget_s, warmup):
+    """pfref oracle, single thread, reference-faithful options (kd-tree, dense-QR LM, std::sort)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pfref
+    import pfsynth
+    seq = pfsynth.Sequence("S64", n_frames=warmup + 2000, seed=0)
+    orc = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=0)
+    for k in range(warmup):
+        orc.frame(seq.frame(k))
+    n, el, k = 0, 0.0, warmup
+    while el < budget_s and n < 2000:
+        x = seq.frame(k)
+        t = time.perf_counter()
+        orc.frame(x)
+        el += time.perf_counter() - t
+        n += 1
+        k += 1
+    return {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": "pfref (oracle/, reference-faithful opts=0) frames %d..%d of the same S64 seed-0 sequence "
+                      "after %d warm-up frames, single thread, %.1f s of CPU time" % (warmup, k - 1, warmup, el)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch  # noqa: F401  (loaded before the HIP library: one HIP runtime per process)
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", init_method="env://")
+        dist = tdist
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+    r = run_gpu(rank, local_rank, world, args.steps, args.warmup, threads, not args.no_graph, barrier)
+    elapsed, frames = r["elapsed"], r["frames"]
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        f = torch.tensor([frames], dtype=torch.int64, device="cuda")
+        dist.all_reduce(f, op=dist.ReduceOp.SUM)
+        total_frames = int(f.item())
+        # the one collective of the design: gather every rank's pose array over RCCL
+        p = torch.from_numpy(np.ascontiguousarray(r["poses"][-frames:])).cuda()
+        gathered = [torch.empty_like(p) for _ in range(world)]
+        dist.all_gather(gathered, p)
+    else:
+        total_frames = frames
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    value = total_frames / elapsed
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / max(1, frames) * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32/f64",
+        "data": "synthetic" if not os.environ.get("PF_KITTI_ROOT") else "kitti",
+        "config": {"workload": "KITTI-00 64-line (configs[1]): S64 synthetic scans, k_new=0 theta_p=0.4 "
+                               "theta_max=75, weightType 0, map_res 0.4, min/max dis 3/90",
+                   "sequence": r["data"], "frames_per_rank": frames,
+                   "mean_points_per_frame": round(r["mean_points"], 1),
+                   "parallelism": "one independent sequence per GPU" if world > 1 else "single sequence",
+                   "graph": not args.no_graph},
+    }
+    log("pipeline: %d frames in %.3f s, last-frame stats %s" % (frames, elapsed, r["stats"]))
+    if world == 1 and not args.no_roofline:
+        try:
+            out["roofline"] = knn_roofline(local_rank)
+        except Exception as e:  # report, never hide
+            log("roofline leg failed: %r" % (e,))
+            out["roofline"] = None
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.warmup)
+        out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

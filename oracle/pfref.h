@@ -94,6 +94,8 @@ void pfref_eigen_sym3(const double a[6], double evals[3], double evecs[9] /* col
 void pfref_plane_fit(const double A[15], double n_out[3]);
 /* PoseSE3Parameterization::Plus */
 void pfref_se3_plus(const double x[7], const double delta[6], double out[7]);
+/* Eigen 3.3 Isometry3d::rotation(): orthogonal polar factor of a 3x3 (row-major in/out) */
+void pfref_rotation_polar(const double m[9], double out[9]);
 /* Edge/SurfNormAnalyticCostFunction::Evaluate: returns residual, J[7] */
 double pfref_edge_eval(const double x[7], const double cur[3], const double a[3], const double b[3],
                        double weight, double J[7]);
@@ -114,6 +116,9 @@ void pfref_odom_get_pose(const pfref_odom* h, double pose[7]);
 int pfref_odom_get_map(const pfref_odom* h, int which, float* xyz, uint8_t* rg, size_t cap, size_t* n);
 int pfref_odom_set_map(pfref_odom* h, int which, const float* xyz, const uint8_t* rg, size_t n);
 void pfref_odom_get_stats(const pfref_odom* h, pfref_stats* s);
+/* set odom / last_odom (poses {qx,qy,qz,qw,tx,ty,tz}) e.g. to replay a fixture from a given state */
+void pfref_odom_set_state(pfref_odom* h, const double odom_pose[7], const double last_pose[7]);
+void pfref_odom_set_opt_count(pfref_odom* h, int n);
 
 /* --- whole frame: featureExtraction then initMapWithPoints (first call) / updatePointsToMap */
 int pfref_odom_frame(pfref_odom* h, const pfref_lidar* lidar, const float* xyzi, size_t n,

@@ -68,6 +68,7 @@ def lib():
         L.pfref_eigen_sym3.argtypes = [_vp, _vp, _vp]
         L.pfref_plane_fit.argtypes = [_vp, _vp]
         L.pfref_se3_plus.argtypes = [_vp, _vp, _vp]
+        L.pfref_rotation_polar.argtypes = [_vp, _vp]
         L.pfref_edge_eval.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_double, _vp]
         L.pfref_edge_eval.restype = ctypes.c_double
         L.pfref_surf_eval.argtypes = [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _vp]
@@ -82,6 +83,8 @@ def lib():
         L.pfref_odom_set_map.argtypes = [_vp, ctypes.c_int, _vp, _vp, _sz]
         L.pfref_odom_get_stats.argtypes = [_vp, ctypes.POINTER(Stats)]
         L.pfref_odom_frame.argtypes = [_vp, ctypes.POINTER(Lidar), _vp, _sz, _vp]
+        L.pfref_odom_set_state.argtypes = [_vp, _vp, _vp]
+        L.pfref_odom_set_opt_count.argtypes = [_vp, ctypes.c_int]
     return _lib
 
 
@@ -175,6 +178,13 @@ def se3_plus(x, delta):
     return out
 
 
+def rotation_polar(m):
+    m = np.ascontiguousarray(m, np.float64).reshape(3, 3)
+    out = np.empty((3, 3))
+    lib().pfref_rotation_polar(m.ctypes.data, out.ctypes.data)
+    return out
+
+
 def edge_eval(x, cur, a, b, w=0.0):
     J = np.empty(7)
     arr = [np.ascontiguousarray(v, np.float64) for v in (x, cur, a, b)]
@@ -244,6 +254,14 @@ class Odom:
         xyz = np.ascontiguousarray(xyz, np.float32)
         rg = np.ascontiguousarray(rg, np.uint8)
         lib().pfref_odom_set_map(self._h, int(which), xyz.ctypes.data, rg.ctypes.data, xyz.shape[0])
+
+    def set_state(self, odom_pose, last_pose=None):
+        a = np.ascontiguousarray(odom_pose, np.float64)
+        b = np.ascontiguousarray(odom_pose if last_pose is None else last_pose, np.float64)
+        lib().pfref_odom_set_state(self._h, a.ctypes.data, b.ctypes.data)
+
+    def set_opt_count(self, n):
+        lib().pfref_odom_set_opt_count(self._h, int(n))
 
     def stats(self):
         s = Stats()

@@ -99,6 +99,122 @@ inline Quat m2q(const M3& a) {
     return {c[0], c[1], c[2], c[3]};
 }
 
+// Eigen 3.3 Transform::rotation(): computeRotationScaling() -> JacobiSVD<Matrix3d>(FullU|FullV),
+// rotation = U' V^T with U'.col(0) /= det(U V^T) (Eigen/src/Geometry/Transform.h, 3.3.7; the
+// Isometry shortcut returning linear() only appeared in Eigen 3.4). Restated step by step from
+// JacobiSVD::compute, real_2x2_jacobi_svd and JacobiRotation::makeJacobi.
+struct JRot { double c, s; };
+inline void jrot_pair(double& x, double& y, const JRot& j) {   // apply_rotation_in_the_plane
+    const double xi = x, yi = y;
+    x = j.c * xi + j.s * yi;
+    y = -j.s * xi + j.c * yi;
+}
+inline JRot jrot_transpose(const JRot& j) { return {j.c, -j.s}; }
+inline JRot jrot_product(const JRot& a, const JRot& b) { return {a.c * b.c - a.s * b.s, a.c * b.s + a.s * b.c}; }
+inline JRot jrot_make_jacobi(double x, double y, double z) {
+    const double deno = 2.0 * std::fabs(y);
+    if (deno < std::numeric_limits<double>::min()) return {1.0, 0.0};
+    const double tau = (x - z) / deno;
+    const double w = std::sqrt(tau * tau + 1.0);
+    double t;
+    if (tau > 0.0) t = 1.0 / (tau + w);
+    else t = 1.0 / (tau - w);
+    const double sign_t = t > 0.0 ? 1.0 : -1.0;
+    const double n = 1.0 / std::sqrt(t * t + 1.0);
+    return {n, -sign_t * (y / std::fabs(y)) * std::fabs(t) * n};
+}
+inline void left_rot(double A[3][3], int p, int q, const JRot& j) {     // A.applyOnTheLeft(p,q,j)
+    if (j.c == 1.0 && j.s == 0.0) return;
+    for (int k = 0; k < 3; ++k) jrot_pair(A[p][k], A[q][k], j);
+}
+inline void right_rot(double A[3][3], int p, int q, const JRot& j) {    // A.applyOnTheRight(p,q,j)
+    const JRot jt = jrot_transpose(j);
+    if (jt.c == 1.0 && jt.s == 0.0) return;
+    for (int k = 0; k < 3; ++k) jrot_pair(A[k][p], A[k][q], jt);
+}
+inline double dot3_eigen(double a0, double a1, double a2, double b0, double b1, double b2) {
+    return a0 * b0 + (a1 * b1 + a2 * b2);     // 3-term redux unrolled as x0 + (x1 + x2)
+}
+inline M3 rotation_polar(const M3& in) {
+    double W[3][3], U[3][3], V[3][3];
+    double scale = 0.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) scale = std::max(scale, std::fabs(in.m[i][j]));
+    if (scale == 0.0) scale = 1.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            W[i][j] = in.m[i][j] / scale;
+            U[i][j] = (i == j) ? 1.0 : 0.0;
+            V[i][j] = (i == j) ? 1.0 : 0.0;
+        }
+    const double precision = 2.0 * std::numeric_limits<double>::epsilon();
+    const double tiny = std::numeric_limits<double>::min();
+    double max_diag = std::max(std::fabs(W[0][0]), std::max(std::fabs(W[1][1]), std::fabs(W[2][2])));
+    bool finished = false;
+    while (!finished) {
+        finished = true;
+        for (int p = 1; p < 3; ++p) {
+            for (int q = 0; q < p; ++q) {
+                const double threshold = std::max(tiny, precision * max_diag);
+                if (std::fabs(W[p][q]) > threshold || std::fabs(W[q][p]) > threshold) {
+                    finished = false;
+                    // real_2x2_jacobi_svd(W, p, q)
+                    double m[2][2] = {{W[p][p], W[p][q]}, {W[q][p], W[q][q]}};
+                    JRot rot1;
+                    const double t = m[0][0] + m[1][1];
+                    const double d = m[1][0] - m[0][1];
+                    if (std::fabs(d) < tiny) {
+                        rot1 = {1.0, 0.0};
+                    } else {
+                        const double u = t / d;
+                        const double tmp = std::sqrt(1.0 + u * u);
+                        rot1 = {u / tmp, 1.0 / tmp};
+                    }
+                    if (!(rot1.c == 1.0 && rot1.s == 0.0))
+                        for (int k = 0; k < 2; ++k) jrot_pair(m[0][k], m[1][k], rot1);
+                    const JRot j_right = jrot_make_jacobi(m[0][0], m[0][1], m[1][1]);
+                    const JRot j_left = jrot_product(rot1, jrot_transpose(j_right));
+                    left_rot(W, p, q, j_left);
+                    right_rot(U, p, q, jrot_transpose(j_left));
+                    right_rot(W, p, q, j_right);
+                    right_rot(V, p, q, j_right);
+                    max_diag = std::max(max_diag, std::max(std::fabs(W[p][p]), std::fabs(W[q][q])));
+                }
+            }
+        }
+    }
+    double sv[3];
+    for (int i = 0; i < 3; ++i) {
+        const double a = W[i][i];
+        sv[i] = std::fabs(a);
+        if (a < 0.0)
+            for (int k = 0; k < 3; ++k) U[k][i] = -U[k][i];
+    }
+    for (int i = 0; i < 3; ++i) {
+        int pos = i;
+        for (int k = i + 1; k < 3; ++k)
+            if (sv[k] > sv[pos]) pos = k;
+        if (pos != i) {
+            std::swap(sv[i], sv[pos]);
+            for (int k = 0; k < 3; ++k) {
+                std::swap(U[k][i], U[k][pos]);
+                std::swap(V[k][i], V[k][pos]);
+            }
+        }
+    }
+    double P[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) P[i][j] = dot3_eigen(U[i][0], U[i][1], U[i][2], V[j][0], V[j][1], V[j][2]);
+    const double det = P[0][0] * (P[1][1] * P[2][2] - P[1][2] * P[2][1]) -
+                       P[0][1] * (P[1][0] * P[2][2] - P[1][2] * P[2][0]) +
+                       P[0][2] * (P[1][0] * P[2][1] - P[1][1] * P[2][0]);
+    for (int k = 0; k < 3; ++k) U[k][0] /= det;
+    M3 r;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r.m[i][j] = dot3_eigen(U[i][0], U[i][1], U[i][2], V[j][0], V[j][1], V[j][2]);
+    return r;
+}
+
 struct Iso { M3 R; V3 t; };  // Eigen::Isometry3d
 inline Iso iso_identity() { return {m3_identity(), {0, 0, 0}}; }
 inline Iso iso_mul(const Iso& a, const Iso& b) {   // Transform * Transform
@@ -305,7 +421,7 @@ inline V3 plane_fit5(const double A_in[5][3]) {
             std::swap(colnorm[k], colnorm[best]);
             std::swap(colnorm_upd[k], colnorm_upd[best]);
         }
-        double x[5], ess[5];
+        double x[5] = {0, 0, 0, 0, 0}, ess[5] = {0, 0, 0, 0, 0};
         int n = R - k;
         for (int i = 0; i < n; ++i) x[i] = A[k + i][k];
         double tau, beta;

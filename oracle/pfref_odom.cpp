@@ -801,7 +801,7 @@ int odom_update(Odom& o, const std::vector<PtC>& edge_in, const std::vector<PtC>
     Iso pred = iso_mul(o.odom, iso_mul(iso_inv(o.last_odom), o.odom)); // :235-237
     o.last_odom = o.odom;
     o.odom = pred;
-    Quat q = m2q(o.odom.R);                                             // :239 (rotation() == linear())
+    Quat q = m2q(rotation_polar(o.odom.R));                             // :239 (Eigen 3.3 rotation())
     o.params[0] = q.x; o.params[1] = q.y; o.params[2] = q.z; o.params[3] = q.w;
     o.params[4] = o.odom.t.x; o.params[5] = o.odom.t.y; o.params[6] = o.odom.t.z;
     const bool stable = (o.opts & PFREF_VG_STABLE) != 0;
@@ -947,6 +947,15 @@ void pfref_plane_fit(const double A[15], double n_out[3]) {
 
 void pfref_se3_plus(const double x[7], const double delta[6], double out[7]) { se3_plus(x, delta, out); }
 
+void pfref_rotation_polar(const double m[9], double out[9]) {
+    M3 a;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) a.m[i][j] = m[3 * i + j];
+    const M3 r = rotation_polar(a);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) out[3 * i + j] = r.m[i][j];
+}
+
 double pfref_edge_eval(const double x[7], const double cur[3], const double a[3], const double b[3], double weight,
                        double J[7]) {
     return edge_eval(x, V3{cur[0], cur[1], cur[2]}, V3{a[0], a[1], a[2]}, V3{b[0], b[1], b[2]}, weight, J);
@@ -993,7 +1002,7 @@ int pfref_odom_init_map(pfref_odom* h, const float* edge, size_t ne, const float
 }
 
 void pfref_odom_get_pose(const pfref_odom* h, double pose[7]) {
-    Quat q = m2q(h->o.odom.R);           // q_current(odom.rotation()) in the node (copy.cpp:105)
+    Quat q = m2q(rotation_polar(h->o.odom.R));  // q_current(odom.rotation()) in the node (copy.cpp:105)
     pose[0] = q.x; pose[1] = q.y; pose[2] = q.z; pose[3] = q.w;
     pose[4] = h->o.odom.t.x; pose[5] = h->o.odom.t.y; pose[6] = h->o.odom.t.z;
 }
@@ -1026,6 +1035,18 @@ int pfref_odom_set_map(pfref_odom* h, int which, const float* xyz, const uint8_t
 }
 
 void pfref_odom_get_stats(const pfref_odom* h, pfref_stats* s) { *s = h->o.stats; }
+
+void pfref_odom_set_state(pfref_odom* h, const double odom_pose[7], const double last_pose[7]) {
+    Quat q{odom_pose[0], odom_pose[1], odom_pose[2], odom_pose[3]};
+    h->o.odom.R = q2m(q);
+    h->o.odom.t = V3{odom_pose[4], odom_pose[5], odom_pose[6]};
+    Quat ql{last_pose[0], last_pose[1], last_pose[2], last_pose[3]};
+    h->o.last_odom.R = q2m(ql);
+    h->o.last_odom.t = V3{last_pose[4], last_pose[5], last_pose[6]};
+    for (int k = 0; k < 7; ++k) h->o.params[k] = odom_pose[k];
+}
+
+void pfref_odom_set_opt_count(pfref_odom* h, int n) { h->o.optimization_count = n; }
 
 int pfref_odom_frame(pfref_odom* h, const pfref_lidar* lidar, const float* xyzi, size_t n, double pose_out[7]) {
     std::vector<PtI> e, s;

@@ -106,6 +106,120 @@ PF_HD qd m2q(const m3& a) {
     return qd{c[0], c[1], c[2], c[3]};
 }
 
+// Transform<double,3,Isometry>::rotation() in Eigen 3.3 (the ROS Noetic / Ubuntu 20.04 Eigen) is
+// NOT linear(): it is the orthogonal polar factor computeRotationScaling() takes from a
+// JacobiSVD<Matrix3d>(ComputeFullU|ComputeFullV). That re-orthonormalisation is what keeps |q|
+// at 1 through the constant-velocity prediction (src/odomEstimationClass.cpp:235-239); without
+// it the norm error is tripled every frame once the heading passes ~90 degrees.
+// Two-sided Jacobi sweep exactly as JacobiSVD::compute (square input: no QR preconditioner).
+struct jrot { double c, s; };
+// rows p,q of A (applyOnTheLeft); x' = c x + s y, y' = -s x + c y
+PF_HD void rot_rows(double A[3][3], int p, int q, jrot j) {
+    if (j.c == 1.0 && j.s == 0.0) return;
+    for (int k = 0; k < 3; ++k) {
+        const double x = A[p][k], y = A[q][k];
+        A[p][k] = j.c * x + j.s * y;
+        A[q][k] = -j.s * x + j.c * y;
+    }
+}
+// columns p,q of A rotated by j (apply_rotation_in_the_plane on two columns)
+PF_HD void rot_cols(double A[3][3], int p, int q, jrot j) {
+    if (j.c == 1.0 && j.s == 0.0) return;
+    for (int k = 0; k < 3; ++k) {
+        const double x = A[k][p], y = A[k][q];
+        A[k][p] = j.c * x + j.s * y;
+        A[k][q] = -j.s * x + j.c * y;
+    }
+}
+PF_HD jrot make_jacobi(double x, double y, double z) {   // JacobiRotation::makeJacobi (real)
+    const double deno = 2.0 * fabs(y);
+    if (deno < DBL_MIN) return jrot{1.0, 0.0};
+    const double tau = (x - z) / deno;
+    const double w = sqrt(tau * tau + 1.0);
+    const double t = tau > 0.0 ? 1.0 / (tau + w) : 1.0 / (tau - w);
+    const double sign_t = t > 0.0 ? 1.0 : -1.0;
+    const double n = 1.0 / sqrt(t * t + 1.0);
+    return jrot{n, -sign_t * (y / fabs(y)) * fabs(t) * n};
+}
+PF_HD m3 polar_rotation(const m3& a) {
+    double W[3][3], U[3][3], V[3][3];
+    double scale = 0.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) scale = fmax(scale, fabs(a.m[i][j]));
+    if (scale == 0.0) scale = 1.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            W[i][j] = a.m[i][j] / scale;
+            U[i][j] = V[i][j] = (i == j) ? 1.0 : 0.0;
+        }
+    const double precision = 2.0 * DBL_EPSILON;
+    double maxdiag = fmax(fmax(fabs(W[0][0]), fabs(W[1][1])), fabs(W[2][2]));
+    bool finished = false;
+    for (int sweep = 0; !finished && sweep < 64; ++sweep) {
+        finished = true;
+        for (int p = 1; p < 3; ++p)
+            for (int q = 0; q < p; ++q) {
+                const double thr = fmax(DBL_MIN, precision * maxdiag);
+                if (!(fabs(W[p][q]) > thr || fabs(W[q][p]) > thr)) continue;
+                finished = false;
+                // real_2x2_jacobi_svd on the (p,q) block
+                double m00 = W[p][p], m01 = W[p][q], m10 = W[q][p], m11 = W[q][q];
+                jrot r1{1.0, 0.0};
+                const double t = m00 + m11, d = m10 - m01;
+                if (fabs(d) >= DBL_MIN) {
+                    const double u = t / d;
+                    const double tmp = sqrt(1.0 + u * u);
+                    r1 = jrot{u / tmp, 1.0 / tmp};
+                }
+                if (!(r1.c == 1.0 && r1.s == 0.0)) {
+                    const double a0 = m00, a1 = m01, b0 = m10, b1 = m11;
+                    m00 = r1.c * a0 + r1.s * b0; m01 = r1.c * a1 + r1.s * b1;
+                    m10 = -r1.s * a0 + r1.c * b0; m11 = -r1.s * a1 + r1.c * b1;
+                }
+                const jrot jr = make_jacobi(m00, m01, m11);
+                // j_left = rot1 * j_right.transpose()
+                const jrot jl{r1.c * jr.c - r1.s * (-jr.s), r1.c * (-jr.s) + r1.s * jr.c};
+                rot_rows(W, p, q, jl);                   // W.applyOnTheLeft(p,q,j_left)
+                rot_cols(U, p, q, jl);                   // U.applyOnTheRight(p,q,j_left.transpose())
+                rot_cols(W, p, q, jrot{jr.c, -jr.s});    // W.applyOnTheRight(p,q,j_right)
+                rot_cols(V, p, q, jrot{jr.c, -jr.s});    // V.applyOnTheRight(p,q,j_right)
+                maxdiag = fmax(maxdiag, fmax(fabs(W[p][p]), fabs(W[q][q])));
+            }
+    }
+    double sv[3];
+    for (int i = 0; i < 3; ++i) {
+        sv[i] = fabs(W[i][i]);
+        if (W[i][i] < 0.0)
+            for (int k = 0; k < 3; ++k) U[k][i] = -U[k][i];
+    }
+    for (int i = 0; i < 3; ++i) {                        // descending order, first max wins
+        int pos = i;
+        for (int k = i + 1; k < 3; ++k)
+            if (sv[k] > sv[pos]) pos = k;
+        if (pos != i) {
+            const double ts = sv[i]; sv[i] = sv[pos]; sv[pos] = ts;
+            for (int k = 0; k < 3; ++k) {
+                double tu = U[k][i]; U[k][i] = U[k][pos]; U[k][pos] = tu;
+                double tv = V[k][i]; V[k][i] = V[k][pos]; V[k][pos] = tv;
+            }
+        }
+    }
+    m3 uvt;                                              // U * V^T
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            uvt.m[i][j] = U[i][0] * V[j][0] + (U[i][1] * V[j][1] + U[i][2] * V[j][2]);
+    const double (*M)[3] = uvt.m;
+    const double x = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1])   // bruteforce_det3_helper
+                   - M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0])
+                   + M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+    for (int k = 0; k < 3; ++k) U[k][0] /= x;
+    m3 r;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            r.m[i][j] = U[i][0] * V[j][0] + (U[i][1] * V[j][1] + U[i][2] * V[j][2]);
+    return r;
+}
+
 struct iso { m3 R; d3 t; };
 PF_HD iso iso_mul(const iso& a, const iso& b) {
     d3 rt = m3_vec(a.R, b.t);

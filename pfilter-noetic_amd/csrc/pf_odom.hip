@@ -73,7 +73,7 @@ __global__ void k_predict(DevState* __restrict__ st, int* __restrict__ cnt, u32*
     const iso pred = iso_mul(odom, iso_mul(iso_inv(last), odom));             // :235
     store_iso(odom, st->lastR, st->lastt);
     store_iso(pred, st->odomR, st->odomt);
-    const qd q = m2q(pred.R);                                                  // :239 (rotation() = linear())
+    const qd q = m2q(polar_rotation(pred.R));                                  // :239 (Eigen 3.3 rotation())
     st->params[0] = q.x; st->params[1] = q.y; st->params[2] = q.z; st->params[3] = q.w;
     st->params[4] = pred.t.x; st->params[5] = pred.t.y; st->params[6] = pred.t.z;
     const int gate = (cnt[C_ME] > 10 && cnt[C_MS] > 50) ? 1 : 0;              // :247
@@ -741,7 +741,7 @@ __global__ void k_finalize(DevState* __restrict__ st, double* __restrict__ poses
         store_iso(o, st->odomR, st->odomt);
     }
     const iso o = load_iso(st->odomR, st->odomt);
-    const qd q = m2q(o.R);
+    const qd q = m2q(polar_rotation(o.R));
     double* P = poses + 7 * (size_t)(st->frame % pose_cap);
     P[0] = q.x; P[1] = q.y; P[2] = q.z; P[3] = q.w;
     P[4] = o.t.x; P[5] = o.t.y; P[6] = o.t.z;

@@ -101,11 +101,15 @@ void add_box(World& w, double cx, double cy, double psi, double hx, double hy, d
     w.boxes.push_back(b);
 }
 
+// One RNG stream per (side, object kind): the objects laid along the road depend only on the seed
+// and the arc length, never on how many frames the sequence has (a prefix of a longer sequence is
+// the same scene).
 void build_scene(World& w) {
-    Rng rng((uint64_t)w.p.seed * 7919ull + 17ull);
     const double s_begin = w.s0 + 5.0;
     const double s_end = w.s0 + (w.path.size() - 2) * w.ds;
     for (int side = -1; side <= 1; side += 2) {
+        const uint64_t base = (uint64_t)w.p.seed * 7919ull + 17ull + (side > 0 ? 100ull : 0ull);
+        Rng rng(base);
         // buildings
         double s = s_begin + rng.u(0.0, 10.0);
         while (s < s_end) {
@@ -125,6 +129,7 @@ void build_scene(World& w) {
             s += L + gap;
         }
         // poles
+        rng = Rng(base + 1);
         s = s_begin + rng.u(0.0, 5.0);
         while (s < s_end) {
             PathSample ps = w.at_s(s);
@@ -139,6 +144,7 @@ void build_scene(World& w) {
             s += rng.u(5.0, 10.0);
         }
         // parked cars
+        rng = Rng(base + 2);
         s = s_begin + rng.u(0.0, 10.0);
         while (s < s_end) {
             if (rng.u() < 0.5) {

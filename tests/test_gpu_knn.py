@@ -1,0 +1,63 @@
+"""GPU: exact radius-gated 5-NN (k_knn_query) against the oracle's brute-force search.
+
+Bit-exact: the same 5 indices (ties by map index) and the same f32 squared distances
+(accumulated x -> y -> z) wherever the oracle's neighbour lies within the 1 m^2 gate that
+src/odomEstimationClass.cpp:299-300 / :447-451 apply; beyond the gate the GPU reports -1 / inf."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(pa, pfref, mp, q):
+    kn = pa.Knn(mp.shape[0], q.shape[0])
+    kn.set_map(mp)
+    gi, gd = kn.query(q)
+    ri, rd = pfref.knn(mp, q, 5, opts=pfref.KNN_BRUTE)
+    inside = rd < 1.0
+    np.testing.assert_array_equal(np.where(inside, ri, -1), gi)
+    np.testing.assert_array_equal(gd[inside].view(np.uint32), rd[inside].view(np.uint32))
+    assert np.all(np.isinf(gd[~inside]))
+    return gi
+
+
+def test_knn_random_with_ties(pa, pfref):
+    rng = np.random.default_rng(0)
+    mp = np.zeros((30000, 4), np.float32)
+    mp[:, :3] = rng.uniform(-12, 12, (30000, 3))
+    mp[:8000, 2] = 0.0                               # plane
+    mp[8000:9000, :3] = np.round(mp[8000:9000, :3])   # lattice points, duplicated distances
+    mp[9000:9100] = mp[9100:9200]                     # exact duplicates
+    q = np.zeros((6000, 4), np.float32)
+    q[:, :3] = rng.uniform(-13, 13, (6000, 3))
+    q[:500, :3] = np.round(q[:500, :3]) + 0.5         # equidistant from lattice neighbours
+    gi = _check(pa, pfref, mp, q)
+    assert (gi[:, 4] >= 0).sum() > 1000
+
+
+def test_knn_dense_map(pa, pfref, pfsynth):
+    mp = pfsynth.dense_map(200000, seed=5)
+    q = pfsynth.dense_queries(mp, 3000, sigma=0.3, seed=6)
+    gi = _check(pa, pfref, mp, q)
+    assert (gi[:, 4] >= 0).mean() > 0.9
+
+
+def test_knn_far_and_negative_coordinates(pa, pfref):
+    rng = np.random.default_rng(1)
+    mp = np.zeros((5000, 4), np.float32)
+    mp[:, :3] = rng.uniform(-2000, -1990, (5000, 3))
+    q = np.zeros((800, 4), np.float32)
+    q[:, :3] = rng.uniform(-2002, -1988, (800, 3))
+    q[:50, :3] = 1e4                                   # nothing anywhere near
+    gi = _check(pa, pfref, mp, q)
+    assert np.all(gi[:50] == -1)
+
+
+def test_knn_tiny_map(pa, pfref):
+    mp = np.array([[0, 0, 0, 0], [0.5, 0, 0, 0], [0, 0.5, 0, 0]], np.float32)
+    q = np.array([[0.1, 0.1, 0, 0], [5, 5, 5, 0]], np.float32)
+    kn = pa.Knn(3, 2)
+    kn.set_map(mp)
+    gi, gd = kn.query(q)
+    assert list(gi[0, :3]) == [0, 1, 2] and np.all(gi[0, 3:] == -1)
+    assert np.all(gi[1] == -1)

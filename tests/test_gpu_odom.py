@@ -1,0 +1,192 @@
+"""GPU: Odom_ES_EstimationClass (src/odomEstimationClass.cpp:182-647) through the C ABI against the
+oracle in GPU_EQUIV mode (stable tie orders + normal-equation LM step).
+
+Tolerances (BASELINE.json north_star): pose within 1e-4 m / 1e-5 rad per frame. Integer work —
+down-sampled counts, residual counts, map sizes, ages / p-index bytes — must be identical, and the
+maps bit-identical, while the poses agree to ~1e-12 (the only difference is the summation order of
+the 6x6 normal equations)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from _util import pose_err
+
+pytestmark = pytest.mark.gpu
+
+TOL_T, TOL_R = 1e-4, 1e-5
+COUNTS = ("n_edge_ds", "n_surf_ds", "n_edge_map", "n_surf_map", "n_edge_res", "n_surf_res", "n_edge_valid",
+          "n_surf_valid", "outer_iterations", "map_too_small")
+
+
+def _pair(pa, pfref, lines=64, map_res=0.4, k_new=0, theta_p=0.4, theta_max=75, wt=0, mn=3.0, mx=90.0):
+    od = pa.Odom_ES_EstimationClass(device=0)
+    od.init(pa.make_lidar(lines, mn, mx), map_res, k_new, theta_p, theta_max, wt)
+    orc = pfref.Odom(pfref.make_lidar(lines, mn, mx), map_res, k_new, theta_p, theta_max, wt, opts=pfref.GPU_EQUIV)
+    return od, orc
+
+
+def _compare_maps(od, orc):
+    for which, (gx, grg) in ((0, od.laserCloudCornerMap), (1, od.laserCloudSurfMap)):
+        rx, rrg = orc.get_map(which)
+        assert gx.shape == rx.shape, (which, gx.shape, rx.shape)
+        np.testing.assert_array_equal(gx.view(np.uint32), rx.view(np.uint32))
+        np.testing.assert_array_equal(grg, rrg)
+
+
+def _run(od, orc, seq, frames, check_maps_every=0):
+    worst = (0.0, 0.0)
+    for i, k in enumerate(frames):
+        x = seq.frame(k)
+        pg = od.frame_host(x)
+        pr = orc.frame(x)
+        dt, dr = pose_err(pg, pr)
+        worst = (max(worst[0], dt), max(worst[1], dr))
+        assert dt < TOL_T and dr < TOL_R, "frame %d: %.3e m %.3e rad" % (k, dt, dr)
+        if i > 0:
+            sg, sr = od.stats(), orc.stats()
+            for c in COUNTS:
+                assert sg[c] == sr[c], (k, c, sg[c], sr[c])
+        if check_maps_every and i % check_maps_every == 0:
+            _compare_maps(od, orc)
+    return worst
+
+
+def test_pose_and_map_parity_kitti_config(pa, pfref, pfsynth):
+    """configs[1]: 64 lines, k_new 0, theta_p 0.4, theta_max 75, weightType 0, map_res 0.4."""
+    seq = pfsynth.Sequence("S64", n_frames=60)
+    od, orc = _pair(pa, pfref)
+    worst = _run(od, orc, seq, range(40), check_maps_every=13)
+    _compare_maps(od, orc)
+    assert worst[0] < 1e-8
+
+
+@pytest.mark.parametrize("wt", [1, 2, 12])
+def test_weight_types(pa, pfref, pfsynth, wt):
+    seq = pfsynth.Sequence("S64", n_frames=20, az_steps=1200)
+    od, orc = _pair(pa, pfref, wt=wt)
+    _run(od, orc, seq, range(12), check_maps_every=11)
+
+
+@pytest.mark.parametrize("k_new,theta_p,theta_max", [(0, 0.0, 0), (2, 0.4, 75), (1, 0.8, 30)])
+def test_pindex_configs(pa, pfref, pfsynth, k_new, theta_p, theta_max):
+    """theta_p 0 = plain FLOAM map (no p-index filter); k_new > 0 keeps young map points."""
+    seq = pfsynth.Sequence("S64", n_frames=20, az_steps=1200)
+    od, orc = _pair(pa, pfref, k_new=k_new, theta_p=theta_p, theta_max=theta_max)
+    _run(od, orc, seq, range(12), check_maps_every=11)
+
+
+def test_campus_32_line(pa, pfref, pfsynth):
+    """configs[2]: 32-line campus scan (launch/pfilter.launch: min/max 3/90), theta_p 1, theta_max 200."""
+    seq = pfsynth.Sequence("S32", n_frames=20)
+    od, orc = _pair(pa, pfref, lines=32, theta_p=1.0, theta_max=200)
+    _run(od, orc, seq, range(12), check_maps_every=11)
+
+
+def test_update_api_matches_oracle(pa, pfref, pfsynth):
+    """initMapWithPoints / updatePointsToMap with host-side features (the node's call pattern)."""
+    seq = pfsynth.Sequence("S64", n_frames=10, az_steps=1500)
+    lid = pfref.make_lidar(64, 3.0, 90.0)
+    od, orc = _pair(pa, pfref)
+    for k in range(6):
+        e, s = pfref.feature_extraction(seq.frame(k), lid, opts=pfref.FE_STABLE_TIES)
+        if k == 0:
+            od.initMapWithPoints(e, s)
+            orc.init_map(e, s)
+            continue
+        pg = od.updatePointsToMap(e, s)
+        pr = orc.update(e, s)
+        dt, dr = pose_err(pg, pr)
+        assert dt < TOL_T and dr < TOL_R
+        np.testing.assert_array_equal(pg, od.odom)
+    _compare_maps(od, orc)
+
+
+def test_device_pipeline_graph_equals_eager(pa, pfsynth):
+    """hipGraph replay of the steady-state frame gives the same bits as eager launches."""
+    seq = pfsynth.Sequence("S64", n_frames=30, az_steps=1500)
+    buf, counts = seq.frames(0, 30)
+    db = pa.DeviceBuffer(buf.nbytes)
+    db.upload(buf)
+    stride = buf.shape[1] * 16
+    res = []
+    for graph in (True, False):
+        od = pa.Odom_ES_EstimationClass(device=0)
+        od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+        od.set_graph(graph)
+        for k in range(30):
+            od.frame_device(db.ptr + k * stride, counts[k])
+        od.sync()
+        res.append((od.poses(), od.laserCloudSurfMap))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1][0], res[1][1][0])
+    np.testing.assert_array_equal(res[0][1][1], res[1][1][1])
+
+
+def test_map_too_small_warning(pa, pfref):
+    """|M_e| <= 10 or |M_s| <= 50: the solve is skipped and the prediction kept (.cpp:247, 274-277)."""
+    rng = np.random.default_rng(0)
+    e = np.zeros((5, 4), np.float32)
+    e[:, :3] = rng.uniform(-5, 5, (5, 3))
+    s = np.zeros((30, 4), np.float32)
+    s[:, :3] = rng.uniform(-5, 5, (30, 3))
+    od, orc = _pair(pa, pfref)
+    od.initMapWithPoints(e, s)
+    orc.init_map(e, s)
+    pg = od.updatePointsToMap(e, s)
+    pr = orc.update(e, s)
+    assert od.last_status == pa.PF_W_MAP_TOO_SMALL
+    assert od.stats()["map_too_small"] == 1 and orc.stats()["map_too_small"] == 1
+    np.testing.assert_allclose(pg, pr, atol=1e-12)
+
+
+def test_set_get_map_roundtrip(pa):
+    od = pa.Odom_ES_EstimationClass(device=0)
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    rng = np.random.default_rng(1)
+    xyz = rng.uniform(-50, 50, (1000, 3)).astype(np.float32)
+    rg = rng.integers(0, 256, (1000, 2)).astype(np.uint8)
+    od.set_map(1, xyz, rg)
+    gx, grg = od.laserCloudSurfMap
+    np.testing.assert_array_equal(gx, xyz)
+    np.testing.assert_array_equal(grg, rg)
+    assert od.laserCloudCornerMap[0].shape[0] == 0
+
+
+def test_invalid_arguments(pa):
+    od = pa.Odom_ES_EstimationClass(device=0)
+    with pytest.raises(pa.PFError) as ei:
+        od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 3)      # weightType 3
+    assert ei.value.code == pa.PF_EINVAL
+    od = pa.Odom_ES_EstimationClass(device=0, max_points=500)
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    with pytest.raises(pa.PFError) as ei:
+        od.frame_host(np.ones((501, 4), np.float32))
+    assert ei.value.code == pa.PF_ECAPACITY
+    L = pa.lib()
+    assert L.pf_odom_update(None, None, 0, 16, None, 0, 16, None) == pa.PF_EINVAL
+    assert L.pf_odom_get_map(od._h, 2, None, None, 0, ctypes.byref(ctypes.c_size_t())) == pa.PF_EINVAL
+
+
+def test_long_sequence_tracks(pa, pfsynth):
+    """Full-size S64 through the device pipeline: 400 frames covering a 90 degree heading change;
+    drift against the generator's ground truth stays below 0.5 % of the distance travelled and |q| = 1."""
+    n = 400
+    seq = pfsynth.Sequence("S64", n_frames=n)
+    od = pa.Odom_ES_EstimationClass(device=0)
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    for f0 in range(0, n, 100):
+        buf, counts = seq.frames(f0, 100)
+        db = pa.DeviceBuffer(buf.nbytes)
+        db.upload(buf)
+        for i in range(100):
+            od.frame_device(db.ptr + i * buf.shape[1] * 16, counts[i])
+        od.sync()
+        db.free()
+    p = od.poses()
+    gt = np.array([seq.gt_pose(k) for k in range(n)])
+    dist = np.sum(np.linalg.norm(np.diff(gt[:, 4:], axis=0), axis=1))
+    assert np.linalg.norm(p[-1, 4:] - gt[-1, 4:]) < 0.005 * dist
+    np.testing.assert_allclose(np.linalg.norm(p[:, :4], axis=1), 1.0, atol=1e-12)
+    yaw_gt = 2 * np.arctan2(gt[-1, 2], gt[-1, 3])
+    assert yaw_gt > 1.5

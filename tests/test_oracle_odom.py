@@ -1,0 +1,67 @@
+"""CPU: the oracle's whole odometry path on synthetic sequences (no GPU).
+
+Checks that the restatement tracks (drift against the generator's ground truth), that the pose
+stays a unit quaternion through the constant-velocity prediction — Eigen 3.3's
+Isometry3d::rotation() re-orthonormalises (SVD polar factor); using linear() instead lets |q|-1
+grow ~3x per frame once the heading passes 90 degrees and the odometry diverges — and that the
+option bits that separate the GPU-equivalent mode from the reference-faithful one only move the
+pose by tie-order / summation-order noise."""
+import numpy as np
+
+from _util import pose_err
+
+
+def yaw(q):
+    return 2 * np.arctan2(q[2], q[3])
+
+
+def test_tracks_and_keeps_unit_quaternion(pfref, pfsynth):
+    seq = pfsynth.Sequence("S64", n_frames=60, az_steps=1000)
+    od = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=pfref.GPU_EQUIV)
+    for k in range(40):
+        p = od.frame(seq.frame(k))
+        assert abs(np.linalg.norm(p[:4]) - 1) < 1e-14
+    gt = seq.gt_pose(39)
+    assert np.linalg.norm(p[4:] - gt[4:]) < 0.2
+    st = od.stats()
+    assert st["n_edge_res"] > 100 and st["n_surf_res"] > 100 and not st["map_too_small"]
+
+
+def test_heading_beyond_90_degrees(pfref, pfsynth):
+    """Start the odometry at a world heading of 2.0 rad: the same scans must give the same
+    trajectory rotated by 2.0 rad (this is where a linear()-based rotation() diverged)."""
+    y0 = 2.0
+    seq = pfsynth.Sequence("S64", n_frames=80, az_steps=900)
+    od = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=pfref.GPU_EQUIV)
+    q0 = np.array([0, 0, np.sin(y0 / 2), np.cos(y0 / 2), 0, 0, 0.0])
+    od.set_state(q0, q0)
+    for k in range(70):
+        p = od.frame(seq.frame(k))
+        err = (yaw(p) - y0 - yaw(seq.gt_pose(k)) + np.pi) % (2 * np.pi) - np.pi
+        assert abs(err) < 0.01, (k, err)
+        assert abs(np.linalg.norm(p[:4]) - 1) < 1e-14
+
+
+def test_option_bits_are_tie_noise(pfref, pfsynth):
+    """opts=0 (std::sort ties, dense QR LM, kd-tree) vs GPU_EQUIV: same counts, poses within
+    the north-star tolerance over a short sequence."""
+    seq = pfsynth.Sequence("S64", n_frames=20, az_steps=1000)
+    a = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=0)
+    b = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=pfref.GPU_EQUIV)
+    for k in range(10):
+        x = seq.frame(k)
+        dt, dr = pose_err(a.frame(x), b.frame(x))
+        assert dt < 1e-4 and dr < 1e-5
+
+
+def test_map_state_invariants(pfref, pfsynth):
+    """Ages (r) and p-index (g) bytes: g <= 255, every map point inside the 100 m crop box."""
+    seq = pfsynth.Sequence("S64", n_frames=20, az_steps=900)
+    od = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=pfref.GPU_EQUIV)
+    for k in range(8):
+        p = od.frame(seq.frame(k))
+    for which in (0, 1):
+        xyz, rg = od.get_map(which)
+        assert xyz.shape[0] > 100
+        assert np.all(np.abs(xyz - p[4:].astype(np.float32)) <= 100.0 + 1e-3)
+        assert rg[:, 1].max() >= 1            # p-index observed at least once

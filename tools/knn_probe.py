@@ -1,0 +1,35 @@
+"""kNN-only workload for profiling k_knn_query (config 5: 2M-point dense map, 200k queries).
+
+  python3 tools/knn_probe.py [--iters N]
+Prints avg kernel ms (HIP events) and algorithmic bytes per launch. Run under
+`rocprofv3 --kernel-trace --stats` or one `--pmc` counter per pass (see tools/gpu_round.sh)."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pfilter-noetic_amd"))
+sys.path.insert(0, os.path.join(ROOT, "pfilter-noetic_amd", "synth"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--nmap", type=int, default=2_000_000)
+    ap.add_argument("--nq", type=int, default=200_000)
+    a = ap.parse_args()
+    import pfilter_amd as pa
+    import pfsynth
+    mp = pfsynth.dense_map(a.nmap, seed=5)
+    q = pfsynth.dense_queries(mp, a.nq, sigma=0.3, seed=6)
+    kn = pa.Knn(a.nmap, a.nq)
+    kn.set_map(mp)
+    kn.query(q)
+    ms, alg = kn.bench(a.iters)
+    print(json.dumps({"avg_kernel_ms": ms, "alg_bytes_per_launch": alg, "launches": a.iters + 2,
+                      "achieved_GBps": alg / (ms * 1e-3) / 1e9}))
+
+
+if __name__ == "__main__":
+    main()
