@@ -180,6 +180,7 @@ static int frame_status(pf_odom* h) {
     PF_HIP_TRY(hipMemcpyAsync(o.h_cnt, o.cnt, sizeof(int) * C_COUNT, hipMemcpyDeviceToHost, o.stream));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     PF_HIP_TRY(hipGetLastError());
+    if (o.h_cnt[C_ERR]) return PF_EHIP;                  // a bounded device-side wait gave up
     if (!o.h_cnt[C_GATE]) return PF_W_MAP_TOO_SMALL;
     if (o.h_cnt[C_EDGE_KEPT] < 20 || o.h_cnt[C_SURF_KEPT] < 20) return PF_W_FEW_CORRESPONDENCES;
     return PF_OK;
@@ -355,6 +356,15 @@ int pf_odom_poses(pf_odom* h, double* poses, size_t cap, size_t* n) {
     if (!poses) return PF_OK;
     if (f > cap || f > o.pose_cap) return PF_ECAPACITY;
     if (f) PF_HIP_TRY(hipMemcpy(poses, o.poses, sizeof(double) * 7 * f, hipMemcpyDeviceToHost));
+    return PF_OK;
+}
+
+// development probe (not part of include/pfilter_hip.h): device timestamps of the last LM solve
+extern "C" int pf_dev_probe(pf_odom* h, unsigned long long* out, int n) {
+    if (!h || !out || n <= 0 || n > 64 || !h->o.dbg) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
+    PF_HIP_TRY(hipMemcpy(out, h->o.dbg, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
     return PF_OK;
 }
 

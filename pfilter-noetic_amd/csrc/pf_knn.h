@@ -88,4 +88,72 @@ __device__ __forceinline__ int knn5(const GridView& gv, int m, float qx, float q
     return found;
 }
 
+// The same search by a team of T lanes (T a power of two <= 64, aligned within the wave): lane l
+// of the team scans cells l, l + T, ... of the 27, keeping its own sorted 5 best, then the team
+// merges its lists in 5 rounds of a (d^2 bits, index) minimum. Keys are unique (distinct map
+// indices), so the merged 5 are exactly the sequential search's. Every lane of the wave must call
+// this (the merge shuffles); `active` is uniform within a team. Results are valid on every lane.
+__device__ __forceinline__ u64 knn_key(float d, int i) {
+    return ((u64)__float_as_uint(d) << 32) | (u64)(u32)i;
+}
+template <int T>
+__device__ __forceinline__ int knn5_team(const GridView& gv, int m, float qx, float qy, float qz, bool active,
+                                         float (&dout)[5], int (&iout)[5]) {
+    float d[5];
+    int id[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { d[k] = 1.0f; id[k] = 0x7fffffff; }
+    const int* dm = gv.dims + 8 * m;
+    if (active && dm[7]) {
+        const int cx = (int)floorf(qx), cy = (int)floorf(qy), cz = (int)floorf(qz);
+        const int minx = dm[0], miny = dm[1], minz = dm[2], dx = dm[3], dy = dm[4], dz = dm[5], base = dm[6];
+        for (int j = lane_id() & (T - 1); j < 27; j += T) {
+            const int x = cx + (j % 3) - 1 - minx, y = cy + (j / 3) % 3 - 1 - miny, z = cz + j / 9 - 1 - minz;
+            if (x < 0 || y < 0 || z < 0 || x >= dx || y >= dy || z >= dz) continue;
+            const int cid = base + (z * dy + y) * dx + x;
+            const u32 b0 = gv.cell_start[cid], b1 = gv.cell_start[cid + 1];
+            for (u32 k = b0; k < b1; ++k) {
+                const float4 p = gv.cpts[k];
+                float r = 0.0f;
+                float t = qx - p.x; r += t * t;
+                t = qy - p.y; r += t * t;
+                t = qz - p.z; r += t * t;
+                if (!(r < 1.0f)) continue;
+                const int idx = __float_as_int(p.w);
+                if (!knn_lt(r, idx, d[4], id[4])) continue;
+                d[4] = r; id[4] = idx;
+#pragma unroll
+                for (int q = 4; q > 0; --q) {
+                    if (knn_lt(d[q], id[q], d[q - 1], id[q - 1])) {
+                        float td = d[q]; d[q] = d[q - 1]; d[q - 1] = td;
+                        int ti = id[q]; id[q] = id[q - 1]; id[q - 1] = ti;
+                    }
+                }
+            }
+        }
+    }
+    const u64 sentinel = knn_key(1.0f, 0x7fffffff);
+    u64 head = knn_key(d[0], id[0]);
+    int found = 0;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+        u64 mn = head;
+#pragma unroll
+        for (int o = T / 2; o > 0; o >>= 1) {
+            const u64 other = __shfl_xor(mn, o, 64);
+            mn = other < mn ? other : mn;
+        }
+        dout[r] = __uint_as_float((u32)(mn >> 32));
+        iout[r] = (int)(u32)(mn & 0xffffffffull);
+        if (mn != sentinel) ++found;
+        if (head == mn && mn != sentinel) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { d[k] = d[k + 1]; id[k] = id[k + 1]; }
+            d[4] = 1.0f; id[4] = 0x7fffffff;
+            head = knn_key(d[0], id[0]);
+        }
+    }
+    return found;
+}
+
 }  // namespace pf

@@ -23,30 +23,39 @@ __device__ __forceinline__ int wave_max_i(int v) {
     return v;
 }
 
-// per-map min/max cell coordinates; one atomic per wave and coordinate
+// per-map min/max cell coordinates: wave then workgroup reduction, one atomic per workgroup
 __global__ void __launch_bounds__(256) k_grid_bounds(const float4* __restrict__ m0, const int* __restrict__ d_m0,
                                                       const float4* __restrict__ m1, const int* __restrict__ d_m1,
                                                       int* __restrict__ bounds) {
+    __shared__ int red[4][12];
     const int n0 = *d_m0, n1 = m1 ? *d_m1 : 0;
-    const int l = lane_id();
-    for (int mi = 0; mi < 2; ++mi) {
-        const float4* mp = mi == 0 ? m0 : m1;
-        const int n = mi == 0 ? n0 : n1;
-        int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
-        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-            const float4 p = mp[i];
-            const int c[3] = {(int)floorf(p.x), (int)floorf(p.y), (int)floorf(p.z)};
+    const int l = lane_id(), w = threadIdx.x >> 6;
+    int v[12];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) { mn[k] = min(mn[k], c[k]); mx[k] = max(mx[k], c[k]); }
-        }
+    for (int k = 0; k < 12; ++k) v[k] = ((k % 6) < 3) ? INT_MAX : INT_MIN;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
+        const int mi = i < n0 ? 0 : 1;
+        const float4 p = mi == 0 ? m0[i] : m1[i - n0];
+        const int c[3] = {(int)floorf(p.x), (int)floorf(p.y), (int)floorf(p.z)};
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const int a = wave_min_i(mn[k]), b = wave_max_i(mx[k]);
-            if (l == 0 && a != INT_MAX) {
-                atomicMin(&bounds[mi * 6 + k], a);
-                atomicMax(&bounds[mi * 6 + 3 + k], b);
-            }
+            if (mi == 0) { v[k] = min(v[k], c[k]); v[3 + k] = max(v[3 + k], c[k]); }
+            else { v[6 + k] = min(v[6 + k], c[k]); v[9 + k] = max(v[9 + k], c[k]); }
         }
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const int r = ((k % 6) < 3) ? wave_min_i(v[k]) : wave_max_i(v[k]);
+        if (l == 0) red[w][k] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        const int k = threadIdx.x;
+        const bool is_min = (k % 6) < 3;
+        int r = red[0][k];
+        for (int ww = 1; ww < 4; ++ww) r = is_min ? min(r, red[ww][k]) : max(r, red[ww][k]);
+        if (is_min && r != INT_MAX) atomicMin(&bounds[k], r);
+        if (!is_min && r != INT_MIN) atomicMax(&bounds[k], r);
     }
 }
 
@@ -119,20 +128,26 @@ __global__ void __launch_bounds__(256) k_grid_scatter(const float4* __restrict__
     }
 }
 
-// standalone query: queries in map 0
+// standalone query: queries in map 0, a team of kKnnTeam lanes per query
+constexpr int kKnnTeam = 16;
 __global__ void __launch_bounds__(256) k_knn_query(GridView gv, const float4* __restrict__ q, int nq,
                                                     int* __restrict__ idx, float* __restrict__ d2) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nq) return;
-    const float4 p = q[i];
+    const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / kKnnTeam);
+    const bool active = i < nq;
+    const float4 p = active ? q[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     float d[5];
     int id[5];
-    knn5(gv, 0, p.x, p.y, p.z, d, id);
+    knn5_team<kKnnTeam>(gv, 0, p.x, p.y, p.z, active, d, id);
+    const int tl = lane_id() & (kKnnTeam - 1);
+    if (active && tl < 5) {
+        float dv = d[0];
+        int iv = id[0];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const bool f = id[k] != 0x7fffffff;
-        idx[5 * i + k] = f ? id[k] : -1;
-        d2[5 * i + k] = f ? d[k] : __int_as_float(0x7f800000);
+        for (int k = 1; k < 5; ++k)
+            if (tl == k) { dv = d[k]; iv = id[k]; }
+        const bool f = iv != 0x7fffffff;
+        idx[5 * i + tl] = f ? iv : -1;
+        d2[5 * i + tl] = f ? dv : __int_as_float(0x7f800000);
     }
 }
 
@@ -194,7 +209,7 @@ void grid_build(GridGPU& g, const float4* map0, const int* d_m0, const float4* m
                 hipStream_t s) {
     const int nb = 512;
     hipLaunchKernelGGL(k_grid_reset, dim3(1), dim3(64), 0, s, g.bounds);
-    hipLaunchKernelGGL(k_grid_bounds, dim3(nb), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.bounds);
+    hipLaunchKernelGGL(k_grid_bounds, dim3(64), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.bounds);
     hipLaunchKernelGGL(k_grid_dims, dim3(1), dim3(64), 0, s, g.bounds, d_m0, d_m1, g.dims, g.d_ncells,
                        (long long)g.cell_cap, g.err);
     hipLaunchKernelGGL(k_grid_clear, dim3(1024), dim3(256), 0, s, g.cell_count, g.d_ncells);
@@ -293,8 +308,8 @@ int pf_knn_query(pf_knn* h, const float* q4, size_t nq, int32_t* idx, float* d2)
     if (nq == 0) return PF_OK;
     PF_HIP_TRY(hipMemcpyAsync(h->d_q, q4, sizeof(float4) * nq, hipMemcpyHostToDevice, h->stream));
     GridView gv{h->grid.dims, h->grid.cell_start, h->grid.cpts};
-    hipLaunchKernelGGL(k_knn_query, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, h->stream, gv, h->d_q, (int)nq,
-                       h->d_idx, h->d_d2);
+    hipLaunchKernelGGL(k_knn_query, dim3((unsigned)((nq * kKnnTeam + 255) / 256)), dim3(256), 0, h->stream, gv,
+                       h->d_q, (int)nq, h->d_idx, h->d_d2);
     if (idx) PF_HIP_TRY(hipMemcpyAsync(idx, h->d_idx, sizeof(int) * 5 * nq, hipMemcpyDeviceToHost, h->stream));
     if (d2) PF_HIP_TRY(hipMemcpyAsync(d2, h->d_d2, sizeof(float) * 5 * nq, hipMemcpyDeviceToHost, h->stream));
     PF_HIP_TRY(hipStreamSynchronize(h->stream));
@@ -306,9 +321,10 @@ int pf_knn_bench(pf_knn* h, int iters, double* avg_ms, double* alg_bytes) {
     if (!h || iters <= 0 || h->nq <= 0) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->device));
     GridView gv{h->grid.dims, h->grid.cell_start, h->grid.cpts};
-    const dim3 grid((unsigned)((h->nq + 255) / 256));
+    const dim3 grid((unsigned)(((size_t)h->nq * kKnnTeam + 255) / 256));
     PF_HIP_TRY(hipMemsetAsync(h->d_pop, 0, sizeof(unsigned long long), h->stream));
-    hipLaunchKernelGGL(k_knn_cellpop, grid, dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_pop);
+    hipLaunchKernelGGL(k_knn_cellpop, dim3((unsigned)((h->nq + 255) / 256)), dim3(256), 0, h->stream, gv, h->d_q,
+                       h->nq, h->d_pop);
     unsigned long long pop = 0;
     PF_HIP_TRY(hipMemcpyAsync(&pop, h->d_pop, sizeof(pop), hipMemcpyDeviceToHost, h->stream));
     hipLaunchKernelGGL(k_knn_query, grid, dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2);  // warm

@@ -42,7 +42,6 @@ struct LMState {
     int iteration, invalid, reuse, done, phase, n_res, pad0, pad1;
 };
 
-constexpr int kLmBlocks = 64;
 constexpr int kLmParts = 30;   // cost, g[6], H[21], bad_r, bad_J
 
 struct OdomGPU {
@@ -51,6 +50,7 @@ struct OdomGPU {
     int device = 0;
     hipStream_t stream = nullptr;
     size_t in_cap = 0, map_cap = 0, sort_cap = 0, pose_cap = 0;
+    int pidx_bits = 32;            // key bits the p-index pair sort needs
     int opt_count_host = 2;
     bool inited = false;
     int frames = 0;
@@ -83,7 +83,9 @@ struct OdomGPU {
     float* observe = nullptr;
     u32* pcnt = nullptr;           // [5 * 2 * in_cap]
     u32* tailinc = nullptr;        // [sort_cap]
-    double* lm_part = nullptr;     // [kLmBlocks * 32]
+    double* lm_part = nullptr;     // [kLmBlocks * 32] per-block LM partials
+    u32* lm_ticket = nullptr;      // LM arrival counter
+    unsigned long long* dbg = nullptr;   // [64] device timestamps (development probe)
     double* poses = nullptr;       // [pose_cap * 7]
     float4* stage = nullptr;       // [2 * in_cap] host staging target
 

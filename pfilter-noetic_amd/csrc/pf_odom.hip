@@ -12,8 +12,8 @@
 //     p-index        (neighbour, query) pairs radix-sorted by neighbour: c_i(n) = earlier valid queries
 //                    sharing neighbour n reproduces the in-order increments of :345-346 / :493-496
 //     k_observe      observe/round skip test (:348-356, :497-505), kept flags, weight statistics
-//     LM             k_lm_init + 5 x (k_lm_eval, k_lm_step): Ceres 1.14 LM (Huber 0.1, Jacobi scaling,
-//                    radius 1e4, <= 4 iterations) on the 6x6 normal equations
+//     k_lm_solve     one workgroup runs Ceres 1.14 LM (Huber 0.1, Jacobi scaling, radius 1e4,
+//                    <= 4 iterations) on the 6x6 normal equations, all iterations in one launch
 //   k_finalize       odom from the solved pose (:278-280), pose output (node: copy.cpp:105-107)
 //   addPointsToMap   transform/append, CropBox +-100 m, rgbds (centroid + max r/g), extractstablepoint,
 //                    ageing (:589-647): batched keys / radix sort / segments / reduce / compaction
@@ -21,6 +21,7 @@
 #include "pf_geom.h"
 
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 
 namespace pf {
@@ -192,6 +193,11 @@ __global__ void __launch_bounds__(256) k_seg_starts(const u32* __restrict__ keys
     }
 }
 
+// one wave per voxel: lanes gather 64 members at a time, the running f32 sums then take them in
+// sorted (stable) order through readlane, so the order of additions is PCL's sequential one
+__device__ __forceinline__ float lane_f(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
 __global__ void __launch_bounds__(256) k_vg_reduce(const float4* __restrict__ e, const float4* __restrict__ s,
                                                     const u32* __restrict__ keys, const u32* __restrict__ vals,
                                                     const u32* __restrict__ segstart, int* __restrict__ cnt,
@@ -204,20 +210,39 @@ __global__ void __launch_bounds__(256) k_vg_reduce(const float4* __restrict__ e,
         cnt[C_SDS] = nseg - nse;
         cnt[C_NQ] = nseg;
     }
-    for (int sg = blockIdx.x * blockDim.x + threadIdx.x; sg < nseg; sg += gridDim.x * blockDim.x) {
+    const int l = lane_id();
+    const int waves = gridDim.x * (blockDim.x >> 6);
+    for (int sg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; sg < nseg; sg += waves) {
         const u32 b0 = segstart[sg], b1 = (sg + 1 < nseg) ? segstart[sg + 1] : (u32)n;
         const int c = (int)(keys[b0] >> 31);
         float sx = 0.f, sy = 0.f, sz = 0.f;
-        for (u32 k = b0; k < b1; ++k) {      // AccumulatorXYZ, sorted (stable) order
-            const u32 i = vals[k];
-            const float4 p = (int)i < n0 ? e[i] : s[i - n0];
-            sx += p.x; sy += p.y; sz += p.z;
+        for (u32 base = b0; base < b1; base += 8 * 64) {   // AccumulatorXYZ, sorted (stable) order
+            u32 idx[8];                                     // up to 512 members in flight at once
+            float4 p[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) idx[c] = base + c * 64 + l < b1 ? vals[base + c * 64 + l] : 0xFFFFFFFFu;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                p[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (idx[c] != 0xFFFFFFFFu) p[c] = (int)idx[c] < n0 ? e[idx[c]] : s[idx[c] - n0];
+            }
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int m = (int)min(64, (int)(b1 - base) - c * 64);
+                for (int j = 0; j < m; ++j) {
+                    sx += lane_f(p[c].x, j);
+                    sy += lane_f(p[c].y, j);
+                    sz += lane_f(p[c].z, j);
+                }
+            }
         }
-        const float nn = (float)(b1 - b0);
-        // rgb of inputs is 0 (copyPointCloud XYZI -> XYZRGB): averages stay 0
-        const float4 o = make_float4(sx / nn, sy / nn, sz / nn, __uint_as_float(0u));
-        if (c == 0) ds_e[sg] = o;
-        else ds_s[sg - nse] = o;
+        if (l == 0) {
+            const float nn = (float)(b1 - b0);
+            // rgb of inputs is 0 (copyPointCloud XYZI -> XYZRGB): averages stay 0
+            const float4 o = make_float4(sx / nn, sy / nn, sz / nn, __uint_as_float(0u));
+            if (c == 0) ds_e[sg] = o;
+            else ds_s[sg - nse] = o;
+        }
     }
 }
 
@@ -239,26 +264,59 @@ struct AssocArgs {
     u32* keys;
     u32* vals;
     u32 map_cap;
+    u32* lm_arrive;
 };
 
+// pointAssociateToMap + exact 5-NN, a team of kAssocTeam lanes per query (:297-300, :445-448)
+constexpr int kAssocTeam = 16;
+__global__ void __launch_bounds__(256) k_assoc_knn(AssocArgs a) {
+    const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
+    if (!a.st->gate) return;
+    double prm[7];
+    for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
+    const int tl = lane_id() & (kAssocTeam - 1);
+    const int teams = gridDim.x * (blockDim.x / kAssocTeam);
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int team = gt / kAssocTeam, wave_team0 = (gt & ~63) / kAssocTeam;
+    for (int off = 0; wave_team0 + off < nq; off += teams) {     // trip count uniform per wave
+        const int q0 = team + off;
+        const bool active = q0 < nq;
+        const int c = q0 < ne ? 0 : 1;
+        float4 pw = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (active) pw = associate(prm, c == 0 ? a.ds_e[q0] : a.ds_s[q0 - ne]);
+        float d[5];
+        int id[5];
+        const int found = knn5_team<kAssocTeam>(a.gv, c, pw.x, pw.y, pw.z, active, d, id);
+        if (active && tl < 5) {
+            int iv = id[0];
+#pragma unroll
+            for (int k = 1; k < 5; ++k)
+                if (tl == k) iv = id[k];
+            a.nbr[5 * q0 + tl] = found == 5 ? iv : -1;
+        }
+    }
+}
+
+// line fit (:302-331) / plane fit (:449-476), round and sparsity, p-index pair keys
 __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
     const int gate = a.st->gate;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *a.lm_arrive = 0u;                                     // LM arrival counter of this iteration
         a.cnt[C_NPAIR] = gate ? 5 * nq : 0;
         a.cnt[C_EDGE_KEPT] = a.cnt[C_SURF_KEPT] = a.cnt[C_EDGE_VALID] = a.cnt[C_SURF_VALID] = 0;
     }
     if (blockIdx.x == 0 && threadIdx.x < 8) a.acc[A_W + threadIdx.x] = (threadIdx.x & 1) ? 0u : 0xFFFFFFFFu;
-    if (!gate) return;
-    double prm[7];
-    for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
+    if (!gate) {                                   // solve skipped: no association is valid
+        for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) a.qflag[q] = 0;
+        return;
+    }
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
         const int c = q < ne ? 0 : 1;
-        const float4 p = c == 0 ? a.ds_e[q] : a.ds_s[q - ne];
-        const float4 pw = associate(prm, p);
-        float d[5];
         int id[5];
-        const int found = knn5(a.gv, c, pw.x, pw.y, pw.z, d, id);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) id[j] = a.nbr[5 * q + j];
+        const int found = id[4] >= 0 ? 5 : 0;
         bool valid = false;
         const float4* mp = c == 0 ? a.map_e : a.map_s;
         if (found == 5) {
@@ -322,7 +380,6 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
         const u32 off = c == 0 ? 0u : a.map_cap;
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
-            a.nbr[5 * q + j] = found == 5 ? id[j] : -1;
             a.keys[5 * q + j] = valid ? off + (u32)id[j] : kSentinel;
             a.vals[5 * q + j] = (u32)(5 * q + j);
         }
@@ -426,30 +483,18 @@ __global__ void __launch_bounds__(256) k_pidx_apply(const u32* __restrict__ keys
 }
 
 // ------------------------------------ LM (B.6) ----------------------------------------------
-__global__ void k_lm_init(const DevState* __restrict__ st, const int* __restrict__ cnt, const u32* __restrict__ acc,
-                          LMState* __restrict__ lm) {
-    if (threadIdx.x != 0) return;
-    const int nres = cnt[C_EDGE_KEPT] + cnt[C_SURF_KEPT];
-    double xn = 0;
-    for (int k = 0; k < 7; ++k) {
-        lm->x[k] = lm->cand[k] = lm->best[k] = st->params[k];
-        xn += lm->x[k] * lm->x[k];
-    }
-    lm->x_norm = sqrt(xn);
-    lm->radius = 1e4;
-    lm->decrease = 2.0;
-    lm->iteration = 0;
-    lm->invalid = 0;
-    lm->reuse = 0;
-    lm->phase = 0;
-    lm->n_res = nres;
-    lm->done = (!st->gate || nres == 0) ? 1 : 0;   // no residual blocks: parameter block untouched
-    for (int c = 0; c < 2; ++c)
-        for (int w = 0; w < 2; ++w) {
-            lm->wmin[c][w] = (double)ord2f(acc[A_W + 4 * c + 2 * w]);
-            lm->wmax[c][w] = (double)ord2f(acc[A_W + 4 * c + 2 * w + 1]);
-        }
-}
+// Ceres 1.14 trust-region loop of one outer iteration in ONE launch of kLmBlocks workgroups. Per
+// evaluation (<= 1 + kMaxIter = 5): every block evaluates a strided subset of the kept residual
+// blocks and reduces it to 30 partials (cost, g, upper J^T J, bad counts); lane 0 stores them and
+// arrives on a counter with an agent-scope release; every block waits for all arrivals (bounded
+// relaxed poll, one agent-scope acquire: cdna_hip_programming.md §6 G16), combines the partials in
+// block order and takes the LM step itself (TrustRegionMinimizer + LevenbergMarquardtStrategy).
+// The step is a deterministic function of identical inputs, so every block holds the same LM state
+// and no state is broadcast. 32 blocks of 256 threads are far below one wave per CU, so all blocks
+// are co-resident; a poll that exceeds its bound sets C_ERR and leaves (no hang).
+constexpr int kLmBlocks = 32;
+constexpr int kLmEvals = 5;
+constexpr unsigned kLmSpinLimit = 1u << 21;
 
 // observeMean (:136-160) / pointSparsityMean (.h:111-126) of one element, given min/max
 __device__ __forceinline__ double norm_weight(double e, double mn, double mx, bool clamp) {
@@ -463,266 +508,403 @@ __device__ __forceinline__ double norm_weight(double e, double mn, double mx, bo
     return e;
 }
 
-struct EvalArgs {
-    const LMState* lm;
-    const int* cnt;
+// packed symmetric 6x6: lm->H holds the upper triangle row by row (i <= j)
+__device__ __forceinline__ int hup(int i, int j) {
+    if (i > j) { const int t = i; i = j; j = t; }
+    return i * 6 - (i * (i - 1)) / 2 + (j - i);
+}
+__device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }   // lower, j <= i
+
+__device__ double grad_max_norm(const double* x, const double* g) {
+    double ng[6], xp[7];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) ng[j] = -g[j];
+    se3_plus(x, ng, xp);
+    double m = 0.0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) m = fmax(m, fabs(x[j] - xp[j]));
+    return m;
+}
+
+// The LM state lane 0 works on, held in registers during a step (loaded from / stored to the
+// LDS LMState around it); every loop is fully unrolled so all indices are static.
+struct LmCore {
+    double x[7], cand[7], best[7], scale[6], g[6], H[21], D[6];
+    double cost, radius, decrease, x_norm, min_cost, mcc;
+    int iteration, invalid, reuse, done, phase;
+};
+__device__ __forceinline__ void core_load(LmCore& c, const LMState& s) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { c.x[k] = s.x[k]; c.cand[k] = s.cand[k]; c.best[k] = s.best[k]; }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { c.scale[k] = s.scale[k]; c.g[k] = s.g[k]; c.D[k] = s.D[k]; }
+#pragma unroll
+    for (int k = 0; k < 21; ++k) c.H[k] = s.H[k];
+    c.cost = s.cost; c.radius = s.radius; c.decrease = s.decrease; c.x_norm = s.x_norm;
+    c.min_cost = s.min_cost; c.mcc = s.mcc;
+    c.iteration = s.iteration; c.invalid = s.invalid; c.reuse = s.reuse; c.done = s.done; c.phase = s.phase;
+}
+__device__ __forceinline__ void core_store(const LmCore& c, LMState& s) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { s.x[k] = c.x[k]; s.cand[k] = c.cand[k]; s.best[k] = c.best[k]; }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { s.scale[k] = c.scale[k]; s.g[k] = c.g[k]; s.D[k] = c.D[k]; }
+#pragma unroll
+    for (int k = 0; k < 21; ++k) s.H[k] = c.H[k];
+    s.cost = c.cost; s.radius = c.radius; s.decrease = c.decrease; s.x_norm = c.x_norm;
+    s.min_cost = c.min_cost; s.mcc = c.mcc;
+    s.iteration = c.iteration; s.invalid = c.invalid; s.reuse = c.reuse; s.done = c.done; s.phase = c.phase;
+}
+
+// TrustRegionMinimizer + LevenbergMarquardtStrategy: next candidate, or done. The scaled
+// J^T J + D is factored in place (packed lower Cholesky); Hs entries are recomputed from H.
+__device__ __forceinline__ void lm_next_step(LmCore& lm) {
+    const int kMaxIter = 4;
+    for (;;) {
+        lm.iteration++;
+        if (!lm.reuse) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j)
+                lm.D[j] = fmin(fmax(lm.scale[j] * lm.H[hup(j, j)] * lm.scale[j], 1e-6), 1e32);
+        }
+        double A[21], y[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j <= i; ++j) A[tri(i, j)] = lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const double ld = sqrt(lm.D[j] / lm.radius);
+            A[tri(j, j)] += ld * ld;
+        }
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+#pragma unroll
+            for (int j = 0; j <= i; ++j) {
+                double s = A[tri(i, j)];
+#pragma unroll
+                for (int k = 0; k < j; ++k) s -= A[tri(i, k)] * A[tri(j, k)];
+                if (i == j) {
+                    ok = ok && (s > 0.0);
+                    A[tri(i, i)] = sqrt(s);
+                } else {
+                    A[tri(i, j)] = s / A[tri(j, j)];
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            double s = lm.scale[i] * lm.g[i];
+#pragma unroll
+            for (int k = 0; k < i; ++k) s -= A[tri(i, k)] * y[k];
+            y[i] = s / A[tri(i, i)];
+        }
+#pragma unroll
+        for (int i = 5; i >= 0; --i) {
+            double s = y[i];
+#pragma unroll
+            for (int k = i + 1; k < 6; ++k) s -= A[tri(k, i)] * y[k];
+            y[i] = s / A[tri(i, i)];
+        }
+#pragma unroll
+        for (int j = 0; j < 6; ++j) ok = ok && isfinite(y[j]);
+        lm.reuse = 1;
+        double mcc = 0.0;
+        if (ok) {
+            double sg = 0.0, sHs = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                sg += -y[i] * (lm.scale[i] * lm.g[i]);
+                double hi = 0.0;
+#pragma unroll
+                for (int j = 0; j < 6; ++j) hi += lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j] * -y[j];
+                sHs += -y[i] * hi;
+            }
+            mcc = -(sg + 0.5 * sHs);
+        }
+        if (!ok || !(mcc > 0.0)) {                       // invalid step (HandleInvalidStep)
+            if (++lm.invalid >= 5) { lm.done = 1; return; }
+            lm.radius = lm.radius / lm.decrease;
+            lm.decrease *= 2.0;
+            if (lm.iteration >= kMaxIter || lm.radius <= 1e-32) { lm.done = 1; return; }
+            continue;
+        }
+        lm.invalid = 0;
+        double delta[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) delta[j] = -y[j] * lm.scale[j];
+        se3_plus(lm.x, delta, lm.cand);
+        lm.mcc = mcc;
+        lm.phase = 1;
+        return;
+    }
+}
+
+// Evaluation `tot` (cost, g, H, bad_r, bad_J) of lm.cand -> update the LM state (lane 0)
+__device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot) {
+    const double cost_c = tot[0];
+    const bool bad_r = tot[28] > 0.0, bad_j = tot[29] > 0.0;
+    const int kMaxIter = 4;
+    if (lm.phase == 0) {                                         // IterationZero
+        if (bad_r || bad_j) {
+            lm.done = 1;
+            return;
+        }
+        lm.cost = cost_c;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) lm.g[k] = tot[1 + k];
+#pragma unroll
+        for (int k = 0; k < 21; ++k) lm.H[k] = tot[7 + k];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) lm.scale[i] = 1.0 / (1.0 + sqrt(lm.H[hup(i, i)]));   // Jacobi, once
+        lm.min_cost = lm.cost;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) lm.best[k] = lm.x[k];
+        if (grad_max_norm(lm.x, lm.g) <= 1e-10) lm.done = 1;
+        else lm_next_step(lm);
+        return;
+    }
+    const double cand_cost = bad_r ? DBL_MAX : cost_c;           // candidate evaluated
+    double sn = 0.0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) sn += (lm.x[j] - lm.cand[j]) * (lm.x[j] - lm.cand[j]);
+    sn = sqrt(sn);
+    if (sn <= 1e-8 * (lm.x_norm + 1e-8)) {
+        lm.done = 1;                                             // parameter tolerance
+        return;
+    }
+    if (fabs(lm.cost - cand_cost) <= 1e-6 * lm.cost) {
+        lm.done = 1;                                             // function tolerance
+        return;
+    }
+    const double rel = (lm.cost - cand_cost) / lm.mcc;
+    bool step_ok = false;
+    if (rel > 1e-3) {
+        double xn = 0;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) { lm.x[j] = lm.cand[j]; xn += lm.x[j] * lm.x[j]; }
+        lm.x_norm = sqrt(xn);
+        if (bad_j) {
+            lm.done = 1;                                         // Jacobian evaluation failed
+            return;
+        }
+        lm.cost = cand_cost;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) lm.g[k] = tot[1 + k];
+#pragma unroll
+        for (int k = 0; k < 21; ++k) lm.H[k] = tot[7 + k];
+        const double f = 1.0 - pow(2.0 * rel - 1.0, 3.0);
+        lm.radius = lm.radius / fmax(1.0 / 3.0, f);
+        lm.radius = fmin(1e16, lm.radius);
+        lm.decrease = 2.0;
+        lm.reuse = 0;
+        step_ok = true;
+        if (lm.cost < lm.min_cost) {
+            lm.min_cost = lm.cost;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) lm.best[k] = lm.x[k];
+        }
+    } else {
+        lm.radius = lm.radius / lm.decrease;
+        lm.decrease *= 2.0;
+        lm.reuse = 1;
+    }
+    if (lm.iteration >= kMaxIter) lm.done = 1;
+    else if (step_ok && grad_max_norm(lm.x, lm.g) <= 1e-10) lm.done = 1;
+    else if (lm.radius <= 1e-32) lm.done = 1;
+    else lm_next_step(lm);
+}
+
+struct LmArgs {
+    DevState* st;
+    int* cnt;
+    const u32* acc;
+    LMState* lm_out;
+    double* part;          // [kLmEvals][kLmBlocks][32]
+    u32* arrive;           // arrival counter, zeroed by k_assoc
     const int* qflag;
     const float4* ds_e;
     const float4* ds_s;
     const double* geo;
     const float* observe;
     const float* spars;
-    double* part;
     int weight_type;
+    unsigned long long* dbg;
 };
 
-__global__ void __launch_bounds__(256) k_lm_eval(EvalArgs a) {
-    if (a.lm->done) return;
-    __shared__ double red[4][kLmParts];
-    const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
-    double x[7];
-    for (int k = 0; k < 7; ++k) x[k] = a.lm->cand[k];
-    double acc[kLmParts];
-#pragma unroll
-    for (int k = 0; k < kLmParts; ++k) acc[k] = 0.0;
-    const int wt = a.weight_type;
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
-        if (!(a.qflag[q] & 2)) continue;
-        const int c = q < ne ? 0 : 1;
-        const float4 p = c == 0 ? a.ds_e[q] : a.ds_s[q - ne];
-        const d3 cur{(double)p.x, (double)p.y, (double)p.z};
-        double w = 0.0;
-        if (wt != 0) {
-            const double wo = norm_weight((double)a.observe[q], a.lm->wmin[c][0], a.lm->wmax[c][0], true);
-            const double ws = norm_weight((double)a.spars[q], a.lm->wmin[c][1], a.lm->wmax[c][1], false);
-            if (wt == 1) w = wo;
-            else if (wt == 2) w = ws;
-            else w = c == 0 ? (ws + wo) / 2 : (wo + ws) / 2;
-        }
-        const double* G = a.geo + 8 * (size_t)q;
-        double J[6];
-        double r = c == 0 ? edge_eval(x, cur, d3{G[0], G[1], G[2]}, d3{G[3], G[4], G[5]}, w, J)
-                          : surf_eval(x, cur, d3{G[0], G[1], G[2]}, G[3], w, J);
-        bool jbad = false;
-        for (int k = 0; k < 6; ++k) jbad |= !isfinite(J[k]);
-        if (!isfinite(r)) { acc[28] += 1.0; continue; }
-        if (jbad) acc[29] += 1.0;
-        const double s = r * r;                                    // HuberLoss(0.1) + Corrector
-        double rho0, rho1;
-        if (s > 0.1 * 0.1) {
-            const double rr = sqrt(s);
-            rho0 = 2.0 * 0.1 * rr - 0.1 * 0.1;
-            rho1 = fmax(DBL_MIN, 0.1 / rr);
-        } else {
-            rho0 = s;
-            rho1 = 1.0;
-        }
-        acc[0] += 0.5 * rho0;
-        const double sr = sqrt(rho1);
-        r *= sr;
-        for (int k = 0; k < 6; ++k) J[k] *= sr;
-        for (int k = 0; k < 6; ++k) acc[1 + k] += J[k] * r;
-        int h = 7;
-        for (int i = 0; i < 6; ++i)
-            for (int j = i; j < 6; ++j) acc[h++] += J[i] * J[j];
-    }
-    const int w = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < kLmParts; ++k) {
-        const double v = wave_sum(acc[k]);
-        if (lane_id() == 0) red[w][k] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < kLmParts) {
-        const int k = threadIdx.x;
-        a.part[blockIdx.x * 32 + k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
-    }
-}
-
-__device__ bool chol6(const double* H, const double* g, double* y) {
-    double L[36];
-    for (int i = 0; i < 36; ++i) L[i] = 0.0;
-    for (int i = 0; i < 6; ++i) {
-        for (int j = 0; j <= i; ++j) {
-            double s = H[i * 6 + j];
-            for (int k = 0; k < j; ++k) s -= L[i * 6 + k] * L[j * 6 + k];
-            if (i == j) {
-                if (!(s > 0.0)) return false;
-                L[i * 6 + i] = sqrt(s);
-            } else {
-                L[i * 6 + j] = s / L[j * 6 + j];
-            }
-        }
-    }
-    double z[6];
-    for (int i = 0; i < 6; ++i) {
-        double s = g[i];
-        for (int k = 0; k < i; ++k) s -= L[i * 6 + k] * z[k];
-        z[i] = s / L[i * 6 + i];
-    }
-    for (int i = 5; i >= 0; --i) {
-        double s = z[i];
-        for (int k = i + 1; k < 6; ++k) s -= L[k * 6 + i] * y[k];
-        y[i] = s / L[i * 6 + i];
-    }
-    return true;
-}
-
-__device__ double grad_max_norm(const double* x, const double* g) {
-    double ng[6], xp[7];
-    for (int j = 0; j < 6; ++j) ng[j] = -g[j];
-    se3_plus(x, ng, xp);
-    double m = 0.0;
-    for (int j = 0; j < 7; ++j) m = fmax(m, fabs(x[j] - xp[j]));
-    return m;
-}
-
-__device__ __forceinline__ void full_h(const double* h21, double* H) {
-    int h = 0;
-    for (int i = 0; i < 6; ++i)
-        for (int j = i; j < 6; ++j) { H[i * 6 + j] = h21[h]; H[j * 6 + i] = h21[h]; ++h; }
-}
-
-// TrustRegionMinimizer + LevenbergMarquardtStrategy state machine (one lane)
-__device__ void lm_next_step(LMState* lm, int* cnt) {
-    const int kMaxIter = 4;
-    double H[36];
-    full_h(lm->H, H);
-    for (;;) {
-        lm->iteration++;
-        double Hs[36], gs[6];
-        for (int i = 0; i < 6; ++i) {
-            gs[i] = lm->scale[i] * lm->g[i];
-            for (int j = 0; j < 6; ++j) Hs[i * 6 + j] = lm->scale[i] * H[i * 6 + j] * lm->scale[j];
-        }
-        if (!lm->reuse)
-            for (int j = 0; j < 6; ++j) lm->D[j] = fmin(fmax(Hs[j * 6 + j], 1e-6), 1e32);
-        double A[36], y[6];
-        for (int i = 0; i < 36; ++i) A[i] = Hs[i];
-        for (int j = 0; j < 6; ++j) {
-            const double ld = sqrt(lm->D[j] / lm->radius);
-            A[j * 6 + j] += ld * ld;
-        }
-        bool ok = chol6(A, gs, y);
-        for (int j = 0; j < 6; ++j) ok = ok && isfinite(y[j]);
-        lm->reuse = 1;
-        double step[6], mcc = 0.0;
-        if (ok) {
-            for (int j = 0; j < 6; ++j) step[j] = -y[j];
-            double sg = 0.0, sHs = 0.0;
-            for (int i = 0; i < 6; ++i) {
-                sg += step[i] * gs[i];
-                double hi = 0.0;
-                for (int j = 0; j < 6; ++j) hi += Hs[i * 6 + j] * step[j];
-                sHs += step[i] * hi;
-            }
-            mcc = -(sg + 0.5 * sHs);
-        }
-        if (!ok || !(mcc > 0.0)) {                       // invalid step (HandleInvalidStep)
-            if (++lm->invalid >= 5) { lm->done = 1; return; }
-            lm->radius = lm->radius / lm->decrease;
-            lm->decrease *= 2.0;
-            if (lm->iteration >= kMaxIter || lm->radius <= 1e-32) { lm->done = 1; return; }
-            continue;
-        }
-        lm->invalid = 0;
-        double delta[6];
-        for (int j = 0; j < 6; ++j) delta[j] = step[j] * lm->scale[j];
-        se3_plus(lm->x, delta, lm->cand);
-        lm->mcc = mcc;
-        lm->phase = 1;
-        return;
-    }
-}
-
-__global__ void __launch_bounds__(256) k_lm_step(LMState* __restrict__ lm, const double* __restrict__ part,
-                                                  DevState* __restrict__ st, int* __restrict__ cnt) {
-    __shared__ double sub[kLmParts][8];
+__global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
+    unsigned long long* dbg = a.dbg;
+    const bool rec = dbg && blockIdx.x == 0 && threadIdx.x == 0;
+    if (rec) dbg[0] = __builtin_amdgcn_s_memrealtime();
+    __shared__ double rows[256][8];                             // per residual: J[6], r, 0.5 rho
+    __shared__ double red9[28][9];
+    __shared__ int nbad[2];
+    __shared__ unsigned char hi_[21], hj_[21];
     __shared__ double tot[kLmParts];
-    if (lm->done) return;
+    __shared__ LMState lm;
+    __shared__ int aborted;
     const int t = threadIdx.x;
-    if (t < kLmParts * 8) {
-        const int k = t >> 3, s = t & 7;
-        double v = 0.0;
-        for (int b = s * (kLmBlocks / 8); b < (s + 1) * (kLmBlocks / 8); ++b) v += part[b * 32 + k];
-        sub[k][s] = v;
-    }
-    __syncthreads();
-    if (t < kLmParts) {
-        double v = 0.0;
-        for (int s = 0; s < 8; ++s) v += sub[t][s];
-        tot[t] = v;
-    }
-    __syncthreads();
-    if (t != 0) return;
-    const double cost_c = tot[0];
-    const bool bad_r = tot[28] > 0.0, bad_j = tot[29] > 0.0;
-    const int kMaxIter = 4;
-    if (lm->phase == 0) {                                        // IterationZero
-        if (bad_r || bad_j) {
-            lm->done = 1;
-        } else {
-            lm->cost = cost_c;
-            for (int k = 0; k < 6; ++k) lm->g[k] = tot[1 + k];
-            for (int k = 0; k < 21; ++k) lm->H[k] = tot[7 + k];
-            int d = 0;
-            for (int i = 0; i < 6; ++i) {
-                lm->scale[i] = 1.0 / (1.0 + sqrt(lm->H[d]));     // Jacobi scaling, computed once
-                d += 6 - i;
-            }
-            lm->min_cost = lm->cost;
-            for (int k = 0; k < 7; ++k) lm->best[k] = lm->x[k];
-            if (grad_max_norm(lm->x, lm->g) <= 1e-10) lm->done = 1;
-            else lm_next_step(lm, cnt);
+    const int nres = a.cnt[C_EDGE_KEPT] + a.cnt[C_SURF_KEPT];
+    if (!a.st->gate || nres == 0) return;                        // no residual blocks: untouched
+    double wmin[2][2], wmax[2][2];
+    for (int c = 0; c < 2; ++c)
+        for (int ww = 0; ww < 2; ++ww) {
+            wmin[c][ww] = (double)ord2f(a.acc[A_W + 4 * c + 2 * ww]);
+            wmax[c][ww] = (double)ord2f(a.acc[A_W + 4 * c + 2 * ww + 1]);
         }
-    } else {                                                     // candidate evaluated
-        const double cand_cost = bad_r ? DBL_MAX : cost_c;
-        double sn = 0.0;
-        for (int j = 0; j < 7; ++j) sn += (lm->x[j] - lm->cand[j]) * (lm->x[j] - lm->cand[j]);
-        sn = sqrt(sn);
-        if (sn <= 1e-8 * (lm->x_norm + 1e-8)) {
-            lm->done = 1;                                        // parameter tolerance
-        } else if (fabs(lm->cost - cand_cost) <= 1e-6 * lm->cost) {
-            lm->done = 1;                                        // function tolerance
-        } else {
-            const double rel = (lm->cost - cand_cost) / lm->mcc;
-            bool step_ok = false;
-            if (rel > 1e-3) {
-                double xn = 0;
-                for (int j = 0; j < 7; ++j) { lm->x[j] = lm->cand[j]; xn += lm->x[j] * lm->x[j]; }
-                lm->x_norm = sqrt(xn);
-                if (bad_j) {
-                    lm->done = 1;                                // Jacobian evaluation failed
-                } else {
-                    lm->cost = cand_cost;
-                    for (int k = 0; k < 6; ++k) lm->g[k] = tot[1 + k];
-                    for (int k = 0; k < 21; ++k) lm->H[k] = tot[7 + k];
-                    const double f = 1.0 - pow(2.0 * rel - 1.0, 3.0);
-                    lm->radius = lm->radius / fmax(1.0 / 3.0, f);
-                    lm->radius = fmin(1e16, lm->radius);
-                    lm->decrease = 2.0;
-                    lm->reuse = 0;
-                    step_ok = true;
-                    if (lm->cost < lm->min_cost) {
-                        lm->min_cost = lm->cost;
-                        for (int k = 0; k < 7; ++k) lm->best[k] = lm->x[k];
-                    }
+    if (t == 0) {                                                // problem set-up (:252-266)
+        double xn = 0;
+        for (int k = 0; k < 7; ++k) {
+            lm.x[k] = lm.cand[k] = lm.best[k] = a.st->params[k];
+            xn += lm.x[k] * lm.x[k];
+        }
+        lm.x_norm = sqrt(xn);
+        lm.radius = 1e4;
+        lm.decrease = 2.0;
+        lm.iteration = lm.invalid = lm.reuse = lm.phase = 0;
+        lm.n_res = nres;
+        lm.done = 0;
+        aborted = 0;
+        int h = 0;
+        for (int i = 0; i < 6; ++i)
+            for (int j = i; j < 6; ++j) { hi_[h] = (unsigned char)i; hj_[h] = (unsigned char)j; ++h; }
+    }
+    __syncthreads();
+    const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
+    const int wt = a.weight_type;
+    // reduction roles: thread (k, p) sums product k (0: cost, 1-6: g, 7-27: upper J^T J) over the
+    // chunk rows p, p + 9, ...; 28 x 9 = 252 threads
+    const int rk = t / 9, rp = t % 9;
+    const int ri = rk >= 7 && rk < 28 ? hi_[rk - 7] : 0, rj_ = rk >= 7 && rk < 28 ? hj_[rk - 7] : 0;
+    for (int ev = 0; ev < kLmEvals; ++ev) {
+        if (lm.done || aborted) break;                           // uniform: every block steps alike
+        double x[7];
+        for (int k = 0; k < 7; ++k) x[k] = lm.cand[k];
+        if (t < 2) nbad[t] = 0;
+        double part = 0.0;
+        for (int base = blockIdx.x * 256; base < nq; base += gridDim.x * 256) {
+            const int q = base + t;
+            double J[6] = {0, 0, 0, 0, 0, 0}, r = 0.0, hc = 0.0;
+            if (q < nq && (a.qflag[q] & 2)) {
+                const int c = q < ne ? 0 : 1;
+                const float4 p = c == 0 ? a.ds_e[q] : a.ds_s[q - ne];
+                const d3 cur{(double)p.x, (double)p.y, (double)p.z};
+                double wgt = 0.0;
+                if (wt != 0) {
+                    const double wo = norm_weight((double)a.observe[q], wmin[c][0], wmax[c][0], true);
+                    const double ws = norm_weight((double)a.spars[q], wmin[c][1], wmax[c][1], false);
+                    if (wt == 1) wgt = wo;
+                    else if (wt == 2) wgt = ws;
+                    else wgt = c == 0 ? (ws + wo) / 2 : (wo + ws) / 2;
                 }
-            } else {
-                lm->radius = lm->radius / lm->decrease;
-                lm->decrease *= 2.0;
-                lm->reuse = 1;
+                const double* G = a.geo + 8 * (size_t)q;
+                r = c == 0 ? edge_eval(x, cur, d3{G[0], G[1], G[2]}, d3{G[3], G[4], G[5]}, wgt, J)
+                           : surf_eval(x, cur, d3{G[0], G[1], G[2]}, G[3], wgt, J);
+                bool jbad = false;
+                for (int k = 0; k < 6; ++k) jbad |= !isfinite(J[k]);
+                if (!isfinite(r)) {
+                    atomicAdd(&nbad[0], 1);
+                    r = 0.0;
+                    for (int k = 0; k < 6; ++k) J[k] = 0.0;
+                } else {
+                    if (jbad) atomicAdd(&nbad[1], 1);
+                    const double s = r * r;                      // HuberLoss(0.1) + Corrector
+                    double rho0, rho1;
+                    if (s > 0.1 * 0.1) {
+                        const double rr = sqrt(s);
+                        rho0 = 2.0 * 0.1 * rr - 0.1 * 0.1;
+                        rho1 = fmax(DBL_MIN, 0.1 / rr);
+                    } else {
+                        rho0 = s;
+                        rho1 = 1.0;
+                    }
+                    hc = 0.5 * rho0;
+                    const double sr = sqrt(rho1);
+                    r *= sr;
+                    for (int k = 0; k < 6; ++k) J[k] *= sr;
+                }
             }
-            if (!lm->done) {
-                if (lm->iteration >= kMaxIter) lm->done = 1;
-                else if (step_ok && grad_max_norm(lm->x, lm->g) <= 1e-10) lm->done = 1;
-                else if (lm->radius <= 1e-32) lm->done = 1;
-                else lm_next_step(lm, cnt);
+            for (int k = 0; k < 6; ++k) rows[t][k] = J[k];
+            rows[t][6] = r;
+            rows[t][7] = hc;
+            __syncthreads();
+            if (rk < 28) {                                       // rows rp*29 .. rp*29+28
+                const int ca = rk == 0 ? 7 : (rk < 7 ? rk - 1 : ri), cb = rk == 0 ? -1 : (rk < 7 ? 6 : rj_);
+                double pa[29], pb[29];
+#pragma unroll
+                for (int i = 0; i < 29; ++i) {
+                    const int j = rp * 29 + i;
+                    pa[i] = j < 256 ? rows[j][ca] : 0.0;
+                    pb[i] = (j < 256 && cb >= 0) ? rows[j][cb] : 1.0;
+                }
+#pragma unroll
+                for (int i = 0; i < 29; ++i) part += pa[i] * pb[i];
+            }
+            __syncthreads();
+        }
+        if (rec) dbg[1 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
+        if (rk < 28) red9[rk][rp] = part;
+        __syncthreads();
+        double* P = a.part + (size_t)ev * kLmBlocks * 32;
+        // publish: write-through (agent-scope atomic) stores of the 30 partials, drained by wave 0,
+        // then a relaxed arrival; consumers poll relaxed and read the partials with agent-scope
+        // atomic loads, so no release / acquire fence is needed (cdna_hip_programming.md §6 G16)
+        if (t < 28) {
+            double v = red9[t][0];
+            for (int k = 1; k < 9; ++k) v += red9[t][k];
+            __hip_atomic_store(P + 32 * blockIdx.x + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (t < 30) {
+            __hip_atomic_store(P + 32 * blockIdx.x + t, (double)nbad[t - 28], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (rec) dbg[2 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
+        if (t < 64) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (t == 0) {
+                __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const u32 target = (u32)(ev + 1) * gridDim.x;
+                unsigned spins = 0;
+                while (__hip_atomic_load(a.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                    if (++spins > kLmSpinLimit) {
+                        aborted = 1;
+                        a.cnt[C_ERR] = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
             }
         }
+        __syncthreads();
+        if (aborted) break;
+        if (rec) dbg[3 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
+        if (t < kLmParts) {
+            double pv[kLmBlocks];                                // all loads in flight, then the sum
+#pragma unroll
+            for (int b = 0; b < kLmBlocks; ++b)
+                pv[b] = __hip_atomic_load(P + 32 * b + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            double v = 0.0;
+#pragma unroll
+            for (int b = 0; b < kLmBlocks; ++b) v += pv[b];
+            tot[t] = v;
+        }
+        __syncthreads();
+        if (rec) dbg[40 + ev] = __builtin_amdgcn_s_memrealtime();
+        if (t == 0) {
+            LmCore c;
+            core_load(c, lm);
+            lm_accept(c, tot);
+            if (ev == kLmEvals - 1) c.done = 1;
+            core_store(c, lm);
+        }
+        __syncthreads();
+        if (rec) dbg[4 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
     }
-    for (int k = 0; k < 7; ++k) st->params[k] = lm->best[k];
-    if (lm->done) atomicAdd(&cnt[C_LM_ITERS], lm->iteration);
+    if (blockIdx.x == 0 && t == 0) {
+        for (int k = 0; k < 7; ++k) a.st->params[k] = lm.best[k];
+        atomicAdd(&a.cnt[C_LM_ITERS], lm.iteration);
+        *a.lm_out = lm;
+    }
 }
 
 // ---------------------------------- pose / map update ---------------------------------------
@@ -949,6 +1131,8 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     o.sort_cap = 2 * map_cap + 2 * in_cap;
     if (o.sort_cap < 10 * in_cap) o.sort_cap = 10 * in_cap;
     o.pose_cap = (size_t)1 << 20;
+    o.pidx_bits = 1;
+    while (((size_t)1 << o.pidx_bits) <= 2 * map_cap && o.pidx_bits < 32) ++o.pidx_bits;
     o.leaf_vg[0] = (float)prm.map_res;
     o.leaf_vg[1] = (float)(prm.map_res * 2);
     o.leaf_rg[0] = (float)prm.map_res;
@@ -984,16 +1168,21 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.segstart, sizeof(u32) * (o.sort_cap + 1));
     PF_ALLOC(o.nbr, sizeof(int) * 5 * nq);
     PF_ALLOC(o.qflag, sizeof(int) * nq);
+    PF_ALLOC(o.lm_part, sizeof(double) * kLmEvals * kLmBlocks * 32);
+    PF_ALLOC(o.lm_ticket, sizeof(u32) * 4);
     PF_ALLOC(o.geo, sizeof(double) * 8 * nq);
     PF_ALLOC(o.spars, sizeof(float) * nq);
     PF_ALLOC(o.roundv, sizeof(float) * nq);
     PF_ALLOC(o.observe, sizeof(float) * nq);
     PF_ALLOC(o.pcnt, sizeof(u32) * 5 * nq);
     PF_ALLOC(o.tailinc, sizeof(u32) * (o.sort_cap + 1));
-    PF_ALLOC(o.lm_part, sizeof(double) * kLmBlocks * 32);
     PF_ALLOC(o.poses, sizeof(double) * 7 * o.pose_cap);
     PF_ALLOC(o.stage, sizeof(float4) * 2 * in_cap);
 #undef PF_ALLOC
+    if (std::getenv("PF_PROBE")) {                 // development probe: LM phase timestamps
+        if (hipMalloc(&o.dbg, sizeof(unsigned long long) * 64) != hipSuccess) return PF_ENOMEM;
+        if (hipMemset(o.dbg, 0, sizeof(unsigned long long) * 64) != hipSuccess) return PF_EHIP;
+    }
     if (hipHostMalloc(&o.h_cnt, sizeof(int) * C_COUNT) != hipSuccess) return PF_ENOMEM;
     if (hipHostMalloc(&o.h_pose, sizeof(double) * 8) != hipSuccess) return PF_ENOMEM;
     // init (:182-208): identity odom / last_odom, parameters {0,0,0,1,0,0,0}, optimization_count 2
@@ -1005,6 +1194,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (hipMemset(o.cnt, 0, sizeof(int) * C_COUNT) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.acc, 0, sizeof(u32) * A_COUNT) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.lm, 0, sizeof(LMState)) != hipSuccess) return PF_EHIP;
+    if (hipMemset(o.lm_ticket, 0, sizeof(u32) * 4) != hipSuccess) return PF_EHIP;
     o.opt_count_host = 2;
     return PF_OK;
 }
@@ -1016,7 +1206,7 @@ void odom_destroy(OdomGPU& o) {
     prim_free(o.prim);
     void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.in_edge, o.in_surf, o.ds_edge, o.ds_surf, o.map_e, o.map_s,
                     o.app_e, o.app_s, o.seg_out, o.keys, o.vals, o.flags, o.scan_out, o.segstart, o.nbr,
-                    o.qflag, o.geo, o.spars, o.roundv, o.observe, o.pcnt, o.tailinc, o.lm_part, o.poses, o.stage};
+                    o.qflag, o.lm_part, o.lm_ticket, o.geo, o.spars, o.roundv, o.observe, o.pcnt, o.tailinc, o.poses, o.stage, o.dbg};
     for (void* p : ptrs) (void)hipFree(p);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
     if (o.h_pose) (void)hipHostFree(o.h_pose);
@@ -1045,29 +1235,29 @@ void odom_enqueue_update(OdomGPU& o, hipStream_t s) {
     scan_exclusive(o.flags, o.scan_out, cnt + C_VGN, (u32*)(cnt + C_NSEG), o.prim, s);
     hipLaunchKernelGGL(k_seg_starts, dim3(kGrid), dim3(256), 0, s, o.keys, cnt + C_VGN, o.flags, o.scan_out,
                        o.segstart, cnt);
-    hipLaunchKernelGGL(k_vg_reduce, dim3(kGrid), dim3(256), 0, s, o.in_edge, o.in_surf, o.keys, o.vals, o.segstart,
-                       cnt, o.ds_edge, o.ds_surf);
+    hipLaunchKernelGGL(k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, o.in_edge, o.in_surf, o.keys, o.vals,
+                       o.segstart, cnt, o.ds_edge, o.ds_surf);
     // grids of the edge / surf maps (kd-tree build, :249-250)
     grid_build(o.grid, o.map_e, cnt + C_ME, o.map_s, cnt + C_MS, o.prim, s);
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
         AssocArgs aa{o.st, cnt, o.acc, gv, o.ds_edge, o.ds_surf, o.map_e, o.map_s, o.nbr, o.qflag, o.geo, o.spars,
-                     o.roundv, o.keys, o.vals, (u32)o.map_cap};
+                     o.roundv, o.keys, o.vals, (u32)o.map_cap, o.lm_ticket};
+        hipLaunchKernelGGL(k_assoc_knn, dim3(kGrid), dim3(256), 0, s, aa);
         hipLaunchKernelGGL(k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
-        radix_sort_pairs(o.keys, o.vals, cnt + C_NPAIR, 32, o.prim, s);
-        hipLaunchKernelGGL(k_pidx_count, dim3(kGrid), dim3(256), 0, s, o.keys, o.vals, cnt, o.pcnt, o.tailinc);
+        // pair keys are < 2 * map_cap (surf maps offset by map_cap) or the all-ones sentinel, so the
+        // low pidx_bits bits order them
+        u32 *pk, *pv;
+        radix_sort_pairs(o.keys, o.vals, cnt + C_NPAIR, o.pidx_bits, o.prim, s, &pk, &pv);
+        hipLaunchKernelGGL(k_pidx_count, dim3(kGrid), dim3(256), 0, s, pk, pv, cnt, o.pcnt, o.tailinc);
         ObsArgs oa{cnt, o.acc, o.map_e, o.map_s, o.ds_edge, o.ds_surf, o.nbr, o.qflag, o.pcnt, o.roundv, o.spars,
                    o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
         hipLaunchKernelGGL(k_observe, dim3(kGrid), dim3(256), 0, s, oa);
-        hipLaunchKernelGGL(k_pidx_apply, dim3(kGrid), dim3(256), 0, s, o.keys, o.tailinc, cnt, o.map_e, o.map_s,
+        hipLaunchKernelGGL(k_pidx_apply, dim3(kGrid), dim3(256), 0, s, pk, o.tailinc, cnt, o.map_e, o.map_s,
                            (u32)o.map_cap);
-        hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(64), 0, s, o.st, cnt, o.acc, o.lm);
-        EvalArgs ea{o.lm, cnt, o.qflag, o.ds_edge, o.ds_surf, o.geo, o.observe, o.spars, o.lm_part,
-                    o.prm.weight_type};
-        for (int e = 0; e < 5; ++e) {
-            hipLaunchKernelGGL(k_lm_eval, dim3(kLmBlocks), dim3(256), 0, s, ea);
-            hipLaunchKernelGGL(k_lm_step, dim3(1), dim3(256), 0, s, o.lm, o.lm_part, o.st, cnt);
-        }
+        LmArgs la{o.st, cnt, o.acc, o.lm, o.lm_part, o.lm_ticket, o.qflag, o.ds_edge, o.ds_surf, o.geo, o.observe,
+                  o.spars, o.prm.weight_type, o.dbg};
+        hipLaunchKernelGGL(k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
     }
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, o.st, o.poses, (int)o.pose_cap, 1, o.acc);
     // addPointsToMap (:589-647)

@@ -9,19 +9,24 @@ constexpr int kSortTile = 2048;       // keys per tile (256 threads x 8)
 constexpr int kScanTile = 1024;       // items per scan tile (256 threads x 4)
 
 struct PrimWork {
-    u32* hist = nullptr;       // 256 * kSortMaxBlocks
-    u32* partials = nullptr;   // kSortMaxBlocks + 1
+    u32* partials = nullptr;   // kSortMaxBlocks + 1 (scan)
     u32* keys_tmp = nullptr;   // cap
     u32* vals_tmp = nullptr;   // cap
-    size_t cap = 0;
+    u32* bhist = nullptr;      // [4 passes][kSortMaxBlocks][256] per-block digit counts
+    u64* status = nullptr;     // [4 passes][max_tiles][256] look-back words
+    u32* tickets = nullptr;    // [4] tile tickets per pass
+    int* err = nullptr;        // look-back spin limit hit (never expected)
+    size_t cap = 0, max_tiles = 0;
 };
 
 int prim_alloc(PrimWork& w, size_t cap);
 void prim_free(PrimWork& w);
 
-// Stable sort of (keys, vals)[0 .. *d_n) by the low `bits` bits of keys (8-bit digits, an even
-// number of passes, so the result is back in keys/vals).
-void radix_sort_pairs(u32* keys, u32* vals, const int* d_n, int bits, PrimWork& w, hipStream_t s);
+// Stable sort of (keys, vals)[0 .. *d_n) by the low `bits` bits of keys (8-bit digits). With kout/vout
+// null the pass count is rounded up to even so the result is back in keys/vals; otherwise *kout/*vout
+// name the buffers holding the result (keys/vals or the PrimWork scratch).
+void radix_sort_pairs(u32* keys, u32* vals, const int* d_n, int bits, PrimWork& w, hipStream_t s,
+                      u32** kout = nullptr, u32** vout = nullptr);
 
 // out[i] = sum(in[0..i)) for i < *d_n; *d_total = sum(in[0..n)) when d_total != nullptr.
 void scan_exclusive(const u32* in, u32* out, const int* d_n, u32* d_total, PrimWork& w, hipStream_t s);

@@ -42,97 +42,145 @@ __device__ __forceinline__ u32 block_excl_scan256(u32 v, u32* lds_w, u32& total)
     return off + inc - v;
 }
 
-__global__ void __launch_bounds__(256) k_rs_hist(const u32* __restrict__ keys, const int* __restrict__ d_n, int shift,
-                                                  u32* __restrict__ hist) {
-    __shared__ u32 lh[256];
+// ---- radix sort: one histogram kernel for every pass, then one kernel per 8-bit pass ----
+// Each pass kernel hands out 2048-key tiles in ticket order; a tile ranks its keys stably (wave
+// match + per-wave digit counts), publishes its per-digit counts, and finds its exclusive prefix by
+// decoupled look-back over the earlier tiles' status words. A status word carries its own payload
+// (tag << 32 | count; tag 1 = tile count, 2 = inclusive prefix), written and polled with agent-scope
+// atomics, so no separate fence is needed (cdna_hip_programming.md §6 G16, R2). Tickets make the
+// protocol independent of dispatch order: a tile only waits for tiles already taken by running blocks.
+constexpr int kOsThreads = 256;
+constexpr int kOsPer = kSortTile / kOsThreads;   // 8 keys per thread per tile
+constexpr unsigned kSpinLimit = 1u << 22;
+
+__global__ void __launch_bounds__(256) k_os_hist(const u32* __restrict__ keys, const int* __restrict__ d_n, int passes,
+                                                  u32* __restrict__ bhist, u64* __restrict__ status,
+                                                  u32* __restrict__ tickets) {
+    __shared__ u32 lh[4][256];
     const int n = *d_n;
     const int G = eff_blocks(n, kSortTile);
-    const int b = blockIdx.x;
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int ntiles = (n + kSortTile - 1) / kSortTile;
+    // reset this sort's look-back state (visible to the pass kernels at the kernel boundary)
+    for (size_t i = (size_t)b * 256 + t; i < (size_t)passes * ntiles * 256; i += (size_t)gridDim.x * 256)
+        status[i] = 0ull;
+    if (b == 0 && t < 4) tickets[t] = 0u;
     if (b >= G) return;
-    const int nt = (n + kSortTile - 1) / kSortTile;
-    const int tpb = (nt + G - 1) / G;
+    for (int p = 0; p < 4; ++p) lh[p][t] = 0;
+    __syncthreads();
+    const int tpb = (ntiles + G - 1) / G;
     const int i0 = b * tpb * kSortTile;
     int i1 = (b + 1) * tpb * kSortTile;
     if (i1 > n) i1 = n;
-    lh[threadIdx.x] = 0;
-    __syncthreads();
-    for (int i = i0 + threadIdx.x; i < i1; i += 256) atomicAdd(&lh[(keys[i] >> shift) & 255u], 1u);
-    __syncthreads();
-    hist[threadIdx.x * kSortMaxBlocks + b] = lh[threadIdx.x];
-}
-
-// exclusive scan of hist in (digit, block) order, in place
-__global__ void __launch_bounds__(1024) k_rs_scan(u32* __restrict__ hist, const int* __restrict__ d_n) {
-    __shared__ u32 lw[16];
-    const int n = *d_n;
-    const int G = eff_blocks(n, kSortTile);
-    if (G == 0) return;
-    const int total = 256 * G;
-    const int per = (total + 1023) / 1024;
-    const int t = threadIdx.x;
-    const int e0 = t * per;
-    u32 s = 0;
-    for (int e = e0; e < e0 + per && e < total; ++e) s += hist[(e / G) * kSortMaxBlocks + (e % G)];
-    // block scan of s (16 waves)
-    const int w = t >> 6, l = lane_id();
-    u32 inc = wave_incl_scan(s);
-    if (l == 63) lw[w] = inc;
-    __syncthreads();
-    u32 off = 0;
-    for (int i = 0; i < w; ++i) off += lw[i];
-    u32 run = off + inc - s;
-    for (int e = e0; e < e0 + per && e < total; ++e) {
-        u32* p = &hist[(e / G) * kSortMaxBlocks + (e % G)];
-        u32 c = *p;
-        *p = run;
-        run += c;
+    for (int i = i0 + t; i < i1; i += 256) {
+        const u32 k = keys[i];
+        for (int p = 0; p < passes; ++p) atomicAdd(&lh[p][(k >> (8 * p)) & 255u], 1u);
     }
+    __syncthreads();
+    for (int p = 0; p < passes; ++p) bhist[((size_t)p * kSortMaxBlocks + b) * 256 + t] = lh[p][t];
 }
 
-__global__ void __launch_bounds__(256) k_rs_scatter(const u32* __restrict__ kin, const u32* __restrict__ vin,
-                                                     u32* __restrict__ kout, u32* __restrict__ vout,
-                                                     const int* __restrict__ d_n, int shift,
-                                                     const u32* __restrict__ hist) {
+__global__ void __launch_bounds__(kOsThreads) k_os_pass(const u32* __restrict__ kin, const u32* __restrict__ vin,
+                                                         u32* __restrict__ kout, u32* __restrict__ vout,
+                                                         const int* __restrict__ d_n, int pass,
+                                                         const u32* __restrict__ bhist, u64* __restrict__ status,
+                                                         u32* __restrict__ tickets, int* __restrict__ err) {
+    __shared__ u32 dbase[256];
     __shared__ u32 run[256];
     __shared__ u32 wcnt[4][256];
+    __shared__ u32 off[256];
+    __shared__ int s_tile;
+    __shared__ u32 lw[4];
     const int n = *d_n;
+    const int ntiles = (n + kSortTile - 1) / kSortTile;
+    if (ntiles == 0) return;
     const int G = eff_blocks(n, kSortTile);
-    const int b = blockIdx.x;
-    if (b >= G) return;
     const int t = threadIdx.x, w = t >> 6, l = lane_id();
-    const int nt = (n + kSortTile - 1) / kSortTile;
-    const int tpb = (nt + G - 1) / G;
-    const int i0 = b * tpb * kSortTile;
-    int i1 = (b + 1) * tpb * kSortTile;
-    if (i1 > n) i1 = n;
-    run[t] = hist[t * kSortMaxBlocks + b];
+    const int shift = 8 * pass;
+    u64* st = status + (size_t)pass * ntiles * 256;
+    {   // global digit bases of this pass (loads issued 8 at a time)
+        u32 c = 0;
+        const u32* hb = bhist + (size_t)pass * kSortMaxBlocks * 256 + t;
+        for (int b0 = 0; b0 < G; b0 += 8) {
+            u32 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = (b0 + k < G) ? hb[(size_t)(b0 + k) * 256] : 0u;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) c += v[k];
+        }
+        u32 tot;
+        dbase[t] = block_excl_scan256(c, lw, tot);
+    }
     const u64 lt = lanemask_lt();
-    for (int base = i0; base < i1; base += 256) {
-        const int i = base + t;
-        const bool valid = i < i1;
-        const u32 key = valid ? kin[i] : 0u;
-        const u32 val = valid ? vin[i] : 0u;
-        const u32 d = (key >> shift) & 255u;
-        wcnt[w][l] = 0; wcnt[w][l + 64] = 0; wcnt[w][l + 128] = 0; wcnt[w][l + 192] = 0;
+    for (;;) {
+        if (t == 0) s_tile = (int)atomicAdd(&tickets[pass], 1u);
+        run[t] = 0;
         __syncthreads();
-        const u64 peers = match_bits(d, 8, valid);
-        const u32 rank = (u32)__popcll(peers & lt);
-        if (valid && rank == 0) wcnt[w][d] = (u32)__popcll(peers);
-        __syncthreads();
-        {
-            u32 r = run[t];
-            for (int ww = 0; ww < 4; ++ww) {
-                u32 c = wcnt[ww][t];
-                wcnt[ww][t] = r;
-                r += c;
+        const int tile = s_tile;
+        if (tile >= ntiles) break;
+        u32 key[kOsPer], val[kOsPer], rk[kOsPer];
+#pragma unroll
+        for (int r = 0; r < kOsPer; ++r) {                      // the whole tile in flight at once
+            const int i = tile * kSortTile + r * kOsThreads + t;
+            key[r] = i < n ? kin[i] : 0xFFFFFFFFu;
+            val[r] = i < n ? vin[i] : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < kOsPer; ++r) {
+            const bool valid = tile * kSortTile + r * kOsThreads + t < n;
+            const u32 d = (key[r] >> shift) & 255u;
+            wcnt[w][l] = 0; wcnt[w][l + 64] = 0; wcnt[w][l + 128] = 0; wcnt[w][l + 192] = 0;
+            __syncthreads();
+            const u64 peers = match_bits(d, 8, valid);
+            const u32 rank = (u32)__popcll(peers & lt);
+            if (valid && rank == 0) wcnt[w][d] = (u32)__popcll(peers);
+            __syncthreads();
+            {
+                u32 a = run[t];
+#pragma unroll
+                for (int ww = 0; ww < 4; ++ww) {
+                    const u32 c = wcnt[ww][t];
+                    wcnt[ww][t] = a;
+                    a += c;
+                }
+                run[t] = a;
             }
-            run[t] = r;
+            __syncthreads();
+            rk[r] = valid ? wcnt[w][d] + rank : 0xFFFFFFFFu;
+            __syncthreads();
+        }
+        {   // decoupled look-back for digit t
+            const u32 cnt = run[t];
+            u64* mine = st + (size_t)tile * 256 + t;
+            u32 excl = 0;
+            if (tile > 0) {
+                __hip_atomic_store(mine, (1ull << 32) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                int j = tile - 1;
+                unsigned spins = 0;
+                for (;;) {
+                    const u64 v = __hip_atomic_load(st + (size_t)j * 256 + t, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+                    const u32 tag = (u32)(v >> 32);
+                    if (tag == 0) {
+                        if (++spins > kSpinLimit) { atomicOr(err, 1); break; }
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    excl += (u32)v;
+                    if (tag == 2 || j == 0) break;
+                    --j;
+                }
+            }
+            __hip_atomic_store(mine, (2ull << 32) | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            off[t] = dbase[t] + excl;
         }
         __syncthreads();
-        if (valid) {
-            const u32 pos = wcnt[w][d] + rank;
-            kout[pos] = key;
-            vout[pos] = val;
+#pragma unroll
+        for (int r = 0; r < kOsPer; ++r) {
+            if (rk[r] == 0xFFFFFFFFu) continue;
+            const u32 pos = off[(key[r] >> shift) & 255u] + rk[r];
+            kout[pos] = key[r];
+            vout[pos] = val[r];
         }
         __syncthreads();
     }
@@ -211,35 +259,48 @@ __global__ void __launch_bounds__(256) k_sc_down(const u32* __restrict__ in, u32
 
 int prim_alloc(PrimWork& w, size_t cap) {
     w.cap = cap;
-    if (hipMalloc(&w.hist, sizeof(u32) * 256 * kSortMaxBlocks) != hipSuccess) return PF_ENOMEM;
+    w.max_tiles = (cap + kSortTile - 1) / kSortTile;
     if (hipMalloc(&w.partials, sizeof(u32) * (kSortMaxBlocks + 1)) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&w.keys_tmp, sizeof(u32) * (cap + 1)) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&w.vals_tmp, sizeof(u32) * (cap + 1)) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&w.bhist, sizeof(u32) * 4 * kSortMaxBlocks * 256) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&w.status, sizeof(u64) * 4 * w.max_tiles * 256) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&w.tickets, sizeof(u32) * 4) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&w.err, sizeof(int)) != hipSuccess) return PF_ENOMEM;
+    if (hipMemset(w.err, 0, sizeof(int)) != hipSuccess) return PF_EHIP;
     return PF_OK;
 }
 
 void prim_free(PrimWork& w) {
-    (void)hipFree(w.hist);
     (void)hipFree(w.partials);
     (void)hipFree(w.keys_tmp);
     (void)hipFree(w.vals_tmp);
+    (void)hipFree(w.bhist);
+    (void)hipFree(w.status);
+    (void)hipFree(w.tickets);
+    (void)hipFree(w.err);
     w = PrimWork{};
 }
 
-void radix_sort_pairs(u32* keys, u32* vals, const int* d_n, int bits, PrimWork& w, hipStream_t s) {
+void radix_sort_pairs(u32* keys, u32* vals, const int* d_n, int bits, PrimWork& w, hipStream_t s, u32** kout,
+                      u32** vout) {
     int passes = (bits + 7) / 8;
-    if (passes & 1) ++passes;
+    if (passes < 1) passes = 1;
     if (passes > 4) passes = 4;
+    if (!kout && (passes & 1)) ++passes;   // caller wants the result in place
+    hipLaunchKernelGGL(k_os_hist, dim3(kSortMaxBlocks), dim3(256), 0, s, keys, d_n, passes, w.bhist, w.status,
+                       w.tickets);
+    const unsigned grid = (unsigned)(w.max_tiles < (size_t)kSortMaxBlocks ? w.max_tiles : kSortMaxBlocks);
     u32 *ka = keys, *va = vals, *kb = w.keys_tmp, *vb = w.vals_tmp;
     for (int p = 0; p < passes; ++p) {
-        const int shift = 8 * p;
-        hipLaunchKernelGGL(k_rs_hist, dim3(kSortMaxBlocks), dim3(256), 0, s, ka, d_n, shift, w.hist);
-        hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(1024), 0, s, w.hist, d_n);
-        hipLaunchKernelGGL(k_rs_scatter, dim3(kSortMaxBlocks), dim3(256), 0, s, ka, va, kb, vb, d_n, shift, w.hist);
+        hipLaunchKernelGGL(k_os_pass, dim3(grid), dim3(kOsThreads), 0, s, ka, va, kb, vb, d_n, p, w.bhist, w.status,
+                           w.tickets, w.err);
         u32* t;
         t = ka; ka = kb; kb = t;
         t = va; va = vb; vb = t;
     }
+    if (kout) *kout = ka;
+    if (vout) *vout = va;
 }
 
 void scan_exclusive(const u32* in, u32* out, const int* d_n, u32* d_total, PrimWork& w, hipStream_t s) {

@@ -1,0 +1,110 @@
+"""Summarise rocprofv3 CSV output into profiles/ (committed evidence for bench.py's numbers).
+
+  python tools/prof_summary.py --round r01 [--out profiles] [--gpurun gpurun_out]
+
+Reads
+  gpurun_out/prof/run_kernel_stats.csv + run_kernel_trace.csv   (--kernel-trace --stats of
+      `bench.py --steps 1000 --no-cpu --no-graph`)
+  gpurun_out/pmc_fetch|pmc_write/run_counter_collection.csv      (--pmc FETCH_SIZE / WRITE_SIZE of
+      tools/knn_probe.py)
+Writes
+  profiles/<round>_kernel_stats.csv    the rocprofv3 stats table as produced
+  profiles/<round>_frame_breakdown.md   per-kernel time per frame, launches per frame
+  profiles/knn_pmc_<round>.json         HBM bytes per k_knn_query launch (FETCH_SIZE x 2 gfx950
+                                        correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM)
+"""
+import argparse
+import csv
+import json
+import os
+import shutil
+import statistics
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    n = name.replace("pf::(anonymous namespace)::", "").replace("(anonymous namespace)::", "")
+    return n.split("(")[0]
+
+
+def frame_breakdown(trace_csv, stats_csv):
+    rows = list(csv.DictReader(open(trace_csv)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if short(r["Kernel_Name"]) == "k_predict"]
+    frames = list(zip(starts[:-1], starts[1:]))[100:]          # steady state
+    per = {}
+    spans = []
+    launches = []
+    for a, b in frames:
+        spans.append((int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3)
+        launches.append(b - a)
+        for r in rows[a:b]:
+            k = short(r["Kernel_Name"])
+            per.setdefault(k, [0.0, 0])
+            per[k][0] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            per[k][1] += 1
+    nf = max(1, len(frames))
+    lines = ["| kernel | launches / frame | us / frame | % of frame |", "|---|---:|---:|---:|"]
+    busy = sum(v[0] for v in per.values()) / nf
+    for k, (us, c) in sorted(per.items(), key=lambda kv: -kv[1][0]):
+        lines.append("| %s | %.2f | %.1f | %.1f |" % (k, c / nf, us / nf, 100 * us / nf / busy))
+    head = ("Steady-state frames analysed: %d (eager launches, `--no-graph`).\n"
+            "Median frame span %.1f us, median launches per frame %d, kernel-busy time %.1f us per frame.\n\n"
+            % (nf, statistics.median(spans), int(statistics.median(launches)), busy))
+    return head + "\n".join(lines) + "\n", {"frames": nf, "median_span_us": statistics.median(spans),
+                                            "launches_per_frame": statistics.median(launches), "busy_us": busy}
+
+
+def pmc(path, counter, kernel="k_knn_query"):
+    vals, durs = [], []
+    for r in csv.DictReader(open(path)):
+        if short(r["Kernel_Name"]) == kernel and r["Counter_Name"] == counter:
+            vals.append(float(r["Counter_Value"]))
+            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    return vals, durs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--round", required=True)
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles"))
+    ap.add_argument("--gpurun", default=os.path.join(ROOT, "gpurun_out"))
+    a = ap.parse_args()
+    os.makedirs(a.out, exist_ok=True)
+    g = a.gpurun
+    stats = os.path.join(g, "prof", "run_kernel_stats.csv")
+    trace = os.path.join(g, "prof", "run_kernel_trace.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(a.out, "%s_kernel_stats.csv" % a.round))
+        md, info = frame_breakdown(trace, stats)
+        with open(os.path.join(a.out, "%s_frame_breakdown.md" % a.round), "w") as f:
+            f.write("# Per-frame kernel breakdown (%s)\n\n" % a.round)
+            f.write("Source: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 1000 --no-cpu --no-graph`\n\n")
+            f.write(md)
+        print(json.dumps(info))
+    fetch = os.path.join(g, "pmc_fetch", "run_counter_collection.csv")
+    write = os.path.join(g, "pmc_write", "run_counter_collection.csv")
+    if os.path.exists(fetch) and os.path.exists(write):
+        fv, fd = pmc(fetch, "FETCH_SIZE")
+        wv, wd = pmc(write, "WRITE_SIZE")
+        fkb, wkb = statistics.median(fv), statistics.median(wv)
+        out = {
+            "kernel": "k_knn_query",
+            "workload": "config 5: 2M-point dense map, 200k queries (tools/knn_probe.py)",
+            "fetch_size_kb_raw": fkb, "write_size_kb_raw": wkb,
+            "hbm_read_bytes_per_launch": fkb * 1024 * 2,      # gfx950: FETCH_SIZE reads half (MICROARCH §HBM)
+            "hbm_write_bytes_per_launch": wkb * 1024,
+            "hbm_bytes_per_launch": fkb * 1024 * 2 + wkb * 1024,
+            "launches": len(fv),
+            "median_kernel_ms_under_pmc": statistics.median(fd),
+            "note": "FETCH_SIZE counts L2 misses to the fabric, Infinity-Cache hits included; x2 per the "
+                    "gfx950 calibration for 16-B-per-lane reads",
+        }
+        with open(os.path.join(a.out, "knn_pmc_%s.json" % a.round), "w") as f:
+            json.dump(out, f, indent=1)
+        print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
