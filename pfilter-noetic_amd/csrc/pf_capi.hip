@@ -141,23 +141,48 @@ int pf_odom_create(const pf_lidar_params* lidar, const pf_odom_params* params, i
 int pf_odom_destroy(pf_odom* h) {
     if (!h) return PF_OK;
     (void)hipSetDevice(h->o.device);
+    (void)hipStreamSynchronize(h->o.stream_a);
     (void)hipStreamSynchronize(h->o.stream);
     odom_destroy(h->o);
     delete h;
     return PF_OK;
 }
 
-static int stage_inputs(pf_odom* h, const float* edge, size_t ne, size_t es, const float* surf, size_t ns,
+// Frame k uses pipeline slot k % 2. Stage A (featureExtraction / VoxelGrid or host staging) of slot p
+// first waits until stage B has finished frame k - 2 (the previous user of the slot); stage B of
+// frame k waits for stage A of frame k. Consecutive frames thus overlap A(k) with B(k - 1).
+static int stage_a_begin(pf_odom* h, int p) {
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipStreamWaitEvent(o.stream_a, o.ev_b[p], 0));
+    return PF_OK;
+}
+static int stage_a_end_b_begin(pf_odom* h, int p) {
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipEventRecord(o.ev_a[p], o.stream_a));
+    PF_HIP_TRY(hipStreamWaitEvent(o.stream, o.ev_a[p], 0));
+    return PF_OK;
+}
+static int stage_b_end(pf_odom* h, int p) {
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipEventRecord(o.ev_b[p], o.stream));
+    o.frames++;
+    return PF_OK;
+}
+
+static int stage_inputs(pf_odom* h, int p, const float* edge, size_t ne, size_t es, const float* surf, size_t ns,
                         size_t ss) {
     OdomGPU& o = h->o;
     if ((!edge && ne) || (!surf && ns) || !valid_stride(es) || !valid_stride(ss)) return PF_EINVAL;
     if (ne > o.in_cap || ns > o.in_cap) return PF_ECAPACITY;
     repack(edge, ne, es, h->host_e);
     repack(surf, ns, ss, h->host_s);
-    if (ne) PF_HIP_TRY(hipMemcpyAsync(o.in_edge, h->host_e.data(), sizeof(float4) * ne, hipMemcpyHostToDevice, o.stream));
-    if (ns) PF_HIP_TRY(hipMemcpyAsync(o.in_surf, h->host_s.data(), sizeof(float4) * ns, hipMemcpyHostToDevice, o.stream));
-    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_EIN, (int)ne);
-    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_SIN, (int)ns);
+    StageBuf& sb = o.sb[p];
+    if (ne) PF_HIP_TRY(hipMemcpyAsync(sb.in_edge, h->host_e.data(), sizeof(float4) * ne, hipMemcpyHostToDevice,
+                                      o.stream_a));
+    if (ns) PF_HIP_TRY(hipMemcpyAsync(sb.in_surf, h->host_s.data(), sizeof(float4) * ns, hipMemcpyHostToDevice,
+                                      o.stream_a));
+    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, sb.cnt + C_EIN, (int)ne);
+    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, sb.cnt + C_SIN, (int)ns);
     return PF_OK;
 }
 
@@ -189,12 +214,17 @@ static int frame_status(pf_odom* h) {
 int pf_odom_init_map(pf_odom* h, const float* edge, size_t ne, size_t edge_stride, const float* surf, size_t ns,
                      size_t surf_stride) {
     if (!h) return PF_EINVAL;
-    PF_HIP_TRY(hipSetDevice(h->o.device));
-    int rc = stage_inputs(h, edge, ne, edge_stride, surf, ns, surf_stride);
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    const int p = o.frames & 1;
+    int rc = stage_a_begin(h, p);
+    if (!rc) rc = stage_inputs(h, p, edge, ne, edge_stride, surf, ns, surf_stride);
+    if (!rc) rc = stage_a_end_b_begin(h, p);
     if (rc) return rc;
-    odom_enqueue_init(h->o, h->o.stream);
-    h->o.frames++;
-    PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
+    odom_enqueue_init(o, p, o.stream);
+    rc = stage_b_end(h, p);
+    if (rc) return rc;
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
     PF_HIP_TRY(hipGetLastError());
     return PF_OK;
 }
@@ -202,11 +232,18 @@ int pf_odom_init_map(pf_odom* h, const float* edge, size_t ne, size_t edge_strid
 int pf_odom_update(pf_odom* h, const float* edge, size_t ne, size_t edge_stride, const float* surf, size_t ns,
                    size_t surf_stride, double pose_out[7]) {
     if (!h) return PF_EINVAL;
-    PF_HIP_TRY(hipSetDevice(h->o.device));
-    int rc = stage_inputs(h, edge, ne, edge_stride, surf, ns, surf_stride);
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    const int p = o.frames & 1;
+    int rc = stage_a_begin(h, p);
+    if (!rc) rc = stage_inputs(h, p, edge, ne, edge_stride, surf, ns, surf_stride);
     if (rc) return rc;
-    odom_enqueue_update(h->o, h->o.stream);
-    h->o.frames++;
+    stage_enqueue_vg(o, p, o.stream_a);
+    rc = stage_a_end_b_begin(h, p);
+    if (rc) return rc;
+    odom_enqueue_update(o, p, o.stream);
+    rc = stage_b_end(h, p);
+    if (rc) return rc;
     if (pose_out) {
         rc = read_pose(h, pose_out);
         if (rc) return rc;
@@ -288,30 +325,57 @@ int pf_odom_get_stats(pf_odom* h, pf_odom_stats* s) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// whole frame on the device. Steady-state frames (optimization_count == 2) replay one captured
-// hipGraph of the ~130-launch frame; the scan is first copied into the handle's fixed staging buffer.
+// whole frame on the device, as two pipelined stages. In steady state (optimization_count == 2)
+// each stage replays a hipGraph captured once per slot; the scan is first copied into the handle's
+// fixed staging buffer and its size written to the slot's counters (both outside the graph).
+static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool stage_a) {
+    hipGraph_t g;
+    PF_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    if (stage_a) {
+        stage_enqueue_fe(o, p, o.stage, s);
+        stage_enqueue_vg(o, p, s);
+    } else {
+        odom_enqueue_update(o, p, s);
+    }
+    PF_HIP_TRY(hipStreamEndCapture(s, &g));
+    PF_HIP_TRY(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
+    (void)hipGraphDestroy(g);
+    return PF_OK;
+}
+
 static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n) {
     OdomGPU& o = h->o;
     if (n > o.in_cap) return PF_ECAPACITY;
-    const bool steady = o.inited && o.opt_count_host <= 2;
-    if (steady && o.graph_enabled) {
-        if (n) PF_HIP_TRY(hipMemcpyAsync(o.stage, d_in, sizeof(float4) * n, hipMemcpyDeviceToDevice, o.stream));
-        hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_NIN, (int)n);
-        if (!o.graph) {
-            hipGraph_t g;
-            PF_HIP_TRY(hipStreamBeginCapture(o.stream, hipStreamCaptureModeThreadLocal));
-            odom_enqueue_frame(o, o.stage, o.stream);
-            PF_HIP_TRY(hipStreamEndCapture(o.stream, &g));
-            PF_HIP_TRY(hipGraphInstantiate(&o.graph, g, nullptr, nullptr, 0));
-            (void)hipGraphDestroy(g);
+    const int p = o.frames & 1;
+    const bool steady = o.inited && o.opt_count_host <= 2 && o.graph_enabled;
+    int rc = stage_a_begin(h, p);
+    if (rc) return rc;
+    if (n) PF_HIP_TRY(hipMemcpyAsync(o.stage, d_in, sizeof(float4) * n, hipMemcpyDeviceToDevice, o.stream_a));
+    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, o.sb[p].cnt + C_NIN, (int)n);
+    if (steady) {
+        if (!o.graph_a[p]) {
+            rc = capture(o.stream_a, &o.graph_a[p], o, p, true);
+            if (rc) return rc;
         }
-        PF_HIP_TRY(hipGraphLaunch(o.graph, o.stream));
+        PF_HIP_TRY(hipGraphLaunch(o.graph_a[p], o.stream_a));
     } else {
-        hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_NIN, (int)n);
-        odom_enqueue_frame(o, d_in, o.stream);
+        stage_enqueue_fe(o, p, o.stage, o.stream_a);
+        if (o.inited) stage_enqueue_vg(o, p, o.stream_a);
     }
-    o.frames++;
-    return PF_OK;
+    rc = stage_a_end_b_begin(h, p);
+    if (rc) return rc;
+    if (steady) {
+        if (!o.graph_b[p]) {
+            rc = capture(o.stream, &o.graph_b[p], o, p, false);
+            if (rc) return rc;
+        }
+        PF_HIP_TRY(hipGraphLaunch(o.graph_b[p], o.stream));
+    } else if (!o.inited) {
+        odom_enqueue_init(o, p, o.stream);
+    } else {
+        odom_enqueue_update(o, p, o.stream);
+    }
+    return stage_b_end(h, p);
 }
 
 int pf_odom_frame_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]) {
@@ -329,18 +393,22 @@ int pf_odom_frame_host(pf_odom* h, const float* xyzi, size_t n, size_t stride_by
     if (n > o.in_cap) return PF_ECAPACITY;
     PF_HIP_TRY(hipSetDevice(o.device));
     repack(xyzi, n, stride_bytes, h->host_e);
+    // the upload goes through fe.d_in_stage on stage A's stream, ordered before the frame's copy
+    // into the staging buffer; the host vector is reused next call, so wait for the copy
     if (n) PF_HIP_TRY(hipMemcpyAsync(o.fe.d_in_stage, h->host_e.data(), sizeof(float4) * n, hipMemcpyHostToDevice,
-                                     o.stream));
+                                     o.stream_a));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
     int rc = enqueue_frame(h, o.fe.d_in_stage, n);
     if (rc) return rc;
     if (pose_out) return read_pose(h, pose_out);
-    PF_HIP_TRY(hipStreamSynchronize(o.stream));   // host staging buffer is reused by the next call
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
     return PF_OK;
 }
 
 int pf_odom_sync(pf_odom* h) {
     if (!h) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->o.device));
+    PF_HIP_TRY(hipStreamSynchronize(h->o.stream_a));
     PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
     PF_HIP_TRY(hipGetLastError());
     return PF_OK;

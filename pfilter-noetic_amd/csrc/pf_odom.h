@@ -44,11 +44,21 @@ struct LMState {
 
 constexpr int kLmParts = 30;   // cost, g[6], H[21], bad_r, bad_J
 
+// One slot of the two-stage frame pipeline: a frame's features and their voxel-grid output, with
+// the counters of that stage. Stage A (stream_a: featureExtraction + VoxelGrid, pose independent)
+// fills slot k % 2 while stage B (stream: the odometry) still works on frame k - 1 in the other slot.
+struct StageBuf {
+    float4 *in_edge = nullptr, *in_surf = nullptr;   // featureExtraction output
+    float4 *ds_edge = nullptr, *ds_surf = nullptr;   // VoxelGrid output (r, g written by the odometry)
+    int* cnt = nullptr;                              // [C_COUNT] stage counters
+};
+
 struct OdomGPU {
     pf_lidar_params lidar{};
     pf_odom_params prm{};
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // stage B: odometry
+    hipStream_t stream_a = nullptr;    // stage A: featureExtraction + VoxelGrid
     size_t in_cap = 0, map_cap = 0, sort_cap = 0, pose_cap = 0;
     int pidx_bits = 32;            // key bits the p-index pair sort needs
     int opt_count_host = 2;
@@ -68,8 +78,14 @@ struct OdomGPU {
     int* h_cnt = nullptr;          // pinned mirror
     double* h_pose = nullptr;      // pinned [7]
 
-    float4 *in_edge = nullptr, *in_surf = nullptr;
-    float4 *ds_edge = nullptr, *ds_surf = nullptr;
+    StageBuf sb[2];
+    u32* acc_a = nullptr;                                   // stage A min/max accumulators
+    u32 *vkeys = nullptr, *vvals = nullptr, *vflags = nullptr, *vscan = nullptr, *vsegstart = nullptr;
+    PrimWork vprim;                                         // stage A sort / scan scratch
+    hipEvent_t ev_a[2] = {nullptr, nullptr};                // stage A done with slot p
+    hipEvent_t ev_b[2] = {nullptr, nullptr};                // stage B done with slot p
+    hipGraphExec_t graph_a[2] = {nullptr, nullptr};         // steady-state replay per slot
+    hipGraphExec_t graph_b[2] = {nullptr, nullptr};
     float4 *map_e = nullptr, *map_s = nullptr;
     float4 *app_e = nullptr, *app_s = nullptr;
     float4* seg_out = nullptr;
@@ -89,20 +105,19 @@ struct OdomGPU {
     double* poses = nullptr;       // [pose_cap * 7]
     float4* stage = nullptr;       // [2 * in_cap] host staging target
 
-    hipGraphExec_t graph = nullptr;
     bool graph_enabled = true;
-    const float4* graph_in = nullptr;
-    int graph_n = -1;
 };
 
 int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& prm, int device, size_t in_cap,
                 size_t map_cap);
 void odom_destroy(OdomGPU& o);
-// enqueue initMapWithPoints from in_edge/in_surf (counts in cnt[C_EIN], cnt[C_SIN])
-void odom_enqueue_init(OdomGPU& o, hipStream_t s);
-// enqueue updatePointsToMap from in_edge/in_surf (device counts); outer iteration count = host mirror
-void odom_enqueue_update(OdomGPU& o, hipStream_t s);
-// enqueue featureExtraction(d_in[0 .. cnt[C_NIN])) followed by init or update
-void odom_enqueue_frame(OdomGPU& o, const float4* d_in, hipStream_t s);
+// stage A: featureExtraction of d_in[0 .. sb[p].cnt[C_NIN]) into slot p
+void stage_enqueue_fe(OdomGPU& o, int p, const float4* d_in, hipStream_t s);
+// stage A: VoxelGrid of slot p's features (counts sb[p].cnt[C_EIN], [C_SIN])
+void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s);
+// stage B: initMapWithPoints from slot p's features
+void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s);
+// stage B: updatePointsToMap from slot p's down-sampled features; outer iteration count = host mirror
+void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s);
 
 }  // namespace pf

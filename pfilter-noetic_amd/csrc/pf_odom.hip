@@ -64,10 +64,24 @@ __device__ __forceinline__ float4 associate(const double* prm, float4 p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ void k_predict(DevState* __restrict__ st, int* __restrict__ cnt, u32* __restrict__ acc) {
-    const int t = threadIdx.x;
-    if (t < 12) acc[A_VG + t] = ((t % 6) < 3) ? 0xFFFFFFFFu : 0u;
-    if (t != 0) return;
+// copies the stage slots a frame's odometry reads from its pipeline slot's counters
+__device__ __forceinline__ void pull_stage_counts(int* cnt, const int* scnt) {
+    cnt[C_NIN] = scnt[C_NIN];
+    cnt[C_EIN] = scnt[C_EIN];
+    cnt[C_SIN] = scnt[C_SIN];
+    cnt[C_VGN] = scnt[C_VGN];
+    cnt[C_EDS] = scnt[C_EDS];
+    cnt[C_SDS] = scnt[C_SDS];
+    cnt[C_NQ] = scnt[C_NQ];
+}
+
+__global__ void k_pull_counts(int* __restrict__ cnt, const int* __restrict__ scnt) {
+    if (threadIdx.x == 0) pull_stage_counts(cnt, scnt);
+}
+
+__global__ void k_predict(DevState* __restrict__ st, int* __restrict__ cnt, const int* __restrict__ scnt) {
+    if (threadIdx.x != 0) return;
+    pull_stage_counts(cnt, scnt);
     if (st->optimization_count > 2) st->optimization_count--;                 // :232-233
     const iso odom = load_iso(st->odomR, st->odomt);
     const iso last = load_iso(st->lastR, st->lastt);
@@ -83,7 +97,13 @@ __global__ void k_predict(DevState* __restrict__ st, int* __restrict__ cnt, u32*
     cnt[C_OUTER] = gate ? st->optimization_count : 0;
     cnt[C_LM_ITERS] = 0;
     cnt[C_EDGE_KEPT] = cnt[C_SURF_KEPT] = cnt[C_EDGE_VALID] = cnt[C_SURF_VALID] = 0;
-    cnt[C_VGN] = cnt[C_EIN] + cnt[C_SIN];
+}
+
+// voxel-grid stage set-up (stream A): reset the min/max accumulators, batch size
+__global__ void k_vg_begin(int* __restrict__ scnt, u32* __restrict__ acc) {
+    const int t = threadIdx.x;
+    if (t < 12) acc[A_VG + t] = ((t % 6) < 3) ? 0xFFFFFFFFu : 0u;
+    if (t == 0) scnt[C_VGN] = scnt[C_EIN] + scnt[C_SIN];
 }
 
 // ----------------------------------- VoxelGrid (B.1) ------------------------------------------
@@ -1138,12 +1158,15 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     o.leaf_rg[0] = (float)prm.map_res;
     o.leaf_rg[1] = (float)prm.map_res * 2;
     if (hipStreamCreateWithFlags(&o.stream, hipStreamNonBlocking) != hipSuccess) return PF_EHIP;
+    if (hipStreamCreateWithFlags(&o.stream_a, hipStreamNonBlocking) != hipSuccess) return PF_EHIP;
     int rc = fe_alloc(o.fe, lidar, in_cap);
     if (rc) return rc;
     // 1 m cells over both maps' bounding boxes: 2 x (201 m)^2 x 400 m covers the +-100 m crop box
     rc = grid_alloc(o.grid, 2 * map_cap, (size_t)1 << 25);
     if (rc) return rc;
     rc = prim_alloc(o.prim, o.sort_cap > ((size_t)1 << 25) + 2 ? o.sort_cap : ((size_t)1 << 25) + 2);
+    if (rc) return rc;
+    rc = prim_alloc(o.vprim, 2 * in_cap);
     if (rc) return rc;
     const size_t nq = 2 * in_cap;
 #define PF_ALLOC(ptr, bytes) \
@@ -1152,10 +1175,22 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.lm, sizeof(LMState));
     PF_ALLOC(o.cnt, sizeof(int) * C_COUNT);
     PF_ALLOC(o.acc, sizeof(u32) * A_COUNT);
-    PF_ALLOC(o.in_edge, sizeof(float4) * in_cap);
-    PF_ALLOC(o.in_surf, sizeof(float4) * in_cap);
-    PF_ALLOC(o.ds_edge, sizeof(float4) * in_cap);
-    PF_ALLOC(o.ds_surf, sizeof(float4) * in_cap);
+    for (int p = 0; p < 2; ++p) {
+        PF_ALLOC(o.sb[p].in_edge, sizeof(float4) * in_cap);
+        PF_ALLOC(o.sb[p].in_surf, sizeof(float4) * in_cap);
+        PF_ALLOC(o.sb[p].ds_edge, sizeof(float4) * in_cap);
+        PF_ALLOC(o.sb[p].ds_surf, sizeof(float4) * in_cap);
+        PF_ALLOC(o.sb[p].cnt, sizeof(int) * C_COUNT);
+        if (hipMemset(o.sb[p].cnt, 0, sizeof(int) * C_COUNT) != hipSuccess) return PF_EHIP;
+        if (hipEventCreateWithFlags(&o.ev_a[p], hipEventDisableTiming) != hipSuccess) return PF_EHIP;
+        if (hipEventCreateWithFlags(&o.ev_b[p], hipEventDisableTiming) != hipSuccess) return PF_EHIP;
+    }
+    PF_ALLOC(o.acc_a, sizeof(u32) * A_COUNT);
+    PF_ALLOC(o.vkeys, sizeof(u32) * (2 * in_cap + 1));
+    PF_ALLOC(o.vvals, sizeof(u32) * (2 * in_cap + 1));
+    PF_ALLOC(o.vflags, sizeof(u32) * (2 * in_cap + 1));
+    PF_ALLOC(o.vscan, sizeof(u32) * (2 * in_cap + 1));
+    PF_ALLOC(o.vsegstart, sizeof(u32) * (2 * in_cap + 1));
     PF_ALLOC(o.map_e, sizeof(float4) * map_cap);
     PF_ALLOC(o.map_s, sizeof(float4) * map_cap);
     PF_ALLOC(o.app_e, sizeof(float4) * in_cap);
@@ -1193,6 +1228,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (hipMemcpy(o.st, &h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.cnt, 0, sizeof(int) * C_COUNT) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.acc, 0, sizeof(u32) * A_COUNT) != hipSuccess) return PF_EHIP;
+    if (hipMemset(o.acc_a, 0, sizeof(u32) * A_COUNT) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.lm, 0, sizeof(LMState)) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.lm_ticket, 0, sizeof(u32) * 4) != hipSuccess) return PF_EHIP;
     o.opt_count_host = 2;
@@ -1200,48 +1236,72 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
 }
 
 void odom_destroy(OdomGPU& o) {
-    if (o.graph) (void)hipGraphExecDestroy(o.graph);
+    for (int p = 0; p < 2; ++p) {
+        if (o.graph_a[p]) (void)hipGraphExecDestroy(o.graph_a[p]);
+        if (o.graph_b[p]) (void)hipGraphExecDestroy(o.graph_b[p]);
+        if (o.ev_a[p]) (void)hipEventDestroy(o.ev_a[p]);
+        if (o.ev_b[p]) (void)hipEventDestroy(o.ev_b[p]);
+        void* sp[] = {o.sb[p].in_edge, o.sb[p].in_surf, o.sb[p].ds_edge, o.sb[p].ds_surf, o.sb[p].cnt};
+        for (void* q : sp) (void)hipFree(q);
+    }
     fe_free(o.fe);
     grid_free(o.grid);
     prim_free(o.prim);
-    void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.in_edge, o.in_surf, o.ds_edge, o.ds_surf, o.map_e, o.map_s,
-                    o.app_e, o.app_s, o.seg_out, o.keys, o.vals, o.flags, o.scan_out, o.segstart, o.nbr,
-                    o.qflag, o.lm_part, o.lm_ticket, o.geo, o.spars, o.roundv, o.observe, o.pcnt, o.tailinc, o.poses, o.stage, o.dbg};
-    for (void* p : ptrs) (void)hipFree(p);
+    prim_free(o.vprim);
+    void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.map_e,
+                    o.map_s, o.app_e, o.app_s, o.seg_out, o.keys, o.vals, o.flags, o.scan_out, o.segstart, o.nbr,
+                    o.qflag, o.lm_part, o.lm_ticket, o.geo, o.spars, o.roundv, o.observe, o.pcnt, o.tailinc,
+                    o.poses, o.stage, o.dbg};
+    for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
     if (o.h_pose) (void)hipHostFree(o.h_pose);
     if (o.stream) (void)hipStreamDestroy(o.stream);
+    if (o.stream_a) (void)hipStreamDestroy(o.stream_a);
     o = OdomGPU{};
 }
 
-void odom_enqueue_init(OdomGPU& o, hipStream_t s) {
-    hipLaunchKernelGGL(k_init_map, dim3(kGrid), dim3(256), 0, s, o.cnt, o.in_edge, o.in_surf, o.map_e, o.map_s);
+void stage_enqueue_fe(OdomGPU& o, int p, const float4* d_in, hipStream_t s) {
+    StageBuf& sb = o.sb[p];
+    fe_enqueue(o.fe, d_in, sb.cnt + C_NIN, sb.in_edge, sb.cnt + C_EIN, sb.in_surf, sb.cnt + C_SIN, s);
+}
+
+void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s) {
+    StageBuf& sb = o.sb[p];
+    int* cnt = sb.cnt;
+    // VoxelGrid of both inputs (:242-245); pose independent, so it runs ahead on stream A
+    hipLaunchKernelGGL(k_vg_begin, dim3(1), dim3(64), 0, s, cnt, o.acc_a);
+    hipLaunchKernelGGL(k_vg_minmax, dim3(128), dim3(256), 0, s, sb.in_edge, sb.in_surf, cnt, o.acc_a);
+    hipLaunchKernelGGL(k_vg_keys, dim3(kGrid), dim3(256), 0, s, sb.in_edge, sb.in_surf, cnt, o.acc_a, o.leaf_vg[0],
+                       o.leaf_vg[1], o.vkeys, o.vvals);
+    radix_sort_pairs(o.vkeys, o.vvals, cnt + C_VGN, 32, o.vprim, s);
+    hipLaunchKernelGGL(k_seg_heads, dim3(kGrid), dim3(256), 0, s, o.vkeys, cnt + C_VGN, o.vflags);
+    scan_exclusive(o.vflags, o.vscan, cnt + C_VGN, (u32*)(cnt + C_NSEG), o.vprim, s);
+    hipLaunchKernelGGL(k_seg_starts, dim3(kGrid), dim3(256), 0, s, o.vkeys, cnt + C_VGN, o.vflags, o.vscan,
+                       o.vsegstart, cnt);
+    hipLaunchKernelGGL(k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, sb.in_edge, sb.in_surf, o.vkeys, o.vvals,
+                       o.vsegstart, cnt, sb.ds_edge, sb.ds_surf);
+}
+
+void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s) {
+    StageBuf& sb = o.sb[p];
+    hipLaunchKernelGGL(k_pull_counts, dim3(1), dim3(64), 0, s, o.cnt, sb.cnt);
+    hipLaunchKernelGGL(k_init_map, dim3(kGrid), dim3(256), 0, s, o.cnt, sb.in_edge, sb.in_surf, o.map_e, o.map_s);
     hipLaunchKernelGGL(k_init_counts, dim3(1), dim3(64), 0, s, o.cnt, o.st);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, o.st, o.poses, (int)o.pose_cap, 0, o.acc);
     o.opt_count_host = 12;
     o.inited = true;
 }
 
-void odom_enqueue_update(OdomGPU& o, hipStream_t s) {
+void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     if (o.opt_count_host > 2) o.opt_count_host--;
+    StageBuf& sb = o.sb[p];
     int* cnt = o.cnt;
-    hipLaunchKernelGGL(k_predict, dim3(1), dim3(64), 0, s, o.st, cnt, o.acc);
-    // VoxelGrid of both inputs (:242-245)
-    hipLaunchKernelGGL(k_vg_minmax, dim3(128), dim3(256), 0, s, o.in_edge, o.in_surf, cnt, o.acc);
-    hipLaunchKernelGGL(k_vg_keys, dim3(kGrid), dim3(256), 0, s, o.in_edge, o.in_surf, cnt, o.acc, o.leaf_vg[0],
-                       o.leaf_vg[1], o.keys, o.vals);
-    radix_sort_pairs(o.keys, o.vals, cnt + C_VGN, 32, o.prim, s);
-    hipLaunchKernelGGL(k_seg_heads, dim3(kGrid), dim3(256), 0, s, o.keys, cnt + C_VGN, o.flags);
-    scan_exclusive(o.flags, o.scan_out, cnt + C_VGN, (u32*)(cnt + C_NSEG), o.prim, s);
-    hipLaunchKernelGGL(k_seg_starts, dim3(kGrid), dim3(256), 0, s, o.keys, cnt + C_VGN, o.flags, o.scan_out,
-                       o.segstart, cnt);
-    hipLaunchKernelGGL(k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, o.in_edge, o.in_surf, o.keys, o.vals,
-                       o.segstart, cnt, o.ds_edge, o.ds_surf);
+    hipLaunchKernelGGL(k_predict, dim3(1), dim3(64), 0, s, o.st, cnt, sb.cnt);
     // grids of the edge / surf maps (kd-tree build, :249-250)
     grid_build(o.grid, o.map_e, cnt + C_ME, o.map_s, cnt + C_MS, o.prim, s);
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
-        AssocArgs aa{o.st, cnt, o.acc, gv, o.ds_edge, o.ds_surf, o.map_e, o.map_s, o.nbr, o.qflag, o.geo, o.spars,
+        AssocArgs aa{o.st, cnt, o.acc, gv, sb.ds_edge, sb.ds_surf, o.map_e, o.map_s, o.nbr, o.qflag, o.geo, o.spars,
                      o.roundv, o.keys, o.vals, (u32)o.map_cap, o.lm_ticket};
         hipLaunchKernelGGL(k_assoc_knn, dim3(kGrid), dim3(256), 0, s, aa);
         hipLaunchKernelGGL(k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
@@ -1250,18 +1310,19 @@ void odom_enqueue_update(OdomGPU& o, hipStream_t s) {
         u32 *pk, *pv;
         radix_sort_pairs(o.keys, o.vals, cnt + C_NPAIR, o.pidx_bits, o.prim, s, &pk, &pv);
         hipLaunchKernelGGL(k_pidx_count, dim3(kGrid), dim3(256), 0, s, pk, pv, cnt, o.pcnt, o.tailinc);
-        ObsArgs oa{cnt, o.acc, o.map_e, o.map_s, o.ds_edge, o.ds_surf, o.nbr, o.qflag, o.pcnt, o.roundv, o.spars,
+        ObsArgs oa{cnt, o.acc, o.map_e, o.map_s, sb.ds_edge, sb.ds_surf, o.nbr, o.qflag, o.pcnt, o.roundv, o.spars,
                    o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
         hipLaunchKernelGGL(k_observe, dim3(kGrid), dim3(256), 0, s, oa);
         hipLaunchKernelGGL(k_pidx_apply, dim3(kGrid), dim3(256), 0, s, pk, o.tailinc, cnt, o.map_e, o.map_s,
                            (u32)o.map_cap);
-        LmArgs la{o.st, cnt, o.acc, o.lm, o.lm_part, o.lm_ticket, o.qflag, o.ds_edge, o.ds_surf, o.geo, o.observe,
+        LmArgs la{o.st, cnt, o.acc, o.lm, o.lm_part, o.lm_ticket, o.qflag, sb.ds_edge, sb.ds_surf, o.geo, o.observe,
                   o.spars, o.prm.weight_type, o.dbg};
         hipLaunchKernelGGL(k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
     }
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, o.st, o.poses, (int)o.pose_cap, 1, o.acc);
     // addPointsToMap (:589-647)
-    hipLaunchKernelGGL(k_map_append, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.ds_edge, o.ds_surf, o.app_e, o.app_s);
+    hipLaunchKernelGGL(k_map_append, dim3(kGrid), dim3(256), 0, s, o.st, cnt, sb.ds_edge, sb.ds_surf, o.app_e,
+                       o.app_s);
     hipLaunchKernelGGL(k_rg_minmax, dim3(128), dim3(256), 0, s, o.st, cnt, o.acc, o.map_e, o.app_e, o.map_s, o.app_s);
     hipLaunchKernelGGL(k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, o.map_e, o.app_e, o.map_s, o.app_s,
                        o.leaf_rg[0], o.leaf_rg[1], o.keys, o.vals);
@@ -1277,12 +1338,6 @@ void odom_enqueue_update(OdomGPU& o, hipStream_t s) {
     hipLaunchKernelGGL(k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, o.flags, o.scan_out, o.map_e,
                        o.map_s);
     hipLaunchKernelGGL(k_map_counts, dim3(1), dim3(64), 0, s, cnt);
-}
-
-void odom_enqueue_frame(OdomGPU& o, const float4* d_in, hipStream_t s) {
-    fe_enqueue(o.fe, d_in, o.cnt + C_NIN, o.in_edge, o.cnt + C_EIN, o.in_surf, o.cnt + C_SIN, s);
-    if (!o.inited) odom_enqueue_init(o, s);
-    else odom_enqueue_update(o, s);
 }
 
 }  // namespace pf
