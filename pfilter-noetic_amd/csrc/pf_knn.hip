@@ -254,7 +254,7 @@ int pf_knn_create(int device, size_t map_capacity, size_t query_capacity, pf_knn
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) rc = PF_EHIP;
     // cells: a 1 m grid over the map bounding box; 64M cells covers e.g. a 400 x 400 x 400 m block
     if (rc == PF_OK) rc = grid_alloc(h->grid, map_capacity, (size_t)1 << 26);
-    if (rc == PF_OK) rc = prim_alloc(h->prim, 1);  // scans only: no sort scratch
+    if (rc == PF_OK) rc = prim_alloc(h->prim, 1, ((size_t)1 << 26) + 2);  // scans of the cell counts only
     if (rc == PF_OK && hipMalloc(&h->d_map, sizeof(float4) * map_capacity) != hipSuccess) rc = PF_ENOMEM;
     if (rc == PF_OK && hipMalloc(&h->d_m, sizeof(int) * 2) != hipSuccess) rc = PF_ENOMEM;
     if (rc == PF_OK && hipMalloc(&h->d_q, sizeof(float4) * query_capacity) != hipSuccess) rc = PF_ENOMEM;

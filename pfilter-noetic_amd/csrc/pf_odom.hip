@@ -1164,7 +1164,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     // 1 m cells over both maps' bounding boxes: 2 x (201 m)^2 x 400 m covers the +-100 m crop box
     rc = grid_alloc(o.grid, 2 * map_cap, (size_t)1 << 25);
     if (rc) return rc;
-    rc = prim_alloc(o.prim, o.sort_cap > ((size_t)1 << 25) + 2 ? o.sort_cap : ((size_t)1 << 25) + 2);
+    rc = prim_alloc(o.prim, o.sort_cap, ((size_t)1 << 25) + 2);   // sorts; scans up to the cell count
     if (rc) return rc;
     rc = prim_alloc(o.vprim, 2 * in_cap);
     if (rc) return rc;

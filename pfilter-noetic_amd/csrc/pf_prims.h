@@ -6,20 +6,21 @@ namespace pf {
 
 constexpr int kSortMaxBlocks = 256;   // max workgroups of the sort / scan grids
 constexpr int kSortTile = 2048;       // keys per tile (256 threads x 8)
-constexpr int kScanTile = 1024;       // items per scan tile (256 threads x 4)
 
 struct PrimWork {
-    u32* partials = nullptr;   // kSortMaxBlocks + 1 (scan)
     u32* keys_tmp = nullptr;   // cap
     u32* vals_tmp = nullptr;   // cap
-    u32* bhist = nullptr;      // [4 passes][kSortMaxBlocks][256] per-block digit counts
+    u32* bhist = nullptr;      // [4 passes][256] global digit counts (zero between sorts)
     u64* status = nullptr;     // [4 passes][max_tiles][256] look-back words
-    u32* tickets = nullptr;    // [4] tile tickets per pass
+    u32* tickets = nullptr;    // [8]: [4] histogram arrivals, [5] scan arrivals
+    u32* dbase = nullptr;      // [4 passes][256] exclusive digit bases
+    u64* scan_status = nullptr;// [max_tiles] scan look-back words (zero between calls)
     int* err = nullptr;        // look-back spin limit hit (never expected)
-    size_t cap = 0, max_tiles = 0;
+    size_t cap = 0, max_tiles = 0, scan_tiles = 0;
 };
 
-int prim_alloc(PrimWork& w, size_t cap);
+// cap: largest sort; scan_cap: largest scan (defaults to cap)
+int prim_alloc(PrimWork& w, size_t cap, size_t scan_cap = 0);
 void prim_free(PrimWork& w);
 
 // Stable sort of (keys, vals)[0 .. *d_n) by the low `bits` bits of keys (8-bit digits). With kout/vout

@@ -54,9 +54,11 @@ constexpr int kOsPer = kSortTile / kOsThreads;   // 8 keys per thread per tile
 constexpr unsigned kSpinLimit = 1u << 22;
 
 __global__ void __launch_bounds__(256) k_os_hist(const u32* __restrict__ keys, const int* __restrict__ d_n, int passes,
-                                                  u32* __restrict__ bhist, u64* __restrict__ status,
-                                                  u32* __restrict__ tickets) {
+                                                  u32* __restrict__ bhist, u32* __restrict__ dbase,
+                                                  u64* __restrict__ status, u32* __restrict__ tickets) {
     __shared__ u32 lh[4][256];
+    __shared__ u32 lw[4];
+    __shared__ int last;
     const int n = *d_n;
     const int G = eff_blocks(n, kSortTile);
     const int b = blockIdx.x, t = threadIdx.x;
@@ -64,7 +66,6 @@ __global__ void __launch_bounds__(256) k_os_hist(const u32* __restrict__ keys, c
     // reset this sort's look-back state (visible to the pass kernels at the kernel boundary)
     for (size_t i = (size_t)b * 256 + t; i < (size_t)passes * ntiles * 256; i += (size_t)gridDim.x * 256)
         status[i] = 0ull;
-    if (b == 0 && t < 4) tickets[t] = 0u;
     if (b >= G) return;
     for (int p = 0; p < 4; ++p) lh[p][t] = 0;
     __syncthreads();
@@ -77,47 +78,52 @@ __global__ void __launch_bounds__(256) k_os_hist(const u32* __restrict__ keys, c
         for (int p = 0; p < passes; ++p) atomicAdd(&lh[p][(k >> (8 * p)) & 255u], 1u);
     }
     __syncthreads();
-    for (int p = 0; p < passes; ++p) bhist[((size_t)p * kSortMaxBlocks + b) * 256 + t] = lh[p][t];
+    // add this block's counts into the global histograms (agent-scope atomics), then the last block
+    // to arrive forms the exclusive digit bases of every pass and clears the histograms for the next
+    // sort (agent-scope loads / stores; no fence needed: G16 R2)
+    for (int p = 0; p < passes; ++p)
+        if (lh[p][t]) __hip_atomic_fetch_add(&bhist[p * 256 + t], lh[p][t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+        const u32 tk = __hip_atomic_fetch_add(&tickets[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = tk == (u32)G - 1 ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last) return;
+    u32 c[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+        c[p] = p < passes ? __hip_atomic_load(&bhist[p * 256 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+        if (p < passes) __hip_atomic_store(&bhist[p * 256 + t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int p = 0; p < passes; ++p) {
+        u32 tot;
+        dbase[p * 256 + t] = block_excl_scan256(c[p], lw, tot);
+    }
+    if (t == 0) __hip_atomic_store(&tickets[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// One pass. Blocks own tiles b, b + G, ... (G <= kSortMaxBlocks co-resident blocks), so a tile's
+// look-back only waits on tiles of running blocks.
 __global__ void __launch_bounds__(kOsThreads) k_os_pass(const u32* __restrict__ kin, const u32* __restrict__ vin,
                                                          u32* __restrict__ kout, u32* __restrict__ vout,
                                                          const int* __restrict__ d_n, int pass,
-                                                         const u32* __restrict__ bhist, u64* __restrict__ status,
-                                                         u32* __restrict__ tickets, int* __restrict__ err) {
-    __shared__ u32 dbase[256];
+                                                         const u32* __restrict__ dbase_g, u64* __restrict__ status,
+                                                         int* __restrict__ err) {
     __shared__ u32 run[256];
     __shared__ u32 wcnt[4][256];
     __shared__ u32 off[256];
-    __shared__ int s_tile;
-    __shared__ u32 lw[4];
     const int n = *d_n;
     const int ntiles = (n + kSortTile - 1) / kSortTile;
-    if (ntiles == 0) return;
-    const int G = eff_blocks(n, kSortTile);
     const int t = threadIdx.x, w = t >> 6, l = lane_id();
+    if ((int)blockIdx.x >= ntiles) return;
     const int shift = 8 * pass;
     u64* st = status + (size_t)pass * ntiles * 256;
-    {   // global digit bases of this pass (loads issued 8 at a time)
-        u32 c = 0;
-        const u32* hb = bhist + (size_t)pass * kSortMaxBlocks * 256 + t;
-        for (int b0 = 0; b0 < G; b0 += 8) {
-            u32 v[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = (b0 + k < G) ? hb[(size_t)(b0 + k) * 256] : 0u;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) c += v[k];
-        }
-        u32 tot;
-        dbase[t] = block_excl_scan256(c, lw, tot);
-    }
+    const u32 dbase = dbase_g[pass * 256 + t];
     const u64 lt = lanemask_lt();
-    for (;;) {
-        if (t == 0) s_tile = (int)atomicAdd(&tickets[pass], 1u);
-        run[t] = 0;
-        __syncthreads();
-        const int tile = s_tile;
-        if (tile >= ntiles) break;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         u32 key[kOsPer], val[kOsPer], rk[kOsPer];
 #pragma unroll
         for (int r = 0; r < kOsPer; ++r) {                      // the whole tile in flight at once
@@ -125,6 +131,7 @@ __global__ void __launch_bounds__(kOsThreads) k_os_pass(const u32* __restrict__ 
             key[r] = i < n ? kin[i] : 0xFFFFFFFFu;
             val[r] = i < n ? vin[i] : 0u;
         }
+        run[t] = 0;
 #pragma unroll
         for (int r = 0; r < kOsPer; ++r) {
             const bool valid = tile * kSortTile + r * kOsThreads + t < n;
@@ -172,7 +179,7 @@ __global__ void __launch_bounds__(kOsThreads) k_os_pass(const u32* __restrict__ 
                 }
             }
             __hip_atomic_store(mine, (2ull << 32) | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            off[t] = dbase[t] + excl;
+            off[t] = dbase + excl;
         }
         __syncthreads();
 #pragma unroll
@@ -186,98 +193,120 @@ __global__ void __launch_bounds__(kOsThreads) k_os_pass(const u32* __restrict__ 
     }
 }
 
-// ---- exclusive scan ----
-__global__ void __launch_bounds__(256) k_sc_reduce(const u32* __restrict__ in, const int* __restrict__ d_n,
-                                                    u32* __restrict__ partials) {
+// ---- exclusive scan: one kernel, decoupled look-back ----
+// Blocks own 2048-item tiles b, b + G, ... (co-resident grid). A tile publishes its aggregate, wave 0
+// looks back over up to 64 predecessors at once (agent-scope atomic words carrying tag << 32 |
+// value), then publishes its inclusive prefix. The last block to finish clears the status words for
+// the next call.
+constexpr int kScanPer = 8;
+__global__ void __launch_bounds__(256) k_scan1(const u32* __restrict__ in, u32* __restrict__ out,
+                                                const int* __restrict__ d_n, u32* __restrict__ d_total,
+                                                u64* __restrict__ status, u32* __restrict__ arrive,
+                                                int* __restrict__ err) {
     __shared__ u32 lw[4];
+    __shared__ u32 s_excl;
+    __shared__ int last;
     const int n = *d_n;
-    const int G = eff_blocks(n, kScanTile);
-    const int b = blockIdx.x;
-    if (b >= G) return;
-    const int nt = (n + kScanTile - 1) / kScanTile;
-    const int tpb = (nt + G - 1) / G;
-    const int i0 = b * tpb * kScanTile;
-    int i1 = (b + 1) * tpb * kScanTile;
-    if (i1 > n) i1 = n;
-    u32 s = 0;
-    for (int i = i0 + threadIdx.x; i < i1; i += 256) s += in[i];
-    u32 tot;
-    block_excl_scan256(s, lw, tot);
-    if (threadIdx.x == 0) partials[b] = tot;
-}
-
-__global__ void __launch_bounds__(256) k_sc_top(u32* __restrict__ partials, const int* __restrict__ d_n,
-                                                 u32* __restrict__ d_total) {
-    __shared__ u32 lw[4];
-    const int n = *d_n;
-    const int G = eff_blocks(n, kScanTile);
-    const int t = threadIdx.x;
-    u32 v = t < G ? partials[t] : 0u;   // G <= 256
-    u32 tot;
-    u32 ex = block_excl_scan256(v, lw, tot);
-    if (t < G) partials[t] = ex;
-    if (t == 0 && d_total) *d_total = tot;
-}
-
-__global__ void __launch_bounds__(256) k_sc_down(const u32* __restrict__ in, u32* __restrict__ out,
-                                                  const int* __restrict__ d_n, const u32* __restrict__ partials) {
-    __shared__ u32 lw[4];
-    const int n = *d_n;
-    const int G = eff_blocks(n, kScanTile);
-    const int b = blockIdx.x;
-    if (b >= G) return;
-    const int nt = (n + kScanTile - 1) / kScanTile;
-    const int tpb = (nt + G - 1) / G;
-    const int i0 = b * tpb * kScanTile;
-    int i1 = (b + 1) * tpb * kScanTile;
-    if (i1 > n) i1 = n;
-    u32 run = partials[b];
-    const int t = threadIdx.x;
-    for (int base = i0; base < i1; base += kScanTile) {
-        u32 v[4];
-        u32 s = 0;
+    const int ntiles = (n + kSortTile - 1) / kSortTile;
+    const int t = threadIdx.x, l = lane_id();
+    const int G = ntiles < (int)gridDim.x ? ntiles : (int)gridDim.x;
+    if (n == 0) {
+        if (blockIdx.x == 0 && t == 0 && d_total) *d_total = 0u;
+        return;
+    }
+    if ((int)blockIdx.x >= G) return;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int base = tile * kSortTile + t * kScanPer;
+        u32 v[kScanPer];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = base + 4 * t + k;
-            v[k] = i < i1 ? in[i] : 0u;
-            s += v[k];
+        for (int k = 0; k < kScanPer; ++k) v[k] = base + k < n ? in[base + k] : 0u;
+        u32 sum = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) sum += v[k];
+        u32 agg;
+        const u32 tex = block_excl_scan256(sum, lw, agg);
+        if (t < 64) {                                           // wave 0: publish + look-back
+            if (t == 0 && tile > 0)
+                __hip_atomic_store(&status[tile], (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            u32 excl = 0;
+            int j = tile - 1;
+            unsigned spins = 0;
+            while (j >= 0) {
+                const int jj = j - l;
+                const u64 sv = jj >= 0 ? __hip_atomic_load(&status[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : (2ull << 32);        // before tile 0: an inclusive zero
+                const u32 tag = (u32)(sv >> 32);
+                const u64 incl = __ballot(tag == 2);
+                const int first = incl ? __ffsll((long long)incl) - 1 : 64;   // nearest inclusive
+                const u64 notready = __ballot(tag == 0) & (first >= 63 ? ~0ull : ((2ull << first) - 1));
+                if (notready) {
+                    if (++spins > kSpinLimit) { if (l == 0) atomicOr(err, 1); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                u32 mine = (l <= first && jj >= 0) ? (u32)sv : 0u;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+                excl += mine;
+                if (first < 64) break;
+                j -= 64;
+            }
+            if (t == 0) {
+                __hip_atomic_store(&status[tile], (2ull << 32) | (excl + agg), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                s_excl = excl;
+                if (tile == ntiles - 1 && d_total) *d_total = excl + agg;
+            }
         }
-        u32 tot;
-        u32 ex = block_excl_scan256(s, lw, tot);
-        u32 r = run + ex;
+        __syncthreads();
+        u32 r = s_excl + tex;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = base + 4 * t + k;
-            if (i < i1) out[i] = r;
+        for (int k = 0; k < kScanPer; ++k) {
+            if (base + k < n) out[base + k] = r;
             r += v[k];
         }
-        run += tot;
+        __syncthreads();
     }
+    // the last block to finish clears the look-back words for the next call
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (u32)G - 1;
+    __syncthreads();
+    if (!last) return;
+    for (int i = t; i < ntiles; i += 256) __hip_atomic_store(&status[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
 
-int prim_alloc(PrimWork& w, size_t cap) {
+int prim_alloc(PrimWork& w, size_t cap, size_t scan_cap) {
+    if (scan_cap < cap) scan_cap = cap;
     w.cap = cap;
     w.max_tiles = (cap + kSortTile - 1) / kSortTile;
-    if (hipMalloc(&w.partials, sizeof(u32) * (kSortMaxBlocks + 1)) != hipSuccess) return PF_ENOMEM;
+    w.scan_tiles = (scan_cap + kSortTile - 1) / kSortTile;
     if (hipMalloc(&w.keys_tmp, sizeof(u32) * (cap + 1)) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&w.vals_tmp, sizeof(u32) * (cap + 1)) != hipSuccess) return PF_ENOMEM;
-    if (hipMalloc(&w.bhist, sizeof(u32) * 4 * kSortMaxBlocks * 256) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&w.bhist, sizeof(u32) * 4 * 256) != hipSuccess) return PF_ENOMEM;
+    if (hipMemset(w.bhist, 0, sizeof(u32) * 4 * 256) != hipSuccess) return PF_EHIP;
     if (hipMalloc(&w.status, sizeof(u64) * 4 * w.max_tiles * 256) != hipSuccess) return PF_ENOMEM;
-    if (hipMalloc(&w.tickets, sizeof(u32) * 4) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&w.tickets, sizeof(u32) * 8) != hipSuccess) return PF_ENOMEM;
+    if (hipMemset(w.tickets, 0, sizeof(u32) * 8) != hipSuccess) return PF_EHIP;
+    if (hipMalloc(&w.dbase, sizeof(u32) * 4 * 256) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&w.scan_status, sizeof(u64) * (w.scan_tiles + 1)) != hipSuccess) return PF_ENOMEM;
+    if (hipMemset(w.scan_status, 0, sizeof(u64) * (w.scan_tiles + 1)) != hipSuccess) return PF_EHIP;
     if (hipMalloc(&w.err, sizeof(int)) != hipSuccess) return PF_ENOMEM;
     if (hipMemset(w.err, 0, sizeof(int)) != hipSuccess) return PF_EHIP;
     return PF_OK;
 }
 
 void prim_free(PrimWork& w) {
-    (void)hipFree(w.partials);
     (void)hipFree(w.keys_tmp);
     (void)hipFree(w.vals_tmp);
     (void)hipFree(w.bhist);
     (void)hipFree(w.status);
     (void)hipFree(w.tickets);
+    (void)hipFree(w.dbase);
+    (void)hipFree(w.scan_status);
     (void)hipFree(w.err);
     w = PrimWork{};
 }
@@ -288,13 +317,13 @@ void radix_sort_pairs(u32* keys, u32* vals, const int* d_n, int bits, PrimWork& 
     if (passes < 1) passes = 1;
     if (passes > 4) passes = 4;
     if (!kout && (passes & 1)) ++passes;   // caller wants the result in place
-    hipLaunchKernelGGL(k_os_hist, dim3(kSortMaxBlocks), dim3(256), 0, s, keys, d_n, passes, w.bhist, w.status,
-                       w.tickets);
+    hipLaunchKernelGGL(k_os_hist, dim3(kSortMaxBlocks), dim3(256), 0, s, keys, d_n, passes, w.bhist, w.dbase,
+                       w.status, w.tickets);
     const unsigned grid = (unsigned)(w.max_tiles < (size_t)kSortMaxBlocks ? w.max_tiles : kSortMaxBlocks);
     u32 *ka = keys, *va = vals, *kb = w.keys_tmp, *vb = w.vals_tmp;
     for (int p = 0; p < passes; ++p) {
-        hipLaunchKernelGGL(k_os_pass, dim3(grid), dim3(kOsThreads), 0, s, ka, va, kb, vb, d_n, p, w.bhist, w.status,
-                           w.tickets, w.err);
+        hipLaunchKernelGGL(k_os_pass, dim3(grid), dim3(kOsThreads), 0, s, ka, va, kb, vb, d_n, p, w.dbase, w.status,
+                           w.err);
         u32* t;
         t = ka; ka = kb; kb = t;
         t = va; va = vb; vb = t;
@@ -304,9 +333,9 @@ void radix_sort_pairs(u32* keys, u32* vals, const int* d_n, int bits, PrimWork& 
 }
 
 void scan_exclusive(const u32* in, u32* out, const int* d_n, u32* d_total, PrimWork& w, hipStream_t s) {
-    hipLaunchKernelGGL(k_sc_reduce, dim3(kSortMaxBlocks), dim3(256), 0, s, in, d_n, w.partials);
-    hipLaunchKernelGGL(k_sc_top, dim3(1), dim3(256), 0, s, w.partials, d_n, d_total);
-    hipLaunchKernelGGL(k_sc_down, dim3(kSortMaxBlocks), dim3(256), 0, s, in, out, d_n, w.partials);
+    const unsigned grid = (unsigned)(w.scan_tiles < (size_t)kSortMaxBlocks ? w.scan_tiles : kSortMaxBlocks);
+    hipLaunchKernelGGL(k_scan1, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, in, out, d_n, d_total, w.scan_status,
+                       w.tickets + 5, w.err);
 }
 
 }  // namespace pf
