@@ -17,6 +17,7 @@ struct GridGPU {
     int* dims = nullptr;        // [2][8]   minx,miny,minz, dx,dy,dz, base, valid
     int* d_ncells = nullptr;    // [1]      total cells + 1 (scan length)
     int* err = nullptr;         // [1]      cell capacity exceeded
+    u32* arrive = nullptr;      // [1]      arrival counter of the bounds kernel
     u32* cell_count = nullptr;  // [cell_cap + 1]
     u32* cell_start = nullptr;  // [cell_cap + 1]
     u32* slot = nullptr;        // [pts_cap]

@@ -7,11 +7,6 @@
 namespace pf {
 namespace {
 
-__global__ void k_grid_reset(int* __restrict__ bounds) {
-    const int t = threadIdx.x;
-    if (t < 12) bounds[t] = ((t % 6) < 3) ? INT_MAX : INT_MIN;
-}
-
 __device__ __forceinline__ int wave_min_i(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
@@ -23,45 +18,8 @@ __device__ __forceinline__ int wave_max_i(int v) {
     return v;
 }
 
-// per-map min/max cell coordinates: wave then workgroup reduction, one atomic per workgroup
-__global__ void __launch_bounds__(256) k_grid_bounds(const float4* __restrict__ m0, const int* __restrict__ d_m0,
-                                                      const float4* __restrict__ m1, const int* __restrict__ d_m1,
-                                                      int* __restrict__ bounds) {
-    __shared__ int red[4][12];
-    const int n0 = *d_m0, n1 = m1 ? *d_m1 : 0;
-    const int l = lane_id(), w = threadIdx.x >> 6;
-    int v[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) v[k] = ((k % 6) < 3) ? INT_MAX : INT_MIN;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
-        const int mi = i < n0 ? 0 : 1;
-        const float4 p = mi == 0 ? m0[i] : m1[i - n0];
-        const int c[3] = {(int)floorf(p.x), (int)floorf(p.y), (int)floorf(p.z)};
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            if (mi == 0) { v[k] = min(v[k], c[k]); v[3 + k] = max(v[3 + k], c[k]); }
-            else { v[6 + k] = min(v[6 + k], c[k]); v[9 + k] = max(v[9 + k], c[k]); }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const int r = ((k % 6) < 3) ? wave_min_i(v[k]) : wave_max_i(v[k]);
-        if (l == 0) red[w][k] = r;
-    }
-    __syncthreads();
-    if (threadIdx.x < 12) {
-        const int k = threadIdx.x;
-        const bool is_min = (k % 6) < 3;
-        int r = red[0][k];
-        for (int ww = 1; ww < 4; ++ww) r = is_min ? min(r, red[ww][k]) : max(r, red[ww][k]);
-        if (is_min && r != INT_MAX) atomicMin(&bounds[k], r);
-        if (!is_min && r != INT_MIN) atomicMax(&bounds[k], r);
-    }
-}
-
-__global__ void k_grid_dims(const int* __restrict__ bounds, const int* __restrict__ d_m0, const int* __restrict__ d_m1,
-                            int* __restrict__ dims, int* __restrict__ d_ncells, long long cell_cap, int* __restrict__ err) {
-    if (threadIdx.x != 0) return;
+__device__ void grid_dims(const int* bounds, const int* d_m0, const int* d_m1, int* dims, int* d_ncells,
+                          long long cell_cap, int* err) {
     long long base = 0;
     for (int mi = 0; mi < 2; ++mi) {
         const int n = mi == 0 ? *d_m0 : (d_m1 ? *d_m1 : 0);
@@ -89,9 +47,61 @@ __global__ void k_grid_dims(const int* __restrict__ bounds, const int* __restric
     *d_ncells = (int)(base + 1);
 }
 
-__global__ void __launch_bounds__(256) k_grid_clear(u32* __restrict__ cnt, const int* __restrict__ d_ncells) {
-    const int n = *d_ncells;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) cnt[i] = 0;
+// per-map min/max cell coordinates: wave then workgroup reduction, one atomic per workgroup. The
+// last workgroup to arrive derives the grid dimensions and resets the bounds for the next build.
+__global__ void __launch_bounds__(256) k_grid_bounds(const float4* __restrict__ m0, const int* __restrict__ d_m0,
+                                                      const float4* __restrict__ m1, const int* __restrict__ d_m1,
+                                                      int* __restrict__ bounds, u32* __restrict__ arrive,
+                                                      int* __restrict__ dims, int* __restrict__ d_ncells,
+                                                      long long cell_cap, int* __restrict__ err) {
+    __shared__ int red[4][12];
+    __shared__ int last;
+    __shared__ int lb[12];
+    const int n0 = *d_m0, n1 = m1 ? *d_m1 : 0;
+    const int l = lane_id(), w = threadIdx.x >> 6;
+    int v[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) v[k] = ((k % 6) < 3) ? INT_MAX : INT_MIN;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
+        const int mi = i < n0 ? 0 : 1;
+        const float4 p = mi == 0 ? m0[i] : m1[i - n0];
+        const int c[3] = {(int)floorf(p.x), (int)floorf(p.y), (int)floorf(p.z)};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (mi == 0) { v[k] = min(v[k], c[k]); v[3 + k] = max(v[3 + k], c[k]); }
+            else { v[6 + k] = min(v[6 + k], c[k]); v[9 + k] = max(v[9 + k], c[k]); }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const int r = ((k % 6) < 3) ? wave_min_i(v[k]) : wave_max_i(v[k]);
+        if (l == 0) red[w][k] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        const int k = threadIdx.x;
+        const bool is_min = (k % 6) < 3;
+        int r = red[0][k];
+        for (int ww = 1; ww < 4; ++ww) r = is_min ? min(r, red[ww][k]) : max(r, red[ww][k]);
+        if (is_min && r != INT_MAX) __hip_atomic_fetch_min(&bounds[k], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!is_min && r != INT_MIN) __hip_atomic_fetch_max(&bounds[k], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x < 12) {
+        const int k = threadIdx.x;
+        lb[k] = __hip_atomic_load(&bounds[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bounds[k], ((k % 6) < 3) ? INT_MAX : INT_MIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        grid_dims(lb, d_m0, d_m1, dims, d_ncells, cell_cap, err);
+        __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __device__ __forceinline__ int cell_of(const int* dm, float4 p) {
@@ -116,7 +126,8 @@ __global__ void __launch_bounds__(256) k_grid_count(const float4* __restrict__ m
 __global__ void __launch_bounds__(256) k_grid_scatter(const float4* __restrict__ m0, const int* __restrict__ d_m0,
                                                        const float4* __restrict__ m1, const int* __restrict__ d_m1,
                                                        const int* __restrict__ dims, const u32* __restrict__ start,
-                                                       const u32* __restrict__ slot, float4* __restrict__ cpts) {
+                                                       const u32* __restrict__ slot, float4* __restrict__ cpts,
+                                                       u32* __restrict__ cnt) {
     const int n0 = *d_m0, n1 = m1 ? *d_m1 : 0;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
         const int mi = i < n0 ? 0 : 1;
@@ -124,7 +135,9 @@ __global__ void __launch_bounds__(256) k_grid_scatter(const float4* __restrict__
         if (!dm[7]) continue;
         const int li = mi == 0 ? i : i - n0;
         const float4 p = mi == 0 ? m0[li] : m1[li];
-        cpts[start[cell_of(dm, p)] + slot[i]] = make_float4(p.x, p.y, p.z, __int_as_float(li));
+        const int cid = cell_of(dm, p);
+        cpts[start[cid] + slot[i]] = make_float4(p.x, p.y, p.z, __int_as_float(li));
+        cnt[cid] = 0u;                        // leaves the count array zero for the next build
     }
 }
 
@@ -189,7 +202,13 @@ int grid_alloc(GridGPU& g, size_t pts_cap, size_t cell_cap) {
     if (hipMalloc(&g.cell_start, sizeof(u32) * (cell_cap + 1)) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&g.slot, sizeof(u32) * pts_cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&g.cpts, sizeof(float4) * pts_cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&g.arrive, sizeof(u32)) != hipSuccess) return PF_ENOMEM;
     if (hipMemset(g.err, 0, sizeof(int)) != hipSuccess) return PF_EHIP;
+    if (hipMemset(g.arrive, 0, sizeof(u32)) != hipSuccess) return PF_EHIP;
+    if (hipMemset(g.cell_count, 0, sizeof(u32) * (cell_cap + 1)) != hipSuccess) return PF_EHIP;
+    const int init[12] = {INT_MAX, INT_MAX, INT_MAX, INT_MIN, INT_MIN, INT_MIN,
+                          INT_MAX, INT_MAX, INT_MAX, INT_MIN, INT_MIN, INT_MIN};
+    if (hipMemcpy(g.bounds, init, sizeof(init), hipMemcpyHostToDevice) != hipSuccess) return PF_EHIP;
     return PF_OK;
 }
 
@@ -202,21 +221,19 @@ void grid_free(GridGPU& g) {
     (void)hipFree(g.cell_start);
     (void)hipFree(g.slot);
     (void)hipFree(g.cpts);
+    (void)hipFree(g.arrive);
     g = GridGPU{};
 }
 
 void grid_build(GridGPU& g, const float4* map0, const int* d_m0, const float4* map1, const int* d_m1, PrimWork& w,
                 hipStream_t s) {
     const int nb = 512;
-    hipLaunchKernelGGL(k_grid_reset, dim3(1), dim3(64), 0, s, g.bounds);
-    hipLaunchKernelGGL(k_grid_bounds, dim3(64), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.bounds);
-    hipLaunchKernelGGL(k_grid_dims, dim3(1), dim3(64), 0, s, g.bounds, d_m0, d_m1, g.dims, g.d_ncells,
-                       (long long)g.cell_cap, g.err);
-    hipLaunchKernelGGL(k_grid_clear, dim3(1024), dim3(256), 0, s, g.cell_count, g.d_ncells);
+    hipLaunchKernelGGL(k_grid_bounds, dim3(64), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.bounds, g.arrive, g.dims,
+                       g.d_ncells, (long long)g.cell_cap, g.err);
     hipLaunchKernelGGL(k_grid_count, dim3(nb), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.dims, g.cell_count, g.slot);
     scan_exclusive(g.cell_count, g.cell_start, g.d_ncells, nullptr, w, s);
     hipLaunchKernelGGL(k_grid_scatter, dim3(nb), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.dims, g.cell_start,
-                       g.slot, g.cpts);
+                       g.slot, g.cpts, g.cell_count);
 }
 
 }  // namespace pf

@@ -178,41 +178,6 @@ __global__ void __launch_bounds__(256) k_vg_keys(const float4* __restrict__ e, c
 }
 
 // segment heads of a sorted key array; sentinel keys never start a segment
-__global__ void __launch_bounds__(256) k_seg_heads(const u32* __restrict__ keys, const int* __restrict__ d_n,
-                                                    u32* __restrict__ flags) {
-    const int n = *d_n;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const u32 k = keys[i];
-        flags[i] = (k != kSentinel && (i == 0 || keys[i - 1] != k)) ? 1u : 0u;
-    }
-}
-
-// segment starts; count of cloud-0 segments and of non-sentinel entries
-__global__ void __launch_bounds__(256) k_seg_starts(const u32* __restrict__ keys, const int* __restrict__ d_n,
-                                                     const u32* __restrict__ flags, const u32* __restrict__ segid,
-                                                     u32* __restrict__ segstart, int* __restrict__ cnt) {
-    const int n = *d_n;
-    const int nseg = cnt[C_NSEG];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (n == 0) { cnt[C_NSEG_E] = 0; cnt[C_NRG_VALID] = 0; }
-        else {
-            if (keys[0] == kSentinel) cnt[C_NRG_VALID] = 0;
-            if ((keys[0] >> 31) != 0) cnt[C_NSEG_E] = 0;
-            const u32 kl = keys[n - 1];
-            if (kl != kSentinel) cnt[C_NRG_VALID] = n;
-            if ((kl >> 31) == 0) cnt[C_NSEG_E] = nseg;
-        }
-    }
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        if (flags[i]) segstart[segid[i]] = (u32)i;
-        if (i > 0) {
-            const u32 k = keys[i], kp = keys[i - 1];
-            if ((kp >> 31) == 0 && (k >> 31) == 1) cnt[C_NSEG_E] = (int)segid[i];
-            if (kp != kSentinel && k == kSentinel) cnt[C_NRG_VALID] = i;
-        }
-    }
-}
-
 // one wave per voxel: lanes gather 64 members at a time, the running f32 sums then take them in
 // sorted (stable) order through readlane, so the order of additions is PCL's sequential one
 __device__ __forceinline__ float lane_f(float v, int j) {
@@ -486,10 +451,10 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
     }
 }
 
-__global__ void __launch_bounds__(256) k_pidx_apply(const u32* __restrict__ keys, const u32* __restrict__ tailinc,
-                                                     const int* __restrict__ cnt, float4* __restrict__ map_e,
-                                                     float4* __restrict__ map_s, u32 map_cap) {
-    const int n = cnt[C_NPAIR];
+// the p-index increments of an outer iteration: g = min(255, g + 1) once per valid query sharing the
+// map point (:345-346, :493-496), applied by the tail pair of each neighbour run
+__device__ __forceinline__ void pidx_apply(const u32* keys, const u32* tailinc, int n, float4* map_e, float4* map_s,
+                                           u32 map_cap) {
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const u32 inc = tailinc[p];
         if (!inc) continue;
@@ -497,7 +462,7 @@ __global__ void __launch_bounds__(256) k_pidx_apply(const u32* __restrict__ keys
         float4* mp = k >= map_cap ? map_s : map_e;
         const u32 idx = k >= map_cap ? k - map_cap : k;
         const float4 m = mp[idx];
-        const u32 g = min(255u, w_g(m) + inc);                       // g = min(255, g + 1), c times
+        const u32 g = min(255u, w_g(m) + inc);
         mp[idx].w = __uint_as_float(pack_rg(w_r(m), g));
     }
 }
@@ -751,6 +716,11 @@ struct LmArgs {
     const float* spars;
     int weight_type;
     unsigned long long* dbg;
+    const u32* pair_keys;  // p-index increments, applied by the LM blocks before the solve
+    const u32* tailinc;
+    float4* map_e;
+    float4* map_s;
+    u32 map_cap;
 };
 
 __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
@@ -765,6 +735,8 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     __shared__ LMState lm;
     __shared__ int aborted;
     const int t = threadIdx.x;
+    // the map's p-index bytes are not read by the solve: apply this iteration's increments here
+    pidx_apply(a.pair_keys, a.tailinc, a.cnt[C_NPAIR], a.map_e, a.map_s, a.map_cap);
     const int nres = a.cnt[C_EDGE_KEPT] + a.cnt[C_SURF_KEPT];
     if (!a.st->gate || nres == 0) return;                        // no residual blocks: untouched
     double wmin[2][2], wmax[2][2];
@@ -930,16 +902,16 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
 // ---------------------------------- pose / map update ---------------------------------------
 // mode 1: odom = (q2m(q), t) from the solved pose (:278-280); mode 0: keep odom. Writes the pose
 // {m2q(odom.rotation()), odom.translation()} of the node (copy.cpp:105-107).
-__global__ void k_finalize(DevState* __restrict__ st, double* __restrict__ poses, int pose_cap, int mode,
-                           u32* __restrict__ acc) {
+__device__ __forceinline__ void finalize_pose(DevState* st, double* poses, int pose_cap, int mode, u32* acc,
+                                              const double* prm) {
     const int t = threadIdx.x;
     if (t < 12) acc[A_RG + t] = ((t % 6) < 3) ? 0xFFFFFFFFu : 0u;
     if (t != 0) return;
     if (mode == 1) {
-        const qd q{st->params[0], st->params[1], st->params[2], st->params[3]};
+        const qd q{prm[0], prm[1], prm[2], prm[3]};
         iso o;
         o.R = q2m(q);
-        o.t = d3{st->params[4], st->params[5], st->params[6]};
+        o.t = d3{prm[4], prm[5], prm[6]};
         store_iso(o, st->odomR, st->odomt);
     }
     const iso o = load_iso(st->odomR, st->odomt);
@@ -950,12 +922,22 @@ __global__ void k_finalize(DevState* __restrict__ st, double* __restrict__ poses
     st->frame++;
 }
 
-__global__ void __launch_bounds__(256) k_map_append(const DevState* __restrict__ st, const int* __restrict__ cnt,
+__global__ void k_finalize(DevState* __restrict__ st, double* __restrict__ poses, int pose_cap, int mode,
+                           u32* __restrict__ acc) {
+    double prm[7];
+    for (int k = 0; k < 7; ++k) prm[k] = st->params[k];
+    finalize_pose(st, poses, pose_cap, mode, acc, prm);
+}
+
+// addPointsToMap transform / append (:592-604); block 0 also finalises the pose (k_finalize mode 1)
+__global__ void __launch_bounds__(256) k_map_append(DevState* __restrict__ st, const int* __restrict__ cnt,
                                                      const float4* __restrict__ ds_e, const float4* __restrict__ ds_s,
-                                                     float4* __restrict__ app_e, float4* __restrict__ app_s) {
+                                                     float4* __restrict__ app_e, float4* __restrict__ app_s,
+                                                     double* __restrict__ poses, int pose_cap, u32* __restrict__ acc) {
     const int ne = cnt[C_EDS], ns = cnt[C_SDS];
     double prm[7];
     for (int k = 0; k < 7; ++k) prm[k] = st->params[k];
+    if (blockIdx.x == 0) finalize_pose(st, poses, pose_cap, 1, acc, prm);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ne + ns; i += gridDim.x * blockDim.x) {
         if (i < ne) app_e[i] = associate(prm, ds_e[i]);           // :592-597 (r, g carried)
         else app_s[i - ne] = associate(prm, ds_s[i - ne]);        // :599-604
@@ -1101,22 +1083,15 @@ __global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const f
                                                    float4* __restrict__ map_e, float4* __restrict__ map_s) {
     const int nseg = cnt[C_NSEG], nse = cnt[C_NSEG_E], total = cnt[C_KEEP_TOTAL];
     const int kept_e = nse < nseg ? (int)pos[nse] : total;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        cnt[C_PAD0] = kept_e;
-        cnt[C_PAD1] = total - kept_e;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                  // no block of this kernel reads them
+        cnt[C_ME] = kept_e;
+        cnt[C_MS] = total - kept_e;
     }
     for (int sg = blockIdx.x * blockDim.x + threadIdx.x; sg < nseg; sg += gridDim.x * blockDim.x) {
         if (!keep[sg]) continue;
         const u32 p = pos[sg];
         if (sg < nse) map_e[p] = seg_out[sg];
         else map_s[p - kept_e] = seg_out[sg];
-    }
-}
-
-__global__ void k_map_counts(int* __restrict__ cnt) {
-    if (threadIdx.x == 0) {
-        cnt[C_ME] = cnt[C_PAD0];
-        cnt[C_MS] = cnt[C_PAD1];
     }
 }
 
@@ -1274,10 +1249,7 @@ void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s) {
     hipLaunchKernelGGL(k_vg_keys, dim3(kGrid), dim3(256), 0, s, sb.in_edge, sb.in_surf, cnt, o.acc_a, o.leaf_vg[0],
                        o.leaf_vg[1], o.vkeys, o.vvals);
     radix_sort_pairs(o.vkeys, o.vvals, cnt + C_VGN, 32, o.vprim, s);
-    hipLaunchKernelGGL(k_seg_heads, dim3(kGrid), dim3(256), 0, s, o.vkeys, cnt + C_VGN, o.vflags);
-    scan_exclusive(o.vflags, o.vscan, cnt + C_VGN, (u32*)(cnt + C_NSEG), o.vprim, s);
-    hipLaunchKernelGGL(k_seg_starts, dim3(kGrid), dim3(256), 0, s, o.vkeys, cnt + C_VGN, o.vflags, o.vscan,
-                       o.vsegstart, cnt);
+    segment_starts(o.vkeys, cnt + C_VGN, o.vsegstart, cnt + C_NSEG, cnt + C_NSEG_E, cnt + C_NRG_VALID, o.vprim, s);
     hipLaunchKernelGGL(k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, sb.in_edge, sb.in_surf, o.vkeys, o.vvals,
                        o.vsegstart, cnt, sb.ds_edge, sb.ds_surf);
 }
@@ -1313,31 +1285,24 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
         ObsArgs oa{cnt, o.acc, o.map_e, o.map_s, sb.ds_edge, sb.ds_surf, o.nbr, o.qflag, o.pcnt, o.roundv, o.spars,
                    o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
         hipLaunchKernelGGL(k_observe, dim3(kGrid), dim3(256), 0, s, oa);
-        hipLaunchKernelGGL(k_pidx_apply, dim3(kGrid), dim3(256), 0, s, pk, o.tailinc, cnt, o.map_e, o.map_s,
-                           (u32)o.map_cap);
         LmArgs la{o.st, cnt, o.acc, o.lm, o.lm_part, o.lm_ticket, o.qflag, sb.ds_edge, sb.ds_surf, o.geo, o.observe,
-                  o.spars, o.prm.weight_type, o.dbg};
+                  o.spars, o.prm.weight_type, o.dbg, pk, o.tailinc, o.map_e, o.map_s, (u32)o.map_cap};
         hipLaunchKernelGGL(k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
     }
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, o.st, o.poses, (int)o.pose_cap, 1, o.acc);
-    // addPointsToMap (:589-647)
+    // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647)
     hipLaunchKernelGGL(k_map_append, dim3(kGrid), dim3(256), 0, s, o.st, cnt, sb.ds_edge, sb.ds_surf, o.app_e,
-                       o.app_s);
+                       o.app_s, o.poses, (int)o.pose_cap, o.acc);
     hipLaunchKernelGGL(k_rg_minmax, dim3(128), dim3(256), 0, s, o.st, cnt, o.acc, o.map_e, o.app_e, o.map_s, o.app_s);
     hipLaunchKernelGGL(k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, o.map_e, o.app_e, o.map_s, o.app_s,
                        o.leaf_rg[0], o.leaf_rg[1], o.keys, o.vals);
     radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s);
-    hipLaunchKernelGGL(k_seg_heads, dim3(kGrid), dim3(256), 0, s, o.keys, cnt + C_NRG, o.flags);
-    scan_exclusive(o.flags, o.scan_out, cnt + C_NRG, (u32*)(cnt + C_NSEG), o.prim, s);
-    hipLaunchKernelGGL(k_seg_starts, dim3(kGrid), dim3(256), 0, s, o.keys, cnt + C_NRG, o.flags, o.scan_out,
-                       o.segstart, cnt);
+    segment_starts(o.keys, cnt + C_NRG, o.segstart, cnt + C_NSEG, cnt + C_NSEG_E, cnt + C_NRG_VALID, o.prim, s);
     RgReduceArgs ra{cnt, o.map_e, o.app_e, o.map_s, o.app_s, o.keys, o.vals, o.segstart, o.seg_out, o.flags,
                     o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
     hipLaunchKernelGGL(k_rg_reduce, dim3(kGrid), dim3(256), 0, s, ra);
     scan_exclusive(o.flags, o.scan_out, cnt + C_NSEG, (u32*)(cnt + C_KEEP_TOTAL), o.prim, s);
     hipLaunchKernelGGL(k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, o.flags, o.scan_out, o.map_e,
                        o.map_s);
-    hipLaunchKernelGGL(k_map_counts, dim3(1), dim3(64), 0, s, cnt);
 }
 
 }  // namespace pf

@@ -29,6 +29,12 @@ void prim_free(PrimWork& w);
 void radix_sort_pairs(u32* keys, u32* vals, const int* d_n, int bits, PrimWork& w, hipStream_t s,
                       u32** kout = nullptr, u32** vout = nullptr);
 
+// Segments of stably sorted keys (bit 31 = cloud id, 0xFFFFFFFF = dropped entries, sorted last):
+// segstart[s] = first index of segment s; *d_nseg = number of segments; *d_nseg_c0 = segments of
+// cloud 0; *d_nvalid = number of non-sentinel keys.
+void segment_starts(const u32* keys, const int* d_n, u32* segstart, int* d_nseg, int* d_nseg_c0, int* d_nvalid,
+                    PrimWork& w, hipStream_t s);
+
 // out[i] = sum(in[0..i)) for i < *d_n; *d_total = sum(in[0..n)) when d_total != nullptr.
 void scan_exclusive(const u32* in, u32* out, const int* d_n, u32* d_total, PrimWork& w, hipStream_t s);
 

@@ -193,22 +193,69 @@ __global__ void __launch_bounds__(kOsThreads) k_os_pass(const u32* __restrict__ 
     }
 }
 
-// ---- exclusive scan: one kernel, decoupled look-back ----
+// ---- single-pass scans: decoupled look-back ----
 // Blocks own 2048-item tiles b, b + G, ... (co-resident grid). A tile publishes its aggregate, wave 0
 // looks back over up to 64 predecessors at once (agent-scope atomic words carrying tag << 32 |
 // value), then publishes its inclusive prefix. The last block to finish clears the status words for
 // the next call.
 constexpr int kScanPer = 8;
+
+// wave 0 (all 64 lanes): publish `agg` for `tile`, return its exclusive prefix (all lanes)
+__device__ u32 tile_lookback(u64* status, int tile, u32 agg, int* err) {
+    const int l = lane_id();
+    if (l == 0 && tile > 0)
+        __hip_atomic_store(&status[tile], (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    u32 excl = 0;
+    int j = tile - 1;
+    unsigned spins = 0;
+    while (j >= 0) {
+        const int jj = j - l;
+        const u64 sv = jj >= 0 ? __hip_atomic_load(&status[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : (2ull << 32);                // before tile 0: an inclusive zero
+        const u32 tag = (u32)(sv >> 32);
+        const u64 incl = __ballot(tag == 2);
+        const int first = incl ? __ffsll((long long)incl) - 1 : 64;       // nearest inclusive prefix
+        const u64 upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
+        if (__ballot(tag == 0) & upto) {
+            if (++spins > kSpinLimit) { if (l == 0) atomicOr(err, 1); break; }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        u32 mine = (l <= first && jj >= 0) ? (u32)sv : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+        excl += mine;
+        if (first < 64) break;
+        j -= 64;
+    }
+    if (l == 0)
+        __hip_atomic_store(&status[tile], (2ull << 32) | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
+// the last block of a look-back launch clears the status words and the arrival counter
+__device__ void lookback_finish(u64* status, int ntiles, u32* arrive, int G) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (u32)G - 1;
+    __syncthreads();
+    if (!last) return;
+    for (int i = threadIdx.x; i < ntiles; i += blockDim.x)
+        __hip_atomic_store(&status[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void __launch_bounds__(256) k_scan1(const u32* __restrict__ in, u32* __restrict__ out,
                                                 const int* __restrict__ d_n, u32* __restrict__ d_total,
                                                 u64* __restrict__ status, u32* __restrict__ arrive,
                                                 int* __restrict__ err) {
     __shared__ u32 lw[4];
     __shared__ u32 s_excl;
-    __shared__ int last;
     const int n = *d_n;
     const int ntiles = (n + kSortTile - 1) / kSortTile;
-    const int t = threadIdx.x, l = lane_id();
+    const int t = threadIdx.x;
     const int G = ntiles < (int)gridDim.x ? ntiles : (int)gridDim.x;
     if (n == 0) {
         if (blockIdx.x == 0 && t == 0 && d_total) *d_total = 0u;
@@ -225,35 +272,9 @@ __global__ void __launch_bounds__(256) k_scan1(const u32* __restrict__ in, u32* 
         for (int k = 0; k < kScanPer; ++k) sum += v[k];
         u32 agg;
         const u32 tex = block_excl_scan256(sum, lw, agg);
-        if (t < 64) {                                           // wave 0: publish + look-back
-            if (t == 0 && tile > 0)
-                __hip_atomic_store(&status[tile], (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            u32 excl = 0;
-            int j = tile - 1;
-            unsigned spins = 0;
-            while (j >= 0) {
-                const int jj = j - l;
-                const u64 sv = jj >= 0 ? __hip_atomic_load(&status[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                       : (2ull << 32);        // before tile 0: an inclusive zero
-                const u32 tag = (u32)(sv >> 32);
-                const u64 incl = __ballot(tag == 2);
-                const int first = incl ? __ffsll((long long)incl) - 1 : 64;   // nearest inclusive
-                const u64 notready = __ballot(tag == 0) & (first >= 63 ? ~0ull : ((2ull << first) - 1));
-                if (notready) {
-                    if (++spins > kSpinLimit) { if (l == 0) atomicOr(err, 1); break; }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                u32 mine = (l <= first && jj >= 0) ? (u32)sv : 0u;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
-                excl += mine;
-                if (first < 64) break;
-                j -= 64;
-            }
+        if (t < 64) {
+            const u32 excl = tile_lookback(status, tile, agg, err);
             if (t == 0) {
-                __hip_atomic_store(&status[tile], (2ull << 32) | (excl + agg), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
                 s_excl = excl;
                 if (tile == ntiles - 1 && d_total) *d_total = excl + agg;
             }
@@ -267,14 +288,72 @@ __global__ void __launch_bounds__(256) k_scan1(const u32* __restrict__ in, u32* 
         }
         __syncthreads();
     }
-    // the last block to finish clears the look-back words for the next call
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (u32)G - 1;
-    __syncthreads();
-    if (!last) return;
-    for (int i = t; i < ntiles; i += 256) __hip_atomic_store(&status[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == 0) __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lookback_finish(status, ntiles, arrive, G);
+}
+
+// Segments of sorted keys (bit 31 = cloud, 0xFFFFFFFF = dropped): segment starts, the number of
+// segments, the number of cloud-0 segments and the number of non-sentinel keys, in one pass.
+__global__ void __launch_bounds__(256) k_segments(const u32* __restrict__ keys, const int* __restrict__ d_n,
+                                                   u32* __restrict__ segstart, int* __restrict__ d_nseg,
+                                                   int* __restrict__ d_nseg_c0, int* __restrict__ d_nvalid,
+                                                   u64* __restrict__ status, u32* __restrict__ arrive,
+                                                   int* __restrict__ err) {
+    constexpr u32 kSent = 0xFFFFFFFFu;
+    __shared__ u32 lw[4];
+    __shared__ u32 s_excl;
+    const int n = *d_n;
+    const int ntiles = (n + kSortTile - 1) / kSortTile;
+    const int t = threadIdx.x;
+    const int G = ntiles < (int)gridDim.x ? ntiles : (int)gridDim.x;
+    if (n == 0) {
+        if (blockIdx.x == 0 && t == 0) { *d_nseg = 0; *d_nseg_c0 = 0; *d_nvalid = 0; }
+        return;
+    }
+    if ((int)blockIdx.x >= G) return;
+    if (blockIdx.x == 0 && t == 0) {                            // cases without an interior boundary
+        const u32 k0 = keys[0], kl = keys[n - 1];
+        if (k0 == kSent) *d_nvalid = 0;
+        if ((k0 >> 31) != 0) *d_nseg_c0 = 0;
+        if (kl != kSent) *d_nvalid = n;
+    }
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int base = tile * kSortTile + t * kScanPer;
+        u32 k[kScanPer + 1];                                    // k[0] = predecessor of the first
+        k[0] = base > 0 && base - 1 < n ? keys[base - 1] : kSent;
+#pragma unroll
+        for (int j = 0; j < kScanPer; ++j) k[j + 1] = base + j < n ? keys[base + j] : kSent;
+        u32 sum = 0;
+#pragma unroll
+        for (int j = 0; j < kScanPer; ++j) {
+            const bool head = base + j < n && k[j + 1] != kSent && (base + j == 0 || k[j] != k[j + 1]);
+            sum += head ? 1u : 0u;
+        }
+        u32 agg;
+        const u32 tex = block_excl_scan256(sum, lw, agg);
+        if (t < 64) {
+            const u32 excl = tile_lookback(status, tile, agg, err);
+            if (t == 0) {
+                s_excl = excl;
+                if (tile == ntiles - 1) {
+                    *d_nseg = (int)(excl + agg);
+                    if ((keys[n - 1] >> 31) == 0) *d_nseg_c0 = (int)(excl + agg);
+                }
+            }
+        }
+        __syncthreads();
+        u32 sid = s_excl + tex;                                 // segments before element base + j
+#pragma unroll
+        for (int j = 0; j < kScanPer; ++j) {
+            const int i = base + j;
+            if (i >= n) break;
+            const u32 kp = k[j], kc = k[j + 1];
+            if (i > 0 && (kp >> 31) == 0 && (kc >> 31) == 1) *d_nseg_c0 = (int)sid;
+            if (i > 0 && kp != kSent && kc == kSent) *d_nvalid = i;
+            if (kc != kSent && (i == 0 || kp != kc)) segstart[sid++] = (u32)i;
+        }
+        __syncthreads();
+    }
+    lookback_finish(status, ntiles, arrive, G);
 }
 
 }  // namespace
@@ -330,6 +409,13 @@ void radix_sort_pairs(u32* keys, u32* vals, const int* d_n, int bits, PrimWork& 
     }
     if (kout) *kout = ka;
     if (vout) *vout = va;
+}
+
+void segment_starts(const u32* keys, const int* d_n, u32* segstart, int* d_nseg, int* d_nseg_c0, int* d_nvalid,
+                    PrimWork& w, hipStream_t s) {
+    const unsigned grid = (unsigned)(w.scan_tiles < (size_t)kSortMaxBlocks ? w.scan_tiles : kSortMaxBlocks);
+    hipLaunchKernelGGL(k_segments, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, keys, d_n, segstart, d_nseg, d_nseg_c0,
+                       d_nvalid, w.scan_status, w.tickets + 5, w.err);
 }
 
 void scan_exclusive(const u32* in, u32* out, const int* d_n, u32* d_total, PrimWork& w, hipStream_t s) {
