@@ -169,6 +169,27 @@ def cpu_baseline(budget_s, warmup):
                       "after %d warm-up frames, single thread, %.1f s of CPU time" % (warmup, k - 1, warmup, el)}
 
 
+def reduce_results(dist, elapsed, frames, poses, device):
+    """Across ranks: the max elapsed time, the total frame count and every rank's pose array. The
+    pose all-gather is the design's only collective (RCCL over xGMI on the GPU box; any
+    torch.distributed backend here)."""
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    f = torch.tensor([frames], dtype=torch.int64, device=device)
+    dist.all_reduce(f, op=dist.ReduceOp.SUM)
+    p = torch.from_numpy(np.ascontiguousarray(poses, dtype=np.float64)).to(device)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(dist.get_world_size())]
+    dist.all_gather(sizes, torch.tensor([p.shape[0]], dtype=torch.int64, device=device))
+    cap = int(max(int(x.item()) for x in sizes))
+    padded = torch.zeros((cap, 7), dtype=torch.float64, device=device)
+    padded[:p.shape[0]] = p
+    gathered = [torch.empty_like(padded) for _ in range(dist.get_world_size())]
+    dist.all_gather(gathered, padded)
+    poses_all = [g[:int(n.item())].cpu().numpy() for g, n in zip(gathered, sizes)]
+    return float(t.item()), int(f.item()), poses_all
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -190,17 +211,7 @@ def main():
     r = run_gpu(rank, local_rank, world, args.steps, args.warmup, threads, not args.no_graph, barrier)
     elapsed, frames = r["elapsed"], r["frames"]
     if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        f = torch.tensor([frames], dtype=torch.int64, device="cuda")
-        dist.all_reduce(f, op=dist.ReduceOp.SUM)
-        total_frames = int(f.item())
-        # the one collective of the design: gather every rank's pose array over RCCL
-        p = torch.from_numpy(np.ascontiguousarray(r["poses"][-frames:])).cuda()
-        gathered = [torch.empty_like(p) for _ in range(world)]
-        dist.all_gather(gathered, p)
+        elapsed, total_frames, _ = reduce_results(dist, elapsed, frames, r["poses"][-frames:], "cuda")
     else:
         total_frames = frames
     if rank != 0:

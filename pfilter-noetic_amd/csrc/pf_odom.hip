@@ -517,6 +517,7 @@ struct LmCore {
     double x[7], cand[7], best[7], scale[6], g[6], H[21], D[6];
     double cost, radius, decrease, x_norm, min_cost, mcc;
     int iteration, invalid, reuse, done, phase;
+    unsigned long long* pp;
 };
 __device__ __forceinline__ void core_load(LmCore& c, const LMState& s) {
 #pragma unroll
@@ -541,6 +542,7 @@ __device__ __forceinline__ void core_store(const LmCore& c, LMState& s) {
     s.iteration = c.iteration; s.invalid = c.invalid; s.reuse = c.reuse; s.done = c.done; s.phase = c.phase;
 }
 
+#define probe(k) do { if (lm.pp) lm.pp[(k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 // TrustRegionMinimizer + LevenbergMarquardtStrategy: next candidate, or done. The scaled
 // J^T J + D is factored in place (packed lower Cholesky); Hs entries are recomputed from H.
 __device__ __forceinline__ void lm_next_step(LmCore& lm) {
@@ -562,6 +564,8 @@ __device__ __forceinline__ void lm_next_step(LmCore& lm) {
             const double ld = sqrt(lm.D[j] / lm.radius);
             A[tri(j, j)] += ld * ld;
         }
+        probe(49);
+        probe(50);
         bool ok = true;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -594,6 +598,7 @@ __device__ __forceinline__ void lm_next_step(LmCore& lm) {
         }
 #pragma unroll
         for (int j = 0; j < 6; ++j) ok = ok && isfinite(y[j]);
+        probe(51);
         lm.reuse = 1;
         double mcc = 0.0;
         if (ok) {
@@ -619,7 +624,9 @@ __device__ __forceinline__ void lm_next_step(LmCore& lm) {
         double delta[6];
 #pragma unroll
         for (int j = 0; j < 6; ++j) delta[j] = -y[j] * lm.scale[j];
+        probe(52);
         se3_plus(lm.x, delta, lm.cand);
+        probe(53);
         lm.mcc = mcc;
         lm.phase = 1;
         return;
@@ -695,6 +702,7 @@ __device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot) {
         lm.decrease *= 2.0;
         lm.reuse = 1;
     }
+    probe(48);
     if (lm.iteration >= kMaxIter) lm.done = 1;
     else if (step_ok && grad_max_norm(lm.x, lm.g) <= 1e-10) lm.done = 1;
     else if (lm.radius <= 1e-32) lm.done = 1;
@@ -884,6 +892,8 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         if (rec) dbg[40 + ev] = __builtin_amdgcn_s_memrealtime();
         if (t == 0) {
             LmCore c;
+            c.pp = (rec && ev == 2) ? dbg : nullptr;
+            if (c.pp) c.pp[47] = __builtin_amdgcn_s_memrealtime();
             core_load(c, lm);
             lm_accept(c, tot);
             if (ev == kLmEvals - 1) c.done = 1;

@@ -1,0 +1,20 @@
+// Drop-in replacement for the ES estimator of the reference's include/odomEstimationClass.h
+// (Odom_ES_EstimationClass, :140-163): same class name, call signatures and public members (odom,
+// laserCloudCornerMap, laserCloudSurfMap) for src/odomEstimationNode copy.cpp, with the whole
+// updatePointsToMap on the MI355X through libpfilter_hip.so.
+#ifndef _ODOM_ESTIMATION_CLASS_H_
+#define _ODOM_ESTIMATION_CLASS_H_
+
+#include <pcl/point_cloud.h>
+#include <pcl/point_types.h>
+
+#include <Eigen/Dense>
+#include <Eigen/Geometry>
+
+#include "lidar.h"
+#include "pfilter_hip_shim.hpp"
+
+typedef pcl::PointXYZRGB PointType;
+using Odom_ES_EstimationClass = pfilter_hip::Odom_ES_EstimationClassT<pcl::PointCloud<PointType>, lidar::Lidar>;
+
+#endif  // _ODOM_ESTIMATION_CLASS_H_

@@ -1,0 +1,234 @@
+// Header-only C++ drop-in for the reference classes on the odometry hot path, over the C ABI of
+// libpfilter_hip.so (include/pfilter_hip.h). Same names, same call signatures, same public members
+// as the reference:
+//
+//   LaserProcessingClass::init / featureExtraction        include/laserProcessingClass.h:36-37
+//   Odom_ES_EstimationClass::init / initMapWithPoints /
+//       updatePointsToMap / getMap, members odom,
+//       laserCloudCornerMap, laserCloudSurfMap            include/odomEstimationClass.h:140-152
+//
+// The classes are templates over the point-cloud and lidar types so this header needs neither PCL nor
+// ROS; shim/laserProcessingClass.h and shim/odomEstimationClass.h instantiate them with the PCL 1.10
+// types the ROS nodes use. Requirements on the types:
+//   Cloud:  Cloud::Ptr (shared pointer), `points` (contiguous vector of points), push_back, clear
+//   Point:  standard layout with float x, y, z at offsets 0, 4, 8 (PCL's 32-byte points qualify);
+//           PointXYZI also has `intensity`, PointXYZRGB the `r`, `g`, `b` bytes
+//   Lidar:  num_lines, min_distance, max_distance, scan_period (lidar::Lidar, include/lidar.h:9-30)
+//
+// Error behaviour mirrors the reference, which prints and continues: the warnings of
+// updatePointsToMap ("not enough points in map to associate, map error", "not enough correct
+// points") are printed to stdout the same way; hard errors (bad arguments, HIP failures) throw
+// pfilter_hip::Error, since the reference would crash or run into undefined behaviour there.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "../../include/pfilter_hip.h"
+
+#ifndef PFILTER_HIP_NO_EIGEN
+#include <Eigen/Geometry>
+#endif
+
+namespace pfilter_hip {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(const char* fn, int c) : std::runtime_error(std::string(fn) + " failed with status " + std::to_string(c)), code(c) {}
+};
+
+inline int check(const char* fn, int rc) {
+    if (rc < 0) throw Error(fn, rc);
+    return rc;
+}
+
+#ifdef PFILTER_HIP_NO_EIGEN
+// minimal stand-in for Eigen::Isometry3d when Eigen is not available (tests)
+struct Pose {
+    double q[4] = {0, 0, 0, 1};   // x, y, z, w
+    double t[3] = {0, 0, 0};
+};
+#endif
+
+template <class Lidar>
+inline pf_lidar_params lidar_params(const Lidar& l) {
+    pf_lidar_params p;
+    p.num_lines = l.num_lines;
+    p.min_dist = l.min_distance;
+    p.max_dist = l.max_distance;
+    p.scan_period = l.scan_period;
+    return p;
+}
+
+// --------------------------------------------------------------------------------------------
+template <class CloudXYZI, class Lidar>
+class LaserProcessingClassT {
+public:
+    using Ptr = typename CloudXYZI::Ptr;
+    using Point = typename std::decay<decltype(std::declval<CloudXYZI>().points[0])>::type;
+
+    explicit LaserProcessingClassT(int device = 0, size_t max_points = 300000) : device_(device), max_points_(max_points) {}
+    ~LaserProcessingClassT() { if (h_) pf_fe_destroy(h_); }
+    LaserProcessingClassT(const LaserProcessingClassT&) = delete;
+    LaserProcessingClassT& operator=(const LaserProcessingClassT&) = delete;
+
+    void init(Lidar lidar_param_in) {
+        if (h_) { pf_fe_destroy(h_); h_ = nullptr; }
+        const pf_lidar_params p = lidar_params(lidar_param_in);
+        check("pf_fe_create", pf_fe_create(&p, device_, max_points_, &h_));
+    }
+
+    // appends to pc_out_edge / pc_out_surf, never modifies pc_in (laserProcessingClass.cpp:10-96)
+    void featureExtraction(const Ptr& pc_in, Ptr& pc_out_edge, Ptr& pc_out_surf) {
+        const size_t n = pc_in->points.size();
+        buf_e_.resize(4 * (n ? n : 1));
+        buf_s_.resize(4 * (n ? n : 1));
+        size_t ne = 0, ns = 0;
+        const float* src = n ? reinterpret_cast<const float*>(&pc_in->points[0]) : nullptr;
+        check("pf_fe_extract", pf_fe_extract(h_, src, n, sizeof(Point), buf_e_.data(), &ne, buf_s_.data(), &ns,
+                                             n ? n : 1));
+        append(buf_e_, ne, *pc_out_edge);
+        append(buf_s_, ns, *pc_out_surf);
+    }
+
+private:
+    static void append(const std::vector<float>& b, size_t n, CloudXYZI& out) {
+        for (size_t i = 0; i < n; ++i) {
+            Point p;
+            p.x = b[4 * i];
+            p.y = b[4 * i + 1];
+            p.z = b[4 * i + 2];
+            p.intensity = b[4 * i + 3];
+            out.push_back(p);
+        }
+    }
+    int device_;
+    size_t max_points_;
+    pf_fe* h_ = nullptr;
+    std::vector<float> buf_e_, buf_s_;
+};
+
+// --------------------------------------------------------------------------------------------
+template <class CloudXYZRGB, class Lidar>
+class Odom_ES_EstimationClassT {
+public:
+    using Ptr = typename CloudXYZRGB::Ptr;
+    using Point = typename std::decay<decltype(std::declval<CloudXYZRGB>().points[0])>::type;
+
+    explicit Odom_ES_EstimationClassT(int device = 0, size_t max_points = 300000, size_t map_capacity = (size_t)1 << 22)
+        : laserCloudCornerMap(new CloudXYZRGB()), laserCloudSurfMap(new CloudXYZRGB()), device_(device),
+          max_points_(max_points), map_capacity_(map_capacity) {}
+    ~Odom_ES_EstimationClassT() { if (h_) pf_odom_destroy(h_); }
+    Odom_ES_EstimationClassT(const Odom_ES_EstimationClassT&) = delete;
+    Odom_ES_EstimationClassT& operator=(const Odom_ES_EstimationClassT&) = delete;
+
+    // include/odomEstimationClass.h:146 (weightType is a double there; 0, 1, 2 or 12)
+    void init(Lidar lidar_param, double map_resolution_in, int k_new_para, float theta_p_para, int theta_max_para,
+              double weightType_para) {
+        if (h_) { pf_odom_destroy(h_); h_ = nullptr; }
+        const pf_lidar_params lp = lidar_params(lidar_param);
+        pf_odom_params op;
+        op.map_res = map_resolution_in;
+        op.k_new = k_new_para;
+        op.theta_p = theta_p_para;
+        op.theta_max = theta_max_para;
+        op.weight_type = (int)weightType_para;
+        check("pf_odom_create", pf_odom_create(&lp, &op, device_, max_points_, map_capacity_, &h_));
+        set_identity();
+        laserCloudCornerMap->clear();
+        laserCloudSurfMap->clear();
+    }
+
+    void initMapWithPoints(const Ptr& edge_in, const Ptr& surf_in) {
+        check("pf_odom_init_map", pf_odom_init_map(h_, data(edge_in), edge_in->points.size(), sizeof(Point),
+                                                   data(surf_in), surf_in->points.size(), sizeof(Point)));
+        refresh();
+    }
+
+    void updatePointsToMap(const Ptr& edge_in, const Ptr& surf_in) {
+        double pose[7];
+        const int rc = check("pf_odom_update", pf_odom_update(h_, data(edge_in), edge_in->points.size(), sizeof(Point),
+                                                              data(surf_in), surf_in->points.size(), sizeof(Point),
+                                                              pose));
+        // the reference's messages (src/odomEstimationClass.cpp:276, 428-431, 574-577)
+        if (rc == PF_W_MAP_TOO_SMALL) std::printf("not enough points in map to associate, map error\n");
+        if (rc == PF_W_FEW_CORRESPONDENCES) std::printf("not enough correct points\n");
+        set_pose(pose);
+        refresh();
+    }
+
+    // surf map then corner map, appended (src/odomEstimationClass.cpp:210-215)
+    void getMap(Ptr& laserCloudMap) {
+        for (const auto& p : laserCloudSurfMap->points) laserCloudMap->push_back(p);
+        for (const auto& p : laserCloudCornerMap->points) laserCloudMap->push_back(p);
+    }
+
+    // false: the map members are only refreshed by syncMaps() (saves the D2H copy per frame when no
+    // subscriber reads them, as in src/odomEstimationNode copy.cpp:129-141)
+    bool refresh_maps_every_frame = true;
+    void syncMaps() { read_map(0, *laserCloudCornerMap); read_map(1, *laserCloudSurfMap); }
+
+#ifndef PFILTER_HIP_NO_EIGEN
+    Eigen::Isometry3d odom = Eigen::Isometry3d::Identity();
+#else
+    Pose odom;
+#endif
+    Ptr laserCloudCornerMap;
+    Ptr laserCloudSurfMap;
+
+private:
+    static const float* data(const Ptr& c) {
+        return c->points.empty() ? nullptr : reinterpret_cast<const float*>(&c->points[0]);
+    }
+    void set_identity() {
+        const double id[7] = {0, 0, 0, 1, 0, 0, 0};
+        set_pose(id);
+    }
+    void set_pose(const double* p) {
+#ifndef PFILTER_HIP_NO_EIGEN
+        // odom = I; linear = q.toRotationMatrix(); translation = t (src/odomEstimationClass.cpp:278-280)
+        const Eigen::Quaterniond q(p[3], p[0], p[1], p[2]);
+        odom = Eigen::Isometry3d::Identity();
+        odom.linear() = q.toRotationMatrix();
+        odom.translation() = Eigen::Vector3d(p[4], p[5], p[6]);
+#else
+        for (int k = 0; k < 4; ++k) odom.q[k] = p[k];
+        for (int k = 0; k < 3; ++k) odom.t[k] = p[4 + k];
+#endif
+    }
+    void refresh() {
+        if (refresh_maps_every_frame) syncMaps();
+    }
+    void read_map(int which, CloudXYZRGB& out) {
+        size_t n = 0;
+        check("pf_odom_get_map", pf_odom_get_map(h_, which, nullptr, nullptr, 0, &n));
+        xyz_.resize(3 * (n ? n : 1));
+        rg_.resize(2 * (n ? n : 1));
+        check("pf_odom_get_map", pf_odom_get_map(h_, which, xyz_.data(), rg_.data(), n, &n));
+        out.clear();
+        for (size_t i = 0; i < n; ++i) {
+            Point p;
+            p.x = xyz_[3 * i];
+            p.y = xyz_[3 * i + 1];
+            p.z = xyz_[3 * i + 2];
+            p.r = rg_[2 * i];        // rounds / age
+            p.g = rg_[2 * i + 1];    // observation count (p-index)
+            p.b = 0;
+            out.push_back(p);
+        }
+    }
+    int device_;
+    size_t max_points_, map_capacity_;
+    pf_odom* h_ = nullptr;
+    std::vector<float> xyz_;
+    std::vector<uint8_t> rg_;
+};
+
+}  // namespace pfilter_hip

@@ -47,3 +47,10 @@ def test_header_compiles_as_c():
             f.write('#include "pfilter_hip.h"\nint main(void){return 0;}\n')
         subprocess.check_call(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
                                "-c", c, "-o", os.path.join(d, "t.o")])
+
+
+def test_cpp_shim_compiles():
+    """The header-only C++ drop-in (pfilter-noetic_amd/shim) compiles against PCL-shaped types."""
+    import subprocess
+    subprocess.check_call(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "shim", "shim_driver.cpp")])

@@ -109,3 +109,14 @@ def test_fe_capacity_error(pa):
     with pytest.raises(pa.PFError) as ei:
         fe.featureExtraction(np.ones((1001, 4), np.float32))
     assert ei.value.code == pa.PF_ECAPACITY
+
+
+def test_fe_golden(pa, pfsynth):
+    """Against the committed oracle vectors (tests/golden/fe_s32_f3.npz)."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fe_s32_f3.npz"))
+    x = pfsynth.Sequence("S32", n_frames=6, az_steps=600).frame(3)
+    fe = _fe(pa, 32)
+    e, s = fe.featureExtraction(x)
+    _same(e, g["edge"])
+    _same(s, g["surf"])

@@ -61,3 +61,15 @@ def test_knn_tiny_map(pa, pfref):
     gi, gd = kn.query(q)
     assert list(gi[0, :3]) == [0, 1, 2] and np.all(gi[0, 3:] == -1)
     assert np.all(gi[1] == -1)
+
+
+def test_knn_golden(pa):
+    """Against the committed vectors (tests/golden/knn_3000x400.npz): gated neighbours bit-exact."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "knn_3000x400.npz"))
+    kn = pa.Knn(g["map"].shape[0], g["queries"].shape[0])
+    kn.set_map(g["map"])
+    gi, gd = kn.query(g["queries"])
+    inside = g["d2"] < 1.0
+    np.testing.assert_array_equal(np.where(inside, g["idx"], -1), gi)
+    np.testing.assert_array_equal(gd[inside].view(np.uint32), g["d2"][inside].view(np.uint32))

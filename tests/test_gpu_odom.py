@@ -195,3 +195,22 @@ def test_long_sequence_matches_oracle(pa, pfref, pfsynth):
     gt = np.array([seq.gt_pose(k) for k in range(n)])
     assert np.max(2 * np.arctan2(gt[:, 2], gt[:, 3])) > 1.5          # heading passed 90 degrees
     assert np.linalg.norm(p[-1, 4:6] - gt[-1, 4:6]) < 0.01 * 400.0     # planar drift < 1 %
+
+
+def test_golden_trajectory(pa):
+    """The device pipeline against the committed oracle trajectory (tests/golden/odom_s64_24f.npz)."""
+    import os
+    import pfsynth
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "odom_s64_24f.npz"))
+    seq = pfsynth.Sequence("S64", n_frames=30, az_steps=1000)
+    od = pa.Odom_ES_EstimationClass(device=0)
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    for k in range(24):
+        p = od.frame_host(seq.frame(k))
+        dt, dr = pose_err(p, g["gpu_equiv_poses"][k])
+        assert dt < TOL_T and dr < TOL_R, (k, dt, dr)
+        st = od.stats()
+        got = [st[c] for c in ("n_edge_in", "n_surf_in", "n_edge_ds", "n_surf_ds", "n_edge_map", "n_surf_map",
+                               "n_edge_res", "n_surf_res")]
+        if k > 0:
+            assert got == list(g["gpu_equiv_counts"][k]), (k, got)

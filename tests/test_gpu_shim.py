@@ -1,0 +1,41 @@
+"""GPU: the C++ drop-in classes (pfilter-noetic_amd/shim) driven like the ROS nodes
+(tests/shim/shim_driver.cpp), against the same frames through the Python binding of the same C ABI:
+identical poses and map sizes."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
+    exe = str(tmp_path / "shim_driver")
+    lib = os.path.join(ROOT, "pfilter-noetic_amd")
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "shim", "shim_driver.cpp"), "-o", exe, "-L", lib,
+                           "-lpfilter_hip", "-Wl,-rpath," + lib, "-Wl,-rpath-link,/opt/rocm/lib"])
+    seq = pfsynth.Sequence("S64", n_frames=8, az_steps=1200)
+    frames = [seq.frame(k) for k in range(8)]
+    with open(tmp_path / "frames.bin", "wb") as f:
+        for x in frames:
+            np.array([x.shape[0]], np.int64).tofile(f)
+            x.astype(np.float32).tofile(f)
+    subprocess.check_call([exe, str(tmp_path / "frames.bin"), str(tmp_path / "poses.txt")], timeout=120)
+    got = np.loadtxt(tmp_path / "poses.txt")
+    lid = pa.make_lidar(64, 3.0, 90.0)
+    fe = pa.LaserProcessingClass()
+    fe.init(lid)
+    od = pa.Odom_ES_EstimationClass()
+    od.init(lid, 0.4, 0, 0.4, 75, 0)
+    for k, x in enumerate(frames):
+        e, s = fe.featureExtraction(x)
+        if k == 0:
+            od.initMapWithPoints(e, s)
+        else:
+            od.updatePointsToMap(e, s)
+        np.testing.assert_array_equal(got[k, :7], od.odom)
+        assert got[k, 7] == od.laserCloudCornerMap[0].shape[0]
+        assert got[k, 8] == od.laserCloudSurfMap[0].shape[0]

@@ -1,0 +1,92 @@
+"""Regenerate tests/golden/*.npz: oracle (pfref) outputs on seeded synthetic inputs.
+
+The reference ships no fixtures and cannot be built here, so these vectors pin the
+oracle against regressions and give the GPU tests an oracle-free comparison; they are NOT outputs of
+the reference itself ("parity unpinned" at the PCL/Eigen/FLANN/Ceres boundary).
+Inputs are regenerated from the seeded generator at test time and checked against the stored hash.
+
+  python tools/make_golden.py
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "pfilter-noetic_amd", "synth")):
+    sys.path.insert(0, p)
+import pfref  # noqa: E402
+import pfsynth  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def fe_case():
+    seq = pfsynth.Sequence("S32", n_frames=6, az_steps=600)
+    x = seq.frame(3)
+    e, s = pfref.feature_extraction(x, pfref.make_lidar(32, 3.0, 90.0), opts=pfref.FE_STABLE_TIES)
+    np.savez_compressed(os.path.join(OUT, "fe_s32_f3.npz"), input_sha=sha(x), n_in=x.shape[0], edge=e, surf=s,
+                        spec=np.array(["S32", "n_frames=6", "az_steps=600", "frame=3", "lines=32", "3-90 m",
+                                       "opts=FE_STABLE_TIES"]))
+    print("fe", x.shape, e.shape, s.shape)
+
+
+def odom_case():
+    seq = pfsynth.Sequence("S64", n_frames=30, az_steps=1000)
+    frames = [seq.frame(k) for k in range(24)]
+    out = {"input_sha": np.array([sha(x) for x in frames])}
+    for name, opts in (("gpu_equiv", pfref.GPU_EQUIV), ("faithful", 0)):
+        od = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=opts)
+        poses, counts = [], []
+        for x in frames:
+            poses.append(od.frame(x))
+            st = od.stats()
+            counts.append([st[k] for k in ("n_edge_in", "n_surf_in", "n_edge_ds", "n_surf_ds", "n_edge_map",
+                                           "n_surf_map", "n_edge_res", "n_surf_res")])
+        out[name + "_poses"] = np.array(poses)
+        out[name + "_counts"] = np.array(counts, np.int64)
+        ex, er = od.get_map(0)
+        sx, sr = od.get_map(1)
+        out[name + "_map_sha"] = np.array([sha(ex), sha(er), sha(sx), sha(sr)])
+    np.savez_compressed(os.path.join(OUT, "odom_s64_24f.npz"), **out,
+                        spec=np.array(["S64", "n_frames=30", "az_steps=1000", "frames 0-23", "lines=64",
+                                       "3-90 m", "map 0.4", "k_new 0", "theta_p 0.4", "theta_max 75", "weight 0"]))
+    print("odom", out["gpu_equiv_poses"][-1])
+
+
+def knn_case():
+    rng = np.random.default_rng(11)
+    mp = np.zeros((3000, 4), np.float32)
+    mp[:, :3] = rng.uniform(-8, 8, (3000, 3))
+    mp[:800, 2] = 0.0
+    q = np.zeros((400, 4), np.float32)
+    q[:, :3] = rng.uniform(-9, 9, (400, 3))
+    idx, d2 = pfref.knn(mp, q, 5, opts=pfref.KNN_BRUTE)
+    np.savez_compressed(os.path.join(OUT, "knn_3000x400.npz"), map=mp, queries=q, idx=idx, d2=d2)
+    print("knn", idx.shape)
+
+
+def grid_case():
+    rng = np.random.default_rng(12)
+    xyz = rng.uniform(-3, 3, (2500, 3)).astype(np.float32)
+    xyz[:400] = np.round(xyz[:400] * 2.5) / np.float32(2.5)
+    r = rng.integers(0, 256, 2500)
+    g = rng.integers(0, 256, 2500)
+    pts = pfref.pack_rgb(xyz, r=r, g=g)
+    vg = pfref.voxel_grid(pts, 0.8, opts=pfref.VG_STABLE)
+    rg = pfref.rgbds(pts, 0.4, opts=pfref.VG_STABLE)
+    np.savez_compressed(os.path.join(OUT, "voxel_2500.npz"), points=pts, voxel_grid_08=vg, rgbds_04=rg)
+    print("voxel", vg.shape, rg.shape)
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    fe_case()
+    odom_case()
+    knn_case()
+    grid_case()
