@@ -239,20 +239,27 @@ PF_HD m3 skew(d3 v) {
     return s;
 }
 
+// getTransformFromSe3 (src/lidarOptimization.cpp:106-143). One sincos of theta/2 serves all four
+// trigonometric terms: sin(theta) = 2 s c and 1 - cos(theta) = 2 s^2 (half-angle identities), and
+// theta^3 is a product where the source calls pow; each differs from the source's libm calls by at
+// most an ulp or two, far inside the pose tolerance, and saves three transcendental evaluations on
+// the LM's serial path.
 PF_HD void se3_exp(const double* se3, qd& q, d3& t) {
     d3 omega{se3[0], se3[1], se3[2]};
     d3 upsilon{se3[3], se3[4], se3[5]};
     m3 Om = skew(omega);
     const double theta = nrm3(omega);
     const double half_theta = 0.5 * theta;
+    double s_h, c_h;
+    sincos(half_theta, &s_h, &c_h);
     double imag_factor;
-    const double real_factor = cos(half_theta);
+    const double real_factor = c_h;
     if (theta < 1e-10) {
         const double theta_sq = theta * theta;
         const double theta_po4 = theta_sq * theta_sq;
         imag_factor = 0.5 - 0.0208333 * theta_sq + 0.000260417 * theta_po4;
     } else {
-        imag_factor = sin(half_theta) / theta;
+        imag_factor = s_h / theta;
     }
     q = qd{imag_factor * omega.x, imag_factor * omega.y, imag_factor * omega.z, real_factor};
     m3 J;
@@ -260,8 +267,8 @@ PF_HD void se3_exp(const double* se3, qd& q, d3& t) {
         J = q2m(q);
     } else {
         m3 Om2 = m3_mul(Om, Om);
-        const double a = (1.0 - cos(theta)) / (theta * theta);
-        const double b = (theta - sin(theta)) / pow(theta, 3.0);
+        const double a = (2.0 * (s_h * s_h)) / (theta * theta);                // (1 - cos) / theta^2
+        const double b = (theta - 2.0 * (s_h * c_h)) / (theta * theta * theta); // (theta - sin) / theta^3
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) J.m[i][j] = (i == j ? 1.0 : 0.0) + a * Om.m[i][j] + b * Om2.m[i][j];
     }

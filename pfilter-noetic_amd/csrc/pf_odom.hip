@@ -500,24 +500,12 @@ __device__ __forceinline__ int hup(int i, int j) {
 }
 __device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }   // lower, j <= i
 
-__device__ double grad_max_norm(const double* x, const double* g) {
-    double ng[6], xp[7];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) ng[j] = -g[j];
-    se3_plus(x, ng, xp);
-    double m = 0.0;
-#pragma unroll
-    for (int j = 0; j < 7; ++j) m = fmax(m, fabs(x[j] - xp[j]));
-    return m;
-}
-
 // The LM state lane 0 works on, held in registers during a step (loaded from / stored to the
 // LDS LMState around it); every loop is fully unrolled so all indices are static.
 struct LmCore {
     double x[7], cand[7], best[7], scale[6], g[6], H[21], D[6];
     double cost, radius, decrease, x_norm, min_cost, mcc;
     int iteration, invalid, reuse, done, phase;
-    unsigned long long* pp;
 };
 __device__ __forceinline__ void core_load(LmCore& c, const LMState& s) {
 #pragma unroll
@@ -542,78 +530,90 @@ __device__ __forceinline__ void core_store(const LmCore& c, LMState& s) {
     s.iteration = c.iteration; s.invalid = c.invalid; s.reuse = c.reuse; s.done = c.done; s.phase = c.phase;
 }
 
-#define probe(k) do { if (lm.pp) lm.pp[(k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-// TrustRegionMinimizer + LevenbergMarquardtStrategy: next candidate, or done. The scaled
-// J^T J + D is factored in place (packed lower Cholesky); Hs entries are recomputed from H.
-__device__ __forceinline__ void lm_next_step(LmCore& lm) {
+// One attempt of LevenbergMarquardtStrategy::ComputeStep on the current state, without mutating it:
+// D (fresh from diag(Hs) unless reused), the packed-lower Cholesky of Hs + D / radius, the step y
+// (delta = -y .* scale) and the model cost change mcc. Hs entries are recomputed from H.
+struct StepTry {
+    double y[6], D[6], mcc;
+    bool ok;
+};
+__device__ __forceinline__ StepTry lm_try_step(const LmCore& lm) {
+    StepTry r;
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+        r.D[j] = lm.reuse ? lm.D[j] : fmin(fmax(lm.scale[j] * lm.H[hup(j, j)] * lm.scale[j], 1e-6), 1e32);
+    double A[21];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) A[tri(i, j)] = lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const double ld = sqrt(r.D[j] / lm.radius);
+        A[tri(j, j)] += ld * ld;
+    }
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+#pragma unroll
+        for (int j = 0; j <= i; ++j) {
+            double s = A[tri(i, j)];
+#pragma unroll
+            for (int k = 0; k < j; ++k) s -= A[tri(i, k)] * A[tri(j, k)];
+            if (i == j) {
+                ok = ok && (s > 0.0);
+                A[tri(i, i)] = sqrt(s);
+            } else {
+                A[tri(i, j)] = s / A[tri(j, j)];
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double s = lm.scale[i] * lm.g[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) s -= A[tri(i, k)] * r.y[k];
+        r.y[i] = s / A[tri(i, i)];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        double s = r.y[i];
+#pragma unroll
+        for (int k = i + 1; k < 6; ++k) s -= A[tri(k, i)] * r.y[k];
+        r.y[i] = s / A[tri(i, i)];
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) ok = ok && isfinite(r.y[j]);
+    r.mcc = 0.0;
+    if (ok) {
+        double sg = 0.0, sHs = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            sg += -r.y[i] * (lm.scale[i] * lm.g[i]);
+            double hi = 0.0;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) hi += lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j] * -r.y[j];
+            sHs += -r.y[i] * hi;
+        }
+        r.mcc = -(sg + 0.5 * sHs);
+    }
+    r.ok = ok && (r.mcc > 0.0);
+    return r;
+}
+
+// TrustRegionMinimizer + LevenbergMarquardtStrategy: next candidate, or done (the retry loop of
+// invalid steps; its first attempt `first` has already been computed)
+__device__ __forceinline__ void lm_next_step(LmCore& lm, StepTry st, const double* cand_first) {
     const int kMaxIter = 4;
-    for (;;) {
+    for (bool first = true;; first = false) {
         lm.iteration++;
+        if (!first) st = lm_try_step(lm);
         if (!lm.reuse) {
 #pragma unroll
-            for (int j = 0; j < 6; ++j)
-                lm.D[j] = fmin(fmax(lm.scale[j] * lm.H[hup(j, j)] * lm.scale[j], 1e-6), 1e32);
+            for (int j = 0; j < 6; ++j) lm.D[j] = st.D[j];
         }
-        double A[21], y[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i)
-#pragma unroll
-            for (int j = 0; j <= i; ++j) A[tri(i, j)] = lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            const double ld = sqrt(lm.D[j] / lm.radius);
-            A[tri(j, j)] += ld * ld;
-        }
-        probe(49);
-        probe(50);
-        bool ok = true;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-#pragma unroll
-            for (int j = 0; j <= i; ++j) {
-                double s = A[tri(i, j)];
-#pragma unroll
-                for (int k = 0; k < j; ++k) s -= A[tri(i, k)] * A[tri(j, k)];
-                if (i == j) {
-                    ok = ok && (s > 0.0);
-                    A[tri(i, i)] = sqrt(s);
-                } else {
-                    A[tri(i, j)] = s / A[tri(j, j)];
-                }
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            double s = lm.scale[i] * lm.g[i];
-#pragma unroll
-            for (int k = 0; k < i; ++k) s -= A[tri(i, k)] * y[k];
-            y[i] = s / A[tri(i, i)];
-        }
-#pragma unroll
-        for (int i = 5; i >= 0; --i) {
-            double s = y[i];
-#pragma unroll
-            for (int k = i + 1; k < 6; ++k) s -= A[tri(k, i)] * y[k];
-            y[i] = s / A[tri(i, i)];
-        }
-#pragma unroll
-        for (int j = 0; j < 6; ++j) ok = ok && isfinite(y[j]);
-        probe(51);
         lm.reuse = 1;
-        double mcc = 0.0;
-        if (ok) {
-            double sg = 0.0, sHs = 0.0;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                sg += -y[i] * (lm.scale[i] * lm.g[i]);
-                double hi = 0.0;
-#pragma unroll
-                for (int j = 0; j < 6; ++j) hi += lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j] * -y[j];
-                sHs += -y[i] * hi;
-            }
-            mcc = -(sg + 0.5 * sHs);
-        }
-        if (!ok || !(mcc > 0.0)) {                       // invalid step (HandleInvalidStep)
+        if (!st.ok) {                                    // invalid step (HandleInvalidStep)
             if (++lm.invalid >= 5) { lm.done = 1; return; }
             lm.radius = lm.radius / lm.decrease;
             lm.decrease *= 2.0;
@@ -621,23 +621,30 @@ __device__ __forceinline__ void lm_next_step(LmCore& lm) {
             continue;
         }
         lm.invalid = 0;
-        double delta[6];
+        if (first) {
 #pragma unroll
-        for (int j = 0; j < 6; ++j) delta[j] = -y[j] * lm.scale[j];
-        probe(52);
-        se3_plus(lm.x, delta, lm.cand);
-        probe(53);
-        lm.mcc = mcc;
+            for (int k = 0; k < 7; ++k) lm.cand[k] = cand_first[k];
+        } else {
+            double delta[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) delta[j] = -st.y[j] * lm.scale[j];
+            se3_plus(lm.x, delta, lm.cand);
+        }
+        lm.mcc = st.mcc;
         lm.phase = 1;
         return;
     }
 }
 
-// Evaluation `tot` (cost, g, H, bad_r, bad_J) of lm.cand -> update the LM state (lane 0)
+// Evaluation `tot` (cost, g, H, bad_r, bad_J) of lm.cand -> update the LM state. Run by lanes 0 and
+// 1 of a wave on identical state: the gradient-norm check x (+) (-g) and the next candidate
+// x (+) delta are the same SE(3) update, so lane 0 evaluates the first and lane 1 the second at
+// once (the candidate is computed speculatively and discarded when the check ends the solve).
 __device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot) {
     const double cost_c = tot[0];
     const bool bad_r = tot[28] > 0.0, bad_j = tot[29] > 0.0;
     const int kMaxIter = 4;
+    bool step_ok = false;
     if (lm.phase == 0) {                                         // IterationZero
         if (bad_r || bad_j) {
             lm.done = 1;
@@ -653,60 +660,74 @@ __device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot) {
         lm.min_cost = lm.cost;
 #pragma unroll
         for (int k = 0; k < 7; ++k) lm.best[k] = lm.x[k];
-        if (grad_max_norm(lm.x, lm.g) <= 1e-10) lm.done = 1;
-        else lm_next_step(lm);
-        return;
-    }
-    const double cand_cost = bad_r ? DBL_MAX : cost_c;           // candidate evaluated
-    double sn = 0.0;
+        step_ok = true;                                          // gradient check below
+    } else {
+        const double cand_cost = bad_r ? DBL_MAX : cost_c;       // candidate evaluated
+        double sn = 0.0;
 #pragma unroll
-    for (int j = 0; j < 7; ++j) sn += (lm.x[j] - lm.cand[j]) * (lm.x[j] - lm.cand[j]);
-    sn = sqrt(sn);
-    if (sn <= 1e-8 * (lm.x_norm + 1e-8)) {
-        lm.done = 1;                                             // parameter tolerance
-        return;
-    }
-    if (fabs(lm.cost - cand_cost) <= 1e-6 * lm.cost) {
-        lm.done = 1;                                             // function tolerance
-        return;
-    }
-    const double rel = (lm.cost - cand_cost) / lm.mcc;
-    bool step_ok = false;
-    if (rel > 1e-3) {
-        double xn = 0;
-#pragma unroll
-        for (int j = 0; j < 7; ++j) { lm.x[j] = lm.cand[j]; xn += lm.x[j] * lm.x[j]; }
-        lm.x_norm = sqrt(xn);
-        if (bad_j) {
-            lm.done = 1;                                         // Jacobian evaluation failed
+        for (int j = 0; j < 7; ++j) sn += (lm.x[j] - lm.cand[j]) * (lm.x[j] - lm.cand[j]);
+        sn = sqrt(sn);
+        if (sn <= 1e-8 * (lm.x_norm + 1e-8)) {
+            lm.done = 1;                                         // parameter tolerance
             return;
         }
-        lm.cost = cand_cost;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) lm.g[k] = tot[1 + k];
-#pragma unroll
-        for (int k = 0; k < 21; ++k) lm.H[k] = tot[7 + k];
-        const double f = 1.0 - pow(2.0 * rel - 1.0, 3.0);
-        lm.radius = lm.radius / fmax(1.0 / 3.0, f);
-        lm.radius = fmin(1e16, lm.radius);
-        lm.decrease = 2.0;
-        lm.reuse = 0;
-        step_ok = true;
-        if (lm.cost < lm.min_cost) {
-            lm.min_cost = lm.cost;
-#pragma unroll
-            for (int k = 0; k < 7; ++k) lm.best[k] = lm.x[k];
+        if (fabs(lm.cost - cand_cost) <= 1e-6 * lm.cost) {
+            lm.done = 1;                                         // function tolerance
+            return;
         }
-    } else {
-        lm.radius = lm.radius / lm.decrease;
-        lm.decrease *= 2.0;
-        lm.reuse = 1;
+        const double rel = (lm.cost - cand_cost) / lm.mcc;
+        if (rel > 1e-3) {
+            double xn = 0;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) { lm.x[j] = lm.cand[j]; xn += lm.x[j] * lm.x[j]; }
+            lm.x_norm = sqrt(xn);
+            if (bad_j) {
+                lm.done = 1;                                     // Jacobian evaluation failed
+                return;
+            }
+            lm.cost = cand_cost;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) lm.g[k] = tot[1 + k];
+#pragma unroll
+            for (int k = 0; k < 21; ++k) lm.H[k] = tot[7 + k];
+            const double f = 1.0 - pow(2.0 * rel - 1.0, 3.0);
+            lm.radius = lm.radius / fmax(1.0 / 3.0, f);
+            lm.radius = fmin(1e16, lm.radius);
+            lm.decrease = 2.0;
+            lm.reuse = 0;
+            step_ok = true;
+            if (lm.cost < lm.min_cost) {
+                lm.min_cost = lm.cost;
+#pragma unroll
+                for (int k = 0; k < 7; ++k) lm.best[k] = lm.x[k];
+            }
+        } else {
+            lm.radius = lm.radius / lm.decrease;
+            lm.decrease *= 2.0;
+            lm.reuse = 1;
+        }
+        if (lm.iteration >= kMaxIter) {
+            lm.done = 1;
+            return;
+        }
     }
-    probe(48);
-    if (lm.iteration >= kMaxIter) lm.done = 1;
-    else if (step_ok && grad_max_norm(lm.x, lm.g) <= 1e-10) lm.done = 1;
-    else if (lm.radius <= 1e-32) lm.done = 1;
-    else lm_next_step(lm);
+    // the first attempt of the next step, and both SE(3) updates on two lanes
+    const StepTry st = lm_try_step(lm);
+    const bool lane1 = (threadIdx.x & 1) != 0;
+    double in[6], out[7];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) in[j] = lane1 ? -st.y[j] * lm.scale[j] : -lm.g[j];
+    se3_plus(lm.x, in, out);
+    double cand[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) cand[k] = __shfl(out[k], (threadIdx.x & ~1) | 1, 64);
+    double gm = 0.0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) gm = fmax(gm, fabs(lm.x[j] - out[j]));
+    gm = __shfl(gm, threadIdx.x & ~1, 64);                       // lane 0's gradient max-norm
+    if (step_ok && gm <= 1e-10) lm.done = 1;
+    else if (lm.phase != 0 && lm.radius <= 1e-32) lm.done = 1;
+    else lm_next_step(lm, st, cand);
 }
 
 struct LmArgs {
@@ -890,14 +911,12 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         }
         __syncthreads();
         if (rec) dbg[40 + ev] = __builtin_amdgcn_s_memrealtime();
-        if (t == 0) {
+        if (t < 2) {                                             // lanes 0 and 1, identical state
             LmCore c;
-            c.pp = (rec && ev == 2) ? dbg : nullptr;
-            if (c.pp) c.pp[47] = __builtin_amdgcn_s_memrealtime();
             core_load(c, lm);
             lm_accept(c, tot);
             if (ev == kLmEvals - 1) c.done = 1;
-            core_store(c, lm);
+            if (t == 0) core_store(c, lm);
         }
         __syncthreads();
         if (rec) dbg[4 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
