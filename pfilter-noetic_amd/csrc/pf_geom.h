@@ -81,6 +81,16 @@ PF_HD m3 q2m(const qd& q) {
     r.m[2][0] = txz - twy;         r.m[2][1] = tyz + twx;         r.m[2][2] = 1.0 - (txx + tyy);
     return r;
 }
+template <int I>
+PF_HD void m2q_branch(const m3& a, double* c) {
+    constexpr int J = (I + 1) % 3, K = (J + 1) % 3;
+    double t = sqrt(a.m[I][I] - a.m[J][J] - a.m[K][K] + 1.0);
+    c[I] = 0.5 * t;
+    t = 0.5 / t;
+    c[3] = (a.m[K][J] - a.m[J][K]) * t;
+    c[J] = (a.m[J][I] + a.m[I][J]) * t;
+    c[K] = (a.m[K][I] + a.m[I][K]) * t;
+}
 PF_HD qd m2q(const m3& a) {
     double c[4];
     double t = a.m[0][0] + a.m[1][1] + a.m[2][2];
@@ -95,13 +105,9 @@ PF_HD qd m2q(const m3& a) {
         int i = 0;
         if (a.m[1][1] > a.m[0][0]) i = 1;
         if (a.m[2][2] > a.m[i][i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(a.m[i][i] - a.m[j][j] - a.m[k][k] + 1.0);
-        c[i] = 0.5 * t;
-        t = 0.5 / t;
-        c[3] = (a.m[k][j] - a.m[j][k]) * t;
-        c[j] = (a.m[j][i] + a.m[i][j]) * t;
-        c[k] = (a.m[k][i] + a.m[i][k]) * t;
+        if (i == 0) m2q_branch<0>(a, c);             // static indices: no scratch arrays
+        else if (i == 1) m2q_branch<1>(a, c);
+        else m2q_branch<2>(a, c);
     }
     return qd{c[0], c[1], c[2], c[3]};
 }
@@ -192,15 +198,20 @@ PF_HD m3 polar_rotation(const m3& a) {
         if (W[i][i] < 0.0)
             for (int k = 0; k < 3; ++k) U[k][i] = -U[k][i];
     }
+#pragma unroll
     for (int i = 0; i < 3; ++i) {                        // descending order, first max wins
         int pos = i;
+        double best = sv[i];
+#pragma unroll
         for (int k = i + 1; k < 3; ++k)
-            if (sv[k] > sv[pos]) pos = k;
-        if (pos != i) {
-            const double ts = sv[i]; sv[i] = sv[pos]; sv[pos] = ts;
+            if (sv[k] > best) { best = sv[k]; pos = k; }
+#pragma unroll
+        for (int pk = i + 1; pk < 3; ++pk) {             // swap with column pos (static indices)
+            if (pk != pos) continue;
+            const double ts = sv[i]; sv[i] = sv[pk]; sv[pk] = ts;
             for (int k = 0; k < 3; ++k) {
-                double tu = U[k][i]; U[k][i] = U[k][pos]; U[k][pos] = tu;
-                double tv = V[k][i]; V[k][i] = V[k][pos]; V[k][pos] = tv;
+                double tu = U[k][i]; U[k][i] = U[k][pk]; U[k][pk] = tu;
+                double tv = V[k][i]; V[k][i] = V[k][pk]; V[k][pk] = tv;
             }
         }
     }
@@ -367,20 +378,16 @@ PF_HD void eig3(double a[3][3], double ev[3], double V[3][3]) {
     }
     double d[3] = {a[0][0], a[1][1], a[2][2]};
     int o[3] = {0, 1, 2};
-    // ascending, ties by index (3-element sorting network)
+    // ascending, ties by index (3-element sorting network on (value, index), columns moved along)
 #define PF_SWP(i, j)                                                                   \
-    if (d[o[j]] < d[o[i]] || (d[o[j]] == d[o[i]] && o[j] < o[i])) {                    \
-        int tt = o[i]; o[i] = o[j]; o[j] = tt;                                         \
+    if (d[j] < d[i] || (d[j] == d[i] && o[j] < o[i])) {                                \
+        const double td = d[i]; d[i] = d[j]; d[j] = td;                                \
+        const int tt = o[i]; o[i] = o[j]; o[j] = tt;                                   \
+        for (int r = 0; r < 3; ++r) { const double tv = V[r][i]; V[r][i] = V[r][j]; V[r][j] = tv; } \
     }
     PF_SWP(0, 1) PF_SWP(1, 2) PF_SWP(0, 1)
 #undef PF_SWP
-    double Vs[3][3];
-    for (int c = 0; c < 3; ++c) {
-        ev[c] = d[o[c]];
-        for (int r = 0; r < 3; ++r) Vs[r][c] = V[r][o[c]];
-    }
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) V[r][c] = Vs[r][c];
+    for (int c = 0; c < 3; ++c) ev[c] = d[c];
 }
 
 PF_HD void householder(const double* x, int n, double* ess, double& tau, double& beta) {
@@ -401,6 +408,8 @@ PF_HD void householder(const double* x, int n, double* ess, double& tau, double&
 
 // least-squares plane normal n with A n = -1, column-pivoting Householder QR (Eigen order)
 PF_HD d3 plane5(const double Ain[5][3]) {
+    // every loop has constant bounds and every pivot swap is written with static indices, so the
+    // arrays stay in registers (no scratch); the arithmetic and its order are Eigen's
     const int R = 5, C = 3;
     double A[5][3];
     for (int i = 0; i < R; ++i)
@@ -411,6 +420,7 @@ PF_HD d3 plane5(const double Ain[5][3]) {
     double cn[3], cu[3];
     const double eps = DBL_EPSILON;
     double maxnorm = 0.0;
+#pragma unroll
     for (int j = 0; j < C; ++j) {
         double s = 0;
         for (int i = 0; i < R; ++i) s += A[i][j] * A[i][j];
@@ -421,17 +431,21 @@ PF_HD d3 plane5(const double Ain[5][3]) {
     const double thr_helper = (maxnorm * eps) * (maxnorm * eps) / (double)R;
     const double downdate_thr = sqrt(eps);
     int nonzero = C;
+#pragma unroll
     for (int k = 0; k < C; ++k) {
         int best = k;
         double bn = cu[k];
+#pragma unroll
         for (int j = k + 1; j < C; ++j)
             if (cu[j] > bn) { bn = cu[j]; best = j; }
         if (nonzero == C && bn * bn < thr_helper * (double)(R - k)) nonzero = k;
-        if (best != k) {
-            for (int i = 0; i < R; ++i) { double t = A[i][k]; A[i][k] = A[i][best]; A[i][best] = t; }
-            int tp = perm[k]; perm[k] = perm[best]; perm[best] = tp;
-            double t1 = cn[k]; cn[k] = cn[best]; cn[best] = t1;
-            double t2 = cu[k]; cu[k] = cu[best]; cu[best] = t2;
+#pragma unroll
+        for (int jb = k + 1; jb < C; ++jb) {
+            if (jb != best) continue;
+            for (int i = 0; i < R; ++i) { double t = A[i][k]; A[i][k] = A[i][jb]; A[i][jb] = t; }
+            int tp = perm[k]; perm[k] = perm[jb]; perm[jb] = tp;
+            double t1 = cn[k]; cn[k] = cn[jb]; cn[jb] = t1;
+            double t2 = cu[k]; cu[k] = cu[jb]; cu[jb] = t2;
         }
         double x[5], ess[5];
         const int n = R - k;
@@ -442,6 +456,7 @@ PF_HD d3 plane5(const double Ain[5][3]) {
         for (int i = 1; i < n; ++i) A[k + i][k] = ess[i];
         hc[k] = tau;
         if (tau != 0.0 && n > 1) {
+#pragma unroll
             for (int j = k + 1; j < C; ++j) {
                 double tmp = 0.0;
                 for (int i = 1; i < n; ++i) tmp += ess[i] * A[k + i][j];
@@ -450,6 +465,7 @@ PF_HD d3 plane5(const double Ain[5][3]) {
                 for (int i = 1; i < n; ++i) A[k + i][j] -= tau * ess[i] * tmp;
             }
         }
+#pragma unroll
         for (int j = k + 1; j < C; ++j) {
             if (cu[j] != 0.0) {
                 double temp = fabs(A[k][j]) / cu[j];
@@ -468,22 +484,31 @@ PF_HD d3 plane5(const double Ain[5][3]) {
             }
         }
     }
-    double out[3] = {0, 0, 0};
     if (nonzero == 0) return d3{0, 0, 0};
-    for (int k = 0; k < nonzero; ++k) {
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
         const int n = R - k;
-        if (hc[k] == 0.0 || n < 2) continue;
+        if (k >= nonzero || hc[k] == 0.0 || n < 2) continue;
         double tmp = 0.0;
         for (int i = 1; i < n; ++i) tmp += A[k + i][k] * b[k + i];
         tmp += b[k];
         b[k] -= hc[k] * tmp;
         for (int i = 1; i < n; ++i) b[k + i] -= hc[k] * A[k + i][k] * tmp;
     }
-    for (int i = nonzero - 1; i >= 0; --i) {
+#pragma unroll
+    for (int i = C - 1; i >= 0; --i) {
+        if (i >= nonzero) continue;
         b[i] /= A[i][i];
         for (int s = 0; s < i; ++s) b[s] -= b[i] * A[s][i];
     }
-    for (int k = 0; k < nonzero; ++k) out[perm[k]] = b[k];
+    double out[3] = {0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+        if (k >= nonzero) continue;
+#pragma unroll
+        for (int j = 0; j < C; ++j)
+            if (perm[k] == j) out[j] = b[k];
+    }
     return d3{out[0], out[1], out[2]};
 }
 

@@ -146,7 +146,9 @@ __global__ void __launch_bounds__(256) k_vg_minmax(const float4* __restrict__ e,
 __global__ void __launch_bounds__(256) k_vg_keys(const float4* __restrict__ e, const float4* __restrict__ s,
                                                   const int* __restrict__ cnt, const u32* __restrict__ acc,
                                                   float leaf0, float leaf1, u32* __restrict__ keys,
-                                                  u32* __restrict__ vals) {
+                                                  u32* __restrict__ vals, SortHist sh) {
+    __shared__ u32 lh[4][256];
+    sort_hist_begin(lh);
     const int n0 = cnt[C_EIN], n1 = cnt[C_SIN];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
         const int c = i < n0 ? 0 : 1;
@@ -174,7 +176,9 @@ __global__ void __launch_bounds__(256) k_vg_keys(const float4* __restrict__ e, c
         }
         keys[i] = key | ((u32)c << 31);
         vals[i] = (u32)i;
+        sort_hist_add(lh, key | ((u32)c << 31), sh.passes);
     }
+    sort_hist_end(lh, sh, n0 + n1, n0 + n1);
 }
 
 // segment heads of a sorted key array; sentinel keys never start a segment
@@ -250,13 +254,100 @@ struct AssocArgs {
     u32* vals;
     u32 map_cap;
     u32* lm_arrive;
+    SortHist sh;           // histogram prologue of the p-index pair sort
 };
 
-// pointAssociateToMap + exact 5-NN, a team of kAssocTeam lanes per query (:297-300, :445-448)
+// line fit (:302-331) / plane fit (:449-476), round and sparsity, p-index pair keys of query q
+__device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, const int* id, int found,
+                                          u32 (*lh)[256]) {
+    bool valid = false;
+    const float4* mp = c == 0 ? a.map_e : a.map_s;
+    if (found == 5) {
+        double px[5], py[5], pz[5];
+        u32 rsum = 0;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const float4 m = mp[id[j]];
+            px[j] = m.x; py[j] = m.y; pz[j] = m.z;
+            rsum += w_r(m);
+        }
+        double* G = a.geo + 8 * (size_t)q;
+        if (c == 0) {                                            // :302-331
+            d3 center{0, 0, 0};
+            for (int j = 0; j < 5; ++j) center = add3(center, d3{px[j], py[j], pz[j]});
+            center = d3{center.x / 5.0, center.y / 5.0, center.z / 5.0};
+            double cov[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+            for (int j = 0; j < 5; ++j) {
+                const double tv[3] = {px[j] - center.x, py[j] - center.y, pz[j] - center.z};
+                for (int r = 0; r < 3; ++r)
+                    for (int cc = 0; cc < 3; ++cc) cov[r][cc] = cov[r][cc] + tv[r] * tv[cc];
+            }
+            double ev[3], V[3][3];
+            eig3(cov, ev, V);
+            if (ev[2] > 3 * ev[1]) {
+                valid = true;
+                const d3 dir{V[0][2], V[1][2], V[2][2]};
+                G[0] = 0.1 * dir.x + center.x; G[1] = 0.1 * dir.y + center.y; G[2] = 0.1 * dir.z + center.z;
+                G[3] = -0.1 * dir.x + center.x; G[4] = -0.1 * dir.y + center.y; G[5] = -0.1 * dir.z + center.z;
+            }
+        } else {                                                 // :449-476
+            double A[5][3];
+            for (int j = 0; j < 5; ++j) { A[j][0] = px[j]; A[j][1] = py[j]; A[j][2] = pz[j]; }
+            d3 n = plane5(A);
+            const double nd = 1 / nrm3(n);
+            const double z = n.x * n.x + n.y * n.y + n.z * n.z;
+            if (z > 0.0) {
+                const double sq = sqrt(z);
+                n = d3{n.x / sq, n.y / sq, n.z / sq};
+            }
+            valid = true;
+            for (int j = 0; j < 5; ++j)
+                if (fabs(n.x * px[j] + n.y * py[j] + n.z * pz[j] + nd) > 0.2) { valid = false; break; }
+            if (valid) {
+                G[0] = n.x; G[1] = n.y; G[2] = n.z;
+                G[3] = (double)(float)nd;                        // surfInfo::negative_OA_dot_norm is float (A.7)
+            }
+        }
+        if (valid) {
+            a.roundv[q] = (float)(rsum / 5.0);                   // :339-344 (r constant within a frame)
+            d3 cn{0, 0, 0};                                      // sparsity, :367-385
+            for (int j = 0; j < 5; ++j) cn = add3(cn, d3{px[j], py[j], pz[j]});
+            cn = d3{cn.x / 5, cn.y / 5, cn.z / 5};
+            float sum = 0;
+            for (int j = 0; j < 5; ++j) sum += nrm3(sub3(cn, d3{px[j], py[j], pz[j]}));
+            sum /= 5.0;
+            a.spars[q] = sum;
+        }
+    }
+    a.qflag[q] = valid ? 1 : 0;
+    const u32 off = c == 0 ? 0u : a.map_cap;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const u32 key = valid ? off + (u32)id[j] : kSentinel;
+        a.keys[5 * q + j] = key;
+        a.vals[5 * q + j] = (u32)(5 * q + j);
+        sort_hist_add(lh, key, a.sh.passes);
+    }
+}
+
+// pointAssociateToMap + exact 5-NN (a team of kAssocTeam lanes per query, :297-300, :445-448), then
+// the fit on the team's first lane; the pair keys' digit histograms for the p-index sort
 constexpr int kAssocTeam = 16;
-__global__ void __launch_bounds__(256) k_assoc_knn(AssocArgs a) {
+__global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
-    if (!a.st->gate) return;
+    const int gate = a.st->gate;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *a.lm_arrive = 0u;                                     // LM arrival counter of this iteration
+        a.cnt[C_NPAIR] = gate ? 5 * nq : 0;
+        a.cnt[C_EDGE_KEPT] = a.cnt[C_SURF_KEPT] = a.cnt[C_EDGE_VALID] = a.cnt[C_SURF_VALID] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 8) a.acc[A_W + threadIdx.x] = (threadIdx.x & 1) ? 0u : 0xFFFFFFFFu;
+    if (!gate) {                                   // solve skipped: no association is valid
+        for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) a.qflag[q] = 0;
+        return;                                    // (no pairs: every block leaves before the prologue)
+    }
+    __shared__ u32 lh[4][256];
+    sort_hist_begin(lh);
     double prm[7];
     for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
     const int tl = lane_id() & (kAssocTeam - 1);
@@ -272,103 +363,16 @@ __global__ void __launch_bounds__(256) k_assoc_knn(AssocArgs a) {
         float d[5];
         int id[5];
         const int found = knn5_team<kAssocTeam>(a.gv, c, pw.x, pw.y, pw.z, active, d, id);
-        if (active && tl < 5) {
+        if (active && tl < 5) {                                  // neighbours, read again by k_observe
             int iv = id[0];
 #pragma unroll
             for (int k = 1; k < 5; ++k)
                 if (tl == k) iv = id[k];
             a.nbr[5 * q0 + tl] = found == 5 ? iv : -1;
         }
+        if (active && tl == 0) assoc_fit(a, q0, c, id, found, lh);
     }
-}
-
-// line fit (:302-331) / plane fit (:449-476), round and sparsity, p-index pair keys
-__global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
-    const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
-    const int gate = a.st->gate;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        *a.lm_arrive = 0u;                                     // LM arrival counter of this iteration
-        a.cnt[C_NPAIR] = gate ? 5 * nq : 0;
-        a.cnt[C_EDGE_KEPT] = a.cnt[C_SURF_KEPT] = a.cnt[C_EDGE_VALID] = a.cnt[C_SURF_VALID] = 0;
-    }
-    if (blockIdx.x == 0 && threadIdx.x < 8) a.acc[A_W + threadIdx.x] = (threadIdx.x & 1) ? 0u : 0xFFFFFFFFu;
-    if (!gate) {                                   // solve skipped: no association is valid
-        for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) a.qflag[q] = 0;
-        return;
-    }
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
-        const int c = q < ne ? 0 : 1;
-        int id[5];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) id[j] = a.nbr[5 * q + j];
-        const int found = id[4] >= 0 ? 5 : 0;
-        bool valid = false;
-        const float4* mp = c == 0 ? a.map_e : a.map_s;
-        if (found == 5) {
-            double px[5], py[5], pz[5];
-            u32 rsum = 0;
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                const float4 m = mp[id[j]];
-                px[j] = m.x; py[j] = m.y; pz[j] = m.z;
-                rsum += w_r(m);
-            }
-            double* G = a.geo + 8 * (size_t)q;
-            if (c == 0) {                                            // :302-331
-                d3 center{0, 0, 0};
-                for (int j = 0; j < 5; ++j) center = add3(center, d3{px[j], py[j], pz[j]});
-                center = d3{center.x / 5.0, center.y / 5.0, center.z / 5.0};
-                double cov[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-                for (int j = 0; j < 5; ++j) {
-                    const double tv[3] = {px[j] - center.x, py[j] - center.y, pz[j] - center.z};
-                    for (int r = 0; r < 3; ++r)
-                        for (int cc = 0; cc < 3; ++cc) cov[r][cc] = cov[r][cc] + tv[r] * tv[cc];
-                }
-                double ev[3], V[3][3];
-                eig3(cov, ev, V);
-                if (ev[2] > 3 * ev[1]) {
-                    valid = true;
-                    const d3 dir{V[0][2], V[1][2], V[2][2]};
-                    G[0] = 0.1 * dir.x + center.x; G[1] = 0.1 * dir.y + center.y; G[2] = 0.1 * dir.z + center.z;
-                    G[3] = -0.1 * dir.x + center.x; G[4] = -0.1 * dir.y + center.y; G[5] = -0.1 * dir.z + center.z;
-                }
-            } else {                                                 // :449-476
-                double A[5][3];
-                for (int j = 0; j < 5; ++j) { A[j][0] = px[j]; A[j][1] = py[j]; A[j][2] = pz[j]; }
-                d3 n = plane5(A);
-                const double nd = 1 / nrm3(n);
-                const double z = n.x * n.x + n.y * n.y + n.z * n.z;
-                if (z > 0.0) {
-                    const double sq = sqrt(z);
-                    n = d3{n.x / sq, n.y / sq, n.z / sq};
-                }
-                valid = true;
-                for (int j = 0; j < 5; ++j)
-                    if (fabs(n.x * px[j] + n.y * py[j] + n.z * pz[j] + nd) > 0.2) { valid = false; break; }
-                if (valid) {
-                    G[0] = n.x; G[1] = n.y; G[2] = n.z;
-                    G[3] = (double)(float)nd;                        // surfInfo::negative_OA_dot_norm is float (A.7)
-                }
-            }
-            if (valid) {
-                a.roundv[q] = (float)(rsum / 5.0);                   // :339-344 (r constant within a frame)
-                d3 cn{0, 0, 0};                                      // sparsity, :367-385
-                for (int j = 0; j < 5; ++j) cn = add3(cn, d3{px[j], py[j], pz[j]});
-                cn = d3{cn.x / 5, cn.y / 5, cn.z / 5};
-                float sum = 0;
-                for (int j = 0; j < 5; ++j) sum += nrm3(sub3(cn, d3{px[j], py[j], pz[j]}));
-                sum /= 5.0;
-                a.spars[q] = sum;
-            }
-        }
-        a.qflag[q] = valid ? 1 : 0;
-        const u32 off = c == 0 ? 0u : a.map_cap;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            a.keys[5 * q + j] = valid ? off + (u32)id[j] : kSentinel;
-            a.vals[5 * q + j] = (u32)(5 * q + j);
-        }
-    }
+    sort_hist_end(lh, a.sh, 5 * nq, nq * kAssocTeam);   // blocks holding queries: ceil(nq * team / 256)
 }
 
 // c_i(n): earlier valid queries sharing neighbour n (pairs sorted stably by neighbour)
@@ -422,19 +426,24 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
         }
         float observe = gs / 5.0 + 1;                        // :332-338 / :480-486
         const float round = a.roundv[q];
-        ++nvalid[c];
+        if (c == 0) ++nvalid[0]; else ++nvalid[1];           // static indices (registers, not scratch)
         if (observe / round > 5) observe = 255;              // :348-349
         if (observe < round * a.theta_p && round > a.k_new && observe < a.theta_max) continue;   // :350-353
-        ++nkept[c];
+        if (c == 0) ++nkept[0]; else ++nkept[1];
         a.qflag[q] = f | 2;
         a.observe[q] = observe;
         const u32 rq = (u32)min(255, int(round)), gq = (u32)min(255, int(observe));   // :354-355
         if (c == 0) a.ds_e[q].w = __uint_as_float(pack_rg(rq, gq));
         else a.ds_s[q - ne].w = __uint_as_float(pack_rg(rq, gq));
         const float sp = a.spars[q];
-        mn[c][0] = fminf(mn[c][0], observe); mx[c][0] = fmaxf(mx[c][0], observe);
-        mn[c][1] = fminf(mn[c][1], sp); mx[c][1] = fmaxf(mx[c][1], sp);
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+            if (cc != c) continue;
+            mn[cc][0] = fminf(mn[cc][0], observe); mx[cc][0] = fmaxf(mx[cc][0], observe);
+            mn[cc][1] = fminf(mn[cc][1], sp); mx[cc][1] = fmaxf(mx[cc][1], sp);
+        }
     }
+#pragma unroll
     for (int c = 0; c < 2; ++c) {
         const int v = wave_sum_i(nvalid[c]), k = wave_sum_i(nkept[c]);
         if (lane_id() == 0) {
@@ -1044,14 +1053,20 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
                                                   const u32* __restrict__ acc, const float4* map_e,
                                                   const float4* app_e, const float4* map_s, const float4* app_s,
                                                   float leaf0, float leaf1, u32* __restrict__ keys,
-                                                  u32* __restrict__ vals) {
+                                                  u32* __restrict__ vals, SortHist sh) {
+    __shared__ u32 lh[4][256];
+    sort_hist_begin(lh);
     const RgView V = rg_view(cnt, map_e, app_e, map_s, app_s);
     const int n = V.total();
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         int c;
         const float4 p = V.at(i, c);
         vals[i] = (u32)i;
-        if (!in_crop(st, p)) { keys[i] = kSentinel; continue; }
+        if (!in_crop(st, p)) {
+            keys[i] = kSentinel;
+            sort_hist_add(lh, kSentinel, sh.passes);
+            continue;
+        }
         const float leaf = c == 0 ? leaf0 : leaf1;
         const u32* a = acc + A_RG + 6 * c;
         int minb[3], div[3];
@@ -1064,7 +1079,9 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
         const int i2 = (int)(floorf(p.z / leaf) - (float)minb[2]);
         const int idx = i0 * 1 + i1 * div[0] + i2 * (div[0] * div[1]);
         keys[i] = ((u32)idx & 0x7fffffffu) | ((u32)c << 31);
+        sort_hist_add(lh, keys[i], sh.passes);
     }
+    sort_hist_end(lh, sh, n, n);
 }
 
 struct RgReduceArgs {
@@ -1276,8 +1293,8 @@ void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s) {
     hipLaunchKernelGGL(k_vg_begin, dim3(1), dim3(64), 0, s, cnt, o.acc_a);
     hipLaunchKernelGGL(k_vg_minmax, dim3(128), dim3(256), 0, s, sb.in_edge, sb.in_surf, cnt, o.acc_a);
     hipLaunchKernelGGL(k_vg_keys, dim3(kGrid), dim3(256), 0, s, sb.in_edge, sb.in_surf, cnt, o.acc_a, o.leaf_vg[0],
-                       o.leaf_vg[1], o.vkeys, o.vvals);
-    radix_sort_pairs(o.vkeys, o.vvals, cnt + C_VGN, 32, o.vprim, s);
+                       o.leaf_vg[1], o.vkeys, o.vvals, sort_hist(o.vprim, 32, true));
+    radix_sort_pairs(o.vkeys, o.vvals, cnt + C_VGN, 32, o.vprim, s, nullptr, nullptr, true);
     segment_starts(o.vkeys, cnt + C_VGN, o.vsegstart, cnt + C_NSEG, cnt + C_NSEG_E, cnt + C_NRG_VALID, o.vprim, s);
     hipLaunchKernelGGL(k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, sb.in_edge, sb.in_surf, o.vkeys, o.vvals,
                        o.vsegstart, cnt, sb.ds_edge, sb.ds_surf);
@@ -1303,13 +1320,13 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
         AssocArgs aa{o.st, cnt, o.acc, gv, sb.ds_edge, sb.ds_surf, o.map_e, o.map_s, o.nbr, o.qflag, o.geo, o.spars,
-                     o.roundv, o.keys, o.vals, (u32)o.map_cap, o.lm_ticket};
-        hipLaunchKernelGGL(k_assoc_knn, dim3(kGrid), dim3(256), 0, s, aa);
+                     o.roundv, o.keys, o.vals, (u32)o.map_cap, o.lm_ticket,
+                     sort_hist(o.prim, o.pidx_bits, false)};
         hipLaunchKernelGGL(k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
         // pair keys are < 2 * map_cap (surf maps offset by map_cap) or the all-ones sentinel, so the
         // low pidx_bits bits order them
         u32 *pk, *pv;
-        radix_sort_pairs(o.keys, o.vals, cnt + C_NPAIR, o.pidx_bits, o.prim, s, &pk, &pv);
+        radix_sort_pairs(o.keys, o.vals, cnt + C_NPAIR, o.pidx_bits, o.prim, s, &pk, &pv, true);
         hipLaunchKernelGGL(k_pidx_count, dim3(kGrid), dim3(256), 0, s, pk, pv, cnt, o.pcnt, o.tailinc);
         ObsArgs oa{cnt, o.acc, o.map_e, o.map_s, sb.ds_edge, sb.ds_surf, o.nbr, o.qflag, o.pcnt, o.roundv, o.spars,
                    o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
@@ -1323,8 +1340,8 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
                        o.app_s, o.poses, (int)o.pose_cap, o.acc);
     hipLaunchKernelGGL(k_rg_minmax, dim3(128), dim3(256), 0, s, o.st, cnt, o.acc, o.map_e, o.app_e, o.map_s, o.app_s);
     hipLaunchKernelGGL(k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, o.map_e, o.app_e, o.map_s, o.app_s,
-                       o.leaf_rg[0], o.leaf_rg[1], o.keys, o.vals);
-    radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s);
+                       o.leaf_rg[0], o.leaf_rg[1], o.keys, o.vals, sort_hist(o.prim, 32, true));
+    radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
     segment_starts(o.keys, cnt + C_NRG, o.segstart, cnt + C_NSEG, cnt + C_NSEG_E, cnt + C_NRG_VALID, o.prim, s);
     RgReduceArgs ra{cnt, o.map_e, o.app_e, o.map_s, o.app_s, o.keys, o.vals, o.segstart, o.seg_out, o.flags,
                     o.prm.k_new, o.prm.theta_p, o.prm.theta_max};

@@ -25,9 +25,104 @@ void prim_free(PrimWork& w);
 
 // Stable sort of (keys, vals)[0 .. *d_n) by the low `bits` bits of keys (8-bit digits). With kout/vout
 // null the pass count is rounded up to even so the result is back in keys/vals; otherwise *kout/*vout
-// name the buffers holding the result (keys/vals or the PrimWork scratch).
+// name the buffers holding the result (keys/vals or the PrimWork scratch). hist_fused: the kernel
+// that produced the keys already ran the histogram prologue below (sort_hist_*), so the separate
+// histogram launch is skipped.
 void radix_sort_pairs(u32* keys, u32* vals, const int* d_n, int bits, PrimWork& w, hipStream_t s,
-                      u32** kout = nullptr, u32** vout = nullptr);
+                      u32** kout = nullptr, u32** vout = nullptr, bool hist_fused = false);
+inline int radix_passes(int bits, bool in_place) {
+    int p = (bits + 7) / 8;
+    if (p < 1) p = 1;
+    if (p > 4) p = 4;
+    if (in_place && (p & 1)) ++p;
+    return p;
+}
+
+// exclusive scan across a 256-thread block; returns this thread's exclusive prefix
+__device__ __forceinline__ u32 wave_incl_scan_u32(u32 v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        u32 t = __shfl_up(v, o, 64);
+        if (l >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ u32 block_excl_scan256(u32 v, u32* lds_w, u32& total) {
+    const int w = threadIdx.x >> 6, l = lane_id();
+    u32 inc = wave_incl_scan_u32(v);
+    if (l == 63) lds_w[w] = inc;
+    __syncthreads();
+    u32 off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        u32 t = lds_w[i];
+        if (i < w) off += t;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return off + inc - v;
+}
+
+// Histogram prologue fused into the kernel that writes a sort's keys (256-thread blocks; every block
+// of the grid must reach sort_hist_end): per-block digit counts of every pass in LDS, added to the
+// global counts; the last block to arrive forms the exclusive digit bases and resets the counts;
+// every block clears its share of the pass kernels' look-back words.
+struct SortHist {
+    u32* ghist;     // [4][256], zero between sorts
+    u32* dbase;     // [4][256]
+    u64* status;    // [passes][ntiles][256]
+    u32* arrive;
+    int passes;
+};
+inline SortHist sort_hist(PrimWork& w, int bits, bool in_place) {
+    return SortHist{w.bhist, w.dbase, w.status, w.tickets + 4, radix_passes(bits, in_place)};
+}
+__device__ __forceinline__ void sort_hist_begin(u32 (*lh)[256]) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) lh[p][threadIdx.x] = 0u;
+    __syncthreads();
+}
+__device__ __forceinline__ void sort_hist_add(u32 (*lh)[256], u32 key, int passes) {
+    for (int p = 0; p < passes; ++p) atomicAdd(&lh[p][(key >> (8 * p)) & 255u], 1u);
+}
+// items: the producer's grid-stride item count; blocks beyond ceil(items / 256) hold no keys and
+// leave at once (only the others count as arrivals)
+__device__ __forceinline__ int sort_hist_blocks(int items) {
+    const int b = (items + 255) / 256;
+    return b < (int)gridDim.x ? b : (int)gridDim.x;
+}
+__device__ __forceinline__ void sort_hist_end(u32 (*lh)[256], const SortHist& sh, int n, int items) {
+    __shared__ u32 lw[4];
+    __shared__ int last;
+    const int t = threadIdx.x;
+    const int G = sort_hist_blocks(items);
+    if ((int)blockIdx.x >= G) return;
+    const int ntiles = (n + kSortTile - 1) / kSortTile;
+    for (size_t i = (size_t)blockIdx.x * 256 + t; i < (size_t)sh.passes * ntiles * 256; i += (size_t)G * 256)
+        sh.status[i] = 0ull;
+    __syncthreads();
+    for (int p = 0; p < sh.passes; ++p)
+        if (lh[p][t]) __hip_atomic_fetch_add(&sh.ghist[p * 256 + t], lh[p][t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) last = __hip_atomic_fetch_add(sh.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (u32)G - 1;
+    __syncthreads();
+    if (!last) return;
+    u32 c[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+        c[p] = p < sh.passes ? __hip_atomic_load(&sh.ghist[p * 256 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+        if (p < sh.passes) __hip_atomic_store(&sh.ghist[p * 256 + t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int p = 0; p < sh.passes; ++p) {
+        u32 tot;
+        sh.dbase[p * 256 + t] = block_excl_scan256(c[p], lw, tot);
+    }
+    if (t == 0) __hip_atomic_store(sh.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Segments of stably sorted keys (bit 31 = cloud id, 0xFFFFFFFF = dropped entries, sorted last):
 // segstart[s] = first index of segment s; *d_nseg = number of segments; *d_nseg_c0 = segments of

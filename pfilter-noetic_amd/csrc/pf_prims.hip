@@ -14,41 +14,6 @@ __device__ __forceinline__ int eff_blocks(int n, int tile) {
     return nt < kSortMaxBlocks ? nt : kSortMaxBlocks;
 }
 
-__device__ __forceinline__ u32 wave_incl_scan(u32 v) {
-    const int l = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        u32 t = __shfl_up(v, o, 64);
-        if (l >= o) v += t;
-    }
-    return v;
-}
-
-// exclusive scan across a 256-thread block; returns this thread's exclusive prefix
-__device__ __forceinline__ u32 block_excl_scan256(u32 v, u32* lds_w, u32& total) {
-    const int w = threadIdx.x >> 6, l = lane_id();
-    u32 inc = wave_incl_scan(v);
-    if (l == 63) lds_w[w] = inc;
-    __syncthreads();
-    u32 off = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        u32 t = lds_w[i];
-        if (i < w) off += t;
-        tot += t;
-    }
-    __syncthreads();
-    total = tot;
-    return off + inc - v;
-}
-
-// ---- radix sort: one histogram kernel for every pass, then one kernel per 8-bit pass ----
-// Each pass kernel hands out 2048-key tiles in ticket order; a tile ranks its keys stably (wave
-// match + per-wave digit counts), publishes its per-digit counts, and finds its exclusive prefix by
-// decoupled look-back over the earlier tiles' status words. A status word carries its own payload
-// (tag << 32 | count; tag 1 = tile count, 2 = inclusive prefix), written and polled with agent-scope
-// atomics, so no separate fence is needed (cdna_hip_programming.md §6 G16, R2). Tickets make the
-// protocol independent of dispatch order: a tile only waits for tiles already taken by running blocks.
 constexpr int kOsThreads = 256;
 constexpr int kOsPer = kSortTile / kOsThreads;   // 8 keys per thread per tile
 constexpr unsigned kSpinLimit = 1u << 22;
@@ -391,12 +356,9 @@ void prim_free(PrimWork& w) {
 }
 
 void radix_sort_pairs(u32* keys, u32* vals, const int* d_n, int bits, PrimWork& w, hipStream_t s, u32** kout,
-                      u32** vout) {
-    int passes = (bits + 7) / 8;
-    if (passes < 1) passes = 1;
-    if (passes > 4) passes = 4;
-    if (!kout && (passes & 1)) ++passes;   // caller wants the result in place
-    hipLaunchKernelGGL(k_os_hist, dim3(kSortMaxBlocks), dim3(256), 0, s, keys, d_n, passes, w.bhist, w.dbase,
+                      u32** vout, bool hist_fused) {
+    const int passes = radix_passes(bits, !kout);   // without kout the result goes back in place
+    if (!hist_fused) hipLaunchKernelGGL(k_os_hist, dim3(kSortMaxBlocks), dim3(256), 0, s, keys, d_n, passes, w.bhist, w.dbase,
                        w.status, w.tickets);
     const unsigned grid = (unsigned)(w.max_tiles < (size_t)kSortMaxBlocks ? w.max_tiles : kSortMaxBlocks);
     u32 *ka = keys, *va = vals, *kb = w.keys_tmp, *vb = w.vals_tmp;
