@@ -60,7 +60,6 @@ struct OdomGPU {
     hipStream_t stream = nullptr;      // stage B: odometry
     hipStream_t stream_a = nullptr;    // stage A: featureExtraction + VoxelGrid
     size_t in_cap = 0, map_cap = 0, sort_cap = 0, pose_cap = 0;
-    int pidx_bits = 32;            // key bits the p-index pair sort needs
     int opt_count_host = 2;
     bool inited = false;
     int frames = 0;
@@ -97,8 +96,9 @@ struct OdomGPU {
     float* spars = nullptr;
     float* roundv = nullptr;
     float* observe = nullptr;
-    u32* pcnt = nullptr;           // [5 * 2 * in_cap]
-    u32* tailinc = nullptr;        // [sort_cap]
+    int* pnext = nullptr;          // [5 * 2 * in_cap] p-index lists: next pair sharing the map point
+    int* phead = nullptr;          // [2 * map_cap] p-index lists: a pair of the map point, -1 empty
+    u32* tailinc = nullptr;        // [5 * 2 * in_cap] increments of a map point, on its last pair
     double* lm_part = nullptr;     // [kLmBlocks * 32] per-block LM partials
     u32* lm_ticket = nullptr;      // LM arrival counter
     unsigned long long* dbg = nullptr;   // [64] device timestamps (development probe)

@@ -250,16 +250,14 @@ struct AssocArgs {
     double* geo;
     float* spars;
     float* roundv;
-    u32* keys;
-    u32* vals;
+    int* phead;            // p-index lists (one per map point, surf points offset by map_cap)
+    int* pnext;
     u32 map_cap;
     u32* lm_arrive;
-    SortHist sh;           // histogram prologue of the p-index pair sort
 };
 
 // line fit (:302-331) / plane fit (:449-476), round and sparsity, p-index pair keys of query q
-__device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, const int* id, int found,
-                                          u32 (*lh)[256]) {
+__device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, const int* id, int found) {
     bool valid = false;
     const float4* mp = c == 0 ? a.map_e : a.map_s;
     if (found == 5) {
@@ -320,18 +318,16 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
         }
     }
     a.qflag[q] = valid ? 1 : 0;
-    const u32 off = c == 0 ? 0u : a.map_cap;
+    if (valid) {               // p-index: push the 5 pairs onto their map points' lists (:345-346, :493-496)
+        const u32 off = c == 0 ? 0u : a.map_cap;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        const u32 key = valid ? off + (u32)id[j] : kSentinel;
-        a.keys[5 * q + j] = key;
-        a.vals[5 * q + j] = (u32)(5 * q + j);
-        sort_hist_add(lh, key, a.sh.passes);
+        for (int j = 0; j < 5; ++j)
+            a.pnext[5 * q + j] = atomicExch(&a.phead[off + (u32)id[j]], 5 * q + j);
     }
 }
 
 // pointAssociateToMap + exact 5-NN (a team of kAssocTeam lanes per query, :297-300, :445-448), then
-// the fit on the team's first lane; the pair keys' digit histograms for the p-index sort
+// the fit on the team's first lane, which pushes the query's pairs onto the p-index lists
 constexpr int kAssocTeam = 16;
 __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
@@ -346,8 +342,6 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
         for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) a.qflag[q] = 0;
         return;                                    // (no pairs: every block leaves before the prologue)
     }
-    __shared__ u32 lh[4][256];
-    sort_hist_begin(lh);
     double prm[7];
     for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
     const int tl = lane_id() & (kAssocTeam - 1);
@@ -370,24 +364,7 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
                 if (tl == k) iv = id[k];
             a.nbr[5 * q0 + tl] = found == 5 ? iv : -1;
         }
-        if (active && tl == 0) assoc_fit(a, q0, c, id, found, lh);
-    }
-    sort_hist_end(lh, a.sh, 5 * nq, nq * kAssocTeam);   // blocks holding queries: ceil(nq * team / 256)
-}
-
-// c_i(n): earlier valid queries sharing neighbour n (pairs sorted stably by neighbour)
-__global__ void __launch_bounds__(256) k_pidx_count(const u32* __restrict__ keys, const u32* __restrict__ vals,
-                                                     const int* __restrict__ cnt, u32* __restrict__ pcnt,
-                                                     u32* __restrict__ tailinc) {
-    const int n = cnt[C_NPAIR];
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
-        const u32 k = keys[p];
-        if (k == kSentinel) { tailinc[p] = 0; continue; }
-        int c = 0;
-        while (p - c - 1 >= 0 && keys[p - c - 1] == k) ++c;
-        pcnt[vals[p]] = (u32)c;
-        const bool tail = (p == n - 1) || keys[p + 1] != k;
-        tailinc[p] = tail ? (u32)(c + 1) : 0u;
+        if (active && tl == 0) assoc_fit(a, q0, c, id, found);
     }
 }
 
@@ -400,7 +377,10 @@ struct ObsArgs {
     float4* ds_s;
     const int* nbr;
     int* qflag;
-    const u32* pcnt;
+    const int* phead;
+    const int* pnext;
+    u32* tailinc;
+    u32 map_cap;
     const float* roundv;
     const float* spars;
     float* observe;
@@ -416,13 +396,41 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
     int nvalid[2] = {0, 0}, nkept[2] = {0, 0};
     for (int q = blockIdx.x * blockDim.x + t; q < nq; q += gridDim.x * blockDim.x) {
         int f = a.qflag[q];
-        if (!(f & 1)) continue;
+        if (!(f & 1)) {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) a.tailinc[5 * q + j] = 0u;
+            continue;
+        }
         const int c = q < ne ? 0 : 1;
         const float4* mp = c == 0 ? a.map_e : a.map_s;
-        int gs = 0;
+        // c_i(n) = valid queries before q sharing neighbour n: walk n's list (pushed in any order by
+        // k_assoc) counting smaller pair ids; the pair with the largest id carries n's increment
+        int nb[5], cur[5], rank[5], len[5];
+#pragma unroll
         for (int j = 0; j < 5; ++j) {
-            const u32 g0 = w_g(mp[a.nbr[5 * q + j]]);
-            gs += min(255u, g0 + a.pcnt[5 * q + j]);
+            nb[j] = a.nbr[5 * q + j];
+            cur[j] = a.phead[(c == 0 ? 0u : a.map_cap) + (u32)nb[j]];
+            rank[j] = len[j] = 0;
+        }
+        for (int step = 0;; ++step) {
+            bool more = false;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                if (cur[j] < 0) continue;
+                ++len[j];
+                rank[j] += cur[j] < 5 * q + j ? 1 : 0;
+                cur[j] = a.pnext[cur[j]];
+                more |= cur[j] >= 0;
+            }
+            if (!more) break;
+            if (step > 5 * nq) { a.cnt[C_ERR] = 1; break; }   // a list longer than every pair: corrupt
+        }
+        int gs = 0;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const u32 g0 = w_g(mp[nb[j]]);
+            gs += min(255u, g0 + (u32)rank[j]);
+            a.tailinc[5 * q + j] = rank[j] == len[j] - 1 ? (u32)len[j] : 0u;
         }
         float observe = gs / 5.0 + 1;                        // :332-338 / :480-486
         const float round = a.roundv[q];
@@ -461,18 +469,20 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
 }
 
 // the p-index increments of an outer iteration: g = min(255, g + 1) once per valid query sharing the
-// map point (:345-346, :493-496), applied by the tail pair of each neighbour run
-__device__ __forceinline__ void pidx_apply(const u32* keys, const u32* tailinc, int n, float4* map_e, float4* map_s,
-                                           u32 map_cap) {
+// map point (:345-346, :493-496), applied by the last pair of each map point's list, which also
+// empties the list for the next iteration
+__device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, int n, int ne, float4* map_e,
+                                           float4* map_s, int* phead, u32 map_cap) {
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const u32 inc = tailinc[p];
         if (!inc) continue;
-        const u32 k = keys[p];
-        float4* mp = k >= map_cap ? map_s : map_e;
-        const u32 idx = k >= map_cap ? k - map_cap : k;
+        const bool surf = p / 5 >= ne;
+        float4* mp = surf ? map_s : map_e;
+        const int idx = nbr[p];
         const float4 m = mp[idx];
         const u32 g = min(255u, w_g(m) + inc);
         mp[idx].w = __uint_as_float(pack_rg(w_r(m), g));
+        phead[(surf ? map_cap : 0u) + (u32)idx] = -1;
     }
 }
 
@@ -754,8 +764,9 @@ struct LmArgs {
     const float* spars;
     int weight_type;
     unsigned long long* dbg;
-    const u32* pair_keys;  // p-index increments, applied by the LM blocks before the solve
+    const int* nbr;        // p-index increments, applied by the LM blocks before the solve
     const u32* tailinc;
+    int* phead;
     float4* map_e;
     float4* map_s;
     u32 map_cap;
@@ -774,7 +785,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     __shared__ int aborted;
     const int t = threadIdx.x;
     // the map's p-index bytes are not read by the solve: apply this iteration's increments here
-    pidx_apply(a.pair_keys, a.tailinc, a.cnt[C_NPAIR], a.map_e, a.map_s, a.map_cap);
+    pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], a.cnt[C_EDS], a.map_e, a.map_s, a.phead, a.map_cap);
     const int nres = a.cnt[C_EDGE_KEPT] + a.cnt[C_SURF_KEPT];
     if (!a.st->gate || nres == 0) return;                        // no residual blocks: untouched
     double wmin[2][2], wmax[2][2];
@@ -1172,8 +1183,6 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     o.sort_cap = 2 * map_cap + 2 * in_cap;
     if (o.sort_cap < 10 * in_cap) o.sort_cap = 10 * in_cap;
     o.pose_cap = (size_t)1 << 20;
-    o.pidx_bits = 1;
-    while (((size_t)1 << o.pidx_bits) <= 2 * map_cap && o.pidx_bits < 32) ++o.pidx_bits;
     o.leaf_vg[0] = (float)prm.map_res;
     o.leaf_vg[1] = (float)(prm.map_res * 2);
     o.leaf_rg[0] = (float)prm.map_res;
@@ -1230,8 +1239,9 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.spars, sizeof(float) * nq);
     PF_ALLOC(o.roundv, sizeof(float) * nq);
     PF_ALLOC(o.observe, sizeof(float) * nq);
-    PF_ALLOC(o.pcnt, sizeof(u32) * 5 * nq);
-    PF_ALLOC(o.tailinc, sizeof(u32) * (o.sort_cap + 1));
+    PF_ALLOC(o.pnext, sizeof(int) * 5 * nq);
+    PF_ALLOC(o.phead, sizeof(int) * 2 * map_cap);
+    PF_ALLOC(o.tailinc, sizeof(u32) * 5 * nq);
     PF_ALLOC(o.poses, sizeof(double) * 7 * o.pose_cap);
     PF_ALLOC(o.stage, sizeof(float4) * 2 * in_cap);
 #undef PF_ALLOC
@@ -1252,6 +1262,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (hipMemset(o.acc_a, 0, sizeof(u32) * A_COUNT) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.lm, 0, sizeof(LMState)) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.lm_ticket, 0, sizeof(u32) * 4) != hipSuccess) return PF_EHIP;
+    if (hipMemset(o.phead, 0xFF, sizeof(int) * 2 * map_cap) != hipSuccess) return PF_EHIP;   // all lists empty
     o.opt_count_host = 2;
     return PF_OK;
 }
@@ -1271,7 +1282,7 @@ void odom_destroy(OdomGPU& o) {
     prim_free(o.vprim);
     void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.map_e,
                     o.map_s, o.app_e, o.app_s, o.seg_out, o.keys, o.vals, o.flags, o.scan_out, o.segstart, o.nbr,
-                    o.qflag, o.lm_part, o.lm_ticket, o.geo, o.spars, o.roundv, o.observe, o.pcnt, o.tailinc,
+                    o.qflag, o.lm_part, o.lm_ticket, o.geo, o.spars, o.roundv, o.observe, o.pnext, o.phead, o.tailinc,
                     o.poses, o.stage, o.dbg};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
@@ -1320,19 +1331,13 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
         AssocArgs aa{o.st, cnt, o.acc, gv, sb.ds_edge, sb.ds_surf, o.map_e, o.map_s, o.nbr, o.qflag, o.geo, o.spars,
-                     o.roundv, o.keys, o.vals, (u32)o.map_cap, o.lm_ticket,
-                     sort_hist(o.prim, o.pidx_bits, false)};
+                     o.roundv, o.phead, o.pnext, (u32)o.map_cap, o.lm_ticket};
         hipLaunchKernelGGL(k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
-        // pair keys are < 2 * map_cap (surf maps offset by map_cap) or the all-ones sentinel, so the
-        // low pidx_bits bits order them
-        u32 *pk, *pv;
-        radix_sort_pairs(o.keys, o.vals, cnt + C_NPAIR, o.pidx_bits, o.prim, s, &pk, &pv, true);
-        hipLaunchKernelGGL(k_pidx_count, dim3(kGrid), dim3(256), 0, s, pk, pv, cnt, o.pcnt, o.tailinc);
-        ObsArgs oa{cnt, o.acc, o.map_e, o.map_s, sb.ds_edge, sb.ds_surf, o.nbr, o.qflag, o.pcnt, o.roundv, o.spars,
-                   o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
+        ObsArgs oa{cnt, o.acc, o.map_e, o.map_s, sb.ds_edge, sb.ds_surf, o.nbr, o.qflag, o.phead, o.pnext, o.tailinc,
+                   (u32)o.map_cap, o.roundv, o.spars, o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
         hipLaunchKernelGGL(k_observe, dim3(kGrid), dim3(256), 0, s, oa);
         LmArgs la{o.st, cnt, o.acc, o.lm, o.lm_part, o.lm_ticket, o.qflag, sb.ds_edge, sb.ds_surf, o.geo, o.observe,
-                  o.spars, o.prm.weight_type, o.dbg, pk, o.tailinc, o.map_e, o.map_s, (u32)o.map_cap};
+                  o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.phead, o.map_e, o.map_s, (u32)o.map_cap};
         hipLaunchKernelGGL(k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
     }
     // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647)
