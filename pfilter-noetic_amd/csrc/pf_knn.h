@@ -89,17 +89,42 @@ __device__ __forceinline__ int knn5(const GridView& gv, int m, float qx, float q
     return found;
 }
 
-// The same search by a team of T lanes (T a power of two <= 64, aligned within the wave): lane l
-// of the team scans cells l, l + T, ... of the 27, keeping its own sorted 5 best, then the team
-// merges its lists in 5 rounds of a (d^2 bits, index) minimum. Keys are unique (distinct map
-// indices), so the merged 5 are exactly the sequential search's. Every lane of the wave must call
-// this (the merge shuffles); `active` is uniform within a team. Results are valid on every lane.
+// The same search by a team of T lanes (T a power of two <= 64, aligned within the wave). The 27
+// cells form 9 x-rows of 3 cells that are contiguous in the cell-sorted point array, so the team
+// reads 9 point ranges (18 cell_start words spread over the team's lanes); lane l takes points
+// l, l + T, ... of every range (consecutive lanes, consecutive points: coalesced), keeping its own
+// sorted 5 best, then the team merges its lists in 5 rounds of a (d^2 bits, index) minimum. Keys
+// are unique (distinct map indices), so the merged 5 are exactly the sequential search's. Every
+// lane of the wave must call this (the merge shuffles); `active` is uniform within a team. Results
+// are valid on every lane.
+#ifndef PF_KNN_GROUP
+#define PF_KNN_GROUP 1
+#endif
 __device__ __forceinline__ u64 knn_key(float d, int i) {
     return ((u64)__float_as_uint(d) << 32) | (u64)(u32)i;
+}
+__device__ __forceinline__ void knn_insert(float qx, float qy, float qz, const float4& p, float (&d)[5],
+                                           int (&id)[5]) {
+    float r = 0.0f;
+    float t = qx - p.x; r += t * t;
+    t = qy - p.y; r += t * t;
+    t = qz - p.z; r += t * t;
+    if (!(r < 1.0f)) return;
+    const int idx = __float_as_int(p.w);
+    if (!knn_lt(r, idx, d[4], id[4])) return;
+    d[4] = r; id[4] = idx;
+#pragma unroll
+    for (int q = 4; q > 0; --q) {
+        if (knn_lt(d[q], id[q], d[q - 1], id[q - 1])) {
+            float td = d[q]; d[q] = d[q - 1]; d[q - 1] = td;
+            int ti = id[q]; id[q] = id[q - 1]; id[q - 1] = ti;
+        }
+    }
 }
 template <int T>
 __device__ __forceinline__ int knn5_team(const GridView& gv, int m, float qx, float qy, float qz, bool active,
                                          float (&dout)[5], int (&iout)[5]) {
+    static_assert(T >= 8 && T <= 64 && (T & (T - 1)) == 0, "team: a power of two, >= 5 result lanes");
     float d[5];
     int id[5];
 #pragma unroll
@@ -108,27 +133,43 @@ __device__ __forceinline__ int knn5_team(const GridView& gv, int m, float qx, fl
     if (active && dm[7]) {
         const int cx = (int)floorf(qx), cy = (int)floorf(qy), cz = (int)floorf(qz);
         const int minx = dm[0], miny = dm[1], minz = dm[2], dx = dm[3], dy = dm[4], dz = dm[5], base = dm[6];
-        for (int j = lane_id() & (T - 1); j < 27; j += T) {
-            const int x = cx + (j % 3) - 1 - minx, y = cy + (j / 3) % 3 - 1 - miny, z = cz + j / 9 - 1 - minz;
-            if (x < 0 || y < 0 || z < 0 || x >= dx || y >= dy || z >= dz) continue;
-            const int cid = base + (z * dy + y) * dx + x;
-            const u32 b0 = gv.cell_start[cid], b1 = gv.cell_start[cid + 1];
-            for (u32 k = b0; k < b1; ++k) {
-                const float4 p = gv.cpts[k];
-                float r = 0.0f;
-                float t = qx - p.x; r += t * t;
-                t = qy - p.y; r += t * t;
-                t = qz - p.z; r += t * t;
-                if (!(r < 1.0f)) continue;
-                const int idx = __float_as_int(p.w);
-                if (!knn_lt(r, idx, d[4], id[4])) continue;
-                d[4] = r; id[4] = idx;
+        const int xlo = max(cx - 1 - minx, 0), xhi = min(cx + 1 - minx, dx - 1);
+        if (xlo <= xhi) {
+            const u32 tl = (u32)(lane_id() & (T - 1));
+            const int tbase = lane_id() & ~(T - 1);
+            // the 18 range words (row r: start of cell xlo, end of cell xhi) spread over the team's
+            // lanes, a few loads per lane, then gathered on every lane with shuffles
+            constexpr int K = (18 + T - 1) / T;
+            u32 wv[K];
 #pragma unroll
-                for (int q = 4; q > 0; --q) {
-                    if (knn_lt(d[q], id[q], d[q - 1], id[q - 1])) {
-                        float td = d[q]; d[q] = d[q - 1]; d[q - 1] = td;
-                        int ti = id[q]; id[q] = id[q - 1]; id[q - 1] = ti;
-                    }
+            for (int k = 0; k < K; ++k) {
+                const int w = (int)tl + T * k;
+                const int r = w >> 1;
+                const int y = cy + (r % 3) - 1 - miny, z = cz + r / 3 - 1 - minz;
+                const bool ok = w < 18 && y >= 0 && y < dy && z >= 0 && z < dz;
+                wv[k] = ok ? gv.cell_start[base + (z * dy + y) * dx + ((w & 1) ? xhi + 1 : xlo)] : 0u;
+            }
+            u32 b0[9], b1[9];
+#pragma unroll
+            for (int r = 0; r < 9; ++r) {
+                b0[r] = (u32)__shfl((int)wv[(2 * r) / T], tbase + (2 * r) % T, 64);
+                b1[r] = (u32)__shfl((int)wv[(2 * r + 1) / T], tbase + (2 * r + 1) % T, 64);
+            }
+            // rows in groups of G: the first point of each row of a group is loaded before any is
+            // used. G = 1 measured fastest (config 5: 71 us vs 99 us for G = 9): full occupancy
+            // (41 VGPRs, 8 waves / SIMD) hides more latency than loads in flight per wave
+            constexpr int G = PF_KNN_GROUP;
+#pragma unroll
+            for (int g = 0; g < 9; g += G) {
+                float4 pf[G];
+#pragma unroll
+                for (int r = 0; r < G; ++r)
+                    if (g + r < 9 && b0[g + r] + tl < b1[g + r]) pf[r] = gv.cpts[b0[g + r] + tl];
+#pragma unroll
+                for (int r = 0; r < G; ++r) {
+                    if (g + r >= 9 || b0[g + r] + tl >= b1[g + r]) continue;
+                    knn_insert(qx, qy, qz, pf[r], d, id);
+                    for (u32 k = b0[g + r] + tl + T; k < b1[g + r]; k += T) knn_insert(qx, qy, qz, gv.cpts[k], d, id);
                 }
             }
         }

@@ -141,17 +141,20 @@ __global__ void __launch_bounds__(256) k_grid_scatter(const float4* __restrict__
     }
 }
 
-// standalone query: queries in map 0, a team of kKnnTeam lanes per query
-constexpr int kKnnTeam = 16;
-__global__ void __launch_bounds__(256) k_knn_query(GridView gv, const float4* __restrict__ q, int nq,
+// standalone query: queries in map 0, a team of T lanes per query
+#ifndef PF_KNN_MINW
+#define PF_KNN_MINW 1
+#endif
+template <int T>
+__global__ void __launch_bounds__(256, PF_KNN_MINW) k_knn_query(GridView gv, const float4* __restrict__ q, int nq,
                                                     int* __restrict__ idx, float* __restrict__ d2) {
-    const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / kKnnTeam);
+    const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / T);
     const bool active = i < nq;
     const float4 p = active ? q[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     float d[5];
     int id[5];
-    knn5_team<kKnnTeam>(gv, 0, p.x, p.y, p.z, active, d, id);
-    const int tl = lane_id() & (kKnnTeam - 1);
+    knn5_team<T>(gv, 0, p.x, p.y, p.z, active, d, id);
+    const int tl = lane_id() & (T - 1);
     if (active && tl < 5) {
         float dv = d[0];
         int iv = id[0];
@@ -256,7 +259,20 @@ struct pf_knn {
     unsigned long long* d_pop = nullptr;
     size_t map_cap = 0, q_cap = 0;
     int nq = 0;
+    int team = 8;                  // lanes per query
 };
+
+namespace pf {
+namespace {
+void launch_knn(const pf_knn* h, const GridView& gv) {
+    const unsigned blocks = (unsigned)(((size_t)h->nq * h->team + 255) / 256);
+    if (h->team == 16)
+        hipLaunchKernelGGL(k_knn_query<16>, dim3(blocks), dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2);
+    else
+        hipLaunchKernelGGL(k_knn_query<8>, dim3(blocks), dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2);
+}
+}  // namespace
+}  // namespace pf
 
 extern "C" {
 
@@ -325,8 +341,7 @@ int pf_knn_query(pf_knn* h, const float* q4, size_t nq, int32_t* idx, float* d2)
     if (nq == 0) return PF_OK;
     PF_HIP_TRY(hipMemcpyAsync(h->d_q, q4, sizeof(float4) * nq, hipMemcpyHostToDevice, h->stream));
     GridView gv{h->grid.dims, h->grid.cell_start, h->grid.cpts};
-    hipLaunchKernelGGL(k_knn_query, dim3((unsigned)((nq * kKnnTeam + 255) / 256)), dim3(256), 0, h->stream, gv,
-                       h->d_q, (int)nq, h->d_idx, h->d_d2);
+    launch_knn(h, gv);
     if (idx) PF_HIP_TRY(hipMemcpyAsync(idx, h->d_idx, sizeof(int) * 5 * nq, hipMemcpyDeviceToHost, h->stream));
     if (d2) PF_HIP_TRY(hipMemcpyAsync(d2, h->d_d2, sizeof(float) * 5 * nq, hipMemcpyDeviceToHost, h->stream));
     PF_HIP_TRY(hipStreamSynchronize(h->stream));
@@ -338,19 +353,18 @@ int pf_knn_bench(pf_knn* h, int iters, double* avg_ms, double* alg_bytes) {
     if (!h || iters <= 0 || h->nq <= 0) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->device));
     GridView gv{h->grid.dims, h->grid.cell_start, h->grid.cpts};
-    const dim3 grid((unsigned)(((size_t)h->nq * kKnnTeam + 255) / 256));
     PF_HIP_TRY(hipMemsetAsync(h->d_pop, 0, sizeof(unsigned long long), h->stream));
     hipLaunchKernelGGL(k_knn_cellpop, dim3((unsigned)((h->nq + 255) / 256)), dim3(256), 0, h->stream, gv, h->d_q,
                        h->nq, h->d_pop);
     unsigned long long pop = 0;
     PF_HIP_TRY(hipMemcpyAsync(&pop, h->d_pop, sizeof(pop), hipMemcpyDeviceToHost, h->stream));
-    hipLaunchKernelGGL(k_knn_query, grid, dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2);  // warm
+    launch_knn(h, gv);  // warm
     hipEvent_t e0, e1;
     PF_HIP_TRY(hipEventCreate(&e0));
     PF_HIP_TRY(hipEventCreate(&e1));
     PF_HIP_TRY(hipEventRecord(e0, h->stream));
     for (int it = 0; it < iters; ++it)
-        hipLaunchKernelGGL(k_knn_query, grid, dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2);
+        launch_knn(h, gv);
     PF_HIP_TRY(hipEventRecord(e1, h->stream));
     PF_HIP_TRY(hipEventSynchronize(e1));
     float ms = 0;
@@ -360,6 +374,13 @@ int pf_knn_bench(pf_knn* h, int iters, double* avg_ms, double* alg_bytes) {
     PF_HIP_TRY(hipGetLastError());
     if (avg_ms) *avg_ms = ms / iters;
     if (alg_bytes) *alg_bytes = (double)h->nq * (16.0 + 40.0 + 27.0 * 8.0) + 16.0 * (double)pop;
+    return PF_OK;
+}
+
+// development: lanes per query of the standalone kernel (8 or 16; not part of the C ABI)
+int pf_knn_set_team(pf_knn* h, int team) {
+    if (!h || (team != 8 && team != 16)) return PF_EINVAL;
+    h->team = team;
     return PF_OK;
 }
 

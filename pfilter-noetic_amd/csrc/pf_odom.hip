@@ -328,7 +328,10 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
 
 // pointAssociateToMap + exact 5-NN (a team of kAssocTeam lanes per query, :297-300, :445-448), then
 // the fit on the team's first lane, which pushes the query's pairs onto the p-index lists
-constexpr int kAssocTeam = 16;
+#ifndef PF_ASSOC_TEAM
+#define PF_ASSOC_TEAM 16
+#endif
+constexpr int kAssocTeam = PF_ASSOC_TEAM;
 __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
     const int gate = a.st->gate;
@@ -659,7 +662,7 @@ __device__ __forceinline__ void lm_next_step(LmCore& lm, StepTry st, const doubl
 // 1 of a wave on identical state: the gradient-norm check x (+) (-g) and the next candidate
 // x (+) delta are the same SE(3) update, so lane 0 evaluates the first and lane 1 the second at
 // once (the candidate is computed speculatively and discarded when the check ends the solve).
-__device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot) {
+__device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot, unsigned long long* pr = nullptr) {
     const double cost_c = tot[0];
     const bool bad_r = tot[28] > 0.0, bad_j = tot[29] > 0.0;
     const int kMaxIter = 4;
@@ -709,7 +712,8 @@ __device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot) {
             for (int k = 0; k < 6; ++k) lm.g[k] = tot[1 + k];
 #pragma unroll
             for (int k = 0; k < 21; ++k) lm.H[k] = tot[7 + k];
-            const double f = 1.0 - pow(2.0 * rel - 1.0, 3.0);
+            const double r3 = 2.0 * rel - 1.0;
+            const double f = 1.0 - r3 * r3 * r3;                 // std::pow(2 rel - 1, 3)
             lm.radius = lm.radius / fmax(1.0 / 3.0, f);
             lm.radius = fmin(1e16, lm.radius);
             lm.decrease = 2.0;
@@ -731,7 +735,9 @@ __device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot) {
         }
     }
     // the first attempt of the next step, and both SE(3) updates on two lanes
+    if (pr) pr[0] = __builtin_amdgcn_s_memrealtime();
     const StepTry st = lm_try_step(lm);
+    if (pr) pr[1] = __builtin_amdgcn_s_memrealtime();
     const bool lane1 = (threadIdx.x & 1) != 0;
     double in[6], out[7];
 #pragma unroll
@@ -744,6 +750,7 @@ __device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot) {
 #pragma unroll
     for (int j = 0; j < 7; ++j) gm = fmax(gm, fabs(lm.x[j] - out[j]));
     gm = __shfl(gm, threadIdx.x & ~1, 64);                       // lane 0's gradient max-norm
+    if (pr) pr[2] = __builtin_amdgcn_s_memrealtime();
     if (step_ok && gm <= 1e-10) lm.done = 1;
     else if (lm.phase != 0 && lm.radius <= 1e-32) lm.done = 1;
     else lm_next_step(lm, st, cand);
@@ -784,10 +791,13 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     __shared__ LMState lm;
     __shared__ int aborted;
     const int t = threadIdx.x;
-    // the map's p-index bytes are not read by the solve: apply this iteration's increments here
-    pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], a.cnt[C_EDS], a.map_e, a.map_s, a.phead, a.map_cap);
+    // the map's p-index bytes are not read by the solve: this iteration's increments are applied
+    // while the blocks wait for the first evaluation's arrivals (or here, when there is no solve)
     const int nres = a.cnt[C_EDGE_KEPT] + a.cnt[C_SURF_KEPT];
-    if (!a.st->gate || nres == 0) return;                        // no residual blocks: untouched
+    if (!a.st->gate || nres == 0) {                              // no residual blocks: untouched
+        pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], a.cnt[C_EDS], a.map_e, a.map_s, a.phead, a.map_cap);
+        return;
+    }
     double wmin[2][2], wmax[2][2];
     for (int c = 0; c < 2; ++c)
         for (int ww = 0; ww < 2; ++ww) {
@@ -902,8 +912,12 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         if (rec) dbg[2 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
         if (t < 64) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (t == 0) __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (ev == 0)
+            pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], a.cnt[C_EDS], a.map_e, a.map_s, a.phead, a.map_cap);
+        {
             if (t == 0) {
-                __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const u32 target = (u32)(ev + 1) * gridDim.x;
                 unsigned spins = 0;
                 while (__hip_atomic_load(a.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -933,8 +947,11 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         if (rec) dbg[40 + ev] = __builtin_amdgcn_s_memrealtime();
         if (t < 2) {                                             // lanes 0 and 1, identical state
             LmCore c;
+            unsigned long long* pr = (rec && ev == 1) ? dbg + 21 : nullptr;
             core_load(c, lm);
-            lm_accept(c, tot);
+            if (pr) pr[4] = __builtin_amdgcn_s_memrealtime();
+            lm_accept(c, tot, pr);
+            if (pr) pr[3] = __builtin_amdgcn_s_memrealtime();
             if (ev == kLmEvals - 1) c.done = 1;
             if (t == 0) core_store(c, lm);
         }

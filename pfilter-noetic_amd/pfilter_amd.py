@@ -18,7 +18,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpfilter_hip.so")
+# PFILTER_HIP_LIB: development override (tools/ variant builds); the in-tree build otherwise
+LIB_PATH = os.environ.get("PFILTER_HIP_LIB") or os.path.join(_HERE, "libpfilter_hip.so")
 
 PF_OK = 0
 PF_W_MAP_TOO_SMALL = 1

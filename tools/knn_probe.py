@@ -18,17 +18,29 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--nmap", type=int, default=2_000_000)
     ap.add_argument("--nq", type=int, default=200_000)
+    ap.add_argument("--team", type=int, default=0, help="lanes per query (development hook; 0 = default)")
+    ap.add_argument("--order", default="stratified", choices=["stratified", "cell", "random"],
+                    help="query order: generator's, sorted by 1 m cell, or shuffled")
     a = ap.parse_args()
     import pfilter_amd as pa
     import pfsynth
     mp = pfsynth.dense_map(a.nmap, seed=5)
     q = pfsynth.dense_queries(mp, a.nq, sigma=0.3, seed=6)
+    import numpy as np
+    if a.order == "cell":
+        c = np.floor(q[:, :3]).astype(np.int64)
+        q = q[np.lexsort((c[:, 0], c[:, 1], c[:, 2]))].copy()
+    elif a.order == "random":
+        q = q[np.random.default_rng(1).permutation(q.shape[0])].copy()
     kn = pa.Knn(a.nmap, a.nq)
     kn.set_map(mp)
+    if a.team:
+        import ctypes
+        assert pa.lib().pf_knn_set_team(ctypes.c_void_p(kn._h), a.team) == 0
     kn.query(q)
     ms, alg = kn.bench(a.iters)
     print(json.dumps({"avg_kernel_ms": ms, "alg_bytes_per_launch": alg, "launches": a.iters + 2,
-                      "achieved_GBps": alg / (ms * 1e-3) / 1e9}))
+                      "achieved_GBps": alg / (ms * 1e-3) / 1e9, "team": a.team, "order": a.order}))
 
 
 if __name__ == "__main__":

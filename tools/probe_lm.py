@@ -35,3 +35,7 @@ for k in range(30):
                 (a[3] - t[40 + ev]) / 100))
             prev = a[3]
         print("frame", k, " | ".join(out), flush=True)
+        p = t[21:26]
+        print("   step ev1: load %.2f accept %.2f try_step %.2f se3+shfl %.2f next %.2f" % (
+            (p[4] - t[40 + 1]) / 100, (p[0] - p[4]) / 100, (p[1] - p[0]) / 100, (p[2] - p[1]) / 100,
+            (p[3] - p[2]) / 100))
