@@ -25,7 +25,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def short(name):
     n = name.replace("pf::(anonymous namespace)::", "").replace("(anonymous namespace)::", "")
-    return n.split("(")[0]
+    n = n.split("(")[0].split("<")[0]          # template kernels: k_knn_query<8> -> k_knn_query
+    return n.split(" ")[-1]                    # "void k_..." (template instantiations carry the type)
 
 
 def frame_breakdown(trace_csv, stats_csv):
