@@ -148,9 +148,10 @@ int pf_odom_destroy(pf_odom* h) {
     return PF_OK;
 }
 
-// Frame k uses pipeline slot k % 2. Stage A (featureExtraction / VoxelGrid or host staging) of slot p
-// first waits until stage B has finished frame k - 2 (the previous user of the slot); stage B of
-// frame k waits for stage A of frame k. Consecutive frames thus overlap A(k) with B(k - 1).
+// Frame k uses pipeline slot k % kSlots. Stage A (featureExtraction / VoxelGrid or host staging) of
+// slot p first waits until stage B has finished frame k - kSlots (the previous user of the slot);
+// stage B of frame k waits for stage A of frame k. Consecutive frames thus overlap A(k) with B(k - 1),
+// and stage A may run up to kSlots - 1 frames ahead.
 static int stage_a_begin(pf_odom* h, int p) {
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipStreamWaitEvent(o.stream_a, o.ev_b[p], 0));
@@ -216,7 +217,7 @@ int pf_odom_init_map(pf_odom* h, const float* edge, size_t ne, size_t edge_strid
     if (!h) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
-    const int p = o.frames & 1;
+    const int p = o.frames % kSlots;
     int rc = stage_a_begin(h, p);
     if (!rc) rc = stage_inputs(h, p, edge, ne, edge_stride, surf, ns, surf_stride);
     if (!rc) rc = stage_a_end_b_begin(h, p);
@@ -234,7 +235,7 @@ int pf_odom_update(pf_odom* h, const float* edge, size_t ne, size_t edge_stride,
     if (!h) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
-    const int p = o.frames & 1;
+    const int p = o.frames % kSlots;
     int rc = stage_a_begin(h, p);
     if (!rc) rc = stage_inputs(h, p, edge, ne, edge_stride, surf, ns, surf_stride);
     if (rc) return rc;
@@ -346,7 +347,7 @@ static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool s
 static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n) {
     OdomGPU& o = h->o;
     if (n > o.in_cap) return PF_ECAPACITY;
-    const int p = o.frames & 1;
+    const int p = o.frames % kSlots;
     const bool steady = o.inited && o.opt_count_host <= 2 && o.graph_enabled;
     int rc = stage_a_begin(h, p);
     if (rc) return rc;

@@ -53,6 +53,10 @@ struct StageBuf {
     int* cnt = nullptr;                              // [C_COUNT] stage counters
 };
 
+// pipeline slots: frame k's stage A output lives in slot k % kSlots, so stage A may run up to
+// kSlots - 1 frames ahead of stage B
+constexpr int kSlots = 3;
+
 struct OdomGPU {
     pf_lidar_params lidar{};
     pf_odom_params prm{};
@@ -77,14 +81,14 @@ struct OdomGPU {
     int* h_cnt = nullptr;          // pinned mirror
     double* h_pose = nullptr;      // pinned [7]
 
-    StageBuf sb[2];
+    StageBuf sb[kSlots];
     u32* acc_a = nullptr;                                   // stage A min/max accumulators
     u32 *vkeys = nullptr, *vvals = nullptr, *vflags = nullptr, *vscan = nullptr, *vsegstart = nullptr;
     PrimWork vprim;                                         // stage A sort / scan scratch
-    hipEvent_t ev_a[2] = {nullptr, nullptr};                // stage A done with slot p
-    hipEvent_t ev_b[2] = {nullptr, nullptr};                // stage B done with slot p
-    hipGraphExec_t graph_a[2] = {nullptr, nullptr};         // steady-state replay per slot
-    hipGraphExec_t graph_b[2] = {nullptr, nullptr};
+    hipEvent_t ev_a[kSlots] = {};                           // stage A done with slot p
+    hipEvent_t ev_b[kSlots] = {};                           // stage B done with slot p
+    hipGraphExec_t graph_a[kSlots] = {};                    // steady-state replay per slot
+    hipGraphExec_t graph_b[kSlots] = {};
     float4 *map_e = nullptr, *map_s = nullptr;
     float4 *app_e = nullptr, *app_s = nullptr;
     float4* seg_out = nullptr;

@@ -1225,7 +1225,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.lm, sizeof(LMState));
     PF_ALLOC(o.cnt, sizeof(int) * C_COUNT);
     PF_ALLOC(o.acc, sizeof(u32) * A_COUNT);
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < kSlots; ++p) {
         PF_ALLOC(o.sb[p].in_edge, sizeof(float4) * in_cap);
         PF_ALLOC(o.sb[p].in_surf, sizeof(float4) * in_cap);
         PF_ALLOC(o.sb[p].ds_edge, sizeof(float4) * in_cap);
@@ -1288,7 +1288,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
 }
 
 void odom_destroy(OdomGPU& o) {
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < kSlots; ++p) {
         if (o.graph_a[p]) (void)hipGraphExecDestroy(o.graph_a[p]);
         if (o.graph_b[p]) (void)hipGraphExecDestroy(o.graph_b[p]);
         if (o.ev_a[p]) (void)hipEventDestroy(o.ev_a[p]);
