@@ -101,7 +101,7 @@ struct OdomGPU {
     float* roundv = nullptr;
     float* observe = nullptr;
     int* pnext = nullptr;          // [5 * 2 * in_cap] p-index lists: next pair sharing the map point
-    int* phead = nullptr;          // [2 * map_cap] p-index lists: a pair of the map point, -1 empty
+    int4* pbkt = nullptr;          // [2 * map_cap] p-index buckets {count, pair, pair, overflow head}
     u32* tailinc = nullptr;        // [5 * 2 * in_cap] increments of a map point, on its last pair
     double* lm_part = nullptr;     // [kLmBlocks * 32] per-block LM partials
     u32* lm_ticket = nullptr;      // LM arrival counter

@@ -252,7 +252,7 @@ struct AssocArgs {
     double* geo;
     float* spars;
     float* roundv;
-    int* phead;            // p-index lists (one per map point, surf points offset by map_cap)
+    int4* pbkt;            // p-index buckets (one per map point, surf points offset by map_cap)
     int* pnext;
     u32 map_cap;
     u32* lm_arrive;
@@ -323,13 +323,19 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
     if (valid) {               // p-index: push the 5 pairs onto their map points' lists (:345-346, :493-496)
         const u32 off = c == 0 ? 0u : a.map_cap;
 #pragma unroll
-        for (int j = 0; j < 5; ++j)
-            a.pnext[5 * q + j] = atomicExch(&a.phead[off + (u32)id[j]], 5 * q + j);
+        for (int j = 0; j < 5; ++j) {
+            int4* b = a.pbkt + off + (u32)id[j];
+            const int p = 5 * q + j;
+            const int slot = atomicAdd(&b->x, 1);                  // {count, pair, pair, overflow head}
+            if (slot == 0) b->y = p;
+            else if (slot == 1) b->z = p;
+            else a.pnext[p] = atomicExch(&b->w, p);
+        }
     }
 }
 
 // pointAssociateToMap + exact 5-NN (a team of kAssocTeam lanes per query, :297-300, :445-448), then
-// the fit on the team's first lane, which pushes the query's pairs onto the p-index lists
+// the fit on the team's first lane, which pushes the query's pairs into the p-index buckets
 #ifndef PF_ASSOC_TEAM
 #define PF_ASSOC_TEAM 16
 #endif
@@ -382,7 +388,7 @@ struct ObsArgs {
     float4* ds_s;
     const int* nbr;
     int* qflag;
-    const int* phead;
+    const int4* pbkt;
     const int* pnext;
     u32* tailinc;
     u32 map_cap;
@@ -408,21 +414,27 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
         }
         const int c = q < ne ? 0 : 1;
         const float4* mp = c == 0 ? a.map_e : a.map_s;
-        // c_i(n) = valid queries before q sharing neighbour n: walk n's list (pushed in any order by
-        // k_assoc) counting smaller pair ids; the pair with the largest id carries n's increment
+        // c_i(n) = valid queries before q sharing neighbour n: count the smaller pair ids in n's bucket
+        // (filled in any order by k_assoc: two pairs inline, the rest on an overflow list); the pair
+        // with the largest id carries n's increment
         int nb[5], cur[5], rank[5], len[5];
 #pragma unroll
+        for (int j = 0; j < 5; ++j) nb[j] = a.nbr[5 * q + j];
+        int4 bk[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) bk[j] = a.pbkt[(c == 0 ? 0u : a.map_cap) + (u32)nb[j]];
+#pragma unroll
         for (int j = 0; j < 5; ++j) {
-            nb[j] = a.nbr[5 * q + j];
-            cur[j] = a.phead[(c == 0 ? 0u : a.map_cap) + (u32)nb[j]];
-            rank[j] = len[j] = 0;
+            const int p = 5 * q + j;
+            len[j] = bk[j].x;
+            rank[j] = (bk[j].x > 0 && bk[j].y < p ? 1 : 0) + (bk[j].x > 1 && bk[j].z < p ? 1 : 0);
+            cur[j] = bk[j].x > 2 ? bk[j].w : -1;
         }
         for (int step = 0;; ++step) {
             bool more = false;
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
                 if (cur[j] < 0) continue;
-                ++len[j];
                 rank[j] += cur[j] < 5 * q + j ? 1 : 0;
                 cur[j] = a.pnext[cur[j]];
                 more |= cur[j] >= 0;
@@ -456,19 +468,38 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
             mn[cc][1] = fminf(mn[cc][1], sp); mx[cc][1] = fmaxf(mx[cc][1], sp);
         }
     }
+    // workgroup totals, then one atomic per statistic and workgroup (not per wave)
+    __shared__ u32 wred[4][12];
+    const int w = t >> 6;
+    u32 v[12];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-        const int v = wave_sum_i(nvalid[c]), k = wave_sum_i(nkept[c]);
-        if (lane_id() == 0) {
-            if (v) atomicAdd(&a.cnt[c == 0 ? C_EDGE_VALID : C_SURF_VALID], v);
-            if (k) atomicAdd(&a.cnt[c == 0 ? C_EDGE_KEPT : C_SURF_KEPT], k);
+        v[c] = (u32)wave_sum_i(nvalid[c]);
+        v[2 + c] = (u32)wave_sum_i(nkept[c]);
+#pragma unroll
+        for (int ww = 0; ww < 2; ++ww) {
+            v[4 + 4 * c + 2 * ww] = f2ord(wave_minf(mn[c][ww]));
+            v[5 + 4 * c + 2 * ww] = f2ord(wave_maxf(mx[c][ww]));
         }
-        for (int w = 0; w < 2; ++w) {
-            const float lo = wave_minf(mn[c][w]), hi = wave_maxf(mx[c][w]);
-            if (lane_id() == 0 && lo != FLT_MAX) {
-                atomicMin(&a.acc[A_W + 4 * c + 2 * w], f2ord(lo));
-                atomicMax(&a.acc[A_W + 4 * c + 2 * w + 1], f2ord(hi));
-            }
+    }
+    if (lane_id() == 0)
+#pragma unroll
+        for (int k = 0; k < 12; ++k) wred[w][k] = v[k];
+    __syncthreads();
+    if (t < 12) {
+        u32 r = wred[0][t];
+        for (int ww = 1; ww < 4; ++ww) {
+            const u32 o = wred[ww][t];
+            if (t < 4) r += o;
+            else r = ((t - 4) & 1) ? max(r, o) : min(r, o);
+        }
+        if (t < 4) {
+            const int slot = t == 0 ? C_EDGE_VALID : t == 1 ? C_SURF_VALID : t == 2 ? C_EDGE_KEPT : C_SURF_KEPT;
+            if (r) atomicAdd(&a.cnt[slot], (int)r);
+        } else if (t & 1) {                                            // A_W + 4 c + 2 ww + 1: max
+            if (r != f2ord(-FLT_MAX)) atomicMax(&a.acc[A_W + t - 4], r);
+        } else if (r != f2ord(FLT_MAX)) {                              // A_W + 4 c + 2 ww: min
+            atomicMin(&a.acc[A_W + t - 4], r);
         }
     }
 }
@@ -477,7 +508,7 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
 // map point (:345-346, :493-496), applied by the last pair of each map point's list, which also
 // empties the list for the next iteration
 __device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, int n, int ne, float4* map_e,
-                                           float4* map_s, int* phead, u32 map_cap) {
+                                           float4* map_s, int4* pbkt, u32 map_cap) {
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const u32 inc = tailinc[p];
         if (!inc) continue;
@@ -487,7 +518,7 @@ __device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, i
         const float4 m = mp[idx];
         const u32 g = min(255u, w_g(m) + inc);
         mp[idx].w = __uint_as_float(pack_rg(w_r(m), g));
-        phead[(surf ? map_cap : 0u) + (u32)idx] = -1;
+        pbkt[(surf ? map_cap : 0u) + (u32)idx] = make_int4(0, -1, -1, -1);   // empty bucket
     }
 }
 
@@ -775,7 +806,7 @@ struct LmArgs {
     unsigned long long* dbg;
     const int* nbr;        // p-index increments, applied by the LM blocks before the solve
     const u32* tailinc;
-    int* phead;
+    int4* pbkt;
     float4* map_e;
     float4* map_s;
     u32 map_cap;
@@ -797,7 +828,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     // while the blocks wait for the first evaluation's arrivals (or here, when there is no solve)
     const int nres = a.cnt[C_EDGE_KEPT] + a.cnt[C_SURF_KEPT];
     if (!a.st->gate || nres == 0) {                              // no residual blocks: untouched
-        pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], a.cnt[C_EDS], a.map_e, a.map_s, a.phead, a.map_cap);
+        pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], a.cnt[C_EDS], a.map_e, a.map_s, a.pbkt, a.map_cap);
         return;
     }
     double wmin[2][2], wmax[2][2];
@@ -917,7 +948,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             if (t == 0) __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (ev == 0)
-            pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], a.cnt[C_EDS], a.map_e, a.map_s, a.phead, a.map_cap);
+            pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], a.cnt[C_EDS], a.map_e, a.map_s, a.pbkt, a.map_cap);
         {
             if (t == 0) {
                 const u32 target = (u32)(ev + 1) * gridDim.x;
@@ -1183,6 +1214,11 @@ __global__ void __launch_bounds__(256) k_init_map(const int* __restrict__ cnt, c
     }
 }
 
+__global__ void k_init_buckets(int4* __restrict__ b, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        b[i] = make_int4(0, -1, -1, -1);
+}
+
 __global__ void k_init_counts(int* __restrict__ cnt, DevState* __restrict__ st) {
     if (threadIdx.x != 0) return;
     cnt[C_ME] += cnt[C_EIN];
@@ -1260,7 +1296,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.roundv, sizeof(float) * nq);
     PF_ALLOC(o.observe, sizeof(float) * nq);
     PF_ALLOC(o.pnext, sizeof(int) * 5 * nq);
-    PF_ALLOC(o.phead, sizeof(int) * 2 * map_cap);
+    PF_ALLOC(o.pbkt, sizeof(int4) * 2 * map_cap);
     PF_ALLOC(o.tailinc, sizeof(u32) * 5 * nq);
     PF_ALLOC(o.poses, sizeof(double) * 7 * o.pose_cap);
     PF_ALLOC(o.stage, sizeof(float4) * 2 * in_cap);
@@ -1282,7 +1318,8 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (hipMemset(o.acc_a, 0, sizeof(u32) * A_COUNT) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.lm, 0, sizeof(LMState)) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.lm_ticket, 0, sizeof(u32) * 4) != hipSuccess) return PF_EHIP;
-    if (hipMemset(o.phead, 0xFF, sizeof(int) * 2 * map_cap) != hipSuccess) return PF_EHIP;   // all lists empty
+    hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, 2 * map_cap);   // all empty
+    if (hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
     o.opt_count_host = 2;
     return PF_OK;
 }
@@ -1302,7 +1339,7 @@ void odom_destroy(OdomGPU& o) {
     prim_free(o.vprim);
     void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.map_e,
                     o.map_s, o.app_e, o.app_s, o.seg_out, o.keys, o.vals, o.flags, o.scan_out, o.segstart, o.nbr,
-                    o.qflag, o.lm_part, o.lm_ticket, o.geo, o.spars, o.roundv, o.observe, o.pnext, o.phead, o.tailinc,
+                    o.qflag, o.lm_part, o.lm_ticket, o.geo, o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc,
                     o.poses, o.stage, o.dbg};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
@@ -1353,13 +1390,13 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
         AssocArgs aa{o.st, cnt, o.acc, gv, sb.ds_edge, sb.ds_surf, o.map_e, o.map_s, o.nbr, o.qflag, o.geo, o.spars,
-                     o.roundv, o.phead, o.pnext, (u32)o.map_cap, o.lm_ticket};
+                     o.roundv, o.pbkt, o.pnext, (u32)o.map_cap, o.lm_ticket};
         hipLaunchKernelGGL(k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
-        ObsArgs oa{cnt, o.acc, o.map_e, o.map_s, sb.ds_edge, sb.ds_surf, o.nbr, o.qflag, o.phead, o.pnext, o.tailinc,
+        ObsArgs oa{cnt, o.acc, o.map_e, o.map_s, sb.ds_edge, sb.ds_surf, o.nbr, o.qflag, o.pbkt, o.pnext, o.tailinc,
                    (u32)o.map_cap, o.roundv, o.spars, o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
         hipLaunchKernelGGL(k_observe, dim3(kGrid), dim3(256), 0, s, oa);
         LmArgs la{o.st, cnt, o.acc, o.lm, o.lm_part, o.lm_ticket, o.qflag, sb.ds_edge, sb.ds_surf, o.geo, o.observe,
-                  o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.phead, o.map_e, o.map_s, (u32)o.map_cap};
+                  o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.pbkt, o.map_e, o.map_s, (u32)o.map_cap};
         hipLaunchKernelGGL(k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
     }
     // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647)
