@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true", help="skip the kNN roofline leg")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--host-leg", type=int, default=0,
+                    help="also time N frames through pf_odom_frame_host (scan in host memory, PCIe copy "
+                         "inside the timed region); reported as pcie_inclusive, never as value")
     return ap.parse_args()
 
 
@@ -145,6 +148,27 @@ def knn_roofline(device=0, nmap=2_000_000, nq=200_000, iters=50):
             "kernel": "k_knn_query (exact radius-gated 5-NN, 1 m cell grid)",
             "workload": "config 5: map %d pts, %d queries, %d with 5 neighbours" % (nmap, nq, found),
             "alg_bytes_per_launch": alg, "avg_kernel_ms": round(ms, 5)}
+
+
+def host_leg(device, nframes, threads):
+    """PCIe-inclusive rate: the same sequence fed from host memory through pf_odom_frame_host (repack +
+    H2D of each scan inside the call), on a fresh handle."""
+    import pfilter_amd as pa
+    import pfsynth
+    seq = pfsynth.Sequence("S64", n_frames=nframes + 20, seed=0)
+    buf, counts = seq.frames(0, nframes + 20, threads=threads)
+    od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
+    od.init(lidar_cfg(), **ODOM_CFG)
+    for k in range(20):
+        od.frame_host(buf[k, :counts[k]], want_pose=False)
+    od.sync()
+    t0 = time.perf_counter()
+    for k in range(20, nframes + 20):
+        od.frame_host(buf[k, :counts[k]], want_pose=False)
+    od.sync()
+    el = time.perf_counter() - t0
+    return {"value": round(nframes / el, 2), "unit": "frames/s", "frames": nframes,
+            "note": "pf_odom_frame_host: scans in pageable host memory, repacked and copied H2D per frame"}
 
 
 def cpu_baseline(budget_s, warmup):
@@ -246,6 +270,8 @@ def main():
         except Exception as e:  # report, never hide
             log("roofline leg failed: %r" % (e,))
             out["roofline"] = None
+    if world == 1 and args.host_leg > 0:
+        out["pcie_inclusive"] = host_leg(local_rank, args.host_leg, threads)
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.warmup)
         out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
