@@ -61,6 +61,16 @@ __device__ __forceinline__ int wave_sum_i(int v) {
     return v;
 }
 
+// XCD-aware block order. The dispatcher deals workgroups to the 8 XCDs round-robin (block b runs on
+// XCD b % 8), and each XCD has its own L2. Renumbering so that XCD x owns one contiguous range of
+// logical blocks keeps neighbouring work (spatially adjacent queries) inside one L2. Bijective for
+// any grid size: XCD x owns q + (x < r) blocks, q = n / 8, r = n % 8.
+constexpr int kXcds = 8;
+__device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned n) {
+    const unsigned q = n / kXcds, r = n % kXcds, x = b % kXcds, l = b / kXcds;
+    return x * q + (x < r ? x : r) + l;
+}
+
 // map point packing: float4(x, y, z, bits(r | g << 8))
 __device__ __host__ __forceinline__ u32 pack_rg(u32 r, u32 g) { return (r & 255u) | ((g & 255u) << 8); }
 

@@ -38,161 +38,197 @@ struct GridView {
     const float4* cpts;
 };
 
-__device__ __forceinline__ bool knn_lt(float da, int ia, float db, int ib) {
-    return da < db || (da == db && ia < ib);
-}
-
-// 5 nearest neighbours with d2 < 1 of query q in map m. Returns the count found (0..5); d/id sorted.
-__device__ __forceinline__ int knn5(const GridView& gv, int m, float qx, float qy, float qz, float (&d)[5],
-                                    int (&id)[5]) {
-#pragma unroll
-    for (int k = 0; k < 5; ++k) { d[k] = 1.0f; id[k] = 0x7fffffff; }
-    const int* dm = gv.dims + 8 * m;
-    if (!dm[7]) return 0;
-    const int cx = (int)floorf(qx), cy = (int)floorf(qy), cz = (int)floorf(qz);
-    const int minx = dm[0], miny = dm[1], minz = dm[2], dx = dm[3], dy = dm[4], dz = dm[5], base = dm[6];
-    for (int oz = -1; oz <= 1; ++oz) {
-        const int z = cz + oz - minz;
-        if (z < 0 || z >= dz) continue;
-        for (int oy = -1; oy <= 1; ++oy) {
-            const int y = cy + oy - miny;
-            if (y < 0 || y >= dy) continue;
-            for (int ox = -1; ox <= 1; ++ox) {
-                const int x = cx + ox - minx;
-                if (x < 0 || x >= dx) continue;
-                const int cid = base + (z * dy + y) * dx + x;
-                const u32 b0 = gv.cell_start[cid], b1 = gv.cell_start[cid + 1];
-                for (u32 k = b0; k < b1; ++k) {
-                    const float4 p = gv.cpts[k];
-                    float r = 0.0f;
-                    float t = qx - p.x; r += t * t;
-                    t = qy - p.y; r += t * t;
-                    t = qz - p.z; r += t * t;
-                    if (!(r < 1.0f)) continue;
-                    const int idx = __float_as_int(p.w);
-                    if (!knn_lt(r, idx, d[4], id[4])) continue;
-                    d[4] = r; id[4] = idx;
-#pragma unroll
-                    for (int q = 4; q > 0; --q) {
-                        if (knn_lt(d[q], id[q], d[q - 1], id[q - 1])) {
-                            float td = d[q]; d[q] = d[q - 1]; d[q - 1] = td;
-                            int ti = id[q]; id[q] = id[q - 1]; id[q - 1] = ti;
-                        }
-                    }
-                }
-            }
-        }
-    }
-    int found = 0;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) found += (id[k] != 0x7fffffff) ? 1 : 0;
-    return found;
-}
-
-// The same search by a team of T lanes (T a power of two <= 64, aligned within the wave). The 27
-// cells form 9 x-rows of 3 cells that are contiguous in the cell-sorted point array, so the team
-// reads 9 point ranges (18 cell_start words spread over the team's lanes); lane l takes points
-// l, l + T, ... of every range (consecutive lanes, consecutive points: coalesced), keeping its own
-// sorted 5 best, then the team merges its lists in 5 rounds of a (d^2 bits, index) minimum. Keys
-// are unique (distinct map indices), so the merged 5 are exactly the sequential search's. Every
-// lane of the wave must call this (the merge shuffles); `active` is uniform within a team. Results
-// are valid on every lane.
-#ifndef PF_KNN_GROUP
-#define PF_KNN_GROUP 1
-#endif
 __device__ __forceinline__ u64 knn_key(float d, int i) {
     return ((u64)__float_as_uint(d) << 32) | (u64)(u32)i;
 }
-__device__ __forceinline__ void knn_insert(float qx, float qy, float qz, const float4& p, float (&d)[5],
-                                           int (&id)[5]) {
+// d^2 in the reference's order (x, then y, then z; no FMA under -ffp-contract=off)
+__device__ __forceinline__ float knn_d2(float qx, float qy, float qz, const float4& p) {
     float r = 0.0f;
     float t = qx - p.x; r += t * t;
     t = qy - p.y; r += t * t;
     t = qz - p.z; r += t * t;
-    if (!(r < 1.0f)) return;
-    const int idx = __float_as_int(p.w);
-    if (!knn_lt(r, idx, d[4], id[4])) return;
-    d[4] = r; id[4] = idx;
-#pragma unroll
-    for (int q = 4; q > 0; --q) {
-        if (knn_lt(d[q], id[q], d[q - 1], id[q - 1])) {
-            float td = d[q]; d[q] = d[q - 1]; d[q - 1] = td;
-            int ti = id[q]; id[q] = id[q - 1]; id[q - 1] = ti;
-        }
-    }
+    return r;
 }
+// Insert a candidate known to beat k[4] into a sorted 5-list of (d^2 bits, index) keys, branch-free:
+// four independent compares, then every slot takes its left neighbour, the key, or itself. Keys are
+// unique (distinct map indices).
+__device__ __forceinline__ void knn_push(u64 key, u64 (&k)[5]) {
+    bool c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[q] = key < k[q];
+#pragma unroll
+    for (int q = 4; q > 0; --q) k[q] = c[q - 1] ? k[q - 1] : (q < 4 && !c[q] ? k[q] : key);
+    k[0] = c[0] ? key : k[0];
+}
+__device__ __forceinline__ void knn_consider(float qx, float qy, float qz, const float4& p, u64 (&k)[5]) {
+    const float r2 = knn_d2(qx, qy, qz, p);
+    const u64 key = r2 < 1.0f ? knn_key(r2, __float_as_int(p.w)) : ~0ull;
+    if (key < k[4]) knn_push(key, k);
+}
+
+// Minimum of a u64 over an aligned team of T lanes, on every lane of the team. Teams of up to 16 use
+// DPP lane moves (quad xor 1, quad xor 2, mirror within 8, mirror within 16): each step pairs every
+// lane with one in the other half of its group, so after log2(T) steps all lanes hold the minimum.
+template <int DPP>
+__device__ __forceinline__ u64 dpp_u64(u64 v) {
+    const int lo = __builtin_amdgcn_mov_dpp((int)(u32)v, DPP, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(u32)(v >> 32), DPP, 0xf, 0xf, false);
+    return ((u64)(u32)hi << 32) | (u64)(u32)lo;
+}
+template <int T>
+__device__ __forceinline__ u64 team_min(u64 v) {
+    u64 o;
+    if (T >= 2) { o = dpp_u64<0xB1>(v); v = o < v ? o : v; }      // quad_perm [1,0,3,2]
+    if (T >= 4) { o = dpp_u64<0x4E>(v); v = o < v ? o : v; }      // quad_perm [2,3,0,1]
+    if (T >= 8) { o = dpp_u64<0x141>(v); v = o < v ? o : v; }     // row_half_mirror
+    if (T >= 16) { o = dpp_u64<0x140>(v); v = o < v ? o : v; }    // row_mirror
+#pragma unroll
+    for (int m = 16; m < T; m <<= 1) { o = __shfl_xor(v, m, 64); v = o < v ? o : v; }
+    return v;
+}
+
+// Exact 5-NN with d^2 < 1 by a team of T lanes (T a power of two <= 64, aligned within the wave).
+//
+// Candidate set. The 27 cells around the query's cell form 9 x-rows of 3 cells, each contiguous in
+// the cell-sorted point array. A row (oy, oz) or an end cell (ox = +-1) of a row is dropped when a
+// float lower bound of d^2 for every point in it is already >= 1. The bound is exact in float: for a
+// point in cell cy - 1, |fl(qy - py)| >= fl(qy - cy) and in cell cy + 1 >= fl((cy + 1) - qy) (float
+// rounding is monotone), and squares and the x -> y -> z sums are monotone too, so the reference's
+// own d^2 of every dropped point is >= 1 and the gate would reject it. That removes about a quarter
+// of the block (27 cells against the 20.6-cell expected volume of a unit ball swept over a cell).
+//
+// Work split. The kept rows' point ranges are concatenated into one index space [0, total); lane l
+// of the team takes indices l, l + T, ... (consecutive lanes, consecutive points: coalesced) and
+// issues U loads before using any, so a lane has U requests in flight instead of one per row. Each
+// lane keeps a sorted 5-list; the team then merges in 5 rounds of a key minimum. The merged 5 are
+// exactly the sequential search's. Every lane of the wave must call this (the merge shuffles);
+// `active` is uniform within a team. Results are valid on every lane.
+#ifndef PF_KNN_UNROLL
+#define PF_KNN_UNROLL 2
+#endif
+#ifndef PF_KNN_ROWS
+#define PF_KNN_ROWS 0
+#endif
 template <int T>
 __device__ __forceinline__ int knn5_team(const GridView& gv, int m, float qx, float qy, float qz, bool active,
                                          float (&dout)[5], int (&iout)[5]) {
-    static_assert(T >= 8 && T <= 64 && (T & (T - 1)) == 0, "team: a power of two, >= 5 result lanes");
-    float d[5];
-    int id[5];
+    static_assert(T >= 1 && T <= 64 && (T & (T - 1)) == 0, "team: a power of two within a wave");
+    constexpr int U = PF_KNN_UNROLL;
+    const u64 sentinel = knn_key(1.0f, 0x7fffffff);
+    u64 k[5];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) { d[k] = 1.0f; id[k] = 0x7fffffff; }
+    for (int q = 0; q < 5; ++q) k[q] = sentinel;
     const int* dm = gv.dims + 8 * m;
     if (active && dm[7]) {
-        const int cx = (int)floorf(qx), cy = (int)floorf(qy), cz = (int)floorf(qz);
+        const float fcx = floorf(qx), fcy = floorf(qy), fcz = floorf(qz);
+        const int cx = (int)fcx, cy = (int)fcy, cz = (int)fcz;
         const int minx = dm[0], miny = dm[1], minz = dm[2], dx = dm[3], dy = dm[4], dz = dm[5], base = dm[6];
-        const int xlo = max(cx - 1 - minx, 0), xhi = min(cx + 1 - minx, dx - 1);
-        if (xlo <= xhi) {
-            const u32 tl = (u32)(lane_id() & (T - 1));
-            const int tbase = lane_id() & ~(T - 1);
-            // the 18 range words (row r: start of cell xlo, end of cell xhi) spread over the team's
-            // lanes, a few loads per lane, then gathered on every lane with shuffles
-            constexpr int K = (18 + T - 1) / T;
-            u32 wv[K];
+        // per-axis lower bounds of |q - p| for the cells at offset -1 / +1
+        const float lx = qx - fcx, hx = (fcx + 1.0f) - qx;
+        const float ly = qy - fcy, hy = (fcy + 1.0f) - qy;
+        const float lz = qz - fcz, hz = (fcz + 1.0f) - qz;
+        const u32 tl = (u32)(lane_id() & (T - 1));
+        const int tbase = lane_id() & ~(T - 1);
+        (void)tbase;
+        // rows spread over the team's lanes: lane tl owns rows tl, tl + T, ... (row r: oy = r % 3 - 1,
+        // oz = r / 3 - 1) and loads that row's two range words
+        constexpr int K = (9 + T - 1) / T;
+        u32 rs[K], rl[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int w = (int)tl + T * k;
-                const int r = w >> 1;
-                const int y = cy + (r % 3) - 1 - miny, z = cz + r / 3 - 1 - minz;
-                const bool ok = w < 18 && y >= 0 && y < dy && z >= 0 && z < dz;
-                wv[k] = ok ? gv.cell_start[base + (z * dy + y) * dx + ((w & 1) ? xhi + 1 : xlo)] : 0u;
+        for (int j = 0; j < K; ++j) {
+            const int r = (int)tl + T * j;
+            const int oy = r % 3 - 1, oz = r / 3 - 1;
+            const float by = oy < 0 ? ly : (oy > 0 ? hy : 0.0f);
+            const float bz = oz < 0 ? lz : (oz > 0 ? hz : 0.0f);
+            const float brow = (0.0f + by * by) + bz * bz;       // bound with bx = 0
+            const float bl = (lx * lx + by * by) + bz * bz;        // cell cx - 1
+            const float bh = (hx * hx + by * by) + bz * bz;        // cell cx + 1
+            const int y = cy + oy - miny, z = cz + oz - minz;
+            const int x0 = max(cx - (bl < 1.0f ? 1 : 0) - minx, 0);
+            const int x1 = min(cx + (bh < 1.0f ? 1 : 0) - minx, dx - 1);
+            const bool ok = r < 9 && brow < 1.0f && y >= 0 && y < dy && z >= 0 && z < dz && x0 <= x1;
+            u32 s = 0, e = 0;
+            if (ok) {
+                const int c = base + (z * dy + y) * dx;
+                s = gv.cell_start[c + x0];
+                e = gv.cell_start[c + x1 + 1];
             }
-            u32 b0[9], b1[9];
+            rs[j] = s;
+            rl[j] = e - s;
+        }
+#if PF_KNN_ROWS
+        // every lane: the rows' starts and lengths. First the leading T points of every row, G rows'
+        // loads in flight at a time, then the tails of rows longer than T.
+        u32 b0[9], ln[9];
 #pragma unroll
-            for (int r = 0; r < 9; ++r) {
-                b0[r] = (u32)__shfl((int)wv[(2 * r) / T], tbase + (2 * r) % T, 64);
-                b1[r] = (u32)__shfl((int)wv[(2 * r + 1) / T], tbase + (2 * r + 1) % T, 64);
-            }
-            // rows in groups of G: the first point of each row of a group is loaded before any is
-            // used. G = 1 measured fastest (config 5: 71 us vs 99 us for G = 9): full occupancy
-            // (41 VGPRs, 8 waves / SIMD) hides more latency than loads in flight per wave
-            constexpr int G = PF_KNN_GROUP;
-#pragma unroll
-            for (int g = 0; g < 9; g += G) {
-                float4 pf[G];
-#pragma unroll
-                for (int r = 0; r < G; ++r)
-                    if (g + r < 9 && b0[g + r] + tl < b1[g + r]) pf[r] = gv.cpts[b0[g + r] + tl];
-#pragma unroll
-                for (int r = 0; r < G; ++r) {
-                    if (g + r >= 9 || b0[g + r] + tl >= b1[g + r]) continue;
-                    knn_insert(qx, qy, qz, pf[r], d, id);
-                    for (u32 k = b0[g + r] + tl + T; k < b1[g + r]; k += T) knn_insert(qx, qy, qz, gv.cpts[k], d, id);
-                }
+        for (int r = 0; r < 9; ++r) {
+            b0[r] = rs[r / T];
+            ln[r] = rl[r / T];
+            if (T > 1) {
+                b0[r] = (u32)__shfl((int)b0[r], tbase + r % T, 64);
+                ln[r] = (u32)__shfl((int)ln[r], tbase + r % T, 64);
             }
         }
+        constexpr int G = PF_KNN_ROWS;
+#pragma unroll
+        for (int g = 0; g < 9; g += G) {
+            float4 p[G];
+#pragma unroll
+            for (int r = 0; r < G; ++r)
+                if (g + r < 9 && tl < ln[g + r]) p[r] = gv.cpts[b0[g + r] + tl];
+#pragma unroll
+            for (int r = 0; r < G; ++r)
+                if (g + r < 9 && tl < ln[g + r]) knn_consider(qx, qy, qz, p[r], k);
+        }
+#pragma unroll
+        for (int r = 0; r < 9; ++r)
+            for (u32 j = tl + T; j < ln[r]; j += T) knn_consider(qx, qy, qz, gv.cpts[b0[r] + j], k);
+#else
+        // every lane: the rows' starts and the running prefix of their lengths; point v of the
+        // concatenation lives at v + off[r] for the last row r with pre[r] <= v
+        int off[9];
+        u32 pre[9];
+        u32 total = 0;
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+            u32 s = rs[r / T], l = rl[r / T];
+            if (T > 1) {
+                s = (u32)__shfl((int)s, tbase + r % T, 64);
+                l = (u32)__shfl((int)l, tbase + r % T, 64);
+            }
+            pre[r] = total;
+            off[r] = (int)(s - total);
+            total += l;
+        }
+        for (u32 v0 = tl; v0 < total; v0 += T * U) {
+            float4 p[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const u32 v = v0 + T * u;
+                int o = off[0];
+#pragma unroll
+                for (int r = 1; r < 9; ++r) o = v >= pre[r] ? off[r] : o;
+                if (v < total) p[u] = gv.cpts[(int)v + o];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (v0 + T * u >= total) break;
+                knn_consider(qx, qy, qz, p[u], k);
+            }
+        }
+#endif
     }
-    const u64 sentinel = knn_key(1.0f, 0x7fffffff);
-    u64 head = knn_key(d[0], id[0]);
     int found = 0;
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
-        u64 mn = head;
-#pragma unroll
-        for (int o = T / 2; o > 0; o >>= 1) {
-            const u64 other = __shfl_xor(mn, o, 64);
-            mn = other < mn ? other : mn;
-        }
+        const u64 mn = team_min<T>(k[0]);
         dout[r] = __uint_as_float((u32)(mn >> 32));
         iout[r] = (int)(u32)(mn & 0xffffffffull);
         if (mn != sentinel) ++found;
-        if (head == mn && mn != sentinel) {
+        if (k[0] == mn && mn != sentinel) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) { d[k] = d[k + 1]; id[k] = id[k + 1]; }
-            d[4] = 1.0f; id[4] = 0x7fffffff;
-            head = knn_key(d[0], id[0]);
+            for (int q = 0; q < 4; ++q) k[q] = k[q + 1];
+            k[4] = sentinel;
         }
     }
     return found;

@@ -148,22 +148,26 @@ __global__ void __launch_bounds__(256) k_grid_scatter(const float4* __restrict__
 template <int T>
 __global__ void __launch_bounds__(256, PF_KNN_MINW) k_knn_query(GridView gv, const float4* __restrict__ q, int nq,
                                                     int* __restrict__ idx, float* __restrict__ d2) {
-    const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / T);
+#ifdef PF_KNN_NO_XCD
+    const unsigned blk = blockIdx.x;
+#else
+    const unsigned blk = xcd_block(blockIdx.x, gridDim.x);
+#endif
+    const int i = (int)((blk * blockDim.x + threadIdx.x) / T);
     const bool active = i < nq;
     const float4 p = active ? q[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     float d[5];
     int id[5];
     knn5_team<T>(gv, 0, p.x, p.y, p.z, active, d, id);
     const int tl = lane_id() & (T - 1);
-    if (active && tl < 5) {
-        float dv = d[0];
-        int iv = id[0];
+    if (active) {
 #pragma unroll
-        for (int k = 1; k < 5; ++k)
-            if (tl == k) { dv = d[k]; iv = id[k]; }
-        const bool f = iv != 0x7fffffff;
-        idx[5 * i + tl] = f ? iv : -1;
-        d2[5 * i + tl] = f ? dv : __int_as_float(0x7f800000);
+        for (int k = 0; k < 5; ++k) {
+            if (k % T != tl) continue;                       // result k written by lane k % T
+            const bool f = id[k] != 0x7fffffff;
+            idx[5 * i + k] = f ? id[k] : -1;
+            d2[5 * i + k] = f ? d[k] : __int_as_float(0x7f800000);
+        }
     }
 }
 
@@ -266,10 +270,13 @@ namespace pf {
 namespace {
 void launch_knn(const pf_knn* h, const GridView& gv) {
     const unsigned blocks = (unsigned)(((size_t)h->nq * h->team + 255) / 256);
-    if (h->team == 16)
-        hipLaunchKernelGGL(k_knn_query<16>, dim3(blocks), dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2);
-    else
-        hipLaunchKernelGGL(k_knn_query<8>, dim3(blocks), dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2);
+    switch (h->team) {
+    case 1: hipLaunchKernelGGL(k_knn_query<1>, dim3(blocks), dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2); break;
+    case 2: hipLaunchKernelGGL(k_knn_query<2>, dim3(blocks), dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2); break;
+    case 4: hipLaunchKernelGGL(k_knn_query<4>, dim3(blocks), dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2); break;
+    case 16: hipLaunchKernelGGL(k_knn_query<16>, dim3(blocks), dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2); break;
+    default: hipLaunchKernelGGL(k_knn_query<8>, dim3(blocks), dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2); break;
+    }
 }
 }  // namespace
 }  // namespace pf
@@ -379,7 +386,7 @@ int pf_knn_bench(pf_knn* h, int iters, double* avg_ms, double* alg_bytes) {
 
 // development: lanes per query of the standalone kernel (8 or 16; not part of the C ABI)
 int pf_knn_set_team(pf_knn* h, int team) {
-    if (!h || (team != 8 && team != 16)) return PF_EINVAL;
+    if (!h || (team != 1 && team != 2 && team != 4 && team != 8 && team != 16)) return PF_EINVAL;
     h->team = team;
     return PF_OK;
 }

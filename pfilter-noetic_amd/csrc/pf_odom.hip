@@ -337,9 +337,10 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
 // pointAssociateToMap + exact 5-NN (a team of kAssocTeam lanes per query, :297-300, :445-448), then
 // the fit on the team's first lane, which pushes the query's pairs into the p-index buckets
 #ifndef PF_ASSOC_TEAM
-#define PF_ASSOC_TEAM 16
+#define PF_ASSOC_TEAM 8
 #endif
 constexpr int kAssocTeam = PF_ASSOC_TEAM;
+static_assert(kAssocTeam >= 5, "k_assoc writes the 5 neighbours from 5 lanes of the team");
 __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
     const int gate = a.st->gate;

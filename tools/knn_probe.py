@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--nmap", type=int, default=2_000_000)
     ap.add_argument("--nq", type=int, default=200_000)
-    ap.add_argument("--team", type=int, default=0, help="lanes per query (development hook; 0 = default)")
+    ap.add_argument("--team", type=int, default=0, help="lanes per query, 1..16 (development hook; 0 = default)")
     ap.add_argument("--order", default="stratified", choices=["stratified", "cell", "random"],
                     help="query order: generator's, sorted by 1 m cell, or shuffled")
     a = ap.parse_args()
