@@ -533,7 +533,10 @@ __device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, i
 // The step is a deterministic function of identical inputs, so every block holds the same LM state
 // and no state is broadcast. 32 blocks of 256 threads are far below one wave per CU, so all blocks
 // are co-resident; a poll that exceeds its bound sets C_ERR and leaves (no hang).
-constexpr int kLmBlocks = 32;
+#ifndef PF_LM_BLOCKS
+#define PF_LM_BLOCKS 32
+#endif
+constexpr int kLmBlocks = PF_LM_BLOCKS;
 constexpr int kLmEvals = 5;
 constexpr unsigned kLmSpinLimit = 1u << 21;
 
