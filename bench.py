@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true", help="skip the kNN roofline leg")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--bpf-frames", type=int, default=1000,
+                    help="frames of the Odom_BPF_EstimationClass leg (SURVEY §8(f) rank 1); 0 = skip")
     ap.add_argument("--host-leg", type=int, default=0,
                     help="also time N frames through pf_odom_frame_host (scan in host memory, PCIe copy "
                          "inside the timed region); reported as pcie_inclusive, never as value")
@@ -171,6 +173,77 @@ def host_leg(device, nframes, threads):
             "note": "pf_odom_frame_host: scans in pageable host memory, repacked and copied H2D per frame"}
 
 
+def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True):
+    """Odom_BPF_EstimationClass (src/odomEstimationClass.cpp:649-1306) frames/s on the same S64 sequence
+    with configs[1]'s parameters. Its inputs are beam / pillar / facade clouds: featureExtraction (on the
+    GPU, untimed) split by pfsynth.bpf_split, the stand-in for the reference's PCA classifier. All clouds
+    are HBM-resident before the timed region; the timed loop is pf_bpf_frame_device per frame."""
+    import pfilter_amd as pa
+    import pfsynth
+    total = warmup + nframes
+    seq = pfsynth.Sequence("S64", n_frames=total, seed=0)
+    fe = pa.LaserProcessingClass(device=device)
+    fe.init(lidar_cfg())
+    clouds = []
+    for f0 in range(0, total, 256):
+        nf = min(256, total - f0)
+        buf, counts = seq.frames(f0, nf, threads=threads)
+        for i in range(nf):
+            clouds.append(pfsynth.bpf_split(*fe.featureExtraction(buf[i, :counts[i]])))
+    bufs, ptrs = [], []
+    for c in range(3):                           # one HBM buffer per class, frames back to back
+        sizes = [cl[c].shape[0] for cl in clouds]
+        flat = np.concatenate([cl[c] for cl in clouds]).astype(np.float32)
+        db = pa.DeviceBuffer(max(flat.nbytes, 16), device=device)
+        db.upload(flat)
+        bufs.append(db)
+        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+        ptrs.append([(db.ptr + int(o) * 16, n) for o, n in zip(offs, sizes)])
+    od = pa.Odom_BPF_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
+    od.init(lidar_cfg(), **ODOM_CFG)
+
+    def run(k):
+        od.frame_device([ptrs[c][k][0] for c in range(3)], [ptrs[c][k][1] for c in range(3)])
+
+    for k in range(warmup):
+        run(k)
+    od.sync()
+    t0 = time.perf_counter()
+    for k in range(warmup, total):
+        run(k)
+    od.sync()
+    el = time.perf_counter() - t0
+    st = od.stats()
+    out = {"value": round(nframes / el, 2), "unit": "frames/s", "frames": nframes,
+           "ms_per_step": round(el / nframes * 1e3, 4),
+           "workload": "Odom_BPF_EstimationClass on S64 seed 0 (configs[1] parameters), beam/pillar/facade = "
+                       "featureExtraction split by pfsynth.bpf_split",
+           "last_frame": {"n_ds": st["n_ds"], "n_map": st["n_map"], "n_res": st["n_res"]}}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pfref
+        lid = pfref.make_lidar(64, 3.0, 90.0)
+        orc = pfref.OdomBPF(lid, 0.4, 0, 0.4, 75, 0, opts=0)
+        n, el, k = 0, 0.0, 0
+        while k < total and (el < cpu_seconds or k < warmup):
+            e, s_ = pfref.feature_extraction(seq.frame(k), lid)
+            cl = pfsynth.bpf_split(e, s_)
+            t = time.perf_counter()
+            if k == 0:
+                orc.init_map(*cl)
+            else:
+                orc.update(*cl)
+            if k >= warmup:
+                el += time.perf_counter() - t
+                n += 1
+            k += 1
+        out["cpu_baseline"] = {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": "pfref OdomBPF (reference-faithful opts=0), frames %d..%d, single thread, "
+                                         "%.1f s of CPU time (updatePointsToMap only)" % (warmup, k - 1, el)}
+        out["speedup_vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
+    return out
+
+
 def cpu_baseline(budget_s, warmup):
     """pfref oracle, single thread, reference-faithful options (kd-tree, dense-QR LM, std::sort)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -270,6 +343,12 @@ def main():
         except Exception as e:  # report, never hide
             log("roofline leg failed: %r" % (e,))
             out["roofline"] = None
+    if world == 1 and args.bpf_frames > 0:
+        try:
+            out["bpf"] = bpf_leg(local_rank, args.bpf_frames, threads, with_cpu=not args.no_cpu)
+        except Exception as e:  # report, never hide
+            log("bpf leg failed: %r" % (e,))
+            out["bpf"] = None
     if world == 1 and args.host_leg > 0:
         out["pcie_inclusive"] = host_leg(local_rank, args.host_leg, threads)
     if world == 1 and not args.no_cpu:

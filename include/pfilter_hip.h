@@ -15,6 +15,10 @@
  *   pf_odom_get_pose               public member `odom` as read by the node (copy.cpp:105-107)
  *   pf_odom_get_map                public members laserCloudCornerMap / laserCloudSurfMap (.h:151-152)
  *                                  and getMap (.h:147, .cpp:210-215)
+ *   pf_bpf_create                  Odom_BPF_EstimationClass::init (.h:175, .cpp:649-681)
+ *   pf_bpf_init_map                Odom_BPF_EstimationClass::initMapWithPoints (.h:177, .cpp:685-691)
+ *   pf_bpf_update                  Odom_BPF_EstimationClass::updatePointsToMap (.h:178, .cpp:702-749)
+ *   pf_odom_get_map (BPF handle)   laserCloudBeamMap / PillarMap / FacadeMap (.h:180-182), getMap (.cpp:683)
  */
 #ifndef PFILTER_HIP_H
 #define PFILTER_HIP_H
@@ -61,6 +65,9 @@ typedef struct {
     int32_t lm_iterations;               /* summed over outer iterations */
     int32_t map_too_small;
     int32_t status;
+    /* per map class (ES: 0 edge, 1 surf; BPF: 0 beam, 1 pillar, 2 facade); the n_edge_* / n_surf_*
+     * fields above repeat classes 0 and 1 */
+    int64_t n_in[3], n_ds[3], n_map[3], n_res[3], n_valid[3];
 } pf_odom_stats;
 
 /* ---------------- feature extraction (LaserProcessingClass) ---------------- */
@@ -88,11 +95,32 @@ int pf_odom_update(pf_odom* h, const float* edge, size_t ne, size_t edge_stride,
                    size_t ns, size_t surf_stride, double pose_out[7]);
 /* pose = {qx, qy, qz, qw, tx, ty, tz} of `odom` (q = Quaterniond(odom.rotation())) */
 int pf_odom_get_pose(pf_odom* h, double pose[7]);
-/* which: 0 = edge (corner) map, 1 = surf map. xyz 3 floats/pt, rg 2 bytes/pt (r=age, g=p-index).
+/* which: the map class. ES: 0 = edge (corner) map, 1 = surf map; BPF: 0 beam, 1 pillar, 2 facade.
+ * xyz 3 floats/pt, rg 2 bytes/pt (r=age, g=p-index).
  * Either output may be NULL; with cap too small *n is set and PF_ECAPACITY returned. */
 int pf_odom_get_map(pf_odom* h, int which, float* xyz, uint8_t* rg, size_t cap, size_t* n);
 int pf_odom_set_map(pf_odom* h, int which, const float* xyz, const uint8_t* rg, size_t n);
 int pf_odom_get_stats(pf_odom* h, pf_odom_stats* s);
+
+/* ---------------- odometry (Odom_BPF_EstimationClass) ----------------
+ * The estimator the fork's built node runs (src/odomEstimationNode.cpp:191-331): three local maps,
+ * beam and pillar (line residuals, leaf map_res) and facade (plane residuals, leaf 2 map_res), from
+ * the classified clouds of the feature classifier. Residual order beam -> pillar -> facade (.cpp:733-735).
+ * The handle type is pf_odom; pf_odom_get_pose / get_map / set_map / get_stats / poses / sync /
+ * set_graph / destroy apply, the ES-only entry points return PF_EINVAL on a BPF handle and back. */
+int pf_bpf_create(const pf_lidar_params* lidar, const pf_odom_params* params, int device,
+                  size_t max_points, size_t map_capacity, pf_odom** out);
+int pf_bpf_init_map(pf_odom* h, const float* beam, size_t nb, size_t beam_stride, const float* pillar,
+                    size_t np, size_t pillar_stride, const float* facade, size_t nf, size_t facade_stride);
+int pf_bpf_update(pf_odom* h, const float* beam, size_t nb, size_t beam_stride, const float* pillar,
+                  size_t np, size_t pillar_stride, const float* facade, size_t nf, size_t facade_stride,
+                  double pose_out[7]);
+/* HBM-resident clouds (packed float4 device pointers): the first call seeds the maps, later calls
+ * run updatePointsToMap; pose_out may be NULL (enqueue only), as pf_odom_frame_device */
+int pf_bpf_frame_device(pf_odom* h, const float* d_beam, size_t nb, const float* d_pillar, size_t np,
+                        const float* d_facade, size_t nf, double pose_out[7]);
+/* number of map classes of a handle: 2 (ES) or 3 (BPF) */
+int pf_odom_classes(pf_odom* h);
 
 /* ---------------- whole-frame device pipeline (featureExtraction -> odometry) ----------------
  * d_xyzi: device pointer to n packed float4 points (HBM-resident scan). The first frame seeds the

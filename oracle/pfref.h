@@ -8,6 +8,8 @@
  *   - LaserProcessingClass::featureExtraction(+FromSector)   src/laserProcessingClass.cpp:10-209
  *   - Odom_ES_EstimationClass init/initMapWithPoints/updatePointsToMap/addEdgeCostFactor/
  *     addSurfCostFactor/addPointsToMap                       src/odomEstimationClass.cpp:182-647
+ *   - Odom_BPF_EstimationClass init/initMapWithPoints/updatePointsToMap/addBeam|Pillar|Facade-
+ *     CostFactor/addPointsToMap (the same sequence over 3 maps)  src/odomEstimationClass.cpp:649-1306
  *   - OdomBaseClass rgbds/extractstablepoint/observeMean/pointAssociateToMap
  *                                                            src/odomEstimationClass.cpp:7-174
  *   - pointSparsityMean                                      include/odomEstimationClass.h:111-126
@@ -70,6 +72,9 @@ typedef struct {
     int32_t map_too_small;               /* 1 when the solve was skipped (odomEstimationClass.cpp:274-277) */
     int32_t status;
     double t_downsample, t_tree, t_assoc, t_solve, t_mapupdate;  /* seconds */
+    /* per map class (ES: 0 corner, 1 surf; BPF: 0 beam, 1 pillar, 2 facade); the n_edge_* /
+     * n_surf_* fields above repeat classes 0 and 1 */
+    int64_t n_in[3], n_ds[3], n_map[3], n_res[3], n_valid[3];
 } pfref_stats;
 
 /* --- feature extraction: LaserProcessingClass::featureExtraction --------------------- */
@@ -119,6 +124,16 @@ void pfref_odom_get_stats(const pfref_odom* h, pfref_stats* s);
 /* set odom / last_odom (poses {qx,qy,qz,qw,tx,ty,tz}) e.g. to replay a fixture from a given state */
 void pfref_odom_set_state(pfref_odom* h, const double odom_pose[7], const double last_pose[7]);
 void pfref_odom_set_opt_count(pfref_odom* h, int n);
+
+/* --- odometry: Odom_BPF_EstimationClass (src/odomEstimationClass.cpp:649-1306) ----------
+ * Three map classes in residual order: 0 beam (line, leaf r), 1 pillar (line, leaf r),
+ * 2 facade (plane, leaf 2r). The same handle type and accessors as the ES estimator; `which` of
+ * get/set_map is the class index. */
+pfref_odom* pfref_bpf_create(const pfref_lidar* lidar, const pfref_odom_params* params, int opts);
+int pfref_odom_classes(const pfref_odom* h);   /* 2 (ES) or 3 (BPF) */
+/* clouds[c]: 4 floats per point (x, y, z, intensity); n[c] points; one per class */
+int pfref_odom_init_map_n(pfref_odom* h, const float* const* clouds, const size_t* n);
+int pfref_odom_update_n(pfref_odom* h, const float* const* clouds, const size_t* n, double pose_out[7]);
 
 /* --- whole frame: featureExtraction then initMapWithPoints (first call) / updatePointsToMap */
 int pfref_odom_frame(pfref_odom* h, const pfref_lidar* lidar, const float* xyzi, size_t n,

@@ -44,10 +44,15 @@ class Stats(ctypes.Structure):
                                               "n_surf_map", "n_edge_res", "n_surf_res", "n_edge_valid",
                                               "n_surf_valid")] + \
                [(n, ctypes.c_int32) for n in ("outer_iterations", "lm_iterations", "map_too_small", "status")] + \
-               [(n, ctypes.c_double) for n in ("t_downsample", "t_tree", "t_assoc", "t_solve", "t_mapupdate")]
+               [(n, ctypes.c_double) for n in ("t_downsample", "t_tree", "t_assoc", "t_solve", "t_mapupdate")] + \
+               [(n, ctypes.c_int64 * 3) for n in ("n_in", "n_ds", "n_map", "n_res", "n_valid")]
 
     def as_dict(self):
-        return {f[0]: getattr(self, f[0]) for f in self._fields_}
+        d = {}
+        for f in self._fields_:
+            v = getattr(self, f[0])
+            d[f[0]] = list(v) if f[0] in ("n_in", "n_ds", "n_map", "n_res", "n_valid") else v
+        return d
 
 
 _lib = None
@@ -85,6 +90,11 @@ def lib():
         L.pfref_odom_frame.argtypes = [_vp, ctypes.POINTER(Lidar), _vp, _sz, _vp]
         L.pfref_odom_set_state.argtypes = [_vp, _vp, _vp]
         L.pfref_odom_set_opt_count.argtypes = [_vp, ctypes.c_int]
+        L.pfref_bpf_create.argtypes = [ctypes.POINTER(Lidar), ctypes.POINTER(OdomParams), ctypes.c_int]
+        L.pfref_bpf_create.restype = _vp
+        L.pfref_odom_classes.argtypes = [_vp]
+        L.pfref_odom_init_map_n.argtypes = [_vp, _vp, _vp]
+        L.pfref_odom_update_n.argtypes = [_vp, _vp, _vp, _vp]
     return _lib
 
 
@@ -201,13 +211,14 @@ def surf_eval(x, cur, n, d, w=0.0):
 
 class Odom:
     """Odom_ES_EstimationClass restated on the CPU."""
+    _create = "pfref_odom_create"
 
     def __init__(self, lidar=None, map_resolution=0.4, k_new=0, theta_p=0.4, theta_max=75, weight_type=0,
                  opts=0):
         self.lidar = lidar if lidar is not None else make_lidar()
         self.params = OdomParams(float(map_resolution), int(k_new), float(theta_p), int(theta_max),
                                  float(weight_type))
-        self._h = lib().pfref_odom_create(ctypes.byref(self.lidar), ctypes.byref(self.params), int(opts))
+        self._h = getattr(lib(), self._create)(ctypes.byref(self.lidar), ctypes.byref(self.params), int(opts))
         if not self._h:
             raise ValueError("invalid odometry parameters")
         self.inited = False
@@ -267,3 +278,30 @@ class Odom:
         s = Stats()
         lib().pfref_odom_get_stats(self._h, ctypes.byref(s))
         return s.as_dict()
+
+
+def _clouds(clouds):
+    arrs = [_f32(c) for c in clouds]
+    ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    ns = (ctypes.c_size_t * len(arrs))(*[a.shape[0] for a in arrs])
+    return arrs, ptrs, ns
+
+
+class OdomBPF(Odom):
+    """Odom_BPF_EstimationClass restated on the CPU (src/odomEstimationClass.cpp:649-1306): map
+    classes 0 beam, 1 pillar (lines, leaf r) and 2 facade (plane, leaf 2r)."""
+    _create = "pfref_bpf_create"
+
+    def init_map(self, beam, pillar, facade):
+        arrs, ptrs, ns = _clouds((beam, pillar, facade))
+        lib().pfref_odom_init_map_n(self._h, ptrs, ns)
+        self.inited = True
+
+    def update(self, beam, pillar, facade):
+        arrs, ptrs, ns = _clouds((beam, pillar, facade))
+        pose = np.empty(7)
+        lib().pfref_odom_update_n(self._h, ptrs, ns, pose.ctypes.data)
+        return pose
+
+    def frame(self, xyzi):
+        raise NotImplementedError("the BPF estimator takes classified beam / pillar / facade clouds")

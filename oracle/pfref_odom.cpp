@@ -544,7 +544,11 @@ struct Odom {
     pfref_lidar lidar;
     int opts;
     float map_resolution;
-    float leaf_edge_vg, leaf_surf_vg;   // downSizeFilter leaf sizes (double -> float)
+    // map classes: ES = {corner (line), surf (plane)}; BPF = {beam (line), pillar (line), facade (plane)}
+    int nc = 2;
+    bool plane[3] = {false, true, true};
+    float leaf_vg[3];                   // downSizeFilter leaf sizes (double -> float)
+    float leaf_rg[3];                   // rgbds leaves (float map_resolution, times 2 for planes)
     int k_new_edge, k_new_surf;
     float theta_p_edge, theta_p_surf;
     int theta_max_edge, theta_max_surf;
@@ -552,8 +556,8 @@ struct Odom {
     double params[7] = {0, 0, 0, 1, 0, 0, 0};
     Iso odom, last_odom;
     int optimization_count;
-    std::vector<PtC> corner_map, surf_map;
-    KdTree tree_edge, tree_surf;
+    std::vector<PtC> maps[3];           // laserCloudCornerMap / SurfMap, or Beam / Pillar / FacadeMap
+    KdTree trees[3];
     pfref_stats stats{};
 
     Quat q() const { return {params[0], params[1], params[2], params[3]}; }
@@ -568,11 +572,14 @@ struct Odom {
         return po;
     }
 
-    void knn(bool edge, const PtC& p, int* ind, float* d2) const {
+    void knn(int c, const PtC& p, int* ind, float* d2) const {
         const float qq[3] = {p.x, p.y, p.z};
-        if (opts & PFREF_KNN_BRUTE) knn_brute(edge ? corner_map : surf_map, qq, 5, ind, d2);
-        else (edge ? tree_edge : tree_surf).knn(qq, 5, ind, d2);
+        if (opts & PFREF_KNN_BRUTE) knn_brute(maps[c], qq, 5, ind, d2);
+        else trees[c].knn(qq, 5, ind, d2);
     }
+    int k_new(int c) const { return plane[c] ? k_new_surf : k_new_edge; }
+    float theta_p(int c) const { return plane[c] ? theta_p_surf : theta_p_edge; }
+    int theta_max(int c) const { return plane[c] ? theta_max_surf : theta_max_edge; }
 };
 
 namespace {
@@ -633,21 +640,23 @@ double sparsity(const std::vector<PtC>& map, const int* ind) {
 }
 }  // namespace
 
-// addEdgeCostFactor (:284-432)
-static void add_edge_factors(Odom& o, std::vector<PtC>& cloud, std::vector<Residual>& out) {
+// addEdgeCostFactor (:284-432); Odom_BPF addBeamCostFactor / addPillarCostFactor (:751-1010) are
+// the same function of their own map with the edge thresholds
+static void add_line_factors(Odom& o, int c, std::vector<PtC>& cloud, std::vector<Residual>& out) {
     struct Info { V3 cur, a, b; float observe, round; };
     std::vector<Info> valid;
     std::vector<double> spars, obs;
+    std::vector<PtC>& map = o.maps[c];
     int64_t n_valid = 0;
     for (size_t i = 0; i < cloud.size(); i++) {
         PtC pt = o.associate(cloud[i]);
         int ind[5]; float d2[5];
-        o.knn(true, pt, ind, d2);
+        o.knn(c, pt, ind, d2);
         if (!(d2[4] < 1.0)) continue;
         V3 near[5];
         V3 center{0, 0, 0};
         for (int j = 0; j < 5; j++) {
-            near[j] = V3{(double)o.corner_map[ind[j]].x, (double)o.corner_map[ind[j]].y, (double)o.corner_map[ind[j]].z};
+            near[j] = V3{(double)map[ind[j]].x, (double)map[ind[j]].y, (double)map[ind[j]].z};
             center = add(center, near[j]);
         }
         center = V3{center.x / 5.0, center.y / 5.0, center.z / 5.0};
@@ -667,11 +676,11 @@ static void add_edge_factors(Odom& o, std::vector<PtC>& cloud, std::vector<Resid
             V3 a{0.1 * dir.x + center.x, 0.1 * dir.y + center.y, 0.1 * dir.z + center.z};
             V3 b{-0.1 * dir.x + center.x, -0.1 * dir.y + center.y, -0.1 * dir.z + center.z};
             float observe, round;
-            if (!pindex(o.corner_map, ind, o.k_new_edge, o.theta_p_edge, o.theta_max_edge, observe, round)) continue;
+            if (!pindex(map, ind, o.k_new(c), o.theta_p(c), o.theta_max(c), observe, round)) continue;
             cloud[i].r = (uint8_t)std::min(255, int(round));
             cloud[i].g = (uint8_t)std::min(255, int(observe));
             valid.push_back({cur, a, b, observe, round});
-            spars.push_back(sparsity(o.corner_map, ind));
+            spars.push_back(sparsity(map, ind));
         }
     }
     const double wt = o.weightType;
@@ -689,24 +698,25 @@ static void add_edge_factors(Odom& o, std::vector<PtC>& cloud, std::vector<Resid
         else r.w = (spars[i] + obs[i]) / 2;
         out.push_back(r);
     }
-    o.stats.n_edge_res = (int64_t)valid.size();
-    o.stats.n_edge_valid = n_valid;
+    o.stats.n_res[c] = (int64_t)valid.size();
+    o.stats.n_valid[c] = n_valid;
 }
 
-// addSurfCostFactor (:434-578)
-static void add_surf_factors(Odom& o, std::vector<PtC>& cloud, std::vector<Residual>& out) {
+// addSurfCostFactor (:434-578); Odom_BPF addFacadeCostFactor (:1012-1193) with the surf thresholds
+static void add_plane_factors(Odom& o, int c, std::vector<PtC>& cloud, std::vector<Residual>& out) {
     struct Info { V3 cur, n; float d, observe, round; };
     std::vector<Info> valid;
     std::vector<double> spars, obs;
+    std::vector<PtC>& map = o.maps[c];
     int64_t n_valid = 0;
     for (size_t i = 0; i < cloud.size(); i++) {
         PtC pt = o.associate(cloud[i]);
         int ind[5]; float d2[5];
-        o.knn(false, pt, ind, d2);
+        o.knn(c, pt, ind, d2);
         if (!(d2[4] < 1.0)) continue;
         double A[5][3];
         for (int j = 0; j < 5; j++) {
-            A[j][0] = o.surf_map[ind[j]].x; A[j][1] = o.surf_map[ind[j]].y; A[j][2] = o.surf_map[ind[j]].z;
+            A[j][0] = map[ind[j]].x; A[j][1] = map[ind[j]].y; A[j][2] = map[ind[j]].z;
         }
         V3 n = plane_fit5(A);
         double negative_OA_dot_norm = 1 / norm(n);
@@ -714,7 +724,7 @@ static void add_surf_factors(Odom& o, std::vector<PtC>& cloud, std::vector<Resid
         if (z > 0.0) { double s = std::sqrt(z); n = V3{n.x / s, n.y / s, n.z / s}; }
         bool planeValid = true;
         for (int j = 0; j < 5; j++) {
-            if (std::fabs(n.x * o.surf_map[ind[j]].x + n.y * o.surf_map[ind[j]].y + n.z * o.surf_map[ind[j]].z +
+            if (std::fabs(n.x * map[ind[j]].x + n.y * map[ind[j]].y + n.z * map[ind[j]].z +
                           negative_OA_dot_norm) > 0.2) {
                 planeValid = false;
                 break;
@@ -724,11 +734,11 @@ static void add_surf_factors(Odom& o, std::vector<PtC>& cloud, std::vector<Resid
         if (planeValid) {
             ++n_valid;
             float observe, round;
-            if (!pindex(o.surf_map, ind, o.k_new_surf, o.theta_p_surf, o.theta_max_surf, observe, round)) continue;
+            if (!pindex(map, ind, o.k_new(c), o.theta_p(c), o.theta_max(c), observe, round)) continue;
             cloud[i].r = (uint8_t)std::min(255, int(round));
             cloud[i].g = (uint8_t)std::min(255, int(observe));
             valid.push_back({cur, n, (float)negative_OA_dot_norm, observe, round});
-            spars.push_back(sparsity(o.surf_map, ind));
+            spars.push_back(sparsity(map, ind));
         }
     }
     const double wt = o.weightType;
@@ -747,8 +757,8 @@ static void add_surf_factors(Odom& o, std::vector<PtC>& cloud, std::vector<Resid
         else r.w = (obs[i] + spars[i]) / 2;
         out.push_back(r);
     }
-    o.stats.n_surf_res = (int64_t)valid.size();
-    o.stats.n_surf_valid = n_valid;
+    o.stats.n_res[c] = (int64_t)valid.size();
+    o.stats.n_valid[c] = n_valid;
 }
 
 // extractstablepoint (:7-25)
@@ -762,11 +772,13 @@ static void extract_stable(std::vector<PtC>& m, int k_new, float theta_p, int th
     m.swap(keep);
 }
 
-// addPointsToMap (:589-647)
-static void add_points_to_map(Odom& o, const std::vector<PtC>& ds_edge, const std::vector<PtC>& ds_surf) {
+// addPointsToMap (:589-647; BPF :1197-1290): append every class, CropBox +-100 m around odom.t,
+// rgbds with the class leaf, extractstablepoint with the class thresholds, ageing. The classes are
+// independent maps, so the reference's order across them (surf before corner, facade first) is moot.
+static void add_points_to_map(Odom& o, const std::vector<PtC>* ds) {
     const bool stable = (o.opts & PFREF_VG_STABLE) != 0;
-    for (const PtC& p : ds_edge) o.corner_map.push_back(o.associate(p));
-    for (const PtC& p : ds_surf) o.surf_map.push_back(o.associate(p));
+    for (int c = 0; c < o.nc; ++c)
+        for (const PtC& p : ds[c]) o.maps[c].push_back(o.associate(p));
     const double tx = o.odom.t.x, ty = o.odom.t.y, tz = o.odom.t.z;
     const float mn[3] = {(float)(tx - 100), (float)(ty - 100), (float)(tz - 100)};
     const float mx[3] = {(float)(tx + 100), (float)(ty + 100), (float)(tz + 100)};
@@ -777,26 +789,33 @@ static void add_points_to_map(Odom& o, const std::vector<PtC>& ds_edge, const st
             out.push_back(p);
         }
     };
-    std::vector<PtC> tmpSurf, tmpCorner;
-    crop(o.surf_map, tmpSurf);
-    crop(o.corner_map, tmpCorner);
-    rgbds(tmpSurf, o.map_resolution * 2, stable, o.surf_map);
-    rgbds(tmpCorner, o.map_resolution, stable, o.corner_map);
-    extract_stable(o.surf_map, o.k_new_surf, o.theta_p_surf, o.theta_max_surf);
-    extract_stable(o.corner_map, o.k_new_edge, o.theta_p_edge, o.theta_max_edge);
-    for (PtC& p : o.surf_map) p.r = p.r > 250 ? 255 : (uint8_t)(p.r + 2);
-    for (PtC& p : o.corner_map) p.r = p.r > 250 ? 255 : (uint8_t)(p.r + 2);
+    for (int c = 0; c < o.nc; ++c) {
+        std::vector<PtC> tmp;
+        crop(o.maps[c], tmp);
+        rgbds(tmp, o.leaf_rg[c], stable, o.maps[c]);
+        extract_stable(o.maps[c], o.k_new(c), o.theta_p(c), o.theta_max(c));
+        for (PtC& p : o.maps[c]) p.r = p.r > 250 ? 255 : (uint8_t)(p.r + 2);
+    }
 }
 
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-int odom_update(Odom& o, const std::vector<PtC>& edge_in, const std::vector<PtC>& surf_in) {
+static void legacy_stats(Odom& o) {       // ES field names: class 0 = edge, class 1 = surf
+    pfref_stats& st = o.stats;
+    st.n_edge_in = st.n_in[0]; st.n_surf_in = st.n_in[1];
+    st.n_edge_ds = st.n_ds[0]; st.n_surf_ds = st.n_ds[1];
+    st.n_edge_map = st.n_map[0]; st.n_surf_map = st.n_map[1];
+    st.n_edge_res = st.n_res[0]; st.n_surf_res = st.n_res[1];
+    st.n_edge_valid = st.n_valid[0]; st.n_surf_valid = st.n_valid[1];
+}
+
+// updatePointsToMap: ES :229-282, BPF :702-749 (the same sequence over 2 or 3 map classes)
+int odom_update(Odom& o, const std::vector<PtC>* in) {
     pfref_stats& st = o.stats;
     st = pfref_stats{};
-    st.n_edge_in = (int64_t)edge_in.size();
-    st.n_surf_in = (int64_t)surf_in.size();
+    for (int c = 0; c < o.nc; ++c) st.n_in[c] = (int64_t)in[c].size();
     if (o.optimization_count > 2) o.optimization_count--;               // :232-233
     Iso pred = iso_mul(o.odom, iso_mul(iso_inv(o.last_odom), o.odom)); // :235-237
     o.last_odom = o.odom;
@@ -806,26 +825,28 @@ int odom_update(Odom& o, const std::vector<PtC>& edge_in, const std::vector<PtC>
     o.params[4] = o.odom.t.x; o.params[5] = o.odom.t.y; o.params[6] = o.odom.t.z;
     const bool stable = (o.opts & PFREF_VG_STABLE) != 0;
     double t0 = now_s();
-    std::vector<PtC> ds_edge, ds_surf;
-    voxel_grid(edge_in, o.leaf_edge_vg, stable, ds_edge);               // :242-245
-    voxel_grid(surf_in, o.leaf_surf_vg, stable, ds_surf);
-    st.n_edge_ds = (int64_t)ds_edge.size();
-    st.n_surf_ds = (int64_t)ds_surf.size();
+    std::vector<PtC> ds[3];
+    for (int c = 0; c < o.nc; ++c) {                                    // :242-245 / :714-719
+        voxel_grid(in[c], o.leaf_vg[c], stable, ds[c]);
+        st.n_ds[c] = (int64_t)ds[c].size();
+    }
     double t1 = now_s();
     st.t_downsample = t1 - t0;
-    if (o.corner_map.size() > 10 && o.surf_map.size() > 50) {           // :247
-        if (!(o.opts & PFREF_KNN_BRUTE)) {
-            o.tree_edge.build(o.corner_map);
-            o.tree_surf.build(o.surf_map);
-        }
+    bool big_enough = true;                                             // :247 / :721
+    for (int c = 0; c < o.nc; ++c) big_enough = big_enough && o.maps[c].size() > (o.plane[c] ? 50u : 10u);
+    if (big_enough) {
+        if (!(o.opts & PFREF_KNN_BRUTE))
+            for (int c = 0; c < o.nc; ++c) o.trees[c].build(o.maps[c]);
         double t2 = now_s();
         st.t_tree = t2 - t1;
         st.outer_iterations = o.optimization_count;
-        for (int it = 0; it < o.optimization_count; it++) {           // :252-272
+        for (int it = 0; it < o.optimization_count; it++) {           // :252-272 / :727-747
             double ta = now_s();
             std::vector<Residual> res;
-            add_edge_factors(o, ds_edge, res);
-            add_surf_factors(o, ds_surf, res);
+            for (int c = 0; c < o.nc; ++c) {
+                if (o.plane[c]) add_plane_factors(o, c, ds[c], res);
+                else add_line_factors(o, c, ds[c], res);
+            }
             double tb = now_s();
             st.lm_iterations += solve_lm(o.params, res, (o.opts & PFREF_LM_NORMAL_EQ) != 0);
             double tc = now_s();
@@ -840,10 +861,10 @@ int odom_update(Odom& o, const std::vector<PtC>& edge_in, const std::vector<PtC>
     o.odom = iso_identity();                                             // :278-280
     o.odom.R = q2m(o.q());
     o.odom.t = o.t();
-    add_points_to_map(o, ds_edge, ds_surf);                              // :281
+    add_points_to_map(o, ds);                                            // :281
     st.t_mapupdate = now_s() - t3;
-    st.n_edge_map = (int64_t)o.corner_map.size();
-    st.n_surf_map = (int64_t)o.surf_map.size();
+    for (int c = 0; c < o.nc; ++c) st.n_map[c] = (int64_t)o.maps[c].size();
+    legacy_stats(o);
     return 0;
 }
 
@@ -966,14 +987,20 @@ double pfref_surf_eval(const double x[7], const double cur[3], const double n[3]
     return surf_eval(x, V3{cur[0], cur[1], cur[2]}, V3{n[0], n[1], n[2]}, d, weight, J);
 }
 
-pfref_odom* pfref_odom_create(const pfref_lidar* lidar, const pfref_odom_params* p, int opts) {
+static pfref_odom* create(const pfref_lidar* lidar, const pfref_odom_params* p, int opts, bool bpf) {
     if (!(p->weight_type == 0 || p->weight_type == 1 || p->weight_type == 2 || p->weight_type == 12)) return nullptr;
     pfref_odom* h = new pfref_odom();
     Odom& o = h->o;
     o.lidar = *lidar;
     o.opts = opts;
-    o.leaf_edge_vg = (float)p->map_resolution;             // setLeafSize(double -> float) (:189-190)
-    o.leaf_surf_vg = (float)(p->map_resolution * 2);
+    o.map_resolution = (float)p->map_resolution;
+    // ES (:186-190): corner leaf r, surf leaf 2r. BPF (:657-659): beam r, pillar r, facade 2r.
+    o.nc = bpf ? 3 : 2;
+    for (int c = 0; c < o.nc; ++c) {
+        o.plane[c] = c == o.nc - 1;
+        o.leaf_vg[c] = o.plane[c] ? (float)(p->map_resolution * 2) : (float)p->map_resolution;  // double -> float
+        o.leaf_rg[c] = o.plane[c] ? o.map_resolution * 2 : o.map_resolution;                    // float
+    }
     o.odom = iso_identity();
     o.last_odom = iso_identity();
     o.optimization_count = 2;
@@ -981,24 +1008,40 @@ pfref_odom* pfref_odom_create(const pfref_lidar* lidar, const pfref_odom_params*
     o.theta_p_surf = o.theta_p_edge = p->theta_p;
     o.theta_max_surf = o.theta_max_edge = p->theta_max;
     o.weightType = p->weight_type;
-    o.map_resolution = (float)p->map_resolution;
     return h;
+}
+
+pfref_odom* pfref_odom_create(const pfref_lidar* lidar, const pfref_odom_params* p, int opts) {
+    return create(lidar, p, opts, false);
+}
+pfref_odom* pfref_bpf_create(const pfref_lidar* lidar, const pfref_odom_params* p, int opts) {
+    return create(lidar, p, opts, true);
 }
 
 void pfref_odom_destroy(pfref_odom* h) { delete h; }
 
-int pfref_odom_init_map(pfref_odom* h, const float* edge, size_t ne, const float* surf, size_t ns) {
-    std::vector<PtC> e = to_ptc(edge, ne), s = to_ptc(surf, ns);   // :217-222
-    h->o.corner_map.insert(h->o.corner_map.end(), e.begin(), e.end());
-    h->o.surf_map.insert(h->o.surf_map.end(), s.begin(), s.end());
-    h->o.optimization_count = 12;
+int pfref_odom_classes(const pfref_odom* h) { return h->o.nc; }
+
+// initMapWithPoints (ES :217-222, BPF :685-691): append the raw clouds, optimization_count = 12
+int pfref_odom_init_map_n(pfref_odom* h, const float* const* clouds, const size_t* n) {
+    Odom& o = h->o;
+    o.stats = pfref_stats{};
+    for (int c = 0; c < o.nc; ++c) {
+        std::vector<PtC> v = to_ptc(clouds[c], n[c]);
+        o.maps[c].insert(o.maps[c].end(), v.begin(), v.end());
+        o.stats.n_in[c] = (int64_t)n[c];
+        o.stats.n_map[c] = (int64_t)o.maps[c].size();
+    }
+    o.optimization_count = 12;
     h->inited = true;
-    h->o.stats = pfref_stats{};
-    h->o.stats.n_edge_in = (int64_t)ne;
-    h->o.stats.n_surf_in = (int64_t)ns;
-    h->o.stats.n_edge_map = (int64_t)h->o.corner_map.size();
-    h->o.stats.n_surf_map = (int64_t)h->o.surf_map.size();
+    legacy_stats(o);
     return 0;
+}
+
+int pfref_odom_init_map(pfref_odom* h, const float* edge, size_t ne, const float* surf, size_t ns) {
+    const float* c[2] = {edge, surf};
+    const size_t n[2] = {ne, ns};
+    return pfref_odom_init_map_n(h, c, n);
 }
 
 void pfref_odom_get_pose(const pfref_odom* h, double pose[7]) {
@@ -1007,14 +1050,23 @@ void pfref_odom_get_pose(const pfref_odom* h, double pose[7]) {
     pose[4] = h->o.odom.t.x; pose[5] = h->o.odom.t.y; pose[6] = h->o.odom.t.z;
 }
 
-int pfref_odom_update(pfref_odom* h, const float* edge, size_t ne, const float* surf, size_t ns, double pose_out[7]) {
-    int rc = odom_update(h->o, to_ptc(edge, ne), to_ptc(surf, ns));
+int pfref_odom_update_n(pfref_odom* h, const float* const* clouds, const size_t* n, double pose_out[7]) {
+    std::vector<PtC> in[3];
+    for (int c = 0; c < h->o.nc; ++c) in[c] = to_ptc(clouds[c], n[c]);
+    int rc = odom_update(h->o, in);
     if (pose_out) pfref_odom_get_pose(h, pose_out);
     return rc;
 }
 
+int pfref_odom_update(pfref_odom* h, const float* edge, size_t ne, const float* surf, size_t ns, double pose_out[7]) {
+    const float* c[2] = {edge, surf};
+    const size_t n[2] = {ne, ns};
+    return pfref_odom_update_n(h, c, n, pose_out);
+}
+
 int pfref_odom_get_map(const pfref_odom* h, int which, float* xyz, uint8_t* rg, size_t cap, size_t* n) {
-    const std::vector<PtC>& m = which == 0 ? h->o.corner_map : h->o.surf_map;
+    if (which < 0 || which >= h->o.nc) return -1;
+    const std::vector<PtC>& m = h->o.maps[which];
     *n = m.size();
     if (m.size() > cap) return -1;
     for (size_t i = 0; i < m.size(); ++i) {
@@ -1025,7 +1077,8 @@ int pfref_odom_get_map(const pfref_odom* h, int which, float* xyz, uint8_t* rg, 
 }
 
 int pfref_odom_set_map(pfref_odom* h, int which, const float* xyz, const uint8_t* rg, size_t n) {
-    std::vector<PtC>& m = which == 0 ? h->o.corner_map : h->o.surf_map;
+    if (which < 0 || which >= h->o.nc) return -1;
+    std::vector<PtC>& m = h->o.maps[which];
     m.resize(n);
     for (size_t i = 0; i < n; ++i) {
         m[i].x = xyz[3 * i]; m[i].y = xyz[3 * i + 1]; m[i].z = xyz[3 * i + 2];
@@ -1049,6 +1102,7 @@ void pfref_odom_set_state(pfref_odom* h, const double odom_pose[7], const double
 void pfref_odom_set_opt_count(pfref_odom* h, int n) { h->o.optimization_count = n; }
 
 int pfref_odom_frame(pfref_odom* h, const pfref_lidar* lidar, const float* xyzi, size_t n, double pose_out[7]) {
+    if (h->o.nc != 2) return -1;                       // featureExtraction feeds the ES estimator only
     std::vector<PtI> e, s;
     feature_extraction(*lidar, h->o.opts, reinterpret_cast<const PtI*>(xyzi), n, e, s);
     const float* ep = reinterpret_cast<const float*>(e.data());

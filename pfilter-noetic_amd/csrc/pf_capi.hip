@@ -46,7 +46,7 @@ struct pf_fe {
 
 struct pf_odom {
     OdomGPU o;
-    std::vector<float4> host_e, host_s;
+    std::vector<float4> host[kMaxC];
 };
 
 extern "C" {
@@ -118,8 +118,8 @@ int pf_fe_extract(pf_fe* h, const float* xyzi, size_t n, size_t stride_bytes, fl
 }
 
 // ------------------------------------------------------------------------------------------------
-int pf_odom_create(const pf_lidar_params* lidar, const pf_odom_params* params, int device, size_t max_points,
-                   size_t map_capacity, pf_odom** out) {
+static int create(const pf_lidar_params* lidar, const pf_odom_params* params, int device, size_t max_points,
+                  size_t map_capacity, int nc, pf_odom** out) {
     if (!lidar || !params || !out) return PF_EINVAL;
     const int wt = params->weight_type;
     if (!(wt == 0 || wt == 1 || wt == 2 || wt == 12)) return PF_EINVAL;   // reference: ROS_ERROR + UB
@@ -129,7 +129,7 @@ int pf_odom_create(const pf_lidar_params* lidar, const pf_odom_params* params, i
     PF_HIP_TRY(hipSetDevice(device));
     pf_odom* h = new (std::nothrow) pf_odom();
     if (!h) return PF_ENOMEM;
-    int rc = odom_create(h->o, *lidar, *params, device, max_points, map_capacity);
+    int rc = odom_create(h->o, *lidar, *params, device, max_points, map_capacity, nc);
     if (rc != PF_OK) {
         pf_odom_destroy(h);
         return rc;
@@ -137,6 +137,18 @@ int pf_odom_create(const pf_lidar_params* lidar, const pf_odom_params* params, i
     *out = h;
     return PF_OK;
 }
+
+int pf_odom_create(const pf_lidar_params* lidar, const pf_odom_params* params, int device, size_t max_points,
+                   size_t map_capacity, pf_odom** out) {
+    return create(lidar, params, device, max_points, map_capacity, 2, out);
+}
+
+int pf_bpf_create(const pf_lidar_params* lidar, const pf_odom_params* params, int device, size_t max_points,
+                  size_t map_capacity, pf_odom** out) {
+    return create(lidar, params, device, max_points, map_capacity, 3, out);
+}
+
+int pf_odom_classes(pf_odom* h) { return h ? h->o.cls.nc : PF_EINVAL; }
 
 int pf_odom_destroy(pf_odom* h) {
     if (!h) return PF_OK;
@@ -170,20 +182,21 @@ static int stage_b_end(pf_odom* h, int p) {
     return PF_OK;
 }
 
-static int stage_inputs(pf_odom* h, int p, const float* edge, size_t ne, size_t es, const float* surf, size_t ns,
-                        size_t ss) {
+// the caller's class clouds (host memory) into slot p's inputs, on stage A's stream
+static int stage_inputs(pf_odom* h, int p, const float* const* cl, const size_t* n, const size_t* stride) {
     OdomGPU& o = h->o;
-    if ((!edge && ne) || (!surf && ns) || !valid_stride(es) || !valid_stride(ss)) return PF_EINVAL;
-    if (ne > o.in_cap || ns > o.in_cap) return PF_ECAPACITY;
-    repack(edge, ne, es, h->host_e);
-    repack(surf, ns, ss, h->host_s);
+    const int nc = o.cls.nc;
+    for (int c = 0; c < nc; ++c) {
+        if ((!cl[c] && n[c]) || !valid_stride(stride[c])) return PF_EINVAL;
+        if (n[c] > o.in_cap) return PF_ECAPACITY;
+    }
     StageBuf& sb = o.sb[p];
-    if (ne) PF_HIP_TRY(hipMemcpyAsync(sb.in_edge, h->host_e.data(), sizeof(float4) * ne, hipMemcpyHostToDevice,
-                                      o.stream_a));
-    if (ns) PF_HIP_TRY(hipMemcpyAsync(sb.in_surf, h->host_s.data(), sizeof(float4) * ns, hipMemcpyHostToDevice,
-                                      o.stream_a));
-    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, sb.cnt + C_EIN, (int)ne);
-    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, sb.cnt + C_SIN, (int)ns);
+    for (int c = 0; c < nc; ++c) {
+        repack(cl[c], n[c], stride[c], h->host[c]);
+        if (n[c]) PF_HIP_TRY(hipMemcpyAsync(sb.in[c], h->host[c].data(), sizeof(float4) * n[c], hipMemcpyHostToDevice,
+                                            o.stream_a));
+        hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, sb.cnt + C_IN + c, (int)n[c]);
+    }
     return PF_OK;
 }
 
@@ -208,18 +221,17 @@ static int frame_status(pf_odom* h) {
     PF_HIP_TRY(hipGetLastError());
     if (o.h_cnt[C_ERR]) return PF_EHIP;                  // a bounded device-side wait gave up
     if (!o.h_cnt[C_GATE]) return PF_W_MAP_TOO_SMALL;
-    if (o.h_cnt[C_EDGE_KEPT] < 20 || o.h_cnt[C_SURF_KEPT] < 20) return PF_W_FEW_CORRESPONDENCES;
+    for (int c = 0; c < o.cls.nc; ++c)               // :428-431 / :574-577, BPF :875-878, :1188-1191
+        if (o.h_cnt[C_KEPT + c] < 20) return PF_W_FEW_CORRESPONDENCES;
     return PF_OK;
 }
 
-int pf_odom_init_map(pf_odom* h, const float* edge, size_t ne, size_t edge_stride, const float* surf, size_t ns,
-                     size_t surf_stride) {
-    if (!h) return PF_EINVAL;
+static int init_map_n(pf_odom* h, const float* const* cl, const size_t* n, const size_t* stride) {
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
     const int p = o.frames % kSlots;
     int rc = stage_a_begin(h, p);
-    if (!rc) rc = stage_inputs(h, p, edge, ne, edge_stride, surf, ns, surf_stride);
+    if (!rc) rc = stage_inputs(h, p, cl, n, stride);
     if (!rc) rc = stage_a_end_b_begin(h, p);
     if (rc) return rc;
     odom_enqueue_init(o, p, o.stream);
@@ -230,14 +242,12 @@ int pf_odom_init_map(pf_odom* h, const float* edge, size_t ne, size_t edge_strid
     return PF_OK;
 }
 
-int pf_odom_update(pf_odom* h, const float* edge, size_t ne, size_t edge_stride, const float* surf, size_t ns,
-                   size_t surf_stride, double pose_out[7]) {
-    if (!h) return PF_EINVAL;
+static int update_n(pf_odom* h, const float* const* cl, const size_t* n, const size_t* stride, double pose_out[7]) {
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
     const int p = o.frames % kSlots;
     int rc = stage_a_begin(h, p);
-    if (!rc) rc = stage_inputs(h, p, edge, ne, edge_stride, surf, ns, surf_stride);
+    if (!rc) rc = stage_inputs(h, p, cl, n, stride);
     if (rc) return rc;
     stage_enqueue_vg(o, p, o.stream_a);
     rc = stage_a_end_b_begin(h, p);
@@ -252,6 +262,38 @@ int pf_odom_update(pf_odom* h, const float* edge, size_t ne, size_t edge_stride,
     return frame_status(h);
 }
 
+int pf_odom_init_map(pf_odom* h, const float* edge, size_t ne, size_t edge_stride, const float* surf, size_t ns,
+                     size_t surf_stride) {
+    if (!h || h->o.cls.nc != 2) return PF_EINVAL;
+    const float* cl[2] = {edge, surf};
+    const size_t n[2] = {ne, ns}, st[2] = {edge_stride, surf_stride};
+    return init_map_n(h, cl, n, st);
+}
+
+int pf_odom_update(pf_odom* h, const float* edge, size_t ne, size_t edge_stride, const float* surf, size_t ns,
+                   size_t surf_stride, double pose_out[7]) {
+    if (!h || h->o.cls.nc != 2) return PF_EINVAL;
+    const float* cl[2] = {edge, surf};
+    const size_t n[2] = {ne, ns}, st[2] = {edge_stride, surf_stride};
+    return update_n(h, cl, n, st, pose_out);
+}
+
+int pf_bpf_init_map(pf_odom* h, const float* beam, size_t nb, size_t beam_stride, const float* pillar, size_t np,
+                    size_t pillar_stride, const float* facade, size_t nf, size_t facade_stride) {
+    if (!h || h->o.cls.nc != 3) return PF_EINVAL;
+    const float* cl[3] = {beam, pillar, facade};
+    const size_t n[3] = {nb, np, nf}, st[3] = {beam_stride, pillar_stride, facade_stride};
+    return init_map_n(h, cl, n, st);
+}
+
+int pf_bpf_update(pf_odom* h, const float* beam, size_t nb, size_t beam_stride, const float* pillar, size_t np,
+                  size_t pillar_stride, const float* facade, size_t nf, size_t facade_stride, double pose_out[7]) {
+    if (!h || h->o.cls.nc != 3) return PF_EINVAL;
+    const float* cl[3] = {beam, pillar, facade};
+    const size_t n[3] = {nb, np, nf}, st[3] = {beam_stride, pillar_stride, facade_stride};
+    return update_n(h, cl, n, st, pose_out);
+}
+
 int pf_odom_get_pose(pf_odom* h, double pose[7]) {
     if (!h || !pose) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->o.device));
@@ -259,17 +301,17 @@ int pf_odom_get_pose(pf_odom* h, double pose[7]) {
 }
 
 int pf_odom_get_map(pf_odom* h, int which, float* xyz, uint8_t* rg, size_t cap, size_t* n) {
-    if (!h || !n || (which != 0 && which != 1)) return PF_EINVAL;
+    if (!h || !n || which < 0 || which >= h->o.cls.nc) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
     PF_HIP_TRY(hipMemcpyAsync(o.h_cnt, o.cnt, sizeof(int) * C_COUNT, hipMemcpyDeviceToHost, o.stream));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
-    const size_t m = (size_t)o.h_cnt[which == 0 ? C_ME : C_MS];
+    const size_t m = (size_t)o.h_cnt[C_M + which];
     *n = m;
     if (!xyz && !rg) return PF_OK;
     if (m > cap) return PF_ECAPACITY;
     std::vector<float4> tmp(m);
-    if (m) PF_HIP_TRY(hipMemcpy(tmp.data(), which == 0 ? o.map_e : o.map_s, sizeof(float4) * m, hipMemcpyDeviceToHost));
+    if (m) PF_HIP_TRY(hipMemcpy(tmp.data(), o.map[which], sizeof(float4) * m, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < m; ++i) {
         if (xyz) { xyz[3 * i] = tmp[i].x; xyz[3 * i + 1] = tmp[i].y; xyz[3 * i + 2] = tmp[i].z; }
         if (rg) {
@@ -283,7 +325,7 @@ int pf_odom_get_map(pf_odom* h, int which, float* xyz, uint8_t* rg, size_t cap, 
 }
 
 int pf_odom_set_map(pf_odom* h, int which, const float* xyz, const uint8_t* rg, size_t n) {
-    if (!h || (which != 0 && which != 1) || (!xyz && n)) return PF_EINVAL;
+    if (!h || which < 0 || which >= h->o.cls.nc || (!xyz && n)) return PF_EINVAL;
     OdomGPU& o = h->o;
     if (n > o.map_cap) return PF_ECAPACITY;
     PF_HIP_TRY(hipSetDevice(o.device));
@@ -294,9 +336,8 @@ int pf_odom_set_map(pf_odom* h, int which, const float* xyz, const uint8_t* rg, 
         std::memcpy(&wf, &w, 4);
         tmp[i] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], wf);
     }
-    if (n) PF_HIP_TRY(hipMemcpyAsync(which == 0 ? o.map_e : o.map_s, tmp.data(), sizeof(float4) * n,
-                                     hipMemcpyHostToDevice, o.stream));
-    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + (which == 0 ? C_ME : C_MS), (int)n);
+    if (n) PF_HIP_TRY(hipMemcpyAsync(o.map[which], tmp.data(), sizeof(float4) * n, hipMemcpyHostToDevice, o.stream));
+    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_M + which, (int)n);
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     return PF_OK;
 }
@@ -309,16 +350,23 @@ int pf_odom_get_stats(pf_odom* h, pf_odom_stats* s) {
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     const int* c = o.h_cnt;
     std::memset(s, 0, sizeof(*s));
-    s->n_edge_in = c[C_EIN];
-    s->n_surf_in = c[C_SIN];
-    s->n_edge_ds = c[C_EDS];
-    s->n_surf_ds = c[C_SDS];
-    s->n_edge_map = c[C_ME];
-    s->n_surf_map = c[C_MS];
-    s->n_edge_res = c[C_EDGE_KEPT];
-    s->n_surf_res = c[C_SURF_KEPT];
-    s->n_edge_valid = c[C_EDGE_VALID];
-    s->n_surf_valid = c[C_SURF_VALID];
+    for (int k = 0; k < o.cls.nc; ++k) {
+        s->n_in[k] = c[C_IN + k];
+        s->n_ds[k] = c[C_DS + k];
+        s->n_map[k] = c[C_M + k];
+        s->n_res[k] = c[C_KEPT + k];
+        s->n_valid[k] = c[C_VALID + k];
+    }
+    s->n_edge_in = s->n_in[0];          // ES names: class 0 = edge (corner), class 1 = surf
+    s->n_surf_in = s->n_in[1];
+    s->n_edge_ds = s->n_ds[0];
+    s->n_surf_ds = s->n_ds[1];
+    s->n_edge_map = s->n_map[0];
+    s->n_surf_map = s->n_map[1];
+    s->n_edge_res = s->n_res[0];
+    s->n_surf_res = s->n_res[1];
+    s->n_edge_valid = s->n_valid[0];
+    s->n_surf_valid = s->n_valid[1];
     s->outer_iterations = c[C_OUTER];
     s->lm_iterations = c[C_LM_ITERS];
     s->map_too_small = c[C_GATE] ? 0 : 1;
@@ -333,7 +381,7 @@ static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool s
     hipGraph_t g;
     PF_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     if (stage_a) {
-        stage_enqueue_fe(o, p, o.stage, s);
+        if (o.cls.nc == 2) stage_enqueue_fe(o, p, o.stage, s);
         stage_enqueue_vg(o, p, s);
     } else {
         odom_enqueue_update(o, p, s);
@@ -344,15 +392,28 @@ static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool s
     return PF_OK;
 }
 
-static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n) {
+// one frame through both stages. ES: the raw scan d_in[0 .. n) is copied to the staging buffer and
+// stage A runs featureExtraction + VoxelGrid. BPF: the class clouds cl[c][0 .. ncl[c]) are copied
+// into the slot's inputs and stage A runs VoxelGrid. The copies and counts stay outside the graphs.
+static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4* const* cl, const size_t* ncl) {
     OdomGPU& o = h->o;
-    if (n > o.in_cap) return PF_ECAPACITY;
+    const int nc = o.cls.nc;
     const int p = o.frames % kSlots;
     const bool steady = o.inited && o.opt_count_host <= 2 && o.graph_enabled;
     int rc = stage_a_begin(h, p);
     if (rc) return rc;
-    if (n) PF_HIP_TRY(hipMemcpyAsync(o.stage, d_in, sizeof(float4) * n, hipMemcpyDeviceToDevice, o.stream_a));
-    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, o.sb[p].cnt + C_NIN, (int)n);
+    if (nc == 2) {
+        if (n > o.in_cap) return PF_ECAPACITY;
+        if (n) PF_HIP_TRY(hipMemcpyAsync(o.stage, d_in, sizeof(float4) * n, hipMemcpyDeviceToDevice, o.stream_a));
+        hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, o.sb[p].cnt + C_NIN, (int)n);
+    } else {
+        for (int c = 0; c < nc; ++c) {
+            if (ncl[c] > o.in_cap) return PF_ECAPACITY;
+            if (ncl[c]) PF_HIP_TRY(hipMemcpyAsync(o.sb[p].in[c], cl[c], sizeof(float4) * ncl[c], hipMemcpyDeviceToDevice,
+                                                  o.stream_a));
+            hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, o.sb[p].cnt + C_IN + c, (int)ncl[c]);
+        }
+    }
     if (steady) {
         if (!o.graph_a[p]) {
             rc = capture(o.stream_a, &o.graph_a[p], o, p, true);
@@ -360,7 +421,7 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n) {
         }
         PF_HIP_TRY(hipGraphLaunch(o.graph_a[p], o.stream_a));
     } else {
-        stage_enqueue_fe(o, p, o.stage, o.stream_a);
+        if (nc == 2) stage_enqueue_fe(o, p, o.stage, o.stream_a);
         if (o.inited) stage_enqueue_vg(o, p, o.stream_a);
     }
     rc = stage_a_end_b_begin(h, p);
@@ -380,29 +441,42 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n) {
 }
 
 int pf_odom_frame_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]) {
-    if (!h || (!d_xyzi && n)) return PF_EINVAL;
+    if (!h || (!d_xyzi && n) || h->o.cls.nc != 2) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->o.device));
-    int rc = enqueue_frame(h, reinterpret_cast<const float4*>(d_xyzi), n);
+    int rc = enqueue_frame(h, reinterpret_cast<const float4*>(d_xyzi), n, nullptr, nullptr);
     if (rc) return rc;
     if (pose_out) return read_pose(h, pose_out);
     return PF_OK;
 }
 
 int pf_odom_frame_host(pf_odom* h, const float* xyzi, size_t n, size_t stride_bytes, double pose_out[7]) {
-    if (!h || (!xyzi && n) || !valid_stride(stride_bytes)) return PF_EINVAL;
+    if (!h || (!xyzi && n) || !valid_stride(stride_bytes) || h->o.cls.nc != 2) return PF_EINVAL;
     OdomGPU& o = h->o;
     if (n > o.in_cap) return PF_ECAPACITY;
     PF_HIP_TRY(hipSetDevice(o.device));
-    repack(xyzi, n, stride_bytes, h->host_e);
+    repack(xyzi, n, stride_bytes, h->host[0]);
     // the upload goes through fe.d_in_stage on stage A's stream, ordered before the frame's copy
     // into the staging buffer; the host vector is reused next call, so wait for the copy
-    if (n) PF_HIP_TRY(hipMemcpyAsync(o.fe.d_in_stage, h->host_e.data(), sizeof(float4) * n, hipMemcpyHostToDevice,
+    if (n) PF_HIP_TRY(hipMemcpyAsync(o.fe.d_in_stage, h->host[0].data(), sizeof(float4) * n, hipMemcpyHostToDevice,
                                      o.stream_a));
     PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
-    int rc = enqueue_frame(h, o.fe.d_in_stage, n);
+    int rc = enqueue_frame(h, o.fe.d_in_stage, n, nullptr, nullptr);
     if (rc) return rc;
     if (pose_out) return read_pose(h, pose_out);
     PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    return PF_OK;
+}
+
+int pf_bpf_frame_device(pf_odom* h, const float* d_beam, size_t nb, const float* d_pillar, size_t np,
+                        const float* d_facade, size_t nf, double pose_out[7]) {
+    if (!h || h->o.cls.nc != 3 || (!d_beam && nb) || (!d_pillar && np) || (!d_facade && nf)) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    const float4* cl[3] = {reinterpret_cast<const float4*>(d_beam), reinterpret_cast<const float4*>(d_pillar),
+                           reinterpret_cast<const float4*>(d_facade)};
+    const size_t n[3] = {nb, np, nf};
+    int rc = enqueue_frame(h, nullptr, 0, cl, n);
+    if (rc) return rc;
+    if (pose_out) return read_pose(h, pose_out);
     return PF_OK;
 }
 

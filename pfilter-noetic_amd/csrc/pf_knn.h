@@ -26,11 +26,18 @@ struct GridGPU {
     size_t cell_cap = 0;
 };
 
+// up to kGridMaps maps share one cell array (map m's cells start at dims[8 m + 6])
+constexpr int kGridMaps = 3;
+struct GridPtrs {                 // maps and their device-resident point counts
+    const float4* m[kGridMaps];
+    const int* n[kGridMaps];
+    int nm;
+};
+
 int grid_alloc(GridGPU& g, size_t pts_cap, size_t cell_cap);
 void grid_free(GridGPU& g);
-// Build the grids of up to two maps (map1 may be null). Counts are device-resident.
-void grid_build(GridGPU& g, const float4* map0, const int* d_m0, const float4* map1, const int* d_m1, PrimWork& w,
-                hipStream_t s);
+// Build the grids of gp.nm maps (counts device-resident). pts_cap must hold all maps' points.
+void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s);
 
 struct GridView {
     const int* dims;

@@ -18,11 +18,10 @@ __device__ __forceinline__ int wave_max_i(int v) {
     return v;
 }
 
-__device__ void grid_dims(const int* bounds, const int* d_m0, const int* d_m1, int* dims, int* d_ncells,
-                          long long cell_cap, int* err) {
+__device__ void grid_dims(const int* bounds, const int* npts, int* dims, int* d_ncells, long long cell_cap, int* err) {
     long long base = 0;
-    for (int mi = 0; mi < 2; ++mi) {
-        const int n = mi == 0 ? *d_m0 : (d_m1 ? *d_m1 : 0);
+    for (int mi = 0; mi < kGridMaps; ++mi) {
+        const int n = npts[mi];
         int* dm = dims + 8 * mi;
         if (n <= 0) {
             for (int k = 0; k < 8; ++k) dm[k] = 0;
@@ -47,38 +46,60 @@ __device__ void grid_dims(const int* bounds, const int* d_m0, const int* d_m1, i
     *d_ncells = (int)(base + 1);
 }
 
+// the concatenation of the maps: point i belongs to map mi at local index li
+struct GridIdx {
+    int end[kGridMaps];
+    int total;
+    __device__ __forceinline__ int map_of(int i) const { return i < end[0] ? 0 : (i < end[1] ? 1 : 2); }
+    __device__ __forceinline__ int start(int mi) const { return mi == 0 ? 0 : end[mi - 1]; }
+};
+__device__ __forceinline__ GridIdx grid_idx(const GridPtrs& gp) {
+    GridIdx g;
+    int acc = 0;
+#pragma unroll
+    for (int k = 0; k < kGridMaps; ++k) {
+        acc += k < gp.nm ? *gp.n[k] : 0;
+        g.end[k] = acc;
+    }
+    g.total = acc;
+    return g;
+}
+
 // per-map min/max cell coordinates: wave then workgroup reduction, one atomic per workgroup. The
 // last workgroup to arrive derives the grid dimensions and resets the bounds for the next build.
-__global__ void __launch_bounds__(256) k_grid_bounds(const float4* __restrict__ m0, const int* __restrict__ d_m0,
-                                                      const float4* __restrict__ m1, const int* __restrict__ d_m1,
-                                                      int* __restrict__ bounds, u32* __restrict__ arrive,
+__global__ void __launch_bounds__(256) k_grid_bounds(GridPtrs gp, int* __restrict__ bounds, u32* __restrict__ arrive,
                                                       int* __restrict__ dims, int* __restrict__ d_ncells,
                                                       long long cell_cap, int* __restrict__ err) {
-    __shared__ int red[4][12];
+    constexpr int NB = 6 * kGridMaps;
+    __shared__ int red[4][NB];
     __shared__ int last;
-    __shared__ int lb[12];
-    const int n0 = *d_m0, n1 = m1 ? *d_m1 : 0;
+    __shared__ int lb[NB];
+    const GridIdx gi = grid_idx(gp);
     const int l = lane_id(), w = threadIdx.x >> 6;
-    int v[12];
+    int v[NB];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) v[k] = ((k % 6) < 3) ? INT_MAX : INT_MIN;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
-        const int mi = i < n0 ? 0 : 1;
-        const float4 p = mi == 0 ? m0[i] : m1[i - n0];
+    for (int k = 0; k < NB; ++k) v[k] = ((k % 6) < 3) ? INT_MAX : INT_MIN;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < gi.total; i += gridDim.x * blockDim.x) {
+        const int mi = gi.map_of(i);
+        const float4 p = gp.m[mi][i - gi.start(mi)];
         const int c[3] = {(int)floorf(p.x), (int)floorf(p.y), (int)floorf(p.z)};
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            if (mi == 0) { v[k] = min(v[k], c[k]); v[3 + k] = max(v[3 + k], c[k]); }
-            else { v[6 + k] = min(v[6 + k], c[k]); v[9 + k] = max(v[9 + k], c[k]); }
+        for (int mm = 0; mm < kGridMaps; ++mm) {
+            if (mm != mi) continue;                   // static register indices
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                v[6 * mm + k] = min(v[6 * mm + k], c[k]);
+                v[6 * mm + 3 + k] = max(v[6 * mm + 3 + k], c[k]);
+            }
         }
     }
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
+    for (int k = 0; k < NB; ++k) {
         const int r = ((k % 6) < 3) ? wave_min_i(v[k]) : wave_max_i(v[k]);
         if (l == 0) red[w][k] = r;
     }
     __syncthreads();
-    if (threadIdx.x < 12) {
+    if (threadIdx.x < NB) {
         const int k = threadIdx.x;
         const bool is_min = (k % 6) < 3;
         int r = red[0][k];
@@ -92,14 +113,16 @@ __global__ void __launch_bounds__(256) k_grid_bounds(const float4* __restrict__ 
         last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     __syncthreads();
     if (!last) return;
-    if (threadIdx.x < 12) {
+    if (threadIdx.x < NB) {
         const int k = threadIdx.x;
         lb[k] = __hip_atomic_load(&bounds[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&bounds[k], ((k % 6) < 3) ? INT_MAX : INT_MIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        grid_dims(lb, d_m0, d_m1, dims, d_ncells, cell_cap, err);
+        int nloc[kGridMaps];
+        for (int k = 0; k < kGridMaps; ++k) nloc[k] = gi.end[k] - (k ? gi.end[k - 1] : 0);
+        grid_dims(lb, nloc, dims, d_ncells, cell_cap, err);
         __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -109,32 +132,28 @@ __device__ __forceinline__ int cell_of(const int* dm, float4 p) {
     return dm[6] + (z * dm[4] + y) * dm[3] + x;
 }
 
-__global__ void __launch_bounds__(256) k_grid_count(const float4* __restrict__ m0, const int* __restrict__ d_m0,
-                                                     const float4* __restrict__ m1, const int* __restrict__ d_m1,
-                                                     const int* __restrict__ dims, u32* __restrict__ cnt,
+__global__ void __launch_bounds__(256) k_grid_count(GridPtrs gp, const int* __restrict__ dims, u32* __restrict__ cnt,
                                                      u32* __restrict__ slot) {
-    const int n0 = *d_m0, n1 = m1 ? *d_m1 : 0;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
-        const int mi = i < n0 ? 0 : 1;
+    const GridIdx gi = grid_idx(gp);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < gi.total; i += gridDim.x * blockDim.x) {
+        const int mi = gi.map_of(i);
         const int* dm = dims + 8 * mi;
         if (!dm[7]) continue;
-        const float4 p = mi == 0 ? m0[i] : m1[i - n0];
+        const float4 p = gp.m[mi][i - gi.start(mi)];
         slot[i] = atomicAdd(&cnt[cell_of(dm, p)], 1u);
     }
 }
 
-__global__ void __launch_bounds__(256) k_grid_scatter(const float4* __restrict__ m0, const int* __restrict__ d_m0,
-                                                       const float4* __restrict__ m1, const int* __restrict__ d_m1,
-                                                       const int* __restrict__ dims, const u32* __restrict__ start,
-                                                       const u32* __restrict__ slot, float4* __restrict__ cpts,
-                                                       u32* __restrict__ cnt) {
-    const int n0 = *d_m0, n1 = m1 ? *d_m1 : 0;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
-        const int mi = i < n0 ? 0 : 1;
+__global__ void __launch_bounds__(256) k_grid_scatter(GridPtrs gp, const int* __restrict__ dims,
+                                                       const u32* __restrict__ start, const u32* __restrict__ slot,
+                                                       float4* __restrict__ cpts, u32* __restrict__ cnt) {
+    const GridIdx gi = grid_idx(gp);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < gi.total; i += gridDim.x * blockDim.x) {
+        const int mi = gi.map_of(i);
         const int* dm = dims + 8 * mi;
         if (!dm[7]) continue;
-        const int li = mi == 0 ? i : i - n0;
-        const float4 p = mi == 0 ? m0[li] : m1[li];
+        const int li = i - gi.start(mi);
+        const float4 p = gp.m[mi][li];
         const int cid = cell_of(dm, p);
         cpts[start[cid] + slot[i]] = make_float4(p.x, p.y, p.z, __int_as_float(li));
         cnt[cid] = 0u;                        // leaves the count array zero for the next build
@@ -201,8 +220,8 @@ __global__ void __launch_bounds__(256) k_knn_cellpop(GridView gv, const float4* 
 int grid_alloc(GridGPU& g, size_t pts_cap, size_t cell_cap) {
     g.pts_cap = pts_cap;
     g.cell_cap = cell_cap;
-    if (hipMalloc(&g.bounds, sizeof(int) * 12) != hipSuccess) return PF_ENOMEM;
-    if (hipMalloc(&g.dims, sizeof(int) * 16) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&g.bounds, sizeof(int) * 6 * kGridMaps) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&g.dims, sizeof(int) * 8 * kGridMaps) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&g.d_ncells, sizeof(int)) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&g.err, sizeof(int)) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&g.cell_count, sizeof(u32) * (cell_cap + 1)) != hipSuccess) return PF_ENOMEM;
@@ -213,8 +232,8 @@ int grid_alloc(GridGPU& g, size_t pts_cap, size_t cell_cap) {
     if (hipMemset(g.err, 0, sizeof(int)) != hipSuccess) return PF_EHIP;
     if (hipMemset(g.arrive, 0, sizeof(u32)) != hipSuccess) return PF_EHIP;
     if (hipMemset(g.cell_count, 0, sizeof(u32) * (cell_cap + 1)) != hipSuccess) return PF_EHIP;
-    const int init[12] = {INT_MAX, INT_MAX, INT_MAX, INT_MIN, INT_MIN, INT_MIN,
-                          INT_MAX, INT_MAX, INT_MAX, INT_MIN, INT_MIN, INT_MIN};
+    int init[6 * kGridMaps];
+    for (int k = 0; k < 6 * kGridMaps; ++k) init[k] = (k % 6) < 3 ? INT_MAX : INT_MIN;
     if (hipMemcpy(g.bounds, init, sizeof(init), hipMemcpyHostToDevice) != hipSuccess) return PF_EHIP;
     return PF_OK;
 }
@@ -232,15 +251,14 @@ void grid_free(GridGPU& g) {
     g = GridGPU{};
 }
 
-void grid_build(GridGPU& g, const float4* map0, const int* d_m0, const float4* map1, const int* d_m1, PrimWork& w,
-                hipStream_t s) {
+void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s) {
     const int nb = 512;
-    hipLaunchKernelGGL(k_grid_bounds, dim3(64), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.bounds, g.arrive, g.dims,
-                       g.d_ncells, (long long)g.cell_cap, g.err);
-    hipLaunchKernelGGL(k_grid_count, dim3(nb), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.dims, g.cell_count, g.slot);
+    hipLaunchKernelGGL(k_grid_bounds, dim3(64), dim3(256), 0, s, gp, g.bounds, g.arrive, g.dims, g.d_ncells,
+                       (long long)g.cell_cap, g.err);
+    hipLaunchKernelGGL(k_grid_count, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot);
     scan_exclusive(g.cell_count, g.cell_start, g.d_ncells, nullptr, w, s);
-    hipLaunchKernelGGL(k_grid_scatter, dim3(nb), dim3(256), 0, s, map0, d_m0, map1, d_m1, g.dims, g.cell_start,
-                       g.slot, g.cpts, g.cell_count);
+    hipLaunchKernelGGL(k_grid_scatter, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_start, g.slot, g.cpts,
+                       g.cell_count);
 }
 
 }  // namespace pf
@@ -332,7 +350,7 @@ int pf_knn_set_map(pf_knn* h, const float* xyz4, size_t m) {
     const int mm[2] = {(int)m, 0};
     if (m) PF_HIP_TRY(hipMemcpyAsync(h->d_map, xyz4, sizeof(float4) * m, hipMemcpyHostToDevice, h->stream));
     PF_HIP_TRY(hipMemcpyAsync(h->d_m, mm, sizeof(mm), hipMemcpyHostToDevice, h->stream));
-    grid_build(h->grid, h->d_map, h->d_m, nullptr, nullptr, h->prim, h->stream);
+    grid_build(h->grid, GridPtrs{{h->d_map, nullptr, nullptr}, {h->d_m, nullptr, nullptr}, 1}, h->prim, h->stream);
     int err = 0;
     PF_HIP_TRY(hipMemcpyAsync(&err, h->grid.err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     PF_HIP_TRY(hipStreamSynchronize(h->stream));

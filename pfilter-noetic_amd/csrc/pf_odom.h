@@ -1,4 +1,5 @@
-// Device-resident Odom_ES_EstimationClass (src/odomEstimationClass.cpp:182-647).
+// Device-resident Odom_ES_EstimationClass (src/odomEstimationClass.cpp:182-647) and
+// Odom_BPF_EstimationClass (:649-1306): one pipeline over 2 or 3 map classes.
 #pragma once
 #include "pf_common.h"
 #include "pf_fe.h"
@@ -7,19 +8,44 @@
 
 namespace pf {
 
-// device counter slots (int32, one array per handle)
+// Map classes. One class = one input cloud, its VoxelGrid leaf, its local map and its residual type.
+//   ES  (Odom_ES_EstimationClass):  0 corner (line, leaf r), 1 surf (plane, leaf 2r)
+//   BPF (Odom_BPF_EstimationClass): 0 beam (line, r), 1 pillar (line, r), 2 facade (plane, 2r)
+// Queries, residuals and maps are concatenated in class order, the reference's factor order.
+constexpr int kMaxC = 3;
+
+// device counter slots (int32, one array per handle); per-class slots are kMaxC consecutive ints
 enum CounterSlot {
-    C_EIN = 0, C_SIN, C_VGN, C_EDS, C_SDS, C_NQ, C_ME, C_MS, C_NPAIR, C_NRG, C_NSEG, C_NSEG_E, C_NRG_VALID,
-    C_KEEP_TOTAL, C_EDGE_KEPT, C_SURF_KEPT, C_EDGE_VALID, C_SURF_VALID, C_LM_ITERS, C_GATE, C_ERR,
-    C_OUTER, C_PAD0, C_PAD1, C_NIN, C_FE_ERR, C_COUNT
+    C_NIN = 0,                  // raw scan points (featureExtraction input)
+    C_IN = 1,                   // [kMaxC] class input clouds (featureExtraction output / caller's clouds)
+    C_VGN = C_IN + kMaxC,       // VoxelGrid batch size
+    C_DS,                       // [kMaxC] down-sampled clouds (queries of each class)
+    C_NQ = C_DS + kMaxC,        // all queries
+    C_M,                        // [kMaxC] map sizes
+    C_NPAIR = C_M + kMaxC,
+    C_NRG, C_NSEG,
+    C_NLT,                      // [3] segments of classes < 1, < 2, < 3 (segment_starts)
+    C_NRG_VALID = C_NLT + 3,
+    C_KEEP_TOTAL,
+    C_KEPT,                     // [kMaxC] residual blocks kept (last outer iteration)
+    C_VALID = C_KEPT + kMaxC,   // [kMaxC] gated + fitted associations
+    C_LM_ITERS = C_VALID + kMaxC,
+    C_GATE, C_ERR, C_OUTER, C_FE_ERR, C_COUNT
 };
 
 // ordered-uint accumulator slots (float min/max via atomics)
 enum AccSlot {
-    A_VG = 0,        // [cloud][6]: min xyz, max xyz  (12)
-    A_RG = 12,       // [cloud][6]                     (12)
-    A_W = 24,        // [class][4]: obs min, obs max, spars min, spars max (8)
-    A_COUNT = 32
+    A_VG = 0,                   // [class][6]: min xyz, max xyz
+    A_RG = 6 * kMaxC,           // [class][6]
+    A_W = 12 * kMaxC,           // [class][4]: obs min, obs max, spars min, spars max
+    A_COUNT = 16 * kMaxC
+};
+
+// the class table every kernel sees: count and which classes are planes (bit c)
+struct ClassCfg {
+    int nc;
+    u32 plane;
+    __host__ __device__ __forceinline__ bool is_plane(int c) const { return (plane >> c) & 1u; }
 };
 
 struct DevState {
@@ -38,7 +64,7 @@ struct LMState {
     double cost, H[21], g[6];
     double D[6];
     double radius, decrease, x_norm, min_cost, mcc;
-    double wmin[2][2], wmax[2][2];   // [class][observe, sparsity]
+    double wmin[kMaxC][2], wmax[kMaxC][2];   // [class][observe, sparsity]
     int iteration, invalid, reuse, done, phase, n_res, pad0, pad1;
 };
 
@@ -48,9 +74,9 @@ constexpr int kLmParts = 30;   // cost, g[6], H[21], bad_r, bad_J
 // the counters of that stage. Stage A (stream_a: featureExtraction + VoxelGrid, pose independent)
 // fills slot k % 2 while stage B (stream: the odometry) still works on frame k - 1 in the other slot.
 struct StageBuf {
-    float4 *in_edge = nullptr, *in_surf = nullptr;   // featureExtraction output
-    float4 *ds_edge = nullptr, *ds_surf = nullptr;   // VoxelGrid output (r, g written by the odometry)
-    int* cnt = nullptr;                              // [C_COUNT] stage counters
+    float4* in[kMaxC] = {};      // class inputs (featureExtraction output or the caller's clouds)
+    float4* ds[kMaxC] = {};      // VoxelGrid output (r, g written by the odometry)
+    int* cnt = nullptr;          // [C_COUNT] stage counters
 };
 
 // pipeline slots: frame k's stage A output lives in slot k % kSlots, so stage A may run up to
@@ -67,8 +93,9 @@ struct OdomGPU {
     int opt_count_host = 2;
     bool inited = false;
     int frames = 0;
-    float leaf_vg[2] = {0, 0};     // downSizeFilterEdge/Surf leaf (double -> float)
-    float leaf_rg[2] = {0, 0};     // rgbds leaves: map_resolution, map_resolution * 2 (float)
+    ClassCfg cls{2, 2u};
+    float leaf_vg[kMaxC] = {};     // downSizeFilter leaves (double -> float)
+    float leaf_rg[kMaxC] = {};     // rgbds leaves: map_resolution, map_resolution * 2 (float)
 
     FeGPU fe;
     GridGPU grid;
@@ -89,35 +116,36 @@ struct OdomGPU {
     hipEvent_t ev_b[kSlots] = {};                           // stage B done with slot p
     hipGraphExec_t graph_a[kSlots] = {};                    // steady-state replay per slot
     hipGraphExec_t graph_b[kSlots] = {};
-    float4 *map_e = nullptr, *map_s = nullptr;
-    float4 *app_e = nullptr, *app_s = nullptr;
+    float4* map[kMaxC] = {};       // local maps
+    float4* app[kMaxC] = {};       // this frame's transformed down-sampled points (appended)
     float4* seg_out = nullptr;
     u32 *keys = nullptr, *vals = nullptr, *flags = nullptr, *scan_out = nullptr, *segstart = nullptr;
 
-    int* nbr = nullptr;            // [5 * 2 * in_cap]
+    int* nbr = nullptr;            // [5 * kMaxC * in_cap]
     int* qflag = nullptr;          // bit0 valid association, bit1 kept
-    double* geo = nullptr;         // [8 * 2 * in_cap]
+    double* geo = nullptr;         // [8 * kMaxC * in_cap]
     float* spars = nullptr;
     float* roundv = nullptr;
     float* observe = nullptr;
-    int* pnext = nullptr;          // [5 * 2 * in_cap] p-index lists: next pair sharing the map point
-    int4* pbkt = nullptr;          // [2 * map_cap] p-index buckets {count, pair, pair, overflow head}
-    u32* tailinc = nullptr;        // [5 * 2 * in_cap] increments of a map point, on its last pair
+    int* pnext = nullptr;          // [5 * kMaxC * in_cap] p-index lists: next pair sharing the map point
+    int4* pbkt = nullptr;          // [nc * map_cap] p-index buckets {count, pair, pair, overflow head}
+    u32* tailinc = nullptr;        // [5 * kMaxC * in_cap] increments of a map point, on its last pair
     double* lm_part = nullptr;     // [kLmBlocks * 32] per-block LM partials
     u32* lm_ticket = nullptr;      // LM arrival counter
     unsigned long long* dbg = nullptr;   // [64] device timestamps (development probe)
     double* poses = nullptr;       // [pose_cap * 7]
-    float4* stage = nullptr;       // [2 * in_cap] host staging target
+    float4* stage = nullptr;       // [kMaxC * in_cap] staging target of the frame entry points
 
     bool graph_enabled = true;
 };
 
+// nc = 2: the ES estimator; nc = 3: the BPF estimator (the last class is the plane class)
 int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& prm, int device, size_t in_cap,
-                size_t map_cap);
+                size_t map_cap, int nc = 2);
 void odom_destroy(OdomGPU& o);
-// stage A: featureExtraction of d_in[0 .. sb[p].cnt[C_NIN]) into slot p
+// stage A: featureExtraction of d_in[0 .. sb[p].cnt[C_NIN]) into slot p's classes 0 / 1 (ES)
 void stage_enqueue_fe(OdomGPU& o, int p, const float4* d_in, hipStream_t s);
-// stage A: VoxelGrid of slot p's features (counts sb[p].cnt[C_EIN], [C_SIN])
+// stage A: VoxelGrid of slot p's class clouds (counts sb[p].cnt[C_IN + c])
 void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s);
 // stage B: initMapWithPoints from slot p's features
 void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s);

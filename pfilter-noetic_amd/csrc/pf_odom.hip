@@ -28,6 +28,7 @@ namespace pf {
 namespace {
 
 constexpr u32 kSentinel = 0xFFFFFFFFu;
+struct VgLeaf { float v[kMaxC]; };     // per-class leaf sizes
 constexpr int kGrid = 512;   // grid-stride workgroups for per-point kernels
 
 __device__ __forceinline__ float wave_minf(float v) {
@@ -63,16 +64,77 @@ __device__ __forceinline__ float4 associate(const double* prm, float4 p) {
     return make_float4((float)w.x, (float)w.y, (float)w.z, p.w);
 }
 
+// per-class pointer sets passed by value (kernel arguments)
+struct Clouds { const float4* p[kMaxC]; };
+struct CloudsW { float4* p[kMaxC]; };
+
+// a concatenation of per-class ranges: element i belongs to class cls(i) at local index i - start(c)
+struct CatIdx {
+    int end[kMaxC];
+    __device__ __forceinline__ int total() const { return end[kMaxC - 1]; }
+    __device__ __forceinline__ int cls(int i) const { return i < end[0] ? 0 : (i < end[1] ? 1 : 2); }
+    __device__ __forceinline__ int start(int c) const { return c == 0 ? 0 : end[c - 1]; }
+};
+__device__ __forceinline__ CatIdx cat_idx(const int* counts, int nc) {
+    CatIdx x;
+    int acc = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxC; ++k) {
+        acc += k < nc ? counts[k] : 0;
+        x.end[k] = acc;
+    }
+    return x;
+}
+
+// per-class float min/max of xyz reduced over the workgroup, one atomic per value and workgroup;
+// v[6 c + k]: min (k < 3) / max (k >= 3) of class c
+__device__ __forceinline__ void minmax_commit(float (&v)[6 * kMaxC], u32* acc) {
+    __shared__ float red[4][6 * kMaxC];
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 6 * kMaxC; ++k) {
+        const float r = ((k % 6) < 3) ? wave_minf(v[k]) : wave_maxf(v[k]);
+        if (lane_id() == 0) red[w][k] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6 * kMaxC) {
+        const int k = threadIdx.x;
+        float r = red[0][k];
+        for (int ww = 1; ww < 4; ++ww) r = ((k % 6) < 3) ? fminf(r, red[ww][k]) : fmaxf(r, red[ww][k]);
+        const bool any = ((k % 6) < 3) ? (r != FLT_MAX) : (r != -FLT_MAX);
+        if (any) {
+            if ((k % 6) < 3) atomicMin(&acc[k], f2ord(r));
+            else atomicMax(&acc[k], f2ord(r));
+        }
+    }
+}
+__device__ __forceinline__ void minmax_add(float (&v)[6 * kMaxC], int c, float4 p) {
+    const float xyz[3] = {p.x, p.y, p.z};
+#pragma unroll
+    for (int cc = 0; cc < kMaxC; ++cc) {
+        if (cc != c) continue;                     // static register indices
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            v[6 * cc + k] = fminf(v[6 * cc + k], xyz[k]);
+            v[6 * cc + 3 + k] = fmaxf(v[6 * cc + 3 + k], xyz[k]);
+        }
+    }
+}
+__device__ __forceinline__ void minmax_init(float (&v)[6 * kMaxC]) {
+#pragma unroll
+    for (int k = 0; k < 6 * kMaxC; ++k) v[k] = ((k % 6) < 3) ? FLT_MAX : -FLT_MAX;
+}
+
 // ---------------------------------------------------------------------------------------------
 // copies the stage slots a frame's odometry reads from its pipeline slot's counters
 __device__ __forceinline__ void pull_stage_counts(int* cnt, const int* scnt) {
     cnt[C_NIN] = scnt[C_NIN];
-    cnt[C_EIN] = scnt[C_EIN];
-    cnt[C_SIN] = scnt[C_SIN];
     cnt[C_VGN] = scnt[C_VGN];
-    cnt[C_EDS] = scnt[C_EDS];
-    cnt[C_SDS] = scnt[C_SDS];
     cnt[C_NQ] = scnt[C_NQ];
+    for (int c = 0; c < kMaxC; ++c) {
+        cnt[C_IN + c] = scnt[C_IN + c];
+        cnt[C_DS + c] = scnt[C_DS + c];
+    }
 }
 
 __global__ void k_pull_counts(int* __restrict__ cnt, const int* __restrict__ scnt) {
@@ -80,8 +142,8 @@ __global__ void k_pull_counts(int* __restrict__ cnt, const int* __restrict__ scn
 }
 
 __global__ void k_predict(DevState* __restrict__ st, int* __restrict__ cnt, const int* __restrict__ scnt,
-                          u32* __restrict__ acc) {
-    if (threadIdx.x < 12) acc[A_RG + threadIdx.x] = ((threadIdx.x % 6) < 3) ? 0xFFFFFFFFu : 0u;  // map-update bounds
+                          u32* __restrict__ acc, ClassCfg cls) {
+    if (threadIdx.x < 6 * kMaxC) acc[A_RG + threadIdx.x] = ((threadIdx.x % 6) < 3) ? 0xFFFFFFFFu : 0u;  // map-update bounds
     if (threadIdx.x != 0) return;
     pull_stage_counts(cnt, scnt);
     if (st->optimization_count > 2) st->optimization_count--;                 // :232-233
@@ -93,69 +155,51 @@ __global__ void k_predict(DevState* __restrict__ st, int* __restrict__ cnt, cons
     const qd q = m2q(polar_rotation(pred.R));                                  // :239 (Eigen 3.3 rotation())
     st->params[0] = q.x; st->params[1] = q.y; st->params[2] = q.z; st->params[3] = q.w;
     st->params[4] = pred.t.x; st->params[5] = pred.t.y; st->params[6] = pred.t.z;
-    const int gate = (cnt[C_ME] > 10 && cnt[C_MS] > 50) ? 1 : 0;              // :247
+    int gate = 1;                                  // :247 / BPF :721: line maps > 10, plane maps > 50
+    for (int c = 0; c < cls.nc; ++c) gate &= cnt[C_M + c] > (cls.is_plane(c) ? 50 : 10) ? 1 : 0;
     st->gate = gate;
     cnt[C_GATE] = gate;
     cnt[C_OUTER] = gate ? st->optimization_count : 0;
     cnt[C_LM_ITERS] = 0;
-    cnt[C_EDGE_KEPT] = cnt[C_SURF_KEPT] = cnt[C_EDGE_VALID] = cnt[C_SURF_VALID] = 0;
+    for (int c = 0; c < kMaxC; ++c) cnt[C_KEPT + c] = cnt[C_VALID + c] = 0;
 }
 
 // voxel-grid stage set-up (stream A): reset the min/max accumulators, batch size
-__global__ void k_vg_begin(int* __restrict__ scnt, u32* __restrict__ acc) {
+__global__ void k_vg_begin(int* __restrict__ scnt, u32* __restrict__ acc, int nc) {
     const int t = threadIdx.x;
-    if (t < 12) acc[A_VG + t] = ((t % 6) < 3) ? 0xFFFFFFFFu : 0u;
-    if (t == 0) scnt[C_VGN] = scnt[C_EIN] + scnt[C_SIN];
+    if (t < 6 * kMaxC) acc[A_VG + t] = ((t % 6) < 3) ? 0xFFFFFFFFu : 0u;
+    if (t == 0) {
+        int n = 0;
+        for (int c = 0; c < nc; ++c) n += scnt[C_IN + c];
+        scnt[C_VGN] = n;
+    }
 }
 
 // ----------------------------------- VoxelGrid (B.1) ------------------------------------------
-__global__ void __launch_bounds__(256) k_vg_minmax(const float4* __restrict__ e, const float4* __restrict__ s,
-                                                    const int* __restrict__ cnt, u32* __restrict__ acc) {
-    __shared__ float red[4][12];
-    const int n0 = cnt[C_EIN], n1 = cnt[C_SIN];
-    float v[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) v[k] = ((k % 6) < 3) ? FLT_MAX : -FLT_MAX;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
-        const int c = i < n0 ? 0 : 1;
-        const float4 p = c == 0 ? e[i] : s[i - n0];
-        const float xyz[3] = {p.x, p.y, p.z};
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            if (c == 0) { v[k] = fminf(v[k], xyz[k]); v[3 + k] = fmaxf(v[3 + k], xyz[k]); }
-            else { v[6 + k] = fminf(v[6 + k], xyz[k]); v[9 + k] = fmaxf(v[9 + k], xyz[k]); }
-        }
+__global__ void __launch_bounds__(256) k_vg_minmax(Clouds in, const int* __restrict__ cnt, u32* __restrict__ acc,
+                                                    int nc) {
+    const CatIdx ci = cat_idx(cnt + C_IN, nc);
+    float v[6 * kMaxC];
+    minmax_init(v);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ci.total(); i += gridDim.x * blockDim.x) {
+        const int c = ci.cls(i);
+        minmax_add(v, c, in.p[c][i - ci.start(c)]);
     }
-    const int w = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const float r = ((k % 6) < 3) ? wave_minf(v[k]) : wave_maxf(v[k]);
-        if (lane_id() == 0) red[w][k] = r;
-    }
-    __syncthreads();
-    if (threadIdx.x < 12) {
-        const int k = threadIdx.x;
-        float r = red[0][k];
-        for (int ww = 1; ww < 4; ++ww) r = ((k % 6) < 3) ? fminf(r, red[ww][k]) : fmaxf(r, red[ww][k]);
-        const bool any = ((k % 6) < 3) ? (r != FLT_MAX) : (r != -FLT_MAX);
-        if (any) {
-            if ((k % 6) < 3) atomicMin(&acc[A_VG + k], f2ord(r));
-            else atomicMax(&acc[A_VG + k], f2ord(r));
-        }
-    }
+    minmax_commit(v, acc + A_VG);
 }
 
-__global__ void __launch_bounds__(256) k_vg_keys(const float4* __restrict__ e, const float4* __restrict__ s,
-                                                  const int* __restrict__ cnt, const u32* __restrict__ acc,
-                                                  float leaf0, float leaf1, u32* __restrict__ keys,
-                                                  u32* __restrict__ vals, SortHist sh) {
+// keys: class in bits 30-31, the voxel index below (sorted by class, then voxel)
+__global__ void __launch_bounds__(256) k_vg_keys(Clouds in, const int* __restrict__ cnt, const u32* __restrict__ acc,
+                                                  int nc, VgLeaf leaf, u32* __restrict__ keys, u32* __restrict__ vals,
+                                                  SortHist sh) {
     __shared__ u32 lh[4][256];
     sort_hist_begin(lh);
-    const int n0 = cnt[C_EIN], n1 = cnt[C_SIN];
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
-        const int c = i < n0 ? 0 : 1;
-        const float4 p = c == 0 ? e[i] : s[i - n0];
-        const float inv = 1.0f / (c == 0 ? leaf0 : leaf1);     // inverse_leaf_size_
+    const CatIdx ci = cat_idx(cnt + C_IN, nc);
+    const int n = ci.total();
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int c = ci.cls(i);
+        const float4 p = in.p[c][i - ci.start(c)];
+        const float inv = 1.0f / leaf.v[c];                      // inverse_leaf_size_
         const u32* a = acc + A_VG + 6 * c;
         const float mn[3] = {ord2f(a[0]), ord2f(a[1]), ord2f(a[2])};
         const float mx[3] = {ord2f(a[3]), ord2f(a[4]), ord2f(a[5])};
@@ -164,7 +208,7 @@ __global__ void __launch_bounds__(256) k_vg_keys(const float4* __restrict__ e, c
         const long long dz = (long long)((mx[2] - mn[2]) * inv) + 1;
         u32 key;
         if (dx * dy * dz > (long long)INT_MAX) {
-            key = (u32)(i - (c == 0 ? 0 : n0));   // "leaf too small": output = input, order kept
+            key = (u32)(i - ci.start(c));        // "leaf too small": output = input, order kept
         } else {
             int minb[3], div[3];
             for (int k = 0; k < 3; ++k) {
@@ -176,54 +220,57 @@ __global__ void __launch_bounds__(256) k_vg_keys(const float4* __restrict__ e, c
             const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
             key = (u32)(i0 + i1 * div[0] + i2 * (div[0] * div[1]));
         }
-        keys[i] = key | ((u32)c << 31);
+        key = (key & 0x3fffffffu) | ((u32)c << 30);
+        keys[i] = key;
         vals[i] = (u32)i;
-        sort_hist_add(lh, key | ((u32)c << 31), sh.passes);
+        sort_hist_add(lh, key, sh.passes);
     }
-    sort_hist_end(lh, sh, n0 + n1, n0 + n1);
+    sort_hist_end(lh, sh, n, n);
 }
 
-// segment heads of a sorted key array; sentinel keys never start a segment
 // one wave per voxel: lanes gather 64 members at a time, the running f32 sums then take them in
 // sorted (stable) order through readlane, so the order of additions is PCL's sequential one
 __device__ __forceinline__ float lane_f(float v, int j) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
-__global__ void __launch_bounds__(256) k_vg_reduce(const float4* __restrict__ e, const float4* __restrict__ s,
-                                                    const u32* __restrict__ keys, const u32* __restrict__ vals,
-                                                    const u32* __restrict__ segstart, int* __restrict__ cnt,
-                                                    float4* __restrict__ ds_e, float4* __restrict__ ds_s) {
-    const int n0 = cnt[C_EIN];
+__global__ void __launch_bounds__(256) k_vg_reduce(Clouds in, const u32* __restrict__ keys, const u32* __restrict__ vals,
+                                                    const u32* __restrict__ segstart, int* __restrict__ cnt, int nc,
+                                                    CloudsW ds) {
+    const CatIdx ci = cat_idx(cnt + C_IN, nc);
     const int n = cnt[C_VGN];
-    const int nseg = cnt[C_NSEG], nse = cnt[C_NSEG_E];
+    const int nseg = cnt[C_NSEG];
+    const int nlt0 = cnt[C_NLT], nlt1 = cnt[C_NLT + 1];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        cnt[C_EDS] = nse;
-        cnt[C_SDS] = nseg - nse;
+        cnt[C_DS] = nlt0;
+        cnt[C_DS + 1] = nc > 1 ? nlt1 - nlt0 : 0;
+        cnt[C_DS + 2] = nc > 2 ? nseg - nlt1 : 0;
         cnt[C_NQ] = nseg;
     }
     const int l = lane_id();
     const int waves = gridDim.x * (blockDim.x >> 6);
     for (int sg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; sg < nseg; sg += waves) {
         const u32 b0 = segstart[sg], b1 = (sg + 1 < nseg) ? segstart[sg + 1] : (u32)n;
-        const int c = (int)(keys[b0] >> 31);
+        const int c = (int)(keys[b0] >> 30);
+        const float4* src = in.p[c];
+        const int s0 = ci.start(c);
         float sx = 0.f, sy = 0.f, sz = 0.f;
         for (u32 base = b0; base < b1; base += 8 * 64) {   // AccumulatorXYZ, sorted (stable) order
             u32 idx[8];                                     // up to 512 members in flight at once
             float4 p[8];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) idx[c] = base + c * 64 + l < b1 ? vals[base + c * 64 + l] : 0xFFFFFFFFu;
+            for (int u = 0; u < 8; ++u) idx[u] = base + u * 64 + l < b1 ? vals[base + u * 64 + l] : 0xFFFFFFFFu;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                p[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (idx[c] != 0xFFFFFFFFu) p[c] = (int)idx[c] < n0 ? e[idx[c]] : s[idx[c] - n0];
+            for (int u = 0; u < 8; ++u) {
+                p[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (idx[u] != 0xFFFFFFFFu) p[u] = src[(int)idx[u] - s0];
             }
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const int m = (int)min(64, (int)(b1 - base) - c * 64);
+            for (int u = 0; u < 8; ++u) {
+                const int m = (int)min(64, (int)(b1 - base) - u * 64);
                 for (int j = 0; j < m; ++j) {
-                    sx += lane_f(p[c].x, j);
-                    sy += lane_f(p[c].y, j);
-                    sz += lane_f(p[c].z, j);
+                    sx += lane_f(p[u].x, j);
+                    sy += lane_f(p[u].y, j);
+                    sz += lane_f(p[u].z, j);
                 }
             }
         }
@@ -231,8 +278,7 @@ __global__ void __launch_bounds__(256) k_vg_reduce(const float4* __restrict__ e,
             const float nn = (float)(b1 - b0);
             // rgb of inputs is 0 (copyPointCloud XYZI -> XYZRGB): averages stay 0
             const float4 o = make_float4(sx / nn, sy / nn, sz / nn, __uint_as_float(0u));
-            if (c == 0) ds_e[sg] = o;
-            else ds_s[sg - nse] = o;
+            ds.p[c][sg - (c == 0 ? 0 : (c == 1 ? nlt0 : nlt1))] = o;
         }
     }
 }
@@ -243,16 +289,15 @@ struct AssocArgs {
     int* cnt;
     u32* acc;
     GridView gv;
-    const float4* ds_e;
-    const float4* ds_s;
-    const float4* map_e;
-    const float4* map_s;
+    ClassCfg cls;
+    Clouds ds;
+    Clouds map;
     int* nbr;
     int* qflag;
     double* geo;
     float* spars;
     float* roundv;
-    int4* pbkt;            // p-index buckets (one per map point, surf points offset by map_cap)
+    int4* pbkt;            // p-index buckets (one per map point, class c's at c * map_cap)
     int* pnext;
     u32 map_cap;
     u32* lm_arrive;
@@ -261,7 +306,7 @@ struct AssocArgs {
 // line fit (:302-331) / plane fit (:449-476), round and sparsity, p-index pair keys of query q
 __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, const int* id, int found) {
     bool valid = false;
-    const float4* mp = c == 0 ? a.map_e : a.map_s;
+    const float4* mp = a.map.p[c];
     if (found == 5) {
         double px[5], py[5], pz[5];
         u32 rsum = 0;
@@ -272,7 +317,7 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
             rsum += w_r(m);
         }
         double* G = a.geo + 8 * (size_t)q;
-        if (c == 0) {                                            // :302-331
+        if (!a.cls.is_plane(c)) {                                // :302-331 (BPF beam / pillar :775-804)
             d3 center{0, 0, 0};
             for (int j = 0; j < 5; ++j) center = add3(center, d3{px[j], py[j], pz[j]});
             center = d3{center.x / 5.0, center.y / 5.0, center.z / 5.0};
@@ -290,7 +335,7 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
                 G[0] = 0.1 * dir.x + center.x; G[1] = 0.1 * dir.y + center.y; G[2] = 0.1 * dir.z + center.z;
                 G[3] = -0.1 * dir.x + center.x; G[4] = -0.1 * dir.y + center.y; G[5] = -0.1 * dir.z + center.z;
             }
-        } else {                                                 // :449-476
+        } else {                                                 // :449-476 (BPF facade :1070-1104)
             double A[5][3];
             for (int j = 0; j < 5; ++j) { A[j][0] = px[j]; A[j][1] = py[j]; A[j][2] = pz[j]; }
             d3 n = plane5(A);
@@ -321,7 +366,7 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
     }
     a.qflag[q] = valid ? 1 : 0;
     if (valid) {               // p-index: push the 5 pairs onto their map points' lists (:345-346, :493-496)
-        const u32 off = c == 0 ? 0u : a.map_cap;
+        const u32 off = (u32)c * a.map_cap;
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
             int4* b = a.pbkt + off + (u32)id[j];
@@ -342,14 +387,15 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
 constexpr int kAssocTeam = PF_ASSOC_TEAM;
 static_assert(kAssocTeam >= 5, "k_assoc writes the 5 neighbours from 5 lanes of the team");
 __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
-    const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
+    const CatIdx qi = cat_idx(a.cnt + C_DS, a.cls.nc);
+    const int nq = a.cnt[C_NQ];
     const int gate = a.st->gate;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         *a.lm_arrive = 0u;                                     // LM arrival counter of this iteration
         a.cnt[C_NPAIR] = gate ? 5 * nq : 0;
-        a.cnt[C_EDGE_KEPT] = a.cnt[C_SURF_KEPT] = a.cnt[C_EDGE_VALID] = a.cnt[C_SURF_VALID] = 0;
+        for (int c = 0; c < kMaxC; ++c) a.cnt[C_KEPT + c] = a.cnt[C_VALID + c] = 0;
     }
-    if (blockIdx.x == 0 && threadIdx.x < 8) a.acc[A_W + threadIdx.x] = (threadIdx.x & 1) ? 0u : 0xFFFFFFFFu;
+    if (blockIdx.x == 0 && threadIdx.x < 4 * kMaxC) a.acc[A_W + threadIdx.x] = (threadIdx.x & 1) ? 0u : 0xFFFFFFFFu;
     if (!gate) {                                   // solve skipped: no association is valid
         for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) a.qflag[q] = 0;
         return;                                    // (no pairs: every block leaves before the prologue)
@@ -363,9 +409,9 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     for (int off = 0; wave_team0 + off < nq; off += teams) {     // trip count uniform per wave
         const int q0 = team + off;
         const bool active = q0 < nq;
-        const int c = q0 < ne ? 0 : 1;
+        const int c = active ? qi.cls(q0) : 0;
         float4 pw = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (active) pw = associate(prm, c == 0 ? a.ds_e[q0] : a.ds_s[q0 - ne]);
+        if (active) pw = associate(prm, a.ds.p[c][q0 - qi.start(c)]);
         float d[5];
         int id[5];
         const int found = knn5_team<kAssocTeam>(a.gv, c, pw.x, pw.y, pw.z, active, d, id);
@@ -383,10 +429,9 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
 struct ObsArgs {
     int* cnt;
     u32* acc;
-    const float4* map_e;
-    const float4* map_s;
-    float4* ds_e;
-    float4* ds_s;
+    ClassCfg cls;
+    Clouds map;
+    CloudsW ds;
     const int* nbr;
     int* qflag;
     const int4* pbkt;
@@ -396,16 +441,23 @@ struct ObsArgs {
     const float* roundv;
     const float* spars;
     float* observe;
-    int k_new;
+    int k_new;             // the edge and surf thresholds are equal (init :198-205, BPF :668-674)
     float theta_p;
     int theta_max;
 };
 
 __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
-    const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
+    const CatIdx qi = cat_idx(a.cnt + C_DS, a.cls.nc);
+    const int nq = a.cnt[C_NQ];
     const int t = threadIdx.x;
-    float mn[2][2] = {{FLT_MAX, FLT_MAX}, {FLT_MAX, FLT_MAX}}, mx[2][2] = {{-FLT_MAX, -FLT_MAX}, {-FLT_MAX, -FLT_MAX}};
-    int nvalid[2] = {0, 0}, nkept[2] = {0, 0};
+    float mn[kMaxC][2], mx[kMaxC][2];
+    int nvalid[kMaxC], nkept[kMaxC];
+#pragma unroll
+    for (int c = 0; c < kMaxC; ++c) {
+        mn[c][0] = mn[c][1] = FLT_MAX;
+        mx[c][0] = mx[c][1] = -FLT_MAX;
+        nvalid[c] = nkept[c] = 0;
+    }
     for (int q = blockIdx.x * blockDim.x + t; q < nq; q += gridDim.x * blockDim.x) {
         int f = a.qflag[q];
         if (!(f & 1)) {
@@ -413,8 +465,8 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
             for (int j = 0; j < 5; ++j) a.tailinc[5 * q + j] = 0u;
             continue;
         }
-        const int c = q < ne ? 0 : 1;
-        const float4* mp = c == 0 ? a.map_e : a.map_s;
+        const int c = qi.cls(q);
+        const float4* mp = a.map.p[c];
         // c_i(n) = valid queries before q sharing neighbour n: count the smaller pair ids in n's bucket
         // (filled in any order by k_assoc: two pairs inline, the rest on an overflow list); the pair
         // with the largest id carries n's increment
@@ -423,7 +475,7 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
         for (int j = 0; j < 5; ++j) nb[j] = a.nbr[5 * q + j];
         int4 bk[5];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) bk[j] = a.pbkt[(c == 0 ? 0u : a.map_cap) + (u32)nb[j]];
+        for (int j = 0; j < 5; ++j) bk[j] = a.pbkt[(u32)c * a.map_cap + (u32)nb[j]];
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
             const int p = 5 * q + j;
@@ -452,55 +504,61 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
         }
         float observe = gs / 5.0 + 1;                        // :332-338 / :480-486
         const float round = a.roundv[q];
-        if (c == 0) ++nvalid[0]; else ++nvalid[1];           // static indices (registers, not scratch)
         if (observe / round > 5) observe = 255;              // :348-349
-        if (observe < round * a.theta_p && round > a.k_new && observe < a.theta_max) continue;   // :350-353
-        if (c == 0) ++nkept[0]; else ++nkept[1];
-        a.qflag[q] = f | 2;
-        a.observe[q] = observe;
-        const u32 rq = (u32)min(255, int(round)), gq = (u32)min(255, int(observe));   // :354-355
-        if (c == 0) a.ds_e[q].w = __uint_as_float(pack_rg(rq, gq));
-        else a.ds_s[q - ne].w = __uint_as_float(pack_rg(rq, gq));
+        const bool skip = observe < round * a.theta_p && round > a.k_new && observe < a.theta_max;   // :350-353
+        if (!skip) {
+            a.qflag[q] = f | 2;
+            a.observe[q] = observe;
+            const u32 rq = (u32)min(255, int(round)), gq = (u32)min(255, int(observe));   // :354-355
+            a.ds.p[c][q - qi.start(c)].w = __uint_as_float(pack_rg(rq, gq));
+        }
         const float sp = a.spars[q];
 #pragma unroll
-        for (int cc = 0; cc < 2; ++cc) {
+        for (int cc = 0; cc < kMaxC; ++cc) {                  // static indices (registers, not scratch)
             if (cc != c) continue;
+            ++nvalid[cc];
+            if (skip) continue;
+            ++nkept[cc];
             mn[cc][0] = fminf(mn[cc][0], observe); mx[cc][0] = fmaxf(mx[cc][0], observe);
             mn[cc][1] = fminf(mn[cc][1], sp); mx[cc][1] = fmaxf(mx[cc][1], sp);
         }
     }
-    // workgroup totals, then one atomic per statistic and workgroup (not per wave)
-    __shared__ u32 wred[4][12];
+    // workgroup totals, then one atomic per statistic and workgroup (not per wave):
+    // v[2 c] valid, v[2 c + 1] kept, v[2 kMaxC + 4 c + 2 ww (+ 1)] min (max) of observe / sparsity
+    constexpr int NV = 6 * kMaxC;
+    __shared__ u32 wred[4][NV];
     const int w = t >> 6;
-    u32 v[12];
+    u32 v[NV];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        v[c] = (u32)wave_sum_i(nvalid[c]);
-        v[2 + c] = (u32)wave_sum_i(nkept[c]);
+    for (int c = 0; c < kMaxC; ++c) {
+        v[2 * c] = (u32)wave_sum_i(nvalid[c]);
+        v[2 * c + 1] = (u32)wave_sum_i(nkept[c]);
 #pragma unroll
         for (int ww = 0; ww < 2; ++ww) {
-            v[4 + 4 * c + 2 * ww] = f2ord(wave_minf(mn[c][ww]));
-            v[5 + 4 * c + 2 * ww] = f2ord(wave_maxf(mx[c][ww]));
+            v[2 * kMaxC + 4 * c + 2 * ww] = f2ord(wave_minf(mn[c][ww]));
+            v[2 * kMaxC + 4 * c + 2 * ww + 1] = f2ord(wave_maxf(mx[c][ww]));
         }
     }
     if (lane_id() == 0)
 #pragma unroll
-        for (int k = 0; k < 12; ++k) wred[w][k] = v[k];
+        for (int k = 0; k < NV; ++k) wred[w][k] = v[k];
     __syncthreads();
-    if (t < 12) {
+    if (t < NV) {
+        const bool count = t < 2 * kMaxC;
+        const int ws = t - 2 * kMaxC;                 // A_W offset of a statistic
         u32 r = wred[0][t];
         for (int ww = 1; ww < 4; ++ww) {
             const u32 o = wred[ww][t];
-            if (t < 4) r += o;
-            else r = ((t - 4) & 1) ? max(r, o) : min(r, o);
+            if (count) r += o;
+            else r = (ws & 1) ? max(r, o) : min(r, o);
         }
-        if (t < 4) {
-            const int slot = t == 0 ? C_EDGE_VALID : t == 1 ? C_SURF_VALID : t == 2 ? C_EDGE_KEPT : C_SURF_KEPT;
+        if (count) {
+            const int slot = (t & 1) ? C_KEPT + t / 2 : C_VALID + t / 2;
             if (r) atomicAdd(&a.cnt[slot], (int)r);
-        } else if (t & 1) {                                            // A_W + 4 c + 2 ww + 1: max
-            if (r != f2ord(-FLT_MAX)) atomicMax(&a.acc[A_W + t - 4], r);
+        } else if (ws & 1) {                                           // A_W + 4 c + 2 ww + 1: max
+            if (r != f2ord(-FLT_MAX)) atomicMax(&a.acc[A_W + ws], r);
         } else if (r != f2ord(FLT_MAX)) {                              // A_W + 4 c + 2 ww: min
-            atomicMin(&a.acc[A_W + t - 4], r);
+            atomicMin(&a.acc[A_W + ws], r);
         }
     }
 }
@@ -508,18 +566,18 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
 // the p-index increments of an outer iteration: g = min(255, g + 1) once per valid query sharing the
 // map point (:345-346, :493-496), applied by the last pair of each map point's list, which also
 // empties the list for the next iteration
-__device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, int n, int ne, float4* map_e,
-                                           float4* map_s, int4* pbkt, u32 map_cap) {
+__device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, int n, const CatIdx& qi, CloudsW map,
+                                           int4* pbkt, u32 map_cap) {
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const u32 inc = tailinc[p];
         if (!inc) continue;
-        const bool surf = p / 5 >= ne;
-        float4* mp = surf ? map_s : map_e;
+        const int c = qi.cls(p / 5);
+        float4* mp = map.p[c];
         const int idx = nbr[p];
         const float4 m = mp[idx];
         const u32 g = min(255u, w_g(m) + inc);
         mp[idx].w = __uint_as_float(pack_rg(w_r(m), g));
-        pbkt[(surf ? map_cap : 0u) + (u32)idx] = make_int4(0, -1, -1, -1);   // empty bucket
+        pbkt[(u32)c * map_cap + (u32)idx] = make_int4(0, -1, -1, -1);   // empty bucket
     }
 }
 
@@ -797,12 +855,12 @@ struct LmArgs {
     DevState* st;
     int* cnt;
     const u32* acc;
+    ClassCfg cls;
     LMState* lm_out;
     double* part;          // [kLmEvals][kLmBlocks][32]
     u32* arrive;           // arrival counter, zeroed by k_assoc
     const int* qflag;
-    const float4* ds_e;
-    const float4* ds_s;
+    Clouds ds;
     const double* geo;
     const float* observe;
     const float* spars;
@@ -811,8 +869,7 @@ struct LmArgs {
     const int* nbr;        // p-index increments, applied by the LM blocks before the solve
     const u32* tailinc;
     int4* pbkt;
-    float4* map_e;
-    float4* map_s;
+    CloudsW map;
     u32 map_cap;
 };
 
@@ -830,13 +887,15 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     const int t = threadIdx.x;
     // the map's p-index bytes are not read by the solve: this iteration's increments are applied
     // while the blocks wait for the first evaluation's arrivals (or here, when there is no solve)
-    const int nres = a.cnt[C_EDGE_KEPT] + a.cnt[C_SURF_KEPT];
+    const CatIdx qi = cat_idx(a.cnt + C_DS, a.cls.nc);
+    int nres = 0;
+    for (int c = 0; c < a.cls.nc; ++c) nres += a.cnt[C_KEPT + c];
     if (!a.st->gate || nres == 0) {                              // no residual blocks: untouched
-        pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], a.cnt[C_EDS], a.map_e, a.map_s, a.pbkt, a.map_cap);
+        pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
         return;
     }
-    double wmin[2][2], wmax[2][2];
-    for (int c = 0; c < 2; ++c)
+    double wmin[kMaxC][2], wmax[kMaxC][2];
+    for (int c = 0; c < kMaxC; ++c)
         for (int ww = 0; ww < 2; ++ww) {
             wmin[c][ww] = (double)ord2f(a.acc[A_W + 4 * c + 2 * ww]);
             wmax[c][ww] = (double)ord2f(a.acc[A_W + 4 * c + 2 * ww + 1]);
@@ -859,7 +918,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             for (int j = i; j < 6; ++j) { hi_[h] = (unsigned char)i; hj_[h] = (unsigned char)j; ++h; }
     }
     __syncthreads();
-    const int nq = a.cnt[C_NQ], ne = a.cnt[C_EDS];
+    const int nq = a.cnt[C_NQ];
     const int wt = a.weight_type;
     // reduction roles: thread (k, p) sums product k (0: cost, 1-6: g, 7-27: upper J^T J) over the
     // chunk rows p, p + 9, ...; 28 x 9 = 252 threads
@@ -875,8 +934,9 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             const int q = base + t;
             double J[6] = {0, 0, 0, 0, 0, 0}, r = 0.0, hc = 0.0;
             if (q < nq && (a.qflag[q] & 2)) {
-                const int c = q < ne ? 0 : 1;
-                const float4 p = c == 0 ? a.ds_e[q] : a.ds_s[q - ne];
+                const int c = qi.cls(q);
+                const bool plane = a.cls.is_plane(c);
+                const float4 p = a.ds.p[c][q - qi.start(c)];
                 const d3 cur{(double)p.x, (double)p.y, (double)p.z};
                 double wgt = 0.0;
                 if (wt != 0) {
@@ -884,11 +944,11 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
                     const double ws = norm_weight((double)a.spars[q], wmin[c][1], wmax[c][1], false);
                     if (wt == 1) wgt = wo;
                     else if (wt == 2) wgt = ws;
-                    else wgt = c == 0 ? (ws + wo) / 2 : (wo + ws) / 2;
+                    else wgt = plane ? (wo + ws) / 2 : (ws + wo) / 2;     // :418 / :565 operand order
                 }
                 const double* G = a.geo + 8 * (size_t)q;
-                r = c == 0 ? edge_eval(x, cur, d3{G[0], G[1], G[2]}, d3{G[3], G[4], G[5]}, wgt, J)
-                           : surf_eval(x, cur, d3{G[0], G[1], G[2]}, G[3], wgt, J);
+                r = plane ? surf_eval(x, cur, d3{G[0], G[1], G[2]}, G[3], wgt, J)
+                          : edge_eval(x, cur, d3{G[0], G[1], G[2]}, d3{G[3], G[4], G[5]}, wgt, J);
                 bool jbad = false;
                 for (int k = 0; k < 6; ++k) jbad |= !isfinite(J[k]);
                 if (!isfinite(r)) {
@@ -951,8 +1011,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (t == 0) __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (ev == 0)
-            pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], a.cnt[C_EDS], a.map_e, a.map_s, a.pbkt, a.map_cap);
+        if (ev == 0) pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
         {
             if (t == 0) {
                 const u32 target = (u32)(ev + 1) * gridDim.x;
@@ -1031,24 +1090,33 @@ __global__ void k_finalize(DevState* __restrict__ st, double* __restrict__ poses
     finalize_pose(st, poses, pose_cap, mode, acc, prm);
 }
 
+// the rgbds input of every class: its map, then its appended points (map c, app c, in class order)
 struct RgView {
-    const float4 *map_e, *app_e, *map_s, *app_s;
-    int me, ne, ms, ns;
-    __device__ __forceinline__ int total() const { return me + ne + ms + ns; }
+    const float4* src[2 * kMaxC];
+    int end[2 * kMaxC];
+    __device__ __forceinline__ int total() const { return end[2 * kMaxC - 1]; }
     __device__ __forceinline__ float4 at(int v, int& c) const {
-        if (v < me) { c = 0; return map_e[v]; }
-        v -= me;
-        if (v < ne) { c = 0; return app_e[v]; }
-        v -= ne;
-        if (v < ms) { c = 1; return map_s[v]; }
-        c = 1;
-        return app_s[v - ms];
+        int r = 0;
+#pragma unroll
+        for (int k = 0; k < 2 * kMaxC - 1; ++k) r += v >= end[k] ? 1 : 0;
+        c = r >> 1;
+        return src[r][v - (r ? end[r - 1] : 0)];
     }
 };
 
-__device__ __forceinline__ RgView rg_view(const int* cnt, const float4* map_e, const float4* app_e,
-                                          const float4* map_s, const float4* app_s) {
-    return RgView{map_e, app_e, map_s, app_s, cnt[C_ME], cnt[C_EDS], cnt[C_MS], cnt[C_SDS]};
+__device__ __forceinline__ RgView rg_view(const int* cnt, int nc, Clouds map, Clouds app) {
+    RgView V;
+    int acc = 0;
+#pragma unroll
+    for (int c = 0; c < kMaxC; ++c) {
+        V.src[2 * c] = map.p[c];
+        V.src[2 * c + 1] = app.p[c];
+        acc += c < nc ? cnt[C_M + c] : 0;
+        V.end[2 * c] = acc;
+        acc += c < nc ? cnt[C_DS + c] : 0;
+        V.end[2 * c + 1] = acc;
+    }
+    return V;
 }
 
 // CropBox bounds t +- 100 as float, inclusive (:606-615, B.2)
@@ -1059,70 +1127,47 @@ __device__ __forceinline__ bool in_crop(const DevState* st, float4 p) {
 }
 
 // addPointsToMap, first pass: the pose (:278-280, k_finalize mode 1, by thread 0 of block 0), the
-// transform / append of the down-sampled features (:592-604, r and g carried) and the CropBox-kept
-// min / max of both clouds for the rgbds grids (:606-615, :40-51). The crop box is odom.t +- 100,
+// transform / append of the down-sampled clouds (:592-604, r and g carried) and the CropBox-kept
+// min / max of every class for the rgbds grids (:606-615, :40-51). The crop box is odom.t +- 100,
 // and odom.t is the solved translation params[4..6] that block 0 stores.
 __global__ void __launch_bounds__(256) k_rg_append_minmax(DevState* __restrict__ st, int* __restrict__ cnt,
-                                                           u32* __restrict__ acc, const float4* __restrict__ map_e,
-                                                           const float4* __restrict__ map_s,
-                                                           const float4* __restrict__ ds_e,
-                                                           const float4* __restrict__ ds_s, float4* __restrict__ app_e,
-                                                           float4* __restrict__ app_s, double* __restrict__ poses,
-                                                           int pose_cap) {
-    __shared__ float red[4][12];
+                                                           u32* __restrict__ acc, int nc, Clouds map, Clouds ds,
+                                                           CloudsW app, double* __restrict__ poses, int pose_cap) {
     double prm[7];
     for (int k = 0; k < 7; ++k) prm[k] = st->params[k];
     if (blockIdx.x == 0) finalize_pose(st, poses, pose_cap, 1, acc, prm);
     const float lox = (float)(prm[4] - 100), loy = (float)(prm[5] - 100), loz = (float)(prm[6] - 100);   // in_crop
     const float hix = (float)(prm[4] + 100), hiy = (float)(prm[5] + 100), hiz = (float)(prm[6] + 100);
-    const int me = cnt[C_ME], ne = cnt[C_EDS], ms = cnt[C_MS], ns = cnt[C_SDS];
-    const int n = me + ne + ms + ns;
+    const RgView V = rg_view(cnt, nc, map, Clouds{{app.p[0], app.p[1], app.p[2]}});
+    const int n = V.total();
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt[C_NRG] = n;
-    float v[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) v[k] = ((k % 6) < 3) ? FLT_MAX : -FLT_MAX;
+    float v[6 * kMaxC];
+    minmax_init(v);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        int r = 0;
+#pragma unroll
+        for (int k = 0; k < 2 * kMaxC - 1; ++k) r += i >= V.end[k] ? 1 : 0;
+        const int c = r >> 1, li = i - (r ? V.end[r - 1] : 0);
         float4 p;
-        int c;
-        if (i < me) { p = map_e[i]; c = 0; }
-        else if (i < me + ne) { p = associate(prm, ds_e[i - me]); app_e[i - me] = p; c = 0; }
-        else if (i < me + ne + ms) { p = map_s[i - me - ne]; c = 1; }
-        else { p = associate(prm, ds_s[i - me - ne - ms]); app_s[i - me - ne - ms] = p; c = 1; }
+        if (r & 1) {                                   // appended: pointAssociateToMap of the ds point
+            p = associate(prm, ds.p[c][li]);
+            app.p[c][li] = p;
+        } else {
+            p = map.p[c][li];
+        }
         if ((p.x < lox || p.y < loy || p.z < loz) || (p.x > hix || p.y > hiy || p.z > hiz)) continue;
-        const float xyz[3] = {p.x, p.y, p.z};
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            if (c == 0) { v[k] = fminf(v[k], xyz[k]); v[3 + k] = fmaxf(v[3 + k], xyz[k]); }
-            else { v[6 + k] = fminf(v[6 + k], xyz[k]); v[9 + k] = fmaxf(v[9 + k], xyz[k]); }
-        }
+        minmax_add(v, c, p);
     }
-    const int w = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const float r = ((k % 6) < 3) ? wave_minf(v[k]) : wave_maxf(v[k]);
-        if (lane_id() == 0) red[w][k] = r;
-    }
-    __syncthreads();
-    if (threadIdx.x < 12) {
-        const int k = threadIdx.x;
-        float r = red[0][k];
-        for (int ww = 1; ww < 4; ++ww) r = ((k % 6) < 3) ? fminf(r, red[ww][k]) : fmaxf(r, red[ww][k]);
-        const bool any = ((k % 6) < 3) ? (r != FLT_MAX) : (r != -FLT_MAX);
-        if (any) {
-            if ((k % 6) < 3) atomicMin(&acc[A_RG + k], f2ord(r));
-            else atomicMax(&acc[A_RG + k], f2ord(r));
-        }
-    }
+    minmax_commit(v, acc + A_RG);
 }
 
 __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st, const int* __restrict__ cnt,
-                                                  const u32* __restrict__ acc, const float4* map_e,
-                                                  const float4* app_e, const float4* map_s, const float4* app_s,
-                                                  float leaf0, float leaf1, u32* __restrict__ keys,
-                                                  u32* __restrict__ vals, SortHist sh) {
+                                                  const u32* __restrict__ acc, int nc, Clouds map, Clouds app,
+                                                  VgLeaf leaf, u32* __restrict__ keys, u32* __restrict__ vals,
+                                                  SortHist sh) {
     __shared__ u32 lh[4][256];
     sort_hist_begin(lh);
-    const RgView V = rg_view(cnt, map_e, app_e, map_s, app_s);
+    const RgView V = rg_view(cnt, nc, map, app);
     const int n = V.total();
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         int c;
@@ -1133,18 +1178,18 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
             sort_hist_add(lh, kSentinel, sh.passes);
             continue;
         }
-        const float leaf = c == 0 ? leaf0 : leaf1;
+        const float lf = leaf.v[c];
         const u32* a = acc + A_RG + 6 * c;
         int minb[3], div[3];
         for (int k = 0; k < 3; ++k) {                                // :46-56 (f32 division)
-            minb[k] = (int)floorf(ord2f(a[k]) / leaf);
-            div[k] = (int)floorf(ord2f(a[3 + k]) / leaf) - minb[k] + 1;
+            minb[k] = (int)floorf(ord2f(a[k]) / lf);
+            div[k] = (int)floorf(ord2f(a[3 + k]) / lf) - minb[k] + 1;
         }
-        const int i0 = (int)(floorf(p.x / leaf) - (float)minb[0]);  // :63-65
-        const int i1 = (int)(floorf(p.y / leaf) - (float)minb[1]);
-        const int i2 = (int)(floorf(p.z / leaf) - (float)minb[2]);
+        const int i0 = (int)(floorf(p.x / lf) - (float)minb[0]);  // :63-65
+        const int i1 = (int)(floorf(p.y / lf) - (float)minb[1]);
+        const int i2 = (int)(floorf(p.z / lf) - (float)minb[2]);
         const int idx = i0 * 1 + i1 * div[0] + i2 * (div[0] * div[1]);
-        keys[i] = ((u32)idx & 0x7fffffffu) | ((u32)c << 31);
+        keys[i] = ((u32)idx & 0x3fffffffu) | ((u32)c << 30);
         sort_hist_add(lh, keys[i], sh.passes);
     }
     sort_hist_end(lh, sh, n, n);
@@ -1152,7 +1197,8 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
 
 struct RgReduceArgs {
     const int* cnt;
-    const float4 *map_e, *app_e, *map_s, *app_s;
+    int nc;
+    Clouds map, app;
     const u32* keys;
     const u32* vals;
     const u32* segstart;
@@ -1164,7 +1210,7 @@ struct RgReduceArgs {
 };
 
 __global__ void __launch_bounds__(256) k_rg_reduce(RgReduceArgs a) {
-    const RgView V = rg_view(a.cnt, a.map_e, a.app_e, a.map_s, a.app_s);
+    const RgView V = rg_view(a.cnt, a.nc, a.map, a.app);
     const int nseg = a.cnt[C_NSEG], nvalid = a.cnt[C_NRG_VALID];
     for (int sg = blockIdx.x * blockDim.x + threadIdx.x; sg < nseg; sg += gridDim.x * blockDim.x) {
         const u32 b0 = a.segstart[sg], b1 = (sg + 1 < nseg) ? a.segstart[sg + 1] : (u32)nvalid;
@@ -1190,31 +1236,35 @@ __global__ void __launch_bounds__(256) k_rg_reduce(RgReduceArgs a) {
     }
 }
 
-__global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const float4* __restrict__ seg_out,
+// compaction: class c's kept voxels are the kept segments in [nlt(c), nlt(c + 1)), in order
+__global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, int nc, const float4* __restrict__ seg_out,
                                                    const u32* __restrict__ keep, const u32* __restrict__ pos,
-                                                   float4* __restrict__ map_e, float4* __restrict__ map_s) {
-    const int nseg = cnt[C_NSEG], nse = cnt[C_NSEG_E], total = cnt[C_KEEP_TOTAL];
-    const int kept_e = nse < nseg ? (int)pos[nse] : total;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {                  // no block of this kernel reads them
-        cnt[C_ME] = kept_e;
-        cnt[C_MS] = total - kept_e;
+                                                   CloudsW map) {
+    const int nseg = cnt[C_NSEG], total = cnt[C_KEEP_TOTAL];
+    int sb[kMaxC + 1], kb[kMaxC + 1];             // segment / kept-voxel start of every class
+    sb[0] = 0;
+    kb[0] = 0;
+#pragma unroll
+    for (int c = 1; c <= kMaxC; ++c) {
+        sb[c] = c < nc ? cnt[C_NLT + c - 1] : nseg;
+        kb[c] = sb[c] < nseg ? (int)pos[sb[c]] : total;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0)      // no block of this kernel reads them
+        for (int c = 0; c < nc; ++c) cnt[C_M + c] = kb[c + 1] - kb[c];
     for (int sg = blockIdx.x * blockDim.x + threadIdx.x; sg < nseg; sg += gridDim.x * blockDim.x) {
         if (!keep[sg]) continue;
-        const u32 p = pos[sg];
-        if (sg < nse) map_e[p] = seg_out[sg];
-        else map_s[p - kept_e] = seg_out[sg];
+        const int c = sg < sb[1] ? 0 : (sg < sb[2] ? 1 : 2);
+        map.p[c][(int)pos[sg] - kb[c]] = seg_out[sg];
     }
 }
 
-// initMapWithPoints (:217-222): append raw clouds (r = g = 0)
-__global__ void __launch_bounds__(256) k_init_map(const int* __restrict__ cnt, const float4* __restrict__ e,
-                                                   const float4* __restrict__ s, float4* __restrict__ map_e,
-                                                   float4* __restrict__ map_s) {
-    const int n0 = cnt[C_EIN], n1 = cnt[C_SIN], b0 = cnt[C_ME], b1 = cnt[C_MS];
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
-        if (i < n0) { const float4 p = e[i]; map_e[b0 + i] = make_float4(p.x, p.y, p.z, __uint_as_float(0u)); }
-        else { const float4 p = s[i - n0]; map_s[b1 + i - n0] = make_float4(p.x, p.y, p.z, __uint_as_float(0u)); }
+// initMapWithPoints (ES :217-222, BPF :685-691): append the raw clouds (r = g = 0)
+__global__ void __launch_bounds__(256) k_init_map(const int* __restrict__ cnt, int nc, Clouds in, CloudsW map) {
+    const CatIdx ci = cat_idx(cnt + C_IN, nc);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ci.total(); i += gridDim.x * blockDim.x) {
+        const int c = ci.cls(i);
+        const float4 p = in.p[c][i - ci.start(c)];
+        map.p[c][cnt[C_M + c] + i - ci.start(c)] = make_float4(p.x, p.y, p.z, __uint_as_float(0u));
     }
 }
 
@@ -1223,10 +1273,9 @@ __global__ void k_init_buckets(int4* __restrict__ b, size_t n) {
         b[i] = make_int4(0, -1, -1, -1);
 }
 
-__global__ void k_init_counts(int* __restrict__ cnt, DevState* __restrict__ st) {
+__global__ void k_init_counts(int* __restrict__ cnt, DevState* __restrict__ st, int nc) {
     if (threadIdx.x != 0) return;
-    cnt[C_ME] += cnt[C_EIN];
-    cnt[C_MS] += cnt[C_SIN];
+    for (int c = 0; c < nc; ++c) cnt[C_M + c] += cnt[C_IN + c];
     st->optimization_count = 12;
 }
 
@@ -1234,31 +1283,34 @@ __global__ void k_init_counts(int* __restrict__ cnt, DevState* __restrict__ st) 
 
 // ==============================================================================================
 int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& prm, int device, size_t in_cap,
-                size_t map_cap) {
+                size_t map_cap, int nc) {
+    if (nc < 2 || nc > kMaxC) return PF_EINVAL;
     o.lidar = lidar;
     o.prm = prm;
     o.device = device;
     o.in_cap = in_cap;
     o.map_cap = map_cap;
-    o.sort_cap = 2 * map_cap + 2 * in_cap;
+    o.cls = ClassCfg{nc, 1u << (nc - 1)};          // the last class is the plane class
+    o.sort_cap = (size_t)nc * (map_cap + in_cap);
     if (o.sort_cap < 10 * in_cap) o.sort_cap = 10 * in_cap;
     o.pose_cap = (size_t)1 << 20;
-    o.leaf_vg[0] = (float)prm.map_res;
-    o.leaf_vg[1] = (float)(prm.map_res * 2);
-    o.leaf_rg[0] = (float)prm.map_res;
-    o.leaf_rg[1] = (float)prm.map_res * 2;
+    for (int c = 0; c < nc; ++c) {
+        const bool plane = o.cls.is_plane(c);
+        o.leaf_vg[c] = plane ? (float)(prm.map_res * 2) : (float)prm.map_res;   // setLeafSize(double -> float)
+        o.leaf_rg[c] = plane ? (float)prm.map_res * 2 : (float)prm.map_res;     // float map_resolution (.h:62)
+    }
     if (hipStreamCreateWithFlags(&o.stream, hipStreamNonBlocking) != hipSuccess) return PF_EHIP;
     if (hipStreamCreateWithFlags(&o.stream_a, hipStreamNonBlocking) != hipSuccess) return PF_EHIP;
     int rc = fe_alloc(o.fe, lidar, in_cap);
     if (rc) return rc;
-    // 1 m cells over both maps' bounding boxes: 2 x (201 m)^2 x 400 m covers the +-100 m crop box
-    rc = grid_alloc(o.grid, 2 * map_cap, (size_t)1 << 25);
+    // 1 m cells over every map's bounding box: 3 x (201 m)^2 x 270 m covers the +-100 m crop box
+    rc = grid_alloc(o.grid, (size_t)nc * map_cap, (size_t)1 << 25);
     if (rc) return rc;
     rc = prim_alloc(o.prim, o.sort_cap, ((size_t)1 << 25) + 2);   // sorts; scans up to the cell count
     if (rc) return rc;
-    rc = prim_alloc(o.vprim, 2 * in_cap);
+    rc = prim_alloc(o.vprim, (size_t)nc * in_cap);
     if (rc) return rc;
-    const size_t nq = 2 * in_cap;
+    const size_t nq = (size_t)nc * in_cap;
 #define PF_ALLOC(ptr, bytes) \
     if (hipMalloc(&(ptr), (bytes)) != hipSuccess) return PF_ENOMEM;
     PF_ALLOC(o.st, sizeof(DevState));
@@ -1266,25 +1318,25 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.cnt, sizeof(int) * C_COUNT);
     PF_ALLOC(o.acc, sizeof(u32) * A_COUNT);
     for (int p = 0; p < kSlots; ++p) {
-        PF_ALLOC(o.sb[p].in_edge, sizeof(float4) * in_cap);
-        PF_ALLOC(o.sb[p].in_surf, sizeof(float4) * in_cap);
-        PF_ALLOC(o.sb[p].ds_edge, sizeof(float4) * in_cap);
-        PF_ALLOC(o.sb[p].ds_surf, sizeof(float4) * in_cap);
+        for (int c = 0; c < nc; ++c) {
+            PF_ALLOC(o.sb[p].in[c], sizeof(float4) * in_cap);
+            PF_ALLOC(o.sb[p].ds[c], sizeof(float4) * in_cap);
+        }
         PF_ALLOC(o.sb[p].cnt, sizeof(int) * C_COUNT);
         if (hipMemset(o.sb[p].cnt, 0, sizeof(int) * C_COUNT) != hipSuccess) return PF_EHIP;
         if (hipEventCreateWithFlags(&o.ev_a[p], hipEventDisableTiming) != hipSuccess) return PF_EHIP;
         if (hipEventCreateWithFlags(&o.ev_b[p], hipEventDisableTiming) != hipSuccess) return PF_EHIP;
     }
     PF_ALLOC(o.acc_a, sizeof(u32) * A_COUNT);
-    PF_ALLOC(o.vkeys, sizeof(u32) * (2 * in_cap + 1));
-    PF_ALLOC(o.vvals, sizeof(u32) * (2 * in_cap + 1));
-    PF_ALLOC(o.vflags, sizeof(u32) * (2 * in_cap + 1));
-    PF_ALLOC(o.vscan, sizeof(u32) * (2 * in_cap + 1));
-    PF_ALLOC(o.vsegstart, sizeof(u32) * (2 * in_cap + 1));
-    PF_ALLOC(o.map_e, sizeof(float4) * map_cap);
-    PF_ALLOC(o.map_s, sizeof(float4) * map_cap);
-    PF_ALLOC(o.app_e, sizeof(float4) * in_cap);
-    PF_ALLOC(o.app_s, sizeof(float4) * in_cap);
+    PF_ALLOC(o.vkeys, sizeof(u32) * (nq + 1));
+    PF_ALLOC(o.vvals, sizeof(u32) * (nq + 1));
+    PF_ALLOC(o.vflags, sizeof(u32) * (nq + 1));
+    PF_ALLOC(o.vscan, sizeof(u32) * (nq + 1));
+    PF_ALLOC(o.vsegstart, sizeof(u32) * (nq + 1));
+    for (int c = 0; c < nc; ++c) {
+        PF_ALLOC(o.map[c], sizeof(float4) * map_cap);
+        PF_ALLOC(o.app[c], sizeof(float4) * in_cap);
+    }
     PF_ALLOC(o.seg_out, sizeof(float4) * o.sort_cap);
     PF_ALLOC(o.keys, sizeof(u32) * (o.sort_cap + 1));
     PF_ALLOC(o.vals, sizeof(u32) * (o.sort_cap + 1));
@@ -1300,10 +1352,10 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.roundv, sizeof(float) * nq);
     PF_ALLOC(o.observe, sizeof(float) * nq);
     PF_ALLOC(o.pnext, sizeof(int) * 5 * nq);
-    PF_ALLOC(o.pbkt, sizeof(int4) * 2 * map_cap);
+    PF_ALLOC(o.pbkt, sizeof(int4) * nc * map_cap);
     PF_ALLOC(o.tailinc, sizeof(u32) * 5 * nq);
     PF_ALLOC(o.poses, sizeof(double) * 7 * o.pose_cap);
-    PF_ALLOC(o.stage, sizeof(float4) * 2 * in_cap);
+    PF_ALLOC(o.stage, sizeof(float4) * nq);
 #undef PF_ALLOC
     if (std::getenv("PF_PROBE")) {                 // development probe: LM phase timestamps
         if (hipMalloc(&o.dbg, sizeof(unsigned long long) * 64) != hipSuccess) return PF_ENOMEM;
@@ -1311,7 +1363,8 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     }
     if (hipHostMalloc(&o.h_cnt, sizeof(int) * C_COUNT) != hipSuccess) return PF_ENOMEM;
     if (hipHostMalloc(&o.h_pose, sizeof(double) * 8) != hipSuccess) return PF_ENOMEM;
-    // init (:182-208): identity odom / last_odom, parameters {0,0,0,1,0,0,0}, optimization_count 2
+    // init (:182-208, BPF :649-681): identity odom / last_odom, parameters {0,0,0,1,0,0,0},
+    // optimization_count 2
     DevState h{};
     h.params[3] = 1.0;
     for (int i = 0; i < 3; ++i) h.odomR[4 * i] = h.lastR[4 * i] = 1.0;
@@ -1322,7 +1375,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (hipMemset(o.acc_a, 0, sizeof(u32) * A_COUNT) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.lm, 0, sizeof(LMState)) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.lm_ticket, 0, sizeof(u32) * 4) != hipSuccess) return PF_EHIP;
-    hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, 2 * map_cap);   // all empty
+    hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)nc * map_cap);   // all empty
     if (hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
     o.opt_count_host = 2;
     return PF_OK;
@@ -1334,17 +1387,23 @@ void odom_destroy(OdomGPU& o) {
         if (o.graph_b[p]) (void)hipGraphExecDestroy(o.graph_b[p]);
         if (o.ev_a[p]) (void)hipEventDestroy(o.ev_a[p]);
         if (o.ev_b[p]) (void)hipEventDestroy(o.ev_b[p]);
-        void* sp[] = {o.sb[p].in_edge, o.sb[p].in_surf, o.sb[p].ds_edge, o.sb[p].ds_surf, o.sb[p].cnt};
-        for (void* q : sp) (void)hipFree(q);
+        for (int c = 0; c < kMaxC; ++c) {
+            (void)hipFree(o.sb[p].in[c]);
+            (void)hipFree(o.sb[p].ds[c]);
+        }
+        (void)hipFree(o.sb[p].cnt);
     }
     fe_free(o.fe);
     grid_free(o.grid);
     prim_free(o.prim);
     prim_free(o.vprim);
-    void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.map_e,
-                    o.map_s, o.app_e, o.app_s, o.seg_out, o.keys, o.vals, o.flags, o.scan_out, o.segstart, o.nbr,
-                    o.qflag, o.lm_part, o.lm_ticket, o.geo, o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc,
-                    o.poses, o.stage, o.dbg};
+    for (int c = 0; c < kMaxC; ++c) {
+        (void)hipFree(o.map[c]);
+        (void)hipFree(o.app[c]);
+    }
+    void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.seg_out,
+                    o.keys, o.vals, o.flags, o.scan_out, o.segstart, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
+                    o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
     if (o.h_pose) (void)hipHostFree(o.h_pose);
@@ -1353,30 +1412,36 @@ void odom_destroy(OdomGPU& o) {
     o = OdomGPU{};
 }
 
+static Clouds clouds(float4* const* p) { return Clouds{{p[0], p[1], p[2]}}; }
+static CloudsW clouds_w(float4* const* p) { return CloudsW{{p[0], p[1], p[2]}}; }
+
 void stage_enqueue_fe(OdomGPU& o, int p, const float4* d_in, hipStream_t s) {
     StageBuf& sb = o.sb[p];
-    fe_enqueue(o.fe, d_in, sb.cnt + C_NIN, sb.in_edge, sb.cnt + C_EIN, sb.in_surf, sb.cnt + C_SIN, s);
+    fe_enqueue(o.fe, d_in, sb.cnt + C_NIN, sb.in[0], sb.cnt + C_IN, sb.in[1], sb.cnt + C_IN + 1, s);
 }
 
 void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s) {
     StageBuf& sb = o.sb[p];
     int* cnt = sb.cnt;
-    // VoxelGrid of both inputs (:242-245); pose independent, so it runs ahead on stream A
-    hipLaunchKernelGGL(k_vg_begin, dim3(1), dim3(64), 0, s, cnt, o.acc_a);
-    hipLaunchKernelGGL(k_vg_minmax, dim3(128), dim3(256), 0, s, sb.in_edge, sb.in_surf, cnt, o.acc_a);
-    hipLaunchKernelGGL(k_vg_keys, dim3(kGrid), dim3(256), 0, s, sb.in_edge, sb.in_surf, cnt, o.acc_a, o.leaf_vg[0],
-                       o.leaf_vg[1], o.vkeys, o.vvals, sort_hist(o.vprim, 32, true));
+    const int nc = o.cls.nc;
+    const VgLeaf leaf{{o.leaf_vg[0], o.leaf_vg[1], o.leaf_vg[2]}};
+    // VoxelGrid of every class (:242-245, BPF :714-719); pose independent, so it runs ahead on stream A
+    hipLaunchKernelGGL(k_vg_begin, dim3(1), dim3(64), 0, s, cnt, o.acc_a, nc);
+    hipLaunchKernelGGL(k_vg_minmax, dim3(128), dim3(256), 0, s, clouds(sb.in), cnt, o.acc_a, nc);
+    hipLaunchKernelGGL(k_vg_keys, dim3(kGrid), dim3(256), 0, s, clouds(sb.in), cnt, o.acc_a, nc, leaf, o.vkeys,
+                       o.vvals, sort_hist(o.vprim, 32, true));
     radix_sort_pairs(o.vkeys, o.vvals, cnt + C_VGN, 32, o.vprim, s, nullptr, nullptr, true);
-    segment_starts(o.vkeys, cnt + C_VGN, o.vsegstart, cnt + C_NSEG, cnt + C_NSEG_E, cnt + C_NRG_VALID, o.vprim, s);
-    hipLaunchKernelGGL(k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, sb.in_edge, sb.in_surf, o.vkeys, o.vvals,
-                       o.vsegstart, cnt, sb.ds_edge, sb.ds_surf);
+    segment_starts(o.vkeys, cnt + C_VGN, o.vsegstart, cnt + C_NSEG, cnt + C_NLT, cnt + C_NRG_VALID, o.vprim, s);
+    hipLaunchKernelGGL(k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, clouds(sb.in), o.vkeys, o.vvals, o.vsegstart,
+                       cnt, nc, clouds_w(sb.ds));
 }
 
 void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s) {
     StageBuf& sb = o.sb[p];
+    const int nc = o.cls.nc;
     hipLaunchKernelGGL(k_pull_counts, dim3(1), dim3(64), 0, s, o.cnt, sb.cnt);
-    hipLaunchKernelGGL(k_init_map, dim3(kGrid), dim3(256), 0, s, o.cnt, sb.in_edge, sb.in_surf, o.map_e, o.map_s);
-    hipLaunchKernelGGL(k_init_counts, dim3(1), dim3(64), 0, s, o.cnt, o.st);
+    hipLaunchKernelGGL(k_init_map, dim3(kGrid), dim3(256), 0, s, o.cnt, nc, clouds(sb.in), clouds_w(o.map));
+    hipLaunchKernelGGL(k_init_counts, dim3(1), dim3(64), 0, s, o.cnt, o.st, nc);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, o.st, o.poses, (int)o.pose_cap, 0, o.acc);
     o.opt_count_host = 12;
     o.inited = true;
@@ -1386,36 +1451,39 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     if (o.opt_count_host > 2) o.opt_count_host--;
     StageBuf& sb = o.sb[p];
     int* cnt = o.cnt;
+    const int nc = o.cls.nc;
     // (a side-stream branch for the single-thread prediction beside the grid build measured slower
     // under graph replay: 2815 vs 2930 frames/s; the fork / join edges cost more than the overlap)
-    hipLaunchKernelGGL(k_predict, dim3(1), dim3(64), 0, s, o.st, cnt, sb.cnt, o.acc);
-    // grids of the edge / surf maps (kd-tree build, :249-250)
-    grid_build(o.grid, o.map_e, cnt + C_ME, o.map_s, cnt + C_MS, o.prim, s);
+    hipLaunchKernelGGL(k_predict, dim3(1), dim3(64), 0, s, o.st, cnt, sb.cnt, o.acc, o.cls);
+    // grids of the class maps (kd-tree builds, :249-250 / BPF :723-725)
+    GridPtrs gp{{o.map[0], o.map[1], o.map[2]}, {cnt + C_M, cnt + C_M + 1, cnt + C_M + 2}, nc};
+    grid_build(o.grid, gp, o.prim, s);
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
-        AssocArgs aa{o.st, cnt, o.acc, gv, sb.ds_edge, sb.ds_surf, o.map_e, o.map_s, o.nbr, o.qflag, o.geo, o.spars,
+        AssocArgs aa{o.st, cnt, o.acc, gv, o.cls, clouds(sb.ds), clouds(o.map), o.nbr, o.qflag, o.geo, o.spars,
                      o.roundv, o.pbkt, o.pnext, (u32)o.map_cap, o.lm_ticket};
         hipLaunchKernelGGL(k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
-        ObsArgs oa{cnt, o.acc, o.map_e, o.map_s, sb.ds_edge, sb.ds_surf, o.nbr, o.qflag, o.pbkt, o.pnext, o.tailinc,
+        ObsArgs oa{cnt, o.acc, o.cls, clouds(o.map), clouds_w(sb.ds), o.nbr, o.qflag, o.pbkt, o.pnext, o.tailinc,
                    (u32)o.map_cap, o.roundv, o.spars, o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
         hipLaunchKernelGGL(k_observe, dim3(kGrid), dim3(256), 0, s, oa);
-        LmArgs la{o.st, cnt, o.acc, o.lm, o.lm_part, o.lm_ticket, o.qflag, sb.ds_edge, sb.ds_surf, o.geo, o.observe,
-                  o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.pbkt, o.map_e, o.map_s, (u32)o.map_cap};
+        LmArgs la{o.st, cnt, o.acc, o.cls, o.lm, o.lm_part, o.lm_ticket, o.qflag, clouds(sb.ds), o.geo, o.observe,
+                  o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.pbkt, clouds_w(o.map), (u32)o.map_cap};
         hipLaunchKernelGGL(k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
     }
-    // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647)
-    hipLaunchKernelGGL(k_rg_append_minmax, dim3(256), dim3(256), 0, s, o.st, cnt, o.acc, o.map_e, o.map_s,
-                       sb.ds_edge, sb.ds_surf, o.app_e, o.app_s, o.poses, (int)o.pose_cap);
-    hipLaunchKernelGGL(k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, o.map_e, o.app_e, o.map_s, o.app_s,
-                       o.leaf_rg[0], o.leaf_rg[1], o.keys, o.vals, sort_hist(o.prim, 32, true));
+    // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647, BPF :1197-1290)
+    const VgLeaf leaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}};
+    hipLaunchKernelGGL(k_rg_append_minmax, dim3(256), dim3(256), 0, s, o.st, cnt, o.acc, nc, clouds(o.map),
+                       clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap);
+    hipLaunchKernelGGL(k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, nc, clouds(o.map), clouds(o.app),
+                       leaf, o.keys, o.vals, sort_hist(o.prim, 32, true));
     radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
-    segment_starts(o.keys, cnt + C_NRG, o.segstart, cnt + C_NSEG, cnt + C_NSEG_E, cnt + C_NRG_VALID, o.prim, s);
-    RgReduceArgs ra{cnt, o.map_e, o.app_e, o.map_s, o.app_s, o.keys, o.vals, o.segstart, o.seg_out, o.flags,
+    segment_starts(o.keys, cnt + C_NRG, o.segstart, cnt + C_NSEG, cnt + C_NLT, cnt + C_NRG_VALID, o.prim, s);
+    RgReduceArgs ra{cnt, nc, clouds(o.map), clouds(o.app), o.keys, o.vals, o.segstart, o.seg_out, o.flags,
                     o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
     hipLaunchKernelGGL(k_rg_reduce, dim3(kGrid), dim3(256), 0, s, ra);
     scan_exclusive(o.flags, o.scan_out, cnt + C_NSEG, (u32*)(cnt + C_KEEP_TOTAL), o.prim, s);
-    hipLaunchKernelGGL(k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, o.flags, o.scan_out, o.map_e,
-                       o.map_s);
+    hipLaunchKernelGGL(k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, nc, o.seg_out, o.flags, o.scan_out,
+                       clouds_w(o.map));
 }
 
 }  // namespace pf

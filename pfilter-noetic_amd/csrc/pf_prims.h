@@ -124,10 +124,10 @@ __device__ __forceinline__ void sort_hist_end(u32 (*lh)[256], const SortHist& sh
     if (t == 0) __hip_atomic_store(sh.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Segments of stably sorted keys (bit 31 = cloud id, 0xFFFFFFFF = dropped entries, sorted last):
-// segstart[s] = first index of segment s; *d_nseg = number of segments; *d_nseg_c0 = segments of
-// cloud 0; *d_nvalid = number of non-sentinel keys.
-void segment_starts(const u32* keys, const int* d_n, u32* segstart, int* d_nseg, int* d_nseg_c0, int* d_nvalid,
+// Segments of stably sorted keys (bits 30-31 = cloud class 0..2, 0xFFFFFFFF = dropped entries, sorted
+// last): segstart[s] = first index of segment s; *d_nseg = number of segments; d_nlt[b - 1] = segments
+// of classes < b (b = 1, 2, 3); *d_nvalid = number of non-sentinel keys.
+void segment_starts(const u32* keys, const int* d_n, u32* segstart, int* d_nseg, int* d_nlt, int* d_nvalid,
                     PrimWork& w, hipStream_t s);
 
 // out[i] = sum(in[0..i)) for i < *d_n; *d_total = sum(in[0..n)) when d_total != nullptr.

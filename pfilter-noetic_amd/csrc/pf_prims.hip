@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(256) k_scan1(const u32* __restrict__ in, u32* 
 // segments, the number of cloud-0 segments and the number of non-sentinel keys, in one pass.
 __global__ void __launch_bounds__(256) k_segments(const u32* __restrict__ keys, const int* __restrict__ d_n,
                                                    u32* __restrict__ segstart, int* __restrict__ d_nseg,
-                                                   int* __restrict__ d_nseg_c0, int* __restrict__ d_nvalid,
+                                                   int* __restrict__ d_nlt, int* __restrict__ d_nvalid,
                                                    u64* __restrict__ status, u32* __restrict__ arrive,
                                                    int* __restrict__ err) {
     constexpr u32 kSent = 0xFFFFFFFFu;
@@ -271,14 +271,15 @@ __global__ void __launch_bounds__(256) k_segments(const u32* __restrict__ keys, 
     const int t = threadIdx.x;
     const int G = ntiles < (int)gridDim.x ? ntiles : (int)gridDim.x;
     if (n == 0) {
-        if (blockIdx.x == 0 && t == 0) { *d_nseg = 0; *d_nseg_c0 = 0; *d_nvalid = 0; }
+        if (blockIdx.x == 0 && t == 0) { *d_nseg = 0; d_nlt[0] = d_nlt[1] = d_nlt[2] = 0; *d_nvalid = 0; }
         return;
     }
     if ((int)blockIdx.x >= G) return;
     if (blockIdx.x == 0 && t == 0) {                            // cases without an interior boundary
         const u32 k0 = keys[0], kl = keys[n - 1];
         if (k0 == kSent) *d_nvalid = 0;
-        if ((k0 >> 31) != 0) *d_nseg_c0 = 0;
+        for (u32 b = 1; b <= 3; ++b)                            // classes below the first key's: none
+            if ((k0 >> 30) >= b) d_nlt[b - 1] = 0;
         if (kl != kSent) *d_nvalid = n;
     }
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -301,7 +302,8 @@ __global__ void __launch_bounds__(256) k_segments(const u32* __restrict__ keys, 
                 s_excl = excl;
                 if (tile == ntiles - 1) {
                     *d_nseg = (int)(excl + agg);
-                    if ((keys[n - 1] >> 31) == 0) *d_nseg_c0 = (int)(excl + agg);
+                    for (u32 b = 1; b <= 3; ++b)                // classes above the last key's: all
+                        if ((keys[n - 1] >> 30) < b) d_nlt[b - 1] = (int)(excl + agg);
                 }
             }
         }
@@ -312,7 +314,8 @@ __global__ void __launch_bounds__(256) k_segments(const u32* __restrict__ keys, 
             const int i = base + j;
             if (i >= n) break;
             const u32 kp = k[j], kc = k[j + 1];
-            if (i > 0 && (kp >> 31) == 0 && (kc >> 31) == 1) *d_nseg_c0 = (int)sid;
+            if (i > 0 && (kp >> 30) < (kc >> 30))              // class boundary: segments before it
+                for (u32 b = (kp >> 30) + 1; b <= (kc >> 30); ++b) d_nlt[b - 1] = (int)sid;
             if (i > 0 && kp != kSent && kc == kSent) *d_nvalid = i;
             if (kc != kSent && (i == 0 || kp != kc)) segstart[sid++] = (u32)i;
         }
@@ -373,10 +376,10 @@ void radix_sort_pairs(u32* keys, u32* vals, const int* d_n, int bits, PrimWork& 
     if (vout) *vout = va;
 }
 
-void segment_starts(const u32* keys, const int* d_n, u32* segstart, int* d_nseg, int* d_nseg_c0, int* d_nvalid,
+void segment_starts(const u32* keys, const int* d_n, u32* segstart, int* d_nseg, int* d_nlt, int* d_nvalid,
                     PrimWork& w, hipStream_t s) {
     const unsigned grid = (unsigned)(w.scan_tiles < (size_t)kSortMaxBlocks ? w.scan_tiles : kSortMaxBlocks);
-    hipLaunchKernelGGL(k_segments, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, keys, d_n, segstart, d_nseg, d_nseg_c0,
+    hipLaunchKernelGGL(k_segments, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, keys, d_n, segstart, d_nseg, d_nlt,
                        d_nvalid, w.scan_status, w.tickets + 5, w.err);
 }
 

@@ -57,17 +57,23 @@ class OdomStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in ("n_edge_in", "n_surf_in", "n_edge_ds", "n_surf_ds", "n_edge_map",
                                               "n_surf_map", "n_edge_res", "n_surf_res", "n_edge_valid",
                                               "n_surf_valid")] + \
-               [(n, ctypes.c_int32) for n in ("outer_iterations", "lm_iterations", "map_too_small", "status")]
+               [(n, ctypes.c_int32) for n in ("outer_iterations", "lm_iterations", "map_too_small", "status")] + \
+               [(n, ctypes.c_int64 * 3) for n in ("n_in", "n_ds", "n_map", "n_res", "n_valid")]
 
     def as_dict(self):
-        return {f[0]: getattr(self, f[0]) for f in self._fields_}
+        d = {}
+        for f in self._fields_:
+            v = getattr(self, f[0])
+            d[f[0]] = list(v) if f[0] in ("n_in", "n_ds", "n_map", "n_res", "n_valid") else v
+        return d
 
 
 EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "pf_odom_destroy",
            "pf_odom_init_map", "pf_odom_update", "pf_odom_get_pose", "pf_odom_get_map", "pf_odom_set_map",
            "pf_odom_get_stats", "pf_odom_frame_device", "pf_odom_frame_host", "pf_odom_sync", "pf_odom_poses",
            "pf_odom_set_graph", "pf_device_count", "pf_dev_malloc", "pf_dev_free", "pf_memcpy_h2d",
-           "pf_memcpy_d2h", "pf_knn_create", "pf_knn_destroy", "pf_knn_set_map", "pf_knn_query", "pf_knn_bench"]
+           "pf_memcpy_d2h", "pf_knn_create", "pf_knn_destroy", "pf_knn_set_map", "pf_knn_query", "pf_knn_bench",
+           "pf_bpf_create", "pf_bpf_init_map", "pf_bpf_update", "pf_bpf_frame_device", "pf_odom_classes"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -109,6 +115,12 @@ def lib():
     L.pf_knn_set_map.argtypes = [_vp, _vp, _sz]
     L.pf_knn_query.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.pf_knn_bench.argtypes = [_vp, _i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    L.pf_bpf_create.argtypes = [ctypes.POINTER(LidarParams), ctypes.POINTER(OdomParams), _i, _sz, _sz,
+                                ctypes.POINTER(_vp)]
+    L.pf_bpf_init_map.argtypes = [_vp, _vp, _sz, _sz, _vp, _sz, _sz, _vp, _sz, _sz]
+    L.pf_bpf_update.argtypes = [_vp, _vp, _sz, _sz, _vp, _sz, _sz, _vp, _sz, _sz, _vp]
+    L.pf_bpf_frame_device.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp]
+    L.pf_odom_classes.argtypes = [_vp]
     _lib = L
     return L
 
@@ -300,6 +312,66 @@ class Odom_ES_EstimationClass:
 
 # the node-facing alias named by the north star
 OdomEstimationClass = Odom_ES_EstimationClass
+
+
+class Odom_BPF_EstimationClass(Odom_ES_EstimationClass):
+    """Drop-in for Odom_BPF_EstimationClass (src/odomEstimationClass.cpp:649-1306): beam / pillar /
+    facade maps, the whole update on the GPU. Map accessors by class: 0 beam, 1 pillar, 2 facade."""
+
+    def init(self, lidar_param, map_resolution, k_new, theta_p, theta_max, weightType):
+        self.lidar = lidar_param
+        prm = OdomParams(float(map_resolution), int(k_new), float(theta_p), int(theta_max), int(weightType))
+        h = _vp()
+        _check("pf_bpf_create", lib().pf_bpf_create(ctypes.byref(lidar_param), ctypes.byref(prm), self.device,
+                                                    self.max_points, self.map_capacity, ctypes.byref(h)))
+        self._h = h.value
+
+    def initMapWithPoints(self, beam_in, pillar_in, facade_in):
+        b, p, f = _f32x4(beam_in), _f32x4(pillar_in), _f32x4(facade_in)
+        _check("pf_bpf_init_map", lib().pf_bpf_init_map(self._h, b.ctypes.data, b.shape[0], 16, p.ctypes.data,
+                                                        p.shape[0], 16, f.ctypes.data, f.shape[0], 16))
+
+    def updatePointsToMap(self, beam_in, pillar_in, facade_in):
+        b, p, f = _f32x4(beam_in), _f32x4(pillar_in), _f32x4(facade_in)
+        pose = np.empty(7)
+        self.last_status = _check("pf_bpf_update", lib().pf_bpf_update(
+            self._h, b.ctypes.data, b.shape[0], 16, p.ctypes.data, p.shape[0], 16, f.ctypes.data, f.shape[0], 16,
+            pose.ctypes.data))
+        return pose
+
+    @property
+    def laserCloudBeamMap(self):
+        return self._map(0)
+
+    @property
+    def laserCloudPillarMap(self):
+        return self._map(1)
+
+    @property
+    def laserCloudFacadeMap(self):
+        return self._map(2)
+
+    @property
+    def laserCloudCornerMap(self):
+        raise AttributeError("Odom_BPF_EstimationClass has beam / pillar / facade maps")
+
+    laserCloudSurfMap = laserCloudCornerMap
+
+    def getMap(self):
+        """beam, pillar, then facade, appended (src/odomEstimationClass.cpp:683-689)"""
+        parts = [self._map(c) for c in range(3)]
+        return np.concatenate([m[0] for m in parts]), np.concatenate([m[1] for m in parts])
+
+    def frame_device(self, d_clouds, counts, want_pose=False):
+        """d_clouds: device pointers of the beam / pillar / facade clouds (packed float4), counts: sizes"""
+        pose = np.empty(7)
+        (b, p, f), (nb, np_, nf) = d_clouds, counts
+        _check("pf_bpf_frame_device", lib().pf_bpf_frame_device(self._h, b, int(nb), p, int(np_), f, int(nf),
+                                                                pose.ctypes.data if want_pose else None))
+        return pose if want_pose else None
+
+    def frame_host(self, xyzi, want_pose=True):
+        raise NotImplementedError("the BPF estimator takes classified beam / pillar / facade clouds")
 
 
 class Knn:

@@ -1,6 +1,7 @@
-// Drop-in replacement for the ES estimator of the reference's include/odomEstimationClass.h
-// (Odom_ES_EstimationClass, :140-163): same class name, call signatures and public members (odom,
-// laserCloudCornerMap, laserCloudSurfMap) for src/odomEstimationNode copy.cpp, with the whole
+// Drop-in replacement for the estimators of the reference's include/odomEstimationClass.h:
+// Odom_ES_EstimationClass (:140-163; members odom, laserCloudCornerMap, laserCloudSurfMap) for
+// src/odomEstimationNode copy.cpp and Odom_BPF_EstimationClass (:169-202; members odom,
+// laserCloudBeam/Pillar/Facade/MergeMap) for src/odomEstimationNode.cpp, with the whole
 // updatePointsToMap on the MI355X through libpfilter_hip.so.
 #ifndef _ODOM_ESTIMATION_CLASS_H_
 #define _ODOM_ESTIMATION_CLASS_H_
@@ -16,5 +17,6 @@
 
 typedef pcl::PointXYZRGB PointType;
 using Odom_ES_EstimationClass = pfilter_hip::Odom_ES_EstimationClassT<pcl::PointCloud<PointType>, lidar::Lidar>;
+using Odom_BPF_EstimationClass = pfilter_hip::Odom_BPF_EstimationClassT<pcl::PointCloud<PointType>, lidar::Lidar>;
 
 #endif  // _ODOM_ESTIMATION_CLASS_H_

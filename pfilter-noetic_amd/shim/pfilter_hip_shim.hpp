@@ -6,6 +6,10 @@
 //   Odom_ES_EstimationClass::init / initMapWithPoints /
 //       updatePointsToMap / getMap, members odom,
 //       laserCloudCornerMap, laserCloudSurfMap            include/odomEstimationClass.h:140-152
+//   Odom_BPF_EstimationClass::init / initMapWithPoints /
+//       updatePointsToMap / getMap / mergeFeatures,
+//       members odom, laserCloudBeamMap, laserCloudPillarMap,
+//       laserCloudFacadeMap, laserCloudMergeMap            include/odomEstimationClass.h:169-202
 //
 // The classes are templates over the point-cloud and lidar types so this header needs neither PCL nor
 // ROS; shim/laserProcessingClass.h and shim/odomEstimationClass.h instantiate them with the PCL 1.10
@@ -220,6 +224,143 @@ private:
             p.z = xyz_[3 * i + 2];
             p.r = rg_[2 * i];        // rounds / age
             p.g = rg_[2 * i + 1];    // observation count (p-index)
+            p.b = 0;
+            out.push_back(p);
+        }
+    }
+    int device_;
+    size_t max_points_, map_capacity_;
+    pf_odom* h_ = nullptr;
+    std::vector<float> xyz_;
+    std::vector<uint8_t> rg_;
+};
+
+// --------------------------------------------------------------------------------------------
+template <class CloudXYZRGB, class Lidar>
+class Odom_BPF_EstimationClassT {
+public:
+    using Ptr = typename CloudXYZRGB::Ptr;
+    using Point = typename std::decay<decltype(std::declval<CloudXYZRGB>().points[0])>::type;
+
+    explicit Odom_BPF_EstimationClassT(int device = 0, size_t max_points = 300000, size_t map_capacity = (size_t)1 << 22)
+        : laserCloudBeamMap(new CloudXYZRGB()), laserCloudPillarMap(new CloudXYZRGB()),
+          laserCloudFacadeMap(new CloudXYZRGB()), laserCloudMergeMap(new CloudXYZRGB()), device_(device),
+          max_points_(max_points), map_capacity_(map_capacity) {}
+    ~Odom_BPF_EstimationClassT() { if (h_) pf_odom_destroy(h_); }
+    Odom_BPF_EstimationClassT(const Odom_BPF_EstimationClassT&) = delete;
+    Odom_BPF_EstimationClassT& operator=(const Odom_BPF_EstimationClassT&) = delete;
+
+    // include/odomEstimationClass.h:175, src/odomEstimationClass.cpp:649-681
+    void init(Lidar lidar_param, double map_resolution_in, int k_new_para, float theta_p_para, int theta_max_para,
+              double weightType_para) {
+        if (h_) { pf_odom_destroy(h_); h_ = nullptr; }
+        const pf_lidar_params lp = lidar_params(lidar_param);
+        pf_odom_params op;
+        op.map_res = map_resolution_in;
+        op.k_new = k_new_para;
+        op.theta_p = theta_p_para;
+        op.theta_max = theta_max_para;
+        op.weight_type = (int)weightType_para;
+        check("pf_bpf_create", pf_bpf_create(&lp, &op, device_, max_points_, map_capacity_, &h_));
+        set_pose(kIdentity);
+        for (Ptr* m : maps()) (*m)->clear();
+        laserCloudMergeMap->clear();
+    }
+
+    // src/odomEstimationClass.cpp:685-691
+    void initMapWithPoints(const Ptr& beam_in, const Ptr& pillar_in, const Ptr& facade_in) {
+        check("pf_bpf_init_map", pf_bpf_init_map(h_, data(beam_in), beam_in->points.size(), sizeof(Point),
+                                                 data(pillar_in), pillar_in->points.size(), sizeof(Point),
+                                                 data(facade_in), facade_in->points.size(), sizeof(Point)));
+        refresh();
+    }
+
+    // src/odomEstimationClass.cpp:702-749
+    void updatePointsToMap(const Ptr& beam_in, const Ptr& pillar_in, const Ptr& facade_in) {
+        double pose[7];
+        const int rc = check("pf_bpf_update",
+                             pf_bpf_update(h_, data(beam_in), beam_in->points.size(), sizeof(Point), data(pillar_in),
+                                           pillar_in->points.size(), sizeof(Point), data(facade_in),
+                                           facade_in->points.size(), sizeof(Point), pose));
+        // the reference's messages (:753, :908, :1058, :1204)
+        if (rc == PF_W_MAP_TOO_SMALL) std::printf("not enough points in map to associate, map error\n");
+        if (rc == PF_W_FEW_CORRESPONDENCES) {
+            pf_odom_stats st;
+            check("pf_odom_get_stats", pf_odom_get_stats(h_, &st));
+            if (st.n_res[0] < 20) std::printf("not enough Beam points\n");
+            if (st.n_res[1] < 20) std::printf("not enough Pillar points\n");
+            if (st.n_res[2] < 20) std::printf("not enough correct points\n");
+        }
+        set_pose(pose);
+        refresh();
+    }
+
+    // beam, pillar, then facade, appended (src/odomEstimationClass.cpp:683-689)
+    void getMap(Ptr& laserCloudMap) {
+        for (Ptr* m : maps())
+            for (const auto& p : (*m)->points) laserCloudMap->push_back(p);
+    }
+
+    // laserCloudMergeMap = beam + facade + pillar (src/odomEstimationClass.cpp:1297-1302; called at the
+    // end of every updatePointsToMap when the maps are refreshed)
+    void mergeFeatures(int mergeGround = 1) {
+        (void)mergeGround;
+        laserCloudMergeMap->clear();
+        for (Ptr m : {laserCloudBeamMap, laserCloudFacadeMap, laserCloudPillarMap})
+            for (const auto& p : m->points) laserCloudMergeMap->push_back(p);
+    }
+
+    bool refresh_maps_every_frame = true;
+    void syncMaps() {
+        int c = 0;
+        for (Ptr* m : maps()) read_map(h_, c++, **m, xyz_, rg_);
+        mergeFeatures(1);
+    }
+
+#ifndef PFILTER_HIP_NO_EIGEN
+    Eigen::Isometry3d odom = Eigen::Isometry3d::Identity();
+#else
+    Pose odom;
+#endif
+    Ptr laserCloudBeamMap;
+    Ptr laserCloudPillarMap;
+    Ptr laserCloudFacadeMap;
+    Ptr laserCloudMergeMap;
+
+private:
+    static constexpr double kIdentity[7] = {0, 0, 0, 1, 0, 0, 0};
+    std::vector<Ptr*> maps() { return {&laserCloudBeamMap, &laserCloudPillarMap, &laserCloudFacadeMap}; }
+    static const float* data(const Ptr& c) {
+        return c->points.empty() ? nullptr : reinterpret_cast<const float*>(&c->points[0]);
+    }
+    void set_pose(const double* p) {
+#ifndef PFILTER_HIP_NO_EIGEN
+        const Eigen::Quaterniond q(p[3], p[0], p[1], p[2]);
+        odom = Eigen::Isometry3d::Identity();
+        odom.linear() = q.toRotationMatrix();
+        odom.translation() = Eigen::Vector3d(p[4], p[5], p[6]);
+#else
+        for (int k = 0; k < 4; ++k) odom.q[k] = p[k];
+        for (int k = 0; k < 3; ++k) odom.t[k] = p[4 + k];
+#endif
+    }
+    void refresh() {
+        if (refresh_maps_every_frame) syncMaps();
+    }
+    static void read_map(pf_odom* h, int which, CloudXYZRGB& out, std::vector<float>& xyz, std::vector<uint8_t>& rg) {
+        size_t n = 0;
+        check("pf_odom_get_map", pf_odom_get_map(h, which, nullptr, nullptr, 0, &n));
+        xyz.resize(3 * (n ? n : 1));
+        rg.resize(2 * (n ? n : 1));
+        check("pf_odom_get_map", pf_odom_get_map(h, which, xyz.data(), rg.data(), n, &n));
+        out.clear();
+        for (size_t i = 0; i < n; ++i) {
+            Point p;
+            p.x = xyz[3 * i];
+            p.y = xyz[3 * i + 1];
+            p.z = xyz[3 * i + 2];
+            p.r = rg[2 * i];
+            p.g = rg[2 * i + 1];
             p.b = 0;
             out.push_back(p);
         }

@@ -116,3 +116,15 @@ def dense_queries(map_xyz4, nq, sigma=0.3, seed=6):
     m = np.ascontiguousarray(map_xyz4, np.float32)
     lib().pfsyn_dense_queries(int(seed), int(nq), float(sigma), m.ctypes.data, m.shape[0], q.ctypes.data)
     return q
+
+
+def bpf_split(edge, surf, pillar_z=-1.0):
+    """Beam / pillar / facade clouds for the BPF estimator from featureExtraction output.
+
+    The reference feeds Odom_BPF_EstimationClass from its PCA feature classifier (include/preProcess.hpp,
+    out of scope: SURVEY §8(f) rank 3). This stand-in is deterministic and keeps every feature point:
+    edge points above `pillar_z` m in the sensor frame (vertical structures: poles, building corners)
+    are pillars, the lower ones beams, and surf points are facades."""
+    edge = np.asarray(edge, np.float32)
+    up = edge[:, 2] > pillar_z
+    return edge[~up].copy(), edge[up].copy(), np.asarray(surf, np.float32).copy()

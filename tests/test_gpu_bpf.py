@@ -1,0 +1,122 @@
+"""GPU: Odom_BPF_EstimationClass (src/odomEstimationClass.cpp:649-1306) through the C ABI against the
+oracle in GPU_EQUIV mode. Beam / pillar / facade inputs come from pfsynth.bpf_split (a deterministic
+stand-in for the reference's PCA classifier, which is outside this path: SURVEY §8(f) rank 3).
+
+Tolerances as for the ES estimator (BASELINE.json north_star): pose within 1e-4 m / 1e-5 rad per
+frame; per-class down-sampled counts, residual counts, map sizes and age / p-index bytes identical."""
+import numpy as np
+import pytest
+
+from _util import pose_err
+
+pytestmark = pytest.mark.gpu
+
+TOL_T, TOL_R = 1e-4, 1e-5
+CLASS_COUNTS = ("n_ds", "n_map", "n_res", "n_valid")
+
+
+def _pair(pa, pfref, map_res=0.4, k_new=0, theta_p=0.4, theta_max=75, wt=0):
+    od = pa.Odom_BPF_EstimationClass(device=0)
+    od.init(pa.make_lidar(64, 3.0, 90.0), map_res, k_new, theta_p, theta_max, wt)
+    orc = pfref.OdomBPF(pfref.make_lidar(64, 3.0, 90.0), map_res, k_new, theta_p, theta_max, wt,
+                        opts=pfref.GPU_EQUIV)
+    return od, orc
+
+
+def _inputs(pfref, pfsynth, seq, k):
+    e, s = pfref.feature_extraction(seq.frame(k), pfref.make_lidar(64, 3.0, 90.0), opts=pfref.FE_STABLE_TIES)
+    return pfsynth.bpf_split(e, s)
+
+
+def _compare_maps(od, orc):
+    for c, (gx, grg) in enumerate((od.laserCloudBeamMap, od.laserCloudPillarMap, od.laserCloudFacadeMap)):
+        rx, rrg = orc.get_map(c)
+        assert gx.shape == rx.shape, (c, gx.shape, rx.shape)
+        np.testing.assert_allclose(gx, rx, rtol=0, atol=TOL_T)
+        np.testing.assert_array_equal(grg, rrg)
+
+
+def _run(od, orc, pfref, pfsynth, seq, frames, check_maps_every=0):
+    worst = (0.0, 0.0)
+    for i, k in enumerate(frames):
+        cl = _inputs(pfref, pfsynth, seq, k)
+        if i == 0:
+            od.initMapWithPoints(*cl)
+            orc.init_map(*cl)
+            continue
+        pg = od.updatePointsToMap(*cl)
+        pr = orc.update(*cl)
+        dt, dr = pose_err(pg, pr)
+        worst = (max(worst[0], dt), max(worst[1], dr))
+        assert dt < TOL_T and dr < TOL_R, "frame %d: %.3e m %.3e rad" % (k, dt, dr)
+        sg, sr = od.stats(), orc.stats()
+        for c in CLASS_COUNTS:
+            assert sg[c] == sr[c], (k, c, sg[c], sr[c])
+        assert sg["outer_iterations"] == sr["outer_iterations"] and sg["map_too_small"] == sr["map_too_small"]
+        if check_maps_every and i % check_maps_every == 0:
+            _compare_maps(od, orc)
+    return worst
+
+
+def test_bpf_parity(pa, pfref, pfsynth):
+    """configs[1] parameters on the three-map estimator, 25 frames, maps compared every 8 frames."""
+    seq = pfsynth.Sequence("S64", n_frames=30)
+    od, orc = _pair(pa, pfref)
+    worst = _run(od, orc, pfref, pfsynth, seq, range(25), check_maps_every=8)
+    _compare_maps(od, orc)
+    assert worst[0] < 1e-6 and worst[1] < 1e-7
+
+
+@pytest.mark.parametrize("wt,k_new,theta_p,theta_max", [(2, 0, 0.4, 75), (12, 1, 0.8, 30), (0, 0, 0.0, 0)])
+def test_bpf_configs(pa, pfref, pfsynth, wt, k_new, theta_p, theta_max):
+    seq = pfsynth.Sequence("S64", n_frames=14, az_steps=1200)
+    od, orc = _pair(pa, pfref, wt=wt, k_new=k_new, theta_p=theta_p, theta_max=theta_max)
+    _run(od, orc, pfref, pfsynth, seq, range(12), check_maps_every=11)
+
+
+def test_bpf_device_frames_match_update_api(pa, pfref, pfsynth):
+    """pf_bpf_frame_device (HBM-resident clouds, two-stage pipeline, graph replay) gives the same bits
+    as the host-input update API."""
+    seq = pfsynth.Sequence("S64", n_frames=24, az_steps=1500)
+    clouds = [_inputs(pfref, pfsynth, seq, k) for k in range(24)]
+    host = pa.Odom_BPF_EstimationClass(device=0)
+    host.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    poses_h = []
+    for k, cl in enumerate(clouds):
+        if k == 0:
+            host.initMapWithPoints(*cl)
+            poses_h.append(host.odom)
+        else:
+            poses_h.append(host.updatePointsToMap(*cl))
+    bufs = []
+    dev = pa.Odom_BPF_EstimationClass(device=0)
+    dev.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    for cl in clouds:
+        ptrs = []
+        for c in cl:
+            b = pa.DeviceBuffer(max(c.nbytes, 16))
+            b.upload(np.ascontiguousarray(c, np.float32))
+            bufs.append(b)
+            ptrs.append(b.ptr)
+        dev.frame_device(ptrs, [c.shape[0] for c in cl])
+    dev.sync()
+    np.testing.assert_array_equal(dev.poses(), np.array(poses_h))
+    for c in range(3):
+        gx, grg = dev._map(c)
+        hx, hrg = host._map(c)
+        np.testing.assert_array_equal(gx, hx)
+        np.testing.assert_array_equal(grg, hrg)
+
+
+def test_bpf_rejects_es_entry_points(pa):
+    od = pa.Odom_BPF_EstimationClass(device=0)
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    z = np.zeros((4, 4), np.float32)
+    assert pa.lib().pf_odom_init_map(od._h, z.ctypes.data, 4, 16, z.ctypes.data, 4, 16) == pa.PF_EINVAL
+    assert pa.lib().pf_odom_frame_host(od._h, z.ctypes.data, 4, 16, None) == pa.PF_EINVAL
+    assert pa.lib().pf_odom_classes(od._h) == 3
+    es = pa.Odom_ES_EstimationClass(device=0)
+    es.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    assert pa.lib().pf_bpf_init_map(es._h, z.ctypes.data, 4, 16, z.ctypes.data, 4, 16, z.ctypes.data, 4,
+                                    16) == pa.PF_EINVAL
+    assert pa.lib().pf_odom_classes(es._h) == 2

@@ -39,3 +39,33 @@ def test_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
         np.testing.assert_array_equal(got[k, :7], od.odom)
         assert got[k, 7] == od.laserCloudCornerMap[0].shape[0]
         assert got[k, 8] == od.laserCloudSurfMap[0].shape[0]
+
+
+def test_bpf_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
+    """Odom_BPF_EstimationClass drop-in (shim) driven like src/odomEstimationNode.cpp:254-264."""
+    exe = str(tmp_path / "shim_bpf_driver")
+    lib = os.path.join(ROOT, "pfilter-noetic_amd")
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "shim", "shim_bpf_driver.cpp"), "-o", exe, "-L", lib,
+                           "-lpfilter_hip", "-Wl,-rpath," + lib, "-Wl,-rpath-link,/opt/rocm/lib"])
+    seq = pfsynth.Sequence("S64", n_frames=8, az_steps=1200)
+    lid = pfref.make_lidar(64, 3.0, 90.0)
+    clouds = [pfsynth.bpf_split(*pfref.feature_extraction(seq.frame(k), lid, opts=pfref.FE_STABLE_TIES))
+              for k in range(8)]
+    with open(tmp_path / "clouds.bin", "wb") as f:
+        for cl in clouds:
+            for c in cl:
+                np.array([c.shape[0]], np.int64).tofile(f)
+                c.astype(np.float32).tofile(f)
+    subprocess.check_call([exe, str(tmp_path / "clouds.bin"), str(tmp_path / "poses.txt")], timeout=120)
+    got = np.loadtxt(tmp_path / "poses.txt")
+    od = pa.Odom_BPF_EstimationClass()
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    for k, cl in enumerate(clouds):
+        if k == 0:
+            od.initMapWithPoints(*cl)
+        else:
+            od.updatePointsToMap(*cl)
+        np.testing.assert_array_equal(got[k, :7], od.odom)
+        sizes = [m[0].shape[0] for m in (od.laserCloudBeamMap, od.laserCloudPillarMap, od.laserCloudFacadeMap)]
+        assert list(got[k, 7:10]) == sizes and got[k, 10] == sum(sizes)

@@ -65,3 +65,30 @@ def test_map_state_invariants(pfref, pfsynth):
         assert xyz.shape[0] > 100
         assert np.all(np.abs(xyz - p[4:].astype(np.float32)) <= 100.0 + 1e-3)
         assert rg[:, 1].max() >= 1            # p-index observed at least once
+
+
+def test_bpf_tracks_and_reduces_to_es_structure(pfref, pfsynth):
+    """Odom_BPF_EstimationClass restated (src/odomEstimationClass.cpp:649-1306): three maps in class
+    order beam / pillar / facade, each with its own p-index bookkeeping. It tracks the generator's
+    trajectory like the ES estimator on the same scans, and each class reports its own counts."""
+    seq = pfsynth.Sequence("S64", n_frames=30, az_steps=1000)
+    lid = pfref.make_lidar(64, 3.0, 90.0)
+    od = pfref.OdomBPF(lid, 0.4, 0, 0.4, 75, 0, opts=pfref.GPU_EQUIV)
+    for k in range(25):
+        e, s = pfref.feature_extraction(seq.frame(k), lid, opts=pfref.FE_STABLE_TIES)
+        cl = pfsynth.bpf_split(e, s)
+        if k == 0:
+            od.init_map(*cl)
+            st = od.stats()
+            assert st["n_map"] == [len(c) for c in cl]
+            continue
+        p = od.update(*cl)
+        assert abs(np.linalg.norm(p[:4]) - 1) < 1e-14
+    st = od.stats()
+    assert all(n > 50 for n in st["n_res"]) and not st["map_too_small"]
+    assert st["n_edge_res"] == st["n_res"][0] and st["n_surf_res"] == st["n_res"][1]
+    assert np.linalg.norm(p[4:] - seq.gt_pose(24)[4:]) < 0.2
+    # the per-class maps stay separate: each rgbds output is voxel-unique at its own leaf
+    for c, leaf in ((0, 0.4), (1, 0.4), (2, 0.8)):
+        xyz, rg = od.get_map(c)
+        assert xyz.shape[0] == st["n_map"][c] and (rg[:, 0] >= 2).all()
