@@ -84,22 +84,23 @@ __global__ void __launch_bounds__(256) k_grid_bounds(GridPtrs gp, int* __restric
         const float4 p = gp.m[mi][i - gi.start(mi)];
         const int c[3] = {(int)floorf(p.x), (int)floorf(p.y), (int)floorf(p.z)};
 #pragma unroll
-        for (int mm = 0; mm < kGridMaps; ++mm) {
-            if (mm != mi) continue;                   // static register indices
+        for (int mm = 0; mm < kGridMaps; ++mm) {      // branch-free: static register indices
+            const bool mine = mm == mi;
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                v[6 * mm + k] = min(v[6 * mm + k], c[k]);
-                v[6 * mm + 3 + k] = max(v[6 * mm + 3 + k], c[k]);
+                v[6 * mm + k] = mine ? min(v[6 * mm + k], c[k]) : v[6 * mm + k];
+                v[6 * mm + 3 + k] = mine ? max(v[6 * mm + 3 + k], c[k]) : v[6 * mm + 3 + k];
             }
         }
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
+        if (k >= 6 * gp.nm) break;                    // uniform: maps not built
         const int r = ((k % 6) < 3) ? wave_min_i(v[k]) : wave_max_i(v[k]);
         if (l == 0) red[w][k] = r;
     }
     __syncthreads();
-    if (threadIdx.x < NB) {
+    if (threadIdx.x < 6 * gp.nm) {
         const int k = threadIdx.x;
         const bool is_min = (k % 6) < 3;
         int r = red[0][k];

@@ -28,7 +28,10 @@ namespace pf {
 namespace {
 
 constexpr u32 kSentinel = 0xFFFFFFFFu;
-struct VgLeaf { float v[kMaxC]; };     // per-class leaf sizes
+struct VgLeaf {                        // per-class leaf sizes
+    float v[kMaxC];
+    __device__ __forceinline__ float at(int c) const { return c == 0 ? v[0] : (c == 1 ? v[1] : v[2]); }
+};
 constexpr int kGrid = 512;   // grid-stride workgroups for per-point kernels
 
 __device__ __forceinline__ float wave_minf(float v) {
@@ -64,23 +67,38 @@ __device__ __forceinline__ float4 associate(const double* prm, float4 p) {
     return make_float4((float)w.x, (float)w.y, (float)w.z, p.w);
 }
 
+// per-class values picked with selects: a per-lane class index into an array would put the array
+// in scratch memory
+template <class T>
+__device__ __forceinline__ T sel3(int c, T a, T b, T d) { return c == 0 ? a : (c == 1 ? b : d); }
+
 // per-class pointer sets passed by value (kernel arguments)
-struct Clouds { const float4* p[kMaxC]; };
-struct CloudsW { float4* p[kMaxC]; };
+struct Clouds {
+    const float4* p[kMaxC];
+    __device__ __forceinline__ const float4* at(int c) const { return sel3(c, p[0], p[1], p[2]); }
+};
+struct CloudsW {
+    float4* p[kMaxC];
+    __device__ __forceinline__ float4* at(int c) const { return sel3(c, p[0], p[1], p[2]); }
+};
 
 // a concatenation of per-class ranges: element i belongs to class cls(i) at local index i - start(c)
+template <int NC>
 struct CatIdx {
     int end[kMaxC];
-    __device__ __forceinline__ int total() const { return end[kMaxC - 1]; }
-    __device__ __forceinline__ int cls(int i) const { return i < end[0] ? 0 : (i < end[1] ? 1 : 2); }
-    __device__ __forceinline__ int start(int c) const { return c == 0 ? 0 : end[c - 1]; }
+    __device__ __forceinline__ int total() const { return end[NC - 1]; }
+    __device__ __forceinline__ int cls(int i) const {
+        return NC == 2 ? (i < end[0] ? 0 : 1) : (i < end[0] ? 0 : (i < end[1] ? 1 : 2));
+    }
+    __device__ __forceinline__ int start(int c) const { return c == 0 ? 0 : (c == 1 ? end[0] : end[1]); }
 };
-__device__ __forceinline__ CatIdx cat_idx(const int* counts, int nc) {
-    CatIdx x;
+template <int NC>
+__device__ __forceinline__ CatIdx<NC> cat_idx(const int* counts) {
+    CatIdx<NC> x;
     int acc = 0;
 #pragma unroll
     for (int k = 0; k < kMaxC; ++k) {
-        acc += k < nc ? counts[k] : 0;
+        acc += k < NC ? counts[k] : 0;
         x.end[k] = acc;
     }
     return x;
@@ -88,16 +106,17 @@ __device__ __forceinline__ CatIdx cat_idx(const int* counts, int nc) {
 
 // per-class float min/max of xyz reduced over the workgroup, one atomic per value and workgroup;
 // v[6 c + k]: min (k < 3) / max (k >= 3) of class c
-__device__ __forceinline__ void minmax_commit(float (&v)[6 * kMaxC], u32* acc) {
+__device__ __forceinline__ void minmax_commit(float (&v)[6 * kMaxC], u32* acc, int nc) {
     __shared__ float red[4][6 * kMaxC];
     const int w = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < 6 * kMaxC; ++k) {
+        if (k >= 6 * nc) break;                    // uniform: classes the handle does not have
         const float r = ((k % 6) < 3) ? wave_minf(v[k]) : wave_maxf(v[k]);
         if (lane_id() == 0) red[w][k] = r;
     }
     __syncthreads();
-    if (threadIdx.x < 6 * kMaxC) {
+    if (threadIdx.x < 6 * nc) {
         const int k = threadIdx.x;
         float r = red[0][k];
         for (int ww = 1; ww < 4; ++ww) r = ((k % 6) < 3) ? fminf(r, red[ww][k]) : fmaxf(r, red[ww][k]);
@@ -108,15 +127,17 @@ __device__ __forceinline__ void minmax_commit(float (&v)[6 * kMaxC], u32* acc) {
         }
     }
 }
+// branch-free per class (a branch per class lets the compiler turn v[] into a scratch array indexed
+// by the class)
 __device__ __forceinline__ void minmax_add(float (&v)[6 * kMaxC], int c, float4 p) {
     const float xyz[3] = {p.x, p.y, p.z};
 #pragma unroll
     for (int cc = 0; cc < kMaxC; ++cc) {
-        if (cc != c) continue;                     // static register indices
+        const bool mine = cc == c;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            v[6 * cc + k] = fminf(v[6 * cc + k], xyz[k]);
-            v[6 * cc + 3 + k] = fmaxf(v[6 * cc + 3 + k], xyz[k]);
+            v[6 * cc + k] = mine ? fminf(v[6 * cc + k], xyz[k]) : v[6 * cc + k];
+            v[6 * cc + 3 + k] = mine ? fmaxf(v[6 * cc + 3 + k], xyz[k]) : v[6 * cc + 3 + k];
         }
     }
 }
@@ -176,30 +197,32 @@ __global__ void k_vg_begin(int* __restrict__ scnt, u32* __restrict__ acc, int nc
 }
 
 // ----------------------------------- VoxelGrid (B.1) ------------------------------------------
-__global__ void __launch_bounds__(256) k_vg_minmax(Clouds in, const int* __restrict__ cnt, u32* __restrict__ acc,
-                                                    int nc) {
-    const CatIdx ci = cat_idx(cnt + C_IN, nc);
+template <int NC>
+__global__ void __launch_bounds__(256) k_vg_minmax(Clouds in, const int* __restrict__ cnt, u32* __restrict__ acc) {
+    constexpr int nc = NC;
+    const CatIdx<NC> ci = cat_idx<NC>(cnt + C_IN);
     float v[6 * kMaxC];
     minmax_init(v);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ci.total(); i += gridDim.x * blockDim.x) {
         const int c = ci.cls(i);
-        minmax_add(v, c, in.p[c][i - ci.start(c)]);
+        minmax_add(v, c, in.at(c)[i - ci.start(c)]);
     }
-    minmax_commit(v, acc + A_VG);
+    minmax_commit(v, acc + A_VG, nc);
 }
 
 // keys: class in bits 30-31, the voxel index below (sorted by class, then voxel)
+template <int NC>
 __global__ void __launch_bounds__(256) k_vg_keys(Clouds in, const int* __restrict__ cnt, const u32* __restrict__ acc,
-                                                  int nc, VgLeaf leaf, u32* __restrict__ keys, u32* __restrict__ vals,
+                                                  VgLeaf leaf, u32* __restrict__ keys, u32* __restrict__ vals,
                                                   SortHist sh) {
     __shared__ u32 lh[4][256];
     sort_hist_begin(lh);
-    const CatIdx ci = cat_idx(cnt + C_IN, nc);
+    const CatIdx<NC> ci = cat_idx<NC>(cnt + C_IN);
     const int n = ci.total();
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int c = ci.cls(i);
-        const float4 p = in.p[c][i - ci.start(c)];
-        const float inv = 1.0f / leaf.v[c];                      // inverse_leaf_size_
+        const float4 p = in.at(c)[i - ci.start(c)];
+        const float inv = 1.0f / leaf.at(c);                      // inverse_leaf_size_
         const u32* a = acc + A_VG + 6 * c;
         const float mn[3] = {ord2f(a[0]), ord2f(a[1]), ord2f(a[2])};
         const float mx[3] = {ord2f(a[3]), ord2f(a[4]), ord2f(a[5])};
@@ -233,10 +256,12 @@ __global__ void __launch_bounds__(256) k_vg_keys(Clouds in, const int* __restric
 __device__ __forceinline__ float lane_f(float v, int j) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
+template <int NC>
 __global__ void __launch_bounds__(256) k_vg_reduce(Clouds in, const u32* __restrict__ keys, const u32* __restrict__ vals,
-                                                    const u32* __restrict__ segstart, int* __restrict__ cnt, int nc,
+                                                    const u32* __restrict__ segstart, int* __restrict__ cnt,
                                                     CloudsW ds) {
-    const CatIdx ci = cat_idx(cnt + C_IN, nc);
+    constexpr int nc = NC;
+    const CatIdx<NC> ci = cat_idx<NC>(cnt + C_IN);
     const int n = cnt[C_VGN];
     const int nseg = cnt[C_NSEG];
     const int nlt0 = cnt[C_NLT], nlt1 = cnt[C_NLT + 1];
@@ -251,7 +276,7 @@ __global__ void __launch_bounds__(256) k_vg_reduce(Clouds in, const u32* __restr
     for (int sg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; sg < nseg; sg += waves) {
         const u32 b0 = segstart[sg], b1 = (sg + 1 < nseg) ? segstart[sg + 1] : (u32)n;
         const int c = (int)(keys[b0] >> 30);
-        const float4* src = in.p[c];
+        const float4* src = in.at(c);
         const int s0 = ci.start(c);
         float sx = 0.f, sy = 0.f, sz = 0.f;
         for (u32 base = b0; base < b1; base += 8 * 64) {   // AccumulatorXYZ, sorted (stable) order
@@ -278,7 +303,7 @@ __global__ void __launch_bounds__(256) k_vg_reduce(Clouds in, const u32* __restr
             const float nn = (float)(b1 - b0);
             // rgb of inputs is 0 (copyPointCloud XYZI -> XYZRGB): averages stay 0
             const float4 o = make_float4(sx / nn, sy / nn, sz / nn, __uint_as_float(0u));
-            ds.p[c][sg - (c == 0 ? 0 : (c == 1 ? nlt0 : nlt1))] = o;
+            ds.at(c)[sg - (c == 0 ? 0 : (c == 1 ? nlt0 : nlt1))] = o;
         }
     }
 }
@@ -306,7 +331,7 @@ struct AssocArgs {
 // line fit (:302-331) / plane fit (:449-476), round and sparsity, p-index pair keys of query q
 __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, const int* id, int found) {
     bool valid = false;
-    const float4* mp = a.map.p[c];
+    const float4* mp = a.map.at(c);
     if (found == 5) {
         double px[5], py[5], pz[5];
         u32 rsum = 0;
@@ -386,8 +411,9 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
 #endif
 constexpr int kAssocTeam = PF_ASSOC_TEAM;
 static_assert(kAssocTeam >= 5, "k_assoc writes the 5 neighbours from 5 lanes of the team");
+template <int NC>
 __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
-    const CatIdx qi = cat_idx(a.cnt + C_DS, a.cls.nc);
+    const CatIdx<NC> qi = cat_idx<NC>(a.cnt + C_DS);
     const int nq = a.cnt[C_NQ];
     const int gate = a.st->gate;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -411,7 +437,7 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
         const bool active = q0 < nq;
         const int c = active ? qi.cls(q0) : 0;
         float4 pw = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (active) pw = associate(prm, a.ds.p[c][q0 - qi.start(c)]);
+        if (active) pw = associate(prm, a.ds.at(c)[q0 - qi.start(c)]);
         float d[5];
         int id[5];
         const int found = knn5_team<kAssocTeam>(a.gv, c, pw.x, pw.y, pw.z, active, d, id);
@@ -446,8 +472,9 @@ struct ObsArgs {
     int theta_max;
 };
 
+template <int NC>
 __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
-    const CatIdx qi = cat_idx(a.cnt + C_DS, a.cls.nc);
+    const CatIdx<NC> qi = cat_idx<NC>(a.cnt + C_DS);
     const int nq = a.cnt[C_NQ];
     const int t = threadIdx.x;
     float mn[kMaxC][2], mx[kMaxC][2];
@@ -466,7 +493,7 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
             continue;
         }
         const int c = qi.cls(q);
-        const float4* mp = a.map.p[c];
+        const float4* mp = a.map.at(c);
         // c_i(n) = valid queries before q sharing neighbour n: count the smaller pair ids in n's bucket
         // (filled in any order by k_assoc: two pairs inline, the rest on an overflow list); the pair
         // with the largest id carries n's increment
@@ -510,7 +537,7 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
             a.qflag[q] = f | 2;
             a.observe[q] = observe;
             const u32 rq = (u32)min(255, int(round)), gq = (u32)min(255, int(observe));   // :354-355
-            a.ds.p[c][q - qi.start(c)].w = __uint_as_float(pack_rg(rq, gq));
+            a.ds.at(c)[q - qi.start(c)].w = __uint_as_float(pack_rg(rq, gq));
         }
         const float sp = a.spars[q];
 #pragma unroll
@@ -528,9 +555,19 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
     constexpr int NV = 6 * kMaxC;
     __shared__ u32 wred[4][NV];
     const int w = t >> 6;
+    constexpr int nc = NC;
     u32 v[NV];
 #pragma unroll
     for (int c = 0; c < kMaxC; ++c) {
+        if (c >= nc) {                             // uniform: classes the handle does not have
+            v[2 * c] = v[2 * c + 1] = 0u;
+#pragma unroll
+            for (int ww = 0; ww < 2; ++ww) {
+                v[2 * kMaxC + 4 * c + 2 * ww] = f2ord(FLT_MAX);
+                v[2 * kMaxC + 4 * c + 2 * ww + 1] = f2ord(-FLT_MAX);
+            }
+            continue;
+        }
         v[2 * c] = (u32)wave_sum_i(nvalid[c]);
         v[2 * c + 1] = (u32)wave_sum_i(nkept[c]);
 #pragma unroll
@@ -566,13 +603,14 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
 // the p-index increments of an outer iteration: g = min(255, g + 1) once per valid query sharing the
 // map point (:345-346, :493-496), applied by the last pair of each map point's list, which also
 // empties the list for the next iteration
-__device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, int n, const CatIdx& qi, CloudsW map,
+template <int NC>
+__device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, int n, const CatIdx<NC>& qi, CloudsW map,
                                            int4* pbkt, u32 map_cap) {
     for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const u32 inc = tailinc[p];
         if (!inc) continue;
         const int c = qi.cls(p / 5);
-        float4* mp = map.p[c];
+        float4* mp = map.at(c);
         const int idx = nbr[p];
         const float4 m = mp[idx];
         const u32 g = min(255u, w_g(m) + inc);
@@ -873,6 +911,7 @@ struct LmArgs {
     u32 map_cap;
 };
 
+template <int NC>
 __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     unsigned long long* dbg = a.dbg;
     const bool rec = dbg && blockIdx.x == 0 && threadIdx.x == 0;
@@ -887,9 +926,9 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     const int t = threadIdx.x;
     // the map's p-index bytes are not read by the solve: this iteration's increments are applied
     // while the blocks wait for the first evaluation's arrivals (or here, when there is no solve)
-    const CatIdx qi = cat_idx(a.cnt + C_DS, a.cls.nc);
+    const CatIdx<NC> qi = cat_idx<NC>(a.cnt + C_DS);
     int nres = 0;
-    for (int c = 0; c < a.cls.nc; ++c) nres += a.cnt[C_KEPT + c];
+    for (int c = 0; c < NC; ++c) nres += a.cnt[C_KEPT + c];
     if (!a.st->gate || nres == 0) {                              // no residual blocks: untouched
         pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
         return;
@@ -935,13 +974,15 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             double J[6] = {0, 0, 0, 0, 0, 0}, r = 0.0, hc = 0.0;
             if (q < nq && (a.qflag[q] & 2)) {
                 const int c = qi.cls(q);
-                const bool plane = a.cls.is_plane(c);
-                const float4 p = a.ds.p[c][q - qi.start(c)];
+                const bool plane = c == NC - 1;                  // the last class is the plane class
+                const float4 p = a.ds.at(c)[q - qi.start(c)];
                 const d3 cur{(double)p.x, (double)p.y, (double)p.z};
                 double wgt = 0.0;
                 if (wt != 0) {
-                    const double wo = norm_weight((double)a.observe[q], wmin[c][0], wmax[c][0], true);
-                    const double ws = norm_weight((double)a.spars[q], wmin[c][1], wmax[c][1], false);
+                    const double wo = norm_weight((double)a.observe[q], sel3(c, wmin[0][0], wmin[1][0], wmin[2][0]),
+                                                  sel3(c, wmax[0][0], wmax[1][0], wmax[2][0]), true);
+                    const double ws = norm_weight((double)a.spars[q], sel3(c, wmin[0][1], wmin[1][1], wmin[2][1]),
+                                                  sel3(c, wmax[0][1], wmax[1][1], wmax[2][1]), false);
                     if (wt == 1) wgt = wo;
                     else if (wt == 2) wgt = ws;
                     else wgt = plane ? (wo + ws) / 2 : (ws + wo) / 2;     // :418 / :565 operand order
@@ -1091,30 +1132,39 @@ __global__ void k_finalize(DevState* __restrict__ st, double* __restrict__ poses
 }
 
 // the rgbds input of every class: its map, then its appended points (map c, app c, in class order)
+template <int NC>
 struct RgView {
-    const float4* src[2 * kMaxC];
-    int end[2 * kMaxC];
-    __device__ __forceinline__ int total() const { return end[2 * kMaxC - 1]; }
+    Clouds map, app;
+    int m[kMaxC];          // map sizes
+    int end[kMaxC];        // cumulative (map + appended) sizes
+    __device__ __forceinline__ int total() const { return end[NC - 1]; }
+    // class c, local index li, appended or not, of element v
+    __device__ __forceinline__ void locate(int v, int& c, int& li, bool& appended) const {
+        c = NC == 2 ? (v < end[0] ? 0 : 1) : (v < end[0] ? 0 : (v < end[1] ? 1 : 2));
+        const int l = v - sel3(c, 0, end[0], end[1]);
+        const int mc = sel3(c, m[0], m[1], m[2]);
+        appended = l >= mc;
+        li = appended ? l - mc : l;
+    }
     __device__ __forceinline__ float4 at(int v, int& c) const {
-        int r = 0;
-#pragma unroll
-        for (int k = 0; k < 2 * kMaxC - 1; ++k) r += v >= end[k] ? 1 : 0;
-        c = r >> 1;
-        return src[r][v - (r ? end[r - 1] : 0)];
+        int li;
+        bool ap;
+        locate(v, c, li, ap);
+        return (ap ? app.at(c) : map.at(c))[li];
     }
 };
 
-__device__ __forceinline__ RgView rg_view(const int* cnt, int nc, Clouds map, Clouds app) {
-    RgView V;
+template <int NC>
+__device__ __forceinline__ RgView<NC> rg_view(const int* cnt, Clouds map, Clouds app) {
+    RgView<NC> V;
+    V.map = map;
+    V.app = app;
     int acc = 0;
 #pragma unroll
     for (int c = 0; c < kMaxC; ++c) {
-        V.src[2 * c] = map.p[c];
-        V.src[2 * c + 1] = app.p[c];
-        acc += c < nc ? cnt[C_M + c] : 0;
-        V.end[2 * c] = acc;
-        acc += c < nc ? cnt[C_DS + c] : 0;
-        V.end[2 * c + 1] = acc;
+        V.m[c] = c < NC ? cnt[C_M + c] : 0;
+        acc += c < NC ? cnt[C_M + c] + cnt[C_DS + c] : 0;
+        V.end[c] = acc;
     }
     return V;
 }
@@ -1130,44 +1180,46 @@ __device__ __forceinline__ bool in_crop(const DevState* st, float4 p) {
 // transform / append of the down-sampled clouds (:592-604, r and g carried) and the CropBox-kept
 // min / max of every class for the rgbds grids (:606-615, :40-51). The crop box is odom.t +- 100,
 // and odom.t is the solved translation params[4..6] that block 0 stores.
+template <int NC>
 __global__ void __launch_bounds__(256) k_rg_append_minmax(DevState* __restrict__ st, int* __restrict__ cnt,
-                                                           u32* __restrict__ acc, int nc, Clouds map, Clouds ds,
+                                                           u32* __restrict__ acc, Clouds map, Clouds ds,
                                                            CloudsW app, double* __restrict__ poses, int pose_cap) {
     double prm[7];
     for (int k = 0; k < 7; ++k) prm[k] = st->params[k];
     if (blockIdx.x == 0) finalize_pose(st, poses, pose_cap, 1, acc, prm);
     const float lox = (float)(prm[4] - 100), loy = (float)(prm[5] - 100), loz = (float)(prm[6] - 100);   // in_crop
     const float hix = (float)(prm[4] + 100), hiy = (float)(prm[5] + 100), hiz = (float)(prm[6] + 100);
-    const RgView V = rg_view(cnt, nc, map, Clouds{{app.p[0], app.p[1], app.p[2]}});
+    constexpr int nc = NC;
+    const RgView<NC> V = rg_view<NC>(cnt, map, Clouds{{app.p[0], app.p[1], app.p[2]}});
     const int n = V.total();
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt[C_NRG] = n;
     float v[6 * kMaxC];
     minmax_init(v);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        int r = 0;
-#pragma unroll
-        for (int k = 0; k < 2 * kMaxC - 1; ++k) r += i >= V.end[k] ? 1 : 0;
-        const int c = r >> 1, li = i - (r ? V.end[r - 1] : 0);
+        int c, li;
+        bool ap;
+        V.locate(i, c, li, ap);
         float4 p;
-        if (r & 1) {                                   // appended: pointAssociateToMap of the ds point
-            p = associate(prm, ds.p[c][li]);
-            app.p[c][li] = p;
+        if (ap) {                                      // appended: pointAssociateToMap of the ds point
+            p = associate(prm, ds.at(c)[li]);
+            app.at(c)[li] = p;
         } else {
-            p = map.p[c][li];
+            p = map.at(c)[li];
         }
         if ((p.x < lox || p.y < loy || p.z < loz) || (p.x > hix || p.y > hiy || p.z > hiz)) continue;
         minmax_add(v, c, p);
     }
-    minmax_commit(v, acc + A_RG);
+    minmax_commit(v, acc + A_RG, nc);
 }
 
+template <int NC>
 __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st, const int* __restrict__ cnt,
-                                                  const u32* __restrict__ acc, int nc, Clouds map, Clouds app,
+                                                  const u32* __restrict__ acc, Clouds map, Clouds app,
                                                   VgLeaf leaf, u32* __restrict__ keys, u32* __restrict__ vals,
                                                   SortHist sh) {
     __shared__ u32 lh[4][256];
     sort_hist_begin(lh);
-    const RgView V = rg_view(cnt, nc, map, app);
+    const RgView<NC> V = rg_view<NC>(cnt, map, app);
     const int n = V.total();
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         int c;
@@ -1178,7 +1230,7 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
             sort_hist_add(lh, kSentinel, sh.passes);
             continue;
         }
-        const float lf = leaf.v[c];
+        const float lf = leaf.at(c);
         const u32* a = acc + A_RG + 6 * c;
         int minb[3], div[3];
         for (int k = 0; k < 3; ++k) {                                // :46-56 (f32 division)
@@ -1209,8 +1261,9 @@ struct RgReduceArgs {
     int theta_max;
 };
 
+template <int NC>
 __global__ void __launch_bounds__(256) k_rg_reduce(RgReduceArgs a) {
-    const RgView V = rg_view(a.cnt, a.nc, a.map, a.app);
+    const RgView<NC> V = rg_view<NC>(a.cnt, a.map, a.app);
     const int nseg = a.cnt[C_NSEG], nvalid = a.cnt[C_NRG_VALID];
     for (int sg = blockIdx.x * blockDim.x + threadIdx.x; sg < nseg; sg += gridDim.x * blockDim.x) {
         const u32 b0 = a.segstart[sg], b1 = (sg + 1 < nseg) ? a.segstart[sg + 1] : (u32)nvalid;
@@ -1237,9 +1290,11 @@ __global__ void __launch_bounds__(256) k_rg_reduce(RgReduceArgs a) {
 }
 
 // compaction: class c's kept voxels are the kept segments in [nlt(c), nlt(c + 1)), in order
-__global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, int nc, const float4* __restrict__ seg_out,
+template <int NC>
+__global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const float4* __restrict__ seg_out,
                                                    const u32* __restrict__ keep, const u32* __restrict__ pos,
                                                    CloudsW map) {
+    constexpr int nc = NC;
     const int nseg = cnt[C_NSEG], total = cnt[C_KEEP_TOTAL];
     int sb[kMaxC + 1], kb[kMaxC + 1];             // segment / kept-voxel start of every class
     sb[0] = 0;
@@ -1253,18 +1308,19 @@ __global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, int nc,
         for (int c = 0; c < nc; ++c) cnt[C_M + c] = kb[c + 1] - kb[c];
     for (int sg = blockIdx.x * blockDim.x + threadIdx.x; sg < nseg; sg += gridDim.x * blockDim.x) {
         if (!keep[sg]) continue;
-        const int c = sg < sb[1] ? 0 : (sg < sb[2] ? 1 : 2);
-        map.p[c][(int)pos[sg] - kb[c]] = seg_out[sg];
+        const int c = NC == 2 ? (sg < sb[1] ? 0 : 1) : (sg < sb[1] ? 0 : (sg < sb[2] ? 1 : 2));
+        map.at(c)[(int)pos[sg] - sel3(c, kb[0], kb[1], kb[2])] = seg_out[sg];
     }
 }
 
 // initMapWithPoints (ES :217-222, BPF :685-691): append the raw clouds (r = g = 0)
-__global__ void __launch_bounds__(256) k_init_map(const int* __restrict__ cnt, int nc, Clouds in, CloudsW map) {
-    const CatIdx ci = cat_idx(cnt + C_IN, nc);
+template <int NC>
+__global__ void __launch_bounds__(256) k_init_map(const int* __restrict__ cnt, Clouds in, CloudsW map) {
+    const CatIdx<NC> ci = cat_idx<NC>(cnt + C_IN);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ci.total(); i += gridDim.x * blockDim.x) {
         const int c = ci.cls(i);
-        const float4 p = in.p[c][i - ci.start(c)];
-        map.p[c][cnt[C_M + c] + i - ci.start(c)] = make_float4(p.x, p.y, p.z, __uint_as_float(0u));
+        const float4 p = in.at(c)[i - ci.start(c)];
+        map.at(c)[cnt[C_M + c] + i - ci.start(c)] = make_float4(p.x, p.y, p.z, __uint_as_float(0u));
     }
 }
 
@@ -1413,6 +1469,13 @@ void odom_destroy(OdomGPU& o) {
 }
 
 static Clouds clouds(float4* const* p) { return Clouds{{p[0], p[1], p[2]}}; }
+
+// kernels specialised on the class count (2: ES, 3: BPF)
+#define PF_LAUNCH_NC(nc, kern, ...)                                   \
+    do {                                                              \
+        if ((nc) == 3) hipLaunchKernelGGL(kern<3>, __VA_ARGS__);      \
+        else hipLaunchKernelGGL(kern<2>, __VA_ARGS__);                \
+    } while (0)
 static CloudsW clouds_w(float4* const* p) { return CloudsW{{p[0], p[1], p[2]}}; }
 
 void stage_enqueue_fe(OdomGPU& o, int p, const float4* d_in, hipStream_t s) {
@@ -1427,20 +1490,20 @@ void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s) {
     const VgLeaf leaf{{o.leaf_vg[0], o.leaf_vg[1], o.leaf_vg[2]}};
     // VoxelGrid of every class (:242-245, BPF :714-719); pose independent, so it runs ahead on stream A
     hipLaunchKernelGGL(k_vg_begin, dim3(1), dim3(64), 0, s, cnt, o.acc_a, nc);
-    hipLaunchKernelGGL(k_vg_minmax, dim3(128), dim3(256), 0, s, clouds(sb.in), cnt, o.acc_a, nc);
-    hipLaunchKernelGGL(k_vg_keys, dim3(kGrid), dim3(256), 0, s, clouds(sb.in), cnt, o.acc_a, nc, leaf, o.vkeys,
-                       o.vvals, sort_hist(o.vprim, 32, true));
+    PF_LAUNCH_NC(nc, k_vg_minmax, dim3(128), dim3(256), 0, s, clouds(sb.in), cnt, o.acc_a);
+    PF_LAUNCH_NC(nc, k_vg_keys, dim3(kGrid), dim3(256), 0, s, clouds(sb.in), cnt, o.acc_a, leaf, o.vkeys, o.vvals,
+                 sort_hist(o.vprim, 32, true));
     radix_sort_pairs(o.vkeys, o.vvals, cnt + C_VGN, 32, o.vprim, s, nullptr, nullptr, true);
     segment_starts(o.vkeys, cnt + C_VGN, o.vsegstart, cnt + C_NSEG, cnt + C_NLT, cnt + C_NRG_VALID, o.vprim, s);
-    hipLaunchKernelGGL(k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, clouds(sb.in), o.vkeys, o.vvals, o.vsegstart,
-                       cnt, nc, clouds_w(sb.ds));
+    PF_LAUNCH_NC(nc, k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, clouds(sb.in), o.vkeys, o.vvals, o.vsegstart, cnt,
+                 clouds_w(sb.ds));
 }
 
 void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s) {
     StageBuf& sb = o.sb[p];
     const int nc = o.cls.nc;
     hipLaunchKernelGGL(k_pull_counts, dim3(1), dim3(64), 0, s, o.cnt, sb.cnt);
-    hipLaunchKernelGGL(k_init_map, dim3(kGrid), dim3(256), 0, s, o.cnt, nc, clouds(sb.in), clouds_w(o.map));
+    PF_LAUNCH_NC(nc, k_init_map, dim3(kGrid), dim3(256), 0, s, o.cnt, clouds(sb.in), clouds_w(o.map));
     hipLaunchKernelGGL(k_init_counts, dim3(1), dim3(64), 0, s, o.cnt, o.st, nc);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, o.st, o.poses, (int)o.pose_cap, 0, o.acc);
     o.opt_count_host = 12;
@@ -1462,28 +1525,27 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     for (int it = 0; it < o.opt_count_host; ++it) {
         AssocArgs aa{o.st, cnt, o.acc, gv, o.cls, clouds(sb.ds), clouds(o.map), o.nbr, o.qflag, o.geo, o.spars,
                      o.roundv, o.pbkt, o.pnext, (u32)o.map_cap, o.lm_ticket};
-        hipLaunchKernelGGL(k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
+        PF_LAUNCH_NC(nc, k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
         ObsArgs oa{cnt, o.acc, o.cls, clouds(o.map), clouds_w(sb.ds), o.nbr, o.qflag, o.pbkt, o.pnext, o.tailinc,
                    (u32)o.map_cap, o.roundv, o.spars, o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
-        hipLaunchKernelGGL(k_observe, dim3(kGrid), dim3(256), 0, s, oa);
+        PF_LAUNCH_NC(nc, k_observe, dim3(kGrid), dim3(256), 0, s, oa);
         LmArgs la{o.st, cnt, o.acc, o.cls, o.lm, o.lm_part, o.lm_ticket, o.qflag, clouds(sb.ds), o.geo, o.observe,
                   o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.pbkt, clouds_w(o.map), (u32)o.map_cap};
-        hipLaunchKernelGGL(k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
+        PF_LAUNCH_NC(nc, k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
     }
     // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647, BPF :1197-1290)
     const VgLeaf leaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}};
-    hipLaunchKernelGGL(k_rg_append_minmax, dim3(256), dim3(256), 0, s, o.st, cnt, o.acc, nc, clouds(o.map),
-                       clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap);
-    hipLaunchKernelGGL(k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, nc, clouds(o.map), clouds(o.app),
-                       leaf, o.keys, o.vals, sort_hist(o.prim, 32, true));
+    PF_LAUNCH_NC(nc, k_rg_append_minmax, dim3(256), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map), clouds(sb.ds),
+                 clouds_w(o.app), o.poses, (int)o.pose_cap);
+    PF_LAUNCH_NC(nc, k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map), clouds(o.app), leaf,
+                 o.keys, o.vals, sort_hist(o.prim, 32, true));
     radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
     segment_starts(o.keys, cnt + C_NRG, o.segstart, cnt + C_NSEG, cnt + C_NLT, cnt + C_NRG_VALID, o.prim, s);
     RgReduceArgs ra{cnt, nc, clouds(o.map), clouds(o.app), o.keys, o.vals, o.segstart, o.seg_out, o.flags,
                     o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
-    hipLaunchKernelGGL(k_rg_reduce, dim3(kGrid), dim3(256), 0, s, ra);
+    PF_LAUNCH_NC(nc, k_rg_reduce, dim3(kGrid), dim3(256), 0, s, ra);
     scan_exclusive(o.flags, o.scan_out, cnt + C_NSEG, (u32*)(cnt + C_KEEP_TOTAL), o.prim, s);
-    hipLaunchKernelGGL(k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, nc, o.seg_out, o.flags, o.scan_out,
-                       clouds_w(o.map));
+    PF_LAUNCH_NC(nc, k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, o.flags, o.scan_out, clouds_w(o.map));
 }
 
 }  // namespace pf

@@ -115,12 +115,13 @@ def lib():
     L.pf_knn_set_map.argtypes = [_vp, _vp, _sz]
     L.pf_knn_query.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.pf_knn_bench.argtypes = [_vp, _i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
-    L.pf_bpf_create.argtypes = [ctypes.POINTER(LidarParams), ctypes.POINTER(OdomParams), _i, _sz, _sz,
-                                ctypes.POINTER(_vp)]
-    L.pf_bpf_init_map.argtypes = [_vp, _vp, _sz, _sz, _vp, _sz, _sz, _vp, _sz, _sz]
-    L.pf_bpf_update.argtypes = [_vp, _vp, _sz, _sz, _vp, _sz, _sz, _vp, _sz, _sz, _vp]
-    L.pf_bpf_frame_device.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp]
-    L.pf_odom_classes.argtypes = [_vp]
+    if hasattr(L, "pf_bpf_create"):     # (absent only in an older library loaded for an A/B run)
+        L.pf_bpf_create.argtypes = [ctypes.POINTER(LidarParams), ctypes.POINTER(OdomParams), _i, _sz, _sz,
+                                    ctypes.POINTER(_vp)]
+        L.pf_bpf_init_map.argtypes = [_vp, _vp, _sz, _sz, _vp, _sz, _sz, _vp, _sz, _sz]
+        L.pf_bpf_update.argtypes = [_vp, _vp, _sz, _sz, _vp, _sz, _sz, _vp, _sz, _sz, _vp]
+        L.pf_bpf_frame_device.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp]
+        L.pf_odom_classes.argtypes = [_vp]
     _lib = L
     return L
 

@@ -1,10 +1,12 @@
 #!/bin/bash
-# A/B of whole-pipeline variants (tools/build_variant.sh): odometry parity tests + bench frames/s.
+# A/B of whole-pipeline variants (tools/build_variant.sh or an older build under var/): bench frames/s,
+# each library run twice in alternation so box drift shows.
 #   tools/bench_ab.sh [variant ...]   ("" = the in-tree library)
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
+for rep in 1 2; do
 for v in "" "$@"; do
-  if [ -n "$v" ]; then export PFILTER_HIP_LIB=pfilter-noetic_amd/var/$v/libpfilter_hip.so; fi
-  echo "== ${v:-main} tests: $(timeout -k 10 300 python -m pytest -x -q -p no:cacheprovider tests/test_gpu_odom.py tests/test_gpu_knn.py -m gpu 2>&1 | tail -1)" || exit 1
-  echo "== ${v:-main} $(timeout -k 10 200 python bench.py --no-cpu --no-roofline | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"])')" || exit 1
+  if [ -n "$v" ]; then export PFILTER_HIP_LIB=pfilter-noetic_amd/var/$v/libpfilter_hip.so; else unset PFILTER_HIP_LIB; fi
+  echo "== ${v:-main} $(timeout -k 10 200 python bench.py --no-cpu --no-roofline --bpf-frames 0 | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"])')" || exit 1
+done
 done
