@@ -84,10 +84,16 @@ int pf_fe_extract(pf_fe* h, const float* xyzi, size_t n, size_t stride_bytes, fl
 
 /* ---------------- odometry (Odom_ES_EstimationClass) ---------------- */
 typedef struct pf_odom pf_odom;
-/* max_points: largest raw scan / edge / surf input; map_capacity: largest local map (per map). */
+/* max_points: largest raw scan / edge / surf input; map_capacity: largest local map (per map).
+ * A device admits CUs / 32 live odometry handles (ES and BPF together; 8 on an MI355X): the LM solve
+ * of every handle may be in flight at once and needs 32 co-resident workgroups. Beyond that,
+ * pf_odom_create / pf_bpf_create return PF_EUNSUPPORTED. */
 int pf_odom_create(const pf_lidar_params* lidar, const pf_odom_params* params, int device,
                    size_t max_points, size_t map_capacity, pf_odom** out);
 int pf_odom_destroy(pf_odom* h);
+/* back to the state right after create/init (identity pose, empty maps; the next frame or init_map
+ * seeds the maps), keeping allocations and captured graphs: the next sequence on the same handle */
+int pf_odom_reset(pf_odom* h);
 /* edge/surf: points with x,y,z at offsets 0,4,8 and the given stride (16 packed, 32 PCL). */
 int pf_odom_init_map(pf_odom* h, const float* edge, size_t ne, size_t edge_stride, const float* surf,
                      size_t ns, size_t surf_stride);

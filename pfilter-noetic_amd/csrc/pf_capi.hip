@@ -1,6 +1,8 @@
 // C ABI (include/pfilter_hip.h) over the device pipeline. Host code here only stages inputs,
 // enqueues work on the handle's stream and copies results back; all arithmetic is on the device.
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -47,7 +49,14 @@ struct pf_fe {
 struct pf_odom {
     OdomGPU o;
     std::vector<float4> host[kMaxC];
+    bool counted = false;
 };
+
+namespace {
+// live odometry handles per device (odom_max_handles: the LM solves' co-residency bound)
+std::mutex g_live_mu;
+std::map<int, int> g_live;
+}  // namespace
 
 extern "C" {
 
@@ -127,8 +136,18 @@ static int create(const pf_lidar_params* lidar, const pf_odom_params* params, in
     if (max_points == 0) max_points = 300000;
     if (map_capacity == 0) map_capacity = (size_t)1 << 22;
     PF_HIP_TRY(hipSetDevice(device));
+    {
+        std::lock_guard<std::mutex> lk(g_live_mu);
+        if (g_live[device] >= odom_max_handles(device)) return PF_EUNSUPPORTED;
+        ++g_live[device];
+    }
     pf_odom* h = new (std::nothrow) pf_odom();
-    if (!h) return PF_ENOMEM;
+    if (!h) {
+        std::lock_guard<std::mutex> lk(g_live_mu);
+        --g_live[device];
+        return PF_ENOMEM;
+    }
+    h->counted = true;
     int rc = odom_create(h->o, *lidar, *params, device, max_points, map_capacity, nc);
     if (rc != PF_OK) {
         pf_odom_destroy(h);
@@ -155,9 +174,20 @@ int pf_odom_destroy(pf_odom* h) {
     (void)hipSetDevice(h->o.device);
     (void)hipStreamSynchronize(h->o.stream_a);
     (void)hipStreamSynchronize(h->o.stream);
+    const int device = h->o.device;
     odom_destroy(h->o);
+    if (h->counted) {
+        std::lock_guard<std::mutex> lk(g_live_mu);
+        --g_live[device];
+    }
     delete h;
     return PF_OK;
+}
+
+int pf_odom_reset(pf_odom* h) {
+    if (!h) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    return odom_reset(h->o);
 }
 
 // Frame k uses pipeline slot k % kSlots. Stage A (featureExtraction / VoxelGrid or host staging) of

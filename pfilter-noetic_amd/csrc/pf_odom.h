@@ -143,6 +143,10 @@ struct OdomGPU {
 int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& prm, int device, size_t in_cap,
                 size_t map_cap, int nc = 2);
 void odom_destroy(OdomGPU& o);
+int odom_reset(OdomGPU& o);
+// live handles a device admits: the LM solve of every handle may be in flight at once and each needs
+// kLmBlocks co-resident workgroups of one CU each (pf_odom.hip)
+int odom_max_handles(int device);
 // stage A: featureExtraction of d_in[0 .. sb[p].cnt[C_NIN]) into slot p's classes 0 / 1 (ES)
 void stage_enqueue_fe(OdomGPU& o, int p, const float4* d_in, hipStream_t s);
 // stage A: VoxelGrid of slot p's class clouds (counts sb[p].cnt[C_IN + c])

@@ -628,7 +628,9 @@ __device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, i
 // block order and takes the LM step itself (TrustRegionMinimizer + LevenbergMarquardtStrategy).
 // The step is a deterministic function of identical inputs, so every block holds the same LM state
 // and no state is broadcast. 32 blocks of 256 threads are far below one wave per CU, so all blocks
-// are co-resident; a poll that exceeds its bound sets C_ERR and leaves (no hang).
+// are co-resident; a poll that exceeds its bound sets C_ERR and leaves (no hang). A block needs a
+// whole CU (374 VGPRs: one wave per SIMD), so co-residency holds while at most CUs / kLmBlocks
+// solves run at once on a device: the C ABI admits that many live handles per device (8 on MI355X).
 #ifndef PF_LM_BLOCKS
 #define PF_LM_BLOCKS 32
 #endif
@@ -1434,6 +1436,36 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)nc * map_cap);   // all empty
     if (hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
     o.opt_count_host = 2;
+    return PF_OK;
+}
+
+int odom_max_handles(int device) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 1;
+    return cus / kLmBlocks > 0 ? cus / kLmBlocks : 1;
+}
+
+// back to the state after init (identity pose, empty maps, optimization_count 2), keeping every
+// allocation and captured graph: the next frame seeds the maps again
+int odom_reset(OdomGPU& o) {
+    if (hipStreamSynchronize(o.stream_a) != hipSuccess || hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
+    DevState h{};
+    h.params[3] = 1.0;
+    for (int i = 0; i < 3; ++i) h.odomR[4 * i] = h.lastR[4 * i] = 1.0;
+    h.optimization_count = 2;
+    if (hipMemcpyAsync(o.st, &h, sizeof(h), hipMemcpyHostToDevice, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.acc, 0, sizeof(u32) * A_COUNT, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.acc_a, 0, sizeof(u32) * A_COUNT, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.lm, 0, sizeof(LMState), o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.lm_ticket, 0, sizeof(u32) * 4, o.stream) != hipSuccess) return PF_EHIP;
+    for (int p = 0; p < kSlots; ++p)
+        if (hipMemsetAsync(o.sb[p].cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
+    hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)o.cls.nc * o.map_cap);
+    if (hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
+    o.opt_count_host = 2;
+    o.inited = false;
+    o.frames = 0;
     return PF_OK;
 }
 

@@ -73,7 +73,8 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_odom_get_stats", "pf_odom_frame_device", "pf_odom_frame_host", "pf_odom_sync", "pf_odom_poses",
            "pf_odom_set_graph", "pf_device_count", "pf_dev_malloc", "pf_dev_free", "pf_memcpy_h2d",
            "pf_memcpy_d2h", "pf_knn_create", "pf_knn_destroy", "pf_knn_set_map", "pf_knn_query", "pf_knn_bench",
-           "pf_bpf_create", "pf_bpf_init_map", "pf_bpf_update", "pf_bpf_frame_device", "pf_odom_classes"]
+           "pf_bpf_create", "pf_bpf_init_map", "pf_bpf_update", "pf_bpf_frame_device", "pf_odom_classes",
+           "pf_odom_reset"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -122,6 +123,7 @@ def lib():
         L.pf_bpf_update.argtypes = [_vp, _vp, _sz, _sz, _vp, _sz, _sz, _vp, _sz, _sz, _vp]
         L.pf_bpf_frame_device.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp]
         L.pf_odom_classes.argtypes = [_vp]
+        L.pf_odom_reset.argtypes = [_vp]
     _lib = L
     return L
 
@@ -304,6 +306,10 @@ class Odom_ES_EstimationClass:
 
     def set_graph(self, enable):
         _check("pf_odom_set_graph", lib().pf_odom_set_graph(self._h, int(bool(enable))))
+
+    def reset(self):
+        """state right after init (a new sequence on the same handle and buffers)"""
+        _check("pf_odom_reset", lib().pf_odom_reset(self._h))
 
     def __del__(self):
         if getattr(self, "_h", None):

@@ -43,3 +43,19 @@ def test_reduce_results_gloo_world2():
         for r in (0, 1):
             exp = np.arange(7 * (3 + r), dtype=np.float64).reshape(-1, 7) + 100 * r
             np.testing.assert_array_equal(np.array(allp[r]), exp)
+
+
+def test_lpt_assignment_of_kitti_sequences():
+    """configs[3]: the 11 KITTI sequences over 1/2/4/8 ranks by longest processing time; every
+    sequence exactly once, and at 8 ranks the makespan is seq 02's length."""
+    sys.path.insert(0, ROOT)
+    import bench
+    L = bench.KITTI_SEQ_FRAMES
+    for world in (1, 2, 4, 8):
+        a = bench.lpt_assign(L, world)
+        assert sorted(s for r in a for s in r) == list(range(11))
+        loads = [sum(L[s] for s in r) for r in a]
+        assert max(loads) - min(loads) <= max(L)
+    a8 = bench.lpt_assign(L, 8)
+    assert max(sum(L[s] for s in r) for r in a8) == L[2] == 4661
+    assert bench.lpt_assign(L, 1) == [[2, 0, 8, 5, 9, 10, 1, 6, 7, 3, 4]]

@@ -215,3 +215,43 @@ def test_golden_trajectory(pa):
                                "n_edge_res", "n_surf_res")]
         if k > 0:
             assert got == list(g["gpu_equiv_counts"][k]), (k, got)
+
+
+def test_reset_replays_like_a_fresh_handle(pa, pfsynth):
+    """pf_odom_reset: the same frames after a reset give the bits of a fresh handle."""
+    seq = pfsynth.Sequence("S64", n_frames=12, az_steps=1200)
+    frames = [seq.frame(k) for k in range(12)]
+    od = pa.Odom_ES_EstimationClass(device=0)
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    first = [od.frame_host(x) for x in frames]
+    od.reset()
+    again = [od.frame_host(x) for x in frames]
+    np.testing.assert_array_equal(np.array(first), np.array(again))
+    assert od.poses().shape == (12, 7)
+
+
+def test_live_handle_limit_per_device(pa):
+    """A device admits CUs / 32 live handles (the LM solves' co-residency bound, pf_odom.hip)."""
+    import gc
+    gc.collect()                                    # handles of earlier tests
+    lid = pa.make_lidar(64, 3.0, 90.0)
+    made = []
+    rc = 0
+    for _ in range(64):
+        h = ctypes.c_void_p()
+        prm = pa.OdomParams(0.4, 0, 0.4, 75, 0)
+        rc = pa.lib().pf_odom_create(ctypes.byref(lid), ctypes.byref(prm), 0, 4096, 4096, ctypes.byref(h))
+        if rc != 0:
+            break
+        made.append(h.value)
+    try:
+        assert rc == pa.PF_EUNSUPPORTED
+        assert 1 <= len(made) <= 8                  # 256 CUs / 32 workgroups on an MI355X
+        pa.lib().pf_odom_destroy(made.pop())
+        h = ctypes.c_void_p()
+        prm = pa.OdomParams(0.4, 0, 0.4, 75, 0)
+        assert pa.lib().pf_bpf_create(ctypes.byref(lid), ctypes.byref(prm), 0, 4096, 4096, ctypes.byref(h)) == 0
+        made.append(h.value)
+    finally:
+        for h in made:
+            pa.lib().pf_odom_destroy(h)
