@@ -36,8 +36,157 @@ struct GridPtrs {                 // maps and their device-resident point counts
 
 int grid_alloc(GridGPU& g, size_t pts_cap, size_t cell_cap);
 void grid_free(GridGPU& g);
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ inline void grid_dims(const int* bounds, const int* npts, int* dims, int* d_ncells, long long cell_cap, int* err) {
+    long long base = 0;
+    for (int mi = 0; mi < kGridMaps; ++mi) {
+        const int n = npts[mi];
+        int* dm = dims + 8 * mi;
+        if (n <= 0) {
+            for (int k = 0; k < 8; ++k) dm[k] = 0;
+            dm[6] = (int)base;
+            continue;
+        }
+        const int* b = bounds + 6 * mi;
+        const long long dx = (long long)b[3] - b[0] + 1, dy = (long long)b[4] - b[1] + 1, dz = (long long)b[5] - b[2] + 1;
+        const long long nc = dx * dy * dz;
+        if (base + nc > cell_cap) {           // grid too large for the handle: mark invalid
+            for (int k = 0; k < 8; ++k) dm[k] = 0;
+            dm[6] = (int)base;
+            atomicOr(err, 1);
+            continue;
+        }
+        dm[0] = b[0]; dm[1] = b[1]; dm[2] = b[2];
+        dm[3] = (int)dx; dm[4] = (int)dy; dm[5] = (int)dz;
+        dm[6] = (int)base;
+        dm[7] = 1;
+        base += nc;
+    }
+    *d_ncells = (int)(base + 1);
+}
+
+// the concatenation of the maps: point i belongs to map mi at local index li
+struct GridIdx {
+    int end[kGridMaps];
+    int total;
+    __device__ __forceinline__ int map_of(int i) const { return i < end[0] ? 0 : (i < end[1] ? 1 : 2); }
+    __device__ __forceinline__ int start(int mi) const { return mi == 0 ? 0 : end[mi - 1]; }
+};
+__device__ __forceinline__ GridIdx grid_idx(const GridPtrs& gp) {
+    GridIdx g;
+    int acc = 0;
+#pragma unroll
+    for (int k = 0; k < kGridMaps; ++k) {
+        acc += k < gp.nm ? *gp.n[k] : 0;
+        g.end[k] = acc;
+    }
+    g.total = acc;
+    return g;
+}
+
+// per-map min/max cell coordinates: wave then workgroup reduction, one atomic per workgroup. The
+// last workgroup to arrive derives the grid dimensions and resets the bounds for the next build.
+// `tail(thread)` runs on workgroup 0 once it has arrived: a caller's independent single-thread work
+// (the odometry's pose prediction) overlaps the other workgroups instead of taking its own launch.
+struct GridBoundsArgs {
+    GridPtrs gp;
+    int* bounds;
+    u32* arrive;
+    int* dims;
+    int* d_ncells;
+    long long cell_cap;
+    int* err;
+};
+struct NoTail {
+    __device__ void operator()(int) const {}
+};
+template <class Tail>
+__global__ void __launch_bounds__(256) k_grid_bounds(GridBoundsArgs ga, Tail tail) {
+    const GridPtrs& gp = ga.gp;
+    int* bounds = ga.bounds;
+    u32* arrive = ga.arrive;
+    int* dims = ga.dims;
+    int* d_ncells = ga.d_ncells;
+    const long long cell_cap = ga.cell_cap;
+    int* err = ga.err;
+    constexpr int NB = 6 * kGridMaps;
+    __shared__ int red[4][NB];
+    __shared__ int last;
+    __shared__ int lb[NB];
+    const GridIdx gi = grid_idx(gp);
+    const int l = lane_id(), w = threadIdx.x >> 6;
+    int v[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) v[k] = ((k % 6) < 3) ? INT_MAX : INT_MIN;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < gi.total; i += gridDim.x * blockDim.x) {
+        const int mi = gi.map_of(i);
+        const float4 p = gp.m[mi][i - gi.start(mi)];
+        const int c[3] = {(int)floorf(p.x), (int)floorf(p.y), (int)floorf(p.z)};
+#pragma unroll
+        for (int mm = 0; mm < kGridMaps; ++mm) {      // branch-free: static register indices
+            const bool mine = mm == mi;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                v[6 * mm + k] = mine ? min(v[6 * mm + k], c[k]) : v[6 * mm + k];
+                v[6 * mm + 3 + k] = mine ? max(v[6 * mm + 3 + k], c[k]) : v[6 * mm + 3 + k];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        if (k >= 6 * gp.nm) break;                    // uniform: maps not built
+        const int r = ((k % 6) < 3) ? wave_min_i(v[k]) : wave_max_i(v[k]);
+        if (l == 0) red[w][k] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6 * gp.nm) {
+        const int k = threadIdx.x;
+        const bool is_min = (k % 6) < 3;
+        int r = red[0][k];
+        for (int ww = 1; ww < 4; ++ww) r = is_min ? min(r, red[ww][k]) : max(r, red[ww][k]);
+        if (is_min && r != INT_MAX) __hip_atomic_fetch_min(&bounds[k], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!is_min && r != INT_MIN) __hip_atomic_fetch_max(&bounds[k], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (blockIdx.x == 0) tail((int)threadIdx.x);
+    if (!last) return;
+    if (threadIdx.x < NB) {
+        const int k = threadIdx.x;
+        lb[k] = __hip_atomic_load(&bounds[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bounds[k], ((k % 6) < 3) ? INT_MAX : INT_MIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int nloc[kGridMaps];
+        for (int k = 0; k < kGridMaps; ++k) nloc[k] = gi.end[k] - (k ? gi.end[k - 1] : 0);
+        grid_dims(lb, nloc, dims, d_ncells, cell_cap, err);
+        __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+inline GridBoundsArgs grid_bounds_args(GridGPU& g, const GridPtrs& gp) {
+    return GridBoundsArgs{gp, g.bounds, g.arrive, g.dims, g.d_ncells, (long long)g.cell_cap, g.err};
+}
+constexpr int kGridBoundsBlocks = 64;
+
 // Build the grids of gp.nm maps (counts device-resident). pts_cap must hold all maps' points.
-void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s);
+// bounds_launched: the caller already ran k_grid_bounds (with its own tail) on this stream.
+void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s, bool bounds_launched = false);
 
 struct GridView {
     const int* dims;

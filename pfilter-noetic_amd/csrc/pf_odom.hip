@@ -2,7 +2,8 @@
 // (src/odomEstimationClass.cpp:217-282) as a fixed sequence of launches with every count kept on
 // the device, so a frame is enqueued without any host round trip (and can be replayed as a graph).
 //
-//   k_predict        constant-velocity prediction, optimization_count schedule, map-size gate (:232-247)
+//   PredictTail      constant-velocity prediction, optimization_count schedule, map-size gate (:232-247),
+//                    as the tail of the grid-bounds kernel
 //   VoxelGrid        k_vg_minmax / k_vg_keys / radix sort / segments / k_vg_reduce: PCL 1.10 VoxelGrid
 //                    (edge leaf 0.4, surf 0.8, :242-245) for both clouds in one batched pass
 //   grid_build       1 m cell grids of the edge and surf maps (the kd-trees of :249-250)
@@ -162,28 +163,36 @@ __global__ void k_pull_counts(int* __restrict__ cnt, const int* __restrict__ scn
     if (threadIdx.x == 0) pull_stage_counts(cnt, scnt);
 }
 
-__global__ void k_predict(DevState* __restrict__ st, int* __restrict__ cnt, const int* __restrict__ scnt,
-                          u32* __restrict__ acc, ClassCfg cls) {
-    if (threadIdx.x < 6 * kMaxC) acc[A_RG + threadIdx.x] = ((threadIdx.x % 6) < 3) ? 0xFFFFFFFFu : 0u;  // map-update bounds
-    if (threadIdx.x != 0) return;
-    pull_stage_counts(cnt, scnt);
-    if (st->optimization_count > 2) st->optimization_count--;                 // :232-233
-    const iso odom = load_iso(st->odomR, st->odomt);
-    const iso last = load_iso(st->lastR, st->lastt);
-    const iso pred = iso_mul(odom, iso_mul(iso_inv(last), odom));             // :235
-    store_iso(odom, st->lastR, st->lastt);
-    store_iso(pred, st->odomR, st->odomt);
-    const qd q = m2q(polar_rotation(pred.R));                                  // :239 (Eigen 3.3 rotation())
-    st->params[0] = q.x; st->params[1] = q.y; st->params[2] = q.z; st->params[3] = q.w;
-    st->params[4] = pred.t.x; st->params[5] = pred.t.y; st->params[6] = pred.t.z;
-    int gate = 1;                                  // :247 / BPF :721: line maps > 10, plane maps > 50
-    for (int c = 0; c < cls.nc; ++c) gate &= cnt[C_M + c] > (cls.is_plane(c) ? 50 : 10) ? 1 : 0;
-    st->gate = gate;
-    cnt[C_GATE] = gate;
-    cnt[C_OUTER] = gate ? st->optimization_count : 0;
-    cnt[C_LM_ITERS] = 0;
-    for (int c = 0; c < kMaxC; ++c) cnt[C_KEPT + c] = cnt[C_VALID + c] = 0;
-}
+// constant-velocity prediction, optimization_count schedule, map-size gate (:232-247); thread 0's
+// chain, thread < 18 reset the map-update bounds. Runs as the tail of the grid-bounds kernel.
+struct PredictTail {
+    DevState* st;
+    int* cnt;
+    const int* scnt;
+    u32* acc;
+    ClassCfg cls;
+    __device__ void operator()(int t) const {
+        if (t < 6 * kMaxC) acc[A_RG + t] = ((t % 6) < 3) ? 0xFFFFFFFFu : 0u;   // map-update bounds
+        if (t != 0) return;
+        pull_stage_counts(cnt, scnt);
+        if (st->optimization_count > 2) st->optimization_count--;                 // :232-233
+        const iso odom = load_iso(st->odomR, st->odomt);
+        const iso last = load_iso(st->lastR, st->lastt);
+        const iso pred = iso_mul(odom, iso_mul(iso_inv(last), odom));             // :235
+        store_iso(odom, st->lastR, st->lastt);
+        store_iso(pred, st->odomR, st->odomt);
+        const qd q = m2q(polar_rotation(pred.R));                                  // :239 (Eigen 3.3 rotation())
+        st->params[0] = q.x; st->params[1] = q.y; st->params[2] = q.z; st->params[3] = q.w;
+        st->params[4] = pred.t.x; st->params[5] = pred.t.y; st->params[6] = pred.t.z;
+        int gate = 1;                              // :247 / BPF :721: line maps > 10, plane maps > 50
+        for (int c = 0; c < cls.nc; ++c) gate &= cnt[C_M + c] > (cls.is_plane(c) ? 50 : 10) ? 1 : 0;
+        st->gate = gate;
+        cnt[C_GATE] = gate;
+        cnt[C_OUTER] = gate ? st->optimization_count : 0;
+        cnt[C_LM_ITERS] = 0;
+        for (int c = 0; c < kMaxC; ++c) cnt[C_KEPT + c] = cnt[C_VALID + c] = 0;
+    }
+};
 
 // voxel-grid stage set-up (stream A): reset the min/max accumulators, batch size
 __global__ void k_vg_begin(int* __restrict__ scnt, u32* __restrict__ acc, int nc) {
@@ -353,7 +362,11 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
                     for (int cc = 0; cc < 3; ++cc) cov[r][cc] = cov[r][cc] + tv[r] * tv[cc];
             }
             double ev[3], V[3][3];
+#ifndef PF_DEV_NOEIG
             eig3(cov, ev, V);
+#else
+            for (int i = 0; i < 3; ++i) { ev[i] = cov[i][i] * (i + 1); for (int j = 0; j < 3; ++j) V[i][j] = cov[i][j]; }
+#endif
             if (ev[2] > 3 * ev[1]) {
                 valid = true;
                 const d3 dir{V[0][2], V[1][2], V[2][2]};
@@ -363,7 +376,11 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
         } else {                                                 // :449-476 (BPF facade :1070-1104)
             double A[5][3];
             for (int j = 0; j < 5; ++j) { A[j][0] = px[j]; A[j][1] = py[j]; A[j][2] = pz[j]; }
+#ifndef PF_DEV_NOQR
             d3 n = plane5(A);
+#else
+            d3 n{A[0][0] * 0.01, A[1][1] * 0.01, 1.0 + A[2][2] * 1e-9};
+#endif
             const double nd = 1 / nrm3(n);
             const double z = n.x * n.x + n.y * n.y + n.z * n.z;
             if (z > 0.0) {
@@ -390,7 +407,11 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
         }
     }
     a.qflag[q] = valid ? 1 : 0;
+#ifdef PF_DEV_NOPUSH
+    if (false) {
+#else
     if (valid) {               // p-index: push the 5 pairs onto their map points' lists (:345-346, :493-496)
+#endif
         const u32 off = (u32)c * a.map_cap;
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
@@ -448,7 +469,11 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
                 if (tl == k) iv = id[k];
             a.nbr[5 * q0 + tl] = found == 5 ? iv : -1;
         }
+#ifndef PF_DEV_NOFIT
         if (active && tl == 0) assoc_fit(a, q0, c, id, found);
+#else
+        if (active && tl == 0) a.qflag[q0] = 0;                  // development: time the kNN alone
+#endif
     }
 }
 
@@ -1548,11 +1573,14 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     int* cnt = o.cnt;
     const int nc = o.cls.nc;
     // (a side-stream branch for the single-thread prediction beside the grid build measured slower
-    // under graph replay: 2815 vs 2930 frames/s; the fork / join edges cost more than the overlap)
-    hipLaunchKernelGGL(k_predict, dim3(1), dim3(64), 0, s, o.st, cnt, sb.cnt, o.acc, o.cls);
-    // grids of the class maps (kd-tree builds, :249-250 / BPF :723-725)
+    // under graph replay: 2815 vs 2930 frames/s; the fork / join edges cost more than the overlap;
+    // as the tail of the bounds kernel it overlaps for free)
+    // grids of the class maps (kd-tree builds, :249-250 / BPF :723-725); the pose prediction rides on
+    // the bounds kernel as its tail (it reads the map sizes of the previous frame, not the grid)
     GridPtrs gp{{o.map[0], o.map[1], o.map[2]}, {cnt + C_M, cnt + C_M + 1, cnt + C_M + 2}, nc};
-    grid_build(o.grid, gp, o.prim, s);
+    hipLaunchKernelGGL(k_grid_bounds<PredictTail>, dim3(kGridBoundsBlocks), dim3(256), 0, s,
+                       grid_bounds_args(o.grid, gp), PredictTail{o.st, cnt, sb.cnt, o.acc, o.cls});
+    grid_build(o.grid, gp, o.prim, s, true);
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
         AssocArgs aa{o.st, cnt, o.acc, gv, o.cls, clouds(sb.ds), clouds(o.map), o.nbr, o.qflag, o.geo, o.spars,

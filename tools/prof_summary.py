@@ -32,7 +32,7 @@ def short(name):
 def frame_breakdown(trace_csv, stats_csv):
     rows = list(csv.DictReader(open(trace_csv)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if short(r["Kernel_Name"]) == "k_predict"]
+    starts = [i for i, r in enumerate(rows) if "PredictTail" in r["Kernel_Name"]]   # stage B head
     frames = list(zip(starts[:-1], starts[1:]))[100:]          # steady state
     per = {}
     spans = []

@@ -6,7 +6,7 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 500
-idx = [i for i, r in enumerate(rows) if 'k_predict' in r['Kernel_Name']]
+idx = [i for i, r in enumerate(rows) if 'PredictTail' in r['Kernel_Name']]   # stage B head
 i0, i1 = idx[k], idx[k + 1]
 t0 = int(rows[i0]['Start_Timestamp'])
 for r in rows[i0:i1]:
