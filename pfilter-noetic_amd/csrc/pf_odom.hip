@@ -33,7 +33,10 @@ struct VgLeaf {                        // per-class leaf sizes
     float v[kMaxC];
     __device__ __forceinline__ float at(int c) const { return c == 0 ? v[0] : (c == 1 ? v[1] : v[2]); }
 };
-constexpr int kGrid = 512;   // grid-stride workgroups for per-point kernels
+#ifndef PF_GRID
+#define PF_GRID 512
+#endif
+constexpr int kGrid = PF_GRID;   // grid-stride workgroups for per-point kernels
 
 __device__ __forceinline__ float wave_minf(float v) {
 #pragma unroll

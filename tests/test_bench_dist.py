@@ -59,3 +59,34 @@ def test_lpt_assignment_of_kitti_sequences():
     a8 = bench.lpt_assign(L, 8)
     assert max(sum(L[s] for s in r) for r in a8) == L[2] == 4661
     assert bench.lpt_assign(L, 1) == [[2, 0, 8, 5, 9, 10, 1, 6, 7, 3, 4]]
+
+
+def _bcast_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import bench
+    dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    arr = np.arange(24, dtype=np.float32).reshape(6, 4) if rank == 0 else None
+    got = bench.broadcast_array(dist, arr, 0, "cpu")
+    out[rank] = (got.tolist(), bench.shard_bounds(200_000, world, rank))
+    dist.destroy_process_group()
+
+
+def test_knn_shard_broadcast_and_bounds_gloo_world2():
+    """configs[4] multi-GPU kNN: the map reaches every rank by one broadcast; the query shards tile
+    [0, Q) exactly."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for world in (1, 2, 3, 8):
+        bounds = [bench.shard_bounds(200_003, world, r) for r in range(world)]
+        assert bounds[0][0] == 0 and bounds[-1][1] == 200_003
+        assert all(bounds[i][1] == bounds[i + 1][0] for i in range(world - 1))
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_bcast_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    for rank in (0, 1):
+        np.testing.assert_array_equal(np.array(res[rank][0]), np.arange(24, dtype=np.float32).reshape(6, 4))
+    assert res[0][1] == (0, 100_000) and res[1][1] == (100_000, 200_000)
