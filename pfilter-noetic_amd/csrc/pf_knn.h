@@ -97,8 +97,9 @@ __device__ __forceinline__ GridIdx grid_idx(const GridPtrs& gp) {
 
 // per-map min/max cell coordinates: wave then workgroup reduction, one atomic per workgroup. The
 // last workgroup to arrive derives the grid dimensions and resets the bounds for the next build.
-// `tail(thread)` runs on workgroup 0 once it has arrived: a caller's independent single-thread work
-// (the odometry's pose prediction) overlaps the other workgroups instead of taking its own launch.
+// A Tail with kActive runs on one extra workgroup (the last), which takes no part in the bounds: a
+// caller's independent single-thread work (the odometry's pose prediction) overlaps the bounds
+// instead of taking its own launch. Launch kGridBoundsBlocks + (Tail::kActive ? 1 : 0) workgroups.
 struct GridBoundsArgs {
     GridPtrs gp;
     int* bounds;
@@ -109,10 +110,16 @@ struct GridBoundsArgs {
     int* err;
 };
 struct NoTail {
+    static constexpr bool kActive = false;
     __device__ void operator()(int) const {}
 };
 template <class Tail>
 __global__ void __launch_bounds__(256) k_grid_bounds(GridBoundsArgs ga, Tail tail) {
+    if (Tail::kActive && blockIdx.x == gridDim.x - 1) {
+        tail((int)threadIdx.x);
+        return;
+    }
+    const unsigned nblk = gridDim.x - (Tail::kActive ? 1u : 0u);   // workgroups sharing the bounds
     const GridPtrs& gp = ga.gp;
     int* bounds = ga.bounds;
     u32* arrive = ga.arrive;
@@ -129,7 +136,7 @@ __global__ void __launch_bounds__(256) k_grid_bounds(GridBoundsArgs ga, Tail tai
     int v[NB];
 #pragma unroll
     for (int k = 0; k < NB; ++k) v[k] = ((k % 6) < 3) ? INT_MAX : INT_MIN;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < gi.total; i += gridDim.x * blockDim.x) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < gi.total; i += nblk * blockDim.x) {
         const int mi = gi.map_of(i);
         const float4 p = gp.m[mi][i - gi.start(mi)];
         const int c[3] = {(int)floorf(p.x), (int)floorf(p.y), (int)floorf(p.z)};
@@ -161,9 +168,8 @@ __global__ void __launch_bounds__(256) k_grid_bounds(GridBoundsArgs ga, Tail tai
     if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+        last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
     __syncthreads();
-    if (blockIdx.x == 0) tail((int)threadIdx.x);
     if (!last) return;
     if (threadIdx.x < NB) {
         const int k = threadIdx.x;

@@ -167,8 +167,9 @@ __global__ void k_pull_counts(int* __restrict__ cnt, const int* __restrict__ scn
 }
 
 // constant-velocity prediction, optimization_count schedule, map-size gate (:232-247); thread 0's
-// chain, thread < 18 reset the map-update bounds. Runs as the tail of the grid-bounds kernel.
+// chain, thread < 18 reset the map-update bounds. Runs on an extra workgroup of the grid-bounds kernel.
 struct PredictTail {
+    static constexpr bool kActive = true;
     DevState* st;
     int* cnt;
     const int* scnt;
@@ -1581,7 +1582,7 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     // grids of the class maps (kd-tree builds, :249-250 / BPF :723-725); the pose prediction rides on
     // the bounds kernel as its tail (it reads the map sizes of the previous frame, not the grid)
     GridPtrs gp{{o.map[0], o.map[1], o.map[2]}, {cnt + C_M, cnt + C_M + 1, cnt + C_M + 2}, nc};
-    hipLaunchKernelGGL(k_grid_bounds<PredictTail>, dim3(kGridBoundsBlocks), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_grid_bounds<PredictTail>, dim3(kGridBoundsBlocks + 1), dim3(256), 0, s,
                        grid_bounds_args(o.grid, gp), PredictTail{o.st, cnt, sb.cnt, o.acc, o.cls});
     grid_build(o.grid, gp, o.prim, s, true);
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
