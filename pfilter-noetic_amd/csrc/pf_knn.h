@@ -271,6 +271,7 @@ __device__ __forceinline__ u64 team_min(u64 v) {
 #ifndef PF_KNN_ROWS
 #define PF_KNN_ROWS 0
 #endif
+
 template <int T>
 __device__ __forceinline__ int knn5_team(const GridView& gv, int m, float qx, float qy, float qz, bool active,
                                          float (&dout)[5], int (&iout)[5]) {
