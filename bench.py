@@ -315,7 +315,7 @@ def host_leg(device, nframes, threads):
             "note": "pf_odom_frame_host: scans in pageable host memory, repacked and copied H2D per frame"}
 
 
-def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True):
+def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True, use_graph=True):
     """Odom_BPF_EstimationClass (src/odomEstimationClass.cpp:649-1306) frames/s on the same S64 sequence
     with configs[1]'s parameters. Its inputs are beam / pillar / facade clouds: featureExtraction (on the
     GPU, untimed) split by pfsynth.bpf_split, the stand-in for the reference's PCA classifier. All clouds
@@ -343,6 +343,7 @@ def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True
         ptrs.append([(db.ptr + int(o) * 16, n) for o, n in zip(offs, sizes)])
     od = pa.Odom_BPF_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lidar_cfg(), **ODOM_CFG)
+    od.set_graph(use_graph)
 
     def run(k):
         od.frame_device([ptrs[c][k][0] for c in range(3)], [ptrs[c][k][1] for c in range(3)])
@@ -491,7 +492,8 @@ def main():
             out["roofline"] = None
     if world == 1 and args.bpf_frames > 0:
         try:
-            out["bpf"] = bpf_leg(local_rank, args.bpf_frames, threads, with_cpu=not args.no_cpu)
+            out["bpf"] = bpf_leg(local_rank, args.bpf_frames, threads, with_cpu=not args.no_cpu,
+                                 use_graph=not args.no_graph)
         except Exception as e:  # report, never hide
             log("bpf leg failed: %r" % (e,))
             out["bpf"] = None
