@@ -19,6 +19,9 @@
  *   pf_bpf_init_map                Odom_BPF_EstimationClass::initMapWithPoints (.h:177, .cpp:685-691)
  *   pf_bpf_update                  Odom_BPF_EstimationClass::updatePointsToMap (.h:178, .cpp:702-749)
  *   pf_odom_get_map (BPF handle)   laserCloudBeamMap / PillarMap / FacadeMap (.h:180-182), getMap (.cpp:683)
+ *   pf_cls_create / pf_cls_extract groundSeg::ground_seg + nongroundExtract::featureExtract, the BPF
+ *                                  front end of src/additionNode.cpp:21-45 (include/preProcess.hpp:
+ *                                  398-505, 646-689)
  */
 #ifndef PFILTER_HIP_H
 #define PFILTER_HIP_H
@@ -127,6 +130,39 @@ int pf_bpf_frame_device(pf_odom* h, const float* d_beam, size_t nb, const float*
                         const float* d_facade, size_t nf, double pose_out[7]);
 /* number of map classes of a handle: 2 (ES) or 3 (BPF) */
 int pf_odom_classes(pf_odom* h);
+
+/* ---------------- BPF front end (groundSeg + nongroundExtract, src/additionNode.cpp:21-45) ----------------
+ * ground_seg (include/preProcess.hpp:398-505): 2-D grid of gf_grid_res cells over the scan's x/y
+ * bounds; per cell the lowest z in (gf_min_ground_height, gf_max_ground_height], the 3x3 neighbourhood
+ * minimum, and the ground / non-ground split. featureExtract (:646-689): per non-ground point the
+ * <= k nearest non-ground points with d^2 < radius^2, their PCA, and the pillar / beam / facade
+ * decision. The DCVC `curvedfilter` stage the launch file can insert between them is not part of
+ * this path: with it off, as here, the non-ground cloud feeds featureExtract. */
+typedef struct {
+    int ground_filter;                 /* additionNode `groundfilter` (pfilter_kitti.launch:10) */
+    int gf_min_grid_pts;               /* gf_grid_pt_num_thre (preProcess.hpp:575) */
+    float gf_grid_res, gf_max_height_diff, gf_neighbor_height_diff, gf_max_ground_height,
+          gf_min_ground_height;        /* :601-605 (double members passed as float, :398-401) */
+    float radius;                      /* neighbor_searching_radius (:703); must be <= 1 */
+    int k, k_min;                      /* neighbor_k (:705; 1..32), neigh_k_min (:706) */
+    float edge_thre, planar_thre, linear_vsin_high, linear_vsin_low, planar_vsin_low,
+          beam_h_max, beam_h_min;      /* :708-715 */
+} pf_cls_params;
+typedef struct pf_cls pf_cls;
+void pf_cls_default_params(pf_cls_params* p);   /* the reference's member defaults */
+int pf_cls_create(const pf_cls_params* p, int device, size_t max_points, pf_cls** out);
+int pf_cls_destroy(pf_cls* h);
+/* One scan (x, y, z floats at the start of each stride-byte record). Outputs are indices into the
+ * scan, in the order the reference publishes the clouds: beam / pillar / facade (cloud_beam /
+ * cloud_pillar / cloud_facade, :660-684) and ground (cloud_ground, :480). Any output pair may be NULL;
+ * each list holds at most cap entries (PF_ECAPACITY with the counts set when one does not fit). */
+int pf_cls_extract(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, int32_t* beam, size_t* nb,
+                   int32_t* pillar, size_t* np, int32_t* facade, size_t* nf, int32_t* ground, size_t* ng,
+                   size_t cap);
+/* featureExtract alone on a cloud (no ground segmentation): per point the index_with_feature code
+ * (0 none, 1 pillar, 2 beam, 3 facade, :663-682) and the neighbour count pt_num (:223); either may
+ * be NULL */
+int pf_cls_classify(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, uint8_t* cls, int32_t* pt_num);
 
 /* ---------------- whole-frame device pipeline (featureExtraction -> odometry) ----------------
  * d_xyzi: device pointer to n packed float4 points (HBM-resident scan). The first frame seeds the

@@ -8,6 +8,7 @@
  *   - LaserProcessingClass::featureExtraction(+FromSector)   src/laserProcessingClass.cpp:10-209
  *   - Odom_ES_EstimationClass init/initMapWithPoints/updatePointsToMap/addEdgeCostFactor/
  *     addSurfCostFactor/addPointsToMap                       src/odomEstimationClass.cpp:182-647
+ *   - groundSeg::ground_seg, nongroundExtract::featureExtract  include/preProcess.hpp:398-505,646-689
  *   - Odom_BPF_EstimationClass init/initMapWithPoints/updatePointsToMap/addBeam|Pillar|Facade-
  *     CostFactor/addPointsToMap (the same sequence over 3 maps)  src/odomEstimationClass.cpp:649-1306
  *   - OdomBaseClass rgbds/extractstablepoint/observeMean/pointAssociateToMap
@@ -134,6 +135,32 @@ int pfref_odom_classes(const pfref_odom* h);   /* 2 (ES) or 3 (BPF) */
 /* clouds[c]: 4 floats per point (x, y, z, intensity); n[c] points; one per class */
 int pfref_odom_init_map_n(pfref_odom* h, const float* const* clouds, const size_t* n);
 int pfref_odom_update_n(pfref_odom* h, const float* const* clouds, const size_t* n, double pose_out[7]);
+
+/* --- BPF front end: groundSeg::ground_seg + nongroundExtract::featureExtract -------------
+ * (include/preProcess.hpp:398-505, :646-689, driven by src/additionNode.cpp:21-45). Parameters
+ * mirror the reference's member defaults (pfref_cls_default_params); same layout as the
+ * product's pf_cls_params. Points: x, y, z floats at the start of each `stride`-byte record. */
+typedef struct {
+    int ground_filter;                 /* additionNode `groundfilter` (pfilter_kitti.launch:10) */
+    int gf_min_grid_pts;               /* gf_grid_pt_num_thre (preProcess.hpp:575) */
+    float gf_grid_res, gf_max_height_diff, gf_neighbor_height_diff, gf_max_ground_height,
+          gf_min_ground_height;        /* :601-605 (double members passed as float) */
+    float radius;                      /* neighbor_searching_radius (:703) */
+    int k, k_min;                      /* neighbor_k, neigh_k_min (:705-706) */
+    float edge_thre, planar_thre, linear_vsin_high, linear_vsin_low, planar_vsin_low,
+          beam_h_max, beam_h_min;      /* :708-715 */
+} pfref_cls_params;
+void pfref_cls_default_params(pfref_cls_params* p);
+/* ground / unground as input indices in the reference's push order */
+int pfref_ground_seg(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, int32_t* ground,
+                     size_t* ng, int32_t* unground, size_t* nu);
+/* per point: 0 none, 1 pillar, 2 beam, 3 facade (index_with_feature); pt_num = neighbours found */
+int pfref_pca_classify(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, uint8_t* cls,
+                       int32_t* pt_num);
+/* the chain: class clouds (input indices, in the published order); any output may be NULL */
+int pfref_bpf_preprocess(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, int32_t* beam,
+                         size_t* nb, int32_t* pillar, size_t* np, int32_t* facade, size_t* nf, int32_t* ground,
+                         size_t* ng);
 
 /* --- whole frame: featureExtraction then initMapWithPoints (first call) / updatePointsToMap */
 int pfref_odom_frame(pfref_odom* h, const pfref_lidar* lidar, const float* xyzi, size_t n,

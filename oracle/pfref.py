@@ -60,6 +60,25 @@ _vp = ctypes.c_void_p
 _sz = ctypes.c_size_t
 
 
+class ClsParams(ctypes.Structure):
+    """groundSeg / nongroundExtract parameters (include/preProcess.hpp:575-605, :703-715)."""
+    _fields_ = [("ground_filter", ctypes.c_int), ("gf_min_grid_pts", ctypes.c_int),
+                ("gf_grid_res", ctypes.c_float), ("gf_max_height_diff", ctypes.c_float),
+                ("gf_neighbor_height_diff", ctypes.c_float), ("gf_max_ground_height", ctypes.c_float),
+                ("gf_min_ground_height", ctypes.c_float), ("radius", ctypes.c_float), ("k", ctypes.c_int),
+                ("k_min", ctypes.c_int), ("edge_thre", ctypes.c_float), ("planar_thre", ctypes.c_float),
+                ("linear_vsin_high", ctypes.c_float), ("linear_vsin_low", ctypes.c_float),
+                ("planar_vsin_low", ctypes.c_float), ("beam_h_max", ctypes.c_float), ("beam_h_min", ctypes.c_float)]
+
+
+def cls_params(**kw):
+    p = ClsParams()
+    lib().pfref_cls_default_params(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -95,6 +114,12 @@ def lib():
         L.pfref_odom_classes.argtypes = [_vp]
         L.pfref_odom_init_map_n.argtypes = [_vp, _vp, _vp]
         L.pfref_odom_update_n.argtypes = [_vp, _vp, _vp, _vp]
+        L.pfref_cls_default_params.argtypes = [ctypes.POINTER(ClsParams)]
+        L.pfref_ground_seg.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams), _vp, ctypes.POINTER(_sz), _vp,
+                                       ctypes.POINTER(_sz)]
+        L.pfref_pca_classify.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams), _vp, _vp]
+        L.pfref_bpf_preprocess.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams)] + \
+            [_vp, ctypes.POINTER(_sz)] * 4
     return _lib
 
 
@@ -305,3 +330,46 @@ class OdomBPF(Odom):
 
     def frame(self, xyzi):
         raise NotImplementedError("the BPF estimator takes classified beam / pillar / facade clouds")
+
+
+# ---- BPF front end (groundSeg + nongroundExtract; include/preProcess.hpp) ----
+
+def ground_seg(xyz, params=None):
+    """(ground, unground) input indices in the reference's push order."""
+    a = np.ascontiguousarray(xyz, dtype=np.float32)
+    n = a.shape[0]
+    p = params or cls_params()
+    g = np.empty(max(n, 1), np.int32)
+    u = np.empty(max(n, 1), np.int32)
+    ng, nu = ctypes.c_size_t(), ctypes.c_size_t()
+    rc = lib().pfref_ground_seg(a.ctypes.data, n, 4 * a.shape[1], ctypes.byref(p), g.ctypes.data, ctypes.byref(ng),
+                                u.ctypes.data, ctypes.byref(nu))
+    assert rc == 0
+    return g[:ng.value].copy(), u[:nu.value].copy()
+
+
+def pca_classify(xyz, params=None):
+    """(class per point: 0 none / 1 pillar / 2 beam / 3 facade, neighbour count per point)."""
+    a = np.ascontiguousarray(xyz, dtype=np.float32)
+    n = a.shape[0]
+    p = params or cls_params()
+    cls = np.empty(max(n, 1), np.uint8)
+    num = np.empty(max(n, 1), np.int32)
+    rc = lib().pfref_pca_classify(a.ctypes.data, n, 4 * a.shape[1], ctypes.byref(p), cls.ctypes.data, num.ctypes.data)
+    assert rc == 0
+    return cls[:n].copy(), num[:n].copy()
+
+
+def bpf_preprocess(xyz, params=None):
+    """additionNode's chain: dict of beam / pillar / facade / ground input-index arrays."""
+    a = np.ascontiguousarray(xyz, dtype=np.float32)
+    n = a.shape[0]
+    p = params or cls_params()
+    bufs = [np.empty(max(n, 1), np.int32) for _ in range(4)]
+    cnt = [ctypes.c_size_t() for _ in range(4)]
+    args = []
+    for b, c in zip(bufs, cnt):
+        args += [b.ctypes.data, ctypes.byref(c)]
+    rc = lib().pfref_bpf_preprocess(a.ctypes.data, n, 4 * a.shape[1], ctypes.byref(p), *args)
+    assert rc == 0
+    return {k: b[:c.value].copy() for k, b, c in zip(("beam", "pillar", "facade", "ground"), bufs, cnt)}

@@ -1,0 +1,641 @@
+// BPF front end kernels (see pf_cls.h) and the pf_cls C ABI.
+#include "pf_cls.h"
+#include "pf_geom.h"
+
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <vector>
+
+namespace pf {
+namespace {
+
+constexpr u32 kKeyDropped = 0xFFFFu;
+constexpr u32 kKeyGround = 0x8000u;
+constexpr size_t kClsCells = (size_t)1 << 23;   // 1 m cells of the U grid
+
+struct ClsDev {          // kernel view of ClsGPU
+    pf_cls_params prm;
+    int* cnt;
+    u32* gb;
+    int* gdim;
+    u32* cell_cnt;
+    u32* cell_minz;
+    float* cell_nb;
+    u32* pcell;
+    u32* keys;
+    u32* vals;
+    float4* U;
+    u32* ckeys;
+    u32* cvals;
+    uint8_t* code;
+    int* ptnum;
+};
+ClsDev dev_view(ClsGPU& c) {
+    return ClsDev{c.prm, c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals,
+                  c.U, c.ckeys, c.cvals, c.code, c.ptnum};
+}
+
+__device__ __forceinline__ float wave_minf(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// ---- ground_seg ------------------------------------------------------------------------------
+
+// get_cloud_bbx (:522-556) over x and y; the last workgroup derives row / col / num_grid (:412-415),
+// clears the grid (:420-424: min_z = FLT_MAX) and the frame's counters
+__global__ void __launch_bounds__(256) k_gs_bounds(const float4* __restrict__ pts, const int* __restrict__ d_n,
+                                                   ClsDev d) {
+    __shared__ float red[4][4];
+    __shared__ int last;
+    __shared__ int sdim[3];
+    const int n = *d_n;
+    float v[4] = {INFINITY, INFINITY, -INFINITY, -INFINITY};
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4 p = pts[i];
+        v[0] = fminf(v[0], p.x); v[1] = fminf(v[1], p.y);
+        v[2] = fmaxf(v[2], p.x); v[3] = fmaxf(v[3], p.y);
+    }
+    const int w = threadIdx.x >> 6;
+    v[0] = wave_minf(v[0]); v[1] = wave_minf(v[1]); v[2] = wave_maxf(v[2]); v[3] = wave_maxf(v[3]);
+    if (lane_id() == 0)
+        for (int k = 0; k < 4; ++k) red[w][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const int k = threadIdx.x;
+        float r = red[0][k];
+        for (int ww = 1; ww < 4; ++ww) r = k < 2 ? fminf(r, red[ww][k]) : fmaxf(r, red[ww][k]);
+        if (k < 2) atomicMin(&d.gb[k], f2ord(r));
+        else atomicMax(&d.gb[k], f2ord(r));
+    }
+    if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(&d.gb[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x == 0) {
+        float b[4];
+        for (int k = 0; k < 4; ++k) {
+            b[k] = ord2f(__hip_atomic_load(&d.gb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            __hip_atomic_store(&d.gb[k], k < 2 ? 0xFFFFFFFFu : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __hip_atomic_store(&d.gb[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double res = (double)d.prm.gf_grid_res;
+        int row = 0, col = 0;
+        long long num = 0;
+        if (n > 0) {
+            row = (int)ceil(((double)b[3] - (double)b[1]) / res);
+            col = (int)ceil(((double)b[2] - (double)b[0]) / res);
+            num = (long long)row * col;
+        }
+        int err = 0;
+        if (num > kGsMaxCells || num < 0) { num = 0; err = 1; }
+        d.gdim[0] = row; d.gdim[1] = col; d.gdim[2] = (int)num;
+        d.gdim[4] = __float_as_int(b[0]); d.gdim[5] = __float_as_int(b[1]);
+        sdim[0] = (int)num;
+        d.cnt[CC_N] = n;
+        d.cnt[CC_NU] = 0; d.cnt[CC_NG] = 0;
+        for (int k = 0; k < 4; ++k) d.cnt[CC_CLS + k] = 0;
+        d.cnt[CC_ERR] = err;
+    }
+    __syncthreads();
+    const u32 fmax_ord = f2ord(FLT_MAX);
+    for (int m = threadIdx.x; m < sdim[0]; m += blockDim.x) {
+        d.cell_cnt[m] = 0;
+        d.cell_minz[m] = fmax_ord;
+    }
+}
+
+// :427-448: cell of every point, the cell's point count, its lowest z in (min, max ground height]
+__global__ void __launch_bounds__(256) k_gs_assign(const float4* __restrict__ pts, const int* __restrict__ d_n, ClsDev d) {
+    const int n = *d_n;
+    const int col = d.gdim[1], num = d.gdim[2];
+    const double minx = (double)__int_as_float(d.gdim[4]), miny = (double)__int_as_float(d.gdim[5]);
+    const double res = (double)d.prm.gf_grid_res;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4 p = pts[i];
+        const int tc = (int)floor(((double)p.x - minx) / res);
+        const int tr = (int)floor(((double)p.y - miny) / res);
+        const long long id = (long long)tr * col + tc;
+        u32 cell = ~0u;
+        if (id >= 0 && id < num) {
+            cell = (u32)id;
+            atomicAdd(&d.cell_cnt[cell], 1u);
+            if (!(p.z > d.prm.gf_max_ground_height) && p.z > d.prm.gf_min_ground_height && p.z < FLT_MAX)
+                atomicMin(&d.cell_minz[cell], f2ord(p.z));
+        }
+        d.pcell[i] = cell;
+    }
+}
+
+// :451-467: the 3x3 minimum of min_z for cells off the grid border
+__global__ void __launch_bounds__(256) k_gs_nbmin(ClsDev d) {
+    const int row = d.gdim[0], col = d.gdim[1], num = d.gdim[2];
+    for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < num; m += gridDim.x * blockDim.x) {
+        float nb = ord2f(d.cell_minz[m]);
+        const int r = m / col, c = m % col;
+        if (r >= 1 && r <= row - 2 && c >= 1 && c <= col - 2)
+            for (int j = -1; j <= 1; ++j)
+                for (int k = -1; k <= 1; ++k) {
+                    const float z = ord2f(d.cell_minz[m + j * col + k]);
+                    if (nb > z) nb = z;
+                }
+        d.cell_nb[m] = nb;
+    }
+}
+
+// :427-494 as a stable sort key: the reference pushes points above the max ground height to
+// cloud_unground in input order during the assignment pass, then walks the cells in order pushing
+// each cell's remaining points (input order) to ground or non-ground; cells with fewer than
+// gf_min_grid_pts points push nothing
+__global__ void __launch_bounds__(256) k_gs_keys(const float4* __restrict__ pts, const int* __restrict__ d_n, ClsDev d) {
+    __shared__ int red[2];
+    if (threadIdx.x < 2) red[threadIdx.x] = 0;
+    __syncthreads();
+    const int n = *d_n;
+    const pf_cls_params& P = d.prm;
+    int nu = 0, ng = 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const u32 cell = d.pcell[i];
+        const float z = pts[i].z;
+        u32 key = kKeyDropped;
+        if (cell != ~0u) {
+            if (z > P.gf_max_ground_height) {
+                key = 0;
+            } else if ((int)d.cell_cnt[cell] >= P.gf_min_grid_pts) {
+                const float minz = ord2f(d.cell_minz[cell]);
+                key = 1 + cell;
+                if (minz - d.cell_nb[cell] < P.gf_neighbor_height_diff && z - minz < P.gf_max_height_diff &&
+                    z > P.gf_min_ground_height)
+                    key = kKeyGround + cell;
+            }
+        }
+        nu += key < kKeyGround;
+        ng += key >= kKeyGround && key < kKeyDropped;
+        d.keys[i] = key;
+        d.vals[i] = (u32)i;
+    }
+    nu = wave_sum_i(nu);
+    ng = wave_sum_i(ng);
+    if (lane_id() == 0) {
+        atomicAdd(&red[0], nu);
+        atomicAdd(&red[1], ng);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (red[0]) atomicAdd(&d.cnt[CC_NU], red[0]);
+        if (red[1]) atomicAdd(&d.cnt[CC_NG], red[1]);
+    }
+}
+
+// pc2pc (:633-644): the non-ground cloud U in push order, xyz only
+__global__ void __launch_bounds__(256) k_gs_gather(const float4* __restrict__ pts, ClsDev d) {
+    const int nu = d.cnt[CC_NU];
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nu; j += gridDim.x * blockDim.x) {
+        const float4 p = pts[d.vals[j]];
+        d.U[j] = make_float4(p.x, p.y, p.z, 0.0f);
+    }
+}
+
+// groundfilter off: U is the input cloud itself
+__global__ void __launch_bounds__(256) k_cls_identity(const float4* __restrict__ pts, const int* __restrict__ d_n, ClsDev d) {
+    const int n = *d_n;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        d.cnt[CC_N] = n; d.cnt[CC_NU] = n; d.cnt[CC_NG] = 0; d.cnt[CC_ERR] = 0;
+        for (int k = 0; k < 4; ++k) d.cnt[CC_CLS + k] = 0;
+    }
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const float4 p = pts[j];
+        d.U[j] = make_float4(p.x, p.y, p.z, 0.0f);
+        d.vals[j] = (u32)j;
+    }
+}
+
+// ---- featureExtract ----------------------------------------------------------------------------
+
+// PCA of the neighbourhood nb[0 .. n) (ascending distance) and the class decision, :653-688 /
+// :283-323, f32 as pcl::PCA computes it; the eigen-decomposition is the f64 cyclic Jacobi (eig3)
+// of the f32 covariance, rounded back to f32. Returns the index_with_feature code.
+__device__ int pca_code(const float (*nb)[4], int n, float qz, const pf_cls_params& P) {
+    if (!(n > P.k_min) || n <= 3) return 0;
+    float sx = 0.f, sy = 0.f, sz = 0.f;
+    for (int e = 0; e < n; ++e) { sx += nb[e][0]; sy += nb[e][1]; sz += nb[e][2]; }
+    const float fn = (float)n;
+    const float mx = sx / fn, my = sy / fn, mz = sz / fn;
+    float cxx = 0.f, cxy = 0.f, cxz = 0.f, cyy = 0.f, cyz = 0.f, czz = 0.f;
+    for (int e = 0; e < n; ++e) {
+        const float dx = nb[e][0] - mx, dy = nb[e][1] - my, dz = nb[e][2] - mz;
+        cxx += dx * dx; cxy += dx * dy; cxz += dx * dz;
+        cyy += dy * dy; cyz += dy * dz; czz += dz * dz;
+    }
+    double A[3][3] = {{cxx, cxy, cxz}, {cxy, cyy, cyz}, {cxz, cyz, czz}};
+    double ev[3], V[3][3];
+    eig3(A, ev, V);
+    const float l1 = (float)ev[2], l2 = (float)ev[1], l3 = (float)ev[0];
+    float v0[3] = {(float)V[0][2], (float)V[1][2], (float)V[2][2]};
+    const float v1[3] = {(float)V[0][1], (float)V[1][1], (float)V[2][1]};
+    float nv[3] = {v0[1] * v1[2] - v0[2] * v1[1], v0[2] * v1[0] - v0[0] * v1[2], v0[0] * v1[1] - v0[1] * v1[0]};
+    float sq = v0[0] * v0[0] + v0[1] * v0[1] + v0[2] * v0[2];
+    if (sq > 0.f) { const float s = sqrtf(sq); v0[0] /= s; v0[1] /= s; v0[2] /= s; }
+    sq = nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2];
+    if (sq > 0.f) { const float s = sqrtf(sq); nv[0] /= s; nv[1] /= s; nv[2] /= s; }
+    const double d1 = l1, d2 = l2, d3 = l3;
+    const double linear_2 = (d1 - d2) / d1;
+    const double planar_2 = (d2 - d3) / d1;
+    if (linear_2 > (double)P.edge_thre) {
+        if (fabsf(v0[2]) > P.linear_vsin_high) return 1;
+        if (fabsf(v0[2]) < P.linear_vsin_low && qz < P.beam_h_max && qz > P.beam_h_min) return 2;
+    } else if (planar_2 > (double)P.planar_thre) {
+        if (fabsf(nv[2]) < P.planar_vsin_low) return 3;
+    }
+    return 0;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// KdTreeFLANN::radiusSearch(i, r, idx, d2, k) + PCA + decision for every U point. A team of T lanes
+// per query scans the 27 cells of the 1 m grid around it (every point with d^2 < r^2 <= 1 lies
+// there, pf_knn.h) T candidates at a time; candidates below the current k-th key (d^2 bits, index)
+// are merged into the team's sorted LDS list by rank (position = rank among the list + rank among
+// the chunk's survivors, all keys distinct). The k-th key only falls, so later chunks mostly pass
+// without a merge. Teams are aligned within a wave and every branch below is team-uniform.
+template <int T>
+__global__ void __launch_bounds__(256) k_cls_pca(ClsDev d, GridView gv) {
+    constexpr int TPB = 256 / T;
+    constexpr int KS = kClsMaxK + 1;                 // list stride (+1: teams on different banks)
+    constexpr int KB = (kClsMaxK + T - 1) / T;       // list entries per lane
+    __shared__ u64 best[TPB * KS];
+    __shared__ u64 buf[TPB * T];
+    __shared__ float nbp[TPB][kClsMaxK][4];
+    __shared__ int ccount[4];
+    if (threadIdx.x < 4) ccount[threadIdx.x] = 0;
+    __syncthreads();
+    const int team = threadIdx.x / T;
+    const u32 tl = threadIdx.x % T;
+    u64* B = best + team * KS;
+    u64* S = buf + team * T;
+    const int K = d.prm.k;
+    const float r2 = (float)((double)d.prm.radius * (double)d.prm.radius);
+    const int nu = d.cnt[CC_NU];
+    const int* dm = gv.dims;
+    const u64 tmask = (T == 64 ? ~0ull : ((1ull << T) - 1)) << (lane_id() & ~(T - 1));
+    const int nteams = gridDim.x * TPB;
+    const int b = (int)xcd_block(blockIdx.x, gridDim.x);
+    int cls_local[4] = {0, 0, 0, 0};
+    for (int q = b * TPB + team; q < nu; q += nteams) {        // uniform within a team
+        const float4 qp = d.U[q];
+        for (int e = (int)tl; e < K; e += T) B[e] = ~0ull;
+        wave_lds_sync();
+        u64 thr = ~0ull;
+        u32 total = 0;
+        int off[9];
+        u32 pre[9];
+        if (dm[7]) {
+            const float fcx = floorf(qp.x), fcy = floorf(qp.y), fcz = floorf(qp.z);
+            const int cx = (int)fcx, cy = (int)fcy, cz = (int)fcz;
+            const int minx = dm[0], miny = dm[1], minz = dm[2], dx = dm[3], dy = dm[4], dz = dm[5], base = dm[6];
+            const float lx = qp.x - fcx, hx = (fcx + 1.0f) - qp.x;
+            const float ly = qp.y - fcy, hy = (fcy + 1.0f) - qp.y;
+            const float lz = qp.z - fcz, hz = (fcz + 1.0f) - qp.z;
+#pragma unroll
+            for (int r = 0; r < 9; ++r) {                      // every lane derives all 9 rows
+                const int oy = r % 3 - 1, oz = r / 3 - 1;
+                const float by = oy < 0 ? ly : (oy > 0 ? hy : 0.0f);
+                const float bz = oz < 0 ? lz : (oz > 0 ? hz : 0.0f);
+                const float brow = (0.0f + by * by) + bz * bz;
+                const float bl = (lx * lx + by * by) + bz * bz;
+                const float bh = (hx * hx + by * by) + bz * bz;
+                const int y = cy + oy - miny, z = cz + oz - minz;
+                const int x0 = max(cx - (bl < r2 ? 1 : 0) - minx, 0);
+                const int x1 = min(cx + (bh < r2 ? 1 : 0) - minx, dx - 1);
+                const bool ok = brow < r2 && y >= 0 && y < dy && z >= 0 && z < dz && x0 <= x1;
+                u32 s = 0, e = 0;
+                if (ok) {
+                    const int c = base + (z * dy + y) * dx;
+                    s = gv.cell_start[c + x0];
+                    e = gv.cell_start[c + x1 + 1];
+                }
+                pre[r] = total;
+                off[r] = (int)(s - total);
+                total += e - s;
+            }
+        }
+        for (u32 v0 = 0; v0 < total; v0 += T) {
+            const u32 v = v0 + tl;
+            u64 key = ~0ull;
+            if (v < total) {
+                int o = off[0];
+#pragma unroll
+                for (int r = 1; r < 9; ++r) o = v >= pre[r] ? off[r] : o;
+                const float4 p = gv.cpts[(int)v + o];
+                const float dd = knn_d2(qp.x, qp.y, qp.z, p);
+                if (dd < r2) key = knn_key(dd, __float_as_int(p.w));
+            }
+            const bool surv = key < thr;
+            if ((__ballot(surv) & tmask) == 0) continue;
+            S[tl] = surv ? key : ~0ull;
+            wave_lds_sync();
+            int ps = K;
+            if (surv) {
+                int r1 = 0, rs = 0;
+                for (int e = 0; e < K; ++e) r1 += B[e] < key;
+#pragma unroll
+                for (int e = 0; e < T; ++e) rs += S[e] < key;
+                ps = r1 + rs;
+            }
+            u64 be[KB];
+            int pe[KB];
+#pragma unroll
+            for (int i = 0; i < KB; ++i) {
+                const int e = (int)tl + T * i;
+                be[i] = ~0ull;
+                pe[i] = K;
+                if (e < K) {
+                    be[i] = B[e];
+                    int rs = 0;
+#pragma unroll
+                    for (int f = 0; f < T; ++f) rs += S[f] < be[i];
+                    pe[i] = e + rs;
+                }
+            }
+            wave_lds_sync();
+            if (ps < K) B[ps] = key;
+#pragma unroll
+            for (int i = 0; i < KB; ++i)
+                if (pe[i] < K) B[pe[i]] = be[i];
+            wave_lds_sync();
+            thr = B[K - 1];
+        }
+        // the neighbourhood, ascending (d^2, index); coordinates from U
+        int found = 0;
+        for (int e = 0; e < K; ++e) found += B[e] != ~0ull;
+        for (int e = (int)tl; e < found; e += T) {
+            const float4 p = d.U[(u32)(B[e] & 0xffffffffull)];
+            nbp[team][e][0] = p.x; nbp[team][e][1] = p.y; nbp[team][e][2] = p.z;
+        }
+        wave_lds_sync();
+        if (tl == 0) {
+            const int code = pca_code(nbp[team], found, qp.z, d.prm);
+            const u32 key = code == 2 ? 0u : (code == 1 ? 1u : (code == 3 ? 2u : 3u));   // beam, pillar, facade, none
+            d.code[q] = (uint8_t)code;
+            d.ptnum[q] = found;
+            d.ckeys[q] = key;
+            d.cvals[q] = (u32)q;
+            cls_local[key]++;
+        }
+        wave_lds_sync();
+    }
+    for (int k = 0; k < 4; ++k)
+        if (cls_local[k]) atomicAdd(&ccount[k], cls_local[k]);
+    __syncthreads();
+    if (threadIdx.x < 4 && ccount[threadIdx.x]) atomicAdd(&d.cnt[CC_CLS + threadIdx.x], ccount[threadIdx.x]);
+}
+
+// the three clouds (U order within a class) and, optionally, their input indices
+__global__ void __launch_bounds__(256) k_cls_out(ClsDev d, const u32* __restrict__ ks, const u32* __restrict__ vs,
+                                                 float4* o0, float4* o1, float4* o2, int* c0, int* c1, int* c2,
+                                                 int* idx_out) {
+    const int nu = d.cnt[CC_NU];
+    const int n0 = d.cnt[CC_CLS], n1 = d.cnt[CC_CLS + 1], n2 = d.cnt[CC_CLS + 2];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (c0) *c0 = n0;
+        if (c1) *c1 = n1;
+        if (c2) *c2 = n2;
+    }
+    const int nout = n0 + n1 + n2;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nout && j < nu; j += gridDim.x * blockDim.x) {
+        const u32 k = ks[j];
+        const u32 u = vs[j];
+        const int pos = j - (k > 0 ? n0 : 0) - (k > 1 ? n1 : 0);
+        float4* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
+        if (o) o[pos] = d.U[u];
+        if (idx_out) idx_out[j] = (int)d.vals[u];
+    }
+}
+
+constexpr int kClsTeam = 16;
+constexpr int kEwBlocks = 512;
+
+}  // namespace
+
+int cls_alloc(ClsGPU& c, size_t cap) {
+    c.cap = cap;
+    const size_t cells = kGsMaxCells;
+    if (hipMalloc(&c.cnt, sizeof(int) * CC_COUNT) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.gb, sizeof(u32) * 8) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.gdim, sizeof(int) * 8) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.cell_cnt, sizeof(u32) * cells) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.cell_minz, sizeof(u32) * cells) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.cell_nb, sizeof(float) * cells) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.pcell, sizeof(u32) * cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.keys, sizeof(u32) * cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.vals, sizeof(u32) * cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.pts, sizeof(float4) * cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.U, sizeof(float4) * cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.ckeys, sizeof(u32) * cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.cvals, sizeof(u32) * cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.code, cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.ptnum, sizeof(int) * cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.idx_out, sizeof(int) * cap) != hipSuccess) return PF_ENOMEM;
+    const u32 gb0[8] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u, 0u, 0u, 0u};
+    if (hipMemcpy(c.gb, gb0, sizeof(gb0), hipMemcpyHostToDevice) != hipSuccess) return PF_EHIP;
+    if (hipMemset(c.cnt, 0, sizeof(int) * CC_COUNT) != hipSuccess) return PF_EHIP;
+    int rc = grid_alloc(c.grid, cap, kClsCells);
+    if (rc) return rc;
+    return prim_alloc(c.w, cap, kClsCells + 2);
+}
+
+void cls_free(ClsGPU& c) {
+    void* ps[] = {c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals, c.pts,
+                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.idx_out};
+    for (void* p : ps) (void)hipFree(p);
+    grid_free(c.grid);
+    prim_free(c.w);
+    c = ClsGPU{};
+}
+
+void cls_enqueue(ClsGPU& c, const float4* d_pts, const int* d_n, float4* const* out, int* const* out_cnt,
+                 bool idx, hipStream_t s) {
+    ClsDev d = dev_view(c);
+    if (c.prm.ground_filter) {
+        hipLaunchKernelGGL(k_gs_bounds, dim3(64), dim3(256), 0, s, d_pts, d_n, d);
+        hipLaunchKernelGGL(k_gs_assign, dim3(kEwBlocks), dim3(256), 0, s, d_pts, d_n, d);
+        hipLaunchKernelGGL(k_gs_nbmin, dim3(128), dim3(256), 0, s, d);
+        hipLaunchKernelGGL(k_gs_keys, dim3(kEwBlocks), dim3(256), 0, s, d_pts, d_n, d);
+        radix_sort_pairs(c.keys, c.vals, d_n, 16, c.w, s);
+        hipLaunchKernelGGL(k_gs_gather, dim3(kEwBlocks), dim3(256), 0, s, d_pts, d);
+    } else {
+        hipLaunchKernelGGL(k_cls_identity, dim3(kEwBlocks), dim3(256), 0, s, d_pts, d_n, d);
+    }
+    GridPtrs gp{};
+    gp.m[0] = c.U;
+    gp.n[0] = c.cnt + CC_NU;
+    gp.nm = 1;
+    grid_build(c.grid, gp, c.w, s);
+    const GridView gv{c.grid.dims, c.grid.cell_start, c.grid.cpts};
+    hipLaunchKernelGGL(k_cls_pca<kClsTeam>, dim3(2048), dim3(256), 0, s, d, gv);
+    u32 *ks = nullptr, *vs = nullptr;
+    radix_sort_pairs(c.ckeys, c.cvals, c.cnt + CC_NU, 8, c.w, s, &ks, &vs);
+    hipLaunchKernelGGL(k_cls_out, dim3(kEwBlocks), dim3(256), 0, s, d, ks, vs, out ? out[0] : nullptr,
+                       out ? out[1] : nullptr, out ? out[2] : nullptr, out_cnt ? out_cnt[0] : nullptr,
+                       out_cnt ? out_cnt[1] : nullptr, out_cnt ? out_cnt[2] : nullptr, idx ? c.idx_out : nullptr);
+}
+
+}  // namespace pf
+
+// ==================================================================================================
+// pf_cls C ABI
+// ==================================================================================================
+using namespace pf;
+
+struct pf_cls {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    ClsGPU c;
+    int* d_n = nullptr;
+    std::vector<float4> host;
+};
+
+namespace {
+bool cls_params_ok(const pf_cls_params* p) {
+    return p && p->k >= 1 && p->k <= kClsMaxK && p->radius > 0.f && p->radius <= 1.0f && p->gf_grid_res > 0.f;
+}
+void repack_xyz(const float* src, size_t n, size_t stride, std::vector<float4>& out) {
+    out.resize(n);
+    const char* b = reinterpret_cast<const char*>(src);
+    for (size_t i = 0; i < n; ++i) {
+        const float* p = reinterpret_cast<const float*>(b + i * stride);
+        out[i] = make_float4(p[0], p[1], p[2], 0.f);
+    }
+}
+int cls_run(pf_cls* h, const float* xyz, size_t n, size_t stride, bool idx) {
+    if (n > h->c.cap) return PF_ECAPACITY;
+    PF_HIP_TRY(hipSetDevice(h->device));
+    repack_xyz(xyz, n, stride, h->host);
+    const int ni = (int)n;
+    if (n) PF_HIP_TRY(hipMemcpyAsync(h->c.pts, h->host.data(), sizeof(float4) * n, hipMemcpyHostToDevice, h->stream));
+    PF_HIP_TRY(hipMemcpyAsync(h->d_n, &ni, sizeof(int), hipMemcpyHostToDevice, h->stream));
+    cls_enqueue(h->c, h->c.pts, h->d_n, nullptr, nullptr, idx, h->stream);
+    PF_HIP_TRY(hipGetLastError());
+    PF_HIP_TRY(hipStreamSynchronize(h->stream));
+    return PF_OK;
+}
+}  // namespace
+
+extern "C" {
+
+void pf_cls_default_params(pf_cls_params* p) {
+    if (!p) return;
+    p->ground_filter = 1;              // pfilter_kitti.launch:10
+    p->gf_min_grid_pts = 8;            // include/preProcess.hpp:575
+    p->gf_grid_res = 3.0f;             // :605
+    p->gf_max_height_diff = 0.3f;      // :604
+    p->gf_neighbor_height_diff = 1.5f; // :603
+    p->gf_max_ground_height = 5.0f;    // :601
+    p->gf_min_ground_height = -5.0f;   // :602
+    p->radius = 1.0f;                  // :703
+    p->k = 25;                         // :705
+    p->k_min = 8;                      // :706
+    p->edge_thre = 0.65f;              // :708
+    p->planar_thre = 0.65f;            // :709
+    p->linear_vsin_high = 0.94f;       // :710
+    p->linear_vsin_low = 0.17f;        // :711
+    p->planar_vsin_low = 0.34f;        // :713
+    p->beam_h_max = FLT_MAX;           // :714
+    p->beam_h_min = 0.5f;              // :715
+}
+
+int pf_cls_create(const pf_cls_params* p, int device, size_t max_points, pf_cls** out) {
+    if (!out || !cls_params_ok(p) || max_points == 0 || max_points > (size_t)INT_MAX / 2) return PF_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    PF_HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(device));
+    pf_cls* h = new pf_cls();
+    h->device = device;
+    h->c.prm = *p;
+    int rc = PF_OK;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) rc = PF_EHIP;
+    if (rc == PF_OK) rc = cls_alloc(h->c, max_points);
+    if (rc == PF_OK && hipMalloc(&h->d_n, sizeof(int)) != hipSuccess) rc = PF_ENOMEM;
+    if (rc != PF_OK) {
+        pf_cls_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return PF_OK;
+}
+
+int pf_cls_destroy(pf_cls* h) {
+    if (!h) return PF_EINVAL;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    cls_free(h->c);
+    (void)hipFree(h->d_n);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return PF_OK;
+}
+
+int pf_cls_extract(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, int32_t* beam, size_t* nb,
+                   int32_t* pillar, size_t* np, int32_t* facade, size_t* nf, int32_t* ground, size_t* ng,
+                   size_t cap) {
+    if (!h || (!xyz && n) || stride_bytes < 12) return PF_EINVAL;
+    int rc = cls_run(h, xyz, n, stride_bytes, true);
+    if (rc) return rc;
+    int cnt[CC_COUNT];
+    PF_HIP_TRY(hipMemcpy(cnt, h->c.cnt, sizeof(cnt), hipMemcpyDeviceToHost));
+    if (cnt[CC_ERR] || h->c.grid.err == nullptr) return PF_ECAPACITY;
+    int gerr = 0;
+    PF_HIP_TRY(hipMemcpy(&gerr, h->c.grid.err, sizeof(int), hipMemcpyDeviceToHost));
+    if (gerr) {
+        (void)hipMemset(h->c.grid.err, 0, sizeof(int));
+        return PF_ECAPACITY;
+    }
+    const size_t n0 = (size_t)cnt[CC_CLS], n1 = (size_t)cnt[CC_CLS + 1], n2 = (size_t)cnt[CC_CLS + 2];
+    const size_t ngr = (size_t)cnt[CC_NG], nu = (size_t)cnt[CC_NU];
+    if (nb) *nb = n0;
+    if (np) *np = n1;
+    if (nf) *nf = n2;
+    if (ng) *ng = ngr;
+    if ((beam && n0 > cap) || (pillar && n1 > cap) || (facade && n2 > cap) || (ground && ngr > cap))
+        return PF_ECAPACITY;
+    if (beam && n0) PF_HIP_TRY(hipMemcpy(beam, h->c.idx_out, sizeof(int) * n0, hipMemcpyDeviceToHost));
+    if (pillar && n1) PF_HIP_TRY(hipMemcpy(pillar, h->c.idx_out + n0, sizeof(int) * n1, hipMemcpyDeviceToHost));
+    if (facade && n2) PF_HIP_TRY(hipMemcpy(facade, h->c.idx_out + n0 + n1, sizeof(int) * n2, hipMemcpyDeviceToHost));
+    if (ground && ngr) PF_HIP_TRY(hipMemcpy(ground, h->c.vals + nu, sizeof(int) * ngr, hipMemcpyDeviceToHost));
+    return PF_OK;
+}
+
+int pf_cls_classify(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, uint8_t* cls, int32_t* pt_num) {
+    if (!h || (!xyz && n) || stride_bytes < 12) return PF_EINVAL;
+    const int gf = h->c.prm.ground_filter;
+    h->c.prm.ground_filter = 0;
+    int rc = cls_run(h, xyz, n, stride_bytes, false);
+    h->c.prm.ground_filter = gf;
+    if (rc) return rc;
+    int gerr = 0;
+    PF_HIP_TRY(hipMemcpy(&gerr, h->c.grid.err, sizeof(int), hipMemcpyDeviceToHost));
+    if (gerr) {
+        (void)hipMemset(h->c.grid.err, 0, sizeof(int));
+        return PF_ECAPACITY;
+    }
+    if (cls && n) PF_HIP_TRY(hipMemcpy(cls, h->c.code, n, hipMemcpyDeviceToHost));
+    if (pt_num && n) PF_HIP_TRY(hipMemcpy(pt_num, h->c.ptnum, sizeof(int) * n, hipMemcpyDeviceToHost));
+    return PF_OK;
+}
+
+}  // extern "C"

@@ -68,13 +68,25 @@ class OdomStats(ctypes.Structure):
         return d
 
 
+class ClsParams(ctypes.Structure):
+    """pf_cls_params: groundSeg / nongroundExtract members (include/preProcess.hpp:575-605, :703-715)."""
+    _fields_ = [("ground_filter", ctypes.c_int), ("gf_min_grid_pts", ctypes.c_int),
+                ("gf_grid_res", ctypes.c_float), ("gf_max_height_diff", ctypes.c_float),
+                ("gf_neighbor_height_diff", ctypes.c_float), ("gf_max_ground_height", ctypes.c_float),
+                ("gf_min_ground_height", ctypes.c_float), ("radius", ctypes.c_float), ("k", ctypes.c_int),
+                ("k_min", ctypes.c_int), ("edge_thre", ctypes.c_float), ("planar_thre", ctypes.c_float),
+                ("linear_vsin_high", ctypes.c_float), ("linear_vsin_low", ctypes.c_float),
+                ("planar_vsin_low", ctypes.c_float), ("beam_h_max", ctypes.c_float), ("beam_h_min", ctypes.c_float)]
+
+
 EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "pf_odom_destroy",
            "pf_odom_init_map", "pf_odom_update", "pf_odom_get_pose", "pf_odom_get_map", "pf_odom_set_map",
            "pf_odom_get_stats", "pf_odom_frame_device", "pf_odom_frame_host", "pf_odom_sync", "pf_odom_poses",
            "pf_odom_set_graph", "pf_device_count", "pf_dev_malloc", "pf_dev_free", "pf_memcpy_h2d",
            "pf_memcpy_d2h", "pf_knn_create", "pf_knn_destroy", "pf_knn_set_map", "pf_knn_query", "pf_knn_bench",
            "pf_bpf_create", "pf_bpf_init_map", "pf_bpf_update", "pf_bpf_frame_device", "pf_odom_classes",
-           "pf_odom_reset"]
+           "pf_odom_reset", "pf_cls_default_params", "pf_cls_create", "pf_cls_destroy", "pf_cls_extract",
+           "pf_cls_classify"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -124,6 +136,13 @@ def lib():
         L.pf_bpf_frame_device.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp]
         L.pf_odom_classes.argtypes = [_vp]
         L.pf_odom_reset.argtypes = [_vp]
+    if hasattr(L, "pf_cls_create"):
+        L.pf_cls_default_params.argtypes = [ctypes.POINTER(ClsParams)]
+        L.pf_cls_default_params.restype = None
+        L.pf_cls_create.argtypes = [ctypes.POINTER(ClsParams), _i, _sz, ctypes.POINTER(_vp)]
+        L.pf_cls_destroy.argtypes = [_vp]
+        L.pf_cls_extract.argtypes = [_vp, _vp, _sz, _sz] + [_vp, ctypes.POINTER(_sz)] * 4 + [_sz]
+        L.pf_cls_classify.argtypes = [_vp, _vp, _sz, _sz, _vp, _vp]
     _lib = L
     return L
 
@@ -410,4 +429,53 @@ class Knn:
     def __del__(self):
         if getattr(self, "_h", None):
             lib().pf_knn_destroy(self._h)
+            self._h = None
+
+
+def cls_params(**kw):
+    """The reference's defaults (pf_cls_default_params) with keyword overrides."""
+    p = ClsParams()
+    lib().pf_cls_default_params(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class BPFFrontEnd:
+    """groundSeg::ground_seg + nongroundExtract::featureExtract as src/additionNode.cpp:21-45 chains them
+    (include/preProcess.hpp:398-505, :646-689): a scan in, the beam / pillar / facade clouds (and the
+    ground cloud) out, as indices into the scan in the published order."""
+
+    def __init__(self, max_points=300000, device=0, **params):
+        self.params = cls_params(**params)
+        h = _vp()
+        _check("pf_cls_create", lib().pf_cls_create(ctypes.byref(self.params), device, int(max_points),
+                                                    ctypes.byref(h)), allow_warn=False)
+        self._h = h.value
+
+    def extract(self, xyz):
+        a = np.ascontiguousarray(xyz, dtype=np.float32)
+        n = a.shape[0]
+        bufs = [np.empty(max(n, 1), np.int32) for _ in range(4)]
+        cnt = [_sz() for _ in range(4)]
+        args = []
+        for b, c in zip(bufs, cnt):
+            args += [b.ctypes.data, ctypes.byref(c)]
+        _check("pf_cls_extract", lib().pf_cls_extract(self._h, a.ctypes.data, n, 4 * a.shape[1], *args, max(n, 1)),
+               allow_warn=False)
+        return {k: b[:c.value].copy() for k, b, c in zip(("beam", "pillar", "facade", "ground"), bufs, cnt)}
+
+    def classify(self, xyz):
+        """featureExtract alone: (index_with_feature code per point, neighbour count per point)."""
+        a = np.ascontiguousarray(xyz, dtype=np.float32)
+        n = a.shape[0]
+        cls = np.empty(max(n, 1), np.uint8)
+        num = np.empty(max(n, 1), np.int32)
+        _check("pf_cls_classify", lib().pf_cls_classify(self._h, a.ctypes.data, n, 4 * a.shape[1], cls.ctypes.data,
+                                                        num.ctypes.data), allow_warn=False)
+        return cls[:n].copy(), num[:n].copy()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().pf_cls_destroy(self._h)
             self._h = None

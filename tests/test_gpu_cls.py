@@ -1,0 +1,75 @@
+"""GPU: the BPF front end (groundSeg::ground_seg + nongroundExtract::featureExtract,
+include/preProcess.hpp:398-505 / :646-689, chained as src/additionNode.cpp:21-45) through the C ABI
+(pf_cls_*) against the oracle.
+
+Integer / index work, so the bar is bit-exact: the ground and non-ground push order, the radius
+k-NN neighbour counts, every point's pillar / beam / facade decision and the order of the published
+clouds equal the oracle's (both compute the PCA with the same f32 sums and f64 eigensolver)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fe(pa):
+    return pa.BPFFrontEnd(max_points=300000, device=0)
+
+
+def _same(got, want):
+    for k in ("beam", "pillar", "facade", "ground"):
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+
+
+@pytest.mark.parametrize("preset,frame", [("S64", 0), ("S64", 7), ("S32", 3)])
+def test_extract_matches_oracle(pa, pfref, pfsynth, fe, preset, frame):
+    x = pfsynth.Sequence(preset, n_frames=frame + 1).frame(frame)
+    got = fe.extract(x)
+    want = pfref.bpf_preprocess(x, pfref.cls_params())
+    _same(got, want)
+    assert len(got["facade"]) > 1000 and len(got["pillar"]) > 50 and len(got["ground"]) > 10000
+
+
+def test_classify_matches_oracle(pa, pfref, pfsynth, fe):
+    x = pfsynth.Sequence("S64", n_frames=3).frame(2)
+    g, u = pfref.ground_seg(x, pfref.cls_params())
+    U = x[u]
+    cls, num = fe.classify(U)
+    ocls, onum = pfref.pca_classify(U, pfref.cls_params())
+    np.testing.assert_array_equal(num, onum)
+    np.testing.assert_array_equal(cls, ocls)
+    assert np.all(num <= 25) and np.mean(num == 25) > 0.5
+
+
+@pytest.mark.parametrize("kw", [dict(k=5), dict(k=32, k_min=3), dict(radius=0.5), dict(ground_filter=0),
+                                dict(gf_grid_res=1.0, gf_min_grid_pts=3), dict(beam_h_min=-10.0, edge_thre=0.5)])
+def test_parameters(pa, pfref, pfsynth, kw):
+    x = pfsynth.Sequence("S32", n_frames=2, az_steps=900).frame(1)
+    f = pa.BPFFrontEnd(max_points=200000, device=0, **kw)
+    _same(f.extract(x), pfref.bpf_preprocess(x, pfref.cls_params(**kw)))
+
+
+def test_edge_cases(pa, pfref, fe):
+    rng = np.random.default_rng(11)
+    cases = [np.zeros((0, 4), np.float32),                                   # empty scan
+             np.array([[1, 2, 0, 0]], np.float32),                             # one point
+             rng.uniform(-1, 1, (7, 4)).astype(np.float32),                    # fewer than one cell's minimum
+             np.c_[rng.uniform(-5, 5, (500, 2)), rng.uniform(6, 9, 500), np.zeros(500)].astype(np.float32),  # all high
+             np.repeat(np.array([[3.0, 4.0, -1.0, 0]], np.float32), 40, 0),   # duplicates: d^2 ties, x range 0
+             np.c_[np.linspace(0, 2.9999, 300), np.linspace(0, 6, 300), np.full(300, -1.7), np.zeros(300)].astype(np.float32)]
+    for x in cases:
+        _same(fe.extract(x), pfref.bpf_preprocess(x, pfref.cls_params()))
+
+
+def test_rejects(pa, pfsynth):
+    with pytest.raises(pa.PFError):
+        pa.BPFFrontEnd(max_points=1000, k=33)
+    with pytest.raises(pa.PFError):
+        pa.BPFFrontEnd(max_points=1000, radius=1.5)
+    small = pa.BPFFrontEnd(max_points=1000)
+    x = pfsynth.Sequence("S32", n_frames=1, az_steps=300).frame(0)
+    with pytest.raises(pa.PFError):
+        small.extract(x)                                                       # larger than max_points
+    far = np.array([[0, 0, 0], [2000.0, 2000.0, 0]], np.float32)               # ground grid > 32766 cells
+    with pytest.raises(pa.PFError):
+        small.extract(far)
