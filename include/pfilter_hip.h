@@ -164,6 +164,14 @@ int pf_cls_extract(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, i
  * be NULL */
 int pf_cls_classify(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, uint8_t* cls, int32_t* pt_num);
 
+/* BPF whole-frame mode: one raw scan (device pointer to n packed float4) per call; stage A runs the
+ * front end above (ground_seg + featureExtract) into the beam / pillar / facade clouds, then the
+ * VoxelGrid, stage B the odometry (the additionNode -> odomEstimationNode chain without ROS).
+ * set_front_end fixes the front end's parameters (default: pf_cls_default_params); n <= the handle's
+ * max_points. pose_out may be NULL (enqueue only), as pf_odom_frame_device. */
+int pf_bpf_set_front_end(pf_odom* h, const pf_cls_params* p);
+int pf_bpf_frame_scan_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]);
+
 /* ---------------- whole-frame device pipeline (featureExtraction -> odometry) ----------------
  * d_xyzi: device pointer to n packed float4 points (HBM-resident scan). The first frame seeds the
  * map (initMapWithPoints), later frames run updatePointsToMap. The pose of every frame is kept on

@@ -407,11 +407,20 @@ int pf_odom_get_stats(pf_odom* h, pf_odom_stats* s) {
 // whole frame on the device, as two pipelined stages. In steady state (optimization_count == 2)
 // each stage replays a hipGraph captured once per slot; the scan is first copied into the handle's
 // fixed staging buffer and its size written to the slot's counters (both outside the graph).
-static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool stage_a) {
+// BPF raw-scan mode, stage A head: the front end (ground_seg + featureExtract) of the staged scan
+// writes slot p's beam / pillar / facade clouds and their device-resident sizes
+static void stage_enqueue_front(OdomGPU& o, int p, hipStream_t s) {
+    float4* out[3] = {o.sb[p].in[0], o.sb[p].in[1], o.sb[p].in[2]};
+    int* cnt[3] = {o.sb[p].cnt + C_IN, o.sb[p].cnt + C_IN + 1, o.sb[p].cnt + C_IN + 2};
+    cls_enqueue(*o.front, o.stage, o.sb[p].cnt + C_NIN, out, cnt, false, s);
+}
+
+static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool stage_a, bool scan = false) {
     hipGraph_t g;
     PF_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     if (stage_a) {
         if (o.cls.nc == 2) stage_enqueue_fe(o, p, o.stage, s);
+        else if (scan) stage_enqueue_front(o, p, s);
         stage_enqueue_vg(o, p, s);
     } else {
         odom_enqueue_update(o, p, s);
@@ -424,15 +433,19 @@ static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool s
 
 // one frame through both stages. ES: the raw scan d_in[0 .. n) is copied to the staging buffer and
 // stage A runs featureExtraction + VoxelGrid. BPF: the class clouds cl[c][0 .. ncl[c]) are copied
-// into the slot's inputs and stage A runs VoxelGrid. The copies and counts stay outside the graphs.
+// into the slot's inputs and stage A runs VoxelGrid; BPF raw-scan mode (cl null): the scan is staged
+// as for ES and stage A runs the front end (pf_cls.h) then VoxelGrid. The copies and counts stay
+// outside the graphs.
 static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4* const* cl, const size_t* ncl) {
     OdomGPU& o = h->o;
     const int nc = o.cls.nc;
+    const bool scan = nc == 3 && !cl;
     const int p = o.frames % kSlots;
     const bool steady = o.inited && o.opt_count_host <= 2 && o.graph_enabled;
+    if (scan && n > o.in_cap) return PF_ECAPACITY;
     int rc = stage_a_begin(h, p);
     if (rc) return rc;
-    if (nc == 2) {
+    if (nc == 2 || scan) {
         if (n > o.in_cap) return PF_ECAPACITY;
         if (n) PF_HIP_TRY(hipMemcpyAsync(o.stage, d_in, sizeof(float4) * n, hipMemcpyDeviceToDevice, o.stream_a));
         hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, o.sb[p].cnt + C_NIN, (int)n);
@@ -445,13 +458,15 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
         }
     }
     if (steady) {
-        if (!o.graph_a[p]) {
-            rc = capture(o.stream_a, &o.graph_a[p], o, p, true);
+        hipGraphExec_t& ga = scan ? o.graph_as[p] : o.graph_a[p];
+        if (!ga) {
+            rc = capture(o.stream_a, &ga, o, p, true, scan);
             if (rc) return rc;
         }
-        PF_HIP_TRY(hipGraphLaunch(o.graph_a[p], o.stream_a));
+        PF_HIP_TRY(hipGraphLaunch(ga, o.stream_a));
     } else {
         if (nc == 2) stage_enqueue_fe(o, p, o.stage, o.stream_a);
+        else if (scan) stage_enqueue_front(o, p, o.stream_a);
         if (o.inited) stage_enqueue_vg(o, p, o.stream_a);
     }
     rc = stage_a_end_b_begin(h, p);
@@ -505,6 +520,47 @@ int pf_bpf_frame_device(pf_odom* h, const float* d_beam, size_t nb, const float*
                            reinterpret_cast<const float4*>(d_facade)};
     const size_t n[3] = {nb, np, nf};
     int rc = enqueue_frame(h, nullptr, 0, cl, n);
+    if (rc) return rc;
+    if (pose_out) return read_pose(h, pose_out);
+    return PF_OK;
+}
+
+int pf_bpf_set_front_end(pf_odom* h, const pf_cls_params* p) {
+    if (!h || h->o.cls.nc != 3 || !p || p->k < 1 || p->k > kClsMaxK || !(p->radius > 0.f) || p->radius > 1.0f ||
+        !(p->gf_grid_res > 0.f))
+        return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    if (!o.front) {
+        o.front = new ClsGPU();
+        const int rc = cls_alloc(*o.front, o.in_cap);
+        if (rc) {
+            cls_free(*o.front);
+            delete o.front;
+            o.front = nullptr;
+            return rc;
+        }
+    }
+    o.front->prm = *p;
+    for (int s = 0; s < kSlots; ++s)        // parameters are baked into the captured kernels
+        if (o.graph_as[s]) {
+            (void)hipGraphExecDestroy(o.graph_as[s]);
+            o.graph_as[s] = nullptr;
+        }
+    return PF_OK;
+}
+
+int pf_bpf_frame_scan_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]) {
+    if (!h || (!d_xyzi && n) || h->o.cls.nc != 3) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    if (!h->o.front) {
+        pf_cls_params p;
+        pf_cls_default_params(&p);
+        const int rc = pf_bpf_set_front_end(h, &p);
+        if (rc) return rc;
+    }
+    int rc = enqueue_frame(h, reinterpret_cast<const float4*>(d_xyzi), n, nullptr, nullptr);
     if (rc) return rc;
     if (pose_out) return read_pose(h, pose_out);
     return PF_OK;

@@ -1,6 +1,7 @@
 // Device-resident Odom_ES_EstimationClass (src/odomEstimationClass.cpp:182-647) and
 // Odom_BPF_EstimationClass (:649-1306): one pipeline over 2 or 3 map classes.
 #pragma once
+#include "pf_cls.h"
 #include "pf_common.h"
 #include "pf_fe.h"
 #include "pf_knn.h"
@@ -116,6 +117,8 @@ struct OdomGPU {
     hipEvent_t ev_b[kSlots] = {};                           // stage B done with slot p
     hipGraphExec_t graph_a[kSlots] = {};                    // steady-state replay per slot
     hipGraphExec_t graph_b[kSlots] = {};
+    ClsGPU* front = nullptr;                                // BPF raw-scan mode: the PCA front end
+    hipGraphExec_t graph_as[kSlots] = {};                   // stage A replay in raw-scan mode
     float4* map[kMaxC] = {};       // local maps
     float4* app[kMaxC] = {};       // this frame's transformed down-sampled points (appended)
     float4* seg_out = nullptr;

@@ -1502,6 +1502,7 @@ void odom_destroy(OdomGPU& o) {
     for (int p = 0; p < kSlots; ++p) {
         if (o.graph_a[p]) (void)hipGraphExecDestroy(o.graph_a[p]);
         if (o.graph_b[p]) (void)hipGraphExecDestroy(o.graph_b[p]);
+        if (o.graph_as[p]) (void)hipGraphExecDestroy(o.graph_as[p]);
         if (o.ev_a[p]) (void)hipEventDestroy(o.ev_a[p]);
         if (o.ev_b[p]) (void)hipEventDestroy(o.ev_b[p]);
         for (int c = 0; c < kMaxC; ++c) {
@@ -1511,6 +1512,10 @@ void odom_destroy(OdomGPU& o) {
         (void)hipFree(o.sb[p].cnt);
     }
     fe_free(o.fe);
+    if (o.front) {
+        cls_free(*o.front);
+        delete o.front;
+    }
     grid_free(o.grid);
     prim_free(o.prim);
     prim_free(o.vprim);

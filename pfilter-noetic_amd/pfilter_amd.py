@@ -86,7 +86,7 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_memcpy_d2h", "pf_knn_create", "pf_knn_destroy", "pf_knn_set_map", "pf_knn_query", "pf_knn_bench",
            "pf_bpf_create", "pf_bpf_init_map", "pf_bpf_update", "pf_bpf_frame_device", "pf_odom_classes",
            "pf_odom_reset", "pf_cls_default_params", "pf_cls_create", "pf_cls_destroy", "pf_cls_extract",
-           "pf_cls_classify"]
+           "pf_cls_classify", "pf_bpf_set_front_end", "pf_bpf_frame_scan_device"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -143,6 +143,8 @@ def lib():
         L.pf_cls_destroy.argtypes = [_vp]
         L.pf_cls_extract.argtypes = [_vp, _vp, _sz, _sz] + [_vp, ctypes.POINTER(_sz)] * 4 + [_sz]
         L.pf_cls_classify.argtypes = [_vp, _vp, _sz, _sz, _vp, _vp]
+        L.pf_bpf_set_front_end.argtypes = [_vp, ctypes.POINTER(ClsParams)]
+        L.pf_bpf_frame_scan_device.argtypes = [_vp, _vp, _sz, _vp]
     _lib = L
     return L
 
@@ -396,8 +398,31 @@ class Odom_BPF_EstimationClass(Odom_ES_EstimationClass):
                                                                 pose.ctypes.data if want_pose else None))
         return pose if want_pose else None
 
+    # ---- raw-scan mode: the front end (ground_seg + featureExtract) in stage A, then the odometry ----
+    def set_front_end(self, **params):
+        """pf_cls_params of the front end (defaults: the reference's members, include/preProcess.hpp)"""
+        self.front_params = cls_params(**params)
+        _check("pf_bpf_set_front_end", lib().pf_bpf_set_front_end(self._h, ctypes.byref(self.front_params)),
+               allow_warn=False)
+
+    def frame_scan_device(self, dptr, n, want_pose=False):
+        """one raw scan already in HBM (packed float4) -> pose"""
+        pose = np.empty(7)
+        _check("pf_bpf_frame_scan_device", lib().pf_bpf_frame_scan_device(
+            self._h, dptr, int(n), pose.ctypes.data if want_pose else None))
+        return pose if want_pose else None
+
     def frame_host(self, xyzi, want_pose=True):
-        raise NotImplementedError("the BPF estimator takes classified beam / pillar / facade clouds")
+        """one raw scan from host memory (staged through a device buffer) -> pose"""
+        x = _f32x4(xyzi)
+        buf = getattr(self, "_scan_buf", None)
+        if buf is None or buf.nbytes < max(x.nbytes, 16):
+            if buf is not None:
+                self.sync()
+            buf = self._scan_buf = DeviceBuffer(max(x.nbytes, 16, 16 * self.max_points), self.device)
+        self.sync()                   # the previous frame's stage A has consumed the buffer
+        buf.upload(x)
+        return self.frame_scan_device(buf.ptr, x.shape[0], want_pose)
 
 
 class Knn:
