@@ -316,37 +316,30 @@ def host_leg(device, nframes, threads):
 
 
 def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True, use_graph=True):
-    """Odom_BPF_EstimationClass (src/odomEstimationClass.cpp:649-1306) frames/s on the same S64 sequence
-    with configs[1]'s parameters. Its inputs are beam / pillar / facade clouds: featureExtraction (on the
-    GPU, untimed) split by pfsynth.bpf_split, the stand-in for the reference's PCA classifier. All clouds
-    are HBM-resident before the timed region; the timed loop is pf_bpf_frame_device per frame."""
+    """The BPF chain frames/s on the same S64 sequence with configs[1]'s odometry parameters: raw scan ->
+    groundSeg::ground_seg + nongroundExtract::featureExtract (include/preProcess.hpp:398-505, 646-689) ->
+    Odom_BPF_EstimationClass (src/odomEstimationClass.cpp:649-1306), i.e. the additionNode ->
+    odomEstimationNode path without ROS. All scans are HBM-resident before the timed region; the timed
+    loop is pf_bpf_frame_scan_device per frame (front end + VoxelGrid in stage A, odometry in stage B)."""
     import pfilter_amd as pa
     import pfsynth
     total = warmup + nframes
     seq = pfsynth.Sequence("S64", n_frames=total, seed=0)
-    fe = pa.LaserProcessingClass(device=device)
-    fe.init(lidar_cfg())
-    clouds = []
+    stride = 128000 * 16                         # bytes per frame slot (S64: <= 128,000 rays)
+    scans = pa.DeviceBuffer(stride * total, device=device)
+    counts = []
     for f0 in range(0, total, 256):
         nf = min(256, total - f0)
-        buf, counts = seq.frames(f0, nf, threads=threads)
+        buf, cnt = seq.frames(f0, nf, threads=threads)
         for i in range(nf):
-            clouds.append(pfsynth.bpf_split(*fe.featureExtraction(buf[i, :counts[i]])))
-    bufs, ptrs = [], []
-    for c in range(3):                           # one HBM buffer per class, frames back to back
-        sizes = [cl[c].shape[0] for cl in clouds]
-        flat = np.concatenate([cl[c] for cl in clouds]).astype(np.float32)
-        db = pa.DeviceBuffer(max(flat.nbytes, 16), device=device)
-        db.upload(flat)
-        bufs.append(db)
-        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
-        ptrs.append([(db.ptr + int(o) * 16, n) for o, n in zip(offs, sizes)])
+            scans.upload(np.ascontiguousarray(buf[i, :cnt[i]], np.float32), (f0 + i) * stride)
+            counts.append(int(cnt[i]))
     od = pa.Odom_BPF_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lidar_cfg(), **ODOM_CFG)
     od.set_graph(use_graph)
 
     def run(k):
-        od.frame_device([ptrs[c][k][0] for c in range(3)], [ptrs[c][k][1] for c in range(3)])
+        od.frame_scan_device(scans.ptr + k * stride, counts[k])
 
     for k in range(warmup):
         run(k)
@@ -359,30 +352,35 @@ def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True
     st = od.stats()
     out = {"value": round(nframes / el, 2), "unit": "frames/s", "frames": nframes,
            "ms_per_step": round(el / nframes * 1e3, 4),
-           "workload": "Odom_BPF_EstimationClass on S64 seed 0 (configs[1] parameters), beam/pillar/facade = "
-                       "featureExtraction split by pfsynth.bpf_split",
-           "last_frame": {"n_ds": st["n_ds"], "n_map": st["n_map"], "n_res": st["n_res"]}}
+           "workload": "raw S64 seed 0 scan -> ground_seg + PCA featureExtract (reference defaults) -> "
+                       "Odom_BPF_EstimationClass (configs[1] parameters)",
+           "last_frame": {"n_in": st["n_in"], "n_ds": st["n_ds"], "n_map": st["n_map"], "n_res": st["n_res"]}}
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pfref
         lid = pfref.make_lidar(64, 3.0, 90.0)
+        cp = pfref.cls_params()
         orc = pfref.OdomBPF(lid, 0.4, 0, 0.4, 75, 0, opts=0)
+        cw = min(warmup, 11)                     # optimization_count reaches its steady 2 after 10 frames
         n, el, k = 0, 0.0, 0
-        while k < total and (el < cpu_seconds or k < warmup):
-            e, s_ = pfref.feature_extraction(seq.frame(k), lid)
-            cl = pfsynth.bpf_split(e, s_)
+        while k < total and (el < cpu_seconds or k < cw):
+            x = seq.frame(k)
             t = time.perf_counter()
+            r = pfref.bpf_preprocess(x, cp)
+            cl = [np.c_[x[r[c], :3], np.zeros(len(r[c]))].astype(np.float32) for c in ("beam", "pillar", "facade")]
             if k == 0:
                 orc.init_map(*cl)
             else:
                 orc.update(*cl)
-            if k >= warmup:
+            if k >= cw:
                 el += time.perf_counter() - t
                 n += 1
             k += 1
         out["cpu_baseline"] = {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-                               "sample": "pfref OdomBPF (reference-faithful opts=0), frames %d..%d, single thread, "
-                                         "%.1f s of CPU time (updatePointsToMap only)" % (warmup, k - 1, el)}
+                               "sample": "pfref front end (radius k-NN over a hash grid, PCA) + OdomBPF "
+                                         "(reference-faithful opts=0), frames %d..%d, single thread (the "
+                                         "reference's PCA loop uses up to 6 OpenMP threads, preProcess.hpp:207), "
+                                         "%.1f s of CPU time" % (cw, k - 1, el)}
         out["speedup_vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
     return out
 

@@ -5,6 +5,7 @@
 #include <cfloat>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 namespace pf {
@@ -114,25 +115,46 @@ __global__ void __launch_bounds__(256) k_gs_bounds(const float4* __restrict__ pt
     }
 }
 
-// :427-448: cell of every point, the cell's point count, its lowest z in (min, max ground height]
+// :427-448: cell of every point, the cell's point count, its lowest z in (min, max ground height].
+// Scan order puts runs of consecutive points into one 3 m cell: a wave takes one count atomic and
+// one min atomic per run (up to 16 runs, the rest per lane) instead of serialising on the cell.
 __global__ void __launch_bounds__(256) k_gs_assign(const float4* __restrict__ pts, const int* __restrict__ d_n, ClsDev d) {
     const int n = *d_n;
     const int col = d.gdim[1], num = d.gdim[2];
     const double minx = (double)__int_as_float(d.gdim[4]), miny = (double)__int_as_float(d.gdim[5]);
     const double res = (double)d.prm.gf_grid_res;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const float4 p = pts[i];
-        const int tc = (int)floor(((double)p.x - minx) / res);
-        const int tr = (int)floor(((double)p.y - miny) / res);
-        const long long id = (long long)tr * col + tc;
+    const int stride = gridDim.x * blockDim.x;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i - lane_id() < n; i += stride) {   // wave-uniform
         u32 cell = ~0u;
-        if (id >= 0 && id < num) {
-            cell = (u32)id;
-            atomicAdd(&d.cell_cnt[cell], 1u);
-            if (!(p.z > d.prm.gf_max_ground_height) && p.z > d.prm.gf_min_ground_height && p.z < FLT_MAX)
-                atomicMin(&d.cell_minz[cell], f2ord(p.z));
+        float zq = INFINITY;                       // z if it may be the cell's min_z
+        if (i < n) {
+            const float4 p = pts[i];
+            const int tc = (int)floor(((double)p.x - minx) / res);
+            const int tr = (int)floor(((double)p.y - miny) / res);
+            const long long id = (long long)tr * col + tc;
+            if (id >= 0 && id < num) {
+                cell = (u32)id;
+                if (!(p.z > d.prm.gf_max_ground_height) && p.z > d.prm.gf_min_ground_height && p.z < FLT_MAX)
+                    zq = p.z;
+            }
+            d.pcell[i] = cell;
         }
-        d.pcell[i] = cell;
+        u64 todo = __ballot(cell != ~0u);
+        for (int it = 0; it < 16 && todo; ++it) {
+            const int leader = __ffsll((unsigned long long)todo) - 1;
+            const u32 c = (u32)__shfl((int)cell, leader, 64);
+            const u64 m = __ballot(cell == c) & todo;
+            const float zm = wave_minf(((m >> lane_id()) & 1ull) ? zq : INFINITY);
+            if (lane_id() == leader) {
+                atomicAdd(&d.cell_cnt[c], (u32)__popcll(m));
+                if (zm < INFINITY) atomicMin(&d.cell_minz[c], f2ord(zm));
+            }
+            todo &= ~m;
+        }
+        if ((todo >> lane_id()) & 1ull) {
+            atomicAdd(&d.cell_cnt[cell], 1u);
+            if (zq < INFINITY) atomicMin(&d.cell_minz[cell], f2ord(zq));
+        }
     }
 }
 
@@ -226,6 +248,9 @@ __global__ void __launch_bounds__(256) k_cls_identity(const float4* __restrict__
 // of the f32 covariance, rounded back to f32. Returns the index_with_feature code.
 __device__ int pca_code(const float (*nb)[4], int n, float qz, const pf_cls_params& P) {
     if (!(n > P.k_min) || n <= 3) return 0;
+#ifdef PF_DEV_NOPCA
+    return 3;                                  // development: the search without the PCA (timing only)
+#endif
     float sx = 0.f, sy = 0.f, sz = 0.f;
     for (int e = 0; e < n; ++e) { sx += nb[e][0]; sy += nb[e][1]; sz += nb[e][2]; }
     const float fn = (float)n;
@@ -265,43 +290,93 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// KdTreeFLANN::radiusSearch(i, r, idx, d2, k) + PCA + decision for every U point. A team of T lanes
-// per query scans the 27 cells of the 1 m grid around it (every point with d^2 < r^2 <= 1 lies
-// there, pf_knn.h) T candidates at a time; candidates below the current k-th key (d^2 bits, index)
-// are merged into the team's sorted LDS list by rank (position = rank among the list + rank among
-// the chunk's survivors, all keys distinct). The k-th key only falls, so later chunks mostly pass
-// without a merge. Teams are aligned within a wave and every branch below is team-uniform.
-template <int T>
+// 64-bit lane move within a DPP row of 16 lanes: lane l takes lane l - 1's value, lane 0 of the row 0
+__device__ __forceinline__ u64 row_shr1_u64(u64 v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(u32)v, 0x111, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(u32)(v >> 32), 0x111, 0xf, 0xf, true);
+    return ((u64)(u32)hi << 32) | (u64)(u32)lo;
+}
+__device__ __forceinline__ u64 shfl_u64(u64 v, int src) {
+    const int lo = __shfl((int)(u32)v, src, 64), hi = __shfl((int)(u32)(v >> 32), src, 64);
+    return ((u64)(u32)hi << 32) | (u64)(u32)lo;
+}
+
+// KdTreeFLANN::radiusSearch(i, r, idx, d2, k) + PCA + decision for every U point. A team of 16 lanes
+// (one DPP row) per query scans the 27 cells of the 1 m grid around it (every point with d^2 < r^2
+// <= 1 lies there, pf_knn.h) 16 candidates at a time, nearest cells first. The team's sorted list
+// of the k best keys (d^2 bits, index) lives in registers, entry j on lane j % 16 (lo: j < 16, hi:
+// j >= 16); a candidate below the k-th key is inserted by one row shift (every entry compares with
+// the key and takes its left neighbour, the key or itself; keys are distinct). Once the list is
+// full, a cell range whose float lower bound exceeds the k-th distance is skipped (exact, pf_knn.h):
+// in dense regions the query's own cell usually settles the list and most cells are never read.
+// Branches are uniform within a team.
+constexpr int kClsTeam = 16;
 __global__ void __launch_bounds__(256) k_cls_pca(ClsDev d, GridView gv) {
-    constexpr int TPB = 256 / T;
-    constexpr int KS = kClsMaxK + 1;                 // list stride (+1: teams on different banks)
-    constexpr int KB = (kClsMaxK + T - 1) / T;       // list entries per lane
-    __shared__ u64 best[TPB * KS];
-    __shared__ u64 buf[TPB * T];
+    constexpr int T = kClsTeam, TPB = 256 / T;
     __shared__ float nbp[TPB][kClsMaxK][4];
     __shared__ int ccount[4];
     if (threadIdx.x < 4) ccount[threadIdx.x] = 0;
     __syncthreads();
     const int team = threadIdx.x / T;
     const u32 tl = threadIdx.x % T;
-    u64* B = best + team * KS;
-    u64* S = buf + team * T;
+    const int tb = lane_id() & ~(T - 1);
     const int K = d.prm.k;
+    const int kl = tb + ((K - 1) & (T - 1));        // lane holding entry K - 1
+    const bool khi = K > T;                          // ... in its hi register
     const float r2 = (float)((double)d.prm.radius * (double)d.prm.radius);
     const int nu = d.cnt[CC_NU];
     const int* dm = gv.dims;
-    const u64 tmask = (T == 64 ? ~0ull : ((1ull << T) - 1)) << (lane_id() & ~(T - 1));
+    const u64 tmask = ((1ull << T) - 1) << tb;
     const int nteams = gridDim.x * TPB;
-    const int b = (int)xcd_block(blockIdx.x, gridDim.x);
+    const int bq = (int)xcd_block(blockIdx.x, gridDim.x);
     int cls_local[4] = {0, 0, 0, 0};
-    for (int q = b * TPB + team; q < nu; q += nteams) {        // uniform within a team
+    for (int q = bq * TPB + team; q < nu; q += nteams) {       // uniform within a team
         const float4 qp = d.U[q];
-        for (int e = (int)tl; e < K; e += T) B[e] = ~0ull;
-        wave_lds_sync();
-        u64 thr = ~0ull;
-        u32 total = 0;
-        int off[9];
-        u32 pre[9];
+        u64 lo = ~0ull, hi = ~0ull;                  // the list: entries tl and T + tl
+        u64 thr = ~0ull;                             // entry K - 1
+        auto insert = [&](u64 key) {
+            const u64 plo = row_shr1_u64(lo);
+            u64 phi = row_shr1_u64(hi);
+            const u64 last_lo = shfl_u64(lo, tb + T - 1);
+            if (tl == 0) phi = last_lo;
+            const u64 nlo = key < plo ? plo : (key < lo ? key : lo);
+            const u64 nhi = key < phi ? phi : (key < hi ? key : hi);
+            lo = nlo;
+            hi = nhi;
+            thr = shfl_u64(khi ? hi : lo, kl);
+        };
+        // one chunk: every candidate below the k-th key, in lane order
+        auto chunk = [&](u32 v0, u32 end, const float4& p) {
+            u64 key = ~0ull;
+            if (v0 + tl < end) {
+                const float dd = knn_d2(qp.x, qp.y, qp.z, p);
+                if (dd < r2) key = knn_key(dd, __float_as_int(p.w));
+            }
+            u64 m = __ballot(key < thr) & tmask;
+            while (m) {                              // uniform within the team
+                const int src = __ffsll((unsigned long long)m) - 1;
+                const u64 kk = shfl_u64(key, src);
+                if (kk < thr) insert(kk);
+                m &= m - 1;
+            }
+        };
+        // a range [a, b) chunk by chunk, the next chunk's load issued before the current one is used
+        auto scan = [&](u32 a, u32 b) {
+            if (a >= b) return;
+            float4 pc = a + tl < b ? gv.cpts[a + tl] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (u32 v0 = a; v0 < b; v0 += T) {
+                const u32 vn = v0 + T + tl;
+                const float4 pn = vn < b ? gv.cpts[vn] : pc;
+                chunk(v0, b, pc);
+                pc = pn;
+            }
+        };
+        // a range can hold a point of the list only if its float lower bound lb of d^2 is < r^2 and,
+        // once the list is full, <= the k-th distance (a point at exactly the k-th distance may still
+        // win on its index)
+        auto open = [&](float lb) {
+            return lb < r2 && (thr == ~0ull || lb <= __uint_as_float((u32)(thr >> 32)));
+        };
         if (dm[7]) {
             const float fcx = floorf(qp.x), fcy = floorf(qp.y), fcz = floorf(qp.z);
             const int cx = (int)fcx, cy = (int)fcy, cz = (int)fcz;
@@ -309,88 +384,60 @@ __global__ void __launch_bounds__(256) k_cls_pca(ClsDev d, GridView gv) {
             const float lx = qp.x - fcx, hx = (fcx + 1.0f) - qp.x;
             const float ly = qp.y - fcy, hy = (fcy + 1.0f) - qp.y;
             const float lz = qp.z - fcz, hz = (fcz + 1.0f) - qp.z;
+            const int xi = cx - minx;                          // the query's own cell is in the grid
+            // lane r < 9 of the team loads x-row r's cell boundaries (r = (oz + 1) * 3 + oy + 1):
+            // starts of cells xi - 1, xi, xi + 1 and the end of xi + 1
+            u32 w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+            if (tl < 9) {
+                const int y = cy + (int)(tl % 3) - 1 - miny, z = cz + (int)(tl / 3) - 1 - minz;
+                if (y >= 0 && y < dy && z >= 0 && z < dz) {
+                    const u32* cs = gv.cell_start + base + (z * dy + y) * dx + xi;
+                    w1 = cs[0];
+                    w2 = cs[1];
+                    w0 = xi > 0 ? cs[-1] : w1;
+                    w3 = xi + 1 < dx ? cs[2] : w2;
+                }
+            }
+            // rows nearest first: the query's own row (own cell, then its x neighbours), the four
+            // face rows, the four corner rows
+            constexpr int order[9] = {4, 3, 5, 1, 7, 0, 2, 6, 8};
 #pragma unroll
-            for (int r = 0; r < 9; ++r) {                      // every lane derives all 9 rows
+            for (int k = 0; k < 9; ++k) {
+                const int r = order[k];
                 const int oy = r % 3 - 1, oz = r / 3 - 1;
+                const u32 s0 = (u32)__shfl((int)w0, tb + r, 64), s1 = (u32)__shfl((int)w1, tb + r, 64);
+                const u32 s2 = (u32)__shfl((int)w2, tb + r, 64), s3 = (u32)__shfl((int)w3, tb + r, 64);
                 const float by = oy < 0 ? ly : (oy > 0 ? hy : 0.0f);
                 const float bz = oz < 0 ? lz : (oz > 0 ? hz : 0.0f);
                 const float brow = (0.0f + by * by) + bz * bz;
                 const float bl = (lx * lx + by * by) + bz * bz;
                 const float bh = (hx * hx + by * by) + bz * bz;
-                const int y = cy + oy - miny, z = cz + oz - minz;
-                const int x0 = max(cx - (bl < r2 ? 1 : 0) - minx, 0);
-                const int x1 = min(cx + (bh < r2 ? 1 : 0) - minx, dx - 1);
-                const bool ok = brow < r2 && y >= 0 && y < dy && z >= 0 && z < dz && x0 <= x1;
-                u32 s = 0, e = 0;
-                if (ok) {
-                    const int c = base + (z * dy + y) * dx;
-                    s = gv.cell_start[c + x0];
-                    e = gv.cell_start[c + x1 + 1];
-                }
-                pre[r] = total;
-                off[r] = (int)(s - total);
-                total += e - s;
-            }
-        }
-        for (u32 v0 = 0; v0 < total; v0 += T) {
-            const u32 v = v0 + tl;
-            u64 key = ~0ull;
-            if (v < total) {
-                int o = off[0];
-#pragma unroll
-                for (int r = 1; r < 9; ++r) o = v >= pre[r] ? off[r] : o;
-                const float4 p = gv.cpts[(int)v + o];
-                const float dd = knn_d2(qp.x, qp.y, qp.z, p);
-                if (dd < r2) key = knn_key(dd, __float_as_int(p.w));
-            }
-            const bool surv = key < thr;
-            if ((__ballot(surv) & tmask) == 0) continue;
-            S[tl] = surv ? key : ~0ull;
-            wave_lds_sync();
-            int ps = K;
-            if (surv) {
-                int r1 = 0, rs = 0;
-                for (int e = 0; e < K; ++e) r1 += B[e] < key;
-#pragma unroll
-                for (int e = 0; e < T; ++e) rs += S[e] < key;
-                ps = r1 + rs;
-            }
-            u64 be[KB];
-            int pe[KB];
-#pragma unroll
-            for (int i = 0; i < KB; ++i) {
-                const int e = (int)tl + T * i;
-                be[i] = ~0ull;
-                pe[i] = K;
-                if (e < K) {
-                    be[i] = B[e];
-                    int rs = 0;
-#pragma unroll
-                    for (int f = 0; f < T; ++f) rs += S[f] < be[i];
-                    pe[i] = e + rs;
+                if (r == 4) {
+                    scan(s1, s2);
+                    if (open(bl)) scan(s0, s1);
+                    if (open(bh)) scan(s2, s3);
+                } else if (open(brow)) {
+                    scan(open(bl) ? s0 : s1, open(bh) ? s3 : s2);
                 }
             }
-            wave_lds_sync();
-            if (ps < K) B[ps] = key;
-#pragma unroll
-            for (int i = 0; i < KB; ++i)
-                if (pe[i] < K) B[pe[i]] = be[i];
-            wave_lds_sync();
-            thr = B[K - 1];
         }
         // the neighbourhood, ascending (d^2, index); coordinates from U
-        int found = 0;
-        for (int e = 0; e < K; ++e) found += B[e] != ~0ull;
-        for (int e = (int)tl; e < found; e += T) {
-            const float4 p = d.U[(u32)(B[e] & 0xffffffffull)];
-            nbp[team][e][0] = p.x; nbp[team][e][1] = p.y; nbp[team][e][2] = p.z;
+        const int found = __popcll(__ballot(lo != ~0ull) & tmask) + __popcll(__ballot(hi != ~0ull) & tmask);
+        const int nf = found < K ? found : K;
+        if ((int)tl < nf) {
+            const float4 p = d.U[(u32)(lo & 0xffffffffull)];
+            nbp[team][tl][0] = p.x; nbp[team][tl][1] = p.y; nbp[team][tl][2] = p.z;
+        }
+        if ((int)(T + tl) < nf) {
+            const float4 p = d.U[(u32)(hi & 0xffffffffull)];
+            nbp[team][T + tl][0] = p.x; nbp[team][T + tl][1] = p.y; nbp[team][T + tl][2] = p.z;
         }
         wave_lds_sync();
         if (tl == 0) {
-            const int code = pca_code(nbp[team], found, qp.z, d.prm);
+            const int code = pca_code(nbp[team], nf, qp.z, d.prm);
             const u32 key = code == 2 ? 0u : (code == 1 ? 1u : (code == 3 ? 2u : 3u));   // beam, pillar, facade, none
             d.code[q] = (uint8_t)code;
-            d.ptnum[q] = found;
+            d.ptnum[q] = nf;
             d.ckeys[q] = key;
             d.cvals[q] = (u32)q;
             cls_local[key]++;
@@ -425,7 +472,6 @@ __global__ void __launch_bounds__(256) k_cls_out(ClsDev d, const u32* __restrict
     }
 }
 
-constexpr int kClsTeam = 16;
 constexpr int kEwBlocks = 512;
 
 }  // namespace
@@ -483,9 +529,9 @@ void cls_enqueue(ClsGPU& c, const float4* d_pts, const int* d_n, float4* const* 
     gp.m[0] = c.U;
     gp.n[0] = c.cnt + CC_NU;
     gp.nm = 1;
-    grid_build(c.grid, gp, c.w, s);
+    grid_build(c.grid, gp, c.w, s, false, true);
     const GridView gv{c.grid.dims, c.grid.cell_start, c.grid.cpts};
-    hipLaunchKernelGGL(k_cls_pca<kClsTeam>, dim3(2048), dim3(256), 0, s, d, gv);
+    hipLaunchKernelGGL(k_cls_pca, dim3(2048), dim3(256), 0, s, d, gv);
     u32 *ks = nullptr, *vs = nullptr;
     radix_sort_pairs(c.ckeys, c.cvals, c.cnt + CC_NU, 8, c.w, s, &ks, &vs);
     hipLaunchKernelGGL(k_cls_out, dim3(kEwBlocks), dim3(256), 0, s, d, ks, vs, out ? out[0] : nullptr,

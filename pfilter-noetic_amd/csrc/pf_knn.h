@@ -192,7 +192,9 @@ constexpr int kGridBoundsBlocks = 64;
 
 // Build the grids of gp.nm maps (counts device-resident). pts_cap must hold all maps' points.
 // bounds_launched: the caller already ran k_grid_bounds (with its own tail) on this stream.
-void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s, bool bounds_launched = false);
+// aggregate: one counter atomic per run of equal cells in a wave (clouds in spatially coherent order)
+void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s, bool bounds_launched = false,
+                bool aggregate = false);
 
 struct GridView {
     const int* dims;

@@ -12,15 +12,39 @@ __device__ __forceinline__ int cell_of(const int* dm, float4 p) {
     return dm[6] + (z * dm[4] + y) * dm[3] + x;
 }
 
+// Agg: clouds whose consecutive points mostly share a cell (the front end's non-ground cloud, in
+// 3 m ground-cell order) take one atomic per run of equal cells in a wave (up to 4 runs; the rest
+// per lane) instead of serialising on the cell's counter. Slots inside a cell are arbitrary either
+// way (the queries order candidates by (d^2, index)).
+template <bool Agg>
 __global__ void __launch_bounds__(256) k_grid_count(GridPtrs gp, const int* __restrict__ dims, u32* __restrict__ cnt,
                                                      u32* __restrict__ slot) {
     const GridIdx gi = grid_idx(gp);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < gi.total; i += gridDim.x * blockDim.x) {
-        const int mi = gi.map_of(i);
-        const int* dm = dims + 8 * mi;
-        if (!dm[7]) continue;
-        const float4 p = gp.m[mi][i - gi.start(mi)];
-        slot[i] = atomicAdd(&cnt[cell_of(dm, p)], 1u);
+    const int stride = gridDim.x * blockDim.x;
+    const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int i = i0; Agg ? (i - (int)threadIdx.x % 64 < gi.total) : (i < gi.total); i += stride) {
+        int cid = -1;
+        if (i < gi.total) {
+            const int mi = gi.map_of(i);
+            const int* dm = dims + 8 * mi;
+            if (dm[7]) cid = cell_of(dm, gp.m[mi][i - gi.start(mi)]);
+        }
+        if (!Agg) {
+            if (cid >= 0) slot[i] = atomicAdd(&cnt[cid], 1u);
+            continue;
+        }
+        u64 todo = __ballot(cid >= 0);
+        for (int it = 0; it < 4 && todo; ++it) {          // wave-uniform
+            const int leader = __ffsll((unsigned long long)todo) - 1;
+            const int c = __shfl(cid, leader, 64);
+            const u64 m = __ballot(cid == c) & todo;
+            u32 b = 0;
+            if (lane_id() == leader) b = atomicAdd(&cnt[c], (u32)__popcll(m));
+            b = (u32)__shfl((int)b, leader, 64);
+            if ((m >> lane_id()) & 1ull) slot[i] = b + (u32)__popcll(m & lanemask_lt());
+            todo &= ~m;
+        }
+        if ((todo >> lane_id()) & 1ull) slot[i] = atomicAdd(&cnt[cid], 1u);
     }
 }
 
@@ -131,12 +155,15 @@ void grid_free(GridGPU& g) {
     g = GridGPU{};
 }
 
-void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s, bool bounds_launched) {
+void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s, bool bounds_launched, bool aggregate) {
     const int nb = 512;
     if (!bounds_launched)
         hipLaunchKernelGGL(k_grid_bounds<NoTail>, dim3(kGridBoundsBlocks), dim3(256), 0, s, grid_bounds_args(g, gp),
                            NoTail{});
-    hipLaunchKernelGGL(k_grid_count, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot);
+    if (aggregate)
+        hipLaunchKernelGGL(k_grid_count<true>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot);
+    else
+        hipLaunchKernelGGL(k_grid_count<false>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot);
     scan_exclusive(g.cell_count, g.cell_start, g.d_ncells, nullptr, w, s);
     hipLaunchKernelGGL(k_grid_scatter, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_start, g.slot, g.cpts,
                        g.cell_count);
