@@ -31,10 +31,12 @@ struct ClsDev {          // kernel view of ClsGPU
     u32* cvals;
     uint8_t* code;
     int* ptnum;
+    int* pos;
+    float4* box;
 };
 ClsDev dev_view(ClsGPU& c) {
     return ClsDev{c.prm, c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals,
-                  c.U, c.ckeys, c.cvals, c.code, c.ptnum};
+                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.pos, c.box};
 }
 
 __device__ __forceinline__ float wave_minf(float v) {
@@ -243,21 +245,94 @@ __global__ void __launch_bounds__(256) k_cls_identity(const float4* __restrict__
 
 // ---- featureExtract ----------------------------------------------------------------------------
 
+// The U grid: 1 m cells (pf_knn.h) whose points are ordered inside each cell by the Morton code of
+// their 0.125 m sub-cell, so that every aligned 16-point chunk of the cell-ordered array is compact;
+// the chunks' bounding boxes let the search skip chunks the way a kd-tree skips leaves.
+__device__ __forceinline__ u32 morton3(u32 x, u32 y, u32 z) {
+    u32 m = 0;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) m |= (((x >> b) & 1u) << (3 * b)) | (((y >> b) & 1u) << (3 * b + 1)) | (((z >> b) & 1u) << (3 * b + 2));
+    return m;
+}
+__device__ __forceinline__ u32 sub8(float v) {
+    const float f = (v - floorf(v)) * 8.0f;
+    const int s = (int)f;
+    return (u32)(s < 0 ? 0 : (s > 7 ? 7 : s));
+}
+__global__ void __launch_bounds__(256) k_u_keys(ClsDev d, const int* __restrict__ dm) {
+    const int nu = d.cnt[CC_NU];
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nu; j += gridDim.x * blockDim.x) {
+        const float4 p = d.U[j];
+        u32 key = 0;
+        if (dm[7]) {
+            const int x = (int)floorf(p.x) - dm[0], y = (int)floorf(p.y) - dm[1], z = (int)floorf(p.z) - dm[2];
+            const u32 cell = (u32)(dm[6] + (z * dm[4] + y) * dm[3] + x);
+            key = (cell << 9) | morton3(sub8(p.x), sub8(p.y), sub8(p.z));
+        }
+        d.ckeys[j] = key;
+        d.cvals[j] = (u32)j;
+    }
+}
+// cell-ordered points (w = U index), U index -> position, and the counts left zero for the next build
+__global__ void __launch_bounds__(256) k_u_place(ClsDev d, float4* __restrict__ cpts, u32* __restrict__ cell_count,
+                                                 const int* __restrict__ dm) {
+    const int nu = d.cnt[CC_NU];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
+        const u32 j = d.cvals[i];
+        const float4 p = d.U[j];
+        cpts[i] = make_float4(p.x, p.y, p.z, __int_as_float((int)j));
+        d.pos[j] = i;
+        if (dm[7]) cell_count[d.ckeys[i] >> 9] = 0u;
+    }
+}
+// bounding box of every aligned 16-point chunk (a DPP row per chunk)
+__global__ void __launch_bounds__(256) k_u_boxes(ClsDev d, const float4* __restrict__ cpts) {
+    const int nu = d.cnt[CC_NU];
+    const int nch = (nu + 15) / 16;
+    const int l = threadIdx.x & 15;
+    for (int c = (blockIdx.x * blockDim.x + threadIdx.x) / 16; c - (int)(threadIdx.x & 63) / 16 < nch;
+         c += gridDim.x * blockDim.x / 16) {
+        const int i = c * 16 + l;
+        float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.f), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+        if (c < nch && i < nu) {
+            const float4 p = cpts[i];
+            lo = make_float4(p.x, p.y, p.z, 0.f);
+            hi = lo;
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            lo.x = fminf(lo.x, __shfl_xor(lo.x, o, 64)); lo.y = fminf(lo.y, __shfl_xor(lo.y, o, 64));
+            lo.z = fminf(lo.z, __shfl_xor(lo.z, o, 64));
+            hi.x = fmaxf(hi.x, __shfl_xor(hi.x, o, 64)); hi.y = fmaxf(hi.y, __shfl_xor(hi.y, o, 64));
+            hi.z = fmaxf(hi.z, __shfl_xor(hi.z, o, 64));
+        }
+        if (c < nch && l == 0) {
+            d.box[2 * c] = lo;
+            d.box[2 * c + 1] = hi;
+        }
+    }
+}
+
 // PCA of the neighbourhood nb[0 .. n) (ascending distance) and the class decision, :653-688 /
 // :283-323, f32 as pcl::PCA computes it; the eigen-decomposition is the f64 cyclic Jacobi (eig3)
 // of the f32 covariance, rounded back to f32. Returns the index_with_feature code.
-__device__ int pca_code(const float (*nb)[4], int n, float qz, const pf_cls_params& P) {
+template <class Get>
+__device__ int pca_code(Get get, int n, float qz, const pf_cls_params& P) {
     if (!(n > P.k_min) || n <= 3) return 0;
 #ifdef PF_DEV_NOPCA
     return 3;                                  // development: the search without the PCA (timing only)
 #endif
     float sx = 0.f, sy = 0.f, sz = 0.f;
-    for (int e = 0; e < n; ++e) { sx += nb[e][0]; sy += nb[e][1]; sz += nb[e][2]; }
+    for (int e = 0; e < n; ++e) {
+        const float4 p = get(e);
+        sx += p.x; sy += p.y; sz += p.z;
+    }
     const float fn = (float)n;
     const float mx = sx / fn, my = sy / fn, mz = sz / fn;
     float cxx = 0.f, cxy = 0.f, cxz = 0.f, cyy = 0.f, cyz = 0.f, czz = 0.f;
-    for (int e = 0; e < n; ++e) {
-        const float dx = nb[e][0] - mx, dy = nb[e][1] - my, dz = nb[e][2] - mz;
+    for (int e = 0; e < n; ++e) {              // the neighbours again (L2-resident) instead of a copy
+        const float4 p = get(e);
+        const float dx = p.x - mx, dy = p.y - my, dz = p.z - mz;
         cxx += dx * dx; cxy += dx * dy; cxz += dx * dz;
         cyy += dy * dy; cyz += dy * dz; czz += dz * dz;
     }
@@ -284,98 +359,97 @@ __device__ int pca_code(const float (*nb)[4], int n, float qz, const pf_cls_para
     return 0;
 }
 
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+__device__ __forceinline__ u64 readlane_u64(u64 v, int lane) {
+    const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, lane);
+    const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), lane);
+    return ((u64)hi << 32) | (u64)lo;
 }
-
-// 64-bit lane move within a DPP row of 16 lanes: lane l takes lane l - 1's value, lane 0 of the row 0
-__device__ __forceinline__ u64 row_shr1_u64(u64 v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(u32)v, 0x111, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(u32)(v >> 32), 0x111, 0xf, 0xf, true);
-    return ((u64)(u32)hi << 32) | (u64)(u32)lo;
-}
-__device__ __forceinline__ u64 shfl_u64(u64 v, int src) {
-    const int lo = __shfl((int)(u32)v, src, 64), hi = __shfl((int)(u32)(v >> 32), src, 64);
+// lane l takes lane l - 1's value, lane 0 takes 0 (DPP wave_shr:1)
+__device__ __forceinline__ u64 wave_shr1_u64(u64 v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(u32)v, 0x138, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(u32)(v >> 32), 0x138, 0xf, 0xf, true);
     return ((u64)(u32)hi << 32) | (u64)(u32)lo;
 }
 
-// KdTreeFLANN::radiusSearch(i, r, idx, d2, k) + PCA + decision for every U point. A team of 16 lanes
-// (one DPP row) per query scans the 27 cells of the 1 m grid around it (every point with d^2 < r^2
-// <= 1 lies there, pf_knn.h) 16 candidates at a time, nearest cells first. The team's sorted list
-// of the k best keys (d^2 bits, index) lives in registers, entry j on lane j % 16 (lo: j < 16, hi:
-// j >= 16); a candidate below the k-th key is inserted by one row shift (every entry compares with
-// the key and takes its left neighbour, the key or itself; keys are distinct). Once the list is
-// full, a cell range whose float lower bound exceeds the k-th distance is skipped (exact, pf_knn.h):
-// in dense regions the query's own cell usually settles the list and most cells are never read.
-// Branches are uniform within a team.
-constexpr int kClsTeam = 16;
-__global__ void __launch_bounds__(256) k_cls_pca(ClsDev d, GridView gv) {
-    constexpr int T = kClsTeam, TPB = 256 / T;
-    __shared__ float nbp[TPB][kClsMaxK][4];
-    __shared__ int ccount[4];
-    if (threadIdx.x < 4) ccount[threadIdx.x] = 0;
-    __syncthreads();
-    const int team = threadIdx.x / T;
-    const u32 tl = threadIdx.x % T;
-    const int tb = lane_id() & ~(T - 1);
+// KdTreeFLANN::radiusSearch(i, r, idx, d2, k) for every U point, one wave per query. The candidates
+// are the 27 cells of the 1 m grid around the query (every point with d^2 < r^2 <= 1 lies there,
+// pf_knn.h), nearest rows first, the query's own 16-point chunk first. The sorted list of the k best
+// keys (d^2 bits, index) lives in registers, entry j on lane j; a candidate below the k-th key is
+// inserted by one wave shift (every entry compares with the key and takes its left neighbour, the
+// key or itself; keys are distinct), with the candidate and the k-th key moved through scalar
+// registers. Chunks are skipped by their boxes' float lower bound of d^2 (exact, pf_knn.h): once the
+// list is full, a chunk whose bound exceeds the k-th distance cannot hold a winner, and in dense
+// regions most of the 27 cells' chunks are never read. Up to 4 open chunks are read per pass, one
+// per 16 lanes. Writes the neighbour lists (ascending) and their sizes.
+__global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* __restrict__ nbr) {
+    constexpr int WPB = 4;
     const int K = d.prm.k;
-    const int kl = tb + ((K - 1) & (T - 1));        // lane holding entry K - 1
-    const bool khi = K > T;                          // ... in its hi register
     const float r2 = (float)((double)d.prm.radius * (double)d.prm.radius);
     const int nu = d.cnt[CC_NU];
     const int* dm = gv.dims;
-    const u64 tmask = ((1ull << T) - 1) << tb;
-    const int nteams = gridDim.x * TPB;
-    const int bq = (int)xcd_block(blockIdx.x, gridDim.x);
-    int cls_local[4] = {0, 0, 0, 0};
-    for (int q = bq * TPB + team; q < nu; q += nteams) {       // uniform within a team
+    const int l = lane_id();
+    const int nw = gridDim.x * WPB;
+    const int wv = (int)xcd_block(blockIdx.x, gridDim.x) * WPB + (int)(threadIdx.x >> 6);
+    for (int q = wv; q < nu; q += nw) {                      // wave-uniform
         const float4 qp = d.U[q];
-        u64 lo = ~0ull, hi = ~0ull;                  // the list: entries tl and T + tl
-        u64 thr = ~0ull;                             // entry K - 1
-        auto insert = [&](u64 key) {
-            const u64 plo = row_shr1_u64(lo);
-            u64 phi = row_shr1_u64(hi);
-            const u64 last_lo = shfl_u64(lo, tb + T - 1);
-            if (tl == 0) phi = last_lo;
-            const u64 nlo = key < plo ? plo : (key < lo ? key : lo);
-            const u64 nhi = key < phi ? phi : (key < hi ? key : hi);
-            lo = nlo;
-            hi = nhi;
-            thr = shfl_u64(khi ? hi : lo, kl);
-        };
-        // one chunk: every candidate below the k-th key, in lane order
-        auto chunk = [&](u32 v0, u32 end, const float4& p) {
-            u64 key = ~0ull;
-            if (v0 + tl < end) {
-                const float dd = knn_d2(qp.x, qp.y, qp.z, p);
-                if (dd < r2) key = knn_key(dd, __float_as_int(p.w));
-            }
-            u64 m = __ballot(key < thr) & tmask;
-            while (m) {                              // uniform within the team
-                const int src = __ffsll((unsigned long long)m) - 1;
-                const u64 kk = shfl_u64(key, src);
-                if (kk < thr) insert(kk);
-                m &= m - 1;
-            }
-        };
-        // a range [a, b) chunk by chunk, the next chunk's load issued before the current one is used
-        auto scan = [&](u32 a, u32 b) {
-            if (a >= b) return;
-            float4 pc = a + tl < b ? gv.cpts[a + tl] : make_float4(0.f, 0.f, 0.f, 0.f);
-            for (u32 v0 = a; v0 < b; v0 += T) {
-                const u32 vn = v0 + T + tl;
-                const float4 pn = vn < b ? gv.cpts[vn] : pc;
-                chunk(v0, b, pc);
-                pc = pn;
-            }
-        };
-        // a range can hold a point of the list only if its float lower bound lb of d^2 is < r^2 and,
-        // once the list is full, <= the k-th distance (a point at exactly the k-th distance may still
-        // win on its index)
+        u64 ent = ~0ull;                                     // list entry l
+        u64 thr = ~0ull;                                     // entry K - 1
         auto open = [&](float lb) {
             return lb < r2 && (thr == ~0ull || lb <= __uint_as_float((u32)(thr >> 32)));
+        };
+        auto box_lb = [&](int c) {
+            const float4 lo = d.box[2 * c], hi = d.box[2 * c + 1];
+            const float tx = qp.x < lo.x ? lo.x - qp.x : (qp.x > hi.x ? qp.x - hi.x : 0.0f);
+            const float ty = qp.y < lo.y ? lo.y - qp.y : (qp.y > hi.y ? qp.y - hi.y : 0.0f);
+            const float tz = qp.z < lo.z ? lo.z - qp.z : (qp.z > hi.z ? qp.z - hi.z : 0.0f);
+            return (0.0f + tx * tx + ty * ty) + tz * tz;
+        };
+        // the aligned 16-point chunks overlapping [a, b): 64 chunks' bounds per round, then the open
+        // ones 4 at a time, each bound re-checked as the k-th distance falls
+        auto scan = [&](u32 a, u32 b) {
+            if (a >= b) return;
+            const int c0 = (int)(a >> 4), c1 = (int)((b - 1) >> 4);
+            for (int g = c0; g <= c1; g += 64) {
+                const int cl = g + l;
+                const float lb = cl <= c1 ? box_lb(cl) : INFINITY;
+                u64 m = __ballot(open(lb));
+                while (m) {
+                    // up to 4 open chunks: lanes 16 i .. 16 i + 15 read the i-th
+                    int src[4];
+                    int nsel = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        src[i] = -1;
+                        while (m && src[i] < 0) {
+                            const int sl = __ffsll((unsigned long long)m) - 1;
+                            m &= m - 1;
+                            if (open(__shfl(lb, sl, 64))) src[i] = sl;
+                        }
+                        nsel += src[i] >= 0;
+                    }
+                    if (!nsel) break;
+                    const int mine = src[l >> 4];
+                    u64 key = ~0ull;
+                    if (mine >= 0) {
+                        const u32 v = (u32)(g + mine) * 16u + (u32)(l & 15);
+                        if (v >= a && v < b) {
+                            const float4 p = gv.cpts[v];
+                            const float dd = knn_d2(qp.x, qp.y, qp.z, p);
+                            if (dd < r2) key = knn_key(dd, __float_as_int(p.w));
+                        }
+                    }
+                    u64 sm = __ballot(key < thr);
+                    while (sm) {
+                        const int sl = __ffsll((unsigned long long)sm) - 1;
+                        sm &= sm - 1;
+                        const u64 kk = readlane_u64(key, sl);
+                        if (!(kk < thr)) continue;
+                        const u64 prev = wave_shr1_u64(ent);
+                        ent = kk < prev ? prev : (kk < ent ? kk : ent);
+                        thr = readlane_u64(ent, K - 1);
+                    }
+                }
+            }
         };
         if (dm[7]) {
             const float fcx = floorf(qp.x), fcy = floorf(qp.y), fcz = floorf(qp.z);
@@ -385,11 +459,11 @@ __global__ void __launch_bounds__(256) k_cls_pca(ClsDev d, GridView gv) {
             const float ly = qp.y - fcy, hy = (fcy + 1.0f) - qp.y;
             const float lz = qp.z - fcz, hz = (fcz + 1.0f) - qp.z;
             const int xi = cx - minx;                          // the query's own cell is in the grid
-            // lane r < 9 of the team loads x-row r's cell boundaries (r = (oz + 1) * 3 + oy + 1):
-            // starts of cells xi - 1, xi, xi + 1 and the end of xi + 1
+            // lane r < 9 loads x-row r's cell boundaries (r = (oz + 1) * 3 + oy + 1): starts of cells
+            // xi - 1, xi, xi + 1 and the end of xi + 1
             u32 w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-            if (tl < 9) {
-                const int y = cy + (int)(tl % 3) - 1 - miny, z = cz + (int)(tl / 3) - 1 - minz;
+            if (l < 9) {
+                const int y = cy + l % 3 - 1 - miny, z = cz + l / 3 - 1 - minz;
                 if (y >= 0 && y < dy && z >= 0 && z < dz) {
                     const u32* cs = gv.cell_start + base + (z * dy + y) * dx + xi;
                     w1 = cs[0];
@@ -398,22 +472,26 @@ __global__ void __launch_bounds__(256) k_cls_pca(ClsDev d, GridView gv) {
                     w3 = xi + 1 < dx ? cs[2] : w2;
                 }
             }
-            // rows nearest first: the query's own row (own cell, then its x neighbours), the four
-            // face rows, the four corner rows
+            // rows nearest first: the query's own row (own chunk, own cell, its x neighbours), the
+            // four face rows, the four corner rows
             constexpr int order[9] = {4, 3, 5, 1, 7, 0, 2, 6, 8};
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
                 const int r = order[k];
                 const int oy = r % 3 - 1, oz = r / 3 - 1;
-                const u32 s0 = (u32)__shfl((int)w0, tb + r, 64), s1 = (u32)__shfl((int)w1, tb + r, 64);
-                const u32 s2 = (u32)__shfl((int)w2, tb + r, 64), s3 = (u32)__shfl((int)w3, tb + r, 64);
+                const u32 s0 = (u32)__builtin_amdgcn_readlane((int)w0, r), s1 = (u32)__builtin_amdgcn_readlane((int)w1, r);
+                const u32 s2 = (u32)__builtin_amdgcn_readlane((int)w2, r), s3 = (u32)__builtin_amdgcn_readlane((int)w3, r);
                 const float by = oy < 0 ? ly : (oy > 0 ? hy : 0.0f);
                 const float bz = oz < 0 ? lz : (oz > 0 ? hz : 0.0f);
                 const float brow = (0.0f + by * by) + bz * bz;
                 const float bl = (lx * lx + by * by) + bz * bz;
                 const float bh = (hx * hx + by * by) + bz * bz;
                 if (r == 4) {
-                    scan(s1, s2);
+                    const u32 oc = (u32)d.pos[q] & ~15u;
+                    const u32 ca = oc > s1 ? oc : s1, cb = oc + 16 < s2 ? oc + 16 : s2;
+                    scan(ca, cb);
+                    scan(s1, ca);
+                    scan(cb, s2);
                     if (open(bl)) scan(s0, s1);
                     if (open(bh)) scan(s2, s3);
                 } else if (open(brow)) {
@@ -421,31 +499,34 @@ __global__ void __launch_bounds__(256) k_cls_pca(ClsDev d, GridView gv) {
                 }
             }
         }
-        // the neighbourhood, ascending (d^2, index); coordinates from U
-        const int found = __popcll(__ballot(lo != ~0ull) & tmask) + __popcll(__ballot(hi != ~0ull) & tmask);
-        const int nf = found < K ? found : K;
-        if ((int)tl < nf) {
-            const float4 p = d.U[(u32)(lo & 0xffffffffull)];
-            nbp[team][tl][0] = p.x; nbp[team][tl][1] = p.y; nbp[team][tl][2] = p.z;
-        }
-        if ((int)(T + tl) < nf) {
-            const float4 p = d.U[(u32)(hi & 0xffffffffull)];
-            nbp[team][T + tl][0] = p.x; nbp[team][T + tl][1] = p.y; nbp[team][T + tl][2] = p.z;
-        }
-        wave_lds_sync();
-        if (tl == 0) {
-            const int code = pca_code(nbp[team], nf, qp.z, d.prm);
-            const u32 key = code == 2 ? 0u : (code == 1 ? 1u : (code == 3 ? 2u : 3u));   // beam, pillar, facade, none
-            d.code[q] = (uint8_t)code;
-            d.ptnum[q] = nf;
-            d.ckeys[q] = key;
-            d.cvals[q] = (u32)q;
-            cls_local[key]++;
-        }
-        wave_lds_sync();
+        const int found = __popcll(__ballot(l < K && ent != ~0ull));
+        if (l < found) nbr[(size_t)q * kClsMaxK + l] = (u32)(ent & 0xffffffffull);
+        if (l == 0) d.ptnum[q] = found;
     }
-    for (int k = 0; k < 4; ++k)
-        if (cls_local[k]) atomicAdd(&ccount[k], cls_local[k]);
+}
+
+// PCA + decision, one thread per U point over its neighbour list (ascending distance)
+__global__ void __launch_bounds__(256) k_cls_decide(ClsDev d, const u32* __restrict__ nbr) {
+    __shared__ int ccount[4];
+    if (threadIdx.x < 4) ccount[threadIdx.x] = 0;
+    __syncthreads();
+    const int nu = d.cnt[CC_NU];
+    int local[4] = {0, 0, 0, 0};
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nu; q += gridDim.x * blockDim.x) {
+        const int n = d.ptnum[q];
+        const u32* lst = nbr + (size_t)q * kClsMaxK;
+        const float4* U = d.U;
+        const int code = pca_code([&](int e) { return U[lst[e]]; }, n, U[q].z, d.prm);
+        const u32 key = code == 2 ? 0u : (code == 1 ? 1u : (code == 3 ? 2u : 3u));   // beam, pillar, facade, none
+        d.code[q] = (uint8_t)code;
+        d.ckeys[q] = key;
+        d.cvals[q] = (u32)q;
+        local[key]++;
+    }
+    for (int k = 0; k < 4; ++k) {
+        const int v = wave_sum_i(local[k]);
+        if (lane_id() == 0 && v) atomicAdd(&ccount[k], v);
+    }
     __syncthreads();
     if (threadIdx.x < 4 && ccount[threadIdx.x]) atomicAdd(&d.cnt[CC_CLS + threadIdx.x], ccount[threadIdx.x]);
 }
@@ -495,6 +576,9 @@ int cls_alloc(ClsGPU& c, size_t cap) {
     if (hipMalloc(&c.code, cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&c.ptnum, sizeof(int) * cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&c.idx_out, sizeof(int) * cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.pos, sizeof(int) * cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.nbr, sizeof(u32) * kClsMaxK * cap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.box, sizeof(float4) * 2 * (cap / 16 + 1)) != hipSuccess) return PF_ENOMEM;
     const u32 gb0[8] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u, 0u, 0u, 0u};
     if (hipMemcpy(c.gb, gb0, sizeof(gb0), hipMemcpyHostToDevice) != hipSuccess) return PF_EHIP;
     if (hipMemset(c.cnt, 0, sizeof(int) * CC_COUNT) != hipSuccess) return PF_EHIP;
@@ -505,7 +589,7 @@ int cls_alloc(ClsGPU& c, size_t cap) {
 
 void cls_free(ClsGPU& c) {
     void* ps[] = {c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals, c.pts,
-                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.idx_out};
+                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.idx_out, c.pos, c.box, c.nbr};
     for (void* p : ps) (void)hipFree(p);
     grid_free(c.grid);
     prim_free(c.w);
@@ -529,9 +613,14 @@ void cls_enqueue(ClsGPU& c, const float4* d_pts, const int* d_n, float4* const* 
     gp.m[0] = c.U;
     gp.n[0] = c.cnt + CC_NU;
     gp.nm = 1;
-    grid_build(c.grid, gp, c.w, s, false, true);
+    grid_count_scan(c.grid, gp, c.w, s);
+    hipLaunchKernelGGL(k_u_keys, dim3(kEwBlocks), dim3(256), 0, s, d, c.grid.dims);
+    radix_sort_pairs(c.ckeys, c.cvals, c.cnt + CC_NU, 32, c.w, s);
+    hipLaunchKernelGGL(k_u_place, dim3(kEwBlocks), dim3(256), 0, s, d, c.grid.cpts, c.grid.cell_count, c.grid.dims);
+    hipLaunchKernelGGL(k_u_boxes, dim3(kEwBlocks), dim3(256), 0, s, d, c.grid.cpts);
     const GridView gv{c.grid.dims, c.grid.cell_start, c.grid.cpts};
-    hipLaunchKernelGGL(k_cls_pca, dim3(2048), dim3(256), 0, s, d, gv);
+    hipLaunchKernelGGL(k_cls_search, dim3(4096), dim3(256), 0, s, d, gv, c.nbr);
+    hipLaunchKernelGGL(k_cls_decide, dim3(kEwBlocks), dim3(256), 0, s, d, c.nbr);
     u32 *ks = nullptr, *vs = nullptr;
     radix_sort_pairs(c.ckeys, c.cvals, c.cnt + CC_NU, 8, c.w, s, &ks, &vs);
     hipLaunchKernelGGL(k_cls_out, dim3(kEwBlocks), dim3(256), 0, s, d, ks, vs, out ? out[0] : nullptr,

@@ -196,6 +196,10 @@ constexpr int kGridBoundsBlocks = 64;
 void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s, bool bounds_launched = false,
                 bool aggregate = false);
 
+// the first half of a build: bounds, per-cell counts (wave-aggregated) and cell_start; the caller
+// places the points itself (cell-major order, e.g. by a sort) and zeroes the counts it used
+void grid_count_scan(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s);
+
 struct GridView {
     const int* dims;
     const u32* cell_start;

@@ -155,6 +155,12 @@ void grid_free(GridGPU& g) {
     g = GridGPU{};
 }
 
+void grid_count_scan(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s) {
+    hipLaunchKernelGGL(k_grid_bounds<NoTail>, dim3(kGridBoundsBlocks), dim3(256), 0, s, grid_bounds_args(g, gp), NoTail{});
+    hipLaunchKernelGGL(k_grid_count<true>, dim3(512), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot);
+    scan_exclusive(g.cell_count, g.cell_start, g.d_ncells, nullptr, w, s);
+}
+
 void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s, bool bounds_launched, bool aggregate) {
     const int nb = 512;
     if (!bounds_launched)

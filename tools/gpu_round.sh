@@ -45,5 +45,11 @@ if [ "$WHAT" = bench ] || [ "$WHAT" = all ]; then
     rc=$?
     if [ $rc -ne 0 ]; then echo "PMC WRITE FAILED rc=$rc"; tail -n 20 $OUT/pmc_write.log; exit $rc; fi
     echo pmc ok
+    # the BPF front end (ground_seg + featureExtract) alone: per-kernel durations
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/cls_prof -o run --output-format csv -- \
+        python3 tools/cls_probe.py --iters 50 > $OUT/cls_prof.log 2>&1
+    rc=$?
+    if [ $rc -ne 0 ]; then echo "CLS PROF FAILED rc=$rc"; tail -n 20 $OUT/cls_prof.log; exit $rc; fi
+    grep ms/frame $OUT/cls_prof.log
     find $OUT/prof $OUT/pmc_fetch $OUT/pmc_write -name "*.csv" | head -20
 fi

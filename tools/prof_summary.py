@@ -84,6 +84,27 @@ def main():
             f.write("Source: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 1000 --no-cpu --no-graph`\n\n")
             f.write(md)
         print(json.dumps(info))
+    cls = os.path.join(g, "cls_prof", "run_kernel_stats.csv")
+    if os.path.exists(cls):
+        shutil.copy(cls, os.path.join(a.out, "%s_front_end_kernel_stats.csv" % a.round))
+        rows = sorted(csv.DictReader(open(cls)), key=lambda r: -float(r["TotalDurationNs"]))
+        calls = max(int(r["Calls"]) for r in rows if short(r["Name"]) == "k_cls_decide")
+        lines = ["# BPF front end per frame (%s)\n" % a.round,
+                 "Source: `rocprofv3 --kernel-trace --stats -- python3 tools/cls_probe.py --iters 50` "
+                 "(ground_seg + featureExtract of S64 frames through pf_cls_extract; %d frames)\n" % calls,
+                 "| kernel | launches / frame | avg us | us / frame |", "|---|---|---|---|"]
+        tot = 0.0
+        for r in rows:
+            n = short(r["Name"])
+            if n.startswith("__amd"):
+                continue
+            per = float(r["TotalDurationNs"]) / 1e3 / calls
+            tot += per
+            lines.append("| %s | %.1f | %.1f | %.1f |" % (n, int(r["Calls"]) / calls, float(r["AverageNs"]) / 1e3, per))
+        lines.append("| **total** | | | **%.1f** |" % tot)
+        with open(os.path.join(a.out, "%s_front_end.md" % a.round), "w") as f:
+            f.write("\n".join(lines) + "\n")
+        print("front end us/frame %.1f" % tot)
     fetch = os.path.join(g, "pmc_fetch", "run_counter_collection.csv")
     write = os.path.join(g, "pmc_write", "run_counter_collection.csv")
     if os.path.exists(fetch) and os.path.exists(write):
