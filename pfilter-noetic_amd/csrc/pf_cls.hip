@@ -359,6 +359,18 @@ __device__ int pca_code(Get get, int n, float qz, const pf_cls_params& P) {
     return 0;
 }
 
+__device__ __forceinline__ u64 shfl_u64(u64 v, int src) {
+    const int lo = __shfl((int)(u32)v, src, 64), hi = __shfl((int)(u32)(v >> 32), src, 64);
+    return ((u64)(u32)hi << 32) | (u64)(u32)lo;
+}
+__device__ __forceinline__ u64 shfl_xor_u64(u64 v, int m) {
+    const int lo = __shfl_xor((int)(u32)v, m, 64), hi = __shfl_xor((int)(u32)(v >> 32), m, 64);
+    return ((u64)(u32)hi << 32) | (u64)(u32)lo;
+}
+#ifndef PF_CLS_BATCH
+#define PF_CLS_BATCH 16
+#endif
+constexpr int kBatch = PF_CLS_BATCH;   // winners in one pass above which the pass is merged as a whole
 __device__ __forceinline__ u64 readlane_u64(u64 v, int lane) {
     const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, lane);
     const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), lane);
@@ -439,6 +451,28 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                         }
                     }
                     u64 sm = __ballot(key < thr);
+                    if (__popcll(sm) > kBatch) {
+                        // many winners (the list is young): sort the pass's keys across the wave and
+                        // merge them with the list in one bitonic network instead of one by one
+                        u64 v = key < thr ? key : ~0ull;
+#pragma unroll
+                        for (int kk = 2; kk <= 64; kk <<= 1)
+#pragma unroll
+                            for (int j = kk >> 1; j > 0; j >>= 1) {
+                                const u64 o = shfl_xor_u64(v, j);
+                                v = (((l & j) == 0) == ((l & kk) == 0)) ? (o < v ? o : v) : (o > v ? o : v);
+                            }
+                        const u64 rev = shfl_u64(v, 63 - l);           // lanes 32.. : the 32 smallest, descending
+                        v = l < 32 ? ent : rev;                         // bitonic: list ascending, then keys descending
+#pragma unroll
+                        for (int j = 32; j > 0; j >>= 1) {
+                            const u64 o = shfl_xor_u64(v, j);
+                            v = (l & j) == 0 ? (o < v ? o : v) : (o > v ? o : v);
+                        }
+                        ent = v;
+                        thr = readlane_u64(ent, K - 1);
+                        sm = 0;
+                    }
                     while (sm) {
                         const int sl = __ffsll((unsigned long long)sm) - 1;
                         sm &= sm - 1;
