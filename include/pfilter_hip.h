@@ -159,6 +159,9 @@ int pf_cls_destroy(pf_cls* h);
 int pf_cls_extract(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, int32_t* beam, size_t* nb,
                    int32_t* pillar, size_t* np, int32_t* facade, size_t* nf, int32_t* ground, size_t* ng,
                    size_t cap);
+/* ground_seg alone (:398-505): ground and non-ground input indices in the reference's push order */
+int pf_cls_ground_seg(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, int32_t* ground, size_t* ng,
+                      int32_t* unground, size_t* nu, size_t cap);
 /* featureExtract alone on a cloud (no ground segmentation): per point the index_with_feature code
  * (0 none, 1 pillar, 2 beam, 3 facade, :663-682) and the neighbour count pt_num (:223); either may
  * be NULL */

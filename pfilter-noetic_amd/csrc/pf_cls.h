@@ -65,7 +65,8 @@ void cls_free(ClsGPU& c);
 // pillar and facade clouds as float4 (x, y, z, 0) and their device-resident sizes. idx: also write
 // the input indices of the three classes (c.idx_out) and of the ground points (c.keys region after
 // U, see cls_ground_offset).
+// ground_only: stop after ground_seg (c.vals: non-ground then ground input indices).
 void cls_enqueue(ClsGPU& c, const float4* d_pts, const int* d_n, float4* const* out, int* const* out_cnt,
-                 bool idx, hipStream_t s);
+                 bool idx, hipStream_t s, bool ground_only = false);
 
 }  // namespace pf

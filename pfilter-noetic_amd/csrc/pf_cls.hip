@@ -631,7 +631,7 @@ void cls_free(ClsGPU& c) {
 }
 
 void cls_enqueue(ClsGPU& c, const float4* d_pts, const int* d_n, float4* const* out, int* const* out_cnt,
-                 bool idx, hipStream_t s) {
+                 bool idx, hipStream_t s, bool ground_only) {
     ClsDev d = dev_view(c);
     if (c.prm.ground_filter) {
         hipLaunchKernelGGL(k_gs_bounds, dim3(64), dim3(256), 0, s, d_pts, d_n, d);
@@ -643,6 +643,7 @@ void cls_enqueue(ClsGPU& c, const float4* d_pts, const int* d_n, float4* const* 
     } else {
         hipLaunchKernelGGL(k_cls_identity, dim3(kEwBlocks), dim3(256), 0, s, d_pts, d_n, d);
     }
+    if (ground_only) return;
     GridPtrs gp{};
     gp.m[0] = c.U;
     gp.n[0] = c.cnt + CC_NU;
@@ -689,14 +690,14 @@ void repack_xyz(const float* src, size_t n, size_t stride, std::vector<float4>& 
         out[i] = make_float4(p[0], p[1], p[2], 0.f);
     }
 }
-int cls_run(pf_cls* h, const float* xyz, size_t n, size_t stride, bool idx) {
+int cls_run(pf_cls* h, const float* xyz, size_t n, size_t stride, bool idx, bool ground_only = false) {
     if (n > h->c.cap) return PF_ECAPACITY;
     PF_HIP_TRY(hipSetDevice(h->device));
     repack_xyz(xyz, n, stride, h->host);
     const int ni = (int)n;
     if (n) PF_HIP_TRY(hipMemcpyAsync(h->c.pts, h->host.data(), sizeof(float4) * n, hipMemcpyHostToDevice, h->stream));
     PF_HIP_TRY(hipMemcpyAsync(h->d_n, &ni, sizeof(int), hipMemcpyHostToDevice, h->stream));
-    cls_enqueue(h->c, h->c.pts, h->d_n, nullptr, nullptr, idx, h->stream);
+    cls_enqueue(h->c, h->c.pts, h->d_n, nullptr, nullptr, idx, h->stream, ground_only);
     PF_HIP_TRY(hipGetLastError());
     PF_HIP_TRY(hipStreamSynchronize(h->stream));
     return PF_OK;
@@ -786,6 +787,26 @@ int pf_cls_extract(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, i
     if (pillar && n1) PF_HIP_TRY(hipMemcpy(pillar, h->c.idx_out + n0, sizeof(int) * n1, hipMemcpyDeviceToHost));
     if (facade && n2) PF_HIP_TRY(hipMemcpy(facade, h->c.idx_out + n0 + n1, sizeof(int) * n2, hipMemcpyDeviceToHost));
     if (ground && ngr) PF_HIP_TRY(hipMemcpy(ground, h->c.vals + nu, sizeof(int) * ngr, hipMemcpyDeviceToHost));
+    return PF_OK;
+}
+
+int pf_cls_ground_seg(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, int32_t* ground, size_t* ng,
+                      int32_t* unground, size_t* nu, size_t cap) {
+    if (!h || (!xyz && n) || stride_bytes < 12) return PF_EINVAL;
+    const int gf = h->c.prm.ground_filter;
+    h->c.prm.ground_filter = 1;
+    int rc = cls_run(h, xyz, n, stride_bytes, false, true);
+    h->c.prm.ground_filter = gf;
+    if (rc) return rc;
+    int cnt[CC_COUNT];
+    PF_HIP_TRY(hipMemcpy(cnt, h->c.cnt, sizeof(cnt), hipMemcpyDeviceToHost));
+    if (cnt[CC_ERR]) return PF_ECAPACITY;
+    const size_t ngr = (size_t)cnt[CC_NG], nun = (size_t)cnt[CC_NU];
+    if (ng) *ng = ngr;
+    if (nu) *nu = nun;
+    if ((ground && ngr > cap) || (unground && nun > cap)) return PF_ECAPACITY;
+    if (unground && nun) PF_HIP_TRY(hipMemcpy(unground, h->c.vals, sizeof(int) * nun, hipMemcpyDeviceToHost));
+    if (ground && ngr) PF_HIP_TRY(hipMemcpy(ground, h->c.vals + nun, sizeof(int) * ngr, hipMemcpyDeviceToHost));
     return PF_OK;
 }
 

@@ -86,7 +86,7 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_memcpy_d2h", "pf_knn_create", "pf_knn_destroy", "pf_knn_set_map", "pf_knn_query", "pf_knn_bench",
            "pf_bpf_create", "pf_bpf_init_map", "pf_bpf_update", "pf_bpf_frame_device", "pf_odom_classes",
            "pf_odom_reset", "pf_cls_default_params", "pf_cls_create", "pf_cls_destroy", "pf_cls_extract",
-           "pf_cls_classify", "pf_bpf_set_front_end", "pf_bpf_frame_scan_device"]
+           "pf_cls_classify", "pf_cls_ground_seg", "pf_bpf_set_front_end", "pf_bpf_frame_scan_device"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -143,6 +143,7 @@ def lib():
         L.pf_cls_destroy.argtypes = [_vp]
         L.pf_cls_extract.argtypes = [_vp, _vp, _sz, _sz] + [_vp, ctypes.POINTER(_sz)] * 4 + [_sz]
         L.pf_cls_classify.argtypes = [_vp, _vp, _sz, _sz, _vp, _vp]
+        L.pf_cls_ground_seg.argtypes = [_vp, _vp, _sz, _sz, _vp, ctypes.POINTER(_sz), _vp, ctypes.POINTER(_sz), _sz]
         L.pf_bpf_set_front_end.argtypes = [_vp, ctypes.POINTER(ClsParams)]
         L.pf_bpf_frame_scan_device.argtypes = [_vp, _vp, _sz, _vp]
     _lib = L
@@ -489,6 +490,17 @@ class BPFFrontEnd:
         _check("pf_cls_extract", lib().pf_cls_extract(self._h, a.ctypes.data, n, 4 * a.shape[1], *args, max(n, 1)),
                allow_warn=False)
         return {k: b[:c.value].copy() for k, b, c in zip(("beam", "pillar", "facade", "ground"), bufs, cnt)}
+
+    def ground_seg(self, xyz):
+        """ground_seg alone: (ground, non-ground) input indices in the reference's push order."""
+        a = np.ascontiguousarray(xyz, dtype=np.float32)
+        n = a.shape[0]
+        g, u = np.empty(max(n, 1), np.int32), np.empty(max(n, 1), np.int32)
+        ng, nu = _sz(), _sz()
+        _check("pf_cls_ground_seg", lib().pf_cls_ground_seg(self._h, a.ctypes.data, n, 4 * a.shape[1], g.ctypes.data,
+                                                            ctypes.byref(ng), u.ctypes.data, ctypes.byref(nu),
+                                                            max(n, 1)), allow_warn=False)
+        return g[:ng.value].copy(), u[:nu.value].copy()
 
     def classify(self, xyz):
         """featureExtract alone: (index_with_feature code per point, neighbour count per point)."""

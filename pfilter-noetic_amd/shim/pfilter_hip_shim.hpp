@@ -10,6 +10,10 @@
 //       updatePointsToMap / getMap / mergeFeatures,
 //       members odom, laserCloudBeamMap, laserCloudPillarMap,
 //       laserCloudFacadeMap, laserCloudMergeMap            include/odomEstimationClass.h:169-202
+//   groundSeg::groundInit / ground_seg, members
+//       groundSeginputCloudPtr, groundCloudPtr, nonGroundCloudPtr, gf_*   include/preProcess.hpp:368-614
+//   nongroundExtract::featureInit / pc2pc / featureExtract, members
+//       cloud_pillar, cloud_beam, cloud_facade, index_with_feature, thresholds   :616-735
 //
 // The classes are templates over the point-cloud and lidar types so this header needs neither PCL nor
 // ROS; shim/laserProcessingClass.h and shim/odomEstimationClass.h instantiate them with the PCL 1.10
@@ -370,6 +374,166 @@ private:
     pf_odom* h_ = nullptr;
     std::vector<float> xyz_;
     std::vector<uint8_t> rg_;
+};
+
+// --------------------------------------------------------------------------------------------
+// groundSeg (include/preProcess.hpp:368-614): the ground filter of src/additionNode.cpp:21-27. The
+// ROS publishers of the reference class are added by shim/preProcess.hpp.
+inline pf_cls_params cls_defaults() {
+    pf_cls_params p;
+    pf_cls_default_params(&p);
+    return p;
+}
+inline bool same_params(const pf_cls_params& a, const pf_cls_params& b) { return std::memcmp(&a, &b, sizeof(a)) == 0; }
+
+// one pf_cls handle, re-created when the parameters it was created with change
+class ClsHandle {
+public:
+    ClsHandle(int device, size_t max_points) : device_(device), max_points_(max_points) {}
+    ~ClsHandle() {
+        if (h_) pf_cls_destroy(h_);
+    }
+    ClsHandle(const ClsHandle&) = delete;
+    ClsHandle& operator=(const ClsHandle&) = delete;
+    pf_cls* get(const pf_cls_params& p, size_t n) {
+        if (!h_ || !same_params(p, prm_) || n > cap_) {
+            if (h_) pf_cls_destroy(h_);
+            h_ = nullptr;
+            cap_ = n > max_points_ ? n : max_points_;
+            check("pf_cls_create", pf_cls_create(&p, device_, cap_, &h_));
+            prm_ = p;
+        }
+        return h_;
+    }
+
+private:
+    int device_;
+    size_t max_points_, cap_ = 0;
+    pf_cls_params prm_{};
+    pf_cls* h_ = nullptr;
+};
+
+template <class CloudXYZI>
+class GroundSegT {
+public:
+    using Ptr = typename CloudXYZI::Ptr;
+    using Point = typename std::decay<decltype(std::declval<CloudXYZI>().points[0])>::type;
+    explicit GroundSegT(int device = 0, size_t max_points = 300000) : cls_(device, max_points) {}
+
+    void groundInit(Ptr& inputCloud) {          // :373-380 (header kept by the ROS layer)
+        groundSeginputCloudPtr = inputCloud;
+        groundCloudPtr = Ptr(new CloudXYZI());
+        nonGroundCloudPtr = Ptr(new CloudXYZI());
+    }
+    // :398-505: appends to cloud_ground / cloud_unground in the reference's push order
+    bool ground_seg(Ptr& cloud_in, Ptr& cloud_ground, Ptr& cloud_unground, int min_grid_pt_num, float grid_resolution,
+                    float max_height_difference, float neighbor_height_diff, float max_ground_height,
+                    float min_ground_height) {
+        static_assert(std::is_standard_layout<Point>::value, "point type must be standard layout");
+        pf_cls_params p = cls_defaults();
+        p.gf_min_grid_pts = min_grid_pt_num;
+        p.gf_grid_res = grid_resolution;
+        p.gf_max_height_diff = max_height_difference;
+        p.gf_neighbor_height_diff = neighbor_height_diff;
+        p.gf_max_ground_height = max_ground_height;
+        p.gf_min_ground_height = min_ground_height;
+        const size_t n = cloud_in->points.size();
+        g_.resize(n ? n : 1);
+        u_.resize(n ? n : 1);
+        size_t ng = 0, nu = 0;
+        check("pf_cls_ground_seg", pf_cls_ground_seg(cls_.get(p, n), n ? &cloud_in->points[0].x : nullptr, n,
+                                                     sizeof(Point), g_.data(), &ng, u_.data(), &nu, n ? n : 1));
+        for (size_t i = 0; i < ng; ++i) cloud_ground->push_back(cloud_in->points[(size_t)g_[i]]);
+        for (size_t i = 0; i < nu; ++i) cloud_unground->push_back(cloud_in->points[(size_t)u_[i]]);
+        std::printf("Ground: [%zu] Unground: [%zu].\n", ng, nu);     // :499
+        return true;
+    }
+
+    // members read by src/additionNode.cpp:24 (include/preProcess.hpp:575, 600-605)
+    int gf_grid_pt_num_thre = 8;
+    double gf_max_ground_height = 5, gf_min_ground_height = -5, gf_neighbor_height_diff = 1.5,
+           gf_max_grid_height_diff = 0.3, gf_grid_resolution = 3.0;
+    Ptr groundSeginputCloudPtr, groundCloudPtr, nonGroundCloudPtr;
+
+private:
+    ClsHandle cls_;
+    std::vector<int32_t> g_, u_;
+};
+
+// nongroundExtract (include/preProcess.hpp:616-735): featureExtract on the non-ground cloud. CloudTpl
+// is the point-cloud template (pcl::PointCloud); PointN the output point (pcl::PointXYZINormal). The
+// outputs carry xyz; the PCA normals the reference also writes into them (assign_normal, :327-346) are
+// not produced — the BPF node copies the clouds to XYZRGB and drops them
+// (src/odomEstimationNode.cpp:236-240).
+template <template <class> class CloudTpl, class PointN>
+class NongroundExtractT {
+public:
+    using CloudN = CloudTpl<PointN>;
+    using PtrN = typename CloudN::Ptr;
+    explicit NongroundExtractT(int device = 0, size_t max_points = 300000) : cls_(device, max_points) {}
+
+    void featureInit() {                                            // :621-631 (clouds reset)
+        normalCloud = PtrN(new CloudN());
+        cloud_pillar = PtrN(new CloudN());
+        cloud_beam = PtrN(new CloudN());
+        cloud_facade = PtrN(new CloudN());
+        cloud_roof = PtrN(new CloudN());
+    }
+    template <class CloudIn>
+    void pc2pc(typename CloudIn::Ptr& cloud_in, PtrN& cloud_out) {   // :633-644 (xyz only)
+        for (const auto& q : cloud_in->points) {
+            PointN pn;
+            pn.x = q.x;
+            pn.y = q.y;
+            pn.z = q.z;
+            cloud_out->push_back(pn);
+        }
+    }
+    // :647-689: the <= neighbor_k nearest within neighbor_searching_radius, PCA, pillar / beam / facade
+    template <class PointT>
+    void featureExtract(typename CloudTpl<PointT>::Ptr& cloud_in) {
+        static_assert(std::is_standard_layout<PointT>::value, "point type must be standard layout");
+        pf_cls_params p = cls_defaults();
+        p.ground_filter = 0;
+        p.radius = neighbor_searching_radius;
+        p.k = neighbor_k;
+        p.k_min = neigh_k_min;
+        p.edge_thre = edge_thre;
+        p.planar_thre = planar_thre;
+        p.linear_vsin_high = linear_vertical_sin_high_thre;
+        p.linear_vsin_low = linear_vertical_sin_low_thre;
+        p.planar_vsin_low = planar_vertical_sin_low_thre;
+        p.beam_h_max = beam_height_max;
+        p.beam_h_min = beam_height_min;
+        const size_t n = cloud_in->points.size();
+        code_.resize(n ? n : 1);
+        check("pf_cls_classify", pf_cls_classify(cls_.get(p, n), n ? &cloud_in->points[0].x : nullptr, n,
+                                                 sizeof(PointT), code_.data(), nullptr));
+        index_with_feature.assign(n, 0);
+        for (size_t i = 0; i < n; ++i) {
+            const int c = code_[i];
+            index_with_feature[i] = c;
+            if (c == 0) continue;
+            PointN pn;
+            pn.x = cloud_in->points[i].x;
+            pn.y = cloud_in->points[i].y;
+            pn.z = cloud_in->points[i].z;
+            (c == 1 ? cloud_pillar : (c == 2 ? cloud_beam : cloud_facade))->push_back(pn);
+        }
+    }
+
+    // members (include/preProcess.hpp:703-731)
+    float neighbor_searching_radius = 1.0f;
+    int neighbor_k = 25, neigh_k_min = 8, pca_down_rate = 2;
+    float edge_thre = 0.65f, planar_thre = 0.65f, linear_vertical_sin_high_thre = 0.94f,
+          linear_vertical_sin_low_thre = 0.17f, planar_vertical_sin_high_thre = 0.98f,
+          planar_vertical_sin_low_thre = 0.34f, beam_height_max = 3.402823466e+38f, beam_height_min = 0.5f;
+    PtrN normalCloud, cloud_pillar, cloud_beam, cloud_facade, cloud_roof;
+    std::vector<int> index_with_feature;
+
+private:
+    ClsHandle cls_;
+    std::vector<uint8_t> code_;
 };
 
 }  // namespace pfilter_hip

@@ -28,6 +28,10 @@ def test_extract_matches_oracle(pa, pfref, pfsynth, fe, preset, frame):
     want = pfref.bpf_preprocess(x, pfref.cls_params())
     _same(got, want)
     assert len(got["facade"]) > 1000 and len(got["pillar"]) > 50 and len(got["ground"]) > 10000
+    g, u = fe.ground_seg(x)                                     # pf_cls_ground_seg alone
+    og, ou = pfref.ground_seg(x, pfref.cls_params())
+    np.testing.assert_array_equal(g, og)
+    np.testing.assert_array_equal(u, ou)
 
 
 def test_classify_matches_oracle(pa, pfref, pfsynth, fe):

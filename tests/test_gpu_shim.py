@@ -69,3 +69,34 @@ def test_bpf_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
         np.testing.assert_array_equal(got[k, :7], od.odom)
         sizes = [m[0].shape[0] for m in (od.laserCloudBeamMap, od.laserCloudPillarMap, od.laserCloudFacadeMap)]
         assert list(got[k, 7:10]) == sizes and got[k, 10] == sum(sizes)
+
+
+def test_front_end_shim_matches_python_binding(pa, pfsynth, tmp_path):
+    """groundSeg + nongroundExtract drop-in (shim) driven like src/additionNode.cpp:21-45: the published
+    beam / pillar / facade clouds equal the C ABI's index lists applied to the scan."""
+    exe = str(tmp_path / "shim_cls_driver")
+    lib = os.path.join(ROOT, "pfilter-noetic_amd")
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "shim", "shim_cls_driver.cpp"), "-o", exe, "-L", lib,
+                           "-lpfilter_hip", "-Wl,-rpath," + lib, "-Wl,-rpath-link,/opt/rocm/lib"])
+    seq = pfsynth.Sequence("S64", n_frames=3, az_steps=1500)
+    scans = [seq.frame(k) for k in range(3)]
+    with open(tmp_path / "scans.bin", "wb") as f:
+        for x in scans:
+            np.array([x.shape[0]], np.int64).tofile(f)
+            x.astype(np.float32).tofile(f)
+    subprocess.check_call([exe, str(tmp_path / "scans.bin"), str(tmp_path / "out.bin")], timeout=120)
+    raw = open(tmp_path / "out.bin", "rb").read()
+    fe = pa.BPFFrontEnd(max_points=200000)
+    off = 0
+    for x in scans:
+        sz = np.frombuffer(raw, np.int64, 5, off)
+        off += 40
+        r = fe.extract(x)
+        g, u = fe.ground_seg(x)
+        assert list(sz) == [len(g), len(u), len(r["beam"]), len(r["pillar"]), len(r["facade"])]
+        np.testing.assert_array_equal(g, r["ground"])
+        for k in ("beam", "pillar", "facade"):
+            xyz = np.frombuffer(raw, np.float32, 3 * len(r[k]), off).reshape(-1, 3)
+            off += 12 * len(r[k])
+            np.testing.assert_array_equal(xyz, x[r[k], :3])
