@@ -77,3 +77,16 @@ def test_rejects(pa, pfsynth):
     far = np.array([[0, 0, 0], [2000.0, 2000.0, 0]], np.float32)               # ground grid > 32766 cells
     with pytest.raises(pa.PFError):
         small.extract(far)
+
+
+def test_matches_committed_fixture(pa, pfsynth, fe):
+    """tests/golden/cls_s32_f2.npz (oracle output, tools/make_golden.py) reproduced on the device."""
+    import hashlib
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cls_s32_f2.npz"))
+    x = pfsynth.Sequence("S32", n_frames=3, az_steps=900).frame(2)
+    assert hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest() == str(g["input_sha"])
+    _same(fe.extract(x), {k: g[k] for k in ("beam", "pillar", "facade", "ground")})
+    cls, num = fe.classify(x[g["unground"]])
+    np.testing.assert_array_equal(cls, g["cls"])
+    np.testing.assert_array_equal(num, g["pt_num"])

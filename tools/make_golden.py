@@ -84,9 +84,19 @@ def grid_case():
     print("voxel", vg.shape, rg.shape)
 
 
+def cls_case():
+    """BPF front end (ground_seg + featureExtract) on one S32 frame: index lists."""
+    x = pfsynth.Sequence("S32", n_frames=3, az_steps=900).frame(2)
+    r = pfref.bpf_preprocess(x, pfref.cls_params())
+    g, u = pfref.ground_seg(x, pfref.cls_params())
+    cls, num = pfref.pca_classify(x[u], pfref.cls_params())
+    np.savez_compressed(os.path.join(OUT, "cls_s32_f2.npz"), input_sha=sha(x), unground=u, pt_num=num, cls=cls,
+                        **r)
+    print("cls", {k: len(v) for k, v in r.items()})
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    fe_case()
-    odom_case()
-    knn_case()
-    grid_case()
+    which = sys.argv[1:] or ["fe", "odom", "knn", "grid", "cls"]
+    for w in which:
+        globals()[w + "_case"]()
