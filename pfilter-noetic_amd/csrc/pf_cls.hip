@@ -383,16 +383,40 @@ __device__ __forceinline__ u64 wave_shr1_u64(u64 v) {
     return ((u64)(u32)hi << 32) | (u64)(u32)lo;
 }
 
+// ascending sort of one u64 per lane across the wave (bitonic network)
+__device__ __forceinline__ u64 wave_sort_u64(u64 v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int kk = 2; kk <= 64; kk <<= 1)
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            const u64 o = shfl_xor_u64(v, j);
+            v = (((l & j) == 0) == ((l & kk) == 0)) ? (o < v ? o : v) : (o > v ? o : v);
+        }
+    return v;
+}
+
+__device__ __forceinline__ u32 wave_sort_u32(u32 v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int kk = 2; kk <= 64; kk <<= 1)
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            const u32 o = (u32)__shfl_xor((int)v, j, 64);
+            v = (((l & j) == 0) == ((l & kk) == 0)) ? (o < v ? o : v) : (o > v ? o : v);
+        }
+    return v;
+}
+
 // KdTreeFLANN::radiusSearch(i, r, idx, d2, k) for every U point, one wave per query. The candidates
 // are the 27 cells of the 1 m grid around the query (every point with d^2 < r^2 <= 1 lies there,
-// pf_knn.h), nearest rows first, the query's own 16-point chunk first. The sorted list of the k best
-// keys (d^2 bits, index) lives in registers, entry j on lane j; a candidate below the k-th key is
-// inserted by one wave shift (every entry compares with the key and takes its left neighbour, the
-// key or itself; keys are distinct), with the candidate and the k-th key moved through scalar
-// registers. Chunks are skipped by their boxes' float lower bound of d^2 (exact, pf_knn.h): once the
-// list is full, a chunk whose bound exceeds the k-th distance cannot hold a winner, and in dense
-// regions most of the 27 cells' chunks are never read. Up to 4 open chunks are read per pass, one
-// per 16 lanes. Writes the neighbour lists (ascending) and their sizes.
+// pf_knn.h), i.e. the aligned 16-point chunks of the cell-ordered cloud that overlap the 9 x-rows.
+// Per round of 64 chunks, every lane bounds one chunk (its box's float lower bound of d^2, exact by
+// the monotone-rounding argument of pf_knn.h) and the wave sorts the (bound, chunk) pairs; chunks are
+// then read nearest first, 4 per pass (16 lanes each), and the round ends at the first bound above
+// the k-th distance. The sorted list of the k best keys (d^2 bits, index) lives in registers, entry j
+// on lane j: the first pass and any pass with more than kBatch winners merge by a bitonic network,
+// single winners by one wave shift (keys are distinct). Writes the neighbour lists and sizes.
 __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* __restrict__ nbr) {
     constexpr int WPB = 4;
     const int K = d.prm.k;
@@ -416,74 +440,17 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
             const float tz = qp.z < lo.z ? lo.z - qp.z : (qp.z > hi.z ? qp.z - hi.z : 0.0f);
             return (0.0f + tx * tx + ty * ty) + tz * tz;
         };
-        // the aligned 16-point chunks overlapping [a, b): 64 chunks' bounds per round, then the open
-        // ones 4 at a time, each bound re-checked as the k-th distance falls
-        auto scan = [&](u32 a, u32 b) {
-            if (a >= b) return;
-            const int c0 = (int)(a >> 4), c1 = (int)((b - 1) >> 4);
-            for (int g = c0; g <= c1; g += 64) {
-                const int cl = g + l;
-                const float lb = cl <= c1 ? box_lb(cl) : INFINITY;
-                u64 m = __ballot(open(lb));
-                while (m) {
-                    // up to 4 open chunks: lanes 16 i .. 16 i + 15 read the i-th
-                    int src[4];
-                    int nsel = 0;
+        auto merge_batch = [&](u64 key) {                    // all keys of a pass below thr, at once
+            u64 v = wave_sort_u64(key < thr ? key : ~0ull);
+            const u64 rev = shfl_u64(v, 63 - l);             // lanes 32.. : the 32 smallest, descending
+            v = l < 32 ? ent : rev;                          // bitonic: list ascending, keys descending
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        src[i] = -1;
-                        while (m && src[i] < 0) {
-                            const int sl = __ffsll((unsigned long long)m) - 1;
-                            m &= m - 1;
-                            if (open(__shfl(lb, sl, 64))) src[i] = sl;
-                        }
-                        nsel += src[i] >= 0;
-                    }
-                    if (!nsel) break;
-                    const int mine = src[l >> 4];
-                    u64 key = ~0ull;
-                    if (mine >= 0) {
-                        const u32 v = (u32)(g + mine) * 16u + (u32)(l & 15);
-                        if (v >= a && v < b) {
-                            const float4 p = gv.cpts[v];
-                            const float dd = knn_d2(qp.x, qp.y, qp.z, p);
-                            if (dd < r2) key = knn_key(dd, __float_as_int(p.w));
-                        }
-                    }
-                    u64 sm = __ballot(key < thr);
-                    if (__popcll(sm) > kBatch) {
-                        // many winners (the list is young): sort the pass's keys across the wave and
-                        // merge them with the list in one bitonic network instead of one by one
-                        u64 v = key < thr ? key : ~0ull;
-#pragma unroll
-                        for (int kk = 2; kk <= 64; kk <<= 1)
-#pragma unroll
-                            for (int j = kk >> 1; j > 0; j >>= 1) {
-                                const u64 o = shfl_xor_u64(v, j);
-                                v = (((l & j) == 0) == ((l & kk) == 0)) ? (o < v ? o : v) : (o > v ? o : v);
-                            }
-                        const u64 rev = shfl_u64(v, 63 - l);           // lanes 32.. : the 32 smallest, descending
-                        v = l < 32 ? ent : rev;                         // bitonic: list ascending, then keys descending
-#pragma unroll
-                        for (int j = 32; j > 0; j >>= 1) {
-                            const u64 o = shfl_xor_u64(v, j);
-                            v = (l & j) == 0 ? (o < v ? o : v) : (o > v ? o : v);
-                        }
-                        ent = v;
-                        thr = readlane_u64(ent, K - 1);
-                        sm = 0;
-                    }
-                    while (sm) {
-                        const int sl = __ffsll((unsigned long long)sm) - 1;
-                        sm &= sm - 1;
-                        const u64 kk = readlane_u64(key, sl);
-                        if (!(kk < thr)) continue;
-                        const u64 prev = wave_shr1_u64(ent);
-                        ent = kk < prev ? prev : (kk < ent ? kk : ent);
-                        thr = readlane_u64(ent, K - 1);
-                    }
-                }
+            for (int j = 32; j > 0; j >>= 1) {
+                const u64 o = shfl_xor_u64(v, j);
+                v = (l & j) == 0 ? (o < v ? o : v) : (o > v ? o : v);
             }
+            ent = v;
+            thr = readlane_u64(ent, K - 1);
         };
         if (dm[7]) {
             const float fcx = floorf(qp.x), fcy = floorf(qp.y), fcz = floorf(qp.z);
@@ -506,12 +473,12 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                     w3 = xi + 1 < dx ? cs[2] : w2;
                 }
             }
-            // rows nearest first: the query's own row (own chunk, own cell, its x neighbours), the
-            // four face rows, the four corner rows
-            constexpr int order[9] = {4, 3, 5, 1, 7, 0, 2, 6, 8};
+            // each row's point range [ra, rb) (end cells dropped when their bound is >= r^2) and the
+            // prefix of the rows' chunk counts
+            u32 ra[9], rb[9], pre[9];
+            u32 total = 0;
 #pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                const int r = order[k];
+            for (int r = 0; r < 9; ++r) {
                 const int oy = r % 3 - 1, oz = r / 3 - 1;
                 const u32 s0 = (u32)__builtin_amdgcn_readlane((int)w0, r), s1 = (u32)__builtin_amdgcn_readlane((int)w1, r);
                 const u32 s2 = (u32)__builtin_amdgcn_readlane((int)w2, r), s3 = (u32)__builtin_amdgcn_readlane((int)w3, r);
@@ -520,16 +487,79 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                 const float brow = (0.0f + by * by) + bz * bz;
                 const float bl = (lx * lx + by * by) + bz * bz;
                 const float bh = (hx * hx + by * by) + bz * bz;
-                if (r == 4) {
-                    const u32 oc = (u32)d.pos[q] & ~15u;
-                    const u32 ca = oc > s1 ? oc : s1, cb = oc + 16 < s2 ? oc + 16 : s2;
-                    scan(ca, cb);
-                    scan(s1, ca);
-                    scan(cb, s2);
-                    if (open(bl)) scan(s0, s1);
-                    if (open(bh)) scan(s2, s3);
-                } else if (open(brow)) {
-                    scan(open(bl) ? s0 : s1, open(bh) ? s3 : s2);
+                u32 a0 = bl < r2 ? s0 : s1, b0 = bh < r2 ? s3 : s2;
+                if (!(brow < r2) || a0 >= b0) a0 = b0 = 0;
+                ra[r] = a0;
+                rb[r] = b0;
+                pre[r] = total;
+                total += a0 < b0 ? ((b0 - 1) >> 4) - (a0 >> 4) + 1 : 0;
+            }
+            // chunk ordinal t -> (chunk, its row's range)
+            auto locate = [&](u32 t, u32& chunk, u32& a0, u32& b0) {
+                int k = 0;
+#pragma unroll
+                for (int r = 1; r < 9; ++r) k = t >= pre[r] ? r : k;
+                u32 pk = pre[0], ak = ra[0], bk = rb[0];
+#pragma unroll
+                for (int r = 1; r < 9; ++r) {
+                    pk = k == r ? pre[r] : pk;
+                    ak = k == r ? ra[r] : ak;
+                    bk = k == r ? rb[r] : bk;
+                }
+                chunk = (ak >> 4) + (t - pk);
+                a0 = ak;
+                b0 = bk;
+            };
+            // sort keys: the bound's float bits with the low 6 bits replaced by the chunk's lane in the
+            // round (truncation only lowers a bound, so stopping at the first truncated bound above
+            // the k-th distance stays exact; a chunk is still read only if its bound may hold a winner)
+            bool first = true;
+            for (u32 g = 0; g < total; g += 64) {
+                const u32 t = g + (u32)l;
+                u32 sk = ~0u;
+                if (t < total) {
+                    u32 c, a0, b0;
+                    locate(t, c, a0, b0);
+                    const float lb = box_lb((int)c);
+                    if (open(lb)) sk = (__float_as_uint(lb) & ~0x3Fu) | (u32)l;
+                }
+                sk = wave_sort_u32(sk);
+                const int nopen = __popcll(__ballot(sk != ~0u));
+                auto lb_of = [](u32 k) { return __uint_as_float(k & ~0x3Fu); };
+                for (int i = 0; i < nopen; i += 4) {
+                    if (!open(lb_of((u32)__builtin_amdgcn_readlane((int)sk, i)))) break;   // sorted: the rest too
+                    const int j = i + (l >> 4);
+                    const u32 k0 = (u32)__builtin_amdgcn_readlane((int)sk, i);
+                    const u32 k1 = (u32)__builtin_amdgcn_readlane((int)sk, i + 1 < 64 ? i + 1 : 63);
+                    const u32 k2 = (u32)__builtin_amdgcn_readlane((int)sk, i + 2 < 64 ? i + 2 : 63);
+                    const u32 k3 = (u32)__builtin_amdgcn_readlane((int)sk, i + 3 < 64 ? i + 3 : 63);
+                    const u32 sj = (l >> 4) == 1 ? k1 : ((l >> 4) == 2 ? k2 : ((l >> 4) == 3 ? k3 : k0));
+                    u64 key = ~0ull;
+                    if (j < nopen && open(lb_of(sj))) {
+                        u32 c, a0, b0;
+                        locate(g + (sj & 0x3Fu), c, a0, b0);
+                        const u32 v = c * 16u + (u32)(l & 15);
+                        if (v >= a0 && v < b0) {
+                            const float4 p = gv.cpts[v];
+                            const float dd = knn_d2(qp.x, qp.y, qp.z, p);
+                            if (dd < r2) key = knn_key(dd, __float_as_int(p.w));
+                        }
+                    }
+                    u64 sm = __ballot(key < thr);
+                    if (first || __popcll(sm) > kBatch) {
+                        if (sm) merge_batch(key);
+                        first = false;
+                        continue;
+                    }
+                    while (sm) {
+                        const int sl = __ffsll((unsigned long long)sm) - 1;
+                        sm &= sm - 1;
+                        const u64 kk = readlane_u64(key, sl);
+                        if (!(kk < thr)) continue;
+                        const u64 prev = wave_shr1_u64(ent);
+                        ent = kk < prev ? prev : (kk < ent ? kk : ent);
+                        thr = readlane_u64(ent, K - 1);
+                    }
                 }
             }
         }
