@@ -171,7 +171,9 @@ int pf_cls_classify(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, 
  * front end above (ground_seg + featureExtract) into the beam / pillar / facade clouds, then the
  * VoxelGrid, stage B the odometry (the additionNode -> odomEstimationNode chain without ROS).
  * set_front_end fixes the front end's parameters (default: pf_cls_default_params); n <= the handle's
- * max_points. pose_out may be NULL (enqueue only), as pf_odom_frame_device. */
+ * max_points. pose_out may be NULL (enqueue only), as pf_odom_frame_device; with pose_out the call
+ * also reports PF_ECAPACITY when the front end's grids exceeded their limits (the frame then ran with
+ * empty class clouds: a ground grid above 32,766 cells of gf_grid_res, or a 1 m grid above 2^23 cells). */
 int pf_bpf_set_front_end(pf_odom* h, const pf_cls_params* p);
 int pf_bpf_frame_scan_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]);
 

@@ -562,8 +562,16 @@ int pf_bpf_frame_scan_device(pf_odom* h, const float* d_xyzi, size_t n, double p
     }
     int rc = enqueue_frame(h, reinterpret_cast<const float4*>(d_xyzi), n, nullptr, nullptr);
     if (rc) return rc;
-    if (pose_out) return read_pose(h, pose_out);
-    return PF_OK;
+    if (!pose_out) return PF_OK;
+    rc = read_pose(h, pose_out);
+    if (rc < 0) return rc;
+    // the front end's capacity flags (ground grid above its cell limit, U grid above its cell
+    // capacity: the frame ran with empty class clouds), checked where the caller waits anyway
+    int err = 0, gerr = 0;
+    PF_HIP_TRY(hipMemcpy(&err, h->o.front->cnt + CC_ERR, sizeof(int), hipMemcpyDeviceToHost));
+    PF_HIP_TRY(hipMemcpy(&gerr, h->o.front->grid.err, sizeof(int), hipMemcpyDeviceToHost));
+    if (gerr) (void)hipMemset(h->o.front->grid.err, 0, sizeof(int));
+    return err || gerr ? PF_ECAPACITY : rc;
 }
 
 int pf_odom_sync(pf_odom* h) {

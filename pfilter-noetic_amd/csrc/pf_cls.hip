@@ -798,7 +798,7 @@ int pf_cls_extract(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, i
     if (rc) return rc;
     int cnt[CC_COUNT];
     PF_HIP_TRY(hipMemcpy(cnt, h->c.cnt, sizeof(cnt), hipMemcpyDeviceToHost));
-    if (cnt[CC_ERR] || h->c.grid.err == nullptr) return PF_ECAPACITY;
+    if (cnt[CC_ERR]) return PF_ECAPACITY;                    // ground grid above kGsMaxCells
     int gerr = 0;
     PF_HIP_TRY(hipMemcpy(&gerr, h->c.grid.err, sizeof(int), hipMemcpyDeviceToHost));
     if (gerr) {
