@@ -96,3 +96,35 @@ def test_kitti_runner_on_synthetic_sequence(pa, pfsynth, tmp_path):
                                atol=2e-9)
     ev = res["eval"]
     assert ev["segments"] > 0 and ev["t_rel_pct"] < 2.0 and ev["ate_rmse_m"] < 1.0
+
+
+@pytest.mark.gpu
+def test_kitti_runner_bpf_chain(pa, pfsynth, tmp_path):
+    """tools/kitti_run.py --estimator bpf: raw KITTI-format scans through the front end and the BPF
+    estimator; the same poses as the in-process raw-scan pipeline, and a bounded segment error."""
+    import kitti
+    n = 120
+    seq = pfsynth.Sequence("S64", n_frames=n)
+    d = tmp_path / "sequences" / "00" / "velodyne"
+    d.mkdir(parents=True)
+    for k in range(n):
+        seq.frame(k).astype(np.float32).tofile(d / ("%06d.bin" % k))
+    (tmp_path / "poses").mkdir()
+    kitti.write_poses(tmp_path / "poses" / "00.txt", np.array([seq.gt_pose(k) for k in range(n)]))
+    out = tmp_path / "00_pred.txt"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "kitti_run.py"), "--root", str(tmp_path),
+                        "--seq", "0", "--out", str(out), "--estimator", "bpf"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["frames"] == n and res["estimator"] == "bpf"
+    od = pa.Odom_BPF_EstimationClass()
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    for k in range(n):
+        od.frame_host(seq.frame(k), want_pose=False)
+    od.sync()
+    np.testing.assert_allclose(kitti.read_poses(out)[:, :3, :4].reshape(n, 12), kitti.poses_to_kitti(od.poses()),
+                               atol=2e-9)
+    ev = res["eval"]
+    print("bpf chain on synthetic S64:", ev)
+    assert ev["segments"] > 0 and ev["t_rel_pct"] < 5.0

@@ -3,7 +3,9 @@
   python tools/kitti_run.py --root $PF_KITTI_ROOT --seq 0 --out results/00_pred.txt
 
 Scans are read from <root>/sequences/<seq>/velodyne/*.bin, staged in HBM and run through
-pf_odom_frame_device (featureExtraction + Odom_ES_EstimationClass, configs[1] parameters unless set);
+pf_odom_frame_device (featureExtraction + Odom_ES_EstimationClass, configs[1] parameters unless set)
+or, with --estimator bpf, pf_bpf_frame_scan_device (ground_seg + PCA featureExtract +
+Odom_BPF_EstimationClass: the additionNode -> odomEstimationNode chain without the DCVC stage);
 poses are written in the KITTI format (camera frame when <root>/sequences/<seq>/calib.txt exists),
 and scored against <root>/poses/<seq>.txt when present (kitti.evaluate). Prints one JSON line."""
 import argparse
@@ -33,6 +35,7 @@ def main():
     ap.add_argument("--weight-type", type=int, default=0)
     ap.add_argument("--max-frames", type=int, default=0)
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--estimator", choices=["es", "bpf"], default="es")
     a = ap.parse_args()
     import kitti
     import pfilter_amd as pa
@@ -48,12 +51,14 @@ def main():
         buf[i, :s.shape[0]] = s
     db = pa.DeviceBuffer(buf.nbytes, device=a.device)
     db.upload(buf)
-    od = pa.Odom_ES_EstimationClass(device=a.device, max_points=max(cap, 1024))
+    cls = pa.Odom_BPF_EstimationClass if a.estimator == "bpf" else pa.Odom_ES_EstimationClass
+    od = cls(device=a.device, max_points=max(cap, 1024))
     od.init(pa.make_lidar(a.lines, a.min_dist, a.max_dist), a.map_res, a.k_new, a.theta_p, a.theta_max,
             a.weight_type)
+    step = od.frame_scan_device if a.estimator == "bpf" else od.frame_device
     t0 = time.perf_counter()
     for i, s in enumerate(scans):
-        od.frame_device(db.ptr + i * cap * 16, s.shape[0])
+        step(db.ptr + i * cap * 16, s.shape[0])
     od.sync()
     el = time.perf_counter() - t0
     poses = od.poses()
@@ -62,7 +67,7 @@ def main():
     tr = kitti.read_calib_tr(calib) if os.path.exists(calib) else None
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     kitti.write_poses(a.out, poses, tr)
-    res = {"seq": "%02d" % a.seq, "frames": len(scans), "seconds": round(el, 4),
+    res = {"seq": "%02d" % a.seq, "estimator": a.estimator, "frames": len(scans), "seconds": round(el, 4),
            "frames_per_s": round(len(scans) / el, 2), "out": a.out, "camera_frame": tr is not None}
     gt = os.path.join(a.root, "poses", "%02d.txt" % a.seq)
     if os.path.exists(gt):
