@@ -19,6 +19,8 @@
  *   pf_bpf_init_map                Odom_BPF_EstimationClass::initMapWithPoints (.h:177, .cpp:685-691)
  *   pf_bpf_update                  Odom_BPF_EstimationClass::updatePointsToMap (.h:178, .cpp:702-749)
  *   pf_odom_get_map (BPF handle)   laserCloudBeamMap / PillarMap / FacadeMap (.h:180-182), getMap (.cpp:683)
+ *   pf_map_create / update / get   LaserMappingClass::init / updateCurrentPointsToMap / getMap
+ *                                  (include/laserMappingClass.h:27-29, src/laserMappingClass.cpp:7-206)
  *   pf_cls_create / pf_cls_extract groundSeg::ground_seg + nongroundExtract::featureExtract, the BPF
  *                                  front end of src/additionNode.cpp:21-45 (include/preProcess.hpp:
  *                                  398-505, 646-689)
@@ -176,6 +178,20 @@ int pf_cls_classify(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, 
  * empty class clouds: a ground grid above 32,766 cells of gf_grid_res, or a 1 m grid above 2^23 cells). */
 int pf_bpf_set_front_end(pf_odom* h, const pf_cls_params* p);
 int pf_bpf_frame_scan_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]);
+
+/* ---------------- global map (LaserMappingClass, src/laserMappingClass.cpp) ----------------
+ * The map of src/laserMappingNode.cpp: 50 m cubes; every update transforms the scan into the world
+ * frame (pose = qx, qy, qz, qw, tx, ty, tz, the odometry message), appends it to its cubes and
+ * VoxelGrid-filters the 5 x 5 x 5 cubes around the pose. max_points bounds the map, max_scan a scan.
+ * update returns PF_EINVAL when a point falls into a cube the reference never allocated (it
+ * dereferences a null cloud there, :171) or lies beyond +-25 km; the map is then unchanged.
+ * pf_map_get: x, y, z, intensity of the whole map in getMap's cube order (xyzi may be NULL). */
+typedef struct pf_map pf_map;
+int pf_map_create(double map_resolution, int device, size_t max_points, size_t max_scan, pf_map** out); /* init :7-33 */
+int pf_map_destroy(pf_map* h);
+int pf_map_update(pf_map* h, const float* xyzi, size_t n, size_t stride_bytes, const double pose[7]); /* :151-189 */
+int pf_map_update_device(pf_map* h, const float* d_xyzi, size_t n, const double pose[7]);
+int pf_map_get(pf_map* h, float* xyzi, size_t cap, size_t* n);                                   /* getMap :194-206 */
 
 /* ---------------- whole-frame device pipeline (featureExtraction -> odometry) ----------------
  * d_xyzi: device pointer to n packed float4 points (HBM-resident scan). The first frame seeds the

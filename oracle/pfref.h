@@ -9,6 +9,7 @@
  *   - Odom_ES_EstimationClass init/initMapWithPoints/updatePointsToMap/addEdgeCostFactor/
  *     addSurfCostFactor/addPointsToMap                       src/odomEstimationClass.cpp:182-647
  *   - groundSeg::ground_seg, nongroundExtract::featureExtract  include/preProcess.hpp:398-505,646-689
+ *   - LaserMappingClass init/updateCurrentPointsToMap/getMap   src/laserMappingClass.cpp:7-206
  *   - Odom_BPF_EstimationClass init/initMapWithPoints/updatePointsToMap/addBeam|Pillar|Facade-
  *     CostFactor/addPointsToMap (the same sequence over 3 maps)  src/odomEstimationClass.cpp:649-1306
  *   - OdomBaseClass rgbds/extractstablepoint/observeMean/pointAssociateToMap
@@ -161,6 +162,16 @@ int pfref_pca_classify(const float* xyz, size_t n, size_t stride, const pfref_cl
 int pfref_bpf_preprocess(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, int32_t* beam,
                          size_t* nb, int32_t* pillar, size_t* np, int32_t* facade, size_t* nf, int32_t* ground,
                          size_t* ng);
+
+/* --- LaserMappingClass (src/laserMappingClass.cpp): the global map of 50 m cubes ------------------
+ * update: xyzi records of `stride` bytes in the sensor frame, pose = qx, qy, qz, qw, tx, ty, tz; returns
+ * -1 when a point falls outside the allocated cubes (reference: null dereference). get: x, y, z,
+ * intensity of the whole map in the reference's cube order (n = size; xyzi may be NULL). */
+typedef struct pfref_map pfref_map;
+pfref_map* pfref_map_create(double map_resolution);
+void pfref_map_destroy(pfref_map* m);
+int pfref_map_update(pfref_map* m, const float* xyzi, size_t n, size_t stride, const double pose[7]);
+int pfref_map_get(const pfref_map* m, float* xyzi, size_t cap, size_t* n);
 
 /* --- whole frame: featureExtraction then initMapWithPoints (first call) / updatePointsToMap */
 int pfref_odom_frame(pfref_odom* h, const pfref_lidar* lidar, const float* xyzi, size_t n,

@@ -118,6 +118,11 @@ def lib():
         L.pfref_ground_seg.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams), _vp, ctypes.POINTER(_sz), _vp,
                                        ctypes.POINTER(_sz)]
         L.pfref_pca_classify.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams), _vp, _vp]
+        L.pfref_map_create.argtypes = [ctypes.c_double]
+        L.pfref_map_create.restype = _vp
+        L.pfref_map_destroy.argtypes = [_vp]
+        L.pfref_map_update.argtypes = [_vp, _vp, _sz, _sz, _vp]
+        L.pfref_map_get.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
         L.pfref_bpf_preprocess.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams)] + \
             [_vp, ctypes.POINTER(_sz)] * 4
     return _lib
@@ -373,3 +378,27 @@ def bpf_preprocess(xyz, params=None):
     rc = lib().pfref_bpf_preprocess(a.ctypes.data, n, 4 * a.shape[1], ctypes.byref(p), *args)
     assert rc == 0
     return {k: b[:c.value].copy() for k, b, c in zip(("beam", "pillar", "facade", "ground"), bufs, cnt)}
+
+
+class GlobalMap:
+    """LaserMappingClass restated (src/laserMappingClass.cpp): update(xyzi, pose7), get() -> (n, 4)."""
+
+    def __init__(self, map_resolution=0.4):
+        self._h = lib().pfref_map_create(float(map_resolution))
+
+    def update(self, xyzi, pose7):
+        a = np.ascontiguousarray(xyzi, dtype=np.float32)
+        pose = np.ascontiguousarray(pose7, dtype=np.float64)
+        return lib().pfref_map_update(self._h, a.ctypes.data, a.shape[0], 4 * a.shape[1], pose.ctypes.data)
+
+    def get(self):
+        n = ctypes.c_size_t()
+        lib().pfref_map_get(self._h, None, 0, ctypes.byref(n))
+        out = np.empty((max(n.value, 1), 4), np.float32)
+        lib().pfref_map_get(self._h, out.ctypes.data, n.value, ctypes.byref(n))
+        return out[:n.value].copy()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().pfref_map_destroy(self._h)
+            self._h = None

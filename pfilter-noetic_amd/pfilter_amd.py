@@ -86,7 +86,8 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_memcpy_d2h", "pf_knn_create", "pf_knn_destroy", "pf_knn_set_map", "pf_knn_query", "pf_knn_bench",
            "pf_bpf_create", "pf_bpf_init_map", "pf_bpf_update", "pf_bpf_frame_device", "pf_odom_classes",
            "pf_odom_reset", "pf_cls_default_params", "pf_cls_create", "pf_cls_destroy", "pf_cls_extract",
-           "pf_cls_classify", "pf_cls_ground_seg", "pf_bpf_set_front_end", "pf_bpf_frame_scan_device"]
+           "pf_cls_classify", "pf_cls_ground_seg", "pf_bpf_set_front_end", "pf_bpf_frame_scan_device", "pf_map_create", "pf_map_destroy", "pf_map_update",
+           "pf_map_update_device", "pf_map_get"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -145,6 +146,12 @@ def lib():
         L.pf_cls_classify.argtypes = [_vp, _vp, _sz, _sz, _vp, _vp]
         L.pf_cls_ground_seg.argtypes = [_vp, _vp, _sz, _sz, _vp, ctypes.POINTER(_sz), _vp, ctypes.POINTER(_sz), _sz]
         L.pf_bpf_set_front_end.argtypes = [_vp, ctypes.POINTER(ClsParams)]
+    if hasattr(L, "pf_map_create"):
+        L.pf_map_create.argtypes = [ctypes.c_double, _i, _sz, _sz, ctypes.POINTER(_vp)]
+        L.pf_map_destroy.argtypes = [_vp]
+        L.pf_map_update.argtypes = [_vp, _vp, _sz, _sz, _vp]
+        L.pf_map_update_device.argtypes = [_vp, _vp, _sz, _vp]
+        L.pf_map_get.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
         L.pf_bpf_frame_scan_device.argtypes = [_vp, _vp, _sz, _vp]
     _lib = L
     return L
@@ -515,4 +522,37 @@ class BPFFrontEnd:
     def __del__(self):
         if getattr(self, "_h", None):
             lib().pf_cls_destroy(self._h)
+            self._h = None
+
+
+class LaserMappingClass:
+    """LaserMappingClass (src/laserMappingClass.cpp): init(map_resolution), updateCurrentPointsToMap(xyzi,
+    pose7 = qx, qy, qz, qw, tx, ty, tz), getMap() -> (n, 4) x, y, z, intensity in the reference's order."""
+
+    def __init__(self, device=0, max_points=1 << 24, max_scan=300000):
+        self.device, self.max_points, self.max_scan = device, int(max_points), int(max_scan)
+        self._h = None
+
+    def init(self, map_resolution):
+        h = _vp()
+        _check("pf_map_create", lib().pf_map_create(float(map_resolution), self.device, self.max_points,
+                                                    self.max_scan, ctypes.byref(h)), allow_warn=False)
+        self._h = h.value
+
+    def updateCurrentPointsToMap(self, xyzi, pose7):
+        a = np.ascontiguousarray(xyzi, dtype=np.float32)
+        pose = np.ascontiguousarray(pose7, dtype=np.float64)
+        _check("pf_map_update", lib().pf_map_update(self._h, a.ctypes.data, a.shape[0], 4 * a.shape[1],
+                                                    pose.ctypes.data), allow_warn=False)
+
+    def getMap(self):
+        n = _sz()
+        _check("pf_map_get", lib().pf_map_get(self._h, None, 0, ctypes.byref(n)))
+        out = np.empty((max(n.value, 1), 4), np.float32)
+        _check("pf_map_get", lib().pf_map_get(self._h, out.ctypes.data, n.value, ctypes.byref(n)))
+        return out[:n.value].copy()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().pf_map_destroy(self._h)
             self._h = None
