@@ -191,6 +191,8 @@ int pf_map_create(double map_resolution, int device, size_t max_points, size_t m
 int pf_map_destroy(pf_map* h);
 int pf_map_update(pf_map* h, const float* xyzi, size_t n, size_t stride_bytes, const double pose[7]); /* :151-189 */
 int pf_map_update_device(pf_map* h, const float* d_xyzi, size_t n, const double pose[7]);
+/* the same with the pose as the Isometry3d itself: row-major [R | t], 12 doubles (the C++ shim) */
+int pf_map_update_mat(pf_map* h, const float* xyzi, size_t n, size_t stride_bytes, const double T[12]);
 int pf_map_get(pf_map* h, float* xyzi, size_t cap, size_t* n);                                   /* getMap :194-206 */
 
 /* ---------------- whole-frame device pipeline (featureExtraction -> odometry) ----------------

@@ -93,15 +93,29 @@ __global__ void __launch_bounds__(256) k_map_transform(const float4* __restrict_
     }
 }
 
+// per-cube bounds: LDS atomics per workgroup (points of a frame crowd into a few cubes; global
+// atomics on 6 x 125 words serialised at ~4 ms), then one global atomic per touched word
 __global__ void __launch_bounds__(256) k_map_bounds(MapDev d) {
+    __shared__ u32 lb[kCubes * 6];
+    for (int k = threadIdx.x; k < kCubes * 6; k += blockDim.x) lb[k] = (k % 6) < 3 ? 0xFFFFFFFFu : 0u;
+    __syncthreads();
     const int tot = d.cnt[0] + d.cnt[1];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x) {
         const int lc = local_cube(d, d.cube[i]);
         if (lc < 0) continue;
         const float4 p = d.pts[i];
-        u32* b = d.bounds + 6 * lc;
+        u32* b = lb + 6 * lc;
         atomicMin(&b[0], f2ord(p.x)); atomicMin(&b[1], f2ord(p.y)); atomicMin(&b[2], f2ord(p.z));
         atomicMax(&b[3], f2ord(p.x)); atomicMax(&b[4], f2ord(p.y)); atomicMax(&b[5], f2ord(p.z));
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kCubes * 6; k += blockDim.x) {
+        const u32 v = lb[k];
+        if ((k % 6) < 3) {
+            if (v != 0xFFFFFFFFu) atomicMin(&d.bounds[k], v);
+        } else if (v != 0u) {
+            atomicMax(&d.bounds[k], v);
+        }
     }
 }
 
@@ -247,19 +261,30 @@ void allocate_around(pf_map* h, int cx, int cy, int cz) {     // init (:7-33) / 
 
 int cube_host(double v) { return (int)std::floor(v / kCell + 0.5); }
 
-int map_update(pf_map* h, const float4* d_scan, size_t n, const double pose[7]) {
-    MapDev& d = h->d;
-    PF_HIP_TRY(hipSetDevice(h->device));
-    if (n > h->scan_cap) return PF_ECAPACITY;
-    PF_HIP_TRY(hipStreamSynchronize(h->stream));
-    if ((size_t)h->h_cnt[0] + n > h->cap) return PF_ECAPACITY;
-    // Eigen: Isometry3d::Identity().rotate(Quaterniond(w, x, y, z)).pretranslate(t), then cast<float>()
-    const double x = pose[0], y = pose[1], z = pose[2], w = pose[3];
+// the node's pose: Isometry3d::Identity().rotate(Quaterniond(w, x, y, z)).pretranslate(t)
+// (src/laserMappingNode.cpp:78-80); Eigen's toRotationMatrix
+void pose_to_T(const double p[7], double T[12]) {
+    const double x = p[0], y = p[1], z = p[2], w = p[3];
     const double tx = 2 * x, ty = 2 * y, tz = 2 * z, twx = tx * w, twy = ty * w, twz = tz * w, txx = tx * x,
                  txy = ty * x, txz = tz * x, tyy = ty * y, tyz = tz * y, tzz = tz * z;
     const double R[3][3] = {{1 - (tyy + tzz), txy - twz, txz + twy},
                             {txy + twz, 1 - (txx + tzz), tyz - twx},
                             {txz - twy, tyz + twx, 1 - (txx + tyy)}};
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) T[4 * r + c] = R[r][c];
+        T[4 * r + 3] = p[4 + r];
+    }
+}
+
+// T: row-major [R | t] (3 x 4) of the Isometry3d the node builds
+int map_update(pf_map* h, const float4* d_scan, size_t n, const double T[12]) {
+    MapDev& d = h->d;
+    PF_HIP_TRY(hipSetDevice(h->device));
+    if (n > h->scan_cap) return PF_ECAPACITY;
+    PF_HIP_TRY(hipStreamSynchronize(h->stream));
+    if ((size_t)h->h_cnt[0] + n > h->cap) return PF_ECAPACITY;
+    const double R[3][3] = {{T[0], T[1], T[2]}, {T[4], T[5], T[6]}, {T[8], T[9], T[10]}};
+    const double pose[7] = {0, 0, 0, 1, T[3], T[7], T[11]};
     d.cx = cube_host(pose[4]);
     d.cy = cube_host(pose[5]);
     d.cz = cube_host(pose[6]);
@@ -382,12 +407,30 @@ int pf_map_update(pf_map* h, const float* xyzi, size_t n, size_t stride_bytes, c
         h->host[i] = make_float4(p[0], p[1], p[2], stride_bytes >= 16 ? p[3] : 0.f);
     }
     if (n) PF_HIP_TRY(hipMemcpyAsync(h->scan_buf, h->host.data(), sizeof(float4) * n, hipMemcpyHostToDevice, h->stream));
-    return map_update(h, h->scan_buf, n, pose);
+    double T[12];
+    pose_to_T(pose, T);
+    return map_update(h, h->scan_buf, n, T);
+}
+
+int pf_map_update_mat(pf_map* h, const float* xyzi, size_t n, size_t stride_bytes, const double T[12]) {
+    if (!h || !T || (!xyzi && n) || stride_bytes < 12) return PF_EINVAL;
+    if (n > h->scan_cap) return PF_ECAPACITY;
+    PF_HIP_TRY(hipSetDevice(h->device));
+    h->host.resize(n);
+    const char* b = reinterpret_cast<const char*>(xyzi);
+    for (size_t i = 0; i < n; ++i) {
+        const float* p = reinterpret_cast<const float*>(b + i * stride_bytes);
+        h->host[i] = make_float4(p[0], p[1], p[2], stride_bytes >= 16 ? p[3] : 0.f);
+    }
+    if (n) PF_HIP_TRY(hipMemcpyAsync(h->scan_buf, h->host.data(), sizeof(float4) * n, hipMemcpyHostToDevice, h->stream));
+    return map_update(h, h->scan_buf, n, T);
 }
 
 int pf_map_update_device(pf_map* h, const float* d_xyzi, size_t n, const double pose[7]) {
     if (!h || !pose || (!d_xyzi && n)) return PF_EINVAL;
-    return map_update(h, reinterpret_cast<const float4*>(d_xyzi), n, pose);
+    double T[12];
+    pose_to_T(pose, T);
+    return map_update(h, reinterpret_cast<const float4*>(d_xyzi), n, T);
 }
 
 int pf_map_get(pf_map* h, float* xyzi, size_t cap, size_t* n) {

@@ -87,7 +87,7 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_bpf_create", "pf_bpf_init_map", "pf_bpf_update", "pf_bpf_frame_device", "pf_odom_classes",
            "pf_odom_reset", "pf_cls_default_params", "pf_cls_create", "pf_cls_destroy", "pf_cls_extract",
            "pf_cls_classify", "pf_cls_ground_seg", "pf_bpf_set_front_end", "pf_bpf_frame_scan_device", "pf_map_create", "pf_map_destroy", "pf_map_update",
-           "pf_map_update_device", "pf_map_get"]
+           "pf_map_update_device", "pf_map_update_mat", "pf_map_get"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -151,6 +151,7 @@ def lib():
         L.pf_map_destroy.argtypes = [_vp]
         L.pf_map_update.argtypes = [_vp, _vp, _sz, _sz, _vp]
         L.pf_map_update_device.argtypes = [_vp, _vp, _sz, _vp]
+        L.pf_map_update_mat.argtypes = [_vp, _vp, _sz, _sz, _vp]
         L.pf_map_get.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
         L.pf_bpf_frame_scan_device.argtypes = [_vp, _vp, _sz, _vp]
     _lib = L

@@ -12,6 +12,7 @@
 //       laserCloudFacadeMap, laserCloudMergeMap            include/odomEstimationClass.h:169-202
 //   groundSeg::groundInit / ground_seg, members
 //       groundSeginputCloudPtr, groundCloudPtr, nonGroundCloudPtr, gf_*   include/preProcess.hpp:368-614
+//   LaserMappingClass::init / updateCurrentPointsToMap / getMap          include/laserMappingClass.h:23-29
 //   nongroundExtract::featureInit / pc2pc / featureExtract, members
 //       cloud_pillar, cloud_beam, cloud_facade, index_with_feature, thresholds   :616-735
 //
@@ -534,6 +535,67 @@ public:
 private:
     ClsHandle cls_;
     std::vector<uint8_t> code_;
+};
+
+// --------------------------------------------------------------------------------------------
+// LaserMappingClass (include/laserMappingClass.h:23-29, src/laserMappingClass.cpp): the global map of
+// src/laserMappingNode.cpp, held on the device.
+template <class CloudXYZI>
+class LaserMappingClassT {
+public:
+    using Ptr = typename CloudXYZI::Ptr;
+    using Point = typename std::decay<decltype(std::declval<CloudXYZI>().points[0])>::type;
+    explicit LaserMappingClassT(int device = 0, size_t max_points = size_t(1) << 24, size_t max_scan = 300000)
+        : device_(device), max_points_(max_points), max_scan_(max_scan) {}
+    ~LaserMappingClassT() {
+        if (h_) pf_map_destroy(h_);
+    }
+    LaserMappingClassT(const LaserMappingClassT&) = delete;
+    LaserMappingClassT& operator=(const LaserMappingClassT&) = delete;
+
+    void init(double map_resolution) {                                   // :7-33
+        if (h_) pf_map_destroy(h_);
+        h_ = nullptr;
+        check("pf_map_create", pf_map_create(map_resolution, device_, max_points_, max_scan_, &h_));
+    }
+    // :151-189 with the pose as row-major [R | t]
+    void updateCurrentPointsToMap(const Ptr& pc_in, const double T[12]) {
+        static_assert(std::is_standard_layout<Point>::value, "point type must be standard layout");
+        const size_t n = pc_in->points.size();
+        check("pf_map_update_mat", pf_map_update_mat(h_, n ? &pc_in->points[0].x : nullptr, n, sizeof(Point), T));
+    }
+#ifndef PFILTER_HIP_NO_EIGEN
+    void updateCurrentPointsToMap(const Ptr& pc_in, const Eigen::Isometry3d& pose_current) {
+        double T[12];
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) T[4 * r + c] = pose_current.linear()(r, c);
+            T[4 * r + 3] = pose_current.translation()(r);
+        }
+        updateCurrentPointsToMap(pc_in, T);
+    }
+#endif
+    Ptr getMap() {                                                       // :194-206
+        size_t n = 0;
+        check("pf_map_get", pf_map_get(h_, nullptr, 0, &n));
+        buf_.resize(4 * (n ? n : 1));
+        check("pf_map_get", pf_map_get(h_, buf_.data(), n, &n));
+        Ptr out(new CloudXYZI());
+        for (size_t i = 0; i < n; ++i) {
+            Point p;
+            p.x = buf_[4 * i];
+            p.y = buf_[4 * i + 1];
+            p.z = buf_[4 * i + 2];
+            p.intensity = buf_[4 * i + 3];
+            out->push_back(p);
+        }
+        return out;
+    }
+
+private:
+    int device_;
+    size_t max_points_, max_scan_;
+    pf_map* h_ = nullptr;
+    std::vector<float> buf_;
 };
 
 }  // namespace pfilter_hip

@@ -100,3 +100,35 @@ def test_front_end_shim_matches_python_binding(pa, pfsynth, tmp_path):
             xyz = np.frombuffer(raw, np.float32, 3 * len(r[k]), off).reshape(-1, 3)
             off += 12 * len(r[k])
             np.testing.assert_array_equal(xyz, x[r[k], :3])
+
+
+def test_mapping_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
+    """LaserMappingClass drop-in (shim) driven like src/laserMappingNode.cpp:72-86, the pose as the
+    Isometry3d matrix: the same map as the pose-quaternion entry point."""
+    exe = str(tmp_path / "shim_map_driver")
+    lib = os.path.join(ROOT, "pfilter-noetic_amd")
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "shim", "shim_map_driver.cpp"), "-o", exe, "-L", lib,
+                           "-lpfilter_hip", "-Wl,-rpath," + lib, "-Wl,-rpath-link,/opt/rocm/lib"])
+    seq = pfsynth.Sequence("S64", n_frames=10, az_steps=800)
+    lid = pfref.make_lidar(64, 3.0, 90.0)
+    m = pa.LaserMappingClass(max_points=1 << 21, max_scan=100000)
+    m.init(0.4)
+    with open(tmp_path / "frames.bin", "wb") as f:
+        for k in range(0, 10, 2):
+            e, s = pfref.feature_extraction(seq.frame(k), lid, opts=pfref.FE_STABLE_TIES)
+            x = np.concatenate([e, s]).astype(np.float32)
+            p = seq.gt_pose(k)
+            qx, qy, qz, qw = p[:4]
+            tx, ty, tz = 2 * qx, 2 * qy, 2 * qz
+            R = np.array([[1 - (ty * qy + tz * qz), ty * qx - tz * qw, tz * qx + ty * qw],
+                          [ty * qx + tz * qw, 1 - (tx * qx + tz * qz), tz * qy - tx * qw],
+                          [tz * qx - ty * qw, tz * qy + tx * qw, 1 - (tx * qx + ty * qy)]])
+            T = np.c_[R, p[4:]].astype(np.float64)
+            np.array([x.shape[0]], np.int64).tofile(f)
+            T.tofile(f)
+            x.tofile(f)
+            m.updateCurrentPointsToMap(x, p)
+    subprocess.check_call([exe, str(tmp_path / "frames.bin"), str(tmp_path / "map.bin")], timeout=120)
+    got = np.fromfile(tmp_path / "map.bin", np.float32).reshape(-1, 4)
+    np.testing.assert_array_equal(got, m.getMap())

@@ -105,6 +105,9 @@ def main():
         with open(os.path.join(a.out, "%s_front_end.md" % a.round), "w") as f:
             f.write("\n".join(lines) + "\n")
         print("front end us/frame %.1f" % tot)
+    mp = os.path.join(g, "map_prof", "run_kernel_stats.csv")
+    if os.path.exists(mp):
+        shutil.copy(mp, os.path.join(a.out, "%s_map_kernel_stats.csv" % a.round))
     fetch = os.path.join(g, "pmc_fetch", "run_counter_collection.csv")
     write = os.path.join(g, "pmc_write", "run_counter_collection.csv")
     if os.path.exists(fetch) and os.path.exists(write):
