@@ -363,6 +363,7 @@ def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True
         orc = pfref.OdomBPF(lid, 0.4, 0, 0.4, 75, 0, opts=0)
         cw = min(warmup, 11)                     # optimization_count reaches its steady 2 after 10 frames
         n, el, k = 0, 0.0, 0
+        pc = pinned_core().__enter__()
         while k < total and (el < cpu_seconds or k < cw):
             x = seq.frame(k)
             t = time.perf_counter()
@@ -376,7 +377,9 @@ def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True
                 el += time.perf_counter() - t
                 n += 1
             k += 1
-        out["cpu_baseline"] = {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+        host = pc.host()
+        pc.__exit__(None, None, None)
+        out["cpu_baseline"] = {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port", "host": host,
                                "sample": "pfref front end (radius k-NN over a hash grid, PCA) + OdomBPF "
                                          "(reference-faithful opts=0), frames %d..%d, single thread (the "
                                          "reference's PCA loop uses up to 6 OpenMP threads, preProcess.hpp:207), "
@@ -385,8 +388,48 @@ def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True
     return out
 
 
+class pinned_core:
+    """Run the CPU baseline on one core (single thread, pinned like `taskset -c 0`), and
+    describe the host: the CPU model and the cores this process may use."""
+
+    def __enter__(self):
+        self.saved = None
+        try:
+            self.saved = os.sched_getaffinity(0)
+            self.core = min(self.saved)
+            os.sched_setaffinity(0, {self.core})
+        except (AttributeError, OSError):
+            self.core = None
+        return self
+
+    def __exit__(self, *exc):
+        if self.saved:
+            os.sched_setaffinity(0, self.saved)
+        return False
+
+    def host(self):
+        model = "unknown"
+        try:
+            with open("/proc/cpuinfo") as f:
+                for line in f:
+                    if line.startswith("model name"):
+                        model = line.split(":", 1)[1].strip()
+                        break
+        except OSError:
+            pass
+        return {"cpu_model": model, "pinned_core": self.core,
+                "cores_available": len(self.saved) if self.saved else os.cpu_count()}
+
+
 def cpu_baseline(budget_s, warmup):
     """pfref oracle, single thread, reference-faithful options (kd-tree, dense-QR LM, std::sort)."""
+    with pinned_core() as pc:
+        out = _cpu_baseline(budget_s, warmup)
+        out["host"] = pc.host()
+    return out
+
+
+def _cpu_baseline(budget_s, warmup):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pfref
     import pfsynth

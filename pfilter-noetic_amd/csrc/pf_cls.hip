@@ -426,8 +426,11 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
     const int l = lane_id();
     const int nw = gridDim.x * WPB;
     const int wv = (int)xcd_block(blockIdx.x, gridDim.x) * WPB + (int)(threadIdx.x >> 6);
-    for (int q = wv; q < nu; q += nw) {                      // wave-uniform
-        const float4 qp = d.U[q];
+    for (int qs = wv; qs < nu; qs += nw) {                   // wave-uniform
+        // queries in cell (Morton) order: neighbouring waves share candidate chunks in L2
+        const float4 qc = gv.cpts[qs];
+        const int q = __float_as_int(qc.w);
+        const float4 qp = make_float4(qc.x, qc.y, qc.z, 0.f);
         u64 ent = ~0ull;                                     // list entry l
         u64 thr = ~0ull;                                     // entry K - 1
         auto open = [&](float lb) {
