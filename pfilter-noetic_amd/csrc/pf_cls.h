@@ -51,7 +51,6 @@ struct ClsGPU {
     uint8_t* code = nullptr;     // [cap] index_with_feature code per U point
     int* ptnum = nullptr;        // [cap] neighbours found per U point
     int* idx_out = nullptr;      // [cap] input indices of beam | pillar | facade
-    int* pos = nullptr;          // [cap] U index -> position in the grid's cell-ordered points
     float4* box = nullptr;       // [2 * (cap / 16 + 1)] bounding box (lo, hi) of every 16-point chunk
     u32* nbr = nullptr;          // [cap * kClsMaxK] neighbour lists (U indices, ascending distance)
     GridGPU grid;

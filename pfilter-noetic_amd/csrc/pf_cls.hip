@@ -31,12 +31,11 @@ struct ClsDev {          // kernel view of ClsGPU
     u32* cvals;
     uint8_t* code;
     int* ptnum;
-    int* pos;
     float4* box;
 };
 ClsDev dev_view(ClsGPU& c) {
     return ClsDev{c.prm, c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals,
-                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.pos, c.box};
+                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.box};
 }
 
 __device__ __forceinline__ float wave_minf(float v) {
@@ -273,7 +272,7 @@ __global__ void __launch_bounds__(256) k_u_keys(ClsDev d, const int* __restrict_
         d.cvals[j] = (u32)j;
     }
 }
-// cell-ordered points (w = U index), U index -> position, and the counts left zero for the next build
+// cell-ordered points (w = U index), and the counts left zero for the next build
 __global__ void __launch_bounds__(256) k_u_place(ClsDev d, float4* __restrict__ cpts, u32* __restrict__ cell_count,
                                                  const int* __restrict__ dm) {
     const int nu = d.cnt[CC_NU];
@@ -281,7 +280,6 @@ __global__ void __launch_bounds__(256) k_u_place(ClsDev d, float4* __restrict__ 
         const u32 j = d.cvals[i];
         const float4 p = d.U[j];
         cpts[i] = make_float4(p.x, p.y, p.z, __int_as_float((int)j));
-        d.pos[j] = i;
         if (dm[7]) cell_count[d.ckeys[i] >> 9] = 0u;
     }
 }
@@ -643,7 +641,6 @@ int cls_alloc(ClsGPU& c, size_t cap) {
     if (hipMalloc(&c.code, cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&c.ptnum, sizeof(int) * cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&c.idx_out, sizeof(int) * cap) != hipSuccess) return PF_ENOMEM;
-    if (hipMalloc(&c.pos, sizeof(int) * cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&c.nbr, sizeof(u32) * kClsMaxK * cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&c.box, sizeof(float4) * 2 * (cap / 16 + 1)) != hipSuccess) return PF_ENOMEM;
     const u32 gb0[8] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u, 0u, 0u, 0u};
@@ -656,7 +653,7 @@ int cls_alloc(ClsGPU& c, size_t cap) {
 
 void cls_free(ClsGPU& c) {
     void* ps[] = {c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals, c.pts,
-                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.idx_out, c.pos, c.box, c.nbr};
+                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.idx_out, c.box, c.nbr};
     for (void* p : ps) (void)hipFree(p);
     grid_free(c.grid);
     prim_free(c.w);
