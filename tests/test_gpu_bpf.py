@@ -4,6 +4,8 @@ stand-in for the reference's PCA classifier, which is outside this path: SURVEY 
 
 Tolerances as for the ES estimator (BASELINE.json north_star): pose within 1e-4 m / 1e-5 rad per
 frame; per-class down-sampled counts, residual counts, map sizes and age / p-index bytes identical."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -151,6 +153,25 @@ def test_bpf_scan_pipeline(pa, pfref, pfsynth):
     dev2.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
     last = [dev2.frame_host(x) for x in scans[:4]][-1]
     np.testing.assert_array_equal(last, poses_h[3])
+
+
+def test_bpf_scan_edge_cases(pa, pfsynth):
+    """Raw-scan mode with an empty scan and a scan of a few points (the front end yields empty class
+    clouds; the estimator warns that the map is too small, as the reference prints and continues), a
+    scan above max_points (PF_ECAPACITY) and front-end parameters outside the supported range."""
+    od = pa.Odom_BPF_EstimationClass(device=0, max_points=200000)
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    buf = pa.DeviceBuffer(16 * 200000)
+    x = pfsynth.Sequence("S64", n_frames=2, az_steps=800).frame(0)
+    buf.upload(x)
+    od.frame_scan_device(buf.ptr, x.shape[0])                          # seeds the maps
+    for n in (0, 5):
+        pose = np.empty(7)
+        rc = pa.lib().pf_bpf_frame_scan_device(od._h, buf.ptr, n, pose.ctypes.data)
+        assert rc >= 0 and np.all(np.isfinite(pose))
+    assert pa.lib().pf_bpf_frame_scan_device(od._h, buf.ptr, 200001, None) == pa.PF_ECAPACITY
+    bad = pa.cls_params(k=40)
+    assert pa.lib().pf_bpf_set_front_end(od._h, ctypes.byref(bad)) == pa.PF_EINVAL
 
 
 def test_bpf_rejects_es_entry_points(pa):

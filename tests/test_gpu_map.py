@@ -81,3 +81,29 @@ def test_device_entry_point(pa, pfref, pfsynth):
         pose = np.ascontiguousarray(p, np.float64)
         assert pa.lib().pf_map_update_device(b._h, buf.ptr, x.shape[0], pose.ctypes.data) == 0
     np.testing.assert_array_equal(a.getMap(), b.getMap())
+
+
+def test_edge_cases(pa, pfref):
+    """Empty scans, a scan above max_scan and a map above max_points (PF_ECAPACITY, map unchanged)."""
+    g, o = _pair(pa, pfref)
+    ident = np.array([0, 0, 0, 1, 0, 0, 0.0])
+    empty = np.zeros((0, 4), np.float32)
+    g.updateCurrentPointsToMap(empty, ident)
+    assert o.update(empty, ident) == 0
+    assert g.getMap().shape == (0, 4)
+    rng = np.random.default_rng(9)
+    x = np.c_[rng.uniform(-20, 20, (500, 3)), np.zeros(500)].astype(np.float32)
+    g.updateCurrentPointsToMap(x, ident)
+    o.update(x, ident)
+    np.testing.assert_array_equal(g.getMap(), o.get())
+    small = pa.LaserMappingClass(max_points=100, max_scan=50)
+    small.init(0.4)
+    with pytest.raises(pa.PFError):
+        small.updateCurrentPointsToMap(x[:60], ident)                  # above max_scan
+    small.updateCurrentPointsToMap(x[:50], ident)
+    small.updateCurrentPointsToMap(x[50:100], ident)
+    n = small.getMap().shape[0]
+    with pytest.raises(pa.PFError):
+        for k in range(2, 10):                                        # the map outgrows max_points
+            small.updateCurrentPointsToMap(x[50 * k:50 * k + 50] + np.float32(0.01 * k), ident)
+    assert small.getMap().shape[0] >= n
