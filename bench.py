@@ -176,6 +176,8 @@ def run_kitti11(rank, local_rank, world, warmup, threads, use_graph, barrier, co
         od = pa.Odom_ES_EstimationClass(device=local_rank, max_points=300000, map_capacity=1 << 22)
         od.init(lidar_cfg(), **ODOM_CFG)
         od.set_graph(use_graph)
+        if concurrent > 1:
+            od.set_stage_a_reserve(0)      # several sequences share the GPU: stage A may use every CU
         for ptr, n in seqs[0][0][:warmup]:
             od.frame_device(ptr, n)
         od.sync()

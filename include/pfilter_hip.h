@@ -205,6 +205,10 @@ int pf_odom_frame_host(pf_odom* h, const float* xyzi, size_t n, size_t stride_by
 int pf_odom_sync(pf_odom* h);
 /* poses of frames processed so far, 7 doubles each */
 int pf_odom_poses(pf_odom* h, double* poses, size_t cap, size_t* n);
+/* compute units stage A (features / front end + VoxelGrid) stays off, so that stage B (the odometry,
+ * whose LM needs 32 co-resident workgroups) starts while stage A runs. Defaults: 128 (ES), 32 (BPF);
+ * 0 = unrestricted, which is better when several handles share one GPU. */
+int pf_odom_set_stage_a_reserve(pf_odom* h, int cus);
 /* enable/disable hipGraph replay of the steady-state frame (default on) */
 int pf_odom_set_graph(pf_odom* h, int enable);
 

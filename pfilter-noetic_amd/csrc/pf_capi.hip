@@ -574,6 +574,13 @@ int pf_bpf_frame_scan_device(pf_odom* h, const float* d_xyzi, size_t n, double p
     return err || gerr ? PF_ECAPACITY : rc;
 }
 
+int pf_odom_set_stage_a_reserve(pf_odom* h, int cus) {
+    if (!h || cus < 0) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
+    return odom_stage_a_stream(h->o, cus);
+}
+
 int pf_odom_sync(pf_odom* h) {
     if (!h) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->o.device));

@@ -140,7 +140,17 @@ struct OdomGPU {
     float4* stage = nullptr;       // [kMaxC * in_cap] staging target of the frame entry points
 
     bool graph_enabled = true;
+    int cu_reserve = 0;            // CUs stage A stays off (odom_stage_a_stream)
 };
+
+// Stage A keeps off the last CUs of the device by default: with one sequence per GPU, stage B's LM
+// (kLmBlocks co-resident workgroups) otherwise waits for stage A's waves to drain. Measured on one
+// MI355X: ES 3.09k -> 3.24k frames/s at 128 CUs reserved (a cliff past 192); the BPF
+// raw-scan chain 1.25k -> 1.79k at 32 (its front end needs the CUs); several concurrent sequences
+// per GPU lose with any reservation (pf_odom_set_stage_a_reserve(h, 0)).
+constexpr int kStageAReserveES = 128;
+constexpr int kStageAReserveBPF = 32;
+int odom_stage_a_stream(OdomGPU& o, int reserve);
 
 // nc = 2: the ES estimator; nc = 3: the BPF estimator (the last class is the plane class)
 int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& prm, int device, size_t in_cap,

@@ -23,6 +23,7 @@
 
 #include <climits>
 #include <cstdlib>
+#include <vector>
 #include <cstring>
 
 namespace pf {
@@ -1369,6 +1370,27 @@ __global__ void k_init_counts(int* __restrict__ cnt, DevState* __restrict__ st, 
 }  // namespace
 
 // ==============================================================================================
+// (Re)create stage A's stream, restricted to all but the last `reserve` CUs (0: unrestricted).
+int odom_stage_a_stream(OdomGPU& o, int reserve) {
+    if (o.stream_a) {
+        if (hipStreamSynchronize(o.stream_a) != hipSuccess) return PF_EHIP;
+        (void)hipStreamDestroy(o.stream_a);
+        o.stream_a = nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, o.device) != hipSuccess) return PF_EHIP;
+    const int ncu = prop.multiProcessorCount;
+    o.cu_reserve = 0;
+    if (reserve > 0 && reserve <= ncu - 32) {
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int c = 0; c < ncu - reserve; ++c) mask[c / 32] |= 1u << (c % 32);
+        if (hipExtStreamCreateWithCUMask(&o.stream_a, (uint32_t)mask.size(), mask.data()) != hipSuccess) return PF_EHIP;
+        o.cu_reserve = reserve;
+        return PF_OK;
+    }
+    return hipStreamCreateWithFlags(&o.stream_a, hipStreamNonBlocking) == hipSuccess ? PF_OK : PF_EHIP;
+}
+
 int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& prm, int device, size_t in_cap,
                 size_t map_cap, int nc) {
     if (nc < 2 || nc > kMaxC) return PF_EINVAL;
@@ -1387,7 +1409,11 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
         o.leaf_rg[c] = plane ? (float)prm.map_res * 2 : (float)prm.map_res;     // float map_resolution (.h:62)
     }
     if (hipStreamCreateWithFlags(&o.stream, hipStreamNonBlocking) != hipSuccess) return PF_EHIP;
-    if (hipStreamCreateWithFlags(&o.stream_a, hipStreamNonBlocking) != hipSuccess) return PF_EHIP;
+    // stage A is kept off the last compute units by default (odom_stage_a_stream), so that stage B's
+    // kernels — the LM needs kLmBlocks co-resident workgroups — find free CUs while stage A runs
+    int reserve = nc == 2 ? kStageAReserveES : kStageAReserveBPF;
+    if (const char* e = std::getenv("PF_STAGE_A_CU_RESERVE")) reserve = std::atoi(e);   // development override
+    if (int rc0 = odom_stage_a_stream(o, reserve)) return rc0;
     int rc = fe_alloc(o.fe, lidar, in_cap);
     if (rc) return rc;
     // 1 m cells over every map's bounding box: 3 x (201 m)^2 x 270 m covers the +-100 m crop box

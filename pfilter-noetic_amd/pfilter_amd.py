@@ -87,7 +87,7 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_bpf_create", "pf_bpf_init_map", "pf_bpf_update", "pf_bpf_frame_device", "pf_odom_classes",
            "pf_odom_reset", "pf_cls_default_params", "pf_cls_create", "pf_cls_destroy", "pf_cls_extract",
            "pf_cls_classify", "pf_cls_ground_seg", "pf_bpf_set_front_end", "pf_bpf_frame_scan_device", "pf_map_create", "pf_map_destroy", "pf_map_update",
-           "pf_map_update_device", "pf_map_update_mat", "pf_map_get"]
+           "pf_map_update_device", "pf_map_update_mat", "pf_map_get", "pf_odom_set_stage_a_reserve"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -119,6 +119,8 @@ def lib():
     L.pf_odom_sync.argtypes = [_vp]
     L.pf_odom_poses.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
     L.pf_odom_set_graph.argtypes = [_vp, _i]
+    if hasattr(L, "pf_odom_set_stage_a_reserve"):
+        L.pf_odom_set_stage_a_reserve.argtypes = [_vp, _i]
     L.pf_device_count.argtypes = [ctypes.POINTER(_i)]
     L.pf_dev_malloc.argtypes = [_i, _sz, ctypes.POINTER(_vp)]
     L.pf_dev_free.argtypes = [_i, _vp]
@@ -336,6 +338,10 @@ class Odom_ES_EstimationClass:
 
     def set_graph(self, enable):
         _check("pf_odom_set_graph", lib().pf_odom_set_graph(self._h, int(bool(enable))))
+
+    def set_stage_a_reserve(self, cus):
+        """CUs stage A stays off (default 128 ES / 32 BPF; 0 when several handles share the GPU)"""
+        _check("pf_odom_set_stage_a_reserve", lib().pf_odom_set_stage_a_reserve(self._h, int(cus)))
 
     def reset(self):
         """state right after init (a new sequence on the same handle and buffers)"""
