@@ -255,3 +255,29 @@ def test_live_handle_limit_per_device(pa):
     finally:
         for h in made:
             pa.lib().pf_odom_destroy(h)
+
+
+def test_stage_a_reservation_does_not_change_results(pa, pfsynth):
+    """The stage-A CU mask (default 128 reserved CUs, pf_odom_set_stage_a_reserve) only moves work
+    between CUs: the same 16 frames give the same bits with the default, with 0 and with 64."""
+    seq = pfsynth.Sequence("S64", n_frames=16, az_steps=1000)
+    buf, counts = seq.frames(0, 16)
+    db = pa.DeviceBuffer(buf.nbytes)
+    db.upload(buf)
+    runs = []
+    for reserve in (None, 0, 64):
+        od = pa.Odom_ES_EstimationClass(device=0)
+        od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+        if reserve is not None:
+            od.set_stage_a_reserve(reserve)
+        for i in range(16):
+            od.frame_device(db.ptr + i * buf.shape[1] * 16, counts[i])
+        od.sync()
+        runs.append(od.poses())
+        del od
+    np.testing.assert_array_equal(runs[0], runs[1])
+    np.testing.assert_array_equal(runs[0], runs[2])
+    with pytest.raises(pa.PFError):
+        od = pa.Odom_ES_EstimationClass(device=0)
+        od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+        od.set_stage_a_reserve(-1)
