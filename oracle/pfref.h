@@ -101,6 +101,11 @@ void pfref_eigen_sym3(const double a[6], double evals[3], double evecs[9] /* col
 void pfref_plane_fit(const double A[15], double n_out[3]);
 /* PoseSE3Parameterization::Plus */
 void pfref_se3_plus(const double x[7], const double delta[6], double out[7]);
+/* GPU_EQUIV SE(3) update: getTransformFromSe3 with one deterministic sincos of theta/2 and the
+ * half-angle identities (the device's arithmetic, pf_geom.h se3_exp) */
+void pfref_se3_plus_half(const double x[7], const double delta[6], double out[7]);
+/* sin/cos from + - * and rint only (fdlibm kernels): bit-identical on the host and the device */
+void pfref_det_sincos(double x, double* s, double* c);
 /* Eigen 3.3 Isometry3d::rotation(): orthogonal polar factor of a 3x3 (row-major in/out) */
 void pfref_rotation_polar(const double m[9], double out[9]);
 /* Edge/SurfNormAnalyticCostFunction::Evaluate: returns residual, J[7] */

@@ -92,6 +92,8 @@ def lib():
         L.pfref_eigen_sym3.argtypes = [_vp, _vp, _vp]
         L.pfref_plane_fit.argtypes = [_vp, _vp]
         L.pfref_se3_plus.argtypes = [_vp, _vp, _vp]
+        L.pfref_se3_plus_half.argtypes = [_vp, _vp, _vp]
+        L.pfref_det_sincos.argtypes = [ctypes.c_double, _vp, _vp]
         L.pfref_rotation_polar.argtypes = [_vp, _vp]
         L.pfref_edge_eval.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_double, _vp]
         L.pfref_edge_eval.restype = ctypes.c_double
@@ -216,6 +218,22 @@ def se3_plus(x, delta):
     out = np.empty(7)
     lib().pfref_se3_plus(x.ctypes.data, d.ctypes.data, out.ctypes.data)
     return out
+
+
+def se3_plus_half(x, delta):
+    """the GPU_EQUIV SE(3) update (one deterministic sincos of theta/2, half-angle identities)"""
+    x = np.ascontiguousarray(x, np.float64)
+    d = np.ascontiguousarray(delta, np.float64)
+    out = np.empty(7)
+    lib().pfref_se3_plus_half(x.ctypes.data, d.ctypes.data, out.ctypes.data)
+    return out
+
+
+def det_sincos(x):
+    s = np.empty(1)
+    c = np.empty(1)
+    lib().pfref_det_sincos(float(x), s.ctypes.data, c.ctypes.data)
+    return float(s[0]), float(c[0])
 
 
 def rotation_polar(m):

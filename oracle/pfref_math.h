@@ -279,6 +279,80 @@ inline void se3_plus(const double* x, const double* delta, double* out) {
     out[4] = tp.x; out[5] = tp.y; out[6] = tp.z;
 }
 
+// --- GPU_EQUIV (PFREF_LM_NORMAL_EQ) SE(3) update -----------------------------------------
+// The device evaluates getTransformFromSe3 with ONE sincos of theta/2 and the half-angle identities
+// sin(theta) = 2 s c, 1 - cos(theta) = 2 s^2, theta^3 as a product, and takes that sincos from a
+// routine built from + - * and rint only, so the host and gfx950 agree to the bit (libm's and the
+// device library's sin/cos differ in the last ulp now and then). Both are restated here; each
+// value is within ~1 ulp of se3_exp above (tests/test_oracle_units.py bounds the difference).
+// Cody-Waite reduction by pi/2 (two 33-bit parts), fdlibm's minimax sin/cos kernels on [-pi/4, pi/4].
+inline void det_sincos(double x, double* sn, double* cs) {
+    const double invpio2 = 6.36619772367581382433e-01;
+    const double pio2_1 = 1.57079632673412561417e+00;
+    const double pio2_1t = 6.07710050650619224932e-11;
+    const double k = std::rint(x * invpio2);
+    const double r = (x - k * pio2_1) - k * pio2_1t;
+    const double z = r * r;
+    const double v = z * r;
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double s = r + v * (S1 + z * (S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)))));
+    const double pc = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double c = w + (((1.0 - w) - hz) + z * pc);
+    const long long n = (k == k && std::fabs(k) < 9.0e15) ? (long long)k : 0;
+    switch ((int)(n & 3)) {
+        case 0: *sn = s; *cs = c; break;
+        case 1: *sn = c; *cs = -s; break;
+        case 2: *sn = -s; *cs = -c; break;
+        default: *sn = -c; *cs = s; break;
+    }
+}
+inline void se3_exp_half(const double se3[6], Quat& q, V3& t) {
+    V3 omega{se3[0], se3[1], se3[2]};
+    V3 upsilon{se3[3], se3[4], se3[5]};
+    M3 Omega = skew(omega);
+    const double theta = norm(omega);
+    const double half_theta = 0.5 * theta;
+    double s_h, c_h;
+    det_sincos(half_theta, &s_h, &c_h);
+    double imag_factor;
+    if (theta < 1e-10) {
+        const double theta_sq = theta * theta;
+        const double theta_po4 = theta_sq * theta_sq;
+        imag_factor = 0.5 - 0.0208333 * theta_sq + 0.000260417 * theta_po4;
+    } else {
+        imag_factor = s_h / theta;
+    }
+    q = {imag_factor * omega.x, imag_factor * omega.y, imag_factor * omega.z, c_h};
+    M3 J;
+    if (theta < 1e-10) {
+        J = q2m(q);
+    } else {
+        M3 Omega2 = mmul(Omega, Omega);
+        const double a = (2.0 * (s_h * s_h)) / (theta * theta);
+        const double b = (theta - 2.0 * (s_h * c_h)) / (theta * theta * theta);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) J.m[i][j] = (i == j ? 1.0 : 0.0) + a * Omega.m[i][j] + b * Omega2.m[i][j];
+    }
+    t = mvec(J, upsilon);
+}
+inline void se3_plus_half(const double* x, const double* delta, double* out) {
+    V3 trans{x[4], x[5], x[6]};
+    Quat dq; V3 dt;
+    se3_exp_half(delta, dq, dt);
+    Quat quater{x[0], x[1], x[2], x[3]};
+    Quat qp = qmul(dq, quater);
+    V3 tp = add(qrot(dq, trans), dt);
+    out[0] = qp.x; out[1] = qp.y; out[2] = qp.z; out[3] = qp.w;
+    out[4] = tp.x; out[5] = tp.y; out[6] = tp.z;
+}
+
 // EdgeAnalyticCostFunction::Evaluate (src/lidarOptimization.cpp:12-46); J has 7 entries, J[6]=0
 inline double edge_eval(const double* x, V3 cur, V3 a, V3 b, double w, double* J) {
     Quat q{x[0], x[1], x[2], x[3]};

@@ -291,6 +291,7 @@ struct Residual {
     V3 cur, a, b;   // edge: line points; surf: a = unit normal
     double d;       // surf: (double)(float)negative_OA_dot_norm
     double w;       // point_weight (0 = none)
+    int q;          // index of the query in the classes' concatenated down-sampled clouds
 };
 
 namespace {
@@ -364,33 +365,248 @@ void householder_solve(std::vector<double>& A, int rows, int cols, std::vector<d
     for (int j = 0; j < cols; ++j) x[j] = rhs[j];
 }
 
-// 6x6 SPD solve by Cholesky (GPU-equivalent normal-equation mode)
-bool chol6(const double H[36], const double g[6], double y[6]) {
-    double L[36] = {0};
-    for (int i = 0; i < 6; ++i) {
+// ---- GPU_EQUIV LM (PFREF_LM_NORMAL_EQ): the device's solve, restated step for step -----------
+// pfilter-noetic_amd/csrc/pf_odom.hip k_lm_solve / lm_accept / lm_try_step / lm_next_step. The
+// same Ceres 1.14 trust-region loop as solve_lm below, on the 6x6 normal equations (Cholesky) with
+// the device's arithmetic order, so that the GPU and this mode agree to the bit over whole
+// sequences: every evaluation reduces (cost, g, upper J^T J) over the residuals in the device's
+// fixed tree, the Jacobi scaling multiplies H instead of J, and the SE(3) update is se3_plus_half.
+constexpr int kDevBlocks = 32;        // pf_odom.hip PF_LM_BLOCKS
+constexpr int kDevChunk = 256;        // rows per block pass (threads per block)
+constexpr int kDevRows = 29;          // rows per reduction thread: 9 threads per product
+constexpr int kDevProducts = 28;      // cost, g[6], upper J^T J (21, row by row)
+constexpr int kDevEvals = 5;          // 1 + max_num_iterations
+
+struct DevLm {
+    double x[7], cand[7], best[7], scale[6], g[6], H[21], D[6];
+    double cost, radius, decrease, x_norm, min_cost, mcc;
+    int iteration, invalid, reuse, done, phase;
+};
+struct DevStep {
+    double y[6], D[6], mcc;
+    bool ok;
+};
+inline int hup(int i, int j) {        // packed upper triangle, row by row
+    if (i > j) std::swap(i, j);
+    return i * 6 - (i * (i - 1)) / 2 + (j - i);
+}
+inline int tri(int i, int j) { return i * (i + 1) / 2 + j; }
+
+// One evaluation at x. The device's tree: residual q (its query index) is row q % 256 of chunk
+// q / 256, chunk n belongs to block n % 32; thread (k, p) of a block sums product k over rows
+// 29 p .. 29 p + 28 of each of its chunks, chunk after chunk; the block adds its 9 thread sums in p
+// order and the total adds the 32 block sums in block order. Queries without a kept residual (and
+// residuals that are not finite) are zero rows there, which leave every partial unchanged, so only
+// the kept residuals are visited, in increasing q as the device takes them.
+void dev_evaluate(const std::vector<Residual>& res, const double* x, double tot[30]) {
+    static thread_local std::vector<double> part;
+    part.assign((size_t)kDevBlocks * kDevProducts * 9, 0.0);
+    int bad_r = 0, bad_j = 0;
+    for (const Residual& rs : res) {
+        double J[7];
+        double r = rs.edge ? edge_eval(x, rs.cur, rs.a, rs.b, rs.w, J) : surf_eval(x, rs.cur, rs.a, rs.d, rs.w, J);
+        bool jbad = false;
+        for (int k = 0; k < 6; ++k) jbad |= !std::isfinite(J[k]);
+        if (!std::isfinite(r)) {
+            ++bad_r;
+            continue;
+        }
+        if (jbad) ++bad_j;
+        const double s = r * r;                                  // HuberLoss(0.1) + Corrector
+        double rho0, rho1;
+        if (s > kHuberB) {
+            const double rr = std::sqrt(s);
+            rho0 = 2.0 * kHuberA * rr - kHuberB;
+            rho1 = std::max(std::numeric_limits<double>::min(), kHuberA / rr);
+        } else {
+            rho0 = s;
+            rho1 = 1.0;
+        }
+        const double hc = 0.5 * rho0;
+        const double sr = std::sqrt(rho1);
+        r *= sr;
+        for (int k = 0; k < 6; ++k) J[k] *= sr;
+        const int blk = (rs.q / kDevChunk) % kDevBlocks, p = (rs.q % kDevChunk) / kDevRows;
+        double* P = &part[(size_t)blk * kDevProducts * 9 + p];
+        P[0] += hc * 1.0;
+        for (int k = 0; k < 6; ++k) P[9 * (1 + k)] += J[k] * r;
+        int h = 7;
+        for (int i = 0; i < 6; ++i)
+            for (int j = i; j < 6; ++j, ++h) P[9 * h] += J[i] * J[j];
+    }
+    for (int k = 0; k < kDevProducts; ++k) {
+        double v = 0.0;
+        for (int b = 0; b < kDevBlocks; ++b) {
+            const double* P = &part[((size_t)b * kDevProducts + k) * 9];
+            double vb = P[0];
+            for (int p = 1; p < 9; ++p) vb += P[p];
+            v += vb;
+        }
+        tot[k] = v;
+    }
+    tot[28] = (double)bad_r;
+    tot[29] = (double)bad_j;
+}
+
+DevStep dev_try_step(const DevLm& lm) {                       // lm_try_step
+    DevStep r;
+    for (int j = 0; j < 6; ++j)
+        r.D[j] = lm.reuse ? lm.D[j] : std::fmin(std::fmax(lm.scale[j] * lm.H[hup(j, j)] * lm.scale[j], 1e-6), 1e32);
+    double A[21];
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j <= i; ++j) A[tri(i, j)] = lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j];
+    for (int j = 0; j < 6; ++j) {
+        const double ld = std::sqrt(r.D[j] / lm.radius);
+        A[tri(j, j)] += ld * ld;
+    }
+    bool ok = true;
+    for (int i = 0; i < 6; ++i)
         for (int j = 0; j <= i; ++j) {
-            double s = H[i * 6 + j];
-            for (int k = 0; k < j; ++k) s -= L[i * 6 + k] * L[j * 6 + k];
+            double s = A[tri(i, j)];
+            for (int k = 0; k < j; ++k) s -= A[tri(i, k)] * A[tri(j, k)];
             if (i == j) {
-                if (!(s > 0.0)) return false;
-                L[i * 6 + i] = std::sqrt(s);
+                ok = ok && (s > 0.0);
+                A[tri(i, i)] = std::sqrt(s);
             } else {
-                L[i * 6 + j] = s / L[j * 6 + j];
+                A[tri(i, j)] = s / A[tri(j, j)];
             }
         }
-    }
-    double z[6];
     for (int i = 0; i < 6; ++i) {
-        double s = g[i];
-        for (int k = 0; k < i; ++k) s -= L[i * 6 + k] * z[k];
-        z[i] = s / L[i * 6 + i];
+        double s = lm.scale[i] * lm.g[i];
+        for (int k = 0; k < i; ++k) s -= A[tri(i, k)] * r.y[k];
+        r.y[i] = s / A[tri(i, i)];
     }
     for (int i = 5; i >= 0; --i) {
-        double s = z[i];
-        for (int k = i + 1; k < 6; ++k) s -= L[k * 6 + i] * y[k];
-        y[i] = s / L[i * 6 + i];
+        double s = r.y[i];
+        for (int k = i + 1; k < 6; ++k) s -= A[tri(k, i)] * r.y[k];
+        r.y[i] = s / A[tri(i, i)];
     }
-    return true;
+    for (int j = 0; j < 6; ++j) ok = ok && std::isfinite(r.y[j]);
+    r.mcc = 0.0;
+    if (ok) {
+        double sg = 0.0, sHs = 0.0;
+        for (int i = 0; i < 6; ++i) {
+            sg += -r.y[i] * (lm.scale[i] * lm.g[i]);
+            double hi = 0.0;
+            for (int j = 0; j < 6; ++j) hi += lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j] * -r.y[j];
+            sHs += -r.y[i] * hi;
+        }
+        r.mcc = -(sg + 0.5 * sHs);
+    }
+    r.ok = ok && (r.mcc > 0.0);
+    return r;
+}
+
+void dev_next_step(DevLm& lm, DevStep st, const double* cand_first) {   // lm_next_step
+    const int kMaxIter = 4;
+    for (bool first = true;; first = false) {
+        lm.iteration++;
+        if (!first) st = dev_try_step(lm);
+        if (!lm.reuse)
+            for (int j = 0; j < 6; ++j) lm.D[j] = st.D[j];
+        lm.reuse = 1;
+        if (!st.ok) {
+            if (++lm.invalid >= 5) { lm.done = 1; return; }
+            lm.radius = lm.radius / lm.decrease;
+            lm.decrease *= 2.0;
+            if (lm.iteration >= kMaxIter || lm.radius <= 1e-32) { lm.done = 1; return; }
+            continue;
+        }
+        lm.invalid = 0;
+        if (first) {
+            for (int k = 0; k < 7; ++k) lm.cand[k] = cand_first[k];
+        } else {
+            double delta[6];
+            for (int j = 0; j < 6; ++j) delta[j] = -st.y[j] * lm.scale[j];
+            se3_plus_half(lm.x, delta, lm.cand);
+        }
+        lm.mcc = st.mcc;
+        lm.phase = 1;
+        return;
+    }
+}
+
+void dev_accept(DevLm& lm, const double* tot) {                     // lm_accept
+    const double cost_c = tot[0];
+    const bool bad_r = tot[28] > 0.0, bad_j = tot[29] > 0.0;
+    const int kMaxIter = 4;
+    bool step_ok = false;
+    if (lm.phase == 0) {
+        if (bad_r || bad_j) { lm.done = 1; return; }
+        lm.cost = cost_c;
+        for (int k = 0; k < 6; ++k) lm.g[k] = tot[1 + k];
+        for (int k = 0; k < 21; ++k) lm.H[k] = tot[7 + k];
+        for (int i = 0; i < 6; ++i) lm.scale[i] = 1.0 / (1.0 + std::sqrt(lm.H[hup(i, i)]));
+        lm.min_cost = lm.cost;
+        for (int k = 0; k < 7; ++k) lm.best[k] = lm.x[k];
+        step_ok = true;
+    } else {
+        const double cand_cost = bad_r ? DBL_MAX : cost_c;
+        double sn = 0.0;
+        for (int j = 0; j < 7; ++j) sn += (lm.x[j] - lm.cand[j]) * (lm.x[j] - lm.cand[j]);
+        sn = std::sqrt(sn);
+        if (sn <= 1e-8 * (lm.x_norm + 1e-8)) { lm.done = 1; return; }
+        if (std::fabs(lm.cost - cand_cost) <= 1e-6 * lm.cost) { lm.done = 1; return; }
+        const double rel = (lm.cost - cand_cost) / lm.mcc;
+        if (rel > 1e-3) {
+            double xn = 0;
+            for (int j = 0; j < 7; ++j) { lm.x[j] = lm.cand[j]; xn += lm.x[j] * lm.x[j]; }
+            lm.x_norm = std::sqrt(xn);
+            if (bad_j) { lm.done = 1; return; }
+            lm.cost = cand_cost;
+            for (int k = 0; k < 6; ++k) lm.g[k] = tot[1 + k];
+            for (int k = 0; k < 21; ++k) lm.H[k] = tot[7 + k];
+            const double r3 = 2.0 * rel - 1.0;
+            const double f = 1.0 - r3 * r3 * r3;
+            lm.radius = lm.radius / std::fmax(1.0 / 3.0, f);
+            lm.radius = std::fmin(1e16, lm.radius);
+            lm.decrease = 2.0;
+            lm.reuse = 0;
+            step_ok = true;
+            if (lm.cost < lm.min_cost) {
+                lm.min_cost = lm.cost;
+                for (int k = 0; k < 7; ++k) lm.best[k] = lm.x[k];
+            }
+        } else {
+            lm.radius = lm.radius / lm.decrease;
+            lm.decrease *= 2.0;
+            lm.reuse = 1;
+        }
+        if (lm.iteration >= kMaxIter) { lm.done = 1; return; }
+    }
+    const DevStep st = dev_try_step(lm);
+    double ng[6], gx[7], delta[6], cand[7];
+    for (int j = 0; j < 6; ++j) { ng[j] = -lm.g[j]; delta[j] = -st.y[j] * lm.scale[j]; }
+    se3_plus_half(lm.x, ng, gx);                                 // gradient max-norm check
+    se3_plus_half(lm.x, delta, cand);                            // the first attempt's candidate
+    double gm = 0.0;
+    for (int j = 0; j < 7; ++j) gm = std::fmax(gm, std::fabs(lm.x[j] - gx[j]));
+    if (step_ok && gm <= 1e-10) lm.done = 1;
+    else if (lm.phase != 0 && lm.radius <= 1e-32) lm.done = 1;
+    else dev_next_step(lm, st, cand);
+}
+
+// Returns the LM iterations; params becomes the best point (unchanged without residuals).
+int solve_lm_dev(double* params, const std::vector<Residual>& res) {
+    if (res.empty()) return 0;
+    DevLm lm{};
+    double xn = 0;
+    for (int k = 0; k < 7; ++k) {
+        lm.x[k] = lm.cand[k] = lm.best[k] = params[k];
+        xn += lm.x[k] * lm.x[k];
+    }
+    lm.x_norm = std::sqrt(xn);
+    lm.radius = 1e4;
+    lm.decrease = 2.0;
+    for (int ev = 0; ev < kDevEvals; ++ev) {
+        if (lm.done) break;
+        double tot[30];
+        dev_evaluate(res, lm.cand, tot);
+        dev_accept(lm, tot);
+        if (ev == kDevEvals - 1) lm.done = 1;
+    }
+    std::copy(lm.best, lm.best + 7, params);
+    return lm.iteration;
 }
 
 double grad_max_norm(const double* x, const double* g) {
@@ -405,6 +621,7 @@ double grad_max_norm(const double* x, const double* g) {
 
 // Returns the number of LM iterations performed. params is updated with the best point.
 int solve_lm(double* params, const std::vector<Residual>& res, bool normal_eq) {
+    if (normal_eq) return solve_lm_dev(params, res);
     const int m = (int)res.size();
     if (m == 0) return 0;  // no residual blocks: parameter block removed, nothing to do
     const int kMaxIter = 4;
@@ -452,22 +669,7 @@ int solve_lm(double* params, const std::vector<Residual>& res, bool normal_eq) {
         double lm_diag[6], y[6], step[6];
         for (int j = 0; j < 6; ++j) lm_diag[j] = std::sqrt(D[j] / radius);
         bool solved = true;
-        if (normal_eq) {
-            double H[36], gs[6];
-            for (int a = 0; a < 6; ++a) {
-                gs[a] = 0.0;
-                for (int b = 0; b < 6; ++b) H[a * 6 + b] = 0.0;
-            }
-            for (int i = 0; i < m; ++i) {
-                const double* Ji = &J[6 * (size_t)i];
-                for (int a = 0; a < 6; ++a) {
-                    gs[a] += Ji[a] * r[i];
-                    for (int b = 0; b < 6; ++b) H[a * 6 + b] += Ji[a] * Ji[b];
-                }
-            }
-            for (int a = 0; a < 6; ++a) H[a * 6 + a] += lm_diag[a] * lm_diag[a];
-            solved = chol6(H, gs, y);
-        } else {
+        {
             const int rows = m + 6;
             A.assign((size_t)rows * 6, 0.0);
             rhs.assign(rows, 0.0);
@@ -642,8 +844,8 @@ double sparsity(const std::vector<PtC>& map, const int* ind) {
 
 // addEdgeCostFactor (:284-432); Odom_BPF addBeamCostFactor / addPillarCostFactor (:751-1010) are
 // the same function of their own map with the edge thresholds
-static void add_line_factors(Odom& o, int c, std::vector<PtC>& cloud, std::vector<Residual>& out) {
-    struct Info { V3 cur, a, b; float observe, round; };
+static void add_line_factors(Odom& o, int c, std::vector<PtC>& cloud, int qbase, std::vector<Residual>& out) {
+    struct Info { V3 cur, a, b; float observe, round; int q; };
     std::vector<Info> valid;
     std::vector<double> spars, obs;
     std::vector<PtC>& map = o.maps[c];
@@ -679,7 +881,7 @@ static void add_line_factors(Odom& o, int c, std::vector<PtC>& cloud, std::vecto
             if (!pindex(map, ind, o.k_new(c), o.theta_p(c), o.theta_max(c), observe, round)) continue;
             cloud[i].r = (uint8_t)std::min(255, int(round));
             cloud[i].g = (uint8_t)std::min(255, int(observe));
-            valid.push_back({cur, a, b, observe, round});
+            valid.push_back({cur, a, b, observe, round, qbase + (int)i});
             spars.push_back(sparsity(map, ind));
         }
     }
@@ -691,7 +893,7 @@ static void add_line_factors(Odom& o, int c, std::vector<PtC>& cloud, std::vecto
     if (wt == 2 || wt == 12) sparsity_mean(spars);
     for (size_t i = 0; i < valid.size(); i++) {
         Residual r;
-        r.edge = true; r.cur = valid[i].cur; r.a = valid[i].a; r.b = valid[i].b; r.d = 0;
+        r.edge = true; r.cur = valid[i].cur; r.a = valid[i].a; r.b = valid[i].b; r.d = 0; r.q = valid[i].q;
         if (wt == 0) r.w = 0;
         else if (wt == 1) r.w = obs[i];
         else if (wt == 2) r.w = spars[i];
@@ -703,8 +905,8 @@ static void add_line_factors(Odom& o, int c, std::vector<PtC>& cloud, std::vecto
 }
 
 // addSurfCostFactor (:434-578); Odom_BPF addFacadeCostFactor (:1012-1193) with the surf thresholds
-static void add_plane_factors(Odom& o, int c, std::vector<PtC>& cloud, std::vector<Residual>& out) {
-    struct Info { V3 cur, n; float d, observe, round; };
+static void add_plane_factors(Odom& o, int c, std::vector<PtC>& cloud, int qbase, std::vector<Residual>& out) {
+    struct Info { V3 cur, n; float d, observe, round; int q; };
     std::vector<Info> valid;
     std::vector<double> spars, obs;
     std::vector<PtC>& map = o.maps[c];
@@ -737,7 +939,7 @@ static void add_plane_factors(Odom& o, int c, std::vector<PtC>& cloud, std::vect
             if (!pindex(map, ind, o.k_new(c), o.theta_p(c), o.theta_max(c), observe, round)) continue;
             cloud[i].r = (uint8_t)std::min(255, int(round));
             cloud[i].g = (uint8_t)std::min(255, int(observe));
-            valid.push_back({cur, n, (float)negative_OA_dot_norm, observe, round});
+            valid.push_back({cur, n, (float)negative_OA_dot_norm, observe, round, qbase + (int)i});
             spars.push_back(sparsity(map, ind));
         }
     }
@@ -749,7 +951,7 @@ static void add_plane_factors(Odom& o, int c, std::vector<PtC>& cloud, std::vect
     if (wt == 2 || wt == 12) sparsity_mean(spars);
     for (size_t i = 0; i < valid.size(); i++) {
         Residual r;
-        r.edge = false; r.cur = valid[i].cur; r.a = valid[i].n; r.b = V3{0, 0, 0};
+        r.edge = false; r.cur = valid[i].cur; r.a = valid[i].n; r.b = V3{0, 0, 0}; r.q = valid[i].q;
         r.d = (double)valid[i].d;       // float member of surfInfo, reloaded into a float (A.7)
         if (wt == 0) r.w = 0;
         else if (wt == 1) r.w = obs[i];
@@ -843,9 +1045,11 @@ int odom_update(Odom& o, const std::vector<PtC>* in) {
         for (int it = 0; it < o.optimization_count; it++) {           // :252-272 / :727-747
             double ta = now_s();
             std::vector<Residual> res;
+            int qbase = 0;
             for (int c = 0; c < o.nc; ++c) {
-                if (o.plane[c]) add_plane_factors(o, c, ds[c], res);
-                else add_line_factors(o, c, ds[c], res);
+                if (o.plane[c]) add_plane_factors(o, c, ds[c], qbase, res);
+                else add_line_factors(o, c, ds[c], qbase, res);
+                qbase += (int)ds[c].size();
             }
             double tb = now_s();
             st.lm_iterations += solve_lm(o.params, res, (o.opts & PFREF_LM_NORMAL_EQ) != 0);
@@ -967,6 +1171,8 @@ void pfref_plane_fit(const double A[15], double n_out[3]) {
 }
 
 void pfref_se3_plus(const double x[7], const double delta[6], double out[7]) { se3_plus(x, delta, out); }
+void pfref_se3_plus_half(const double x[7], const double delta[6], double out[7]) { se3_plus_half(x, delta, out); }
+void pfref_det_sincos(double x, double* s, double* c) { det_sincos(x, s, c); }
 
 void pfref_rotation_polar(const double m[9], double out[9]) {
     M3 a;

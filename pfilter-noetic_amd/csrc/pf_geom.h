@@ -250,6 +250,42 @@ PF_HD m3 skew(d3 v) {
     return s;
 }
 
+// sin and cos of x from + - * and rint only (no libm, no FMA under -ffp-contract=off), so the host
+// and gfx950 produce the same bits: the oracle's GPU_EQUIV mode restates this function and follows
+// the device's SE(3) updates bit for bit over a whole sequence (libm's and the device library's
+// sin/cos differ in the last ulp now and then, and an ulp in the pose moves f32 map points).
+// Cody-Waite reduction by pi/2 in two 33-bit parts (exact products for |k| < 2^20), then the
+// classic fdlibm minimax kernels on [-pi/4, pi/4]; error <= 1 ulp there. Arguments beyond 2^19 pi
+// still give deterministic (if inexact) values; NaN and inf give NaN.
+PF_HD void det_sincos(double x, double* sn, double* cs) {
+    const double invpio2 = 6.36619772367581382433e-01;
+    const double pio2_1 = 1.57079632673412561417e+00;    // first 33 bits of pi/2
+    const double pio2_1t = 6.07710050650619224932e-11;   // pi/2 - pio2_1
+    const double k = rint(x * invpio2);
+    const double r = (x - k * pio2_1) - k * pio2_1t;
+    const double z = r * r;
+    const double v = z * r;
+    const double ps = 8.33333333332248946124e-03 +
+                      z * (-1.98412698298579493134e-04 +
+                           z * (2.75573137070700676789e-06 + z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
+    const double s = r + v * (-1.66666666666666324348e-01 + z * ps);
+    const double pc = z * (4.16666666666666019037e-02 +
+                           z * (-1.38888888888741095749e-03 +
+                                z * (2.48015872894767294178e-05 +
+                                     z * (-2.75573143513906633035e-07 +
+                                          z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double c = w + (((1.0 - w) - hz) + z * pc);
+    const long long n = (k == k && fabs(k) < 9.0e15) ? (long long)k : 0;
+    switch ((int)(n & 3)) {
+        case 0: *sn = s; *cs = c; break;
+        case 1: *sn = c; *cs = -s; break;
+        case 2: *sn = -s; *cs = -c; break;
+        default: *sn = -c; *cs = s; break;
+    }
+}
+
 // getTransformFromSe3 (src/lidarOptimization.cpp:106-143). One sincos of theta/2 serves all four
 // trigonometric terms: sin(theta) = 2 s c and 1 - cos(theta) = 2 s^2 (half-angle identities), and
 // theta^3 is a product where the source calls pow; each differs from the source's libm calls by at
@@ -262,7 +298,7 @@ PF_HD void se3_exp(const double* se3, qd& q, d3& t) {
     const double theta = nrm3(omega);
     const double half_theta = 0.5 * theta;
     double s_h, c_h;
-    sincos(half_theta, &s_h, &c_h);
+    det_sincos(half_theta, &s_h, &c_h);
     double imag_factor;
     const double real_factor = c_h;
     if (theta < 1e-10) {

@@ -50,6 +50,34 @@ def test_se3_plus_small_angle_branch(pfref):
     np.testing.assert_allclose(pfref.se3_plus(x, np.zeros(6)), x, atol=0)
 
 
+def test_det_sincos_accuracy(pfref):
+    """The deterministic sincos (GPU_EQUIV, pf_geom.h det_sincos) is within 2 ulp of libm over the
+    LM's range (half-angles up to pi) and stays close out to 1e4; NaN in gives NaN out."""
+    rng = np.random.default_rng(3)
+    xs = np.r_[0.0, 1e-300, 1e-12, 1e-6, np.pi / 4, np.pi / 2, np.pi, -np.pi / 3,
+               rng.uniform(0, np.pi, 2000), rng.uniform(-50, 50, 500), rng.uniform(-1e4, 1e4, 200)]
+    for x in xs:
+        s, c = pfref.det_sincos(x)
+        tol = 2 * np.spacing(1.0) if abs(x) <= np.pi else 1e-12 * max(1.0, abs(x))
+        assert abs(s - np.sin(x)) <= max(tol, 2 * np.spacing(abs(np.sin(x)))), x
+        assert abs(c - np.cos(x)) <= max(tol, 2 * np.spacing(abs(np.cos(x)))), x
+    assert pfref.det_sincos(0.0) == (0.0, 1.0)
+    s, c = pfref.det_sincos(float("nan"))
+    assert np.isnan(s) and np.isnan(c)
+
+
+def test_se3_plus_half_angle_matches_faithful(pfref):
+    """GPU_EQUIV's SE(3) update (one sincos of theta/2, half-angle identities) agrees with the
+    faithful getTransformFromSe3 to ~1e-15 relative: the two modes differ only in rounding."""
+    rng = np.random.default_rng(4)
+    for scale in (1e-11, 1e-6, 1e-3, 0.3, 2.0):
+        for _ in range(40):
+            x = np.r_[rand_quat(rng), rng.normal(size=3) * 50]
+            d = rng.normal(size=6) * scale
+            a, b = pfref.se3_plus_half(x, d), pfref.se3_plus(x, d)
+            assert np.all(np.abs(a - b) <= 1e-13 * (1 + np.abs(b))), (scale, a - b)
+
+
 def _fd_jac(f, x, eps=1e-7):
     J = np.zeros(6)
     for i in range(6):

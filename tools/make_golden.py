@@ -59,6 +59,43 @@ def odom_case():
     print("odom", out["gpu_equiv_poses"][-1])
 
 
+FULL_COUNTS = ("n_edge_in", "n_surf_in", "n_edge_ds", "n_surf_ds", "n_edge_map", "n_surf_map", "n_edge_res",
+               "n_surf_res", "n_edge_valid", "n_surf_valid")
+
+
+def odom_full_case(n=4541):
+    """configs[1] over the whole bench sequence (S64 seed 0, 4541 frames, bench.py's generator
+    call): the GPU_EQUIV trajectory, every frame's counts and the final maps' hashes. The GPU test
+    (tests/test_gpu_odom.py::test_full_sequence_bench_path) replays it through the bench's path."""
+    seq = pfsynth.Sequence("S64", n_frames=n, seed=0)
+    od = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=pfref.GPU_EQUIV)
+    poses = np.zeros((n, 7))
+    counts = np.zeros((n, len(FULL_COUNTS)), np.int32)
+    in_sha = []
+    for f0 in range(0, n, 256):
+        nf = min(256, n - f0)
+        buf, cnt = seq.frames(f0, nf, threads=8)
+        for i in range(nf):
+            k = f0 + i
+            x = buf[i, :cnt[i]]
+            if k % 500 == 0 or k == n - 1:
+                in_sha.append((k, sha(x)))
+            poses[k] = od.frame(x)
+            st = od.stats()
+            counts[k] = [st[c] for c in FULL_COUNTS]
+        print("frame", f0 + nf, poses[f0 + nf - 1][4:], flush=True)
+    ex, er = od.get_map(0)
+    sx, sr = od.get_map(1)
+    np.savez_compressed(os.path.join(OUT, "odom_s64_full.npz"), poses=poses, counts=counts,
+                        count_names=np.array(FULL_COUNTS), input_frames=np.array([k for k, _ in in_sha]),
+                        input_sha=np.array([h for _, h in in_sha]),
+                        map_sha=np.array([sha(ex), sha(er), sha(sx), sha(sr)]),
+                        map_sizes=np.array([ex.shape[0], sx.shape[0]]),
+                        spec=np.array(["S64", "n_frames=%d" % n, "seed=0", "lines=64", "3-90 m", "map 0.4",
+                                       "k_new 0", "theta_p 0.4", "theta_max 75", "weight 0", "opts=GPU_EQUIV"]))
+    print("odom_full", poses[-1], ex.shape, sx.shape)
+
+
 def knn_case():
     rng = np.random.default_rng(11)
     mp = np.zeros((3000, 4), np.float32)
