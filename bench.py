@@ -9,7 +9,9 @@ All scans are resident in HBM before the timed region. Per-frame poses stay on t
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1: one process per GPU (torch.distributed.run), one independent sequence per rank (weak
-scaling); RCCL all-gather of the per-rank pose arrays after the timed region.
+scaling); RCCL all-gather of the per-rank pose arrays after the timed region. Run as
+`python bench.py --gpus N` outside torch.distributed.run, the script launches the N ranks itself
+(torch.distributed.run as a child process, before anything touches the GPU) and exits with its code.
 
 Extra legs (rank 0, N=1 only, outside the timed region):
   roofline     exact 5-NN kernel on config 5 (2M-point map, 200k queries) timed with HIP events on
@@ -39,9 +41,11 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks). Without WORLD_SIZE in the environment and N > 1, the ranks are "
+                         "launched here; under torch.distributed.run it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=KITTI00_FRAMES - 20)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -55,13 +59,46 @@ def parse():
                     help="configs[4] kNN leg over the ranks: map broadcast once (RCCL), queries sharded")
     ap.add_argument("--concurrent", type=int, default=4,
                     help="kitti11: host threads per GPU, each driving its share of the sequences on its own "
-                         "handle and streams (at most the 8 live handles a device admits)")
+                         "handle and streams")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the rocprofv3 PMC passes that measure the kNN kernel's fabric traffic")
     ap.add_argument("--bpf-frames", type=int, default=1000,
                     help="frames of the Odom_BPF_EstimationClass leg (SURVEY §8(f) rank 1); 0 = skip")
     ap.add_argument("--host-leg", type=int, default=0,
                     help="also time N frames through pf_odom_frame_host (scan in host memory, PCIe copy "
                          "inside the timed region); reported as pcie_inclusive, never as value")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def resolve_world(args, env):
+    """(world, launch): the rank count and whether this process must launch the ranks itself.
+    Refuses a --gpus that disagrees with a torch.distributed.run world."""
+    env_world = env.get("WORLD_SIZE")
+    if env_world is not None:
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+        return world, False
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    return n, n > 1
+
+
+def launch_ranks(n, argv, port=None):
+    """Runs this script under torch.distributed.run with n ranks (a child process: nothing here has
+    touched the GPU) and returns its exit code."""
+    import socket
+    import subprocess
+    if port is None:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def lidar_cfg():
@@ -141,11 +178,13 @@ def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier)
     t0 = time.perf_counter()
     for k in range(warmup, len(ptrs)):
         od.frame_device(*ptrs[k])
-    od.sync()
+    od.sync()                      # raises on a sticky device error: a failed frame is never counted
     barrier()
     t1 = time.perf_counter()
     poses = od.poses()
     stats = od.stats()
+    if stats["errors"]:
+        raise RuntimeError("device error words 0x%x during the timed region" % stats["errors"])
     nframes = len(ptrs) - warmup
     return dict(elapsed=t1 - t0, frames=nframes, poses=poses, stats=stats, data=data_desc,
                 mean_points=float(np.mean(npts)) if npts else 0.0, od=od, bufs=bufs, ptrs=ptrs)
@@ -190,13 +229,19 @@ def run_kitti11(rank, local_rank, world, warmup, threads, use_graph, barrier, co
         shares[j].append(ptrs)
         loads[j] += len(ptrs)
 
+    errors = []
+
     def drive(od, items):          # ctypes releases the GIL inside every C call
-        for k, ptrs in enumerate(items):
-            if k:
-                od.reset()
-            for ptr, n in ptrs:
-                od.frame_device(ptr, n)
-        od.sync()
+        try:
+            for k, ptrs in enumerate(items):
+                if k:
+                    od.sync()          # raises on a sticky device error of the finished sequence
+                    od.reset()
+                for ptr, n in ptrs:
+                    od.frame_device(ptr, n)
+            od.sync()
+        except Exception as e:     # re-raised in the main thread: a failed frame is never counted
+            errors.append(repr(e))
 
     barrier()
     t0 = time.perf_counter()
@@ -207,6 +252,10 @@ def run_kitti11(rank, local_rank, world, warmup, threads, use_graph, barrier, co
         th.join()
     barrier()
     el = time.perf_counter() - t0
+    if errors:
+        raise RuntimeError("kitti11: device errors on rank %d: %s" % (rank, errors))
+    for od in handles:
+        assert od.stats()["errors"] == 0
     return dict(elapsed=el, frames=sum(len(p) for p, _ in seqs), sequences=["%02d" % sq for sq in mine])
 
 
@@ -269,7 +318,7 @@ def main_knn_shard(args, rank, local_rank, world, dist, barrier):
         dist.destroy_process_group()
 
 
-def knn_roofline(device=0, nmap=2_000_000, nq=200_000, iters=50):
+def knn_roofline(device=0, nmap=2_000_000, nq=200_000, iters=50, pmc=True):
     """Config 5: exact 5-NN of 200k jittered queries against a 2M-point dense map."""
     import pfilter_amd as pa
     import pfsynth
@@ -281,19 +330,59 @@ def knn_roofline(device=0, nmap=2_000_000, nq=200_000, iters=50):
     ms, alg = kn.bench(iters)
     achieved = alg / (ms * 1e-3) / 1e9
     found = int((idx[:, 4] >= 0).sum())
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "knn_pmc_r01.json")
-    if os.path.exists(pmc):
-        try:
-            with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "k_knn_query (exact radius-gated 5-NN, 1 m cell grid)",
-            "workload": "config 5: map %d pts, %d queries, %d with 5 neighbours" % (nmap, nq, found),
-            "alg_bytes_per_launch": alg, "avg_kernel_ms": round(ms, 5)}
+    out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+           "kernel": "k_knn_query (exact radius-gated 5-NN, 1 m cell grid)",
+           "workload": "config 5: map %d pts, %d queries, %d with 5 neighbours" % (nmap, nq, found),
+           "alg_bytes_per_launch": alg, "avg_kernel_ms": round(ms, 5)}
+    if pmc:
+        t = knn_pmc_traffic()
+        if t is not None:
+            out["traffic"] = t["bytes_per_launch"]
+            out["traffic_frac"] = round(t["bytes_per_launch"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            out["traffic_source"] = t["source"]
+    return out
+
+
+def knn_pmc_traffic(timeout_s=90):
+    """HBM (fabric) bytes per launch of k_knn_query, measured now: two rocprofv3 --pmc passes
+    (FETCH_SIZE, then WRITE_SIZE: they do not fit one pass) over tools/knn_probe.py as child processes.
+    MI355X_MICROARCH.md: FETCH_SIZE is doubled on gfx950 (128-B requests tallied at 64 B); WRITE_SIZE
+    is exact. None when rocprofv3 is unavailable or a pass fails (never a stale number)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return None
+    vals = {}
+    tmp = tempfile.mkdtemp(prefix="pf_pmc_")
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr)
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), "rocprofv3", "--pmc", ctr, "-d", d, "-o", "run",
+                   "--output-format", "csv", "--", sys.executable, os.path.join(ROOT, "tools", "knn_probe.py"),
+                   "--iters", "5"]
+            env = dict(os.environ, TMPDIR="/tmp")
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, cwd="/tmp")
+            if r.returncode != 0:
+                log("pmc pass %s failed (rc %d): %s" % (ctr, r.returncode, r.stderr[-400:]))
+                return None
+            xs = []
+            for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+                for row in csv.DictReader(open(f)):
+                    if "k_knn_query" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                        xs.append(float(row["Counter_Value"]))
+            if not xs:
+                return None
+            vals[ctr] = float(np.median(xs)) * 1024.0          # kB -> bytes, per launch
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    rd, wr = 2.0 * vals["FETCH_SIZE"], vals["WRITE_SIZE"]
+    return {"bytes_per_launch": round(rd + wr), "read": round(rd), "write": round(wr),
+            "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, measured in this run "
+                      "(tools/knn_probe.py, median over launches)"}
 
 
 def host_leg(device, nframes, threads):
@@ -447,9 +536,39 @@ def _cpu_baseline(budget_s, warmup):
         el += time.perf_counter() - t
         n += 1
         k += 1
-    return {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+    return {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port", "frames": [warmup, k],
             "sample": "pfref (oracle/, reference-faithful opts=0) frames %d..%d of the same S64 seed-0 sequence "
                       "after %d warm-up frames, single thread, %.1f s of CPU time" % (warmup, k - 1, warmup, el)}
+
+
+def gpu_window(device, f0, f1, threads, use_graph=True):
+    """The GPU pipeline timed over exactly frames [f0, f1) of S64 seed 0 (frames 0..f0-1 run untimed
+    first, as the CPU baseline's warm-up): the CPU baseline's own window, for a like-for-like ratio."""
+    import pfilter_amd as pa
+    od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
+    od.init(lidar_cfg(), **ODOM_CFG)
+    od.set_graph(use_graph)
+    bufs, ptrs = [], []
+    for _, buf, counts, _ in load_frames(0, f1, threads):
+        db = pa.DeviceBuffer(buf.nbytes, device=device)
+        db.upload(buf)
+        ptrs += [(db.ptr + i * buf.shape[1] * 16, int(counts[i])) for i in range(buf.shape[0])]
+        bufs.append(db)
+    for k in range(f0):
+        od.frame_device(*ptrs[k])
+    od.sync()
+    t0 = time.perf_counter()
+    for k in range(f0, f1):
+        od.frame_device(*ptrs[k])
+    od.sync()
+    el = time.perf_counter() - t0
+    return {"value": round((f1 - f0) / el, 2), "frames": [f0, f1]}
+
+
+def stub_run(rank, steps):
+    """Stand-in for run_gpu in the CPU test of the rank plumbing: rank r 'takes' 1 + r seconds."""
+    poses = np.tile(np.array([0, 0, 0, 1, rank, 0, 0], np.float64), (steps, 1))
+    return dict(elapsed=1.0 + rank, frames=steps, poses=poses, stats={}, data="stub", mean_points=0.0)
 
 
 def reduce_results(dist, elapsed, frames, poses, device):
@@ -473,17 +592,25 @@ def reduce_results(dist, elapsed, frames, poses, device):
     return float(t.item()), int(f.item()), poses_all
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    world, launch = resolve_world(args, os.environ)
+    if launch:                     # nothing has touched the GPU yet
+        sys.exit(launch_ranks(world, argv))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # PF_BENCH_BACKEND=gloo / PF_BENCH_STUB=1: the CPU test of the rank plumbing (tests/test_bench_dist.py)
+    backend = os.environ.get("PF_BENCH_BACKEND", "nccl")
+    stub = os.environ.get("PF_BENCH_STUB") == "1"
+    dev = "cuda" if backend == "nccl" else "cpu"
     dist = None
     if world > 1:
         import torch  # noqa: F401  (loaded before the HIP library: one HIP runtime per process)
         import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl", init_method="env://")
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        tdist.init_process_group(backend, init_method="env://")
         dist = tdist
 
     def barrier():
@@ -495,10 +622,13 @@ def main():
         return main_knn_shard(args, rank, local_rank, world, dist, barrier)
     if args.sequences == "kitti11":
         return main_kitti11(args, rank, local_rank, world, dist, barrier, threads)
-    r = run_gpu(rank, local_rank, world, args.steps, args.warmup, threads, not args.no_graph, barrier)
+    if stub:
+        r = stub_run(rank, args.steps)
+    else:
+        r = run_gpu(rank, local_rank, world, args.steps, args.warmup, threads, not args.no_graph, barrier)
     elapsed, frames = r["elapsed"], r["frames"]
     if dist is not None:
-        elapsed, total_frames, _ = reduce_results(dist, elapsed, frames, r["poses"][-frames:], "cuda")
+        elapsed, total_frames, _ = reduce_results(dist, elapsed, frames, r["poses"][-frames:], dev)
     else:
         total_frames = frames
     if rank != 0:
@@ -527,24 +657,32 @@ def main():
                    "graph": not args.no_graph},
     }
     log("pipeline: %d frames in %.3f s, last-frame stats %s" % (frames, elapsed, r["stats"]))
-    if world == 1 and not args.no_roofline:
+    if stub:
+        out["stub"] = True
+    elif world == 1 and not args.no_roofline:
         try:
-            out["roofline"] = knn_roofline(local_rank)
+            out["roofline"] = knn_roofline(local_rank, pmc=not args.no_pmc)
         except Exception as e:  # report, never hide
             log("roofline leg failed: %r" % (e,))
             out["roofline"] = None
-    if world == 1 and args.bpf_frames > 0:
+    if world == 1 and args.bpf_frames > 0 and not stub:
         try:
             out["bpf"] = bpf_leg(local_rank, args.bpf_frames, threads, with_cpu=not args.no_cpu,
                                  use_graph=not args.no_graph)
         except Exception as e:  # report, never hide
             log("bpf leg failed: %r" % (e,))
             out["bpf"] = None
-    if world == 1 and args.host_leg > 0:
+    if world == 1 and args.host_leg > 0 and not stub:
         out["pcie_inclusive"] = host_leg(local_rank, args.host_leg, threads)
-    if world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.warmup)
-        out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 2)
+    if world == 1 and not args.no_cpu and not stub:
+        cb = cpu_baseline(args.cpu_seconds, args.warmup)
+        f0, f1 = cb.pop("frames")
+        # the GPU on exactly the CPU sample's frames, for a like-for-like ratio
+        gw = gpu_window(local_rank, f0, f1, threads, not args.no_graph)
+        cb["gpu_same_frames"] = gw
+        cb["speedup_same_frames"] = round(gw["value"] / cb["value"], 2)
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu"] = round(value / cb["value"], 2)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -73,6 +73,12 @@ typedef struct {
     /* per map class (ES: 0 edge, 1 surf; BPF: 0 beam, 1 pillar, 2 facade); the n_edge_* / n_surf_*
      * fields above repeat classes 0 and 1 */
     int64_t n_in[3], n_ds[3], n_map[3], n_res[3], n_valid[3];
+    /* sticky device error words seen since create / reset (bit k set = word k was raised):
+     * 0 LM chunk wait gave up or corrupt p-index list, 1 featureExtraction sector above 4096 points
+     * dropped, 2 map grid above its cell capacity, 3 / 4 stage B / A sort look-back wait gave up,
+     * 5 BPF front end ground grid above its cell limit, 6 front end 1 m grid above its capacity */
+    int32_t errors;
+    int32_t pad_;
 } pf_odom_stats;
 
 /* ---------------- feature extraction (LaserProcessingClass) ---------------- */
@@ -90,9 +96,15 @@ int pf_fe_extract(pf_fe* h, const float* xyzi, size_t n, size_t stride_bytes, fl
 /* ---------------- odometry (Odom_ES_EstimationClass) ---------------- */
 typedef struct pf_odom pf_odom;
 /* max_points: largest raw scan / edge / surf input; map_capacity: largest local map (per map).
- * A device admits CUs / 32 live odometry handles (ES and BPF together; 8 on an MI355X): the LM solve
- * of every handle may be in flight at once and needs 32 co-resident workgroups. Beyond that,
- * pf_odom_create / pf_bpf_create return PF_EUNSUPPORTED. */
+ * Any number of handles may share a device (bounded by device memory): no kernel of the pipeline
+ * depends on its workgroups being co-resident with each other or with other handles' kernels.
+ *
+ * Device-side failures (a bounded wait that gave up, a featureExtraction sector above 4096 points,
+ * a map grid or front-end grid above capacity) latch sticky error words on the device. They are
+ * reported once, at the next call that waits for the handle's work (pf_odom_sync, pf_odom_poses,
+ * a frame / update call with pose_out, pf_odom_get_pose): PF_EHIP for a wait that gave up,
+ * PF_ECAPACITY for a capacity overflow (the outputs of those calls are still written).
+ * pf_odom_get_stats reports the words seen since create / reset in `errors`. */
 int pf_odom_create(const pf_lidar_params* lidar, const pf_odom_params* params, int device,
                    size_t max_points, size_t map_capacity, pf_odom** out);
 int pf_odom_destroy(pf_odom* h);
@@ -205,9 +217,9 @@ int pf_odom_frame_host(pf_odom* h, const float* xyzi, size_t n, size_t stride_by
 int pf_odom_sync(pf_odom* h);
 /* poses of frames processed so far, 7 doubles each */
 int pf_odom_poses(pf_odom* h, double* poses, size_t cap, size_t* n);
-/* compute units stage A (features / front end + VoxelGrid) stays off, so that stage B (the odometry,
- * whose LM needs 32 co-resident workgroups) starts while stage A runs. Defaults: 128 (ES), 32 (BPF);
- * 0 = unrestricted, which is better when several handles share one GPU. */
+/* compute units stage A (features / front end + VoxelGrid) stays off, so that stage B (the odometry)
+ * finds free CUs while stage A runs. Defaults: 128 (ES), 32 (BPF); 0 = unrestricted, which is better
+ * when several handles share one GPU. A reserve leaving stage A fewer than 32 CUs is PF_EINVAL. */
 int pf_odom_set_stage_a_reserve(pf_odom* h, int cus);
 /* enable/disable hipGraph replay of the steady-state frame (default on) */
 int pf_odom_set_graph(pf_odom* h, int enable);

@@ -49,14 +49,8 @@ struct pf_fe {
 struct pf_odom {
     OdomGPU o;
     std::vector<float4> host[kMaxC];
-    bool counted = false;
 };
 
-namespace {
-// live odometry handles per device (odom_max_handles: the LM solves' co-residency bound)
-std::mutex g_live_mu;
-std::map<int, int> g_live;
-}  // namespace
 
 extern "C" {
 
@@ -136,18 +130,8 @@ static int create(const pf_lidar_params* lidar, const pf_odom_params* params, in
     if (max_points == 0) max_points = 300000;
     if (map_capacity == 0) map_capacity = (size_t)1 << 22;
     PF_HIP_TRY(hipSetDevice(device));
-    {
-        std::lock_guard<std::mutex> lk(g_live_mu);
-        if (g_live[device] >= odom_max_handles(device)) return PF_EUNSUPPORTED;
-        ++g_live[device];
-    }
     pf_odom* h = new (std::nothrow) pf_odom();
-    if (!h) {
-        std::lock_guard<std::mutex> lk(g_live_mu);
-        --g_live[device];
-        return PF_ENOMEM;
-    }
-    h->counted = true;
+    if (!h) return PF_ENOMEM;
     int rc = odom_create(h->o, *lidar, *params, device, max_points, map_capacity, nc);
     if (rc != PF_OK) {
         pf_odom_destroy(h);
@@ -174,12 +158,7 @@ int pf_odom_destroy(pf_odom* h) {
     (void)hipSetDevice(h->o.device);
     (void)hipStreamSynchronize(h->o.stream_a);
     (void)hipStreamSynchronize(h->o.stream);
-    const int device = h->o.device;
     odom_destroy(h->o);
-    if (h->counted) {
-        std::lock_guard<std::mutex> lk(g_live_mu);
-        --g_live[device];
-    }
     delete h;
     return PF_OK;
 }
@@ -230,6 +209,25 @@ static int stage_inputs(pf_odom* h, int p, const float* const* cl, const size_t*
     return PF_OK;
 }
 
+// The handle's sticky error words (ErrWord, pf_odom.h), read on stage B's stream after the work
+// enqueued so far: any word set since the last report is reported once and cleared. A bounded
+// device wait that gave up (LM chunks, sort look-back) is PF_EHIP; a dropped sector, an overfull map
+// grid or a front-end grid limit is PF_ECAPACITY. `peek` reads without reporting (get_stats).
+static int sticky_status(OdomGPU& o, bool peek = false) {
+    int* e = o.h_cnt + C_COUNT;
+    PF_HIP_TRY(hipMemcpyAsync(e, o.errw, sizeof(int) * E_COUNT, hipMemcpyDeviceToHost, o.stream));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    int bits = 0;
+    for (int k = 0; k < E_COUNT; ++k)
+        if (e[k]) bits |= 1 << k;
+    o.err_seen |= bits;
+    if (!bits || peek) return PF_OK;
+    PF_HIP_TRY(hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    const int hip_bits = (1 << E_LM) | (1 << E_SORT_A) | (1 << E_SORT_B);
+    return (bits & hip_bits) ? PF_EHIP : PF_ECAPACITY;
+}
+
 static int read_pose(pf_odom* h, double pose[7]) {
     OdomGPU& o = h->o;
     if (o.frames == 0) {
@@ -241,7 +239,7 @@ static int read_pose(pf_odom* h, double pose[7]) {
     PF_HIP_TRY(hipMemcpyAsync(o.h_pose, o.poses + 7 * slot, sizeof(double) * 7, hipMemcpyDeviceToHost, o.stream));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     std::memcpy(pose, o.h_pose, sizeof(double) * 7);
-    return PF_OK;
+    return sticky_status(o);
 }
 
 static int frame_status(pf_odom* h) {
@@ -249,6 +247,7 @@ static int frame_status(pf_odom* h) {
     PF_HIP_TRY(hipMemcpyAsync(o.h_cnt, o.cnt, sizeof(int) * C_COUNT, hipMemcpyDeviceToHost, o.stream));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     PF_HIP_TRY(hipGetLastError());
+    if (int rc = sticky_status(o)) return rc;
     if (o.h_cnt[C_ERR]) return PF_EHIP;                  // a bounded device-side wait gave up
     if (!o.h_cnt[C_GATE]) return PF_W_MAP_TOO_SMALL;
     for (int c = 0; c < o.cls.nc; ++c)               // :428-431 / :574-577, BPF :875-878, :1188-1191
@@ -341,7 +340,10 @@ int pf_odom_get_map(pf_odom* h, int which, float* xyz, uint8_t* rg, size_t cap, 
     if (!xyz && !rg) return PF_OK;
     if (m > cap) return PF_ECAPACITY;
     std::vector<float4> tmp(m);
-    if (m) PF_HIP_TRY(hipMemcpy(tmp.data(), o.map[which], sizeof(float4) * m, hipMemcpyDeviceToHost));
+    if (m) {
+        PF_HIP_TRY(hipMemcpyAsync(tmp.data(), o.map[which], sizeof(float4) * m, hipMemcpyDeviceToHost, o.stream));
+        PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    }
     for (size_t i = 0; i < m; ++i) {
         if (xyz) { xyz[3 * i] = tmp[i].x; xyz[3 * i + 1] = tmp[i].y; xyz[3 * i + 2] = tmp[i].z; }
         if (rg) {
@@ -400,6 +402,8 @@ int pf_odom_get_stats(pf_odom* h, pf_odom_stats* s) {
     s->outer_iterations = c[C_OUTER];
     s->lm_iterations = c[C_LM_ITERS];
     s->map_too_small = c[C_GATE] ? 0 : 1;
+    if (int rc = sticky_status(o, true)) return rc;
+    s->errors = o.err_seen;
     return PF_OK;
 }
 
@@ -541,6 +545,8 @@ int pf_bpf_set_front_end(pf_odom* h, const pf_cls_params* p) {
             o.front = nullptr;
             return rc;
         }
+        o.front->sticky = o.errw + E_FRONT;                     // CC_ERR latches into the handle
+        alias_err(o.front->grid.err, o.errw + E_FRONT_GRID);
     }
     o.front->prm = *p;
     for (int s = 0; s < kSlots; ++s)        // parameters are baked into the captured kernels
@@ -562,16 +568,10 @@ int pf_bpf_frame_scan_device(pf_odom* h, const float* d_xyzi, size_t n, double p
     }
     int rc = enqueue_frame(h, reinterpret_cast<const float4*>(d_xyzi), n, nullptr, nullptr);
     if (rc) return rc;
-    if (!pose_out) return PF_OK;
-    rc = read_pose(h, pose_out);
-    if (rc < 0) return rc;
     // the front end's capacity flags (ground grid above its cell limit, U grid above its cell
-    // capacity: the frame ran with empty class clouds), checked where the caller waits anyway
-    int err = 0, gerr = 0;
-    PF_HIP_TRY(hipMemcpy(&err, h->o.front->cnt + CC_ERR, sizeof(int), hipMemcpyDeviceToHost));
-    PF_HIP_TRY(hipMemcpy(&gerr, h->o.front->grid.err, sizeof(int), hipMemcpyDeviceToHost));
-    if (gerr) (void)hipMemset(h->o.front->grid.err, 0, sizeof(int));
-    return err || gerr ? PF_ECAPACITY : rc;
+    // capacity: the frame ran with empty class clouds) are sticky error words, reported here
+    if (pose_out) return read_pose(h, pose_out);
+    return PF_OK;
 }
 
 int pf_odom_set_stage_a_reserve(pf_odom* h, int cus) {
@@ -587,7 +587,7 @@ int pf_odom_sync(pf_odom* h) {
     PF_HIP_TRY(hipStreamSynchronize(h->o.stream_a));
     PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
     PF_HIP_TRY(hipGetLastError());
-    return PF_OK;
+    return sticky_status(h->o);
 }
 
 int pf_odom_poses(pf_odom* h, double* poses, size_t cap, size_t* n) {
@@ -599,8 +599,11 @@ int pf_odom_poses(pf_odom* h, double* poses, size_t cap, size_t* n) {
     *n = f;
     if (!poses) return PF_OK;
     if (f > cap || f > o.pose_cap) return PF_ECAPACITY;
-    if (f) PF_HIP_TRY(hipMemcpy(poses, o.poses, sizeof(double) * 7 * f, hipMemcpyDeviceToHost));
-    return PF_OK;
+    if (f) {
+        PF_HIP_TRY(hipMemcpyAsync(poses, o.poses, sizeof(double) * 7 * f, hipMemcpyDeviceToHost, o.stream));
+        PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    }
+    return sticky_status(o);
 }
 
 // development probe (not part of include/pfilter_hip.h): device timestamps of the last LM solve

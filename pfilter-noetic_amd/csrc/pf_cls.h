@@ -55,6 +55,7 @@ struct ClsGPU {
     u32* nbr = nullptr;          // [cap * kClsMaxK] neighbour lists (U indices, ascending distance)
     GridGPU grid;
     PrimWork w;
+    int* sticky = nullptr;       // not owned: where CC_ERR is also latched (OdomGPU::errw)
 };
 
 int cls_alloc(ClsGPU& c, size_t cap);

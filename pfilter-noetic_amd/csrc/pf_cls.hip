@@ -32,10 +32,11 @@ struct ClsDev {          // kernel view of ClsGPU
     uint8_t* code;
     int* ptnum;
     float4* box;
+    int* sticky;         // optional: a sticky copy of CC_ERR (the odometry handle's error word)
 };
 ClsDev dev_view(ClsGPU& c) {
     return ClsDev{c.prm, c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals,
-                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.box};
+                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.box, c.sticky};
 }
 
 __device__ __forceinline__ float wave_minf(float v) {
@@ -107,6 +108,7 @@ __global__ void __launch_bounds__(256) k_gs_bounds(const float4* __restrict__ pt
         d.cnt[CC_NU] = 0; d.cnt[CC_NG] = 0;
         for (int k = 0; k < 4; ++k) d.cnt[CC_CLS + k] = 0;
         d.cnt[CC_ERR] = err;
+        if (err && d.sticky) *d.sticky = 1;
     }
     __syncthreads();
     const u32 fmax_ord = f2ord(FLT_MAX);

@@ -34,6 +34,21 @@ enum CounterSlot {
     C_GATE, C_ERR, C_OUTER, C_FE_ERR, C_COUNT
 };
 
+// Sticky device error words of a handle (OdomGPU::errw). Kernels set a word when a bounded wait gave
+// up or a capacity was exceeded; it stays set across frames until the host reports it (PF_EHIP for
+// E_LM / E_SORT_*, PF_ECAPACITY for the rest) at the next pf_odom_sync / poses / pose read, and
+// clears it. The feature, grid, sort and front-end flags of the sub-objects point into this array.
+enum ErrWord {
+    E_LM = 0,          // LM chunk wait gave up, or a p-index list was corrupt (C_ERR)
+    E_FE_SECTOR,       // featureExtraction: a sector above kSecCap points was dropped
+    E_GRID,            // map grid above its cell capacity: the frame's kNN saw an empty map
+    E_SORT_B,          // stage B sort / scan look-back wait gave up
+    E_SORT_A,          // stage A sort / scan look-back wait gave up
+    E_FRONT,           // BPF front end: ground grid above its cell limit (CC_ERR)
+    E_FRONT_GRID,      // BPF front end: U grid above its cell capacity
+    E_COUNT = 8
+};
+
 // ordered-uint accumulator slots (float min/max via atomics)
 enum AccSlot {
     A_VG = 0,                   // [class][6]: min xyz, max xyz
@@ -70,6 +85,7 @@ struct LMState {
 };
 
 constexpr int kLmParts = 30;   // cost, g[6], H[21], bad_r, bad_J
+constexpr int kLmEvalSlots = 8; // LM claim / done counter pairs per solve (>= evaluations per solve)
 
 // One slot of the two-stage frame pipeline: a frame's features and their voxel-grid output, with
 // the counters of that stage. Stage A (stream_a: featureExtraction + VoxelGrid, pose independent)
@@ -106,6 +122,8 @@ struct OdomGPU {
     LMState* lm = nullptr;
     int* cnt = nullptr;
     u32* acc = nullptr;
+    int* errw = nullptr;           // [E_COUNT] sticky error words (ErrWord)
+    int err_seen = 0;              // bits of the words reported since create / reset (pf_odom_stats)
     int* h_cnt = nullptr;          // pinned mirror
     double* h_pose = nullptr;      // pinned [7]
 
@@ -157,9 +175,8 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
                 size_t map_cap, int nc = 2);
 void odom_destroy(OdomGPU& o);
 int odom_reset(OdomGPU& o);
-// live handles a device admits: the LM solve of every handle may be in flight at once and each needs
-// kLmBlocks co-resident workgroups of one CU each (pf_odom.hip)
-int odom_max_handles(int device);
+// point a sub-object's error flag at a sticky error word (frees the flag's own allocation)
+void alias_err(int*& flag, int* word);
 // stage A: featureExtraction of d_in[0 .. sb[p].cnt[C_NIN]) into slot p's classes 0 / 1 (ES)
 void stage_enqueue_fe(OdomGPU& o, int p, const float4* d_in, hipStream_t s);
 // stage A: VoxelGrid of slot p's class clouds (counts sb[p].cnt[C_IN + c])

@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     const int nq = a.cnt[C_NQ];
     const int gate = a.st->gate;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        *a.lm_arrive = 0u;                                     // LM arrival counter of this iteration
+        for (int k = 0; k < 2 * kLmEvalSlots; ++k) a.lm_arrive[k] = 0u;   // LM claim / done counters
         a.cnt[C_NPAIR] = gate ? 5 * nq : 0;
         for (int c = 0; c < kMaxC; ++c) a.cnt[C_KEPT + c] = a.cnt[C_VALID + c] = 0;
     }
@@ -500,6 +500,7 @@ struct ObsArgs {
     int k_new;             // the edge and surf thresholds are equal (init :198-205, BPF :668-674)
     float theta_p;
     int theta_max;
+    int* err;              // sticky error word E_LM
 };
 
 template <int NC>
@@ -550,7 +551,7 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
                 more |= cur[j] >= 0;
             }
             if (!more) break;
-            if (step > 5 * nq) { a.cnt[C_ERR] = 1; break; }   // a list longer than every pair: corrupt
+            if (step > 5 * nq) { a.cnt[C_ERR] = 1; *a.err = 1; break; }   // a list longer than every pair: corrupt
         }
         int gs = 0;
 #pragma unroll
@@ -650,23 +651,27 @@ __device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, i
 }
 
 // ------------------------------------ LM (B.6) ----------------------------------------------
-// Ceres 1.14 trust-region loop of one outer iteration in ONE launch of kLmBlocks workgroups. Per
-// evaluation (<= 1 + kMaxIter = 5): every block evaluates a strided subset of the kept residual
-// blocks and reduces it to 30 partials (cost, g, upper J^T J, bad counts); lane 0 stores them and
-// arrives on a counter with an agent-scope release; every block waits for all arrivals (bounded
-// relaxed poll, one agent-scope acquire: cdna_hip_programming.md §6 G16), combines the partials in
-// block order and takes the LM step itself (TrustRegionMinimizer + LevenbergMarquardtStrategy).
-// The step is a deterministic function of identical inputs, so every block holds the same LM state
-// and no state is broadcast. 32 blocks of 256 threads are far below one wave per CU, so all blocks
-// are co-resident; a poll that exceeds its bound sets C_ERR and leaves (no hang). A block needs a
-// whole CU (374 VGPRs: one wave per SIMD), so co-residency holds while at most CUs / kLmBlocks
-// solves run at once on a device: the C ABI admits that many live handles per device (8 on MI355X).
+// Ceres 1.14 trust-region loop of one outer iteration in ONE launch. Per evaluation (<= 1 + kMaxIter
+// = 5) the kept residual blocks are split into kLmBlocks fixed *chunks* (chunk c = the queries
+// c * 256 + k * kLmBlocks * 256, k = 0, 1, ...); a running workgroup claims chunks from a per-
+// evaluation counter, reduces each to 30 partials (cost, g, upper J^T J, bad counts), stores them
+// write-through and counts the chunk done. Once all kLmBlocks chunks of the evaluation are done,
+// every workgroup combines the partials in chunk order and takes the LM step itself
+// (TrustRegionMinimizer + LevenbergMarquardtStrategy): the step is a deterministic function of
+// identical inputs, so every workgroup holds the same LM state and nothing is broadcast.
+// Forward progress does not depend on co-residency: a workgroup waits only for chunks that running
+// workgroups have claimed, and one that starts late claims what is left (or, once the evaluation is
+// complete, replays the steps from the stored partials). So any number of solves may be in flight
+// on a device. The reduction tree (chunk partials summed in chunk order) is independent of which
+// workgroup ran which chunk, so the result is bit-identical however the chunks were dealt out.
+// A wait that exceeds its bound (a bug, never expected) sets C_ERR and the sticky error word.
 #ifndef PF_LM_BLOCKS
 #define PF_LM_BLOCKS 32
 #endif
 constexpr int kLmBlocks = PF_LM_BLOCKS;
 constexpr int kLmEvals = 5;
 constexpr unsigned kLmSpinLimit = 1u << 21;
+constexpr unsigned kLmStealPolls = 64;      // polls (~1 us each) before a waiting block steals chunks
 
 // observeMean (:136-160) / pointSparsityMean (.h:111-126) of one element, given min/max
 __device__ __forceinline__ double norm_weight(double e, double mn, double mx, bool clamp) {
@@ -941,6 +946,7 @@ struct LmArgs {
     int4* pbkt;
     CloudsW map;
     u32 map_cap;
+    int* err;              // sticky error word E_LM
 };
 
 template <int NC>
@@ -995,13 +1001,23 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     // chunk rows p, p + 9, ...; 28 x 9 = 252 threads
     const int rk = t / 9, rp = t % 9;
     const int ri = rk >= 7 && rk < 28 ? hi_[rk - 7] : 0, rj_ = rk >= 7 && rk < 28 ? hj_[rk - 7] : 0;
-    for (int ev = 0; ev < kLmEvals; ++ev) {
-        if (lm.done || aborted) break;                           // uniform: every block steps alike
-        double x[7];
-        for (int k = 0; k < 7; ++k) x[k] = lm.cand[k];
-        if (t < 2) nbad[t] = 0;
+    // chunk c of an evaluation = the queries c * 256 + k * kLmBlocks * 256; block b first reduces its
+    // home chunk b and claims it with one atomicOr on the evaluation's claim mask, whose result is
+    // only needed when the partials are published (the atomic's latency hides behind the reduction).
+    // A block waiting for the evaluation to complete steals unclaimed chunks after kLmStealPolls
+    // polls: only chunks of workgroups that have not started yet stay unclaimed that long.
+    static_assert(kLmBlocks <= 32, "one claim-mask word per evaluation");
+    constexpr u32 kFull = kLmBlocks == 32 ? 0xFFFFFFFFu : ((1u << kLmBlocks) - 1u);
+    __shared__ int s_won, s_state, s_steal;
+    u32* claim = a.arrive;                                       // [kLmEvalSlots] claim masks
+    u32* done = a.arrive + kLmEvalSlots;                         // [kLmEvalSlots] chunks published
+    if (t < 2) nbad[t] = 0;
+    double x[7];
+    // reduce chunk ch of evaluation ev at x into 30 partials; publish them and count the chunk done
+    // unless another block claimed it first (own_claim: claim_old is this block's atomicOr result)
+    auto reduce_chunk = [&](int ch, int ev, u32 claim_old, bool own_claim) {
         double part = 0.0;
-        for (int base = blockIdx.x * 256; base < nq; base += gridDim.x * 256) {
+        for (int base = ch * 256; base < nq; base += kLmBlocks * 256) {
             const int q = base + t;
             double J[6] = {0, 0, 0, 0, 0, 0}, r = 0.0, hc = 0.0;
             if (q < nq && (a.qflag[q] & 2)) {
@@ -1064,44 +1080,79 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             }
             __syncthreads();
         }
-        if (rec) dbg[1 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
         if (rk < 28) red9[rk][rp] = part;
+        if (t == 0) s_won = own_claim ? ((claim_old >> ch) & 1u) == 0u : 1;
         __syncthreads();
-        double* P = a.part + (size_t)ev * kLmBlocks * 32;
         // publish: write-through (agent-scope atomic) stores of the 30 partials, drained by wave 0,
-        // then a relaxed arrival; consumers poll relaxed and read the partials with agent-scope
-        // atomic loads, so no release / acquire fence is needed (cdna_hip_programming.md §6 G16)
+        // then a relaxed done count; consumers poll relaxed and read the partials with agent-scope
+        // atomic loads, so no release / acquire fence is needed (cdna_hip_programming.md G16)
+        double* P = a.part + (size_t)ev * kLmBlocks * 32;
+        const bool pub = s_won != 0;
         if (t < 28) {
             double v = red9[t][0];
             for (int k = 1; k < 9; ++k) v += red9[t][k];
-            __hip_atomic_store(P + 32 * blockIdx.x + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (pub) __hip_atomic_store(P + 32 * ch + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else if (t < 30) {
-            __hip_atomic_store(P + 32 * blockIdx.x + t, (double)nbad[t - 28], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            if (pub) __hip_atomic_store(P + 32 * ch + t, (double)nbad[t - 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            nbad[t - 28] = 0;                                    // for the next chunk (after the barrier)
         }
-        if (rec) dbg[2 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
         if (t < 64) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (t == 0) __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == 0 && pub) __hip_atomic_fetch_add(&done[ev], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        __syncthreads();
+    };
+    for (int ev = 0; ev < kLmEvals; ++ev) {
+        if (lm.done || aborted) break;                           // uniform: every block steps alike
+        for (int k = 0; k < 7; ++k) x[k] = lm.cand[k];
+        const int home = blockIdx.x;                             // grid == kLmBlocks
+        u32 old = 0;
+        if (t == 0) old = __hip_atomic_fetch_or(&claim[ev], 1u << home, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        reduce_chunk(home, ev, old, true);
+        if (rec && ev == 0) dbg[1] = __builtin_amdgcn_s_memrealtime();
         if (ev == 0) pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
-        {
+        for (;;) {                                               // wait for all chunks; steal if starved
             if (t == 0) {
-                const u32 target = (u32)(ev + 1) * gridDim.x;
-                unsigned spins = 0;
-                while (__hip_atomic_load(a.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                    if (++spins > kLmSpinLimit) {
+                int st = 0;
+                unsigned polls = 0;
+                for (;;) {
+                    if (__hip_atomic_load(&done[ev], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (u32)kLmBlocks) {
+                        st = 1;
+                        break;
+                    }
+                    ++polls;
+                    if (polls > kLmStealPolls) {
+                        const u32 m = __hip_atomic_load(&claim[ev], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (m != kFull) {
+                            const int c = __ffs(~m & kFull) - 1;
+                            const u32 o2 = __hip_atomic_fetch_or(&claim[ev], 1u << c, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT);
+                            if (!((o2 >> c) & 1u)) {
+                                s_steal = c;
+                                st = 2;
+                                break;
+                            }
+                            continue;
+                        }
+                    }
+                    if (polls > kLmSpinLimit) {
                         aborted = 1;
                         a.cnt[C_ERR] = 1;
+                        *a.err = 1;
+                        st = 1;
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
+                s_state = st;
             }
+            __syncthreads();
+            if (s_state != 2) break;
+            reduce_chunk(s_steal, ev, 0u, false);
         }
-        __syncthreads();
         if (aborted) break;
         if (rec) dbg[3 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
+        const double* P = a.part + (size_t)ev * kLmBlocks * 32;
         if (t < kLmParts) {
             double pv[kLmBlocks];                                // all loads in flight, then the sum
 #pragma unroll
@@ -1371,24 +1422,33 @@ __global__ void k_init_counts(int* __restrict__ cnt, DevState* __restrict__ st, 
 
 // ==============================================================================================
 // (Re)create stage A's stream, restricted to all but the last `reserve` CUs (0: unrestricted).
+// A reserve that would leave stage A fewer than 32 CUs is PF_EINVAL. The new stream is created
+// before the old one is destroyed, so a failure leaves the handle's stage A stream valid. The masked
+// stream is a blocking stream (hipExtStreamCreateWithCUMask takes no flags), so the C ABI keeps every
+// copy stream-ordered on the handle's streams and never uses the null stream.
 int odom_stage_a_stream(OdomGPU& o, int reserve) {
-    if (o.stream_a) {
-        if (hipStreamSynchronize(o.stream_a) != hipSuccess) return PF_EHIP;
-        (void)hipStreamDestroy(o.stream_a);
-        o.stream_a = nullptr;
-    }
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, o.device) != hipSuccess) return PF_EHIP;
-    const int ncu = prop.multiProcessorCount;
-    o.cu_reserve = 0;
-    if (reserve > 0 && reserve <= ncu - 32) {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, o.device) != hipSuccess) return PF_EHIP;
+    if (reserve < 0 || (reserve > 0 && reserve > ncu - 32)) return PF_EINVAL;
+    if (o.stream_a && hipStreamSynchronize(o.stream_a) != hipSuccess) return PF_EHIP;
+    hipStream_t s = nullptr;
+    if (reserve > 0) {
         std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
         for (int c = 0; c < ncu - reserve; ++c) mask[c / 32] |= 1u << (c % 32);
-        if (hipExtStreamCreateWithCUMask(&o.stream_a, (uint32_t)mask.size(), mask.data()) != hipSuccess) return PF_EHIP;
-        o.cu_reserve = reserve;
-        return PF_OK;
+        if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) return PF_EHIP;
+    } else if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        return PF_EHIP;
     }
-    return hipStreamCreateWithFlags(&o.stream_a, hipStreamNonBlocking) == hipSuccess ? PF_OK : PF_EHIP;
+    if (o.stream_a) (void)hipStreamDestroy(o.stream_a);
+    o.stream_a = s;
+    o.cu_reserve = reserve;
+    // graphs were captured on the old stream's work; they are stream-independent, keep them
+    return PF_OK;
+}
+
+void alias_err(int*& flag, int* word) {
+    if (flag != word) (void)hipFree(flag);
+    flag = word;
 }
 
 int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& prm, int device, size_t in_cap,
@@ -1413,7 +1473,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     // kernels — the LM needs kLmBlocks co-resident workgroups — find free CUs while stage A runs
     int reserve = nc == 2 ? kStageAReserveES : kStageAReserveBPF;
     if (const char* e = std::getenv("PF_STAGE_A_CU_RESERVE")) reserve = std::atoi(e);   // development override
-    if (int rc0 = odom_stage_a_stream(o, reserve)) return rc0;
+    if (odom_stage_a_stream(o, reserve) != PF_OK && odom_stage_a_stream(o, 0) != PF_OK) return PF_EHIP;
     int rc = fe_alloc(o.fe, lidar, in_cap);
     if (rc) return rc;
     // 1 m cells over every map's bounding box: 3 x (201 m)^2 x 270 m covers the +-100 m crop box
@@ -1459,7 +1519,8 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.nbr, sizeof(int) * 5 * nq);
     PF_ALLOC(o.qflag, sizeof(int) * nq);
     PF_ALLOC(o.lm_part, sizeof(double) * kLmEvals * kLmBlocks * 32);
-    PF_ALLOC(o.lm_ticket, sizeof(u32) * 4);
+    PF_ALLOC(o.lm_ticket, sizeof(u32) * 2 * kLmEvalSlots);
+    PF_ALLOC(o.errw, sizeof(int) * E_COUNT);
     PF_ALLOC(o.geo, sizeof(double) * 8 * nq);
     PF_ALLOC(o.spars, sizeof(float) * nq);
     PF_ALLOC(o.roundv, sizeof(float) * nq);
@@ -1474,7 +1535,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
         if (hipMalloc(&o.dbg, sizeof(unsigned long long) * 64) != hipSuccess) return PF_ENOMEM;
         if (hipMemset(o.dbg, 0, sizeof(unsigned long long) * 64) != hipSuccess) return PF_EHIP;
     }
-    if (hipHostMalloc(&o.h_cnt, sizeof(int) * C_COUNT) != hipSuccess) return PF_ENOMEM;
+    if (hipHostMalloc(&o.h_cnt, sizeof(int) * (C_COUNT + E_COUNT)) != hipSuccess) return PF_ENOMEM;   // + errw mirror
     if (hipHostMalloc(&o.h_pose, sizeof(double) * 8) != hipSuccess) return PF_ENOMEM;
     // init (:182-208, BPF :649-681): identity odom / last_odom, parameters {0,0,0,1,0,0,0},
     // optimization_count 2
@@ -1487,17 +1548,17 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (hipMemset(o.acc, 0, sizeof(u32) * A_COUNT) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.acc_a, 0, sizeof(u32) * A_COUNT) != hipSuccess) return PF_EHIP;
     if (hipMemset(o.lm, 0, sizeof(LMState)) != hipSuccess) return PF_EHIP;
-    if (hipMemset(o.lm_ticket, 0, sizeof(u32) * 4) != hipSuccess) return PF_EHIP;
+    if (hipMemset(o.lm_ticket, 0, sizeof(u32) * 2 * kLmEvalSlots) != hipSuccess) return PF_EHIP;
+    if (hipMemset(o.errw, 0, sizeof(int) * E_COUNT) != hipSuccess) return PF_EHIP;
+    // the sub-objects' overflow / wait flags latch into the handle's sticky error words
+    alias_err(o.fe.err, o.errw + E_FE_SECTOR);
+    alias_err(o.grid.err, o.errw + E_GRID);
+    alias_err(o.prim.err, o.errw + E_SORT_B);
+    alias_err(o.vprim.err, o.errw + E_SORT_A);
     hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)nc * map_cap);   // all empty
     if (hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
     o.opt_count_host = 2;
     return PF_OK;
-}
-
-int odom_max_handles(int device) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 1;
-    return cus / kLmBlocks > 0 ? cus / kLmBlocks : 1;
 }
 
 // back to the state after init (identity pose, empty maps, optimization_count 2), keeping every
@@ -1513,7 +1574,8 @@ int odom_reset(OdomGPU& o) {
     if (hipMemsetAsync(o.acc, 0, sizeof(u32) * A_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.acc_a, 0, sizeof(u32) * A_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.lm, 0, sizeof(LMState), o.stream) != hipSuccess) return PF_EHIP;
-    if (hipMemsetAsync(o.lm_ticket, 0, sizeof(u32) * 4, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.lm_ticket, 0, sizeof(u32) * 2 * kLmEvalSlots, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     for (int p = 0; p < kSlots; ++p)
         if (hipMemsetAsync(o.sb[p].cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)o.cls.nc * o.map_cap);
@@ -1521,6 +1583,7 @@ int odom_reset(OdomGPU& o) {
     o.opt_count_host = 2;
     o.inited = false;
     o.frames = 0;
+    o.err_seen = 0;
     return PF_OK;
 }
 
@@ -1537,6 +1600,14 @@ void odom_destroy(OdomGPU& o) {
         }
         (void)hipFree(o.sb[p].cnt);
     }
+    // aliased flags point into errw (freed below), not at their own allocations
+    if (o.errw) {
+        o.fe.err = nullptr;
+        o.grid.err = nullptr;
+        o.prim.err = nullptr;
+        o.vprim.err = nullptr;
+        if (o.front) o.front->grid.err = nullptr;
+    }
     fe_free(o.fe);
     if (o.front) {
         cls_free(*o.front);
@@ -1551,7 +1622,7 @@ void odom_destroy(OdomGPU& o) {
     }
     void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.seg_out,
                     o.keys, o.vals, o.flags, o.scan_out, o.segstart, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
-                    o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg};
+                    o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg, o.errw};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
     if (o.h_pose) (void)hipHostFree(o.h_pose);
@@ -1622,10 +1693,12 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
                      o.roundv, o.pbkt, o.pnext, (u32)o.map_cap, o.lm_ticket};
         PF_LAUNCH_NC(nc, k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
         ObsArgs oa{cnt, o.acc, o.cls, clouds(o.map), clouds_w(sb.ds), o.nbr, o.qflag, o.pbkt, o.pnext, o.tailinc,
-                   (u32)o.map_cap, o.roundv, o.spars, o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
+                   (u32)o.map_cap, o.roundv, o.spars, o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max,
+                   o.errw + E_LM};
         PF_LAUNCH_NC(nc, k_observe, dim3(kGrid), dim3(256), 0, s, oa);
         LmArgs la{o.st, cnt, o.acc, o.cls, o.lm, o.lm_part, o.lm_ticket, o.qflag, clouds(sb.ds), o.geo, o.observe,
-                  o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.pbkt, clouds_w(o.map), (u32)o.map_cap};
+                  o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.pbkt, clouds_w(o.map), (u32)o.map_cap,
+                  o.errw + E_LM};
         PF_LAUNCH_NC(nc, k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
     }
     // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647, BPF :1197-1290)

@@ -58,7 +58,8 @@ class OdomStats(ctypes.Structure):
                                               "n_surf_map", "n_edge_res", "n_surf_res", "n_edge_valid",
                                               "n_surf_valid")] + \
                [(n, ctypes.c_int32) for n in ("outer_iterations", "lm_iterations", "map_too_small", "status")] + \
-               [(n, ctypes.c_int64 * 3) for n in ("n_in", "n_ds", "n_map", "n_res", "n_valid")]
+               [(n, ctypes.c_int64 * 3) for n in ("n_in", "n_ds", "n_map", "n_res", "n_valid")] + \
+               [("errors", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
     def as_dict(self):
         d = {}

@@ -90,3 +90,34 @@ def test_knn_shard_broadcast_and_bounds_gloo_world2():
     for rank in (0, 1):
         np.testing.assert_array_equal(np.array(res[rank][0]), np.arange(24, dtype=np.float32).reshape(6, 4))
     assert res[0][1] == (0, 100_000) and res[1][1] == (100_000, 200_000)
+
+
+def test_gpus_flag_launches_the_ranks():
+    """`python bench.py --gpus 2` outside torch.distributed.run launches 2 ranks itself (gloo and a
+    stubbed pipeline here): n_gpus 2, frames summed over ranks, time = the slowest rank's."""
+    import json
+    import subprocess
+    env = dict(os.environ, PF_BENCH_BACKEND="gloo", PF_BENCH_STUB="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "10",
+                        "--warmup", "0", "--no-cpu"], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["stub"]
+    assert abs(out["value"] - 20 / 2.0) < 1e-9           # 2 x 10 frames over the slower rank's 2 s
+
+
+def test_gpus_flag_must_match_world():
+    sys.path.insert(0, ROOT)
+    import bench
+    a = bench.parse(["--gpus", "4"])
+    assert bench.resolve_world(a, {}) == (4, True)
+    assert bench.resolve_world(a, {"WORLD_SIZE": "4"}) == (4, False)
+    assert bench.resolve_world(bench.parse([]), {"WORLD_SIZE": "2"}) == (2, False)
+    assert bench.resolve_world(bench.parse([]), {}) == (1, False)
+    import pytest
+    with pytest.raises(SystemExit):
+        bench.resolve_world(a, {"WORLD_SIZE": "2"})

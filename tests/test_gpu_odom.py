@@ -292,31 +292,72 @@ def test_reset_replays_like_a_fresh_handle(pa, pfsynth):
     assert od.poses().shape == (12, 7)
 
 
-def test_live_handle_limit_per_device(pa):
-    """A device admits CUs / 32 live handles (the LM solves' co-residency bound, pf_odom.hip)."""
-    import gc
-    gc.collect()                                    # handles of earlier tests
-    lid = pa.make_lidar(64, 3.0, 90.0)
-    made = []
-    rc = 0
-    for _ in range(64):
-        h = ctypes.c_void_p()
-        prm = pa.OdomParams(0.4, 0, 0.4, 75, 0)
-        rc = pa.lib().pf_odom_create(ctypes.byref(lid), ctypes.byref(prm), 0, 4096, 4096, ctypes.byref(h))
-        if rc != 0:
-            break
-        made.append(h.value)
-    try:
-        assert rc == pa.PF_EUNSUPPORTED
-        assert 1 <= len(made) <= 8                  # 256 CUs / 32 workgroups on an MI355X
-        pa.lib().pf_odom_destroy(made.pop())
-        h = ctypes.c_void_p()
-        prm = pa.OdomParams(0.4, 0, 0.4, 75, 0)
-        assert pa.lib().pf_bpf_create(ctypes.byref(lid), ctypes.byref(prm), 0, 4096, 4096, ctypes.byref(h)) == 0
-        made.append(h.value)
-    finally:
-        for h in made:
-            pa.lib().pf_odom_destroy(h)
+def _run_handle(pa, db, row_floats, counts, reserve=None):
+    od = pa.Odom_ES_EstimationClass(device=0)
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    if reserve is not None:
+        od.set_stage_a_reserve(reserve)
+    for i in range(len(counts)):
+        od.frame_device(db.ptr + i * row_floats * 4, counts[i])
+    od.sync()                                       # raises on any sticky device error
+    poses = od.poses()
+    assert od.stats()["errors"] == 0
+    return od, poses
+
+
+@pytest.mark.parametrize("reserve", [None, 0])
+def test_concurrent_handles_match_solo_runs(pa, pfsynth, reserve):
+    """configs[3] mode: 12 handles (one sequence each, own host thread, own streams) on one device at
+    once — more LM solves in flight than the CUs could hold as co-resident 32-workgroup grids, the
+    case that deadlocked before the LM claimed its chunks dynamically (pf_odom.hip k_lm_solve). Every
+    trajectory is bit-identical to the same sequence run alone; no sticky error word is raised.
+    reserve None = the default stage-A CU mask (128 CUs kept free), 0 = unrestricted."""
+    import threading
+    n_handles, n_frames = 12, 40
+    seqs = []
+    for s in range(n_handles):
+        seq = pfsynth.Sequence("S64", n_frames=n_frames, az_steps=900, seed=s)
+        buf, counts = seq.frames(0, n_frames)
+        db = pa.DeviceBuffer(buf.nbytes)
+        db.upload(buf)
+        seqs.append((db, buf.shape[1] * 4, counts))
+    solo = []
+    for db, row, counts in seqs:
+        od, p = _run_handle(pa, db, row, counts, reserve)
+        solo.append(p)
+        del od
+    out = [None] * n_handles
+    errs = []
+    start = threading.Barrier(n_handles)
+
+    def work(k):
+        try:
+            db, row, counts = seqs[k]
+            od = pa.Odom_ES_EstimationClass(device=0)
+            od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+            if reserve is not None:
+                od.set_stage_a_reserve(reserve)
+            start.wait()
+            for i in range(len(counts)):
+                od.frame_device(db.ptr + i * row * 4, counts[i])
+            od.sync()
+            out[k] = od.poses()
+            assert od.stats()["errors"] == 0
+            del od
+        except Exception as e:                      # reported below, in the main thread
+            errs.append((k, repr(e)))
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(n_handles)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a handle thread did not finish"
+    assert not errs, errs
+    for k in range(n_handles):
+        np.testing.assert_array_equal(out[k], solo[k], err_msg="handle %d" % k)
+    for db, _, _ in seqs:
+        db.free()
 
 
 def test_stage_a_reservation_does_not_change_results(pa, pfsynth):
