@@ -92,6 +92,12 @@ int pf_fe_destroy(pf_fe* h);
  * each output in points. */
 int pf_fe_extract(pf_fe* h, const float* xyzi, size_t n, size_t stride_bytes, float* edge_out,
                   size_t* n_edge, float* surf_out, size_t* n_surf, size_t cap);
+/* EXTENSION (not in the reference): a linear beam model for line counts the reference has no ring
+ * formula for (src/laserProcessingClass.cpp:58-61 puts every point of such a scan into ring 0):
+ * ring = int((top_deg - elevation_deg) * num_lines / (top_deg - bottom_deg)), points outside
+ * [0, num_lines) dropped. SURVEY 8(d) config 5 (synthetic 128-line scans, -25..+15 deg) runs with it.
+ * top_deg == bottom_deg == 0 restores the reference's formulas (the default). */
+int pf_fe_set_ring_model(pf_fe* h, double top_deg, double bottom_deg);
 
 /* ---------------- odometry (Odom_ES_EstimationClass) ---------------- */
 typedef struct pf_odom pf_odom;
@@ -221,6 +227,8 @@ int pf_odom_poses(pf_odom* h, double* poses, size_t cap, size_t* n);
  * finds free CUs while stage A runs. Defaults: 128 (ES), 32 (BPF); 0 = unrestricted, which is better
  * when several handles share one GPU. A reserve leaving stage A fewer than 32 CUs is PF_EINVAL. */
 int pf_odom_set_stage_a_reserve(pf_odom* h, int cus);
+/* the ring model extension of pf_fe_set_ring_model for the handle's featureExtraction */
+int pf_odom_set_ring_model(pf_odom* h, double top_deg, double bottom_deg);
 /* enable/disable hipGraph replay of the steady-state frame (default on) */
 int pf_odom_set_graph(pf_odom* h, int enable);
 

@@ -43,6 +43,9 @@ typedef struct {            /* lidar::Lidar fields read on the path (include/lid
     double min_distance;
     double max_distance;
     double scan_period;
+    /* EXTENSION (pf_fe_set_ring_model): ring_bottom < ring_top selects the linear beam model
+     * ring = int((ring_top - elevation) * num_lines / (ring_top - ring_bottom)); 0, 0 = reference */
+    double ring_top, ring_bottom;
 } pfref_lidar;
 
 typedef struct {            /* Odom_ES_EstimationClass::init arguments (include/odomEstimationClass.h:146) */
@@ -93,6 +96,8 @@ int pfref_voxel_grid(const float* pts, size_t n, float leaf, int opts, float* ou
 /* OdomBaseClass::rgbds (a15): same point layout. */
 int pfref_rgbds(const float* pts, size_t n, float leaf, int opts, float* out, size_t* n_out);
 /* exact kNN (d^2 in float accumulated x->y->z), ties by index. map/queries 4 floats/pt. */
+/* sum over queries of the map points in the 27 1 m cells around each query (SURVEY 8(d) |C(q)|) */
+unsigned long long pfref_knn_cellpop(const float* map, size_t m, const float* queries, size_t q);
 int pfref_knn(const float* map, size_t m, const float* queries, size_t q, int k, int opts,
               int32_t* idx_out, float* d2_out);
 /* 3x3 symmetric eigen (ascending). a = {a00,a01,a02,a11,a12,a22}. */

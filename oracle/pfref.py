@@ -31,7 +31,8 @@ def build(force=False):
 
 class Lidar(ctypes.Structure):
     _fields_ = [("num_lines", ctypes.c_int), ("min_distance", ctypes.c_double),
-                ("max_distance", ctypes.c_double), ("scan_period", ctypes.c_double)]
+                ("max_distance", ctypes.c_double), ("scan_period", ctypes.c_double),
+                ("ring_top", ctypes.c_double), ("ring_bottom", ctypes.c_double)]
 
 
 class OdomParams(ctypes.Structure):
@@ -89,6 +90,8 @@ def lib():
         L.pfref_voxel_grid.argtypes = [_vp, _sz, ctypes.c_float, ctypes.c_int, _vp, ctypes.POINTER(_sz)]
         L.pfref_rgbds.argtypes = [_vp, _sz, ctypes.c_float, ctypes.c_int, _vp, ctypes.POINTER(_sz)]
         L.pfref_knn.argtypes = [_vp, _sz, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp, _vp]
+        L.pfref_knn_cellpop.argtypes = [_vp, _sz, _vp, _sz]
+        L.pfref_knn_cellpop.restype = ctypes.c_ulonglong
         L.pfref_eigen_sym3.argtypes = [_vp, _vp, _vp]
         L.pfref_plane_fit.argtypes = [_vp, _vp]
         L.pfref_se3_plus.argtypes = [_vp, _vp, _vp]
@@ -136,8 +139,11 @@ def _f32(a, cols=4):
     return a
 
 
-def make_lidar(num_lines=64, min_distance=3.0, max_distance=90.0, scan_period=0.1):
-    return Lidar(int(num_lines), float(min_distance), float(max_distance), float(scan_period))
+def make_lidar(num_lines=64, min_distance=3.0, max_distance=90.0, scan_period=0.1, ring_model=None):
+    """ring_model=(top_deg, bottom_deg): the linear beam-model extension (S128)"""
+    top, bottom = ring_model if ring_model else (0.0, 0.0)
+    return Lidar(int(num_lines), float(min_distance), float(max_distance), float(scan_period), float(top),
+                 float(bottom))
 
 
 def feature_extraction(xyzi, lidar, opts=0):
@@ -183,6 +189,13 @@ def rgbds(pts, leaf, opts=0):
     n = _sz()
     lib().pfref_rgbds(p.ctypes.data, p.shape[0], float(leaf), int(opts), out.ctypes.data, ctypes.byref(n))
     return out[:n.value].copy()
+
+
+def knn_cellpop(map_pts, queries):
+    """sum over the queries of |C(q)| (map points in the 27 1 m cells around q)"""
+    m = _f32(map_pts)
+    q = _f32(queries)
+    return int(lib().pfref_knn_cellpop(m.ctypes.data, m.shape[0], q.ctypes.data, q.shape[0]))
 
 
 def knn(map_pts, queries, k=5, opts=0):

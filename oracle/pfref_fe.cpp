@@ -68,7 +68,11 @@ int ring_id(const pfref_lidar& lp, const PtI& p, bool sqrt_double) {
     if (distance < lp.min_distance || distance > lp.max_distance) return -1;
     double angle = std::atan(p.z / distance) * 180 / M_PI;
     int scanID = 0;
-    if (N_SCANS == 16) {
+    if (lp.ring_top > lp.ring_bottom) {    // extension: linear beam model (pf_fe_set_ring_model)
+        const double scale = (double)N_SCANS / (lp.ring_top - lp.ring_bottom);
+        scanID = int((lp.ring_top - angle) * scale);
+        if (!(lp.ring_top - angle >= 0.0) || scanID > N_SCANS - 1) return -1;
+    } else if (N_SCANS == 16) {
         scanID = int((angle + 15) / 2 + 0.5);
         if (scanID > (N_SCANS - 1) || scanID < 0) return -1;
     } else if (N_SCANS == 32) {
@@ -111,7 +115,7 @@ void feature_extraction(const pfref_lidar& lp, int opts, const PtI* in, size_t n
     for (size_t i = 0; i < n; i++) {
         int id = ring_id(lp, in[i], sqrt_double);
         if (id < 0) continue;
-        if (N_SCANS != 16 && N_SCANS != 32 && N_SCANS != 64 && !warned) {
+        if (N_SCANS != 16 && N_SCANS != 32 && N_SCANS != 64 && !(lp.ring_top > lp.ring_bottom) && !warned) {
             std::printf("wrong scan number\n");
             warned = true;
         }

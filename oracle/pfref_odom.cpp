@@ -8,6 +8,8 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <array>
+#include <map>
 #include <memory>
 
 namespace pfref {
@@ -1152,6 +1154,29 @@ int pfref_knn(const float* map, size_t m, const float* queries, size_t q, int k,
         for (int j = 0; j < k; ++j) { idx_out[i * k + j] = ind[j]; d2_out[i * k + j] = d2[j]; }
     }
     return 0;
+}
+
+// Sum over the queries of |C(q)|: the map points in the 3 x 3 x 3 block of 1 m cells (cell =
+// floor(p / 1 m)) around each query's cell, the set any exact 5-NN under the d^2 < 1 gate of
+// src/odomEstimationClass.cpp:299-300 / :447-451 must inspect (algorithmic bytes).
+unsigned long long pfref_knn_cellpop(const float* map, size_t m, const float* queries, size_t q) {
+    auto cell = [](const float* p) {
+        return std::array<long long, 3>{(long long)std::floor(p[0]), (long long)std::floor(p[1]),
+                                        (long long)std::floor(p[2])};
+    };
+    std::map<std::array<long long, 3>, unsigned long long> count;
+    for (size_t i = 0; i < m; ++i) ++count[cell(map + 4 * i)];
+    unsigned long long total = 0;
+    for (size_t i = 0; i < q; ++i) {
+        const auto c = cell(queries + 4 * i);
+        for (long long dz = -1; dz <= 1; ++dz)
+            for (long long dy = -1; dy <= 1; ++dy)
+                for (long long dx = -1; dx <= 1; ++dx) {
+                    const auto it = count.find({c[0] + dx, c[1] + dy, c[2] + dz});
+                    if (it != count.end()) total += it->second;
+                }
+    }
+    return total;
 }
 
 void pfref_eigen_sym3(const double a[6], double evals[3], double evecs[9]) {

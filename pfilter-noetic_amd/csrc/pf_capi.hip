@@ -120,6 +120,11 @@ int pf_fe_extract(pf_fe* h, const float* xyzi, size_t n, size_t stride_bytes, fl
     return PF_OK;
 }
 
+int pf_fe_set_ring_model(pf_fe* h, double top_deg, double bottom_deg) {
+    if (!h) return PF_EINVAL;
+    return fe_set_ring_model(h->fe, top_deg, bottom_deg);
+}
+
 // ------------------------------------------------------------------------------------------------
 static int create(const pf_lidar_params* lidar, const pf_odom_params* params, int device, size_t max_points,
                   size_t map_capacity, int nc, pf_odom** out) {
@@ -612,6 +617,21 @@ extern "C" int pf_dev_probe(pf_odom* h, unsigned long long* out, int n) {
     PF_HIP_TRY(hipSetDevice(h->o.device));
     PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
     PF_HIP_TRY(hipMemcpy(out, h->o.dbg, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
+    return PF_OK;
+}
+
+int pf_odom_set_ring_model(pf_odom* h, double top_deg, double bottom_deg) {
+    if (!h) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    const int rc = fe_set_ring_model(o.fe, top_deg, bottom_deg);
+    if (rc) return rc;
+    for (int s = 0; s < kSlots; ++s)        // the ring model is baked into the captured stage-A kernels
+        if (o.graph_a[s]) {
+            (void)hipGraphExecDestroy(o.graph_a[s]);
+            o.graph_a[s] = nullptr;
+        }
     return PF_OK;
 }
 

@@ -12,6 +12,9 @@ constexpr int kEdgePerSector = 20; // src/laserProcessingClass.cpp:121
 struct FeGPU {
     pf_lidar_params lidar{};
     int sqrt_double = 0;         // 0: sqrtf overload (default), 1: double sqrt
+    // ring model extension (pf_fe_set_ring_model): scale > 0 selects a linear beam model, ring =
+    // int((ring_top - elevation_deg) * ring_scale), for line counts the reference has no formula for
+    double ring_top = 0.0, ring_scale = 0.0;
     size_t cap = 0;              // max input points
     int nblk_cap = 0;            // ceil(cap / 256)
     int rings = 0;               // number of ring lists (num_lines)
@@ -29,6 +32,9 @@ struct FeGPU {
 };
 
 int fe_alloc(FeGPU& f, const pf_lidar_params& lidar, size_t cap);
+// linear beam model for L = num_lines rings between top_deg and bottom_deg (top > bottom), or the
+// reference's ring formulas again (top == bottom == 0); PF_EINVAL otherwise
+int fe_set_ring_model(FeGPU& f, double top_deg, double bottom_deg);
 void fe_free(FeGPU& f);
 // Enqueue feature extraction of *d_n device points (count read on the device). Outputs: edge/surf
 // float4 arrays with device counts d_ne / d_ns (capacity: edge >= rings*120, surf >= n).

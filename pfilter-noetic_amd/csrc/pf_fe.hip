@@ -16,13 +16,17 @@
 namespace pf {
 namespace {
 
-__device__ __forceinline__ int ring_of(const float4 p, int L, double mind, double maxd, int sqrt_double) {
+__device__ __forceinline__ int ring_of(const float4 p, int L, double mind, double maxd, int sqrt_double, double top,
+                                       double scale) {
     const float sq = p.x * p.x + p.y * p.y;   // float expression (:23)
     const double distance = sqrt_double ? sqrt((double)sq) : (double)sqrtf(sq);
     if (distance < mind || distance > maxd) return -1;
     const double angle = atan(p.z / distance) * 180 / M_PI;
     int scanID = 0;
-    if (L == 16) {
+    if (scale > 0.0) {                       // extension: linear beam model (pf_fe_set_ring_model)
+        scanID = int((top - angle) * scale);
+        if (!(top - angle >= 0.0) || scanID > L - 1) return -1;
+    } else if (L == 16) {
         scanID = int((angle + 15) / 2 + 0.5);
         if (scanID > (L - 1) || scanID < 0) return -1;
     } else if (L == 32) {
@@ -41,8 +45,8 @@ __device__ __forceinline__ int ring_of(const float4 p, int L, double mind, doubl
 }
 
 __global__ void __launch_bounds__(256) k_fe_ring(const float4* __restrict__ in, const int* __restrict__ d_n, int L,
-                                                  double mind, double maxd, int sqrt_double, int* __restrict__ ring,
-                                                  u32* __restrict__ blkhist) {
+                                                  double mind, double maxd, int sqrt_double, double top, double scale,
+                                                  int* __restrict__ ring, u32* __restrict__ blkhist) {
     __shared__ u32 h[kMaxRings];
     const int n = *d_n;
     const int nblk = n > 0 ? (n + 255) / 256 : 1;
@@ -52,7 +56,7 @@ __global__ void __launch_bounds__(256) k_fe_ring(const float4* __restrict__ in, 
     __syncthreads();
     const int i = blockIdx.x * 256 + t;
     if (i < n) {
-        const int r = ring_of(in[i], L, mind, maxd, sqrt_double);
+        const int r = ring_of(in[i], L, mind, maxd, sqrt_double, top, scale);
         ring[i] = r;
         if (r >= 0) atomicAdd(&h[r], 1u);
     }
@@ -341,6 +345,17 @@ int fe_alloc(FeGPU& f, const pf_lidar_params& lidar, size_t cap) {
     return PF_OK;
 }
 
+int fe_set_ring_model(FeGPU& f, double top_deg, double bottom_deg) {
+    if (top_deg == 0.0 && bottom_deg == 0.0) {
+        f.ring_top = f.ring_scale = 0.0;
+        return PF_OK;
+    }
+    if (!(top_deg > bottom_deg) || !(top_deg - bottom_deg <= 180.0)) return PF_EINVAL;
+    f.ring_top = top_deg;
+    f.ring_scale = (double)f.rings / (top_deg - bottom_deg);
+    return PF_OK;
+}
+
 void fe_free(FeGPU& f) {
     (void)hipFree(f.ring);
     (void)hipFree(f.blkhist);
@@ -359,7 +374,7 @@ void fe_enqueue(FeGPU& f, const float4* d_in, const int* d_n, float4* edge, int*
                 hipStream_t s) {
     const int L = f.rings;
     hipLaunchKernelGGL(k_fe_ring, dim3(f.nblk_cap), dim3(256), 0, s, d_in, d_n, L, f.lidar.min_dist, f.lidar.max_dist,
-                       f.sqrt_double, f.ring, f.blkhist);
+                       f.sqrt_double, f.ring_top, f.ring_scale, f.ring, f.blkhist);
     hipLaunchKernelGGL(k_fe_ring_scan, dim3(1), dim3(1024), 0, s, f.blkhist, L, d_n, f.ring_start);
     hipLaunchKernelGGL(k_fe_scatter, dim3(f.nblk_cap), dim3(256), 0, s, d_in, d_n, f.ring, f.blkhist, f.rp);
     hipLaunchKernelGGL(k_fe_sector, dim3(L * 6), dim3(256), 0, s, f.rp, f.ring_start, f.sec_edge_ids,

@@ -88,7 +88,8 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_bpf_create", "pf_bpf_init_map", "pf_bpf_update", "pf_bpf_frame_device", "pf_odom_classes",
            "pf_odom_reset", "pf_cls_default_params", "pf_cls_create", "pf_cls_destroy", "pf_cls_extract",
            "pf_cls_classify", "pf_cls_ground_seg", "pf_bpf_set_front_end", "pf_bpf_frame_scan_device", "pf_map_create", "pf_map_destroy", "pf_map_update",
-           "pf_map_update_device", "pf_map_update_mat", "pf_map_get", "pf_odom_set_stage_a_reserve"]
+           "pf_map_update_device", "pf_map_update_mat", "pf_map_get", "pf_odom_set_stage_a_reserve",
+           "pf_fe_set_ring_model", "pf_odom_set_ring_model"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -122,6 +123,8 @@ def lib():
     L.pf_odom_set_graph.argtypes = [_vp, _i]
     if hasattr(L, "pf_odom_set_stage_a_reserve"):
         L.pf_odom_set_stage_a_reserve.argtypes = [_vp, _i]
+    L.pf_fe_set_ring_model.argtypes = [_vp, ctypes.c_double, ctypes.c_double]
+    L.pf_odom_set_ring_model.argtypes = [_vp, ctypes.c_double, ctypes.c_double]
     L.pf_device_count.argtypes = [ctypes.POINTER(_i)]
     L.pf_dev_malloc.argtypes = [_i, _sz, ctypes.POINTER(_vp)]
     L.pf_dev_free.argtypes = [_i, _vp]
@@ -174,8 +177,12 @@ def _f32x4(a):
     return a
 
 
-def make_lidar(num_lines=64, min_dist=3.0, max_dist=90.0, scan_period=0.1):
-    return LidarParams(int(num_lines), float(min_dist), float(max_dist), float(scan_period))
+def make_lidar(num_lines=64, min_dist=3.0, max_dist=90.0, scan_period=0.1, ring_model=None):
+    """lidar::Lidar. ring_model=(top_deg, bottom_deg): the linear beam-model EXTENSION
+    (pf_fe_set_ring_model) for line counts the reference has no ring formula for (S128)."""
+    lp = LidarParams(int(num_lines), float(min_dist), float(max_dist), float(scan_period))
+    lp.ring_model = tuple(ring_model) if ring_model else None
+    return lp
 
 
 def device_count():
@@ -227,6 +234,9 @@ class LaserProcessingClass:
                                                   ctypes.byref(h)))
         self._h = h.value
         self._rings = lidar_param.num_lines
+        rm = getattr(lidar_param, "ring_model", None)
+        if rm:
+            _check("pf_fe_set_ring_model", lib().pf_fe_set_ring_model(self._h, float(rm[0]), float(rm[1])))
 
     def featureExtraction(self, pc_in):
         x = _f32x4(pc_in)
@@ -260,6 +270,9 @@ class Odom_ES_EstimationClass:
         _check("pf_odom_create", lib().pf_odom_create(ctypes.byref(lidar_param), ctypes.byref(prm), self.device,
                                                       self.max_points, self.map_capacity, ctypes.byref(h)))
         self._h = h.value
+        rm = getattr(lidar_param, "ring_model", None)
+        if rm:
+            _check("pf_odom_set_ring_model", lib().pf_odom_set_ring_model(self._h, float(rm[0]), float(rm[1])))
 
     def initMapWithPoints(self, edge_in, surf_in):
         e, s = _f32x4(edge_in), _f32x4(surf_in)

@@ -90,3 +90,37 @@ def test_matches_committed_fixture(pa, pfsynth, fe):
     cls, num = fe.classify(x[g["unground"]])
     np.testing.assert_array_equal(cls, g["cls"])
     np.testing.assert_array_equal(num, g["pt_num"])
+
+
+def _boundary_clouds(rng):
+    """Clouds that put the search's index math at its edges: points exactly on 1 m cell faces (the
+    query's cell at the grid's first / last x, y, z index, rows missing at the borders), a one-cell
+    grid, axis lines on integer coordinates, chunks cut by cell ends (sizes around multiples of 16)
+    and dense duplicates (d^2 ties)."""
+    out = []
+    for n in (1, 2, 15, 16, 17, 31, 33, 64, 65, 257, 1000, 4099):
+        out.append(rng.integers(-2, 3, (n, 3)).astype(np.float32))             # integer lattice: all on faces
+        out.append(rng.uniform(0.0, 0.999, (n, 3)).astype(np.float32))         # one cell
+    t = np.linspace(-3, 3, 601, dtype=np.float32)
+    z = np.zeros_like(t)
+    out.append(np.c_[t, z, z])                                                  # line along x through cell faces
+    out.append(np.c_[z, t, z + 1])                                              # along y
+    out.append(np.c_[z + 2, z - 1, t])                                          # along z
+    out.append(np.repeat(rng.uniform(-1, 1, (8, 3)), 40, 0).astype(np.float32))  # 8 points x 40 duplicates
+    g = np.stack(np.meshgrid(*[np.arange(-1.5, 1.51, 0.25)] * 3), -1).reshape(-1, 3).astype(np.float32)
+    out.append(g)                                                               # 13^3 grid, 0.25 m pitch
+    out.append(np.r_[g, g + np.float32(0.5)])
+    return out
+
+
+def test_search_index_edges_match_oracle(pa, pfref, fe):
+    """The radius k-NN search and PCA decision (k_cls_search / k_cls_decide) on clouds that stress
+    the cell-row, chunk and border index math, bit-exact against the oracle, k = 25 and k = 32."""
+    rng = np.random.default_rng(2024)
+    f32 = pa.BPFFrontEnd(max_points=300000, device=0, k=32, k_min=3)
+    for i, U in enumerate(_boundary_clouds(rng)):
+        for f, prm in ((fe, pfref.cls_params()), (f32, pfref.cls_params(k=32, k_min=3))):
+            cls, num = f.classify(U)
+            ocls, onum = pfref.pca_classify(U, prm)
+            np.testing.assert_array_equal(num, onum, err_msg="cloud %d (n=%d)" % (i, len(U)))
+            np.testing.assert_array_equal(cls, ocls, err_msg="cloud %d (n=%d)" % (i, len(U)))

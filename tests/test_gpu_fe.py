@@ -120,3 +120,27 @@ def test_fe_golden(pa, pfsynth):
     e, s = fe.featureExtraction(x)
     _same(e, g["edge"])
     _same(s, g["surf"])
+
+
+def test_fe_s128_linear_ring_model(pa, pfref, pfsynth):
+    """configs[4] scans (128 lines, -25..+15 deg) through the linear beam-model extension
+    (pf_fe_set_ring_model), bit-exact against the oracle with the same model. Without the model the
+    reference puts every point into ring 0 (src/laserProcessingClass.cpp:58-61): its six sectors of
+    ~33k points exceed the device's 4096-entry sector sort, which is reported (PF_EUNSUPPORTED),
+    never silently dropped."""
+    seq = pfsynth.Sequence("S128", n_frames=4)
+    x = seq.frame(3)
+    model = (15.0, -25.0)
+    fe = pa.LaserProcessingClass(device=0)
+    fe.init(pa.make_lidar(128, 3.0, 90.0, ring_model=model))
+    ge, gs = fe.featureExtraction(x)
+    re_, rs_ = pfref.feature_extraction(x, pfref.make_lidar(128, 3.0, 90.0, ring_model=model),
+                                        opts=pfref.FE_STABLE_TIES)
+    _same(ge, re_)
+    _same(gs, rs_)
+    assert ge.shape[0] > 128 * 6 * 5
+    fe0 = pa.LaserProcessingClass(device=0)
+    fe0.init(pa.make_lidar(128, 3.0, 90.0))
+    with pytest.raises(pa.PFError) as ei:
+        fe0.featureExtraction(x)
+    assert ei.value.code == pa.PF_EUNSUPPORTED

@@ -73,3 +73,27 @@ def test_knn_golden(pa):
     inside = g["d2"] < 1.0
     np.testing.assert_array_equal(np.where(inside, g["idx"], -1), gi)
     np.testing.assert_array_equal(gd[inside].view(np.uint32), g["d2"][inside].view(np.uint32))
+
+
+def test_knn_config5_full_size(pa, pfref, pfsynth):
+    """configs[4] at full size: the 2M-point dense map and the 200k jittered queries of the roofline
+    leg (bench.py knn_roofline), every gated idx / d^2 bit-exact against the oracle's kd-tree (itself
+    checked against brute force on every 100th query), and the kernel's algorithmic byte count built
+    from the GPU's own |C(q)| (k_knn_cellpop) equal to the oracle's count."""
+    mp = pfsynth.dense_map(2_000_000, seed=5)
+    q = pfsynth.dense_queries(mp, 200_000, sigma=0.3, seed=6)
+    kn = pa.Knn(mp.shape[0], q.shape[0])
+    kn.set_map(mp)
+    gi, gd = kn.query(q)
+    ri, rd = pfref.knn(mp, q, 5)                      # kd-tree
+    bi, bd = pfref.knn(mp, q[::100], 5, opts=pfref.KNN_BRUTE)
+    ins = bd < 1.0
+    np.testing.assert_array_equal(np.where(ins, bi, -1), np.where(ins, ri[::100], -1))
+    inside = rd < 1.0
+    np.testing.assert_array_equal(np.where(inside, ri, -1), gi)
+    np.testing.assert_array_equal(gd[inside].view(np.uint32), rd[inside].view(np.uint32))
+    assert np.all(np.isinf(gd[~inside]))
+    assert (gi[:, 4] >= 0).sum() == 181836
+    _, alg = kn.bench(1)
+    pop = pfref.knn_cellpop(mp, q)
+    assert alg == q.shape[0] * (16 + 40 + 27 * 8) + 16 * pop

@@ -384,3 +384,31 @@ def test_stage_a_reservation_does_not_change_results(pa, pfsynth):
         od = pa.Odom_ES_EstimationClass(device=0)
         od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
         od.set_stage_a_reserve(-1)
+
+
+def test_s128_odometry_with_2m_point_map(pa, pfref, pfsynth):
+    """configs[4] as a pipeline: synthetic 128-line scans (~200k points) through featureExtraction
+    with the linear beam-model extension (pf_odom_set_ring_model(15, -25): the reference has no
+    128-line ring formula) and updatePointsToMap against a 2,000,000-point surf
+    map seeded by pf_odom_set_map (voxel centroids of the dense synthetic block at the 0.8 m surf leaf,
+    a fixed point of rgbds). FLOAM parameters (theta_p 0) keep the map at its size. Poses within the
+    tolerance and every count identical per frame; both maps compared at the end."""
+    seq = pfsynth.Sequence("S128", n_frames=16)
+    od = pa.Odom_ES_EstimationClass(device=0)
+    od.init(pa.make_lidar(128, 3.0, 90.0, ring_model=(15.0, -25.0)), 0.4, 0, 0.0, 0, 0)
+    orc = pfref.Odom(pfref.make_lidar(128, 3.0, 90.0, ring_model=(15.0, -25.0)), 0.4, 0, 0.0, 0, 0,
+                     opts=pfref.GPU_EQUIV)
+    x = seq.frame(0)
+    assert x.shape[0] > 190000
+    od.frame_host(x)
+    orc.frame(x)
+    m = pfref.rgbds(pfsynth.dense_map(7_000_000, seed=5), 0.8)[:2_000_000, :3]
+    assert m.shape[0] == 2_000_000
+    rg = np.zeros((m.shape[0], 2), np.uint8)
+    od.set_map(1, m, rg)
+    orc.set_map(1, m, rg)
+    worst = _run(od, orc, seq, range(1, 13))
+    st = od.stats()
+    assert st["n_surf_map"] > 1_900_000 and st["n_surf_res"] > 500 and st["n_edge_res"] > 500
+    _compare_maps(od, orc)
+    assert worst[0] < TOL_T and worst[1] < TOL_R

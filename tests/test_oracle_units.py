@@ -254,3 +254,19 @@ def test_knn_kdtree_equals_brute_and_numpy(pfref):
     d2 = ((d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]).astype(np.float32)
     ref = np.lexsort((np.broadcast_to(np.arange(4000), d2.shape), d2), axis=1)[:, :5]
     np.testing.assert_array_equal(i_brute, ref)
+
+
+def test_knn_cellpop_matches_numpy(pfref):
+    """|C(q)| of SURVEY 8(d) (the algorithmic bytes' candidate set) against a numpy count."""
+    rng = np.random.default_rng(3)
+    mp = np.zeros((4000, 4), np.float32)
+    mp[:, :3] = rng.uniform(-6, 6, (4000, 3))
+    mp[:300, :3] = np.round(mp[:300, :3])                         # on cell faces
+    q = np.zeros((500, 4), np.float32)
+    q[:, :3] = rng.uniform(-8, 8, (500, 3))
+    cm = np.floor(mp[:, :3]).astype(np.int64)
+    cq = np.floor(q[:, :3]).astype(np.int64)
+    want = 0
+    for c in cq:
+        want += int(np.all(np.abs(cm - c) <= 1, axis=1).sum())
+    assert pfref.knn_cellpop(mp, q) == want

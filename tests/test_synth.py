@@ -45,3 +45,24 @@ def test_dense_map_and_queries(pfsynth):
     assert m.shape == (20000, 4) and q.shape == (1000, 4)
     np.testing.assert_array_equal(m, pfsynth.dense_map(20000, seed=5))
     assert np.isfinite(q).all()
+
+
+def test_s128_rings_round_trip_the_linear_model(pfsynth, pfref):
+    """the S128 generator's beams (15 - 40 (k + 0.5) / 128 deg) come back as
+    ring k through the linear beam-model extension (pf_fe_set_ring_model(15, -25)) evaluated as the
+    device and the oracle do (float x^2 + y^2, sqrtf, atan in double); and the oracle's feature
+    extraction with the model keeps every ring populated."""
+    s = pfsynth.Sequence("S128", n_frames=2)
+    x, ring = s.frame(1, with_ring=True)
+    assert x.shape[0] > 150000
+    sq = (x[:, 0] * x[:, 0] + x[:, 1] * x[:, 1]).astype(np.float32)
+    dist = np.sqrt(sq).astype(np.float32).astype(np.float64)
+    keep = (dist >= 3.0) & (dist <= 90.0)
+    angle = np.arctan(x[:, 2].astype(np.float64) / dist) * 180 / np.pi
+    sid = ((15.0 - angle) * (128 / 40.0)).astype(np.int64)
+    np.testing.assert_array_equal(sid[keep], ring[keep])
+    lid = pfref.make_lidar(128, 3.0, 90.0, ring_model=(15.0, -25.0))
+    e, su = pfref.feature_extraction(x, lid, opts=pfref.FE_STABLE_TIES)
+    assert e.shape[0] > 128 * 6 * 5 and su.shape[0] > 40000
+    e0, s0 = pfref.feature_extraction(x, pfref.make_lidar(128, 3.0, 90.0), opts=pfref.FE_STABLE_TIES)
+    assert e0.shape[0] <= 6 * 20                               # the reference: every point in ring 0
