@@ -227,6 +227,7 @@ static int sticky_status(OdomGPU& o, bool peek = false) {
         if (e[k]) bits |= 1 << k;
     o.err_seen |= bits;
     if (!bits || peek) return PF_OK;
+    for (int k = 0; k < E_COUNT; ++k) o.err_last[k] = e[k];
     PF_HIP_TRY(hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     const int hip_bits = (1 << E_LM) | (1 << E_SORT_A) | (1 << E_SORT_B);
@@ -632,6 +633,13 @@ int pf_odom_set_ring_model(pf_odom* h, double top_deg, double bottom_deg) {
             (void)hipGraphExecDestroy(o.graph_a[s]);
             o.graph_a[s] = nullptr;
         }
+    return PF_OK;
+}
+
+// development probe (not part of include/pfilter_hip.h): the sticky error words at their last report
+extern "C" int pf_dev_errors(pf_odom* h, int* out, int n) {
+    if (!h || !out || n <= 0 || n > E_COUNT) return PF_EINVAL;
+    for (int k = 0; k < n; ++k) out[k] = h->o.err_last[k];
     return PF_OK;
 }
 

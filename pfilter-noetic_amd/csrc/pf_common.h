@@ -74,4 +74,10 @@ __device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned n) {
 // map point packing: float4(x, y, z, bits(r | g << 8))
 __device__ __host__ __forceinline__ u32 pack_rg(u32 r, u32 g) { return (r & 255u) | ((g & 255u) << 8); }
 
+// Bounded device waits: a wait that has not completed after kWaitTicks of the 100 MHz real-time
+// counter (0.25 s, about 10^4 times the longest wait ever measured) gives up and latches a sticky
+// error word instead of hanging the queue.
+constexpr unsigned long long kWaitTicks = 25000000ull;
+__device__ __forceinline__ unsigned long long rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+
 }  // namespace pf

@@ -124,6 +124,7 @@ struct OdomGPU {
     u32* acc = nullptr;
     int* errw = nullptr;           // [E_COUNT] sticky error words (ErrWord)
     int err_seen = 0;              // bits of the words reported since create / reset (pf_odom_stats)
+    int err_last[E_COUNT] = {};    // values of the words at their last report (pf_dev_errors)
     int* h_cnt = nullptr;          // pinned mirror
     double* h_pose = nullptr;      // pinned [7]
 

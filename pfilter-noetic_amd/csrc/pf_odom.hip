@@ -551,7 +551,7 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
                 more |= cur[j] >= 0;
             }
             if (!more) break;
-            if (step > 5 * nq) { a.cnt[C_ERR] = 1; *a.err = 1; break; }   // a list longer than every pair: corrupt
+            if (step > 5 * nq) { a.cnt[C_ERR] = 1; atomicOr(a.err, 2); break; }   // a list longer than every pair: corrupt
         }
         int gs = 0;
 #pragma unroll
@@ -670,7 +670,6 @@ __device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, i
 #endif
 constexpr int kLmBlocks = PF_LM_BLOCKS;
 constexpr int kLmEvals = 5;
-constexpr unsigned kLmSpinLimit = 1u << 21;
 constexpr unsigned kLmStealPolls = 64;      // polls (~1 us each) before a waiting block steals chunks
 
 // observeMean (:136-160) / pointSparsityMean (.h:111-126) of one element, given min/max
@@ -1115,6 +1114,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             if (t == 0) {
                 int st = 0;
                 unsigned polls = 0;
+                const unsigned long long t0 = rt_now();
                 for (;;) {
                     if (__hip_atomic_load(&done[ev], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (u32)kLmBlocks) {
                         st = 1;
@@ -1135,10 +1135,10 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
                             continue;
                         }
                     }
-                    if (polls > kLmSpinLimit) {
+                    if (rt_now() - t0 > kWaitTicks) {
                         aborted = 1;
                         a.cnt[C_ERR] = 1;
-                        *a.err = 1;
+                        atomicOr(a.err, 1);
                         st = 1;
                         break;
                     }

@@ -16,7 +16,6 @@ __device__ __forceinline__ int eff_blocks(int n, int tile) {
 
 constexpr int kOsThreads = 256;
 constexpr int kOsPer = kSortTile / kOsThreads;   // 8 keys per thread per tile
-constexpr unsigned kSpinLimit = 1u << 22;
 
 __global__ void __launch_bounds__(256) k_os_hist(const u32* __restrict__ keys, const int* __restrict__ d_n, int passes,
                                                   u32* __restrict__ bhist, u32* __restrict__ dbase,
@@ -128,13 +127,15 @@ __global__ void __launch_bounds__(kOsThreads) k_os_pass(const u32* __restrict__ 
             if (tile > 0) {
                 __hip_atomic_store(mine, (1ull << 32) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 int j = tile - 1;
-                unsigned spins = 0;
+                unsigned long long t0 = 0;
                 for (;;) {
                     const u64 v = __hip_atomic_load(st + (size_t)j * 256 + t, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
                     const u32 tag = (u32)(v >> 32);
                     if (tag == 0) {
-                        if (++spins > kSpinLimit) { atomicOr(err, 1); break; }
+                        const unsigned long long now = rt_now();
+                        if (!t0) t0 = now;
+                        else if (now - t0 > kWaitTicks) { atomicOr(err, 1); break; }
                         __builtin_amdgcn_s_sleep(1);
                         continue;
                     }
@@ -172,7 +173,7 @@ __device__ u32 tile_lookback(u64* status, int tile, u32 agg, int* err) {
         __hip_atomic_store(&status[tile], (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     u32 excl = 0;
     int j = tile - 1;
-    unsigned spins = 0;
+    unsigned long long t0 = 0;
     while (j >= 0) {
         const int jj = j - l;
         const u64 sv = jj >= 0 ? __hip_atomic_load(&status[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -182,7 +183,9 @@ __device__ u32 tile_lookback(u64* status, int tile, u32 agg, int* err) {
         const int first = incl ? __ffsll((long long)incl) - 1 : 64;       // nearest inclusive prefix
         const u64 upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
         if (__ballot(tag == 0) & upto) {
-            if (++spins > kSpinLimit) { if (l == 0) atomicOr(err, 1); break; }
+            const unsigned long long now = rt_now();
+            if (!t0) t0 = now;
+            else if (now - t0 > kWaitTicks) { if (l == 0) atomicOr(err, 2); break; }
             __builtin_amdgcn_s_sleep(1);
             continue;
         }

@@ -164,6 +164,13 @@ def lib():
     return L
 
 
+def dev_errors(h):
+    """development: the sticky device error words of a handle at their last report (ErrWord order)"""
+    out = (ctypes.c_int * 8)()
+    lib().pf_dev_errors(ctypes.c_void_p(h), out, 8)
+    return list(out)
+
+
 def _check(fn, rc, allow_warn=True):
     if rc < 0 or (rc > 0 and not allow_warn):
         raise PFError(fn, rc)
@@ -341,7 +348,9 @@ class Odom_ES_EstimationClass:
         return pose if want_pose else None
 
     def sync(self):
-        _check("pf_odom_sync", lib().pf_odom_sync(self._h))
+        rc = lib().pf_odom_sync(self._h)
+        if rc < 0:
+            raise PFError("pf_odom_sync (device error words %s)" % dev_errors(self._h), rc)
 
     def poses(self):
         n = _sz()
