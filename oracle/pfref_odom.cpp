@@ -454,34 +454,36 @@ DevStep dev_try_step(const DevLm& lm) {                       // lm_try_step
     DevStep r;
     for (int j = 0; j < 6; ++j)
         r.D[j] = lm.reuse ? lm.D[j] : std::fmin(std::fmax(lm.scale[j] * lm.H[hup(j, j)] * lm.scale[j], 1e-6), 1e32);
+    // Hs + D / radius (D times the reciprocal radius), LDL^T with reciprocal pivots: the device's
+    // operation order (W_ij = L_ij d_j accumulated first, L_ij = W_ij / d_j as a product)
     double A[21];
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j <= i; ++j) A[tri(i, j)] = lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j];
-    for (int j = 0; j < 6; ++j) {
-        const double ld = std::sqrt(r.D[j] / lm.radius);
-        A[tri(j, j)] += ld * ld;
-    }
+    const double ir = 1.0 / lm.radius;
+    for (int j = 0; j < 6; ++j) A[tri(j, j)] += r.D[j] * ir;
+    double W[21], inv[6];
     bool ok = true;
-    for (int i = 0; i < 6; ++i)
-        for (int j = 0; j <= i; ++j) {
-            double s = A[tri(i, j)];
-            for (int k = 0; k < j; ++k) s -= A[tri(i, k)] * A[tri(j, k)];
-            if (i == j) {
-                ok = ok && (s > 0.0);
-                A[tri(i, i)] = std::sqrt(s);
-            } else {
-                A[tri(i, j)] = s / A[tri(j, j)];
-            }
-        }
     for (int i = 0; i < 6; ++i) {
+        for (int j = 0; j < i; ++j) {
+            double s = A[tri(i, j)];
+            for (int k = 0; k < j; ++k) s -= W[tri(i, k)] * A[tri(j, k)];
+            W[tri(i, j)] = s;
+            A[tri(i, j)] = s * inv[j];
+        }
+        double d = A[tri(i, i)];
+        for (int k = 0; k < i; ++k) d -= W[tri(i, k)] * A[tri(i, k)];
+        ok = ok && (d > 0.0);
+        inv[i] = 1.0 / d;
+    }
+    for (int i = 0; i < 6; ++i) {                               // L z = scale .* g
         double s = lm.scale[i] * lm.g[i];
         for (int k = 0; k < i; ++k) s -= A[tri(i, k)] * r.y[k];
-        r.y[i] = s / A[tri(i, i)];
+        r.y[i] = s;
     }
-    for (int i = 5; i >= 0; --i) {
-        double s = r.y[i];
+    for (int i = 5; i >= 0; --i) {                              // L^T y = D^-1 z
+        double s = r.y[i] * inv[i];
         for (int k = i + 1; k < 6; ++k) s -= A[tri(k, i)] * r.y[k];
-        r.y[i] = s / A[tri(i, i)];
+        r.y[i] = s;
     }
     for (int j = 0; j < 6; ++j) ok = ok && std::isfinite(r.y[j]);
     r.mcc = 0.0;

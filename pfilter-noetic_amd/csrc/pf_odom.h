@@ -85,7 +85,12 @@ struct LMState {
 };
 
 constexpr int kLmParts = 30;   // cost, g[6], H[21], bad_r, bad_J
-constexpr int kLmEvalSlots = 8; // LM claim / done counter pairs per solve (>= evaluations per solve)
+constexpr int kLmEvalSlots = 8; // LM claim masks per solve (>= evaluations per solve)
+constexpr int kLmEvals = 5;      // evaluations per solve: 1 + max_num_iterations (4)
+constexpr int kLmBlocks = 32;    // LM workgroups = residual chunks per evaluation
+// an LM partial not yet published (a NaN payload no arithmetic produces); k_assoc writes it over
+// every partial slot before each solve
+constexpr unsigned long long kPartSentinel = 0x7FF4C0DE5E47F00Dull;
 
 // One slot of the two-stage frame pipeline: a frame's features and their voxel-grid output, with
 // the counters of that stage. Stage A (stream_a: featureExtraction + VoxelGrid, pose independent)

@@ -340,6 +340,7 @@ struct AssocArgs {
     int* pnext;
     u32 map_cap;
     u32* lm_arrive;
+    double* lm_part;       // [kLmEvals][kLmBlocks][32] LM partials, reset to kPartSentinel here
 };
 
 // line fit (:302-331) / plane fit (:449-476), round and sparsity, p-index pair keys of query q
@@ -443,11 +444,13 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     const int nq = a.cnt[C_NQ];
     const int gate = a.st->gate;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        for (int k = 0; k < 2 * kLmEvalSlots; ++k) a.lm_arrive[k] = 0u;   // LM claim / done counters
+        for (int k = 0; k < kLmEvalSlots; ++k) a.lm_arrive[k] = 0u;       // LM claim masks
         a.cnt[C_NPAIR] = gate ? 5 * nq : 0;
         for (int c = 0; c < kMaxC; ++c) a.cnt[C_KEPT + c] = a.cnt[C_VALID + c] = 0;
     }
     if (blockIdx.x == 0 && threadIdx.x < 4 * kMaxC) a.acc[A_W + threadIdx.x] = (threadIdx.x & 1) ? 0u : 0xFFFFFFFFu;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < kLmEvals * kLmBlocks * 32; i += gridDim.x * blockDim.x)
+        reinterpret_cast<unsigned long long*>(a.lm_part)[i] = kPartSentinel;   // LM partials: none published
     if (!gate) {                                   // solve skipped: no association is valid
         for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) a.qflag[q] = 0;
         return;                                    // (no pairs: every block leaves before the prologue)
@@ -653,23 +656,18 @@ __device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, i
 // ------------------------------------ LM (B.6) ----------------------------------------------
 // Ceres 1.14 trust-region loop of one outer iteration in ONE launch. Per evaluation (<= 1 + kMaxIter
 // = 5) the kept residual blocks are split into kLmBlocks fixed *chunks* (chunk c = the queries
-// c * 256 + k * kLmBlocks * 256, k = 0, 1, ...); a running workgroup claims chunks from a per-
-// evaluation counter, reduces each to 30 partials (cost, g, upper J^T J, bad counts), stores them
-// write-through and counts the chunk done. Once all kLmBlocks chunks of the evaluation are done,
+// c * 256 + k * kLmBlocks * 256, k = 0, 1, ...); workgroup b reduces its home chunk b to 30 partials
+// (cost, g, upper J^T J, bad counts) and stores them write-through over sentinel values, so each
+// partial is its own completion flag. Once no partial of the evaluation is a sentinel any more,
 // every workgroup combines the partials in chunk order and takes the LM step itself
 // (TrustRegionMinimizer + LevenbergMarquardtStrategy): the step is a deterministic function of
 // identical inputs, so every workgroup holds the same LM state and nothing is broadcast.
-// Forward progress does not depend on co-residency: a workgroup waits only for chunks that running
-// workgroups have claimed, and one that starts late claims what is left (or, once the evaluation is
-// complete, replays the steps from the stored partials). So any number of solves may be in flight
+// Forward progress does not depend on co-residency: chunks are claimed on a per-evaluation mask, a
+// waiting workgroup claims and reduces the chunks nobody has claimed (home workgroups not started),
+// and one that starts late finds its chunk claimed and replays the steps from the stored partials. So any number of solves may be in flight
 // on a device. The reduction tree (chunk partials summed in chunk order) is independent of which
 // workgroup ran which chunk, so the result is bit-identical however the chunks were dealt out.
 // A wait that exceeds its bound (a bug, never expected) sets C_ERR and the sticky error word.
-#ifndef PF_LM_BLOCKS
-#define PF_LM_BLOCKS 32
-#endif
-constexpr int kLmBlocks = PF_LM_BLOCKS;
-constexpr int kLmEvals = 5;
 constexpr unsigned kLmStealPolls = 64;      // polls (~1 us each) before a waiting block steals chunks
 
 // observeMean (:136-160) / pointSparsityMean (.h:111-126) of one element, given min/max
@@ -722,8 +720,11 @@ __device__ __forceinline__ void core_store(const LmCore& c, LMState& s) {
 }
 
 // One attempt of LevenbergMarquardtStrategy::ComputeStep on the current state, without mutating it:
-// D (fresh from diag(Hs) unless reused), the packed-lower Cholesky of Hs + D / radius, the step y
-// (delta = -y .* scale) and the model cost change mcc. Hs entries are recomputed from H.
+// D (fresh from diag(Hs) unless reused), the LDL^T factorisation of Hs + D / radius (no square
+// roots; one reciprocal per pivot, multiplied in: 6 divisions on the serial chain instead of the
+// 27 of a Cholesky with divided substitutions), the step y (delta = -y .* scale) and the model cost
+// change mcc. Hs entries are recomputed from H. A pivot <= 0 rejects the step, as a Cholesky's
+// non-positive square-root argument does (both test positive definiteness).
 struct StepTry {
     double y[6], D[6], mcc;
     bool ok;
@@ -738,40 +739,41 @@ __device__ __forceinline__ StepTry lm_try_step(const LmCore& lm) {
     for (int i = 0; i < 6; ++i)
 #pragma unroll
         for (int j = 0; j <= i; ++j) A[tri(i, j)] = lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j];
+    const double ir = 1.0 / lm.radius;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        const double ld = sqrt(r.D[j] / lm.radius);
-        A[tri(j, j)] += ld * ld;
-    }
+    for (int j = 0; j < 6; ++j) A[tri(j, j)] += r.D[j] * ir;
+    // LDL^T in place: A[tri(i, j)] (j < i) becomes L_ij, W holds L_ij d_j, inv[j] = 1 / d_j
+    double W[21], inv[6];
     bool ok = true;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
 #pragma unroll
-        for (int j = 0; j <= i; ++j) {
+        for (int j = 0; j < i; ++j) {
             double s = A[tri(i, j)];
 #pragma unroll
-            for (int k = 0; k < j; ++k) s -= A[tri(i, k)] * A[tri(j, k)];
-            if (i == j) {
-                ok = ok && (s > 0.0);
-                A[tri(i, i)] = sqrt(s);
-            } else {
-                A[tri(i, j)] = s / A[tri(j, j)];
-            }
+            for (int k = 0; k < j; ++k) s -= W[tri(i, k)] * A[tri(j, k)];
+            W[tri(i, j)] = s;
+            A[tri(i, j)] = s * inv[j];
         }
+        double d = A[tri(i, i)];
+#pragma unroll
+        for (int k = 0; k < i; ++k) d -= W[tri(i, k)] * A[tri(i, k)];
+        ok = ok && (d > 0.0);
+        inv[i] = 1.0 / d;
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < 6; ++i) {                                // L z = scale .* g
         double s = lm.scale[i] * lm.g[i];
 #pragma unroll
         for (int k = 0; k < i; ++k) s -= A[tri(i, k)] * r.y[k];
-        r.y[i] = s / A[tri(i, i)];
+        r.y[i] = s;
     }
 #pragma unroll
-    for (int i = 5; i >= 0; --i) {
-        double s = r.y[i];
+    for (int i = 5; i >= 0; --i) {                               // L^T y = D^-1 z
+        double s = r.y[i] * inv[i];
 #pragma unroll
         for (int k = i + 1; k < 6; ++k) s -= A[tri(k, i)] * r.y[k];
-        r.y[i] = s / A[tri(i, i)];
+        r.y[i] = s;
     }
 #pragma unroll
     for (int j = 0; j < 6; ++j) ok = ok && isfinite(r.y[j]);
@@ -925,6 +927,14 @@ __device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot, unsigne
     else lm_next_step(lm, st, cand);
 }
 
+// the inputs of one residual block as the evaluation reads them
+struct ResIn {
+    d3 cur;
+    double G[6];
+    double wgt;
+    bool kept, plane;
+};
+
 struct LmArgs {
     DevState* st;
     int* cnt;
@@ -1003,15 +1013,38 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     // chunk c of an evaluation = the queries c * 256 + k * kLmBlocks * 256; block b first reduces its
     // home chunk b and claims it with one atomicOr on the evaluation's claim mask, whose result is
     // only needed when the partials are published (the atomic's latency hides behind the reduction).
-    // A block waiting for the evaluation to complete steals unclaimed chunks after kLmStealPolls
+    // A block waiting for the evaluation to complete claims unclaimed chunks after kLmStealPolls
     // polls: only chunks of workgroups that have not started yet stay unclaimed that long.
     static_assert(kLmBlocks <= 32, "one claim-mask word per evaluation");
     constexpr u32 kFull = kLmBlocks == 32 ? 0xFFFFFFFFu : ((1u << kLmBlocks) - 1u);
     __shared__ int s_won, s_state, s_steal;
     u32* claim = a.arrive;                                       // [kLmEvalSlots] claim masks
-    u32* done = a.arrive + kLmEvalSlots;                         // [kLmEvalSlots] chunks published
     if (t < 2) nbad[t] = 0;
     double x[7];
+    // one residual's inputs: the down-sampled point, the line (a, b) or plane (n, d) and the weight
+    auto load_res = [&](int q) {
+        ResIn in{};
+        if (q < nq && (a.qflag[q] & 2)) {
+            in.kept = true;
+            const int c = qi.cls(q);
+            in.plane = c == NC - 1;                              // the last class is the plane class
+            const float4 p = a.ds.at(c)[q - qi.start(c)];
+            in.cur = d3{(double)p.x, (double)p.y, (double)p.z};
+            if (wt != 0) {
+                const double wo = norm_weight((double)a.observe[q], sel3(c, wmin[0][0], wmin[1][0], wmin[2][0]),
+                                              sel3(c, wmax[0][0], wmax[1][0], wmax[2][0]), true);
+                const double ws = norm_weight((double)a.spars[q], sel3(c, wmin[0][1], wmin[1][1], wmin[2][1]),
+                                              sel3(c, wmax[0][1], wmax[1][1], wmax[2][1]), false);
+                if (wt == 1) in.wgt = wo;
+                else if (wt == 2) in.wgt = ws;
+                else in.wgt = in.plane ? (wo + ws) / 2 : (ws + wo) / 2;     // :418 / :565 operand order
+            }
+            const double* G = a.geo + 8 * (size_t)q;
+            for (int k = 0; k < 6; ++k) in.G[k] = G[k];
+        }
+        return in;
+    };
+    const ResIn mine = load_res((int)blockIdx.x * 256 + t);
     // reduce chunk ch of evaluation ev at x into 30 partials; publish them and count the chunk done
     // unless another block claimed it first (own_claim: claim_old is this block's atomicOr result)
     auto reduce_chunk = [&](int ch, int ev, u32 claim_old, bool own_claim) {
@@ -1019,24 +1052,14 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         for (int base = ch * 256; base < nq; base += kLmBlocks * 256) {
             const int q = base + t;
             double J[6] = {0, 0, 0, 0, 0, 0}, r = 0.0, hc = 0.0;
-            if (q < nq && (a.qflag[q] & 2)) {
-                const int c = qi.cls(q);
-                const bool plane = c == NC - 1;                  // the last class is the plane class
-                const float4 p = a.ds.at(c)[q - qi.start(c)];
-                const d3 cur{(double)p.x, (double)p.y, (double)p.z};
-                double wgt = 0.0;
-                if (wt != 0) {
-                    const double wo = norm_weight((double)a.observe[q], sel3(c, wmin[0][0], wmin[1][0], wmin[2][0]),
-                                                  sel3(c, wmax[0][0], wmax[1][0], wmax[2][0]), true);
-                    const double ws = norm_weight((double)a.spars[q], sel3(c, wmin[0][1], wmin[1][1], wmin[2][1]),
-                                                  sel3(c, wmax[0][1], wmax[1][1], wmax[2][1]), false);
-                    if (wt == 1) wgt = wo;
-                    else if (wt == 2) wgt = ws;
-                    else wgt = plane ? (wo + ws) / 2 : (ws + wo) / 2;     // :418 / :565 operand order
-                }
-                const double* G = a.geo + 8 * (size_t)q;
-                r = plane ? surf_eval(x, cur, d3{G[0], G[1], G[2]}, G[3], wgt, J)
-                          : edge_eval(x, cur, d3{G[0], G[1], G[2]}, d3{G[3], G[4], G[5]}, wgt, J);
+            // the inputs of this thread's residual: from registers for the home chunk's first rows
+            // (`mine`, loaded once per launch), from memory otherwise
+            const bool cached = ch == (int)blockIdx.x && base == ch * 256;
+            const ResIn in = cached ? mine : load_res(q);
+            if (in.kept) {
+                r = in.plane ? surf_eval(x, in.cur, d3{in.G[0], in.G[1], in.G[2]}, in.G[3], in.wgt, J)
+                             : edge_eval(x, in.cur, d3{in.G[0], in.G[1], in.G[2]}, d3{in.G[3], in.G[4], in.G[5]},
+                                         in.wgt, J);
                 bool jbad = false;
                 for (int k = 0; k < 6; ++k) jbad |= !isfinite(J[k]);
                 if (!isfinite(r)) {
@@ -1082,9 +1105,9 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         if (rk < 28) red9[rk][rp] = part;
         if (t == 0) s_won = own_claim ? ((claim_old >> ch) & 1u) == 0u : 1;
         __syncthreads();
-        // publish: write-through (agent-scope atomic) stores of the 30 partials, drained by wave 0,
-        // then a relaxed done count; consumers poll relaxed and read the partials with agent-scope
-        // atomic loads, so no release / acquire fence is needed (cdna_hip_programming.md G16)
+        // publish: write-through (agent-scope atomic) stores of the 30 partials over the sentinels
+        // k_assoc left there; each value is its own completion flag, so nothing waits for the stores
+        // and no counter is bumped (consumers poll the values with agent-scope atomic loads)
         double* P = a.part + (size_t)ev * kLmBlocks * 32;
         const bool pub = s_won != 0;
         if (t < 28) {
@@ -1095,10 +1118,6 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             if (pub) __hip_atomic_store(P + 32 * ch + t, (double)nbad[t - 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             nbad[t - 28] = 0;                                    // for the next chunk (after the barrier)
         }
-        if (t < 64) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (t == 0 && pub) __hip_atomic_fetch_add(&done[ev], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
         __syncthreads();
     };
     for (int ev = 0; ev < kLmEvals; ++ev) {
@@ -1108,56 +1127,52 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         u32 old = 0;
         if (t == 0) old = __hip_atomic_fetch_or(&claim[ev], 1u << home, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         reduce_chunk(home, ev, old, true);
-        if (rec && ev == 0) dbg[1] = __builtin_amdgcn_s_memrealtime();
+        if (rec) dbg[1 + 4 * ev] = dbg[2 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
         if (ev == 0) pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
-        for (;;) {                                               // wait for all chunks; steal if starved
+        // wait until no partial of this evaluation is the sentinel any more (threads t < 30 poll
+        // their product over the 32 chunks); after kLmStealPolls rounds, claim and reduce chunks
+        // nobody has claimed (their home workgroups have not started)
+        const double* P = a.part + (size_t)ev * kLmBlocks * 32;
+        const unsigned long long t0 = rt_now();
+        double pv[kLmBlocks];
+        for (unsigned polls = 0;; ++polls) {
+            bool ok = true;
+            if (t < kLmParts) {
+#pragma unroll
+                for (int b = 0; b < kLmBlocks; ++b)
+                    pv[b] = __hip_atomic_load(P + 32 * b + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int b = 0; b < kLmBlocks; ++b) ok = ok && __double_as_longlong(pv[b]) != (long long)kPartSentinel;
+            }
+            if (__syncthreads_and(ok)) break;
             if (t == 0) {
-                int st = 0;
-                unsigned polls = 0;
-                const unsigned long long t0 = rt_now();
-                for (;;) {
-                    if (__hip_atomic_load(&done[ev], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (u32)kLmBlocks) {
-                        st = 1;
-                        break;
-                    }
-                    ++polls;
-                    if (polls > kLmStealPolls) {
-                        const u32 m = __hip_atomic_load(&claim[ev], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (m != kFull) {
-                            const int c = __ffs(~m & kFull) - 1;
-                            const u32 o2 = __hip_atomic_fetch_or(&claim[ev], 1u << c, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT);
-                            if (!((o2 >> c) & 1u)) {
-                                s_steal = c;
-                                st = 2;
-                                break;
-                            }
-                            continue;
+                s_state = 0;
+                if (polls >= kLmStealPolls) {
+                    const u32 m = __hip_atomic_load(&claim[ev], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (m != kFull) {
+                        const int c = __ffs(~m & kFull) - 1;
+                        const u32 o2 = __hip_atomic_fetch_or(&claim[ev], 1u << c, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+                        if (!((o2 >> c) & 1u)) {
+                            s_steal = c;
+                            s_state = 2;
                         }
                     }
-                    if (rt_now() - t0 > kWaitTicks) {
-                        aborted = 1;
-                        a.cnt[C_ERR] = 1;
-                        atomicOr(a.err, 1);
-                        st = 1;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
                 }
-                s_state = st;
+                if (s_state == 0 && rt_now() - t0 > kWaitTicks) {
+                    aborted = 1;
+                    a.cnt[C_ERR] = 1;
+                    atomicOr(a.err, 1);
+                }
             }
             __syncthreads();
-            if (s_state != 2) break;
-            reduce_chunk(s_steal, ev, 0u, false);
+            if (aborted) break;
+            if (s_state == 2) reduce_chunk(s_steal, ev, 0u, false);
+            else __builtin_amdgcn_s_sleep(1);
         }
         if (aborted) break;
         if (rec) dbg[3 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
-        const double* P = a.part + (size_t)ev * kLmBlocks * 32;
         if (t < kLmParts) {
-            double pv[kLmBlocks];                                // all loads in flight, then the sum
-#pragma unroll
-            for (int b = 0; b < kLmBlocks; ++b)
-                pv[b] = __hip_atomic_load(P + 32 * b + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             double v = 0.0;
 #pragma unroll
             for (int b = 0; b < kLmBlocks; ++b) v += pv[b];
@@ -1690,7 +1705,7 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
         AssocArgs aa{o.st, cnt, o.acc, gv, o.cls, clouds(sb.ds), clouds(o.map), o.nbr, o.qflag, o.geo, o.spars,
-                     o.roundv, o.pbkt, o.pnext, (u32)o.map_cap, o.lm_ticket};
+                     o.roundv, o.pbkt, o.pnext, (u32)o.map_cap, o.lm_ticket, o.lm_part};
         PF_LAUNCH_NC(nc, k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
         ObsArgs oa{cnt, o.acc, o.cls, clouds(o.map), clouds_w(sb.ds), o.nbr, o.qflag, o.pbkt, o.pnext, o.tailinc,
                    (u32)o.map_cap, o.roundv, o.spars, o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max,
