@@ -6,7 +6,8 @@
 namespace pf {
 
 constexpr int kMaxRings = 128;
-constexpr int kSecCap = 4096;      // max curvature entries per sector (KITTI-64: ~330)
+constexpr int kSecLds = 2048;      // sectors up to this many curvature entries sort in LDS (KITTI-64: ~330);
+                                   // larger ones (any size) sort in global scratch
 constexpr int kEdgePerSector = 20; // src/laserProcessingClass.cpp:121
 
 struct FeGPU {
@@ -24,10 +25,13 @@ struct FeGPU {
     int* ring_start = nullptr;   // [kMaxRings + 1]
     float4* rp = nullptr;        // [cap] ring-ordered points
     int* sec_edge_ids = nullptr; // [rings*6*20]
-    int* sec_surf_ids = nullptr; // [rings*6*kSecCap]
+    int* sec_surf_ids = nullptr; // [cap]  surf ids of the sector starting at ring point base + cs, from there
+    double* big_val = nullptr;   // [2 cap] sort scratch of sectors above kSecLds entries
+    int* big_id = nullptr;       // [2 cap]
+    unsigned char* big_picked = nullptr, *big_gap = nullptr;   // [2 cap]
     int* sec_cnt = nullptr;      // [rings*6*2]  edge, surf counts
     int* sec_off = nullptr;      // [rings*6*2]  output offsets
-    int* err = nullptr;          // [1] sector overflow flag
+    int* err = nullptr;          // [1] error flag (unused since sectors of any size are handled; kept for the ABI)
     float4* d_in_stage = nullptr;// [cap] staging for host inputs
 };
 

@@ -74,46 +74,69 @@ __device__ __forceinline__ u32 wave_incl_scan_u32(u32 v) {
     return v;
 }
 
-// Exclusive scan of data[0..total) in place by one 1024-thread workgroup: each wave owns a
-// contiguous chunk read 64 entries at a time (coalesced). on_entry(e, prefix) sees every entry.
+// Exclusive scan of data[0..total) in place by one 1024-thread workgroup, in LDS chunks of
+// kScanChunk entries: a chunk is loaded with every load in flight (entry t + 1024 i on thread t),
+// each thread sums its 16 contiguous LDS entries, the 1024 sums are scanned across the waves, and
+// the prefixes are written back coalesced. on_entry(e, prefix) sees every entry.
+constexpr int kScanChunk = 16384;
+__device__ __forceinline__ int scan_pad(int e) { return e + (e >> 4); }   // +1 word per 16: no bank conflicts
 template <typename F>
-__device__ __forceinline__ u32 block1024_scan_inplace(u32* data, int total, u32* lw, F on_entry) {
+__device__ __forceinline__ u32 block1024_scan_inplace(u32* data, int total, u32* buf, u32* lw, F on_entry) {
     const int t = threadIdx.x, w = t >> 6, l = lane_id();
-    int chunk = (total + 15) / 16;
-    chunk = (chunk + 63) & ~63;
-    const int c0 = w * chunk;
-    const int c1 = min(total, c0 + chunk);
-    u32 s = 0;
-    for (int e = c0 + l; e < c1; e += 64) s += data[e];
+    constexpr int kPer = kScanChunk / 1024;
+    u32 carry = 0;
+    for (int c0 = 0; c0 < total; c0 += kScanChunk) {
+        const int n = min(kScanChunk, total - c0);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (l == 0) lw[w] = s;
-    __syncthreads();
-    u32 run = 0, tot = 0;
-    for (int k = 0; k < 16; ++k) {
-        if (k < w) run += lw[k];
-        tot += lw[k];
-    }
-    for (int base = c0; base < c1; base += 64) {
-        const int e = base + l;
-        const u32 v = e < c1 ? data[e] : 0u;
-        const u32 inc = wave_incl_scan_u32(v);
-        if (e < c1) {
-            data[e] = run + inc - v;
-            on_entry(e, run + inc - v);
+        for (int i = 0; i < kPer; ++i) {
+            const int e = t + 1024 * i;
+            buf[scan_pad(e)] = e < n ? data[c0 + e] : 0u;
         }
-        run += __shfl(inc, 63, 64);
+        __syncthreads();
+        u32 v[kPer], s = 0;
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            v[i] = buf[scan_pad(kPer * t + i)];
+            s += v[i];
+        }
+        const u32 inc = wave_incl_scan_u32(s);
+        if (l == 63) lw[w] = inc;
+        __syncthreads();
+        u32 run = carry, tot = carry;
+        for (int k = 0; k < 16; ++k) {
+            if (k < w) run += lw[k];
+            tot += lw[k];
+        }
+        run += inc - s;                                   // exclusive prefix of this thread's segment
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            buf[scan_pad(kPer * t + i)] = run;
+            run += v[i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int e = t + 1024 * i;
+            if (e < n) {
+                const u32 pre = buf[scan_pad(e)];
+                data[c0 + e] = pre;
+                on_entry(c0 + e, pre);
+            }
+        }
+        carry = tot;
+        __syncthreads();                                  // buf and lw are reused by the next chunk
     }
-    return tot;
+    return carry;
 }
 
 // exclusive scan over (ring, block) in ring-major order; ring_start[r] = first offset of ring r
 __global__ void __launch_bounds__(1024) k_fe_ring_scan(u32* __restrict__ blkhist, int L, const int* __restrict__ d_n,
                                                         int* __restrict__ ring_start) {
+    __shared__ u32 buf[kScanChunk + kScanChunk / 16];
     __shared__ u32 lw[16];
     const int n = *d_n;
     const int nblk = n > 0 ? (n + 255) / 256 : 1;
-    const u32 tot = block1024_scan_inplace(blkhist, L * nblk, lw, [&](int e, u32 pre) {
+    const u32 tot = block1024_scan_inplace(blkhist, L * nblk, buf, lw, [&](int e, u32 pre) {
         if (e % nblk == 0) ring_start[e / nblk] = (int)pre;
     });
     if (threadIdx.x == 0) ring_start[L] = (int)tot;
@@ -158,36 +181,16 @@ __device__ __forceinline__ bool kv_greater(double va, int ia, double vb, int ib)
     return va > vb || (va == vb && ia > ib);
 }
 
-__global__ void __launch_bounds__(256) k_fe_sector(const float4* __restrict__ rp, const int* __restrict__ ring_start,
-                                                    int* __restrict__ sec_edge_ids, int* __restrict__ sec_surf_ids,
-                                                    int* __restrict__ sec_cnt, int* __restrict__ err) {
-    __shared__ double sval[kSecCap];
-    __shared__ int sid[kSecCap];
-    __shared__ unsigned char picked[kSecCap + 16];
-    __shared__ unsigned char gapbig[kSecCap + 16];
-    __shared__ int sedge[kEdgePerSector + 1];
-    __shared__ int snedge;
-    __shared__ u32 lw[4];
-
-    const int sec = blockIdx.x;
-    const int r = sec / 6, s = sec % 6;
+// One sector's selection (:99-209) on arrays that live in LDS (sectors up to kSecLds entries) or in
+// global scratch (larger sectors: any size, as the reference). sval / sid: P >= size slots,
+// picked / gapbig: the window of ring positions [cs, cs + size + 10). 256 threads.
+template <bool kGlobal>
+__device__ __forceinline__ void sector_select(const float4* __restrict__ rr, int cs, int size, int base, int sec,
+                                              double* sval, int* sid, unsigned char* picked,
+                                              unsigned char* gapbig, int* sedge, int* lw_int, int* ivl_lo, int* ivl_hi,
+                                              int* __restrict__ sec_edge_ids, int* __restrict__ surf_ids,
+                                              int* __restrict__ sec_cnt) {
     const int t = threadIdx.x;
-    const int base = ring_start[r];
-    const int nr = ring_start[r + 1] - base;
-    if (nr < 131) {                                            // :67
-        if (t == 0) { sec_cnt[2 * sec] = 0; sec_cnt[2 * sec + 1] = 0; }
-        return;
-    }
-    const int total = nr - 10;                                 // :68
-    const int len = total / 6;                                 // :82
-    const int cs = len * s;
-    const int ce = (s == 5) ? total - 1 : len * (s + 1) - 1;   // half-open (:84-88)
-    const int size = ce - cs;
-    if (size > kSecCap) {
-        if (t == 0) { sec_cnt[2 * sec] = 0; sec_cnt[2 * sec + 1] = 0; atomicOr(err, 1); }
-        return;
-    }
-    const float4* rr = rp + base;
     int P = 64;
     while (P < size) P <<= 1;
     for (int k = t; k < P; k += 256) {
@@ -201,12 +204,11 @@ __global__ void __launch_bounds__(256) k_fe_sector(const float4* __restrict__ rp
         }
     }
     // window of ring positions [cs, cs + size + 10): picked flags and gaps to the previous point
-    const int ws = cs;
     for (int w = t; w < size + 10; w += 256) {
         picked[w] = 0;
         unsigned char g = 0;
         if (w >= 1) {
-            const float4 a = rr[ws + w], b = rr[ws + w - 1];
+            const float4 a = rr[cs + w], b = rr[cs + w - 1];
             const double dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;  // float differences (:129-131)
             g = (dx * dx + dy * dy + dz * dz > 0.05) ? 1 : 0;
         }
@@ -231,56 +233,127 @@ __global__ void __launch_bounds__(256) k_fe_sector(const float4* __restrict__ rp
             __syncthreads();
         }
     }
-    // greedy edge pick from the largest curvature (:110-148)
-    if (t == 0) {
+    // Greedy edge pick from the largest curvature (:110-148), wave 0. The reference walks the sorted
+    // list downwards: a picked point is skipped, the first unpicked point at curvature <= 0.1 ends
+    // the walk, otherwise the point is picked (the 21st pick only marks itself and ends the walk)
+    // and up to 5 neighbours on each side, up to the first big gap, are marked picked. Here 64
+    // candidates at a time sit on the lanes (lane 0 = largest); a pick is the lowest lane that is
+    // neither marked nor below the threshold, and every lane tests its own position against the
+    // pick's marked interval [w - left, w + right] (and against every earlier pick's interval when a
+    // new batch is loaded), so each pick costs a ballot and a broadcast instead of a walk.
+    if (t < 64) {
+        const int l = t;
         int count = 0, ne = 0;
-        for (int i = size - 1; i >= 0; --i) {
-            const int ind = sid[i];
-            const int w = ind - ws;
-            if (picked[w]) continue;
-            if (sval[i] <= 0.1) break;
-            ++count;
-            picked[w] = 1;
-            if (count <= kEdgePerSector) sedge[ne++] = ind;
-            else break;
-            for (int k = 1; k <= 5; ++k) {
-                if (gapbig[w + k]) break;
-                picked[w + k] = 1;
+        bool stop = false;
+        for (int b0 = 0; b0 < size && !stop; b0 += 64) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the intervals stored by lane 0
+            const int i = size - 1 - (b0 + l);
+            bool live = i >= 0;
+            int w = 0, lft = 0, rgt = 0, ind = 0;
+            double v = 0.0;
+            if (live) {
+                v = sval[i];
+                ind = sid[i];
+                w = ind - cs;
+                for (int k = 1; k <= 5 && !gapbig[w + k]; ++k) rgt = k;
+                for (int k = 1; k <= 5 && !gapbig[w - k + 1]; ++k) lft = k;
+                for (int p = 0; p < count; ++p) live = live && !(w >= ivl_lo[p] && w <= ivl_hi[p]);
             }
-            for (int k = 1; k <= 5; ++k) {
-                if (gapbig[w - k + 1]) break;
-                picked[w - k] = 1;
+            for (;;) {
+                const u64 m = __ballot(live);
+                if (!m) break;
+                const int pl = __ffsll((unsigned long long)m) - 1;
+                const double pv = __shfl(v, pl, 64);
+                if (pv <= 0.1) { stop = true; break; }                    // unpicked, below the threshold
+                const int pw = __shfl(w, pl, 64), pind = __shfl(ind, pl, 64);
+                ++count;
+                int lo = pw, hi = pw;
+                if (count <= kEdgePerSector) {
+                    lo = pw - __shfl(lft, pl, 64);
+                    hi = pw + __shfl(rgt, pl, 64);
+                    if (l == 0) sedge[ne] = pind;
+                    ++ne;
+                }
+                if (l == 0) {
+                    ivl_lo[count - 1] = lo;
+                    ivl_hi[count - 1] = hi;
+                }
+                live = live && !(w >= lo && w <= hi);
+                if (count > kEdgePerSector) { stop = true; break; }
             }
         }
-        snedge = ne;
+        // the marked positions, for the surf sweep
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int p = 0; p < count; ++p)
+            if (l <= ivl_hi[p] - ivl_lo[p]) picked[ivl_lo[p] + l] = 1;
+        if (l == 0) lw_int[4] = ne;
     }
     __syncthreads();
-    const int ne = snedge;
+    const int ne = lw_int[4];
     if (t < ne) sec_edge_ids[sec * kEdgePerSector + t] = sedge[t];
     // surf sweep in ascending order (:198-205), order-preserving compaction
     u32 run = 0;
     for (int b0 = 0; b0 < size; b0 += 256) {
         const int i = b0 + t;
-        const bool keep = (i < size) && !picked[sid[i] - ws];
-        u32 tot;
+        const bool keep = (i < size) && !picked[sid[i] - cs];
         const int wv = t >> 6, l = lane_id();
         const u64 bal = __ballot(keep);
         const u32 inw = (u32)__popcll(bal & lanemask_lt());
-        if (l == 0) lw[wv] = (u32)__popcll(bal);
+        if (l == 0) lw_int[wv] = (int)__popcll(bal);
         __syncthreads();
-        u32 off = 0;
-        tot = 0;
+        u32 off = 0, tot = 0;
         for (int q = 0; q < 4; ++q) {
-            if (q < wv) off += lw[q];
-            tot += lw[q];
+            if (q < wv) off += (u32)lw_int[q];
+            tot += (u32)lw_int[q];
         }
-        if (keep) sec_surf_ids[(size_t)sec * kSecCap + run + off + inw] = sid[i];
+        if (keep) surf_ids[base + cs + run + off + inw] = sid[i];
         run += tot;
         __syncthreads();
     }
     if (t == 0) {
         sec_cnt[2 * sec] = ne;
         sec_cnt[2 * sec + 1] = (int)run;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_fe_sector(const float4* __restrict__ rp, const int* __restrict__ ring_start,
+                                                    int* __restrict__ sec_edge_ids, int* __restrict__ surf_ids,
+                                                    int* __restrict__ sec_cnt, double* __restrict__ g_val,
+                                                    int* __restrict__ g_id, unsigned char* __restrict__ g_picked,
+                                                    unsigned char* __restrict__ g_gap) {
+    __shared__ double sval[kSecLds];
+    __shared__ int sid[kSecLds];
+    __shared__ unsigned char picked[kSecLds + 16];
+    __shared__ unsigned char gapbig[kSecLds + 16];
+    __shared__ int sedge[kEdgePerSector + 1];
+    __shared__ int lw_int[8];
+    __shared__ int ivl_lo[kEdgePerSector + 1], ivl_hi[kEdgePerSector + 1];
+
+    const int sec = blockIdx.x;
+    const int r = sec / 6, s = sec % 6;
+    const int t = threadIdx.x;
+    const int base = ring_start[r];
+    const int nr = ring_start[r + 1] - base;
+    if (nr < 131) {                                            // :67
+        if (t == 0) { sec_cnt[2 * sec] = 0; sec_cnt[2 * sec + 1] = 0; }
+        return;
+    }
+    const int total = nr - 10;                                 // :68
+    const int len = total / 6;                                 // :82
+    const int cs = len * s;
+    const int ce = (s == 5) ? total - 1 : len * (s + 1) - 1;   // half-open (:84-88)
+    const int size = ce - cs;
+    const float4* rr = rp + base;
+    if (size <= kSecLds) {
+        sector_select<false>(rr, cs, size, base, sec, sval, sid, picked, gapbig, sedge, lw_int, ivl_lo, ivl_hi,
+                             sec_edge_ids, surf_ids, sec_cnt);
+    } else {
+        // a sector larger than LDS (e.g. every point in ring 0 for a line count without a ring
+        // formula, :58-61): the same selection on global scratch; slots 2 (base + cs) .. of the
+        // scratch arrays are this sector's own (P <= 2 size, windows of size + 10 <= 2 size bytes)
+        const size_t o = 2 * (size_t)(base + cs);
+        sector_select<true>(rr, cs, size, base, sec, g_val + o, g_id + o, g_picked + o, g_gap + o, sedge, lw_int, ivl_lo,
+                            ivl_hi, sec_edge_ids, surf_ids, sec_cnt);
     }
 }
 
@@ -310,15 +383,17 @@ __global__ void __launch_bounds__(1024) k_fe_out_scan(const int* __restrict__ se
 
 __global__ void __launch_bounds__(256) k_fe_gather(const float4* __restrict__ rp, const int* __restrict__ ring_start,
                                                     const int* __restrict__ sec_edge_ids,
-                                                    const int* __restrict__ sec_surf_ids, const int* __restrict__ sec_cnt,
+                                                    const int* __restrict__ surf_ids, const int* __restrict__ sec_cnt,
                                                     const int* __restrict__ sec_off, float4* __restrict__ edge,
                                                     float4* __restrict__ surf) {
     const int sec = blockIdx.x;
-    const int base = ring_start[sec / 6];
+    const int r = sec / 6, s = sec % 6;
+    const int base = ring_start[r];
     const int ne = sec_cnt[2 * sec], ns = sec_cnt[2 * sec + 1];
     const int eo = sec_off[2 * sec], so = sec_off[2 * sec + 1];
+    const int cs = ((ring_start[r + 1] - base - 10) / 6) * s;    // the sector's surf ids start at base + cs
     for (int k = threadIdx.x; k < ne; k += 256) edge[eo + k] = rp[base + sec_edge_ids[sec * kEdgePerSector + k]];
-    for (int k = threadIdx.x; k < ns; k += 256) surf[so + k] = rp[base + sec_surf_ids[(size_t)sec * kSecCap + k]];
+    for (int k = threadIdx.x; k < ns; k += 256) surf[so + k] = rp[base + surf_ids[base + cs + k]];
 }
 
 }  // namespace
@@ -336,7 +411,12 @@ int fe_alloc(FeGPU& f, const pf_lidar_params& lidar, size_t cap) {
     if (hipMalloc(&f.ring_start, sizeof(int) * (kMaxRings + 1)) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&f.rp, sizeof(float4) * cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&f.sec_edge_ids, sizeof(int) * nsec * kEdgePerSector) != hipSuccess) return PF_ENOMEM;
-    if (hipMalloc(&f.sec_surf_ids, sizeof(int) * (size_t)nsec * kSecCap) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&f.sec_surf_ids, sizeof(int) * cap) != hipSuccess) return PF_ENOMEM;
+    // scratch of sectors larger than LDS: 2 slots per ring point (a sector's P <= 2 size)
+    if (hipMalloc(&f.big_val, sizeof(double) * 2 * cap + 64) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&f.big_id, sizeof(int) * 2 * cap + 64) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&f.big_picked, 2 * cap + 64) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&f.big_gap, 2 * cap + 64) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&f.sec_cnt, sizeof(int) * nsec * 2) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&f.sec_off, sizeof(int) * nsec * 2) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&f.err, sizeof(int)) != hipSuccess) return PF_ENOMEM;
@@ -363,6 +443,10 @@ void fe_free(FeGPU& f) {
     (void)hipFree(f.rp);
     (void)hipFree(f.sec_edge_ids);
     (void)hipFree(f.sec_surf_ids);
+    (void)hipFree(f.big_val);
+    (void)hipFree(f.big_id);
+    (void)hipFree(f.big_picked);
+    (void)hipFree(f.big_gap);
     (void)hipFree(f.sec_cnt);
     (void)hipFree(f.sec_off);
     (void)hipFree(f.err);
@@ -378,7 +462,7 @@ void fe_enqueue(FeGPU& f, const float4* d_in, const int* d_n, float4* edge, int*
     hipLaunchKernelGGL(k_fe_ring_scan, dim3(1), dim3(1024), 0, s, f.blkhist, L, d_n, f.ring_start);
     hipLaunchKernelGGL(k_fe_scatter, dim3(f.nblk_cap), dim3(256), 0, s, d_in, d_n, f.ring, f.blkhist, f.rp);
     hipLaunchKernelGGL(k_fe_sector, dim3(L * 6), dim3(256), 0, s, f.rp, f.ring_start, f.sec_edge_ids,
-                       f.sec_surf_ids, f.sec_cnt, f.err);
+                       f.sec_surf_ids, f.sec_cnt, f.big_val, f.big_id, f.big_picked, f.big_gap);
     hipLaunchKernelGGL(k_fe_out_scan, dim3(1), dim3(1024), 0, s, f.sec_cnt, L * 6, f.sec_off, d_ne, d_ns);
     hipLaunchKernelGGL(k_fe_gather, dim3(L * 6), dim3(256), 0, s, f.rp, f.ring_start, f.sec_edge_ids,
                        f.sec_surf_ids, f.sec_cnt, f.sec_off, edge, surf);

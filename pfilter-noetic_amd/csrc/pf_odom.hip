@@ -1016,7 +1016,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     // A block waiting for the evaluation to complete claims unclaimed chunks after kLmStealPolls
     // polls: only chunks of workgroups that have not started yet stay unclaimed that long.
     static_assert(kLmBlocks <= 32, "one claim-mask word per evaluation");
-    constexpr u32 kFull = kLmBlocks == 32 ? 0xFFFFFFFFu : ((1u << kLmBlocks) - 1u);
+    constexpr u32 kFull = (u32)((1ull << kLmBlocks) - 1ull);
     __shared__ int s_won, s_state, s_steal;
     u32* claim = a.arrive;                                       // [kLmEvalSlots] claim masks
     if (t < 2) nbad[t] = 0;

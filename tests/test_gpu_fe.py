@@ -125,22 +125,30 @@ def test_fe_golden(pa, pfsynth):
 def test_fe_s128_linear_ring_model(pa, pfref, pfsynth):
     """configs[4] scans (128 lines, -25..+15 deg) through the linear beam-model extension
     (pf_fe_set_ring_model), bit-exact against the oracle with the same model. Without the model the
-    reference puts every point into ring 0 (src/laserProcessingClass.cpp:58-61): its six sectors of
-    ~33k points exceed the device's 4096-entry sector sort, which is reported (PF_EUNSUPPORTED),
-    never silently dropped."""
+    reference puts every point into ring 0 (src/laserProcessingClass.cpp:58-61): six sectors of
+    ~25k points, far above the LDS sort's 2048 entries, which the device sorts in global scratch
+    (any sector size, as the reference) — also bit-exact."""
     seq = pfsynth.Sequence("S128", n_frames=4)
     x = seq.frame(3)
-    model = (15.0, -25.0)
-    fe = pa.LaserProcessingClass(device=0)
-    fe.init(pa.make_lidar(128, 3.0, 90.0, ring_model=model))
-    ge, gs = fe.featureExtraction(x)
-    re_, rs_ = pfref.feature_extraction(x, pfref.make_lidar(128, 3.0, 90.0, ring_model=model),
-                                        opts=pfref.FE_STABLE_TIES)
-    _same(ge, re_)
-    _same(gs, rs_)
-    assert ge.shape[0] > 128 * 6 * 5
-    fe0 = pa.LaserProcessingClass(device=0)
-    fe0.init(pa.make_lidar(128, 3.0, 90.0))
-    with pytest.raises(pa.PFError) as ei:
-        fe0.featureExtraction(x)
-    assert ei.value.code == pa.PF_EUNSUPPORTED
+    for model in ((15.0, -25.0), None):
+        fe = pa.LaserProcessingClass(device=0)
+        fe.init(pa.make_lidar(128, 3.0, 90.0, ring_model=model))
+        ge, gs = fe.featureExtraction(x)
+        re_, rs_ = pfref.feature_extraction(x, pfref.make_lidar(128, 3.0, 90.0, ring_model=model),
+                                            opts=pfref.FE_STABLE_TIES)
+        _same(ge, re_)
+        _same(gs, rs_)
+        assert ge.shape[0] > (128 * 6 * 5 if model else 6 * 5)
+
+
+def test_fe_sector_sizes_around_the_lds_limit(pa, pfref, pfsynth):
+    """Sectors on both sides of the 2048-entry LDS sort: S32 scans binned as 16 lines (the
+    reference's 16-line formula folds beams together) at 2,000 to 9,000 azimuth steps give sectors
+    of ~300 to ~3,900 entries in one scan; features bit-exact against the oracle."""
+    for az in (2000, 6100, 9000):
+        x = pfsynth.Sequence("S32", n_frames=1, az_steps=az).frame(0)
+        fe = _fe(pa, 16)
+        ge, gs = fe.featureExtraction(x)
+        re_, rs_ = _ref(pfref, x, 16)
+        _same(ge, re_)
+        _same(gs, rs_)
