@@ -265,8 +265,10 @@ __global__ void __launch_bounds__(256) k_vg_keys(Clouds in, const int* __restric
     sort_hist_end(lh, sh, n, n);
 }
 
-// one wave per voxel: lanes gather 64 members at a time, the running f32 sums then take them in
-// sorted (stable) order through readlane, so the order of additions is PCL's sequential one
+// One wave per voxel: the lanes gather up to 512 members at a time into the wave's LDS buffer, then
+// lanes 0, 1, 2 run the x, y, z sums over them in sorted (stable) order, one LDS read and one f32
+// add per member, so the order of additions is PCL's sequential one (the chain of the largest voxel
+// is the kernel's critical path: a few hundred ground points under the sensor at the surf leaf)
 __device__ __forceinline__ float lane_f(float v, int j) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
@@ -274,6 +276,7 @@ template <int NC>
 __global__ void __launch_bounds__(256) k_vg_reduce(Clouds in, const u32* __restrict__ keys, const u32* __restrict__ vals,
                                                     const u32* __restrict__ segstart, int* __restrict__ cnt,
                                                     CloudsW ds) {
+    __shared__ float mem[4][8 * 64 * 4];                 // per wave: 512 members, x y z w
     constexpr int nc = NC;
     const CatIdx<NC> ci = cat_idx<NC>(cnt + C_IN);
     const int n = cnt[C_VGN];
@@ -286,13 +289,14 @@ __global__ void __launch_bounds__(256) k_vg_reduce(Clouds in, const u32* __restr
         cnt[C_NQ] = nseg;
     }
     const int l = lane_id();
+    float* wm = mem[threadIdx.x >> 6];
     const int waves = gridDim.x * (blockDim.x >> 6);
     for (int sg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; sg < nseg; sg += waves) {
         const u32 b0 = segstart[sg], b1 = (sg + 1 < nseg) ? segstart[sg + 1] : (u32)n;
         const int c = (int)(keys[b0] >> 30);
         const float4* src = in.at(c);
         const int s0 = ci.start(c);
-        float sx = 0.f, sy = 0.f, sz = 0.f;
+        float acc = 0.f;                                    // lane k < 3: the sum of component k
         for (u32 base = b0; base < b1; base += 8 * 64) {   // AccumulatorXYZ, sorted (stable) order
             u32 idx[8];                                     // up to 512 members in flight at once
             float4 p[8];
@@ -304,15 +308,25 @@ __global__ void __launch_bounds__(256) k_vg_reduce(Clouds in, const u32* __restr
                 if (idx[u] != 0xFFFFFFFFu) p[u] = src[(int)idx[u] - s0];
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int m = (int)min(64, (int)(b1 - base) - u * 64);
-                for (int j = 0; j < m; ++j) {
-                    sx += lane_f(p[u].x, j);
-                    sy += lane_f(p[u].y, j);
-                    sz += lane_f(p[u].z, j);
+            for (int u = 0; u < 8; ++u) reinterpret_cast<float4*>(wm)[u * 64 + l] = p[u];
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const int m = (int)min(512u, b1 - base);
+            if (l < 3) {
+                int j = 0;
+                for (; j + 4 <= m; j += 4) {               // reads run ahead of the dependent adds
+                    const float a0 = wm[4 * j + l], a1 = wm[4 * (j + 1) + l];
+                    const float a2 = wm[4 * (j + 2) + l], a3 = wm[4 * (j + 3) + l];
+                    acc += a0;
+                    acc += a1;
+                    acc += a2;
+                    acc += a3;
                 }
+                for (; j < m; ++j) acc += wm[4 * j + l];
             }
+            __builtin_amdgcn_wave_barrier();               // the buffer is refilled by the next round
         }
+        const float sx = lane_f(acc, 0), sy = lane_f(acc, 1), sz = lane_f(acc, 2);
         if (l == 0) {
             const float nn = (float)(b1 - b0);
             // rgb of inputs is 0 (copyPointCloud XYZI -> XYZRGB): averages stay 0

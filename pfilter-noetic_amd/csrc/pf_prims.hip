@@ -70,14 +70,18 @@ __global__ void __launch_bounds__(256) k_os_hist(const u32* __restrict__ keys, c
 }
 
 // One pass. Blocks own tiles b, b + G, ... (G <= kSortMaxBlocks co-resident blocks), so a tile's
-// look-back only waits on tiles of running blocks.
-__global__ void __launch_bounds__(kOsThreads) k_os_pass(const u32* __restrict__ kin, const u32* __restrict__ vin,
+// look-back only waits on tiles of running blocks. Inside a tile, wave w owns the contiguous 512
+// keys w * 512 .. (lane l of round u: key w * 512 + 64 u + l), so the waves rank independently: a
+// key's rank among equal digits of its wave is the wave's running count of that digit (a wave-
+// private LDS row, updated by one leader lane per digit and round) plus the equal lanes below it;
+// one block barrier then turns the four waves' digit counts into per-wave offsets. Stable: keys keep
+// their index order within a digit. Two barriers per tile instead of four per round.
+__global__ void __launch_bounds__(256) k_os_pass(const u32* __restrict__ kin, const u32* __restrict__ vin,
                                                          u32* __restrict__ kout, u32* __restrict__ vout,
                                                          const int* __restrict__ d_n, int pass,
                                                          const u32* __restrict__ dbase_g, u64* __restrict__ status,
                                                          int* __restrict__ err) {
-    __shared__ u32 run[256];
-    __shared__ u32 wcnt[4][256];
+    __shared__ u32 wcnt[4][256];                 // per wave: running digit counts, then its offsets
     __shared__ u32 off[256];
     const int n = *d_n;
     const int ntiles = (n + kSortTile - 1) / kSortTile;
@@ -88,40 +92,37 @@ __global__ void __launch_bounds__(kOsThreads) k_os_pass(const u32* __restrict__ 
     const u32 dbase = dbase_g[pass * 256 + t];
     const u64 lt = lanemask_lt();
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int i0 = tile * kSortTile + w * (kSortTile / 4);
         u32 key[kOsPer], val[kOsPer], rk[kOsPer];
 #pragma unroll
         for (int r = 0; r < kOsPer; ++r) {                      // the whole tile in flight at once
-            const int i = tile * kSortTile + r * kOsThreads + t;
+            const int i = i0 + r * 64 + l;
             key[r] = i < n ? kin[i] : 0xFFFFFFFFu;
             val[r] = i < n ? vin[i] : 0u;
         }
-        run[t] = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wcnt[w][l + 64 * k] = 0;   // this wave's row only
 #pragma unroll
         for (int r = 0; r < kOsPer; ++r) {
-            const bool valid = tile * kSortTile + r * kOsThreads + t < n;
+            const bool valid = i0 + r * 64 + l < n;
             const u32 d = (key[r] >> shift) & 255u;
-            wcnt[w][l] = 0; wcnt[w][l + 64] = 0; wcnt[w][l + 128] = 0; wcnt[w][l + 192] = 0;
-            __syncthreads();
             const u64 peers = match_bits(d, 8, valid);
-            const u32 rank = (u32)__popcll(peers & lt);
-            if (valid && rank == 0) wcnt[w][d] = (u32)__popcll(peers);
-            __syncthreads();
-            {
-                u32 a = run[t];
-#pragma unroll
-                for (int ww = 0; ww < 4; ++ww) {
-                    const u32 c = wcnt[ww][t];
-                    wcnt[ww][t] = a;
-                    a += c;
-                }
-                run[t] = a;
-            }
-            __syncthreads();
-            rk[r] = valid ? wcnt[w][d] + rank : 0xFFFFFFFFu;
-            __syncthreads();
+            const u32 below = (u32)__popcll(peers & lt);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous round's leader updates
+            const u32 run = valid ? wcnt[w][d] : 0u;
+            rk[r] = valid ? run + below : 0xFFFFFFFFu;
+            if (valid && below == 0) wcnt[w][d] = run + (u32)__popcll(peers);
         }
-        {   // decoupled look-back for digit t
-            const u32 cnt = run[t];
+        __syncthreads();
+        {   // digit t: the waves' counts -> per-wave exclusive offsets, the tile's count -> look-back
+            u32 a = 0;
+#pragma unroll
+            for (int ww = 0; ww < 4; ++ww) {
+                const u32 c = wcnt[ww][t];
+                wcnt[ww][t] = a;
+                a += c;
+            }
+            const u32 cnt = a;
             u64* mine = st + (size_t)tile * 256 + t;
             u32 excl = 0;
             if (tile > 0) {
@@ -151,7 +152,8 @@ __global__ void __launch_bounds__(kOsThreads) k_os_pass(const u32* __restrict__ 
 #pragma unroll
         for (int r = 0; r < kOsPer; ++r) {
             if (rk[r] == 0xFFFFFFFFu) continue;
-            const u32 pos = off[(key[r] >> shift) & 255u] + rk[r];
+            const u32 d = (key[r] >> shift) & 255u;
+            const u32 pos = off[d] + wcnt[w][d] + rk[r];
             kout[pos] = key[r];
             vout[pos] = val[r];
         }
