@@ -229,6 +229,24 @@ int pf_odom_poses(pf_odom* h, double* poses, size_t cap, size_t* n);
 int pf_odom_set_stage_a_reserve(pf_odom* h, int cus);
 /* the ring model extension of pf_fe_set_ring_model for the handle's featureExtraction */
 int pf_odom_set_ring_model(pf_odom* h, double top_deg, double bottom_deg);
+/* The public members of OdomBaseClass (include/odomEstimationClass.h:52-58, 71): `parameters`
+ * (q_w_curr = parameters[0..3] as x, y, z, w; t_w_curr = parameters[4..6]) after the last solve,
+ * `last_odom` as a row-major 3 x 4 [R | t], and `optimization_count`. Any output may be NULL. */
+int pf_odom_get_state(pf_odom* h, double parameters[7], double last_odom[12], int* optimization_count);
+/* Snapshot of a handle's whole estimator state (pose, last pose, optimization count, the maps with
+ * their age / p-index bytes, the counters), for golden-vector capture and checkpoint / resume. buf NULL:
+ * *size = the bytes needed. restore() loads a snapshot into a handle created with the same parameters
+ * (PF_EINVAL otherwise); the next frame continues exactly as the snapshot handle's next frame would
+ * (its pose history restarts with the snapshot's pose). */
+int pf_odom_snapshot(pf_odom* h, void* buf, size_t cap, size_t* size);
+int pf_odom_restore(pf_odom* h, const void* buf, size_t size);
+/* Map export: with enable, every frame / update writes the maps (x, y, z, bits(r | g << 8) as 4
+ * floats per point) and their sizes straight into mapped pinned host memory at the end of the
+ * odometry (one kernel, no extra host round trip). map_export returns the pointer and size of map
+ * `which` for the last completed call (valid until the next one): what the C++ shim copies into
+ * laserCloudCornerMap / laserCloudSurfMap (or the BPF maps) after every update. */
+int pf_odom_set_map_export(pf_odom* h, int enable);
+int pf_odom_map_export(pf_odom* h, int which, const float** xyzw, size_t* n);
 /* enable/disable hipGraph replay of the steady-state frame (default on) */
 int pf_odom_set_graph(pf_odom* h, int enable);
 

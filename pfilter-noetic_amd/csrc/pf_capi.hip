@@ -270,6 +270,7 @@ static int init_map_n(pf_odom* h, const float* const* cl, const size_t* n, const
     if (!rc) rc = stage_a_end_b_begin(h, p);
     if (rc) return rc;
     odom_enqueue_init(o, p, o.stream);
+    odom_enqueue_export(o, o.stream);
     rc = stage_b_end(h, p);
     if (rc) return rc;
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
@@ -288,6 +289,7 @@ static int update_n(pf_odom* h, const float* const* cl, const size_t* n, const s
     rc = stage_a_end_b_begin(h, p);
     if (rc) return rc;
     odom_enqueue_update(o, p, o.stream);
+    odom_enqueue_export(o, o.stream);
     rc = stage_b_end(h, p);
     if (rc) return rc;
     if (pose_out) {
@@ -434,6 +436,7 @@ static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool s
         stage_enqueue_vg(o, p, s);
     } else {
         odom_enqueue_update(o, p, s);
+        odom_enqueue_export(o, s);
     }
     PF_HIP_TRY(hipStreamEndCapture(s, &g));
     PF_HIP_TRY(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
@@ -489,8 +492,10 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
         PF_HIP_TRY(hipGraphLaunch(o.graph_b[p], o.stream));
     } else if (!o.inited) {
         odom_enqueue_init(o, p, o.stream);
+        odom_enqueue_export(o, o.stream);
     } else {
         odom_enqueue_update(o, p, o.stream);
+        odom_enqueue_export(o, o.stream);
     }
     return stage_b_end(h, p);
 }
@@ -633,6 +638,174 @@ int pf_odom_set_ring_model(pf_odom* h, double top_deg, double bottom_deg) {
             (void)hipGraphExecDestroy(o.graph_a[s]);
             o.graph_a[s] = nullptr;
         }
+    return PF_OK;
+}
+
+// ---- state access: the public members of OdomBaseClass, snapshot / restore, map export ----------
+int pf_odom_get_state(pf_odom* h, double parameters[7], double last_odom[12], int* optimization_count) {
+    if (!h) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    DevState st;
+    PF_HIP_TRY(hipMemcpyAsync(&st, o.st, sizeof(st), hipMemcpyDeviceToHost, o.stream));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    if (parameters) std::memcpy(parameters, st.params, sizeof(st.params));
+    if (last_odom)
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) last_odom[4 * i + j] = st.lastR[3 * i + j];
+            last_odom[4 * i + 3] = st.lastt[i];
+        }
+    if (optimization_count) *optimization_count = st.optimization_count;
+    return sticky_status(o);
+}
+
+namespace {
+// snapshot blob: header, the device state, the counters, the latest pose, then the maps
+struct SnapHeader {
+    uint32_t magic, version;
+    int32_t nc, inited, opt_count_host, frames;
+    int32_t num_lines, k_new, theta_max, weight_type;
+    double map_res, min_dist, max_dist, ring_top, ring_scale;
+    float theta_p;
+    int32_t pad;
+    uint64_t map_n[kMaxC];
+};
+constexpr uint32_t kSnapMagic = 0x4e534650u;   // "PFSN"
+size_t snap_bytes(const SnapHeader& hd) {
+    size_t b = sizeof(SnapHeader) + sizeof(DevState) + sizeof(int) * C_COUNT + sizeof(double) * 7;
+    for (int c = 0; c < hd.nc; ++c) b += sizeof(float4) * hd.map_n[c];
+    return b;
+}
+}  // namespace
+
+int pf_odom_snapshot(pf_odom* h, void* buf, size_t cap, size_t* size) {
+    if (!h || !size) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(hipMemcpyAsync(o.h_cnt, o.cnt, sizeof(int) * C_COUNT, hipMemcpyDeviceToHost, o.stream));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    SnapHeader hd{};
+    hd.magic = kSnapMagic;
+    hd.version = 1;
+    hd.nc = o.cls.nc;
+    hd.inited = o.inited ? 1 : 0;
+    hd.opt_count_host = o.opt_count_host;
+    hd.frames = o.frames;
+    hd.num_lines = o.lidar.num_lines;
+    hd.k_new = o.prm.k_new;
+    hd.theta_max = o.prm.theta_max;
+    hd.weight_type = o.prm.weight_type;
+    hd.map_res = o.prm.map_res;
+    hd.min_dist = o.lidar.min_dist;
+    hd.max_dist = o.lidar.max_dist;
+    hd.ring_top = o.fe.ring_top;
+    hd.ring_scale = o.fe.ring_scale;
+    hd.theta_p = o.prm.theta_p;
+    for (int c = 0; c < o.cls.nc; ++c) hd.map_n[c] = (uint64_t)o.h_cnt[C_M + c];
+    *size = snap_bytes(hd);
+    if (!buf) return PF_OK;
+    if (cap < *size) return PF_ECAPACITY;
+    char* b = static_cast<char*>(buf);
+    std::memcpy(b, &hd, sizeof(hd));
+    b += sizeof(hd);
+    PF_HIP_TRY(hipMemcpyAsync(b, o.st, sizeof(DevState), hipMemcpyDeviceToHost, o.stream));
+    b += sizeof(DevState);
+    std::memcpy(b, o.h_cnt, sizeof(int) * C_COUNT);
+    b += sizeof(int) * C_COUNT;
+    double pose[7] = {0, 0, 0, 1, 0, 0, 0};
+    if (o.frames > 0)
+        PF_HIP_TRY(hipMemcpyAsync(pose, o.poses + 7 * ((size_t)(o.frames - 1) % o.pose_cap), sizeof(pose),
+                                  hipMemcpyDeviceToHost, o.stream));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    std::memcpy(b, pose, sizeof(pose));
+    b += sizeof(pose);
+    for (int c = 0; c < o.cls.nc; ++c) {
+        if (hd.map_n[c])
+            PF_HIP_TRY(hipMemcpyAsync(b, o.map[c], sizeof(float4) * hd.map_n[c], hipMemcpyDeviceToHost, o.stream));
+        b += sizeof(float4) * hd.map_n[c];
+    }
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    return sticky_status(o);
+}
+
+int pf_odom_restore(pf_odom* h, const void* buf, size_t size) {
+    if (!h || !buf || size < sizeof(SnapHeader)) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    SnapHeader hd;
+    std::memcpy(&hd, buf, sizeof(hd));
+    if (hd.magic != kSnapMagic || hd.version != 1 || hd.nc != o.cls.nc || size != snap_bytes(hd)) return PF_EINVAL;
+    // the snapshot's estimator must be this handle's (the kernels and graphs carry its parameters)
+    if (hd.num_lines != o.lidar.num_lines || hd.k_new != o.prm.k_new || hd.theta_max != o.prm.theta_max ||
+        hd.weight_type != o.prm.weight_type || hd.map_res != o.prm.map_res || hd.theta_p != o.prm.theta_p ||
+        hd.min_dist != o.lidar.min_dist || hd.max_dist != o.lidar.max_dist || hd.ring_top != o.fe.ring_top ||
+        hd.ring_scale != o.fe.ring_scale)
+        return PF_EINVAL;
+    for (int c = 0; c < hd.nc; ++c)
+        if (hd.map_n[c] > o.map_cap) return PF_ECAPACITY;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    int rc = odom_reset(o);                    // quiesces both streams, empties the p-index buckets
+    if (rc) return rc;
+    const char* b = static_cast<const char*>(buf) + sizeof(hd);
+    DevState st;
+    std::memcpy(&st, b, sizeof(st));
+    b += sizeof(st);
+    int cnt[C_COUNT];
+    std::memcpy(cnt, b, sizeof(cnt));
+    b += sizeof(cnt);
+    double pose[7];
+    std::memcpy(pose, b, sizeof(pose));
+    b += sizeof(pose);
+    // the restored handle's pose history starts with the snapshot's pose
+    const bool has_pose = hd.frames > 0;
+    st.frame = has_pose ? 1 : 0;
+    PF_HIP_TRY(hipMemcpyAsync(o.st, &st, sizeof(st), hipMemcpyHostToDevice, o.stream));
+    PF_HIP_TRY(hipMemcpyAsync(o.cnt, cnt, sizeof(cnt), hipMemcpyHostToDevice, o.stream));
+    if (has_pose) PF_HIP_TRY(hipMemcpyAsync(o.poses, pose, sizeof(pose), hipMemcpyHostToDevice, o.stream));
+    for (int c = 0; c < hd.nc; ++c) {
+        if (hd.map_n[c])
+            PF_HIP_TRY(hipMemcpyAsync(o.map[c], b, sizeof(float4) * hd.map_n[c], hipMemcpyHostToDevice, o.stream));
+        b += sizeof(float4) * hd.map_n[c];
+    }
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    o.inited = hd.inited != 0;
+    o.opt_count_host = hd.opt_count_host;
+    o.frames = has_pose ? 1 : 0;
+    return PF_OK;
+}
+
+int pf_odom_set_map_export(pf_odom* h, int enable) {
+    if (!h) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    if (enable && !o.h_map[0]) {
+        for (int c = 0; c < o.cls.nc; ++c) {
+            if (hipHostMalloc(&o.h_map[c], sizeof(float4) * o.map_cap, hipHostMallocMapped) != hipSuccess)
+                return PF_ENOMEM;
+            PF_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&o.h_map_dev[c]), o.h_map[c], 0));
+        }
+        if (hipHostMalloc(&o.h_map_n, sizeof(int) * kMaxC, hipHostMallocMapped) != hipSuccess) return PF_ENOMEM;
+        PF_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&o.h_map_n_dev), o.h_map_n, 0));
+        std::memset(o.h_map_n, 0, sizeof(int) * kMaxC);
+    }
+    if ((enable != 0) != o.export_maps)
+        for (int s = 0; s < kSlots; ++s)      // the export kernel is part of the captured stage B
+            if (o.graph_b[s]) {
+                (void)hipGraphExecDestroy(o.graph_b[s]);
+                o.graph_b[s] = nullptr;
+            }
+    o.export_maps = enable != 0;
+    return PF_OK;
+}
+
+int pf_odom_map_export(pf_odom* h, int which, const float** xyzw, size_t* n) {
+    if (!h || !xyzw || !n || which < 0 || which >= h->o.cls.nc || !h->o.export_maps) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));     // (already idle after a call that read the pose)
+    *xyzw = reinterpret_cast<const float*>(o.h_map[which]);
+    *n = (size_t)o.h_map_n[which];
     return PF_OK;
 }
 

@@ -132,6 +132,13 @@ struct OdomGPU {
     int err_last[E_COUNT] = {};    // values of the words at their last report (pf_dev_errors)
     int* h_cnt = nullptr;          // pinned mirror
     double* h_pose = nullptr;      // pinned [7]
+    // map export (pf_odom_set_map_export): after every update the maps are written straight into
+    // mapped pinned host memory by k_map_export (device-resident sizes, no host round trip)
+    bool export_maps = false;
+    float4* h_map[kMaxC] = {};     // pinned, map_cap points each
+    float4* h_map_dev[kMaxC] = {}; // their device-side addresses
+    int* h_map_n = nullptr;        // pinned [kMaxC] sizes written with them
+    int* h_map_n_dev = nullptr;
 
     StageBuf sb[kSlots];
     u32* acc_a = nullptr;                                   // stage A min/max accumulators
@@ -191,5 +198,7 @@ void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s);
 void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s);
 // stage B: updatePointsToMap from slot p's down-sampled features; outer iteration count = host mirror
 void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s);
+// stage B tail when map export is on: the maps and their sizes into the mapped pinned buffers
+void odom_enqueue_export(OdomGPU& o, hipStream_t s);
 
 }  // namespace pf

@@ -1436,6 +1436,17 @@ __global__ void __launch_bounds__(256) k_init_map(const int* __restrict__ cnt, C
     }
 }
 
+// the maps (x, y, z, bits(r | g << 8)) and their sizes into mapped pinned host memory (PCIe writes)
+__global__ void __launch_bounds__(256) k_map_export(const int* __restrict__ cnt, CloudsW map, CloudsW out,
+                                                     int* __restrict__ out_n, int nc) {
+    for (int c = 0; c < nc; ++c) {
+        const int n = cnt[C_M + c];
+        if (blockIdx.x == 0 && threadIdx.x == 0) out_n[c] = n;
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+            out.at(c)[i] = map.at(c)[i];
+    }
+}
+
 __global__ void k_init_buckets(int4* __restrict__ b, size_t n) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         b[i] = make_int4(0, -1, -1, -1);
@@ -1655,6 +1666,9 @@ void odom_destroy(OdomGPU& o) {
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
     if (o.h_pose) (void)hipHostFree(o.h_pose);
+    for (int c = 0; c < kMaxC; ++c)
+        if (o.h_map[c]) (void)hipHostFree(o.h_map[c]);
+    if (o.h_map_n) (void)hipHostFree(o.h_map_n);
     if (o.stream) (void)hipStreamDestroy(o.stream);
     if (o.stream_a) (void)hipStreamDestroy(o.stream_a);
     o = OdomGPU{};
@@ -1689,6 +1703,12 @@ void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s) {
     segment_starts(o.vkeys, cnt + C_VGN, o.vsegstart, cnt + C_NSEG, cnt + C_NLT, cnt + C_NRG_VALID, o.vprim, s);
     PF_LAUNCH_NC(nc, k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, clouds(sb.in), o.vkeys, o.vvals, o.vsegstart, cnt,
                  clouds_w(sb.ds));
+}
+
+void odom_enqueue_export(OdomGPU& o, hipStream_t s) {
+    if (!o.export_maps) return;
+    hipLaunchKernelGGL(k_map_export, dim3(256), dim3(256), 0, s, o.cnt, clouds_w(o.map), clouds_w(o.h_map_dev),
+                       o.h_map_n_dev, o.cls.nc);
 }
 
 void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s) {

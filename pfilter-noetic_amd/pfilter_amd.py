@@ -89,7 +89,8 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_odom_reset", "pf_cls_default_params", "pf_cls_create", "pf_cls_destroy", "pf_cls_extract",
            "pf_cls_classify", "pf_cls_ground_seg", "pf_bpf_set_front_end", "pf_bpf_frame_scan_device", "pf_map_create", "pf_map_destroy", "pf_map_update",
            "pf_map_update_device", "pf_map_update_mat", "pf_map_get", "pf_odom_set_stage_a_reserve",
-           "pf_fe_set_ring_model", "pf_odom_set_ring_model"]
+           "pf_fe_set_ring_model", "pf_odom_set_ring_model", "pf_odom_get_state", "pf_odom_snapshot",
+           "pf_odom_restore", "pf_odom_set_map_export", "pf_odom_map_export"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -125,6 +126,11 @@ def lib():
         L.pf_odom_set_stage_a_reserve.argtypes = [_vp, _i]
     L.pf_fe_set_ring_model.argtypes = [_vp, ctypes.c_double, ctypes.c_double]
     L.pf_odom_set_ring_model.argtypes = [_vp, ctypes.c_double, ctypes.c_double]
+    L.pf_odom_get_state.argtypes = [_vp, _vp, _vp, ctypes.POINTER(_i)]
+    L.pf_odom_snapshot.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
+    L.pf_odom_restore.argtypes = [_vp, _vp, _sz]
+    L.pf_odom_set_map_export.argtypes = [_vp, _i]
+    L.pf_odom_map_export.argtypes = [_vp, _i, ctypes.POINTER(ctypes.POINTER(ctypes.c_float)), ctypes.POINTER(_sz)]
     L.pf_device_count.argtypes = [ctypes.POINTER(_i)]
     L.pf_dev_malloc.argtypes = [_i, _sz, ctypes.POINTER(_vp)]
     L.pf_dev_free.argtypes = [_i, _vp]
@@ -361,6 +367,38 @@ class Odom_ES_EstimationClass:
 
     def set_graph(self, enable):
         _check("pf_odom_set_graph", lib().pf_odom_set_graph(self._h, int(bool(enable))))
+
+    # ---- OdomBaseClass public members and state capture ----
+    def state(self):
+        """{parameters (q_w_curr x, y, z, w, t_w_curr), last_odom (3 x 4 [R | t]), optimization_count}"""
+        prm, last, oc = np.empty(7), np.empty(12), _i()
+        _check("pf_odom_get_state", lib().pf_odom_get_state(self._h, prm.ctypes.data, last.ctypes.data,
+                                                            ctypes.byref(oc)))
+        return {"parameters": prm, "last_odom": last.reshape(3, 4), "optimization_count": oc.value}
+
+    def snapshot(self):
+        """the whole estimator state as bytes (pf_odom_snapshot)"""
+        n = _sz()
+        _check("pf_odom_snapshot", lib().pf_odom_snapshot(self._h, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value)
+        _check("pf_odom_snapshot", lib().pf_odom_snapshot(self._h, buf, n.value, ctypes.byref(n)))
+        return buf.raw
+
+    def restore(self, blob):
+        buf = ctypes.create_string_buffer(bytes(blob), len(blob))
+        _check("pf_odom_restore", lib().pf_odom_restore(self._h, buf, len(blob)))
+
+    def set_map_export(self, enable):
+        _check("pf_odom_set_map_export", lib().pf_odom_set_map_export(self._h, int(bool(enable))))
+
+    def map_export(self, which):
+        """(xyz [n, 3] float32, rg [n, 2] uint8) of map `which` from the pinned export buffer"""
+        ptr, n = ctypes.POINTER(ctypes.c_float)(), _sz()
+        _check("pf_odom_map_export", lib().pf_odom_map_export(self._h, int(which), ctypes.byref(ptr), ctypes.byref(n)))
+        a = np.ctypeslib.as_array(ptr, shape=(max(n.value, 1), 4))[:n.value].copy()
+        w = a[:, 3].view(np.uint32)
+        rg = np.stack([(w & 255), (w >> 8) & 255], 1).astype(np.uint8)
+        return a[:, :3].copy(), rg
 
     def set_stage_a_reserve(self, cus):
         """CUs stage A stays off (default 128 ES / 32 BPF; 0 when several handles share the GPU)"""

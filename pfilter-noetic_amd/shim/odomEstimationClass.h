@@ -18,5 +18,7 @@
 typedef pcl::PointXYZRGB PointType;
 using Odom_ES_EstimationClass = pfilter_hip::Odom_ES_EstimationClassT<pcl::PointCloud<PointType>, lidar::Lidar>;
 using Odom_BPF_EstimationClass = pfilter_hip::Odom_BPF_EstimationClassT<pcl::PointCloud<PointType>, lidar::Lidar>;
+// the north star's name for the ES estimator (the fork calls it Odom_ES_EstimationClass)
+using OdomEstimationClass = Odom_ES_EstimationClass;
 
 #endif  // _ODOM_ESTIMATION_CLASS_H_

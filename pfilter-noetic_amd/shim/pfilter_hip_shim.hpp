@@ -125,8 +125,91 @@ private:
 };
 
 // --------------------------------------------------------------------------------------------
+// OdomBaseClass's public optimisation members (include/odomEstimationClass.h:52-58, 71), refreshed
+// from the device after every initMapWithPoints / updatePointsToMap (pf_odom_get_state), and the
+// map copy both estimators share: with refresh_maps_every_frame the maps arrive in pinned host
+// memory at the end of the device update (pf_odom_set_map_export), so refreshing the public clouds
+// costs no extra device round trip.
+class OdomBaseMembers {
+public:
+    double parameters[7] = {0, 0, 0, 1, 0, 0, 0};
+#ifndef PFILTER_HIP_NO_EIGEN
+    Eigen::Map<Eigen::Quaterniond> q_w_curr = Eigen::Map<Eigen::Quaterniond>(parameters);
+    Eigen::Map<Eigen::Vector3d> t_w_curr = Eigen::Map<Eigen::Vector3d>(parameters + 4);
+    Eigen::Isometry3d last_odom = Eigen::Isometry3d::Identity();
+#else
+    double last_odom[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};   // row-major [R | t]
+#endif
+    int optimization_count = 2;
+
+protected:
+    void pull_state(pf_odom* h) {
+        double lo[12];
+        check("pf_odom_get_state", pf_odom_get_state(h, parameters, lo, &optimization_count));
+#ifndef PFILTER_HIP_NO_EIGEN
+        last_odom = Eigen::Isometry3d::Identity();
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) last_odom.linear()(i, j) = lo[4 * i + j];
+            last_odom.translation()(i) = lo[4 * i + 3];
+        }
+#else
+        for (int k = 0; k < 12; ++k) last_odom[k] = lo[k];
+#endif
+    }
+    // keep the device-side map export in step with refresh_maps_every_frame (before each call)
+    void sync_export(pf_odom* h, bool refresh) {
+        if (refresh != export_on_) {
+            check("pf_odom_set_map_export", pf_odom_set_map_export(h, refresh ? 1 : 0));
+            export_on_ = refresh;
+        }
+    }
+    // map `which` into a PointXYZRGB cloud: from the export buffer when the last call wrote it,
+    // otherwise by pf_odom_get_map (r = age / rounds, g = p-index / observation count)
+    template <class Cloud>
+    void fill_map(pf_odom* h, int which, Cloud& out) {
+        using Point = typename std::decay<decltype(out.points[0])>::type;
+        out.clear();
+        if (export_on_) {
+            const float* a = nullptr;
+            size_t n = 0;
+            check("pf_odom_map_export", pf_odom_map_export(h, which, &a, &n));
+            for (size_t i = 0; i < n; ++i) {
+                Point p;
+                p.x = a[4 * i];
+                p.y = a[4 * i + 1];
+                p.z = a[4 * i + 2];
+                uint32_t w;
+                std::memcpy(&w, a + 4 * i + 3, 4);
+                p.r = (uint8_t)(w & 255u);
+                p.g = (uint8_t)((w >> 8) & 255u);
+                p.b = 0;
+                out.push_back(p);
+            }
+            return;
+        }
+        size_t n = 0;
+        check("pf_odom_get_map", pf_odom_get_map(h, which, nullptr, nullptr, 0, &n));
+        xyz_.resize(3 * (n ? n : 1));
+        rg_.resize(2 * (n ? n : 1));
+        check("pf_odom_get_map", pf_odom_get_map(h, which, xyz_.data(), rg_.data(), n, &n));
+        for (size_t i = 0; i < n; ++i) {
+            Point p;
+            p.x = xyz_[3 * i];
+            p.y = xyz_[3 * i + 1];
+            p.z = xyz_[3 * i + 2];
+            p.r = rg_[2 * i];
+            p.g = rg_[2 * i + 1];
+            p.b = 0;
+            out.push_back(p);
+        }
+    }
+    bool export_on_ = false;
+    std::vector<float> xyz_;
+    std::vector<uint8_t> rg_;
+};
+
 template <class CloudXYZRGB, class Lidar>
-class Odom_ES_EstimationClassT {
+class Odom_ES_EstimationClassT : public OdomBaseMembers {
 public:
     using Ptr = typename CloudXYZRGB::Ptr;
     using Point = typename std::decay<decltype(std::declval<CloudXYZRGB>().points[0])>::type;
@@ -150,12 +233,14 @@ public:
         op.theta_max = theta_max_para;
         op.weight_type = (int)weightType_para;
         check("pf_odom_create", pf_odom_create(&lp, &op, device_, max_points_, map_capacity_, &h_));
+        export_on_ = false;
         set_identity();
         laserCloudCornerMap->clear();
         laserCloudSurfMap->clear();
     }
 
     void initMapWithPoints(const Ptr& edge_in, const Ptr& surf_in) {
+        sync_export(h_, refresh_maps_every_frame);
         check("pf_odom_init_map", pf_odom_init_map(h_, data(edge_in), edge_in->points.size(), sizeof(Point),
                                                    data(surf_in), surf_in->points.size(), sizeof(Point)));
         refresh();
@@ -163,6 +248,7 @@ public:
 
     void updatePointsToMap(const Ptr& edge_in, const Ptr& surf_in) {
         double pose[7];
+        sync_export(h_, refresh_maps_every_frame);
         const int rc = check("pf_odom_update", pf_odom_update(h_, data(edge_in), edge_in->points.size(), sizeof(Point),
                                                               data(surf_in), surf_in->points.size(), sizeof(Point),
                                                               pose));
@@ -182,7 +268,7 @@ public:
     // false: the map members are only refreshed by syncMaps() (saves the D2H copy per frame when no
     // subscriber reads them, as in src/odomEstimationNode copy.cpp:129-141)
     bool refresh_maps_every_frame = true;
-    void syncMaps() { read_map(0, *laserCloudCornerMap); read_map(1, *laserCloudSurfMap); }
+    void syncMaps() { fill_map(h_, 0, *laserCloudCornerMap); fill_map(h_, 1, *laserCloudSurfMap); }
 
 #ifndef PFILTER_HIP_NO_EIGEN
     Eigen::Isometry3d odom = Eigen::Isometry3d::Identity();
@@ -213,36 +299,17 @@ private:
 #endif
     }
     void refresh() {
+        pull_state(h_);
         if (refresh_maps_every_frame) syncMaps();
-    }
-    void read_map(int which, CloudXYZRGB& out) {
-        size_t n = 0;
-        check("pf_odom_get_map", pf_odom_get_map(h_, which, nullptr, nullptr, 0, &n));
-        xyz_.resize(3 * (n ? n : 1));
-        rg_.resize(2 * (n ? n : 1));
-        check("pf_odom_get_map", pf_odom_get_map(h_, which, xyz_.data(), rg_.data(), n, &n));
-        out.clear();
-        for (size_t i = 0; i < n; ++i) {
-            Point p;
-            p.x = xyz_[3 * i];
-            p.y = xyz_[3 * i + 1];
-            p.z = xyz_[3 * i + 2];
-            p.r = rg_[2 * i];        // rounds / age
-            p.g = rg_[2 * i + 1];    // observation count (p-index)
-            p.b = 0;
-            out.push_back(p);
-        }
     }
     int device_;
     size_t max_points_, map_capacity_;
     pf_odom* h_ = nullptr;
-    std::vector<float> xyz_;
-    std::vector<uint8_t> rg_;
 };
 
 // --------------------------------------------------------------------------------------------
 template <class CloudXYZRGB, class Lidar>
-class Odom_BPF_EstimationClassT {
+class Odom_BPF_EstimationClassT : public OdomBaseMembers {
 public:
     using Ptr = typename CloudXYZRGB::Ptr;
     using Point = typename std::decay<decltype(std::declval<CloudXYZRGB>().points[0])>::type;
@@ -267,6 +334,7 @@ public:
         op.theta_max = theta_max_para;
         op.weight_type = (int)weightType_para;
         check("pf_bpf_create", pf_bpf_create(&lp, &op, device_, max_points_, map_capacity_, &h_));
+        export_on_ = false;
         set_pose(kIdentity);
         for (Ptr* m : maps()) (*m)->clear();
         laserCloudMergeMap->clear();
@@ -274,6 +342,7 @@ public:
 
     // src/odomEstimationClass.cpp:685-691
     void initMapWithPoints(const Ptr& beam_in, const Ptr& pillar_in, const Ptr& facade_in) {
+        sync_export(h_, refresh_maps_every_frame);
         check("pf_bpf_init_map", pf_bpf_init_map(h_, data(beam_in), beam_in->points.size(), sizeof(Point),
                                                  data(pillar_in), pillar_in->points.size(), sizeof(Point),
                                                  data(facade_in), facade_in->points.size(), sizeof(Point)));
@@ -283,6 +352,7 @@ public:
     // src/odomEstimationClass.cpp:702-749
     void updatePointsToMap(const Ptr& beam_in, const Ptr& pillar_in, const Ptr& facade_in) {
         double pose[7];
+        sync_export(h_, refresh_maps_every_frame);
         const int rc = check("pf_bpf_update",
                              pf_bpf_update(h_, data(beam_in), beam_in->points.size(), sizeof(Point), data(pillar_in),
                                            pillar_in->points.size(), sizeof(Point), data(facade_in),
@@ -318,7 +388,7 @@ public:
     bool refresh_maps_every_frame = true;
     void syncMaps() {
         int c = 0;
-        for (Ptr* m : maps()) read_map(h_, c++, **m, xyz_, rg_);
+        for (Ptr* m : maps()) fill_map(h_, c++, **m);
         mergeFeatures(1);
     }
 
@@ -350,31 +420,12 @@ private:
 #endif
     }
     void refresh() {
+        pull_state(h_);
         if (refresh_maps_every_frame) syncMaps();
-    }
-    static void read_map(pf_odom* h, int which, CloudXYZRGB& out, std::vector<float>& xyz, std::vector<uint8_t>& rg) {
-        size_t n = 0;
-        check("pf_odom_get_map", pf_odom_get_map(h, which, nullptr, nullptr, 0, &n));
-        xyz.resize(3 * (n ? n : 1));
-        rg.resize(2 * (n ? n : 1));
-        check("pf_odom_get_map", pf_odom_get_map(h, which, xyz.data(), rg.data(), n, &n));
-        out.clear();
-        for (size_t i = 0; i < n; ++i) {
-            Point p;
-            p.x = xyz[3 * i];
-            p.y = xyz[3 * i + 1];
-            p.z = xyz[3 * i + 2];
-            p.r = rg[2 * i];
-            p.g = rg[2 * i + 1];
-            p.b = 0;
-            out.push_back(p);
-        }
     }
     int device_;
     size_t max_points_, map_capacity_;
     pf_odom* h_ = nullptr;
-    std::vector<float> xyz_;
-    std::vector<uint8_t> rg_;
 };
 
 // --------------------------------------------------------------------------------------------

@@ -43,9 +43,17 @@ int main(int argc, char** argv) {
         for (const auto& p : s->points) { mock::PointXYZRGB q; q.x = p.x; q.y = p.y; q.z = p.z; s2->push_back(q); }
         if (!inited) { odom.initMapWithPoints(e2, s2); inited = true; }
         else odom.updatePointsToMap(e2, s2);
-        std::fprintf(o, "%.17g %.17g %.17g %.17g %.17g %.17g %.17g %zu %zu\n", odom.odom.q[0], odom.odom.q[1],
+        std::fprintf(o, "%.17g %.17g %.17g %.17g %.17g %.17g %.17g %zu %zu", odom.odom.q[0], odom.odom.q[1],
                      odom.odom.q[2], odom.odom.q[3], odom.odom.t[0], odom.odom.t[1], odom.odom.t[2],
                      odom.laserCloudCornerMap->size(), odom.laserCloudSurfMap->size());
+        // the OdomBaseClass members (parameters, last_odom translation, optimization_count) and a
+        // checksum of the surf map's ages / p-index bytes (refreshed through the pinned map export)
+        for (int k = 0; k < 7; ++k) std::fprintf(o, " %.17g", odom.parameters[k]);
+        std::fprintf(o, " %.17g %.17g %.17g %d", odom.last_odom[3], odom.last_odom[7], odom.last_odom[11],
+                     odom.optimization_count);
+        unsigned long long cs = 0;
+        for (const auto& p : odom.laserCloudSurfMap->points) cs = cs * 1000003ull + (unsigned)p.r * 256u + p.g;
+        std::fprintf(o, " %llu\n", cs);
     }
     std::fclose(f);
     std::fclose(o);

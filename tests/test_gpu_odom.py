@@ -412,3 +412,50 @@ def test_s128_odometry_with_2m_point_map(pa, pfref, pfsynth):
     assert st["n_surf_map"] > 1_900_000 and st["n_surf_res"] > 500 and st["n_edge_res"] > 500
     _compare_maps(od, orc)
     assert worst[0] < TOL_T and worst[1] < TOL_R
+
+
+def test_snapshot_restore_continues_bit_identically(pa, pfsynth):
+    """pf_odom_snapshot after frame 6, pf_odom_restore into a fresh handle: frames 7..13 give the
+    bits of the uninterrupted run (poses, both maps with their age / p-index bytes, the
+    OdomBaseClass members); a snapshot does not load into a handle with other parameters."""
+    seq = pfsynth.Sequence("S64", n_frames=14, az_steps=1200)
+    frames = [seq.frame(k) for k in range(14)]
+    a = pa.Odom_ES_EstimationClass(device=0)
+    a.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    for k in range(7):
+        a.frame_host(frames[k])
+    blob = a.snapshot()
+    st6, pose6 = a.state(), a.odom
+    want = [a.frame_host(x) for x in frames[7:]]
+    b = pa.Odom_ES_EstimationClass(device=0)
+    b.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    b.restore(blob)
+    np.testing.assert_array_equal(b.odom, pose6)
+    s = b.state()
+    np.testing.assert_array_equal(s["parameters"], st6["parameters"])
+    assert s["optimization_count"] == st6["optimization_count"]
+    got = [b.frame_host(x) for x in frames[7:]]
+    np.testing.assert_array_equal(np.array(got), np.array(want))
+    for which in (0, 1):
+        np.testing.assert_array_equal(b._map(which)[0], a._map(which)[0])
+        np.testing.assert_array_equal(b._map(which)[1], a._map(which)[1])
+    c = pa.Odom_ES_EstimationClass(device=0)
+    c.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.0, 0, 0)           # other theta_p / theta_max
+    with pytest.raises(pa.PFError):
+        c.restore(blob)
+
+
+def test_map_export_equals_get_map(pa, pfsynth):
+    """pf_odom_set_map_export: the maps written into pinned host memory at the end of every frame
+    (graph replay and the update API) equal pf_odom_get_map's copy, every frame."""
+    seq = pfsynth.Sequence("S64", n_frames=12, az_steps=1000)
+    od = pa.Odom_ES_EstimationClass(device=0)
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    od.set_map_export(True)
+    for k in range(12):
+        od.frame_host(seq.frame(k))
+        for which in (0, 1):
+            ex, er = od.map_export(which)
+            gx, gr = od._map(which)
+            np.testing.assert_array_equal(ex, gx)
+            np.testing.assert_array_equal(er, gr)

@@ -25,6 +25,7 @@ def test_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
             x.astype(np.float32).tofile(f)
     subprocess.check_call([exe, str(tmp_path / "frames.bin"), str(tmp_path / "poses.txt")], timeout=120)
     got = np.loadtxt(tmp_path / "poses.txt")
+    lines = open(tmp_path / "poses.txt").read().splitlines()
     lid = pa.make_lidar(64, 3.0, 90.0)
     fe = pa.LaserProcessingClass()
     fe.init(lid)
@@ -39,6 +40,14 @@ def test_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
         np.testing.assert_array_equal(got[k, :7], od.odom)
         assert got[k, 7] == od.laserCloudCornerMap[0].shape[0]
         assert got[k, 8] == od.laserCloudSurfMap[0].shape[0]
+        st = od.state()                                      # OdomBaseClass members through the shim
+        np.testing.assert_array_equal(got[k, 9:16], st["parameters"])
+        np.testing.assert_array_equal(got[k, 16:19], st["last_odom"][:, 3])
+        assert got[k, 19] == st["optimization_count"]
+        cs = 0
+        for r, g in od.laserCloudSurfMap[1]:
+            cs = (cs * 1000003 + int(r) * 256 + int(g)) % (1 << 64)
+        assert int(lines[k].split()[20]) == cs
 
 
 def test_bpf_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
