@@ -64,6 +64,10 @@ def parse(argv=None):
                     help="skip the rocprofv3 PMC passes that measure the kNN kernel's fabric traffic")
     ap.add_argument("--bpf-frames", type=int, default=1000,
                     help="frames of the Odom_BPF_EstimationClass leg (SURVEY §8(f) rank 1); 0 = skip")
+    ap.add_argument("--leg-frames", type=int, default=1000,
+                    help="frames of each extra ES leg (configs[0] theta=0 on S64; the S64V dense scene at "
+                         "configs[1] and at theta=0); 0 = skip them")
+    ap.add_argument("--leg-cpu-seconds", type=float, default=8.0, help="CPU baseline sample of each extra leg")
     ap.add_argument("--host-leg", type=int, default=0,
                     help="also time N frames through pf_odom_frame_host (scan in host memory, PCIe copy "
                          "inside the timed region); reported as pcie_inclusive, never as value")
@@ -125,9 +129,9 @@ def lpt_assign(lengths, world):
     return out
 
 
-def load_frames(seq_id, total, threads):
-    """Yields (frame_index, [nf,cap,4] chunk, counts, description) of sequence `seq_id` (synthetic S64
-    with seed = seq_id, or KITTI sequence seq_id under PF_KITTI_ROOT)."""
+def load_frames(seq_id, total, threads, preset="S64"):
+    """Yields (frame_index, [nf,cap,4] chunk, counts, description) of sequence `seq_id` (synthetic
+    `preset` with seed = seq_id, or KITTI sequence seq_id under PF_KITTI_ROOT)."""
     import pfsynth
     rank = seq_id
     kroot = os.environ.get("PF_KITTI_ROOT")
@@ -143,12 +147,12 @@ def load_frames(seq_id, total, threads):
             counts[i] = f.shape[0]
         yield 0, buf, counts, "kitti-%02d" % rank
         return
-    seq = pfsynth.Sequence("S64", n_frames=total, seed=rank)
+    seq = pfsynth.Sequence(preset, n_frames=total, seed=rank)
     chunk = 256
     for f0 in range(0, total, chunk):
         nf = min(chunk, total - f0)
         buf, counts = seq.frames(f0, nf, threads=threads)
-        yield f0, buf, counts, "synthetic S64 seed %d" % rank
+        yield f0, buf, counts, "synthetic %s seed %d" % (preset, rank)
 
 
 def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier):
@@ -520,16 +524,16 @@ def cpu_baseline(budget_s, warmup):
     return out
 
 
-def _cpu_baseline(budget_s, warmup):
+def _cpu_baseline(budget_s, warmup, preset="S64", theta=(0.4, 75), max_frames=2000):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pfref
     import pfsynth
-    seq = pfsynth.Sequence("S64", n_frames=warmup + 2000, seed=0)
-    orc = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=0)
+    seq = pfsynth.Sequence(preset, n_frames=warmup + max_frames, seed=0)
+    orc = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, theta[0], theta[1], 0, opts=0)
     for k in range(warmup):
         orc.frame(seq.frame(k))
     n, el, k = 0, 0.0, warmup
-    while el < budget_s and n < 2000:
+    while el < budget_s and n < max_frames:
         x = seq.frame(k)
         t = time.perf_counter()
         orc.frame(x)
@@ -537,8 +541,85 @@ def _cpu_baseline(budget_s, warmup):
         n += 1
         k += 1
     return {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port", "frames": [warmup, k],
-            "sample": "pfref (oracle/, reference-faithful opts=0) frames %d..%d of the same S64 seed-0 sequence "
-                      "after %d warm-up frames, single thread, %.1f s of CPU time" % (warmup, k - 1, warmup, el)}
+            "sample": "pfref (oracle/, reference-faithful opts=0) frames %d..%d of the same %s seed-0 sequence "
+                      "after %d warm-up frames, single thread, %.1f s of CPU time" % (warmup, k - 1, preset, warmup, el)}
+
+
+ES_LEGS = {
+    # name: (preset, theta_p, theta_max, what it is)
+    "theta0": ("S64", 0.0, 0, "configs[0] parameters (k_new=0 theta_p=0 theta_max=0, FLOAM-equivalent) on S64"),
+    "dense": ("S64V", 0.4, 75, "configs[1] parameters on S64V: residential scene with vegetation and rough "
+                               "ground, denser features and maps than S64 (KITTI-00-like sizes)"),
+    "dense_theta0": ("S64V", 0.0, 0, "configs[0] parameters on S64V (the largest maps: no stability filter)"),
+}
+
+
+def es_leg(name, device, nframes, threads, cpu_seconds, warmup=20, use_graph=True, with_cpu=True):
+    """One extra ES line: the device pipeline over `nframes` frames of the leg's sequence (scans
+    HBM-resident, graph replay, timed like the headline), then the same frames again on a fresh handle
+    with per-stage device timing (pf_odom_set_stage_timing: stage A = featureExtraction + VoxelGrid,
+    stage B = odometry), and the CPU port on the leg's first frames after the same warm-up."""
+    import pfilter_amd as pa
+    preset, tp, tm, what = ES_LEGS[name]
+    cfg = dict(ODOM_CFG, theta_p=tp, theta_max=tm)
+    total = warmup + nframes
+    bufs, ptrs = [], []
+    for _, buf, counts, _ in load_frames(0, total, threads, preset):
+        db = pa.DeviceBuffer(buf.nbytes, device=device)
+        db.upload(buf)
+        ptrs += [(db.ptr + i * buf.shape[1] * 16, int(counts[i])) for i in range(buf.shape[0])]
+        bufs.append(db)
+
+    def run(timing):
+        od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
+        od.init(lidar_cfg(), **cfg)
+        od.set_graph(use_graph)
+        for k in range(warmup):
+            od.frame_device(*ptrs[k])
+        od.sync()
+        if timing:
+            od.set_stage_timing(True)
+        t0 = time.perf_counter()
+        for k in range(warmup, total):
+            od.frame_device(*ptrs[k])
+        od.sync()
+        el = time.perf_counter() - t0
+        st = od.stats()
+        assert st["errors"] == 0
+        return el, st, (od.stage_times() if timing else None)
+
+    el, st, _ = run(False)
+    _, _, stg = run(True)
+    out = {"value": round(nframes / el, 2), "unit": "frames/s", "frames": nframes, "ms_per_step": round(el / nframes * 1e3, 4),
+           "workload": what, "sequence": "synthetic %s seed 0" % preset,
+           "stage_us": {"A_features_voxelgrid": round(stg["a_us"], 1), "B_odometry": round(stg["b_us"], 1),
+                        "frames": stg["frames"]},
+           "last_frame": {k: st[k] for k in ("n_in", "n_ds", "n_map", "n_res")}}
+    if with_cpu:
+        with pinned_core() as pc:
+            cb = _cpu_baseline(cpu_seconds, warmup, preset=preset, theta=(tp, tm), max_frames=nframes)
+            cb["host"] = pc.host()
+        f0, f1 = cb.pop("frames")
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu"] = round(out["value"] / cb["value"], 2)
+    return out
+
+
+def stage_pass(device, ptrs, warmup, nframes, use_graph=True):
+    """Per-stage device time of the headline workload: the first `nframes` timed frames again on a
+    fresh handle with pf_odom_set_stage_timing (outside the timed region)."""
+    import pfilter_amd as pa
+    od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
+    od.init(lidar_cfg(), **ODOM_CFG)
+    od.set_graph(use_graph)
+    for k in range(warmup):
+        od.frame_device(*ptrs[k])
+    od.sync()
+    od.set_stage_timing(True)
+    for k in range(warmup, min(len(ptrs), warmup + nframes)):
+        od.frame_device(*ptrs[k])
+    st = od.stage_times()
+    return {"A_features_voxelgrid": round(st["a_us"], 1), "B_odometry": round(st["b_us"], 1), "frames": st["frames"]}
 
 
 def gpu_window(device, f0, f1, threads, use_graph=True):
@@ -657,6 +738,8 @@ def main(argv=None):
                    "graph": not args.no_graph},
     }
     log("pipeline: %d frames in %.3f s, last-frame stats %s" % (frames, elapsed, r["stats"]))
+    if world == 1 and not stub:
+        out["stage_us"] = stage_pass(local_rank, r["ptrs"], args.warmup, min(1000, frames), not args.no_graph)
     if stub:
         out["stub"] = True
     elif world == 1 and not args.no_roofline:
@@ -672,6 +755,14 @@ def main(argv=None):
         except Exception as e:  # report, never hide
             log("bpf leg failed: %r" % (e,))
             out["bpf"] = None
+    if world == 1 and args.leg_frames > 0 and not stub:
+        for name in ES_LEGS:
+            try:
+                out[name] = es_leg(name, local_rank, args.leg_frames, threads, args.leg_cpu_seconds,
+                                   use_graph=not args.no_graph, with_cpu=not args.no_cpu)
+            except Exception as e:  # report, never hide
+                log("%s leg failed: %r" % (name, e))
+                out[name] = None
     if world == 1 and args.host_leg > 0 and not stub:
         out["pcie_inclusive"] = host_leg(local_rank, args.host_leg, threads)
     if world == 1 and not args.no_cpu and not stub:

@@ -249,6 +249,14 @@ int pf_odom_set_map_export(pf_odom* h, int enable);
 int pf_odom_map_export(pf_odom* h, int which, const float** xyzw, size_t* n);
 /* enable/disable hipGraph replay of the steady-state frame (default on) */
 int pf_odom_set_graph(pf_odom* h, int enable);
+/* Per-stage device time (the reference's per-stage timers, src/laserProcessingNode.cpp:71-79 and
+ * src/odomEstimationNode copy.cpp:92-100, as HIP events on the handle's two streams): with enable,
+ * every frame records when stage A (featureExtraction / front end + VoxelGrid) and stage B (the
+ * odometry) start and end on the device. stage_times waits for the handle's work and returns the mean
+ * stage A and stage B durations (us) over the frames since the last enable, and how many. Adds four
+ * event records per frame: leave it off in timed runs. */
+int pf_odom_set_stage_timing(pf_odom* h, int enable);
+int pf_odom_stage_times(pf_odom* h, double* a_us, double* b_us, size_t* frames);
 
 /* ---------------- device memory helpers (scan staging without a framework) ---------------- */
 int pf_device_count(int* n);

@@ -46,10 +46,59 @@ struct pf_fe {
     std::vector<float4> host;
 };
 
+// per-stage device timing (pf_odom_set_stage_timing): a ring of event quadruples {A start, A end,
+// B start, B end}; a quadruple is harvested (its elapsed times summed) before its ring slot is reused
+struct StageTiming {
+    static constexpr int kRing = 256;
+    bool on = false;
+    hipEvent_t ev[kRing][4] = {};
+    bool pending[kRing] = {};
+    long long next = 0;
+    double sum_a = 0, sum_b = 0;
+    size_t frames = 0;
+};
+
 struct pf_odom {
     OdomGPU o;
     std::vector<float4> host[kMaxC];
+    StageTiming* timing = nullptr;
 };
+
+static int timing_harvest(StageTiming& t, int j) {
+    if (!t.pending[j]) return PF_OK;
+    PF_HIP_TRY(hipEventSynchronize(t.ev[j][3]));
+    float a = 0.f, b = 0.f;
+    PF_HIP_TRY(hipEventElapsedTime(&a, t.ev[j][0], t.ev[j][1]));
+    PF_HIP_TRY(hipEventElapsedTime(&b, t.ev[j][2], t.ev[j][3]));
+    t.sum_a += 1e3 * a;
+    t.sum_b += 1e3 * b;
+    t.frames++;
+    t.pending[j] = false;
+    return PF_OK;
+}
+static void timing_free(pf_odom* h) {
+    if (!h->timing) return;
+    for (auto& q : h->timing->ev)
+        for (hipEvent_t& e : q)
+            if (e) (void)hipEventDestroy(e);
+    delete h->timing;
+    h->timing = nullptr;
+}
+// marks k = 0..3 (A start, A end, B start, B end) of the current frame
+static int timing_mark(pf_odom* h, int k) {
+    StageTiming* t = h->timing;
+    if (!t || !t->on) return PF_OK;
+    const int j = (int)(t->next % StageTiming::kRing);
+    if (k == 0) {
+        if (int rc = timing_harvest(*t, j)) return rc;
+    }
+    PF_HIP_TRY(hipEventRecord(t->ev[j][k], k < 2 ? h->o.stream_a : h->o.stream));
+    if (k == 3) {
+        t->pending[j] = true;
+        t->next++;
+    }
+    return PF_OK;
+}
 
 
 extern "C" {
@@ -163,6 +212,7 @@ int pf_odom_destroy(pf_odom* h) {
     (void)hipSetDevice(h->o.device);
     (void)hipStreamSynchronize(h->o.stream_a);
     (void)hipStreamSynchronize(h->o.stream);
+    timing_free(h);
     odom_destroy(h->o);
     delete h;
     return PF_OK;
@@ -457,6 +507,7 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
     const bool steady = o.inited && o.opt_count_host <= 2 && o.graph_enabled;
     if (scan && n > o.in_cap) return PF_ECAPACITY;
     int rc = stage_a_begin(h, p);
+    if (!rc) rc = timing_mark(h, 0);
     if (rc) return rc;
     if (nc == 2 || scan) {
         if (n > o.in_cap) return PF_ECAPACITY;
@@ -482,7 +533,9 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
         else if (scan) stage_enqueue_front(o, p, o.stream_a);
         if (o.inited) stage_enqueue_vg(o, p, o.stream_a);
     }
-    rc = stage_a_end_b_begin(h, p);
+    rc = timing_mark(h, 1);
+    if (!rc) rc = stage_a_end_b_begin(h, p);
+    if (!rc) rc = timing_mark(h, 2);
     if (rc) return rc;
     if (steady) {
         if (!o.graph_b[p]) {
@@ -497,6 +550,8 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
         odom_enqueue_update(o, p, o.stream);
         odom_enqueue_export(o, o.stream);
     }
+    rc = timing_mark(h, 3);
+    if (rc) return rc;
     return stage_b_end(h, p);
 }
 
@@ -599,6 +654,49 @@ int pf_odom_sync(pf_odom* h) {
     PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
     PF_HIP_TRY(hipGetLastError());
     return sticky_status(h->o);
+}
+
+int pf_odom_set_stage_timing(pf_odom* h, int enable) {
+    if (!h) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    PF_HIP_TRY(hipStreamSynchronize(h->o.stream_a));
+    PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
+    if (!enable) {
+        timing_free(h);
+        return PF_OK;
+    }
+    if (!h->timing) {
+        h->timing = new StageTiming();
+        for (auto& q : h->timing->ev)
+            for (hipEvent_t& e : q)
+                if (hipEventCreate(&e) != hipSuccess) {
+                    timing_free(h);
+                    return PF_EHIP;
+                }
+    }
+    StageTiming& t = *h->timing;
+    for (bool& pd : t.pending) pd = false;
+    t.next = 0;
+    t.sum_a = t.sum_b = 0;
+    t.frames = 0;
+    t.on = true;
+    return PF_OK;
+}
+
+int pf_odom_stage_times(pf_odom* h, double* a_us, double* b_us, size_t* frames) {
+    if (!h) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    PF_HIP_TRY(hipStreamSynchronize(h->o.stream_a));
+    PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
+    StageTiming* t = h->timing;
+    if (t)
+        for (int j = 0; j < StageTiming::kRing; ++j)
+            if (int rc = timing_harvest(*t, j)) return rc;
+    const size_t f = t ? t->frames : 0;
+    if (frames) *frames = f;
+    if (a_us) *a_us = f ? t->sum_a / (double)f : 0.0;
+    if (b_us) *b_us = f ? t->sum_b / (double)f : 0.0;
+    return PF_OK;
 }
 
 int pf_odom_poses(pf_odom* h, double* poses, size_t cap, size_t* n) {

@@ -90,7 +90,8 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_cls_classify", "pf_cls_ground_seg", "pf_bpf_set_front_end", "pf_bpf_frame_scan_device", "pf_map_create", "pf_map_destroy", "pf_map_update",
            "pf_map_update_device", "pf_map_update_mat", "pf_map_get", "pf_odom_set_stage_a_reserve",
            "pf_fe_set_ring_model", "pf_odom_set_ring_model", "pf_odom_get_state", "pf_odom_snapshot",
-           "pf_odom_restore", "pf_odom_set_map_export", "pf_odom_map_export"]
+           "pf_odom_restore", "pf_odom_set_map_export", "pf_odom_map_export", "pf_odom_set_stage_timing",
+           "pf_odom_stage_times"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -122,6 +123,9 @@ def lib():
     L.pf_odom_sync.argtypes = [_vp]
     L.pf_odom_poses.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
     L.pf_odom_set_graph.argtypes = [_vp, _i]
+    L.pf_odom_set_stage_timing.argtypes = [_vp, _i]
+    L.pf_odom_stage_times.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(_sz)]
     if hasattr(L, "pf_odom_set_stage_a_reserve"):
         L.pf_odom_set_stage_a_reserve.argtypes = [_vp, _i]
     L.pf_fe_set_ring_model.argtypes = [_vp, ctypes.c_double, ctypes.c_double]
@@ -367,6 +371,17 @@ class Odom_ES_EstimationClass:
 
     def set_graph(self, enable):
         _check("pf_odom_set_graph", lib().pf_odom_set_graph(self._h, int(bool(enable))))
+
+    def set_stage_timing(self, enable):
+        _check("pf_odom_set_stage_timing", lib().pf_odom_set_stage_timing(self._h, int(bool(enable))))
+
+    def stage_times(self):
+        """{a_us, b_us, frames}: mean device time of stage A (features + VoxelGrid) and stage B (odometry)
+        per frame since set_stage_timing(True)"""
+        a, b, n = ctypes.c_double(), ctypes.c_double(), _sz()
+        _check("pf_odom_stage_times", lib().pf_odom_stage_times(self._h, ctypes.byref(a), ctypes.byref(b),
+                                                                ctypes.byref(n)))
+        return {"a_us": a.value, "b_us": b.value, "frames": n.value}
 
     # ---- OdomBaseClass public members and state capture ----
     def state(self):

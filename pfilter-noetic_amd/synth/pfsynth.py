@@ -28,7 +28,7 @@ class Params(ctypes.Structure):
                 ("range_noise", ctypes.c_double), ("max_range", ctypes.c_double),
                 ("sensor_height", ctypes.c_double), ("building_prob", ctypes.c_double),
                 ("setback_min", ctypes.c_double), ("setback_max", ctypes.c_double),
-                ("seed", ctypes.c_int)]
+                ("seed", ctypes.c_int), ("vegetation", ctypes.c_double), ("terrain", ctypes.c_double)]
 
 
 _lib = None
@@ -52,7 +52,7 @@ def lib():
     return _lib
 
 
-PRESETS = {"S64": 0, "S32": 1, "S128": 2}
+PRESETS = {"S64": 0, "S32": 1, "S128": 2, "S64V": 3}
 
 
 class Sequence:

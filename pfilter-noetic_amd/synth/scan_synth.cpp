@@ -30,8 +30,11 @@ struct Rng {  // sequential generator for world building
     double u(double a, double b) { return a + (b - a) * u(); }
 };
 
-struct Box { double cx, cy, c, s, hx, hy, z0, z1, br; };
+struct Box { double cx, cy, c, s, hx, hy, z0, z1, br, pen; uint64_t key; };   // pen > 0: porous (hedge)
 struct Cyl { double cx, cy, r, z0, z1; };
+struct Sph { double cx, cy, cz, r; uint64_t key; };               // porous tree crown
+constexpr double kCrownPen = 0.35;                                // mean penetration depth into foliage (m)
+constexpr int kSphBase = 1 << 28;                                 // primitive ids >= kSphBase: crowns
 
 struct PathSample { double x, y, psi; };
 
@@ -43,6 +46,7 @@ struct World {
     std::vector<PathSample> path;
     std::vector<Box> boxes;
     std::vector<Cyl> cyls;
+    std::vector<Sph> sphs;
     std::vector<double> elev;  // beam elevations (rad)
 
     double heading_at_time(double t) const {
@@ -93,11 +97,23 @@ void build_path(World& w) {
     }
 }
 
-void add_box(World& w, double cx, double cy, double psi, double hx, double hy, double z0, double z1) {
+// a porous object's hash key from its position (not its index: the scene of a longer sequence has
+// more objects, and a prefix must stay the same scene)
+inline uint64_t obj_key(double cx, double cy) {
+    uint64_t a, b;
+    std::memcpy(&a, &cx, 8);
+    std::memcpy(&b, &cy, 8);
+    return mix64(a ^ mix64(b));
+}
+
+void add_box(World& w, double cx, double cy, double psi, double hx, double hy, double z0, double z1,
+             double pen = 0.0) {
     Box b;
     b.cx = cx; b.cy = cy; b.c = std::cos(psi); b.s = std::sin(psi);
     b.hx = hx; b.hy = hy; b.z0 = z0; b.z1 = z1;
     b.br = std::sqrt(hx * hx + hy * hy);
+    b.pen = pen;
+    b.key = obj_key(cx, cy);
     w.boxes.push_back(b);
 }
 
@@ -155,7 +171,64 @@ void build_scene(World& w) {
             }
             s += rng.u(6.0, 20.0);
         }
+        if (w.p.vegetation <= 0) continue;
+        // trees: a trunk and a porous crown, spacing shrinking with the vegetation density
+        rng = Rng(base + 3);
+        s = s_begin + rng.u(0.0, 6.0);
+        while (s < s_end) {
+            PathSample ps = w.at_s(s);
+            double lat = rng.u(5.5, 16.0) * side;
+            double cx = ps.x - std::sin(ps.psi) * lat, cy = ps.y + std::cos(ps.psi) * lat;
+            double r = rng.u(1.5, 3.5);
+            double cz = rng.u(2.5, 5.5) + 0.5 * r;
+            Cyl t;
+            t.cx = cx; t.cy = cy; t.r = rng.u(0.12, 0.3); t.z0 = 0.0; t.z1 = cz - 0.5 * r;
+            w.cyls.push_back(t);
+            w.sphs.push_back(Sph{cx, cy, cz, r, obj_key(cx, cy)});
+            s += rng.u(4.0, 12.0) / w.p.vegetation;
+        }
+        // the wooded background behind the kerb-side row (yards, parks): crowns only, denser
+        rng = Rng(base + 5);
+        s = s_begin + rng.u(0.0, 3.0);
+        while (s < s_end) {
+            PathSample ps = w.at_s(s);
+            double lat = rng.u(16.0, 60.0) * side;
+            double r = rng.u(2.0, 5.0);
+            double cz = rng.u(3.0, 8.0) + 0.5 * r;
+            double cx = ps.x - std::sin(ps.psi) * lat, cy = ps.y + std::cos(ps.psi) * lat;
+            Cyl t;
+            t.cx = cx; t.cy = cy; t.r = rng.u(0.15, 0.4); t.z0 = 0.0; t.z1 = cz - 0.5 * r;
+            w.cyls.push_back(t);
+            w.sphs.push_back(Sph{cx, cy, cz, r, obj_key(cx, cy)});
+            s += rng.u(2.0, 6.0) / w.p.vegetation;
+        }
+        // hedges and bushes along the kerb: porous boxes
+        rng = Rng(base + 4);
+        s = s_begin + rng.u(0.0, 8.0);
+        while (s < s_end) {
+            double L = rng.u(2.0, 10.0);
+            if (rng.u() < 0.6 * std::min(1.0, w.p.vegetation)) {
+                PathSample ps = w.at_s(s + 0.5 * L);
+                double lat = rng.u(4.5, 7.0) * side;
+                add_box(w, ps.x - std::sin(ps.psi) * lat, ps.y + std::cos(ps.psi) * lat, ps.psi + rng.u(-0.1, 0.1),
+                        0.5 * L, 0.5 * rng.u(0.6, 1.5), 0.0, rng.u(0.6, 1.8), 0.25);
+            }
+            s += L + rng.u(3.0, 15.0);
+        }
     }
+}
+
+// rough ground: bilinear value noise on a 0.7 m lattice, amplitude p.terrain
+double terrain_h(const World& w, double x, double y) {
+    const double g = 0.7;
+    const double fx = std::floor(x / g), fy = std::floor(y / g);
+    const double ax = x / g - fx, ay = y / g - fy;
+    auto v = [&](double i, double j) {
+        return 2.0 * u01(key4((uint64_t)w.p.seed, (uint64_t)(int64_t)i, (uint64_t)(int64_t)j, 77)) - 1.0;
+    };
+    const double a = v(fx, fy) * (1 - ax) + v(fx + 1, fy) * ax;
+    const double b = v(fx, fy + 1) * (1 - ax) + v(fx + 1, fy + 1) * ax;
+    return w.p.terrain * (a * (1 - ay) + b * ay);
 }
 
 void build_beams(World& w) {
@@ -175,7 +248,7 @@ void build_beams(World& w) {
 }
 
 inline bool hit_box(const Box& b, double ox, double oy, double oz, double dx, double dy, double dz,
-                    double& t) {
+                    double& t, uint64_t hash = 0) {
     double px = ox - b.cx, py = oy - b.cy;
     double lx = b.c * px + b.s * py, ly = -b.s * px + b.c * py;
     double ux = b.c * dx + b.s * dy, uy = -b.s * dx + b.c * dy;
@@ -191,7 +264,29 @@ inline bool hit_box(const Box& b, double ox, double oy, double oz, double dx, do
     if (!slab(lx, ux, -b.hx, b.hx)) return false;
     if (!slab(ly, uy, -b.hy, b.hy)) return false;
     if (!slab(oz, dz, b.z0, b.z1)) return false;
+    if (b.pen > 0) {                        // porous: the ray stops inside or passes through
+        const double d = -std::log(std::max(u01(hash), 1e-300)) * b.pen;
+        if (t0 + d > t1) return false;
+        t = t0 + d;
+        return true;
+    }
     t = t0;
+    return true;
+}
+
+inline bool hit_sph(const Sph& c, double ox, double oy, double oz, double dx, double dy, double dz, double& t,
+                    uint64_t hash) {
+    const double px = ox - c.cx, py = oy - c.cy, pz = oz - c.cz;
+    const double B = px * dx + py * dy + pz * dz;            // |d| = 1
+    const double C = px * px + py * py + pz * pz - c.r * c.r;
+    const double disc = B * B - C;
+    if (disc < 0) return false;
+    const double sq = std::sqrt(disc);
+    const double t0 = std::max(-B - sq, 1e-3), t1 = -B + sq;
+    if (t1 <= t0) return false;
+    const double d = -std::log(std::max(u01(hash), 1e-300)) * kCrownPen;
+    if (t0 + d > t1) return false;          // through a gap in the foliage
+    t = t0 + d;
     return true;
 }
 
@@ -242,6 +337,8 @@ size_t cast_frame(const World& w, int frame, float* out, size_t cap, int* ring_o
         add_interval((int)i, w.boxes[i].cx, w.boxes[i].cy, w.boxes[i].br);
     for (size_t i = 0; i < w.cyls.size(); ++i)
         add_interval(~(int)i, w.cyls[i].cx, w.cyls[i].cy, w.cyls[i].r);
+    for (size_t i = 0; i < w.sphs.size(); ++i)
+        add_interval(kSphBase + (int)i, w.sphs[i].cx, w.sphs[i].cy, w.sphs[i].r);
 
     const int L = (int)w.elev.size();
     size_t n = 0;
@@ -264,12 +361,20 @@ size_t cast_frame(const World& w, int frame, float* out, size_t cap, int* ring_o
             bool hit = false;
             if (dz < -1e-12) {
                 double tg = -sz / dz;
-                if (tg < best) { best = tg; hit = true; }
+                if (p.terrain > 0) {            // one fixed-point step onto the height field
+                    const double h = terrain_h(w, sx + tg * dx, sy + tg * dy);
+                    tg = (h - sz) / dz;
+                }
+                if (tg > 0 && tg < best) { best = tg; hit = true; }
             }
             for (int id : cand) {
                 double th;
-                if (id >= 0) {
-                    if (hit_box(w.boxes[id], sx, sy, sz, dx, dy, dz, th) && th < best) { best = th; hit = true; }
+                if (id >= kSphBase) {
+                    const uint64_t hs = key4((uint64_t)p.seed, (uint64_t)frame, ray, w.sphs[id - kSphBase].key);
+                    if (hit_sph(w.sphs[id - kSphBase], sx, sy, sz, dx, dy, dz, th, hs) && th < best) { best = th; hit = true; }
+                } else if (id >= 0) {
+                    const uint64_t hs = w.boxes[id].pen > 0 ? key4((uint64_t)p.seed, (uint64_t)frame, ray, w.boxes[id].key) : 0;
+                    if (hit_box(w.boxes[id], sx, sy, sz, dx, dy, dz, th, hs) && th < best) { best = th; hit = true; }
                 } else {
                     if (hit_cyl(w.cyls[~id], sx, sy, sz, dx, dy, dz, th) && th < best) { best = th; hit = true; }
                 }
@@ -313,6 +418,10 @@ void pfsyn_default_params(int preset, pfsyn_params* p) {
     } else if (preset == 2) {   // S128
         p->lines = 128; p->az_steps = 1563; p->speed = 10.0; p->seed = 5;
         p->building_prob = 0.85; p->setback_min = 6.0; p->setback_max = 20.0;
+    } else if (preset == 3) {   // S64V: residential, vegetation and rough ground (KITTI-00 density)
+        p->lines = 64; p->az_steps = 2000; p->speed = 8.0; p->seed = 0;
+        p->building_prob = 0.35; p->setback_min = 8.0; p->setback_max = 30.0;
+        p->vegetation = 1.0; p->terrain = 0.08;
     } else {                    // S64 KITTI-like
         p->lines = 64; p->az_steps = 2000; p->speed = 10.0; p->seed = 0;
         p->building_prob = 0.85; p->setback_min = 6.0; p->setback_max = 20.0;

@@ -3,7 +3,8 @@
  *
  * This is workload input for tests and bench.py, not part of the odometry hot
  * path. The scene model follows SURVEY.md §8(d): ground plane 1.73 m below the
- * sensor, box buildings set back from a curving road, poles and parked cars,
+ * sensor, box buildings set back from a curving road, poles and parked cars (S64V adds
+ * porous tree crowns, trunks and hedges and a rough ground height field),
  * ray-cast per beam/azimuth with N(0, 0.02 m) range noise and random dropout.
  * Points are emitted azimuth-major (all beams of one azimuth step, then the
  * next), so each ring is in azimuth order, as in a Velodyne sweep.
@@ -29,9 +30,12 @@ typedef struct {
     double building_prob;   /* probability a building slot is filled */
     double setback_min, setback_max;
     int seed;
+    double vegetation;      /* 0: none; > 0: trees / hedges per metre of road (porous volumes) */
+    double terrain;         /* amplitude (m) of the rough-ground height field (0: flat) */
 } pfsyn_params;
 
-/* preset 0: S64 KITTI-like (config 1/2/4), 1: S32 campus (config 3), 2: S128 (config 5) */
+/* preset 0: S64 KITTI-like (config 1/2/4), 1: S32 campus (config 3), 2: S128 (config 5),
+ * 3: S64V, S64 in a residential scene with vegetation and rough ground (KITTI-00 density) */
 void pfsyn_default_params(int preset, pfsyn_params* p);
 
 /* Builds the world along the trajectory for n_frames frames. Returns NULL on error. */

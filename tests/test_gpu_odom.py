@@ -84,6 +84,45 @@ def test_campus_32_line(pa, pfref, pfsynth):
     _run(od, orc, seq, range(12), check_maps_every=11)
 
 
+@pytest.mark.parametrize("theta_p,theta_max", [(0.4, 75), (0.0, 0)])
+def test_dense_vegetation_scene(pa, pfref, pfsynth, theta_p, theta_max):
+    """S64V (bench.py's dense legs): porous tree crowns, hedges and rough ground give about twice the
+    down-sampled surf points of S64 and, at theta = 0, maps of 4e4-9e4 points (SURVEY §8 KITTI sizes)."""
+    seq = pfsynth.Sequence("S64V", n_frames=40)
+    od, orc = _pair(pa, pfref, theta_p=theta_p, theta_max=theta_max)
+    _run(od, orc, seq, range(30), check_maps_every=14)
+    _compare_maps(od, orc)
+
+
+def test_stage_timing(pa, pfsynth):
+    """pf_odom_set_stage_timing / pf_odom_stage_times: per-stage device time over the frames since
+    enable; results unchanged by the event records."""
+    seq = pfsynth.Sequence("S64", n_frames=30, az_steps=1500)
+    buf, counts = seq.frames(0, 30)
+    db = pa.DeviceBuffer(buf.nbytes)
+    db.upload(buf)
+    ptr = lambda k: (db.ptr + k * buf.shape[1] * 16, int(counts[k]))
+    runs = []
+    for timing in (False, True):
+        od = pa.Odom_ES_EstimationClass(device=0)
+        od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+        for k in range(12):
+            od.frame_device(*ptr(k))
+        if timing:
+            od.set_stage_timing(True)
+        for k in range(12, 30):
+            od.frame_device(*ptr(k))
+        od.sync()
+        runs.append(od.poses())
+        if timing:
+            st = od.stage_times()
+            assert st["frames"] == 18
+            assert 5.0 < st["a_us"] < 5e4 and 5.0 < st["b_us"] < 5e4, st
+            od.set_stage_timing(False)
+            assert od.stage_times()["frames"] == 0
+    np.testing.assert_array_equal(runs[0], runs[1])
+
+
 def test_update_api_matches_oracle(pa, pfref, pfsynth):
     """initMapWithPoints / updatePointsToMap with host-side features (the node's call pattern)."""
     seq = pfsynth.Sequence("S64", n_frames=10, az_steps=1500)

@@ -66,3 +66,23 @@ def test_s128_rings_round_trip_the_linear_model(pfsynth, pfref):
     assert e.shape[0] > 128 * 6 * 5 and su.shape[0] > 40000
     e0, s0 = pfref.feature_extraction(x, pfref.make_lidar(128, 3.0, 90.0), opts=pfref.FE_STABLE_TIES)
     assert e0.shape[0] <= 6 * 20                               # the reference: every point in ring 0
+
+
+def test_s64v_vegetation_scene(pfsynth, pfref):
+    """S64V: the S64 sensor in a residential scene (fewer buildings, porous tree crowns and hedges,
+    a rough ground height field). Deterministic like S64, and denser where the odometry works: more
+    down-sampled surf points per frame (VoxelGrid 0.8 m of featureExtraction's surf cloud)."""
+    a = pfsynth.Sequence("S64V", n_frames=10, az_steps=1000)
+    b = pfsynth.Sequence("S64V", n_frames=300, az_steps=1000)
+    np.testing.assert_array_equal(a.frame(4), b.frame(4))
+    buf1, c1 = a.frames(2, 3, threads=1)
+    buf3, c3 = a.frames(2, 3, threads=3)
+    np.testing.assert_array_equal(c1, c3)
+    np.testing.assert_array_equal(buf1[1, :int(c1[1])], buf3[1, :int(c3[1])])
+    lid = pfref.make_lidar(64, 3.0, 90.0)
+    ds = {}
+    for preset in ("S64", "S64V"):
+        x = pfsynth.Sequence(preset, n_frames=30).frame(25)
+        e, su = pfref.feature_extraction(x, lid, opts=pfref.FE_STABLE_TIES)
+        ds[preset] = pfref.voxel_grid(su, 0.8).shape[0]
+    assert ds["S64V"] > 1.5 * ds["S64"], ds
