@@ -233,6 +233,12 @@ int pf_odom_set_ring_model(pf_odom* h, double top_deg, double bottom_deg);
  * (q_w_curr = parameters[0..3] as x, y, z, w; t_w_curr = parameters[4..6]) after the last solve,
  * `last_odom` as a row-major 3 x 4 [R | t], and `optimization_count`. Any output may be NULL. */
 int pf_odom_get_state(pf_odom* h, double parameters[7], double last_odom[12], int* optimization_count);
+/* Sets those members from poses {qx, qy, qz, qw, tx, ty, tz}: odom = (R(q), t) and parameters =
+ * odom_pose, last_odom from last_pose (NULL: the same pose), and optimization_count. With
+ * pf_odom_set_map it resumes a handle from an externally held estimator state (a reference node's
+ * members, or the oracle's in the per-frame parity test); the handle is marked initialised, so the
+ * next frame runs updatePointsToMap. */
+int pf_odom_set_state(pf_odom* h, const double odom_pose[7], const double last_pose[7], int optimization_count);
 /* Snapshot of a handle's whole estimator state (pose, last pose, optimization count, the maps with
  * their age / p-index bytes, the counters), for golden-vector capture and checkpoint / resume. buf NULL:
  * *size = the bytes needed. restore() loads a snapshot into a handle created with the same parameters

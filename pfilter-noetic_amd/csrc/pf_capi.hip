@@ -8,6 +8,7 @@
 
 #include "pf_fe.h"
 #include "pf_odom.h"
+#include "pf_geom.h"
 
 using namespace pf;
 
@@ -755,6 +756,33 @@ int pf_odom_get_state(pf_odom* h, double parameters[7], double last_odom[12], in
         }
     if (optimization_count) *optimization_count = st.optimization_count;
     return sticky_status(o);
+}
+
+int pf_odom_set_state(pf_odom* h, const double odom_pose[7], const double last_pose[7], int optimization_count) {
+    if (!h || !odom_pose || optimization_count < 0) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    DevState st;
+    PF_HIP_TRY(hipMemcpy(&st, o.st, sizeof(st), hipMemcpyDeviceToHost));
+    const double* lp = last_pose ? last_pose : odom_pose;
+    const pf::m3 R = pf::q2m(pf::qd{odom_pose[0], odom_pose[1], odom_pose[2], odom_pose[3]});
+    const pf::m3 L = pf::q2m(pf::qd{lp[0], lp[1], lp[2], lp[3]});
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) {
+            st.odomR[3 * i + j] = R.m[i][j];
+            st.lastR[3 * i + j] = L.m[i][j];
+        }
+        st.odomt[i] = odom_pose[4 + i];
+        st.lastt[i] = lp[4 + i];
+    }
+    for (int k = 0; k < 7; ++k) st.params[k] = odom_pose[k];
+    st.optimization_count = optimization_count;
+    PF_HIP_TRY(hipMemcpy(o.st, &st, sizeof(st), hipMemcpyHostToDevice));
+    o.opt_count_host = optimization_count;
+    o.inited = true;                       // the next frame runs updatePointsToMap on the set maps
+    return PF_OK;
 }
 
 namespace {

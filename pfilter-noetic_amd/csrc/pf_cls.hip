@@ -33,11 +33,32 @@ struct ClsDev {          // kernel view of ClsGPU
     int* ptnum;
     float4* box;
     int* sticky;         // optional: a sticky copy of CC_ERR (the odometry handle's error word)
+    u32 cap;             // allocation sizes, for the bounds-checked development build (PF_DEV_BOUNDS)
+    u32 cell_cap;
 };
 ClsDev dev_view(ClsGPU& c) {
     return ClsDev{c.prm, c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals,
-                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.box, c.sticky};
+                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.box, c.sticky, (u32)c.cap, (u32)c.grid.cell_cap};
 }
+
+// Development build with -DPF_DEV_BOUNDS (tools/build_variant.sh): every indexed global access of the
+// front-end kernels is checked against its allocation; a violation sets cnt[CC_ERR] = 2 and, inside
+// a BPF handle, its sticky error word (the C ABI then returns PF_ECAPACITY, so a test fails loudly)
+// and the access is redirected to element 0. The
+// shipped build compiles the checks out. Used to audit the index math (front-end faults).
+#ifdef PF_DEV_BOUNDS
+#define PF_IDX(d, i, bound) pf_idx_checked((d), (long long)(i), (long long)(bound))
+__device__ __forceinline__ long long pf_idx_checked(const ClsDev& d, long long i, long long bound) {
+    if (i < 0 || i >= bound) {
+        d.cnt[CC_ERR] = 2;
+        if (d.sticky) *d.sticky = 2;     // the odometry handle's error word: PF_ECAPACITY at its sync
+        return 0;
+    }
+    return i;
+}
+#else
+#define PF_IDX(d, i, bound) (i)
+#endif
 
 __device__ __forceinline__ float wave_minf(float v) {
 #pragma unroll
@@ -170,7 +191,7 @@ __global__ void __launch_bounds__(256) k_gs_nbmin(ClsDev d) {
         if (r >= 1 && r <= row - 2 && c >= 1 && c <= col - 2)
             for (int j = -1; j <= 1; ++j)
                 for (int k = -1; k <= 1; ++k) {
-                    const float z = ord2f(d.cell_minz[m + j * col + k]);
+                    const float z = ord2f(d.cell_minz[PF_IDX(d, m + j * col + k, num)]);
                     if (nb > z) nb = z;
                 }
         d.cell_nb[m] = nb;
@@ -191,6 +212,9 @@ __global__ void __launch_bounds__(256) k_gs_keys(const float4* __restrict__ pts,
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const u32 cell = d.pcell[i];
         const float z = pts[i].z;
+#ifdef PF_DEV_BOUNDS
+        if (cell != ~0u) (void)PF_IDX(d, cell, d.gdim[2]);
+#endif
         u32 key = kKeyDropped;
         if (cell != ~0u) {
             if (z > P.gf_max_ground_height) {
@@ -225,7 +249,7 @@ __global__ void __launch_bounds__(256) k_gs_keys(const float4* __restrict__ pts,
 __global__ void __launch_bounds__(256) k_gs_gather(const float4* __restrict__ pts, ClsDev d) {
     const int nu = d.cnt[CC_NU];
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nu; j += gridDim.x * blockDim.x) {
-        const float4 p = pts[d.vals[j]];
+        const float4 p = pts[PF_IDX(d, d.vals[j], d.cnt[CC_N])];
         d.U[j] = make_float4(p.x, p.y, p.z, 0.0f);
     }
 }
@@ -267,7 +291,7 @@ __global__ void __launch_bounds__(256) k_u_keys(ClsDev d, const int* __restrict_
         u32 key = 0;
         if (dm[7]) {
             const int x = (int)floorf(p.x) - dm[0], y = (int)floorf(p.y) - dm[1], z = (int)floorf(p.z) - dm[2];
-            const u32 cell = (u32)(dm[6] + (z * dm[4] + y) * dm[3] + x);
+            const u32 cell = (u32)PF_IDX(d, (long long)dm[6] + (long long)(z * dm[4] + y) * dm[3] + x, d.cell_cap);
             key = (cell << 9) | morton3(sub8(p.x), sub8(p.y), sub8(p.z));
         }
         d.ckeys[j] = key;
@@ -280,7 +304,7 @@ __global__ void __launch_bounds__(256) k_u_place(ClsDev d, float4* __restrict__ 
     const int nu = d.cnt[CC_NU];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
         const u32 j = d.cvals[i];
-        const float4 p = d.U[j];
+        const float4 p = d.U[PF_IDX(d, j, nu)];
         cpts[i] = make_float4(p.x, p.y, p.z, __int_as_float((int)j));
         if (dm[7]) cell_count[d.ckeys[i] >> 9] = 0u;
     }
@@ -428,7 +452,7 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
     const int wv = (int)xcd_block(blockIdx.x, gridDim.x) * WPB + (int)(threadIdx.x >> 6);
     for (int qs = wv; qs < nu; qs += nw) {                   // wave-uniform
         // queries in cell (Morton) order: neighbouring waves share candidate chunks in L2
-        const float4 qc = gv.cpts[qs];
+        const float4 qc = gv.cpts[PF_IDX(d, qs, d.cap)];
         const int q = __float_as_int(qc.w);
         const float4 qp = make_float4(qc.x, qc.y, qc.z, 0.f);
         u64 ent = ~0ull;                                     // list entry l
@@ -437,7 +461,8 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
             return lb < r2 && (thr == ~0ull || lb <= __uint_as_float((u32)(thr >> 32)));
         };
         auto box_lb = [&](int c) {
-            const float4 lo = d.box[2 * c], hi = d.box[2 * c + 1];
+            const float4 lo = d.box[PF_IDX(d, 2 * c, 2 * (d.cap / 16 + 1))];
+            const float4 hi = d.box[PF_IDX(d, 2 * c + 1, 2 * (d.cap / 16 + 1))];
             const float tx = qp.x < lo.x ? lo.x - qp.x : (qp.x > hi.x ? qp.x - hi.x : 0.0f);
             const float ty = qp.y < lo.y ? lo.y - qp.y : (qp.y > hi.y ? qp.y - hi.y : 0.0f);
             const float tz = qp.z < lo.z ? lo.z - qp.z : (qp.z > hi.z ? qp.z - hi.z : 0.0f);
@@ -469,11 +494,12 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
             if (l < 9) {
                 const int y = cy + l % 3 - 1 - miny, z = cz + l / 3 - 1 - minz;
                 if (y >= 0 && y < dy && z >= 0 && z < dz) {
-                    const u32* cs = gv.cell_start + base + (z * dy + y) * dx + xi;
-                    w1 = cs[0];
-                    w2 = cs[1];
-                    w0 = xi > 0 ? cs[-1] : w1;
-                    w3 = xi + 1 < dx ? cs[2] : w2;
+                    const long long c0 = (long long)base + (long long)(z * dy + y) * dx + xi;
+                    const u32* cs = gv.cell_start;
+                    w1 = cs[PF_IDX(d, c0, d.cell_cap + 1)];
+                    w2 = cs[PF_IDX(d, c0 + 1, d.cell_cap + 1)];
+                    w0 = xi > 0 ? cs[PF_IDX(d, c0 - 1, d.cell_cap + 1)] : w1;
+                    w3 = xi + 1 < dx ? cs[PF_IDX(d, c0 + 2, d.cell_cap + 1)] : w2;
                 }
             }
             // each row's point range [ra, rb) (end cells dropped when their bound is >= r^2) and the
@@ -543,7 +569,7 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                         locate(g + (sj & 0x3Fu), c, a0, b0);
                         const u32 v = c * 16u + (u32)(l & 15);
                         if (v >= a0 && v < b0) {
-                            const float4 p = gv.cpts[v];
+                            const float4 p = gv.cpts[PF_IDX(d, v, nu)];
                             const float dd = knn_d2(qp.x, qp.y, qp.z, p);
                             if (dd < r2) key = knn_key(dd, __float_as_int(p.w));
                         }
@@ -567,8 +593,8 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
             }
         }
         const int found = __popcll(__ballot(l < K && ent != ~0ull));
-        if (l < found) nbr[(size_t)q * kClsMaxK + l] = (u32)(ent & 0xffffffffull);
-        if (l == 0) d.ptnum[q] = found;
+        if (l < found) nbr[PF_IDX(d, (size_t)q * kClsMaxK + l, (long long)d.cap * kClsMaxK)] = (u32)(ent & 0xffffffffull);
+        if (l == 0) d.ptnum[PF_IDX(d, q, nu)] = found;
     }
 }
 
@@ -583,7 +609,10 @@ __global__ void __launch_bounds__(256) k_cls_decide(ClsDev d, const u32* __restr
         const int n = d.ptnum[q];
         const u32* lst = nbr + (size_t)q * kClsMaxK;
         const float4* U = d.U;
-        const int code = pca_code([&](int e) { return U[lst[e]]; }, n, U[q].z, d.prm);
+#ifdef PF_DEV_BOUNDS
+        if (n > d.prm.k) (void)PF_IDX(d, n, 0);             // a list longer than k: flagged
+#endif
+        const int code = pca_code([&](int e) { return U[PF_IDX(d, lst[e], nu)]; }, n, U[q].z, d.prm);
         const u32 key = code == 2 ? 0u : (code == 1 ? 1u : (code == 3 ? 2u : 3u));   // beam, pillar, facade, none
         d.code[q] = (uint8_t)code;
         d.ckeys[q] = key;
@@ -615,7 +644,7 @@ __global__ void __launch_bounds__(256) k_cls_out(ClsDev d, const u32* __restrict
         const u32 u = vs[j];
         const int pos = j - (k > 0 ? n0 : 0) - (k > 1 ? n1 : 0);
         float4* o = k == 0 ? o0 : (k == 1 ? o1 : o2);
-        if (o) o[pos] = d.U[u];
+        if (o) o[PF_IDX(d, pos, nout)] = d.U[PF_IDX(d, u, nu)];
         if (idx_out) idx_out[j] = (int)d.vals[u];
     }
 }

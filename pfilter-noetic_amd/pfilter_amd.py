@@ -91,7 +91,7 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_map_update_device", "pf_map_update_mat", "pf_map_get", "pf_odom_set_stage_a_reserve",
            "pf_fe_set_ring_model", "pf_odom_set_ring_model", "pf_odom_get_state", "pf_odom_snapshot",
            "pf_odom_restore", "pf_odom_set_map_export", "pf_odom_map_export", "pf_odom_set_stage_timing",
-           "pf_odom_stage_times"]
+           "pf_odom_stage_times", "pf_odom_set_state"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -124,6 +124,7 @@ def lib():
     L.pf_odom_poses.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
     L.pf_odom_set_graph.argtypes = [_vp, _i]
     L.pf_odom_set_stage_timing.argtypes = [_vp, _i]
+    L.pf_odom_set_state.argtypes = [_vp, _vp, _vp, _i]
     L.pf_odom_stage_times.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(_sz)]
     if hasattr(L, "pf_odom_set_stage_a_reserve"):
@@ -390,6 +391,13 @@ class Odom_ES_EstimationClass:
         _check("pf_odom_get_state", lib().pf_odom_get_state(self._h, prm.ctypes.data, last.ctypes.data,
                                                             ctypes.byref(oc)))
         return {"parameters": prm, "last_odom": last.reshape(3, 4), "optimization_count": oc.value}
+
+    def set_state(self, odom_pose, last_pose=None, optimization_count=2):
+        """odom = (R(q), t) of `odom_pose`, last_odom of `last_pose`, optimization_count (pf_odom_set_state)"""
+        a = np.ascontiguousarray(odom_pose, np.float64)
+        b = None if last_pose is None else np.ascontiguousarray(last_pose, np.float64)
+        _check("pf_odom_set_state", lib().pf_odom_set_state(self._h, a.ctypes.data, None if b is None else b.ctypes.data,
+                                                            int(optimization_count)))
 
     def snapshot(self):
         """the whole estimator state as bytes (pf_odom_snapshot)"""

@@ -94,6 +94,47 @@ def test_dense_vegetation_scene(pa, pfref, pfsynth, theta_p, theta_max):
     _compare_maps(od, orc)
 
 
+def test_per_frame_parity_vs_reference_faithful_oracle(pa, pfref, pfsynth):
+    """The north star's per-frame criterion against the oracle's reference-faithful option set
+    (opts=0: libstdc++ std::sort tie order in VoxelGrid / rgbds / the sector sort as PCL and
+    src/odomEstimationClass.cpp:74 call it, Householder-QR LM as Ceres DENSE_QR, the FLANN-style
+    kd-tree): on identical input clouds and an identical estimator state, the device pose within
+    1e-4 m / 1e-5 rad. The faithful oracle runs the sequence itself; before every sampled frame its
+    maps (with the age / p-index bytes) and its odom / last_odom / optimization_count are loaded into
+    the device handle (pf_odom_set_map, pf_odom_set_state) and into the oracle alike, then both run
+    the frame. (Over whole sequences the two tie orders make trajectories separate after ~50 frames,
+    as any change of sort implementation would make the reference's own: tools/parity_report.py.)"""
+    n = 300
+    sample = set(range(12, n, 12))
+    seq = pfsynth.Sequence("S64", n_frames=n)
+    lid = 64, 3.0, 90.0
+    orc = pfref.Odom(pfref.make_lidar(*lid), 0.4, 0, 0.4, 75, 0, opts=0)
+    od = pa.Odom_ES_EstimationClass(device=0)
+    od.init(pa.make_lidar(*lid), 0.4, 0, 0.4, 75, 0)
+    poses, worst, same_counts = [], (0.0, 0.0), 0
+    for k in range(n):
+        x = seq.frame(k)
+        if k in sample:
+            for which in (0, 1):
+                xyz, rg = orc.get_map(which)
+                od.set_map(which, xyz, rg)
+            od.set_state(poses[-1], poses[-2], 2)
+            orc.set_state(poses[-1], poses[-2])
+            orc.set_opt_count(2)
+            pg = od.frame_host(x)
+        pr = orc.frame(x)
+        poses.append(pr)
+        if k in sample:
+            dt, dr = pose_err(pg, pr)
+            worst = (max(worst[0], dt), max(worst[1], dr))
+            assert dt < TOL_T and dr < TOL_R, "frame %d: %.3e m %.3e rad" % (k, dt, dr)
+            sg, sr = od.stats(), orc.stats()
+            same_counts += all(sg[c] == sr[c] for c in ("n_edge_ds", "n_surf_ds", "n_edge_map", "n_surf_map"))
+    print("per-frame parity vs the faithful oracle: %d frames, worst %.3e m %.3e rad, counts identical in %d"
+          % (len(sample), worst[0], worst[1], same_counts))
+    assert same_counts == len(sample)
+
+
 def test_stage_timing(pa, pfsynth):
     """pf_odom_set_stage_timing / pf_odom_stage_times: per-stage device time over the frames since
     enable; results unchanged by the event records."""
