@@ -524,12 +524,12 @@ def cpu_baseline(budget_s, warmup):
     return out
 
 
-def _cpu_baseline(budget_s, warmup, preset="S64", theta=(0.4, 75), max_frames=2000):
+def _cpu_baseline(budget_s, warmup, preset="S64", theta=(0.4, 75), max_frames=2000, lines=64):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pfref
     import pfsynth
     seq = pfsynth.Sequence(preset, n_frames=warmup + max_frames, seed=0)
-    orc = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, theta[0], theta[1], 0, opts=0)
+    orc = pfref.Odom(pfref.make_lidar(lines, 3.0, 90.0), 0.4, 0, theta[0], theta[1], 0, opts=0)
     for k in range(warmup):
         orc.frame(seq.frame(k))
     n, el, k = 0, 0.0, warmup
@@ -548,6 +548,7 @@ def _cpu_baseline(budget_s, warmup, preset="S64", theta=(0.4, 75), max_frames=20
 ES_LEGS = {
     # name: (preset, theta_p, theta_max, what it is)
     "theta0": ("S64", 0.0, 0, "configs[0] parameters (k_new=0 theta_p=0 theta_max=0, FLOAM-equivalent) on S64"),
+    "campus32": ("S32", 1.0, 200, "configs[2]: 32-line campus scans (S32, 2 m/s), k_new=0 theta_p=1 theta_max=200"),
     "dense": ("S64V", 0.4, 75, "configs[1] parameters on S64V: residential scene with vegetation and rough "
                                "ground, denser features and maps than S64 (KITTI-00-like sizes)"),
     "dense_theta0": ("S64V", 0.0, 0, "configs[0] parameters on S64V (the largest maps: no stability filter)"),
@@ -562,6 +563,7 @@ def es_leg(name, device, nframes, threads, cpu_seconds, warmup=20, use_graph=Tru
     import pfilter_amd as pa
     preset, tp, tm, what = ES_LEGS[name]
     cfg = dict(ODOM_CFG, theta_p=tp, theta_max=tm)
+    lines = 32 if preset == "S32" else 64
     total = warmup + nframes
     bufs, ptrs = [], []
     for _, buf, counts, _ in load_frames(0, total, threads, preset):
@@ -572,7 +574,7 @@ def es_leg(name, device, nframes, threads, cpu_seconds, warmup=20, use_graph=Tru
 
     def run(timing):
         od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
-        od.init(lidar_cfg(), **cfg)
+        od.init(pa.make_lidar(lines, 3.0, 90.0, 0.1), **cfg)
         od.set_graph(use_graph)
         for k in range(warmup):
             od.frame_device(*ptrs[k])
@@ -597,7 +599,7 @@ def es_leg(name, device, nframes, threads, cpu_seconds, warmup=20, use_graph=Tru
            "last_frame": {k: st[k] for k in ("n_in", "n_ds", "n_map", "n_res")}}
     if with_cpu:
         with pinned_core() as pc:
-            cb = _cpu_baseline(cpu_seconds, warmup, preset=preset, theta=(tp, tm), max_frames=nframes)
+            cb = _cpu_baseline(cpu_seconds, warmup, preset=preset, theta=(tp, tm), max_frames=nframes, lines=lines)
             cb["host"] = pc.host()
         f0, f1 = cb.pop("frames")
         out["cpu_baseline"] = cb
