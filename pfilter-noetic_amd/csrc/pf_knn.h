@@ -403,4 +403,89 @@ __device__ __forceinline__ int knn5_team(const GridView& gv, int m, float qx, fl
     return found;
 }
 
+// ---- thick-row layout (standalone queries against a static map) ------------------------------
+// Every cell (x, y, z) of the thick layout holds the points of cells (x, y, z - 1), (x, y, z) and
+// (x, y, z + 1), in that order, and consecutive x of one (y, z) are consecutive in memory, so the
+// 27-cell block of a query is 3 contiguous ranges (oy = -1, 0, 1) instead of 9 x-rows: each point is
+// stored three times (48 B per map point; 96 MB for config 5's 2M points), and the per-candidate
+// 9-way row select becomes a 2-compare select. The end cells (ox = +-1) of a range are dropped by the
+// same exact float bound as knn5_team's, taken with bz = 0 (every z layer of the range shares it).
+struct ThickView {
+    const int* dims;           // the cell grid's dims (map 0)
+    const u32* tstart;         // [ncells + 1] exclusive scan of the thick cell sizes
+    const float4* tpts;        // thick layout (x, y, z, bits(map index))
+};
+
+template <int T>
+__device__ __forceinline__ int knn5_thick(const ThickView& tv, float qx, float qy, float qz, bool active,
+                                          float (&dout)[5], int (&iout)[5]) {
+    static_assert(T >= 4 && T <= 64 && (T & (T - 1)) == 0, "team: a power of two >= 4 within a wave");
+    constexpr int U = PF_KNN_UNROLL;
+    const u64 sentinel = knn_key(1.0f, 0x7fffffff);
+    u64 k[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) k[q] = sentinel;
+    const int* dm = tv.dims;
+    if (active && dm[7]) {
+        const float fcx = floorf(qx), fcy = floorf(qy), fcz = floorf(qz);
+        const int cx = (int)fcx, cy = (int)fcy, cz = (int)fcz;
+        const int minx = dm[0], miny = dm[1], minz = dm[2], dx = dm[3], dy = dm[4], dz = dm[5];
+        const float lx = qx - fcx, hx = (fcx + 1.0f) - qx;
+        const float ly = qy - fcy, hy = (fcy + 1.0f) - qy;
+        const u32 tl = (u32)(lane_id() & (T - 1));
+        const int tbase = lane_id() & ~(T - 1);
+        // lane tl < 3 owns range oy = tl - 1: thick cells cx - 1 .. cx + 1 of row (cy + oy, cz)
+        u32 s = 0, e = 0;
+        {
+            const int oy = (int)tl - 1;
+            const float by = oy < 0 ? ly : (oy > 0 ? hy : 0.0f);
+            const float bl = (lx * lx + by * by) + 0.0f * 0.0f;
+            const float bh = (hx * hx + by * by) + 0.0f * 0.0f;
+            // a query one layer below / above the grid reads the nearest thick layer (its extra layer
+            // lies >= 1 m away in z, so the gate rejects it)
+            const int y = cy + oy - miny, zq = cz - minz, z = min(max(zq, 0), dz - 1);
+            const int x0 = max(cx - (bl < 1.0f ? 1 : 0) - minx, 0);
+            const int x1 = min(cx + (bh < 1.0f ? 1 : 0) - minx, dx - 1);
+            if (tl < 3 && y >= 0 && y < dy && zq >= -1 && zq <= dz && x0 <= x1) {
+                const int c = (z * dy + y) * dx;
+                s = tv.tstart[c + x0];
+                e = tv.tstart[c + x1 + 1];
+            }
+        }
+        const u32 s0 = (u32)__shfl((int)s, tbase, 64), e0 = (u32)__shfl((int)e, tbase, 64);
+        const u32 s1 = (u32)__shfl((int)s, tbase + 1, 64), e1 = (u32)__shfl((int)e, tbase + 1, 64);
+        const u32 s2 = (u32)__shfl((int)s, tbase + 2, 64), e2 = (u32)__shfl((int)e, tbase + 2, 64);
+        const u32 p1 = e0 - s0, p2 = p1 + (e1 - s1), total = p2 + (e2 - s2);
+        const int o0 = (int)s0, o1 = (int)(s1 - p1), o2 = (int)(s2 - p2);
+        for (u32 v0 = tl; v0 < total; v0 += T * U) {
+            float4 p[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const u32 v = v0 + T * u;
+                const int o = v >= p2 ? o2 : (v >= p1 ? o1 : o0);
+                if (v < total) p[u] = tv.tpts[(int)v + o];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (v0 + T * u >= total) break;
+                knn_consider(qx, qy, qz, p[u], k);
+            }
+        }
+    }
+    int found = 0;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+        const u64 mn = team_min<T>(k[0]);
+        dout[r] = __uint_as_float((u32)(mn >> 32));
+        iout[r] = (int)(u32)(mn & 0xffffffffull);
+        if (mn != sentinel) ++found;
+        if (k[0] == mn && mn != sentinel) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) k[q] = k[q + 1];
+            k[4] = sentinel;
+        }
+    }
+    return found;
+}
+
 }  // namespace pf

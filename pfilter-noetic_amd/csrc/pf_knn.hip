@@ -94,6 +94,69 @@ __global__ void __launch_bounds__(256, PF_KNN_MINW) k_knn_query(GridView gv, con
     }
 }
 
+// the thick-row layout of a built grid (pf_knn.h): sizes, then the triple copies
+__global__ void __launch_bounds__(256) k_thick_count(const int* __restrict__ dims, const u32* __restrict__ start,
+                                                      u32* __restrict__ tcount, int* __restrict__ d_n) {
+    const int dx = dims[3], dy = dims[4], dz = dims[5];
+    const int nc = dims[7] ? dx * dy * dz : 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *d_n = nc + 1;
+        tcount[nc] = 0u;                      // the scan's last element: tstart[nc] = the total
+    }
+    const int L = dx * dy;
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += gridDim.x * blockDim.x) {
+        const int z = c / L;
+        u32 n = start[c + 1] - start[c];
+        if (z > 0) n += start[c - L + 1] - start[c - L];
+        if (z + 1 < dz) n += start[c + L + 1] - start[c + L];
+        tcount[c] = n;
+    }
+}
+__global__ void __launch_bounds__(256) k_thick_scatter(const float4* __restrict__ pts, const int* __restrict__ d_m,
+                                                        const int* __restrict__ dims, const u32* __restrict__ start,
+                                                        const u32* __restrict__ slot, const u32* __restrict__ tstart,
+                                                        float4* __restrict__ tpts) {
+    const int n = *d_m;
+    if (!dims[7]) return;
+    const int L = dims[3] * dims[4], dz = dims[5];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4 p = pts[i];
+        const int c = cell_of(dims, p);
+        const int z = (c - dims[6]) / L;
+        const u32 sl = slot[i];
+        const float4 v = make_float4(p.x, p.y, p.z, __int_as_float(i));
+        const u32 below = z > 0 ? start[c - L + 1] - start[c - L] : 0u;
+        tpts[tstart[c] + below + sl] = v;                               // own layer: after z - 1
+        if (z + 1 < dz) tpts[tstart[c + L] + sl] = v;                   // as layer z - 1 of cell z + 1
+        if (z > 0) {                                                    // as layer z + 1 of cell z - 1
+            const u32 b2 = z > 1 ? start[c - 2 * L + 1] - start[c - 2 * L] : 0u;
+            tpts[tstart[c - L] + b2 + (start[c - L + 1] - start[c - L]) + sl] = v;
+        }
+    }
+}
+
+template <int T>
+__global__ void __launch_bounds__(256, PF_KNN_MINW) k_knn_thick(ThickView tv, const float4* __restrict__ q, int nq,
+                                                                int* __restrict__ idx, float* __restrict__ d2) {
+    const unsigned blk = xcd_block(blockIdx.x, gridDim.x);
+    const int i = (int)((blk * blockDim.x + threadIdx.x) / T);
+    const bool active = i < nq;
+    const float4 p = active ? q[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float d[5];
+    int id[5];
+    knn5_thick<T>(tv, p.x, p.y, p.z, active, d, id);
+    const int tl = lane_id() & (T - 1);
+    if (active) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            if (k % T != tl) continue;
+            const bool f = id[k] != 0x7fffffff;
+            idx[5 * i + k] = f ? id[k] : -1;
+            d2[5 * i + k] = f ? d[k] : __int_as_float(0x7f800000);
+        }
+    }
+}
+
 // |C(q)|: points in the 27 cells around each query (algorithmic byte count)
 __global__ void __launch_bounds__(256) k_knn_cellpop(GridView gv, const float4* __restrict__ q, int nq,
                                                       unsigned long long* __restrict__ total) {
@@ -196,12 +259,26 @@ struct pf_knn {
     size_t map_cap = 0, q_cap = 0;
     int nq = 0;
     int team = 8;                  // lanes per query
+    bool thick = true;             // query the thick-row layout (pf_knn.h); false: the 9-row grid walk
+    u32* tstart = nullptr;         // [cell_cap + 1]
+    u32* tcount = nullptr;         // [cell_cap + 1]
+    float4* tpts = nullptr;        // [3 * map_cap]
+    int* d_nt = nullptr;           // thick scan length
 };
 
 namespace pf {
 namespace {
 void launch_knn(const pf_knn* h, const GridView& gv) {
     const unsigned blocks = (unsigned)(((size_t)h->nq * h->team + 255) / 256);
+    if (h->thick) {
+        const ThickView tv{h->grid.dims, h->tstart, h->tpts};
+        switch (h->team) {
+        case 4: hipLaunchKernelGGL(k_knn_thick<4>, dim3(blocks), dim3(256), 0, h->stream, tv, h->d_q, h->nq, h->d_idx, h->d_d2); break;
+        case 16: hipLaunchKernelGGL(k_knn_thick<16>, dim3(blocks), dim3(256), 0, h->stream, tv, h->d_q, h->nq, h->d_idx, h->d_d2); break;
+        default: hipLaunchKernelGGL(k_knn_thick<8>, dim3((unsigned)(((size_t)h->nq * 8 + 255) / 256)), dim3(256), 0, h->stream, tv, h->d_q, h->nq, h->d_idx, h->d_d2); break;
+        }
+        return;
+    }
     switch (h->team) {
     case 1: hipLaunchKernelGGL(k_knn_query<1>, dim3(blocks), dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2); break;
     case 2: hipLaunchKernelGGL(k_knn_query<2>, dim3(blocks), dim3(256), 0, h->stream, gv, h->d_q, h->nq, h->d_idx, h->d_d2); break;
@@ -233,6 +310,10 @@ int pf_knn_create(int device, size_t map_capacity, size_t query_capacity, pf_knn
     if (rc == PF_OK && hipMalloc(&h->d_idx, sizeof(int) * 5 * query_capacity) != hipSuccess) rc = PF_ENOMEM;
     if (rc == PF_OK && hipMalloc(&h->d_d2, sizeof(float) * 5 * query_capacity) != hipSuccess) rc = PF_ENOMEM;
     if (rc == PF_OK && hipMalloc(&h->d_pop, sizeof(unsigned long long)) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMalloc(&h->tstart, sizeof(u32) * (((size_t)1 << 26) + 1)) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMalloc(&h->tcount, sizeof(u32) * (((size_t)1 << 26) + 1)) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMalloc(&h->tpts, sizeof(float4) * 3 * map_capacity) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMalloc(&h->d_nt, sizeof(int)) != hipSuccess) rc = PF_ENOMEM;
     if (rc != PF_OK) {
         pf_knn_destroy(h);
         return rc;
@@ -252,6 +333,10 @@ int pf_knn_destroy(pf_knn* h) {
     (void)hipFree(h->d_idx);
     (void)hipFree(h->d_d2);
     (void)hipFree(h->d_pop);
+    (void)hipFree(h->tstart);
+    (void)hipFree(h->tcount);
+    (void)hipFree(h->tpts);
+    (void)hipFree(h->d_nt);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return PF_OK;
@@ -265,6 +350,12 @@ int pf_knn_set_map(pf_knn* h, const float* xyz4, size_t m) {
     if (m) PF_HIP_TRY(hipMemcpyAsync(h->d_map, xyz4, sizeof(float4) * m, hipMemcpyHostToDevice, h->stream));
     PF_HIP_TRY(hipMemcpyAsync(h->d_m, mm, sizeof(mm), hipMemcpyHostToDevice, h->stream));
     grid_build(h->grid, GridPtrs{{h->d_map, nullptr, nullptr}, {h->d_m, nullptr, nullptr}, 1}, h->prim, h->stream);
+    // the thick-row copy: sizes, scan, triple scatter (the grid's slots and cell_start)
+    hipLaunchKernelGGL(k_thick_count, dim3(1024), dim3(256), 0, h->stream, h->grid.dims, h->grid.cell_start, h->tcount,
+                       h->d_nt);
+    scan_exclusive(h->tcount, h->tstart, h->d_nt, nullptr, h->prim, h->stream);
+    hipLaunchKernelGGL(k_thick_scatter, dim3(1024), dim3(256), 0, h->stream, h->d_map, h->d_m, h->grid.dims,
+                       h->grid.cell_start, h->grid.slot, h->tstart, h->tpts);
     int err = 0;
     PF_HIP_TRY(hipMemcpyAsync(&err, h->grid.err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     PF_HIP_TRY(hipStreamSynchronize(h->stream));
@@ -320,6 +411,14 @@ int pf_knn_bench(pf_knn* h, int iters, double* avg_ms, double* alg_bytes) {
 int pf_knn_set_team(pf_knn* h, int team) {
     if (!h || (team != 1 && team != 2 && team != 4 && team != 8 && team != 16)) return PF_EINVAL;
     h->team = team;
+    return PF_OK;
+}
+
+// development: 1 = the thick-row layout (default), 0 = the 9-row walk of the cell grid
+int pf_knn_set_layout(pf_knn* h, int thick) {
+    if (!h) return PF_EINVAL;
+    h->thick = thick != 0;
+    if (!h->thick && h->team > 16) h->team = 8;
     return PF_OK;
 }
 

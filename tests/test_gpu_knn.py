@@ -97,3 +97,25 @@ def test_knn_config5_full_size(pa, pfref, pfsynth):
     _, alg = kn.bench(1)
     pop = pfref.knn_cellpop(mp, q)
     assert alg == q.shape[0] * (16 + 40 + 27 * 8) + 16 * pop
+
+
+def test_knn_thick_layout_equals_grid_walk(pa, pfsynth):
+    """The standalone kNN's thick-row layout (every cell holding its z - 1, z, z + 1 layers, pf_knn.h)
+    gives the same bits as the 9-row walk of the plain cell grid, including queries one layer below
+    and above the map's bounding box and outside it."""
+    import ctypes
+    mp = pfsynth.dense_map(300000, seed=5)
+    q = pfsynth.dense_queries(mp, 20000, sigma=0.3, seed=6)
+    lo, hi = mp[:, :3].min(0), mp[:, :3].max(0)
+    q[:300, 2] = lo[2] - np.linspace(0.01, 1.5, 300)              # below the grid, in and out of reach
+    q[300:600, 2] = hi[2] + np.linspace(0.01, 1.5, 300)           # above it
+    q[600:700, :2] = lo[:2] - 0.5                                  # off a corner
+    out = []
+    for layout in (1, 0):
+        kn = pa.Knn(mp.shape[0], q.shape[0])
+        assert pa.lib().pf_knn_set_layout(ctypes.c_void_p(kn._h), layout) == 0
+        kn.set_map(mp)
+        out.append(kn.query(q))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1].view(np.uint32), out[1][1].view(np.uint32))
+    assert (out[0][0][:600, 0] >= 0).sum() > 50                      # some off-grid queries found neighbours

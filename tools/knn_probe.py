@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--nmap", type=int, default=2_000_000)
     ap.add_argument("--nq", type=int, default=200_000)
     ap.add_argument("--team", type=int, default=0, help="lanes per query, 1..16 (development hook; 0 = default)")
+    ap.add_argument("--layout", type=int, default=1, help="1: thick-row layout (default), 0: 9-row grid walk")
     ap.add_argument("--order", default="stratified", choices=["stratified", "cell", "random"],
                     help="query order: generator's, sorted by 1 m cell, or shuffled")
     a = ap.parse_args()
@@ -33,6 +34,8 @@ def main():
     elif a.order == "random":
         q = q[np.random.default_rng(1).permutation(q.shape[0])].copy()
     kn = pa.Knn(a.nmap, a.nq)
+    import ctypes
+    assert pa.lib().pf_knn_set_layout(ctypes.c_void_p(kn._h), a.layout) == 0
     kn.set_map(mp)
     if a.team:
         import ctypes
@@ -40,7 +43,7 @@ def main():
     kn.query(q)
     ms, alg = kn.bench(a.iters)
     print(json.dumps({"avg_kernel_ms": ms, "alg_bytes_per_launch": alg, "launches": a.iters + 2,
-                      "achieved_GBps": alg / (ms * 1e-3) / 1e9, "team": a.team, "order": a.order}))
+                      "achieved_GBps": alg / (ms * 1e-3) / 1e9, "team": a.team, "order": a.order, "layout": a.layout}))
 
 
 if __name__ == "__main__":
