@@ -186,6 +186,12 @@ int pf_cls_ground_seg(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes
  * (0 none, 1 pillar, 2 beam, 3 facade, :663-682) and the neighbour count pt_num (:223); either may
  * be NULL */
 int pf_cls_classify(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, uint8_t* cls, int32_t* pt_num);
+/* The normals nongroundExtract's assign_normal (include/preProcess.hpp:327-346) writes into the
+ * classified points, 4 floats per point: (principal direction, linear_2) for pillar and beam points,
+ * (normal direction, planar_2) for facade points, zeros for unclassified points. Per point of the last
+ * pf_cls_classify call (input order) or, after pf_cls_extract, per non-ground point in ground_seg's
+ * push order. n = the number of points wanted (at most that call's point count). */
+int pf_cls_normals(pf_cls* h, float* normal4, size_t n);
 
 /* BPF whole-frame mode: one raw scan (device pointer to n packed float4) per call; stage A runs the
  * front end above (ground_seg + featureExtract) into the beam / pillar / facade clouds, then the

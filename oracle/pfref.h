@@ -168,6 +168,11 @@ int pfref_ground_seg(const float* xyz, size_t n, size_t stride, const pfref_cls_
 /* per point: 0 none, 1 pillar, 2 beam, 3 facade (index_with_feature); pt_num = neighbours found */
 int pfref_pca_classify(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, uint8_t* cls,
                        int32_t* pt_num);
+/* the same, and the normal the reference's assign_normal writes into each classified point (:327-346):
+ * 4 floats per point, (principal direction, linear_2) for pillar / beam, (normal direction,
+ * planar_2) for facade, zeros for unclassified points */
+int pfref_pca_classify_normals(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, uint8_t* cls,
+                               int32_t* pt_num, float* normal4);
 /* the chain: class clouds (input indices, in the published order); any output may be NULL */
 int pfref_bpf_preprocess(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, int32_t* beam,
                          size_t* nb, int32_t* pillar, size_t* np, int32_t* facade, size_t* nf, int32_t* ground,

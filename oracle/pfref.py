@@ -123,6 +123,7 @@ def lib():
         L.pfref_ground_seg.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams), _vp, ctypes.POINTER(_sz), _vp,
                                        ctypes.POINTER(_sz)]
         L.pfref_pca_classify.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams), _vp, _vp]
+        L.pfref_pca_classify_normals.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams), _vp, _vp, _vp]
         L.pfref_map_create.argtypes = [ctypes.c_double]
         L.pfref_map_create.restype = _vp
         L.pfref_map_destroy.argtypes = [_vp]
@@ -384,15 +385,20 @@ def ground_seg(xyz, params=None):
     return g[:ng.value].copy(), u[:nu.value].copy()
 
 
-def pca_classify(xyz, params=None):
-    """(class per point: 0 none / 1 pillar / 2 beam / 3 facade, neighbour count per point)."""
+def pca_classify(xyz, params=None, normals=False):
+    """(class per point: 0 none / 1 pillar / 2 beam / 3 facade, neighbour count per point[, the normal
+    assign_normal writes: [n, 4] float32])."""
     a = np.ascontiguousarray(xyz, dtype=np.float32)
     n = a.shape[0]
     p = params or cls_params()
     cls = np.empty(max(n, 1), np.uint8)
     num = np.empty(max(n, 1), np.int32)
-    rc = lib().pfref_pca_classify(a.ctypes.data, n, 4 * a.shape[1], ctypes.byref(p), cls.ctypes.data, num.ctypes.data)
+    nrm = np.empty((max(n, 1), 4), np.float32)
+    rc = lib().pfref_pca_classify_normals(a.ctypes.data, n, 4 * a.shape[1], ctypes.byref(p), cls.ctypes.data,
+                                          num.ctypes.data, nrm.ctypes.data if normals else None)
     assert rc == 0
+    if normals:
+        return cls[:n].copy(), num[:n].copy(), nrm[:n].copy()
     return cls[:n].copy(), num[:n].copy()
 
 

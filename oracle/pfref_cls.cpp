@@ -137,8 +137,9 @@ void radius_knn(const std::vector<P3>& c, const CellGrid& g, int i, float r2, in
 // PCA of one point's neighbourhood and the featureExtract decision (:653-688): 0 none, 1 pillar,
 // 2 beam, 3 facade (the reference's index_with_feature codes)
 int pca_class(const std::vector<P3>& c, const std::vector<std::pair<float, int>>& nb, float qz,
-              const pfref_cls_params& p) {
+              const pfref_cls_params& p, float* normal4 = nullptr) {
     const int n = (int)nb.size();
+    if (normal4) normal4[0] = normal4[1] = normal4[2] = normal4[3] = 0.f;
     if (!(n > p.k_min) || n <= 3) return 0;                            // :657 (and :289)
     float sx = 0.f, sy = 0.f, sz = 0.f;                                // compute3DCentroid
     for (const auto& e : nb) {
@@ -169,11 +170,16 @@ int pca_class(const std::vector<P3>& c, const std::vector<std::pair<float, int>>
     const double d1 = l1, d2 = l2, d3 = l3;                            // eigenvalue_t is double (:77-82)
     const double linear_2 = (d1 - d2) / d1;                            // :315-316
     const double planar_2 = (d2 - d3) / d1;
+    // assign_normal (:327-346): pillar / beam carry the principal direction and linear_2, a facade the
+    // normal direction and planar_2 (pt.normal[3], a float)
+    auto put = [&](const float* v, double w) {
+        if (normal4) { normal4[0] = v[0]; normal4[1] = v[1]; normal4[2] = v[2]; normal4[3] = (float)w; }
+    };
     if (linear_2 > p.edge_thre) {                                      // :659-674
-        if (std::fabs(v0[2]) > p.linear_vsin_high) return 1;
-        if (std::fabs(v0[2]) < p.linear_vsin_low && qz < p.beam_h_max && qz > p.beam_h_min) return 2;
+        if (std::fabs(v0[2]) > p.linear_vsin_high) { put(v0, linear_2); return 1; }
+        if (std::fabs(v0[2]) < p.linear_vsin_low && qz < p.beam_h_max && qz > p.beam_h_min) { put(v0, linear_2); return 2; }
     } else if (planar_2 > p.planar_thre) {                             // :676-684
-        if (std::fabs(nv[2]) < p.planar_vsin_low) return 3;
+        if (std::fabs(nv[2]) < p.planar_vsin_low) { put(nv, planar_2); return 3; }
     }
     return 0;
 }
@@ -218,6 +224,11 @@ int pfref_ground_seg(const float* xyz, size_t n, size_t stride, const pfref_cls_
 
 int pfref_pca_classify(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, uint8_t* cls,
                        int32_t* pt_num) {
+    return pfref_pca_classify_normals(xyz, n, stride, p, cls, pt_num, nullptr);
+}
+
+int pfref_pca_classify_normals(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, uint8_t* cls,
+                               int32_t* pt_num, float* normal4) {
     if (!p || (!xyz && n) || stride < 12 || p->k < 1) return -1;
     std::vector<P3> c(n);
     for (size_t i = 0; i < n; ++i) c[i] = *at(xyz, stride, i);
@@ -228,7 +239,8 @@ int pfref_pca_classify(const float* xyz, size_t n, size_t stride, const pfref_cl
     for (size_t i = 0; i < n; ++i) {
         radius_knn(c, g, (int)i, r2, p->k, nb);
         if (pt_num) pt_num[i] = (int32_t)nb.size();
-        if (cls) cls[i] = (uint8_t)pca_class(c, nb, c[i].z, *p);
+        const int code = pca_class(c, nb, c[i].z, *p, normal4 ? normal4 + 4 * i : nullptr);
+        if (cls) cls[i] = (uint8_t)code;
     }
     return 0;
 }

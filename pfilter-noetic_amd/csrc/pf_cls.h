@@ -52,6 +52,7 @@ struct ClsGPU {
     int* ptnum = nullptr;        // [cap] neighbours found per U point
     int* idx_out = nullptr;      // [cap] input indices of beam | pillar | facade
     float4* box = nullptr;       // [2 * (cap / 16 + 1)] bounding box (lo, hi) of every 16-point chunk
+    float4* nrm = nullptr;       // [cap] per U point: the normal assign_normal writes (preProcess.hpp:327-346)
     u32* nbr = nullptr;          // [cap * kClsMaxK] neighbour lists (U indices, ascending distance)
     GridGPU grid;
     PrimWork w;

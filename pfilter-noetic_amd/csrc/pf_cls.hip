@@ -35,10 +35,11 @@ struct ClsDev {          // kernel view of ClsGPU
     int* sticky;         // optional: a sticky copy of CC_ERR (the odometry handle's error word)
     u32 cap;             // allocation sizes, for the bounds-checked development build (PF_DEV_BOUNDS)
     u32 cell_cap;
+    float4* nrm;         // per U point: the normal assign_normal writes (zeros when unclassified)
 };
 ClsDev dev_view(ClsGPU& c) {
     return ClsDev{c.prm, c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals,
-                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.box, c.sticky, (u32)c.cap, (u32)c.grid.cell_cap};
+                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.box, c.sticky, (u32)c.cap, (u32)c.grid.cell_cap, c.nrm};
 }
 
 // Development build with -DPF_DEV_BOUNDS (tools/build_variant.sh): every indexed global access of the
@@ -339,9 +340,12 @@ __global__ void __launch_bounds__(256) k_u_boxes(ClsDev d, const float4* __restr
 
 // PCA of the neighbourhood nb[0 .. n) (ascending distance) and the class decision, :653-688 /
 // :283-323, f32 as pcl::PCA computes it; the eigen-decomposition is the f64 cyclic Jacobi (eig3)
-// of the f32 covariance, rounded back to f32. Returns the index_with_feature code.
+// of the f32 covariance, rounded back to f32. Returns the index_with_feature code; nrm receives what
+// assign_normal (:327-346) writes into a classified point: (principal direction, linear_2) for a
+// pillar or beam, (normal direction, planar_2) for a facade, zeros otherwise.
 template <class Get>
-__device__ int pca_code(Get get, int n, float qz, const pf_cls_params& P) {
+__device__ int pca_code(Get get, int n, float qz, const pf_cls_params& P, float4& nrm) {
+    nrm = make_float4(0.f, 0.f, 0.f, 0.f);
     if (!(n > P.k_min) || n <= 3) return 0;
 #ifdef PF_DEV_NOPCA
     return 3;                                  // development: the search without the PCA (timing only)
@@ -375,10 +379,14 @@ __device__ int pca_code(Get get, int n, float qz, const pf_cls_params& P) {
     const double linear_2 = (d1 - d2) / d1;
     const double planar_2 = (d2 - d3) / d1;
     if (linear_2 > (double)P.edge_thre) {
-        if (fabsf(v0[2]) > P.linear_vsin_high) return 1;
-        if (fabsf(v0[2]) < P.linear_vsin_low && qz < P.beam_h_max && qz > P.beam_h_min) return 2;
+        const float4 pr = make_float4(v0[0], v0[1], v0[2], (float)linear_2);
+        if (fabsf(v0[2]) > P.linear_vsin_high) { nrm = pr; return 1; }
+        if (fabsf(v0[2]) < P.linear_vsin_low && qz < P.beam_h_max && qz > P.beam_h_min) { nrm = pr; return 2; }
     } else if (planar_2 > (double)P.planar_thre) {
-        if (fabsf(nv[2]) < P.planar_vsin_low) return 3;
+        if (fabsf(nv[2]) < P.planar_vsin_low) {
+            nrm = make_float4(nv[0], nv[1], nv[2], (float)planar_2);
+            return 3;
+        }
     }
     return 0;
 }
@@ -612,7 +620,9 @@ __global__ void __launch_bounds__(256) k_cls_decide(ClsDev d, const u32* __restr
 #ifdef PF_DEV_BOUNDS
         if (n > d.prm.k) (void)PF_IDX(d, n, 0);             // a list longer than k: flagged
 #endif
-        const int code = pca_code([&](int e) { return U[PF_IDX(d, lst[e], nu)]; }, n, U[q].z, d.prm);
+        float4 nv;
+        const int code = pca_code([&](int e) { return U[PF_IDX(d, lst[e], nu)]; }, n, U[q].z, d.prm, nv);
+        d.nrm[q] = nv;
         const u32 key = code == 2 ? 0u : (code == 1 ? 1u : (code == 3 ? 2u : 3u));   // beam, pillar, facade, none
         d.code[q] = (uint8_t)code;
         d.ckeys[q] = key;
@@ -674,6 +684,7 @@ int cls_alloc(ClsGPU& c, size_t cap) {
     if (hipMalloc(&c.idx_out, sizeof(int) * cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&c.nbr, sizeof(u32) * kClsMaxK * cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&c.box, sizeof(float4) * 2 * (cap / 16 + 1)) != hipSuccess) return PF_ENOMEM;
+    if (hipMalloc(&c.nrm, sizeof(float4) * cap) != hipSuccess) return PF_ENOMEM;
     const u32 gb0[8] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u, 0u, 0u, 0u};
     if (hipMemcpy(c.gb, gb0, sizeof(gb0), hipMemcpyHostToDevice) != hipSuccess) return PF_EHIP;
     if (hipMemset(c.cnt, 0, sizeof(int) * CC_COUNT) != hipSuccess) return PF_EHIP;
@@ -684,7 +695,7 @@ int cls_alloc(ClsGPU& c, size_t cap) {
 
 void cls_free(ClsGPU& c) {
     void* ps[] = {c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals, c.pts,
-                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.idx_out, c.box, c.nbr};
+                  c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.idx_out, c.box, c.nbr, c.nrm};
     for (void* p : ps) (void)hipFree(p);
     grid_free(c.grid);
     prim_free(c.w);
@@ -868,6 +879,16 @@ int pf_cls_ground_seg(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes
     if ((ground && ngr > cap) || (unground && nun > cap)) return PF_ECAPACITY;
     if (unground && nun) PF_HIP_TRY(hipMemcpy(unground, h->c.vals, sizeof(int) * nun, hipMemcpyDeviceToHost));
     if (ground && ngr) PF_HIP_TRY(hipMemcpy(ground, h->c.vals + nun, sizeof(int) * ngr, hipMemcpyDeviceToHost));
+    return PF_OK;
+}
+
+int pf_cls_normals(pf_cls* h, float* normal4, size_t n) {
+    if (!h || (!normal4 && n)) return PF_EINVAL;
+    int cnt[CC_COUNT];
+    PF_HIP_TRY(hipSetDevice(h->device));
+    PF_HIP_TRY(hipMemcpy(cnt, h->c.cnt, sizeof(cnt), hipMemcpyDeviceToHost));
+    if (n > (size_t)cnt[CC_NU]) return PF_ECAPACITY;
+    if (n) PF_HIP_TRY(hipMemcpy(normal4, h->c.nrm, sizeof(float4) * n, hipMemcpyDeviceToHost));
     return PF_OK;
 }
 

@@ -91,7 +91,7 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_map_update_device", "pf_map_update_mat", "pf_map_get", "pf_odom_set_stage_a_reserve",
            "pf_fe_set_ring_model", "pf_odom_set_ring_model", "pf_odom_get_state", "pf_odom_snapshot",
            "pf_odom_restore", "pf_odom_set_map_export", "pf_odom_map_export", "pf_odom_set_stage_timing",
-           "pf_odom_stage_times", "pf_odom_set_state"]
+           "pf_odom_stage_times", "pf_odom_set_state", "pf_cls_normals"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -125,6 +125,7 @@ def lib():
     L.pf_odom_set_graph.argtypes = [_vp, _i]
     L.pf_odom_set_stage_timing.argtypes = [_vp, _i]
     L.pf_odom_set_state.argtypes = [_vp, _vp, _vp, _i]
+    L.pf_cls_normals.argtypes = [_vp, _vp, _sz]
     L.pf_odom_stage_times.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(_sz)]
     if hasattr(L, "pf_odom_set_stage_a_reserve"):
@@ -600,15 +601,20 @@ class BPFFrontEnd:
                                                             max(n, 1)), allow_warn=False)
         return g[:ng.value].copy(), u[:nu.value].copy()
 
-    def classify(self, xyz):
-        """featureExtract alone: (index_with_feature code per point, neighbour count per point)."""
+    def classify(self, xyz, normals=False):
+        """featureExtract alone: (index_with_feature code per point, neighbour count per point[, the
+        normal assign_normal writes per point, [n, 4] float32])."""
         a = np.ascontiguousarray(xyz, dtype=np.float32)
         n = a.shape[0]
         cls = np.empty(max(n, 1), np.uint8)
         num = np.empty(max(n, 1), np.int32)
         _check("pf_cls_classify", lib().pf_cls_classify(self._h, a.ctypes.data, n, 4 * a.shape[1], cls.ctypes.data,
                                                         num.ctypes.data), allow_warn=False)
-        return cls[:n].copy(), num[:n].copy()
+        if not normals:
+            return cls[:n].copy(), num[:n].copy()
+        nrm = np.empty((max(n, 1), 4), np.float32)
+        _check("pf_cls_normals", lib().pf_cls_normals(self._h, nrm.ctypes.data, n), allow_warn=False)
+        return cls[:n].copy(), num[:n].copy(), nrm[:n].copy()
 
     def __del__(self):
         if getattr(self, "_h", None):

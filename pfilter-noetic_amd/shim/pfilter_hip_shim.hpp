@@ -513,10 +513,20 @@ private:
 };
 
 // nongroundExtract (include/preProcess.hpp:616-735): featureExtract on the non-ground cloud. CloudTpl
-// is the point-cloud template (pcl::PointCloud); PointN the output point (pcl::PointXYZINormal). The
-// outputs carry xyz; the PCA normals the reference also writes into them (assign_normal, :327-346) are
-// not produced — the BPF node copies the clouds to XYZRGB and drops them
-// (src/odomEstimationNode.cpp:236-240).
+// is the point-cloud template (pcl::PointCloud); PointN the output point (pcl::PointXYZINormal). As the
+// reference's assign_normal (:327-346) does, every classified point of the input cloud gets its PCA
+// normal (normal_x / _y / _z and the fourth float of the normal block, pt.normal[3]: linear_2 or
+// planar_2) before it is pushed to its class cloud.
+template <class P>
+auto set_pca_normal(P& pt, const float* n4, int) -> decltype((void)pt.normal_x, void()) {
+    pt.normal_x = n4[0];
+    pt.normal_y = n4[1];
+    pt.normal_z = n4[2];
+    (&pt.normal_x)[3] = n4[3];          // PCL's data_n[3], which the reference writes as pt.normal[3]
+}
+template <class P>
+void set_pca_normal(P&, const float*, long) {}     // a point type without normals: xyz only
+
 template <template <class> class CloudTpl, class PointN>
 class NongroundExtractT {
 public:
@@ -559,17 +569,22 @@ public:
         p.beam_h_min = beam_height_min;
         const size_t n = cloud_in->points.size();
         code_.resize(n ? n : 1);
-        check("pf_cls_classify", pf_cls_classify(cls_.get(p, n), n ? &cloud_in->points[0].x : nullptr, n,
-                                                 sizeof(PointT), code_.data(), nullptr));
+        pf_cls* h = cls_.get(p, n);
+        check("pf_cls_classify", pf_cls_classify(h, n ? &cloud_in->points[0].x : nullptr, n, sizeof(PointT),
+                                                 code_.data(), nullptr));
+        nrm_.resize(4 * (n ? n : 1));
+        check("pf_cls_normals", pf_cls_normals(h, nrm_.data(), n));
         index_with_feature.assign(n, 0);
         for (size_t i = 0; i < n; ++i) {
             const int c = code_[i];
             index_with_feature[i] = c;
             if (c == 0) continue;
+            set_pca_normal(cloud_in->points[i], &nrm_[4 * i], 0);
             PointN pn;
             pn.x = cloud_in->points[i].x;
             pn.y = cloud_in->points[i].y;
             pn.z = cloud_in->points[i].z;
+            set_pca_normal(pn, &nrm_[4 * i], 0);
             (c == 1 ? cloud_pillar : (c == 2 ? cloud_beam : cloud_facade))->push_back(pn);
         }
     }
@@ -586,6 +601,7 @@ public:
 private:
     ClsHandle cls_;
     std::vector<uint8_t> code_;
+    std::vector<float> nrm_;
 };
 
 // --------------------------------------------------------------------------------------------

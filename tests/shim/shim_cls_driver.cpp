@@ -52,8 +52,8 @@ int main(int argc, char** argv) {
         std::fwrite(sz, sizeof(long long), 5, o);
         for (const auto& c : {extra.cloud_beam, extra.cloud_pillar, extra.cloud_facade})
             for (const auto& q : c->points) {
-                const float v[3] = {q.x, q.y, q.z};
-                std::fwrite(v, sizeof(float), 3, o);
+                const float v[7] = {q.x, q.y, q.z, q.normal_x, q.normal_y, q.normal_z, q.curvature};
+                std::fwrite(v, sizeof(float), 7, o);
             }
     }
     std::fclose(o);

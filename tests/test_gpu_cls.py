@@ -45,6 +45,21 @@ def test_classify_matches_oracle(pa, pfref, pfsynth, fe):
     assert np.all(num <= 25) and np.mean(num == 25) > 0.5
 
 
+def test_normals_match_oracle(pa, pfref, pfsynth, fe):
+    """pf_cls_normals: the normal assign_normal writes into every classified point, bit-exact against
+    the oracle (same f32 PCA sums, same f64 eigensolver rounded to f32); zeros elsewhere."""
+    x = pfsynth.Sequence("S64", n_frames=6).frame(5)
+    g, u = pfref.ground_seg(x, pfref.cls_params())
+    U = x[u]
+    cls, num, nrm = fe.classify(U, normals=True)
+    ocls, onum, onrm = pfref.pca_classify(U, pfref.cls_params(), normals=True)
+    np.testing.assert_array_equal(cls, ocls)
+    np.testing.assert_array_equal(nrm.view(np.uint32), onrm.view(np.uint32))
+    on = cls > 0
+    np.testing.assert_allclose(np.linalg.norm(nrm[on, :3], axis=1), 1.0, atol=1e-5)
+    assert np.all(nrm[~on] == 0)
+
+
 @pytest.mark.parametrize("kw", [dict(k=5), dict(k=32, k_min=3), dict(radius=0.5), dict(ground_filter=0),
                                 dict(gf_grid_res=1.0, gf_min_grid_pts=3), dict(beam_h_min=-10.0, edge_thre=0.5)])
 def test_parameters(pa, pfref, pfsynth, kw):

@@ -82,7 +82,8 @@ def test_bpf_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
 
 def test_front_end_shim_matches_python_binding(pa, pfsynth, tmp_path):
     """groundSeg + nongroundExtract drop-in (shim) driven like src/additionNode.cpp:21-45: the published
-    beam / pillar / facade clouds equal the C ABI's index lists applied to the scan."""
+    beam / pillar / facade clouds equal the C ABI's index lists applied to the scan, and carry the
+    PCA normals assign_normal writes (include/preProcess.hpp:327-346) as pf_cls_normals reports them."""
     exe = str(tmp_path / "shim_cls_driver")
     lib = os.path.join(ROOT, "pfilter-noetic_amd")
     subprocess.check_call(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
@@ -105,10 +106,13 @@ def test_front_end_shim_matches_python_binding(pa, pfsynth, tmp_path):
         g, u = fe.ground_seg(x)
         assert list(sz) == [len(g), len(u), len(r["beam"]), len(r["pillar"]), len(r["facade"])]
         np.testing.assert_array_equal(g, r["ground"])
-        for k in ("beam", "pillar", "facade"):
-            xyz = np.frombuffer(raw, np.float32, 3 * len(r[k]), off).reshape(-1, 3)
-            off += 12 * len(r[k])
-            np.testing.assert_array_equal(xyz, x[r[k], :3])
+        U = x[u]
+        cls, _, nrm = fe.classify(U, normals=True)
+        for k, code in (("beam", 2), ("pillar", 1), ("facade", 3)):
+            rec = np.frombuffer(raw, np.float32, 7 * len(r[k]), off).reshape(-1, 7)
+            off += 28 * len(r[k])
+            np.testing.assert_array_equal(rec[:, :3], x[r[k], :3])
+            np.testing.assert_array_equal(rec[:, 3:].view(np.uint32), nrm[cls == code].view(np.uint32))
 
 
 def test_mapping_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):

@@ -205,6 +205,31 @@ def test_pca_known_geometry(pfref):
     assert list(num) == [2, 2, 3]                                    # d^2 = 1 exactly is outside
 
 
+def test_pca_normals_known_geometry(pfref):
+    """assign_normal (include/preProcess.hpp:327-346): a pole's points carry the principal direction
+    (+-z) with linear_2 = 1 in the fourth float, a wall's facade points the wall normal (+-y) with
+    planar_2 there; unclassified points carry zeros."""
+    p = pfref.cls_params()
+    t = np.linspace(0, 4, 81, dtype=np.float32)
+    pole = np.c_[np.zeros(81), np.zeros(81), t - 1].astype(np.float32)
+    cls, num, nrm = pfref.pca_classify(pole, p, normals=True)
+    on = cls == 1
+    assert on.sum() > 10
+    np.testing.assert_allclose(np.abs(nrm[on, 2]), 1.0, atol=1e-6)
+    np.testing.assert_allclose(nrm[on, 3], 1.0, atol=1e-6)
+    assert np.all(nrm[~on] == 0)
+    rng = np.random.default_rng(7)
+    u, v = rng.uniform(0, 3, (2, 2000))
+    wall = np.c_[u + 30, np.full(u.size, 5.0), v].astype(np.float32)
+    cls, num, nrm = pfref.pca_classify(wall, p, normals=True)
+    f = cls == 3
+    assert f.sum() > 100
+    np.testing.assert_allclose(np.abs(nrm[f, 1]), 1.0, atol=1e-5)
+    assert np.all((nrm[f, 3] > 0.65) & (nrm[f, 3] <= 1.0))
+    c2, n2 = pfref.pca_classify(wall, p)                       # the plain entry point: same classes
+    np.testing.assert_array_equal(c2, cls)
+
+
 def test_preprocess_chain(pfref, pfsynth):
     x = pfsynth.Sequence("S32", n_frames=2, az_steps=500).frame(1)
     p = pfref.cls_params()
