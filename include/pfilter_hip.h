@@ -156,8 +156,9 @@ int pf_odom_classes(pf_odom* h);
  * bounds; per cell the lowest z in (gf_min_ground_height, gf_max_ground_height], the 3x3 neighbourhood
  * minimum, and the ground / non-ground split. featureExtract (:646-689): per non-ground point the
  * <= k nearest non-ground points with d^2 < radius^2, their PCA, and the pillar / beam / facade
- * decision. The DCVC `curvedfilter` stage the launch file can insert between them is not part of
- * this path: with it off, as here, the non-ground cloud feeds featureExtract. */
+ * decision. The DCVC `curvedfilter` stage the KITTI launch file inserts between them
+ * (pfilter_kitti.launch:8) is enabled per handle with pf_cls_set_dcvc / pf_bpf_set_dcvc (below);
+ * with it off the non-ground cloud feeds featureExtract directly. */
 typedef struct {
     int ground_filter;                 /* additionNode `groundfilter` (pfilter_kitti.launch:10) */
     int gf_min_grid_pts;               /* gf_grid_pt_num_thre (preProcess.hpp:575) */
@@ -193,6 +194,34 @@ int pf_cls_classify(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, 
  * push order. n = the number of points wanted (at most that call's point count). */
 int pf_cls_normals(pf_cls* h, float* normal4, size_t n);
 
+/* ---------------- curvedVoxel (DCVC, src/additionClass.cpp:1-497) ----------------
+ * Polar (range, pitch, azimuth) voxels with range rings growing by start_r - k * delta_r, the 27-voxel
+ * neighbourhood of searchKNN (:196-225, its azimuth wrap and pitch-layer quirks kept), clusters of
+ * neighbouring occupied voxels, and the points of clusters larger than min_seg, cluster by cluster by
+ * size (ties: first point), each in input order (pointCloudSegPtr, :360-372). The reference's loops
+ * race under OpenMP; the device computes the connected components of the voxel neighbourhood (DESIGN.md
+ * §2 gives the statistical bar against the serial reading). The first call of a handle starts the
+ * range rings at 5 m (the member default, include/additionClass.hpp:105), later calls at 0. */
+typedef struct {
+    double start_r, delta_r, delta_p, delta_a;   /* config/config.yaml:50-53 (1, 0.003, 1.2, 1.2) */
+    int min_seg;                                 /* :54 (80) */
+    double min_range, max_range;                 /* velodyne sensorMinRange / sensorMaxRange (1, 120) */
+} pf_dcvc_params;
+typedef struct pf_dcvc pf_dcvc;
+void pf_dcvc_default_params(pf_dcvc_params* p);
+int pf_dcvc_create(const pf_dcvc_params* p, int device, size_t max_points, pf_dcvc** out);
+int pf_dcvc_destroy(pf_dcvc* h);
+/* curvedVoxel::run on one cloud (x, y, z floats at the start of each stride-byte record): the kept
+ * points as input indices in the published order (out_idx, cap entries; *n_out = their count) and
+ * per point its cluster's rank (1 = largest) or 0 (dropped); out_idx / label may be NULL. */
+int pf_dcvc_run(pf_dcvc* h, const float* xyz, size_t n, size_t stride_bytes, int32_t* out_idx, size_t* n_out,
+                int32_t* label, size_t cap);
+/* the next call is a first call again (a new sequence) */
+int pf_dcvc_reset(pf_dcvc* h);
+/* curvedfilter in the front end: DCVC runs on the non-ground cloud and featureExtract on its output
+ * (src/additionNode.cpp:29-39); p NULL turns it off (the default) */
+int pf_cls_set_dcvc(pf_cls* h, const pf_dcvc_params* p);
+
 /* BPF whole-frame mode: one raw scan (device pointer to n packed float4) per call; stage A runs the
  * front end above (ground_seg + featureExtract) into the beam / pillar / facade clouds, then the
  * VoxelGrid, stage B the odometry (the additionNode -> odomEstimationNode chain without ROS).
@@ -201,6 +230,8 @@ int pf_cls_normals(pf_cls* h, float* normal4, size_t n);
  * also reports PF_ECAPACITY when the front end's grids exceeded their limits (the frame then ran with
  * empty class clouds: a ground grid above 32,766 cells of gf_grid_res, or a 1 m grid above 2^23 cells). */
 int pf_bpf_set_front_end(pf_odom* h, const pf_cls_params* p);
+/* curvedfilter in the raw-scan BPF pipeline (the KITTI launch's default); p NULL turns it off */
+int pf_bpf_set_dcvc(pf_odom* h, const pf_dcvc_params* p);
 int pf_bpf_frame_scan_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]);
 
 /* ---------------- global map (LaserMappingClass, src/laserMappingClass.cpp) ----------------

@@ -173,6 +173,27 @@ int pfref_pca_classify(const float* xyz, size_t n, size_t stride, const pfref_cl
  * planar_2) for facade, zeros for unclassified points */
 int pfref_pca_classify_normals(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, uint8_t* cls,
                                int32_t* pt_num, float* normal4);
+/* curvedVoxel (DCVC, src/additionClass.cpp), serial semantics (pfref_dcvc.cpp header) */
+typedef struct {
+    double start_r, delta_r, delta_p, delta_a;   /* config/config.yaml:50-53 curvedVoxel */
+    int min_seg;                                 /* :54 */
+    double min_range, max_range;                 /* :7-8 velodyne sensorMinRange / sensorMaxRange */
+} pfref_dcvc_params;
+void pfref_dcvc_default_params(pfref_dcvc_params* p);
+/* out_idx: input indices of the kept points in the published order (pointCloudSegPtr); label: per
+ * point its cluster's rank (1 = largest) or 0 (dropped); first_frame: the node's first call (the
+ * polar range starts from the member default 5 m instead of 0). Any output may be NULL. */
+int pfref_dcvc(const float* xyz, size_t n, size_t stride, const pfref_dcvc_params* p, int first_frame,
+               int32_t* out_idx, size_t* n_out, int32_t* label);
+/* mode 0 = pfref_dcvc; mode 1 = connected components of the same neighbourhood (the device's reading) */
+int pfref_dcvc_mode(const float* xyz, size_t n, size_t stride, const pfref_dcvc_params* p, int first_frame,
+                    int mode, int32_t* out_idx, size_t* n_out, int32_t* label);
+/* the additionNode chain with curvedfilter on (src/additionNode.cpp:21-45): ground_seg -> DCVC on the
+ * non-ground cloud -> featureExtract on DCVC's output; class clouds as input indices */
+int pfref_bpf_preprocess_dcvc(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p,
+                              const pfref_dcvc_params* dp, int first_frame, int dcvc_mode, int32_t* beam, size_t* nb,
+                              int32_t* pillar, size_t* np, int32_t* facade, size_t* nf, int32_t* ground,
+                              size_t* ng);
 /* the chain: class clouds (input indices, in the published order); any output may be NULL */
 int pfref_bpf_preprocess(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, int32_t* beam,
                          size_t* nb, int32_t* pillar, size_t* np, int32_t* facade, size_t* nf, int32_t* ground,

@@ -80,6 +80,37 @@ def cls_params(**kw):
     return p
 
 
+class DcvcParams(ctypes.Structure):
+    """curvedVoxel parameters (config/config.yaml:7-8, 49-54)."""
+    _fields_ = [("start_r", ctypes.c_double), ("delta_r", ctypes.c_double), ("delta_p", ctypes.c_double),
+                ("delta_a", ctypes.c_double), ("min_seg", ctypes.c_int), ("min_range", ctypes.c_double),
+                ("max_range", ctypes.c_double)]
+
+
+def dcvc_params(**kw):
+    p = DcvcParams()
+    lib().pfref_dcvc_default_params(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def dcvc(xyz, params=None, first_frame=False, components=False):
+    """curvedVoxel::run: (input indices of the kept points in the published order, per-point cluster
+    rank 1.. or 0 for dropped points). components=False: the serial reading of the reference;
+    True: connected components of the same voxel neighbourhood (the device's reading)."""
+    a = np.ascontiguousarray(xyz, dtype=np.float32)
+    n = a.shape[0]
+    p = params or dcvc_params()
+    idx = np.empty(max(n, 1), np.int32)
+    lab = np.empty(max(n, 1), np.int32)
+    k = ctypes.c_size_t()
+    rc = lib().pfref_dcvc_mode(a.ctypes.data, n, 4 * a.shape[1], ctypes.byref(p), int(bool(first_frame)),
+                               int(bool(components)), idx.ctypes.data, ctypes.byref(k), lab.ctypes.data)
+    assert rc == 0
+    return idx[:k.value].copy(), lab[:n].copy()
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -124,6 +155,12 @@ def lib():
                                        ctypes.POINTER(_sz)]
         L.pfref_pca_classify.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams), _vp, _vp]
         L.pfref_pca_classify_normals.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams), _vp, _vp, _vp]
+        L.pfref_dcvc.argtypes = [_vp, _sz, _sz, ctypes.POINTER(DcvcParams), ctypes.c_int, _vp, ctypes.POINTER(_sz), _vp]
+        L.pfref_dcvc_default_params.argtypes = [ctypes.POINTER(DcvcParams)]
+        L.pfref_dcvc_mode.argtypes = [_vp, _sz, _sz, ctypes.POINTER(DcvcParams), ctypes.c_int, ctypes.c_int, _vp,
+                                      ctypes.POINTER(_sz), _vp]
+        L.pfref_bpf_preprocess_dcvc.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams), ctypes.POINTER(DcvcParams),
+                                                ctypes.c_int, ctypes.c_int] + [_vp, ctypes.POINTER(_sz)] * 4
         L.pfref_map_create.argtypes = [ctypes.c_double]
         L.pfref_map_create.restype = _vp
         L.pfref_map_destroy.argtypes = [_vp]
@@ -402,8 +439,10 @@ def pca_classify(xyz, params=None, normals=False):
     return cls[:n].copy(), num[:n].copy()
 
 
-def bpf_preprocess(xyz, params=None):
-    """additionNode's chain: dict of beam / pillar / facade / ground input-index arrays."""
+def bpf_preprocess(xyz, params=None, dcvc=None, first_frame=False, components=False):
+    """additionNode's chain: dict of beam / pillar / facade / ground input-index arrays. dcvc: DcvcParams
+    to run curvedVoxel between ground_seg and featureExtract (curvedfilter on); components: its
+    connected-components reading (the device's) instead of the serial one."""
     a = np.ascontiguousarray(xyz, dtype=np.float32)
     n = a.shape[0]
     p = params or cls_params()
@@ -412,7 +451,11 @@ def bpf_preprocess(xyz, params=None):
     args = []
     for b, c in zip(bufs, cnt):
         args += [b.ctypes.data, ctypes.byref(c)]
-    rc = lib().pfref_bpf_preprocess(a.ctypes.data, n, 4 * a.shape[1], ctypes.byref(p), *args)
+    if dcvc is not None:
+        rc = lib().pfref_bpf_preprocess_dcvc(a.ctypes.data, n, 4 * a.shape[1], ctypes.byref(p), ctypes.byref(dcvc),
+                                             int(bool(first_frame)), int(bool(components)), *args)
+    else:
+        rc = lib().pfref_bpf_preprocess(a.ctypes.data, n, 4 * a.shape[1], ctypes.byref(p), *args)
     assert rc == 0
     return {k: b[:c.value].copy() for k, b, c in zip(("beam", "pillar", "facade", "ground"), bufs, cnt)}
 

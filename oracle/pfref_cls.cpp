@@ -246,6 +246,28 @@ int pfref_pca_classify_normals(const float* xyz, size_t n, size_t stride, const 
 }
 
 // the additionNode chain (groundfilter -> featurePreExtract): class clouds as input indices
+// featureExtract on the points u (input indices, in that order): class clouds as input indices
+static void classify_into(const float* xyz, size_t stride, const pfref_cls_params& p, const std::vector<int>& u,
+                          int32_t* beam, size_t* nb, int32_t* pillar, size_t* np, int32_t* facade, size_t* nf) {
+    std::vector<P3> c(u.size());
+    for (size_t i = 0; i < u.size(); ++i) c[i] = *at(xyz, stride, (size_t)u[i]);
+    CellGrid grid;
+    grid.build(c);
+    const float r2 = (float)((double)p.radius * (double)p.radius);
+    std::vector<std::pair<float, int>> nbh;
+    size_t cnt[4] = {0, 0, 0, 0};
+    for (size_t i = 0; i < c.size(); ++i) {
+        radius_knn(c, grid, (int)i, r2, p.k, nbh);
+        const int k = pca_class(c, nbh, c[i].z, p);
+        int32_t* dst = k == 1 ? pillar : (k == 2 ? beam : (k == 3 ? facade : nullptr));
+        if (k && dst) dst[cnt[k]] = u[i];
+        cnt[k]++;
+    }
+    if (np) *np = cnt[1];
+    if (nb) *nb = cnt[2];
+    if (nf) *nf = cnt[3];
+}
+
 int pfref_bpf_preprocess(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p, int32_t* beam,
                          size_t* nb, int32_t* pillar, size_t* np, int32_t* facade, size_t* nf, int32_t* ground,
                          size_t* ng) {
@@ -257,24 +279,36 @@ int pfref_bpf_preprocess(const float* xyz, size_t n, size_t stride, const pfref_
         u.resize(n);
         for (size_t i = 0; i < n; ++i) u[i] = (int)i;
     }
-    std::vector<P3> c(u.size());
-    for (size_t i = 0; i < u.size(); ++i) c[i] = *at(xyz, stride, (size_t)u[i]);
-    CellGrid grid;
-    grid.build(c);
-    const float r2 = (float)((double)p->radius * (double)p->radius);
-    std::vector<std::pair<float, int>> nbh;
-    size_t cnt[4] = {0, 0, 0, 0};
-    for (size_t i = 0; i < c.size(); ++i) {
-        radius_knn(c, grid, (int)i, r2, p->k, nbh);
-        const int k = pca_class(c, nbh, c[i].z, *p);
-        int32_t* dst = k == 1 ? pillar : (k == 2 ? beam : (k == 3 ? facade : nullptr));
-        if (k && dst) dst[cnt[k]] = u[i];
-        cnt[k]++;
-    }
+    classify_into(xyz, stride, *p, u, beam, nb, pillar, np, facade, nf);
     if (ground) std::copy(g.begin(), g.end(), ground);
-    if (np) *np = cnt[1];
-    if (nb) *nb = cnt[2];
-    if (nf) *nf = cnt[3];
+    if (ng) *ng = g.size();
+    return 0;
+}
+
+int pfref_bpf_preprocess_dcvc(const float* xyz, size_t n, size_t stride, const pfref_cls_params* p,
+                              const pfref_dcvc_params* dp, int first_frame, int dcvc_mode, int32_t* beam, size_t* nb,
+                              int32_t* pillar, size_t* np, int32_t* facade, size_t* nf, int32_t* ground,
+                              size_t* ng) {
+    if (!p || !dp || (!xyz && n) || stride < 12) return -1;
+    std::vector<int> g, u;
+    if (p->ground_filter) {
+        ground_seg(xyz, n, stride, *p, g, u);
+    } else {
+        u.resize(n);
+        for (size_t i = 0; i < n; ++i) u[i] = (int)i;
+    }
+    std::vector<float> uc(3 * (u.size() ? u.size() : 1));
+    for (size_t i = 0; i < u.size(); ++i) {
+        const P3* q = at(xyz, stride, (size_t)u[i]);
+        uc[3 * i] = q->x; uc[3 * i + 1] = q->y; uc[3 * i + 2] = q->z;
+    }
+    std::vector<int32_t> kept(u.size() ? u.size() : 1);
+    size_t nk = 0;
+    if (pfref_dcvc_mode(uc.data(), u.size(), 12, dp, first_frame, dcvc_mode, kept.data(), &nk, nullptr)) return -1;
+    std::vector<int> v(nk);
+    for (size_t i = 0; i < nk; ++i) v[i] = u[(size_t)kept[i]];
+    classify_into(xyz, stride, *p, v, beam, nb, pillar, np, facade, nf);
+    if (ground) std::copy(g.begin(), g.end(), ground);
     if (ng) *ng = g.size();
     return 0;
 }

@@ -624,6 +624,27 @@ int pf_bpf_set_front_end(pf_odom* h, const pf_cls_params* p) {
     return PF_OK;
 }
 
+int pf_bpf_set_dcvc(pf_odom* h, const pf_dcvc_params* p) {
+    if (!h || h->o.cls.nc != 3) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    if (!o.front) {
+        pf_cls_params fp;
+        pf_cls_default_params(&fp);
+        const int rc = pf_bpf_set_front_end(h, &fp);
+        if (rc) return rc;
+    }
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    const int rc = cls_set_dcvc(*o.front, p);
+    if (rc) return rc;
+    for (int s = 0; s < kSlots; ++s)        // the front end's kernel sequence changed
+        if (o.graph_as[s]) {
+            (void)hipGraphExecDestroy(o.graph_as[s]);
+            o.graph_as[s] = nullptr;
+        }
+    return PF_OK;
+}
+
 int pf_bpf_frame_scan_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]) {
     if (!h || (!d_xyzi && n) || h->o.cls.nc != 3) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->o.device));

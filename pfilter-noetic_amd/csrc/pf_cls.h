@@ -15,6 +15,7 @@
 //                  radix sort by class (stable) + k_cls_out -> beam / pillar / facade clouds in U order
 #pragma once
 #include "pf_common.h"
+#include "pf_dcvc.h"
 #include "pf_knn.h"
 #include "pf_prims.h"
 
@@ -29,6 +30,7 @@ enum ClsCounter {
     CC_NG,           // ground points
     CC_CLS,          // [4] class sizes in key order: beam, pillar, facade, none
     CC_ERR = CC_CLS + 4,   // 1: ground grid larger than kGsMaxCells
+    CC_NUG,          // ground_seg's non-ground count (CC_NU after DCVC, when it runs, is its output's)
     CC_COUNT
 };
 
@@ -57,7 +59,12 @@ struct ClsGPU {
     GridGPU grid;
     PrimWork w;
     int* sticky = nullptr;       // not owned: where CC_ERR is also latched (OdomGPU::errw)
+    DcvcGPU* dcvc = nullptr;     // curvedfilter (pf_cls_set_dcvc / pf_bpf_set_dcvc); null: off
+    float4* dU = nullptr;        // [cap] DCVC output staging
+    u32* dV = nullptr;           // [cap]
 };
+// curvedfilter on / off (p null); allocates the DCVC state on first use
+int cls_set_dcvc(ClsGPU& c, const pf_dcvc_params* p);
 
 int cls_alloc(ClsGPU& c, size_t cap);
 void cls_free(ClsGPU& c);

@@ -249,6 +249,7 @@ __global__ void __launch_bounds__(256) k_gs_keys(const float4* __restrict__ pts,
 // pc2pc (:633-644): the non-ground cloud U in push order, xyz only
 __global__ void __launch_bounds__(256) k_gs_gather(const float4* __restrict__ pts, ClsDev d) {
     const int nu = d.cnt[CC_NU];
+    if (blockIdx.x == 0 && threadIdx.x == 0) d.cnt[CC_NUG] = nu;
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nu; j += gridDim.x * blockDim.x) {
         const float4 p = pts[PF_IDX(d, d.vals[j], d.cnt[CC_N])];
         d.U[j] = make_float4(p.x, p.y, p.z, 0.0f);
@@ -259,13 +260,39 @@ __global__ void __launch_bounds__(256) k_gs_gather(const float4* __restrict__ pt
 __global__ void __launch_bounds__(256) k_cls_identity(const float4* __restrict__ pts, const int* __restrict__ d_n, ClsDev d) {
     const int n = *d_n;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        d.cnt[CC_N] = n; d.cnt[CC_NU] = n; d.cnt[CC_NG] = 0; d.cnt[CC_ERR] = 0;
+        d.cnt[CC_N] = n; d.cnt[CC_NU] = n; d.cnt[CC_NUG] = n; d.cnt[CC_NG] = 0; d.cnt[CC_ERR] = 0;
         for (int k = 0; k < 4; ++k) d.cnt[CC_CLS + k] = 0;
     }
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
         const float4 p = pts[j];
         d.U[j] = make_float4(p.x, p.y, p.z, 0.0f);
         d.vals[j] = (u32)j;
+    }
+}
+
+// ---- curvedfilter: DCVC's output becomes the cloud featureExtract sees (src/additionNode.cpp:29-39) --
+// the kept points (DCVC's published order) and their input indices into staging, then back over U /
+// vals[0 ..) (the ground indices after ground_seg's non-ground count stay where pf_cls_extract reads them)
+__global__ void __launch_bounds__(256) k_dc_gather(ClsDev d, const u32* __restrict__ idx, const int* __restrict__ ddim,
+                                                    float4* __restrict__ tu, u32* __restrict__ tv) {
+    const int nk = ddim[D_NKEPT];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && ddim[D_ERR]) {       // too many rings / clusters
+        d.cnt[CC_ERR] = 3;
+        if (d.sticky) *d.sticky = 3;
+    }
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nk; j += gridDim.x * blockDim.x) {
+        const u32 u = idx[j];
+        tu[j] = d.U[u];
+        tv[j] = d.vals[u];
+    }
+}
+__global__ void __launch_bounds__(256) k_dc_commit(ClsDev d, const int* __restrict__ ddim, const float4* __restrict__ tu,
+                                                    const u32* __restrict__ tv) {
+    const int nk = ddim[D_ERR] ? 0 : ddim[D_NKEPT];
+    if (blockIdx.x == 0 && threadIdx.x == 0) d.cnt[CC_NU] = nk;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nk; j += gridDim.x * blockDim.x) {
+        d.U[j] = tu[j];
+        d.vals[j] = tv[j];
     }
 }
 
@@ -693,10 +720,41 @@ int cls_alloc(ClsGPU& c, size_t cap) {
     return prim_alloc(c.w, cap, kClsCells + 2);
 }
 
+int cls_set_dcvc(ClsGPU& c, const pf_dcvc_params* p) {
+    if (!p) {
+        if (c.dcvc) {
+            dcvc_free(*c.dcvc);
+            delete c.dcvc;
+            c.dcvc = nullptr;
+        }
+        return PF_OK;
+    }
+    if (!(p->delta_p > 0) || !(p->delta_a > 0) || !(p->start_r > 0) || p->delta_r < 0 || !(p->max_range > 0) ||
+        p->max_range >= 1e5 || p->min_seg < 0)
+        return PF_EINVAL;
+    if (!c.dcvc) {
+        c.dcvc = new DcvcGPU();
+        int rc = dcvc_alloc(*c.dcvc, c.cap);
+        if (rc == PF_OK && !c.dU && hipMalloc(&c.dU, sizeof(float4) * c.cap) != hipSuccess) rc = PF_ENOMEM;
+        if (rc == PF_OK && !c.dV && hipMalloc(&c.dV, sizeof(u32) * c.cap) != hipSuccess) rc = PF_ENOMEM;
+        if (rc) {
+            dcvc_free(*c.dcvc);
+            delete c.dcvc;
+            c.dcvc = nullptr;
+            return rc;
+        }
+    }
+    c.dcvc->prm = *p;
+    return PF_OK;
+}
+
 void cls_free(ClsGPU& c) {
     void* ps[] = {c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals, c.pts,
                   c.U, c.ckeys, c.cvals, c.code, c.ptnum, c.idx_out, c.box, c.nbr, c.nrm};
     for (void* p : ps) (void)hipFree(p);
+    (void)cls_set_dcvc(c, nullptr);
+    (void)hipFree(c.dU);
+    (void)hipFree(c.dV);
     grid_free(c.grid);
     prim_free(c.w);
     c = ClsGPU{};
@@ -716,6 +774,12 @@ void cls_enqueue(ClsGPU& c, const float4* d_pts, const int* d_n, float4* const* 
         hipLaunchKernelGGL(k_cls_identity, dim3(kEwBlocks), dim3(256), 0, s, d_pts, d_n, d);
     }
     if (ground_only) return;
+    if (c.dcvc) {                                    // curvedfilter: DCVC on the non-ground cloud
+        u32* kept = nullptr;
+        dcvc_enqueue(*c.dcvc, c.U, c.cnt + CC_NU, s, &kept);
+        hipLaunchKernelGGL(k_dc_gather, dim3(kEwBlocks), dim3(256), 0, s, d, kept, c.dcvc->dim, c.dU, c.dV);
+        hipLaunchKernelGGL(k_dc_commit, dim3(kEwBlocks), dim3(256), 0, s, d, c.dcvc->dim, c.dU, c.dV);
+    }
     GridPtrs gp{};
     gp.m[0] = c.U;
     gp.n[0] = c.cnt + CC_NU;
@@ -858,7 +922,8 @@ int pf_cls_extract(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, i
     if (beam && n0) PF_HIP_TRY(hipMemcpy(beam, h->c.idx_out, sizeof(int) * n0, hipMemcpyDeviceToHost));
     if (pillar && n1) PF_HIP_TRY(hipMemcpy(pillar, h->c.idx_out + n0, sizeof(int) * n1, hipMemcpyDeviceToHost));
     if (facade && n2) PF_HIP_TRY(hipMemcpy(facade, h->c.idx_out + n0 + n1, sizeof(int) * n2, hipMemcpyDeviceToHost));
-    if (ground && ngr) PF_HIP_TRY(hipMemcpy(ground, h->c.vals + nu, sizeof(int) * ngr, hipMemcpyDeviceToHost));
+    if (ground && ngr) PF_HIP_TRY(hipMemcpy(ground, h->c.vals + cnt[CC_NUG], sizeof(int) * ngr, hipMemcpyDeviceToHost));
+    (void)nu;
     return PF_OK;
 }
 
@@ -882,6 +947,13 @@ int pf_cls_ground_seg(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes
     return PF_OK;
 }
 
+int pf_cls_set_dcvc(pf_cls* h, const pf_dcvc_params* p) {
+    if (!h) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->device));
+    PF_HIP_TRY(hipStreamSynchronize(h->stream));
+    return cls_set_dcvc(h->c, p);
+}
+
 int pf_cls_normals(pf_cls* h, float* normal4, size_t n) {
     if (!h || (!normal4 && n)) return PF_EINVAL;
     int cnt[CC_COUNT];
@@ -895,9 +967,12 @@ int pf_cls_normals(pf_cls* h, float* normal4, size_t n) {
 int pf_cls_classify(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, uint8_t* cls, int32_t* pt_num) {
     if (!h || (!xyz && n) || stride_bytes < 12) return PF_EINVAL;
     const int gf = h->c.prm.ground_filter;
+    DcvcGPU* dc = h->c.dcvc;                          // featureExtract alone: no ground_seg, no DCVC
     h->c.prm.ground_filter = 0;
+    h->c.dcvc = nullptr;
     int rc = cls_run(h, xyz, n, stride_bytes, false);
     h->c.prm.ground_filter = gf;
+    h->c.dcvc = dc;
     if (rc) return rc;
     int gerr = 0;
     PF_HIP_TRY(hipMemcpy(&gerr, h->c.grid.err, sizeof(int), hipMemcpyDeviceToHost));

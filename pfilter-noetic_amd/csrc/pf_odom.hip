@@ -1619,6 +1619,7 @@ int odom_reset(OdomGPU& o) {
     for (int p = 0; p < kSlots; ++p)
         if (hipMemsetAsync(o.sb[p].cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)o.cls.nc * o.map_cap);
+    if (o.front && o.front->dcvc && dcvc_reset(*o.front->dcvc, o.stream) != PF_OK) return PF_EHIP;   // a first frame again
     if (hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
     o.opt_count_host = 2;
     o.inited = false;

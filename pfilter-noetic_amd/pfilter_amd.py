@@ -69,6 +69,51 @@ class OdomStats(ctypes.Structure):
         return d
 
 
+class DcvcParams(ctypes.Structure):
+    """pf_dcvc_params: curvedVoxel (config/config.yaml:7-8, 49-54)."""
+    _fields_ = [("start_r", ctypes.c_double), ("delta_r", ctypes.c_double), ("delta_p", ctypes.c_double),
+                ("delta_a", ctypes.c_double), ("min_seg", ctypes.c_int), ("min_range", ctypes.c_double),
+                ("max_range", ctypes.c_double)]
+
+
+def dcvc_params(**kw):
+    p = DcvcParams()
+    lib().pf_dcvc_default_params(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class Dcvc:
+    """curvedVoxel on the device (pf_dcvc_*): run(xyz) -> (kept input indices in the published order,
+    per-point cluster rank 1.. / 0). The first call of a handle (or after reset) is a first frame."""
+
+    def __init__(self, max_points=300000, device=0, **params):
+        self._h = None
+        h = _vp()
+        _check("pf_dcvc_create", lib().pf_dcvc_create(ctypes.byref(dcvc_params(**params)), device, max_points,
+                                                      ctypes.byref(h)), allow_warn=False)
+        self._h = h
+
+    def run(self, xyz):
+        a = np.ascontiguousarray(xyz, dtype=np.float32)
+        n = a.shape[0]
+        idx = np.empty(max(n, 1), np.int32)
+        lab = np.empty(max(n, 1), np.int32)
+        k = _sz()
+        _check("pf_dcvc_run", lib().pf_dcvc_run(self._h, a.ctypes.data, n, 4 * a.shape[1], idx.ctypes.data,
+                                                ctypes.byref(k), lab.ctypes.data, max(n, 1)), allow_warn=False)
+        return idx[:k.value].copy(), lab[:n].copy()
+
+    def reset(self):
+        _check("pf_dcvc_reset", lib().pf_dcvc_reset(self._h), allow_warn=False)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().pf_dcvc_destroy(self._h)
+            self._h = None
+
+
 class ClsParams(ctypes.Structure):
     """pf_cls_params: groundSeg / nongroundExtract members (include/preProcess.hpp:575-605, :703-715)."""
     _fields_ = [("ground_filter", ctypes.c_int), ("gf_min_grid_pts", ctypes.c_int),
@@ -91,7 +136,8 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_map_update_device", "pf_map_update_mat", "pf_map_get", "pf_odom_set_stage_a_reserve",
            "pf_fe_set_ring_model", "pf_odom_set_ring_model", "pf_odom_get_state", "pf_odom_snapshot",
            "pf_odom_restore", "pf_odom_set_map_export", "pf_odom_map_export", "pf_odom_set_stage_timing",
-           "pf_odom_stage_times", "pf_odom_set_state", "pf_cls_normals"]
+           "pf_odom_stage_times", "pf_odom_set_state", "pf_cls_normals", "pf_dcvc_default_params",
+           "pf_dcvc_create", "pf_dcvc_destroy", "pf_dcvc_run", "pf_dcvc_reset", "pf_cls_set_dcvc", "pf_bpf_set_dcvc"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -126,6 +172,13 @@ def lib():
     L.pf_odom_set_stage_timing.argtypes = [_vp, _i]
     L.pf_odom_set_state.argtypes = [_vp, _vp, _vp, _i]
     L.pf_cls_normals.argtypes = [_vp, _vp, _sz]
+    L.pf_dcvc_default_params.argtypes = [ctypes.POINTER(DcvcParams)]
+    L.pf_dcvc_create.argtypes = [ctypes.POINTER(DcvcParams), _i, _sz, ctypes.POINTER(_vp)]
+    L.pf_dcvc_destroy.argtypes = [_vp]
+    L.pf_dcvc_run.argtypes = [_vp, _vp, _sz, _sz, _vp, ctypes.POINTER(_sz), _vp, _sz]
+    L.pf_dcvc_reset.argtypes = [_vp]
+    L.pf_cls_set_dcvc.argtypes = [_vp, ctypes.POINTER(DcvcParams)]
+    L.pf_bpf_set_dcvc.argtypes = [_vp, ctypes.POINTER(DcvcParams)]
     L.pf_odom_stage_times.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(_sz)]
     if hasattr(L, "pf_odom_set_stage_a_reserve"):
@@ -505,6 +558,11 @@ class Odom_BPF_EstimationClass(Odom_ES_EstimationClass):
         _check("pf_bpf_set_front_end", lib().pf_bpf_set_front_end(self._h, ctypes.byref(self.front_params)),
                allow_warn=False)
 
+    def set_dcvc(self, enable=True, **params):
+        """curvedfilter (pf_bpf_set_dcvc): DCVC between ground_seg and featureExtract in raw-scan mode"""
+        p = ctypes.byref(dcvc_params(**params)) if enable else None
+        _check("pf_bpf_set_dcvc", lib().pf_bpf_set_dcvc(self._h, p), allow_warn=False)
+
     def frame_scan_device(self, dptr, n, want_pose=False):
         """one raw scan already in HBM (packed float4) -> pose"""
         pose = np.empty(7)
@@ -577,6 +635,11 @@ class BPFFrontEnd:
         _check("pf_cls_create", lib().pf_cls_create(ctypes.byref(self.params), device, int(max_points),
                                                     ctypes.byref(h)), allow_warn=False)
         self._h = h.value
+
+    def set_dcvc(self, enable=True, **params):
+        """curvedfilter (pf_cls_set_dcvc): extract() runs DCVC on the non-ground cloud first"""
+        p = ctypes.byref(dcvc_params(**params)) if enable else None
+        _check("pf_cls_set_dcvc", lib().pf_cls_set_dcvc(self._h, p), allow_warn=False)
 
     def extract(self, xyz):
         a = np.ascontiguousarray(xyz, dtype=np.float32)
