@@ -1491,9 +1491,16 @@ void alias_err(int*& flag, int* word) {
     flag = word;
 }
 
+// development: PF_TRACE_CREATE=1 prints the create steps (stderr)
+static void trace_create(const char* step) {
+    static const bool on = std::getenv("PF_TRACE_CREATE") != nullptr;
+    if (on) std::fprintf(stderr, "pf create: %s\n", step);
+}
+
 int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& prm, int device, size_t in_cap,
                 size_t map_cap, int nc) {
     if (nc < 2 || nc > kMaxC) return PF_EINVAL;
+    trace_create("begin");
     o.lidar = lidar;
     o.prm = prm;
     o.device = device;
@@ -1509,13 +1516,16 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
         o.leaf_rg[c] = plane ? (float)prm.map_res * 2 : (float)prm.map_res;     // float map_resolution (.h:62)
     }
     if (hipStreamCreateWithFlags(&o.stream, hipStreamNonBlocking) != hipSuccess) return PF_EHIP;
+    trace_create("stream");
     // stage A is kept off the last compute units by default (odom_stage_a_stream), so that stage B's
     // kernels — the LM needs kLmBlocks co-resident workgroups — find free CUs while stage A runs
     int reserve = nc == 2 ? kStageAReserveES : kStageAReserveBPF;
     if (const char* e = std::getenv("PF_STAGE_A_CU_RESERVE")) reserve = std::atoi(e);   // development override
     if (odom_stage_a_stream(o, reserve) != PF_OK && odom_stage_a_stream(o, 0) != PF_OK) return PF_EHIP;
+    trace_create("stage A stream");
     int rc = fe_alloc(o.fe, lidar, in_cap);
     if (rc) return rc;
+    trace_create("fe_alloc");
     // 1 m cells over every map's bounding box: 3 x (201 m)^2 x 270 m covers the +-100 m crop box
     rc = grid_alloc(o.grid, (size_t)nc * map_cap, (size_t)1 << 25);
     if (rc) return rc;
@@ -1523,6 +1533,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (rc) return rc;
     rc = prim_alloc(o.vprim, (size_t)nc * in_cap);
     if (rc) return rc;
+    trace_create("grid / prims");
     const size_t nq = (size_t)nc * in_cap;
 #define PF_ALLOC(ptr, bytes) \
     if (hipMalloc(&(ptr), (bytes)) != hipSuccess) return PF_ENOMEM;
@@ -1536,7 +1547,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
             PF_ALLOC(o.sb[p].ds[c], sizeof(float4) * in_cap);
         }
         PF_ALLOC(o.sb[p].cnt, sizeof(int) * C_COUNT);
-        if (hipMemset(o.sb[p].cnt, 0, sizeof(int) * C_COUNT) != hipSuccess) return PF_EHIP;
+        if (hipMemsetAsync(o.sb[p].cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
         if (hipEventCreateWithFlags(&o.ev_a[p], hipEventDisableTiming) != hipSuccess) return PF_EHIP;
         if (hipEventCreateWithFlags(&o.ev_b[p], hipEventDisableTiming) != hipSuccess) return PF_EHIP;
     }
@@ -1571,6 +1582,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.poses, sizeof(double) * 7 * o.pose_cap);
     PF_ALLOC(o.stage, sizeof(float4) * nq);
 #undef PF_ALLOC
+    trace_create("buffers");
     if (std::getenv("PF_PROBE")) {                 // development probe: LM phase timestamps
         if (hipMalloc(&o.dbg, sizeof(unsigned long long) * 64) != hipSuccess) return PF_ENOMEM;
         if (hipMemset(o.dbg, 0, sizeof(unsigned long long) * 64) != hipSuccess) return PF_EHIP;
@@ -1583,20 +1595,26 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     h.params[3] = 1.0;
     for (int i = 0; i < 3; ++i) h.odomR[4 * i] = h.lastR[4 * i] = 1.0;
     h.optimization_count = 2;
-    if (hipMemcpy(o.st, &h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) return PF_EHIP;
-    if (hipMemset(o.cnt, 0, sizeof(int) * C_COUNT) != hipSuccess) return PF_EHIP;
-    if (hipMemset(o.acc, 0, sizeof(u32) * A_COUNT) != hipSuccess) return PF_EHIP;
-    if (hipMemset(o.acc_a, 0, sizeof(u32) * A_COUNT) != hipSuccess) return PF_EHIP;
-    if (hipMemset(o.lm, 0, sizeof(LMState)) != hipSuccess) return PF_EHIP;
-    if (hipMemset(o.lm_ticket, 0, sizeof(u32) * 2 * kLmEvalSlots) != hipSuccess) return PF_EHIP;
-    if (hipMemset(o.errw, 0, sizeof(int) * E_COUNT) != hipSuccess) return PF_EHIP;
+    trace_create("pinned");
+    // stream-ordered on the handle's own non-blocking stream (null-stream copies would also wait for
+    // every blocking stream of the process, e.g. other handles' CU-masked stage-A streams)
+    if (hipMemcpyAsync(o.st, &h, sizeof(h), hipMemcpyHostToDevice, o.stream) != hipSuccess) return PF_EHIP;
+    trace_create("state copy");
+    if (hipMemsetAsync(o.cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.acc, 0, sizeof(u32) * A_COUNT, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.acc_a, 0, sizeof(u32) * A_COUNT, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.lm, 0, sizeof(LMState), o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.lm_ticket, 0, sizeof(u32) * 2 * kLmEvalSlots, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     // the sub-objects' overflow / wait flags latch into the handle's sticky error words
     alias_err(o.fe.err, o.errw + E_FE_SECTOR);
     alias_err(o.grid.err, o.errw + E_GRID);
     alias_err(o.prim.err, o.errw + E_SORT_B);
     alias_err(o.vprim.err, o.errw + E_SORT_A);
+    trace_create("memsets");
     hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)nc * map_cap);   // all empty
     if (hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
+    trace_create("done");
     o.opt_count_host = 2;
     return PF_OK;
 }
