@@ -410,7 +410,7 @@ def host_leg(device, nframes, threads):
             "note": "pf_odom_frame_host: scans in pageable host memory, repacked and copied H2D per frame"}
 
 
-def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True, use_graph=True):
+def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True, use_graph=True, dcvc=False):
     """The BPF chain frames/s on the same S64 sequence with configs[1]'s odometry parameters: raw scan ->
     groundSeg::ground_seg + nongroundExtract::featureExtract (include/preProcess.hpp:398-505, 646-689) ->
     Odom_BPF_EstimationClass (src/odomEstimationClass.cpp:649-1306), i.e. the additionNode ->
@@ -432,6 +432,8 @@ def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True
     od = pa.Odom_BPF_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lidar_cfg(), **ODOM_CFG)
     od.set_graph(use_graph)
+    if dcvc:
+        od.set_dcvc(True)                        # curvedfilter on, as launch/pfilter_kitti.launch:8
 
     def run(k):
         od.frame_scan_device(scans.ptr + k * stride, counts[k])
@@ -447,14 +449,15 @@ def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True
     st = od.stats()
     out = {"value": round(nframes / el, 2), "unit": "frames/s", "frames": nframes,
            "ms_per_step": round(el / nframes * 1e3, 4),
-           "workload": "raw S64 seed 0 scan -> ground_seg + PCA featureExtract (reference defaults) -> "
-                       "Odom_BPF_EstimationClass (configs[1] parameters)",
+           "workload": "raw S64 seed 0 scan -> ground_seg + %sPCA featureExtract (reference defaults) -> "
+                       "Odom_BPF_EstimationClass (configs[1] parameters)" % ("DCVC (curvedfilter) + " if dcvc else ""),
            "last_frame": {"n_in": st["n_in"], "n_ds": st["n_ds"], "n_map": st["n_map"], "n_res": st["n_res"]}}
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pfref
         lid = pfref.make_lidar(64, 3.0, 90.0)
         cp = pfref.cls_params()
+        dp = pfref.dcvc_params() if dcvc else None
         orc = pfref.OdomBPF(lid, 0.4, 0, 0.4, 75, 0, opts=0)
         cw = min(warmup, 11)                     # optimization_count reaches its steady 2 after 10 frames
         n, el, k = 0, 0.0, 0
@@ -462,7 +465,7 @@ def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True
         while k < total and (el < cpu_seconds or k < cw):
             x = seq.frame(k)
             t = time.perf_counter()
-            r = pfref.bpf_preprocess(x, cp)
+            r = pfref.bpf_preprocess(x, cp, dcvc=dp, first_frame=(k == 0))
             cl = [np.c_[x[r[c], :3], np.zeros(len(r[c]))].astype(np.float32) for c in ("beam", "pillar", "facade")]
             if k == 0:
                 orc.init_map(*cl)
@@ -751,12 +754,13 @@ def main(argv=None):
             log("roofline leg failed: %r" % (e,))
             out["roofline"] = None
     if world == 1 and args.bpf_frames > 0 and not stub:
-        try:
-            out["bpf"] = bpf_leg(local_rank, args.bpf_frames, threads, with_cpu=not args.no_cpu,
-                                 use_graph=not args.no_graph)
-        except Exception as e:  # report, never hide
-            log("bpf leg failed: %r" % (e,))
-            out["bpf"] = None
+        for name, dc in (("bpf", False), ("bpf_dcvc", True)):
+            try:
+                out[name] = bpf_leg(local_rank, args.bpf_frames, threads, with_cpu=not args.no_cpu,
+                                    use_graph=not args.no_graph, dcvc=dc)
+            except Exception as e:  # report, never hide
+                log("%s leg failed: %r" % (name, e))
+                out[name] = None
     if world == 1 and args.leg_frames > 0 and not stub:
         for name in ES_LEGS:
             try:

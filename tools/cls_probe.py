@@ -12,10 +12,13 @@ import pfsynth  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=50)
+ap.add_argument("--dcvc", action="store_true", help="curvedfilter on (DCVC between ground_seg and featureExtract)")
 a = ap.parse_args()
 seq = pfsynth.Sequence("S64", n_frames=8, seed=0)
 frames = [seq.frame(k) for k in range(8)]
 fe = pa.BPFFrontEnd(max_points=300000)
+if a.dcvc:
+    fe.set_dcvc(True)
 fe.extract(frames[0])
 t = time.perf_counter()
 for i in range(a.iters):

@@ -51,6 +51,11 @@ if [ "$WHAT" = bench ] || [ "$WHAT" = all ]; then
     rc=$?
     if [ $rc -ne 0 ]; then echo "CLS PROF FAILED rc=$rc"; tail -n 20 $OUT/cls_prof.log; exit $rc; fi
     grep ms/frame $OUT/cls_prof.log
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/dcvc_prof -o run --output-format csv -- \
+        python3 tools/cls_probe.py --iters 50 --dcvc > $OUT/dcvc_prof.log 2>&1
+    rc=$?
+    if [ $rc -ne 0 ]; then echo "DCVC PROF FAILED rc=$rc"; tail -n 20 $OUT/dcvc_prof.log; exit $rc; fi
+    grep ms/frame $OUT/dcvc_prof.log
     # the global map (LaserMappingClass) updates
     timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/map_prof -o run --output-format csv -- \
         python3 tools/map_probe.py --frames 200 > $OUT/map_prof.log 2>&1
