@@ -744,8 +744,7 @@ int cls_set_dcvc(ClsGPU& c, const pf_dcvc_params* p) {
             return rc;
         }
     }
-    c.dcvc->prm = *p;
-    return PF_OK;
+    return dcvc_set_params(*c.dcvc, *p);
 }
 
 void cls_free(ClsGPU& c) {

@@ -8,10 +8,15 @@
 //                 sequential doubles) and counts the call (the first call starts the range at 5 m)
 //   k_dc_keys     per point: polar / pitch / azimuth index and voxel index (createHashTable :143-177)
 //   radix sort    (voxel, point) stable, segments = voxels
-//   k_dc_union    per voxel: its <= 27 search positions (searchKNN :196-225 with its azimuth wrap /
-//                 clamp and pitch-layer quirks), union with every occupied one (lock-free union-find,
-//                 smaller root wins)
-//   k_dc_sizes    per voxel: its component's point count and first point
+//   k_dc_voxels   per voxel: key, point count; its slot entered in a dense table over the voxel index
+//                 space (cleared again by k_dc_compress), so a neighbour lookup is one load
+//   k_dc_link     per voxel: its <= 27 search positions (searchKNN :196-225 with its azimuth wrap /
+//                 clamp and pitch-layer quirks) looked up at once; parent = the smallest (ECL-CC style
+//                 first link), the other edges listed (a two-way edge at its smaller end only)
+//   k_dc_union    per voxel: union over its listed edges (lock-free union-find: smaller root wins,
+//                 path halving)
+//   k_dc_compress per voxel: full compression, its component's point count and first point (one atomic
+//                 pair per distinct root and wave), the voxel table emptied
 //   k_dc_rank     one workgroup: components larger than minSeg ranked by size, then first point
 //   k_dc_label    per voxel: its points' sort keys (component rank or dropped), then a stable sort by
 //                 rank gives the published order (labelAnalysis :325-355, colorSegmentation :360-372)
@@ -52,10 +57,16 @@ struct DcvcGPU {
     u32* plab = nullptr;         // [cap] per point: its component's rank + 1, or 0 (dropped)
     u32* ukey = nullptr;         // [cap] per voxel: its key
     u32* ucount = nullptr;       // [cap] per voxel: its point count
+    int* vtab = nullptr;         // [vtab_cells] voxel slot of every cell of the index space, -1 empty
+    long long vtab_cells = 0;    // (0: the index space is too large, voxels are found by binary search)
+    u32* edges = nullptr;        // [cap][26] per voxel: the search edges it unions (k_dc_link)
+    u32* ecount = nullptr;       // [cap]
     PrimWork w;
 };
 
 int dcvc_alloc(DcvcGPU& d, size_t cap);
+// the parameters, and the voxel table sized for their index space (allocated outside any capture)
+int dcvc_set_params(DcvcGPU& d, const pf_dcvc_params& p);
 void dcvc_free(DcvcGPU& d);
 // the call counter back to 0 (the next call is a first frame)
 int dcvc_reset(DcvcGPU& d, hipStream_t s);

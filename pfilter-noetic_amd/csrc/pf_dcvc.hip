@@ -2,6 +2,7 @@
 #include "pf_dcvc.h"
 
 #include <cfloat>
+#include <cstdlib>
 #include <climits>
 #include <cmath>
 #include <vector>
@@ -21,6 +22,10 @@ struct DcvcDev {
     int* seg_aux;
     u32 *parent, *csize, *cfirst, *crank, *okeys, *ovals, *plab;
     u32 *ukey, *ucount;
+    int* vtab;
+    long long vtab_cells;
+    u32* edges;        // [cap][26] per voxel: the search edges it unions
+    u32* ecount;       // [cap]
 };
 
 __device__ __forceinline__ u64 dord(double d) {       // order-preserving bits of a double
@@ -140,9 +145,10 @@ __global__ void __launch_bounds__(256) k_dc_voxels(DcvcDev d) {
     const int nseg = d.seg_aux[0], nvalid = d.seg_aux[4];
     for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
         const u32 b0 = d.segstart[s], b1 = s + 1 < nseg ? d.segstart[s + 1] : (u32)nvalid;
-        d.ukey[s] = d.keys[b0];
+        const u32 key = d.keys[b0];
+        d.ukey[s] = key;
         d.ucount[s] = b1 - b0;
-        d.parent[s] = (u32)s;
+        if ((long long)key < d.vtab_cells) d.vtab[key] = s;
         d.csize[s] = 0u;
         d.cfirst[s] = 0xFFFFFFFFu;
         d.crank[s] = 0u;
@@ -152,85 +158,175 @@ __global__ void __launch_bounds__(256) k_dc_voxels(DcvcDev d) {
 __device__ __forceinline__ u32 dc_parent(const DcvcDev& d, u32 v) {
     return __hip_atomic_load(&d.parent[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// root of v, halving the path on the way (every store replaces a parent by one of its ancestors, so
+// concurrent finds and hooks see a forest with the same roots)
 __device__ __forceinline__ u32 dc_find(const DcvcDev& d, u32 v) {
-    for (u32 p = dc_parent(d, v); p != v; p = dc_parent(d, v)) v = p;   // parents only decrease: ends
-    return v;
+    for (;;) {
+        const u32 p = dc_parent(d, v);
+        if (p == v) return v;
+        const u32 gp = dc_parent(d, p);
+        if (gp == p) return p;
+        __hip_atomic_store(&d.parent[v], gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = gp;
+    }
 }
 
-// searchKNN (:196-225) of every voxel, unioned with each occupied position (lock-free, the smaller
-// root wins, so the components do not depend on the order of the unions)
-__global__ void __launch_bounds__(256) k_dc_union(DcvcDev d) {
+// slot of the occupied voxel with key nk, or -1: the table, or a binary search over the sorted keys
+__device__ __forceinline__ int dc_lookup(const DcvcDev& d, long long nk, int nseg) {
+    if (nk < d.vtab_cells) return d.vtab[nk];
+    int lo = 0, hi = nseg;
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if ((long long)d.ukey[m] < nk) lo = m + 1; else hi = m;
+    }
+    return (lo < nseg && (long long)d.ukey[lo] == nk) ? lo : -1;
+}
+
+// the occupied search positions of voxel s (searchKNN :196-225: pitch layers above `height` skipped,
+// azimuth -1 wrapped to width - 1, azimuth above 300 clamped to 300), -1 where empty
+__device__ __forceinline__ void dc_search(const DcvcDev& d, int s, int nseg, int P, int W, int H, long long L,
+                                          int (&nb)[27], int& x0, int& z0) {
+    const long long key = d.ukey[s];
+    z0 = (int)(key / L);
+    const int rem = (int)(key % L);
+    x0 = rem / (P + 1);
+    const int y0 = rem % (P + 1);
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+        const int z = z0 - 1 + k / 9, y = y0 - 1 + (k / 3) % 3, x = x0 - 1 + k % 3;
+        int ax = x;
+        if (ax < 0) ax = W - 1;
+        if (ax > 300) ax = 300;
+        const long long nk = ((long long)ax * (P + 1) + y) + (long long)z * L;
+        nb[k] = (z < 0 || z > H || y < 0 || y > P) ? -1 : dc_lookup(d, nk, nseg);
+    }
+}
+
+// per voxel: its occupied search positions; the smallest (or itself) becomes its parent (ECL-CC style
+// initialisation, so the trees the unions walk start shallow) and the other edges it must union are
+// listed (an edge whose reverse is also a search edge is listed at its smaller end only)
+__device__ __forceinline__ bool dc_take(const DcvcDev& d, int s, int v, int m, int x0, int z0, int P, int W, int H,
+                                        long long L);
+__global__ void __launch_bounds__(256) k_dc_link(DcvcDev d) {
     const int nseg = d.seg_aux[0];
     const int P = d.dim[D_POLAR], W = d.dim[D_WIDTH], H = d.dim[D_HEIGHT];
     const long long L = (long long)(P + 1) * (W + 1);
     for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
-        const long long key = d.ukey[s];
-        const int z0 = (int)(key / L), rem = (int)(key % L);
-        const int x0 = rem / (P + 1), y0 = rem % (P + 1);
-        for (int z = z0 - 1; z <= z0 + 1; ++z) {
-            if (z < 0 || z > H) continue;
-            for (int y = y0 - 1; y <= y0 + 1; ++y) {
-                if (y < 0 || y > P) continue;
-                for (int x = x0 - 1; x <= x0 + 1; ++x) {
-                    int ax = x;
-                    if (ax < 0) ax = W - 1;
-                    if (ax > 300) ax = 300;
-                    const long long nk = ((long long)ax * (P + 1) + y) + (long long)z * L;
-                    int lo = 0, hi = nseg;                  // the occupied voxel with key nk, if any
-                    while (lo < hi) {
-                        const int m = (lo + hi) >> 1;
-                        if ((long long)d.ukey[m] < nk) lo = m + 1; else hi = m;
-                    }
-                    if (lo >= nseg || (long long)d.ukey[lo] != nk || lo == s) continue;
-                    u32 a = dc_find(d, (u32)s), b = dc_find(d, (u32)lo);
-                    while (a != b) {
-                        if (a > b) { const u32 t = a; a = b; b = t; }
-                        u32 exp = b;
-                        if (__hip_atomic_compare_exchange_strong(&d.parent[b], &exp, a, __ATOMIC_RELAXED,
-                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                            break;
-                        b = dc_find(d, exp);
-                        a = dc_find(d, a);
-                    }
-                }
+        int nb[27], x0, z0;
+        dc_search(d, s, nseg, P, W, H, L, nb, x0, z0);
+        int m = s;
+#pragma unroll
+        for (int k = 0; k < 27; ++k)
+            if (nb[k] >= 0 && nb[k] < m) m = nb[k];
+        d.parent[s] = (u32)m;
+        u32* e = d.edges + (size_t)s * 26;
+        u32 ne = 0;
+#pragma unroll
+        for (int k = 0; k < 27; ++k)
+            if (dc_take(d, s, nb[k], m, x0, z0, P, W, H, L)) e[ne++] = (u32)nb[k];
+        d.ecount[s] = ne;
+    }
+}
+
+// every search edge s -> nb unioned (lock-free, the smaller root wins, so the components do not depend
+// on the order of the unions). An edge whose reverse nb -> s is also a search edge is taken from its
+// smaller end only; the edge to the smallest position is the initial link already.
+__device__ __forceinline__ bool dc_take(const DcvcDev& d, int s, int v, int m, int x0, int z0, int P, int W, int H,
+                                        long long L) {
+    if (v < 0 || v == s || v == m) return false;
+    if (v < s && z0 <= H) {                                   // taken from v's side if v finds s
+        const int x1 = (int)(((long long)d.ukey[v] % L) / (P + 1));
+        int xl = x1 - 1, xr = x1 + 1;
+        if (xl < 0) xl = W - 1;
+        if (xl > 300) xl = 300;
+        if (xr > 300) xr = 300;
+        if (x0 == x1 || x0 == xl || x0 == xr) return false;
+    }
+    return true;
+}
+
+__global__ void __launch_bounds__(256) k_dc_union(DcvcDev d) {
+    const int nseg = d.seg_aux[0];
+    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
+        const u32* e = d.edges + (size_t)s * 26;
+        const u32 ne = d.ecount[s];
+        u32 a = (u32)s;                                       // this voxel's root, refreshed per edge
+        for (u32 j = 0; j < ne; ++j) {
+            a = dc_find(d, a);
+            u32 b = dc_find(d, e[j]);
+            while (a != b) {
+                if (a > b) { const u32 t = a; a = b; b = t; }
+                u32 exp = b;
+                if (__hip_atomic_compare_exchange_strong(&d.parent[b], &exp, a, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    break;
+                b = dc_find(d, exp);
+                a = dc_find(d, a);
             }
         }
     }
 }
 
-// full compression, then each component's point count and first point at its root
-__global__ void __launch_bounds__(256) k_dc_compress(DcvcDev d) {
-    const int nseg = d.seg_aux[0];
-    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
-        u32 v = (u32)s;
-        while (d.parent[v] != v) v = d.parent[v];
-        d.parent[s] = v;
-    }
-}
-__global__ void __launch_bounds__(256) k_dc_sizes(DcvcDev d) {
-    const int nseg = d.seg_aux[0];
-    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += gridDim.x * blockDim.x) {
-        const u32 r = d.parent[s];
-        atomicAdd(&d.csize[r], d.ucount[s]);
-        atomicMin(&d.cfirst[r], d.vals[d.segstart[s]]);     // points of a voxel in index order
+// component point counts and first points at the roots: one atomic pair per distinct root of a wave
+// (voxel s of this lane, r its root)
+__device__ __forceinline__ void dc_sizes_wave(const DcvcDev& d, int s, int nseg, u32 r) {
+    const int l = lane_id();
+    bool todo = s < nseg;
+    const u32 c = todo ? d.ucount[s] : 0u;
+    const u32 f = todo ? d.vals[d.segstart[s]] : 0xFFFFFFFFu;   // points of a voxel in index order
+    for (;;) {
+        const u64 m = __ballot(todo);
+        if (!m) break;
+        const int lead = __ffsll((long long)m) - 1;
+        const u32 r0 = __shfl(r, lead, 64);
+        const bool mine = todo && r == r0;
+        u32 cs = mine ? c : 0u, fm = mine ? f : 0xFFFFFFFFu;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            cs += __shfl_xor(cs, o, 64);
+            fm = min(fm, (u32)__shfl_xor(fm, o, 64));
+        }
+        if (l == lead) {
+            atomicAdd(&d.csize[r0], cs);
+            atomicMin(&d.cfirst[r0], fm);
+        }
+        todo = todo && !mine;
     }
 }
 
-// labelAnalysis (:325-355), one workgroup: the components larger than minSeg ranked by size (ties by
-// first point); crank[root] = rank + 1
-__global__ void __launch_bounds__(1024) k_dc_rank(DcvcDev d) {
-    __shared__ u64 key[kDcMaxClusters];
-    __shared__ int cnt;
-    __shared__ u32 kept;
+// full compression (every voxel's parent its root), each component's point count and first point at
+// its root, and the voxel table emptied for the next call
+__global__ void __launch_bounds__(256) k_dc_compress(DcvcDev d) {
     const int nseg = d.seg_aux[0];
+    for (int s0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63); s0 < nseg; s0 += gridDim.x * blockDim.x) {
+        const int s = s0 + lane_id();                          // uniform trip count per wave
+        u32 v = (u32)s;
+        if (s < nseg) {
+            while (d.parent[v] != v) v = d.parent[v];
+            d.parent[s] = v;
+            const u32 key = d.ukey[s];
+            if ((long long)key < d.vtab_cells) d.vtab[key] = -1;
+        }
+        dc_sizes_wave(d, s, nseg, v);
+    }
+}
+
+// labelAnalysis (:325-355), one workgroup of 1024: the components larger than minSeg ranked by size
+// (ties by first point); crank[root] = rank + 1. key: kDcMaxClusters LDS words; root(v): v's root;
+// the sizes are read back with agent-scope loads (they were formed by atomics)
+template <class RootF>
+__device__ __forceinline__ void dc_rank(const DcvcDev& d, int nseg, u64* key, int& cnt, u32& kept, RootF root) {
     if (threadIdx.x == 0) { cnt = 0; kept = 0; }
     __syncthreads();
     for (int s = threadIdx.x; s < nseg; s += blockDim.x) {
-        if (d.parent[s] != (u32)s || (int)d.csize[s] <= d.prm.min_seg) continue;
+        if (root(s) != (u32)s) continue;
+        const u32 cs = __hip_atomic_load(&d.csize[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int)cs <= d.prm.min_seg) continue;
+        const u32 cf = __hip_atomic_load(&d.cfirst[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int k = atomicAdd(&cnt, 1);
-        if (k < kDcMaxClusters) key[k] = ((u64)(~d.csize[s]) << 32) | (u64)d.cfirst[s];
+        if (k < kDcMaxClusters) key[k] = ((u64)(~cs) << 32) | (u64)cf;
         else d.dim[D_ERR] = 2;
-        atomicAdd(&kept, d.csize[s]);
+        atomicAdd(&kept, cs);
     }
     __syncthreads();
     const int m = cnt < kDcMaxClusters ? cnt : kDcMaxClusters;
@@ -254,12 +350,20 @@ __global__ void __launch_bounds__(1024) k_dc_rank(DcvcDev d) {
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
         const u32 f = (u32)(key[i] & 0xffffffffull);
         const u32 vk = d.okeys[f];                           // k_dc_pointvox: voxel slot of point f
-        d.crank[d.parent[vk]] = (u32)(i + 1);
+        d.crank[root((int)vk)] = (u32)(i + 1);
     }
     if (threadIdx.x == 0) {
         d.dim[D_NCLUST] = m;
         d.dim[D_NKEPT] = (int)kept;
     }
+}
+
+__global__ void __launch_bounds__(1024) k_dc_rank(DcvcDev d) {
+    __shared__ u64 key[kDcMaxClusters];
+    __shared__ int cnt;
+    __shared__ u32 kept;
+    const int nseg = d.seg_aux[0];
+    dc_rank(d, nseg, key, cnt, kept, [&](int v) { return d.parent[v]; });
 }
 
 // voxel slot of every point (okeys, reused before the final keys are written)
@@ -294,7 +398,8 @@ int dcvc_alloc(DcvcGPU& g, size_t cap) {
         !A(&g.vals, sizeof(u32) * cap) || !A(&g.segstart, sizeof(u32) * (cap + 1)) || !A(&g.seg_aux, sizeof(int) * 8) ||
         !A(&g.parent, sizeof(u32) * cap) || !A(&g.csize, sizeof(u32) * cap) || !A(&g.cfirst, sizeof(u32) * cap) ||
         !A(&g.crank, sizeof(u32) * cap) || !A(&g.okeys, sizeof(u32) * cap) || !A(&g.ovals, sizeof(u32) * cap) ||
-        !A(&g.plab, sizeof(u32) * cap) || !A(&g.ukey, sizeof(u32) * cap) || !A(&g.ucount, sizeof(u32) * cap))
+        !A(&g.plab, sizeof(u32) * cap) || !A(&g.ukey, sizeof(u32) * cap) || !A(&g.ucount, sizeof(u32) * cap) ||
+        !A(&g.edges, sizeof(u32) * 26 * cap) || !A(&g.ecount, sizeof(u32) * cap))
         return PF_ENOMEM;
     const u64 r0[8] = {0ull, ~0ull, 0ull, 0ull, ~0ull, 0ull, 0ull, 0ull};
     if (hipMemcpy(g.red, r0, sizeof(r0), hipMemcpyHostToDevice) != hipSuccess) return PF_EHIP;
@@ -304,7 +409,7 @@ int dcvc_alloc(DcvcGPU& g, size_t cap) {
 
 void dcvc_free(DcvcGPU& g) {
     void* ps[] = {g.red, g.bounds, g.dim, g.pol, g.keys, g.vals, g.segstart, g.seg_aux, g.parent, g.csize,
-                  g.cfirst, g.crank, g.okeys, g.ovals, g.plab, g.ukey, g.ucount};
+                  g.cfirst, g.crank, g.okeys, g.ovals, g.plab, g.ukey, g.ucount, g.vtab, g.edges, g.ecount};
     for (void* p : ps) (void)hipFree(p);
     prim_free(g.w);
     g = DcvcGPU{};
@@ -315,24 +420,45 @@ int dcvc_reset(DcvcGPU& g, hipStream_t s) {
     return PF_OK;
 }
 
-// key bits of the voxel index: (polarNum + 1) (width + 1) (height + 2) with polarNum bounded by the
-// rings up to max(5 m, max_range) and the pitch span by 180 degrees
-static int dcvc_key_bits(const pf_dcvc_params& p) {
+// cells of the voxel index space: (polarNum + 1) (width + 1) (height + 3), polarNum bounded by the
+// rings up to max(5 m, max_range) and the pitch layers (height + 1 of them, plus the top layer quirk)
+// by 180 degrees
+static long long dcvc_key_cells(const pf_dcvc_params& p) {
     double range = 0.0;
     long long P = 0;
     const double top = p.max_range > 5.0 ? p.max_range : 5.0;
     for (int step = 1; range <= top && P < kDcMaxBounds; ++step, ++P) range += (p.start_r - step * p.delta_r);
     const long long W = (long long)(std::round(360.0 / p.delta_a) + 1);
     const long long H = (long long)(180.0 / p.delta_p) + 2;
-    const long long m = (P + 1) * (W + 1) * (H + 1);
+    return (P + 1) * (W + 1) * (H + 1);
+}
+static int dcvc_key_bits(const pf_dcvc_params& p) {
+    const long long m = dcvc_key_cells(p);
     int b = 1;
     while (b < 32 && (1ll << b) < m) ++b;
     return b;
 }
 
+constexpr long long kDcTableMaxCells = 1ll << 26;          // 256 MB of table at most
+
+int dcvc_set_params(DcvcGPU& g, const pf_dcvc_params& p) {
+    g.prm = p;
+    const long long m = dcvc_key_cells(p);
+    if (m <= g.vtab_cells) return PF_OK;
+    (void)hipFree(g.vtab);
+    g.vtab = nullptr;
+    g.vtab_cells = 0;
+    if (m > kDcTableMaxCells) return PF_OK;                 // binary-search lookups
+    if (hipMalloc(&g.vtab, sizeof(int) * (size_t)m) != hipSuccess) return PF_ENOMEM;
+    if (hipMemset(g.vtab, 0xFF, sizeof(int) * (size_t)m) != hipSuccess) return PF_EHIP;
+    if (hipDeviceSynchronize() != hipSuccess) return PF_EHIP;
+    g.vtab_cells = m;
+    return PF_OK;
+}
+
 void dcvc_enqueue(DcvcGPU& g, const float4* pts, const int* d_n, hipStream_t s, u32** out_idx) {
     DcvcDev d{g.prm, g.red, g.bounds, g.dim, g.pol, g.keys, g.vals, g.segstart, g.seg_aux, g.parent,
-              g.csize, g.cfirst, g.crank, g.okeys, g.ovals, g.plab, g.ukey, g.ucount};
+              g.csize, g.cfirst, g.crank, g.okeys, g.ovals, g.plab, g.ukey, g.ucount, g.vtab, g.vtab_cells, g.edges, g.ecount};
     hipLaunchKernelGGL(k_dc_polar, dim3(kDcGrid), dim3(256), 0, s, pts, d_n, d);
     hipLaunchKernelGGL(k_dc_keys, dim3(kDcGrid), dim3(256), 0, s, d_n, d);
     u32 *ks = nullptr, *vs = nullptr;                       // sorted (voxel, point) pairs
@@ -341,10 +467,10 @@ void dcvc_enqueue(DcvcGPU& g, const float4* pts, const int* d_n, hipStream_t s, 
     d.vals = vs;
     segment_starts(ks, d_n, g.segstart, g.seg_aux, g.seg_aux + 1, g.seg_aux + 4, g.w, s);
     hipLaunchKernelGGL(k_dc_voxels, dim3(kDcGrid), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_dc_pointvox, dim3(kDcGrid), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_dc_link, dim3(kDcGrid), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_dc_union, dim3(kDcGrid), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_dc_compress, dim3(kDcGrid), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_dc_sizes, dim3(kDcGrid), dim3(256), 0, s, d);
-    hipLaunchKernelGGL(k_dc_pointvox, dim3(kDcGrid), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_dc_rank, dim3(1), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(k_dc_label, dim3(kDcGrid), dim3(256), 0, s, d, d_n);
     radix_sort_pairs(g.okeys, g.ovals, d_n, 16, g.w, s);
@@ -400,7 +526,7 @@ int pf_dcvc_create(const pf_dcvc_params* p, int device, size_t max_points, pf_dc
     int rc = PF_OK;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) rc = PF_EHIP;
     if (rc == PF_OK) rc = dcvc_alloc(h->g, max_points);
-    h->g.prm = *p;
+    if (rc == PF_OK) rc = dcvc_set_params(h->g, *p);
     if (rc == PF_OK && hipMalloc(&h->d_pts, sizeof(float4) * max_points) != hipSuccess) rc = PF_ENOMEM;
     if (rc == PF_OK && hipMalloc(&h->d_n, sizeof(int)) != hipSuccess) rc = PF_ENOMEM;
     if (rc != PF_OK) {

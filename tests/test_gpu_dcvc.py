@@ -55,6 +55,22 @@ def test_dcvc_matches_components_oracle_and_serial_statistics(pa, pfref, pfsynth
     assert len(idx) > 0.8 * len(U)
 
 
+@pytest.mark.parametrize("kw", [dict(delta_a=1.0, delta_p=0.8), dict(delta_a=0.1, delta_p=0.2, min_seg=20),
+                                dict(start_r=0.5, delta_r=0.001)])
+def test_dcvc_other_grids(pa, pfref, pfsynth, kw):
+    """Grids other than config.yaml's: width 361 (azimuth 301..360 search the clamped column 300, a
+    one-way neighbourhood the unions must take from its only side), an index space too large for the
+    device's voxel table (binary-search lookups), finer rings. Bit-exact against the components mode."""
+    U = _nonground(pfref, pfsynth.Sequence("S64", n_frames=8).frame(7))
+    dc = pa.Dcvc(max_points=200000, **kw)
+    dc.run(U[:50])
+    idx, lab = dc.run(U)
+    oidx, olab = pfref.dcvc(U, pfref.dcvc_params(**kw), components=True)
+    np.testing.assert_array_equal(idx, oidx)
+    np.testing.assert_array_equal(lab, olab)
+    assert len(idx) > 0
+
+
 def test_dcvc_first_frame_and_reset(pa, pfref, pfsynth):
     """The first call of a handle (and the first after reset) starts the range rings at the member
     default 5 m (include/additionClass.hpp:105-106), later calls at 0 m (resetParams :445-449)."""

@@ -1,0 +1,76 @@
+"""Per-dispatch PMC means of the frame-path kernels from tools/frame_pmc.sh's rocprofv3 passes.
+
+  python3 tools/frame_pmc.py gpurun_out/framepmc [--out profiles/r02_frame_pmc.json]
+
+Derived figures (MI355X_MICROARCH.md §rocprofv3 PMC slots): SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_*
+count quad-cycles, so their ratios are fractions of a wave's lifetime; HBM read bytes = FETCH_SIZE
+(KiB) x 1024 x 2 (the gfx950 FETCH_SIZE correction bench.py also applies), write = WRITE_SIZE x 1024.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+from collections import defaultdict
+
+KERNELS = ["k_lm_solve", "k_os_pass", "k_fe_sector", "k_assoc", "k_observe", "k_vg_reduce", "k_segments",
+           "k_scan1", "k_rg_keys"]
+
+
+def short(name):
+    for k in KERNELS:                  # names read "void pf::(anonymous namespace)::k_x<2>(pf::Args)"
+        if re.search(r"\b%s\b" % k, name):
+            return k
+    return ""
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(a.root + "/**/*counter_collection.csv", recursive=True):
+        for row in csv.DictReader(open(f)):
+            k = short(row.get("Kernel_Name", ""))
+            if k in KERNELS:
+                # one row per (dispatch, counter): sum over the per-XCD / per-SE dimension rows of a dispatch
+                acc[k][(row["Counter_Name"], row.get("Dispatch_Id", ""))].append(float(row["Counter_Value"]))
+    out = {"source": "rocprofv3 --pmc passes (tools/frame_pmc.sh) over bench.py --steps 100 --no-graph (configs[1], S64)",
+           "kernels": {}}
+    for k in KERNELS:
+        if k not in acc:
+            continue
+        per = defaultdict(list)
+        for (ctr, _), vals in acc[k].items():
+            per[ctr].append(sum(vals))
+        m = {c: sum(v) / len(v) for c, v in per.items()}
+        d = {"dispatches": max(len(v) for v in per.values()), "mean_per_dispatch": m}
+        wc = m.get("SQ_WAVE_CYCLES")
+        if wc:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
+                if c in m:
+                    d["frac_of_wave_cycles_" + c[3:].lower()] = m[c] / wc
+        if m.get("SQ_WAVES"):
+            for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
+                if c in m:
+                    d[c[3:].lower() + "_per_wave"] = m[c] / m["SQ_WAVES"]
+        if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
+            d["lds_bank_conflict_frac"] = m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"]
+        if "FETCH_SIZE" in m:
+            d["hbm_read_bytes"] = m["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in m:
+            d["hbm_write_bytes"] = m["WRITE_SIZE"] * 1024
+        out["kernels"][k] = d
+    s = json.dumps(out, indent=1)
+    print(s)
+    if a.out:
+        os.makedirs(os.path.dirname(a.out), exist_ok=True)
+        open(a.out, "w").write(s + "\n")
+    else:
+        open(os.path.join(a.root, "frame_pmc.json"), "w").write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -57,7 +57,7 @@ def frame_breakdown(trace_csv, stats_csv):
                                             "launches_per_frame": statistics.median(launches), "busy_us": busy}
 
 
-def pmc(path, counter, kernel="k_knn_query"):
+def pmc(path, counter, kernel="k_knn_thick"):
     vals, durs = [], []
     for r in csv.DictReader(open(path)):
         if short(r["Kernel_Name"]) == kernel and r["Counter_Name"] == counter:
@@ -105,6 +105,30 @@ def main():
         with open(os.path.join(a.out, "%s_front_end.md" % a.round), "w") as f:
             f.write("\n".join(lines) + "\n")
         print("front end us/frame %.1f" % tot)
+    dc = os.path.join(g, "dcvc_prof", "run_kernel_stats.csv")
+    if os.path.exists(dc):
+        shutil.copy(dc, os.path.join(a.out, "%s_dcvc_kernel_stats.csv" % a.round))
+        rows = sorted(csv.DictReader(open(dc)), key=lambda r: -float(r["TotalDurationNs"]))
+        calls = max(int(r["Calls"]) for r in rows if short(r["Name"]) == "k_dc_rank")
+        lines = ["# BPF front end with curvedfilter (DCVC) per frame (%s)\n" % a.round,
+                 "Source: `rocprofv3 --kernel-trace --stats -- python3 tools/cls_probe.py --iters 50 --dcvc` "
+                 "(ground_seg + DCVC + featureExtract of S64 frames; %d frames)\n" % calls,
+                 "| kernel | launches / frame | avg us | us / frame |", "|---|---|---|---|"]
+        tot = dtot = 0.0
+        for r in rows:
+            n = short(r["Name"])
+            if n.startswith("__amd"):
+                continue
+            per = float(r["TotalDurationNs"]) / 1e3 / calls
+            tot += per
+            if n.startswith("k_dc_"):
+                dtot += per
+            lines.append("| %s | %.1f | %.1f | %.1f |" % (n, int(r["Calls"]) / calls, float(r["AverageNs"]) / 1e3, per))
+        lines.append("| **total** | | | **%.1f** |" % tot)
+        lines.append("| of which `k_dc_*` | | | %.1f |" % dtot)
+        with open(os.path.join(a.out, "%s_dcvc.md" % a.round), "w") as f:
+            f.write("\n".join(lines) + "\n")
+        print("front end with DCVC us/frame %.1f (k_dc_* %.1f)" % (tot, dtot))
     mp = os.path.join(g, "map_prof", "run_kernel_stats.csv")
     if os.path.exists(mp):
         shutil.copy(mp, os.path.join(a.out, "%s_map_kernel_stats.csv" % a.round))
@@ -115,7 +139,7 @@ def main():
         wv, wd = pmc(write, "WRITE_SIZE")
         fkb, wkb = statistics.median(fv), statistics.median(wv)
         out = {
-            "kernel": "k_knn_query",
+            "kernel": "k_knn_thick",
             "workload": "config 5: 2M-point dense map, 200k queries (tools/knn_probe.py)",
             "fetch_size_kb_raw": fkb, "write_size_kb_raw": wkb,
             "hbm_read_bytes_per_launch": fkb * 1024 * 2,      # gfx950: FETCH_SIZE reads half (MICROARCH §HBM)
