@@ -25,7 +25,8 @@ enum CounterSlot {
     C_M,                        // [kMaxC] map sizes
     C_NPAIR = C_M + kMaxC,
     C_NRG, C_NSEG,
-    C_NLT,                      // [3] segments of classes < 1, < 2, < 3 (segment_starts)
+    C_NLT,                      // [3] per class bound b = 1, 2, 3: VoxelGrid segments of classes < b (stage A),
+                                //     kept map voxels of classes < b (stage B, k_rg_tail)
     C_NRG_VALID = C_NLT + 3,
     C_KEEP_TOTAL,
     C_KEPT,                     // [kMaxC] residual blocks kept (last outer iteration)
@@ -153,7 +154,9 @@ struct OdomGPU {
     float4* map[kMaxC] = {};       // local maps
     float4* app[kMaxC] = {};       // this frame's transformed down-sampled points (appended)
     float4* seg_out = nullptr;
-    u32 *keys = nullptr, *vals = nullptr, *flags = nullptr, *scan_out = nullptr, *segstart = nullptr;
+    u32 *keys = nullptr, *vals = nullptr;
+    u64* tail_status = nullptr;   // k_rg_tail look-back words [tail_tiles] + arrival counter
+    size_t tail_tiles = 0;
 
     int* nbr = nullptr;            // [5 * kMaxC * in_cap]
     int* qflag = nullptr;          // bit0 valid association, bit1 kept

@@ -1359,69 +1359,151 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
     sort_hist_end(lh, sh, n, n);
 }
 
-struct RgReduceArgs {
-    const int* cnt;
-    int nc;
+struct RgTailArgs {
+    int* cnt;
     Clouds map, app;
-    const u32* keys;
+    const u32* keys;       // sorted (bits 30-31 class, 0xFFFFFFFF cropped), cnt[C_NRG] of them
     const u32* vals;
-    const u32* segstart;
-    float4* seg_out;
-    u32* keep;
+    float4* seg_out;       // the kept voxels, compacted in key order
     int k_new;
     float theta_p;
     int theta_max;
+    u64* status;           // look-back words (zero between calls)
+    u32* arrive;
+    int* err;
 };
 
+// The rest of addPointsToMap in one pass over the sorted keys (one tile of 256 x kTailPer keys per
+// workgroup turn, kTailPer consecutive keys per thread, their points loaded at once): every voxel (segment of equal keys) is reduced by the thread holding
+// its first key, walking its points in key order (the Vector4f centroid and r / g maxima of :108-125,
+// extractstablepoint :12-14, the ageing :634-646); the kept voxels are counted per tile and a
+// decoupled look-back over the tile counts gives each kept voxel its place in seg_out, so segment
+// starts, their reduction, the keep-flag scan and the compaction need no separate launches.
+// cnt[C_NLT + b - 1] = kept voxels of classes < b, cnt[C_KEEP_TOTAL] = all kept voxels.
+#ifndef PF_RG_TAIL_PER
+#define PF_RG_TAIL_PER 2
+#endif
+constexpr int kTailPer = PF_RG_TAIL_PER;                        // keys per thread
+constexpr int kTailTile = 256 * kTailPer;
 template <int NC>
-__global__ void __launch_bounds__(256) k_rg_reduce(RgReduceArgs a) {
+__global__ void __launch_bounds__(256) k_rg_tail(RgTailArgs a) {
+    constexpr u32 kSent = 0xFFFFFFFFu;
+    constexpr int kPer = kTailPer;
+    __shared__ u32 lw[4];
+    __shared__ u32 s_excl;
     const RgView<NC> V = rg_view<NC>(a.cnt, a.map, a.app);
-    const int nseg = a.cnt[C_NSEG], nvalid = a.cnt[C_NRG_VALID];
-    for (int sg = blockIdx.x * blockDim.x + threadIdx.x; sg < nseg; sg += gridDim.x * blockDim.x) {
-        const u32 b0 = a.segstart[sg], b1 = (sg + 1 < nseg) ? a.segstart[sg + 1] : (u32)nvalid;
-        float cx = 0.f, cy = 0.f, cz = 0.f;                            // Vector4f centroid (:108-125)
-        int r_max = -1;
-        float g_max = -1;
-        for (u32 k = b0; k < b1; ++k) {
-            int c;
-            const float4 p = V.at((int)a.vals[k], c);
-            cx += p.x; cy += p.y; cz += p.z;
-            const int r = (int)w_r(p);
-            const float g = (float)w_g(p);
-            if (r > r_max) r_max = r;
-            if (g > g_max) g_max = g;
+    int* kb = a.cnt + C_NLT;
+    const int n = a.cnt[C_NRG];
+    const int ntiles = (n + kTailTile - 1) / kTailTile;
+    const int t = threadIdx.x;
+    const int G = ntiles < (int)gridDim.x ? ntiles : (int)gridDim.x;
+    if (n == 0) {
+        if (blockIdx.x == 0 && t == 0) {
+            a.cnt[C_KEEP_TOTAL] = 0;
+            kb[0] = kb[1] = kb[2] = 0;
         }
-        const float nn = (float)(b1 - b0);
-        const u32 r = (u32)r_max & 255u, g = (u32)g_max & 255u;         // stored into uint8 r, g
-        // extractstablepoint (:12-14) on the voxel's uint8 r, g
-        const bool drop = ((float)g < (float)r * a.theta_p) && ((int)r > a.k_new) && ((int)g < a.theta_max + 1);
-        const u32 aged = r > 250 ? 255u : r + 2u;                       // :634-646
-        a.seg_out[sg] = make_float4(cx / nn, cy / nn, cz / nn, __uint_as_float(pack_rg(aged, g)));
-        a.keep[sg] = drop ? 0u : 1u;
+        return;
     }
+    if ((int)blockIdx.x >= G) return;
+    if (blockIdx.x == 0 && t == 0) {                            // classes below the first key's: none
+        const u32 k0 = a.keys[0];
+        for (u32 b = 1; b <= 3; ++b)
+            if ((k0 >> 30) >= b) kb[b - 1] = 0;
+    }
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int base = tile * kTailTile + t * kPer;
+        u32 k[kPer + 1];                                        // k[0] = predecessor of the first
+        k[0] = base > 0 && base - 1 < n ? a.keys[base - 1] : kSent;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) k[j + 1] = base + j < n ? a.keys[base + j] : kSent;
+        float4 pt[kPer];                                        // this thread's points, loaded at once
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            int c;
+            pt[j] = base + j < n && k[j + 1] != kSent ? V.at((int)a.vals[base + j], c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float4 out[kPer];
+        u32 keepm = 0u;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int i = base + j;
+            out[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!(i < n && k[j + 1] != kSent && (i == 0 || k[j] != k[j + 1]))) continue;   // not a voxel's first key
+            float cx = 0.f, cy = 0.f, cz = 0.f;                 // Vector4f centroid (:108-125)
+            int r_max = -1;
+            float g_max = -1;
+            int e = i;
+            for (;;) {
+                float4 p;
+                if (e - base < kPer) {
+#pragma unroll
+                    for (int jj = 0; jj < kPer; ++jj)           // static register index
+                        if (jj == e - base) p = pt[jj];
+                } else {                                        // the voxel runs past this thread's keys
+                    int c;
+                    p = V.at((int)a.vals[e], c);
+                }
+                cx += p.x; cy += p.y; cz += p.z;
+                const int r = (int)w_r(p);
+                const float g = (float)w_g(p);
+                if (r > r_max) r_max = r;
+                if (g > g_max) g_max = g;
+                if (++e >= n) break;
+                const u32 ke = e - base < kPer ? k[e - base + 1] : a.keys[e];
+                if (ke != k[j + 1]) break;
+            }
+            const float nn = (float)(e - i);
+            const u32 r = (u32)r_max & 255u, g = (u32)g_max & 255u;     // stored into uint8 r, g
+            // extractstablepoint (:12-14) on the voxel's uint8 r, g
+            const bool drop = ((float)g < (float)r * a.theta_p) && ((int)r > a.k_new) && ((int)g < a.theta_max + 1);
+            const u32 aged = r > 250 ? 255u : r + 2u;                   // :634-646
+            out[j] = make_float4(cx / nn, cy / nn, cz / nn, __uint_as_float(pack_rg(aged, g)));
+            if (!drop) keepm |= 1u << j;
+        }
+        u32 agg;
+        const u32 tex = block_excl_scan256((u32)__popc(keepm), lw, agg);
+        if (t < 64) {
+            const u32 excl = tile_lookback(a.status, tile, agg, a.err);
+            if (t == 0) {
+                s_excl = excl;
+                if (tile == ntiles - 1) {
+                    a.cnt[C_KEEP_TOTAL] = (int)(excl + agg);
+                    for (u32 b = 1; b <= 3; ++b)                // classes above the last key's: all
+                        if ((a.keys[n - 1] >> 30) < b) kb[b - 1] = (int)(excl + agg);
+                }
+            }
+        }
+        __syncthreads();
+        u32 pos = s_excl + tex;                                 // kept voxels before key base + j
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int i = base + j;
+            if (i >= n) break;
+            const u32 kp = k[j], kc = k[j + 1];
+            if (i > 0 && (kp >> 30) < (kc >> 30))              // class boundary: kept voxels before it
+                for (u32 b = (kp >> 30) + 1; b <= (kc >> 30); ++b) kb[b - 1] = (int)pos;
+            if ((keepm >> j) & 1u) a.seg_out[pos++] = out[j];
+        }
+        __syncthreads();
+    }
+    lookback_finish(a.status, ntiles, a.arrive, G);
 }
 
-// compaction: class c's kept voxels are the kept segments in [nlt(c), nlt(c + 1)), in order
+// the kept voxels into the class maps (class c's are seg_out[kb(c) .. kb(c + 1)), in order)
 template <int NC>
 __global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const float4* __restrict__ seg_out,
-                                                   const u32* __restrict__ keep, const u32* __restrict__ pos,
                                                    CloudsW map) {
     constexpr int nc = NC;
-    const int nseg = cnt[C_NSEG], total = cnt[C_KEEP_TOTAL];
-    int sb[kMaxC + 1], kb[kMaxC + 1];             // segment / kept-voxel start of every class
-    sb[0] = 0;
+    const int total = cnt[C_KEEP_TOTAL];
+    int kb[kMaxC + 1];                             // kept-voxel start of every class
     kb[0] = 0;
 #pragma unroll
-    for (int c = 1; c <= kMaxC; ++c) {
-        sb[c] = c < nc ? cnt[C_NLT + c - 1] : nseg;
-        kb[c] = sb[c] < nseg ? (int)pos[sb[c]] : total;
-    }
+    for (int c = 1; c <= kMaxC; ++c) kb[c] = c < nc ? cnt[C_NLT + c - 1] : total;
     if (blockIdx.x == 0 && threadIdx.x == 0)      // no block of this kernel reads them
         for (int c = 0; c < nc; ++c) cnt[C_M + c] = kb[c + 1] - kb[c];
-    for (int sg = blockIdx.x * blockDim.x + threadIdx.x; sg < nseg; sg += gridDim.x * blockDim.x) {
-        if (!keep[sg]) continue;
-        const int c = NC == 2 ? (sg < sb[1] ? 0 : 1) : (sg < sb[1] ? 0 : (sg < sb[2] ? 1 : 2));
-        map.at(c)[(int)pos[sg] - sel3(c, kb[0], kb[1], kb[2])] = seg_out[sg];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int c = NC == 2 ? (i < kb[1] ? 0 : 1) : (i < kb[1] ? 0 : (i < kb[2] ? 1 : 2));
+        map.at(c)[i - sel3(c, kb[0], kb[1], kb[2])] = seg_out[i];
     }
 }
 
@@ -1562,11 +1644,10 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
         PF_ALLOC(o.app[c], sizeof(float4) * in_cap);
     }
     PF_ALLOC(o.seg_out, sizeof(float4) * o.sort_cap);
+    o.tail_tiles = (o.sort_cap + kTailTile - 1) / kTailTile;
+    PF_ALLOC(o.tail_status, sizeof(u64) * (o.tail_tiles + 1));    // look-back words + the arrival counter
     PF_ALLOC(o.keys, sizeof(u32) * (o.sort_cap + 1));
     PF_ALLOC(o.vals, sizeof(u32) * (o.sort_cap + 1));
-    PF_ALLOC(o.flags, sizeof(u32) * (o.sort_cap + 1));
-    PF_ALLOC(o.scan_out, sizeof(u32) * (o.sort_cap + 1));
-    PF_ALLOC(o.segstart, sizeof(u32) * (o.sort_cap + 1));
     PF_ALLOC(o.nbr, sizeof(int) * 5 * nq);
     PF_ALLOC(o.qflag, sizeof(int) * nq);
     PF_ALLOC(o.lm_part, sizeof(double) * kLmEvals * kLmBlocks * 32);
@@ -1606,6 +1687,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (hipMemsetAsync(o.lm, 0, sizeof(LMState), o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.lm_ticket, 0, sizeof(u32) * 2 * kLmEvalSlots, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.tail_status, 0, sizeof(u64) * (o.tail_tiles + 1), o.stream) != hipSuccess) return PF_EHIP;
     // the sub-objects' overflow / wait flags latch into the handle's sticky error words
     alias_err(o.fe.err, o.errw + E_FE_SECTOR);
     alias_err(o.grid.err, o.errw + E_GRID);
@@ -1634,6 +1716,7 @@ int odom_reset(OdomGPU& o) {
     if (hipMemsetAsync(o.lm, 0, sizeof(LMState), o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.lm_ticket, 0, sizeof(u32) * 2 * kLmEvalSlots, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.tail_status, 0, sizeof(u64) * (o.tail_tiles + 1), o.stream) != hipSuccess) return PF_EHIP;
     for (int p = 0; p < kSlots; ++p)
         if (hipMemsetAsync(o.sb[p].cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)o.cls.nc * o.map_cap);
@@ -1680,7 +1763,7 @@ void odom_destroy(OdomGPU& o) {
         (void)hipFree(o.app[c]);
     }
     void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.seg_out,
-                    o.keys, o.vals, o.flags, o.scan_out, o.segstart, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
+                    o.keys, o.vals, o.tail_status, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
                     o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg, o.errw};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
@@ -1776,12 +1859,11 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     PF_LAUNCH_NC(nc, k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map), clouds(o.app), leaf,
                  o.keys, o.vals, sort_hist(o.prim, 32, true));
     radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
-    segment_starts(o.keys, cnt + C_NRG, o.segstart, cnt + C_NSEG, cnt + C_NLT, cnt + C_NRG_VALID, o.prim, s);
-    RgReduceArgs ra{cnt, nc, clouds(o.map), clouds(o.app), o.keys, o.vals, o.segstart, o.seg_out, o.flags,
-                    o.prm.k_new, o.prm.theta_p, o.prm.theta_max};
-    PF_LAUNCH_NC(nc, k_rg_reduce, dim3(kGrid), dim3(256), 0, s, ra);
-    scan_exclusive(o.flags, o.scan_out, cnt + C_NSEG, (u32*)(cnt + C_KEEP_TOTAL), o.prim, s);
-    PF_LAUNCH_NC(nc, k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, o.flags, o.scan_out, clouds_w(o.map));
+    RgTailArgs ta{cnt, clouds(o.map), clouds(o.app), o.keys, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,
+                  o.prm.theta_max, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err};
+    const unsigned tail_grid = (unsigned)(o.tail_tiles < (size_t)kSortMaxBlocks ? o.tail_tiles : kSortMaxBlocks);
+    PF_LAUNCH_NC(nc, k_rg_tail, dim3(tail_grid > 0 ? tail_grid : 1), dim3(256), 0, s, ta);
+    PF_LAUNCH_NC(nc, k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, clouds_w(o.map));
 }
 
 }  // namespace pf

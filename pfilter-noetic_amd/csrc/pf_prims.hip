@@ -161,61 +161,7 @@ __global__ void __launch_bounds__(256) k_os_pass(const u32* __restrict__ kin, co
     }
 }
 
-// ---- single-pass scans: decoupled look-back ----
-// Blocks own 2048-item tiles b, b + G, ... (co-resident grid). A tile publishes its aggregate, wave 0
-// looks back over up to 64 predecessors at once (agent-scope atomic words carrying tag << 32 |
-// value), then publishes its inclusive prefix. The last block to finish clears the status words for
-// the next call.
 constexpr int kScanPer = 8;
-
-// wave 0 (all 64 lanes): publish `agg` for `tile`, return its exclusive prefix (all lanes)
-__device__ u32 tile_lookback(u64* status, int tile, u32 agg, int* err) {
-    const int l = lane_id();
-    if (l == 0 && tile > 0)
-        __hip_atomic_store(&status[tile], (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    u32 excl = 0;
-    int j = tile - 1;
-    unsigned long long t0 = 0;
-    while (j >= 0) {
-        const int jj = j - l;
-        const u64 sv = jj >= 0 ? __hip_atomic_load(&status[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : (2ull << 32);                // before tile 0: an inclusive zero
-        const u32 tag = (u32)(sv >> 32);
-        const u64 incl = __ballot(tag == 2);
-        const int first = incl ? __ffsll((long long)incl) - 1 : 64;       // nearest inclusive prefix
-        const u64 upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
-        if (__ballot(tag == 0) & upto) {
-            const unsigned long long now = rt_now();
-            if (!t0) t0 = now;
-            else if (now - t0 > kWaitTicks) { if (l == 0) atomicOr(err, 2); break; }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        u32 mine = (l <= first && jj >= 0) ? (u32)sv : 0u;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
-        excl += mine;
-        if (first < 64) break;
-        j -= 64;
-    }
-    if (l == 0)
-        __hip_atomic_store(&status[tile], (2ull << 32) | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return excl;
-}
-
-// the last block of a look-back launch clears the status words and the arrival counter
-__device__ void lookback_finish(u64* status, int ntiles, u32* arrive, int G) {
-    __shared__ int last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (u32)G - 1;
-    __syncthreads();
-    if (!last) return;
-    for (int i = threadIdx.x; i < ntiles; i += blockDim.x)
-        __hip_atomic_store(&status[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0) __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 __global__ void __launch_bounds__(256) k_scan1(const u32* __restrict__ in, u32* __restrict__ out,
                                                 const int* __restrict__ d_n, u32* __restrict__ d_total,
