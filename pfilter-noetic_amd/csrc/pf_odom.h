@@ -14,6 +14,12 @@ namespace pf {
 //   BPF (Odom_BPF_EstimationClass): 0 beam (line, r), 1 pillar (line, r), 2 facade (plane, 2r)
 // Queries, residuals and maps are concatenated in class order, the reference's factor order.
 constexpr int kMaxC = 3;
+// p-index bucket of a map point (the valid queries of an outer iteration that have it as a neighbour):
+// 16 ints = {pair count, the first kBktInline pair ids, head of the overflow list}, read by k_observe
+// in one round of loads (the overflow list only past kBktInline pairs)
+constexpr int kBktQuads = 4;
+constexpr int kBktInline = 4 * kBktQuads - 2;
+constexpr int kBktHead = 4 * kBktQuads - 1;
 
 // device counter slots (int32, one array per handle); per-class slots are kMaxC consecutive ints
 enum CounterSlot {
@@ -165,7 +171,7 @@ struct OdomGPU {
     float* roundv = nullptr;
     float* observe = nullptr;
     int* pnext = nullptr;          // [5 * kMaxC * in_cap] p-index lists: next pair sharing the map point
-    int4* pbkt = nullptr;          // [nc * map_cap] p-index buckets {count, pair, pair, overflow head}
+    int4* pbkt = nullptr;          // [nc * map_cap][kBktQuads] p-index buckets {count, kBktInline pairs, overflow head}
     u32* tailinc = nullptr;        // [5 * kMaxC * in_cap] increments of a map point, on its last pair
     double* lm_part = nullptr;     // [kLmBlocks * 32] per-block LM partials
     u32* lm_ticket = nullptr;      // LM arrival counter

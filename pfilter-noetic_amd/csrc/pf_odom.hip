@@ -435,12 +435,11 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
         const u32 off = (u32)c * a.map_cap;
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
-            int4* b = a.pbkt + off + (u32)id[j];
+            int* b = reinterpret_cast<int*>(a.pbkt + (size_t)kBktQuads * (off + (u32)id[j]));
             const int p = 5 * q + j;
-            const int slot = atomicAdd(&b->x, 1);                  // {count, pair, pair, overflow head}
-            if (slot == 0) b->y = p;
-            else if (slot == 1) b->z = p;
-            else a.pnext[p] = atomicExch(&b->w, p);
+            const int slot = atomicAdd(&b[0], 1);                  // {count, kBktInline pairs, overflow head}
+            if (slot < kBktInline) b[1 + slot] = p;
+            else a.pnext[p] = atomicExch(&b[kBktHead], p);
         }
     }
 }
@@ -548,15 +547,23 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
         int nb[5], cur[5], rank[5], len[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) nb[j] = a.nbr[5 * q + j];
-        int4 bk[5];
+        int4 bk[5][kBktQuads];                               // every bucket read at once
 #pragma unroll
-        for (int j = 0; j < 5; ++j) bk[j] = a.pbkt[(u32)c * a.map_cap + (u32)nb[j]];
+        for (int j = 0; j < 5; ++j)
+#pragma unroll
+            for (int k = 0; k < kBktQuads; ++k) bk[j][k] = a.pbkt[(size_t)kBktQuads * ((u32)c * a.map_cap + (u32)nb[j]) + k];
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
             const int p = 5 * q + j;
-            len[j] = bk[j].x;
-            rank[j] = (bk[j].x > 0 && bk[j].y < p ? 1 : 0) + (bk[j].x > 1 && bk[j].z < p ? 1 : 0);
-            cur[j] = bk[j].x > 2 ? bk[j].w : -1;
+            const int* w = reinterpret_cast<const int*>(bk[j]);
+            len[j] = w[0];
+            rank[j] = 0;
+#pragma unroll
+            for (int k = 0; k < kBktInline; ++k) rank[j] += (w[0] > k && w[1 + k] < p) ? 1 : 0;
+            cur[j] = w[0] > kBktInline ? w[kBktHead] : -1;
+#ifdef PF_DEV_NOCHAIN
+            cur[j] = -1;                                     // development: time without the list walks
+#endif
         }
         for (int step = 0;; ++step) {
             bool more = false;
@@ -663,7 +670,9 @@ __device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, i
         const float4 m = mp[idx];
         const u32 g = min(255u, w_g(m) + inc);
         mp[idx].w = __uint_as_float(pack_rg(w_r(m), g));
-        pbkt[(u32)c * map_cap + (u32)idx] = make_int4(0, -1, -1, -1);   // empty bucket
+        int4* b = pbkt + (size_t)kBktQuads * ((u32)c * map_cap + (u32)idx);   // empty bucket
+        b[0].x = 0;
+        reinterpret_cast<int*>(b)[kBktHead] = -1;
     }
 }
 
@@ -1529,9 +1538,9 @@ __global__ void __launch_bounds__(256) k_map_export(const int* __restrict__ cnt,
     }
 }
 
-__global__ void k_init_buckets(int4* __restrict__ b, size_t n) {
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        b[i] = make_int4(0, -1, -1, -1);
+__global__ void k_init_buckets(int4* __restrict__ b, size_t n) {   // n buckets
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n * kBktQuads; i += (size_t)gridDim.x * blockDim.x)
+        b[i] = (i % kBktQuads) == 0 ? make_int4(0, -1, -1, -1) : make_int4(-1, -1, -1, -1);
 }
 
 __global__ void k_init_counts(int* __restrict__ cnt, DevState* __restrict__ st, int nc) {
@@ -1658,7 +1667,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.roundv, sizeof(float) * nq);
     PF_ALLOC(o.observe, sizeof(float) * nq);
     PF_ALLOC(o.pnext, sizeof(int) * 5 * nq);
-    PF_ALLOC(o.pbkt, sizeof(int4) * nc * map_cap);
+    PF_ALLOC(o.pbkt, sizeof(int4) * kBktQuads * nc * map_cap);
     PF_ALLOC(o.tailinc, sizeof(u32) * 5 * nq);
     PF_ALLOC(o.poses, sizeof(double) * 7 * o.pose_cap);
     PF_ALLOC(o.stage, sizeof(float4) * nq);
