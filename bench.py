@@ -182,6 +182,7 @@ def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier)
     t0 = time.perf_counter()
     for k in range(warmup, len(ptrs)):
         od.frame_device(*ptrs[k])
+    t_enq = time.perf_counter()    # the host's enqueue time (frames are submitted asynchronously)
     od.sync()                      # raises on a sticky device error: a failed frame is never counted
     barrier()
     t1 = time.perf_counter()
@@ -190,7 +191,7 @@ def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier)
     if stats["errors"]:
         raise RuntimeError("device error words 0x%x during the timed region" % stats["errors"])
     nframes = len(ptrs) - warmup
-    return dict(elapsed=t1 - t0, frames=nframes, poses=poses, stats=stats, data=data_desc,
+    return dict(elapsed=t1 - t0, frames=nframes, poses=poses, stats=stats, data=data_desc, enqueue=t_enq - t0,
                 mean_points=float(np.mean(npts)) if npts else 0.0, od=od, bufs=bufs, ptrs=ptrs)
 
 
@@ -742,7 +743,10 @@ def main(argv=None):
                    "parallelism": "one independent sequence per GPU" if world > 1 else "single sequence",
                    "graph": not args.no_graph},
     }
-    log("pipeline: %d frames in %.3f s, last-frame stats %s" % (frames, elapsed, r["stats"]))
+    log("pipeline: %d frames in %.3f s (host enqueue %.3f s), last-frame stats %s"
+        % (frames, elapsed, r.get("enqueue", 0.0), r["stats"]))
+    if "enqueue" in r:
+        out["config"]["host_enqueue_us_per_frame"] = round(r["enqueue"] / max(1, frames) * 1e6, 1)
     if world == 1 and not stub:
         out["stage_us"] = stage_pass(local_rank, r["ptrs"], args.warmup, min(1000, frames), not args.no_graph)
     if stub:

@@ -17,7 +17,10 @@ constexpr int kMaxC = 3;
 // p-index bucket of a map point (the valid queries of an outer iteration that have it as a neighbour):
 // 16 ints = {pair count, the first kBktInline pair ids, head of the overflow list}, read by k_observe
 // in one round of loads (the overflow list only past kBktInline pairs)
-constexpr int kBktQuads = 4;
+#ifndef PF_BKT_QUADS
+#define PF_BKT_QUADS 4
+#endif
+constexpr int kBktQuads = PF_BKT_QUADS;
 constexpr int kBktInline = 4 * kBktQuads - 2;
 constexpr int kBktHead = 4 * kBktQuads - 1;
 
