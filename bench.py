@@ -337,7 +337,7 @@ def knn_roofline(device=0, nmap=2_000_000, nq=200_000, iters=50, pmc=True):
     found = int((idx[:, 4] >= 0).sum())
     out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-           "kernel": "k_knn_query (exact radius-gated 5-NN, 1 m cell grid)",
+           "kernel": "k_knn_thick (exact radius-gated 5-NN, 1 m cell grid, thick-row layout)",
            "workload": "config 5: map %d pts, %d queries, %d with 5 neighbours" % (nmap, nq, found),
            "alg_bytes_per_launch": alg, "avg_kernel_ms": round(ms, 5)}
     if pmc:
@@ -350,7 +350,7 @@ def knn_roofline(device=0, nmap=2_000_000, nq=200_000, iters=50, pmc=True):
 
 
 def knn_pmc_traffic(timeout_s=90):
-    """HBM (fabric) bytes per launch of k_knn_query, measured now: two rocprofv3 --pmc passes
+    """HBM (fabric) bytes per launch of k_knn_thick (the standalone query's kernel), measured now: two rocprofv3 --pmc passes
     (FETCH_SIZE, then WRITE_SIZE: they do not fit one pass) over tools/knn_probe.py as child processes.
     MI355X_MICROARCH.md: FETCH_SIZE is doubled on gfx950 (128-B requests tallied at 64 B); WRITE_SIZE
     is exact. None when rocprofv3 is unavailable or a pass fails (never a stale number)."""
@@ -377,7 +377,7 @@ def knn_pmc_traffic(timeout_s=90):
             xs = []
             for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
                 for row in csv.DictReader(open(f)):
-                    if "k_knn_query" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                    if "k_knn_thick" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
                         xs.append(float(row["Counter_Value"]))
             if not xs:
                 return None

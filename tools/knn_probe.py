@@ -1,4 +1,4 @@
-"""kNN-only workload for profiling k_knn_query (config 5: 2M-point dense map, 200k queries).
+"""kNN-only workload for profiling the standalone kNN (k_knn_thick; --layout grid: k_knn_query) (config 5: 2M-point dense map, 200k queries).
 
   python3 tools/knn_probe.py [--iters N]
 Prints avg kernel ms (HIP events) and algorithmic bytes per launch. Run under

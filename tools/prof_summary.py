@@ -10,7 +10,7 @@ Reads
 Writes
   profiles/<round>_kernel_stats.csv    the rocprofv3 stats table as produced
   profiles/<round>_frame_breakdown.md   per-kernel time per frame, launches per frame
-  profiles/knn_pmc_<round>.json         HBM bytes per k_knn_query launch (FETCH_SIZE x 2 gfx950
+  profiles/knn_pmc_<round>.json         HBM bytes per k_knn_thick launch (FETCH_SIZE x 2 gfx950
                                         correction + WRITE_SIZE, MI355X_MICROARCH.md §HBM)
 """
 import argparse
