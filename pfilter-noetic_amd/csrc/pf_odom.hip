@@ -712,31 +712,31 @@ __device__ __forceinline__ int hup(int i, int j) {
 }
 __device__ __forceinline__ int tri(int i, int j) { return i * (i + 1) / 2 + j; }   // lower, j <= i
 
-// The LM state lane 0 works on, held in registers during a step (loaded from / stored to the
-// LDS LMState around it); every loop is fully unrolled so all indices are static.
+// The LM state lanes 0 and 1 work on during a step: x, cand and the scalars in registers (loaded
+// from / stored to the LDS LMState around it); scale, g, H and D are read and written in place in
+// the LDS LMState (both lanes write identical values), so the step's live set fits the 256
+// architected VGPRs (held in registers, the 6x6 state spilled into AGPR moves: a third of the
+// step's instructions). Every loop is fully unrolled so all indices are static.
 struct LmCore {
-    double x[7], cand[7], best[7], scale[6], g[6], H[21], D[6];
+    double x[7], cand[7];
+    double *scale, *g, *H, *D;                                   // -> LMState (LDS)
     double cost, radius, decrease, x_norm, min_cost, mcc;
     int iteration, invalid, reuse, done, phase;
 };
-__device__ __forceinline__ void core_load(LmCore& c, const LMState& s) {
+__device__ __forceinline__ void core_load(LmCore& c, LMState& s) {
+    c.scale = s.scale;
+    c.g = s.g;
+    c.H = s.H;
+    c.D = s.D;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) { c.x[k] = s.x[k]; c.cand[k] = s.cand[k]; c.best[k] = s.best[k]; }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) { c.scale[k] = s.scale[k]; c.g[k] = s.g[k]; c.D[k] = s.D[k]; }
-#pragma unroll
-    for (int k = 0; k < 21; ++k) c.H[k] = s.H[k];
+    for (int k = 0; k < 7; ++k) { c.x[k] = s.x[k]; c.cand[k] = s.cand[k]; }
     c.cost = s.cost; c.radius = s.radius; c.decrease = s.decrease; c.x_norm = s.x_norm;
     c.min_cost = s.min_cost; c.mcc = s.mcc;
     c.iteration = s.iteration; c.invalid = s.invalid; c.reuse = s.reuse; c.done = s.done; c.phase = s.phase;
 }
 __device__ __forceinline__ void core_store(const LmCore& c, LMState& s) {
 #pragma unroll
-    for (int k = 0; k < 7; ++k) { s.x[k] = c.x[k]; s.cand[k] = c.cand[k]; s.best[k] = c.best[k]; }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) { s.scale[k] = c.scale[k]; s.g[k] = c.g[k]; s.D[k] = c.D[k]; }
-#pragma unroll
-    for (int k = 0; k < 21; ++k) s.H[k] = c.H[k];
+    for (int k = 0; k < 7; ++k) { s.x[k] = c.x[k]; s.cand[k] = c.cand[k]; }
     s.cost = c.cost; s.radius = c.radius; s.decrease = c.decrease; s.x_norm = c.x_norm;
     s.min_cost = c.min_cost; s.mcc = c.mcc;
     s.iteration = c.iteration; s.invalid = c.invalid; s.reuse = c.reuse; s.done = c.done; s.phase = c.phase;
@@ -856,7 +856,8 @@ __device__ __forceinline__ void lm_next_step(LmCore& lm, StepTry st, const doubl
 // 1 of a wave on identical state: the gradient-norm check x (+) (-g) and the next candidate
 // x (+) delta are the same SE(3) update, so lane 0 evaluates the first and lane 1 the second at
 // once (the candidate is computed speculatively and discarded when the check ends the solve).
-__device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot, unsigned long long* pr = nullptr) {
+// best: the LDS copy (LMState::best), written by both lanes with identical values
+__device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot, double* best, unsigned long long* pr = nullptr) {
     const double cost_c = tot[0];
     const bool bad_r = tot[28] > 0.0, bad_j = tot[29] > 0.0;
     const int kMaxIter = 4;
@@ -875,7 +876,7 @@ __device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot, unsigne
         for (int i = 0; i < 6; ++i) lm.scale[i] = 1.0 / (1.0 + sqrt(lm.H[hup(i, i)]));   // Jacobi, once
         lm.min_cost = lm.cost;
 #pragma unroll
-        for (int k = 0; k < 7; ++k) lm.best[k] = lm.x[k];
+        for (int k = 0; k < 7; ++k) best[k] = lm.x[k];
         step_ok = true;                                          // gradient check below
     } else {
         const double cand_cost = bad_r ? DBL_MAX : cost_c;       // candidate evaluated
@@ -916,7 +917,7 @@ __device__ __forceinline__ void lm_accept(LmCore& lm, const double* tot, unsigne
             if (lm.cost < lm.min_cost) {
                 lm.min_cost = lm.cost;
 #pragma unroll
-                for (int k = 0; k < 7; ++k) lm.best[k] = lm.x[k];
+                for (int k = 0; k < 7; ++k) best[k] = lm.x[k];
             }
         } else {
             lm.radius = lm.radius / lm.decrease;
@@ -1003,12 +1004,15 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
         return;
     }
-    double wmin[kMaxC][2], wmax[kMaxC][2];
-    for (int c = 0; c < kMaxC; ++c)
-        for (int ww = 0; ww < 2; ++ww) {
-            wmin[c][ww] = (double)ord2f(a.acc[A_W + 4 * c + 2 * ww]);
-            wmax[c][ww] = (double)ord2f(a.acc[A_W + 4 * c + 2 * ww + 1]);
-        }
+    // the weight bounds and this thread's home residual live in LDS, not in registers: the serial
+    // LM step of lanes 0 / 1 needs the register file (long-lived values spill it to AGPR moves)
+    __shared__ double wmin[kMaxC][2], wmax[kMaxC][2];
+    __shared__ ResIn s_mine[256];
+    if (t < 2 * kMaxC) {
+        const int c = t >> 1, ww = t & 1;
+        wmin[c][ww] = (double)ord2f(a.acc[A_W + 4 * c + 2 * ww]);
+        wmax[c][ww] = (double)ord2f(a.acc[A_W + 4 * c + 2 * ww + 1]);
+    }
     if (t == 0) {                                                // problem set-up (:252-266)
         double xn = 0;
         for (int k = 0; k < 7; ++k) {
@@ -1067,7 +1071,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         }
         return in;
     };
-    const ResIn mine = load_res((int)blockIdx.x * 256 + t);
+    s_mine[t] = load_res((int)blockIdx.x * 256 + t);
     // reduce chunk ch of evaluation ev at x into 30 partials; publish them and count the chunk done
     // unless another block claimed it first (own_claim: claim_old is this block's atomicOr result)
     auto reduce_chunk = [&](int ch, int ev, u32 claim_old, bool own_claim) {
@@ -1076,9 +1080,9 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             const int q = base + t;
             double J[6] = {0, 0, 0, 0, 0, 0}, r = 0.0, hc = 0.0;
             // the inputs of this thread's residual: from registers for the home chunk's first rows
-            // (`mine`, loaded once per launch), from memory otherwise
+            // (`s_mine`, loaded once per launch), from memory otherwise
             const bool cached = ch == (int)blockIdx.x && base == ch * 256;
-            const ResIn in = cached ? mine : load_res(q);
+            const ResIn in = cached ? s_mine[t] : load_res(q);
             if (in.kept) {
                 r = in.plane ? surf_eval(x, in.cur, d3{in.G[0], in.G[1], in.G[2]}, in.G[3], in.wgt, J)
                              : edge_eval(x, in.cur, d3{in.G[0], in.G[1], in.G[2]}, d3{in.G[3], in.G[4], in.G[5]},
@@ -1208,7 +1212,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             unsigned long long* pr = (rec && ev == 1) ? dbg + 21 : nullptr;
             core_load(c, lm);
             if (pr) pr[4] = __builtin_amdgcn_s_memrealtime();
-            lm_accept(c, tot, pr);
+            lm_accept(c, tot, lm.best, pr);
             if (pr) pr[3] = __builtin_amdgcn_s_memrealtime();
             if (ev == kLmEvals - 1) c.done = 1;
             if (t == 0) core_store(c, lm);
@@ -1300,14 +1304,20 @@ __device__ __forceinline__ bool in_crop(const DevState* st, float4 p) {
 // addPointsToMap, first pass: the pose (:278-280, k_finalize mode 1, by thread 0 of block 0), the
 // transform / append of the down-sampled clouds (:592-604, r and g carried) and the CropBox-kept
 // min / max of every class for the rgbds grids (:606-615, :40-51). The crop box is odom.t +- 100,
-// and odom.t is the solved translation params[4..6] that block 0 stores.
+// and odom.t is the solved translation params[4..6] that the pose step stores. The pose step (a
+// single-thread SVD polar factor, finalize_pose) runs on the grid's last workgroup, which takes no
+// part in the points, so it overlaps them instead of delaying block 0's share.
 template <int NC>
 __global__ void __launch_bounds__(256) k_rg_append_minmax(DevState* __restrict__ st, int* __restrict__ cnt,
                                                            u32* __restrict__ acc, Clouds map, Clouds ds,
                                                            CloudsW app, double* __restrict__ poses, int pose_cap) {
     double prm[7];
     for (int k = 0; k < 7; ++k) prm[k] = st->params[k];
-    if (blockIdx.x == 0) finalize_pose(st, poses, pose_cap, 1, acc, prm);
+    if (blockIdx.x == gridDim.x - 1) {
+        finalize_pose(st, poses, pose_cap, 1, acc, prm);
+        return;
+    }
+    const int nblk = (int)gridDim.x - 1;
     const float lox = (float)(prm[4] - 100), loy = (float)(prm[5] - 100), loz = (float)(prm[6] - 100);   // in_crop
     const float hix = (float)(prm[4] + 100), hiy = (float)(prm[5] + 100), hiz = (float)(prm[6] + 100);
     constexpr int nc = NC;
@@ -1316,7 +1326,7 @@ __global__ void __launch_bounds__(256) k_rg_append_minmax(DevState* __restrict__
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt[C_NRG] = n;
     float v[6 * kMaxC];
     minmax_init(v);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
         int c, li;
         bool ap;
         V.locate(i, c, li, ap);
@@ -1863,7 +1873,7 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     }
     // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647, BPF :1197-1290)
     const VgLeaf leaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}};
-    PF_LAUNCH_NC(nc, k_rg_append_minmax, dim3(256), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map), clouds(sb.ds),
+    PF_LAUNCH_NC(nc, k_rg_append_minmax, dim3(256 + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map), clouds(sb.ds),
                  clouds_w(o.app), o.poses, (int)o.pose_cap);
     PF_LAUNCH_NC(nc, k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map), clouds(o.app), leaf,
                  o.keys, o.vals, sort_hist(o.prim, 32, true));
