@@ -228,9 +228,12 @@ __device__ __forceinline__ void knn_push(u64 key, u64 (&k)[5]) {
     for (int q = 4; q > 0; --q) k[q] = c[q - 1] ? k[q - 1] : (q < 4 && !c[q] ? k[q] : key);
     k[0] = c[0] ? key : k[0];
 }
+// The empty-slot key is (1.0f, index 0): every candidate with d^2 >= 1 (or NaN) has a key >= it and
+// never enters the list, so the radius gate (d^2 < 1) needs no compare / select of its own, and every
+// candidate with d^2 < 1 has a key below it.
+constexpr u64 kKnnEmpty = (u64)0x3f800000u << 32;
 __device__ __forceinline__ void knn_consider(float qx, float qy, float qz, const float4& p, u64 (&k)[5]) {
-    const float r2 = knn_d2(qx, qy, qz, p);
-    const u64 key = r2 < 1.0f ? knn_key(r2, __float_as_int(p.w)) : ~0ull;
+    const u64 key = knn_key(knn_d2(qx, qy, qz, p), __float_as_int(p.w));
     if (key < k[4]) knn_push(key, k);
 }
 
@@ -283,7 +286,7 @@ __device__ __forceinline__ int knn5_team(const GridView& gv, int m, float qx, fl
                                          float (&dout)[5], int (&iout)[5]) {
     static_assert(T >= 1 && T <= 64 && (T & (T - 1)) == 0, "team: a power of two within a wave");
     constexpr int U = PF_KNN_UNROLL;
-    const u64 sentinel = knn_key(1.0f, 0x7fffffff);
+    const u64 sentinel = kKnnEmpty;
     u64 k[5];
 #pragma unroll
     for (int q = 0; q < 5; ++q) k[q] = sentinel;
@@ -416,12 +419,17 @@ struct ThickView {
     const float4* tpts;        // thick layout (x, y, z, bits(map index))
 };
 
+// loads in flight per lane (team 8, config 5, µs: U = 2 / 3 / 4 / 5 / 6 / 8 -> 34.4 / 33.1 / 32.6-32.8 /
+// 32.6 / 32.7 / 32.9)
+#ifndef PF_KNN_THICK_UNROLL
+#define PF_KNN_THICK_UNROLL 4
+#endif
 template <int T>
 __device__ __forceinline__ int knn5_thick(const ThickView& tv, float qx, float qy, float qz, bool active,
                                           float (&dout)[5], int (&iout)[5]) {
     static_assert(T >= 4 && T <= 64 && (T & (T - 1)) == 0, "team: a power of two >= 4 within a wave");
-    constexpr int U = PF_KNN_UNROLL;
-    const u64 sentinel = knn_key(1.0f, 0x7fffffff);
+    constexpr int U = PF_KNN_THICK_UNROLL;
+    const u64 sentinel = kKnnEmpty;
     u64 k[5];
 #pragma unroll
     for (int q = 0; q < 5; ++q) k[q] = sentinel;
@@ -456,20 +464,25 @@ __device__ __forceinline__ int knn5_thick(const ThickView& tv, float qx, float q
         const u32 s1 = (u32)__shfl((int)s, tbase + 1, 64), e1 = (u32)__shfl((int)e, tbase + 1, 64);
         const u32 s2 = (u32)__shfl((int)s, tbase + 2, 64), e2 = (u32)__shfl((int)e, tbase + 2, 64);
         const u32 p1 = e0 - s0, p2 = p1 + (e1 - s1), total = p2 + (e2 - s2);
-        const int o0 = (int)s0, o1 = (int)(s1 - p1), o2 = (int)(s2 - p2);
+        const u32 o0 = s0, o1 = s1 - p1, o2 = s2 - p2;
+        // branch-free body: the U loads are unconditional (an index past the end is clamped to the
+        // last point, whose copy is then given a NaN x so its key can never enter the list), and the
+        // addresses are 32-bit byte offsets from the layout's base (host: < 4 GB)
+        const char* tb = reinterpret_cast<const char*>(tv.tpts);
         for (u32 v0 = tl; v0 < total; v0 += T * U) {
             float4 p[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const u32 v = v0 + T * u;
-                const int o = v >= p2 ? o2 : (v >= p1 ? o1 : o0);
-                if (v < total) p[u] = tv.tpts[(int)v + o];
+                const u32 v = u == 0 ? v0 : min(v0 + T * u, total - 1);
+                const u32 o = v >= p2 ? o2 : (v >= p1 ? o1 : o0);
+                p[u] = *reinterpret_cast<const float4*>(tb + ((v + o) << 4));
             }
+            __builtin_amdgcn_sched_barrier(0);                   // all U loads issued before any use
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (v0 + T * u >= total) break;
-                knn_consider(qx, qy, qz, p[u], k);
-            }
+            for (int u = 1; u < U; ++u)
+                if (v0 + T * u >= total) p[u].x = __int_as_float(0x7fc00000);
+#pragma unroll
+            for (int u = 0; u < U; ++u) knn_consider(qx, qy, qz, p[u], k);
         }
     }
     int found = 0;

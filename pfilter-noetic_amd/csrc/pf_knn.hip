@@ -81,13 +81,13 @@ __global__ void __launch_bounds__(256, PF_KNN_MINW) k_knn_query(GridView gv, con
     const float4 p = active ? q[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     float d[5];
     int id[5];
-    knn5_team<T>(gv, 0, p.x, p.y, p.z, active, d, id);
+    const int found = knn5_team<T>(gv, 0, p.x, p.y, p.z, active, d, id);
     const int tl = lane_id() & (T - 1);
     if (active) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             if (k % T != tl) continue;                       // result k written by lane k % T
-            const bool f = id[k] != 0x7fffffff;
+            const bool f = k < found;
             idx[5 * i + k] = f ? id[k] : -1;
             d2[5 * i + k] = f ? d[k] : __int_as_float(0x7f800000);
         }
@@ -144,13 +144,13 @@ __global__ void __launch_bounds__(256, PF_KNN_MINW) k_knn_thick(ThickView tv, co
     const float4 p = active ? q[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     float d[5];
     int id[5];
-    knn5_thick<T>(tv, p.x, p.y, p.z, active, d, id);
+    const int found = knn5_thick<T>(tv, p.x, p.y, p.z, active, d, id);
     const int tl = lane_id() & (T - 1);
     if (active) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             if (k % T != tl) continue;
-            const bool f = id[k] != 0x7fffffff;
+            const bool f = k < found;
             idx[5 * i + k] = f ? id[k] : -1;
             d2[5 * i + k] = f ? d[k] : __int_as_float(0x7f800000);
         }
