@@ -119,3 +119,25 @@ def test_knn_thick_layout_equals_grid_walk(pa, pfsynth):
     np.testing.assert_array_equal(out[0][0], out[1][0])
     np.testing.assert_array_equal(out[0][1].view(np.uint32), out[1][1].view(np.uint32))
     assert (out[0][0][:600, 0] >= 0).sum() > 50                      # some off-grid queries found neighbours
+
+
+def test_knn_gate_boundary_both_layouts(pa, pfref):
+    """d^2 == 1.0 exactly is outside the gate (the empty list slot is keyed (1.0, index 0), pf_knn.h):
+    map point 0 and others at exactly 1 m along the axes are never reported, points just inside are,
+    in the thick-row layout and in the 9-row walk alike."""
+    import ctypes
+    just_in = np.nextafter(np.float32(1.0), np.float32(0.0))
+    mp = np.array([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, -1, 0], [just_in, 0, 0, 0], [0, -just_in, 0, 0],
+                   [0.5, 0.5, 0.5, 0], [3, 3, 3, 0]], np.float32)
+    q = np.array([[0, 0, 0, 0], [2, 0, 0, 0], [1, 1, 0, 0]], np.float32)
+    ri, rd = pfref.knn(mp, q, 5, opts=pfref.KNN_BRUTE)
+    inside = rd < 1.0
+    for layout in (1, 0):
+        kn = pa.Knn(mp.shape[0], q.shape[0])
+        assert pa.lib().pf_knn_set_layout(ctypes.c_void_p(kn._h), layout) == 0
+        kn.set_map(mp)
+        gi, gd = kn.query(q)
+        np.testing.assert_array_equal(np.where(inside, ri, -1), gi)
+        np.testing.assert_array_equal(gd[inside].view(np.uint32), rd[inside].view(np.uint32))
+        assert sorted(gi[0][gi[0] >= 0]) == [3, 4, 5]          # the exact-1 m points 0, 1, 2 are out
+        assert 0 not in gi[1]                                  # (2,0,0) -> point 0 at exactly 1 m
