@@ -372,21 +372,24 @@ __device__ __forceinline__ int knn5_team(const GridView& gv, int m, float qx, fl
             off[r] = (int)(s - total);
             total += l;
         }
+        // branch-free body as in knn5_thick below: unconditional loads (an index past the end clamped
+        // to the last point, whose copy gets a NaN x), all U loads issued before the first use
         for (u32 v0 = tl; v0 < total; v0 += T * U) {
             float4 p[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const u32 v = v0 + T * u;
+                const u32 v = u == 0 ? v0 : min(v0 + T * u, total - 1);
                 int o = off[0];
 #pragma unroll
                 for (int r = 1; r < 9; ++r) o = v >= pre[r] ? off[r] : o;
-                if (v < total) p[u] = gv.cpts[(int)v + o];
+                p[u] = gv.cpts[(int)v + o];
             }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (v0 + T * u >= total) break;
-                knn_consider(qx, qy, qz, p[u], k);
-            }
+            for (int u = 1; u < U; ++u)
+                if (v0 + T * u >= total) p[u].x = __int_as_float(0x7fc00000);
+#pragma unroll
+            for (int u = 0; u < U; ++u) knn_consider(qx, qy, qz, p[u], k);
         }
 #endif
     }

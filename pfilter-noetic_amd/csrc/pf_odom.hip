@@ -22,6 +22,7 @@
 #include "pf_geom.h"
 
 #include <climits>
+#include <cmath>
 #include <cstdlib>
 #include <vector>
 #include <cstring>
@@ -1378,6 +1379,78 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
     sort_hist_end(lh, sh, n, n);
 }
 
+// addPointsToMap's first pass and the rgbds keys in one launch, when the crop box bounds the key
+// grid (rg_fused_keys): the rgbds grid of the reference starts at the voxel of the kept points'
+// minimum (:40-56), but the sort only needs the keys' order, and idx = i0 + div0 (i1 + div1 i2) with
+// 0 <= i < div orders voxels lexicographically by (i2, i1, i0) for any origin at or below the minimum
+// and any extent covering the maximum. The crop box t +- 100 is such a box (kept points satisfy
+// lo <= p <= hi, and fl(p / leaf) and floor are monotone), so keys taken on its voxel grid sort the
+// points exactly as the reference's do, equal keys being the same voxels: no min / max pass, no
+// second launch. Pose step on the last workgroup as in k_rg_append_minmax.
+template <int NC>
+__global__ void __launch_bounds__(256) k_rg_append_keys(DevState* __restrict__ st, int* __restrict__ cnt,
+                                                         u32* __restrict__ acc, Clouds map, Clouds ds, CloudsW app,
+                                                         double* __restrict__ poses, int pose_cap, VgLeaf leaf,
+                                                         u32* __restrict__ keys, u32* __restrict__ vals,
+                                                         SortHist sh) {
+    double prm[7];
+    for (int k = 0; k < 7; ++k) prm[k] = st->params[k];
+    if (blockIdx.x == gridDim.x - 1) {
+        finalize_pose(st, poses, pose_cap, 1, acc, prm);
+        return;                                    // holds no keys: not counted by sort_hist_end
+    }
+    __shared__ u32 lh[4][256];
+    sort_hist_begin(lh);
+    const int nblk = (int)gridDim.x - 1;
+    const float lo[3] = {(float)(prm[4] - 100), (float)(prm[5] - 100), (float)(prm[6] - 100)};   // in_crop
+    const float hi[3] = {(float)(prm[4] + 100), (float)(prm[5] + 100), (float)(prm[6] + 100)};
+    const RgView<NC> V = rg_view<NC>(cnt, map, Clouds{{app.p[0], app.p[1], app.p[2]}});
+    const int n = V.total();
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[C_NRG] = n;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
+        int c, li;
+        bool ap;
+        V.locate(i, c, li, ap);
+        float4 p;
+        if (ap) {                                      // appended: pointAssociateToMap of the ds point
+            p = associate(prm, ds.at(c)[li]);
+            app.at(c)[li] = p;
+        } else {
+            p = map.at(c)[li];
+        }
+        vals[i] = (u32)i;
+        u32 key = kSentinel;
+        if (!((p.x < lo[0] || p.y < lo[1] || p.z < lo[2]) || (p.x > hi[0] || p.y > hi[1] || p.z > hi[2]))) {
+            const float lf = leaf.at(c);
+            int minb[3], div[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                minb[k] = (int)floorf(lo[k] / lf);
+                div[k] = (int)floorf(hi[k] / lf) - minb[k] + 1;
+            }
+            const int i0 = (int)(floorf(p.x / lf) - (float)minb[0]);
+            const int i1 = (int)(floorf(p.y / lf) - (float)minb[1]);
+            const int i2 = (int)(floorf(p.z / lf) - (float)minb[2]);
+            const int idx = i0 * 1 + i1 * div[0] + i2 * (div[0] * div[1]);
+            key = ((u32)idx & 0x3fffffffu) | ((u32)c << 30);
+        }
+        keys[i] = key;
+        sort_hist_add(lh, key, sh.passes);
+    }
+    const int items = n < nblk * 256 ? n : nblk * 256;  // blocks holding keys: the first ceil(items / 256)
+    sort_hist_end(lh, sh, n, items);
+}
+
+// whether the crop box's voxel grid of every class fits the 30 key bits (k_rg_append_keys); the
+// extent is at most floor(200 / leaf) + 2 voxels per axis
+inline bool rg_fused_keys(const float* leaf, int nc) {
+    for (int c = 0; c < nc; ++c) {
+        const double d = std::floor(200.0 / (double)leaf[c]) + 3.0;
+        if (!(d * d * d < (double)(1u << 30))) return false;
+    }
+    return true;
+}
+
 struct RgTailArgs {
     int* cnt;
     Clouds map, app;
@@ -1873,10 +1946,16 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     }
     // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647, BPF :1197-1290)
     const VgLeaf leaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}};
-    PF_LAUNCH_NC(nc, k_rg_append_minmax, dim3(256 + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map), clouds(sb.ds),
-                 clouds_w(o.app), o.poses, (int)o.pose_cap);
-    PF_LAUNCH_NC(nc, k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map), clouds(o.app), leaf,
-                 o.keys, o.vals, sort_hist(o.prim, 32, true));
+    if (rg_fused_keys(o.leaf_rg, nc)) {
+        PF_LAUNCH_NC(nc, k_rg_append_keys, dim3(kGrid + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map),
+                     clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap, leaf, o.keys, o.vals,
+                     sort_hist(o.prim, 32, true));
+    } else {
+        PF_LAUNCH_NC(nc, k_rg_append_minmax, dim3(256 + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map),
+                     clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap);
+        PF_LAUNCH_NC(nc, k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map), clouds(o.app),
+                     leaf, o.keys, o.vals, sort_hist(o.prim, 32, true));
+    }
     radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
     RgTailArgs ta{cnt, clouds(o.map), clouds(o.app), o.keys, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,
                   o.prm.theta_max, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err};
