@@ -233,7 +233,7 @@ void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s, bool
         hipLaunchKernelGGL(k_grid_count<true>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot);
     else
         hipLaunchKernelGGL(k_grid_count<false>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot);
-    scan_exclusive(g.cell_count, g.cell_start, g.d_ncells, nullptr, w, s);
+    scan_exclusive(g.cell_count, g.cell_start, g.d_ncells, nullptr, w, s, true);
     hipLaunchKernelGGL(k_grid_scatter, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_start, g.slot, g.cpts,
                        g.cell_count);
 }

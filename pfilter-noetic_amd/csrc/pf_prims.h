@@ -184,7 +184,9 @@ __device__ __forceinline__ void sort_hist_end(u32 (*lh)[256], const SortHist& sh
 void segment_starts(const u32* keys, const int* d_n, u32* segstart, int* d_nseg, int* d_nlt, int* d_nvalid,
                     PrimWork& w, hipStream_t s);
 
-// out[i] = sum(in[0..i)) for i < *d_n; *d_total = sum(in[0..n)) when d_total != nullptr.
-void scan_exclusive(const u32* in, u32* out, const int* d_n, u32* d_total, PrimWork& w, hipStream_t s);
+// out[i] = sum(in[0..i)) for i < *d_n; *d_total = sum(in[0..n)) when d_total != nullptr. wide: tiles of
+// 8192 items (32 per thread, 16-byte loads and stores; in / out 16-byte aligned) for long scans.
+void scan_exclusive(const u32* in, u32* out, const int* d_n, u32* d_total, PrimWork& w, hipStream_t s,
+                    bool wide = false);
 
 }  // namespace pf

@@ -163,14 +163,19 @@ __global__ void __launch_bounds__(256) k_os_pass(const u32* __restrict__ kin, co
 
 constexpr int kScanPer = 8;
 
+// PER items per thread, tiles of 256 * PER items (PER = 8: 2048, the sort tile; the cell-count scans
+// of the kNN grids use 32: a few hundred tiles over a grid of up to 256 workgroups, so a workgroup
+// scans about one tile with all of its loads in flight instead of a chain of look-backs)
+template <int PER>
 __global__ void __launch_bounds__(256) k_scan1(const u32* __restrict__ in, u32* __restrict__ out,
                                                 const int* __restrict__ d_n, u32* __restrict__ d_total,
                                                 u64* __restrict__ status, u32* __restrict__ arrive,
                                                 int* __restrict__ err) {
+    constexpr int kTile = 256 * PER;
     __shared__ u32 lw[4];
     __shared__ u32 s_excl;
     const int n = *d_n;
-    const int ntiles = (n + kSortTile - 1) / kSortTile;
+    const int ntiles = (n + kTile - 1) / kTile;
     const int t = threadIdx.x;
     const int G = ntiles < (int)gridDim.x ? ntiles : (int)gridDim.x;
     if (n == 0) {
@@ -179,13 +184,21 @@ __global__ void __launch_bounds__(256) k_scan1(const u32* __restrict__ in, u32* 
     }
     if ((int)blockIdx.x >= G) return;
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int base = tile * kSortTile + t * kScanPer;
-        u32 v[kScanPer];
+        const int base = tile * kTile + t * PER;
+        u32 v[PER];
+        if (base + PER <= n) {                                  // whole: 16-byte loads
 #pragma unroll
-        for (int k = 0; k < kScanPer; ++k) v[k] = base + k < n ? in[base + k] : 0u;
+            for (int k = 0; k < PER; k += 4) {
+                const uint4 q = *reinterpret_cast<const uint4*>(in + base + k);
+                v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PER; ++k) v[k] = base + k < n ? in[base + k] : 0u;
+        }
         u32 sum = 0;
 #pragma unroll
-        for (int k = 0; k < kScanPer; ++k) sum += v[k];
+        for (int k = 0; k < PER; ++k) sum += v[k];
         u32 agg;
         const u32 tex = block_excl_scan256(sum, lw, agg);
         if (t < 64) {
@@ -197,10 +210,22 @@ __global__ void __launch_bounds__(256) k_scan1(const u32* __restrict__ in, u32* 
         }
         __syncthreads();
         u32 r = s_excl + tex;
+        if (base + PER <= n) {
 #pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            if (base + k < n) out[base + k] = r;
-            r += v[k];
+            for (int k = 0; k < PER; k += 4) {
+                uint4 q;
+                q.x = r; r += v[k];
+                q.y = r; r += v[k + 1];
+                q.z = r; r += v[k + 2];
+                q.w = r; r += v[k + 3];
+                *reinterpret_cast<uint4*>(out + base + k) = q;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                if (base + k < n) out[base + k] = r;
+                r += v[k];
+            }
         }
         __syncthreads();
     }
@@ -334,10 +359,14 @@ void segment_starts(const u32* keys, const int* d_n, u32* segstart, int* d_nseg,
                        d_nvalid, w.scan_status, w.tickets + 5, w.err);
 }
 
-void scan_exclusive(const u32* in, u32* out, const int* d_n, u32* d_total, PrimWork& w, hipStream_t s) {
+void scan_exclusive(const u32* in, u32* out, const int* d_n, u32* d_total, PrimWork& w, hipStream_t s, bool wide) {
     const unsigned grid = (unsigned)(w.scan_tiles < (size_t)kSortMaxBlocks ? w.scan_tiles : kSortMaxBlocks);
-    hipLaunchKernelGGL(k_scan1, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, in, out, d_n, d_total, w.scan_status,
-                       w.tickets + 5, w.err);
+    if (wide)   // in and out 16-byte aligned (hipMalloc'd)
+        hipLaunchKernelGGL(k_scan1<32>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, in, out, d_n, d_total,
+                           w.scan_status, w.tickets + 5, w.err);
+    else
+        hipLaunchKernelGGL(k_scan1<kScanPer>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, in, out, d_n, d_total,
+                           w.scan_status, w.tickets + 5, w.err);
 }
 
 }  // namespace pf

@@ -84,6 +84,18 @@ def test_campus_32_line(pa, pfref, pfsynth):
     _run(od, orc, seq, range(12), check_maps_every=11)
 
 
+@pytest.mark.parametrize("map_res", [0.15, 0.25])
+def test_rgbds_key_grids(pa, pfref, pfsynth, map_res):
+    """The two rgbds key paths of addPointsToMap (pf_odom.hip): map_res 0.25 keys on the crop box's
+    voxel grid in the fused append+keys launch; at 0.15 that grid would overflow the 30 key bits
+    (rg_fused_keys), so the min/max pass and the reference's own key grid run. Both sort as the
+    reference does: counts, maps and poses against the oracle."""
+    seq = pfsynth.Sequence("S64", n_frames=20, az_steps=1200)
+    od, orc = _pair(pa, pfref, map_res=map_res)
+    _run(od, orc, seq, range(12), check_maps_every=11)
+    _compare_maps(od, orc)
+
+
 @pytest.mark.parametrize("theta_p,theta_max", [(0.4, 75), (0.0, 0)])
 def test_dense_vegetation_scene(pa, pfref, pfsynth, theta_p, theta_max):
     """S64V (bench.py's dense legs): porous tree crowns, hedges and rough ground give about twice the
