@@ -203,10 +203,14 @@ __global__ void __launch_bounds__(256) k_gs_nbmin(ClsDev d) {
 // cloud_unground in input order during the assignment pass, then walks the cells in order pushing
 // each cell's remaining points (input order) to ground or non-ground; cells with fewer than
 // gf_min_grid_pts points push nothing
-__global__ void __launch_bounds__(256) k_gs_keys(const float4* __restrict__ pts, const int* __restrict__ d_n, ClsDev d) {
+// the sorts' digit histograms are fused into their key producers (k_gs_keys, k_u_keys, k_cls_decide:
+// sort_hist_*, pf_prims.h), so no separate histogram launch precedes a sort
+__global__ void __launch_bounds__(256) k_gs_keys(const float4* __restrict__ pts, const int* __restrict__ d_n, ClsDev d,
+                                                  SortHist sh) {
     __shared__ int red[2];
+    __shared__ u32 lh[4][256];
     if (threadIdx.x < 2) red[threadIdx.x] = 0;
-    __syncthreads();
+    sort_hist_begin(lh);
     const int n = *d_n;
     const pf_cls_params& P = d.prm;
     int nu = 0, ng = 0;
@@ -232,6 +236,7 @@ __global__ void __launch_bounds__(256) k_gs_keys(const float4* __restrict__ pts,
         ng += key >= kKeyGround && key < kKeyDropped;
         d.keys[i] = key;
         d.vals[i] = (u32)i;
+        sort_hist_add(lh, key, sh.passes);
     }
     nu = wave_sum_i(nu);
     ng = wave_sum_i(ng);
@@ -244,6 +249,7 @@ __global__ void __launch_bounds__(256) k_gs_keys(const float4* __restrict__ pts,
         if (red[0]) atomicAdd(&d.cnt[CC_NU], red[0]);
         if (red[1]) atomicAdd(&d.cnt[CC_NG], red[1]);
     }
+    sort_hist_end(lh, sh, n, n);
 }
 
 // pc2pc (:633-644): the non-ground cloud U in push order, xyz only
@@ -312,7 +318,9 @@ __device__ __forceinline__ u32 sub8(float v) {
     const int s = (int)f;
     return (u32)(s < 0 ? 0 : (s > 7 ? 7 : s));
 }
-__global__ void __launch_bounds__(256) k_u_keys(ClsDev d, const int* __restrict__ dm) {
+__global__ void __launch_bounds__(256) k_u_keys(ClsDev d, const int* __restrict__ dm, SortHist sh) {
+    __shared__ u32 lh[4][256];
+    sort_hist_begin(lh);
     const int nu = d.cnt[CC_NU];
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nu; j += gridDim.x * blockDim.x) {
         const float4 p = d.U[j];
@@ -324,7 +332,9 @@ __global__ void __launch_bounds__(256) k_u_keys(ClsDev d, const int* __restrict_
         }
         d.ckeys[j] = key;
         d.cvals[j] = (u32)j;
+        sort_hist_add(lh, key, sh.passes);
     }
+    sort_hist_end(lh, sh, nu, nu);
 }
 // cell-ordered points (w = U index), and the counts left zero for the next build
 __global__ void __launch_bounds__(256) k_u_place(ClsDev d, float4* __restrict__ cpts, u32* __restrict__ cell_count,
@@ -634,10 +644,11 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
 }
 
 // PCA + decision, one thread per U point over its neighbour list (ascending distance)
-__global__ void __launch_bounds__(256) k_cls_decide(ClsDev d, const u32* __restrict__ nbr) {
+__global__ void __launch_bounds__(256) k_cls_decide(ClsDev d, const u32* __restrict__ nbr, SortHist sh) {
     __shared__ int ccount[4];
+    __shared__ u32 lh[4][256];
     if (threadIdx.x < 4) ccount[threadIdx.x] = 0;
-    __syncthreads();
+    sort_hist_begin(lh);
     const int nu = d.cnt[CC_NU];
     int local[4] = {0, 0, 0, 0};
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nu; q += gridDim.x * blockDim.x) {
@@ -655,6 +666,7 @@ __global__ void __launch_bounds__(256) k_cls_decide(ClsDev d, const u32* __restr
         d.ckeys[q] = key;
         d.cvals[q] = (u32)q;
         local[key]++;
+        sort_hist_add(lh, key, sh.passes);
     }
     for (int k = 0; k < 4; ++k) {
         const int v = wave_sum_i(local[k]);
@@ -662,6 +674,7 @@ __global__ void __launch_bounds__(256) k_cls_decide(ClsDev d, const u32* __restr
     }
     __syncthreads();
     if (threadIdx.x < 4 && ccount[threadIdx.x]) atomicAdd(&d.cnt[CC_CLS + threadIdx.x], ccount[threadIdx.x]);
+    sort_hist_end(lh, sh, nu, nu);
 }
 
 // the three clouds (U order within a class) and, optionally, their input indices
@@ -766,8 +779,8 @@ void cls_enqueue(ClsGPU& c, const float4* d_pts, const int* d_n, float4* const* 
         hipLaunchKernelGGL(k_gs_bounds, dim3(64), dim3(256), 0, s, d_pts, d_n, d);
         hipLaunchKernelGGL(k_gs_assign, dim3(kEwBlocks), dim3(256), 0, s, d_pts, d_n, d);
         hipLaunchKernelGGL(k_gs_nbmin, dim3(128), dim3(256), 0, s, d);
-        hipLaunchKernelGGL(k_gs_keys, dim3(kEwBlocks), dim3(256), 0, s, d_pts, d_n, d);
-        radix_sort_pairs(c.keys, c.vals, d_n, 16, c.w, s);
+        hipLaunchKernelGGL(k_gs_keys, dim3(kEwBlocks), dim3(256), 0, s, d_pts, d_n, d, sort_hist(c.w, 16, true));
+        radix_sort_pairs(c.keys, c.vals, d_n, 16, c.w, s, nullptr, nullptr, true);
         hipLaunchKernelGGL(k_gs_gather, dim3(kEwBlocks), dim3(256), 0, s, d_pts, d);
     } else {
         hipLaunchKernelGGL(k_cls_identity, dim3(kEwBlocks), dim3(256), 0, s, d_pts, d_n, d);
@@ -784,15 +797,15 @@ void cls_enqueue(ClsGPU& c, const float4* d_pts, const int* d_n, float4* const* 
     gp.n[0] = c.cnt + CC_NU;
     gp.nm = 1;
     grid_count_scan(c.grid, gp, c.w, s);
-    hipLaunchKernelGGL(k_u_keys, dim3(kEwBlocks), dim3(256), 0, s, d, c.grid.dims);
-    radix_sort_pairs(c.ckeys, c.cvals, c.cnt + CC_NU, 32, c.w, s);
+    hipLaunchKernelGGL(k_u_keys, dim3(kEwBlocks), dim3(256), 0, s, d, c.grid.dims, sort_hist(c.w, 32, true));
+    radix_sort_pairs(c.ckeys, c.cvals, c.cnt + CC_NU, 32, c.w, s, nullptr, nullptr, true);
     hipLaunchKernelGGL(k_u_place, dim3(kEwBlocks), dim3(256), 0, s, d, c.grid.cpts, c.grid.cell_count, c.grid.dims);
     hipLaunchKernelGGL(k_u_boxes, dim3(kEwBlocks), dim3(256), 0, s, d, c.grid.cpts);
     const GridView gv{c.grid.dims, c.grid.cell_start, c.grid.cpts};
     hipLaunchKernelGGL(k_cls_search, dim3(4096), dim3(256), 0, s, d, gv, c.nbr);
-    hipLaunchKernelGGL(k_cls_decide, dim3(kEwBlocks), dim3(256), 0, s, d, c.nbr);
+    hipLaunchKernelGGL(k_cls_decide, dim3(kEwBlocks), dim3(256), 0, s, d, c.nbr, sort_hist(c.w, 8, false));
     u32 *ks = nullptr, *vs = nullptr;
-    radix_sort_pairs(c.ckeys, c.cvals, c.cnt + CC_NU, 8, c.w, s, &ks, &vs);
+    radix_sort_pairs(c.ckeys, c.cvals, c.cnt + CC_NU, 8, c.w, s, &ks, &vs, true);
     hipLaunchKernelGGL(k_cls_out, dim3(kEwBlocks), dim3(256), 0, s, d, ks, vs, out ? out[0] : nullptr,
                        out ? out[1] : nullptr, out ? out[2] : nullptr, out_cnt ? out_cnt[0] : nullptr,
                        out_cnt ? out_cnt[1] : nullptr, out_cnt ? out_cnt[2] : nullptr, idx ? c.idx_out : nullptr);
