@@ -120,7 +120,10 @@ __global__ void __launch_bounds__(256) k_dc_polar(const float4* __restrict__ pts
 }
 
 // createHashTable (:143-177): polar / pitch / azimuth index and the voxel index of every point
-__global__ void __launch_bounds__(256) k_dc_keys(const int* __restrict__ d_n, DcvcDev d) {
+// (the digit histograms of both sorts are fused into their key kernels, k_dc_keys and k_dc_label)
+__global__ void __launch_bounds__(256) k_dc_keys(const int* __restrict__ d_n, DcvcDev d, SortHist sh) {
+    __shared__ u32 lh[4][256];
+    sort_hist_begin(lh);
     const int n = *d_n;
     const int P = d.dim[D_POLAR], W = d.dim[D_WIDTH];
     const double minPitch = d.bounds[kDcMaxBounds];
@@ -137,7 +140,9 @@ __global__ void __launch_bounds__(256) k_dc_keys(const int* __restrict__ d_n, Dc
         const int vox = (az * (P + 1) + polar) + pitch * (P + 1) * (W + 1);
         d.keys[i] = (u32)vox;
         d.vals[i] = (u32)i;
+        sort_hist_add(lh, (u32)vox, sh.passes);
     }
+    sort_hist_end(lh, sh, n, n);
 }
 
 // per voxel (segment of the sorted keys): its key, point count; union-find and component state reset
@@ -376,14 +381,19 @@ __global__ void __launch_bounds__(256) k_dc_pointvox(DcvcDev d) {
 }
 
 // per point: sort key = its component's rank (published order) or dropped, label = rank + 1 or 0
-__global__ void __launch_bounds__(256) k_dc_label(DcvcDev d, const int* __restrict__ d_n) {
+__global__ void __launch_bounds__(256) k_dc_label(DcvcDev d, const int* __restrict__ d_n, SortHist sh) {
+    __shared__ u32 lh[4][256];
+    sort_hist_begin(lh);
     const int n = *d_n;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const u32 r = d.crank[d.parent[d.okeys[i]]];
+        const u32 key = r ? r - 1 : 0xFFFFFFFFu;
         d.plab[i] = r;
-        d.okeys[i] = r ? r - 1 : 0xFFFFFFFFu;
+        d.okeys[i] = key;
         d.ovals[i] = (u32)i;
+        sort_hist_add(lh, key, sh.passes);
     }
+    sort_hist_end(lh, sh, n, n);
 }
 
 constexpr int kDcGrid = 256;
@@ -460,9 +470,9 @@ void dcvc_enqueue(DcvcGPU& g, const float4* pts, const int* d_n, hipStream_t s, 
     DcvcDev d{g.prm, g.red, g.bounds, g.dim, g.pol, g.keys, g.vals, g.segstart, g.seg_aux, g.parent,
               g.csize, g.cfirst, g.crank, g.okeys, g.ovals, g.plab, g.ukey, g.ucount, g.vtab, g.vtab_cells, g.edges, g.ecount};
     hipLaunchKernelGGL(k_dc_polar, dim3(kDcGrid), dim3(256), 0, s, pts, d_n, d);
-    hipLaunchKernelGGL(k_dc_keys, dim3(kDcGrid), dim3(256), 0, s, d_n, d);
+    hipLaunchKernelGGL(k_dc_keys, dim3(kDcGrid), dim3(256), 0, s, d_n, d, sort_hist(g.w, dcvc_key_bits(g.prm), false));
     u32 *ks = nullptr, *vs = nullptr;                       // sorted (voxel, point) pairs
-    radix_sort_pairs(g.keys, g.vals, d_n, dcvc_key_bits(g.prm), g.w, s, &ks, &vs);
+    radix_sort_pairs(g.keys, g.vals, d_n, dcvc_key_bits(g.prm), g.w, s, &ks, &vs, true);
     d.keys = ks;
     d.vals = vs;
     segment_starts(ks, d_n, g.segstart, g.seg_aux, g.seg_aux + 1, g.seg_aux + 4, g.w, s);
@@ -472,8 +482,8 @@ void dcvc_enqueue(DcvcGPU& g, const float4* pts, const int* d_n, hipStream_t s, 
     hipLaunchKernelGGL(k_dc_union, dim3(kDcGrid), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_dc_compress, dim3(kDcGrid), dim3(256), 0, s, d);
     hipLaunchKernelGGL(k_dc_rank, dim3(1), dim3(1024), 0, s, d);
-    hipLaunchKernelGGL(k_dc_label, dim3(kDcGrid), dim3(256), 0, s, d, d_n);
-    radix_sort_pairs(g.okeys, g.ovals, d_n, 16, g.w, s);
+    hipLaunchKernelGGL(k_dc_label, dim3(kDcGrid), dim3(256), 0, s, d, d_n, sort_hist(g.w, 16, true));
+    radix_sort_pairs(g.okeys, g.ovals, d_n, 16, g.w, s, nullptr, nullptr, true);
     if (out_idx) *out_idx = g.ovals;
 }
 
