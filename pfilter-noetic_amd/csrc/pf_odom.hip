@@ -445,10 +445,11 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
     }
 }
 
-// pointAssociateToMap + exact 5-NN (a team of kAssocTeam lanes per query, :297-300, :445-448), then
+// pointAssociateToMap + exact 5-NN (a team of kAssocTeam lanes per query, :297-300, :445-448; teams of
+// 8 / 16 / 32 lanes: ES 3781 / 3843 / 3563 frames/s at the end of round 2), then
 // the fit on the team's first lane, which pushes the query's pairs into the p-index buckets
 #ifndef PF_ASSOC_TEAM
-#define PF_ASSOC_TEAM 8
+#define PF_ASSOC_TEAM 16
 #endif
 constexpr int kAssocTeam = PF_ASSOC_TEAM;
 static_assert(kAssocTeam >= 5, "k_assoc writes the 5 neighbours from 5 lanes of the team");
