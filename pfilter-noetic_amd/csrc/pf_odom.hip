@@ -445,14 +445,45 @@ __device__ __forceinline__ void assoc_fit(const AssocArgs& a, int q, int c, cons
     }
 }
 
-// pointAssociateToMap + exact 5-NN (a team of kAssocTeam lanes per query, :297-300, :445-448; teams of
-// 8 / 16 / 32 lanes: ES 3781 / 3843 / 3563 frames/s at the end of round 2), then
-// the fit on the team's first lane, which pushes the query's pairs into the p-index buckets
-#ifndef PF_ASSOC_TEAM
-#define PF_ASSOC_TEAM 16
+// pointAssociateToMap + exact 5-NN (a team of T lanes per query, :297-300, :445-448), then the fit on
+// the team's first lane, which pushes the query's pairs into the p-index buckets. The team size
+// follows the frame's query count (uniform over the grid, so every wave takes the same branch): 16
+// lanes up to kAssocWideMax queries, 8 above. End of round 2, frames/s with teams of 8 / 16 / 32: S64
+// (~6k queries) 3781 / 3843 / 3563; the dense S64V scene (~10k) 3726 / 3645 with 8 / 16.
+#ifndef PF_ASSOC_WIDE_MAX
+#define PF_ASSOC_WIDE_MAX 8192
 #endif
-constexpr int kAssocTeam = PF_ASSOC_TEAM;
-static_assert(kAssocTeam >= 5, "k_assoc writes the 5 neighbours from 5 lanes of the team");
+constexpr int kAssocWideMax = PF_ASSOC_WIDE_MAX;
+template <int NC, int T>
+__device__ __forceinline__ void assoc_queries(const AssocArgs& a, const CatIdx<NC>& qi, int nq, const double* prm) {
+    static_assert(T >= 5, "k_assoc writes the 5 neighbours from 5 lanes of the team");
+    const int tl = lane_id() & (T - 1);
+    const int teams = gridDim.x * (blockDim.x / T);
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int team = gt / T, wave_team0 = (gt & ~63) / T;
+    for (int off = 0; wave_team0 + off < nq; off += teams) {     // trip count uniform per wave
+        const int q0 = team + off;
+        const bool active = q0 < nq;
+        const int c = active ? qi.cls(q0) : 0;
+        float4 pw = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (active) pw = associate(prm, a.ds.at(c)[q0 - qi.start(c)]);
+        float d[5];
+        int id[5];
+        const int found = knn5_team<T>(a.gv, c, pw.x, pw.y, pw.z, active, d, id);
+        if (active && tl < 5) {                                  // neighbours, read again by k_observe
+            int iv = id[0];
+#pragma unroll
+            for (int k = 1; k < 5; ++k)
+                if (tl == k) iv = id[k];
+            a.nbr[5 * q0 + tl] = found == 5 ? iv : -1;
+        }
+#ifndef PF_DEV_NOFIT
+        if (active && tl == 0) assoc_fit(a, q0, c, id, found);
+#else
+        if (active && tl == 0) a.qflag[q0] = 0;                  // development: time the kNN alone
+#endif
+    }
+}
 template <int NC>
 __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     const CatIdx<NC> qi = cat_idx<NC>(a.cnt + C_DS);
@@ -472,32 +503,8 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     }
     double prm[7];
     for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
-    const int tl = lane_id() & (kAssocTeam - 1);
-    const int teams = gridDim.x * (blockDim.x / kAssocTeam);
-    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-    const int team = gt / kAssocTeam, wave_team0 = (gt & ~63) / kAssocTeam;
-    for (int off = 0; wave_team0 + off < nq; off += teams) {     // trip count uniform per wave
-        const int q0 = team + off;
-        const bool active = q0 < nq;
-        const int c = active ? qi.cls(q0) : 0;
-        float4 pw = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (active) pw = associate(prm, a.ds.at(c)[q0 - qi.start(c)]);
-        float d[5];
-        int id[5];
-        const int found = knn5_team<kAssocTeam>(a.gv, c, pw.x, pw.y, pw.z, active, d, id);
-        if (active && tl < 5) {                                  // neighbours, read again by k_observe
-            int iv = id[0];
-#pragma unroll
-            for (int k = 1; k < 5; ++k)
-                if (tl == k) iv = id[k];
-            a.nbr[5 * q0 + tl] = found == 5 ? iv : -1;
-        }
-#ifndef PF_DEV_NOFIT
-        if (active && tl == 0) assoc_fit(a, q0, c, id, found);
-#else
-        if (active && tl == 0) a.qflag[q0] = 0;                  // development: time the kNN alone
-#endif
-    }
+    if (nq <= kAssocWideMax) assoc_queries<NC, 16>(a, qi, nq, prm);
+    else assoc_queries<NC, 8>(a, qi, nq, prm);
 }
 
 struct ObsArgs {
