@@ -455,7 +455,8 @@ DevStep dev_try_step(const DevLm& lm) {                       // lm_try_step
     for (int j = 0; j < 6; ++j)
         r.D[j] = lm.reuse ? lm.D[j] : std::fmin(std::fmax(lm.scale[j] * lm.H[hup(j, j)] * lm.scale[j], 1e-6), 1e32);
     // Hs + D / radius (D times the reciprocal radius), LDL^T with reciprocal pivots: the device's
-    // operation order (W_ij = L_ij d_j accumulated first, L_ij = W_ij / d_j as a product)
+    // operation order (W_ij = L_ij d_j accumulated first, L_ij = W_ij / d_j as a product) and its
+    // fused multiply-adds (std::fma: one rounding, as v_fma_f64)
     double A[21];
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j <= i; ++j) A[tri(i, j)] = lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j];
@@ -466,23 +467,23 @@ DevStep dev_try_step(const DevLm& lm) {                       // lm_try_step
     for (int i = 0; i < 6; ++i) {
         for (int j = 0; j < i; ++j) {
             double s = A[tri(i, j)];
-            for (int k = 0; k < j; ++k) s -= W[tri(i, k)] * A[tri(j, k)];
+            for (int k = 0; k < j; ++k) s = std::fma(-W[tri(i, k)], A[tri(j, k)], s);
             W[tri(i, j)] = s;
             A[tri(i, j)] = s * inv[j];
         }
         double d = A[tri(i, i)];
-        for (int k = 0; k < i; ++k) d -= W[tri(i, k)] * A[tri(i, k)];
+        for (int k = 0; k < i; ++k) d = std::fma(-W[tri(i, k)], A[tri(i, k)], d);
         ok = ok && (d > 0.0);
         inv[i] = 1.0 / d;
     }
     for (int i = 0; i < 6; ++i) {                               // L z = scale .* g
         double s = lm.scale[i] * lm.g[i];
-        for (int k = 0; k < i; ++k) s -= A[tri(i, k)] * r.y[k];
+        for (int k = 0; k < i; ++k) s = std::fma(-A[tri(i, k)], r.y[k], s);
         r.y[i] = s;
     }
     for (int i = 5; i >= 0; --i) {                              // L^T y = D^-1 z
         double s = r.y[i] * inv[i];
-        for (int k = i + 1; k < 6; ++k) s -= A[tri(k, i)] * r.y[k];
+        for (int k = i + 1; k < 6; ++k) s = std::fma(-A[tri(k, i)], r.y[k], s);
         r.y[i] = s;
     }
     for (int j = 0; j < 6; ++j) ok = ok && std::isfinite(r.y[j]);
@@ -490,10 +491,10 @@ DevStep dev_try_step(const DevLm& lm) {                       // lm_try_step
     if (ok) {
         double sg = 0.0, sHs = 0.0;
         for (int i = 0; i < 6; ++i) {
-            sg += -r.y[i] * (lm.scale[i] * lm.g[i]);
+            sg = std::fma(-r.y[i], lm.scale[i] * lm.g[i], sg);
             double hi = 0.0;
-            for (int j = 0; j < 6; ++j) hi += lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j] * -r.y[j];
-            sHs += -r.y[i] * hi;
+            for (int j = 0; j < 6; ++j) hi = std::fma(lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j], -r.y[j], hi);
+            sHs = std::fma(-r.y[i], hi, sHs);
         }
         r.mcc = -(sg + 0.5 * sHs);
     }

@@ -755,7 +755,9 @@ __device__ __forceinline__ void core_store(const LmCore& c, LMState& s) {
 // D (fresh from diag(Hs) unless reused), the LDL^T factorisation of Hs + D / radius (no square
 // roots; one reciprocal per pivot, multiplied in: 6 divisions on the serial chain instead of the
 // 27 of a Cholesky with divided substitutions), the step y (delta = -y .* scale) and the model cost
-// change mcc. Hs entries are recomputed from H. A pivot <= 0 rejects the step, as a Cholesky's
+// change mcc. Every multiply-subtract of the factorisation, the two solves and the mcc sums is one
+// explicit fused multiply-add (one rounding; the oracle's GPU_EQUIV restates it with std::fma), which
+// halves the dependent chain of the serial step. Hs entries are recomputed from H. A pivot <= 0 rejects the step, as a Cholesky's
 // non-positive square-root argument does (both test positive definiteness).
 struct StepTry {
     double y[6], D[6], mcc;
@@ -783,13 +785,13 @@ __device__ __forceinline__ StepTry lm_try_step(const LmCore& lm) {
         for (int j = 0; j < i; ++j) {
             double s = A[tri(i, j)];
 #pragma unroll
-            for (int k = 0; k < j; ++k) s -= W[tri(i, k)] * A[tri(j, k)];
+            for (int k = 0; k < j; ++k) s = fma(-W[tri(i, k)], A[tri(j, k)], s);
             W[tri(i, j)] = s;
             A[tri(i, j)] = s * inv[j];
         }
         double d = A[tri(i, i)];
 #pragma unroll
-        for (int k = 0; k < i; ++k) d -= W[tri(i, k)] * A[tri(i, k)];
+        for (int k = 0; k < i; ++k) d = fma(-W[tri(i, k)], A[tri(i, k)], d);
         ok = ok && (d > 0.0);
         inv[i] = 1.0 / d;
     }
@@ -797,14 +799,14 @@ __device__ __forceinline__ StepTry lm_try_step(const LmCore& lm) {
     for (int i = 0; i < 6; ++i) {                                // L z = scale .* g
         double s = lm.scale[i] * lm.g[i];
 #pragma unroll
-        for (int k = 0; k < i; ++k) s -= A[tri(i, k)] * r.y[k];
+        for (int k = 0; k < i; ++k) s = fma(-A[tri(i, k)], r.y[k], s);
         r.y[i] = s;
     }
 #pragma unroll
     for (int i = 5; i >= 0; --i) {                               // L^T y = D^-1 z
         double s = r.y[i] * inv[i];
 #pragma unroll
-        for (int k = i + 1; k < 6; ++k) s -= A[tri(k, i)] * r.y[k];
+        for (int k = i + 1; k < 6; ++k) s = fma(-A[tri(k, i)], r.y[k], s);
         r.y[i] = s;
     }
 #pragma unroll
@@ -814,11 +816,11 @@ __device__ __forceinline__ StepTry lm_try_step(const LmCore& lm) {
         double sg = 0.0, sHs = 0.0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            sg += -r.y[i] * (lm.scale[i] * lm.g[i]);
+            sg = fma(-r.y[i], lm.scale[i] * lm.g[i], sg);
             double hi = 0.0;
 #pragma unroll
-            for (int j = 0; j < 6; ++j) hi += lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j] * -r.y[j];
-            sHs += -r.y[i] * hi;
+            for (int j = 0; j < 6; ++j) hi = fma(lm.scale[i] * lm.H[hup(i, j)] * lm.scale[j], -r.y[j], hi);
+            sHs = fma(-r.y[i], hi, sHs);
         }
         r.mcc = -(sg + 0.5 * sHs);
     }
