@@ -68,9 +68,13 @@ def parse(argv=None):
                     help="frames of each extra ES leg (configs[0] theta=0 on S64; the S64V dense scene at "
                          "configs[1] and at theta=0); 0 = skip them")
     ap.add_argument("--leg-cpu-seconds", type=float, default=8.0, help="CPU baseline sample of each extra leg")
-    ap.add_argument("--host-leg", type=int, default=0,
-                    help="also time N frames through pf_odom_frame_host (scan in host memory, PCIe copy "
-                         "inside the timed region); reported as pcie_inclusive, never as value")
+    ap.add_argument("--no-pcie", action="store_true",
+                    help="skip the PCIe-inclusive leg (the headline's frames from pinned host RAM through "
+                         "pf_odom_frame_host; reported as pcie_inclusive, never as value)")
+    ap.add_argument("--pageable-frames", type=int, default=500,
+                    help="frames of pf_odom_frame_host from pageable memory (pcie_pageable); 0 = skip")
+    ap.add_argument("--node-frames", type=int, default=1000,
+                    help="frames of the node call pattern (pf_fe_extract -> pf_odom_update); 0 = skip")
     return ap.parse_args(argv)
 
 
@@ -155,7 +159,10 @@ def load_frames(seq_id, total, threads, preset="S64"):
         yield f0, buf, counts, "synthetic %s seed %d" % (preset, rank)
 
 
-def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier):
+def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier, keep_host=False):
+    """The headline: every scan HBM-resident before the timed region. keep_host: the scans also stay in
+    pinned host RAM (pf_host_alloc; the HBM copies are uploaded from there) for the PCIe-inclusive and
+    node-pattern legs, which read the same frames."""
     import pfilter_amd as pa
     total = warmup + steps
     lid = lidar_cfg()
@@ -163,18 +170,27 @@ def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier)
     od.init(lid, **ODOM_CFG)
     od.set_graph(use_graph)
     # stage every scan in HBM (untimed)
-    bufs, ptrs = [], []
+    bufs, ptrs, hbufs, hptrs = [], [], [], []
     data_desc = None
     npts = []
     for f0, buf, counts, desc in load_frames(rank, total, threads):
         data_desc = desc
+        src = buf
+        if keep_host:
+            hb = pa.HostBuffer(buf.nbytes)
+            src = hb.view(buf.shape)
+            src[...] = buf
+            hbufs.append(hb)
         db = pa.DeviceBuffer(buf.nbytes, device=local_rank)
-        db.upload(buf)
+        db.upload(src)
         stride = buf.shape[1] * 16
         for i in range(buf.shape[0]):
             ptrs.append((db.ptr + i * stride, int(counts[i])))
+            if keep_host:
+                hptrs.append((hb.ptr + i * stride, int(counts[i])))
             npts.append(int(counts[i]))
         bufs.append(db)
+        del buf, src
     for k in range(min(warmup, len(ptrs))):
         od.frame_device(*ptrs[k])
     od.sync()
@@ -192,7 +208,8 @@ def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier)
         raise RuntimeError("device error words 0x%x during the timed region" % stats["errors"])
     nframes = len(ptrs) - warmup
     return dict(elapsed=t1 - t0, frames=nframes, poses=poses, stats=stats, data=data_desc, enqueue=t_enq - t0,
-                mean_points=float(np.mean(npts)) if npts else 0.0, od=od, bufs=bufs, ptrs=ptrs)
+                mean_points=float(np.mean(npts)) if npts else 0.0, od=od, bufs=bufs, ptrs=ptrs, hbufs=hbufs,
+                hptrs=hptrs)
 
 
 def run_kitti11(rank, local_rank, world, warmup, threads, use_graph, barrier, concurrent=1):
@@ -282,32 +299,38 @@ def broadcast_array(dist, arr, src, device):
     return t.cpu().numpy()
 
 
-def main_knn_shard(args, rank, local_rank, world, dist, barrier):
+def main_knn_shard(args, rank, local_rank, world, dist, barrier, dev="cuda", stub=False):
     """configs[4] at N GPUs: the 2M-point map is generated on rank 0 and broadcast once; every rank runs
     the exact 5-NN kernel on its contiguous shard of the 200k queries (timed with HIP events on its
-    stream, as the roofline leg); value = all queries / the slowest rank's kernel time."""
-    import pfilter_amd as pa
+    stream, as the roofline leg); value = all queries / the slowest rank's kernel time. stub (the CPU
+    test of the rank plumbing): a 20k-point map and 2k queries go through the same broadcasts and
+    reductions, and rank r 'takes' 1 + r ms per launch."""
     import pfsynth
-    nmap, nq, iters = 2_000_000, 200_000, 50
+    nmap, nq, iters = (20_000, 2_000, 5) if stub else (2_000_000, 200_000, 50)
     mp = q = None
     if rank == 0:
         mp = pfsynth.dense_map(nmap, seed=5)
         q = pfsynth.dense_queries(mp, nq, sigma=0.3, seed=6)
     if dist is not None:
-        mp = broadcast_array(dist, mp, 0, "cuda")
-        q = broadcast_array(dist, q, 0, "cuda")
+        mp = broadcast_array(dist, mp, 0, dev)
+        q = broadcast_array(dist, q, 0, dev)
     a, b = shard_bounds(nq, world, rank)
-    kn = pa.Knn(nmap, max(1, b - a), device=local_rank)
-    kn.set_map(mp)
-    kn.query(q[a:b])
-    barrier()
-    ms, alg = kn.bench(iters)
+    if stub:
+        assert mp.shape == (nmap, 4) and q.shape == (nq, 4)
+        ms, alg = 1.0 + rank, float(b - a) * 1000.0
+    else:
+        import pfilter_amd as pa
+        kn = pa.Knn(nmap, max(1, b - a), device=local_rank)
+        kn.set_map(mp)
+        kn.query(q[a:b])
+        barrier()
+        ms, alg = kn.bench(iters)
     worst_ms, tot_alg = ms, alg
     if dist is not None:
         import torch
-        t = torch.tensor([ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        g = torch.tensor([alg], dtype=torch.float64, device="cuda")
+        g = torch.tensor([alg], dtype=torch.float64, device=dev)
         dist.all_reduce(g, op=dist.ReduceOp.SUM)
         worst_ms, tot_alg = float(t.item()), float(g.item())
     if rank == 0:
@@ -318,6 +341,8 @@ def main_knn_shard(args, rank, local_rank, world, dist, barrier):
                "config": {"workload": "configs[4] kNN: dense map replicated by broadcast, queries sharded",
                           "parallelism": "queries over GPUs"},
                "aggregate_alg_GBps": round(tot_alg / (worst_ms * 1e-3) / 1e9, 1)}
+        if stub:
+            out["stub"] = True
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -390,25 +415,95 @@ def knn_pmc_traffic(timeout_s=90):
                       "(tools/knn_probe.py, median over launches)"}
 
 
-def host_leg(device, nframes, threads):
-    """PCIe-inclusive rate: the same sequence fed from host memory through pf_odom_frame_host (repack +
-    H2D of each scan inside the call), on a fresh handle."""
+def pcie_leg(device, hptrs, warmup, use_graph=True):
+    """The headline's frames again, fed from pinned host RAM through pf_odom_frame_host (the scan's H2D
+    DMA inside the timed region, on the handle's copy stream, overlapping the previous frames' kernels;
+    pose_out NULL as the headline's frame_device). SURVEY 8(d)'s frame boundary: scans preloaded in
+    pinned host RAM, H2D included."""
     import pfilter_amd as pa
-    import pfsynth
-    seq = pfsynth.Sequence("S64", n_frames=nframes + 20, seed=0)
-    buf, counts = seq.frames(0, nframes + 20, threads=threads)
     od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lidar_cfg(), **ODOM_CFG)
-    for k in range(20):
-        od.frame_host(buf[k, :counts[k]], want_pose=False)
+    od.set_graph(use_graph)
+    for ptr, n in hptrs[:warmup]:
+        od.frame_host_ptr(ptr, n)
     od.sync()
     t0 = time.perf_counter()
-    for k in range(20, nframes + 20):
-        od.frame_host(buf[k, :counts[k]], want_pose=False)
+    for ptr, n in hptrs[warmup:]:
+        od.frame_host_ptr(ptr, n)
+    t_enq = time.perf_counter()
+    od.sync()
+    el = time.perf_counter() - t0
+    assert od.stats()["errors"] == 0
+    nf = len(hptrs) - warmup
+    return {"value": round(nf / el, 2), "unit": "frames/s", "frames": nf, "ms_per_step": round(el / nf * 1e3, 4),
+            "host_us_per_frame": round((t_enq - t0) / nf * 1e6, 1), "poses": od.poses(),
+            "note": "pf_odom_frame_host over the headline's frames from pinned host RAM (pf_host_alloc): "
+                    "H2D DMA of every scan inside the timed region"}
+
+
+def pageable_leg(device, nframes, threads, warmup=20):
+    """pf_odom_frame_host from ordinary (pageable) numpy memory: each scan repacked into the handle's
+    pinned staging, then the same DMA path (frames warmup .. warmup + nframes of the headline sequence)."""
+    import pfilter_amd as pa
+    import pfsynth
+    seq = pfsynth.Sequence("S64", n_frames=nframes + warmup, seed=0)
+    buf, counts = seq.frames(0, nframes + warmup, threads=threads)
+    scans = [np.ascontiguousarray(buf[k, :counts[k]]) for k in range(nframes + warmup)]
+    del buf
+    od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
+    od.init(lidar_cfg(), **ODOM_CFG)
+    for k in range(warmup):
+        od.frame_host(scans[k], want_pose=False)
+    od.sync()
+    t0 = time.perf_counter()
+    for k in range(warmup, nframes + warmup):
+        od.frame_host(scans[k], want_pose=False)
     od.sync()
     el = time.perf_counter() - t0
     return {"value": round(nframes / el, 2), "unit": "frames/s", "frames": nframes,
-            "note": "pf_odom_frame_host: scans in pageable host memory, repacked and copied H2D per frame"}
+            "note": "pf_odom_frame_host from pageable numpy memory (repacked into pinned staging per frame)"}
+
+
+def node_pattern_leg(device, hptrs, warmup, nframes):
+    """The drop-in call pattern of the reference's nodes: laserProcessingNode's featureExtraction
+    (src/laserProcessingNode.cpp:62-78) returns the edge / surf clouds to the host, and the odometry
+    node hands them to updatePointsToMap (src/odomEstimationNode copy.cpp:74-100), which returns the
+    pose: pf_fe_extract -> pf_odom_update per frame, both synchronous, clouds in pinned host RAM. The
+    reference's two timers are reported as fe_us / odom_us."""
+    import ctypes
+    import pfilter_amd as pa
+    L = pa.lib()
+    lid = lidar_cfg()
+    fe = ctypes.c_void_p()
+    pa._check("pf_fe_create", L.pf_fe_create(ctypes.byref(lid), device, 300000, ctypes.byref(fe)))
+    od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
+    od.init(lid, **ODOM_CFG)
+    eb, sb = pa.HostBuffer(300000 * 16), pa.HostBuffer(300000 * 16)
+    ne, ns = ctypes.c_size_t(), ctypes.c_size_t()
+    pose = np.empty(7)
+    t_fe = t_od = 0.0
+    total = min(len(hptrs), warmup + nframes)
+    for k in range(total):
+        ptr, n = hptrs[k]
+        a = time.perf_counter()
+        pa._check("pf_fe_extract", L.pf_fe_extract(fe, ptr, n, 16, eb.ptr, ctypes.byref(ne), sb.ptr,
+                                                   ctypes.byref(ns), 300000))
+        b = time.perf_counter()
+        if k == 0:
+            pa._check("pf_odom_init_map", L.pf_odom_init_map(od._h, eb.ptr, ne.value, 16, sb.ptr, ns.value, 16))
+        else:
+            pa._check("pf_odom_update", L.pf_odom_update(od._h, eb.ptr, ne.value, 16, sb.ptr, ns.value, 16,
+                                                         pose.ctypes.data))
+        c = time.perf_counter()
+        if k >= warmup:
+            t_fe += b - a
+            t_od += c - b
+    L.pf_fe_destroy(fe)
+    nf = total - warmup
+    return {"value": round(nf / (t_fe + t_od), 2), "unit": "frames/s", "frames": nf,
+            "fe_us": round(t_fe / nf * 1e6, 1), "odom_us": round(t_od / nf * 1e6, 1), "poses": od.poses(),
+            "note": "pf_fe_extract -> pf_odom_update per frame (the nodes' synchronous calls), clouds in "
+                    "pinned host RAM; frames %d..%d of the headline sequence" % (warmup, total - 1)}
 
 
 def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True, use_graph=True, dcvc=False):
@@ -706,13 +801,15 @@ def main(argv=None):
 
     threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
     if args.knn_shard:
-        return main_knn_shard(args, rank, local_rank, world, dist, barrier)
+        return main_knn_shard(args, rank, local_rank, world, dist, barrier, dev, stub)
     if args.sequences == "kitti11":
-        return main_kitti11(args, rank, local_rank, world, dist, barrier, threads)
+        return main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev, stub)
+    host_legs = world == 1 and not stub and (not args.no_pcie or args.node_frames > 0)
     if stub:
         r = stub_run(rank, args.steps)
     else:
-        r = run_gpu(rank, local_rank, world, args.steps, args.warmup, threads, not args.no_graph, barrier)
+        r = run_gpu(rank, local_rank, world, args.steps, args.warmup, threads, not args.no_graph, barrier,
+                    keep_host=host_legs)
     elapsed, frames = r["elapsed"], r["frames"]
     if dist is not None:
         elapsed, total_frames, _ = reduce_results(dist, elapsed, frames, r["poses"][-frames:], dev)
@@ -773,8 +870,21 @@ def main(argv=None):
             except Exception as e:  # report, never hide
                 log("%s leg failed: %r" % (name, e))
                 out[name] = None
-    if world == 1 and args.host_leg > 0 and not stub:
-        out["pcie_inclusive"] = host_leg(local_rank, args.host_leg, threads)
+    if host_legs and not args.no_pcie:
+        pc = pcie_leg(local_rank, r["hptrs"], args.warmup, not args.no_graph)
+        pp = pc.pop("poses")
+        pc["ratio_to_value"] = round(pc["value"] / value, 4)
+        pc["poses_equal_headline"] = bool(np.array_equal(pp, r["poses"]))
+        out["pcie_inclusive"] = pc
+        log("pcie_inclusive: %s" % pc)
+    if host_legs and args.node_frames > 0:
+        nd = node_pattern_leg(local_rank, r["hptrs"], args.warmup, args.node_frames)
+        npo = nd.pop("poses")
+        nd["poses_equal_headline"] = bool(np.array_equal(npo, r["poses"][:npo.shape[0]]))
+        out["node_pattern"] = nd
+        log("node_pattern: %s" % nd)
+    if world == 1 and not stub and args.pageable_frames > 0:
+        out["pcie_pageable"] = pageable_leg(local_rank, args.pageable_frames, threads)
     if world == 1 and not args.no_cpu and not stub:
         cb = cpu_baseline(args.cpu_seconds, args.warmup)
         f0, f1 = cb.pop("frames")
@@ -789,14 +899,19 @@ def main(argv=None):
         dist.destroy_process_group()
 
 
-def main_kitti11(args, rank, local_rank, world, dist, barrier, threads):
-    r = run_kitti11(rank, local_rank, world, args.warmup, threads, not args.no_graph, barrier, args.concurrent)
+def main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev="cuda", stub=False):
+    if stub:                       # CPU test of the rank plumbing: rank r 'takes' 1 + r seconds
+        mine = lpt_assign(KITTI_SEQ_FRAMES, world)[rank]
+        r = dict(elapsed=1.0 + rank, frames=sum(KITTI_SEQ_FRAMES[sq] for sq in mine),
+                 sequences=["%02d" % sq for sq in mine])
+    else:
+        r = run_kitti11(rank, local_rank, world, args.warmup, threads, not args.no_graph, barrier, args.concurrent)
     elapsed, frames = r["elapsed"], r["frames"]
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        f = torch.tensor([frames], dtype=torch.int64, device="cuda")
+        f = torch.tensor([frames], dtype=torch.int64, device=dev)
         dist.all_reduce(f, op=dist.ReduceOp.SUM)
         elapsed, total = float(t.item()), int(f.item())
     else:
@@ -811,6 +926,8 @@ def main_kitti11(args, rank, local_rank, world, dist, barrier, threads):
                           "assignment": lpt_assign(KITTI_SEQ_FRAMES, world), "rank0_sequences": r["sequences"],
                           "parallelism": "sequences over GPUs", "concurrent_per_gpu": args.concurrent,
                           "graph": not args.no_graph}}
+        if stub:
+            out["stub"] = True
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -187,9 +187,11 @@ int pf_cls_ground_seg(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes
  * (0 none, 1 pillar, 2 beam, 3 facade, :663-682) and the neighbour count pt_num (:223); either may
  * be NULL */
 int pf_cls_classify(pf_cls* h, const float* xyz, size_t n, size_t stride_bytes, uint8_t* cls, int32_t* pt_num);
-/* The normals nongroundExtract's assign_normal (include/preProcess.hpp:327-346) writes into the
- * classified points, 4 floats per point: (principal direction, linear_2) for pillar and beam points,
- * (normal direction, planar_2) for facade points, zeros for unclassified points. Per point of the last
+/* The normals assign_normal (include/preProcess.hpp:327-346) leaves in the points, 4 floats per point:
+ * (principal direction, linear_2) for pillar and beam points (featureExtract, :663-674); (normal
+ * direction, planar_2) for every other point with more than 3 neighbours (get_pc_pca_feature,
+ * :238-239); zeros with 0-3 neighbours (the zero-initialised feature; the reference leaves points with
+ * 0-1 neighbours untouched, which the C++ shim does too, using the pt_num counts). Per point of the last
  * pf_cls_classify call (input order) or, after pf_cls_extract, per non-ground point in ground_seg's
  * push order. n = the number of points wanted (at most that call's point count). */
 int pf_cls_normals(pf_cls* h, float* normal4, size_t n);
@@ -256,6 +258,9 @@ int pf_map_get(pf_map* h, float* xyzi, size_t cap, size_t* n);                  
  * the device (pf_odom_poses). pose_out may be NULL, in which case the call only enqueues work on
  * the handle's stream and returns without waiting. */
 int pf_odom_frame_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]);
+/* The same from host memory (stride as pf_fe_extract): the scan is uploaded by DMA on the handle's copy
+ * stream, overlapping the previous frames' kernels; with pose_out NULL the call only enqueues, as
+ * pf_odom_frame_device. The caller's buffer may change as soon as the call returns. */
 int pf_odom_frame_host(pf_odom* h, const float* xyzi, size_t n, size_t stride_bytes, double pose_out[7]);
 int pf_odom_sync(pf_odom* h);
 /* poses of frames processed so far, 7 doubles each */
@@ -306,6 +311,14 @@ int pf_device_count(int* n);
 int pf_dev_malloc(int device, size_t bytes, void** d);
 int pf_dev_free(int device, void* d);
 int pf_memcpy_h2d(int device, void* dst, const void* src, size_t bytes);
+/* Pinned (page-locked), device-mapped host memory usable with any device. The host-input entry points
+ * (pf_fe_extract, pf_odom_frame_host, pf_odom_init_map / update, pf_bpf_init_map / update) DMA a
+ * 16-byte-stride cloud straight from such a block, and pf_fe_extract writes its outputs straight into
+ * one; other memory is repacked into the handle's own pinned staging first. The reference's nodes
+ * hold their clouds in host RAM (src/laserProcessingNode.cpp:62-66), so this is how a caller keeps
+ * scans "preloaded in pinned host RAM" (SURVEY 8(d)). */
+int pf_host_alloc(size_t bytes, void** p);
+int pf_host_free(void* p);
 int pf_memcpy_d2h(int device, void* dst, const void* src, size_t bytes);
 
 /* ---------------- exact radius-gated 5-NN (the roofline kernel) ----------------

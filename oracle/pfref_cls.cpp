@@ -140,7 +140,7 @@ int pca_class(const std::vector<P3>& c, const std::vector<std::pair<float, int>>
               const pfref_cls_params& p, float* normal4 = nullptr) {
     const int n = (int)nb.size();
     if (normal4) normal4[0] = normal4[1] = normal4[2] = normal4[3] = 0.f;
-    if (!(n > p.k_min) || n <= 3) return 0;                            // :657 (and :289)
+    if (n <= 3) return 0;                                              // :289 (features zero-initialised, :206)
     float sx = 0.f, sy = 0.f, sz = 0.f;                                // compute3DCentroid
     for (const auto& e : nb) {
         sx += c[(size_t)e.second].x;
@@ -170,16 +170,19 @@ int pca_class(const std::vector<P3>& c, const std::vector<std::pair<float, int>>
     const double d1 = l1, d2 = l2, d3 = l3;                            // eigenvalue_t is double (:77-82)
     const double linear_2 = (d1 - d2) / d1;                            // :315-316
     const double planar_2 = (d2 - d3) / d1;
-    // assign_normal (:327-346): pillar / beam carry the principal direction and linear_2, a facade the
-    // normal direction and planar_2 (pt.normal[3], a float)
+    // assign_normal (:327-346): get_pc_pca_feature gives every point with more than min_k = 1
+    // neighbours the normal direction and planar_2 (:238-239, pt.normal[3] a float); featureExtract
+    // then gives pillar / beam points the principal direction and linear_2 (:663-674)
     auto put = [&](const float* v, double w) {
         if (normal4) { normal4[0] = v[0]; normal4[1] = v[1]; normal4[2] = v[2]; normal4[3] = (float)w; }
     };
+    put(nv, planar_2);
+    if (!(n > p.k_min)) return 0;                                      // :657
     if (linear_2 > p.edge_thre) {                                      // :659-674
         if (std::fabs(v0[2]) > p.linear_vsin_high) { put(v0, linear_2); return 1; }
         if (std::fabs(v0[2]) < p.linear_vsin_low && qz < p.beam_h_max && qz > p.beam_h_min) { put(v0, linear_2); return 2; }
     } else if (planar_2 > p.planar_thre) {                             // :676-684
-        if (std::fabs(nv[2]) < p.planar_vsin_low) { put(nv, planar_2); return 3; }
+        if (std::fabs(nv[2]) < p.planar_vsin_low) return 3;
     }
     return 0;
 }

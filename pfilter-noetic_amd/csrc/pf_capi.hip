@@ -1,5 +1,6 @@
 // C ABI (include/pfilter_hip.h) over the device pipeline. Host code here only stages inputs,
 // enqueues work on the handle's stream and copies results back; all arithmetic is on the device.
+#include <climits>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -20,8 +21,11 @@ __global__ void k_set_int(int* p, int v) {
 
 // repack points with x,y,z at offsets 0,4,8 (+ intensity at 16 for a 32-byte PCL stride, at 12 for
 // 16-byte packing) into packed float4
-void repack(const float* src, size_t n, size_t stride, std::vector<float4>& out) {
-    out.resize(n);
+void repack(const float* src, size_t n, size_t stride, float4* out) {
+    if (stride == 16) {
+        if (n) std::memcpy(out, src, sizeof(float4) * n);
+        return;
+    }
     const char* b = reinterpret_cast<const char*>(src);
     for (size_t i = 0; i < n; ++i) {
         const float* p = reinterpret_cast<const float*>(b + i * stride);
@@ -34,6 +38,58 @@ void repack(const float* src, size_t n, size_t stride, std::vector<float4>& out)
 
 bool valid_stride(size_t s) { return s == 16 || s == 32 || s >= 12; }
 
+// pf_host_alloc blocks (pinned, mapped, portable): host base -> (bytes, device-side address). Host-input
+// entry points DMA straight from such a block instead of repacking the caller's memory first.
+struct PinnedBlock {
+    size_t bytes;
+    char* dev;
+};
+std::mutex g_pin_mu;
+std::map<uintptr_t, PinnedBlock> g_pinned;
+
+// the device-side address of [p, p + bytes) when it lies inside one pf_host_alloc block, else nullptr
+void* pinned_dev(const void* p, size_t bytes) {
+    if (!p) return nullptr;
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pinned.upper_bound((uintptr_t)p);
+    if (it == g_pinned.begin()) return nullptr;
+    --it;
+    const uintptr_t a = (uintptr_t)p;
+    if (a + bytes > it->first + it->second.bytes) return nullptr;
+    return it->second.dev + (a - it->first);
+}
+
+// read_pose's one gather: counters, sticky error words, the latest pose (identity before the first
+// frame) and the estimator state into mapped pinned host memory
+__global__ void k_readback(const int* __restrict__ cnt, const int* __restrict__ errw, const double* __restrict__ pose,
+                           const DevState* __restrict__ st, HostRead* __restrict__ out) {
+    const int t = threadIdx.x;
+    if (t < C_COUNT) out->cnt[t] = cnt[t];
+    if (t < E_COUNT) out->err[t] = errw[t];
+    if (t < 7) out->pose[t] = pose ? pose[t] : (t == 3 ? 1.0 : 0.0);
+    constexpr int nw = (int)(sizeof(DevState) / 4);
+    for (int i = t; i < nw; i += blockDim.x) reinterpret_cast<int*>(&out->st)[i] = reinterpret_cast<const int*>(st)[i];
+}
+
+// fe handle output: the counts and, when they fit `cap`, the edge / surf points into the caller's
+// (mapped) memory or the handle's mapped staging; one launch after featureExtraction, no count round trip
+__global__ void k_fe_out(const int* __restrict__ cnt, const int* __restrict__ ferr, const float4* __restrict__ e,
+                         const float4* __restrict__ sf, float4* __restrict__ oe, float4* __restrict__ os, int cap,
+                         int* __restrict__ hcnt) {
+    const int ne = cnt[1], ns = cnt[2];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        hcnt[0] = ne;
+        hcnt[1] = ns;
+        hcnt[2] = *ferr;
+    }
+    if (ne > cap || ns > cap) return;
+    const int stride = gridDim.x * blockDim.x;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ne + ns; i += stride) {
+        if (i < ne) oe[i] = e[i];
+        else os[i - ne] = sf[i - ne];
+    }
+}
+
 }  // namespace
 
 struct pf_fe {
@@ -43,8 +99,11 @@ struct pf_fe {
     float4* d_edge = nullptr;
     float4* d_surf = nullptr;
     int* d_cnt = nullptr;   // [0] n, [1] ne, [2] ns
-    int* h_cnt = nullptr;   // pinned
-    std::vector<float4> host;
+    int* h_cnt = nullptr;   // mapped pinned: ne, ns, featureExtraction error word
+    int* h_cnt_dev = nullptr;
+    float4* h_in = nullptr;   // pinned staging of a repacked scan (max_points)
+    float4* h_out = nullptr;  // mapped pinned staging of the outputs (2 x max_points)
+    float4* h_out_dev = nullptr;
 };
 
 // per-stage device timing (pf_odom_set_stage_timing): a ring of event quadruples {A start, A end,
@@ -61,7 +120,6 @@ struct StageTiming {
 
 struct pf_odom {
     OdomGPU o;
-    std::vector<float4> host[kMaxC];
     StageTiming* timing = nullptr;
 };
 
@@ -117,7 +175,14 @@ int pf_fe_create(const pf_lidar_params* lidar, int device, size_t max_points, pf
     if (rc == PF_OK && hipMalloc(&h->d_edge, sizeof(float4) * ecap) != hipSuccess) rc = PF_ENOMEM;
     if (rc == PF_OK && hipMalloc(&h->d_surf, sizeof(float4) * max_points) != hipSuccess) rc = PF_ENOMEM;
     if (rc == PF_OK && hipMalloc(&h->d_cnt, sizeof(int) * 4) != hipSuccess) rc = PF_ENOMEM;
-    if (rc == PF_OK && hipHostMalloc(&h->h_cnt, sizeof(int) * 4) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipHostMalloc(&h->h_cnt, sizeof(int) * 4, hipHostMallocMapped) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_cnt_dev), h->h_cnt, 0) != hipSuccess)
+        rc = PF_EHIP;
+    if (rc == PF_OK && hipHostMalloc(&h->h_in, sizeof(float4) * max_points) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipHostMalloc(&h->h_out, sizeof(float4) * 2 * max_points, hipHostMallocMapped) != hipSuccess)
+        rc = PF_ENOMEM;
+    if (rc == PF_OK && hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_out_dev), h->h_out, 0) != hipSuccess)
+        rc = PF_EHIP;
     if (rc != PF_OK) {
         pf_fe_destroy(h);
         return rc;
@@ -129,44 +194,55 @@ int pf_fe_create(const pf_lidar_params* lidar, int device, size_t max_points, pf
 int pf_fe_destroy(pf_fe* h) {
     if (!h) return PF_OK;
     (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
     fe_free(h->fe);
     (void)hipFree(h->d_edge);
     (void)hipFree(h->d_surf);
     (void)hipFree(h->d_cnt);
     if (h->h_cnt) (void)hipHostFree(h->h_cnt);
+    if (h->h_in) (void)hipHostFree(h->h_in);
+    if (h->h_out) (void)hipHostFree(h->h_out);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return PF_OK;
 }
 
+// One synchronisation per call: the scan goes up by DMA (straight from a pf_host_alloc block with a
+// 16-byte stride, else repacked into pinned staging first), featureExtraction runs, and k_fe_out writes
+// the counts and the clouds into mapped host memory (the caller's own pf_host_alloc outputs, or the
+// handle's staging, copied out after the synchronisation).
 int pf_fe_extract(pf_fe* h, const float* xyzi, size_t n, size_t stride_bytes, float* edge_out, size_t* n_edge,
                   float* surf_out, size_t* n_surf, size_t cap) {
     if (!h || (!xyzi && n) || !n_edge || !n_surf || !valid_stride(stride_bytes)) return PF_EINVAL;
     if (n > h->fe.cap) return PF_ECAPACITY;
     PF_HIP_TRY(hipSetDevice(h->device));
-    repack(xyzi, n, stride_bytes, h->host);
-    if (n) PF_HIP_TRY(hipMemcpyAsync(h->fe.d_in_stage, h->host.data(), sizeof(float4) * n, hipMemcpyHostToDevice,
-                                     h->stream));
+    if (n) {
+        const void* src = stride_bytes == 16 && pinned_dev(xyzi, sizeof(float4) * n) ? (const void*)xyzi : nullptr;
+        if (!src) {
+            repack(xyzi, n, stride_bytes, h->h_in);
+            src = h->h_in;
+        }
+        PF_HIP_TRY(hipMemcpyAsync(h->fe.d_in_stage, src, sizeof(float4) * n, hipMemcpyHostToDevice, h->stream));
+    }
     hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, h->stream, h->d_cnt, (int)n);
     fe_enqueue(h->fe, h->fe.d_in_stage, h->d_cnt, h->d_edge, h->d_cnt + 1, h->d_surf, h->d_cnt + 2, h->stream);
-    PF_HIP_TRY(hipMemcpyAsync(h->h_cnt, h->d_cnt, sizeof(int) * 3, hipMemcpyDeviceToHost, h->stream));
-    int ferr = 0;
-    PF_HIP_TRY(hipMemcpyAsync(&ferr, h->fe.err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    const size_t ocap = cap < (size_t)INT_MAX ? cap : (size_t)INT_MAX;
+    float4* de = edge_out ? static_cast<float4*>(pinned_dev(edge_out, sizeof(float4) * ocap)) : nullptr;
+    float4* ds = surf_out ? static_cast<float4*>(pinned_dev(surf_out, sizeof(float4) * ocap)) : nullptr;
+    hipLaunchKernelGGL(k_fe_out, dim3(256), dim3(256), 0, h->stream, h->d_cnt, h->fe.err, h->d_edge, h->d_surf,
+                       de ? de : h->h_out_dev, ds ? ds : h->h_out_dev + h->fe.cap, (int)ocap, h->h_cnt_dev);
     PF_HIP_TRY(hipStreamSynchronize(h->stream));
     PF_HIP_TRY(hipGetLastError());
-    if (ferr) {
-        (void)hipMemsetAsync(h->fe.err, 0, sizeof(int), h->stream);
+    if (h->h_cnt[2]) {
+        PF_HIP_TRY(hipMemsetAsync(h->fe.err, 0, sizeof(int), h->stream));
         return PF_EUNSUPPORTED;
     }
-    const size_t ne = (size_t)h->h_cnt[1], ns = (size_t)h->h_cnt[2];
+    const size_t ne = (size_t)h->h_cnt[0], ns = (size_t)h->h_cnt[1];
     *n_edge = ne;
     *n_surf = ns;
     if (ne > cap || ns > cap) return PF_ECAPACITY;
-    if (ne && edge_out)
-        PF_HIP_TRY(hipMemcpyAsync(edge_out, h->d_edge, sizeof(float4) * ne, hipMemcpyDeviceToHost, h->stream));
-    if (ns && surf_out)
-        PF_HIP_TRY(hipMemcpyAsync(surf_out, h->d_surf, sizeof(float4) * ns, hipMemcpyDeviceToHost, h->stream));
-    PF_HIP_TRY(hipStreamSynchronize(h->stream));
+    if (edge_out && !de && ne) std::memcpy(edge_out, h->h_out, sizeof(float4) * ne);
+    if (surf_out && !ds && ns) std::memcpy(surf_out, h->h_out + h->fe.cap, sizeof(float4) * ns);
     return PF_OK;
 }
 
@@ -247,32 +323,81 @@ static int stage_b_end(pf_odom* h, int p) {
     return PF_OK;
 }
 
-// the caller's class clouds (host memory) into slot p's inputs, on stage A's stream
-static int stage_inputs(pf_odom* h, int p, const float* const* cl, const size_t* n, const size_t* stride) {
-    OdomGPU& o = h->o;
-    const int nc = o.cls.nc;
-    for (int c = 0; c < nc; ++c) {
-        if ((!cl[c] && n[c]) || !valid_stride(stride[c])) return PF_EINVAL;
-        if (n[c] > o.in_cap) return PF_ECAPACITY;
-    }
-    StageBuf& sb = o.sb[p];
-    for (int c = 0; c < nc; ++c) {
-        repack(cl[c], n[c], stride[c], h->host[c]);
-        if (n[c]) PF_HIP_TRY(hipMemcpyAsync(sb.in[c], h->host[c].data(), sizeof(float4) * n[c], hipMemcpyHostToDevice,
-                                            o.stream_a));
-        hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, sb.cnt + C_IN + c, (int)n[c]);
+// Host-input staging (HostStage), allocated by the first host-input call of a handle
+static int host_stage(OdomGPU& o) {
+    if (o.hs) return PF_OK;
+    HostStage* hs = new (std::nothrow) HostStage();
+    if (!hs) return PF_ENOMEM;
+    o.hs = hs;              // freed by odom_destroy, also after a partial allocation
+    const size_t pts = (size_t)kMaxC * o.in_cap;
+    if (hipStreamCreateWithFlags(&hs->stream, hipStreamNonBlocking) != hipSuccess) return PF_EHIP;
+    for (int p = 0; p < kSlots; ++p) {
+        if (hipHostMalloc(&hs->h[p], sizeof(float4) * pts) != hipSuccess) return PF_ENOMEM;
+        if (hipMalloc(&hs->d[p], sizeof(float4) * pts) != hipSuccess) return PF_ENOMEM;
+        if (hipEventCreateWithFlags(&hs->ev[p], hipEventDisableTiming) != hipSuccess) return PF_EHIP;
     }
     return PF_OK;
 }
 
-// The handle's sticky error words (ErrWord, pf_odom.h), read on stage B's stream after the work
-// enqueued so far: any word set since the last report is reported once and cleared. A bounded
-// device wait that gave up (LM chunks, sort look-back) is PF_EHIP; a dropped sector, an overfull map
-// grid or a front-end grid limit is PF_ECAPACITY. `peek` reads without reporting (get_stats).
-static int sticky_status(OdomGPU& o, bool peek = false) {
-    int* e = o.h_cnt + C_COUNT;
-    PF_HIP_TRY(hipMemcpyAsync(e, o.errw, sizeof(int) * E_COUNT, hipMemcpyDeviceToHost, o.stream));
-    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+// Uploads nc host clouds for the frame in slot p into hs->d[p] (cloud c at offset c * in_cap) on the
+// copy stream and makes stage A's stream wait for the copy. A cloud with a 16-byte stride inside a
+// pf_host_alloc block goes up straight from the caller's memory; any other is repacked into the
+// slot's pinned buffer first. The device slot is rewritten only after stage A of the slot's previous
+// frame (ev_a[p]) and the pinned slot only after its previous copy (hs->ev[p]), so neither the host
+// nor the streams wait for each other in steady state. *direct: some cloud was read from the caller's
+// memory (the caller must wait for hs->ev[p] before its buffers may change).
+static int host_upload(OdomGPU& o, int p, int nc, const float* const* cl, const size_t* n, const size_t* stride,
+                       bool* direct) {
+    if (int rc = host_stage(o)) return rc;
+    HostStage& hs = *o.hs;
+    *direct = false;
+    bool repacked = false;
+    for (int c = 0; c < nc; ++c) {
+        if ((!cl[c] && n[c]) || !valid_stride(stride[c])) return PF_EINVAL;
+        if (n[c] > o.in_cap) return PF_ECAPACITY;
+    }
+    PF_HIP_TRY(hipStreamWaitEvent(hs.stream, o.ev_a[p], 0));
+    for (int c = 0; c < nc; ++c) {
+        if (!n[c]) continue;
+        const void* src = stride[c] == 16 && pinned_dev(cl[c], sizeof(float4) * n[c]) ? (const void*)cl[c] : nullptr;
+        if (src) {
+            *direct = true;
+        } else {
+            if (!repacked) PF_HIP_TRY(hipEventSynchronize(hs.ev[p]));   // the pinned slot's last copy is done
+            repacked = true;
+            float4* dst = hs.h[p] + (size_t)c * o.in_cap;
+            repack(cl[c], n[c], stride[c], dst);
+            src = dst;
+        }
+        PF_HIP_TRY(hipMemcpyAsync(hs.d[p] + (size_t)c * o.in_cap, src, sizeof(float4) * n[c], hipMemcpyHostToDevice,
+                                  hs.stream));
+    }
+    PF_HIP_TRY(hipEventRecord(hs.ev[p], hs.stream));
+    PF_HIP_TRY(hipStreamWaitEvent(o.stream_a, hs.ev[p], 0));
+    return PF_OK;
+}
+
+// the caller's class clouds (host memory) into slot p's inputs, on stage A's stream
+static int stage_inputs(pf_odom* h, int p, const float* const* cl, const size_t* n, const size_t* stride) {
+    OdomGPU& o = h->o;
+    const int nc = o.cls.nc;
+    bool direct = false;
+    if (int rc = host_upload(o, p, nc, cl, n, stride, &direct)) return rc;
+    StageBuf& sb = o.sb[p];
+    for (int c = 0; c < nc; ++c) {
+        if (n[c]) PF_HIP_TRY(hipMemcpyAsync(sb.in[c], o.hs->d[p] + (size_t)c * o.in_cap, sizeof(float4) * n[c],
+                                            hipMemcpyDeviceToDevice, o.stream_a));
+        hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, sb.cnt + C_IN + c, (int)n[c]);
+    }
+    if (direct) PF_HIP_TRY(hipEventSynchronize(o.hs->ev[p]));   // the caller's buffers are free on return
+    return PF_OK;
+}
+
+// The handle's sticky error words (ErrWord, pf_odom.h) as read into e[0 .. E_COUNT): any word set since
+// the last report is reported once and cleared. A bounded device wait that gave up (LM chunks, sort
+// look-back) is PF_EHIP; a dropped sector, an overfull map grid or a front-end grid limit is PF_ECAPACITY.
+// `peek` reads without reporting (get_stats).
+static int sticky_report(OdomGPU& o, const int* e, bool peek) {
     int bits = 0;
     for (int k = 0; k < E_COUNT; ++k)
         if (e[k]) bits |= 1 << k;
@@ -285,30 +410,40 @@ static int sticky_status(OdomGPU& o, bool peek = false) {
     return (bits & hip_bits) ? PF_EHIP : PF_ECAPACITY;
 }
 
-static int read_pose(pf_odom* h, double pose[7]) {
-    OdomGPU& o = h->o;
-    if (o.frames == 0) {
-        const double id[7] = {0, 0, 0, 1, 0, 0, 0};
-        std::memcpy(pose, id, sizeof(id));
-        return PF_OK;
-    }
-    const size_t slot = (size_t)(o.frames - 1) % o.pose_cap;
-    PF_HIP_TRY(hipMemcpyAsync(o.h_pose, o.poses + 7 * slot, sizeof(double) * 7, hipMemcpyDeviceToHost, o.stream));
+// the sticky words read on stage B's stream after the work enqueued so far
+static int sticky_status(OdomGPU& o, bool peek = false) {
+    int* e = o.h_cnt + C_COUNT;
+    PF_HIP_TRY(hipMemcpyAsync(e, o.errw, sizeof(int) * E_COUNT, hipMemcpyDeviceToHost, o.stream));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
-    std::memcpy(pose, o.h_pose, sizeof(double) * 7);
-    return sticky_status(o);
+    return sticky_report(o, e, peek);
 }
 
-static int frame_status(pf_odom* h) {
+// After the work enqueued so far: counters, error words, the latest pose and the estimator state in
+// one gather (k_readback) and one synchronisation; reports the sticky words. The state read stays
+// cached for pf_odom_get_state until the next frame / update / set_state.
+static int readback(pf_odom* h) {
     OdomGPU& o = h->o;
-    PF_HIP_TRY(hipMemcpyAsync(o.h_cnt, o.cnt, sizeof(int) * C_COUNT, hipMemcpyDeviceToHost, o.stream));
+    const double* pose = o.frames > 0 ? o.poses + 7 * ((size_t)(o.frames - 1) % o.pose_cap) : nullptr;
+    hipLaunchKernelGGL(k_readback, dim3(1), dim3(64), 0, o.stream, o.cnt, o.errw, pose, o.st, o.h_rd_dev);
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     PF_HIP_TRY(hipGetLastError());
-    if (int rc = sticky_status(o)) return rc;
-    if (o.h_cnt[C_ERR]) return PF_EHIP;                  // a bounded device-side wait gave up
-    if (!o.h_cnt[C_GATE]) return PF_W_MAP_TOO_SMALL;
-    for (int c = 0; c < o.cls.nc; ++c)               // :428-431 / :574-577, BPF :875-878, :1188-1191
-        if (o.h_cnt[C_KEPT + c] < 20) return PF_W_FEW_CORRESPONDENCES;
+    o.rd_frames = o.frames;
+    return sticky_report(o, o.h_rd->err, false);
+}
+
+static int read_pose(pf_odom* h, double pose[7]) {
+    const int rc = readback(h);
+    std::memcpy(pose, h->o.h_rd->pose, sizeof(double) * 7);
+    return rc;
+}
+
+// the update / init_map status from the counters of the last readback: the reference's messages
+static int frame_status(pf_odom* h) {
+    const int* c = h->o.h_rd->cnt;
+    if (c[C_ERR]) return PF_EHIP;                        // a bounded device-side wait gave up
+    if (!c[C_GATE]) return PF_W_MAP_TOO_SMALL;
+    for (int k = 0; k < h->o.cls.nc; ++k)              // :428-431 / :574-577, BPF :875-878, :1188-1191
+        if (c[C_KEPT + k] < 20) return PF_W_FEW_CORRESPONDENCES;
     return PF_OK;
 }
 
@@ -324,11 +459,11 @@ static int init_map_n(pf_odom* h, const float* const* cl, const size_t* n, const
     odom_enqueue_export(o, o.stream);
     rc = stage_b_end(h, p);
     if (rc) return rc;
-    PF_HIP_TRY(hipStreamSynchronize(o.stream));
-    PF_HIP_TRY(hipGetLastError());
-    return PF_OK;
+    return readback(h);
 }
 
+// updatePointsToMap is synchronous in the reference (the node reads `odom` right after it): one
+// readback per call reports the pose, the status and the sticky words
 static int update_n(pf_odom* h, const float* const* cl, const size_t* n, const size_t* stride, double pose_out[7]) {
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
@@ -343,10 +478,9 @@ static int update_n(pf_odom* h, const float* const* cl, const size_t* n, const s
     odom_enqueue_export(o, o.stream);
     rc = stage_b_end(h, p);
     if (rc) return rc;
-    if (pose_out) {
-        rc = read_pose(h, pose_out);
-        if (rc) return rc;
-    }
+    rc = readback(h);
+    if (pose_out) std::memcpy(pose_out, o.h_rd->pose, sizeof(double) * 7);
+    if (rc) return rc;
     return frame_status(h);
 }
 
@@ -565,21 +699,23 @@ int pf_odom_frame_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_
     return PF_OK;
 }
 
+// The scan goes up by DMA on the copy stream (host_upload) and stage A's stream waits for it: no host
+// wait on the device. With pose_out NULL the call only enqueues (the frame pipeline of
+// pf_odom_frame_device); from a pf_host_alloc block with a 16-byte stride the call returns once the
+// DMA has read the caller's scan, otherwise once the scan is repacked into pinned staging.
 int pf_odom_frame_host(pf_odom* h, const float* xyzi, size_t n, size_t stride_bytes, double pose_out[7]) {
     if (!h || (!xyzi && n) || !valid_stride(stride_bytes) || h->o.cls.nc != 2) return PF_EINVAL;
     OdomGPU& o = h->o;
     if (n > o.in_cap) return PF_ECAPACITY;
     PF_HIP_TRY(hipSetDevice(o.device));
-    repack(xyzi, n, stride_bytes, h->host[0]);
-    // the upload goes through fe.d_in_stage on stage A's stream, ordered before the frame's copy
-    // into the staging buffer; the host vector is reused next call, so wait for the copy
-    if (n) PF_HIP_TRY(hipMemcpyAsync(o.fe.d_in_stage, h->host[0].data(), sizeof(float4) * n, hipMemcpyHostToDevice,
-                                     o.stream_a));
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
-    int rc = enqueue_frame(h, o.fe.d_in_stage, n, nullptr, nullptr);
+    const int p = o.frames % kSlots;
+    bool direct = false;
+    int rc = host_upload(o, p, 1, &xyzi, &n, &stride_bytes, &direct);
     if (rc) return rc;
+    rc = enqueue_frame(h, o.hs->d[p], n, nullptr, nullptr);
+    if (rc) return rc;
+    if (direct) PF_HIP_TRY(hipEventSynchronize(o.hs->ev[p]));
     if (pose_out) return read_pose(h, pose_out);
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
     return PF_OK;
 }
 
@@ -766,9 +902,9 @@ int pf_odom_get_state(pf_odom* h, double parameters[7], double last_odom[12], in
     if (!h) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
-    DevState st;
-    PF_HIP_TRY(hipMemcpyAsync(&st, o.st, sizeof(st), hipMemcpyDeviceToHost, o.stream));
-    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    int rc = PF_OK;
+    if (o.rd_frames != o.frames) rc = readback(h);      // else: the state read with the last pose
+    const DevState& st = o.h_rd->st;
     if (parameters) std::memcpy(parameters, st.params, sizeof(st.params));
     if (last_odom)
         for (int i = 0; i < 3; ++i) {
@@ -776,7 +912,7 @@ int pf_odom_get_state(pf_odom* h, double parameters[7], double last_odom[12], in
             last_odom[4 * i + 3] = st.lastt[i];
         }
     if (optimization_count) *optimization_count = st.optimization_count;
-    return sticky_status(o);
+    return rc;
 }
 
 int pf_odom_set_state(pf_odom* h, const double odom_pose[7], const double last_pose[7], int optimization_count) {
@@ -803,6 +939,7 @@ int pf_odom_set_state(pf_odom* h, const double odom_pose[7], const double last_p
     PF_HIP_TRY(hipMemcpy(o.st, &st, sizeof(st), hipMemcpyHostToDevice));
     o.opt_count_host = optimization_count;
     o.inited = true;                       // the next frame runs updatePointsToMap on the set maps
+    o.rd_frames = -1;
     return PF_OK;
 }
 
@@ -918,6 +1055,7 @@ int pf_odom_restore(pf_odom* h, const void* buf, size_t size) {
     o.inited = hd.inited != 0;
     o.opt_count_host = hd.opt_count_host;
     o.frames = has_pose ? 1 : 0;
+    o.rd_frames = -1;
     return PF_OK;
 }
 
@@ -986,6 +1124,34 @@ int pf_dev_malloc(int device, size_t bytes, void** d) {
 int pf_dev_free(int device, void* d) {
     PF_HIP_TRY(hipSetDevice(device));
     PF_HIP_TRY(hipFree(d));
+    return PF_OK;
+}
+
+int pf_host_alloc(size_t bytes, void** p) {
+    if (!p || !bytes) return PF_EINVAL;
+    *p = nullptr;
+    void* h = nullptr;
+    if (hipHostMalloc(&h, bytes, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess) return PF_ENOMEM;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipHostFree(h);
+        return PF_EHIP;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        g_pinned[(uintptr_t)h] = PinnedBlock{bytes, static_cast<char*>(d)};
+    }
+    *p = h;
+    return PF_OK;
+}
+
+int pf_host_free(void* p) {
+    if (!p) return PF_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        if (!g_pinned.erase((uintptr_t)p)) return PF_EINVAL;
+    }
+    PF_HIP_TRY(hipHostFree(p));
     return PF_OK;
 }
 

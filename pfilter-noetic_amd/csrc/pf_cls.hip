@@ -35,7 +35,7 @@ struct ClsDev {          // kernel view of ClsGPU
     int* sticky;         // optional: a sticky copy of CC_ERR (the odometry handle's error word)
     u32 cap;             // allocation sizes, for the bounds-checked development build (PF_DEV_BOUNDS)
     u32 cell_cap;
-    float4* nrm;         // per U point: the normal assign_normal writes (zeros when unclassified)
+    float4* nrm;         // per U point: the normal assign_normal leaves (pca_code)
 };
 ClsDev dev_view(ClsGPU& c) {
     return ClsDev{c.prm, c.cnt, c.gb, c.gdim, c.cell_cnt, c.cell_minz, c.cell_nb, c.pcell, c.keys, c.vals,
@@ -378,12 +378,14 @@ __global__ void __launch_bounds__(256) k_u_boxes(ClsDev d, const float4* __restr
 // PCA of the neighbourhood nb[0 .. n) (ascending distance) and the class decision, :653-688 /
 // :283-323, f32 as pcl::PCA computes it; the eigen-decomposition is the f64 cyclic Jacobi (eig3)
 // of the f32 covariance, rounded back to f32. Returns the index_with_feature code; nrm receives what
-// assign_normal (:327-346) writes into a classified point: (principal direction, linear_2) for a
-// pillar or beam, (normal direction, planar_2) for a facade, zeros otherwise.
+// assign_normal (:327-346) leaves in the point: get_pc_pca_feature writes (normal direction,
+// planar_2) into every point with more than 3 neighbours (:238-239; with 2-3 the zero-initialised
+// feature, :206), featureExtract then overwrites pillar and beam points with (principal direction,
+// linear_2) (:663-674); zeros for 0-3 neighbours.
 template <class Get>
 __device__ int pca_code(Get get, int n, float qz, const pf_cls_params& P, float4& nrm) {
     nrm = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (!(n > P.k_min) || n <= 3) return 0;
+    if (n <= 3) return 0;
 #ifdef PF_DEV_NOPCA
     return 3;                                  // development: the search without the PCA (timing only)
 #endif
@@ -415,15 +417,14 @@ __device__ int pca_code(Get get, int n, float qz, const pf_cls_params& P, float4
     const double d1 = l1, d2 = l2, d3 = l3;
     const double linear_2 = (d1 - d2) / d1;
     const double planar_2 = (d2 - d3) / d1;
+    nrm = make_float4(nv[0], nv[1], nv[2], (float)planar_2);    // assign_normal(plane), :238-239
+    if (!(n > P.k_min)) return 0;                               // :657
     if (linear_2 > (double)P.edge_thre) {
         const float4 pr = make_float4(v0[0], v0[1], v0[2], (float)linear_2);
         if (fabsf(v0[2]) > P.linear_vsin_high) { nrm = pr; return 1; }
         if (fabsf(v0[2]) < P.linear_vsin_low && qz < P.beam_h_max && qz > P.beam_h_min) { nrm = pr; return 2; }
     } else if (planar_2 > (double)P.planar_thre) {
-        if (fabsf(nv[2]) < P.planar_vsin_low) {
-            nrm = make_float4(nv[0], nv[1], nv[2], (float)planar_2);
-            return 3;
-        }
+        if (fabsf(nv[2]) < P.planar_vsin_low) return 3;
     }
     return 0;
 }

@@ -103,6 +103,7 @@ __global__ void __launch_bounds__(256) k_dc_polar(const float4* __restrict__ pts
             const int height = (int)((maxPitch - minPitch) / d.prm.delta_p);
             double range = minPolar;                        // :127-134
             int step = 1, k = 0;
+            d.dim[D_ERR] = 0;                               // per call: a past overflow does not stick
             while (range <= maxPolar) {
                 if (k >= kDcMaxBounds) { d.dim[D_ERR] = 1; break; }
                 range += (d.prm.start_r - step * d.prm.delta_r);
@@ -427,6 +428,7 @@ void dcvc_free(DcvcGPU& g) {
 
 int dcvc_reset(DcvcGPU& g, hipStream_t s) {
     PF_HIP_TRY(hipMemsetAsync(g.dim + D_CALLS, 0, sizeof(int), s));
+    PF_HIP_TRY(hipMemsetAsync(g.dim + D_ERR, 0, sizeof(int), s));
     return PF_OK;
 }
 
@@ -504,9 +506,21 @@ struct pf_dcvc {
 };
 
 namespace {
+// The ring widths start_r - k delta_r (:127-134) must stay positive out to max(5 m, max_range) within
+// kDcMaxBounds rings; otherwise the reference's loop never reaches the far points (an endless loop
+// there, an overflow here), so such a parameter set is refused.
 bool dcvc_params_ok(const pf_dcvc_params* p) {
-    return p && p->delta_p > 0 && p->delta_a > 0 && p->start_r > 0 && p->delta_r >= 0 && p->max_range > 0 &&
-           p->max_range < 1e5 && p->min_seg >= 0;
+    if (!(p && p->delta_p > 0 && p->delta_a > 0 && p->start_r > 0 && p->delta_r >= 0 && p->max_range > 0 &&
+          p->max_range < 1e5 && p->min_seg >= 0))
+        return false;
+    const double top = p->max_range > 5.0 ? p->max_range : 5.0;
+    double range = 0.0;
+    for (int step = 1; range <= top; ++step) {
+        const double w = p->start_r - step * p->delta_r;
+        if (!(w > 0) || step > kDcMaxBounds) return false;
+        range += w;
+    }
+    return true;
 }
 }  // namespace
 

@@ -115,6 +115,26 @@ struct StageBuf {
 // kSlots - 1 frames ahead of stage B
 constexpr int kSlots = 3;
 
+// What the host reads back after a call that reports a pose (read_pose): the counters, the sticky
+// error words, the latest pose and the estimator state, gathered by one kernel into mapped pinned
+// host memory, so a frame's report costs one stream synchronisation.
+struct HostRead {
+    int cnt[C_COUNT];
+    int err[E_COUNT];
+    double pose[7];
+    DevState st;
+};
+
+// Host-input staging (pf_odom_frame_host / update / init_map): per pipeline slot a pinned host buffer
+// (the repacked caller clouds) and a device buffer the copy stream fills by DMA; stage A's stream
+// waits for the slot's copy event instead of the host waiting for the copy.
+struct HostStage {
+    hipStream_t stream = nullptr;          // copy stream (H2D)
+    float4* h[kSlots] = {};                // pinned, kMaxC * in_cap points each
+    float4* d[kSlots] = {};                // device, kMaxC * in_cap points each
+    hipEvent_t ev[kSlots] = {};            // slot's copy done
+};
+
 struct OdomGPU {
     pf_lidar_params lidar{};
     pf_odom_params prm{};
@@ -142,6 +162,10 @@ struct OdomGPU {
     int err_last[E_COUNT] = {};    // values of the words at their last report (pf_dev_errors)
     int* h_cnt = nullptr;          // pinned mirror
     double* h_pose = nullptr;      // pinned [7]
+    HostRead* h_rd = nullptr;      // mapped pinned (read_pose)
+    HostRead* h_rd_dev = nullptr;  // its device-side address
+    int rd_frames = -1;            // `frames` at the last read_pose (-1: the cached state is stale)
+    HostStage* hs = nullptr;       // host-input staging, allocated by the first host-input call
     // map export (pf_odom_set_map_export): after every update the maps are written straight into
     // mapped pinned host memory by k_map_export (device-resident sizes, no host round trip)
     bool export_maps = false;

@@ -1037,6 +1037,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         lm.n_res = nres;
         lm.done = 0;
         aborted = 0;
+        nbad[0] = nbad[1] = 0;                                   // before the barrier: every wave may count
         int h = 0;
         for (int i = 0; i < 6; ++i)
             for (int j = i; j < 6; ++j) { hi_[h] = (unsigned char)i; hj_[h] = (unsigned char)j; ++h; }
@@ -1057,7 +1058,6 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     constexpr u32 kFull = (u32)((1ull << kLmBlocks) - 1ull);
     __shared__ int s_won, s_state, s_steal;
     u32* claim = a.arrive;                                       // [kLmEvalSlots] claim masks
-    if (t < 2) nbad[t] = 0;
     double x[7];
     // one residual's inputs: the down-sampled point, the line (a, b) or plane (n, d) and the weight
     auto load_res = [&](int q) {
@@ -1772,6 +1772,8 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     }
     if (hipHostMalloc(&o.h_cnt, sizeof(int) * (C_COUNT + E_COUNT)) != hipSuccess) return PF_ENOMEM;   // + errw mirror
     if (hipHostMalloc(&o.h_pose, sizeof(double) * 8) != hipSuccess) return PF_ENOMEM;
+    if (hipHostMalloc(&o.h_rd, sizeof(HostRead), hipHostMallocMapped) != hipSuccess) return PF_ENOMEM;
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&o.h_rd_dev), o.h_rd, 0) != hipSuccess) return PF_EHIP;
     // init (:182-208, BPF :649-681): identity odom / last_odom, parameters {0,0,0,1,0,0,0},
     // optimization_count 2
     DevState h{};
@@ -1828,6 +1830,7 @@ int odom_reset(OdomGPU& o) {
     o.inited = false;
     o.frames = 0;
     o.err_seen = 0;
+    o.rd_frames = -1;
     return PF_OK;
 }
 
@@ -1870,6 +1873,16 @@ void odom_destroy(OdomGPU& o) {
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
     if (o.h_pose) (void)hipHostFree(o.h_pose);
+    if (o.h_rd) (void)hipHostFree(o.h_rd);
+    if (o.hs) {
+        for (int p = 0; p < kSlots; ++p) {
+            if (o.hs->h[p]) (void)hipHostFree(o.hs->h[p]);
+            (void)hipFree(o.hs->d[p]);
+            if (o.hs->ev[p]) (void)hipEventDestroy(o.hs->ev[p]);
+        }
+        if (o.hs->stream) (void)hipStreamDestroy(o.hs->stream);
+        delete o.hs;
+    }
     for (int c = 0; c < kMaxC; ++c)
         if (o.h_map[c]) (void)hipHostFree(o.h_map[c]);
     if (o.h_map_n) (void)hipHostFree(o.h_map_n);

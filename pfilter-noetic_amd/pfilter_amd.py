@@ -137,7 +137,8 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_fe_set_ring_model", "pf_odom_set_ring_model", "pf_odom_get_state", "pf_odom_snapshot",
            "pf_odom_restore", "pf_odom_set_map_export", "pf_odom_map_export", "pf_odom_set_stage_timing",
            "pf_odom_stage_times", "pf_odom_set_state", "pf_cls_normals", "pf_dcvc_default_params",
-           "pf_dcvc_create", "pf_dcvc_destroy", "pf_dcvc_run", "pf_dcvc_reset", "pf_cls_set_dcvc", "pf_bpf_set_dcvc"]
+           "pf_dcvc_create", "pf_dcvc_destroy", "pf_dcvc_run", "pf_dcvc_reset", "pf_cls_set_dcvc", "pf_bpf_set_dcvc",
+           "pf_host_alloc", "pf_host_free"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -195,6 +196,8 @@ def lib():
     L.pf_dev_free.argtypes = [_i, _vp]
     L.pf_memcpy_h2d.argtypes = [_i, _vp, _vp, _sz]
     L.pf_memcpy_d2h.argtypes = [_i, _vp, _vp, _sz]
+    L.pf_host_alloc.argtypes = [_sz, ctypes.POINTER(_vp)]
+    L.pf_host_free.argtypes = [_vp]
     L.pf_knn_create.argtypes = [_i, _sz, _sz, ctypes.POINTER(_vp)]
     L.pf_knn_destroy.argtypes = [_vp]
     L.pf_knn_set_map.argtypes = [_vp, _vp, _sz]
@@ -284,6 +287,35 @@ class DeviceBuffer:
     def free(self):
         if self.ptr:
             lib().pf_dev_free(self.device, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class HostBuffer:
+    """Pinned, device-mapped host memory (pf_host_alloc): what a caller keeps its scans in so that the
+    host-input entry points DMA them without a repack. view() gives numpy arrays over it."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        p = _vp()
+        _check("pf_host_alloc", lib().pf_host_alloc(self.nbytes, ctypes.byref(p)), allow_warn=False)
+        self.ptr = p.value
+
+    def view(self, shape, dtype=np.float32, offset=0):
+        dt = np.dtype(dtype)
+        count = int(np.prod(shape))
+        assert offset + count * dt.itemsize <= self.nbytes
+        raw = (ctypes.c_char * (count * dt.itemsize)).from_address(self.ptr + offset)
+        return np.frombuffer(raw, dtype=dt, count=count).reshape(shape)
+
+    def free(self):
+        if self.ptr:
+            lib().pf_host_free(self.ptr)
             self.ptr = None
 
     def __del__(self):
@@ -403,6 +435,13 @@ class Odom_ES_EstimationClass:
         x = _f32x4(xyzi)
         pose = np.empty(7)
         _check("pf_odom_frame_host", lib().pf_odom_frame_host(self._h, x.ctypes.data, x.shape[0], 16,
+                                                              pose.ctypes.data if want_pose else None))
+        return pose if want_pose else None
+
+    def frame_host_ptr(self, hptr, n, want_pose=False):
+        """one packed float4 scan at a host address (a HostBuffer: DMA straight from it)"""
+        pose = np.empty(7)
+        _check("pf_odom_frame_host", lib().pf_odom_frame_host(self._h, hptr, int(n), 16,
                                                               pose.ctypes.data if want_pose else None))
         return pose if want_pose else None
 

@@ -514,9 +514,11 @@ private:
 
 // nongroundExtract (include/preProcess.hpp:616-735): featureExtract on the non-ground cloud. CloudTpl
 // is the point-cloud template (pcl::PointCloud); PointN the output point (pcl::PointXYZINormal). As the
-// reference's assign_normal (:327-346) does, every classified point of the input cloud gets its PCA
-// normal (normal_x / _y / _z and the fourth float of the normal block, pt.normal[3]: linear_2 or
-// planar_2) before it is pushed to its class cloud.
+// reference's assign_normal (:327-346) does, every point of the input cloud with more than one
+// neighbour gets the normal get_pc_pca_feature leaves (:238-239: the PCA normal direction and
+// planar_2, zeros with 2-3 neighbours), and classified points the one featureExtract writes before it
+// pushes them to their class cloud (normal_x / _y / _z and the fourth float of the normal block,
+// pt.normal[3]: linear_2 for pillar / beam, planar_2 for facade).
 template <class P>
 auto set_pca_normal(P& pt, const float* n4, int) -> decltype((void)pt.normal_x, void()) {
     pt.normal_x = n4[0];
@@ -569,17 +571,18 @@ public:
         p.beam_h_min = beam_height_min;
         const size_t n = cloud_in->points.size();
         code_.resize(n ? n : 1);
+        pt_num_.resize(n ? n : 1);
         pf_cls* h = cls_.get(p, n);
         check("pf_cls_classify", pf_cls_classify(h, n ? &cloud_in->points[0].x : nullptr, n, sizeof(PointT),
-                                                 code_.data(), nullptr));
+                                                 code_.data(), pt_num_.data()));
         nrm_.resize(4 * (n ? n : 1));
         check("pf_cls_normals", pf_cls_normals(h, nrm_.data(), n));
         index_with_feature.assign(n, 0);
         for (size_t i = 0; i < n; ++i) {
             const int c = code_[i];
             index_with_feature[i] = c;
+            if (pt_num_[i] > 1) set_pca_normal(cloud_in->points[i], &nrm_[4 * i], 0);   // min_k = 1 (:238)
             if (c == 0) continue;
-            set_pca_normal(cloud_in->points[i], &nrm_[4 * i], 0);
             PointN pn;
             pn.x = cloud_in->points[i].x;
             pn.y = cloud_in->points[i].y;
@@ -601,6 +604,7 @@ public:
 private:
     ClsHandle cls_;
     std::vector<uint8_t> code_;
+    std::vector<int32_t> pt_num_;
     std::vector<float> nrm_;
 };
 

@@ -121,3 +121,43 @@ def test_gpus_flag_must_match_world():
     import pytest
     with pytest.raises(SystemExit):
         bench.resolve_world(a, {"WORLD_SIZE": "2"})
+
+
+def _launch(extra):
+    import json
+    import subprocess
+    env = dict(os.environ, PF_BENCH_BACKEND="gloo", PF_BENCH_STUB="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + extra, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_kitti11_mode_gloo_world2():
+    """configs[3] (`--sequences kitti11`) at 2 ranks over gloo with the stubbed pipeline: one JSON line,
+    n_gpus 2, all 23,201 frames of the 11 sequences counted once, time = the slowest rank's."""
+    out = _launch(["--sequences", "kitti11", "--warmup", "0"])
+    assert out["n_gpus"] == 2 and out["stub"] and out["scaling"] == "strong"
+    assert out["steps"] == sum(bench_frames()) == 23201
+    assert abs(out["value"] - 23201 / 2.0) < 1e-6
+    assert sorted(s for r in out["config"]["assignment"] for s in r) == list(range(11))
+
+
+def bench_frames():
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.KITTI_SEQ_FRAMES
+
+
+def test_knn_shard_mode_gloo_world2():
+    """configs[4] kNN over 2 ranks (`--knn-shard`) over gloo with the stubbed kernel: the map and queries
+    are broadcast from rank 0, the slowest rank's time and the summed algorithmic bytes reduced."""
+    out = _launch(["--knn-shard"])
+    assert out["n_gpus"] == 2 and out["stub"]
+    assert abs(out["ms_per_step"] - 2.0) < 1e-9                  # rank 1's 2 ms
+    assert abs(out["value"] - 2000 / 2e-3) < 1e-3
+    assert abs(out["aggregate_alg_GBps"] - 2000 * 1000.0 / 2e-3 / 1e9) < 0.1

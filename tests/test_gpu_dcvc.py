@@ -140,3 +140,44 @@ def test_bpf_scan_pipeline_with_curvedfilter(pa, pfsynth):
         assert od.stats()["errors"] == 0
     np.testing.assert_array_equal(out[0], out[1])
     assert np.isfinite(out[0]).all() and np.linalg.norm(out[0][-1, 4:6]) > 1.0
+
+
+def _isolated_points():
+    """6,000 single-point clusters: every third azimuth bin, every third 1 m range ring, two pitch
+    layers 9.6 degrees apart, so no two points share a 27-voxel neighbourhood (> kDcMaxClusters)"""
+    az = np.deg2rad(np.arange(0, 360, 3.6))
+    rng = 10.0 + 3.0 * np.arange(30)
+    pit = np.deg2rad([2.0, 11.6])
+    a, r, p = np.meshgrid(az, rng, pit, indexing="ij")
+    xyz = np.stack([r * np.cos(p) * np.cos(a), r * np.cos(p) * np.sin(a), r * np.sin(p)], -1).reshape(-1, 3)
+    return xyz.astype(np.float32)
+
+
+def test_curvedfilter_overflow_does_not_stick(pa, pfref, pfsynth):
+    """a frame whose kept clusters exceed the device's cluster table raises PF_ECAPACITY for
+    that frame only; the next frames run normally again (the DCVC error word is per call) and equal the
+    oracle chain, and so does a frame after pf_dcvc-style reset of the sequence."""
+    fe = pa.BPFFrontEnd(max_points=300000, device=0, ground_filter=0)
+    fe.set_dcvc(True, min_seg=0)
+    seq = pfsynth.Sequence("S64", n_frames=3)
+    x0 = seq.frame(0)
+    fe.extract(x0)                                      # first call: rings from 5 m
+    with pytest.raises(pa.PFError) as ei:
+        fe.extract(_isolated_points())
+    assert ei.value.code == pa.PF_ECAPACITY
+    for k in (1, 2):
+        x = seq.frame(k)
+        got = fe.extract(x)
+        want = pfref.bpf_preprocess(x, pfref.cls_params(ground_filter=0), dcvc=pfref.dcvc_params(min_seg=0),
+                                    components=True)
+        for key in ("beam", "pillar", "facade"):
+            np.testing.assert_array_equal(got[key], want[key], err_msg="%d %s" % (k, key))
+
+
+def test_dcvc_rejects_rings_that_never_reach_max_range(pa):
+    """start_r - k * delta_r reaches 0 at about 166 m with the default widths: a max_range past that
+    is refused at create (the reference would loop forever building its ring bounds, :127-134)."""
+    with pytest.raises(pa.PFError) as ei:
+        pa.Dcvc(max_points=1000, max_range=200.0)
+    assert ei.value.code == pa.PF_EINVAL
+    pa.Dcvc(max_points=1000, max_range=150.0)

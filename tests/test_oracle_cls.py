@@ -208,7 +208,9 @@ def test_pca_known_geometry(pfref):
 def test_pca_normals_known_geometry(pfref):
     """assign_normal (include/preProcess.hpp:327-346): a pole's points carry the principal direction
     (+-z) with linear_2 = 1 in the fourth float, a wall's facade points the wall normal (+-y) with
-    planar_2 there; unclassified points carry zeros."""
+    planar_2 there. Every other point with more than 3 neighbours keeps what get_pc_pca_feature wrote
+    (:238-239): its PCA normal direction and planar_2 (about 0 on a pole); points with 0-3 neighbours
+    carry the zero-initialised feature's zeros."""
     p = pfref.cls_params()
     t = np.linspace(0, 4, 81, dtype=np.float32)
     pole = np.c_[np.zeros(81), np.zeros(81), t - 1].astype(np.float32)
@@ -217,7 +219,15 @@ def test_pca_normals_known_geometry(pfref):
     assert on.sum() > 10
     np.testing.assert_allclose(np.abs(nrm[on, 2]), 1.0, atol=1e-6)
     np.testing.assert_allclose(nrm[on, 3], 1.0, atol=1e-6)
-    assert np.all(nrm[~on] == 0)
+    sparse = np.c_[np.zeros(14), np.zeros(14), np.arange(14) * 0.3 - 1].astype(np.float32)
+    cls, num, nrm = pfref.pca_classify(sparse, p, normals=True)
+    rest = (num > 3) & (cls == 0)                  # 4-7 neighbours: unclassified (k_min 8) but normal set
+    assert rest.sum() > 5
+    np.testing.assert_allclose(np.linalg.norm(nrm[rest, :3], axis=1), 1.0, atol=1e-5)
+    assert np.all(np.abs(nrm[rest, 3]) < 1e-3)
+    few = np.c_[np.zeros(3), np.zeros(3), np.arange(3) * 0.3].astype(np.float32)
+    cls, num, nrm = pfref.pca_classify(few, p, normals=True)
+    assert list(num) == [3, 3, 3] and np.all(nrm == 0)          # the point itself counts
     rng = np.random.default_rng(7)
     u, v = rng.uniform(0, 3, (2, 2000))
     wall = np.c_[u + 30, np.full(u.size, 5.0), v].astype(np.float32)
