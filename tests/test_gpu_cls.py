@@ -46,8 +46,9 @@ def test_classify_matches_oracle(pa, pfref, pfsynth, fe):
 
 
 def test_normals_match_oracle(pa, pfref, pfsynth, fe):
-    """pf_cls_normals: the normal assign_normal writes into every classified point, bit-exact against
-    the oracle (same f32 PCA sums, same f64 eigensolver rounded to f32); zeros elsewhere."""
+    """pf_cls_normals: the normal assign_normal leaves in every point, bit-exact against the oracle
+    (same f32 PCA sums, same f64 eigensolver rounded to f32): the class's direction for classified
+    points, the PCA normal for other points with more than 3 neighbours (:238-239), zeros with 0-3."""
     x = pfsynth.Sequence("S64", n_frames=6).frame(5)
     g, u = pfref.ground_seg(x, pfref.cls_params())
     U = x[u]
@@ -55,9 +56,10 @@ def test_normals_match_oracle(pa, pfref, pfsynth, fe):
     ocls, onum, onrm = pfref.pca_classify(U, pfref.cls_params(), normals=True)
     np.testing.assert_array_equal(cls, ocls)
     np.testing.assert_array_equal(nrm.view(np.uint32), onrm.view(np.uint32))
-    on = cls > 0
+    on = num > 3
     np.testing.assert_allclose(np.linalg.norm(nrm[on, :3], axis=1), 1.0, atol=1e-5)
     assert np.all(nrm[~on] == 0)
+    assert ((cls == 0) & on).sum() > 100                     # unclassified points with a normal
 
 
 @pytest.mark.parametrize("kw", [dict(k=5), dict(k=32, k_min=3), dict(radius=0.5), dict(ground_filter=0),
