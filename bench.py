@@ -441,7 +441,7 @@ def pcie_leg(device, hptrs, warmup, use_graph=True):
                     "H2D DMA of every scan inside the timed region"}
 
 
-def pageable_leg(device, nframes, threads, warmup=20):
+def pageable_leg(device, nframes, threads, warmup=20, use_graph=True):
     """pf_odom_frame_host from ordinary (pageable) numpy memory: each scan repacked into the handle's
     pinned staging, then the same DMA path (frames warmup .. warmup + nframes of the headline sequence)."""
     import pfilter_amd as pa
@@ -452,6 +452,7 @@ def pageable_leg(device, nframes, threads, warmup=20):
     del buf
     od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lidar_cfg(), **ODOM_CFG)
+    od.set_graph(use_graph)
     for k in range(warmup):
         od.frame_host(scans[k], want_pose=False)
     od.sync()
@@ -884,7 +885,7 @@ def main(argv=None):
         out["node_pattern"] = nd
         log("node_pattern: %s" % nd)
     if world == 1 and not stub and args.pageable_frames > 0:
-        out["pcie_pageable"] = pageable_leg(local_rank, args.pageable_frames, threads)
+        out["pcie_pageable"] = pageable_leg(local_rank, args.pageable_frames, threads, use_graph=not args.no_graph)
     if world == 1 and not args.no_cpu and not stub:
         cb = cpu_baseline(args.cpu_seconds, args.warmup)
         f0, f1 = cb.pop("frames")

@@ -1331,6 +1331,7 @@ void pfref_odom_set_state(pfref_odom* h, const double odom_pose[7], const double
     h->o.last_odom.R = q2m(ql);
     h->o.last_odom.t = V3{last_pose[4], last_pose[5], last_pose[6]};
     for (int k = 0; k < 7; ++k) h->o.params[k] = odom_pose[k];
+    h->inited = true;                                   // the next frame runs updatePointsToMap
 }
 
 void pfref_odom_set_opt_count(pfref_odom* h, int n) { h->o.optimization_count = n; }

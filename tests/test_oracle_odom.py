@@ -92,3 +92,32 @@ def test_bpf_tracks_and_reduces_to_es_structure(pfref, pfsynth):
     for c, leaf in ((0, 0.4), (1, 0.4), (2, 0.8)):
         xyz, rg = od.get_map(c)
         assert xyz.shape[0] == st["n_map"][c] and (rg[:, 0] >= 2).all()
+
+
+def test_synced_parity_worker_reproduces_a_free_run(pfref, pfsynth):
+    """The synced parity test's worker (tests/_parity_worker.py) rebuilds a fresh oracle from a state
+    (maps with their r / g bytes, odom / last_odom poses, optimization_count) and runs one frame: fed
+    the states of a free-running faithful oracle it must give that oracle's next frame (to the 1e-16
+    the quaternion round trip of the state leaves), counts and map bytes identical."""
+    import _parity_worker as pw
+    from _util import pose_err
+    n = 14
+    lid, prm = (64, 3.0, 90.0), (0.4, 0, 0.4, 75, 0)
+    pw.init("S64", n, 0, lid, None, prm, 0)
+    seq = pfsynth.Sequence("S64", n_frames=n, seed=0)
+    orc = pfref.Odom(pfref.make_lidar(*lid), *prm, opts=0)
+    poses = [orc.frame(seq.frame(0))]
+    report = dict(frames=0, worst_t=0.0, worst_r=0.0, worst_xyz=0.0, xyz_bitexact_frames=0, pose_bad=[],
+                  count_bad=[], map_bad=[])
+    for k in range(1, n):
+        maps = [orc.get_map(0), orc.get_map(1)]
+        opt = 12 if k == 1 else max(2, 13 - k)
+        task = (k, maps, poses[k - 1], poses[max(k - 2, 0)], opt)
+        pose = orc.frame(seq.frame(k))
+        poses.append(pose)
+        st = orc.stats()
+        _, wp, wc, wm = pw.run(task)
+        pw.compare(k, (pose, {c: int(st[c]) for c in pw.COUNTS}, [orc.get_map(0), orc.get_map(1)]),
+                   (wp, wc, wm), report, 1e-12, 1e-12, pose_err, tol_xyz=1e-4)
+    assert report["frames"] == n - 1 and report["worst_xyz"] < 1e-4
+    assert not report["pose_bad"] and not report["count_bad"] and not report["map_bad"]
