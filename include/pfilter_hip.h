@@ -297,6 +297,12 @@ int pf_odom_set_map_export(pf_odom* h, int enable);
 int pf_odom_map_export(pf_odom* h, int which, const float** xyzw, size_t* n);
 /* enable/disable hipGraph replay of the steady-state frame (default on) */
 int pf_odom_set_graph(pf_odom* h, int enable);
+/* Reference tie order (default off): VoxelGrid (stage A) and rgbds (stage B) order the points of a
+ * voxel as libstdc++'s std::sort leaves them -- the reference's own sorts (PCL 1.10 VoxelGrid, SURVEY
+ * B.1; src/odomEstimationClass.cpp:74), which are not stable -- instead of in input order, so that every
+ * f32 centroid is summed in the reference's order. A parity mode: it runs introsort's recursion levels
+ * on the device (a few ms per frame); off, the sorts are stable radix sorts. */
+int pf_odom_set_tie_order(pf_odom* h, int enable);
 /* Per-stage device time (the reference's per-stage timers, src/laserProcessingNode.cpp:71-79 and
  * src/odomEstimationNode copy.cpp:92-100, as HIP events on the handle's two streams): with enable,
  * every frame records when stage A (featureExtraction / front end + VoxelGrid) and stage B (the

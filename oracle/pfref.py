@@ -21,8 +21,9 @@ GPU_EQUIV = FE_STABLE_TIES | VG_STABLE | LM_NORMAL_EQ
 
 
 def build(force=False):
-    srcs = [os.path.join(_HERE, f) for f in ("pfref_fe.cpp", "pfref_odom.cpp", "pfref.h", "pfref_internal.h",
-                                              "pfref_math.h")]
+    srcs = [os.path.join(_HERE, f) for f in ("pfref_fe.cpp", "pfref_odom.cpp", "pfref_cls.cpp", "pfref_map.cpp",
+                                              "pfref_dcvc.cpp", "pfref_sort.cpp", "pfref.h", "pfref_internal.h",
+                                              "pfref_math.h", "Makefile")]
     newest = max(os.path.getmtime(s) for s in srcs)
     if force or not os.path.exists(_LIB) or os.path.getmtime(_LIB) < newest:
         subprocess.check_call(["make", "-s", "-C", _HERE])
@@ -168,6 +169,9 @@ def lib():
         L.pfref_map_get.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
         L.pfref_bpf_preprocess.argtypes = [_vp, _sz, _sz, ctypes.POINTER(ClsParams)] + \
             [_vp, ctypes.POINTER(_sz)] * 4
+        L.pfref_std_sort_perm.argtypes = [_vp, _sz, _vp]
+        L.pfref_introsort_literal.argtypes = [_vp, _sz, ctypes.c_int, _vp]
+        L.pfref_introsort_levels.argtypes = [_vp, _sz, ctypes.c_int, _vp]
     return _lib
 
 
@@ -246,6 +250,21 @@ def knn(map_pts, queries, k=5, opts=0):
     if rc != 0:
         raise RuntimeError("pfref_knn failed")
     return idx, d2
+
+
+def sort_perm(keys, how="std", depth=-1):
+    """the permutation of (key, index) pairs sorted by key only: how = "std" (libstdc++ std::sort itself,
+    as PCL's VoxelGrid and rgbds call it), "literal" (its line-by-line restatement, depth limit
+    settable), "levels" (the level-synchronous form of the device's reference-tie-order mode)"""
+    k = np.ascontiguousarray(keys, np.uint32)
+    out = np.empty(max(k.size, 1), np.uint32)
+    if how == "std":
+        lib().pfref_std_sort_perm(k.ctypes.data, k.size, out.ctypes.data)
+    elif how == "literal":
+        lib().pfref_introsort_literal(k.ctypes.data, k.size, int(depth), out.ctypes.data)
+    else:
+        lib().pfref_introsort_levels(k.ctypes.data, k.size, int(depth), out.ctypes.data)
+    return out[:k.size].copy()
 
 
 def eigen_sym3(a6):

@@ -1101,6 +1101,79 @@ extern "C" int pf_dev_errors(pf_odom* h, int* out, int n) {
     return PF_OK;
 }
 
+int pf_odom_set_tie_order(pf_odom* h, int enable) {
+    if (!h) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    if (enable && !o.tie_a) {
+        o.tie_a = new (std::nothrow) TieSort();
+        o.tie_b = new (std::nothrow) TieSort();
+        if (!o.tie_a || !o.tie_b) return PF_ENOMEM;
+        if (int rc = tie_alloc(*o.tie_a, (size_t)o.cls.nc * o.in_cap)) return rc;
+        if (int rc = tie_alloc(*o.tie_b, o.sort_cap)) return rc;
+    }
+    if ((enable != 0) != o.tie_order)
+        for (int s = 0; s < kSlots; ++s) {          // both stages' captured kernel sequences change
+            for (hipGraphExec_t* g : {&o.graph_a[s], &o.graph_b[s], &o.graph_as[s]})
+                if (*g) {
+                    (void)hipGraphExecDestroy(*g);
+                    *g = nullptr;
+                }
+        }
+    o.tie_order = enable != 0;
+    return PF_OK;
+}
+
+// development / test probe (not part of include/pfilter_hip.h): the reference-tie-order sort alone on
+// n host keys (bits 30-31 the class, 0xFFFFFFFF dropped); perm receives the vals (input indices) of the
+// kept pairs in std::sort's order, *n_out their count
+extern "C" int pf_dev_tie_sort(int device, const uint32_t* keys, size_t n, uint32_t* perm, size_t* n_out) {
+    if ((!keys && n) || !perm || !n_out || n > (size_t)INT_MAX / 2) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(device));
+    const size_t cap = n ? n : 1;
+    TieSort t;
+    PrimWork w;
+    u32 *dk = nullptr, *dv = nullptr;
+    int* dn = nullptr;
+    hipStream_t s = nullptr;
+    int rc = tie_alloc(t, cap);
+    if (!rc) rc = prim_alloc(w, cap);
+    if (!rc && (hipMalloc(&dk, sizeof(u32) * cap) != hipSuccess || hipMalloc(&dv, sizeof(u32) * cap) != hipSuccess ||
+                hipMalloc(&dn, sizeof(int)) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess))
+        rc = PF_ENOMEM;
+    std::vector<u32> iota(cap);
+    for (size_t i = 0; i < cap; ++i) iota[i] = (u32)i;
+    const int ni = (int)n;
+    if (!rc && (hipMemcpyAsync(dk, keys, sizeof(u32) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+                hipMemcpyAsync(dv, iota.data(), sizeof(u32) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+                hipMemcpyAsync(dn, &ni, sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess))
+        rc = PF_EHIP;
+    if (!rc) {
+        tie_sort_enqueue(t, dk, dv, dn, w, s);
+        tie_sort_finish(t, dk, dv, s);
+        int cnt[8];
+        if (hipMemcpyAsync(cnt, t.cnt, sizeof(cnt), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            rc = PF_EHIP;
+        else {
+            *n_out = (size_t)(u32)cnt[5];
+            if (*n_out && (hipMemcpy(perm, dv, sizeof(u32) * *n_out, hipMemcpyDeviceToHost) != hipSuccess)) rc = PF_EHIP;
+        }
+        int err = 0;
+        if (!rc && hipMemcpy(&err, w.err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess && err) rc = PF_EHIP;
+    }
+    if (s) (void)hipStreamSynchronize(s);
+    (void)hipFree(dk);
+    (void)hipFree(dv);
+    (void)hipFree(dn);
+    if (s) (void)hipStreamDestroy(s);
+    tie_free(t);
+    prim_free(w);
+    return rc;
+}
+
 int pf_odom_set_graph(pf_odom* h, int enable) {
     if (!h) return PF_EINVAL;
     h->o.graph_enabled = enable != 0;

@@ -6,6 +6,7 @@
 #include "pf_fe.h"
 #include "pf_knn.h"
 #include "pf_prims.h"
+#include "pf_tie.h"
 
 namespace pf {
 
@@ -208,6 +209,11 @@ struct OdomGPU {
 
     bool graph_enabled = true;
     int cu_reserve = 0;            // CUs stage A stays off (odom_stage_a_stream)
+    // reference tie order (pf_odom_set_tie_order, pf_tie.h): VoxelGrid (stage A) and rgbds (stage B)
+    // order equal keys as libstdc++'s std::sort does; each stage has its own scratch
+    bool tie_order = false;
+    TieSort* tie_a = nullptr;
+    TieSort* tie_b = nullptr;
 };
 
 // Stage A keeps off the last CUs of the device by default: with one sequence per GPU, stage B's LM

@@ -1888,6 +1888,11 @@ void odom_destroy(OdomGPU& o) {
     if (o.h_map_n) (void)hipHostFree(o.h_map_n);
     if (o.stream) (void)hipStreamDestroy(o.stream);
     if (o.stream_a) (void)hipStreamDestroy(o.stream_a);
+    for (TieSort* t : {o.tie_a, o.tie_b})
+        if (t) {
+            tie_free(*t);
+            delete t;
+        }
     o = OdomGPU{};
 }
 
@@ -1916,7 +1921,9 @@ void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s) {
     PF_LAUNCH_NC(nc, k_vg_minmax, dim3(128), dim3(256), 0, s, clouds(sb.in), cnt, o.acc_a);
     PF_LAUNCH_NC(nc, k_vg_keys, dim3(kGrid), dim3(256), 0, s, clouds(sb.in), cnt, o.acc_a, leaf, o.vkeys, o.vvals,
                  sort_hist(o.vprim, 32, true));
+    if (o.tie_order) tie_sort_enqueue(*o.tie_a, o.vkeys, o.vvals, cnt + C_VGN, o.vprim, s);
     radix_sort_pairs(o.vkeys, o.vvals, cnt + C_VGN, 32, o.vprim, s, nullptr, nullptr, true);
+    if (o.tie_order) tie_sort_finish(*o.tie_a, o.vkeys, o.vvals, s);      // std::sort's order of equal keys
     segment_starts(o.vkeys, cnt + C_VGN, o.vsegstart, cnt + C_NSEG, cnt + C_NLT, cnt + C_NRG_VALID, o.vprim, s);
     PF_LAUNCH_NC(nc, k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, clouds(sb.in), o.vkeys, o.vvals, o.vsegstart, cnt,
                  clouds_w(sb.ds));
@@ -1979,7 +1986,9 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
         PF_LAUNCH_NC(nc, k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map), clouds(o.app),
                      leaf, o.keys, o.vals, sort_hist(o.prim, 32, true));
     }
+    if (o.tie_order) tie_sort_enqueue(*o.tie_b, o.keys, o.vals, cnt + C_NRG, o.prim, s);
     radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
+    if (o.tie_order) tie_sort_finish(*o.tie_b, o.keys, o.vals, s);        // std::sort's order (:74)
     RgTailArgs ta{cnt, clouds(o.map), clouds(o.app), o.keys, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,
                   o.prm.theta_max, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err};
     const unsigned tail_grid = (unsigned)(o.tail_tiles < (size_t)kSortMaxBlocks ? o.tail_tiles : kSortMaxBlocks);

@@ -138,7 +138,7 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_odom_restore", "pf_odom_set_map_export", "pf_odom_map_export", "pf_odom_set_stage_timing",
            "pf_odom_stage_times", "pf_odom_set_state", "pf_cls_normals", "pf_dcvc_default_params",
            "pf_dcvc_create", "pf_dcvc_destroy", "pf_dcvc_run", "pf_dcvc_reset", "pf_cls_set_dcvc", "pf_bpf_set_dcvc",
-           "pf_host_alloc", "pf_host_free"]
+           "pf_host_alloc", "pf_host_free", "pf_odom_set_tie_order"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -196,6 +196,8 @@ def lib():
     L.pf_dev_free.argtypes = [_i, _vp]
     L.pf_memcpy_h2d.argtypes = [_i, _vp, _vp, _sz]
     L.pf_memcpy_d2h.argtypes = [_i, _vp, _vp, _sz]
+    L.pf_odom_set_tie_order.argtypes = [_vp, _i]
+    L.pf_dev_tie_sort.argtypes = [_i, _vp, _sz, _vp, ctypes.POINTER(_sz)]
     L.pf_host_alloc.argtypes = [_sz, ctypes.POINTER(_vp)]
     L.pf_host_free.argtypes = [_vp]
     L.pf_knn_create.argtypes = [_i, _sz, _sz, ctypes.POINTER(_vp)]
@@ -258,6 +260,17 @@ def make_lidar(num_lines=64, min_dist=3.0, max_dist=90.0, scan_period=0.1, ring_
     lp = LidarParams(int(num_lines), float(min_dist), float(max_dist), float(scan_period))
     lp.ring_model = tuple(ring_model) if ring_model else None
     return lp
+
+
+def tie_sort(keys, device=0):
+    """development probe pf_dev_tie_sort: the input indices of the kept keys (not 0xFFFFFFFF) in the
+    order the device's reference-tie-order sort (libstdc++ std::sort per class, bits 30-31) puts them"""
+    k = np.ascontiguousarray(keys, np.uint32)
+    out = np.empty(max(k.size, 1), np.uint32)
+    n = _sz()
+    _check("pf_dev_tie_sort", lib().pf_dev_tie_sort(device, k.ctypes.data, k.size, out.ctypes.data, ctypes.byref(n)),
+           allow_warn=False)
+    return out[:n.value].copy()
 
 
 def device_count():
@@ -503,6 +516,10 @@ class Odom_ES_EstimationClass:
     def restore(self, blob):
         buf = ctypes.create_string_buffer(bytes(blob), len(blob))
         _check("pf_odom_restore", lib().pf_odom_restore(self._h, buf, len(blob)))
+
+    def set_tie_order(self, enable):
+        """pf_odom_set_tie_order: VoxelGrid / rgbds order equal keys as libstdc++ std::sort (parity mode)"""
+        _check("pf_odom_set_tie_order", lib().pf_odom_set_tie_order(self._h, int(bool(enable))), allow_warn=False)
 
     def set_map_export(self, enable):
         _check("pf_odom_set_map_export", lib().pf_odom_set_map_export(self._h, int(bool(enable))))

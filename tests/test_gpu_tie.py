@@ -1,0 +1,49 @@
+"""GPU: the reference-tie-order sort (pf_tie.h, pf_odom_set_tie_order) against libstdc++'s std::sort
+itself -- the reference's own VoxelGrid / rgbds sort (src/odomEstimationClass.cpp:74),
+which leaves equal keys in an order only introsort defines. The device's permutation of the input
+indices must be std::sort's exactly, per class (key bits 30-31), with 0xFFFFFFFF keys dropped."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs():
+    rng = np.random.default_rng(21)
+    yield np.zeros(0, np.uint32)
+    yield np.array([3], np.uint32)
+    for n in (2, 16, 17, 18, 100, 5000, 65000):
+        yield rng.integers(0, max(2, n // 7), n).astype(np.uint32)
+        yield rng.integers(0, 1 << 30, n).astype(np.uint32)
+        yield np.sort(rng.integers(0, 50, n)).astype(np.uint32)
+        yield np.sort(rng.integers(0, 50, n))[::-1].astype(np.uint32).copy()
+        yield np.full(n, 9, np.uint32)
+    k = np.sort(rng.integers(0, 40000, 60000)).astype(np.uint32)            # voxel-ordered map + new points
+    yield np.concatenate([k, rng.integers(0, 40000, 6000).astype(np.uint32)])
+
+
+def _expected(pfref, keys):
+    out = []
+    for c in range(4):
+        idx = np.nonzero((keys != 0xFFFFFFFF) & ((keys >> 30) == c))[0]
+        out.append(idx[pfref.sort_perm(keys[idx], "std")])
+    return np.concatenate(out).astype(np.uint32) if out else np.zeros(0, np.uint32)
+
+
+def test_tie_sort_is_std_sort(pa, pfref):
+    for keys in _inputs():
+        np.testing.assert_array_equal(pa.tie_sort(keys), _expected(pfref, keys), err_msg="n=%d" % keys.size)
+
+
+def test_tie_sort_classes_and_dropped_keys(pa, pfref):
+    """rgbds / VoxelGrid batches: several classes back to back (the reference sorts each cloud on its
+    own), cropped points (0xFFFFFFFF) interleaved and dropped, map-like tie-heavy keys."""
+    rng = np.random.default_rng(22)
+    for sizes in ((30000, 9000), (7000, 52000), (500, 800, 1200), (20, 5, 40000)):
+        parts = []
+        for c, n in enumerate(sizes):
+            k = (rng.integers(0, max(2, n // 4), n).astype(np.uint32) & 0x3FFFFFFF) | np.uint32(c << 30)
+            k[rng.random(n) < 0.05] = 0xFFFFFFFF
+            parts.append(k)
+        keys = np.concatenate(parts)
+        np.testing.assert_array_equal(pa.tie_sort(keys), _expected(pfref, keys))

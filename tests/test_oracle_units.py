@@ -270,3 +270,41 @@ def test_knn_cellpop_matches_numpy(pfref):
     for c in cq:
         want += int(np.all(np.abs(cm - c) <= 1, axis=1).sum())
     assert pfref.knn_cellpop(mp, q) == want
+
+
+def _sort_inputs():
+    rng = np.random.default_rng(11)
+    yield np.zeros(0, np.uint32)
+    yield np.array([5], np.uint32)
+    for n in (2, 3, 15, 16, 17, 18, 33, 100, 1000, 20000):
+        yield rng.integers(0, max(2, n // 7), n).astype(np.uint32)         # many ties (voxels)
+        yield rng.integers(0, 1 << 30, n).astype(np.uint32)                # few ties
+        yield np.sort(rng.integers(0, 50, n)).astype(np.uint32)            # sorted runs
+        yield np.sort(rng.integers(0, 50, n))[::-1].astype(np.uint32).copy()
+        yield np.full(n, 7, np.uint32)
+    k = np.sort(rng.integers(0, 20000, 30000)).astype(np.uint32)           # a voxel-ordered map + a tail
+    yield np.concatenate([k, rng.integers(0, 20000, 3000).astype(np.uint32)])
+    n = 4096                                                               # organ pipe
+    yield np.concatenate([np.arange(n // 2), np.arange(n // 2)[::-1]]).astype(np.uint32)
+
+
+def test_introsort_restatements_equal_std_sort(pfref):
+    """libstdc++ std::sort (the reference's VoxelGrid / rgbds sort, src/odomEstimationClass.cpp:74)
+    leaves equal keys in an order only its algorithm defines. The literal restatement of its introsort
+    and the level-synchronous form the device's reference-tie-order mode runs give exactly its
+    permutation on tie-heavy, sorted, reversed, constant and map-like inputs."""
+    for keys in _sort_inputs():
+        want = pfref.sort_perm(keys, "std")
+        np.testing.assert_array_equal(pfref.sort_perm(keys, "literal"), want)
+        np.testing.assert_array_equal(pfref.sort_perm(keys, "levels"), want)
+        assert np.all(np.diff(keys[want].astype(np.int64)) >= 0)
+
+
+def test_introsort_levels_heap_branch(pfref):
+    """The depth-limit branch (make_heap + sort_heap) of both restatements agrees at every small depth
+    limit, where most segments end in it."""
+    rng = np.random.default_rng(12)
+    for n in (17, 40, 300, 5000):
+        keys = rng.integers(0, max(2, n // 5), n).astype(np.uint32)
+        for depth in (0, 1, 2, 3, 5):
+            np.testing.assert_array_equal(pfref.sort_perm(keys, "levels", depth), pfref.sort_perm(keys, "literal", depth))
