@@ -15,6 +15,8 @@
 //   LaserMappingClass::init / updateCurrentPointsToMap / getMap          include/laserMappingClass.h:23-29
 //   nongroundExtract::featureInit / pc2pc / featureExtract, members
 //       cloud_pillar, cloud_beam, cloud_facade, index_with_feature, thresholds   :616-735
+//   curvedVoxel::run, members pointCloudPtr, pointCloudSegPtr, labelRecords,
+//       startR / deltaR / deltaP / deltaA / minSeg, sensorMinRange / MaxRange    include/additionClass.hpp:3-120
 //
 // The classes are templates over the point-cloud and lidar types so this header needs neither PCL nor
 // ROS; shim/laserProcessingClass.h and shim/odomEstimationClass.h instantiate them with the PCL 1.10
@@ -34,6 +36,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -667,6 +670,107 @@ private:
     size_t max_points_, max_scan_;
     pf_map* h_ = nullptr;
     std::vector<float> buf_;
+};
+
+// curvedVoxel (include/additionClass.hpp:3-120, src/additionClass.cpp:457-497): the DCVC clustering of
+// additionNode's `curvedfilter` stage on the device (pf_dcvc_run). run() leaves in pointCloudSegPtr
+// the points of the clusters larger than minSeg, cluster by cluster from the largest (ties: first
+// point), each cluster's points in input order, and in labelRecords {rank, {size, input indices}} per
+// kept cluster (labelAnalysis, :319-356). The reference fills pointCloudSegPtr from several OpenMP
+// threads at once (colorSegmentation, :364-416), so its order is not defined; DESIGN.md §2 gives the
+// statistical bar against its serial reading. The parameters are the members, as init() reads them
+// from the yaml file (:17-52); the device handle is shared by copies of the object (the node binds
+// the object by value, src/additionNode.cpp:88-89), and its first run starts the range rings at 5 m
+// (minPolar's member default, .hpp:105), later runs at 0 (resetParams, :442-455).
+template <class Cloud>
+class CurvedVoxelT {
+public:
+    using Ptr = typename Cloud::Ptr;
+    using Point = typename std::decay<decltype(std::declval<Cloud>().points[0])>::type;
+    struct segInfo {                                                 // .hpp:69-73
+        int clusterNum{-1};
+        std::vector<int> index{};
+    };
+    explicit CurvedVoxelT(int device = 0, size_t max_points = 300000)
+        : st_(std::make_shared<State>(device, max_points)) {}
+
+    // :457-497 without the ROS publishing (the ROS layer adds init / colorSegmentation / publishData)
+    bool run(Ptr& inputCloud) {
+        static_assert(std::is_standard_layout<Point>::value, "point type must be standard layout");
+        pointCloudPtr = inputCloud;
+        labelRecords.clear();
+        pointCloudSegPtr = Ptr(new Cloud());
+        const size_t n = pointCloudPtr ? pointCloudPtr->points.size() : 0;
+        if (n == 0) {
+            std::printf("not enough point to convert\n");                    // :461-463 (ROS_ERROR)
+            return false;
+        }
+        pf_dcvc* h = st_->get(params(), n);
+        idx_.resize(n);
+        lab_.resize(n);
+        size_t nk = 0;
+        check("pf_dcvc_run", pf_dcvc_run(h, &pointCloudPtr->points[0].x, n, sizeof(Point), idx_.data(), &nk,
+                                         lab_.data(), n));
+        pointCloudSegPtr->points.reserve(nk);
+        for (size_t j = 0; j < nk; ++j) {
+            const int i = idx_[j];
+            const int r = lab_[(size_t)i];
+            pointCloudSegPtr->push_back(pointCloudPtr->points[(size_t)i]);
+            if (labelRecords.empty() || labelRecords.back().first != r) labelRecords.emplace_back(r, segInfo{0, {}});
+            labelRecords.back().second.clusterNum++;
+            labelRecords.back().second.index.push_back(i);
+        }
+        return true;
+    }
+    // per input point of the last run: its cluster's rank (1 = largest) or 0 when dropped
+    const std::vector<int32_t>& labels() const { return lab_; }
+
+    // members (include/additionClass.hpp:73-115), defaults of config/config.yaml:7-8, 49-54
+    Ptr pointCloudPtr, pointCloudSegPtr;
+    std::vector<std::pair<int, segInfo>> labelRecords;
+    double sensorMinRange{1.0}, sensorMaxRange{120.0};
+    double startR{1.0}, deltaR{0.003}, deltaP{1.2}, deltaA{1.2};
+    int minSeg{80};
+
+private:
+    pf_dcvc_params params() const {
+        pf_dcvc_params p;
+        pf_dcvc_default_params(&p);
+        p.start_r = startR;
+        p.delta_r = deltaR;
+        p.delta_p = deltaP;
+        p.delta_a = deltaA;
+        p.min_seg = minSeg;
+        p.min_range = sensorMinRange;
+        p.max_range = sensorMaxRange;
+        return p;
+    }
+    // the device handle, re-created (a first run again) when the parameters or the capacity change
+    struct State {
+        State(int device, size_t max_points) : device(device), max_points(max_points) {}
+        ~State() {
+            if (h) pf_dcvc_destroy(h);
+        }
+        pf_dcvc* get(const pf_dcvc_params& p, size_t n) {
+            const bool same = p.start_r == prm.start_r && p.delta_r == prm.delta_r && p.delta_p == prm.delta_p &&
+                              p.delta_a == prm.delta_a && p.min_seg == prm.min_seg && p.min_range == prm.min_range &&
+                              p.max_range == prm.max_range;
+            if (!h || !same || n > cap) {
+                if (h) pf_dcvc_destroy(h);
+                h = nullptr;
+                cap = n > max_points ? n : max_points;
+                check("pf_dcvc_create", pf_dcvc_create(&p, device, cap, &h));
+                prm = p;
+            }
+            return h;
+        }
+        int device;
+        size_t max_points, cap = 0;
+        pf_dcvc_params prm{};
+        pf_dcvc* h = nullptr;
+    };
+    std::shared_ptr<State> st_;
+    std::vector<int32_t> idx_, lab_;
 };
 
 }  // namespace pfilter_hip

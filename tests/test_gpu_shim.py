@@ -145,3 +145,41 @@ def test_mapping_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
     subprocess.check_call([exe, str(tmp_path / "frames.bin"), str(tmp_path / "map.bin")], timeout=120)
     got = np.fromfile(tmp_path / "map.bin", np.float32).reshape(-1, 4)
     np.testing.assert_array_equal(got, m.getMap())
+
+
+def test_curved_voxel_shim_matches_c_abi(pa, pfsynth, tmp_path):
+    """curvedVoxel drop-in (pfilter_hip::CurvedVoxelT, the class shim/additionClass.hpp gives
+    additionNode.cpp) driven per frame like src/additionNode.cpp:29-39: pointCloudSegPtr and labelRecords
+    equal pf_dcvc_run's kept points and cluster ranks bit for bit, the first frame included (rings from
+    5 m, then from 0, through the device handle the object's copies share)."""
+    exe = str(tmp_path / "shim_dcvc_driver")
+    lib = os.path.join(ROOT, "pfilter-noetic_amd")
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "shim", "shim_dcvc_driver.cpp"), "-o", exe, "-L", lib,
+                           "-lpfilter_hip", "-Wl,-rpath," + lib, "-Wl,-rpath-link,/opt/rocm/lib"])
+    seq = pfsynth.Sequence("S64", n_frames=4, az_steps=1500)
+    frames = [seq.frame(k) for k in range(4)]
+    with open(tmp_path / "frames.bin", "wb") as f:
+        for x in frames:
+            np.array([x.shape[0]], np.int64).tofile(f)
+            x.astype(np.float32).tofile(f)
+    subprocess.check_call([exe, str(tmp_path / "frames.bin"), str(tmp_path / "out.bin")], timeout=120)
+    raw = open(tmp_path / "out.bin", "rb").read()
+    dc = pa.Dcvc(max_points=300000)
+    off = 0
+    for x in frames:
+        idx, lab = dc.run(x[:, :3])
+        nk, nc = np.frombuffer(raw, np.int64, 2, off)
+        off += 16
+        xyz = np.frombuffer(raw, np.float32, 3 * nk, off).reshape(-1, 3)
+        off += 12 * nk
+        rec = np.frombuffer(raw, np.int32, 3 * nc, off).reshape(-1, 3)
+        off += 12 * nc
+        assert nk == idx.size and nk > 1000
+        np.testing.assert_array_equal(xyz.view(np.uint32), x[idx, :3].view(np.uint32))
+        ranks, sizes = np.unique(lab[lab > 0], return_counts=True)
+        np.testing.assert_array_equal(rec[:, 0], ranks)
+        np.testing.assert_array_equal(rec[:, 1], sizes)
+        starts = np.cumsum(np.r_[0, sizes[:-1]])
+        np.testing.assert_array_equal(rec[:, 2], idx[starts])
+    assert off == len(raw)

@@ -9,7 +9,8 @@ mkdir -p $OUT/parity
 cd $R
 export PF_PARITY_OUT=$OUT/parity
 K=${1:-synced}
-timeout -k 10 1100 python -u -m pytest tests/test_gpu_parity_synced.py -m gpu -k "$K" -v -s -p no:cacheprovider \
+T=${2:-tests/test_gpu_parity_synced.py}
+timeout -k 10 1100 python -u -m pytest $T -m gpu -k "$K" -v -s -p no:cacheprovider \
     --timeout 900 --timeout-method thread > $OUT/parity_tests.log 2>&1
 rc=$?
 grep -E "PASSED|FAILED|passed|failed|frame [0-9]+,|Error" $OUT/parity_tests.log | tail -n 40
