@@ -52,6 +52,7 @@ def test_header_compiles_as_c():
 def test_cpp_shim_compiles():
     """The header-only C++ drop-in (pfilter-noetic_amd/shim) compiles against PCL-shaped types."""
     import subprocess
-    for drv in ("shim_driver.cpp", "shim_bpf_driver.cpp", "shim_cls_driver.cpp", "shim_map_driver.cpp"):   # ES + LaserProcessing, BPF, front end
+    for drv in ("shim_driver.cpp", "shim_bpf_driver.cpp", "shim_cls_driver.cpp", "shim_map_driver.cpp",
+                "shim_dcvc_driver.cpp"):   # ES + LaserProcessing, BPF, front end, global map, curvedVoxel
         subprocess.check_call(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", "-I",
                                os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "shim", drv)])
