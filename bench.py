@@ -73,6 +73,8 @@ def parse(argv=None):
                          "pf_odom_frame_host; reported as pcie_inclusive, never as value)")
     ap.add_argument("--pageable-frames", type=int, default=500,
                     help="frames of pf_odom_frame_host from pageable memory (pcie_pageable); 0 = skip")
+    ap.add_argument("--configs4-frames", type=int, default=100,
+                    help="frames of the configs[4] pipeline leg (S128 scans, 2M-point map); 0 = skip")
     ap.add_argument("--node-frames", type=int, default=1000,
                     help="frames of the node call pattern (pf_fe_extract -> pf_odom_update); 0 = skip")
     return ap.parse_args(argv)
@@ -507,6 +509,82 @@ def node_pattern_leg(device, hptrs, warmup, nframes):
                     "pinned host RAM; frames %d..%d of the headline sequence" % (warmup, total - 1)}
 
 
+def configs4_leg(device, nframes, threads, warmup=3, timing_frames=20, use_graph=True):
+    """BASELINE.json configs[4] as a pipeline: synthetic 128-line scans (~200k points; the reference has
+    no 128-line ring formula, so the linear beam-model extension pf_odom_set_ring_model(15, -25) bins
+    them) against a 2,000,000-point surf map (pfsynth.voxel_map: voxel centroids
+    of the dense block at the 0.8 m surf leaf) seeded by pf_odom_set_map after frame 0; FLOAM
+    parameters (theta 0: no stability filter, the map keeps its size), scans HBM-resident, graph replay.
+    Then the association's kNN alone on the last frame (pf_odom_probe_assoc: the exact 5-NN of k_assoc
+    against the 2M-point grid, HIP events, algorithmic bytes per SURVEY 8(d)) and, for comparison, the
+    standalone thick-row kNN (k_knn_thick) on the same surf map and the same surf queries."""
+    import pfilter_amd as pa
+    import pfsynth
+    total = 1 + warmup + nframes + timing_frames
+    seq = pfsynth.Sequence("S128", n_frames=total)
+    bufs, ptrs = [], []
+    for f0 in range(0, total, 64):
+        nf = min(64, total - f0)
+        buf, counts = seq.frames(f0, nf, threads=threads)
+        db = pa.DeviceBuffer(buf.nbytes, device=device)
+        db.upload(buf)
+        ptrs += [(db.ptr + i * buf.shape[1] * 16, int(counts[i])) for i in range(nf)]
+        bufs.append(db)
+        del buf
+    lid = pa.make_lidar(128, 3.0, 90.0, 0.1, ring_model=(15.0, -25.0))
+    od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
+    od.init(lid, 0.4, 0, 0.0, 0, 0)
+    od.set_graph(use_graph)
+    od.frame_device(*ptrs[0])
+    od.sync()
+    m = pfsynth.voxel_map(2_000_000, 0.8, seed=5)
+    od.set_map(1, m, np.zeros((m.shape[0], 2), np.uint8))
+    for k in range(1, 1 + warmup):
+        od.frame_device(*ptrs[k])
+    od.sync()
+    t0 = time.perf_counter()
+    for k in range(1 + warmup, 1 + warmup + nframes):
+        od.frame_device(*ptrs[k])
+    od.sync()
+    el = time.perf_counter() - t0
+    st = od.stats()
+    assert st["errors"] == 0
+    od.set_stage_timing(True)
+    for k in range(1 + warmup + nframes, total):
+        od.frame_device(*ptrs[k])
+    stg = od.stage_times()
+    od.set_stage_timing(False)
+    ms, alg, nq, q = od.probe_assoc(iters=20, queries=True)
+    out = {"value": round(nframes / el, 2), "unit": "frames/s", "frames": nframes,
+           "ms_per_step": round(el / nframes * 1e3, 4),
+           "workload": "configs[4]: S128 synthetic 128-line scans (linear beam model 15..-25 deg), 2,000,000-point "
+                       "surf map seeded after frame 0, k_new 0 theta_p 0 theta_max 0, weightType 0, map_res 0.4",
+           "mean_points_per_frame": round(float(np.mean([n for _, n in ptrs])), 1),
+           "stage_us": {"A_features_voxelgrid": round(stg["a_us"], 1), "B_odometry": round(stg["b_us"], 1),
+                        "frames": stg["frames"]},
+           "last_frame": {k: st[k] for k in ("n_in", "n_ds", "n_map", "n_res")}}
+    ach = alg / (ms * 1e-3) / 1e9
+    out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                       "kernel": "k_assoc's exact 5-NN (knn5_team on the 1 m grid of the frame's maps), "
+                                 "pf_odom_probe_assoc on the last frame",
+                       "queries": nq, "alg_bytes_per_launch": alg, "avg_kernel_ms": round(ms, 5)}
+    surf = q[q[:, 3].view(np.int32) == 1]
+    mxyz = od._map(1)[0]
+    if surf.shape[0] and mxyz.shape[0]:
+        kn = pa.Knn(mxyz.shape[0], surf.shape[0], device=device)
+        kn.set_map(np.c_[mxyz, np.zeros(mxyz.shape[0], np.float32)])
+        kn.query(np.c_[surf[:, :3], np.zeros(surf.shape[0], np.float32)])
+        tms, talg = kn.bench(20)
+        out["thick_knn_same_queries"] = {"avg_kernel_ms": round(tms, 5), "alg_bytes_per_launch": talg,
+                                         "frac": round(talg / (tms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                         "queries": int(surf.shape[0]), "map_points": int(mxyz.shape[0]),
+                                         "kernel": "k_knn_thick (standalone pf_knn, thick-row layout)"}
+    for db in bufs:
+        db.free()
+    return out
+
+
 def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True, use_graph=True, dcvc=False):
     """The BPF chain frames/s on the same S64 sequence with configs[1]'s odometry parameters: raw scan ->
     groundSeg::ground_seg + nongroundExtract::featureExtract (include/preProcess.hpp:398-505, 646-689) ->
@@ -884,6 +962,13 @@ def main(argv=None):
         nd["poses_equal_headline"] = bool(np.array_equal(npo, r["poses"][:npo.shape[0]]))
         out["node_pattern"] = nd
         log("node_pattern: %s" % nd)
+    if world == 1 and not stub and args.configs4_frames > 0:
+        try:
+            out["configs4"] = configs4_leg(local_rank, args.configs4_frames, threads, use_graph=not args.no_graph)
+            log("configs4: %s" % out["configs4"])
+        except Exception as e:  # report, never hide
+            log("configs4 leg failed: %r" % (e,))
+            out["configs4"] = None
     if world == 1 and not stub and args.pageable_frames > 0:
         out["pcie_pageable"] = pageable_leg(local_rank, args.pageable_frames, threads, use_graph=not args.no_graph)
     if world == 1 and not args.no_cpu and not stub:

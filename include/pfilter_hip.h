@@ -303,6 +303,14 @@ int pf_odom_set_graph(pf_odom* h, int enable);
  * f32 centroid is summed in the reference's order. A parity mode: it runs introsort's recursion levels
  * on the device (a few ms per frame); off, the sorts are stable radix sorts. */
 int pf_odom_set_tie_order(pf_odom* h, int enable);
+/* Measurement: the association's kNN alone (the exact 5-NN of k_assoc, src/odomEstimationClass.cpp:299,
+ * 447) on the last frame's queries -- its down-sampled points through the solved pose -- against the
+ * grid that frame searched, `iters` launches timed with HIP events on the handle's stream. avg_ms: per
+ * launch; alg_bytes: SURVEY 8(d)'s algorithmic bytes of those queries (16 + 40 + 27 x 8 + 16 |C(q)| each);
+ * nq: the query count; queries (optional, 4 floats each: x, y, z, bits(class)) when cap >= nq. The
+ * estimator's state is not changed. PF_EINVAL before the second frame. */
+int pf_odom_probe_assoc(pf_odom* h, int iters, double* avg_ms, double* alg_bytes, size_t* nq, float* queries,
+                        size_t cap);
 /* Per-stage device time (the reference's per-stage timers, src/laserProcessingNode.cpp:71-79 and
  * src/odomEstimationNode copy.cpp:92-100, as HIP events on the handle's two streams): with enable,
  * every frame records when stage A (featureExtraction / front end + VoxelGrid) and stage B (the

@@ -1174,6 +1174,16 @@ extern "C" int pf_dev_tie_sort(int device, const uint32_t* keys, size_t n, uint3
     return rc;
 }
 
+int pf_odom_probe_assoc(pf_odom* h, int iters, double* avg_ms, double* alg_bytes, size_t* nq, float* queries,
+                        size_t cap) {
+    if (!h || !avg_ms || !alg_bytes || !nq) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->o.device));
+    int n = 0;
+    const int rc = odom_probe_assoc(h->o, iters, avg_ms, alg_bytes, &n, reinterpret_cast<float4*>(queries), cap);
+    *nq = (size_t)(n > 0 ? n : 0);
+    return rc;
+}
+
 int pf_odom_set_graph(pf_odom* h, int enable) {
     if (!h) return PF_EINVAL;
     h->o.graph_enabled = enable != 0;

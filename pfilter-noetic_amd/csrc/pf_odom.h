@@ -242,5 +242,7 @@ void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s);
 void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s);
 // stage B tail when map export is on: the maps and their sizes into the mapped pinned buffers
 void odom_enqueue_export(OdomGPU& o, hipStream_t s);
+// k_assoc's kNN alone, `iters` times, on the last frame's queries and grid (pf_odom_probe_assoc)
+int odom_probe_assoc(OdomGPU& o, int iters, double* avg_ms, double* alg_bytes, int* nq, float4* q_host, size_t q_cap);
 
 }  // namespace pf

@@ -507,6 +507,80 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     else assoc_queries<NC, 8>(a, qi, nq, prm);
 }
 
+// ---- association kNN probe (pf_odom_probe_assoc): k_assoc's kNN alone on the last frame ---------
+// The queries of the last frame (its down-sampled points through the solved pose), the same grid and
+// the same team search as k_assoc, neighbours into scratch: nothing of the estimator's state changes.
+template <int NC, int T>
+__device__ __forceinline__ void assoc_probe(const DevState* __restrict__ st, const int* __restrict__ cnt, GridView gv,
+                                            Clouds ds, int* __restrict__ nbr, float4* __restrict__ qout) {
+    const CatIdx<NC> qi = cat_idx<NC>(cnt + C_DS);
+    const int nq = cnt[C_NQ];
+    double prm[7];
+    for (int k = 0; k < 7; ++k) prm[k] = st->params[k];
+    const int tl = lane_id() & (T - 1);
+    const int teams = gridDim.x * (blockDim.x / T);
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int team = gt / T, wave_team0 = (gt & ~63) / T;
+    for (int off = 0; wave_team0 + off < nq; off += teams) {
+        const int q0 = team + off;
+        const bool active = q0 < nq;
+        const int c = active ? qi.cls(q0) : 0;
+        float4 pw = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (active) pw = associate(prm, ds.at(c)[q0 - qi.start(c)]);
+        float d[5];
+        int id[5];
+        const int found = knn5_team<T>(gv, c, pw.x, pw.y, pw.z, active, d, id);
+        if (active && tl == 0) {
+            nbr[q0] = found == 5 ? id[4] : -1;
+            if (qout) qout[q0] = make_float4(pw.x, pw.y, pw.z, __int_as_float(c));
+        }
+    }
+}
+
+template <int NC>
+__global__ void __launch_bounds__(256) k_assoc_probe_t16(const DevState* st, const int* cnt, GridView gv, Clouds ds,
+                                                          int* nbr, float4* qout) {
+    assoc_probe<NC, 16>(st, cnt, gv, ds, nbr, qout);
+}
+template <int NC>
+__global__ void __launch_bounds__(256) k_assoc_probe_t8(const DevState* st, const int* cnt, GridView gv, Clouds ds,
+                                                         int* nbr, float4* qout) {
+    assoc_probe<NC, 8>(st, cnt, gv, ds, nbr, qout);
+}
+
+// SURVEY 8(d)'s algorithmic bytes of those queries: 16 + 40 + 27 x 8 + 16 |C(q)| each, |C(q)| = the
+// map points in the 27 cells of the query's class grid around its cell
+template <int NC>
+__global__ void __launch_bounds__(256) k_assoc_cellpop(const DevState* __restrict__ st, const int* __restrict__ cnt,
+                                                        GridView gv, Clouds ds, unsigned long long* __restrict__ out) {
+    const CatIdx<NC> qi = cat_idx<NC>(cnt + C_DS);
+    const int nq = cnt[C_NQ];
+    double prm[7];
+    for (int k = 0; k < 7; ++k) prm[k] = st->params[k];
+    unsigned long long acc = 0;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+        const int c = qi.cls(q);
+        const float4 pw = associate(prm, ds.at(c)[q - qi.start(c)]);
+        const int* dm = gv.dims + 8 * c;
+        unsigned long long pop = 0;
+        if (dm[7]) {
+            const int cx = (int)floorf(pw.x), cy = (int)floorf(pw.y), cz = (int)floorf(pw.z);
+            for (int oz = -1; oz <= 1; ++oz)
+                for (int oy = -1; oy <= 1; ++oy) {
+                    const int y = cy + oy - dm[1], z = cz + oz - dm[2];
+                    if (y < 0 || y >= dm[4] || z < 0 || z >= dm[5]) continue;
+                    const int x0 = max(cx - 1 - dm[0], 0), x1 = min(cx + 1 - dm[0], dm[3] - 1);
+                    if (x0 > x1) continue;
+                    const int row = dm[6] + (z * dm[4] + y) * dm[3];
+                    pop += gv.cell_start[row + x1 + 1] - gv.cell_start[row + x0];
+                }
+        }
+        acc += 16ull + 40ull + 27ull * 8ull + 16ull * pop;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane_id() == 0 && acc) atomicAdd(out, acc);
+}
+
 struct ObsArgs {
     int* cnt;
     u32* acc;
@@ -1994,6 +2068,59 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     const unsigned tail_grid = (unsigned)(o.tail_tiles < (size_t)kSortMaxBlocks ? o.tail_tiles : kSortMaxBlocks);
     PF_LAUNCH_NC(nc, k_rg_tail, dim3(tail_grid > 0 ? tail_grid : 1), dim3(256), 0, s, ta);
     PF_LAUNCH_NC(nc, k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, clouds_w(o.map));
+}
+
+// the association kNN probe (pf_odom.h)
+int odom_probe_assoc(OdomGPU& o, int iters, double* avg_ms, double* alg_bytes, int* nq_out, float4* q_host,
+                     size_t q_cap) {
+    if (!o.inited || o.frames < 2 || iters < 1) return PF_EINVAL;
+    const int nc = o.cls.nc;
+    const int p = (o.frames - 1) % kSlots;
+    int nq = 0;
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    PF_HIP_TRY(hipMemcpy(&nq, o.cnt + C_NQ, sizeof(int), hipMemcpyDeviceToHost));
+    *nq_out = nq;
+    if (nq <= 0) return PF_EINVAL;
+    int* nbr = nullptr;
+    float4* qd = nullptr;
+    unsigned long long* bytes = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = PF_OK;
+    if (hipMalloc(&nbr, sizeof(int) * (size_t)nq) != hipSuccess || hipMalloc(&qd, sizeof(float4) * (size_t)nq) != hipSuccess ||
+        hipMalloc(&bytes, sizeof(unsigned long long)) != hipSuccess)
+        rc = PF_ENOMEM;
+    if (!rc && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) rc = PF_EHIP;
+    const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
+    const Clouds ds = clouds(o.sb[p].ds);
+    if (!rc) {
+        auto launch = [&](float4* qo) {
+            if (nq <= kAssocWideMax) PF_LAUNCH_NC(nc, k_assoc_probe_t16, dim3(kGrid), dim3(256), 0, o.stream, o.st, o.cnt, gv, ds, nbr, qo);
+            else PF_LAUNCH_NC(nc, k_assoc_probe_t8, dim3(kGrid), dim3(256), 0, o.stream, o.st, o.cnt, gv, ds, nbr, qo);
+        };
+        launch(qd);                                   // warm-up, and the queries for the caller
+        (void)hipMemsetAsync(bytes, 0, sizeof(unsigned long long), o.stream);
+        PF_LAUNCH_NC(nc, k_assoc_cellpop, dim3(kGrid), dim3(256), 0, o.stream, o.st, o.cnt, gv, ds, bytes);
+        (void)hipEventRecord(e0, o.stream);
+        for (int i = 0; i < iters; ++i) launch(nullptr);
+        (void)hipEventRecord(e1, o.stream);
+        float ms = 0.f;
+        unsigned long long b = 0;
+        if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess ||
+            hipMemcpy(&b, bytes, sizeof(b), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = PF_EHIP;
+        *avg_ms = (double)ms / iters;
+        *alg_bytes = (double)b;
+        if (!rc && q_host && q_cap >= (size_t)nq &&
+            hipMemcpy(q_host, qd, sizeof(float4) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = PF_EHIP;
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(nbr);
+    (void)hipFree(qd);
+    (void)hipFree(bytes);
+    return rc;
 }
 
 }  // namespace pf

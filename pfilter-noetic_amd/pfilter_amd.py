@@ -138,7 +138,7 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_odom_restore", "pf_odom_set_map_export", "pf_odom_map_export", "pf_odom_set_stage_timing",
            "pf_odom_stage_times", "pf_odom_set_state", "pf_cls_normals", "pf_dcvc_default_params",
            "pf_dcvc_create", "pf_dcvc_destroy", "pf_dcvc_run", "pf_dcvc_reset", "pf_cls_set_dcvc", "pf_bpf_set_dcvc",
-           "pf_host_alloc", "pf_host_free", "pf_odom_set_tie_order"]
+           "pf_host_alloc", "pf_host_free", "pf_odom_set_tie_order", "pf_odom_probe_assoc"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -197,6 +197,8 @@ def lib():
     L.pf_memcpy_h2d.argtypes = [_i, _vp, _vp, _sz]
     L.pf_memcpy_d2h.argtypes = [_i, _vp, _vp, _sz]
     L.pf_odom_set_tie_order.argtypes = [_vp, _i]
+    L.pf_odom_probe_assoc.argtypes = [_vp, _i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(_sz), _vp, _sz]
     L.pf_dev_tie_sort.argtypes = [_i, _vp, _sz, _vp, ctypes.POINTER(_sz)]
     L.pf_host_alloc.argtypes = [_sz, ctypes.POINTER(_vp)]
     L.pf_host_free.argtypes = [_vp]
@@ -516,6 +518,18 @@ class Odom_ES_EstimationClass:
     def restore(self, blob):
         buf = ctypes.create_string_buffer(bytes(blob), len(blob))
         _check("pf_odom_restore", lib().pf_odom_restore(self._h, buf, len(blob)))
+
+    def probe_assoc(self, iters=20, queries=False, cap=400000):
+        """pf_odom_probe_assoc: (avg ms per launch of the association's kNN on the last frame, algorithmic
+        bytes per launch, query count[, queries [nq, 4] float32: x, y, z, bits(class)])"""
+        ms, b, n = ctypes.c_double(), ctypes.c_double(), _sz()
+        q = np.empty((cap, 4), np.float32) if queries else None
+        _check("pf_odom_probe_assoc", lib().pf_odom_probe_assoc(self._h, int(iters), ctypes.byref(ms), ctypes.byref(b),
+                                                                ctypes.byref(n), q.ctypes.data if queries else None,
+                                                                cap if queries else 0), allow_warn=False)
+        if queries:
+            return ms.value, b.value, n.value, q[:n.value].copy()
+        return ms.value, b.value, n.value
 
     def set_tie_order(self, enable):
         """pf_odom_set_tie_order: VoxelGrid / rgbds order equal keys as libstdc++ std::sort (parity mode)"""

@@ -111,6 +111,26 @@ def dense_map(n, seed=5):
     return out
 
 
+def voxel_map(n, leaf=0.8, seed=5, oversample=3.5):
+    """configs[4]'s local map: n voxel centroids (float32 [n, 3]) of the dense synthetic block at `leaf`
+    (the surf map's 0.8 m), in ascending voxel order (z, then y, then x), one point per voxel, so the
+    map is a fixed point of the map update's re-voxelisation (rgbds) and keeps its size"""
+    p = dense_map(int(n * oversample), seed=seed)[:, :3].astype(np.float64)
+    ijk = np.floor(p / leaf).astype(np.int64)
+    ijk -= ijk.min(axis=0)
+    dims = ijk.max(axis=0) + 1
+    key = ijk[:, 0] + dims[0] * (ijk[:, 1] + dims[1] * ijk[:, 2])
+    order = np.argsort(key, kind="stable")
+    ks = key[order]
+    starts = np.r_[0, np.nonzero(np.diff(ks))[0] + 1]
+    if starts.size < n:
+        raise ValueError("the dense block has only %d voxels at leaf %g" % (starts.size, leaf))
+    starts = starts[:n + 1]
+    sums = np.add.reduceat(p[order[:starts[-1]]], starts[:-1], axis=0)
+    cnt = np.diff(starts).astype(np.float64)
+    return (sums[:n] / cnt[:n, None]).astype(np.float32)
+
+
 def dense_queries(map_xyz4, nq, sigma=0.3, seed=6):
     q = np.empty((nq, 4), np.float32)
     m = np.ascontiguousarray(map_xyz4, np.float32)

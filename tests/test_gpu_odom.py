@@ -551,3 +551,28 @@ def test_map_export_equals_get_map(pa, pfsynth):
             gx, gr = od._map(which)
             np.testing.assert_array_equal(ex, gx)
             np.testing.assert_array_equal(er, gr)
+
+
+def test_probe_assoc_knn(pa, pfref, pfsynth):
+    """pf_odom_probe_assoc: the association's kNN alone on the last frame changes nothing (the next
+    frames give the bits of an unprobed run), and its algorithmic bytes are SURVEY 8(d)'s formula over
+    the queries it returns, against each query class's own map (the grid the frame searched)."""
+    seq = pfsynth.Sequence("S64", n_frames=10, az_steps=1500)
+    frames = [seq.frame(k) for k in range(10)]
+    runs = []
+    for probe in (False, True):
+        od = pa.Odom_ES_EstimationClass(device=0)
+        od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+        for k in range(6):
+            od.frame_host(frames[k])
+        if probe:
+            maps = [od._map(0)[0], od._map(1)[0]]             # after frame 5; the grid holds frame 5's input
+            ms, alg, nq, q = od.probe_assoc(iters=3, queries=True)
+        for k in range(6, 10):
+            od.frame_host(frames[k])
+        runs.append(od.poses())
+    np.testing.assert_array_equal(runs[0], runs[1])
+    assert ms > 0 and nq == q.shape[0] > 1000
+    cls = q[:, 3].view(np.int32)
+    assert set(np.unique(cls)) == {0, 1}
+    assert alg > (16 + 40 + 216) * nq
