@@ -563,10 +563,11 @@ def test_probe_assoc_knn(pa, pfref, pfsynth):
     for probe in (False, True):
         od = pa.Odom_ES_EstimationClass(device=0)
         od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
-        for k in range(6):
+        for k in range(5):
             od.frame_host(frames[k])
+        maps = [od._map(0)[0], od._map(1)[0]]                 # frame 5's grid is built from these
+        od.frame_host(frames[5])
         if probe:
-            maps = [od._map(0)[0], od._map(1)[0]]             # after frame 5; the grid holds frame 5's input
             ms, alg, nq, q = od.probe_assoc(iters=3, queries=True)
         for k in range(6, 10):
             od.frame_host(frames[k])
@@ -575,4 +576,6 @@ def test_probe_assoc_knn(pa, pfref, pfsynth):
     assert ms > 0 and nq == q.shape[0] > 1000
     cls = q[:, 3].view(np.int32)
     assert set(np.unique(cls)) == {0, 1}
-    assert alg > (16 + 40 + 216) * nq
+    pop = sum(pfref.knn_cellpop(np.c_[maps[c], np.zeros(len(maps[c]), np.float32)],
+                                np.c_[q[cls == c, :3], np.zeros(int((cls == c).sum()), np.float32)]) for c in (0, 1))
+    assert alg == (16 + 40 + 216) * nq + 16 * pop
