@@ -16,7 +16,8 @@ _LIB = os.path.join(_HERE, "libpfsynth.so")
 
 def build(force=False):
     src = os.path.join(_HERE, "scan_synth.cpp")
-    if force or not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(src):
+    hdr = os.path.join(_HERE, "scan_synth.h")
+    if force or not os.path.exists(_LIB) or os.path.getmtime(_LIB) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
         subprocess.check_call(["g++", "-O2", "-fopenmp", "-fPIC", "-shared", "-o", _LIB, src])
     return _LIB
 
@@ -28,7 +29,8 @@ class Params(ctypes.Structure):
                 ("range_noise", ctypes.c_double), ("max_range", ctypes.c_double),
                 ("sensor_height", ctypes.c_double), ("building_prob", ctypes.c_double),
                 ("setback_min", ctypes.c_double), ("setback_max", ctypes.c_double),
-                ("seed", ctypes.c_int), ("vegetation", ctypes.c_double), ("terrain", ctypes.c_double)]
+                ("seed", ctypes.c_int), ("vegetation", ctypes.c_double), ("terrain", ctypes.c_double),
+                ("cross", ctypes.c_double)]
 
 
 _lib = None
@@ -52,7 +54,7 @@ def lib():
     return _lib
 
 
-PRESETS = {"S64": 0, "S32": 1, "S128": 2, "S64V": 3}
+PRESETS = {"S64": 0, "S32": 1, "S128": 2, "S64V": 3, "S64T": 4}
 
 
 class Sequence:

@@ -131,6 +131,7 @@ void build_scene(World& w) {
         while (s < s_end) {
             double L = rng.u(6.0, 16.0);
             double gap = rng.u(1.0, 5.0);
+            if (w.p.cross > 0 && rng.u() < 0.25) gap += rng.u(12.0, 25.0);       // a cross street
             if (rng.u() < w.p.building_prob) {
                 double sm = s + 0.5 * L;
                 PathSample ps = w.at_s(sm);
@@ -170,6 +171,34 @@ void build_scene(World& w) {
                 add_box(w, ps.x - std::sin(ps.psi) * lat, ps.y + std::cos(ps.psi) * lat, psi, 2.2, 0.9, 0.25, 1.5);
             }
             s += rng.u(6.0, 20.0);
+        }
+        if (w.p.cross > 0) {
+            // walls and buildings across the road axis (their broad faces look along the road)
+            rng = Rng(base + 6);
+            s = s_begin + rng.u(0.0, 20.0);
+            while (s < s_end) {
+                PathSample ps = w.at_s(s);
+                double lat = rng.u(10.0, 40.0) * side;
+                double hx = rng.u(3.0, 8.0), hy = rng.u(0.3, 4.0), top = rng.u(2.5, 12.0);
+                add_box(w, ps.x - std::sin(ps.psi) * lat, ps.y + std::cos(ps.psi) * lat,
+                        ps.psi + 0.5 * M_PI + rng.u(-0.3, 0.3), hx, hy, 0.0, top);
+                s += rng.u(20.0, 50.0) / w.p.cross;
+            }
+            // landmarks scattered off the road axis: posts, lamp masts, tree trunks
+            rng = Rng(base + 7);
+            s = s_begin + rng.u(0.0, 8.0);
+            while (s < s_end) {
+                PathSample ps = w.at_s(s);
+                double lat = rng.u(6.0, 45.0) * side;
+                Cyl c;
+                c.cx = ps.x - std::sin(ps.psi) * lat;
+                c.cy = ps.y + std::cos(ps.psi) * lat;
+                c.r = rng.u(0.2, 0.6);
+                c.z0 = 0.0;
+                c.z1 = rng.u(2.0, 9.0);
+                w.cyls.push_back(c);
+                s += rng.u(6.0, 15.0) / w.p.cross;
+            }
         }
         if (w.p.vegetation <= 0) continue;
         // trees: a trunk and a porous crown, spacing shrinking with the vegetation density
@@ -422,6 +451,11 @@ void pfsyn_default_params(int preset, pfsyn_params* p) {
         p->lines = 64; p->az_steps = 2000; p->speed = 8.0; p->seed = 0;
         p->building_prob = 0.35; p->setback_min = 8.0; p->setback_max = 30.0;
         p->vegetation = 1.0; p->terrain = 0.08;
+    } else if (preset == 4) {   // S64T: the well-conditioned town
+        p->lines = 64; p->az_steps = 2000; p->speed = 10.0; p->seed = 0;
+        p->building_prob = 0.35; p->setback_min = 10.0; p->setback_max = 35.0;
+        p->yaw_amp = 0.2; p->yaw_period = 40.0;
+        p->cross = 1.0;
     } else {                    // S64 KITTI-like
         p->lines = 64; p->az_steps = 2000; p->speed = 10.0; p->seed = 0;
         p->building_prob = 0.85; p->setback_min = 6.0; p->setback_max = 20.0;

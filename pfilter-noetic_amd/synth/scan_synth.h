@@ -32,10 +32,14 @@ typedef struct {
     int seed;
     double vegetation;      /* 0: none; > 0: trees / hedges per metre of road (porous volumes) */
     double terrain;         /* amplitude (m) of the rough-ground height field (0: flat) */
+    double cross;           /* 0: none; > 0: cross streets, walls across the road and landmarks off the
+                               road axis per metre of road (S64T) */
 } pfsyn_params;
 
 /* preset 0: S64 KITTI-like (config 1/2/4), 1: S32 campus (config 3), 2: S128 (config 5),
- * 3: S64V, S64 in a residential scene with vegetation and rough ground (KITTI-00 density) */
+ * 3: S64V, S64 in a residential scene with vegetation and rough ground (KITTI-00 density),
+ * 4: S64T, a well-conditioned town: turns, cross streets, walls across the road and landmarks off
+ *    the road axis, so every direction of the pose is observed (the free-running parity scene) */
 void pfsyn_default_params(int preset, pfsyn_params* p);
 
 /* Builds the world along the trajectory for n_frames frames. Returns NULL on error. */

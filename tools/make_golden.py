@@ -96,6 +96,50 @@ def odom_full_case(n=4541):
     print("odom_full", poses[-1], ex.shape, sx.shape)
 
 
+def faithful_traj(preset, n, theta, name, lines=64, seed=0):
+    """A whole sequence through the reference-faithful oracle (opts=0: libstdc++ std::sort tie orders,
+    Householder-QR LM, FLANN-style kd-tree), free-running: every frame's pose and counts and the final
+    maps' hashes. The GPU test (tests/test_gpu_parity_free.py) runs the device free-running in the
+    reference-tie-order mode against it."""
+    seq = pfsynth.Sequence(preset, n_frames=n, seed=seed)
+    od = pfref.Odom(pfref.make_lidar(lines, 3.0, 90.0), 0.4, 0, theta[0], theta[1], 0, opts=0)
+    poses = np.zeros((n, 7))
+    counts = np.zeros((n, len(FULL_COUNTS)), np.int32)
+    in_sha = []
+    for f0 in range(0, n, 256):
+        nf = min(256, n - f0)
+        buf, cnt = seq.frames(f0, nf, threads=8)
+        for i in range(nf):
+            k = f0 + i
+            x = buf[i, :cnt[i]]
+            if k % 500 == 0 or k == n - 1:
+                in_sha.append((k, sha(x)))
+            poses[k] = od.frame(x)
+            st = od.stats()
+            counts[k] = [st[c] for c in FULL_COUNTS]
+        print(name, "frame", f0 + nf, poses[f0 + nf - 1][4:], flush=True)
+    ex, er = od.get_map(0)
+    sx, sr = od.get_map(1)
+    gt = np.array([seq.gt_pose(k) for k in range(n)])
+    np.savez_compressed(os.path.join(OUT, "odom_%s_faithful.npz" % name), poses=poses, counts=counts, gt=gt,
+                        count_names=np.array(FULL_COUNTS), input_frames=np.array([k for k, _ in in_sha]),
+                        input_sha=np.array([h for _, h in in_sha]),
+                        map_sha=np.array([sha(ex), sha(er), sha(sx), sha(sr)]),
+                        map_sizes=np.array([ex.shape[0], sx.shape[0]]),
+                        spec=np.array([preset, "n_frames=%d" % n, "seed=%d" % seed, "lines=%d" % lines, "3-90 m",
+                                       "map 0.4", "k_new 0", "theta_p %g" % theta[0], "theta_max %d" % theta[1],
+                                       "weight 0", "opts=0 (faithful)"]))
+    print(name, "faithful", poses[-1], ex.shape, sx.shape)
+
+
+def faithful_s64_case():
+    faithful_traj("S64", 4541, (0.4, 75), "s64")
+
+
+def faithful_s64t_case():
+    faithful_traj("S64T", 4541, (0.4, 75), "s64t")
+
+
 def knn_case():
     rng = np.random.default_rng(11)
     mp = np.zeros((3000, 4), np.float32)
