@@ -10,8 +10,7 @@ the oracle: ~1e-12 m per frame, tests/test_gpu_parity_synced.py), which a free r
 S64T (pfsynth preset 4) is the well-conditioned town: turns, cross streets, walls and landmarks off
 the road axis (the faithful oracle drifts < 1 % against the generator's ground truth,
 tests/test_synth.py); there every frame of the 4541 must stay within 1e-4 m / 1e-5 rad with identical
-counts. On S64, the near-degenerate street canyon of the headline, the run is recorded (first frame
-past the tolerance) and must stay within it for the first 1000 frames."""
+counts. The same bar holds on S64, the street canyon of the headline, over all 4541 frames."""
 import hashlib
 import json
 import os
@@ -94,12 +93,17 @@ def test_free_running_s64t_every_frame(pa, pfsynth):
 
 
 def test_free_running_s64_headline_scene(pa, pfsynth):
-    """configs[1] on S64 (the headline's street canyon), 4541 frames free-running in tie mode."""
+    """configs[1] on S64 (the headline's street canyon), 4541 frames free-running in tie mode: every
+    frame within the tolerance of the faithful oracle's free run, every count identical (measured: a
+    worst 5.9e-12 m over the sequence, profiles/r03_parity_free/)."""
     rep = free_run(pa, pfsynth, "s64", "S64", (0.4, 75))
-    assert rep["worst_m_within_first_1000"] < TOL_T, rep
+    assert rep["frames_past_tolerance"] == 0, rep
+    assert rep["first_count_mismatch"] is None, rep
 
 
-def test_free_running_s64t_stable_order(pa, pfsynth):
-    """The default (stable radix) order on the well-conditioned town: recorded."""
-    rep = free_run(pa, pfsynth, "s64t", "S64T", (0.4, 75), tie_order=False)
+@pytest.mark.parametrize("name,preset", [("s64", "S64"), ("s64t", "S64T")])
+def test_free_running_stable_order(pa, pfsynth, name, preset):
+    """The default (stable radix) order, free-running: the last bits of the centroids differ from the
+    reference's from frame 1 on, so the trajectories separate; where is recorded."""
+    rep = free_run(pa, pfsynth, name, preset, (0.4, 75), tie_order=False)
     assert rep["frames"] == 4541
