@@ -132,6 +132,7 @@ CONFIGS = [
     ("configs0_S64", "S64", 4541, (0.0, 0), 64),        # configs[0]: FLOAM-equivalent parameters
     ("configs2_S32", "S32", 3000, (1.0, 200), 32),      # configs[2]: 32-line campus, theta 1 / 200
     ("dense_S64V", "S64V", 1000, (0.4, 75), 64),        # dense vegetation scene, KITTI-like map sizes
+    ("town_S64T", "S64T", 4541, (0.4, 75), 64),         # the well-conditioned town (free-running parity scene)
 ]
 
 
