@@ -93,8 +93,9 @@ def test_free_running_s64t(pa, pfsynth):
     """The town, configs[1] parameters, 4541 frames free-running in tie mode: every frame before the
     first discrete difference (frame 338 measured) within 1e-9 m of the faithful oracle's own run."""
     rep = free_run(pa, pfsynth, "s64t", "S64T", (0.4, 75))
-    assert rep["first_count_mismatch"] is not None and rep["first_count_mismatch"] >= 300, rep
-    assert rep["first_frame_past_tolerance"] >= rep["first_count_mismatch"], rep
+    fc, fp = rep["first_count_mismatch"], rep["first_frame_past_tolerance"]
+    assert fc is None or fc >= 300, rep
+    assert fp is None or (fc is not None and fp >= fc), rep       # poses part only after a discrete flip
     assert rep["worst_m_before_first_count_mismatch"] < 1e-9, rep
 
 
