@@ -68,6 +68,9 @@ def parse(argv=None):
                     help="frames of each extra ES leg (configs[0] theta=0 on S64; the S64V dense scene at "
                          "configs[1] and at theta=0); 0 = skip them")
     ap.add_argument("--leg-cpu-seconds", type=float, default=8.0, help="CPU baseline sample of each extra leg")
+    ap.add_argument("--only-headline", action="store_true",
+                    help="the headline line alone (no roofline, CPU, BPF, ES, PCIe, node, pageable or configs4 "
+                         "legs): for profiling the frame path")
     ap.add_argument("--no-pcie", action="store_true",
                     help="skip the PCIe-inclusive leg (the headline's frames from pinned host RAM through "
                          "pf_odom_frame_host; reported as pcie_inclusive, never as value)")
@@ -77,7 +80,11 @@ def parse(argv=None):
                     help="frames of the configs[4] pipeline leg (S128 scans, 2M-point map); 0 = skip")
     ap.add_argument("--node-frames", type=int, default=1000,
                     help="frames of the node call pattern (pf_fe_extract -> pf_odom_update); 0 = skip")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.only_headline:
+        a.no_roofline = a.no_cpu = a.no_pcie = True
+        a.bpf_frames = a.leg_frames = a.pageable_frames = a.node_frames = a.configs4_frames = 0
+    return a
 
 
 def resolve_world(args, env):

@@ -22,7 +22,7 @@ rc=$?
 cat $OUT/quick_bench.json; tail -n 3 $OUT/quick_bench.err
 if [ $rc -ne 0 ]; then echo "BENCH FAILED rc=$rc"; exit $rc; fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/qprof -o run --output-format csv -- \
-    python3 bench.py --steps 1000 --no-cpu --no-graph --bpf-frames 0 --leg-frames 0 --no-roofline --no-pcie --node-frames 0 --pageable-frames 0 > $OUT/qprof.json 2> $OUT/qprof.log
+    python3 bench.py --steps 1000 --no-graph --only-headline > $OUT/qprof.json 2> $OUT/qprof.log
 rc=$?
 if [ $rc -ne 0 ]; then echo "PROF FAILED rc=$rc"; tail -n 20 $OUT/qprof.log; exit $rc; fi
 python3 tools/kstats.py $(find $OUT/qprof -name "*kernel_stats.csv" | head -1) 14

@@ -32,7 +32,7 @@ if [ "$WHAT" = bench ] || [ "$WHAT" = all ]; then
     if [ $rc -ne 0 ]; then echo "BENCH FAILED rc=$rc"; exit $rc; fi
     # kernel durations: eager launches (--no-graph) so every kernel is traced individually
     timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-        python3 bench.py --steps 1000 --no-cpu --no-graph --bpf-frames 0 --leg-frames 0 > $OUT/prof_bench.json 2> $OUT/prof.log
+        python3 bench.py --steps 1000 --no-graph --only-headline > $OUT/prof_bench.json 2> $OUT/prof.log
     rc=$?
     if [ $rc -ne 0 ]; then echo "PROF FAILED rc=$rc"; tail -n 20 $OUT/prof.log; exit $rc; fi
     echo prof ok
