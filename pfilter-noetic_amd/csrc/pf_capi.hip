@@ -1,6 +1,8 @@
 // C ABI (include/pfilter_hip.h) over the device pipeline. Host code here only stages inputs,
 // enqueues work on the handle's stream and copies results back; all arithmetic is on the device.
+#include <chrono>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -290,6 +292,7 @@ int pf_odom_destroy(pf_odom* h) {
     (void)hipStreamSynchronize(h->o.stream_a);
     (void)hipStreamSynchronize(h->o.stream);
     timing_free(h);
+    host_prof_report();
     odom_destroy(h->o);
     delete h;
     return PF_OK;
@@ -629,6 +632,33 @@ static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool s
     return PF_OK;
 }
 
+// development: PF_HOST_PROFILE=1 prints the mean host time of every HIP call site of enqueue_frame
+// when the handle is destroyed
+struct HostProf {
+    static constexpr int kSites = 8;
+    double us[kSites] = {};
+    long long n[kSites] = {};
+    bool on = std::getenv("PF_HOST_PROFILE") != nullptr;
+};
+static HostProf g_hprof;
+#define PF_HT(site, expr)                                                                        \
+    do {                                                                                         \
+        if (!g_hprof.on) { expr; break; }                                                        \
+        const auto t0_ = std::chrono::steady_clock::now();                                       \
+        expr;                                                                                    \
+        g_hprof.us[site] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0_).count(); \
+        g_hprof.n[site]++;                                                                       \
+    } while (0)
+static void host_prof_report() {
+    if (!g_hprof.on) return;
+    static const char* names[HostProf::kSites] = {"wait ev_b", "scan D2D copy", "k_set_int", "graph A",
+                                                 "record ev_a + wait", "graph B", "record ev_b", "whole call"};
+    for (int k = 0; k < HostProf::kSites; ++k)
+        if (g_hprof.n[k])
+            std::fprintf(stderr, "pf host profile: %-20s %8.2f us x %lld\n", names[k], g_hprof.us[k] / g_hprof.n[k],
+                         g_hprof.n[k]);
+}
+
 // one frame through both stages. ES: the raw scan d_in[0 .. n) is copied to the staging buffer and
 // stage A runs featureExtraction + VoxelGrid. BPF: the class clouds cl[c][0 .. ncl[c]) are copied
 // into the slot's inputs and stage A runs VoxelGrid; BPF raw-scan mode (cl null): the scan is staged
@@ -641,13 +671,14 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
     const int p = o.frames % kSlots;
     const bool steady = o.inited && o.opt_count_host <= 2 && o.graph_enabled;
     if (scan && n > o.in_cap) return PF_ECAPACITY;
-    int rc = stage_a_begin(h, p);
+    int rc = 0;
+    PF_HT(0, rc = stage_a_begin(h, p));
     if (!rc) rc = timing_mark(h, 0);
     if (rc) return rc;
     if (nc == 2 || scan) {
         if (n > o.in_cap) return PF_ECAPACITY;
-        if (n) PF_HIP_TRY(hipMemcpyAsync(o.stage, d_in, sizeof(float4) * n, hipMemcpyDeviceToDevice, o.stream_a));
-        hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, o.sb[p].cnt + C_NIN, (int)n);
+        if (n) PF_HT(1, PF_HIP_TRY(hipMemcpyAsync(o.stage, d_in, sizeof(float4) * n, hipMemcpyDeviceToDevice, o.stream_a)));
+        PF_HT(2, hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, o.sb[p].cnt + C_NIN, (int)n));
     } else {
         for (int c = 0; c < nc; ++c) {
             if (ncl[c] > o.in_cap) return PF_ECAPACITY;
@@ -662,14 +693,14 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
             rc = capture(o.stream_a, &ga, o, p, true, scan);
             if (rc) return rc;
         }
-        PF_HIP_TRY(hipGraphLaunch(ga, o.stream_a));
+        PF_HT(3, PF_HIP_TRY(hipGraphLaunch(ga, o.stream_a)));
     } else {
         if (nc == 2) stage_enqueue_fe(o, p, o.stage, o.stream_a);
         else if (scan) stage_enqueue_front(o, p, o.stream_a);
         if (o.inited) stage_enqueue_vg(o, p, o.stream_a);
     }
     rc = timing_mark(h, 1);
-    if (!rc) rc = stage_a_end_b_begin(h, p);
+    if (!rc) PF_HT(4, rc = stage_a_end_b_begin(h, p));
     if (!rc) rc = timing_mark(h, 2);
     if (rc) return rc;
     if (steady) {
@@ -677,7 +708,7 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
             rc = capture(o.stream, &o.graph_b[p], o, p, false);
             if (rc) return rc;
         }
-        PF_HIP_TRY(hipGraphLaunch(o.graph_b[p], o.stream));
+        PF_HT(5, PF_HIP_TRY(hipGraphLaunch(o.graph_b[p], o.stream)));
     } else if (!o.inited) {
         odom_enqueue_init(o, p, o.stream);
         odom_enqueue_export(o, o.stream);
@@ -687,13 +718,15 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
     }
     rc = timing_mark(h, 3);
     if (rc) return rc;
-    return stage_b_end(h, p);
+    PF_HT(6, rc = stage_b_end(h, p));
+    return rc;
 }
 
 int pf_odom_frame_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]) {
     if (!h || (!d_xyzi && n) || h->o.cls.nc != 2) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->o.device));
-    int rc = enqueue_frame(h, reinterpret_cast<const float4*>(d_xyzi), n, nullptr, nullptr);
+    int rc = 0;
+    PF_HT(7, rc = enqueue_frame(h, reinterpret_cast<const float4*>(d_xyzi), n, nullptr, nullptr));
     if (rc) return rc;
     if (pose_out) return read_pose(h, pose_out);
     return PF_OK;

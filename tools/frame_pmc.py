@@ -14,15 +14,15 @@ import os
 import re
 from collections import defaultdict
 
-KERNELS = ["k_lm_solve", "k_os_pass", "k_fe_sector", "k_assoc", "k_observe", "k_vg_reduce", "k_segments",
-           "k_scan1", "k_rg_keys"]
+# every kernel of the frame path: stage A (featureExtraction + VoxelGrid) and stage B (odometry)
+STAGE_B = ["k_grid_bounds", "k_grid_count", "k_scan1", "k_grid_scatter", "k_assoc", "k_observe", "k_lm_solve",
+           "k_rg_append_keys", "k_os_pass", "k_rg_tail", "k_rg_write"]
 
 
 def short(name):
-    for k in KERNELS:                  # names read "void pf::(anonymous namespace)::k_x<2>(pf::Args)"
-        if re.search(r"\b%s\b" % k, name):
-            return k
-    return ""
+    """names read "void pf::(anonymous namespace)::k_x<2>(pf::Args)": the k_ identifier"""
+    m = re.search(r"\b(k_\w+?)(<|\(|$)", name)
+    return m.group(1) if m else ""
 
 
 def main():
@@ -34,19 +34,18 @@ def main():
     for f in glob.glob(a.root + "/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             k = short(row.get("Kernel_Name", ""))
-            if k in KERNELS:
+            if k:
                 # one row per (dispatch, counter): sum over the per-XCD / per-SE dimension rows of a dispatch
                 acc[k][(row["Counter_Name"], row.get("Dispatch_Id", ""))].append(float(row["Counter_Value"]))
     out = {"source": "rocprofv3 --pmc passes (tools/frame_pmc.sh) over bench.py --steps 100 --no-graph (configs[1], S64)",
            "kernels": {}}
-    for k in KERNELS:
-        if k not in acc:
-            continue
+    for k in sorted(acc, key=lambda x: (x not in STAGE_B, x)):
         per = defaultdict(list)
         for (ctr, _), vals in acc[k].items():
             per[ctr].append(sum(vals))
         m = {c: sum(v) / len(v) for c, v in per.items()}
-        d = {"dispatches": max(len(v) for v in per.values()), "mean_per_dispatch": m}
+        d = {"stage": "B" if k in STAGE_B else "A", "dispatches": max(len(v) for v in per.values()),
+             "mean_per_dispatch": m}
         wc = m.get("SQ_WAVE_CYCLES")
         if wc:
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
