@@ -286,6 +286,8 @@ int pf_bpf_create(const pf_lidar_params* lidar, const pf_odom_params* params, in
 
 int pf_odom_classes(pf_odom* h) { return h ? h->o.cls.nc : PF_EINVAL; }
 
+static void host_prof_report();
+
 int pf_odom_destroy(pf_odom* h) {
     if (!h) return PF_OK;
     (void)hipSetDevice(h->o.device);
