@@ -311,6 +311,12 @@ int pf_odom_set_tie_order(pf_odom* h, int enable);
  * estimator's state is not changed. PF_EINVAL before the second frame. */
 int pf_odom_probe_assoc(pf_odom* h, int iters, double* avg_ms, double* alg_bytes, size_t* nq, float* queries,
                         size_t cap);
+/* rgbds bookkeeping (the default order merges this frame's sorted appended points into the map, which
+ * stays in voxel order): how many updates since create / reset had to sort every element instead (the
+ * first update after initMapWithPoints or pf_odom_set_map, a centroid that rounded into a neighbouring
+ * voxel, or more than 65536 appended points), and the largest appended-point count seen. Waits for
+ * the handle's work. */
+int pf_odom_merge_stats(pf_odom* h, int* full_sorts, int* max_appended);
 /* Per-stage device time (the reference's per-stage timers, src/laserProcessingNode.cpp:71-79 and
  * src/odomEstimationNode copy.cpp:92-100, as HIP events on the handle's two streams): with enable,
  * every frame records when stage A (featureExtraction / front end + VoxelGrid) and stage B (the

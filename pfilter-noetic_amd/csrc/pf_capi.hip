@@ -1,5 +1,6 @@
 // C ABI (include/pfilter_hip.h) over the device pipeline. Host code here only stages inputs,
 // enqueues work on the handle's stream and copies results back; all arithmetic is on the device.
+#include <algorithm>
 #include <chrono>
 #include <climits>
 #include <cstdlib>
@@ -640,6 +641,7 @@ struct HostProf {
     static constexpr int kSites = 8;
     double us[kSites] = {};
     long long n[kSites] = {};
+    std::vector<float> samp[kSites];
     bool on = std::getenv("PF_HOST_PROFILE") != nullptr;
 };
 static HostProf g_hprof;
@@ -648,17 +650,31 @@ static HostProf g_hprof;
         if (!g_hprof.on) { expr; break; }                                                        \
         const auto t0_ = std::chrono::steady_clock::now();                                       \
         expr;                                                                                    \
-        g_hprof.us[site] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0_).count(); \
+        const double dt_ = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0_).count(); \
+        g_hprof.us[site] += dt_;                                                                 \
         g_hprof.n[site]++;                                                                       \
+        g_hprof.samp[site].push_back((float)dt_);                                                \
     } while (0)
 static void host_prof_report() {
     if (!g_hprof.on) return;
     static const char* names[HostProf::kSites] = {"wait ev_b", "scan D2D copy", "k_set_int", "graph A",
                                                  "record ev_a + wait", "graph B", "record ev_b", "whole call"};
     for (int k = 0; k < HostProf::kSites; ++k)
-        if (g_hprof.n[k])
-            std::fprintf(stderr, "pf host profile: %-20s %8.2f us x %lld\n", names[k], g_hprof.us[k] / g_hprof.n[k],
-                         g_hprof.n[k]);
+        if (g_hprof.n[k]) {
+            std::vector<float>& v = g_hprof.samp[k];
+            double first = 0;
+            const size_t nf = v.size() < 100 ? v.size() : 100;
+            for (size_t i = 0; i < nf; ++i) first += v[i];
+            std::sort(v.begin(), v.end());
+            auto q = [&](double f) { return v[(size_t)(f * (v.size() - 1))]; };
+            std::fprintf(stderr,
+                         "pf host profile: %-20s mean %8.2f us x %lld  p10 %.1f p50 %.1f p90 %.1f max %.1f  first100 "
+                         "mean %.1f\n",
+                         names[k], g_hprof.us[k] / g_hprof.n[k], g_hprof.n[k], q(0.1), q(0.5), q(0.9), q(1.0),
+                         first / (nf ? nf : 1));
+            v.clear();
+        }
+    g_hprof = HostProf{};
 }
 
 // one frame through both stages. ES: the raw scan d_in[0 .. n) is copied to the staging buffer and
@@ -1161,6 +1177,24 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
     return PF_OK;
 }
 
+// development / test switch (not part of include/pfilter_hip.h): rgbds in the default order by the
+// full radix sort of every element (the path before the merge) instead of the merge, for A/B checks
+extern "C" int pf_dev_set_rg_radix(pf_odom* h, int enable) {
+    if (!h) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    if ((enable != 0) != o.rg_radix)
+        for (int s = 0; s < kSlots; ++s)
+            if (o.graph_b[s]) {
+                (void)hipGraphExecDestroy(o.graph_b[s]);
+                o.graph_b[s] = nullptr;
+            }
+    o.rg_radix = enable != 0;
+    return PF_OK;
+}
+
 // development / test probe (not part of include/pfilter_hip.h): the reference-tie-order sort alone on
 // n host keys (bits 30-31 the class, 0xFFFFFFFF dropped); perm receives the vals (input indices) of the
 // kept pairs in std::sort's order, *n_out their count
@@ -1217,6 +1251,19 @@ int pf_odom_probe_assoc(pf_odom* h, int iters, double* avg_ms, double* alg_bytes
     const int rc = odom_probe_assoc(h->o, iters, avg_ms, alg_bytes, &n, reinterpret_cast<float4*>(queries), cap);
     *nq = (size_t)(n > 0 ? n : 0);
     return rc;
+}
+
+int pf_odom_merge_stats(pf_odom* h, int* full_sorts, int* max_appended) {
+    if (!h || !full_sorts || !max_appended) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    int st[4];
+    PF_HIP_TRY(hipMemcpy(st, o.rgm_stat, sizeof(st), hipMemcpyDeviceToHost));
+    *full_sorts = st[1];
+    *max_appended = st[2];
+    return PF_OK;
 }
 
 int pf_odom_set_graph(pf_odom* h, int enable) {

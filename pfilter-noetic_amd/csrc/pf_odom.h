@@ -95,6 +95,9 @@ struct LMState {
     int iteration, invalid, reuse, done, phase, n_res, pad0, pad1;
 };
 
+// rgbds merge: the appended points are sorted in runs of kRgmRun by one 1024-thread workgroup each
+constexpr int kRgmRun = 4096;
+constexpr int kRgmRuns = 16;
 constexpr int kLmParts = 30;   // cost, g[6], H[21], bad_r, bad_J
 constexpr int kLmEvalSlots = 8; // LM claim masks per solve (>= evaluations per solve)
 constexpr int kLmEvals = 5;      // evaluations per solve: 1 + max_num_iterations (4)
@@ -191,6 +194,17 @@ struct OdomGPU {
     u32 *keys = nullptr, *vals = nullptr;
     u64* tail_status = nullptr;   // k_rg_tail look-back words [tail_tiles] + arrival counter
     size_t tail_tiles = 0;
+    // rgbds by merge (k_rgm_keys / k_rgm_merge / k_rg_tail64, the default order): the map is kept in
+    // voxel order, so only this frame's appended points are sorted and then merged into it
+    u64* rgm_okey = nullptr;       // [nc * map_cap] voxel keys of the map points, map order
+    u64* rgm_key64 = nullptr;      // [sort_cap] voxel keys of every element, element order
+    u32* rgm_vtag = nullptr;       // [sort_cap] element index | cropped << 31
+    u64* rgm_akey = nullptr;       // [kRgmRuns * kRgmRun] sorted runs of the appended points
+    u32* rgm_atag = nullptr;
+    u64* rgm_kout = nullptr;       // [sort_cap] merged keys (vals: `vals`)
+    u64* rgm_ktmp = nullptr;       // [sort_cap] fallback sort scratch
+    u32* rgm_vtmp = nullptr;
+    int* rgm_stat = nullptr;       // [4]: fallback this frame, fallbacks so far, largest append, spare
 
     int* nbr = nullptr;            // [5 * kMaxC * in_cap]
     int* qflag = nullptr;          // bit0 valid association, bit1 kept
@@ -212,6 +226,7 @@ struct OdomGPU {
     // reference tie order (pf_odom_set_tie_order, pf_tie.h): VoxelGrid (stage A) and rgbds (stage B)
     // order equal keys as libstdc++'s std::sort does; each stage has its own scratch
     bool tie_order = false;
+    bool rg_radix = false;         // development: rgbds by the full radix sort instead of the merge
     TieSort* tie_a = nullptr;
     TieSort* tie_b = nullptr;
 };

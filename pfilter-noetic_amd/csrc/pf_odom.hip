@@ -1683,6 +1683,514 @@ __global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const f
     }
 }
 
+// ---------------------------- rgbds by merge (the default order) ----------------------------
+// addPointsToMap's rgbds (:606-626, :34-134) orders the elements (map points, then this frame's
+// appended points, per class) by voxel index and, within a voxel, by element index (the stable order;
+// the reference-tie-order mode keeps the radix path above). The voxel index orders voxels
+// lexicographically by (z, y, x) on any grid covering the points (k_rg_append_keys), so the 64-bit key
+// class << 62 | z << 40 | y << 20 | x of the voxel coordinates (20 bits each, biased) orders them the
+// same way on every frame. The map that the previous rgbds wrote is already in that order (its points
+// are voxel centroids, written in key order), so only the appended points need sorting: k_rgm_keys
+// sorts them in runs of kRgmRun (one 1024-thread workgroup per run, a bitonic network in LDS) while
+// the other workgroups key the map points and check that they are still in order; k_rgm_merge places
+// every element by binary searches; k_rg_tail64 reduces the voxels. Cropped elements stay in the
+// merged sequence, flagged, and are skipped by the reduction. When the map is not in key order (the
+// first update after initMapWithPoints or pf_odom_set_map, or a centroid that rounds into a
+// neighbouring voxel) or more points are appended than the runs hold, k_rgm_merge's first workgroup
+// sorts all elements itself (a stable LSD radix sort over the 64-bit keys) instead.
+constexpr int kRgmThreads = 1024;
+constexpr int kRgmOldBlocks = 256;
+constexpr int kRgmMergeBlocks = 64;
+constexpr u32 kRgmDrop = 0x80000000u;
+
+struct RgmArgs {
+    DevState* st;
+    int* cnt;
+    u32* acc;
+    Clouds map, ds;
+    CloudsW app;
+    double* poses;
+    int pose_cap;
+    VgLeaf leaf;
+    u64* okey;             // [map points] keys, map order
+    u64* key64;            // [elements] keys, element order
+    u32* vtag;             // [elements] element | cropped << 31
+    u64* akey;             // [kRgmRuns * kRgmRun] sorted runs of the appended points
+    u32* atag;
+    u64* kout;             // merged keys / tags (-> k_rg_tail64)
+    u32* vout;
+    u64* ktmp;             // fallback scratch
+    u32* vtmp;
+    int* stat;             // [4] (OdomGPU::rgm_stat)
+};
+
+// the frame's crop box and its voxel origin per class (as k_rg_append_keys)
+struct RgmBox {
+    float lo[3], hi[3];
+    __device__ __forceinline__ bool in(float4 p) const {
+        return !((p.x < lo[0] || p.y < lo[1] || p.z < lo[2]) || (p.x > hi[0] || p.y > hi[1] || p.z > hi[2]));
+    }
+};
+__device__ __forceinline__ RgmBox rgm_box(const double* prm) {
+    RgmBox b;
+    for (int k = 0; k < 3; ++k) {
+        b.lo[k] = (float)(prm[4 + k] - 100);
+        b.hi[k] = (float)(prm[4 + k] + 100);
+    }
+    return b;
+}
+// voxel coordinate floor(v / lf) relative to the crop box's voxel origin, biased by 2^19 and clamped
+// (monotone, so the order of clamped keys is the order of the points; inside the box exact)
+__device__ __forceinline__ u64 rgm_axis(float v, float lo, float lf) {
+    float d = floorf(v / lf) - (float)(int)floorf(lo / lf);
+    d = fminf(fmaxf(d, -524288.f), 524287.f);
+    return (u64)((int)d + 524288);
+}
+__device__ __forceinline__ u64 rgm_key(float4 p, int c, float lf, const RgmBox& b) {
+    return ((u64)c << 62) | (rgm_axis(p.z, b.lo[2], lf) << 40) | (rgm_axis(p.y, b.lo[1], lf) << 20) |
+           rgm_axis(p.x, b.lo[0], lf);
+}
+__device__ __forceinline__ bool rgm_less(u64 ka, u32 ta, u64 kb, u32 tb) {
+    return ka < kb || (ka == kb && (ta & ~kRgmDrop) < (tb & ~kRgmDrop));
+}
+
+// element index of map point g (map order over the classes) / appended point a
+template <int NC>
+__device__ __forceinline__ int rgm_old_elem(const RgView<NC>& V, int g, int& c, int& li) {
+    int start = 0, acc = 0;
+    c = NC - 1;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        const int mk = V.m[k];
+        if (g < acc + mk) { c = k; break; }
+        acc += mk;
+        start = V.end[k];
+    }
+    li = g - acc;
+    return start + li;
+}
+template <int NC>
+__device__ __forceinline__ int rgm_app_elem(const RgView<NC>& V, int a, int& c, int& li) {
+    int start = 0, acc = 0;
+    c = NC - 1;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        const int ak = V.end[k] - (k ? V.end[k - 1] : 0) - V.m[k];
+        if (a < acc + ak) { c = k; break; }
+        acc += ak;
+        start = V.end[k];
+    }
+    li = a - acc;
+    const int mc = sel3(c, V.m[0], V.m[1], V.m[2]);
+    return start + mc + li;
+}
+
+// blocks [0, kRgmRuns): one run of appended points each; block kRgmRuns: the pose step (as in
+// k_rg_append_keys); the rest: the map points (keys, crop flags, order check)
+template <int NC>
+__global__ void __launch_bounds__(kRgmThreads) k_rgm_keys(RgmArgs a) {
+    __shared__ u64 sk[kRgmRun];
+    __shared__ u32 si[kRgmRun];
+    double prm[7];
+    for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
+    const int t = threadIdx.x;
+    const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
+    const int n = V.total();
+    int M = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) M += V.m[c];
+    const int A = n - M;
+    const RgmBox box = rgm_box(prm);
+    if (blockIdx.x == kRgmRuns) {
+        finalize_pose(a.st, a.poses, a.pose_cap, 1, a.acc, prm);
+        if (t == 0) {
+            a.cnt[C_NRG] = n;
+            if (A > a.stat[2]) a.stat[2] = A;
+            if (A > kRgmRuns * kRgmRun) a.stat[0] = 1;
+        }
+        return;
+    }
+    if (blockIdx.x < kRgmRuns) {                       // a run of appended points
+        const int a0 = (int)blockIdx.x * kRgmRun;
+        if (a0 >= A) return;
+        const int len = min(kRgmRun, A - a0);
+        for (int s = t; s < kRgmRun; s += kRgmThreads) {
+            u64 key = ~0ull;
+            u32 tag = ~0u;
+            if (s < len) {
+                int c, li;
+                const int e = rgm_app_elem<NC>(V, a0 + s, c, li);
+                const float4 p = associate(prm, a.ds.at(c)[li]);   // pointAssociateToMap (:592-604)
+                a.app.at(c)[li] = p;
+                key = rgm_key(p, c, a.leaf.at(c), box);
+                tag = (u32)e | (box.in(p) ? 0u : kRgmDrop);
+                a.key64[e] = key;
+                a.vtag[e] = tag;
+            }
+            sk[s] = key;
+            si[s] = tag;
+        }
+        __syncthreads();
+        for (int k = 2; k <= kRgmRun; k <<= 1) {        // bitonic sort of (key, element)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = t; i < kRgmRun; i += kRgmThreads) {
+                    const int l = i ^ j;
+                    if (l > i) {
+                        const u64 ki = sk[i], kl = sk[l];
+                        const u32 ti = si[i], tl = si[l];
+                        const bool up = (i & k) == 0;
+                        if (up ? rgm_less(kl, tl, ki, ti) : rgm_less(ki, ti, kl, tl)) {
+                            sk[i] = kl; sk[l] = ki;
+                            si[i] = tl; si[l] = ti;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (int s = t; s < len; s += kRgmThreads) {
+            a.akey[a0 + s] = sk[s];
+            a.atag[a0 + s] = si[s];
+        }
+        return;
+    }
+    // map points (and appended points past the runs, for the fallback sort)
+    const int nb = (int)gridDim.x - kRgmRuns - 1;
+    const int extra = A > kRgmRuns * kRgmRun ? A - kRgmRuns * kRgmRun : 0;
+    bool unsorted = false;
+    for (int g = ((int)blockIdx.x - kRgmRuns - 1) * kRgmThreads + t; g < M + extra; g += nb * kRgmThreads) {
+        if (g >= M) {
+            int c, li;
+            const int e = rgm_app_elem<NC>(V, kRgmRuns * kRgmRun + g - M, c, li);
+            const float4 p = associate(prm, a.ds.at(c)[li]);
+            a.app.at(c)[li] = p;
+            a.key64[e] = rgm_key(p, c, a.leaf.at(c), box);
+            a.vtag[e] = (u32)e | (box.in(p) ? 0u : kRgmDrop);
+            continue;
+        }
+        int c, li;
+        const int e = rgm_old_elem<NC>(V, g, c, li);
+        const float4 p = a.map.at(c)[li];
+        const u64 key = rgm_key(p, c, a.leaf.at(c), box);
+        a.okey[g] = key;
+        a.key64[e] = key;
+        a.vtag[e] = (u32)e | (box.in(p) ? 0u : kRgmDrop);
+        if (g + 1 < M) {                               // still in key order?
+            int c1, li1;
+            (void)rgm_old_elem<NC>(V, g + 1, c1, li1);
+            unsorted |= rgm_key(a.map.at(c1)[li1], c1, a.leaf.at(c1), box) < key;
+        }
+    }
+    if (__any(unsorted) && lane_id() == 0) a.stat[0] = 1;
+}
+
+// lower / upper bound of k in sorted keys[0 .. n)
+__device__ __forceinline__ int rgm_lower(const u64* keys, int n, u64 k) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < k) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int rgm_upper(const u64* keys, int n, u64 k) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] <= k) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Fallback: one 1024-thread workgroup sorts all n (key64, vtag) pairs of element order stably by
+// key into (kout, vout): LSD radix over 8-bit digits, passes whose digit is the same for every key
+// skipped; tiles of 4096 keys ranked as in k_os_pass (a wave's 256 keys by match_bits, wave offsets
+// by one barrier), one running digit base instead of a look-back.
+__device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
+    __shared__ u32 hist[8][256];
+    __shared__ u32 wcnt[kRgmThreads / 64][256];
+    __shared__ u32 gbase[256], toff[256];
+    const int t = threadIdx.x, w = t >> 6, l = lane_id();
+    const u64 lt = lanemask_lt();
+    for (int i = t; i < 8 * 256; i += kRgmThreads) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    for (int i = t; i < n; i += kRgmThreads) {
+        const u64 k = a.key64[i];
+#pragma unroll
+        for (int p = 0; p < 8; ++p) atomicAdd(&hist[p][(u32)(k >> (8 * p)) & 255u], 1u);
+    }
+    __syncthreads();
+    int active[8], P = 0;
+    for (int p = 0; p < 8; ++p) {
+        bool one = false;                              // uniform: every thread reads the same LDS
+        for (int d = 0; d < 256; ++d) one |= hist[p][d] == (u32)n;
+        if (!one) active[P++] = p;
+    }
+    const u64* ks = a.key64;
+    const u32* vs = a.vtag;
+    if (P == 0) {
+        for (int i = t; i < n; i += kRgmThreads) {
+            a.kout[i] = ks[i];
+            a.vout[i] = vs[i];
+        }
+        return;
+    }
+    u64* kd = (P & 1) ? a.kout : a.ktmp;
+    u32* vd = (P & 1) ? a.vout : a.vtmp;
+    for (int pi = 0; pi < P; ++pi) {
+        const int p = active[pi];
+        const int shift = 8 * p;
+        if (t < 256) {                                 // exclusive digit bases
+            u32 s = 0;
+            for (int d = 0; d < t; ++d) s += hist[p][d];
+            gbase[t] = s;
+        }
+        __syncthreads();
+        for (int base = 0; base < n; base += kRgmThreads * 4) {
+            u64 key[4];
+            u32 val[4], rk[4], dg[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = base + w * 256 + r * 64 + l;
+                key[r] = i < n ? ks[i] : 0ull;
+                val[r] = i < n ? vs[i] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) wcnt[w][l + 64 * k] = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool valid = base + w * 256 + r * 64 + l < n;
+                const u32 d = (u32)(key[r] >> shift) & 255u;
+                dg[r] = d;
+                const u64 peers = match_bits(d, 8, valid);
+                const u32 below = (u32)__popcll(peers & lt);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const u32 run = valid ? wcnt[w][d] : 0u;
+                rk[r] = valid ? run + below : 0xFFFFFFFFu;
+                if (valid && below == 0) wcnt[w][d] = run + (u32)__popcll(peers);
+            }
+            __syncthreads();
+            if (t < 256) {
+                u32 acc = 0;
+                for (int ww = 0; ww < kRgmThreads / 64; ++ww) {
+                    const u32 c = wcnt[ww][t];
+                    wcnt[ww][t] = acc;
+                    acc += c;
+                }
+                toff[t] = gbase[t];
+                gbase[t] += acc;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (rk[r] == 0xFFFFFFFFu) continue;
+                const u32 pos = toff[dg[r]] + wcnt[w][dg[r]] + rk[r];
+                kd[pos] = key[r];
+                vd[pos] = val[r];
+            }
+            __syncthreads();
+        }
+        // global writes of this pass before the next pass reads them (one workgroup: a barrier
+        // after the stores have completed)
+        __threadfence_block();
+        __syncthreads();
+        ks = kd;
+        vs = vd;
+        kd = (kd == a.kout) ? a.ktmp : a.kout;
+        vd = (vd == a.vout) ? a.vtmp : a.vout;
+    }
+}
+
+template <int NC>
+__global__ void __launch_bounds__(kRgmThreads) k_rgm_merge(RgmArgs a) {
+    const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
+    const int n = V.total();
+    if (a.stat[0]) {                                   // not mergeable: one workgroup sorts everything
+        if (blockIdx.x == 0) {
+            rgm_fallback_sort(a, n);
+            if (threadIdx.x == 0) a.stat[1]++;
+        }
+        return;
+    }
+    int M = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) M += V.m[c];
+    const int A = n - M;
+    const int nruns = (A + kRgmRun - 1) / kRgmRun;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        if (e < M) {                                   // map point g = e: ties go to the map point
+            const u64 k = a.okey[e];
+            int c, li;
+            const int el = rgm_old_elem<NC>(V, e, c, li);
+            int pos = e;
+            for (int q = 0; q < nruns; ++q)
+                pos += rgm_lower(a.akey + q * kRgmRun, min(kRgmRun, A - q * kRgmRun), k);
+            a.kout[pos] = k;
+            a.vout[pos] = a.vtag[el];
+        } else {                                       // appended point in sorted run q, rank r
+            const int s = e - M, q = s / kRgmRun, r = s - q * kRgmRun;
+            const u64 k = a.akey[s];
+            int pos = rgm_upper(a.okey, M, k) + r;
+            for (int qq = 0; qq < nruns; ++qq) {
+                if (qq == q) continue;
+                const u64* run = a.akey + qq * kRgmRun;
+                const int len = min(kRgmRun, A - qq * kRgmRun);
+                pos += qq < q ? rgm_upper(run, len, k) : rgm_lower(run, len, k);
+            }
+            a.kout[pos] = k;
+            a.vout[pos] = a.atag[s];
+        }
+    }
+}
+
+struct RgTail64Args {
+    int* cnt;
+    Clouds map, app;
+    const u64* keys;       // merged, cnt[C_NRG] of them
+    const u32* vals;       // element | cropped << 31
+    float4* seg_out;
+    int k_new;
+    float theta_p;
+    int theta_max;
+    u64* status;
+    u32* arrive;
+    int* err;
+    int* stat;             // rgm_stat: the fallback flag is cleared here
+};
+
+// k_rg_tail over the merged sequence: cropped elements stay in it, so a voxel's first element is its
+// first uncropped one (no uncropped element of the same key before it) and its walk skips cropped ones
+template <int NC>
+__global__ void __launch_bounds__(256) k_rg_tail64(RgTail64Args a) {
+    constexpr int kPer = kTailPer;
+    __shared__ u32 lw[4];
+    __shared__ u32 s_excl;
+    const RgView<NC> V = rg_view<NC>(a.cnt, a.map, a.app);
+    int* kb = a.cnt + C_NLT;
+    const int n = a.cnt[C_NRG];
+    const int ntiles = (n + kTailTile - 1) / kTailTile;
+    const int t = threadIdx.x;
+    const int G = ntiles < (int)gridDim.x ? ntiles : (int)gridDim.x;
+    if (blockIdx.x == 0 && t == 0) a.stat[0] = 0;
+    if (n == 0) {
+        if (blockIdx.x == 0 && t == 0) {
+            a.cnt[C_KEEP_TOTAL] = 0;
+            kb[0] = kb[1] = kb[2] = 0;
+        }
+        return;
+    }
+    if ((int)blockIdx.x >= G) return;
+    if (blockIdx.x == 0 && t == 0) {                            // classes below the first key's: none
+        const u32 c0 = (u32)(a.keys[0] >> 62);
+        for (u32 b = 1; b <= 3; ++b)
+            if (c0 >= b) kb[b - 1] = 0;
+    }
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int base = tile * kTailTile + t * kPer;
+        u64 k[kPer + 1];                                        // k[0] = predecessor of the first
+        u32 v[kPer + 1];
+        k[0] = base > 0 && base - 1 < n ? a.keys[base - 1] : ~0ull;
+        v[0] = base > 0 && base - 1 < n ? a.vals[base - 1] : kRgmDrop;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            k[j + 1] = base + j < n ? a.keys[base + j] : ~0ull;
+            v[j + 1] = base + j < n ? a.vals[base + j] : kRgmDrop;
+        }
+        float4 pt[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            int c;
+            pt[j] = base + j < n && !(v[j + 1] & kRgmDrop) ? V.at((int)v[j + 1], c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float4 out[kPer];
+        u32 keepm = 0u;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int i = base + j;
+            out[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i >= n || (v[j + 1] & kRgmDrop)) continue;
+            const u64 K = k[j + 1];
+            // a voxel's first uncropped element: no uncropped element of the same key before it
+            bool first = true;
+            if (i > 0 && k[j] == K) {
+                if (!(v[j] & kRgmDrop)) first = false;
+                else
+                    for (int b = i - 2; b >= 0; --b) {
+                        if (a.keys[b] != K) break;
+                        if (!(a.vals[b] & kRgmDrop)) { first = false; break; }
+                    }
+            }
+            if (!first) continue;
+            float cx = 0.f, cy = 0.f, cz = 0.f;                 // Vector4f centroid (:108-125)
+            int r_max = -1;
+            float g_max = -1;
+            int cntv = 0;
+            for (int e = i;;) {
+                float4 p;
+                bool use;
+                if (e - base < kPer) {
+                    use = true;
+#pragma unroll
+                    for (int jj = 0; jj < kPer; ++jj)           // static register index
+                        if (jj == e - base) { p = pt[jj]; use = !(v[jj + 1] & kRgmDrop); }
+                } else {
+                    const u32 ve = a.vals[e];
+                    use = !(ve & kRgmDrop);
+                    int c;
+                    if (use) p = V.at((int)ve, c);
+                }
+                if (use) {
+                    cx += p.x; cy += p.y; cz += p.z;
+                    const int r = (int)w_r(p);
+                    const float g = (float)w_g(p);
+                    if (r > r_max) r_max = r;
+                    if (g > g_max) g_max = g;
+                    ++cntv;
+                }
+                if (++e >= n) break;
+                const u64 ke = e - base < kPer ? k[e - base + 1] : a.keys[e];
+                if (ke != K) break;
+            }
+            const float nn = (float)cntv;
+            const u32 r = (u32)r_max & 255u, g = (u32)g_max & 255u;     // stored into uint8 r, g
+            // extractstablepoint (:12-14) on the voxel's uint8 r, g
+            const bool drop = ((float)g < (float)r * a.theta_p) && ((int)r > a.k_new) && ((int)g < a.theta_max + 1);
+            const u32 aged = r > 250 ? 255u : r + 2u;                   // :634-646
+            out[j] = make_float4(cx / nn, cy / nn, cz / nn, __uint_as_float(pack_rg(aged, g)));
+            if (!drop) keepm |= 1u << j;
+        }
+        u32 agg;
+        const u32 tex = block_excl_scan256((u32)__popc(keepm), lw, agg);
+        if (t < 64) {
+            const u32 excl = tile_lookback(a.status, tile, agg, a.err);
+            if (t == 0) {
+                s_excl = excl;
+                if (tile == ntiles - 1) {
+                    a.cnt[C_KEEP_TOTAL] = (int)(excl + agg);
+                    const u32 cl = (u32)(a.keys[n - 1] >> 62);
+                    for (u32 b = 1; b <= 3; ++b)                // classes above the last key's: all
+                        if (cl < b) kb[b - 1] = (int)(excl + agg);
+                }
+            }
+        }
+        __syncthreads();
+        u32 pos = s_excl + tex;                                 // kept voxels before key base + j
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int i = base + j;
+            if (i >= n) break;
+            const u32 cp = (u32)(k[j] >> 62), cc = (u32)(k[j + 1] >> 62);
+            if (i > 0 && cp < cc)                              // class boundary: kept voxels before it
+                for (u32 b = cp + 1; b <= cc; ++b) kb[b - 1] = (int)pos;
+            if ((keepm >> j) & 1u) a.seg_out[pos++] = out[j];
+        }
+        __syncthreads();
+    }
+    lookback_finish(a.status, ntiles, a.arrive, G);
+}
+
 // initMapWithPoints (ES :217-222, BPF :685-691): append the raw clouds (r = g = 0)
 template <int NC>
 __global__ void __launch_bounds__(256) k_init_map(const int* __restrict__ cnt, Clouds in, CloudsW map) {
@@ -1838,6 +2346,15 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.tailinc, sizeof(u32) * 5 * nq);
     PF_ALLOC(o.poses, sizeof(double) * 7 * o.pose_cap);
     PF_ALLOC(o.stage, sizeof(float4) * nq);
+    PF_ALLOC(o.rgm_okey, sizeof(u64) * nc * map_cap);
+    PF_ALLOC(o.rgm_key64, sizeof(u64) * o.sort_cap);
+    PF_ALLOC(o.rgm_vtag, sizeof(u32) * o.sort_cap);
+    PF_ALLOC(o.rgm_akey, sizeof(u64) * kRgmRuns * kRgmRun);
+    PF_ALLOC(o.rgm_atag, sizeof(u32) * kRgmRuns * kRgmRun);
+    PF_ALLOC(o.rgm_kout, sizeof(u64) * o.sort_cap);
+    PF_ALLOC(o.rgm_ktmp, sizeof(u64) * o.sort_cap);
+    PF_ALLOC(o.rgm_vtmp, sizeof(u32) * o.sort_cap);
+    PF_ALLOC(o.rgm_stat, sizeof(int) * 4);
 #undef PF_ALLOC
     trace_create("buffers");
     if (std::getenv("PF_PROBE")) {                 // development probe: LM phase timestamps
@@ -1866,6 +2383,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (hipMemsetAsync(o.lm_ticket, 0, sizeof(u32) * 2 * kLmEvalSlots, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.tail_status, 0, sizeof(u64) * (o.tail_tiles + 1), o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.rgm_stat, 0, sizeof(int) * 4, o.stream) != hipSuccess) return PF_EHIP;
     // the sub-objects' overflow / wait flags latch into the handle's sticky error words
     alias_err(o.fe.err, o.errw + E_FE_SECTOR);
     alias_err(o.grid.err, o.errw + E_GRID);
@@ -1895,6 +2413,7 @@ int odom_reset(OdomGPU& o) {
     if (hipMemsetAsync(o.lm_ticket, 0, sizeof(u32) * 2 * kLmEvalSlots, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.tail_status, 0, sizeof(u64) * (o.tail_tiles + 1), o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.rgm_stat, 0, sizeof(int) * 4, o.stream) != hipSuccess) return PF_EHIP;
     for (int p = 0; p < kSlots; ++p)
         if (hipMemsetAsync(o.sb[p].cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)o.cls.nc * o.map_cap);
@@ -1943,7 +2462,9 @@ void odom_destroy(OdomGPU& o) {
     }
     void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.seg_out,
                     o.keys, o.vals, o.tail_status, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
-                    o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg, o.errw};
+                    o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg, o.errw,
+                    o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_akey, o.rgm_atag, o.rgm_kout, o.rgm_ktmp,
+                    o.rgm_vtmp, o.rgm_stat};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
     if (o.h_pose) (void)hipHostFree(o.h_pose);
@@ -2050,6 +2571,19 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     }
     // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647, BPF :1197-1290)
     const VgLeaf leaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}};
+    if (!o.tie_order && !o.rg_radix) {                    // rgbds by merge (the map stays in key order)
+        RgmArgs ra{o.st, cnt, o.acc, clouds(o.map), clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap, leaf,
+                   o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_akey, o.rgm_atag, o.rgm_kout, o.vals, o.rgm_ktmp,
+                   o.rgm_vtmp, o.rgm_stat};
+        PF_LAUNCH_NC(nc, k_rgm_keys, dim3(kRgmRuns + 1 + kRgmOldBlocks), dim3(kRgmThreads), 0, s, ra);
+        PF_LAUNCH_NC(nc, k_rgm_merge, dim3(kRgmMergeBlocks), dim3(kRgmThreads), 0, s, ra);
+        RgTail64Args ta{cnt, clouds(o.map), clouds(o.app), o.rgm_kout, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,
+                        o.prm.theta_max, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err, o.rgm_stat};
+        const unsigned tail_grid = (unsigned)(o.tail_tiles < (size_t)kSortMaxBlocks ? o.tail_tiles : kSortMaxBlocks);
+        PF_LAUNCH_NC(nc, k_rg_tail64, dim3(tail_grid > 0 ? tail_grid : 1), dim3(256), 0, s, ta);
+        PF_LAUNCH_NC(nc, k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, clouds_w(o.map));
+        return;
+    }
     if (rg_fused_keys(o.leaf_rg, nc)) {
         PF_LAUNCH_NC(nc, k_rg_append_keys, dim3(kGrid + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map),
                      clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap, leaf, o.keys, o.vals,

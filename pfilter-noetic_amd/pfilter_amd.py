@@ -138,7 +138,8 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_odom_restore", "pf_odom_set_map_export", "pf_odom_map_export", "pf_odom_set_stage_timing",
            "pf_odom_stage_times", "pf_odom_set_state", "pf_cls_normals", "pf_dcvc_default_params",
            "pf_dcvc_create", "pf_dcvc_destroy", "pf_dcvc_run", "pf_dcvc_reset", "pf_cls_set_dcvc", "pf_bpf_set_dcvc",
-           "pf_host_alloc", "pf_host_free", "pf_odom_set_tie_order", "pf_odom_probe_assoc"]
+           "pf_host_alloc", "pf_host_free", "pf_odom_set_tie_order", "pf_odom_probe_assoc",
+           "pf_odom_merge_stats"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -199,6 +200,7 @@ def lib():
     L.pf_odom_set_tie_order.argtypes = [_vp, _i]
     L.pf_odom_probe_assoc.argtypes = [_vp, _i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(_sz), _vp, _sz]
+    L.pf_odom_merge_stats.argtypes = [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]
     L.pf_dev_tie_sort.argtypes = [_i, _vp, _sz, _vp, ctypes.POINTER(_sz)]
     L.pf_host_alloc.argtypes = [_sz, ctypes.POINTER(_vp)]
     L.pf_host_free.argtypes = [_vp]
@@ -530,6 +532,18 @@ class Odom_ES_EstimationClass:
         if queries:
             return ms.value, b.value, n.value, q[:n.value].copy()
         return ms.value, b.value, n.value
+
+    def set_rg_radix(self, enable):
+        """development switch pf_dev_set_rg_radix: rgbds by the full radix sort instead of the merge"""
+        L = lib()
+        L.pf_dev_set_rg_radix.argtypes = [_vp, _i]
+        _check("pf_dev_set_rg_radix", L.pf_dev_set_rg_radix(self._h, int(bool(enable))))
+
+    def merge_stats(self):
+        """pf_odom_merge_stats: (updates that sorted every element, largest appended-point count)"""
+        f, m = _i(), _i()
+        _check("pf_odom_merge_stats", lib().pf_odom_merge_stats(self._h, ctypes.byref(f), ctypes.byref(m)))
+        return f.value, m.value
 
     def set_tie_order(self, enable):
         """pf_odom_set_tie_order: VoxelGrid / rgbds order equal keys as libstdc++ std::sort (parity mode)"""
