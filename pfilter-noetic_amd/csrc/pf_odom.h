@@ -95,9 +95,6 @@ struct LMState {
     int iteration, invalid, reuse, done, phase, n_res, pad0, pad1;
 };
 
-// rgbds merge: the appended points are sorted in runs of kRgmRun by one 1024-thread workgroup each
-constexpr int kRgmRun = 4096;
-constexpr int kRgmRuns = 16;
 constexpr int kLmParts = 30;   // cost, g[6], H[21], bad_r, bad_J
 constexpr int kLmEvalSlots = 8; // LM claim masks per solve (>= evaluations per solve)
 constexpr int kLmEvals = 5;      // evaluations per solve: 1 + max_num_iterations (4)
@@ -194,13 +191,11 @@ struct OdomGPU {
     u32 *keys = nullptr, *vals = nullptr;
     u64* tail_status = nullptr;   // k_rg_tail look-back words [tail_tiles] + arrival counter
     size_t tail_tiles = 0;
-    // rgbds by merge (k_rgm_keys / k_rgm_merge / k_rg_tail64, the default order): the map is kept in
-    // voxel order, so only this frame's appended points are sorted and then merged into it
+    // rgbds by merge (k_rgm_bucket / k_rgm_fallback / k_rg_tail64, the default order): the map is kept
+    // in voxel order, so only this frame's appended points are sorted and then merged into it
     u64* rgm_okey = nullptr;       // [nc * map_cap] voxel keys of the map points, map order
     u64* rgm_key64 = nullptr;      // [sort_cap] voxel keys of every element, element order
     u32* rgm_vtag = nullptr;       // [sort_cap] element index | cropped << 31
-    u64* rgm_akey = nullptr;       // [kRgmRuns * kRgmRun] sorted runs of the appended points
-    u32* rgm_atag = nullptr;
     u64* rgm_kout = nullptr;       // [sort_cap] merged keys (vals: `vals`)
     u64* rgm_ktmp = nullptr;       // [sort_cap] fallback sort scratch
     u32* rgm_vtmp = nullptr;

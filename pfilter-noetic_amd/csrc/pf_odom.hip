@@ -1689,18 +1689,22 @@ __global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const f
 // the reference-tie-order mode keeps the radix path above). The voxel index orders voxels
 // lexicographically by (z, y, x) on any grid covering the points (k_rg_append_keys), so the 64-bit key
 // class << 62 | z << 40 | y << 20 | x of the voxel coordinates (20 bits each, biased) orders them the
-// same way on every frame. The map that the previous rgbds wrote is already in that order (its points
-// are voxel centroids, written in key order), so only the appended points need sorting: k_rgm_keys
-// sorts them in runs of kRgmRun (one 1024-thread workgroup per run, a bitonic network in LDS) while
-// the other workgroups key the map points and check that they are still in order; k_rgm_merge places
-// every element by binary searches; k_rg_tail64 reduces the voxels. Cropped elements stay in the
-// merged sequence, flagged, and are skipped by the reduction. When the map is not in key order (the
-// first update after initMapWithPoints or pf_odom_set_map, or a centroid that rounds into a
-// neighbouring voxel) or more points are appended than the runs hold, k_rgm_merge's first workgroup
-// sorts all elements itself (a stable LSD radix sort over the 64-bit keys) instead.
+// same way on every frame. The map the previous rgbds wrote is already in that order (its points are
+// voxel centroids written in key order), so the map's own keys split the key range into kRgmBuckets
+// buckets of equal map-point counts, and one workgroup per bucket does everything for it with no
+// exchange between workgroups: it keys its map points and checks their order, scans all appended
+// points (transforming them, as pointAssociateToMap :592-604) keeping those of its bucket and counting
+// those below it, sorts its appended points by (key, element) in registers and LDS (a bitonic network,
+// shuffles within a wave), and places every element by binary searches in its own bucket. Cropped
+// elements stay in the merged sequence, flagged, and k_rg_tail64 skips them. When the map is not in
+// key order (the first update after initMapWithPoints or pf_odom_set_map, or a centroid that rounded
+// into a neighbouring voxel) or a bucket holds more than kRgmBucketCap appended points, the placement
+// is void and k_rgm_fallback's single workgroup sorts every element (a stable LSD radix sort over the
+// 64-bit keys) instead.
 constexpr int kRgmThreads = 1024;
-constexpr int kRgmOldBlocks = 256;
-constexpr int kRgmMergeBlocks = 64;
+constexpr int kRgmBuckets = 32;
+constexpr int kRgmBucketCap = 4096;     // appended points a bucket sorts
+constexpr int kRgmOldLds = 4096;        // map points of a bucket cached in LDS for the searches
 constexpr u32 kRgmDrop = 0x80000000u;
 
 struct RgmArgs {
@@ -1715,8 +1719,6 @@ struct RgmArgs {
     u64* okey;             // [map points] keys, map order
     u64* key64;            // [elements] keys, element order
     u32* vtag;             // [elements] element | cropped << 31
-    u64* akey;             // [kRgmRuns * kRgmRun] sorted runs of the appended points
-    u32* atag;
     u64* kout;             // merged keys / tags (-> k_rg_tail64)
     u32* vout;
     u64* ktmp;             // fallback scratch
@@ -1724,18 +1726,19 @@ struct RgmArgs {
     int* stat;             // [4] (OdomGPU::rgm_stat)
 };
 
-// the frame's crop box and its voxel origin per class (as k_rg_append_keys)
+// the frame's crop box (as k_rg_append_keys)
 struct RgmBox {
     float lo[3], hi[3];
     __device__ __forceinline__ bool in(float4 p) const {
         return !((p.x < lo[0] || p.y < lo[1] || p.z < lo[2]) || (p.x > hi[0] || p.y > hi[1] || p.z > hi[2]));
     }
 };
-__device__ __forceinline__ RgmBox rgm_box(const double* prm) {
+__device__ __forceinline__ RgmBox rgm_box(const DevState* st) {
     RgmBox b;
+#pragma unroll
     for (int k = 0; k < 3; ++k) {
-        b.lo[k] = (float)(prm[4 + k] - 100);
-        b.hi[k] = (float)(prm[4 + k] + 100);
+        b.lo[k] = (float)(st->params[4 + k] - 100);
+        b.hi[k] = (float)(st->params[4 + k] + 100);
     }
     return b;
 }
@@ -1784,107 +1787,14 @@ __device__ __forceinline__ int rgm_app_elem(const RgView<NC>& V, int a, int& c, 
     const int mc = sel3(c, V.m[0], V.m[1], V.m[2]);
     return start + mc + li;
 }
-
-// blocks [0, kRgmRuns): one run of appended points each; block kRgmRuns: the pose step (as in
-// k_rg_append_keys); the rest: the map points (keys, crop flags, order check)
 template <int NC>
-__global__ void __launch_bounds__(kRgmThreads) k_rgm_keys(RgmArgs a) {
-    __shared__ u64 sk[kRgmRun];
-    __shared__ u32 si[kRgmRun];
-    double prm[7];
-    for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
-    const int t = threadIdx.x;
-    const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
-    const int n = V.total();
-    int M = 0;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) M += V.m[c];
-    const int A = n - M;
-    const RgmBox box = rgm_box(prm);
-    if (blockIdx.x == kRgmRuns) {
-        finalize_pose(a.st, a.poses, a.pose_cap, 1, a.acc, prm);
-        if (t == 0) {
-            a.cnt[C_NRG] = n;
-            if (A > a.stat[2]) a.stat[2] = A;
-            if (A > kRgmRuns * kRgmRun) a.stat[0] = 1;
-        }
-        return;
-    }
-    if (blockIdx.x < kRgmRuns) {                       // a run of appended points
-        const int a0 = (int)blockIdx.x * kRgmRun;
-        if (a0 >= A) return;
-        const int len = min(kRgmRun, A - a0);
-        for (int s = t; s < kRgmRun; s += kRgmThreads) {
-            u64 key = ~0ull;
-            u32 tag = ~0u;
-            if (s < len) {
-                int c, li;
-                const int e = rgm_app_elem<NC>(V, a0 + s, c, li);
-                const float4 p = associate(prm, a.ds.at(c)[li]);   // pointAssociateToMap (:592-604)
-                a.app.at(c)[li] = p;
-                key = rgm_key(p, c, a.leaf.at(c), box);
-                tag = (u32)e | (box.in(p) ? 0u : kRgmDrop);
-                a.key64[e] = key;
-                a.vtag[e] = tag;
-            }
-            sk[s] = key;
-            si[s] = tag;
-        }
-        __syncthreads();
-        for (int k = 2; k <= kRgmRun; k <<= 1) {        // bitonic sort of (key, element)
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = t; i < kRgmRun; i += kRgmThreads) {
-                    const int l = i ^ j;
-                    if (l > i) {
-                        const u64 ki = sk[i], kl = sk[l];
-                        const u32 ti = si[i], tl = si[l];
-                        const bool up = (i & k) == 0;
-                        if (up ? rgm_less(kl, tl, ki, ti) : rgm_less(ki, ti, kl, tl)) {
-                            sk[i] = kl; sk[l] = ki;
-                            si[i] = tl; si[l] = ti;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        for (int s = t; s < len; s += kRgmThreads) {
-            a.akey[a0 + s] = sk[s];
-            a.atag[a0 + s] = si[s];
-        }
-        return;
-    }
-    // map points (and appended points past the runs, for the fallback sort)
-    const int nb = (int)gridDim.x - kRgmRuns - 1;
-    const int extra = A > kRgmRuns * kRgmRun ? A - kRgmRuns * kRgmRun : 0;
-    bool unsorted = false;
-    for (int g = ((int)blockIdx.x - kRgmRuns - 1) * kRgmThreads + t; g < M + extra; g += nb * kRgmThreads) {
-        if (g >= M) {
-            int c, li;
-            const int e = rgm_app_elem<NC>(V, kRgmRuns * kRgmRun + g - M, c, li);
-            const float4 p = associate(prm, a.ds.at(c)[li]);
-            a.app.at(c)[li] = p;
-            a.key64[e] = rgm_key(p, c, a.leaf.at(c), box);
-            a.vtag[e] = (u32)e | (box.in(p) ? 0u : kRgmDrop);
-            continue;
-        }
-        int c, li;
-        const int e = rgm_old_elem<NC>(V, g, c, li);
-        const float4 p = a.map.at(c)[li];
-        const u64 key = rgm_key(p, c, a.leaf.at(c), box);
-        a.okey[g] = key;
-        a.key64[e] = key;
-        a.vtag[e] = (u32)e | (box.in(p) ? 0u : kRgmDrop);
-        if (g + 1 < M) {                               // still in key order?
-            int c1, li1;
-            (void)rgm_old_elem<NC>(V, g + 1, c1, li1);
-            unsorted |= rgm_key(a.map.at(c1)[li1], c1, a.leaf.at(c1), box) < key;
-        }
-    }
-    if (__any(unsorted) && lane_id() == 0) a.stat[0] = 1;
+__device__ __forceinline__ u64 rgm_old_key(const RgView<NC>& V, const VgLeaf& leaf, const RgmBox& box, int g) {
+    int c, li;
+    (void)rgm_old_elem<NC>(V, g, c, li);
+    return rgm_key(V.map.at(c)[li], c, leaf.at(c), box);
 }
 
-// lower / upper bound of k in sorted keys[0 .. n)
+// lower / upper bound of k in sorted keys[0 .. n) (LDS or global)
 __device__ __forceinline__ int rgm_lower(const u64* keys, int n, u64 k) {
     int lo = 0, hi = n;
     while (lo < hi) {
@@ -1904,6 +1814,175 @@ __device__ __forceinline__ int rgm_upper(const u64* keys, int n, u64 k) {
     return lo;
 }
 
+// block b < kRgmBuckets: bucket b (map points [lo, hi) = [b M / R, (b + 1) M / R), appended points
+// with key in [key(lo), key(hi))); block kRgmBuckets: the pose step (as in k_rg_append_keys)
+template <int NC>
+__global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
+    __shared__ u64 bk[kRgmBucketCap];
+    __shared__ u32 bt[kRgmBucketCap];
+    __shared__ u64 ok[kRgmOldLds];
+    __shared__ u64 s_split[kRgmBuckets];
+    __shared__ int s_cnt, s_before[kRgmThreads / 64];
+    const int t = threadIdx.x, b = blockIdx.x;
+    const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
+    const int n = V.total();
+    int M = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) M += V.m[c];
+    const int A = n - M;
+    if (b == kRgmBuckets) {
+        double prm[7];
+        for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
+        finalize_pose(a.st, a.poses, a.pose_cap, 1, a.acc, prm);
+        if (t == 0) {
+            a.cnt[C_NRG] = n;
+            if (A > a.stat[2]) a.stat[2] = A;
+        }
+        return;
+    }
+    double prm[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
+    const RgmBox box = rgm_box(a.st);
+    const int lo = (int)(((long long)b * M) / kRgmBuckets), hi = (int)(((long long)(b + 1) * M) / kRgmBuckets);
+    const int nold = hi - lo;
+    const bool cache = nold <= kRgmOldLds;
+    // 1. this bucket's map points: keys, crop flags, still in key order?
+    bool unsorted = false;
+    for (int g = lo + t; g < hi; g += kRgmThreads) {
+        int c, li;
+        const int e = rgm_old_elem<NC>(V, g, c, li);
+        const float4 p = a.map.at(c)[li];
+        const u64 key = rgm_key(p, c, a.leaf.at(c), box);
+        a.okey[g] = key;
+        if (cache) ok[g - lo] = key;
+        a.key64[e] = key;
+        a.vtag[e] = (u32)e | (box.in(p) ? 0u : kRgmDrop);
+        if (g + 1 < M) unsorted |= rgm_old_key<NC>(V, a.leaf, box, g + 1) < key;
+    }
+    if (t < kRgmBuckets) {                             // every bucket's lower splitter (the key of its first map point)
+        const int lt_ = (int)(((long long)t * M) / kRgmBuckets);
+        s_split[t] = t == 0 ? 0ull : (lt_ >= M ? ~0ull : rgm_old_key<NC>(V, a.leaf, box, lt_));
+    }
+    if (t == 0) s_cnt = 0;
+    if (__any(unsorted) && lane_id() == 0) a.stat[0] = 1;
+    __syncthreads();
+    // 2. every appended point: its bucket is the number of splitters 1 .. R - 1 at or below its key (a
+    // binary search; on keys out of order still one bucket per point, so the fallback sees every key);
+    // those of lower buckets are counted, this bucket's kept
+    int before = 0;
+    for (int q = t; q < A; q += kRgmThreads) {
+        int c, li;
+        const int e = rgm_app_elem<NC>(V, q, c, li);
+        const float4 p = associate(prm, a.ds.at(c)[li]);
+        const u64 key = rgm_key(p, c, a.leaf.at(c), box);
+        int o = 0;                                    // largest bucket with s_split[o] <= key
+#pragma unroll
+        for (int step = kRgmBuckets / 2; step > 0; step >>= 1)
+            if (s_split[o + step] <= key) o += step;
+        if (o < b) {
+            ++before;
+        } else if (o == b) {
+            a.app.at(c)[li] = p;
+            const u32 tag = (u32)e | (box.in(p) ? 0u : kRgmDrop);
+            a.key64[e] = key;
+            a.vtag[e] = tag;
+            const int slot = atomicAdd(&s_cnt, 1);
+            if (slot < kRgmBucketCap) {
+                bk[slot] = key;
+                bt[slot] = tag;
+            }
+        }
+    }
+    before = wave_sum_i(before);
+    if (lane_id() == 0) s_before[t >> 6] = before;
+    __syncthreads();
+    int nbefore = 0;
+#pragma unroll
+    for (int w = 0; w < kRgmThreads / 64; ++w) nbefore += s_before[w];
+    const int cb = s_cnt;
+    if (cb > kRgmBucketCap) {                            // too many for the bucket: the fallback sorts
+        if (t == 0) a.stat[0] = 1;
+        return;
+    }
+    // 3. sort the bucket's appended points by (key, element)
+    if (cb <= kRgmThreads) {
+        // one element per thread; partners within a wave by shuffles, across waves through LDS
+        u64 k = t < cb ? bk[t] : ~0ull;
+        u32 g = t < cb ? bt[t] : ~0u;
+        __syncthreads();
+        for (int kk = 2; kk <= kRgmThreads; kk <<= 1) {
+            for (int j = kk >> 1; j > 0; j >>= 1) {
+                u64 pk;
+                u32 pg;
+                if (j < 64) {
+                    const u32 lo32 = (u32)__shfl_xor((int)(u32)k, j, 64), hi32 = (u32)__shfl_xor((int)(u32)(k >> 32), j, 64);
+                    pk = ((u64)hi32 << 32) | lo32;
+                    pg = (u32)__shfl_xor((int)g, j, 64);
+                } else {
+                    bk[t] = k;
+                    bt[t] = g;
+                    __syncthreads();
+                    pk = bk[t ^ j];
+                    pg = bt[t ^ j];
+                    __syncthreads();
+                }
+                const bool up = (t & kk) == 0, lower = (t & j) == 0;
+                const bool pless = rgm_less(pk, pg, k, g);
+                // the lower index of an ascending pair keeps the smaller element
+                if ((lower == up) ? pless : !pless && !(pk == k && pg == g)) {
+                    k = pk;
+                    g = pg;
+                }
+            }
+        }
+        bk[t] = k;
+        bt[t] = g;
+    } else {
+        int S = kRgmThreads;
+        while (S < cb) S <<= 1;
+        for (int i = cb + t; i < S; i += kRgmThreads) {
+            bk[i] = ~0ull;
+            bt[i] = ~0u;
+        }
+        __syncthreads();
+        for (int kk = 2; kk <= S; kk <<= 1)
+            for (int j = kk >> 1; j > 0; j >>= 1) {
+                for (int i = t; i < S; i += kRgmThreads) {
+                    const int l = i ^ j;
+                    if (l > i) {
+                        const u64 ki = bk[i], kl = bk[l];
+                        const u32 ti = bt[i], tl = bt[l];
+                        const bool up = (i & kk) == 0;
+                        if (up ? rgm_less(kl, tl, ki, ti) : rgm_less(ki, ti, kl, tl)) {
+                            bk[i] = kl; bk[l] = ki;
+                            bt[i] = tl; bt[l] = ti;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+    }
+    __syncthreads();
+    // 4. place: a map point after the appended points below it (ties: the map point first), an
+    // appended point after the map points at or below it
+    for (int g = lo + t; g < hi; g += kRgmThreads) {
+        const u64 key = cache ? ok[g - lo] : a.okey[g];
+        int c, li;
+        const int e = rgm_old_elem<NC>(V, g, c, li);
+        const int pos = g + nbefore + rgm_lower(bk, cb, key);
+        a.kout[pos] = key;
+        a.vout[pos] = a.vtag[e];
+    }
+    for (int r = t; r < cb; r += kRgmThreads) {
+        const u64 key = bk[r];
+        const int below = cache ? rgm_upper(ok, nold, key) : rgm_upper(a.okey + lo, nold, key);
+        const int pos = lo + below + nbefore + r;
+        a.kout[pos] = key;
+        a.vout[pos] = bt[r];
+    }
+}
+
 // Fallback: one 1024-thread workgroup sorts all n (key64, vtag) pairs of element order stably by
 // key into (kout, vout): LSD radix over 8-bit digits, passes whose digit is the same for every key
 // skipped; tiles of 4096 keys ranked as in k_os_pass (a wave's 256 keys by match_bits, wave offsets
@@ -1912,9 +1991,11 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
     __shared__ u32 hist[8][256];
     __shared__ u32 wcnt[kRgmThreads / 64][256];
     __shared__ u32 gbase[256], toff[256];
+    __shared__ int s_one[8];
     const int t = threadIdx.x, w = t >> 6, l = lane_id();
     const u64 lt = lanemask_lt();
     for (int i = t; i < 8 * 256; i += kRgmThreads) (&hist[0][0])[i] = 0;
+    if (t < 8) s_one[t] = 0;
     __syncthreads();
     for (int i = t; i < n; i += kRgmThreads) {
         const u64 k = a.key64[i];
@@ -1922,12 +2003,12 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
         for (int p = 0; p < 8; ++p) atomicAdd(&hist[p][(u32)(k >> (8 * p)) & 255u], 1u);
     }
     __syncthreads();
+    for (int i = t; i < 8 * 256; i += kRgmThreads)
+        if ((&hist[0][0])[i] == (u32)n) s_one[i >> 8] = 1;       // a digit the same for every key
+    __syncthreads();
     int active[8], P = 0;
-    for (int p = 0; p < 8; ++p) {
-        bool one = false;                              // uniform: every thread reads the same LDS
-        for (int d = 0; d < 256; ++d) one |= hist[p][d] == (u32)n;
-        if (!one) active[P++] = p;
-    }
+    for (int p = 0; p < 8; ++p)
+        if (!s_one[p]) active[P++] = p;
     const u64* ks = a.key64;
     const u32* vs = a.vtag;
     if (P == 0) {
@@ -1992,8 +2073,7 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
             }
             __syncthreads();
         }
-        // global writes of this pass before the next pass reads them (one workgroup: a barrier
-        // after the stores have completed)
+        // this pass's global stores before the next pass reads them (one workgroup)
         __threadfence_block();
         __syncthreads();
         ks = kd;
@@ -2004,45 +2084,11 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
 }
 
 template <int NC>
-__global__ void __launch_bounds__(kRgmThreads) k_rgm_merge(RgmArgs a) {
+__global__ void __launch_bounds__(kRgmThreads) k_rgm_fallback(RgmArgs a) {
+    if (!a.stat[0]) return;                            // the buckets' placement stands
     const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
-    const int n = V.total();
-    if (a.stat[0]) {                                   // not mergeable: one workgroup sorts everything
-        if (blockIdx.x == 0) {
-            rgm_fallback_sort(a, n);
-            if (threadIdx.x == 0) a.stat[1]++;
-        }
-        return;
-    }
-    int M = 0;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) M += V.m[c];
-    const int A = n - M;
-    const int nruns = (A + kRgmRun - 1) / kRgmRun;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-        if (e < M) {                                   // map point g = e: ties go to the map point
-            const u64 k = a.okey[e];
-            int c, li;
-            const int el = rgm_old_elem<NC>(V, e, c, li);
-            int pos = e;
-            for (int q = 0; q < nruns; ++q)
-                pos += rgm_lower(a.akey + q * kRgmRun, min(kRgmRun, A - q * kRgmRun), k);
-            a.kout[pos] = k;
-            a.vout[pos] = a.vtag[el];
-        } else {                                       // appended point in sorted run q, rank r
-            const int s = e - M, q = s / kRgmRun, r = s - q * kRgmRun;
-            const u64 k = a.akey[s];
-            int pos = rgm_upper(a.okey, M, k) + r;
-            for (int qq = 0; qq < nruns; ++qq) {
-                if (qq == q) continue;
-                const u64* run = a.akey + qq * kRgmRun;
-                const int len = min(kRgmRun, A - qq * kRgmRun);
-                pos += qq < q ? rgm_upper(run, len, k) : rgm_lower(run, len, k);
-            }
-            a.kout[pos] = k;
-            a.vout[pos] = a.atag[s];
-        }
-    }
+    rgm_fallback_sort(a, V.total());
+    if (threadIdx.x == 0) a.stat[1]++;
 }
 
 struct RgTail64Args {
@@ -2349,8 +2395,6 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.rgm_okey, sizeof(u64) * nc * map_cap);
     PF_ALLOC(o.rgm_key64, sizeof(u64) * o.sort_cap);
     PF_ALLOC(o.rgm_vtag, sizeof(u32) * o.sort_cap);
-    PF_ALLOC(o.rgm_akey, sizeof(u64) * kRgmRuns * kRgmRun);
-    PF_ALLOC(o.rgm_atag, sizeof(u32) * kRgmRuns * kRgmRun);
     PF_ALLOC(o.rgm_kout, sizeof(u64) * o.sort_cap);
     PF_ALLOC(o.rgm_ktmp, sizeof(u64) * o.sort_cap);
     PF_ALLOC(o.rgm_vtmp, sizeof(u32) * o.sort_cap);
@@ -2463,7 +2507,7 @@ void odom_destroy(OdomGPU& o) {
     void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.seg_out,
                     o.keys, o.vals, o.tail_status, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
                     o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg, o.errw,
-                    o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_akey, o.rgm_atag, o.rgm_kout, o.rgm_ktmp,
+                    o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.rgm_ktmp,
                     o.rgm_vtmp, o.rgm_stat};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
@@ -2573,10 +2617,9 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     const VgLeaf leaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}};
     if (!o.tie_order && !o.rg_radix) {                    // rgbds by merge (the map stays in key order)
         RgmArgs ra{o.st, cnt, o.acc, clouds(o.map), clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap, leaf,
-                   o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_akey, o.rgm_atag, o.rgm_kout, o.vals, o.rgm_ktmp,
-                   o.rgm_vtmp, o.rgm_stat};
-        PF_LAUNCH_NC(nc, k_rgm_keys, dim3(kRgmRuns + 1 + kRgmOldBlocks), dim3(kRgmThreads), 0, s, ra);
-        PF_LAUNCH_NC(nc, k_rgm_merge, dim3(kRgmMergeBlocks), dim3(kRgmThreads), 0, s, ra);
+                   o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp, o.rgm_stat};
+        PF_LAUNCH_NC(nc, k_rgm_bucket, dim3(kRgmBuckets + 1), dim3(kRgmThreads), 0, s, ra);
+        PF_LAUNCH_NC(nc, k_rgm_fallback, dim3(1), dim3(kRgmThreads), 0, s, ra);
         RgTail64Args ta{cnt, clouds(o.map), clouds(o.app), o.rgm_kout, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,
                         o.prm.theta_max, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err, o.rgm_stat};
         const unsigned tail_grid = (unsigned)(o.tail_tiles < (size_t)kSortMaxBlocks ? o.tail_tiles : kSortMaxBlocks);
