@@ -2196,7 +2196,14 @@ __global__ void __launch_bounds__(256) k_rg_tail64(RgTail64Args a) {
                     ++cntv;
                 }
                 if (++e >= n) break;
-                const u64 ke = e - base < kPer ? k[e - base + 1] : a.keys[e];
+                u64 ke;
+                if (e - base < kPer) {
+#pragma unroll
+                    for (int jj = 0; jj < kPer; ++jj)           // static register index
+                        if (jj == e - base) ke = k[jj + 1];
+                } else {
+                    ke = a.keys[e];
+                }
                 if (ke != K) break;
             }
             const float nn = (float)cntv;
