@@ -191,15 +191,18 @@ struct OdomGPU {
     u32 *keys = nullptr, *vals = nullptr;
     u64* tail_status = nullptr;   // k_rg_tail look-back words [tail_tiles] + arrival counter
     size_t tail_tiles = 0;
-    // rgbds by merge (k_rgm_bucket / k_rgm_fallback / k_rg_tail64, the default order): the map is kept
+    // rgbds by merge (k_rgm_bucket / k_rgm_fallback, the default order): the map is kept
     // in voxel order, so only this frame's appended points are sorted and then merged into it
     u64* rgm_okey = nullptr;       // [nc * map_cap] voxel keys of the map points, map order
     u64* rgm_key64 = nullptr;      // [sort_cap] voxel keys of every element, element order
     u32* rgm_vtag = nullptr;       // [sort_cap] element index | cropped << 31
-    u64* rgm_kout = nullptr;       // [sort_cap] merged keys (vals: `vals`)
+    float4* rgm_vox = nullptr;     // [sort_cap] voxel outputs at merged positions
+    u32* rgm_kflag = nullptr;      // [sort_cap] kept flags / ranks at merged positions
+    u64* rgm_kout = nullptr;       // [sort_cap] fallback: sorted keys (vals: `vals`)
     u64* rgm_ktmp = nullptr;       // [sort_cap] fallback sort scratch
     u32* rgm_vtmp = nullptr;
-    int* rgm_stat = nullptr;       // [4]: fallback this frame, fallbacks so far, largest append, spare
+    int* rgm_stat = nullptr;       // [8]: fallback this frame, fallbacks so far, largest append, spare,
+                                   // kept voxels per class (accumulated over the buckets)
 
     int* nbr = nullptr;            // [5 * kMaxC * in_cap]
     int* qflag = nullptr;          // bit0 valid association, bit1 kept

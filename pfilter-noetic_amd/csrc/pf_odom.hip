@@ -1686,25 +1686,26 @@ __global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const f
 // ---------------------------- rgbds by merge (the default order) ----------------------------
 // addPointsToMap's rgbds (:606-626, :34-134) orders the elements (map points, then this frame's
 // appended points, per class) by voxel index and, within a voxel, by element index (the stable order;
-// the reference-tie-order mode keeps the radix path above). The voxel index orders voxels
-// lexicographically by (z, y, x) on any grid covering the points (k_rg_append_keys), so the 64-bit key
-// class << 62 | z << 40 | y << 20 | x of the voxel coordinates (20 bits each, biased) orders them the
-// same way on every frame. The map the previous rgbds wrote is already in that order (its points are
-// voxel centroids written in key order), so the map's own keys split the key range into kRgmBuckets
-// buckets of equal map-point counts, and one workgroup per bucket does everything for it with no
-// exchange between workgroups: it keys its map points and checks their order, scans all appended
-// points (transforming them, as pointAssociateToMap :592-604) keeping those of its bucket and counting
-// those below it, sorts its appended points by (key, element) in registers and LDS (a bitonic network,
-// shuffles within a wave), and places every element by binary searches in its own bucket. Cropped
-// elements stay in the merged sequence, flagged, and k_rg_tail64 skips them. When the map is not in
-// key order (the first update after initMapWithPoints or pf_odom_set_map, or a centroid that rounded
-// into a neighbouring voxel) or a bucket holds more than kRgmBucketCap appended points, the placement
-// is void and k_rgm_fallback's single workgroup sorts every element (a stable LSD radix sort over the
-// 64-bit keys) instead.
+// the reference-tie-order mode keeps the radix path above), then reduces every voxel. The voxel index
+// orders voxels lexicographically by (z, y, x) on any grid covering the points (k_rg_append_keys), so
+// the 64-bit key class << 62 | z << 40 | y << 20 | x of the voxel coordinates (20 bits each, biased)
+// orders them the same way on every frame. The map the previous rgbds wrote is already in that order
+// (its points are voxel centroids written in key order), so the map's own keys split the key range into
+// kRgmBuckets buckets of equal map-point counts, and one workgroup per bucket does all of its work:
+// it keys its map points and checks their order; scans every appended point (pointAssociateToMap
+// :592-604), keeping those of its bucket and counting those below it; sorts its appended points by
+// (key, element) in registers and LDS (a bitonic network, shuffles within a wave); reduces the voxels
+// of its bucket (the Vector4f centroid and r / g maxima of :108-125, extractstablepoint :12-14, the
+// ageing :634-646, cropped elements skipped); ranks the kept voxels in merged order and places them by
+// a look-back over the buckets; the last bucket to finish writes the class boundaries. When the map
+// is not in key order (the first update after initMapWithPoints or pf_odom_set_map, or a centroid that
+// rounded into a neighbouring voxel) or a bucket holds more than kRgmBucketCap appended points, the
+// buckets' output is void and k_rgm_fallback's single workgroup sorts every element (a stable LSD
+// radix sort over the 64-bit keys) and reduces the voxels itself.
 constexpr int kRgmThreads = 1024;
 constexpr int kRgmBuckets = 32;
 constexpr int kRgmBucketCap = 4096;     // appended points a bucket sorts
-constexpr int kRgmOldLds = 4096;        // map points of a bucket cached in LDS for the searches
+constexpr int kRgmOldLds = 4096;        // map points of a bucket cached in LDS
 constexpr u32 kRgmDrop = 0x80000000u;
 
 struct RgmArgs {
@@ -1716,14 +1717,23 @@ struct RgmArgs {
     double* poses;
     int pose_cap;
     VgLeaf leaf;
+    int k_new;
+    float theta_p;
+    int theta_max;
     u64* okey;             // [map points] keys, map order
-    u64* key64;            // [elements] keys, element order
+    u64* key64;            // [elements] keys, element order (for the fallback)
     u32* vtag;             // [elements] element | cropped << 31
-    u64* kout;             // merged keys / tags (-> k_rg_tail64)
+    float4* vox;           // [elements] a voxel's output at its merged position
+    u32* kflag;            // [elements] kept flag, then rank + 1, at merged positions
+    float4* seg_out;       // the kept voxels in key order (-> k_rg_write)
+    u64* status;           // look-back words over the buckets (zero between calls) + arrival counter
+    u32* arrive;
+    int* err;
+    u64* kout;             // fallback: sorted keys / tags and scratch
     u32* vout;
-    u64* ktmp;             // fallback scratch
+    u64* ktmp;
     u32* vtmp;
-    int* stat;             // [4] (OdomGPU::rgm_stat)
+    int* stat;             // [8] (OdomGPU::rgm_stat)
 };
 
 // the frame's crop box (as k_rg_append_keys)
@@ -1788,10 +1798,16 @@ __device__ __forceinline__ int rgm_app_elem(const RgView<NC>& V, int a, int& c, 
     return start + mc + li;
 }
 template <int NC>
-__device__ __forceinline__ u64 rgm_old_key(const RgView<NC>& V, const VgLeaf& leaf, const RgmBox& box, int g) {
-    int c, li;
+__device__ __forceinline__ float4 rgm_old_point(const RgView<NC>& V, int g, int& c) {
+    int li;
     (void)rgm_old_elem<NC>(V, g, c, li);
-    return rgm_key(V.map.at(c)[li], c, leaf.at(c), box);
+    return V.map.at(c)[li];
+}
+template <int NC>
+__device__ __forceinline__ u64 rgm_old_key(const RgView<NC>& V, const VgLeaf& leaf, const RgmBox& box, int g) {
+    int c;
+    const float4 p = rgm_old_point<NC>(V, g, c);
+    return rgm_key(p, c, leaf.at(c), box);
 }
 
 // lower / upper bound of k in sorted keys[0 .. n) (LDS or global)
@@ -1814,15 +1830,60 @@ __device__ __forceinline__ int rgm_upper(const u64* keys, int n, u64 k) {
     return lo;
 }
 
+// one voxel of rgbds: the f32 centroid of its points in order and the maxima of r and g (:108-125),
+// then extractstablepoint (:12-14) and the ageing (:634-646)
+struct RgmVox {
+    float cx = 0.f, cy = 0.f, cz = 0.f;
+    int r_max = -1;
+    float g_max = -1;
+    int n = 0;
+    __device__ __forceinline__ void add(float4 p) {
+        cx += p.x; cy += p.y; cz += p.z;
+        const int r = (int)w_r(p);
+        const float g = (float)w_g(p);
+        if (r > r_max) r_max = r;
+        if (g > g_max) g_max = g;
+        ++n;
+    }
+    // the output point; returns whether the voxel is kept
+    __device__ __forceinline__ bool finish(int k_new, float theta_p, int theta_max, float4& out) const {
+        const float nn = (float)n;
+        const u32 r = (u32)r_max & 255u, g = (u32)g_max & 255u;     // stored into uint8 r, g
+        const bool drop = ((float)g < (float)r * theta_p) && ((int)r > k_new) && ((int)g < theta_max + 1);
+        const u32 aged = r > 250 ? 255u : r + 2u;
+        out = make_float4(cx / nn, cy / nn, cz / nn, __uint_as_float(pack_rg(aged, g)));
+        return !drop;
+    }
+};
+
+// exclusive scan across a 1024-thread block (lds: 16 words)
+__device__ __forceinline__ u32 block_excl_scan1024(u32 v, u32* lds, u32& total) {
+    const int w = threadIdx.x >> 6, l = lane_id();
+    const u32 inc = wave_incl_scan_u32(v);
+    if (l == 63) lds[w] = inc;
+    __syncthreads();
+    u32 off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kRgmThreads / 64; ++i) {
+        const u32 x = lds[i];
+        if (i < w) off += x;
+        tot += x;
+    }
+    __syncthreads();
+    total = tot;
+    return off + inc - v;
+}
+
 // block b < kRgmBuckets: bucket b (map points [lo, hi) = [b M / R, (b + 1) M / R), appended points
-// with key in [key(lo), key(hi))); block kRgmBuckets: the pose step (as in k_rg_append_keys)
+// whose key lies in [key(lo), key(hi))); block kRgmBuckets: the pose step (as in k_rg_append_keys)
 template <int NC>
 __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     __shared__ u64 bk[kRgmBucketCap];
     __shared__ u32 bt[kRgmBucketCap];
     __shared__ u64 ok[kRgmOldLds];
     __shared__ u64 s_split[kRgmBuckets];
-    __shared__ int s_cnt, s_before[kRgmThreads / 64];
+    __shared__ int s_cnt, s_before[kRgmThreads / 64], s_cls[kMaxC], s_last;
+    __shared__ u32 s_w[kRgmThreads / 64], s_off;
     const int t = threadIdx.x, b = blockIdx.x;
     const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
     const int n = V.total();
@@ -1860,11 +1921,12 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         a.vtag[e] = (u32)e | (box.in(p) ? 0u : kRgmDrop);
         if (g + 1 < M) unsorted |= rgm_old_key<NC>(V, a.leaf, box, g + 1) < key;
     }
-    if (t < kRgmBuckets) {                             // every bucket's lower splitter (the key of its first map point)
-        const int lt_ = (int)(((long long)t * M) / kRgmBuckets);
-        s_split[t] = t == 0 ? 0ull : (lt_ >= M ? ~0ull : rgm_old_key<NC>(V, a.leaf, box, lt_));
+    if (t < kRgmBuckets) {                     // every bucket's lower splitter (the key of its first map point)
+        const int l0 = (int)(((long long)t * M) / kRgmBuckets);
+        s_split[t] = t == 0 ? 0ull : (l0 >= M ? ~0ull : rgm_old_key<NC>(V, a.leaf, box, l0));
     }
     if (t == 0) s_cnt = 0;
+    if (t < kMaxC) s_cls[t] = 0;
     if (__any(unsorted) && lane_id() == 0) a.stat[0] = 1;
     __syncthreads();
     // 2. every appended point: its bucket is the number of splitters 1 .. R - 1 at or below its key (a
@@ -1900,11 +1962,9 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     int nbefore = 0;
 #pragma unroll
     for (int w = 0; w < kRgmThreads / 64; ++w) nbefore += s_before[w];
-    const int cb = s_cnt;
-    if (cb > kRgmBucketCap) {                            // too many for the bucket: the fallback sorts
-        if (t == 0) a.stat[0] = 1;
-        return;
-    }
+    const bool overflow = s_cnt > kRgmBucketCap;       // too many: the fallback sorts (still take part below)
+    const int cb = overflow ? 0 : s_cnt;
+    if (overflow && t == 0) a.stat[0] = 1;
     // 3. sort the bucket's appended points by (key, element)
     if (cb <= kRgmThreads) {
         // one element per thread; partners within a wave by shuffles, across waves through LDS
@@ -1964,23 +2024,115 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
             }
     }
     __syncthreads();
-    // 4. place: a map point after the appended points below it (ties: the map point first), an
-    // appended point after the map points at or below it
-    for (int g = lo + t; g < hi; g += kRgmThreads) {
-        const u64 key = cache ? ok[g - lo] : a.okey[g];
-        int c, li;
-        const int e = rgm_old_elem<NC>(V, g, c, li);
-        const int pos = g + nbefore + rgm_lower(bk, cb, key);
-        a.kout[pos] = key;
-        a.vout[pos] = a.vtag[e];
+    // 4. voxels. Merged order: a map point after the appended points below it (equal keys: map points
+    // first), an appended point after the map points at or below it. A voxel (a run of equal keys) is
+    // reduced by the thread of its first element in this bucket: its map points in map order, then its
+    // appended points; the voxel that opens the bucket may have map points in earlier buckets (equal
+    // keys across a split), which leave it to this one. Every element writes its kept flag at its
+    // merged position, a voxel's output sits at its first element's.
+    const int L = nold + cb;
+    const int base = lo + nbefore;
+    const u64 s_next = b + 1 < kRgmBuckets ? s_split[b + 1] : ~0ull;
+    auto okey_at = [&](int i) -> u64 { return cache ? ok[i] : a.okey[lo + i]; };
+    auto add_old = [&](RgmVox& v, int g) {
+        int c;
+        const float4 p = rgm_old_point<NC>(V, g, c);
+        if (box.in(p)) v.add(p);
+    };
+    auto add_app = [&](RgmVox& v, u32 tag) {
+        if (tag & kRgmDrop) return;
+        int c;
+        v.add(V.at((int)tag, c));
+    };
+    for (int i = t; i < nold; i += kRgmThreads) {
+        const u64 K = okey_at(i);
+        const int lb = rgm_lower(bk, cb, K);
+        const int P = base + i + lb;
+        u32 flag = 0;
+        if ((i == 0 || okey_at(i - 1) != K) && (K < s_next || b == kRgmBuckets - 1)) {
+            RgmVox v;
+            if (i == 0) {                              // its map points in earlier buckets, in map order
+                int g0 = lo;
+                while (g0 > 0 && rgm_old_key<NC>(V, a.leaf, box, g0 - 1) == K) --g0;
+                for (int g = g0; g < lo; ++g) add_old(v, g);
+            }
+            for (int j = i; j < nold && okey_at(j) == K; ++j) add_old(v, lo + j);
+            for (int r = lb; r < cb && bk[r] == K; ++r) add_app(v, bt[r]);
+            if (v.n) {
+                float4 out;
+                if (v.finish(a.k_new, a.theta_p, a.theta_max, out)) {
+                    flag = 1;
+                    atomicAdd(&s_cls[(int)(K >> 62)], 1);
+                }
+                a.vox[P] = out;
+            }
+        }
+        a.kflag[P] = flag;
     }
     for (int r = t; r < cb; r += kRgmThreads) {
-        const u64 key = bk[r];
-        const int below = cache ? rgm_upper(ok, nold, key) : rgm_upper(a.okey + lo, nold, key);
-        const int pos = lo + below + nbefore + r;
-        a.kout[pos] = key;
-        a.vout[pos] = bt[r];
+        const u64 K = bk[r];
+        const int ub = cache ? rgm_upper(ok, nold, K) : rgm_upper(a.okey + lo, nold, K);
+        const int P = base + r + ub;
+        u32 flag = 0;
+        if ((r == 0 || bk[r - 1] != K) && (ub == 0 || okey_at(ub - 1) != K)) {   // a voxel without map points
+            RgmVox v;
+            for (int q = r; q < cb && bk[q] == K; ++q) add_app(v, bt[q]);
+            if (v.n) {
+                float4 out;
+                if (v.finish(a.k_new, a.theta_p, a.theta_max, out)) {
+                    flag = 1;
+                    atomicAdd(&s_cls[(int)(K >> 62)], 1);
+                }
+                a.vox[P] = out;
+            }
+        }
+        a.kflag[P] = flag;
     }
+    __syncthreads();
+    // 5. the kept voxels' ranks in merged order (tiles of 1024), then their offset over the buckets
+    u32 run = 0;
+    for (int t0 = 0; t0 < L; t0 += kRgmThreads) {
+        const int p = t0 + t;
+        const u32 f = p < L && a.kflag[base + p] ? 1u : 0u;
+        u32 tot;
+        const u32 ex = block_excl_scan1024(f, s_w, tot);
+        if (p < L && f) a.kflag[base + p] = run + ex + 1;
+        run += tot;
+    }
+    if (t < 64) {
+        const u32 excl = tile_lookback(a.status, b, run, a.err);
+        if (t == 0) s_off = excl;
+    }
+    __syncthreads();
+    const u32 off = s_off;
+    for (int p = t; p < L; p += kRgmThreads) {
+        const u32 f = a.kflag[base + p];
+        if (f) a.seg_out[off + f - 1] = a.vox[base + p];
+    }
+    // 6. the kept voxels of every class: summed over the buckets; the last bucket to arrive writes the
+    // class boundaries (cnt[C_NLT + c - 1] = kept voxels of classes < c) and the total, and clears the
+    // accumulators and the look-back words for the next call
+    if (t < NC && s_cls[t]) __hip_atomic_fetch_add(&a.stat[4 + t], s_cls[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0)
+        s_last = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (u32)kRgmBuckets - 1;
+    __syncthreads();
+    if (!s_last) return;
+    if (t == 0) {
+        int kc[kMaxC], tot = 0;
+        for (int c = 0; c < kMaxC; ++c) {
+            kc[c] = __hip_atomic_load(&a.stat[4 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.stat[4 + c], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        for (int c = 1; c <= kMaxC; ++c) {
+            tot += kc[c - 1];
+            a.cnt[C_NLT + c - 1] = tot;
+        }
+        a.cnt[C_KEEP_TOTAL] = tot;
+        __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t < kRgmBuckets) __hip_atomic_store(&a.status[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Fallback: one 1024-thread workgroup sorts all n (key64, vtag) pairs of element order stably by
@@ -2016,6 +2168,7 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
             a.kout[i] = ks[i];
             a.vout[i] = vs[i];
         }
+        __syncthreads();
         return;
     }
     u64* kd = (P & 1) ? a.kout : a.ktmp;
@@ -2083,165 +2236,68 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
     }
 }
 
+// Fallback, second half: the voxels of the sorted (kout, vout) reduced by the same workgroup, tile by
+// tile in key order with a running count of kept voxels (cropped elements skipped; a voxel's first
+// element is its first uncropped one)
 template <int NC>
-__global__ void __launch_bounds__(kRgmThreads) k_rgm_fallback(RgmArgs a) {
-    if (!a.stat[0]) return;                            // the buckets' placement stands
-    const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
-    rgm_fallback_sort(a, V.total());
-    if (threadIdx.x == 0) a.stat[1]++;
+__device__ void rgm_fallback_tail(const RgmArgs& a, const RgView<NC>& V, int n) {
+    __shared__ u32 s_w[kRgmThreads / 64];
+    __shared__ int s_cls[kMaxC];
+    const int t = threadIdx.x;
+    if (t < kMaxC) s_cls[t] = 0;
+    __syncthreads();
+    u32 run = 0;
+    for (int t0 = 0; t0 < n; t0 += kRgmThreads) {
+        const int i = t0 + t;
+        u32 flag = 0;
+        float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < n && !(a.vout[i] & kRgmDrop)) {
+            const u64 K = a.kout[i];
+            bool first = true;
+            for (int j = i - 1; j >= 0 && a.kout[j] == K; --j)
+                if (!(a.vout[j] & kRgmDrop)) { first = false; break; }
+            if (first) {
+                RgmVox v;
+                for (int e = i; e < n && a.kout[e] == K; ++e) {
+                    const u32 tg = a.vout[e];
+                    if (tg & kRgmDrop) continue;
+                    int c;
+                    v.add(V.at((int)tg, c));
+                }
+                if (v.finish(a.k_new, a.theta_p, a.theta_max, out)) {
+                    flag = 1;
+                    atomicAdd(&s_cls[(int)(K >> 62)], 1);
+                }
+            }
+        }
+        u32 tot;
+        const u32 ex = block_excl_scan1024(flag, s_w, tot);
+        if (flag) a.seg_out[run + ex] = out;
+        run += tot;
+    }
+    __syncthreads();
+    if (t == 0) {
+        int tot = 0;
+        for (int c = 1; c <= kMaxC; ++c) {
+            tot += s_cls[c - 1];
+            a.cnt[C_NLT + c - 1] = tot;
+        }
+        a.cnt[C_KEEP_TOTAL] = tot;
+    }
 }
 
-struct RgTail64Args {
-    int* cnt;
-    Clouds map, app;
-    const u64* keys;       // merged, cnt[C_NRG] of them
-    const u32* vals;       // element | cropped << 31
-    float4* seg_out;
-    int k_new;
-    float theta_p;
-    int theta_max;
-    u64* status;
-    u32* arrive;
-    int* err;
-    int* stat;             // rgm_stat: the fallback flag is cleared here
-};
-
-// k_rg_tail over the merged sequence: cropped elements stay in it, so a voxel's first element is its
-// first uncropped one (no uncropped element of the same key before it) and its walk skips cropped ones
 template <int NC>
-__global__ void __launch_bounds__(256) k_rg_tail64(RgTail64Args a) {
-    constexpr int kPer = kTailPer;
-    __shared__ u32 lw[4];
-    __shared__ u32 s_excl;
-    const RgView<NC> V = rg_view<NC>(a.cnt, a.map, a.app);
-    int* kb = a.cnt + C_NLT;
-    const int n = a.cnt[C_NRG];
-    const int ntiles = (n + kTailTile - 1) / kTailTile;
-    const int t = threadIdx.x;
-    const int G = ntiles < (int)gridDim.x ? ntiles : (int)gridDim.x;
-    if (blockIdx.x == 0 && t == 0) a.stat[0] = 0;
-    if (n == 0) {
-        if (blockIdx.x == 0 && t == 0) {
-            a.cnt[C_KEEP_TOTAL] = 0;
-            kb[0] = kb[1] = kb[2] = 0;
-        }
-        return;
+__global__ void __launch_bounds__(kRgmThreads) k_rgm_fallback(RgmArgs a) {
+    if (!a.stat[0]) return;                            // the buckets' output stands
+    const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
+    rgm_fallback_sort(a, V.total());
+    __threadfence_block();
+    __syncthreads();
+    rgm_fallback_tail<NC>(a, V, V.total());
+    if (threadIdx.x == 0) {
+        a.stat[1]++;
+        a.stat[0] = 0;
     }
-    if ((int)blockIdx.x >= G) return;
-    if (blockIdx.x == 0 && t == 0) {                            // classes below the first key's: none
-        const u32 c0 = (u32)(a.keys[0] >> 62);
-        for (u32 b = 1; b <= 3; ++b)
-            if (c0 >= b) kb[b - 1] = 0;
-    }
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int base = tile * kTailTile + t * kPer;
-        u64 k[kPer + 1];                                        // k[0] = predecessor of the first
-        u32 v[kPer + 1];
-        k[0] = base > 0 && base - 1 < n ? a.keys[base - 1] : ~0ull;
-        v[0] = base > 0 && base - 1 < n ? a.vals[base - 1] : kRgmDrop;
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            k[j + 1] = base + j < n ? a.keys[base + j] : ~0ull;
-            v[j + 1] = base + j < n ? a.vals[base + j] : kRgmDrop;
-        }
-        float4 pt[kPer];
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            int c;
-            pt[j] = base + j < n && !(v[j + 1] & kRgmDrop) ? V.at((int)v[j + 1], c) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        float4 out[kPer];
-        u32 keepm = 0u;
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int i = base + j;
-            out[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (i >= n || (v[j + 1] & kRgmDrop)) continue;
-            const u64 K = k[j + 1];
-            // a voxel's first uncropped element: no uncropped element of the same key before it
-            bool first = true;
-            if (i > 0 && k[j] == K) {
-                if (!(v[j] & kRgmDrop)) first = false;
-                else
-                    for (int b = i - 2; b >= 0; --b) {
-                        if (a.keys[b] != K) break;
-                        if (!(a.vals[b] & kRgmDrop)) { first = false; break; }
-                    }
-            }
-            if (!first) continue;
-            float cx = 0.f, cy = 0.f, cz = 0.f;                 // Vector4f centroid (:108-125)
-            int r_max = -1;
-            float g_max = -1;
-            int cntv = 0;
-            for (int e = i;;) {
-                float4 p;
-                bool use;
-                if (e - base < kPer) {
-                    use = true;
-#pragma unroll
-                    for (int jj = 0; jj < kPer; ++jj)           // static register index
-                        if (jj == e - base) { p = pt[jj]; use = !(v[jj + 1] & kRgmDrop); }
-                } else {
-                    const u32 ve = a.vals[e];
-                    use = !(ve & kRgmDrop);
-                    int c;
-                    if (use) p = V.at((int)ve, c);
-                }
-                if (use) {
-                    cx += p.x; cy += p.y; cz += p.z;
-                    const int r = (int)w_r(p);
-                    const float g = (float)w_g(p);
-                    if (r > r_max) r_max = r;
-                    if (g > g_max) g_max = g;
-                    ++cntv;
-                }
-                if (++e >= n) break;
-                u64 ke;
-                if (e - base < kPer) {
-#pragma unroll
-                    for (int jj = 0; jj < kPer; ++jj)           // static register index
-                        if (jj == e - base) ke = k[jj + 1];
-                } else {
-                    ke = a.keys[e];
-                }
-                if (ke != K) break;
-            }
-            const float nn = (float)cntv;
-            const u32 r = (u32)r_max & 255u, g = (u32)g_max & 255u;     // stored into uint8 r, g
-            // extractstablepoint (:12-14) on the voxel's uint8 r, g
-            const bool drop = ((float)g < (float)r * a.theta_p) && ((int)r > a.k_new) && ((int)g < a.theta_max + 1);
-            const u32 aged = r > 250 ? 255u : r + 2u;                   // :634-646
-            out[j] = make_float4(cx / nn, cy / nn, cz / nn, __uint_as_float(pack_rg(aged, g)));
-            if (!drop) keepm |= 1u << j;
-        }
-        u32 agg;
-        const u32 tex = block_excl_scan256((u32)__popc(keepm), lw, agg);
-        if (t < 64) {
-            const u32 excl = tile_lookback(a.status, tile, agg, a.err);
-            if (t == 0) {
-                s_excl = excl;
-                if (tile == ntiles - 1) {
-                    a.cnt[C_KEEP_TOTAL] = (int)(excl + agg);
-                    const u32 cl = (u32)(a.keys[n - 1] >> 62);
-                    for (u32 b = 1; b <= 3; ++b)                // classes above the last key's: all
-                        if (cl < b) kb[b - 1] = (int)(excl + agg);
-                }
-            }
-        }
-        __syncthreads();
-        u32 pos = s_excl + tex;                                 // kept voxels before key base + j
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int i = base + j;
-            if (i >= n) break;
-            const u32 cp = (u32)(k[j] >> 62), cc = (u32)(k[j + 1] >> 62);
-            if (i > 0 && cp < cc)                              // class boundary: kept voxels before it
-                for (u32 b = cp + 1; b <= cc; ++b) kb[b - 1] = (int)pos;
-            if ((keepm >> j) & 1u) a.seg_out[pos++] = out[j];
-        }
-        __syncthreads();
-    }
-    lookback_finish(a.status, ntiles, a.arrive, G);
 }
 
 // initMapWithPoints (ES :217-222, BPF :685-691): append the raw clouds (r = g = 0)
@@ -2405,7 +2461,9 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.rgm_kout, sizeof(u64) * o.sort_cap);
     PF_ALLOC(o.rgm_ktmp, sizeof(u64) * o.sort_cap);
     PF_ALLOC(o.rgm_vtmp, sizeof(u32) * o.sort_cap);
-    PF_ALLOC(o.rgm_stat, sizeof(int) * 4);
+    PF_ALLOC(o.rgm_vox, sizeof(float4) * o.sort_cap);
+    PF_ALLOC(o.rgm_kflag, sizeof(u32) * o.sort_cap);
+    PF_ALLOC(o.rgm_stat, sizeof(int) * 8);
 #undef PF_ALLOC
     trace_create("buffers");
     if (std::getenv("PF_PROBE")) {                 // development probe: LM phase timestamps
@@ -2434,7 +2492,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (hipMemsetAsync(o.lm_ticket, 0, sizeof(u32) * 2 * kLmEvalSlots, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.tail_status, 0, sizeof(u64) * (o.tail_tiles + 1), o.stream) != hipSuccess) return PF_EHIP;
-    if (hipMemsetAsync(o.rgm_stat, 0, sizeof(int) * 4, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.rgm_stat, 0, sizeof(int) * 8, o.stream) != hipSuccess) return PF_EHIP;
     // the sub-objects' overflow / wait flags latch into the handle's sticky error words
     alias_err(o.fe.err, o.errw + E_FE_SECTOR);
     alias_err(o.grid.err, o.errw + E_GRID);
@@ -2464,7 +2522,7 @@ int odom_reset(OdomGPU& o) {
     if (hipMemsetAsync(o.lm_ticket, 0, sizeof(u32) * 2 * kLmEvalSlots, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.tail_status, 0, sizeof(u64) * (o.tail_tiles + 1), o.stream) != hipSuccess) return PF_EHIP;
-    if (hipMemsetAsync(o.rgm_stat, 0, sizeof(int) * 4, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.rgm_stat, 0, sizeof(int) * 8, o.stream) != hipSuccess) return PF_EHIP;
     for (int p = 0; p < kSlots; ++p)
         if (hipMemsetAsync(o.sb[p].cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)o.cls.nc * o.map_cap);
@@ -2514,7 +2572,7 @@ void odom_destroy(OdomGPU& o) {
     void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.seg_out,
                     o.keys, o.vals, o.tail_status, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
                     o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg, o.errw,
-                    o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.rgm_ktmp,
+                    o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.rgm_ktmp, o.rgm_vox, o.rgm_kflag,
                     o.rgm_vtmp, o.rgm_stat};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
@@ -2624,13 +2682,11 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     const VgLeaf leaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}};
     if (!o.tie_order && !o.rg_radix) {                    // rgbds by merge (the map stays in key order)
         RgmArgs ra{o.st, cnt, o.acc, clouds(o.map), clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap, leaf,
-                   o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp, o.rgm_stat};
+                   o.prm.k_new, o.prm.theta_p, o.prm.theta_max, o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_vox,
+                   o.rgm_kflag, o.seg_out, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err,
+                   o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp, o.rgm_stat};
         PF_LAUNCH_NC(nc, k_rgm_bucket, dim3(kRgmBuckets + 1), dim3(kRgmThreads), 0, s, ra);
         PF_LAUNCH_NC(nc, k_rgm_fallback, dim3(1), dim3(kRgmThreads), 0, s, ra);
-        RgTail64Args ta{cnt, clouds(o.map), clouds(o.app), o.rgm_kout, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,
-                        o.prm.theta_max, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err, o.rgm_stat};
-        const unsigned tail_grid = (unsigned)(o.tail_tiles < (size_t)kSortMaxBlocks ? o.tail_tiles : kSortMaxBlocks);
-        PF_LAUNCH_NC(nc, k_rg_tail64, dim3(tail_grid > 0 ? tail_grid : 1), dim3(256), 0, s, ta);
         PF_LAUNCH_NC(nc, k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, clouds_w(o.map));
         return;
     }
