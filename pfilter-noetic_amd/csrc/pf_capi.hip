@@ -462,7 +462,7 @@ static int init_map_n(pf_odom* h, const float* const* cl, const size_t* n, const
     if (!rc) rc = stage_a_end_b_begin(h, p);
     if (rc) return rc;
     odom_enqueue_init(o, p, o.stream);
-    odom_enqueue_export(o, o.stream);
+    odom_enqueue_export(o, o.stream, false);
     rc = stage_b_end(h, p);
     if (rc) return rc;
     return readback(h);
@@ -481,7 +481,8 @@ static int update_n(pf_odom* h, const float* const* cl, const size_t* n, const s
     rc = stage_a_end_b_begin(h, p);
     if (rc) return rc;
     odom_enqueue_update(o, p, o.stream);
-    odom_enqueue_export(o, o.stream);
+    odom_enqueue_export(o, o.stream, true);
+    odom_update_done(o);
     rc = stage_b_end(h, p);
     if (rc) return rc;
     rc = readback(h);
@@ -540,7 +541,7 @@ int pf_odom_get_map(pf_odom* h, int which, float* xyz, uint8_t* rg, size_t cap, 
     if (m > cap) return PF_ECAPACITY;
     std::vector<float4> tmp(m);
     if (m) {
-        PF_HIP_TRY(hipMemcpyAsync(tmp.data(), o.map[which], sizeof(float4) * m, hipMemcpyDeviceToHost, o.stream));
+        PF_HIP_TRY(hipMemcpyAsync(tmp.data(), map_cur(o)[which], sizeof(float4) * m, hipMemcpyDeviceToHost, o.stream));
         PF_HIP_TRY(hipStreamSynchronize(o.stream));
     }
     for (size_t i = 0; i < m; ++i) {
@@ -567,7 +568,7 @@ int pf_odom_set_map(pf_odom* h, int which, const float* xyz, const uint8_t* rg, 
         std::memcpy(&wf, &w, 4);
         tmp[i] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], wf);
     }
-    if (n) PF_HIP_TRY(hipMemcpyAsync(o.map[which], tmp.data(), sizeof(float4) * n, hipMemcpyHostToDevice, o.stream));
+    if (n) PF_HIP_TRY(hipMemcpyAsync(map_cur(o)[which], tmp.data(), sizeof(float4) * n, hipMemcpyHostToDevice, o.stream));
     hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_M + which, (int)n);
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     return PF_OK;
@@ -618,6 +619,14 @@ static void stage_enqueue_front(OdomGPU& o, int p, hipStream_t s) {
     cls_enqueue(*o.front, o.stage, o.sb[p].cnt + C_NIN, out, cnt, false, s);
 }
 
+static void drop_graphs_b(OdomGPU& o) {
+    for (hipGraphExec_t& g : o.graph_b)
+        if (g) {
+            (void)hipGraphExecDestroy(g);
+            g = nullptr;
+        }
+}
+
 static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool stage_a, bool scan = false) {
     hipGraph_t g;
     PF_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
@@ -627,7 +636,7 @@ static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool s
         stage_enqueue_vg(o, p, s);
     } else {
         odom_enqueue_update(o, p, s);
-        odom_enqueue_export(o, s);
+        odom_enqueue_export(o, s, true);
     }
     PF_HIP_TRY(hipStreamEndCapture(s, &g));
     PF_HIP_TRY(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
@@ -722,17 +731,20 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
     if (!rc) rc = timing_mark(h, 2);
     if (rc) return rc;
     if (steady) {
-        if (!o.graph_b[p]) {
-            rc = capture(o.stream, &o.graph_b[p], o, p, false);
+        hipGraphExec_t& gb = o.graph_b[p + kSlots * o.mpar];
+        if (!gb) {
+            rc = capture(o.stream, &gb, o, p, false);
             if (rc) return rc;
         }
-        PF_HT(5, PF_HIP_TRY(hipGraphLaunch(o.graph_b[p], o.stream)));
+        PF_HT(5, PF_HIP_TRY(hipGraphLaunch(gb, o.stream)));
+        odom_update_done(o);
     } else if (!o.inited) {
         odom_enqueue_init(o, p, o.stream);
-        odom_enqueue_export(o, o.stream);
+        odom_enqueue_export(o, o.stream, false);
     } else {
         odom_enqueue_update(o, p, o.stream);
-        odom_enqueue_export(o, o.stream);
+        odom_enqueue_export(o, o.stream, true);
+        odom_update_done(o);
     }
     rc = timing_mark(h, 3);
     if (rc) return rc;
@@ -1057,7 +1069,7 @@ int pf_odom_snapshot(pf_odom* h, void* buf, size_t cap, size_t* size) {
     b += sizeof(pose);
     for (int c = 0; c < o.cls.nc; ++c) {
         if (hd.map_n[c])
-            PF_HIP_TRY(hipMemcpyAsync(b, o.map[c], sizeof(float4) * hd.map_n[c], hipMemcpyDeviceToHost, o.stream));
+            PF_HIP_TRY(hipMemcpyAsync(b, map_cur(o)[c], sizeof(float4) * hd.map_n[c], hipMemcpyDeviceToHost, o.stream));
         b += sizeof(float4) * hd.map_n[c];
     }
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
@@ -1099,7 +1111,7 @@ int pf_odom_restore(pf_odom* h, const void* buf, size_t size) {
     if (has_pose) PF_HIP_TRY(hipMemcpyAsync(o.poses, pose, sizeof(pose), hipMemcpyHostToDevice, o.stream));
     for (int c = 0; c < hd.nc; ++c) {
         if (hd.map_n[c])
-            PF_HIP_TRY(hipMemcpyAsync(o.map[c], b, sizeof(float4) * hd.map_n[c], hipMemcpyHostToDevice, o.stream));
+            PF_HIP_TRY(hipMemcpyAsync(map_cur(o)[c], b, sizeof(float4) * hd.map_n[c], hipMemcpyHostToDevice, o.stream));
         b += sizeof(float4) * hd.map_n[c];
     }
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
@@ -1126,11 +1138,7 @@ int pf_odom_set_map_export(pf_odom* h, int enable) {
         std::memset(o.h_map_n, 0, sizeof(int) * kMaxC);
     }
     if ((enable != 0) != o.export_maps)
-        for (int s = 0; s < kSlots; ++s)      // the export kernel is part of the captured stage B
-            if (o.graph_b[s]) {
-                (void)hipGraphExecDestroy(o.graph_b[s]);
-                o.graph_b[s] = nullptr;
-            }
+        drop_graphs_b(o);                      // the export kernel is part of the captured stage B
     o.export_maps = enable != 0;
     return PF_OK;
 }
@@ -1165,14 +1173,15 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
         if (int rc = tie_alloc(*o.tie_a, (size_t)o.cls.nc * o.in_cap)) return rc;
         if (int rc = tie_alloc(*o.tie_b, o.sort_cap)) return rc;
     }
-    if ((enable != 0) != o.tie_order)
-        for (int s = 0; s < kSlots; ++s) {          // both stages' captured kernel sequences change
-            for (hipGraphExec_t* g : {&o.graph_a[s], &o.graph_b[s], &o.graph_as[s]})
+    if ((enable != 0) != o.tie_order) {             // both stages' captured kernel sequences change
+        for (int s = 0; s < kSlots; ++s)
+            for (hipGraphExec_t* g : {&o.graph_a[s], &o.graph_as[s]})
                 if (*g) {
                     (void)hipGraphExecDestroy(*g);
                     *g = nullptr;
                 }
-        }
+        drop_graphs_b(o);
+    }
     o.tie_order = enable != 0;
     return PF_OK;
 }
@@ -1185,12 +1194,7 @@ extern "C" int pf_dev_set_rg_radix(pf_odom* h, int enable) {
     PF_HIP_TRY(hipSetDevice(o.device));
     PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
-    if ((enable != 0) != o.rg_radix)
-        for (int s = 0; s < kSlots; ++s)
-            if (o.graph_b[s]) {
-                (void)hipGraphExecDestroy(o.graph_b[s]);
-                o.graph_b[s] = nullptr;
-            }
+    if ((enable != 0) != o.rg_radix) drop_graphs_b(o);
     o.rg_radix = enable != 0;
     return PF_OK;
 }

@@ -57,6 +57,7 @@ enum ErrWord {
     E_SORT_A,          // stage A sort / scan look-back wait gave up
     E_FRONT,           // BPF front end: ground grid above its cell limit (CC_ERR)
     E_FRONT_GRID,      // BPF front end: U grid above its cell capacity
+    E_MAP,             // a class map above map_cap after rgbds: the voxels past it were dropped
     E_COUNT = 8
 };
 
@@ -182,10 +183,14 @@ struct OdomGPU {
     hipEvent_t ev_a[kSlots] = {};                           // stage A done with slot p
     hipEvent_t ev_b[kSlots] = {};                           // stage B done with slot p
     hipGraphExec_t graph_a[kSlots] = {};                    // steady-state replay per slot
-    hipGraphExec_t graph_b[kSlots] = {};
+    hipGraphExec_t graph_b[2 * kSlots] = {};                // [slot + kSlots * mpar]
     ClsGPU* front = nullptr;                                // BPF raw-scan mode: the PCA front end
     hipGraphExec_t graph_as[kSlots] = {};                   // stage A replay in raw-scan mode
-    float4* map[kMaxC] = {};       // local maps
+    // local maps, double-buffered: an update reads mapset[mpar] and writes the new maps into
+    // mapset[mpar ^ 1] (rgbds cannot overwrite the map it is still reading), then the host flips mpar
+    // (odom_update_done); graph B is captured per (slot, mpar)
+    float4* mapset[2][kMaxC] = {};
+    int mpar = 0;
     float4* app[kMaxC] = {};       // this frame's transformed down-sampled points (appended)
     float4* seg_out = nullptr;
     u32 *keys = nullptr, *vals = nullptr;
@@ -253,8 +258,14 @@ void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s);
 void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s);
 // stage B: updatePointsToMap from slot p's down-sampled features; outer iteration count = host mirror
 void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s);
+// after an update has been enqueued (or its graph launched): the maps it wrote become the current ones
+inline void odom_update_done(OdomGPU& o) { o.mpar ^= 1; }
+inline float4* const* map_cur(const OdomGPU& o) { return o.mapset[o.mpar]; }
+inline float4* const* map_next(const OdomGPU& o) { return o.mapset[o.mpar ^ 1]; }
 // stage B tail when map export is on: the maps and their sizes into the mapped pinned buffers
-void odom_enqueue_export(OdomGPU& o, hipStream_t s);
+// the maps into the mapped pinned export buffers: after_update, the maps the update just wrote
+// (enqueued before odom_update_done), else the current ones
+void odom_enqueue_export(OdomGPU& o, hipStream_t s, bool after_update);
 // k_assoc's kNN alone, `iters` times, on the last frame's queries and grid (pf_odom_probe_assoc)
 int odom_probe_assoc(OdomGPU& o, int iters, double* avg_ms, double* alg_bytes, int* nq, float4* q_host, size_t q_cap);
 

@@ -1696,8 +1696,10 @@ __global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const f
 // :592-604), keeping those of its bucket and counting those below it; sorts its appended points by
 // (key, element) in registers and LDS (a bitonic network, shuffles within a wave); reduces the voxels
 // of its bucket (the Vector4f centroid and r / g maxima of :108-125, extractstablepoint :12-14, the
-// ageing :634-646, cropped elements skipped); ranks the kept voxels in merged order and places them by
-// a look-back over the buckets; the last bucket to finish writes the class boundaries. When the map
+// ageing :634-646, cropped elements skipped); ranks the kept voxels in merged order and writes them
+// straight into the other map set (mapset[mpar ^ 1]) at their class-map index, the class-c voxels of
+// earlier buckets counted by a look-back per class; the last bucket to finish writes the map sizes.
+// When the map
 // is not in key order (the first update after initMapWithPoints or pf_odom_set_map, or a centroid that
 // rounded into a neighbouring voxel) or a bucket holds more than kRgmBucketCap appended points, the
 // buckets' output is void and k_rgm_fallback's single workgroup sorts every element (a stable LSD
@@ -1724,9 +1726,11 @@ struct RgmArgs {
     u64* key64;            // [elements] keys, element order (for the fallback)
     u32* vtag;             // [elements] element | cropped << 31
     float4* vox;           // [elements] a voxel's output at its merged position
-    u32* kflag;            // [elements] kept flag, then rank + 1, at merged positions
-    float4* seg_out;       // the kept voxels in key order (-> k_rg_write)
-    u64* status;           // look-back words over the buckets (zero between calls) + arrival counter
+    u32* kflag;            // [elements] class << 30 | kept flag, then class << 30 | rank + 1, at merged positions
+    CloudsW mapw;          // the new class maps (the other map set)
+    u32 map_cap;
+    int* err_map;          // sticky error word E_MAP
+    u64* status;           // look-back words, [class][bucket] (zero between calls), and an arrival counter
     u32* arrive;
     int* err;
     u64* kout;             // fallback: sorted keys / tags and scratch
@@ -1883,7 +1887,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     __shared__ u64 ok[kRgmOldLds];
     __shared__ u64 s_split[kRgmBuckets];
     __shared__ int s_cnt, s_before[kRgmThreads / 64], s_cls[kMaxC], s_last;
-    __shared__ u32 s_w[kRgmThreads / 64], s_off;
+    __shared__ u32 s_w[kRgmThreads / 64], s_pref[kMaxC];
     const int t = threadIdx.x, b = blockIdx.x;
     const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
     const int n = V.total();
@@ -1891,14 +1895,10 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) M += V.m[c];
     const int A = n - M;
-    if (b == kRgmBuckets) {
+    if (b == kRgmBuckets) {                            // (reads no counter: the last bucket rewrites them)
         double prm[7];
         for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
         finalize_pose(a.st, a.poses, a.pose_cap, 1, a.acc, prm);
-        if (t == 0) {
-            a.cnt[C_NRG] = n;
-            if (A > a.stat[2]) a.stat[2] = A;
-        }
         return;
     }
     double prm[7];
@@ -2061,7 +2061,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
             if (v.n) {
                 float4 out;
                 if (v.finish(a.k_new, a.theta_p, a.theta_max, out)) {
-                    flag = 1;
+                    flag = 1u | (u32)(K >> 62) << 30;
                     atomicAdd(&s_cls[(int)(K >> 62)], 1);
                 }
                 a.vox[P] = out;
@@ -2080,7 +2080,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
             if (v.n) {
                 float4 out;
                 if (v.finish(a.k_new, a.theta_p, a.theta_max, out)) {
-                    flag = 1;
+                    flag = 1u | (u32)(K >> 62) << 30;
                     atomicAdd(&s_cls[(int)(K >> 62)], 1);
                 }
                 a.vox[P] = out;
@@ -2089,29 +2089,48 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         a.kflag[P] = flag;
     }
     __syncthreads();
-    // 5. the kept voxels' ranks in merged order (tiles of 1024), then their offset over the buckets
+    // 5. the kept voxels' ranks in merged order (tiles of 1024); per class, the kept voxels of earlier
+    // buckets by a look-back (wave c for class c); a voxel of class c goes to mapw[c] at (its bucket's
+    // class-c offset) + (its rank among the bucket's class-c voxels), classes being contiguous in key
+    // order
     u32 run = 0;
     for (int t0 = 0; t0 < L; t0 += kRgmThreads) {
         const int p = t0 + t;
-        const u32 f = p < L && a.kflag[base + p] ? 1u : 0u;
+        const u32 fl = p < L ? a.kflag[base + p] : 0u;
+        const u32 f = fl & 0x3FFFFFFFu ? 1u : 0u;
         u32 tot;
         const u32 ex = block_excl_scan1024(f, s_w, tot);
-        if (p < L && f) a.kflag[base + p] = run + ex + 1;
+        if (f) a.kflag[base + p] = (fl & 0xC0000000u) | (run + ex + 1);
         run += tot;
     }
-    if (t < 64) {
-        const u32 excl = tile_lookback(a.status, b, run, a.err);
-        if (t == 0) s_off = excl;
+    if ((t >> 6) < NC) {
+        const int c = t >> 6;
+        const u32 excl = tile_lookback(a.status + c * kRgmBuckets, b, (u32)s_cls[c], a.err);
+        if (lane_id() == 0) s_pref[c] = excl;
     }
     __syncthreads();
-    const u32 off = s_off;
+    u32 first_rank[kMaxC];                             // bucket-local rank of the first voxel of class c
+    {
+        u32 acc = 0;
+#pragma unroll
+        for (int c = 0; c < kMaxC; ++c) {
+            first_rank[c] = acc;
+            acc += c < NC ? (u32)s_cls[c] : 0u;
+        }
+    }
+    bool over = false;
     for (int p = t; p < L; p += kRgmThreads) {
         const u32 f = a.kflag[base + p];
-        if (f) a.seg_out[off + f - 1] = a.vox[base + p];
+        if (!(f & 0x3FFFFFFFu)) continue;
+        const int c = min((int)(f >> 30), NC - 1);
+        const u32 idx = s_pref[c] + (f & 0x3FFFFFFFu) - 1u - first_rank[c];
+        if (idx < a.map_cap) a.mapw.at(c)[idx] = a.vox[base + p];
+        else over = true;
     }
-    // 6. the kept voxels of every class: summed over the buckets; the last bucket to arrive writes the
-    // class boundaries (cnt[C_NLT + c - 1] = kept voxels of classes < c) and the total, and clears the
-    // accumulators and the look-back words for the next call
+    if (over && !a.stat[0]) atomicOr(a.err_map, 1);     // (out-of-order input: the fallback redoes it)
+    // 6. the kept voxels of every class summed over the buckets; the last bucket to arrive writes the
+    // map sizes (cnt[C_M + c]), the class boundaries (cnt[C_NLT + c - 1] = kept voxels of classes < c)
+    // and the total unless the fallback will, and clears the accumulators and the look-back words
     if (t < NC && s_cls[t]) __hip_atomic_fetch_add(&a.stat[4 + t], s_cls[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -2125,14 +2144,19 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
             kc[c] = __hip_atomic_load(&a.stat[4 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&a.stat[4 + c], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        for (int c = 1; c <= kMaxC; ++c) {
-            tot += kc[c - 1];
-            a.cnt[C_NLT + c - 1] = tot;
+        if (!__hip_atomic_load(&a.stat[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            for (int c = 1; c <= kMaxC; ++c) {
+                tot += kc[c - 1];
+                a.cnt[C_NLT + c - 1] = tot;
+            }
+            for (int c = 0; c < NC; ++c) a.cnt[C_M + c] = min(kc[c], (int)a.map_cap);
+            a.cnt[C_KEEP_TOTAL] = tot;
+            a.cnt[C_NRG] = n;
+            if (A > a.stat[2]) a.stat[2] = A;
         }
-        a.cnt[C_KEEP_TOTAL] = tot;
         __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (t < kRgmBuckets) __hip_atomic_store(&a.status[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t < NC * kRgmBuckets) __hip_atomic_store(&a.status[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Fallback: one 1024-thread workgroup sorts all n (key64, vtag) pairs of element order stably by
@@ -2238,7 +2262,8 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
 
 // Fallback, second half: the voxels of the sorted (kout, vout) reduced by the same workgroup, tile by
 // tile in key order with a running count of kept voxels (cropped elements skipped; a voxel's first
-// element is its first uncropped one)
+// element is its first uncropped one); the kept voxels then go to the other map set at their
+// class-map index, and the map sizes and class boundaries are written
 template <int NC>
 __device__ void rgm_fallback_tail(const RgmArgs& a, const RgView<NC>& V, int n) {
     __shared__ u32 s_w[kRgmThreads / 64];
@@ -2249,7 +2274,7 @@ __device__ void rgm_fallback_tail(const RgmArgs& a, const RgView<NC>& V, int n) 
     u32 run = 0;
     for (int t0 = 0; t0 < n; t0 += kRgmThreads) {
         const int i = t0 + t;
-        u32 flag = 0;
+        u32 flag = 0, cls = 0;
         float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
         if (i < n && !(a.vout[i] & kRgmDrop)) {
             const u64 K = a.kout[i];
@@ -2266,23 +2291,38 @@ __device__ void rgm_fallback_tail(const RgmArgs& a, const RgView<NC>& V, int n) 
                 }
                 if (v.finish(a.k_new, a.theta_p, a.theta_max, out)) {
                     flag = 1;
-                    atomicAdd(&s_cls[(int)(K >> 62)], 1);
+                    cls = (u32)(K >> 62);
+                    atomicAdd(&s_cls[cls], 1);
                 }
             }
         }
         u32 tot;
         const u32 ex = block_excl_scan1024(flag, s_w, tot);
-        if (flag) a.seg_out[run + ex] = out;
+        if (flag) {                                    // by kept rank: the output and its class
+            a.vox[run + ex] = out;
+            a.kflag[run + ex] = cls;
+        }
         run += tot;
     }
+    __threadfence_block();
     __syncthreads();
+    int low[kMaxC + 1];
+    low[0] = 0;
+#pragma unroll
+    for (int c = 1; c <= kMaxC; ++c) low[c] = low[c - 1] + s_cls[c - 1];
+    bool over = false;
+    for (u32 r = t; r < run; r += kRgmThreads) {
+        const int c = min((int)a.kflag[r], NC - 1);
+        const u32 idx = r - (u32)low[c];
+        if (idx < a.map_cap) a.mapw.at(c)[idx] = a.vox[r];
+        else over = true;
+    }
+    if (over) atomicOr(a.err_map, 1);
     if (t == 0) {
-        int tot = 0;
-        for (int c = 1; c <= kMaxC; ++c) {
-            tot += s_cls[c - 1];
-            a.cnt[C_NLT + c - 1] = tot;
-        }
-        a.cnt[C_KEEP_TOTAL] = tot;
+        for (int c = 1; c <= kMaxC; ++c) a.cnt[C_NLT + c - 1] = low[c];
+        for (int c = 0; c < NC; ++c) a.cnt[C_M + c] = min(s_cls[c], (int)a.map_cap);
+        a.cnt[C_KEEP_TOTAL] = low[kMaxC];
+        a.cnt[C_NRG] = n;
     }
 }
 
@@ -2290,12 +2330,16 @@ template <int NC>
 __global__ void __launch_bounds__(kRgmThreads) k_rgm_fallback(RgmArgs a) {
     if (!a.stat[0]) return;                            // the buckets' output stands
     const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
-    rgm_fallback_sort(a, V.total());
+    const int n = V.total();
+    __syncthreads();                                   // every thread has read the map sizes
+    rgm_fallback_sort(a, n);
     __threadfence_block();
     __syncthreads();
-    rgm_fallback_tail<NC>(a, V, V.total());
+    rgm_fallback_tail<NC>(a, V, n);
     if (threadIdx.x == 0) {
         a.stat[1]++;
+        if (n - (V.m[0] + (NC > 1 ? V.m[1] : 0) + (NC > 2 ? V.m[2] : 0)) > a.stat[2])
+            a.stat[2] = n - (V.m[0] + (NC > 1 ? V.m[1] : 0) + (NC > 2 ? V.m[2] : 0));
         a.stat[0] = 0;
     }
 }
@@ -2433,11 +2477,13 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.vscan, sizeof(u32) * (nq + 1));
     PF_ALLOC(o.vsegstart, sizeof(u32) * (nq + 1));
     for (int c = 0; c < nc; ++c) {
-        PF_ALLOC(o.map[c], sizeof(float4) * map_cap);
+        PF_ALLOC(o.mapset[0][c], sizeof(float4) * map_cap);
+        PF_ALLOC(o.mapset[1][c], sizeof(float4) * map_cap);
         PF_ALLOC(o.app[c], sizeof(float4) * in_cap);
     }
     PF_ALLOC(o.seg_out, sizeof(float4) * o.sort_cap);
     o.tail_tiles = (o.sort_cap + kTailTile - 1) / kTailTile;
+    if (o.tail_tiles < (size_t)kMaxC * kRgmBuckets) o.tail_tiles = (size_t)kMaxC * kRgmBuckets;   // rgm look-backs
     PF_ALLOC(o.tail_status, sizeof(u64) * (o.tail_tiles + 1));    // look-back words + the arrival counter
     PF_ALLOC(o.keys, sizeof(u32) * (o.sort_cap + 1));
     PF_ALLOC(o.vals, sizeof(u32) * (o.sort_cap + 1));
@@ -2539,7 +2585,8 @@ int odom_reset(OdomGPU& o) {
 void odom_destroy(OdomGPU& o) {
     for (int p = 0; p < kSlots; ++p) {
         if (o.graph_a[p]) (void)hipGraphExecDestroy(o.graph_a[p]);
-        if (o.graph_b[p]) (void)hipGraphExecDestroy(o.graph_b[p]);
+        for (int q = 0; q < 2; ++q)
+            if (o.graph_b[p + kSlots * q]) (void)hipGraphExecDestroy(o.graph_b[p + kSlots * q]);
         if (o.graph_as[p]) (void)hipGraphExecDestroy(o.graph_as[p]);
         if (o.ev_a[p]) (void)hipEventDestroy(o.ev_a[p]);
         if (o.ev_b[p]) (void)hipEventDestroy(o.ev_b[p]);
@@ -2566,7 +2613,7 @@ void odom_destroy(OdomGPU& o) {
     prim_free(o.prim);
     prim_free(o.vprim);
     for (int c = 0; c < kMaxC; ++c) {
-        (void)hipFree(o.map[c]);
+        for (int q = 0; q < 2; ++q) (void)hipFree(o.mapset[q][c]);
         (void)hipFree(o.app[c]);
     }
     void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.seg_out,
@@ -2633,9 +2680,10 @@ void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s) {
                  clouds_w(sb.ds));
 }
 
-void odom_enqueue_export(OdomGPU& o, hipStream_t s) {
+void odom_enqueue_export(OdomGPU& o, hipStream_t s, bool after_update) {
     if (!o.export_maps) return;
-    hipLaunchKernelGGL(k_map_export, dim3(256), dim3(256), 0, s, o.cnt, clouds_w(o.map), clouds_w(o.h_map_dev),
+    hipLaunchKernelGGL(k_map_export, dim3(256), dim3(256), 0, s, o.cnt,
+                       clouds_w(after_update ? map_next(o) : map_cur(o)), clouds_w(o.h_map_dev),
                        o.h_map_n_dev, o.cls.nc);
 }
 
@@ -2643,7 +2691,7 @@ void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s) {
     StageBuf& sb = o.sb[p];
     const int nc = o.cls.nc;
     hipLaunchKernelGGL(k_pull_counts, dim3(1), dim3(64), 0, s, o.cnt, sb.cnt);
-    PF_LAUNCH_NC(nc, k_init_map, dim3(kGrid), dim3(256), 0, s, o.cnt, clouds(sb.in), clouds_w(o.map));
+    PF_LAUNCH_NC(nc, k_init_map, dim3(kGrid), dim3(256), 0, s, o.cnt, clouds(sb.in), clouds_w(map_cur(o)));
     hipLaunchKernelGGL(k_init_counts, dim3(1), dim3(64), 0, s, o.cnt, o.st, nc);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, o.st, o.poses, (int)o.pose_cap, 0, o.acc);
     o.opt_count_host = 12;
@@ -2660,54 +2708,54 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     // as the tail of the bounds kernel it overlaps for free)
     // grids of the class maps (kd-tree builds, :249-250 / BPF :723-725); the pose prediction rides on
     // the bounds kernel as its tail (it reads the map sizes of the previous frame, not the grid)
-    GridPtrs gp{{o.map[0], o.map[1], o.map[2]}, {cnt + C_M, cnt + C_M + 1, cnt + C_M + 2}, nc};
+    GridPtrs gp{{map_cur(o)[0], map_cur(o)[1], map_cur(o)[2]}, {cnt + C_M, cnt + C_M + 1, cnt + C_M + 2}, nc};
     hipLaunchKernelGGL(k_grid_bounds<PredictTail>, dim3(kGridBoundsBlocks + 1), dim3(256), 0, s,
                        grid_bounds_args(o.grid, gp), PredictTail{o.st, cnt, sb.cnt, o.acc, o.cls});
     grid_build(o.grid, gp, o.prim, s, true);
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
-        AssocArgs aa{o.st, cnt, o.acc, gv, o.cls, clouds(sb.ds), clouds(o.map), o.nbr, o.qflag, o.geo, o.spars,
+        AssocArgs aa{o.st, cnt, o.acc, gv, o.cls, clouds(sb.ds), clouds(map_cur(o)), o.nbr, o.qflag, o.geo, o.spars,
                      o.roundv, o.pbkt, o.pnext, (u32)o.map_cap, o.lm_ticket, o.lm_part};
         PF_LAUNCH_NC(nc, k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
-        ObsArgs oa{cnt, o.acc, o.cls, clouds(o.map), clouds_w(sb.ds), o.nbr, o.qflag, o.pbkt, o.pnext, o.tailinc,
+        ObsArgs oa{cnt, o.acc, o.cls, clouds(map_cur(o)), clouds_w(sb.ds), o.nbr, o.qflag, o.pbkt, o.pnext, o.tailinc,
                    (u32)o.map_cap, o.roundv, o.spars, o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max,
                    o.errw + E_LM};
         PF_LAUNCH_NC(nc, k_observe, dim3(kGrid), dim3(256), 0, s, oa);
         LmArgs la{o.st, cnt, o.acc, o.cls, o.lm, o.lm_part, o.lm_ticket, o.qflag, clouds(sb.ds), o.geo, o.observe,
-                  o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.pbkt, clouds_w(o.map), (u32)o.map_cap,
+                  o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.pbkt, clouds_w(map_cur(o)), (u32)o.map_cap,
                   o.errw + E_LM};
         PF_LAUNCH_NC(nc, k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
     }
     // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647, BPF :1197-1290)
     const VgLeaf leaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}};
     if (!o.tie_order && !o.rg_radix) {                    // rgbds by merge (the map stays in key order)
-        RgmArgs ra{o.st, cnt, o.acc, clouds(o.map), clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap, leaf,
-                   o.prm.k_new, o.prm.theta_p, o.prm.theta_max, o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_vox,
-                   o.rgm_kflag, o.seg_out, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err,
-                   o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp, o.rgm_stat};
+        RgmArgs ra{o.st, cnt, o.acc, clouds(map_cur(o)), clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap,
+                   leaf, o.prm.k_new, o.prm.theta_p, o.prm.theta_max, o.rgm_okey, o.rgm_key64, o.rgm_vtag,
+                   o.rgm_vox, o.rgm_kflag, clouds_w(map_next(o)), (u32)o.map_cap, o.errw + E_MAP, o.tail_status,
+                   (u32*)(o.tail_status + o.tail_tiles), o.prim.err, o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp,
+                   o.rgm_stat};
         PF_LAUNCH_NC(nc, k_rgm_bucket, dim3(kRgmBuckets + 1), dim3(kRgmThreads), 0, s, ra);
         PF_LAUNCH_NC(nc, k_rgm_fallback, dim3(1), dim3(kRgmThreads), 0, s, ra);
-        PF_LAUNCH_NC(nc, k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, clouds_w(o.map));
         return;
     }
     if (rg_fused_keys(o.leaf_rg, nc)) {
-        PF_LAUNCH_NC(nc, k_rg_append_keys, dim3(kGrid + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map),
+        PF_LAUNCH_NC(nc, k_rg_append_keys, dim3(kGrid + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(map_cur(o)),
                      clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap, leaf, o.keys, o.vals,
                      sort_hist(o.prim, 32, true));
     } else {
-        PF_LAUNCH_NC(nc, k_rg_append_minmax, dim3(256 + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map),
+        PF_LAUNCH_NC(nc, k_rg_append_minmax, dim3(256 + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(map_cur(o)),
                      clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap);
-        PF_LAUNCH_NC(nc, k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, clouds(o.map), clouds(o.app),
+        PF_LAUNCH_NC(nc, k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, clouds(map_cur(o)), clouds(o.app),
                      leaf, o.keys, o.vals, sort_hist(o.prim, 32, true));
     }
     if (o.tie_order) tie_sort_enqueue(*o.tie_b, o.keys, o.vals, cnt + C_NRG, o.prim, s);
     radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
     if (o.tie_order) tie_sort_finish(*o.tie_b, o.keys, o.vals, s);        // std::sort's order (:74)
-    RgTailArgs ta{cnt, clouds(o.map), clouds(o.app), o.keys, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,
+    RgTailArgs ta{cnt, clouds(map_cur(o)), clouds(o.app), o.keys, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,
                   o.prm.theta_max, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err};
     const unsigned tail_grid = (unsigned)(o.tail_tiles < (size_t)kSortMaxBlocks ? o.tail_tiles : kSortMaxBlocks);
     PF_LAUNCH_NC(nc, k_rg_tail, dim3(tail_grid > 0 ? tail_grid : 1), dim3(256), 0, s, ta);
-    PF_LAUNCH_NC(nc, k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, clouds_w(o.map));
+    PF_LAUNCH_NC(nc, k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, clouds_w(map_next(o)));
 }
 
 // the association kNN probe (pf_odom.h)
