@@ -1738,6 +1738,7 @@ struct RgmArgs {
     u64* ktmp;
     u32* vtmp;
     int* stat;             // [8] (OdomGPU::rgm_stat)
+    unsigned long long* dbg;   // development probe (PF_PROBE): [64 + 10 b + i] phase timestamps of bucket b
 };
 
 // the frame's crop box (as k_rg_append_keys)
@@ -1880,6 +1881,10 @@ __device__ __forceinline__ u32 block_excl_scan1024(u32 v, u32* lds, u32& total) 
 
 // block b < kRgmBuckets: bucket b (map points [lo, hi) = [b M / R, (b + 1) M / R), appended points
 // whose key lies in [key(lo), key(hi))); block kRgmBuckets: the pose step (as in k_rg_append_keys)
+#define RGM_MARK(i)                                                                              \
+    do {                                                                                         \
+        if (a.dbg && t == 0) a.dbg[64 + 10 * b + (i)] = __builtin_amdgcn_s_memrealtime();        \
+    } while (0)
 template <int NC>
 __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     __shared__ u64 bk[kRgmBucketCap];
@@ -1906,6 +1911,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
     const RgmBox box = rgm_box(a.st);
     const int lo = (int)(((long long)b * M) / kRgmBuckets), hi = (int)(((long long)(b + 1) * M) / kRgmBuckets);
+    RGM_MARK(0);
     const int nold = hi - lo;
     const bool cache = nold <= kRgmOldLds;
     // 1. this bucket's map points: keys, crop flags, still in key order?
@@ -1929,6 +1935,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     if (t < kMaxC) s_cls[t] = 0;
     if (__any(unsorted) && lane_id() == 0) a.stat[0] = 1;
     __syncthreads();
+    RGM_MARK(1);
     // 2. every appended point: its bucket is the number of splitters 1 .. R - 1 at or below its key (a
     // binary search; on keys out of order still one bucket per point, so the fallback sees every key);
     // those of lower buckets are counted, this bucket's kept
@@ -1964,6 +1971,8 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     for (int w = 0; w < kRgmThreads / 64; ++w) nbefore += s_before[w];
     const bool overflow = s_cnt > kRgmBucketCap;       // too many: the fallback sorts (still take part below)
     const int cb = overflow ? 0 : s_cnt;
+    RGM_MARK(2);
+    if (a.dbg && t == 0) a.dbg[64 + 10 * b + 9] = (unsigned long long)s_cnt;
     if (overflow && t == 0) a.stat[0] = 1;
     // 3. sort the bucket's appended points by (key, element)
     if (cb <= kRgmThreads) {
@@ -2024,6 +2033,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
             }
     }
     __syncthreads();
+    RGM_MARK(3);
     // 4. voxels. Merged order: a map point after the appended points below it (equal keys: map points
     // first), an appended point after the map points at or below it. A voxel (a run of equal keys) is
     // reduced by the thread of its first element in this bucket: its map points in map order, then its
@@ -2089,6 +2099,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         a.kflag[P] = flag;
     }
     __syncthreads();
+    RGM_MARK(4);
     // 5. the kept voxels' ranks in merged order (tiles of 1024); per class, the kept voxels of earlier
     // buckets by a look-back (wave c for class c); a voxel of class c goes to mapw[c] at (its bucket's
     // class-c offset) + (its rank among the bucket's class-c voxels), classes being contiguous in key
@@ -2103,12 +2114,15 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         if (f) a.kflag[base + p] = (fl & 0xC0000000u) | (run + ex + 1);
         run += tot;
     }
+    RGM_MARK(5);
     if ((t >> 6) < NC) {
+    
         const int c = t >> 6;
         const u32 excl = tile_lookback(a.status + c * kRgmBuckets, b, (u32)s_cls[c], a.err);
         if (lane_id() == 0) s_pref[c] = excl;
     }
     __syncthreads();
+    RGM_MARK(6);
     u32 first_rank[kMaxC];                             // bucket-local rank of the first voxel of class c
     {
         u32 acc = 0;
@@ -2128,6 +2142,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         else over = true;
     }
     if (over && !a.stat[0]) atomicOr(a.err_map, 1);     // (out-of-order input: the fallback redoes it)
+    RGM_MARK(7);
     // 6. the kept voxels of every class summed over the buckets; the last bucket to arrive writes the
     // map sizes (cnt[C_M + c]), the class boundaries (cnt[C_NLT + c - 1] = kept voxels of classes < c)
     // and the total unless the fallback will, and clears the accumulators and the look-back words
@@ -2513,8 +2528,8 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
 #undef PF_ALLOC
     trace_create("buffers");
     if (std::getenv("PF_PROBE")) {                 // development probe: LM phase timestamps
-        if (hipMalloc(&o.dbg, sizeof(unsigned long long) * 64) != hipSuccess) return PF_ENOMEM;
-        if (hipMemset(o.dbg, 0, sizeof(unsigned long long) * 64) != hipSuccess) return PF_EHIP;
+        if (hipMalloc(&o.dbg, sizeof(unsigned long long) * 512) != hipSuccess) return PF_ENOMEM;
+        if (hipMemset(o.dbg, 0, sizeof(unsigned long long) * 512) != hipSuccess) return PF_EHIP;
     }
     if (hipHostMalloc(&o.h_cnt, sizeof(int) * (C_COUNT + E_COUNT)) != hipSuccess) return PF_ENOMEM;   // + errw mirror
     if (hipHostMalloc(&o.h_pose, sizeof(double) * 8) != hipSuccess) return PF_ENOMEM;
@@ -2733,7 +2748,7 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
                    leaf, o.prm.k_new, o.prm.theta_p, o.prm.theta_max, o.rgm_okey, o.rgm_key64, o.rgm_vtag,
                    o.rgm_vox, o.rgm_kflag, clouds_w(map_next(o)), (u32)o.map_cap, o.errw + E_MAP, o.tail_status,
                    (u32*)(o.tail_status + o.tail_tiles), o.prim.err, o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp,
-                   o.rgm_stat};
+                   o.rgm_stat, o.dbg};
         PF_LAUNCH_NC(nc, k_rgm_bucket, dim3(kRgmBuckets + 1), dim3(kRgmThreads), 0, s, ra);
         PF_LAUNCH_NC(nc, k_rgm_fallback, dim3(1), dim3(kRgmThreads), 0, s, ra);
         return;
