@@ -2174,27 +2174,29 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     if (t < NC * kRgmBuckets) __hip_atomic_store(&a.status[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Fallback: one 1024-thread workgroup sorts all n (key64, vtag) pairs of element order stably by
+constexpr int kFbThreads = 256;
+
+// Fallback: one 256-thread workgroup (a cheap launch when it has nothing to do) sorts all n (key64, vtag) pairs of element order stably by
 // key into (kout, vout): LSD radix over 8-bit digits, passes whose digit is the same for every key
-// skipped; tiles of 4096 keys ranked as in k_os_pass (a wave's 256 keys by match_bits, wave offsets
+// skipped; tiles of 1024 keys ranked as in k_os_pass (a wave's 256 keys by match_bits, wave offsets
 // by one barrier), one running digit base instead of a look-back.
 __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
     __shared__ u32 hist[8][256];
-    __shared__ u32 wcnt[kRgmThreads / 64][256];
+    __shared__ u32 wcnt[kFbThreads / 64][256];
     __shared__ u32 gbase[256], toff[256];
     __shared__ int s_one[8];
     const int t = threadIdx.x, w = t >> 6, l = lane_id();
     const u64 lt = lanemask_lt();
-    for (int i = t; i < 8 * 256; i += kRgmThreads) (&hist[0][0])[i] = 0;
+    for (int i = t; i < 8 * 256; i += kFbThreads) (&hist[0][0])[i] = 0;
     if (t < 8) s_one[t] = 0;
     __syncthreads();
-    for (int i = t; i < n; i += kRgmThreads) {
+    for (int i = t; i < n; i += kFbThreads) {
         const u64 k = a.key64[i];
 #pragma unroll
         for (int p = 0; p < 8; ++p) atomicAdd(&hist[p][(u32)(k >> (8 * p)) & 255u], 1u);
     }
     __syncthreads();
-    for (int i = t; i < 8 * 256; i += kRgmThreads)
+    for (int i = t; i < 8 * 256; i += kFbThreads)
         if ((&hist[0][0])[i] == (u32)n) s_one[i >> 8] = 1;       // a digit the same for every key
     __syncthreads();
     int active[8], P = 0;
@@ -2203,7 +2205,7 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
     const u64* ks = a.key64;
     const u32* vs = a.vtag;
     if (P == 0) {
-        for (int i = t; i < n; i += kRgmThreads) {
+        for (int i = t; i < n; i += kFbThreads) {
             a.kout[i] = ks[i];
             a.vout[i] = vs[i];
         }
@@ -2221,7 +2223,7 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
             gbase[t] = s;
         }
         __syncthreads();
-        for (int base = 0; base < n; base += kRgmThreads * 4) {
+        for (int base = 0; base < n; base += kFbThreads * 4) {
             u64 key[4];
             u32 val[4], rk[4], dg[4];
 #pragma unroll
@@ -2247,7 +2249,7 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
             __syncthreads();
             if (t < 256) {
                 u32 acc = 0;
-                for (int ww = 0; ww < kRgmThreads / 64; ++ww) {
+                for (int ww = 0; ww < kFbThreads / 64; ++ww) {
                     const u32 c = wcnt[ww][t];
                     wcnt[ww][t] = acc;
                     acc += c;
@@ -2281,13 +2283,13 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
 // class-map index, and the map sizes and class boundaries are written
 template <int NC>
 __device__ void rgm_fallback_tail(const RgmArgs& a, const RgView<NC>& V, int n) {
-    __shared__ u32 s_w[kRgmThreads / 64];
+    __shared__ u32 s_w[kFbThreads / 64];
     __shared__ int s_cls[kMaxC];
     const int t = threadIdx.x;
     if (t < kMaxC) s_cls[t] = 0;
     __syncthreads();
     u32 run = 0;
-    for (int t0 = 0; t0 < n; t0 += kRgmThreads) {
+    for (int t0 = 0; t0 < n; t0 += kFbThreads) {
         const int i = t0 + t;
         u32 flag = 0, cls = 0;
         float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2312,7 +2314,7 @@ __device__ void rgm_fallback_tail(const RgmArgs& a, const RgView<NC>& V, int n) 
             }
         }
         u32 tot;
-        const u32 ex = block_excl_scan1024(flag, s_w, tot);
+        const u32 ex = block_excl_scan256(flag, s_w, tot);
         if (flag) {                                    // by kept rank: the output and its class
             a.vox[run + ex] = out;
             a.kflag[run + ex] = cls;
@@ -2326,7 +2328,7 @@ __device__ void rgm_fallback_tail(const RgmArgs& a, const RgView<NC>& V, int n) 
 #pragma unroll
     for (int c = 1; c <= kMaxC; ++c) low[c] = low[c - 1] + s_cls[c - 1];
     bool over = false;
-    for (u32 r = t; r < run; r += kRgmThreads) {
+    for (u32 r = t; r < run; r += kFbThreads) {
         const int c = min((int)a.kflag[r], NC - 1);
         const u32 idx = r - (u32)low[c];
         if (idx < a.map_cap) a.mapw.at(c)[idx] = a.vox[r];
@@ -2342,7 +2344,7 @@ __device__ void rgm_fallback_tail(const RgmArgs& a, const RgView<NC>& V, int n) 
 }
 
 template <int NC>
-__global__ void __launch_bounds__(kRgmThreads) k_rgm_fallback(RgmArgs a) {
+__global__ void __launch_bounds__(kFbThreads) k_rgm_fallback(RgmArgs a) {
     if (!a.stat[0]) return;                            // the buckets' output stands
     const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
     const int n = V.total();
@@ -2750,7 +2752,7 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
                    (u32*)(o.tail_status + o.tail_tiles), o.prim.err, o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp,
                    o.rgm_stat, o.dbg};
         PF_LAUNCH_NC(nc, k_rgm_bucket, dim3(kRgmBuckets + 1), dim3(kRgmThreads), 0, s, ra);
-        PF_LAUNCH_NC(nc, k_rgm_fallback, dim3(1), dim3(kRgmThreads), 0, s, ra);
+        PF_LAUNCH_NC(nc, k_rgm_fallback, dim3(1), dim3(kFbThreads), 0, s, ra);
         return;
     }
     if (rg_fused_keys(o.leaf_rg, nc)) {
