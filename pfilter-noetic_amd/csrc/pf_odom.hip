@@ -1881,6 +1881,85 @@ __device__ __forceinline__ u32 block_excl_scan1024(u32 v, u32* lds, u32& total) 
 
 // block b < kRgmBuckets: bucket b (map points [lo, hi) = [b M / R, (b + 1) M / R), appended points
 // whose key lies in [key(lo), key(hi))); block kRgmBuckets: the pose step (as in k_rg_append_keys)
+// Bitonic sort of bk / bt[0 .. cb) (cb <= E * 1024) by (key, element), E elements per thread in
+// registers: element e of thread t is index e * 1024 + t, so partners at distance >= 1024 are in the
+// same thread (register compare), at 64 .. 512 in another wave (through LDS, two barriers), below 64 in
+// the same wave (shuffles)
+template <int E>
+__device__ __forceinline__ void rgm_sort_regs(u64* bk, u32* bt, int cb) {
+    const int t = threadIdx.x;
+    constexpr int S = E * kRgmThreads;
+    u64 k[E];
+    u32 g[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = e * kRgmThreads + t;
+        k[e] = i < cb ? bk[i] : ~0ull;
+        g[e] = i < cb ? bt[i] : ~0u;
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= S; kk <<= 1) {
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j >= kRgmThreads) {
+                const int je = j / kRgmThreads;
+#pragma unroll
+                for (int e = 0; e < E; ++e)
+#pragma unroll
+                    for (int e2 = e + 1; e2 < E; ++e2) {           // static register indices
+                        if ((e & je) || e2 != (e | je)) continue;
+                        const bool up = ((e * kRgmThreads + t) & kk) == 0;
+                        const bool sw = up ? rgm_less(k[e2], g[e2], k[e], g[e]) : rgm_less(k[e], g[e], k[e2], g[e2]);
+                        if (sw) {
+                            const u64 tk = k[e]; k[e] = k[e2]; k[e2] = tk;
+                            const u32 tg = g[e]; g[e] = g[e2]; g[e2] = tg;
+                        }
+                    }
+                continue;
+            }
+            u64 pk[E];
+            u32 pg[E];
+            if (j < 64) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const u32 lo32 = (u32)__shfl_xor((int)(u32)k[e], j, 64);
+                    const u32 hi32 = (u32)__shfl_xor((int)(u32)(k[e] >> 32), j, 64);
+                    pk[e] = ((u64)hi32 << 32) | lo32;
+                    pg[e] = (u32)__shfl_xor((int)g[e], j, 64);
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    bk[e * kRgmThreads + t] = k[e];
+                    bt[e * kRgmThreads + t] = g[e];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    pk[e] = bk[e * kRgmThreads + (t ^ j)];
+                    pg[e] = bt[e * kRgmThreads + (t ^ j)];
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int i = e * kRgmThreads + t;
+                const bool up = (i & kk) == 0, lower = (t & j) == 0;
+                const bool pless = rgm_less(pk[e], pg[e], k[e], g[e]);
+                // the lower index of an ascending pair keeps the smaller element
+                if ((lower == up) ? pless : !pless && !(pk[e] == k[e] && pg[e] == g[e])) {
+                    k[e] = pk[e];
+                    g[e] = pg[e];
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        bk[e * kRgmThreads + t] = k[e];
+        bt[e * kRgmThreads + t] = g[e];
+    }
+}
+
 #define RGM_MARK(i)                                                                              \
     do {                                                                                         \
         if (a.dbg && t == 0) a.dbg[64 + 10 * b + (i)] = __builtin_amdgcn_s_memrealtime();        \
@@ -1975,63 +2054,9 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     if (a.dbg && t == 0) a.dbg[64 + 10 * b + 9] = (unsigned long long)s_cnt;
     if (overflow && t == 0) a.stat[0] = 1;
     // 3. sort the bucket's appended points by (key, element)
-    if (cb <= kRgmThreads) {
-        // one element per thread; partners within a wave by shuffles, across waves through LDS
-        u64 k = t < cb ? bk[t] : ~0ull;
-        u32 g = t < cb ? bt[t] : ~0u;
-        __syncthreads();
-        for (int kk = 2; kk <= kRgmThreads; kk <<= 1) {
-            for (int j = kk >> 1; j > 0; j >>= 1) {
-                u64 pk;
-                u32 pg;
-                if (j < 64) {
-                    const u32 lo32 = (u32)__shfl_xor((int)(u32)k, j, 64), hi32 = (u32)__shfl_xor((int)(u32)(k >> 32), j, 64);
-                    pk = ((u64)hi32 << 32) | lo32;
-                    pg = (u32)__shfl_xor((int)g, j, 64);
-                } else {
-                    bk[t] = k;
-                    bt[t] = g;
-                    __syncthreads();
-                    pk = bk[t ^ j];
-                    pg = bt[t ^ j];
-                    __syncthreads();
-                }
-                const bool up = (t & kk) == 0, lower = (t & j) == 0;
-                const bool pless = rgm_less(pk, pg, k, g);
-                // the lower index of an ascending pair keeps the smaller element
-                if ((lower == up) ? pless : !pless && !(pk == k && pg == g)) {
-                    k = pk;
-                    g = pg;
-                }
-            }
-        }
-        bk[t] = k;
-        bt[t] = g;
-    } else {
-        int S = kRgmThreads;
-        while (S < cb) S <<= 1;
-        for (int i = cb + t; i < S; i += kRgmThreads) {
-            bk[i] = ~0ull;
-            bt[i] = ~0u;
-        }
-        __syncthreads();
-        for (int kk = 2; kk <= S; kk <<= 1)
-            for (int j = kk >> 1; j > 0; j >>= 1) {
-                for (int i = t; i < S; i += kRgmThreads) {
-                    const int l = i ^ j;
-                    if (l > i) {
-                        const u64 ki = bk[i], kl = bk[l];
-                        const u32 ti = bt[i], tl = bt[l];
-                        const bool up = (i & kk) == 0;
-                        if (up ? rgm_less(kl, tl, ki, ti) : rgm_less(ki, ti, kl, tl)) {
-                            bk[i] = kl; bk[l] = ki;
-                            bt[i] = tl; bt[l] = ti;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-    }
+    if (cb <= kRgmThreads) rgm_sort_regs<1>(bk, bt, cb);
+    else if (cb <= 2 * kRgmThreads) rgm_sort_regs<2>(bk, bt, cb);
+    else rgm_sort_regs<4>(bk, bt, cb);
     __syncthreads();
     RGM_MARK(3);
     // 4. voxels. Merged order: a map point after the appended points below it (equal keys: map points
