@@ -104,7 +104,7 @@ PF_HD qd m2q(const m3& a) {
     } else {
         int i = 0;
         if (a.m[1][1] > a.m[0][0]) i = 1;
-        if (a.m[2][2] > a.m[i][i]) i = 2;
+        if (a.m[2][2] > (i == 0 ? a.m[0][0] : a.m[1][1])) i = 2;     // a.m[i][i], statically indexed
         if (i == 0) m2q_branch<0>(a, c);             // static indices: no scratch arrays
         else if (i == 1) m2q_branch<1>(a, c);
         else m2q_branch<2>(a, c);

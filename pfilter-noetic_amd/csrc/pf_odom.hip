@@ -759,6 +759,176 @@ __device__ __forceinline__ void pidx_apply(const int* nbr, const u32* tailinc, i
     }
 }
 
+// the rgbds input of every class: its map, then its appended points (map c, app c, in class order)
+template <int NC>
+struct RgView {
+    Clouds map, app;
+    int m[kMaxC];          // map sizes
+    int end[kMaxC];        // cumulative (map + appended) sizes
+    __device__ __forceinline__ int total() const { return end[NC - 1]; }
+    // class c, local index li, appended or not, of element v
+    __device__ __forceinline__ void locate(int v, int& c, int& li, bool& appended) const {
+        c = NC == 2 ? (v < end[0] ? 0 : 1) : (v < end[0] ? 0 : (v < end[1] ? 1 : 2));
+        const int l = v - sel3(c, 0, end[0], end[1]);
+        const int mc = sel3(c, m[0], m[1], m[2]);
+        appended = l >= mc;
+        li = appended ? l - mc : l;
+    }
+    __device__ __forceinline__ float4 at(int v, int& c) const {
+        int li;
+        bool ap;
+        locate(v, c, li, ap);
+        return (ap ? app.at(c) : map.at(c))[li];
+    }
+};
+
+template <int NC>
+__device__ __forceinline__ RgView<NC> rg_view(const int* cnt, Clouds map, Clouds app) {
+    RgView<NC> V;
+    V.map = map;
+    V.app = app;
+    int acc = 0;
+#pragma unroll
+    for (int c = 0; c < kMaxC; ++c) {
+        V.m[c] = c < NC ? cnt[C_M + c] : 0;
+        acc += c < NC ? cnt[C_M + c] + cnt[C_DS + c] : 0;
+        V.end[c] = acc;
+    }
+    return V;
+}
+
+constexpr int kRgmThreads = 256;
+constexpr int kRgmBuckets = 128;
+constexpr int kRgmBucketCap = 2048;     // appended points a bucket sorts
+constexpr int kRgmOldLds = 2048;        // map points of a bucket cached in LDS
+constexpr u32 kRgmDrop = 0x80000000u;
+
+// the frame's crop box (as k_rg_append_keys)
+struct RgmBox {
+    float lo[3], hi[3];
+    __device__ __forceinline__ bool in(float4 p) const {
+        return !((p.x < lo[0] || p.y < lo[1] || p.z < lo[2]) || (p.x > hi[0] || p.y > hi[1] || p.z > hi[2]));
+    }
+};
+__device__ __forceinline__ RgmBox rgm_box(const double* prm) {
+    RgmBox b;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        b.lo[k] = (float)(prm[4 + k] - 100);
+        b.hi[k] = (float)(prm[4 + k] + 100);
+    }
+    return b;
+}
+// voxel coordinate floor(v / lf) relative to the crop box's voxel origin, biased by 2^19 and clamped
+// (monotone, so the order of clamped keys is the order of the points; inside the box exact)
+__device__ __forceinline__ u64 rgm_axis(float v, float lo, float lf) {
+    float d = floorf(v / lf) - (float)(int)floorf(lo / lf);
+    d = fminf(fmaxf(d, -524288.f), 524287.f);
+    return (u64)((int)d + 524288);
+}
+__device__ __forceinline__ u64 rgm_key(float4 p, int c, float lf, const RgmBox& b) {
+    return ((u64)c << 62) | (rgm_axis(p.z, b.lo[2], lf) << 40) | (rgm_axis(p.y, b.lo[1], lf) << 20) |
+           rgm_axis(p.x, b.lo[0], lf);
+}
+__device__ __forceinline__ bool rgm_less(u64 ka, u32 ta, u64 kb, u32 tb) {
+    return ka < kb || (ka == kb && (ta & ~kRgmDrop) < (tb & ~kRgmDrop));
+}
+
+// element index of map point g (map order over the classes) / appended point a
+template <int NC>
+__device__ __forceinline__ int rgm_old_elem(const RgView<NC>& V, int g, int& c, int& li) {
+    int start = 0, acc = 0;
+    c = NC - 1;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        const int mk = V.m[k];
+        if (g < acc + mk) { c = k; break; }
+        acc += mk;
+        start = V.end[k];
+    }
+    li = g - acc;
+    return start + li;
+}
+template <int NC>
+__device__ __forceinline__ int rgm_app_elem(const RgView<NC>& V, int a, int& c, int& li) {
+    int start = 0, acc = 0;
+    c = NC - 1;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        const int ak = V.end[k] - (k ? V.end[k - 1] : 0) - V.m[k];
+        if (a < acc + ak) { c = k; break; }
+        acc += ak;
+        start = V.end[k];
+    }
+    li = a - acc;
+    const int mc = sel3(c, V.m[0], V.m[1], V.m[2]);
+    return start + mc + li;
+}
+template <int NC>
+__device__ __forceinline__ float4 rgm_old_point(const RgView<NC>& V, int g, int& c) {
+    int li;
+    (void)rgm_old_elem<NC>(V, g, c, li);
+    return V.map.at(c)[li];
+}
+template <int NC>
+__device__ __forceinline__ u64 rgm_old_key(const RgView<NC>& V, const VgLeaf& leaf, const RgmBox& box, int g) {
+    int c;
+    const float4 p = rgm_old_point<NC>(V, g, c);
+    return rgm_key(p, c, leaf.at(c), box);
+}
+
+// lower / upper bound of k in sorted keys[0 .. n) (LDS or global)
+__device__ __forceinline__ int rgm_lower(const u64* keys, int n, u64 k) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < k) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int rgm_upper(const u64* keys, int n, u64 k) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] <= k) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// The rgbds merge's appended points, prepared by the last LM launch of an update (k_lm_solve's
+// workgroups, once the pose is solved): pointAssociateToMap (:592-604) of every down-sampled point
+// with the solved parameters x, its voxel key and its crop flag (k_rgm_bucket reads them)
+struct RgmPrep {
+    int on;
+    Clouds ds;
+    CloudsW app;
+    u64* key64;
+    u32* vtag;
+    VgLeaf leaf;
+};
+template <int NC>
+__device__ __forceinline__ void rgm_prep_apps(const RgmPrep& r, const int* cnt, const double* x) {
+    const RgView<NC> V = rg_view<NC>(cnt, Clouds{{nullptr, nullptr, nullptr}}, Clouds{{nullptr, nullptr, nullptr}});
+    int M = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) M += V.m[c];
+    const int A = V.total() - M;
+    double prm[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) prm[k] = x[k];
+    const RgmBox box = rgm_box(prm);
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < A; q += gridDim.x * blockDim.x) {
+        int c, li;
+        const int e = rgm_app_elem<NC>(V, q, c, li);
+        const float4 p = associate(prm, r.ds.at(c)[li]);
+        r.app.at(c)[li] = p;
+        r.key64[e] = rgm_key(p, c, r.leaf.at(c), box);
+        r.vtag[e] = (u32)e | (box.in(p) ? 0u : kRgmDrop);
+    }
+}
+
 // ------------------------------------ LM (B.6) ----------------------------------------------
 // Ceres 1.14 trust-region loop of one outer iteration in ONE launch. Per evaluation (<= 1 + kMaxIter
 // = 5) the kept residual blocks are split into kLmBlocks fixed *chunks* (chunk c = the queries
@@ -1065,6 +1235,7 @@ struct LmArgs {
     CloudsW map;
     u32 map_cap;
     int* err;              // sticky error word E_LM
+    RgmPrep prep;          // the last launch of an update prepares the rgbds merge's appended points
 };
 
 template <int NC>
@@ -1087,6 +1258,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     for (int c = 0; c < NC; ++c) nres += a.cnt[C_KEPT + c];
     if (!a.st->gate || nres == 0) {                              // no residual blocks: untouched
         pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
+        if (a.prep.on) rgm_prep_apps<NC>(a.prep, a.cnt, a.st->params);
         return;
     }
     // the weight bounds and this thread's home residual live in LDS, not in registers: the serial
@@ -1310,6 +1482,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         atomicAdd(&a.cnt[C_LM_ITERS], lm.iteration);
         *a.lm_out = lm;
     }
+    if (a.prep.on) rgm_prep_apps<NC>(a.prep, a.cnt, lm.best);   // every workgroup holds the solution
 }
 
 // ---------------------------------- pose / map update ---------------------------------------
@@ -1341,43 +1514,6 @@ __global__ void k_finalize(DevState* __restrict__ st, double* __restrict__ poses
     finalize_pose(st, poses, pose_cap, mode, acc, prm);
 }
 
-// the rgbds input of every class: its map, then its appended points (map c, app c, in class order)
-template <int NC>
-struct RgView {
-    Clouds map, app;
-    int m[kMaxC];          // map sizes
-    int end[kMaxC];        // cumulative (map + appended) sizes
-    __device__ __forceinline__ int total() const { return end[NC - 1]; }
-    // class c, local index li, appended or not, of element v
-    __device__ __forceinline__ void locate(int v, int& c, int& li, bool& appended) const {
-        c = NC == 2 ? (v < end[0] ? 0 : 1) : (v < end[0] ? 0 : (v < end[1] ? 1 : 2));
-        const int l = v - sel3(c, 0, end[0], end[1]);
-        const int mc = sel3(c, m[0], m[1], m[2]);
-        appended = l >= mc;
-        li = appended ? l - mc : l;
-    }
-    __device__ __forceinline__ float4 at(int v, int& c) const {
-        int li;
-        bool ap;
-        locate(v, c, li, ap);
-        return (ap ? app.at(c) : map.at(c))[li];
-    }
-};
-
-template <int NC>
-__device__ __forceinline__ RgView<NC> rg_view(const int* cnt, Clouds map, Clouds app) {
-    RgView<NC> V;
-    V.map = map;
-    V.app = app;
-    int acc = 0;
-#pragma unroll
-    for (int c = 0; c < kMaxC; ++c) {
-        V.m[c] = c < NC ? cnt[C_M + c] : 0;
-        acc += c < NC ? cnt[C_M + c] + cnt[C_DS + c] : 0;
-        V.end[c] = acc;
-    }
-    return V;
-}
 
 // CropBox bounds t +- 100 as float, inclusive (:606-615, B.2)
 __device__ __forceinline__ bool in_crop(const DevState* st, float4 p) {
@@ -1704,11 +1840,6 @@ __global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const f
 // rounded into a neighbouring voxel) or a bucket holds more than kRgmBucketCap appended points, the
 // buckets' output is void and k_rgm_fallback's single workgroup sorts every element (a stable LSD
 // radix sort over the 64-bit keys) and reduces the voxels itself.
-constexpr int kRgmThreads = 1024;
-constexpr int kRgmBuckets = 32;
-constexpr int kRgmBucketCap = 4096;     // appended points a bucket sorts
-constexpr int kRgmOldLds = 4096;        // map points of a bucket cached in LDS
-constexpr u32 kRgmDrop = 0x80000000u;
 
 struct RgmArgs {
     DevState* st;
@@ -1740,100 +1871,6 @@ struct RgmArgs {
     int* stat;             // [8] (OdomGPU::rgm_stat)
     unsigned long long* dbg;   // development probe (PF_PROBE): [64 + 10 b + i] phase timestamps of bucket b
 };
-
-// the frame's crop box (as k_rg_append_keys)
-struct RgmBox {
-    float lo[3], hi[3];
-    __device__ __forceinline__ bool in(float4 p) const {
-        return !((p.x < lo[0] || p.y < lo[1] || p.z < lo[2]) || (p.x > hi[0] || p.y > hi[1] || p.z > hi[2]));
-    }
-};
-__device__ __forceinline__ RgmBox rgm_box(const DevState* st) {
-    RgmBox b;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        b.lo[k] = (float)(st->params[4 + k] - 100);
-        b.hi[k] = (float)(st->params[4 + k] + 100);
-    }
-    return b;
-}
-// voxel coordinate floor(v / lf) relative to the crop box's voxel origin, biased by 2^19 and clamped
-// (monotone, so the order of clamped keys is the order of the points; inside the box exact)
-__device__ __forceinline__ u64 rgm_axis(float v, float lo, float lf) {
-    float d = floorf(v / lf) - (float)(int)floorf(lo / lf);
-    d = fminf(fmaxf(d, -524288.f), 524287.f);
-    return (u64)((int)d + 524288);
-}
-__device__ __forceinline__ u64 rgm_key(float4 p, int c, float lf, const RgmBox& b) {
-    return ((u64)c << 62) | (rgm_axis(p.z, b.lo[2], lf) << 40) | (rgm_axis(p.y, b.lo[1], lf) << 20) |
-           rgm_axis(p.x, b.lo[0], lf);
-}
-__device__ __forceinline__ bool rgm_less(u64 ka, u32 ta, u64 kb, u32 tb) {
-    return ka < kb || (ka == kb && (ta & ~kRgmDrop) < (tb & ~kRgmDrop));
-}
-
-// element index of map point g (map order over the classes) / appended point a
-template <int NC>
-__device__ __forceinline__ int rgm_old_elem(const RgView<NC>& V, int g, int& c, int& li) {
-    int start = 0, acc = 0;
-    c = NC - 1;
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-        const int mk = V.m[k];
-        if (g < acc + mk) { c = k; break; }
-        acc += mk;
-        start = V.end[k];
-    }
-    li = g - acc;
-    return start + li;
-}
-template <int NC>
-__device__ __forceinline__ int rgm_app_elem(const RgView<NC>& V, int a, int& c, int& li) {
-    int start = 0, acc = 0;
-    c = NC - 1;
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-        const int ak = V.end[k] - (k ? V.end[k - 1] : 0) - V.m[k];
-        if (a < acc + ak) { c = k; break; }
-        acc += ak;
-        start = V.end[k];
-    }
-    li = a - acc;
-    const int mc = sel3(c, V.m[0], V.m[1], V.m[2]);
-    return start + mc + li;
-}
-template <int NC>
-__device__ __forceinline__ float4 rgm_old_point(const RgView<NC>& V, int g, int& c) {
-    int li;
-    (void)rgm_old_elem<NC>(V, g, c, li);
-    return V.map.at(c)[li];
-}
-template <int NC>
-__device__ __forceinline__ u64 rgm_old_key(const RgView<NC>& V, const VgLeaf& leaf, const RgmBox& box, int g) {
-    int c;
-    const float4 p = rgm_old_point<NC>(V, g, c);
-    return rgm_key(p, c, leaf.at(c), box);
-}
-
-// lower / upper bound of k in sorted keys[0 .. n) (LDS or global)
-__device__ __forceinline__ int rgm_lower(const u64* keys, int n, u64 k) {
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (keys[mid] < k) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-__device__ __forceinline__ int rgm_upper(const u64* keys, int n, u64 k) {
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (keys[mid] <= k) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
 
 // one voxel of rgbds: the f32 centroid of its points in order and the maxima of r and g (:108-125),
 // then extractstablepoint (:12-14) and the ageing (:634-646)
@@ -1980,15 +2017,10 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     for (int c = 0; c < NC; ++c) M += V.m[c];
     const int A = n - M;
     if (b == kRgmBuckets) {                            // (reads no counter: the last bucket rewrites them)
-        double prm[7];
-        for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
-        finalize_pose(a.st, a.poses, a.pose_cap, 1, a.acc, prm);
+        finalize_pose(a.st, a.poses, a.pose_cap, 1, a.acc, a.st->params);
         return;
     }
-    double prm[7];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) prm[k] = a.st->params[k];
-    const RgmBox box = rgm_box(a.st);
+    const RgmBox box = rgm_box(a.st->params);
     const int lo = (int)(((long long)b * M) / kRgmBuckets), hi = (int)(((long long)(b + 1) * M) / kRgmBuckets);
     RGM_MARK(0);
     const int nold = hi - lo;
@@ -2022,8 +2054,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     for (int q = t; q < A; q += kRgmThreads) {
         int c, li;
         const int e = rgm_app_elem<NC>(V, q, c, li);
-        const float4 p = associate(prm, a.ds.at(c)[li]);
-        const u64 key = rgm_key(p, c, a.leaf.at(c), box);
+        const u64 key = a.key64[e];                   // transformed and keyed by the last LM launch
         int o = 0;                                    // largest bucket with s_split[o] <= key
 #pragma unroll
         for (int step = kRgmBuckets / 2; step > 0; step >>= 1)
@@ -2031,14 +2062,10 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         if (o < b) {
             ++before;
         } else if (o == b) {
-            a.app.at(c)[li] = p;
-            const u32 tag = (u32)e | (box.in(p) ? 0u : kRgmDrop);
-            a.key64[e] = key;
-            a.vtag[e] = tag;
             const int slot = atomicAdd(&s_cnt, 1);
             if (slot < kRgmBucketCap) {
                 bk[slot] = key;
-                bt[slot] = tag;
+                bt[slot] = a.vtag[e];
             }
         }
     }
@@ -2056,7 +2083,8 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     // 3. sort the bucket's appended points by (key, element)
     if (cb <= kRgmThreads) rgm_sort_regs<1>(bk, bt, cb);
     else if (cb <= 2 * kRgmThreads) rgm_sort_regs<2>(bk, bt, cb);
-    else rgm_sort_regs<4>(bk, bt, cb);
+    else if (cb <= 4 * kRgmThreads) rgm_sort_regs<4>(bk, bt, cb);
+    else rgm_sort_regs<8>(bk, bt, cb);
     __syncthreads();
     RGM_MARK(3);
     // 4. voxels. Merged order: a map point after the appended points below it (equal keys: map points
@@ -2162,7 +2190,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         const u32 f = a.kflag[base + p];
         if (!(f & 0x3FFFFFFFu)) continue;
         const int c = min((int)(f >> 30), NC - 1);
-        const u32 idx = s_pref[c] + (f & 0x3FFFFFFFu) - 1u - first_rank[c];
+        const u32 idx = s_pref[c] + (f & 0x3FFFFFFFu) - 1u - sel3(c, first_rank[0], first_rank[1], first_rank[2]);
         if (idx < a.map_cap) a.mapw.at(c)[idx] = a.vox[base + p];
         else over = true;
     }
@@ -2180,15 +2208,18 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     if (!s_last) return;
     if (t == 0) {
         int kc[kMaxC], tot = 0;
+#pragma unroll
         for (int c = 0; c < kMaxC; ++c) {
             kc[c] = __hip_atomic_load(&a.stat[4 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&a.stat[4 + c], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (!__hip_atomic_load(&a.stat[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+#pragma unroll
             for (int c = 1; c <= kMaxC; ++c) {
                 tot += kc[c - 1];
                 a.cnt[C_NLT + c - 1] = tot;
             }
+#pragma unroll
             for (int c = 0; c < NC; ++c) a.cnt[C_M + c] = min(kc[c], (int)a.map_cap);
             a.cnt[C_KEEP_TOTAL] = tot;
             a.cnt[C_NRG] = n;
@@ -2196,7 +2227,8 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         }
         __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (t < NC * kRgmBuckets) __hip_atomic_store(&a.status[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = t; i < NC * kRgmBuckets; i += kRgmThreads)
+        __hip_atomic_store(&a.status[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 constexpr int kFbThreads = 256;
@@ -2224,9 +2256,13 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
     for (int i = t; i < 8 * 256; i += kFbThreads)
         if ((&hist[0][0])[i] == (u32)n) s_one[i >> 8] = 1;       // a digit the same for every key
     __syncthreads();
-    int active[8], P = 0;
+    u32 active = 0;                                    // digits that vary, as a bit mask
+    int P = 0;
     for (int p = 0; p < 8; ++p)
-        if (!s_one[p]) active[P++] = p;
+        if (!s_one[p]) {
+            active |= 1u << p;
+            ++P;
+        }
     const u64* ks = a.key64;
     const u32* vs = a.vtag;
     if (P == 0) {
@@ -2240,7 +2276,8 @@ __device__ void rgm_fallback_sort(const RgmArgs& a, int n) {
     u64* kd = (P & 1) ? a.kout : a.ktmp;
     u32* vd = (P & 1) ? a.vout : a.vtmp;
     for (int pi = 0; pi < P; ++pi) {
-        const int p = active[pi];
+        const int p = __ffs(active) - 1;
+        active &= active - 1;
         const int shift = 8 * p;
         if (t < 256) {                                 // exclusive digit bases
             u32 s = 0;
@@ -2763,9 +2800,12 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
                    (u32)o.map_cap, o.roundv, o.spars, o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max,
                    o.errw + E_LM};
         PF_LAUNCH_NC(nc, k_observe, dim3(kGrid), dim3(256), 0, s, oa);
+        const bool merge = !o.tie_order && !o.rg_radix;
+        const RgmPrep prep{merge && it == o.opt_count_host - 1, clouds(sb.ds), clouds_w(o.app), o.rgm_key64,
+                           o.rgm_vtag, VgLeaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}}};
         LmArgs la{o.st, cnt, o.acc, o.cls, o.lm, o.lm_part, o.lm_ticket, o.qflag, clouds(sb.ds), o.geo, o.observe,
                   o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.pbkt, clouds_w(map_cur(o)), (u32)o.map_cap,
-                  o.errw + E_LM};
+                  o.errw + E_LM, prep};
         PF_LAUNCH_NC(nc, k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
     }
     // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647, BPF :1197-1290)
