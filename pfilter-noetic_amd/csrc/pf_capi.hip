@@ -938,7 +938,7 @@ int pf_odom_poses(pf_odom* h, double* poses, size_t cap, size_t* n) {
 
 // development probe (not part of include/pfilter_hip.h): device timestamps of the last LM solve
 extern "C" int pf_dev_probe(pf_odom* h, unsigned long long* out, int n) {
-    if (!h || !out || n <= 0 || n > 512 || !h->o.dbg) return PF_EINVAL;
+    if (!h || !out || n <= 0 || n > kDbgWords || !h->o.dbg) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->o.device));
     PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
     PF_HIP_TRY(hipMemcpy(out, h->o.dbg, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));

@@ -1871,6 +1871,7 @@ struct RgmArgs {
     int* stat;             // [8] (OdomGPU::rgm_stat)
     unsigned long long* dbg;   // development probe (PF_PROBE): [64 + 10 b + i] phase timestamps of bucket b
 };
+static_assert(64 + 10 * (kRgmBuckets + 1) <= kDbgWords, "probe words");
 
 // one voxel of rgbds: the f32 centroid of its points in order and the maxima of r and g (:108-125),
 // then extractstablepoint (:12-14) and the ageing (:634-646)
@@ -2592,8 +2593,8 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
 #undef PF_ALLOC
     trace_create("buffers");
     if (std::getenv("PF_PROBE")) {                 // development probe: LM phase timestamps
-        if (hipMalloc(&o.dbg, sizeof(unsigned long long) * 512) != hipSuccess) return PF_ENOMEM;
-        if (hipMemset(o.dbg, 0, sizeof(unsigned long long) * 512) != hipSuccess) return PF_EHIP;
+        if (hipMalloc(&o.dbg, sizeof(unsigned long long) * kDbgWords) != hipSuccess) return PF_ENOMEM;
+        if (hipMemset(o.dbg, 0, sizeof(unsigned long long) * kDbgWords) != hipSuccess) return PF_EHIP;
     }
     if (hipHostMalloc(&o.h_cnt, sizeof(int) * (C_COUNT + E_COUNT)) != hipSuccess) return PF_ENOMEM;   // + errw mirror
     if (hipHostMalloc(&o.h_pose, sizeof(double) * 8) != hipSuccess) return PF_ENOMEM;
