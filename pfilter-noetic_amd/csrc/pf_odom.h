@@ -96,7 +96,7 @@ struct LMState {
     int iteration, invalid, reuse, done, phase, n_res, pad0, pad1;
 };
 
-constexpr int kDbgWords = 2048;   // development probe buffer (PF_PROBE): LM [0, 64), rgbds buckets after
+constexpr int kDbgWords = 4096;   // development probe buffer (PF_PROBE): LM [0, 64), rgbds buckets after
 constexpr int kLmParts = 30;   // cost, g[6], H[21], bad_r, bad_J
 constexpr int kLmEvalSlots = 8; // LM claim masks per solve (>= evaluations per solve)
 constexpr int kLmEvals = 5;      // evaluations per solve: 1 + max_num_iterations (4)
@@ -202,6 +202,9 @@ struct OdomGPU {
     u64* rgm_okey = nullptr;       // [nc * map_cap] voxel keys of the map points, map order
     u64* rgm_key64 = nullptr;      // [sort_cap] voxel keys of every element, element order
     u32* rgm_vtag = nullptr;       // [sort_cap] element index | cropped << 31
+    u32* rgm_bcount = nullptr;     // [kRgmBuckets] appended points per bucket (lists built by the LM)
+    u64* rgm_bkey = nullptr;       // [kRgmBuckets * kRgmBucketCap] the lists: keys, tags
+    u32* rgm_btag = nullptr;
     float4* rgm_vox = nullptr;     // [sort_cap] voxel outputs at merged positions
     u32* rgm_kflag = nullptr;      // [sort_cap] kept flags / ranks at merged positions
     u64* rgm_kout = nullptr;       // [sort_cap] fallback: sorted keys (vals: `vals`)

@@ -798,7 +798,7 @@ __device__ __forceinline__ RgView<NC> rg_view(const int* cnt, Clouds map, Clouds
 }
 
 constexpr int kRgmThreads = 256;
-constexpr int kRgmBuckets = 128;
+constexpr int kRgmBuckets = 256;
 constexpr int kRgmBucketCap = 2048;     // appended points a bucket sorts
 constexpr int kRgmOldLds = 2048;        // map points of a bucket cached in LDS
 constexpr u32 kRgmDrop = 0x80000000u;
@@ -899,18 +899,26 @@ __device__ __forceinline__ int rgm_upper(const u64* keys, int n, u64 k) {
 
 // The rgbds merge's appended points, prepared by the last LM launch of an update (k_lm_solve's
 // workgroups, once the pose is solved): pointAssociateToMap (:592-604) of every down-sampled point
-// with the solved parameters x, its voxel key and its crop flag (k_rgm_bucket reads them)
+// with the solved parameters x, its voxel key and crop flag, and its bucket (k_rgm_bucket): every
+// workgroup takes the buckets' splitters (the keys of map points b M / R) into LDS, and each point is
+// appended to its bucket's list (unordered; the bucket sorts it) with one counter atomic. A list
+// past kRgmBucketCap points sets the fallback flag.
 struct RgmPrep {
     int on;
-    Clouds ds;
+    Clouds map, ds;
     CloudsW app;
     u64* key64;
     u32* vtag;
     VgLeaf leaf;
+    u32* bcount;           // [kRgmBuckets] list sizes (zeroed by the bucket kernel's last workgroup)
+    u64* bkey;             // [kRgmBuckets][kRgmBucketCap]
+    u32* btag;
+    int* stat;             // rgm_stat: [0] fallback flag
 };
 template <int NC>
-__device__ __forceinline__ void rgm_prep_apps(const RgmPrep& r, const int* cnt, const double* x) {
-    const RgView<NC> V = rg_view<NC>(cnt, Clouds{{nullptr, nullptr, nullptr}}, Clouds{{nullptr, nullptr, nullptr}});
+__device__ void rgm_prep_apps(const RgmPrep& r, const int* cnt, const double* x) {
+    __shared__ u64 s_sp[kRgmBuckets];
+    const RgView<NC> V = rg_view<NC>(cnt, r.map, Clouds{{nullptr, nullptr, nullptr}});
     int M = 0;
 #pragma unroll
     for (int c = 0; c < NC; ++c) M += V.m[c];
@@ -919,13 +927,31 @@ __device__ __forceinline__ void rgm_prep_apps(const RgmPrep& r, const int* cnt, 
 #pragma unroll
     for (int k = 0; k < 7; ++k) prm[k] = x[k];
     const RgmBox box = rgm_box(prm);
+    for (int i = threadIdx.x; i < kRgmBuckets; i += blockDim.x) {
+        const int l0 = (int)(((long long)i * M) / kRgmBuckets);
+        s_sp[i] = i == 0 ? 0ull : (l0 >= M ? ~0ull : rgm_old_key<NC>(V, r.leaf, box, l0));
+    }
+    __syncthreads();
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < A; q += gridDim.x * blockDim.x) {
         int c, li;
         const int e = rgm_app_elem<NC>(V, q, c, li);
         const float4 p = associate(prm, r.ds.at(c)[li]);
         r.app.at(c)[li] = p;
-        r.key64[e] = rgm_key(p, c, r.leaf.at(c), box);
-        r.vtag[e] = (u32)e | (box.in(p) ? 0u : kRgmDrop);
+        const u64 key = rgm_key(p, c, r.leaf.at(c), box);
+        const u32 tag = (u32)e | (box.in(p) ? 0u : kRgmDrop);
+        r.key64[e] = key;
+        r.vtag[e] = tag;
+        int o = 0;                                    // largest bucket whose splitter is <= key
+#pragma unroll
+        for (int step = kRgmBuckets / 2; step > 0; step >>= 1)
+            if (s_sp[o + step] <= key) o += step;
+        const u32 slot = atomicAdd(&r.bcount[o], 1u);
+        if (slot < (u32)kRgmBucketCap) {
+            r.bkey[(size_t)o * kRgmBucketCap + slot] = key;
+            r.btag[(size_t)o * kRgmBucketCap + slot] = tag;
+        } else {
+            r.stat[0] = 1;
+        }
     }
 }
 
@@ -1869,6 +1895,9 @@ struct RgmArgs {
     u64* ktmp;
     u32* vtmp;
     int* stat;             // [8] (OdomGPU::rgm_stat)
+    u32* bcount;           // the appended points' bucket lists (RgmPrep)
+    const u64* bkey;
+    const u32* btag;
     unsigned long long* dbg;   // development probe (PF_PROBE): [64 + 10 b + i] phase timestamps of bucket b
 };
 static_assert(64 + 10 * (kRgmBuckets + 1) <= kDbgWords, "probe words");
@@ -1926,7 +1955,13 @@ __device__ __forceinline__ u32 block_excl_scan1024(u32 v, u32* lds, u32& total) 
 template <int E>
 __device__ __forceinline__ void rgm_sort_regs(u64* bk, u32* bt, int cb) {
     const int t = threadIdx.x;
-    constexpr int S = E * kRgmThreads;
+    // one element per thread: the network of the next power of two >= cb (at least a wave); threads
+    // past it hold padding and only meet padding
+    int S = E * kRgmThreads;
+    if (E == 1) {
+        S = 64;
+        while (S < cb) S <<= 1;
+    }
     u64 k[E];
     u32 g[E];
 #pragma unroll
@@ -2007,7 +2042,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     __shared__ u64 bk[kRgmBucketCap];
     __shared__ u32 bt[kRgmBucketCap];
     __shared__ u64 ok[kRgmOldLds];
-    __shared__ u64 s_split[kRgmBuckets];
+    __shared__ u64 s_nextk;
     __shared__ int s_cnt, s_before[kRgmThreads / 64], s_cls[kMaxC], s_last;
     __shared__ u32 s_w[kRgmThreads / 64], s_pref[kMaxC];
     const int t = threadIdx.x, b = blockIdx.x;
@@ -2039,43 +2074,29 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         a.vtag[e] = (u32)e | (box.in(p) ? 0u : kRgmDrop);
         if (g + 1 < M) unsorted |= rgm_old_key<NC>(V, a.leaf, box, g + 1) < key;
     }
-    if (t < kRgmBuckets) {                     // every bucket's lower splitter (the key of its first map point)
-        const int l0 = (int)(((long long)t * M) / kRgmBuckets);
-        s_split[t] = t == 0 ? 0ull : (l0 >= M ? ~0ull : rgm_old_key<NC>(V, a.leaf, box, l0));
-    }
-    if (t == 0) s_cnt = 0;
+    if (t == 0)                                // the next bucket's splitter: the key of its first map point
+        s_nextk = b + 1 < kRgmBuckets && hi < M ? rgm_old_key<NC>(V, a.leaf, box, hi) : ~0ull;
     if (t < kMaxC) s_cls[t] = 0;
     if (__any(unsorted) && lane_id() == 0) a.stat[0] = 1;
     __syncthreads();
     RGM_MARK(1);
-    // 2. every appended point: its bucket is the number of splitters 1 .. R - 1 at or below its key (a
-    // binary search; on keys out of order still one bucket per point, so the fallback sees every key);
-    // those of lower buckets are counted, this bucket's kept
+    // 2. this bucket's appended points (listed by the last LM launch) and how many lie below it
     int before = 0;
-    for (int q = t; q < A; q += kRgmThreads) {
-        int c, li;
-        const int e = rgm_app_elem<NC>(V, q, c, li);
-        const u64 key = a.key64[e];                   // transformed and keyed by the last LM launch
-        int o = 0;                                    // largest bucket with s_split[o] <= key
-#pragma unroll
-        for (int step = kRgmBuckets / 2; step > 0; step >>= 1)
-            if (s_split[o + step] <= key) o += step;
-        if (o < b) {
-            ++before;
-        } else if (o == b) {
-            const int slot = atomicAdd(&s_cnt, 1);
-            if (slot < kRgmBucketCap) {
-                bk[slot] = key;
-                bt[slot] = a.vtag[e];
-            }
-        }
-    }
+    for (int i = t; i < b; i += kRgmThreads) before += (int)a.bcount[i];
+    if (t == 0) s_cnt = (int)a.bcount[b];
     before = wave_sum_i(before);
     if (lane_id() == 0) s_before[t >> 6] = before;
     __syncthreads();
     int nbefore = 0;
 #pragma unroll
     for (int w = 0; w < kRgmThreads / 64; ++w) nbefore += s_before[w];
+    {
+        const int c0 = min(s_cnt, kRgmBucketCap);
+        for (int i = t; i < c0; i += kRgmThreads) {
+            bk[i] = a.bkey[(size_t)b * kRgmBucketCap + i];
+            bt[i] = a.btag[(size_t)b * kRgmBucketCap + i];
+        }
+    }
     const bool overflow = s_cnt > kRgmBucketCap;       // too many: the fallback sorts (still take part below)
     const int cb = overflow ? 0 : s_cnt;
     RGM_MARK(2);
@@ -2096,7 +2117,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     // merged position, a voxel's output sits at its first element's.
     const int L = nold + cb;
     const int base = lo + nbefore;
-    const u64 s_next = b + 1 < kRgmBuckets ? s_split[b + 1] : ~0ull;
+    const u64 s_next = s_nextk;
     auto okey_at = [&](int i) -> u64 { return cache ? ok[i] : a.okey[lo + i]; };
     auto add_old = [&](RgmVox& v, int g) {
         int c;
@@ -2230,6 +2251,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     }
     for (int i = t; i < NC * kRgmBuckets; i += kRgmThreads)
         __hip_atomic_store(&a.status[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = t; i < kRgmBuckets; i += kRgmThreads) a.bcount[i] = 0u;      // the lists of the next update
 }
 
 constexpr int kFbThreads = 256;
@@ -2587,6 +2609,9 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.rgm_kout, sizeof(u64) * o.sort_cap);
     PF_ALLOC(o.rgm_ktmp, sizeof(u64) * o.sort_cap);
     PF_ALLOC(o.rgm_vtmp, sizeof(u32) * o.sort_cap);
+    PF_ALLOC(o.rgm_bcount, sizeof(u32) * kRgmBuckets);
+    PF_ALLOC(o.rgm_bkey, sizeof(u64) * kRgmBuckets * kRgmBucketCap);
+    PF_ALLOC(o.rgm_btag, sizeof(u32) * kRgmBuckets * kRgmBucketCap);
     PF_ALLOC(o.rgm_vox, sizeof(float4) * o.sort_cap);
     PF_ALLOC(o.rgm_kflag, sizeof(u32) * o.sort_cap);
     PF_ALLOC(o.rgm_stat, sizeof(int) * 8);
@@ -2619,6 +2644,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.tail_status, 0, sizeof(u64) * (o.tail_tiles + 1), o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.rgm_stat, 0, sizeof(int) * 8, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.rgm_bcount, 0, sizeof(u32) * kRgmBuckets, o.stream) != hipSuccess) return PF_EHIP;
     // the sub-objects' overflow / wait flags latch into the handle's sticky error words
     alias_err(o.fe.err, o.errw + E_FE_SECTOR);
     alias_err(o.grid.err, o.errw + E_GRID);
@@ -2649,6 +2675,7 @@ int odom_reset(OdomGPU& o) {
     if (hipMemsetAsync(o.errw, 0, sizeof(int) * E_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.tail_status, 0, sizeof(u64) * (o.tail_tiles + 1), o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.rgm_stat, 0, sizeof(int) * 8, o.stream) != hipSuccess) return PF_EHIP;
+    if (hipMemsetAsync(o.rgm_bcount, 0, sizeof(u32) * kRgmBuckets, o.stream) != hipSuccess) return PF_EHIP;
     for (int p = 0; p < kSlots; ++p)
         if (hipMemsetAsync(o.sb[p].cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)o.cls.nc * o.map_cap);
@@ -2699,7 +2726,8 @@ void odom_destroy(OdomGPU& o) {
     void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.seg_out,
                     o.keys, o.vals, o.tail_status, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
                     o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg, o.errw,
-                    o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.rgm_ktmp, o.rgm_vox, o.rgm_kflag,
+                    o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.rgm_ktmp, o.rgm_vox, o.rgm_kflag, o.rgm_bcount, o.rgm_bkey,
+                    o.rgm_btag,
                     o.rgm_vtmp, o.rgm_stat};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
@@ -2802,8 +2830,9 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
                    o.errw + E_LM};
         PF_LAUNCH_NC(nc, k_observe, dim3(kGrid), dim3(256), 0, s, oa);
         const bool merge = !o.tie_order && !o.rg_radix;
-        const RgmPrep prep{merge && it == o.opt_count_host - 1, clouds(sb.ds), clouds_w(o.app), o.rgm_key64,
-                           o.rgm_vtag, VgLeaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}}};
+        const RgmPrep prep{merge && it == o.opt_count_host - 1, clouds(map_cur(o)), clouds(sb.ds), clouds_w(o.app),
+                           o.rgm_key64, o.rgm_vtag, VgLeaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}}, o.rgm_bcount,
+                           o.rgm_bkey, o.rgm_btag, o.rgm_stat};
         LmArgs la{o.st, cnt, o.acc, o.cls, o.lm, o.lm_part, o.lm_ticket, o.qflag, clouds(sb.ds), o.geo, o.observe,
                   o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.pbkt, clouds_w(map_cur(o)), (u32)o.map_cap,
                   o.errw + E_LM, prep};
@@ -2816,7 +2845,7 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
                    leaf, o.prm.k_new, o.prm.theta_p, o.prm.theta_max, o.rgm_okey, o.rgm_key64, o.rgm_vtag,
                    o.rgm_vox, o.rgm_kflag, clouds_w(map_next(o)), (u32)o.map_cap, o.errw + E_MAP, o.tail_status,
                    (u32*)(o.tail_status + o.tail_tiles), o.prim.err, o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp,
-                   o.rgm_stat, o.dbg};
+                   o.rgm_stat, o.rgm_bcount, o.rgm_bkey, o.rgm_btag, o.dbg};
         PF_LAUNCH_NC(nc, k_rgm_bucket, dim3(kRgmBuckets + 1), dim3(kRgmThreads), 0, s, ra);
         PF_LAUNCH_NC(nc, k_rgm_fallback, dim3(1), dim3(kFbThreads), 0, s, ra);
         return;

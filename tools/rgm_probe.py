@@ -14,7 +14,7 @@ import pfilter_amd as pa  # noqa: E402
 import pfsynth  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-R = 128                                   # kRgmBuckets
+R = 256                                   # kRgmBuckets
 seq = pfsynth.Sequence("S64", n_frames=N)
 buf, cnt = seq.frames(0, N, threads=16)
 db = pa.DeviceBuffer(buf.nbytes)
@@ -29,8 +29,8 @@ for k in range(N):
     od.frame_device(db.ptr + k * buf.shape[1] * 16, int(cnt[k]))
     if k >= N - 20:
         od.sync()
-        t = np.zeros(2048, np.uint64)
-        assert L.pf_dev_probe(od._h, t.ctypes.data, 2048) == 0
+        t = np.zeros(4096, np.uint64)
+        assert L.pf_dev_probe(od._h, t.ctypes.data, 4096) == 0
         r = t[64:64 + 10 * R].astype(np.int64).reshape(R, 10)
         acc.append(r)
 a = np.array(acc)                         # [frames, bucket, 10]
