@@ -96,7 +96,7 @@ struct LMState {
     int iteration, invalid, reuse, done, phase, n_res, pad0, pad1;
 };
 
-constexpr int kDbgWords = 4096;   // development probe buffer (PF_PROBE): LM [0, 64), rgbds buckets after
+constexpr int kDbgWords = 8192;   // development probe buffer (PF_PROBE): LM [0, 64), rgbds buckets after
 constexpr int kLmParts = 30;   // cost, g[6], H[21], bad_r, bad_J
 constexpr int kLmEvalSlots = 8; // LM claim masks per solve (>= evaluations per solve)
 constexpr int kLmEvals = 5;      // evaluations per solve: 1 + max_num_iterations (4)

@@ -798,7 +798,7 @@ __device__ __forceinline__ RgView<NC> rg_view(const int* cnt, Clouds map, Clouds
 }
 
 constexpr int kRgmThreads = 256;
-constexpr int kRgmBuckets = 256;
+constexpr int kRgmBuckets = 512;
 constexpr int kRgmBucketCap = 2048;     // appended points a bucket sorts
 constexpr int kRgmOldLds = 2048;        // map points of a bucket cached in LDS
 constexpr u32 kRgmDrop = 0x80000000u;
