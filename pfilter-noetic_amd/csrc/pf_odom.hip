@@ -800,7 +800,8 @@ __device__ __forceinline__ RgView<NC> rg_view(const int* cnt, Clouds map, Clouds
 constexpr int kRgmThreads = 256;
 constexpr int kRgmBuckets = 512;
 constexpr int kRgmBucketCap = 2048;     // appended points a bucket sorts
-constexpr int kRgmOldLds = 2048;        // map points of a bucket cached in LDS
+constexpr int kRgmOldLds = 1024;        // map points (keys, points) of a bucket cached in LDS
+constexpr int kRgmAppLds = 512;         // appended points of a bucket cached in LDS (sorted order)
 constexpr u32 kRgmDrop = 0x80000000u;
 
 // the frame's crop box (as k_rg_append_keys)
@@ -1992,6 +1993,7 @@ __device__ __forceinline__ void rgm_sort_regs(u64* bk, u32* bt, int cb) {
             u64 pk[E];
             u32 pg[E];
             if (j < 64) {
+                if (E == 1 && t >= S) continue;             // padding waves (wave-uniform: S >= 64)
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
                     const u32 lo32 = (u32)__shfl_xor((int)(u32)k[e], j, 64);
@@ -2042,6 +2044,8 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     __shared__ u64 bk[kRgmBucketCap];
     __shared__ u32 bt[kRgmBucketCap];
     __shared__ u64 ok[kRgmOldLds];
+    __shared__ float4 opt[kRgmOldLds];                 // the bucket's map points (when cached)
+    __shared__ float4 apt[kRgmAppLds];                 // its appended points in sorted order (when cached)
     __shared__ u64 s_nextk;
     __shared__ int s_cnt, s_before[kRgmThreads / 64], s_cls[kMaxC], s_last;
     __shared__ u32 s_w[kRgmThreads / 64], s_pref[kMaxC];
@@ -2069,7 +2073,10 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         const float4 p = a.map.at(c)[li];
         const u64 key = rgm_key(p, c, a.leaf.at(c), box);
         a.okey[g] = key;
-        if (cache) ok[g - lo] = key;
+        if (cache) {
+            ok[g - lo] = key;
+            opt[g - lo] = p;
+        }
         a.key64[e] = key;
         a.vtag[e] = (u32)e | (box.in(p) ? 0u : kRgmDrop);
         if (g + 1 < M) unsorted |= rgm_old_key<NC>(V, a.leaf, box, g + 1) < key;
@@ -2108,6 +2115,13 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     else if (cb <= 4 * kRgmThreads) rgm_sort_regs<4>(bk, bt, cb);
     else rgm_sort_regs<8>(bk, bt, cb);
     __syncthreads();
+    const bool acache = cb <= kRgmAppLds;              // the voxel walks then read LDS only
+    if (acache)
+        for (int r = t; r < cb; r += kRgmThreads) {
+            int c;
+            apt[r] = V.at((int)(bt[r] & ~kRgmDrop), c);
+        }
+    __syncthreads();
     RGM_MARK(3);
     // 4. voxels. Merged order: a map point after the appended points below it (equal keys: map points
     // first), an appended point after the map points at or below it. A voxel (a run of equal keys) is
@@ -2121,13 +2135,14 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     auto okey_at = [&](int i) -> u64 { return cache ? ok[i] : a.okey[lo + i]; };
     auto add_old = [&](RgmVox& v, int g) {
         int c;
-        const float4 p = rgm_old_point<NC>(V, g, c);
+        const float4 p = cache && g >= lo ? opt[g - lo] : rgm_old_point<NC>(V, g, c);
         if (box.in(p)) v.add(p);
     };
-    auto add_app = [&](RgmVox& v, u32 tag) {
+    auto add_app = [&](RgmVox& v, int r) {            // sorted position r
+        const u32 tag = bt[r];
         if (tag & kRgmDrop) return;
         int c;
-        v.add(V.at((int)tag, c));
+        v.add(acache ? apt[r] : V.at((int)tag, c));
     };
     for (int i = t; i < nold; i += kRgmThreads) {
         const u64 K = okey_at(i);
@@ -2142,7 +2157,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
                 for (int g = g0; g < lo; ++g) add_old(v, g);
             }
             for (int j = i; j < nold && okey_at(j) == K; ++j) add_old(v, lo + j);
-            for (int r = lb; r < cb && bk[r] == K; ++r) add_app(v, bt[r]);
+            for (int r = lb; r < cb && bk[r] == K; ++r) add_app(v, r);
             if (v.n) {
                 float4 out;
                 if (v.finish(a.k_new, a.theta_p, a.theta_max, out)) {
@@ -2161,7 +2176,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         u32 flag = 0;
         if ((r == 0 || bk[r - 1] != K) && (ub == 0 || okey_at(ub - 1) != K)) {   // a voxel without map points
             RgmVox v;
-            for (int q = r; q < cb && bk[q] == K; ++q) add_app(v, bt[q]);
+            for (int q = r; q < cb && bk[q] == K; ++q) add_app(v, q);
             if (v.n) {
                 float4 out;
                 if (v.finish(a.k_new, a.theta_p, a.theta_max, out)) {
