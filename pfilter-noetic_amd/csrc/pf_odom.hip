@@ -2110,8 +2110,20 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     if (a.dbg && t == 0) a.dbg[64 + 10 * b + 9] = (unsigned long long)s_cnt;
     if (overflow && t == 0) a.stat[0] = 1;
     // 3. sort the bucket's appended points by (key, element)
-    if (cb <= kRgmThreads) rgm_sort_regs<1>(bk, bt, cb);
-    else if (cb <= 2 * kRgmThreads) rgm_sort_regs<2>(bk, bt, cb);
+    if (cb <= kRgmThreads) {
+        // rank by counting: every element against every other through LDS broadcast reads (no
+        // dependent stages; the typical bucket holds a few dozen appended points)
+        const u64 k = t < cb ? bk[t] : ~0ull;
+        const u32 g = t < cb ? bt[t] : ~0u;
+        int rank = 0;
+        if (t < cb)
+            for (int j = 0; j < cb; ++j) rank += rgm_less(bk[j], bt[j], k, g) ? 1 : 0;
+        __syncthreads();
+        if (t < cb) {
+            bk[rank] = k;
+            bt[rank] = g;
+        }
+    } else if (cb <= 2 * kRgmThreads) rgm_sort_regs<2>(bk, bt, cb);
     else if (cb <= 4 * kRgmThreads) rgm_sort_regs<4>(bk, bt, cb);
     else rgm_sort_regs<8>(bk, bt, cb);
     __syncthreads();
