@@ -2065,7 +2065,23 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     RGM_MARK(0);
     const int nold = hi - lo;
     const bool cache = nold <= kRgmOldLds;
-    // 1. this bucket's map points: keys, crop flags, still in key order?
+    // 1. this bucket's appended points (listed by the last LM launch), how many lie below it, and its
+    // map points (keys, crop flags, still in key order?): all loads issued before any is waited on
+    constexpr int kPerT = kRgmBucketCap / kRgmThreads;
+    const int cnt_b = (int)a.bcount[b];
+    int before = 0;
+    for (int i = t; i < b; i += kRgmThreads) before += (int)a.bcount[i];
+    const int c0 = min(cnt_b, kRgmBucketCap);
+    u64 lk[kPerT];
+    u32 lt[kPerT];
+#pragma unroll
+    for (int u = 0; u < kPerT; ++u) {
+        const int i = t + u * kRgmThreads;
+        if (i < c0) {
+            lk[u] = a.bkey[(size_t)b * kRgmBucketCap + i];
+            lt[u] = a.btag[(size_t)b * kRgmBucketCap + i];
+        }
+    }
     bool unsorted = false;
     for (int g = lo + t; g < hi; g += kRgmThreads) {
         int c, li;
@@ -2081,29 +2097,27 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         a.vtag[e] = (u32)e | (box.in(p) ? 0u : kRgmDrop);
         if (g + 1 < M) unsorted |= rgm_old_key<NC>(V, a.leaf, box, g + 1) < key;
     }
-    if (t == 0)                                // the next bucket's splitter: the key of its first map point
+    if (t == 0) {                              // the next bucket's splitter: the key of its first map point
         s_nextk = b + 1 < kRgmBuckets && hi < M ? rgm_old_key<NC>(V, a.leaf, box, hi) : ~0ull;
+        s_cnt = cnt_b;
+    }
     if (t < kMaxC) s_cls[t] = 0;
     if (__any(unsorted) && lane_id() == 0) a.stat[0] = 1;
-    __syncthreads();
-    RGM_MARK(1);
-    // 2. this bucket's appended points (listed by the last LM launch) and how many lie below it
-    int before = 0;
-    for (int i = t; i < b; i += kRgmThreads) before += (int)a.bcount[i];
-    if (t == 0) s_cnt = (int)a.bcount[b];
+#pragma unroll
+    for (int u = 0; u < kPerT; ++u) {
+        const int i = t + u * kRgmThreads;
+        if (i < c0) {
+            bk[i] = lk[u];
+            bt[i] = lt[u];
+        }
+    }
     before = wave_sum_i(before);
     if (lane_id() == 0) s_before[t >> 6] = before;
     __syncthreads();
+    RGM_MARK(1);
     int nbefore = 0;
 #pragma unroll
     for (int w = 0; w < kRgmThreads / 64; ++w) nbefore += s_before[w];
-    {
-        const int c0 = min(s_cnt, kRgmBucketCap);
-        for (int i = t; i < c0; i += kRgmThreads) {
-            bk[i] = a.bkey[(size_t)b * kRgmBucketCap + i];
-            bt[i] = a.btag[(size_t)b * kRgmBucketCap + i];
-        }
-    }
     const bool overflow = s_cnt > kRgmBucketCap;       // too many: the fallback sorts (still take part below)
     const int cb = overflow ? 0 : s_cnt;
     RGM_MARK(2);
