@@ -1924,7 +1924,8 @@ struct RgmArgs {
     const u32* btag;
     int* pre;              // OdomGPU::pre: [0] grid dims set, [1] prediction in pred
     double* pred;
-    int* gbounds;          // the map grid (GridGPU): bounds accumulators, dims, cell count, capacity
+    int* bslot;            // [kRgmBuckets][6 kMaxC] each bucket's cell bounds of its kept voxels
+    int* gbounds;          // the map grid (GridGPU): bounds accumulators (untouched), dims, cell count, capacity
     int* gdims;
     int* gncells;
     long long gcell_cap;
@@ -2079,6 +2080,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     __shared__ u64 s_nextk;
     __shared__ int s_cnt, s_before[kRgmThreads / 64], s_cls[kMaxC], s_last;
     __shared__ u32 s_w[kRgmThreads / 64], s_pref[kMaxC];
+    __shared__ int s_bb[kRgmThreads / 64][6 * kMaxC];
     const int t = threadIdx.x, b = blockIdx.x;
     const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
     const int n = V.total();
@@ -2311,16 +2313,25 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
                 bmax[m][k] = m == c ? max(bmax[m][k], cc[k]) : bmax[m][k];
             }
     }
+    // the bucket's bounds: waves, then the block (LDS), into its own slot (the last bucket reduces the
+    // slots: no contended atomics)
 #pragma unroll
-    for (int m = 0; m < NC; ++m)
+    for (int m = 0; m < kMaxC; ++m)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int lo_ = wave_min_i(bmin[m][k]), hi_ = wave_max_i(bmax[m][k]);
             if (lane_id() == 0) {
-                if (lo_ != INT_MAX) __hip_atomic_fetch_min(&a.gbounds[6 * m + k], lo_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (hi_ != INT_MIN) __hip_atomic_fetch_max(&a.gbounds[6 * m + 3 + k], hi_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_bb[t >> 6][6 * m + k] = lo_;
+                s_bb[t >> 6][6 * m + 3 + k] = hi_;
             }
         }
+    __syncthreads();
+    if (t < 6 * kMaxC) {
+        int r = s_bb[0][t];
+#pragma unroll
+        for (int w = 1; w < kRgmThreads / 64; ++w) r = (t % 6) < 3 ? min(r, s_bb[w][t]) : max(r, s_bb[w][t]);
+        a.bslot[(size_t)b * 6 * kMaxC + t] = r;
+    }
     if (over && !a.stat[0]) atomicOr(a.err_map, 1);     // (out-of-order input: the fallback redoes it)
     RGM_MARK(7);
     // 6. the kept voxels of every class summed over the buckets; the last bucket to arrive writes the
@@ -2333,6 +2344,23 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         s_last = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (u32)kRgmBuckets - 1;
     __syncthreads();
     if (!s_last) return;
+    {                                                  // the new maps' cell bounds over all buckets
+        int r[6 * kMaxC];
+#pragma unroll
+        for (int k = 0; k < 6 * kMaxC; ++k) r[k] = (k % 6) < 3 ? INT_MAX : INT_MIN;
+        for (int bb = t; bb < kRgmBuckets; bb += kRgmThreads)
+#pragma unroll
+            for (int k = 0; k < 6 * kMaxC; ++k) {
+                const int v = a.bslot[(size_t)bb * 6 * kMaxC + k];
+                r[k] = (k % 6) < 3 ? min(r[k], v) : max(r[k], v);
+            }
+#pragma unroll
+        for (int k = 0; k < 6 * kMaxC; ++k) {
+            const int v = (k % 6) < 3 ? wave_min_i(r[k]) : wave_max_i(r[k]);
+            if (lane_id() == 0) s_bb[t >> 6][k] = v;
+        }
+        __syncthreads();
+    }
     if (t == 0) {
         int kc[kMaxC], tot = 0;
 #pragma unroll
@@ -2353,14 +2381,16 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
             if (A > a.stat[2]) a.stat[2] = A;
             // the next frame's map grid (k_grid_bounds' dims from these bounds: its workgroups skip)
             int lb[6 * kGridMaps], nloc[kGridMaps];
-            for (int k = 0; k < 6 * kGridMaps; ++k)
-                lb[k] = __hip_atomic_load(&a.gbounds[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int k = 0; k < 6 * kGridMaps; ++k) {
+                int v = s_bb[0][k];
+                for (int w = 1; w < kRgmThreads / 64; ++w) v = (k % 6) < 3 ? min(v, s_bb[w][k]) : max(v, s_bb[w][k]);
+                lb[k] = v;
+            }
             for (int m = 0; m < kGridMaps; ++m) nloc[m] = m < NC ? min(kc[m], (int)a.map_cap) : 0;
             grid_dims(lb, nloc, a.gdims, a.gncells, a.gcell_cap, a.gerr);
             a.pre[0] = 1;
         }
-        for (int k = 0; k < 6 * kGridMaps; ++k)        // bounds accumulators back to empty
-            __hip_atomic_store(&a.gbounds[k], (k % 6) < 3 ? INT_MAX : INT_MIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
         __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     for (int i = t; i < NC * kRgmBuckets; i += kRgmThreads)
@@ -2730,6 +2760,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.rgm_kflag, sizeof(u32) * o.sort_cap);
     PF_ALLOC(o.rgm_stat, sizeof(int) * 8);
     PF_ALLOC(o.pre, sizeof(int) * 4);
+    PF_ALLOC(o.rgm_bslot, sizeof(int) * kRgmBuckets * 6 * kMaxC);
     PF_ALLOC(o.pred, sizeof(double) * 16);
 #undef PF_ALLOC
     trace_create("buffers");
@@ -2845,7 +2876,7 @@ void odom_destroy(OdomGPU& o) {
                     o.keys, o.vals, o.tail_status, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
                     o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg, o.errw,
                     o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.rgm_ktmp, o.rgm_vox, o.rgm_kflag, o.rgm_bcount, o.rgm_bkey,
-                    o.rgm_btag, o.pre, o.pred,
+                    o.rgm_btag, o.pre, o.pred, o.rgm_bslot,
                     o.rgm_vtmp, o.rgm_stat};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
@@ -2965,7 +2996,7 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
                    leaf, o.prm.k_new, o.prm.theta_p, o.prm.theta_max, o.rgm_okey, o.rgm_key64, o.rgm_vtag,
                    o.rgm_vox, o.rgm_kflag, clouds_w(map_next(o)), (u32)o.map_cap, o.errw + E_MAP, o.tail_status,
                    (u32*)(o.tail_status + o.tail_tiles), o.prim.err, o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp,
-                   o.rgm_stat, o.rgm_bcount, o.rgm_bkey, o.rgm_btag, o.pre, o.pred, o.grid.bounds, o.grid.dims,
+                   o.rgm_stat, o.rgm_bcount, o.rgm_bkey, o.rgm_btag, o.pre, o.pred, o.rgm_bslot, o.grid.bounds, o.grid.dims,
                    o.grid.d_ncells, (long long)o.grid.cell_cap, o.grid.err, o.dbg};
         PF_LAUNCH_NC(nc, k_rgm_bucket, dim3(kRgmBuckets + 1), dim3(kRgmThreads), 0, s, ra);
         PF_LAUNCH_NC(nc, k_rgm_fallback, dim3(1), dim3(kFbThreads), 0, s, ra);
