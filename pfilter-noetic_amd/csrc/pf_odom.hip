@@ -2141,7 +2141,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         s_cnt = cnt_b;
     }
     if (t < kMaxC) s_cls[t] = 0;
-    if (__any(unsorted) && lane_id() == 0) a.stat[0] = 1;
+    if (__any(unsorted) && lane_id() == 0) __hip_atomic_store(&a.stat[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int u = 0; u < kPerT; ++u) {
         const int i = t + u * kRgmThreads;
@@ -2161,7 +2161,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     const int cb = overflow ? 0 : s_cnt;
     RGM_MARK(2);
     if (a.dbg && t == 0) a.dbg[64 + 10 * b + 9] = (unsigned long long)s_cnt;
-    if (overflow && t == 0) a.stat[0] = 1;
+    if (overflow && t == 0) __hip_atomic_store(&a.stat[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // 3. sort the bucket's appended points by (key, element)
     if (cb <= kRgmThreads) {
         // rank by counting: every element against every other through LDS broadcast reads (no
@@ -2330,7 +2330,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         int r = s_bb[0][t];
 #pragma unroll
         for (int w = 1; w < kRgmThreads / 64; ++w) r = (t % 6) < 3 ? min(r, s_bb[w][t]) : max(r, s_bb[w][t]);
-        a.bslot[(size_t)b * 6 * kMaxC + t] = r;
+        __hip_atomic_store(&a.bslot[(size_t)b * 6 * kMaxC + t], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (over && !a.stat[0]) atomicOr(a.err_map, 1);     // (out-of-order input: the fallback redoes it)
     RGM_MARK(7);
@@ -2351,7 +2351,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         for (int bb = t; bb < kRgmBuckets; bb += kRgmThreads)
 #pragma unroll
             for (int k = 0; k < 6 * kMaxC; ++k) {
-                const int v = a.bslot[(size_t)bb * 6 * kMaxC + k];
+                const int v = __hip_atomic_load(&a.bslot[(size_t)bb * 6 * kMaxC + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 r[k] = (k % 6) < 3 ? min(r[k], v) : max(r[k], v);
             }
 #pragma unroll
@@ -2583,6 +2583,7 @@ __global__ void __launch_bounds__(kFbThreads) k_rgm_fallback(RgmArgs a) {
     __syncthreads();
     rgm_fallback_tail<NC>(a, V, n);
     if (threadIdx.x == 0) {
+        a.pre[0] = 0;                                  // the buckets' grid dims (if any) are void
         a.stat[1]++;
         if (n - (V.m[0] + (NC > 1 ? V.m[1] : 0) + (NC > 2 ? V.m[2] : 0)) > a.stat[2])
             a.stat[2] = n - (V.m[0] + (NC > 1 ? V.m[1] : 0) + (NC > 2 ? V.m[2] : 0));
