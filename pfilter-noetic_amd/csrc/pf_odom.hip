@@ -2332,7 +2332,8 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         for (int w = 1; w < kRgmThreads / 64; ++w) r = (t % 6) < 3 ? min(r, s_bb[w][t]) : max(r, s_bb[w][t]);
         __hip_atomic_store(&a.bslot[(size_t)b * 6 * kMaxC + t], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (over && !a.stat[0]) atomicOr(a.err_map, 1);     // (out-of-order input: the fallback redoes it)
+    if (over && !__hip_atomic_load(&a.stat[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicOr(a.err_map, 1);                        // (out-of-order input: the fallback redoes it)
     RGM_MARK(7);
     // 6. the kept voxels of every class summed over the buckets; the last bucket to arrive writes the
     // map sizes (cnt[C_M + c]), the class boundaries (cnt[C_NLT + c - 1] = kept voxels of classes < c)
