@@ -11,6 +11,13 @@ __device__ __forceinline__ int cell_of(const int* dm, float4 p) {
     const int x = (int)floorf(p.x) - dm[0], y = (int)floorf(p.y) - dm[1], z = (int)floorf(p.z) - dm[2];
     return dm[6] + (z * dm[4] + y) * dm[3] + x;
 }
+// the same, -1 for a point outside the grid's bounds (never, when the dims come from these points'
+// own bounds: a guard that turns inconsistent dims into a reported error instead of stray writes)
+__device__ __forceinline__ int cell_of_checked(const int* dm, float4 p) {
+    const int x = (int)floorf(p.x) - dm[0], y = (int)floorf(p.y) - dm[1], z = (int)floorf(p.z) - dm[2];
+    if ((unsigned)x >= (unsigned)dm[3] || (unsigned)y >= (unsigned)dm[4] || (unsigned)z >= (unsigned)dm[5]) return -1;
+    return dm[6] + (z * dm[4] + y) * dm[3] + x;
+}
 
 // Agg: clouds whose consecutive points mostly share a cell (the front end's non-ground cloud, in
 // 3 m ground-cell order) take one atomic per run of equal cells in a wave (up to 4 runs; the rest
@@ -18,7 +25,7 @@ __device__ __forceinline__ int cell_of(const int* dm, float4 p) {
 // way (the queries order candidates by (d^2, index)).
 template <bool Agg>
 __global__ void __launch_bounds__(256) k_grid_count(GridPtrs gp, const int* __restrict__ dims, u32* __restrict__ cnt,
-                                                     u32* __restrict__ slot) {
+                                                     u32* __restrict__ slot, int* __restrict__ err) {
     const GridIdx gi = grid_idx(gp);
     const int stride = gridDim.x * blockDim.x;
     const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -27,7 +34,10 @@ __global__ void __launch_bounds__(256) k_grid_count(GridPtrs gp, const int* __re
         if (i < gi.total) {
             const int mi = gi.map_of(i);
             const int* dm = dims + 8 * mi;
-            if (dm[7]) cid = cell_of(dm, gp.m[mi][i - gi.start(mi)]);
+            if (dm[7]) {
+                cid = cell_of_checked(dm, gp.m[mi][i - gi.start(mi)]);
+                if (cid < 0) atomicOr(err, 1);
+            }
         }
         if (!Agg) {
             if (cid >= 0) slot[i] = atomicAdd(&cnt[cid], 1u);
@@ -58,7 +68,8 @@ __global__ void __launch_bounds__(256) k_grid_scatter(GridPtrs gp, const int* __
         if (!dm[7]) continue;
         const int li = i - gi.start(mi);
         const float4 p = gp.m[mi][li];
-        const int cid = cell_of(dm, p);
+        const int cid = cell_of_checked(dm, p);
+        if (cid < 0) continue;                // (counted as an error by k_grid_count)
         cpts[start[cid] + slot[i]] = make_float4(p.x, p.y, p.z, __int_as_float(li));
         cnt[cid] = 0u;                        // leaves the count array zero for the next build
     }
@@ -220,7 +231,7 @@ void grid_free(GridGPU& g) {
 
 void grid_count_scan(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s) {
     hipLaunchKernelGGL(k_grid_bounds<NoTail>, dim3(kGridBoundsBlocks), dim3(256), 0, s, grid_bounds_args(g, gp), NoTail{});
-    hipLaunchKernelGGL(k_grid_count<true>, dim3(512), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot);
+    hipLaunchKernelGGL(k_grid_count<true>, dim3(512), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot, g.err);
     scan_exclusive(g.cell_count, g.cell_start, g.d_ncells, nullptr, w, s);
 }
 
@@ -230,9 +241,9 @@ void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s, bool
         hipLaunchKernelGGL(k_grid_bounds<NoTail>, dim3(kGridBoundsBlocks), dim3(256), 0, s, grid_bounds_args(g, gp),
                            NoTail{});
     if (aggregate)
-        hipLaunchKernelGGL(k_grid_count<true>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot);
+        hipLaunchKernelGGL(k_grid_count<true>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot, g.err);
     else
-        hipLaunchKernelGGL(k_grid_count<false>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot);
+        hipLaunchKernelGGL(k_grid_count<false>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot, g.err);
     scan_exclusive(g.cell_count, g.cell_start, g.d_ncells, nullptr, w, s, true);
     hipLaunchKernelGGL(k_grid_scatter, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_start, g.slot, g.cpts,
                        g.cell_count);
