@@ -2319,7 +2319,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     for (int m = 0; m < kMaxC; ++m)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const int lo_ = wave_min_i(bmin[m][k]), hi_ = wave_max_i(bmax[m][k]);
+            const int lo_ = m < NC ? wave_min_i(bmin[m][k]) : INT_MAX, hi_ = m < NC ? wave_max_i(bmax[m][k]) : INT_MIN;
             if (lane_id() == 0) {
                 s_bb[t >> 6][6 * m + k] = lo_;
                 s_bb[t >> 6][6 * m + 3 + k] = hi_;
@@ -2357,7 +2357,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
             }
 #pragma unroll
         for (int k = 0; k < 6 * kMaxC; ++k) {
-            const int v = (k % 6) < 3 ? wave_min_i(r[k]) : wave_max_i(r[k]);
+            const int v = k >= 6 * NC ? r[k] : ((k % 6) < 3 ? wave_min_i(r[k]) : wave_max_i(r[k]));
             if (lane_id() == 0) s_bb[t >> 6][k] = v;
         }
         __syncthreads();
