@@ -4,9 +4,9 @@
 #   tools/bench_ab.sh [variant ...]   ("" = the in-tree library)
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
 for v in "" "$@"; do
   if [ -n "$v" ]; then export PFILTER_HIP_LIB=pfilter-noetic_amd/var/$v/libpfilter_hip.so; else unset PFILTER_HIP_LIB; fi
-  echo "== ${v:-main} $(timeout -k 10 200 python bench.py --no-cpu --no-roofline --bpf-frames 0 --leg-frames 0 | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d.get("stage_us"))')" || exit 1
+  echo "== ${v:-main} $(timeout -k 10 200 python bench.py --only-headline | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["value"], d["ms_per_step"], d.get("stage_us"))')" || exit 1
 done
 done
