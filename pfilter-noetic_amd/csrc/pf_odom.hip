@@ -2081,14 +2081,14 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     __shared__ int s_cnt, s_before[kRgmThreads / 64], s_cls[kMaxC], s_last;
     __shared__ u32 s_w[kRgmThreads / 64], s_pref[kMaxC];
     __shared__ int s_bb[kRgmThreads / 64][6 * kMaxC];
-    const int t = threadIdx.x, b = blockIdx.x;
+    const int t = threadIdx.x, b = (int)blockIdx.x - 1;   // block 0: the pose step (dispatched first)
     const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
     const int n = V.total();
     int M = 0;
 #pragma unroll
     for (int c = 0; c < NC; ++c) M += V.m[c];
     const int A = n - M;
-    if (b == kRgmBuckets) {                            // (reads no counter: the last bucket rewrites them)
+    if (b < 0) {                                       // (reads no counter: the last bucket rewrites them)
         finalize_pose(a.st, a.poses, a.pose_cap, 1, a.acc, a.st->params);
         if (t == 0) {                                  // and the next frame's prediction (PredictTail)
             iso pr;
@@ -2306,12 +2306,13 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         else over = true;
         const int cc[3] = {(int)floorf(v.x), (int)floorf(v.y), (int)floorf(v.z)};
 #pragma unroll
-        for (int m = 0; m < kMaxC; ++m)
+        for (int m = 0; m < NC; ++m)                   // (a bucket's voxels are nearly always one class)
+            if (m == c)
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                bmin[m][k] = m == c ? min(bmin[m][k], cc[k]) : bmin[m][k];
-                bmax[m][k] = m == c ? max(bmax[m][k], cc[k]) : bmax[m][k];
-            }
+                for (int k = 0; k < 3; ++k) {
+                    bmin[m][k] = min(bmin[m][k], cc[k]);
+                    bmax[m][k] = max(bmax[m][k], cc[k]);
+                }
     }
     // the bucket's bounds: waves, then the block (LDS), into its own slot (the last bucket reduces the
     // slots: no contended atomics)
