@@ -461,7 +461,6 @@ static int init_map_n(pf_odom* h, const float* const* cl, const size_t* n, const
     if (!rc) rc = stage_inputs(h, p, cl, n, stride);
     if (!rc) rc = stage_a_end_b_begin(h, p);
     if (rc) return rc;
-    PF_HIP_TRY(hipMemsetAsync(o.pre, 0, sizeof(int) * 4, o.stream));
     odom_enqueue_init(o, p, o.stream);
     odom_enqueue_export(o, o.stream, false);
     rc = stage_b_end(h, p);
@@ -569,7 +568,6 @@ int pf_odom_set_map(pf_odom* h, int which, const float* xyz, const uint8_t* rg, 
         std::memcpy(&wf, &w, 4);
         tmp[i] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], wf);
     }
-    PF_HIP_TRY(hipMemsetAsync(o.pre, 0, sizeof(int) * 4, o.stream));      // the precomputed grid is stale
     if (n) PF_HIP_TRY(hipMemcpyAsync(map_cur(o)[which], tmp.data(), sizeof(float4) * n, hipMemcpyHostToDevice, o.stream));
     hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_M + which, (int)n);
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
@@ -741,7 +739,6 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
         PF_HT(5, PF_HIP_TRY(hipGraphLaunch(gb, o.stream)));
         odom_update_done(o);
     } else if (!o.inited) {
-        PF_HIP_TRY(hipMemsetAsync(o.pre, 0, sizeof(int) * 4, o.stream));
         odom_enqueue_init(o, p, o.stream);
         odom_enqueue_export(o, o.stream, false);
     } else {
@@ -989,7 +986,6 @@ int pf_odom_set_state(pf_odom* h, const double odom_pose[7], const double last_p
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     DevState st;
     PF_HIP_TRY(hipMemcpy(&st, o.st, sizeof(st), hipMemcpyDeviceToHost));
-    PF_HIP_TRY(hipMemset(o.pre, 0, sizeof(int) * 4));                        // the precomputed prediction is stale
     const double* lp = last_pose ? last_pose : odom_pose;
     const pf::m3 R = pf::q2m(pf::qd{odom_pose[0], odom_pose[1], odom_pose[2], odom_pose[3]});
     const pf::m3 L = pf::q2m(pf::qd{lp[0], lp[1], lp[2], lp[3]});

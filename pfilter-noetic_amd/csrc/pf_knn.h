@@ -108,8 +108,6 @@ struct GridBoundsArgs {
     int* d_ncells;
     long long cell_cap;
     int* err;
-    const int* ready;      // optional: nonzero when the dims are already set for these maps (the bounds
-                           // workgroups then leave at once; the flag's owner clears it after the build)
 };
 struct NoTail {
     static constexpr bool kActive = false;
@@ -121,7 +119,6 @@ __global__ void __launch_bounds__(256) k_grid_bounds(GridBoundsArgs ga, Tail tai
         tail((int)threadIdx.x);
         return;
     }
-    if (ga.ready && *ga.ready) return;
     const unsigned nblk = gridDim.x - (Tail::kActive ? 1u : 0u);   // workgroups sharing the bounds
     const GridPtrs& gp = ga.gp;
     int* bounds = ga.bounds;
@@ -189,7 +186,7 @@ __global__ void __launch_bounds__(256) k_grid_bounds(GridBoundsArgs ga, Tail tai
 }
 
 inline GridBoundsArgs grid_bounds_args(GridGPU& g, const GridPtrs& gp) {
-    return GridBoundsArgs{gp, g.bounds, g.arrive, g.dims, g.d_ncells, (long long)g.cell_cap, g.err, nullptr};
+    return GridBoundsArgs{gp, g.bounds, g.arrive, g.dims, g.d_ncells, (long long)g.cell_cap, g.err};
 }
 constexpr int kGridBoundsBlocks = 64;
 

@@ -210,12 +210,6 @@ struct OdomGPU {
     u64* rgm_kout = nullptr;       // [sort_cap] fallback: sorted keys (vals: `vals`)
     u64* rgm_ktmp = nullptr;       // [sort_cap] fallback sort scratch
     u32* rgm_vtmp = nullptr;
-    // computed ahead by the rgbds merge for the next frame: [0] the map grid's dims are set, [1] the
-    // pose prediction is in `pred` (cleared by k_assoc, and by every host call that changes the maps
-    // or the state)
-    int* pre = nullptr;
-    int* rgm_bslot = nullptr;      // [kRgmBuckets][6 kMaxC] per-bucket cell bounds of the new maps
-    double* pred = nullptr;        // [16]: predicted R (9), t (3), params quaternion (4)
     int* rgm_stat = nullptr;       // [8]: fallback this frame, fallbacks so far, largest append, spare,
                                    // kept voxels per class (accumulated over the buckets)
 

@@ -170,19 +170,6 @@ __global__ void k_pull_counts(int* __restrict__ cnt, const int* __restrict__ scn
 
 // constant-velocity prediction, optimization_count schedule, map-size gate (:232-247); thread 0's
 // chain, thread < 18 reset the map-update bounds. Runs on an extra workgroup of the grid-bounds kernel.
-// the constant-velocity prediction of the next frame's pose (:235-239): odom * (last^-1 * odom), its
-// rotation's orthogonal polar factor as a quaternion (Eigen 3.3 rotation())
-__device__ __forceinline__ void predict_pose(const DevState* st, iso& pred, qd& q) {
-    const iso odom = load_iso(st->odomR, st->odomt);
-    const iso last = load_iso(st->lastR, st->lastt);
-    pred = iso_mul(odom, iso_mul(iso_inv(last), odom));
-    q = m2q(polar_rotation(pred.R));
-}
-__device__ __forceinline__ void store_pred(double* pr, const iso& pred, const qd& q) {
-    store_iso(pred, pr, pr + 9);
-    pr[12] = q.x; pr[13] = q.y; pr[14] = q.z; pr[15] = q.w;
-}
-
 struct PredictTail {
     static constexpr bool kActive = true;
     DevState* st;
@@ -190,25 +177,17 @@ struct PredictTail {
     const int* scnt;
     u32* acc;
     ClassCfg cls;
-    const int* pre;        // pre[1]: the prediction was computed at the end of the previous update
-    const double* pred;
     __device__ void operator()(int t) const {
         if (t < 6 * kMaxC) acc[A_RG + t] = ((t % 6) < 3) ? 0xFFFFFFFFu : 0u;   // map-update bounds
         if (t != 0) return;
         pull_stage_counts(cnt, scnt);
         if (st->optimization_count > 2) st->optimization_count--;                 // :232-233
         const iso odom = load_iso(st->odomR, st->odomt);
-        iso pr;
-        qd q;
-        if (pre && pre[1]) {
-            pr = load_iso(pred, pred + 9);
-            q = qd{pred[12], pred[13], pred[14], pred[15]};
-        } else {
-            predict_pose(st, pr, q);                                               // :235-239
-        }
+        const iso last = load_iso(st->lastR, st->lastt);
+        const iso pred = iso_mul(odom, iso_mul(iso_inv(last), odom));             // :235
         store_iso(odom, st->lastR, st->lastt);
-        store_iso(pr, st->odomR, st->odomt);
-        const iso& pred = pr;
+        store_iso(pred, st->odomR, st->odomt);
+        const qd q = m2q(polar_rotation(pred.R));                                  // :239 (Eigen 3.3 rotation())
         st->params[0] = q.x; st->params[1] = q.y; st->params[2] = q.z; st->params[3] = q.w;
         st->params[4] = pred.t.x; st->params[5] = pred.t.y; st->params[6] = pred.t.z;
         int gate = 1;                              // :247 / BPF :721: line maps > 10, plane maps > 50
@@ -377,7 +356,6 @@ struct AssocArgs {
     u32 map_cap;
     u32* lm_arrive;
     double* lm_part;       // [kLmEvals][kLmBlocks][32] LM partials, reset to kPartSentinel here
-    int* pre;              // OdomGPU::pre, consumed by this frame's grid build: cleared here
 };
 
 // line fit (:302-331) / plane fit (:449-476), round and sparsity, p-index pair keys of query q
@@ -513,7 +491,6 @@ __global__ void __launch_bounds__(256) k_assoc(AssocArgs a) {
     const int gate = a.st->gate;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int k = 0; k < kLmEvalSlots; ++k) a.lm_arrive[k] = 0u;       // LM claim masks
-        a.pre[0] = a.pre[1] = 0;
         a.cnt[C_NPAIR] = gate ? 5 * nq : 0;
         for (int c = 0; c < kMaxC; ++c) a.cnt[C_KEPT + c] = a.cnt[C_VALID + c] = 0;
     }
@@ -1922,14 +1899,6 @@ struct RgmArgs {
     u32* bcount;           // the appended points' bucket lists (RgmPrep)
     const u64* bkey;
     const u32* btag;
-    int* pre;              // OdomGPU::pre: [0] grid dims set, [1] prediction in pred
-    double* pred;
-    int* bslot;            // [kRgmBuckets][6 kMaxC] each bucket's cell bounds of its kept voxels
-    int* gbounds;          // the map grid (GridGPU): bounds accumulators (untouched), dims, cell count, capacity
-    int* gdims;
-    int* gncells;
-    long long gcell_cap;
-    int* gerr;
     unsigned long long* dbg;   // development probe (PF_PROBE): [64 + 10 b + i] phase timestamps of bucket b
 };
 static_assert(64 + 10 * (kRgmBuckets + 1) <= kDbgWords, "probe words");
@@ -2080,23 +2049,15 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     __shared__ u64 s_nextk;
     __shared__ int s_cnt, s_before[kRgmThreads / 64], s_cls[kMaxC], s_last;
     __shared__ u32 s_w[kRgmThreads / 64], s_pref[kMaxC];
-    __shared__ int s_bb[kRgmThreads / 64][6 * kMaxC];
-    const int t = threadIdx.x, b = (int)blockIdx.x - 1;   // block 0: the pose step (dispatched first)
+    const int t = threadIdx.x, b = blockIdx.x;
     const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
     const int n = V.total();
     int M = 0;
 #pragma unroll
     for (int c = 0; c < NC; ++c) M += V.m[c];
     const int A = n - M;
-    if (b < 0) {                                       // (reads no counter: the last bucket rewrites them)
+    if (b == kRgmBuckets) {                            // (reads no counter: the last bucket rewrites them)
         finalize_pose(a.st, a.poses, a.pose_cap, 1, a.acc, a.st->params);
-        if (t == 0) {                                  // and the next frame's prediction (PredictTail)
-            iso pr;
-            qd q;
-            predict_pose(a.st, pr, q);
-            store_pred(a.pred, pr, q);
-            a.pre[1] = 1;
-        }
         return;
     }
     const RgmBox box = rgm_box(a.st->params);
@@ -2288,50 +2249,13 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         }
     }
     bool over = false;
-    int bmin[kMaxC][3], bmax[kMaxC][3];                // the new maps' 1 m cell bounds (k_grid_bounds)
-#pragma unroll
-    for (int c = 0; c < kMaxC; ++c)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            bmin[c][k] = INT_MAX;
-            bmax[c][k] = INT_MIN;
-        }
     for (int p = t; p < L; p += kRgmThreads) {
         const u32 f = a.kflag[base + p];
         if (!(f & 0x3FFFFFFFu)) continue;
         const int c = min((int)(f >> 30), NC - 1);
         const u32 idx = s_pref[c] + (f & 0x3FFFFFFFu) - 1u - sel3(c, first_rank[0], first_rank[1], first_rank[2]);
-        const float4 v = a.vox[base + p];
-        if (idx < a.map_cap) a.mapw.at(c)[idx] = v;
+        if (idx < a.map_cap) a.mapw.at(c)[idx] = a.vox[base + p];
         else over = true;
-        const int cc[3] = {(int)floorf(v.x), (int)floorf(v.y), (int)floorf(v.z)};
-#pragma unroll
-        for (int m = 0; m < NC; ++m)                   // (a bucket's voxels are nearly always one class)
-            if (m == c)
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    bmin[m][k] = min(bmin[m][k], cc[k]);
-                    bmax[m][k] = max(bmax[m][k], cc[k]);
-                }
-    }
-    // the bucket's bounds: waves, then the block (LDS), into its own slot (the last bucket reduces the
-    // slots: no contended atomics)
-#pragma unroll
-    for (int m = 0; m < kMaxC; ++m)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int lo_ = m < NC ? wave_min_i(bmin[m][k]) : INT_MAX, hi_ = m < NC ? wave_max_i(bmax[m][k]) : INT_MIN;
-            if (lane_id() == 0) {
-                s_bb[t >> 6][6 * m + k] = lo_;
-                s_bb[t >> 6][6 * m + 3 + k] = hi_;
-            }
-        }
-    __syncthreads();
-    if (t < 6 * kMaxC) {
-        int r = s_bb[0][t];
-#pragma unroll
-        for (int w = 1; w < kRgmThreads / 64; ++w) r = (t % 6) < 3 ? min(r, s_bb[w][t]) : max(r, s_bb[w][t]);
-        __hip_atomic_store(&a.bslot[(size_t)b * 6 * kMaxC + t], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (over && !__hip_atomic_load(&a.stat[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         atomicOr(a.err_map, 1);                        // (out-of-order input: the fallback redoes it)
@@ -2346,23 +2270,6 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         s_last = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (u32)kRgmBuckets - 1;
     __syncthreads();
     if (!s_last) return;
-    {                                                  // the new maps' cell bounds over all buckets
-        int r[6 * kMaxC];
-#pragma unroll
-        for (int k = 0; k < 6 * kMaxC; ++k) r[k] = (k % 6) < 3 ? INT_MAX : INT_MIN;
-        for (int bb = t; bb < kRgmBuckets; bb += kRgmThreads)
-#pragma unroll
-            for (int k = 0; k < 6 * kMaxC; ++k) {
-                const int v = __hip_atomic_load(&a.bslot[(size_t)bb * 6 * kMaxC + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                r[k] = (k % 6) < 3 ? min(r[k], v) : max(r[k], v);
-            }
-#pragma unroll
-        for (int k = 0; k < 6 * kMaxC; ++k) {
-            const int v = k >= 6 * NC ? r[k] : ((k % 6) < 3 ? wave_min_i(r[k]) : wave_max_i(r[k]));
-            if (lane_id() == 0) s_bb[t >> 6][k] = v;
-        }
-        __syncthreads();
-    }
     if (t == 0) {
         int kc[kMaxC], tot = 0;
 #pragma unroll
@@ -2381,18 +2288,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
             a.cnt[C_KEEP_TOTAL] = tot;
             a.cnt[C_NRG] = n;
             if (A > a.stat[2]) a.stat[2] = A;
-            // the next frame's map grid (k_grid_bounds' dims from these bounds: its workgroups skip)
-            int lb[6 * kGridMaps], nloc[kGridMaps];
-            for (int k = 0; k < 6 * kGridMaps; ++k) {
-                int v = s_bb[0][k];
-                for (int w = 1; w < kRgmThreads / 64; ++w) v = (k % 6) < 3 ? min(v, s_bb[w][k]) : max(v, s_bb[w][k]);
-                lb[k] = v;
-            }
-            for (int m = 0; m < kGridMaps; ++m) nloc[m] = m < NC ? min(kc[m], (int)a.map_cap) : 0;
-            grid_dims(lb, nloc, a.gdims, a.gncells, a.gcell_cap, a.gerr);
-            a.pre[0] = 1;
         }
-
         __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     for (int i = t; i < NC * kRgmBuckets; i += kRgmThreads)
@@ -2585,7 +2481,6 @@ __global__ void __launch_bounds__(kFbThreads) k_rgm_fallback(RgmArgs a) {
     __syncthreads();
     rgm_fallback_tail<NC>(a, V, n);
     if (threadIdx.x == 0) {
-        a.pre[0] = 0;                                  // the buckets' grid dims (if any) are void
         a.stat[1]++;
         if (n - (V.m[0] + (NC > 1 ? V.m[1] : 0) + (NC > 2 ? V.m[2] : 0)) > a.stat[2])
             a.stat[2] = n - (V.m[0] + (NC > 1 ? V.m[1] : 0) + (NC > 2 ? V.m[2] : 0));
@@ -2762,9 +2657,6 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.rgm_vox, sizeof(float4) * o.sort_cap);
     PF_ALLOC(o.rgm_kflag, sizeof(u32) * o.sort_cap);
     PF_ALLOC(o.rgm_stat, sizeof(int) * 8);
-    PF_ALLOC(o.pre, sizeof(int) * 4);
-    PF_ALLOC(o.rgm_bslot, sizeof(int) * kRgmBuckets * 6 * kMaxC);
-    PF_ALLOC(o.pred, sizeof(double) * 16);
 #undef PF_ALLOC
     trace_create("buffers");
     if (std::getenv("PF_PROBE")) {                 // development probe: LM phase timestamps
@@ -2795,7 +2687,6 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (hipMemsetAsync(o.tail_status, 0, sizeof(u64) * (o.tail_tiles + 1), o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.rgm_stat, 0, sizeof(int) * 8, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.rgm_bcount, 0, sizeof(u32) * kRgmBuckets, o.stream) != hipSuccess) return PF_EHIP;
-    if (hipMemsetAsync(o.pre, 0, sizeof(int) * 4, o.stream) != hipSuccess) return PF_EHIP;
     // the sub-objects' overflow / wait flags latch into the handle's sticky error words
     alias_err(o.fe.err, o.errw + E_FE_SECTOR);
     alias_err(o.grid.err, o.errw + E_GRID);
@@ -2827,7 +2718,6 @@ int odom_reset(OdomGPU& o) {
     if (hipMemsetAsync(o.tail_status, 0, sizeof(u64) * (o.tail_tiles + 1), o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.rgm_stat, 0, sizeof(int) * 8, o.stream) != hipSuccess) return PF_EHIP;
     if (hipMemsetAsync(o.rgm_bcount, 0, sizeof(u32) * kRgmBuckets, o.stream) != hipSuccess) return PF_EHIP;
-    if (hipMemsetAsync(o.pre, 0, sizeof(int) * 4, o.stream) != hipSuccess) return PF_EHIP;
     for (int p = 0; p < kSlots; ++p)
         if (hipMemsetAsync(o.sb[p].cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)o.cls.nc * o.map_cap);
@@ -2879,7 +2769,7 @@ void odom_destroy(OdomGPU& o) {
                     o.keys, o.vals, o.tail_status, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
                     o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg, o.errw,
                     o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.rgm_ktmp, o.rgm_vox, o.rgm_kflag, o.rgm_bcount, o.rgm_bkey,
-                    o.rgm_btag, o.pre, o.pred, o.rgm_bslot,
+                    o.rgm_btag,
                     o.rgm_vtmp, o.rgm_stat};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
@@ -2969,15 +2859,13 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     // grids of the class maps (kd-tree builds, :249-250 / BPF :723-725); the pose prediction rides on
     // the bounds kernel as its tail (it reads the map sizes of the previous frame, not the grid)
     GridPtrs gp{{map_cur(o)[0], map_cur(o)[1], map_cur(o)[2]}, {cnt + C_M, cnt + C_M + 1, cnt + C_M + 2}, nc};
-    GridBoundsArgs gba = grid_bounds_args(o.grid, gp);
-    gba.ready = o.pre;                                    // dims set by the previous rgbds merge
-    hipLaunchKernelGGL(k_grid_bounds<PredictTail>, dim3(kGridBoundsBlocks + 1), dim3(256), 0, s, gba,
-                       PredictTail{o.st, cnt, sb.cnt, o.acc, o.cls, o.pre, o.pred});
+    hipLaunchKernelGGL(k_grid_bounds<PredictTail>, dim3(kGridBoundsBlocks + 1), dim3(256), 0, s,
+                       grid_bounds_args(o.grid, gp), PredictTail{o.st, cnt, sb.cnt, o.acc, o.cls});
     grid_build(o.grid, gp, o.prim, s, true);
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
         AssocArgs aa{o.st, cnt, o.acc, gv, o.cls, clouds(sb.ds), clouds(map_cur(o)), o.nbr, o.qflag, o.geo, o.spars,
-                     o.roundv, o.pbkt, o.pnext, (u32)o.map_cap, o.lm_ticket, o.lm_part, o.pre};
+                     o.roundv, o.pbkt, o.pnext, (u32)o.map_cap, o.lm_ticket, o.lm_part};
         PF_LAUNCH_NC(nc, k_assoc, dim3(kGrid), dim3(256), 0, s, aa);
         ObsArgs oa{cnt, o.acc, o.cls, clouds(map_cur(o)), clouds_w(sb.ds), o.nbr, o.qflag, o.pbkt, o.pnext, o.tailinc,
                    (u32)o.map_cap, o.roundv, o.spars, o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max,
@@ -2999,8 +2887,7 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
                    leaf, o.prm.k_new, o.prm.theta_p, o.prm.theta_max, o.rgm_okey, o.rgm_key64, o.rgm_vtag,
                    o.rgm_vox, o.rgm_kflag, clouds_w(map_next(o)), (u32)o.map_cap, o.errw + E_MAP, o.tail_status,
                    (u32*)(o.tail_status + o.tail_tiles), o.prim.err, o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp,
-                   o.rgm_stat, o.rgm_bcount, o.rgm_bkey, o.rgm_btag, o.pre, o.pred, o.rgm_bslot, o.grid.bounds, o.grid.dims,
-                   o.grid.d_ncells, (long long)o.grid.cell_cap, o.grid.err, o.dbg};
+                   o.rgm_stat, o.rgm_bcount, o.rgm_bkey, o.rgm_btag, o.dbg};
         PF_LAUNCH_NC(nc, k_rgm_bucket, dim3(kRgmBuckets + 1), dim3(kRgmThreads), 0, s, ra);
         PF_LAUNCH_NC(nc, k_rgm_fallback, dim3(1), dim3(kFbThreads), 0, s, ra);
         return;
