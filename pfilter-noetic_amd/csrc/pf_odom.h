@@ -197,12 +197,13 @@ struct OdomGPU {
     u32 *keys = nullptr, *vals = nullptr;
     u64* tail_status = nullptr;   // k_rg_tail look-back words [tail_tiles] + arrival counter
     size_t tail_tiles = 0;
-    // rgbds by merge (k_rgm_bucket / k_rgm_fallback, the default order): the map is kept
+    // rgbds by merge (k_rgm_bucket / k_rgm_finish, the default order): the map is kept
     // in voxel order, so only this frame's appended points are sorted and then merged into it
     u64* rgm_okey = nullptr;       // [nc * map_cap] voxel keys of the map points, map order
     u64* rgm_key64 = nullptr;      // [sort_cap] voxel keys of every element, element order
     u32* rgm_vtag = nullptr;       // [sort_cap] element index | cropped << 31
     u32* rgm_bcount = nullptr;     // [kRgmBuckets] appended points per bucket (lists built by the LM)
+    int* rgm_bmeta = nullptr;      // [kRgmBuckets][8] each bucket's merged base, length, kept voxels per class
     u64* rgm_bkey = nullptr;       // [kRgmBuckets * kRgmBucketCap] the lists: keys, tags
     u32* rgm_btag = nullptr;
     float4* rgm_vox = nullptr;     // [sort_cap] voxel outputs at merged positions

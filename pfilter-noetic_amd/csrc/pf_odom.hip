@@ -911,7 +911,7 @@ struct RgmPrep {
     u64* key64;
     u32* vtag;
     VgLeaf leaf;
-    u32* bcount;           // [kRgmBuckets] list sizes (zeroed by the bucket kernel's last workgroup)
+    u32* bcount;           // [kRgmBuckets] list sizes (each zeroed by k_rgm_finish after its bucket is merged)
     u64* bkey;             // [kRgmBuckets][kRgmBucketCap]
     u32* btag;
     int* stat;             // rgm_stat: [0] fallback flag
@@ -1860,13 +1860,15 @@ __global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const f
 // (key, element) in registers and LDS (a bitonic network, shuffles within a wave); reduces the voxels
 // of its bucket (the Vector4f centroid and r / g maxima of :108-125, extractstablepoint :12-14, the
 // ageing :634-646, cropped elements skipped); ranks the kept voxels in merged order and writes them
-// straight into the other map set (mapset[mpar ^ 1]) at their class-map index, the class-c voxels of
-// earlier buckets counted by a look-back per class; the last bucket to finish writes the map sizes.
-// When the map
-// is not in key order (the first update after initMapWithPoints or pf_odom_set_map, or a centroid that
-// rounded into a neighbouring voxel) or a bucket holds more than kRgmBucketCap appended points, the
-// buckets' output is void and k_rgm_fallback's single workgroup sorts every element (a stable LSD
-// radix sort over the 64-bit keys) and reduces the voxels itself.
+// and publishes its length and kept voxels per class. k_rgm_finish (a second launch, one workgroup per
+// bucket) then writes each bucket's kept voxels into the other map set (mapset[mpar ^ 1]) at their
+// class-map index and the map sizes. No workgroup of a launch waits on another (a look-back across
+// buckets deadlocked when many handles' launches shared the CUs: nothing guarantees that the bucket a
+// workgroup waits on is resident). When the map is not in key order (the first update after
+// initMapWithPoints or pf_odom_set_map, or a centroid that rounded into a neighbouring voxel) or a
+// bucket holds more than kRgmBucketCap appended points, the buckets' output is void and k_rgm_finish's
+// workgroup 0 sorts every element (a stable LSD radix sort over the 64-bit keys) and reduces the voxels
+// itself.
 
 struct RgmArgs {
     DevState* st;
@@ -1888,14 +1890,12 @@ struct RgmArgs {
     CloudsW mapw;          // the new class maps (the other map set)
     u32 map_cap;
     int* err_map;          // sticky error word E_MAP
-    u64* status;           // look-back words, [class][bucket] (zero between calls), and an arrival counter
-    u32* arrive;
-    int* err;
     u64* kout;             // fallback: sorted keys / tags and scratch
     u32* vout;
     u64* ktmp;
     u32* vtmp;
     int* stat;             // [8] (OdomGPU::rgm_stat)
+    int* bmeta;            // [kRgmBuckets][8]: merged base, length, kept voxels per class (-> k_rgm_finish)
     u32* bcount;           // the appended points' bucket lists (RgmPrep)
     const u64* bkey;
     const u32* btag;
@@ -2047,16 +2047,14 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     __shared__ float4 opt[kRgmOldLds];                 // the bucket's map points (when cached)
     __shared__ float4 apt[kRgmAppLds];                 // its appended points in sorted order (when cached)
     __shared__ u64 s_nextk;
-    __shared__ int s_cnt, s_before[kRgmThreads / 64], s_cls[kMaxC], s_last;
-    __shared__ u32 s_w[kRgmThreads / 64], s_pref[kMaxC];
+    __shared__ int s_cnt, s_before[kRgmThreads / 64], s_cls[kMaxC];
+    __shared__ u32 s_w[kRgmThreads / 64];
     const int t = threadIdx.x, b = blockIdx.x;
     const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
-    const int n = V.total();
     int M = 0;
 #pragma unroll
     for (int c = 0; c < NC; ++c) M += V.m[c];
-    const int A = n - M;
-    if (b == kRgmBuckets) {                            // (reads no counter: the last bucket rewrites them)
+    if (b == kRgmBuckets) {                            // (k_rgm_finish rewrites the counters after)
         finalize_pose(a.st, a.poses, a.pose_cap, 1, a.acc, a.st->params);
         return;
     }
@@ -2216,10 +2214,9 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     }
     __syncthreads();
     RGM_MARK(4);
-    // 5. the kept voxels' ranks in merged order (tiles of 1024); per class, the kept voxels of earlier
-    // buckets by a look-back (wave c for class c); a voxel of class c goes to mapw[c] at (its bucket's
-    // class-c offset) + (its rank among the bucket's class-c voxels), classes being contiguous in key
-    // order
+    // 5. the kept voxels' ranks in merged order, and the bucket's numbers for k_rgm_finish (which places
+    // them in the other map set once every bucket is done: no workgroup waits on another here, so any
+    // number of handles may run this kernel at once)
     u32 run = 0;
     for (int t0 = 0; t0 < L; t0 += kRgmThreads) {
         const int p = t0 + t;
@@ -2231,69 +2228,13 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         run += tot;
     }
     RGM_MARK(5);
-    if ((t >> 6) < NC) {
-    
-        const int c = t >> 6;
-        const u32 excl = tile_lookback(a.status + c * kRgmBuckets, b, (u32)s_cls[c], a.err);
-        if (lane_id() == 0) s_pref[c] = excl;
-    }
-    __syncthreads();
-    RGM_MARK(6);
-    u32 first_rank[kMaxC];                             // bucket-local rank of the first voxel of class c
-    {
-        u32 acc = 0;
-#pragma unroll
-        for (int c = 0; c < kMaxC; ++c) {
-            first_rank[c] = acc;
-            acc += c < NC ? (u32)s_cls[c] : 0u;
-        }
-    }
-    bool over = false;
-    for (int p = t; p < L; p += kRgmThreads) {
-        const u32 f = a.kflag[base + p];
-        if (!(f & 0x3FFFFFFFu)) continue;
-        const int c = min((int)(f >> 30), NC - 1);
-        const u32 idx = s_pref[c] + (f & 0x3FFFFFFFu) - 1u - sel3(c, first_rank[0], first_rank[1], first_rank[2]);
-        if (idx < a.map_cap) a.mapw.at(c)[idx] = a.vox[base + p];
-        else over = true;
-    }
-    if (over && !__hip_atomic_load(&a.stat[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicOr(a.err_map, 1);                        // (out-of-order input: the fallback redoes it)
-    RGM_MARK(7);
-    // 6. the kept voxels of every class summed over the buckets; the last bucket to arrive writes the
-    // map sizes (cnt[C_M + c]), the class boundaries (cnt[C_NLT + c - 1] = kept voxels of classes < c)
-    // and the total unless the fallback will, and clears the accumulators and the look-back words
-    if (t < NC && s_cls[t]) __hip_atomic_fetch_add(&a.stat[4 + t], s_cls[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0)
-        s_last = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (u32)kRgmBuckets - 1;
-    __syncthreads();
-    if (!s_last) return;
     if (t == 0) {
-        int kc[kMaxC], tot = 0;
+        int* m = a.bmeta + 8 * b;
+        m[0] = base;
+        m[1] = L;
 #pragma unroll
-        for (int c = 0; c < kMaxC; ++c) {
-            kc[c] = __hip_atomic_load(&a.stat[4 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.stat[4 + c], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (!__hip_atomic_load(&a.stat[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-#pragma unroll
-            for (int c = 1; c <= kMaxC; ++c) {
-                tot += kc[c - 1];
-                a.cnt[C_NLT + c - 1] = tot;
-            }
-#pragma unroll
-            for (int c = 0; c < NC; ++c) a.cnt[C_M + c] = min(kc[c], (int)a.map_cap);
-            a.cnt[C_KEEP_TOTAL] = tot;
-            a.cnt[C_NRG] = n;
-            if (A > a.stat[2]) a.stat[2] = A;
-        }
-        __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int c = 0; c < kMaxC; ++c) m[2 + c] = c < NC ? s_cls[c] : 0;
     }
-    for (int i = t; i < NC * kRgmBuckets; i += kRgmThreads)
-        __hip_atomic_store(&a.status[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int i = t; i < kRgmBuckets; i += kRgmThreads) a.bcount[i] = 0u;      // the lists of the next update
 }
 
 constexpr int kFbThreads = 256;
@@ -2470,21 +2411,113 @@ __device__ void rgm_fallback_tail(const RgmArgs& a, const RgView<NC>& V, int n) 
     }
 }
 
+// The second half of the merge (one workgroup per bucket, after every bucket is done): bucket b's
+// kept voxels go to their class-map index in the other map set (the class-c voxels of the buckets
+// before it counted from their numbers); workgroup 0 also writes the map sizes, the class boundaries
+// and the total. When the merge is void, workgroup 0 runs the fallback instead (a single-workgroup
+// sort and reduction of every element) and the others only reset their bucket's list.
 template <int NC>
-__global__ void __launch_bounds__(kFbThreads) k_rgm_fallback(RgmArgs a) {
-    if (!a.stat[0]) return;                            // the buckets' output stands
-    const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
-    const int n = V.total();
-    __syncthreads();                                   // every thread has read the map sizes
-    rgm_fallback_sort(a, n);
-    __threadfence_block();
+__global__ void __launch_bounds__(kFbThreads) k_rgm_finish(RgmArgs a) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    __shared__ int s_red[kFbThreads / 64][kMaxC];
+    __shared__ int s_pre[kMaxC], s_tot[kMaxC];
+    const bool fb = a.stat[0] != 0;
+    if (fb) {
+        if (b != 0) {
+            if (t == 0) a.bcount[b] = 0u;
+            return;
+        }
+        const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
+        const int n = V.total();
+        __syncthreads();                               // every thread has read the map sizes
+        rgm_fallback_sort(a, n);
+        __threadfence_block();
+        __syncthreads();
+        rgm_fallback_tail<NC>(a, V, n);
+        if (t == 0) {
+            a.bcount[0] = 0u;
+            a.stat[1]++;
+            const int A = n - (V.m[0] + (NC > 1 ? V.m[1] : 0) + (NC > 2 ? V.m[2] : 0));
+            if (A > a.stat[2]) a.stat[2] = A;
+            a.stat[0] = 0;
+        }
+        return;
+    }
+    // the kept class-c voxels of the buckets before b (and of all buckets, for workgroup 0)
+    int pre[kMaxC] = {0, 0, 0}, all[kMaxC] = {0, 0, 0};
+    for (int bb = t; bb < kRgmBuckets; bb += kFbThreads) {
+        const int* m = a.bmeta + 8 * bb;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int v = m[2 + c];
+            if (bb < b) pre[c] += v;
+            all[c] += v;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        pre[c] = wave_sum_i(pre[c]);
+        all[c] = wave_sum_i(all[c]);
+    }
+    if (lane_id() == 0)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) s_red[t >> 6][c] = pre[c];
     __syncthreads();
-    rgm_fallback_tail<NC>(a, V, n);
-    if (threadIdx.x == 0) {
-        a.stat[1]++;
-        if (n - (V.m[0] + (NC > 1 ? V.m[1] : 0) + (NC > 2 ? V.m[2] : 0)) > a.stat[2])
-            a.stat[2] = n - (V.m[0] + (NC > 1 ? V.m[1] : 0) + (NC > 2 ? V.m[2] : 0));
-        a.stat[0] = 0;
+    if (t < NC) {
+        int v = 0;
+        for (int w = 0; w < kFbThreads / 64; ++w) v += s_red[w][t];
+        s_pre[t] = v;
+    }
+    __syncthreads();
+    if (lane_id() == 0)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) s_red[t >> 6][c] = all[c];
+    __syncthreads();
+    if (t < NC) {
+        int v = 0;
+        for (int w = 0; w < kFbThreads / 64; ++w) v += s_red[w][t];
+        s_tot[t] = v;
+    }
+    __syncthreads();
+    const int* m = a.bmeta + 8 * b;
+    const int base = m[0], L = m[1];
+    u32 first_rank[kMaxC];                             // bucket-local rank of the first voxel of class c
+    {
+        u32 acc = 0;
+#pragma unroll
+        for (int c = 0; c < kMaxC; ++c) {
+            first_rank[c] = acc;
+            acc += c < NC ? (u32)m[2 + c] : 0u;
+        }
+    }
+    bool over = false;
+    for (int p = t; p < L; p += kFbThreads) {
+        const u32 f = a.kflag[base + p];
+        if (!(f & 0x3FFFFFFFu)) continue;
+        const int c = min((int)(f >> 30), NC - 1);
+        const u32 idx = (u32)sel3(c, s_pre[0], s_pre[1], s_pre[2]) + (f & 0x3FFFFFFFu) - 1u -
+                        sel3(c, first_rank[0], first_rank[1], first_rank[2]);
+        if (idx < a.map_cap) a.mapw.at(c)[idx] = a.vox[base + p];
+        else over = true;
+    }
+    if (over) atomicOr(a.err_map, 1);
+    if (t == 0) {
+        a.bcount[b] = 0u;                              // the list of the next update
+        if (b == 0) {
+            const RgView<NC> V = rg_view<NC>(a.cnt, a.map, a.map);
+            const int n = V.total();
+            int M = 0;
+            for (int c = 0; c < NC; ++c) M += V.m[c];
+            int tot = 0;
+            for (int c = 1; c <= kMaxC; ++c) {
+                tot += c - 1 < NC ? s_tot[c - 1] : 0;
+                a.cnt[C_NLT + c - 1] = tot;
+            }
+            for (int c = 0; c < NC; ++c) a.cnt[C_M + c] = min(s_tot[c], (int)a.map_cap);
+            a.cnt[C_KEEP_TOTAL] = tot;
+            a.cnt[C_NRG] = n;
+            if (n - M > a.stat[2]) a.stat[2] = n - M;
+        }
     }
 }
 
@@ -2627,7 +2660,6 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     }
     PF_ALLOC(o.seg_out, sizeof(float4) * o.sort_cap);
     o.tail_tiles = (o.sort_cap + kTailTile - 1) / kTailTile;
-    if (o.tail_tiles < (size_t)kMaxC * kRgmBuckets) o.tail_tiles = (size_t)kMaxC * kRgmBuckets;   // rgm look-backs
     PF_ALLOC(o.tail_status, sizeof(u64) * (o.tail_tiles + 1));    // look-back words + the arrival counter
     PF_ALLOC(o.keys, sizeof(u32) * (o.sort_cap + 1));
     PF_ALLOC(o.vals, sizeof(u32) * (o.sort_cap + 1));
@@ -2652,6 +2684,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.rgm_ktmp, sizeof(u64) * o.sort_cap);
     PF_ALLOC(o.rgm_vtmp, sizeof(u32) * o.sort_cap);
     PF_ALLOC(o.rgm_bcount, sizeof(u32) * kRgmBuckets);
+    PF_ALLOC(o.rgm_bmeta, sizeof(int) * 8 * kRgmBuckets);
     PF_ALLOC(o.rgm_bkey, sizeof(u64) * kRgmBuckets * kRgmBucketCap);
     PF_ALLOC(o.rgm_btag, sizeof(u32) * kRgmBuckets * kRgmBucketCap);
     PF_ALLOC(o.rgm_vox, sizeof(float4) * o.sort_cap);
@@ -2768,7 +2801,7 @@ void odom_destroy(OdomGPU& o) {
     void* ptrs[] = {o.st, o.lm, o.cnt, o.acc, o.acc_a, o.vkeys, o.vvals, o.vflags, o.vscan, o.vsegstart, o.seg_out,
                     o.keys, o.vals, o.tail_status, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
                     o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg, o.errw,
-                    o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.rgm_ktmp, o.rgm_vox, o.rgm_kflag, o.rgm_bcount, o.rgm_bkey,
+                    o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.rgm_ktmp, o.rgm_vox, o.rgm_kflag, o.rgm_bcount, o.rgm_bmeta, o.rgm_bkey,
                     o.rgm_btag,
                     o.rgm_vtmp, o.rgm_stat};
     for (void* q : ptrs) (void)hipFree(q);
@@ -2885,11 +2918,10 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     if (!o.tie_order && !o.rg_radix) {                    // rgbds by merge (the map stays in key order)
         RgmArgs ra{o.st, cnt, o.acc, clouds(map_cur(o)), clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap,
                    leaf, o.prm.k_new, o.prm.theta_p, o.prm.theta_max, o.rgm_okey, o.rgm_key64, o.rgm_vtag,
-                   o.rgm_vox, o.rgm_kflag, clouds_w(map_next(o)), (u32)o.map_cap, o.errw + E_MAP, o.tail_status,
-                   (u32*)(o.tail_status + o.tail_tiles), o.prim.err, o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp,
-                   o.rgm_stat, o.rgm_bcount, o.rgm_bkey, o.rgm_btag, o.dbg};
+                   o.rgm_vox, o.rgm_kflag, clouds_w(map_next(o)), (u32)o.map_cap, o.errw + E_MAP, o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp,
+                   o.rgm_stat, o.rgm_bmeta, o.rgm_bcount, o.rgm_bkey, o.rgm_btag, o.dbg};
         PF_LAUNCH_NC(nc, k_rgm_bucket, dim3(kRgmBuckets + 1), dim3(kRgmThreads), 0, s, ra);
-        PF_LAUNCH_NC(nc, k_rgm_fallback, dim3(1), dim3(kFbThreads), 0, s, ra);
+        PF_LAUNCH_NC(nc, k_rgm_finish, dim3(kRgmBuckets), dim3(kFbThreads), 0, s, ra);
         return;
     }
     if (rg_fused_keys(o.leaf_rg, nc)) {

@@ -23,7 +23,7 @@ od = pa.Odom_ES_EstimationClass()
 od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
 L = pa.lib()
 L.pf_dev_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-names = ["keys", "apps", "sort", "voxels", "scan", "lookback", "write"]
+names = ["keys", "apps", "sort", "voxels", "scan"]
 acc = []
 for k in range(N):
     od.frame_device(db.ptr + k * buf.shape[1] * 16, int(cnt[k]))
@@ -38,7 +38,7 @@ t0 = a[:, :, 0].min(axis=1)[:, None]
 for i, nm in enumerate(names):
     d = (a[:, :, i + 1] - a[:, :, i]) / 100.0
     print("%-9s us: median over buckets %.2f, max %.2f" % (nm, np.median(d), np.median(d.max(axis=1))))
-span = (a[:, :, 7].max(axis=1) - a[:, :, 0].min(axis=1)) / 100.0
+span = (a[:, :, 5].max(axis=1) - a[:, :, 0].min(axis=1)) / 100.0
 start = (a[:, :, 0].max(axis=1) - a[:, :, 0].min(axis=1)) / 100.0
 print("bucket start spread us (median) %.2f; first start -> last mark %.2f" % (np.median(start), np.median(span)))
 print("appended points per bucket (last frame): max %d, mean %.1f" % (a[-1, :, 9].max(), a[-1, :, 9].mean()))
