@@ -338,8 +338,10 @@ __global__ void __launch_bounds__(256) k_u_keys(ClsDev d, const int* __restrict_
 }
 // cell-ordered points (w = U index), and the counts left zero for the next build
 __global__ void __launch_bounds__(256) k_u_place(ClsDev d, float4* __restrict__ cpts, u32* __restrict__ cell_count,
-                                                 const int* __restrict__ dm) {
+                                                 const int* __restrict__ dm, u32* __restrict__ ttot, int ttiles) {
     const int nu = d.cnt[CC_NU];
+    if (blockIdx.x == 0)                          // the grid scan's tile totals, for the next build
+        for (int j = threadIdx.x; j < ttiles; j += blockDim.x) ttot[j] = 0u;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
         const u32 j = d.cvals[i];
         const float4 p = d.U[PF_IDX(d, j, nu)];
@@ -800,7 +802,8 @@ void cls_enqueue(ClsGPU& c, const float4* d_pts, const int* d_n, float4* const* 
     grid_count_scan(c.grid, gp, c.w, s);
     hipLaunchKernelGGL(k_u_keys, dim3(kEwBlocks), dim3(256), 0, s, d, c.grid.dims, sort_hist(c.w, 32, true));
     radix_sort_pairs(c.ckeys, c.cvals, c.cnt + CC_NU, 32, c.w, s, nullptr, nullptr, true);
-    hipLaunchKernelGGL(k_u_place, dim3(kEwBlocks), dim3(256), 0, s, d, c.grid.cpts, c.grid.cell_count, c.grid.dims);
+    hipLaunchKernelGGL(k_u_place, dim3(kEwBlocks), dim3(256), 0, s, d, c.grid.cpts, c.grid.cell_count, c.grid.dims,
+                       c.grid.ttot, c.grid.ttiles);
     hipLaunchKernelGGL(k_u_boxes, dim3(kEwBlocks), dim3(256), 0, s, d, c.grid.cpts);
     const GridView gv{c.grid.dims, c.grid.cell_start, c.grid.cpts};
     hipLaunchKernelGGL(k_cls_search, dim3(4096), dim3(256), 0, s, d, gv, c.nbr);

@@ -22,9 +22,15 @@ struct GridGPU {
     u32* cell_start = nullptr;  // [cell_cap + 1]
     u32* slot = nullptr;        // [pts_cap]
     float4* cpts = nullptr;     // [pts_cap] cell-ordered (x, y, z, bits(map index))
+    u32* ttot = nullptr;        // [ttiles] points per scan tile of kGridScanTile cells (k_grid_count)
+    int ttiles = 0;
     size_t pts_cap = 0;
     size_t cell_cap = 0;
 };
+// cells per tile of the cell-count scan: k_grid_count also counts the points of each tile, so a
+// tile's exclusive prefix is a sum of those totals (no look-back across workgroups)
+constexpr int kGridScanPer = 32;
+constexpr int kGridScanTile = 256 * kGridScanPer;
 
 // up to kGridMaps maps share one cell array (map m's cells start at dims[8 m + 6])
 constexpr int kGridMaps = 3;

@@ -22,14 +22,16 @@ __device__ __forceinline__ int cell_of_checked(const int* dm, float4 p) {
 // Agg: clouds whose consecutive points mostly share a cell (the front end's non-ground cloud, in
 // 3 m ground-cell order) take one atomic per run of equal cells in a wave (up to 4 runs; the rest
 // per lane) instead of serialising on the cell's counter. Slots inside a cell are arbitrary either
-// way (the queries order candidates by (d^2, index)).
+// way (the queries order candidates by (d^2, index)). Every point is also counted in its scan tile
+// (ttot, one atomic per distinct tile in a wave: consecutive points share a tile).
 template <bool Agg>
 __global__ void __launch_bounds__(256) k_grid_count(GridPtrs gp, const int* __restrict__ dims, u32* __restrict__ cnt,
-                                                     u32* __restrict__ slot, int* __restrict__ err) {
+                                                     u32* __restrict__ slot, u32* __restrict__ ttot,
+                                                     int* __restrict__ err) {
     const GridIdx gi = grid_idx(gp);
     const int stride = gridDim.x * blockDim.x;
     const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
-    for (int i = i0; Agg ? (i - (int)threadIdx.x % 64 < gi.total) : (i < gi.total); i += stride) {
+    for (int i = i0; i - (int)threadIdx.x % 64 < gi.total; i += stride) {   // trip count uniform per wave
         int cid = -1;
         if (i < gi.total) {
             const int mi = gi.map_of(i);
@@ -37,6 +39,17 @@ __global__ void __launch_bounds__(256) k_grid_count(GridPtrs gp, const int* __re
             if (dm[7]) {
                 cid = cell_of_checked(dm, gp.m[mi][i - gi.start(mi)]);
                 if (cid < 0) atomicOr(err, 1);
+            }
+        }
+        {
+            const int tt = cid >= 0 ? cid / kGridScanTile : -1;
+            u64 todo = __ballot(tt >= 0);
+            while (todo) {                                 // wave-uniform
+                const int leader = __ffsll((unsigned long long)todo) - 1;
+                const int c = __shfl(tt, leader, 64);
+                const u64 m = __ballot(tt == c) & todo;
+                if (lane_id() == leader) atomicAdd(&ttot[c], (u32)__popcll(m));
+                todo &= ~m;
             }
         }
         if (!Agg) {
@@ -58,10 +71,67 @@ __global__ void __launch_bounds__(256) k_grid_count(GridPtrs gp, const int* __re
     }
 }
 
+// exclusive scan of the cell counts (d_n = cells + 1 items): tile t's prefix is the sum of the point
+// totals of tiles < t, so every workgroup scans its tiles independently
+__global__ void __launch_bounds__(256) k_grid_scan(const u32* __restrict__ in, u32* __restrict__ out,
+                                                    const int* __restrict__ d_n, const u32* __restrict__ ttot) {
+    constexpr int PER = kGridScanPer;
+    __shared__ u32 lw[4];
+    __shared__ u32 lp[4];
+    const int n = *d_n;
+    const int ntiles = (n + kGridScanTile - 1) / kGridScanTile;
+    const int t = threadIdx.x;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int base = tile * kGridScanTile + t * PER;
+        u32 v[PER];
+        if (base + PER <= n) {                                  // whole: 16-byte loads
+#pragma unroll
+            for (int k = 0; k < PER; k += 4) {
+                const uint4 q = *reinterpret_cast<const uint4*>(in + base + k);
+                v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PER; ++k) v[k] = base + k < n ? in[base + k] : 0u;
+        }
+        u32 pre = 0;
+        for (int j = t; j < tile; j += 256) pre += ttot[j];
+        pre = (u32)wave_sum_i((int)pre);
+        if (lane_id() == 0) lp[t >> 6] = pre;
+        u32 sum = 0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) sum += v[k];
+        u32 agg;
+        const u32 tex = block_excl_scan256(sum, lw, agg);       // (its barriers publish lp)
+        u32 r = lp[0] + lp[1] + lp[2] + lp[3] + tex;
+        if (base + PER <= n) {
+#pragma unroll
+            for (int k = 0; k < PER; k += 4) {
+                uint4 q;
+                q.x = r; r += v[k];
+                q.y = r; r += v[k + 1];
+                q.z = r; r += v[k + 2];
+                q.w = r; r += v[k + 3];
+                *reinterpret_cast<uint4*>(out + base + k) = q;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                if (base + k < n) out[base + k] = r;
+                r += v[k];
+            }
+        }
+        __syncthreads();                                        // lp reused by the next tile
+    }
+}
+
 __global__ void __launch_bounds__(256) k_grid_scatter(GridPtrs gp, const int* __restrict__ dims,
                                                        const u32* __restrict__ start, const u32* __restrict__ slot,
-                                                       float4* __restrict__ cpts, u32* __restrict__ cnt) {
+                                                       float4* __restrict__ cpts, u32* __restrict__ cnt,
+                                                       u32* __restrict__ ttot, int ttiles) {
     const GridIdx gi = grid_idx(gp);
+    if (blockIdx.x == 0)                      // the tile totals of the next build (the scan has read them)
+        for (int j = threadIdx.x; j < ttiles; j += blockDim.x) ttot[j] = 0u;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < gi.total; i += gridDim.x * blockDim.x) {
         const int mi = gi.map_of(i);
         const int* dm = dims + 8 * mi;
@@ -207,6 +277,9 @@ int grid_alloc(GridGPU& g, size_t pts_cap, size_t cell_cap) {
     if (hipMalloc(&g.slot, sizeof(u32) * pts_cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&g.cpts, sizeof(float4) * pts_cap) != hipSuccess) return PF_ENOMEM;
     if (hipMalloc(&g.arrive, sizeof(u32)) != hipSuccess) return PF_ENOMEM;
+    g.ttiles = (int)((cell_cap + 1 + kGridScanTile - 1) / kGridScanTile);
+    if (hipMalloc(&g.ttot, sizeof(u32) * g.ttiles) != hipSuccess) return PF_ENOMEM;
+    if (hipMemset(g.ttot, 0, sizeof(u32) * g.ttiles) != hipSuccess) return PF_EHIP;
     if (hipMemset(g.err, 0, sizeof(int)) != hipSuccess) return PF_EHIP;
     if (hipMemset(g.arrive, 0, sizeof(u32)) != hipSuccess) return PF_EHIP;
     if (hipMemset(g.cell_count, 0, sizeof(u32) * (cell_cap + 1)) != hipSuccess) return PF_EHIP;
@@ -226,27 +299,38 @@ void grid_free(GridGPU& g) {
     (void)hipFree(g.slot);
     (void)hipFree(g.cpts);
     (void)hipFree(g.arrive);
+    (void)hipFree(g.ttot);
     g = GridGPU{};
 }
 
+static void grid_scan(GridGPU& g, hipStream_t s) {
+    const int grid = g.ttiles < kSortMaxBlocks ? g.ttiles : kSortMaxBlocks;
+    hipLaunchKernelGGL(k_grid_scan, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, g.cell_count, g.cell_start, g.d_ncells,
+                       g.ttot);
+}
+
 void grid_count_scan(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s) {
+    (void)w;
     hipLaunchKernelGGL(k_grid_bounds<NoTail>, dim3(kGridBoundsBlocks), dim3(256), 0, s, grid_bounds_args(g, gp), NoTail{});
-    hipLaunchKernelGGL(k_grid_count<true>, dim3(512), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot, g.err);
-    scan_exclusive(g.cell_count, g.cell_start, g.d_ncells, nullptr, w, s);
+    hipLaunchKernelGGL(k_grid_count<true>, dim3(512), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot, g.ttot, g.err);
+    grid_scan(g, s);
 }
 
 void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s, bool bounds_launched, bool aggregate) {
+    (void)w;
     const int nb = 512;
     if (!bounds_launched)
         hipLaunchKernelGGL(k_grid_bounds<NoTail>, dim3(kGridBoundsBlocks), dim3(256), 0, s, grid_bounds_args(g, gp),
                            NoTail{});
     if (aggregate)
-        hipLaunchKernelGGL(k_grid_count<true>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot, g.err);
+        hipLaunchKernelGGL(k_grid_count<true>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot, g.ttot,
+                           g.err);
     else
-        hipLaunchKernelGGL(k_grid_count<false>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot, g.err);
-    scan_exclusive(g.cell_count, g.cell_start, g.d_ncells, nullptr, w, s, true);
+        hipLaunchKernelGGL(k_grid_count<false>, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_count, g.slot, g.ttot,
+                           g.err);
+    grid_scan(g, s);
     hipLaunchKernelGGL(k_grid_scatter, dim3(nb), dim3(256), 0, s, gp, g.dims, g.cell_start, g.slot, g.cpts,
-                       g.cell_count);
+                       g.cell_count, g.ttot, g.ttiles);
 }
 
 }  // namespace pf
