@@ -570,6 +570,7 @@ int pf_odom_set_map(pf_odom* h, int which, const float* xyz, const uint8_t* rg, 
     }
     if (n) PF_HIP_TRY(hipMemcpyAsync(map_cur(o)[which], tmp.data(), sizeof(float4) * n, hipMemcpyHostToDevice, o.stream));
     hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_M + which, (int)n);
+    o.dims_fresh = false;                               // the next update's grid takes its bounds pass
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     return PF_OK;
 }
@@ -696,7 +697,9 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
     const int nc = o.cls.nc;
     const bool scan = nc == 3 && !cl;
     const int p = o.frames % kSlots;
-    const bool steady = o.inited && o.opt_count_host <= 2 && o.graph_enabled;
+    // (graph B of the merge path starts from the grid dims of the previous update: a frame after a
+    // host map write runs eagerly)
+    const bool steady = o.inited && o.opt_count_host <= 2 && o.graph_enabled && (o.dims_fresh || !odom_merge_mode(o));
     if (scan && n > o.in_cap) return PF_ECAPACITY;
     int rc = 0;
     PF_HT(0, rc = stage_a_begin(h, p));

@@ -191,6 +191,75 @@ __global__ void __launch_bounds__(256) k_grid_bounds(GridBoundsArgs ga, Tail tai
     }
 }
 
+__device__ __forceinline__ int cell_of(const int* dm, float4 p) {
+    const int x = (int)floorf(p.x) - dm[0], y = (int)floorf(p.y) - dm[1], z = (int)floorf(p.z) - dm[2];
+    return dm[6] + (z * dm[4] + y) * dm[3] + x;
+}
+// the same, -1 for a point outside the grid's bounds (never, when the dims come from these points'
+// own bounds: a guard that turns inconsistent dims into a reported error instead of stray writes)
+__device__ __forceinline__ int cell_of_checked(const int* dm, float4 p) {
+    const int x = (int)floorf(p.x) - dm[0], y = (int)floorf(p.y) - dm[1], z = (int)floorf(p.z) - dm[2];
+    if ((unsigned)x >= (unsigned)dm[3] || (unsigned)y >= (unsigned)dm[4] || (unsigned)z >= (unsigned)dm[5]) return -1;
+    return dm[6] + (z * dm[4] + y) * dm[3] + x;
+}
+
+// Agg: clouds whose consecutive points mostly share a cell (the front end's non-ground cloud, in
+// 3 m ground-cell order) take one atomic per run of equal cells in a wave (up to 4 runs; the rest
+// per lane) instead of serialising on the cell's counter. Slots inside a cell are arbitrary either
+// way (the queries order candidates by (d^2, index)). Every point is also counted in its scan tile
+// (ttot, one atomic per distinct tile in a wave: consecutive points share a tile).
+// A Tail with kActive runs on one extra workgroup (the last), as in k_grid_bounds.
+template <bool Agg, class Tail>
+__global__ void __launch_bounds__(256) k_grid_count(GridPtrs gp, const int* __restrict__ dims, u32* __restrict__ cnt,
+                                                     u32* __restrict__ slot, u32* __restrict__ ttot,
+                                                     int* __restrict__ err, Tail tail) {
+    if (Tail::kActive && blockIdx.x == gridDim.x - 1) {
+        tail((int)threadIdx.x);
+        return;
+    }
+    const GridIdx gi = grid_idx(gp);
+    const int stride = (gridDim.x - (Tail::kActive ? 1 : 0)) * blockDim.x;
+    const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int i = i0; i - (int)threadIdx.x % 64 < gi.total; i += stride) {   // trip count uniform per wave
+        int cid = -1;
+        if (i < gi.total) {
+            const int mi = gi.map_of(i);
+            const int* dm = dims + 8 * mi;
+            if (dm[7]) {
+                cid = cell_of_checked(dm, gp.m[mi][i - gi.start(mi)]);
+                if (cid < 0) atomicOr(err, 1);
+            }
+        }
+        {
+            const int tt = cid >= 0 ? cid / kGridScanTile : -1;
+            u64 todo = __ballot(tt >= 0);
+            while (todo) {                                 // wave-uniform
+                const int leader = __ffsll((unsigned long long)todo) - 1;
+                const int c = __shfl(tt, leader, 64);
+                const u64 m = __ballot(tt == c) & todo;
+                if (lane_id() == leader) atomicAdd(&ttot[c], (u32)__popcll(m));
+                todo &= ~m;
+            }
+        }
+        if (!Agg) {
+            if (cid >= 0) slot[i] = atomicAdd(&cnt[cid], 1u);
+            continue;
+        }
+        u64 todo = __ballot(cid >= 0);
+        for (int it = 0; it < 4 && todo; ++it) {          // wave-uniform
+            const int leader = __ffsll((unsigned long long)todo) - 1;
+            const int c = __shfl(cid, leader, 64);
+            const u64 m = __ballot(cid == c) & todo;
+            u32 b = 0;
+            if (lane_id() == leader) b = atomicAdd(&cnt[c], (u32)__popcll(m));
+            b = (u32)__shfl((int)b, leader, 64);
+            if ((m >> lane_id()) & 1ull) slot[i] = b + (u32)__popcll(m & lanemask_lt());
+            todo &= ~m;
+        }
+        if ((todo >> lane_id()) & 1ull) slot[i] = atomicAdd(&cnt[cid], 1u);
+    }
+}
+
 inline GridBoundsArgs grid_bounds_args(GridGPU& g, const GridPtrs& gp) {
     return GridBoundsArgs{gp, g.bounds, g.arrive, g.dims, g.d_ncells, (long long)g.cell_cap, g.err};
 }
@@ -205,6 +274,11 @@ void grid_build(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s, bool
 // the first half of a build: bounds, per-cell counts (wave-aggregated) and cell_start; the caller
 // places the points itself (cell-major order, e.g. by a sort) and zeroes the counts it used
 void grid_count_scan(GridGPU& g, const GridPtrs& gp, PrimWork& w, hipStream_t s);
+
+// the second half of grid_build: the scan of the counts and the placement (after k_grid_count, which
+// a caller launches itself with its own tail on dims computed elsewhere)
+constexpr int kGridCountBlocks = 512;
+void grid_scan_scatter(GridGPU& g, const GridPtrs& gp, hipStream_t s);
 
 struct GridView {
     const int* dims;

@@ -192,6 +192,9 @@ struct OdomGPU {
     // (odom_update_done); graph B is captured per (slot, mpar)
     float4* mapset[2][kMaxC] = {};
     int mpar = 0;
+    // the map grid's dims of map_cur() were computed by the update that wrote it (k_rgm_finish), so
+    // the next update's grid build skips its bounds pass; false after any other map write
+    bool dims_fresh = false;
     float4* app[kMaxC] = {};       // this frame's transformed down-sampled points (appended)
     float4* seg_out = nullptr;
     u32 *keys = nullptr, *vals = nullptr;
@@ -203,7 +206,10 @@ struct OdomGPU {
     u64* rgm_key64 = nullptr;      // [sort_cap] voxel keys of every element, element order
     u32* rgm_vtag = nullptr;       // [sort_cap] element index | cropped << 31
     u32* rgm_bcount = nullptr;     // [kRgmBuckets] appended points per bucket (lists built by the LM)
-    int* rgm_bmeta = nullptr;      // [kRgmBuckets][8] each bucket's merged base, length, kept voxels per class
+    int* rgm_bmeta = nullptr;      // [kRgmBuckets][32] each bucket's merged base, length, kept voxels and
+                                   // kept-voxel cell bounds per class
+    int* dims_next = nullptr;      // [8 * kGridMaps + 1] the map grid dims and scan length of map_next(),
+                                   // written by k_rgm_finish (copied into the grid by the next build)
     u64* rgm_bkey = nullptr;       // [kRgmBuckets * kRgmBucketCap] the lists: keys, tags
     u32* rgm_btag = nullptr;
     float4* rgm_vox = nullptr;     // [sort_cap] voxel outputs at merged positions
@@ -265,6 +271,7 @@ void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s);
 void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s);
 // after an update has been enqueued (or its graph launched): the maps it wrote become the current ones
 inline void odom_update_done(OdomGPU& o) { o.mpar ^= 1; }
+inline bool odom_merge_mode(const OdomGPU& o) { return !o.tie_order && !o.rg_radix; }
 inline float4* const* map_cur(const OdomGPU& o) { return o.mapset[o.mpar]; }
 inline float4* const* map_next(const OdomGPU& o) { return o.mapset[o.mpar ^ 1]; }
 // stage B tail when map export is on: the maps and their sizes into the mapped pinned buffers

@@ -200,6 +200,22 @@ struct PredictTail {
     }
 };
 
+// the first kernel of an update whose grid dims k_rgm_finish computed (OdomGPU::dims_fresh): the
+// count reads dims_next; its tail workgroup copies them into the grid (read by the scan, the placement
+// and the kNN, all later kernels) and runs the pose prediction
+struct FreshTail {
+    static constexpr bool kActive = true;
+    PredictTail pred;
+    const int* dims_next;
+    int* dims;
+    int* d_ncells;
+    __device__ void operator()(int t) const {
+        if (t < 8 * kGridMaps) dims[t] = dims_next[t];
+        if (t == 8 * kGridMaps) *d_ncells = dims_next[t];
+        pred(t);
+    }
+};
+
 // voxel-grid stage set-up (stream A): reset the min/max accumulators, batch size
 __global__ void k_vg_begin(int* __restrict__ scnt, u32* __restrict__ acc, int nc) {
     const int t = threadIdx.x;
@@ -1895,13 +1911,30 @@ struct RgmArgs {
     u64* ktmp;
     u32* vtmp;
     int* stat;             // [8] (OdomGPU::rgm_stat)
-    int* bmeta;            // [kRgmBuckets][8]: merged base, length, kept voxels per class (-> k_rgm_finish)
+    int* bmeta;            // [kRgmBuckets][kRgmMeta]: merged base, length, kept voxels per class, and the
+                           // cell bounds of its kept voxels per class (min x y z, max x y z) (-> k_rgm_finish)
+    int* gdims;            // the next update's map grid: dims, scan length, error word (grid_dims)
+    int* gncells;
+    long long gcell_cap;
+    int* gerr;
     u32* bcount;           // the appended points' bucket lists (RgmPrep)
     const u64* bkey;
     const u32* btag;
     unsigned long long* dbg;   // development probe (PF_PROBE): [64 + 10 b + i] phase timestamps of bucket b
 };
 static_assert(64 + 10 * (kRgmBuckets + 1) <= kDbgWords, "probe words");
+constexpr int kRgmMeta = 32;                           // ints per bucket in bmeta
+constexpr int kRgmBnd = 8;                             // bmeta offset of the bounds
+
+// per-class cell bounds (the grid's 1 m cells, as k_grid_bounds computes them) in LDS
+__device__ __forceinline__ void rgm_bound_init(int (*bnd)[6], int t) {
+    if (t < 6 * kMaxC) bnd[t / 6][t % 6] = (t % 6) < 3 ? INT_MAX : INT_MIN;
+}
+__device__ __forceinline__ void rgm_bound_add(int (*bnd)[6], int c, float4 p) {
+    const int x = (int)floorf(p.x), y = (int)floorf(p.y), z = (int)floorf(p.z);
+    atomicMin(&bnd[c][0], x); atomicMin(&bnd[c][1], y); atomicMin(&bnd[c][2], z);
+    atomicMax(&bnd[c][3], x); atomicMax(&bnd[c][4], y); atomicMax(&bnd[c][5], z);
+}
 
 // one voxel of rgbds: the f32 centroid of its points in order and the maxima of r and g (:108-125),
 // then extractstablepoint (:12-14) and the ageing (:634-646)
@@ -2049,6 +2082,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
     __shared__ u64 s_nextk;
     __shared__ int s_cnt, s_before[kRgmThreads / 64], s_cls[kMaxC];
     __shared__ u32 s_w[kRgmThreads / 64];
+    __shared__ int s_bnd[kMaxC][6];
     const int t = threadIdx.x, b = blockIdx.x;
     const RgView<NC> V = rg_view<NC>(a.cnt, a.map, Clouds{{a.app.p[0], a.app.p[1], a.app.p[2]}});
     int M = 0;
@@ -2100,6 +2134,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         s_cnt = cnt_b;
     }
     if (t < kMaxC) s_cls[t] = 0;
+    rgm_bound_init(s_bnd, t);
     if (__any(unsorted) && lane_id() == 0) __hip_atomic_store(&a.stat[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int u = 0; u < kPerT; ++u) {
@@ -2187,6 +2222,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
                 if (v.finish(a.k_new, a.theta_p, a.theta_max, out)) {
                     flag = 1u | (u32)(K >> 62) << 30;
                     atomicAdd(&s_cls[(int)(K >> 62)], 1);
+                    rgm_bound_add(s_bnd, (int)(K >> 62), out);
                 }
                 a.vox[P] = out;
             }
@@ -2206,6 +2242,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
                 if (v.finish(a.k_new, a.theta_p, a.theta_max, out)) {
                     flag = 1u | (u32)(K >> 62) << 30;
                     atomicAdd(&s_cls[(int)(K >> 62)], 1);
+                    rgm_bound_add(s_bnd, (int)(K >> 62), out);
                 }
                 a.vox[P] = out;
             }
@@ -2228,13 +2265,14 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         run += tot;
     }
     RGM_MARK(5);
+    int* m = a.bmeta + kRgmMeta * b;
     if (t == 0) {
-        int* m = a.bmeta + 8 * b;
         m[0] = base;
         m[1] = L;
 #pragma unroll
         for (int c = 0; c < kMaxC; ++c) m[2 + c] = c < NC ? s_cls[c] : 0;
     }
+    if (t < 6 * NC) m[kRgmBnd + t] = s_bnd[t / 6][t % 6];
 }
 
 constexpr int kFbThreads = 256;
@@ -2389,6 +2427,8 @@ __device__ void rgm_fallback_tail(const RgmArgs& a, const RgView<NC>& V, int n) 
         }
         run += tot;
     }
+    __shared__ int s_bnd[kMaxC][6];
+    rgm_bound_init(s_bnd, t);
     __threadfence_block();
     __syncthreads();
     int low[kMaxC + 1];
@@ -2399,15 +2439,23 @@ __device__ void rgm_fallback_tail(const RgmArgs& a, const RgView<NC>& V, int n) 
     for (u32 r = t; r < run; r += kFbThreads) {
         const int c = min((int)a.kflag[r], NC - 1);
         const u32 idx = r - (u32)low[c];
-        if (idx < a.map_cap) a.mapw.at(c)[idx] = a.vox[r];
-        else over = true;
+        const float4 v = a.vox[r];
+        if (idx < a.map_cap) {
+            a.mapw.at(c)[idx] = v;
+            rgm_bound_add(s_bnd, c, v);
+        } else {
+            over = true;
+        }
     }
     if (over) atomicOr(a.err_map, 1);
+    __syncthreads();
     if (t == 0) {
         for (int c = 1; c <= kMaxC; ++c) a.cnt[C_NLT + c - 1] = low[c];
-        for (int c = 0; c < NC; ++c) a.cnt[C_M + c] = min(s_cls[c], (int)a.map_cap);
+        int nloc[kGridMaps] = {0, 0, 0};
+        for (int c = 0; c < NC; ++c) a.cnt[C_M + c] = nloc[c] = min(s_cls[c], (int)a.map_cap);
         a.cnt[C_KEEP_TOTAL] = low[kMaxC];
         a.cnt[C_NRG] = n;
+        grid_dims(&s_bnd[0][0], nloc, a.gdims, a.gncells, a.gcell_cap, a.gerr);   // the next update's grid
     }
 }
 
@@ -2420,6 +2468,7 @@ template <int NC>
 __global__ void __launch_bounds__(kFbThreads) k_rgm_finish(RgmArgs a) {
     const int b = blockIdx.x, t = threadIdx.x;
     __shared__ int s_red[kFbThreads / 64][kMaxC];
+    __shared__ int s_red6[kFbThreads / 64][6 * kMaxC];
     __shared__ int s_pre[kMaxC], s_tot[kMaxC];
     const bool fb = a.stat[0] != 0;
     if (fb) {
@@ -2446,7 +2495,7 @@ __global__ void __launch_bounds__(kFbThreads) k_rgm_finish(RgmArgs a) {
     // the kept class-c voxels of the buckets before b (and of all buckets, for workgroup 0)
     int pre[kMaxC] = {0, 0, 0}, all[kMaxC] = {0, 0, 0};
     for (int bb = t; bb < kRgmBuckets; bb += kFbThreads) {
-        const int* m = a.bmeta + 8 * bb;
+        const int* m = a.bmeta + kRgmMeta * bb;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             const int v = m[2 + c];
@@ -2479,7 +2528,7 @@ __global__ void __launch_bounds__(kFbThreads) k_rgm_finish(RgmArgs a) {
         s_tot[t] = v;
     }
     __syncthreads();
-    const int* m = a.bmeta + 8 * b;
+    const int* m = a.bmeta + kRgmMeta * b;
     const int base = m[0], L = m[1];
     u32 first_rank[kMaxC];                             // bucket-local rank of the first voxel of class c
     {
@@ -2501,6 +2550,30 @@ __global__ void __launch_bounds__(kFbThreads) k_rgm_finish(RgmArgs a) {
         else over = true;
     }
     if (over) atomicOr(a.err_map, 1);
+    __shared__ int s_bnd[kMaxC][6];
+    if (b == 0) {                                      // the map grid's bounds: over every bucket's
+        int v[6 * kMaxC];
+#pragma unroll
+        for (int k = 0; k < 6 * kMaxC; ++k) v[k] = (k % 6) < 3 ? INT_MAX : INT_MIN;
+        for (int bb = t; bb < kRgmBuckets; bb += kFbThreads) {
+            const int* mb = a.bmeta + kRgmMeta * bb + kRgmBnd;
+#pragma unroll
+            for (int k = 0; k < 6 * NC; ++k) v[k] = (k % 6) < 3 ? min(v[k], mb[k]) : max(v[k], mb[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 6 * NC; ++k) {
+            v[k] = (k % 6) < 3 ? wave_min_i(v[k]) : wave_max_i(v[k]);
+            if (lane_id() == 0) s_red6[t >> 6][k] = v[k];
+        }
+        __syncthreads();
+        if (t < 6 * kMaxC) {
+            int r = (t % 6) < 3 ? INT_MAX : INT_MIN;
+            if (t < 6 * NC)
+                for (int w = 0; w < kFbThreads / 64; ++w) r = (t % 6) < 3 ? min(r, s_red6[w][t]) : max(r, s_red6[w][t]);
+            s_bnd[t / 6][t % 6] = r;
+        }
+        __syncthreads();
+    }
     if (t == 0) {
         a.bcount[b] = 0u;                              // the list of the next update
         if (b == 0) {
@@ -2513,10 +2586,12 @@ __global__ void __launch_bounds__(kFbThreads) k_rgm_finish(RgmArgs a) {
                 tot += c - 1 < NC ? s_tot[c - 1] : 0;
                 a.cnt[C_NLT + c - 1] = tot;
             }
-            for (int c = 0; c < NC; ++c) a.cnt[C_M + c] = min(s_tot[c], (int)a.map_cap);
+            int nloc[kGridMaps] = {0, 0, 0};
+            for (int c = 0; c < NC; ++c) a.cnt[C_M + c] = nloc[c] = min(s_tot[c], (int)a.map_cap);
             a.cnt[C_KEEP_TOTAL] = tot;
             a.cnt[C_NRG] = n;
             if (n - M > a.stat[2]) a.stat[2] = n - M;
+            grid_dims(&s_bnd[0][0], nloc, a.gdims, a.gncells, a.gcell_cap, a.gerr);   // the next update's grid
         }
     }
 }
@@ -2684,7 +2759,8 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     PF_ALLOC(o.rgm_ktmp, sizeof(u64) * o.sort_cap);
     PF_ALLOC(o.rgm_vtmp, sizeof(u32) * o.sort_cap);
     PF_ALLOC(o.rgm_bcount, sizeof(u32) * kRgmBuckets);
-    PF_ALLOC(o.rgm_bmeta, sizeof(int) * 8 * kRgmBuckets);
+    PF_ALLOC(o.rgm_bmeta, sizeof(int) * kRgmMeta * kRgmBuckets);
+    PF_ALLOC(o.dims_next, sizeof(int) * (8 * kGridMaps + 1));
     PF_ALLOC(o.rgm_bkey, sizeof(u64) * kRgmBuckets * kRgmBucketCap);
     PF_ALLOC(o.rgm_btag, sizeof(u32) * kRgmBuckets * kRgmBucketCap);
     PF_ALLOC(o.rgm_vox, sizeof(float4) * o.sort_cap);
@@ -2758,6 +2834,7 @@ int odom_reset(OdomGPU& o) {
     if (hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
     o.opt_count_host = 2;
     o.inited = false;
+    o.dims_fresh = false;
     o.frames = 0;
     o.err_seen = 0;
     o.rd_frames = -1;
@@ -2802,8 +2879,7 @@ void odom_destroy(OdomGPU& o) {
                     o.keys, o.vals, o.tail_status, o.nbr, o.qflag, o.lm_part, o.lm_ticket, o.geo,
                     o.spars, o.roundv, o.observe, o.pnext, o.pbkt, o.tailinc, o.poses, o.stage, o.dbg, o.errw,
                     o.rgm_okey, o.rgm_key64, o.rgm_vtag, o.rgm_kout, o.rgm_ktmp, o.rgm_vox, o.rgm_kflag, o.rgm_bcount, o.rgm_bmeta, o.rgm_bkey,
-                    o.rgm_btag,
-                    o.rgm_vtmp, o.rgm_stat};
+                    o.rgm_btag, o.rgm_vtmp, o.rgm_stat, o.dims_next};
     for (void* q : ptrs) (void)hipFree(q);
     if (o.h_cnt) (void)hipHostFree(o.h_cnt);
     if (o.h_pose) (void)hipHostFree(o.h_pose);
@@ -2879,6 +2955,7 @@ void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, o.st, o.poses, (int)o.pose_cap, 0, o.acc);
     o.opt_count_host = 12;
     o.inited = true;
+    o.dims_fresh = false;
 }
 
 void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
@@ -2892,9 +2969,17 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     // grids of the class maps (kd-tree builds, :249-250 / BPF :723-725); the pose prediction rides on
     // the bounds kernel as its tail (it reads the map sizes of the previous frame, not the grid)
     GridPtrs gp{{map_cur(o)[0], map_cur(o)[1], map_cur(o)[2]}, {cnt + C_M, cnt + C_M + 1, cnt + C_M + 2}, nc};
-    hipLaunchKernelGGL(k_grid_bounds<PredictTail>, dim3(kGridBoundsBlocks + 1), dim3(256), 0, s,
-                       grid_bounds_args(o.grid, gp), PredictTail{o.st, cnt, sb.cnt, o.acc, o.cls});
-    grid_build(o.grid, gp, o.prim, s, true);
+    const PredictTail pred{o.st, cnt, sb.cnt, o.acc, o.cls};
+    if (o.dims_fresh) {                       // dims from the previous update's k_rgm_finish: the count first
+        hipLaunchKernelGGL((k_grid_count<false, FreshTail>), dim3(kGridCountBlocks + 1), dim3(256), 0, s, gp,
+                           o.dims_next, o.grid.cell_count, o.grid.slot, o.grid.ttot, o.grid.err,
+                           FreshTail{pred, o.dims_next, o.grid.dims, o.grid.d_ncells});
+        grid_scan_scatter(o.grid, gp, s);
+    } else {
+        hipLaunchKernelGGL(k_grid_bounds<PredictTail>, dim3(kGridBoundsBlocks + 1), dim3(256), 0, s,
+                           grid_bounds_args(o.grid, gp), pred);
+        grid_build(o.grid, gp, o.prim, s, true);
+    }
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
         AssocArgs aa{o.st, cnt, o.acc, gv, o.cls, clouds(sb.ds), clouds(map_cur(o)), o.nbr, o.qflag, o.geo, o.spars,
@@ -2919,11 +3004,15 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
         RgmArgs ra{o.st, cnt, o.acc, clouds(map_cur(o)), clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap,
                    leaf, o.prm.k_new, o.prm.theta_p, o.prm.theta_max, o.rgm_okey, o.rgm_key64, o.rgm_vtag,
                    o.rgm_vox, o.rgm_kflag, clouds_w(map_next(o)), (u32)o.map_cap, o.errw + E_MAP, o.rgm_kout, o.vals, o.rgm_ktmp, o.rgm_vtmp,
-                   o.rgm_stat, o.rgm_bmeta, o.rgm_bcount, o.rgm_bkey, o.rgm_btag, o.dbg};
+                   o.rgm_stat, o.rgm_bmeta, o.dims_next, o.dims_next + 8 * kGridMaps, (long long)o.grid.cell_cap,
+                   o.grid.err,
+                   o.rgm_bcount, o.rgm_bkey, o.rgm_btag, o.dbg};
         PF_LAUNCH_NC(nc, k_rgm_bucket, dim3(kRgmBuckets + 1), dim3(kRgmThreads), 0, s, ra);
         PF_LAUNCH_NC(nc, k_rgm_finish, dim3(kRgmBuckets), dim3(kFbThreads), 0, s, ra);
+        o.dims_fresh = true;
         return;
     }
+    o.dims_fresh = false;
     if (rg_fused_keys(o.leaf_rg, nc)) {
         PF_LAUNCH_NC(nc, k_rg_append_keys, dim3(kGrid + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(map_cur(o)),
                      clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap, leaf, o.keys, o.vals,
