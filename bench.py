@@ -52,6 +52,9 @@ def parse(argv=None):
     ap.add_argument("--no-roofline", action="store_true", help="skip the kNN roofline leg")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph-mode", type=int, default=4,
+                    help="pf_odom_set_graph: bit 0 stage A, bit 1 stage B, 4 = auto (the default: stage A, and "
+                         "stage B when the process holds several handles)")
     ap.add_argument("--sequences", default="one", choices=["one", "kitti11"],
                     help="one: an independent sequence per rank (weak scaling, the default); kitti11: "
                          "configs[3], KITTI 00-10 LPT-assigned to the ranks (strong scaling)")
@@ -166,6 +169,14 @@ def load_frames(seq_id, total, threads, preset="S64"):
         nf = min(chunk, total - f0)
         buf, counts = seq.frames(f0, nf, threads=threads)
         yield f0, buf, counts, "synthetic %s seed %d" % (preset, rank)
+
+
+GRAPH_NAMES = {0: "none", 1: "stage A", 2: "stage B", 3: "stages A and B", 4: "auto"}
+
+
+def graph_mode(args):
+    """pf_odom_set_graph mode: --no-graph = eager launches in both stages"""
+    return 0 if args.no_graph else args.graph_mode
 
 
 def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier, keep_host=False):
@@ -897,7 +908,7 @@ def main(argv=None):
     if stub:
         r = stub_run(rank, args.steps)
     else:
-        r = run_gpu(rank, local_rank, world, args.steps, args.warmup, threads, not args.no_graph, barrier,
+        r = run_gpu(rank, local_rank, world, args.steps, args.warmup, threads, graph_mode(args), barrier,
                     keep_host=host_legs)
     elapsed, frames = r["elapsed"], r["frames"]
     if dist is not None:
@@ -927,14 +938,14 @@ def main(argv=None):
                    "sequence": r["data"], "frames_per_rank": frames,
                    "mean_points_per_frame": round(r["mean_points"], 1),
                    "parallelism": "one independent sequence per GPU" if world > 1 else "single sequence",
-                   "graph": not args.no_graph},
+                   "graph": GRAPH_NAMES[graph_mode(args)]},
     }
     log("pipeline: %d frames in %.3f s (host enqueue %.3f s), last-frame stats %s"
         % (frames, elapsed, r.get("enqueue", 0.0), r["stats"]))
     if "enqueue" in r:
         out["config"]["host_enqueue_us_per_frame"] = round(r["enqueue"] / max(1, frames) * 1e6, 1)
     if world == 1 and not stub:
-        out["stage_us"] = stage_pass(local_rank, r["ptrs"], args.warmup, min(1000, frames), not args.no_graph)
+        out["stage_us"] = stage_pass(local_rank, r["ptrs"], args.warmup, min(1000, frames), graph_mode(args))
     if stub:
         out["stub"] = True
     elif world == 1 and not args.no_roofline:
@@ -947,7 +958,7 @@ def main(argv=None):
         for name, dc in (("bpf", False), ("bpf_dcvc", True)):
             try:
                 out[name] = bpf_leg(local_rank, args.bpf_frames, threads, with_cpu=not args.no_cpu,
-                                    use_graph=not args.no_graph, dcvc=dc)
+                                    use_graph=graph_mode(args), dcvc=dc)
             except Exception as e:  # report, never hide
                 log("%s leg failed: %r" % (name, e))
                 out[name] = None
@@ -955,12 +966,12 @@ def main(argv=None):
         for name in ES_LEGS:
             try:
                 out[name] = es_leg(name, local_rank, args.leg_frames, threads, args.leg_cpu_seconds,
-                                   use_graph=not args.no_graph, with_cpu=not args.no_cpu)
+                                   use_graph=graph_mode(args), with_cpu=not args.no_cpu)
             except Exception as e:  # report, never hide
                 log("%s leg failed: %r" % (name, e))
                 out[name] = None
     if host_legs and not args.no_pcie:
-        pc = pcie_leg(local_rank, r["hptrs"], args.warmup, not args.no_graph)
+        pc = pcie_leg(local_rank, r["hptrs"], args.warmup, graph_mode(args))
         pp = pc.pop("poses")
         pc["ratio_to_value"] = round(pc["value"] / value, 4)
         pc["poses_equal_headline"] = bool(np.array_equal(pp, r["poses"]))
@@ -974,18 +985,18 @@ def main(argv=None):
         log("node_pattern: %s" % nd)
     if world == 1 and not stub and args.configs4_frames > 0:
         try:
-            out["configs4"] = configs4_leg(local_rank, args.configs4_frames, threads, use_graph=not args.no_graph)
+            out["configs4"] = configs4_leg(local_rank, args.configs4_frames, threads, use_graph=graph_mode(args))
             log("configs4: %s" % out["configs4"])
         except Exception as e:  # report, never hide
             log("configs4 leg failed: %r" % (e,))
             out["configs4"] = None
     if world == 1 and not stub and args.pageable_frames > 0:
-        out["pcie_pageable"] = pageable_leg(local_rank, args.pageable_frames, threads, use_graph=not args.no_graph)
+        out["pcie_pageable"] = pageable_leg(local_rank, args.pageable_frames, threads, use_graph=graph_mode(args))
     if world == 1 and not args.no_cpu and not stub:
         cb = cpu_baseline(args.cpu_seconds, args.warmup)
         f0, f1 = cb.pop("frames")
         # the GPU on exactly the CPU sample's frames, for a like-for-like ratio
-        gw = gpu_window(local_rank, f0, f1, threads, not args.no_graph)
+        gw = gpu_window(local_rank, f0, f1, threads, graph_mode(args))
         cb["gpu_same_frames"] = gw
         cb["speedup_same_frames"] = round(gw["value"] / cb["value"], 2)
         out["cpu_baseline"] = cb
@@ -1001,7 +1012,7 @@ def main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev="cud
         r = dict(elapsed=1.0 + rank, frames=sum(KITTI_SEQ_FRAMES[sq] for sq in mine),
                  sequences=["%02d" % sq for sq in mine])
     else:
-        r = run_kitti11(rank, local_rank, world, args.warmup, threads, not args.no_graph, barrier, args.concurrent)
+        r = run_kitti11(rank, local_rank, world, args.warmup, threads, graph_mode(args), barrier, args.concurrent)
     elapsed, frames = r["elapsed"], r["frames"]
     if dist is not None:
         import torch
@@ -1021,7 +1032,7 @@ def main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev="cud
                                       "by sequence) as independent streams, LPT-assigned to the GPUs",
                           "assignment": lpt_assign(KITTI_SEQ_FRAMES, world), "rank0_sequences": r["sequences"],
                           "parallelism": "sequences over GPUs", "concurrent_per_gpu": args.concurrent,
-                          "graph": not args.no_graph}}
+                          "graph": GRAPH_NAMES[graph_mode(args)]}}
         if stub:
             out["stub"] = True
         print(json.dumps(out), flush=True)

@@ -295,8 +295,19 @@ int pf_odom_restore(pf_odom* h, const void* buf, size_t size);
  * laserCloudCornerMap / laserCloudSurfMap (or the BPF maps) after every update. */
 int pf_odom_set_map_export(pf_odom* h, int enable);
 int pf_odom_map_export(pf_odom* h, int which, const float** xyzw, size_t* n);
-/* enable/disable hipGraph replay of the steady-state frame (default on) */
-int pf_odom_set_graph(pf_odom* h, int enable);
+/* hipGraph replay of the steady-state frame, per stage: a bit mask of PF_GRAPH_STAGE_A (the front
+ * end / VoxelGrid stage) and PF_GRAPH_STAGE_B (the odometry stage), 0 = eager launches, or
+ * PF_GRAPH_AUTO (the default): stage A replays its graph; stage B launches eagerly while this is the
+ * process's only handle and replays its graph when several handles share the host's launch path.
+ * Measured on MI355X (configs[1], 4521 frames): a graph replay costs about 0.4 us more per kernel
+ * boundary than eager launches (tools/mb/graph_gap.hip) and stage B is the critical path, so one
+ * sequence runs 4525-4557 frames/s with stage B eager against 4404-4452 with both graphs; four
+ * concurrent handles (configs[3]) run 6558 frames/s with both graphs against 5459 with stage B
+ * eager (their host threads contend on the launch path). */
+#define PF_GRAPH_STAGE_A 1
+#define PF_GRAPH_STAGE_B 2
+#define PF_GRAPH_AUTO 4
+int pf_odom_set_graph(pf_odom* h, int mode);
 /* Reference tie order (default off): VoxelGrid (stage A) and rgbds (stage B) order the points of a
  * voxel as libstdc++'s std::sort leaves them -- the reference's own sorts (PCL 1.10 VoxelGrid, SURVEY
  * B.1; src/odomEstimationClass.cpp:74), which are not stable -- instead of in input order, so that every

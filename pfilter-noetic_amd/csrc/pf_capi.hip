@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -124,6 +125,7 @@ struct StageTiming {
 struct pf_odom {
     OdomGPU o;
     StageTiming* timing = nullptr;
+    bool counted = false;      // in g_live_handles
 };
 
 static int timing_harvest(StageTiming& t, int j) {
@@ -255,6 +257,10 @@ int pf_fe_set_ring_model(pf_fe* h, double top_deg, double bottom_deg) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// live handles of the process (PF_GRAPH_AUTO: stage B replays its graph when several handles share
+// the host's launch path)
+static std::atomic<int> g_live_handles{0};
+
 static int create(const pf_lidar_params* lidar, const pf_odom_params* params, int device, size_t max_points,
                   size_t map_capacity, int nc, pf_odom** out) {
     if (!lidar || !params || !out) return PF_EINVAL;
@@ -271,6 +277,8 @@ static int create(const pf_lidar_params* lidar, const pf_odom_params* params, in
         pf_odom_destroy(h);
         return rc;
     }
+    h->counted = true;
+    g_live_handles.fetch_add(1);
     *out = h;
     return PF_OK;
 }
@@ -297,6 +305,7 @@ int pf_odom_destroy(pf_odom* h) {
     timing_free(h);
     host_prof_report();
     odom_destroy(h->o);
+    if (h->counted) g_live_handles.fetch_sub(1);
     delete h;
     return PF_OK;
 }
@@ -697,9 +706,15 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
     const int nc = o.cls.nc;
     const bool scan = nc == 3 && !cl;
     const int p = o.frames % kSlots;
-    // (graph B of the merge path starts from the grid dims of the previous update: a frame after a
-    // host map write runs eagerly)
-    const bool steady = o.inited && o.opt_count_host <= 2 && o.graph_enabled && (o.dims_fresh || !odom_merge_mode(o));
+    // steady state: each stage replays its graph when its bit of the graph mode is set (graph B of the
+    // merge path starts from the grid dims of the previous update: a frame after a host map write runs
+    // eagerly)
+    const bool steady = o.inited && o.opt_count_host <= 2;
+    const int gm = o.graph_mode != PF_GRAPH_AUTO
+                       ? o.graph_mode
+                       : PF_GRAPH_STAGE_A | (g_live_handles.load(std::memory_order_relaxed) > 1 ? PF_GRAPH_STAGE_B : 0);
+    const bool steady_a = steady && (gm & PF_GRAPH_STAGE_A);
+    const bool steady_b = steady && (gm & PF_GRAPH_STAGE_B) && (o.dims_fresh || !odom_merge_mode(o));
     if (scan && n > o.in_cap) return PF_ECAPACITY;
     int rc = 0;
     PF_HT(0, rc = stage_a_begin(h, p));
@@ -717,7 +732,7 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
             hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, o.sb[p].cnt + C_IN + c, (int)ncl[c]);
         }
     }
-    if (steady) {
+    if (steady_a) {
         hipGraphExec_t& ga = scan ? o.graph_as[p] : o.graph_a[p];
         if (!ga) {
             rc = capture(o.stream_a, &ga, o, p, true, scan);
@@ -733,7 +748,7 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
     if (!rc) PF_HT(4, rc = stage_a_end_b_begin(h, p));
     if (!rc) rc = timing_mark(h, 2);
     if (rc) return rc;
-    if (steady) {
+    if (steady_b) {
         hipGraphExec_t& gb = o.graph_b[p + kSlots * o.mpar];
         if (!gb) {
             rc = capture(o.stream, &gb, o, p, false);
@@ -1273,9 +1288,9 @@ int pf_odom_merge_stats(pf_odom* h, int* full_sorts, int* max_appended) {
     return PF_OK;
 }
 
-int pf_odom_set_graph(pf_odom* h, int enable) {
-    if (!h) return PF_EINVAL;
-    h->o.graph_enabled = enable != 0;
+int pf_odom_set_graph(pf_odom* h, int mode) {
+    if (!h || mode < 0 || mode > PF_GRAPH_AUTO) return PF_EINVAL;
+    h->o.graph_mode = mode;
     return PF_OK;
 }
 

@@ -235,7 +235,7 @@ struct OdomGPU {
     double* poses = nullptr;       // [pose_cap * 7]
     float4* stage = nullptr;       // [kMaxC * in_cap] staging target of the frame entry points
 
-    bool graph_enabled = true;
+    int graph_mode = PF_GRAPH_AUTO;      // pf_odom_set_graph
     int cu_reserve = 0;            // CUs stage A stays off (odom_stage_a_stream)
     // reference tie order (pf_odom_set_tie_order, pf_tie.h): VoxelGrid (stage A) and rgbds (stage B)
     // order equal keys as libstdc++'s std::sort does; each stage has its own scratch

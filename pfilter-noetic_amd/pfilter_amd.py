@@ -480,8 +480,11 @@ class Odom_ES_EstimationClass:
         _check("pf_odom_poses", lib().pf_odom_poses(self._h, out.ctypes.data, n.value, ctypes.byref(n)))
         return out[:n.value].copy()
 
-    def set_graph(self, enable):
-        _check("pf_odom_set_graph", lib().pf_odom_set_graph(self._h, int(bool(enable))))
+    def set_graph(self, mode):
+        """hipGraph replay per stage (pf_odom_set_graph): 1 = stage A, 2 = stage B, 3 = both, 0 / False
+        = eager launches, 4 / True = PF_GRAPH_AUTO (the default: stage A, and stage B when the process
+        holds several handles)"""
+        _check("pf_odom_set_graph", lib().pf_odom_set_graph(self._h, 4 if mode is True else int(mode)))
 
     def set_stage_timing(self, enable):
         _check("pf_odom_set_stage_timing", lib().pf_odom_set_stage_timing(self._h, int(bool(enable))))

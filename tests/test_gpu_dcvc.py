@@ -128,7 +128,7 @@ def test_bpf_scan_pipeline_with_curvedfilter(pa, pfsynth):
     db = pa.DeviceBuffer(buf.nbytes)
     db.upload(buf)
     out = []
-    for graph in (True, False):
+    for graph in (3, 0):
         od = pa.Odom_BPF_EstimationClass(device=0)
         od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
         od.set_graph(graph)

@@ -196,14 +196,15 @@ def test_update_api_matches_oracle(pa, pfref, pfsynth):
 
 
 def test_device_pipeline_graph_equals_eager(pa, pfsynth):
-    """hipGraph replay of the steady-state frame gives the same bits as eager launches."""
+    """hipGraph replay of the steady-state frame gives the same bits as eager launches, for every
+    graph mode (pf_odom_set_graph: stage A, stage B, both)."""
     seq = pfsynth.Sequence("S64", n_frames=30, az_steps=1500)
     buf, counts = seq.frames(0, 30)
     db = pa.DeviceBuffer(buf.nbytes)
     db.upload(buf)
     stride = buf.shape[1] * 16
     res = []
-    for graph in (True, False):
+    for graph in (3, 1, 2, 0):
         od = pa.Odom_ES_EstimationClass(device=0)
         od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
         od.set_graph(graph)
@@ -211,9 +212,10 @@ def test_device_pipeline_graph_equals_eager(pa, pfsynth):
             od.frame_device(db.ptr + k * stride, counts[k])
         od.sync()
         res.append((od.poses(), od.laserCloudSurfMap))
-    np.testing.assert_array_equal(res[0][0], res[1][0])
-    np.testing.assert_array_equal(res[0][1][0], res[1][1][0])
-    np.testing.assert_array_equal(res[0][1][1], res[1][1][1])
+    for r in res[:-1]:
+        np.testing.assert_array_equal(r[0], res[-1][0])
+        np.testing.assert_array_equal(r[1][0], res[-1][1][0])
+        np.testing.assert_array_equal(r[1][1], res[-1][1][1])
 
 
 def test_map_too_small_warning(pa, pfref):

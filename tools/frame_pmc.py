@@ -15,7 +15,7 @@ import re
 from collections import defaultdict
 
 # every kernel of the frame path: stage A (featureExtraction + VoxelGrid) and stage B (odometry)
-STAGE_B = ["k_grid_bounds", "k_grid_count", "k_scan1", "k_grid_scatter", "k_assoc", "k_observe", "k_lm_solve",
+STAGE_B = ["k_grid_bounds", "k_grid_count", "k_grid_scan", "k_grid_scatter", "k_assoc", "k_observe", "k_lm_solve",
            "k_rgm_bucket", "k_rgm_finish", "k_rg_append_keys", "k_rg_tail", "k_rg_write"]
 
 
