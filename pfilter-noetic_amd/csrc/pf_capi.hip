@@ -1206,6 +1206,18 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
 
 // development / test switch (not part of include/pfilter_hip.h): rgbds in the default order by the
 // full radix sort of every element (the path before the merge) instead of the merge, for A/B checks
+// development: the separate k_observe launch at weightType 0 too (the path before the fused observe)
+extern "C" int pf_dev_set_fuse_observe(pf_odom* h, int enable) {
+    if (!h) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    if ((enable == 0) != o.no_fuse_obs) drop_graphs_b(o);
+    o.no_fuse_obs = enable == 0;
+    return PF_OK;
+}
+
 extern "C" int pf_dev_set_rg_radix(pf_odom* h, int enable) {
     if (!h) return PF_EINVAL;
     OdomGPU& o = h->o;

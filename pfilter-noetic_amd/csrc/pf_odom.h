@@ -97,7 +97,7 @@ struct LMState {
 };
 
 constexpr int kDbgWords = 8192;   // development probe buffer (PF_PROBE): LM [0, 64), rgbds buckets after
-constexpr int kLmParts = 30;   // cost, g[6], H[21], bad_r, bad_J
+constexpr int kLmParts = 31;   // cost, g[6], H[21], bad_r, bad_J, kept rows
 constexpr int kLmEvalSlots = 8; // LM claim masks per solve (>= evaluations per solve)
 constexpr int kLmEvals = 5;      // evaluations per solve: 1 + max_num_iterations (4)
 constexpr int kLmBlocks = 32;    // LM workgroups = residual chunks per evaluation
@@ -195,6 +195,7 @@ struct OdomGPU {
     // the map grid's dims of map_cur() were computed by the update that wrote it (k_rgm_finish), so
     // the next update's grid build skips its bounds pass; false after any other map write
     bool dims_fresh = false;
+    bool no_fuse_obs = false;      // development (pf_dev_set_fuse_observe): k_observe even at weightType 0
     float4* app[kMaxC] = {};       // this frame's transformed down-sampled points (appended)
     float4* seg_out = nullptr;
     u32 *keys = nullptr, *vals = nullptr;

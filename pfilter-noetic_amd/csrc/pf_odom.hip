@@ -618,6 +618,99 @@ struct ObsArgs {
     int* err;              // sticky error word E_LM
 };
 
+// observeMean / the skip test of one query (:332-356, :480-505), reads only: its pairs' ranks in their
+// map points' p-index buckets, the observe value and the skip decision (applied by observe_commit)
+struct ObsRes {
+    int f;                 // qflag: bit 0 valid association
+    int c;
+    bool skip;
+    float observe, round;
+    u32 tinc[5];           // p-index increments carried by the query's pairs (k_lm_solve applies them)
+};
+template <int NC>
+__device__ __forceinline__ void observe_eval(const ObsArgs& a, const CatIdx<NC>& qi, int nq, int q, ObsRes& r) {
+    r.f = a.qflag[q];
+    r.c = 0;
+    r.skip = true;
+    r.observe = r.round = 0.f;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) r.tinc[j] = 0u;
+    if (!(r.f & 1)) return;
+    const int c = qi.cls(q);
+    r.c = c;
+    const float4* mp = a.map.at(c);
+    // c_i(n) = valid queries before q sharing neighbour n: count the smaller pair ids in n's bucket
+    // (filled in any order by k_assoc: two pairs inline, the rest on an overflow list); the pair
+    // with the largest id carries n's increment
+    int nb[5], cur[5], rank[5], len[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) nb[j] = a.nbr[5 * q + j];
+    int4 bk[5][kBktQuads];                               // every bucket read at once
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+        for (int k = 0; k < kBktQuads; ++k) bk[j][k] = a.pbkt[(size_t)kBktQuads * ((u32)c * a.map_cap + (u32)nb[j]) + k];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const int p = 5 * q + j;
+        const int* w = reinterpret_cast<const int*>(bk[j]);
+        len[j] = w[0];
+        rank[j] = 0;
+#pragma unroll
+        for (int k = 0; k < kBktInline; ++k) rank[j] += (w[0] > k && w[1 + k] < p) ? 1 : 0;
+        cur[j] = w[0] > kBktInline ? w[kBktHead] : -1;
+#ifdef PF_DEV_NOCHAIN
+        cur[j] = -1;                                     // development: time without the list walks
+#endif
+    }
+    for (int step = 0;; ++step) {
+        bool more = false;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            if (cur[j] < 0) continue;
+            rank[j] += cur[j] < 5 * q + j ? 1 : 0;
+            cur[j] = a.pnext[cur[j]];
+            more |= cur[j] >= 0;
+        }
+        if (!more) break;
+        if (step > 5 * nq) { a.cnt[C_ERR] = 1; atomicOr(a.err, 2); break; }   // a list longer than every pair: corrupt
+    }
+    int gs = 0;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const u32 g0 = w_g(mp[nb[j]]);
+        gs += min(255u, g0 + (u32)rank[j]);
+        r.tinc[j] = rank[j] == len[j] - 1 ? (u32)len[j] : 0u;
+    }
+    float observe = gs / 5.0 + 1;                        // :332-338 / :480-486
+    const float round = a.roundv[q];
+    if (observe / round > 5) observe = 255;              // :348-349
+    r.skip = observe < round * a.theta_p && round > a.k_new && observe < a.theta_max;   // :350-353
+    r.observe = observe;
+    r.round = round;
+}
+// the query's outputs: pair increments, and for a kept residual the kept bit, observe and the r / g
+// bytes of its down-sampled point (:354-355). shared: the kept bit and the r / g word are read by other
+// workgroups of the same launch (k_lm_solve with the observe pass fused), so they are written through
+// (agent-scope atomic stores)
+template <int NC>
+__device__ __forceinline__ void observe_commit(const ObsArgs& a, const CatIdx<NC>& qi, int q, const ObsRes& r,
+                                               bool shared) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) a.tailinc[5 * q + j] = r.tinc[j];
+    if (!(r.f & 1) || r.skip) return;
+    const u32 rq = (u32)min(255, int(r.round)), gq = (u32)min(255, int(r.observe));
+    float* wp = &a.ds.at(r.c)[q - qi.start(r.c)].w;
+    a.observe[q] = r.observe;
+    if (shared) {
+        __hip_atomic_store(&a.qflag[q], r.f | 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<u32*>(wp), pack_rg(rq, gq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        a.qflag[q] = r.f | 2;
+        *wp = __uint_as_float(pack_rg(rq, gq));
+    }
+}
+
 template <int NC>
 __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
     const CatIdx<NC> qi = cat_idx<NC>(a.cnt + C_DS);
@@ -632,68 +725,14 @@ __global__ void __launch_bounds__(256) k_observe(ObsArgs a) {
         nvalid[c] = nkept[c] = 0;
     }
     for (int q = blockIdx.x * blockDim.x + t; q < nq; q += gridDim.x * blockDim.x) {
-        int f = a.qflag[q];
-        if (!(f & 1)) {
-#pragma unroll
-            for (int j = 0; j < 5; ++j) a.tailinc[5 * q + j] = 0u;
-            continue;
-        }
-        const int c = qi.cls(q);
-        const float4* mp = a.map.at(c);
-        // c_i(n) = valid queries before q sharing neighbour n: count the smaller pair ids in n's bucket
-        // (filled in any order by k_assoc: two pairs inline, the rest on an overflow list); the pair
-        // with the largest id carries n's increment
-        int nb[5], cur[5], rank[5], len[5];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) nb[j] = a.nbr[5 * q + j];
-        int4 bk[5][kBktQuads];                               // every bucket read at once
-#pragma unroll
-        for (int j = 0; j < 5; ++j)
-#pragma unroll
-            for (int k = 0; k < kBktQuads; ++k) bk[j][k] = a.pbkt[(size_t)kBktQuads * ((u32)c * a.map_cap + (u32)nb[j]) + k];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const int p = 5 * q + j;
-            const int* w = reinterpret_cast<const int*>(bk[j]);
-            len[j] = w[0];
-            rank[j] = 0;
-#pragma unroll
-            for (int k = 0; k < kBktInline; ++k) rank[j] += (w[0] > k && w[1 + k] < p) ? 1 : 0;
-            cur[j] = w[0] > kBktInline ? w[kBktHead] : -1;
-#ifdef PF_DEV_NOCHAIN
-            cur[j] = -1;                                     // development: time without the list walks
-#endif
-        }
-        for (int step = 0;; ++step) {
-            bool more = false;
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                if (cur[j] < 0) continue;
-                rank[j] += cur[j] < 5 * q + j ? 1 : 0;
-                cur[j] = a.pnext[cur[j]];
-                more |= cur[j] >= 0;
-            }
-            if (!more) break;
-            if (step > 5 * nq) { a.cnt[C_ERR] = 1; atomicOr(a.err, 2); break; }   // a list longer than every pair: corrupt
-        }
-        int gs = 0;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const u32 g0 = w_g(mp[nb[j]]);
-            gs += min(255u, g0 + (u32)rank[j]);
-            a.tailinc[5 * q + j] = rank[j] == len[j] - 1 ? (u32)len[j] : 0u;
-        }
-        float observe = gs / 5.0 + 1;                        // :332-338 / :480-486
-        const float round = a.roundv[q];
-        if (observe / round > 5) observe = 255;              // :348-349
-        const bool skip = observe < round * a.theta_p && round > a.k_new && observe < a.theta_max;   // :350-353
-        if (!skip) {
-            a.qflag[q] = f | 2;
-            a.observe[q] = observe;
-            const u32 rq = (u32)min(255, int(round)), gq = (u32)min(255, int(observe));   // :354-355
-            a.ds.at(c)[q - qi.start(c)].w = __uint_as_float(pack_rg(rq, gq));
-        }
+        ObsRes r;
+        observe_eval<NC>(a, qi, nq, q, r);
+        observe_commit<NC>(a, qi, q, r, false);
+        if (!(r.f & 1)) continue;
         const float sp = a.spars[q];
+        const bool skip = r.skip;
+        const float observe = r.observe;
+        const int c = r.c;
 #pragma unroll
         for (int cc = 0; cc < kMaxC; ++cc) {                  // static indices (registers, not scratch)
             if (cc != c) continue;
@@ -952,7 +991,10 @@ __device__ void rgm_prep_apps(const RgmPrep& r, const int* cnt, const double* x)
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < A; q += gridDim.x * blockDim.x) {
         int c, li;
         const int e = rgm_app_elem<NC>(V, q, c, li);
-        const float4 p = associate(prm, r.ds.at(c)[li]);
+        float4 p = r.ds.at(c)[li];
+        p.w = __uint_as_float(__hip_atomic_load(reinterpret_cast<const u32*>(&r.ds.at(c)[li].w), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT));   // r / g: the fused observe pass
+        p = associate(prm, p);
         r.app.at(c)[li] = p;
         const u64 key = rgm_key(p, c, r.leaf.at(c), box);
         const u32 tag = (u32)e | (box.in(p) ? 0u : kRgmDrop);
@@ -1279,7 +1321,22 @@ struct LmArgs {
     u32 map_cap;
     int* err;              // sticky error word E_LM
     RgmPrep prep;          // the last launch of an update prepares the rgbds merge's appended points
+    ObsArgs obs;           // fuse: the observe pass runs here, chunk by chunk (weightType 0; k_observe not launched)
+    int fuse;
 };
+
+// one pair's p-index increment (pidx_apply's body)
+__device__ __forceinline__ void pidx_apply_pair(const int* nbr, u32 inc, int p, int c, CloudsW map, int4* pbkt,
+                                                u32 map_cap) {
+    float4* mp = map.at(c);
+    const int idx = nbr[p];
+    const float4 m = mp[idx];
+    const u32 g = min(255u, w_g(m) + inc);
+    mp[idx].w = __uint_as_float(pack_rg(w_r(m), g));
+    int4* b = pbkt + (size_t)kBktQuads * ((u32)c * map_cap + (u32)idx);   // empty bucket
+    b[0].x = 0;
+    reinterpret_cast<int*>(b)[kBktHead] = -1;
+}
 
 template <int NC>
 __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
@@ -1288,7 +1345,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     if (rec) dbg[0] = __builtin_amdgcn_s_memrealtime();
     __shared__ double rows[256][8];                             // per residual: J[6], r, 0.5 rho
     __shared__ double red9[28][9];
-    __shared__ int nbad[2];
+    __shared__ int nbad[3];                                     // bad residuals, bad Jacobians, kept rows
     __shared__ unsigned char hi_[21], hj_[21];
     __shared__ double tot[kLmParts];
     __shared__ LMState lm;
@@ -1297,10 +1354,14 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     // the map's p-index bytes are not read by the solve: this iteration's increments are applied
     // while the blocks wait for the first evaluation's arrivals (or here, when there is no solve)
     const CatIdx<NC> qi = cat_idx<NC>(a.cnt + C_DS);
+    // fused observe pass (weightType 0): the residual count is known after the first evaluation
+    // (its partials carry each chunk's kept rows); without a gate there is nothing to observe
+    const bool fuse = a.fuse != 0;
     int nres = 0;
-    for (int c = 0; c < NC; ++c) nres += a.cnt[C_KEPT + c];
-    if (!a.st->gate || nres == 0) {                              // no residual blocks: untouched
-        pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
+    if (!fuse)
+        for (int c = 0; c < NC; ++c) nres += a.cnt[C_KEPT + c];
+    if (!a.st->gate || (!fuse && nres == 0)) {                   // no residual blocks: untouched
+        if (!fuse) pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
         if (a.prep.on) rgm_prep_apps<NC>(a.prep, a.cnt, a.st->params);
         return;
     }
@@ -1326,7 +1387,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         lm.n_res = nres;
         lm.done = 0;
         aborted = 0;
-        nbad[0] = nbad[1] = 0;                                   // before the barrier: every wave may count
+        nbad[0] = nbad[1] = nbad[2] = 0;                         // before the barrier: every wave may count
         int h = 0;
         for (int i = 0; i < 6; ++i)
             for (int j = i; j < 6; ++j) { hi_[h] = (unsigned char)i; hj_[h] = (unsigned char)j; ++h; }
@@ -1349,9 +1410,13 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     u32* claim = a.arrive;                                       // [kLmEvalSlots] claim masks
     double x[7];
     // one residual's inputs: the down-sampled point, the line (a, b) or plane (n, d) and the weight
-    auto load_res = [&](int q) {
+    // (fused: the kept bit may come from another workgroup of this launch, written through)
+    auto load_flag = [&](int q) {
+        return fuse ? __hip_atomic_load(&a.qflag[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.qflag[q];
+    };
+    auto load_res_k = [&](int q, bool kept) {
         ResIn in{};
-        if (q < nq && (a.qflag[q] & 2)) {
+        if (kept) {
             in.kept = true;
             const int c = qi.cls(q);
             in.plane = c == NC - 1;                              // the last class is the plane class
@@ -1371,7 +1436,71 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         }
         return in;
     };
-    s_mine[t] = load_res((int)blockIdx.x * 256 + t);
+    auto load_res = [&](int q) { return load_res_k(q, q < nq && (load_flag(q) & 2)); };
+    // the observe pass of chunk ch (fused): every slice's queries evaluated, their outputs committed
+    // when this workgroup owns the chunk's first evaluation (won), the valid / kept counts added
+    __shared__ u32 s_commit, s_claim0;
+    __shared__ int s_ocnt[2 * kMaxC];
+    auto observe_chunk = [&](int ch, bool home_claim) -> bool {
+        if (t < 2 * kMaxC) s_ocnt[t] = 0;
+        bool kept0 = false, won = true;
+        for (int base = ch * 256, k = 0; base < nq; base += kLmBlocks * 256, ++k) {
+            const int q = base + t;
+            ObsRes r;
+            r.f = 0;
+            if (q < nq) observe_eval<NC>(a.obs, qi, nq, q, r);
+            if (k == 0) {
+                __syncthreads();                                 // s_claim0 (thread 0's claim) and s_ocnt
+                won = !home_claim || ((s_claim0 >> ch) & 1u) == 0u;
+                kept0 = (r.f & 1) && !r.skip;
+            }
+            if (won && q < nq) {
+                observe_commit<NC>(a.obs, qi, q, r, true);
+                if (r.f & 1) {
+                    atomicAdd(&s_ocnt[2 * r.c], 1);
+                    if (!r.skip) atomicAdd(&s_ocnt[2 * r.c + 1], 1);
+                }
+            }
+        }
+        // the commits complete before this chunk's partials are published (consumers that see the
+        // partials read the kept bits)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (won && t < 2 * NC && s_ocnt[t]) atomicAdd(&a.cnt[(t & 1) ? C_KEPT + t / 2 : C_VALID + t / 2], s_ocnt[t]);
+        if (won && t == 0) s_commit |= 1u << ch;
+        return kept0;
+    };
+    // the p-index increments of the chunks this workgroup observed, by the threads that computed them
+    // (after the first evaluation: every observe pass of the launch has read the map's g bytes)
+    auto apply_commits = [&]() {
+        const u32 m = s_commit;
+        for (int ch = 0; ch < kLmBlocks; ++ch) {
+            if (!((m >> ch) & 1u)) continue;
+            for (int base = ch * 256; base < nq; base += kLmBlocks * 256) {
+                const int q = base + t;
+                if (q >= nq) continue;
+                const int c = qi.cls(q);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const u32 inc = a.tailinc[5 * q + j];
+                    if (inc) pidx_apply_pair(a.nbr, inc, 5 * q + j, c, a.map, a.pbkt, a.map_cap);
+                }
+            }
+        }
+    };
+    u32 old0 = 0;
+    bool applied = !fuse;
+    if (fuse) {
+        if (t == 0) {
+            s_commit = 0u;
+            s_claim0 = __hip_atomic_fetch_or(&claim[0], 1u << blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const bool kept0 = observe_chunk((int)blockIdx.x, true);
+        old0 = s_claim0;
+        s_mine[t] = load_res_k((int)blockIdx.x * 256 + t, kept0);
+    } else {
+        s_mine[t] = load_res((int)blockIdx.x * 256 + t);
+    }
     // reduce chunk ch of evaluation ev at x into 30 partials; publish them and count the chunk done
     // unless another block claimed it first (own_claim: claim_old is this block's atomicOr result)
     auto reduce_chunk = [&](int ch, int ev, u32 claim_old, bool own_claim) {
@@ -1384,6 +1513,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             const bool cached = ch == (int)blockIdx.x && base == ch * 256;
             const ResIn in = cached ? s_mine[t] : load_res(q);
             if (in.kept) {
+                atomicAdd(&nbad[2], 1);
                 r = in.plane ? surf_eval(x, in.cur, d3{in.G[0], in.G[1], in.G[2]}, in.G[3], in.wgt, J)
                              : edge_eval(x, in.cur, d3{in.G[0], in.G[1], in.G[2]}, d3{in.G[3], in.G[4], in.G[5]},
                                          in.wgt, J);
@@ -1441,7 +1571,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             double v = red9[t][0];
             for (int k = 1; k < 9; ++k) v += red9[t][k];
             if (pub) __hip_atomic_store(P + 32 * ch + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (t < 30) {
+        } else if (t < kLmParts) {
             if (pub) __hip_atomic_store(P + 32 * ch + t, (double)nbad[t - 28], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             nbad[t - 28] = 0;                                    // for the next chunk (after the barrier)
         }
@@ -1452,10 +1582,15 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         for (int k = 0; k < 7; ++k) x[k] = lm.cand[k];
         const int home = blockIdx.x;                             // grid == kLmBlocks
         u32 old = 0;
-        if (t == 0) old = __hip_atomic_fetch_or(&claim[ev], 1u << home, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (fuse && ev == 0) old = old0;                         // claimed before the observe pass
+        else if (t == 0) old = __hip_atomic_fetch_or(&claim[ev], 1u << home, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         reduce_chunk(home, ev, old, true);
         if (rec) dbg[1 + 4 * ev] = dbg[2 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
-        if (ev == 0) pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
+        if (!fuse && ev == 0) pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
+        if (fuse && ev == 1 && !applied) {                      // overlaps this evaluation's wait
+            apply_commits();
+            applied = true;
+        }
         // wait until no partial of this evaluation is the sentinel any more (threads t < 30 poll
         // their product over the 32 chunks); after kLmStealPolls rounds, claim and reduce chunks
         // nobody has claimed (their home workgroups have not started)
@@ -1494,8 +1629,12 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             }
             __syncthreads();
             if (aborted) break;
-            if (s_state == 2) reduce_chunk(s_steal, ev, 0u, false);
-            else __builtin_amdgcn_s_sleep(1);
+            if (s_state == 2) {
+                if (fuse && ev == 0) observe_chunk(s_steal, false);   // the chunk's observe pass is ours
+                reduce_chunk(s_steal, ev, 0u, false);
+            } else {
+                __builtin_amdgcn_s_sleep(1);
+            }
         }
         if (aborted) break;
         if (rec) dbg[3 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
@@ -1506,6 +1645,15 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             tot[t] = v;
         }
         __syncthreads();
+        if (fuse && ev == 0) {                                   // the residual count (kept rows)
+            const int nr = (int)tot[kLmParts - 1];
+            if (nr == 0) {                                       // no residual blocks: untouched
+                apply_commits();
+                if (a.prep.on) rgm_prep_apps<NC>(a.prep, a.cnt, a.st->params);
+                return;
+            }
+            if (t == 0) lm.n_res = nr;
+        }
         if (rec) dbg[40 + ev] = __builtin_amdgcn_s_memrealtime();
         if (t < 2) {                                             // lanes 0 and 1, identical state
             LmCore c;
@@ -1520,6 +1668,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         __syncthreads();
         if (rec) dbg[4 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
     }
+    if (!applied) apply_commits();
     if (blockIdx.x == 0 && t == 0) {
         for (int k = 0; k < 7; ++k) a.st->params[k] = lm.best[k];
         atomicAdd(&a.cnt[C_LM_ITERS], lm.iteration);
@@ -2988,14 +3137,17 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
         ObsArgs oa{cnt, o.acc, o.cls, clouds(map_cur(o)), clouds_w(sb.ds), o.nbr, o.qflag, o.pbkt, o.pnext, o.tailinc,
                    (u32)o.map_cap, o.roundv, o.spars, o.observe, o.prm.k_new, o.prm.theta_p, o.prm.theta_max,
                    o.errw + E_LM};
-        PF_LAUNCH_NC(nc, k_observe, dim3(kGrid), dim3(256), 0, s, oa);
+        // weightType 0 needs no frame-wide observe / sparsity bounds before the solve: the observe pass
+        // runs inside k_lm_solve, chunk by chunk, and k_observe is not launched
+        const bool fuse = o.prm.weight_type == 0 && !o.no_fuse_obs;
+        if (!fuse) PF_LAUNCH_NC(nc, k_observe, dim3(kGrid), dim3(256), 0, s, oa);
         const bool merge = !o.tie_order && !o.rg_radix;
         const RgmPrep prep{merge && it == o.opt_count_host - 1, clouds(map_cur(o)), clouds(sb.ds), clouds_w(o.app),
                            o.rgm_key64, o.rgm_vtag, VgLeaf{{o.leaf_rg[0], o.leaf_rg[1], o.leaf_rg[2]}}, o.rgm_bcount,
                            o.rgm_bkey, o.rgm_btag, o.rgm_stat};
         LmArgs la{o.st, cnt, o.acc, o.cls, o.lm, o.lm_part, o.lm_ticket, o.qflag, clouds(sb.ds), o.geo, o.observe,
                   o.spars, o.prm.weight_type, o.dbg, o.nbr, o.tailinc, o.pbkt, clouds_w(map_cur(o)), (u32)o.map_cap,
-                  o.errw + E_LM, prep};
+                  o.errw + E_LM, prep, oa, fuse ? 1 : 0};
         PF_LAUNCH_NC(nc, k_lm_solve, dim3(kLmBlocks), dim3(256), 0, s, la);   // grid must be kLmBlocks
     }
     // pose (:278-280, node copy.cpp:105-107) and addPointsToMap (:589-647, BPF :1197-1290)

@@ -542,6 +542,12 @@ class Odom_ES_EstimationClass:
         L.pf_dev_set_rg_radix.argtypes = [_vp, _i]
         _check("pf_dev_set_rg_radix", L.pf_dev_set_rg_radix(self._h, int(bool(enable))))
 
+    def set_fuse_observe(self, enable):
+        """development switch pf_dev_set_fuse_observe: False = the separate k_observe launch at weightType 0"""
+        L = lib()
+        L.pf_dev_set_fuse_observe.argtypes = [_vp, _i]
+        _check("pf_dev_set_fuse_observe", L.pf_dev_set_fuse_observe(self._h, int(bool(enable))))
+
     def merge_stats(self):
         """pf_odom_merge_stats: (updates that sorted every element, largest appended-point count)"""
         f, m = _i(), _i()

@@ -581,3 +581,43 @@ def test_probe_assoc_knn(pa, pfref, pfsynth):
     pop = sum(pfref.knn_cellpop(np.c_[maps[c], np.zeros(len(maps[c]), np.float32)],
                                 np.c_[q[cls == c, :3], np.zeros(int((cls == c).sum()), np.float32)]) for c in (0, 1))
     assert alg == (16 + 40 + 216) * nq + 16 * pop
+
+
+@pytest.mark.parametrize("preset,frames,bpf", [("S64", 300, False), ("S64V", 200, False), ("S64", 120, True)])
+def test_fused_observe_equals_separate_launch(pa, pfsynth, preset, frames, bpf):
+    """weightType 0 runs the observe pass inside k_lm_solve (chunk by chunk, k_observe not launched):
+    poses, maps (r / g bytes included) and the per-frame counts must be those of the separate
+    k_observe launch (development switch pf_dev_set_fuse_observe), under graph replay of both stages."""
+    seq = pfsynth.Sequence(preset, n_frames=frames, seed=0)
+    buf, cnt = seq.frames(0, frames, threads=16)
+    db = pa.DeviceBuffer(buf.nbytes)
+    db.upload(buf)
+    out = []
+    try:
+        for fused in (True, False):
+            if bpf:
+                od = pa.Odom_BPF_EstimationClass(device=0)
+            else:
+                od = pa.Odom_ES_EstimationClass(device=0, max_points=300000, map_capacity=1 << 21)
+            od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+            od.set_graph(3)
+            od.set_fuse_observe(fused)
+            stats = []
+            for i in range(frames):
+                if bpf:
+                    od.frame_scan_device(db.ptr + i * buf.shape[1] * 16, int(cnt[i]))
+                else:
+                    od.frame_device(db.ptr + i * buf.shape[1] * 16, int(cnt[i]))
+                if i % 50 == 49:
+                    st = od.stats()
+                    stats.append((st["n_res"], st["n_valid"], st["n_map"], st["errors"]))
+            od.sync()
+            out.append((od.poses(), [od._map(w) for w in range(3 if bpf else 2)], stats))
+    finally:
+        db.free()
+    assert np.array_equal(out[0][0], out[1][0])
+    for w in range(len(out[0][1])):
+        assert np.array_equal(out[0][1][w][0].view(np.uint32), out[1][1][w][0].view(np.uint32)), w
+        assert np.array_equal(out[0][1][w][1], out[1][1][w][1]), w
+    assert out[0][2] == out[1][2]
+    assert all(s[3] == 0 for s in out[0][2])
