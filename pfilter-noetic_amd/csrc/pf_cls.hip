@@ -480,6 +480,15 @@ __device__ __forceinline__ u32 wave_sort_u32(u32 v) {
     return v;
 }
 
+#ifdef PF_DEV_CLS_STATS
+// development (tools/build_variant.sh NAME -DPF_DEV_CLS_STATS): per-query work counters of the search,
+// summed over a call and printed by k_cls_decide's first thread: queries, chunk rounds, chunks in the
+// rows, chunks opened, read passes, candidates in range, candidates inside r, batch merges, single inserts
+__device__ unsigned long long g_cls_stats[10];
+#define CLS_STAT(i, v) do { if (lane_id() == 0) atomicAdd(&g_cls_stats[i], (unsigned long long)(v)); } while (0)
+#else
+#define CLS_STAT(i, v) do { } while (0)
+#endif
 // KdTreeFLANN::radiusSearch(i, r, idx, d2, k) for every U point, one wave per query. The candidates
 // are the 27 cells of the 1 m grid around the query (every point with d^2 < r^2 <= 1 lies there,
 // pf_knn.h), i.e. the aligned 16-point chunks of the cell-ordered cloud that overlap the 9 x-rows.
@@ -591,7 +600,10 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
             // round (truncation only lowers a bound, so stopping at the first truncated bound above
             // the k-th distance stays exact; a chunk is still read only if its bound may hold a winner)
             bool first = true;
+            CLS_STAT(0, 1);
+            CLS_STAT(2, total);
             for (u32 g = 0; g < total; g += 64) {
+                CLS_STAT(1, 1);
                 const u32 t = g + (u32)l;
                 u32 sk = ~0u;
                 if (t < total) {
@@ -602,10 +614,12 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                 }
                 sk = wave_sort_u32(sk);
                 const int nopen = __popcll(__ballot(sk != ~0u));
+                CLS_STAT(3, nopen);
                 auto lb_of = [](u32 k) { return __uint_as_float(k & ~0x3Fu); };
                 for (int i = 0; i < nopen; i += 4) {
                     if (!open(lb_of((u32)__builtin_amdgcn_readlane((int)sk, i)))) break;   // sorted: the rest too
                     const int j = i + (l >> 4);
+                    CLS_STAT(4, 1);
                     const u32 k0 = (u32)__builtin_amdgcn_readlane((int)sk, i);
                     const u32 k1 = (u32)__builtin_amdgcn_readlane((int)sk, i + 1 < 64 ? i + 1 : 63);
                     const u32 k2 = (u32)__builtin_amdgcn_readlane((int)sk, i + 2 < 64 ? i + 2 : 63);
@@ -617,13 +631,23 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                         locate(g + (sj & 0x3Fu), c, a0, b0);
                         const u32 v = c * 16u + (u32)(l & 15);
                         if (v >= a0 && v < b0) {
+#ifdef PF_DEV_CLS_STATS
+                            atomicAdd(&g_cls_stats[5], 1ull);
+#endif
                             const float4 p = gv.cpts[PF_IDX(d, v, nu)];
                             const float dd = knn_d2(qp.x, qp.y, qp.z, p);
                             if (dd < r2) key = knn_key(dd, __float_as_int(p.w));
                         }
                     }
                     u64 sm = __ballot(key < thr);
+#ifdef PF_DEV_CLS_STATS
+                    {
+                        const u64 inr = __ballot(key != ~0ull);
+                        CLS_STAT(6, __popcll(inr));
+                    }
+#endif
                     if (first || __popcll(sm) > kBatch) {
+                        if (sm) CLS_STAT(7, 1);
                         if (sm) merge_batch(key);
                         first = false;
                         continue;
@@ -633,6 +657,7 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                         sm &= sm - 1;
                         const u64 kk = readlane_u64(key, sl);
                         if (!(kk < thr)) continue;
+                        CLS_STAT(8, 1);
                         const u64 prev = wave_shr1_u64(ent);
                         ent = kk < prev ? prev : (kk < ent ? kk : ent);
                         thr = readlane_u64(ent, K - 1);
@@ -653,6 +678,14 @@ __global__ void __launch_bounds__(256) k_cls_decide(ClsDev d, const u32* __restr
     if (threadIdx.x < 4) ccount[threadIdx.x] = 0;
     sort_hist_begin(lh);
     const int nu = d.cnt[CC_NU];
+#ifdef PF_DEV_CLS_STATS
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        unsigned long long* g = g_cls_stats;
+        printf("CLS_STATS q=%llu rounds=%llu chunks=%llu opened=%llu passes=%llu inrange=%llu inr=%llu merges=%llu inserts=%llu\n",
+               g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8]);
+        for (int i = 0; i < 10; ++i) g[i] = 0ull;
+    }
+#endif
     int local[4] = {0, 0, 0, 0};
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nu; q += gridDim.x * blockDim.x) {
         const int n = d.ptnum[q];
