@@ -32,7 +32,9 @@ def short(name):
 def frame_breakdown(trace_csv, stats_csv):
     rows = list(csv.DictReader(open(trace_csv)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "PredictTail" in r["Kernel_Name"]]   # stage B head
+    starts = [i for i, r in enumerate(rows) if "PredictTail" in r["Kernel_Name"]]   # stage B head (r01-r02)
+    if len(starts) < 200:   # r03: the pose prediction runs in k_grid_count's tail; one k_rgm_finish per frame
+        starts = [i for i, r in enumerate(rows) if "k_rgm_finish" in r["Kernel_Name"]]
     frames = list(zip(starts[:-1], starts[1:]))[100:]          # steady state
     per = {}
     spans = []
