@@ -149,14 +149,14 @@ static void timing_free(pf_odom* h) {
     h->timing = nullptr;
 }
 // marks k = 0..3 (A start, A end, B start, B end) of the current frame
-static int timing_mark(pf_odom* h, int k) {
+static int timing_mark(pf_odom* h, int k, hipStream_t s = nullptr) {
     StageTiming* t = h->timing;
     if (!t || !t->on) return PF_OK;
     const int j = (int)(t->next % StageTiming::kRing);
     if (k == 0) {
         if (int rc = timing_harvest(*t, j)) return rc;
     }
-    PF_HIP_TRY(hipEventRecord(t->ev[j][k], k < 2 ? h->o.stream_a : h->o.stream));
+    PF_HIP_TRY(hipEventRecord(t->ev[j][k], s ? s : (k < 2 ? h->o.stream_a : h->o.stream)));
     if (k == 3) {
         t->pending[j] = true;
         t->next++;
@@ -300,7 +300,7 @@ static void host_prof_report();
 int pf_odom_destroy(pf_odom* h) {
     if (!h) return PF_OK;
     (void)hipSetDevice(h->o.device);
-    (void)hipStreamSynchronize(h->o.stream_a);
+    (void)odom_sync_a(h->o);
     (void)hipStreamSynchronize(h->o.stream);
     timing_free(h);
     host_prof_report();
@@ -629,6 +629,54 @@ static void stage_enqueue_front(OdomGPU& o, int p, hipStream_t s) {
     cls_enqueue(*o.front, o.stage, o.sb[p].cnt + C_NIN, out, cnt, false, s);
 }
 
+// front-end lane `lane` of the frame in slot p: the staged scan of that lane through its instance
+static void stage_enqueue_front_lane(OdomGPU& o, int p, int lane, hipStream_t s) {
+    float4* out[3] = {o.sb[p].in[0], o.sb[p].in[1], o.sb[p].in[2]};
+    int* cnt[3] = {o.sb[p].cnt + C_IN, o.sb[p].cnt + C_IN + 1, o.sb[p].cnt + C_IN + 2};
+    cls_enqueue(lane ? *o.front2 : *o.front, lane ? o.stage2 : o.stage, o.sb[p].cnt + C_NIN, out, cnt, false, s);
+}
+
+static void drop_graphs_f(OdomGPU& o) {
+    for (hipGraphExec_t& g : o.graph_f)
+        if (g) {
+            (void)hipGraphExecDestroy(g);
+            g = nullptr;
+        }
+}
+
+// The second front-end lane of a BPF raw-scan handle (OdomGPU::front_lanes): both lanes' streams
+// (stage A's CU mask), the slot events, and lane 1's front end (lane 0's parameters and DCVC) and
+// scan staging. Called by the first raw-scan frame with two lanes.
+static int front_lanes_ready(OdomGPU& o) {
+    if (o.front2) return PF_OK;
+    for (int l = 0; l < 2; ++l)
+        if (!o.stream_f[l])
+            if (int rc = odom_masked_stream(o.device, o.cu_reserve, &o.stream_f[l])) return rc;
+    for (int p = 0; p < kSlots; ++p)
+        if (!o.ev_f[p]) PF_HIP_TRY(hipEventCreateWithFlags(&o.ev_f[p], hipEventDisableTiming));
+    if (!o.stage2) PF_HIP_TRY(hipMalloc(&o.stage2, sizeof(float4) * kMaxC * o.in_cap));
+    ClsGPU* f = new (std::nothrow) ClsGPU();
+    if (!f) return PF_ENOMEM;
+    int rc = cls_alloc(*f, o.in_cap);
+    if (!rc) {
+        f->prm = o.front->prm;
+        f->sticky = o.errw + E_FRONT;
+        alias_err(f->grid.err, o.errw + E_FRONT_GRID);
+        if (o.front->dcvc) {
+            rc = cls_set_dcvc(*f, &o.front->dcvc->prm);
+            if (!rc) rc = dcvc_mark_called(*f->dcvc, o.stream_f[1]);
+        }
+    }
+    if (rc) {
+        if (f->grid.err == o.errw + E_FRONT_GRID) f->grid.err = nullptr;
+        cls_free(*f);
+        delete f;
+        return rc;
+    }
+    o.front2 = f;
+    return PF_OK;
+}
+
 static void drop_graphs_b(OdomGPU& o) {
     for (hipGraphExec_t& g : o.graph_b)
         if (g) {
@@ -648,6 +696,16 @@ static int capture(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, bool s
         odom_enqueue_update(o, p, s);
         odom_enqueue_export(o, s, true);
     }
+    PF_HIP_TRY(hipStreamEndCapture(s, &g));
+    PF_HIP_TRY(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
+    (void)hipGraphDestroy(g);
+    return PF_OK;
+}
+
+static int capture_front(hipStream_t s, hipGraphExec_t* out, OdomGPU& o, int p, int lane) {
+    hipGraph_t g;
+    PF_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    stage_enqueue_front_lane(o, p, lane, s);
     PF_HIP_TRY(hipStreamEndCapture(s, &g));
     PF_HIP_TRY(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
     (void)hipGraphDestroy(g);
@@ -717,10 +775,39 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
     const bool steady_b = steady && (gm & PF_GRAPH_STAGE_B) && (o.dims_fresh || !odom_merge_mode(o));
     if (scan && n > o.in_cap) return PF_ECAPACITY;
     int rc = 0;
+    const bool lanes = scan && o.front_lanes == 2;
+    if (lanes && (rc = front_lanes_ready(o))) return rc;
     PF_HT(0, rc = stage_a_begin(h, p));
-    if (!rc) rc = timing_mark(h, 0);
     if (rc) return rc;
-    if (nc == 2 || scan) {
+    if (lanes) {
+        // the front end on lane (frame & 1) once slot p is free, then VoxelGrid on stream_a in frame
+        // order after it: two consecutive frames' front ends run at once
+        const int lane = o.frames & 1;
+        hipStream_t fs = o.stream_f[lane];
+        PF_HIP_TRY(hipStreamWaitEvent(fs, o.ev_b[p], 0));
+        if ((rc = timing_mark(h, 0, fs))) return rc;
+        if (n) PF_HIP_TRY(hipMemcpyAsync(lane ? o.stage2 : o.stage, d_in, sizeof(float4) * n, hipMemcpyDeviceToDevice, fs));
+        hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, fs, o.sb[p].cnt + C_NIN, (int)n);
+        if (steady_a) {
+            hipGraphExec_t& gf = o.graph_f[p + kSlots * lane];
+            if (!gf && (rc = capture_front(fs, &gf, o, p, lane))) return rc;
+            PF_HIP_TRY(hipGraphLaunch(gf, fs));
+        } else {
+            stage_enqueue_front_lane(o, p, lane, fs);
+        }
+        PF_HIP_TRY(hipEventRecord(o.ev_f[p], fs));
+        PF_HIP_TRY(hipStreamWaitEvent(o.stream_a, o.ev_f[p], 0));
+        if (steady_a) {
+            hipGraphExec_t& ga = o.graph_a[p];                 // nc == 3 without scan: VoxelGrid only
+            if (!ga && (rc = capture(o.stream_a, &ga, o, p, true, false))) return rc;
+            PF_HIP_TRY(hipGraphLaunch(ga, o.stream_a));
+        } else if (o.inited) {
+            stage_enqueue_vg(o, p, o.stream_a);
+        }
+    }
+    if (!lanes && (rc = timing_mark(h, 0))) return rc;
+    if (lanes) {
+    } else if (nc == 2 || scan) {
         if (n > o.in_cap) return PF_ECAPACITY;
         if (n) PF_HT(1, PF_HIP_TRY(hipMemcpyAsync(o.stage, d_in, sizeof(float4) * n, hipMemcpyDeviceToDevice, o.stream_a)));
         PF_HT(2, hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, o.sb[p].cnt + C_NIN, (int)n));
@@ -732,7 +819,8 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
             hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, o.sb[p].cnt + C_IN + c, (int)ncl[c]);
         }
     }
-    if (steady_a) {
+    if (lanes) {
+    } else if (steady_a) {
         hipGraphExec_t& ga = scan ? o.graph_as[p] : o.graph_a[p];
         if (!ga) {
             rc = capture(o.stream_a, &ga, o, p, true, scan);
@@ -819,7 +907,7 @@ int pf_bpf_set_front_end(pf_odom* h, const pf_cls_params* p) {
         return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(odom_sync_a(o));
     if (!o.front) {
         o.front = new ClsGPU();
         const int rc = cls_alloc(*o.front, o.in_cap);
@@ -833,11 +921,13 @@ int pf_bpf_set_front_end(pf_odom* h, const pf_cls_params* p) {
         alias_err(o.front->grid.err, o.errw + E_FRONT_GRID);
     }
     o.front->prm = *p;
+    if (o.front2) o.front2->prm = *p;
     for (int s = 0; s < kSlots; ++s)        // parameters are baked into the captured kernels
         if (o.graph_as[s]) {
             (void)hipGraphExecDestroy(o.graph_as[s]);
             o.graph_as[s] = nullptr;
         }
+    drop_graphs_f(o);
     return PF_OK;
 }
 
@@ -851,14 +941,31 @@ int pf_bpf_set_dcvc(pf_odom* h, const pf_dcvc_params* p) {
         const int rc = pf_bpf_set_front_end(h, &fp);
         if (rc) return rc;
     }
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
-    const int rc = cls_set_dcvc(*o.front, p);
+    PF_HIP_TRY(odom_sync_a(o));
+    int rc = cls_set_dcvc(*o.front, p);
+    if (!rc && o.front2) {
+        const bool fresh = p && !o.front2->dcvc;
+        rc = cls_set_dcvc(*o.front2, p);
+        if (!rc && fresh) rc = dcvc_mark_called(*o.front2->dcvc, o.stream);
+        if (!rc && fresh) PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    }
     if (rc) return rc;
     for (int s = 0; s < kSlots; ++s)        // the front end's kernel sequence changed
         if (o.graph_as[s]) {
             (void)hipGraphExecDestroy(o.graph_as[s]);
             o.graph_as[s] = nullptr;
         }
+    drop_graphs_f(o);
+    return PF_OK;
+}
+
+int pf_bpf_set_front_lanes(pf_odom* h, int lanes) {
+    if (!h || h->o.cls.nc != 3 || lanes < 1 || lanes > 2) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(odom_sync_a(o));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    o.front_lanes = lanes;
     return PF_OK;
 }
 
@@ -889,7 +996,7 @@ int pf_odom_set_stage_a_reserve(pf_odom* h, int cus) {
 int pf_odom_sync(pf_odom* h) {
     if (!h) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->o.device));
-    PF_HIP_TRY(hipStreamSynchronize(h->o.stream_a));
+    PF_HIP_TRY(odom_sync_a(h->o));
     PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
     PF_HIP_TRY(hipGetLastError());
     return sticky_status(h->o);
@@ -898,7 +1005,7 @@ int pf_odom_sync(pf_odom* h) {
 int pf_odom_set_stage_timing(pf_odom* h, int enable) {
     if (!h) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->o.device));
-    PF_HIP_TRY(hipStreamSynchronize(h->o.stream_a));
+    PF_HIP_TRY(odom_sync_a(h->o));
     PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
     if (!enable) {
         timing_free(h);
@@ -925,7 +1032,7 @@ int pf_odom_set_stage_timing(pf_odom* h, int enable) {
 int pf_odom_stage_times(pf_odom* h, double* a_us, double* b_us, size_t* frames) {
     if (!h) return PF_EINVAL;
     PF_HIP_TRY(hipSetDevice(h->o.device));
-    PF_HIP_TRY(hipStreamSynchronize(h->o.stream_a));
+    PF_HIP_TRY(odom_sync_a(h->o));
     PF_HIP_TRY(hipStreamSynchronize(h->o.stream));
     StageTiming* t = h->timing;
     if (t)
@@ -967,7 +1074,7 @@ int pf_odom_set_ring_model(pf_odom* h, double top_deg, double bottom_deg) {
     if (!h) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(odom_sync_a(o));
     const int rc = fe_set_ring_model(o.fe, top_deg, bottom_deg);
     if (rc) return rc;
     for (int s = 0; s < kSlots; ++s)        // the ring model is baked into the captured stage-A kernels
@@ -1000,7 +1107,7 @@ int pf_odom_set_state(pf_odom* h, const double odom_pose[7], const double last_p
     if (!h || !odom_pose || optimization_count < 0) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(odom_sync_a(o));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     DevState st;
     PF_HIP_TRY(hipMemcpy(&st, o.st, sizeof(st), hipMemcpyDeviceToHost));
@@ -1047,7 +1154,7 @@ int pf_odom_snapshot(pf_odom* h, void* buf, size_t cap, size_t* size) {
     if (!h || !size) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(odom_sync_a(o));
     PF_HIP_TRY(hipMemcpyAsync(o.h_cnt, o.cnt, sizeof(int) * C_COUNT, hipMemcpyDeviceToHost, o.stream));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     SnapHeader hd{};
@@ -1182,7 +1289,7 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
     if (!h) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(odom_sync_a(o));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     if (enable && !o.tie_a) {
         o.tie_a = new (std::nothrow) TieSort();
@@ -1198,6 +1305,7 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
                     (void)hipGraphExecDestroy(*g);
                     *g = nullptr;
                 }
+        drop_graphs_f(o);
         drop_graphs_b(o);
     }
     o.tie_order = enable != 0;
@@ -1211,7 +1319,7 @@ extern "C" int pf_dev_set_fuse_observe(pf_odom* h, int enable) {
     if (!h) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(odom_sync_a(o));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     if ((enable == 0) != o.no_fuse_obs) drop_graphs_b(o);
     o.no_fuse_obs = enable == 0;
@@ -1222,7 +1330,7 @@ extern "C" int pf_dev_set_rg_radix(pf_odom* h, int enable) {
     if (!h) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(odom_sync_a(o));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     if ((enable != 0) != o.rg_radix) drop_graphs_b(o);
     o.rg_radix = enable != 0;
@@ -1291,7 +1399,7 @@ int pf_odom_merge_stats(pf_odom* h, int* full_sorts, int* max_appended) {
     if (!h || !full_sorts || !max_appended) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(odom_sync_a(o));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     int st[4];
     PF_HIP_TRY(hipMemcpy(st, o.rgm_stat, sizeof(st), hipMemcpyDeviceToHost));

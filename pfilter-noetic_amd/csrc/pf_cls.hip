@@ -442,6 +442,15 @@ __device__ __forceinline__ u64 shfl_xor_u64(u64 v, int m) {
 #ifndef PF_CLS_BATCH
 #define PF_CLS_BATCH 16
 #endif
+#ifndef PF_CLS_NOSORT
+#define PF_CLS_NOSORT 4
+#endif
+constexpr int kClsNoSort = PF_CLS_NOSORT;   // open chunks in a round up to which the round is not sorted
+#ifdef PF_CLS_ROWS_PLAIN
+__constant__ constexpr int kClsRowOrder[9] = {0, 1, 2, 3, 4, 5, 6, 7, 8};
+#else
+__constant__ constexpr int kClsRowOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // row r = (oz + 1) * 3 + oy + 1
+#endif
 constexpr int kBatch = PF_CLS_BATCH;   // winners in one pass above which the pass is merged as a whole
 __device__ __forceinline__ u64 readlane_u64(u64 v, int lane) {
     const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, lane);
@@ -564,7 +573,10 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
             u32 ra[9], rb[9], pre[9];
             u32 total = 0;
 #pragma unroll
-            for (int r = 0; r < 9; ++r) {
+            for (int k = 0; k < 9; ++k) {
+                // rows in processing order: the query's own row, the four sharing a face with it,
+                // then the four diagonal ones (the nearest candidates fill the list first)
+                const int r = kClsRowOrder[k];
                 const int oy = r % 3 - 1, oz = r / 3 - 1;
                 const u32 s0 = (u32)__builtin_amdgcn_readlane((int)w0, r), s1 = (u32)__builtin_amdgcn_readlane((int)w1, r);
                 const u32 s2 = (u32)__builtin_amdgcn_readlane((int)w2, r), s3 = (u32)__builtin_amdgcn_readlane((int)w3, r);
@@ -575,9 +587,9 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                 const float bh = (hx * hx + by * by) + bz * bz;
                 u32 a0 = bl < r2 ? s0 : s1, b0 = bh < r2 ? s3 : s2;
                 if (!(brow < r2) || a0 >= b0) a0 = b0 = 0;
-                ra[r] = a0;
-                rb[r] = b0;
-                pre[r] = total;
+                ra[k] = a0;
+                rb[k] = b0;
+                pre[k] = total;
                 total += a0 < b0 ? ((b0 - 1) >> 4) - (a0 >> 4) + 1 : 0;
             }
             // chunk ordinal t -> (chunk, its row's range)
@@ -612,18 +624,34 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                     const float lb = box_lb((int)c);
                     if (open(lb)) sk = (__float_as_uint(lb) & ~0x3Fu) | (u32)l;
                 }
-                sk = wave_sort_u32(sk);
-                const int nopen = __popcll(__ballot(sk != ~0u));
+                u64 om = __ballot(sk != ~0u);
+                const int nopen = __popcll(om);
                 CLS_STAT(3, nopen);
+                // up to one pass of open chunks: read them as they lie (no sort); else nearest first
+                const bool few = nopen <= kClsNoSort;
+                u32 f0 = ~0u, f1 = ~0u, f2 = ~0u, f3 = ~0u;
+                if (few) {
+                    if (!om) continue;
+                    f0 = (u32)__builtin_amdgcn_readlane((int)sk, __ffsll((unsigned long long)om) - 1);
+                    om &= om - 1;
+                    if (om) f1 = (u32)__builtin_amdgcn_readlane((int)sk, __ffsll((unsigned long long)om) - 1);
+                    if (om) om &= om - 1;
+                    if (om) f2 = (u32)__builtin_amdgcn_readlane((int)sk, __ffsll((unsigned long long)om) - 1);
+                    if (om) om &= om - 1;
+                    if (om) f3 = (u32)__builtin_amdgcn_readlane((int)sk, __ffsll((unsigned long long)om) - 1);
+                } else {
+                    sk = wave_sort_u32(sk);
+                }
                 auto lb_of = [](u32 k) { return __uint_as_float(k & ~0x3Fu); };
                 for (int i = 0; i < nopen; i += 4) {
-                    if (!open(lb_of((u32)__builtin_amdgcn_readlane((int)sk, i)))) break;   // sorted: the rest too
+                    // sorted: a closed chunk closes the rest too
+                    if (!few && !open(lb_of((u32)__builtin_amdgcn_readlane((int)sk, i)))) break;
                     const int j = i + (l >> 4);
                     CLS_STAT(4, 1);
-                    const u32 k0 = (u32)__builtin_amdgcn_readlane((int)sk, i);
-                    const u32 k1 = (u32)__builtin_amdgcn_readlane((int)sk, i + 1 < 64 ? i + 1 : 63);
-                    const u32 k2 = (u32)__builtin_amdgcn_readlane((int)sk, i + 2 < 64 ? i + 2 : 63);
-                    const u32 k3 = (u32)__builtin_amdgcn_readlane((int)sk, i + 3 < 64 ? i + 3 : 63);
+                    const u32 k0 = few ? f0 : (u32)__builtin_amdgcn_readlane((int)sk, i);
+                    const u32 k1 = few ? f1 : (u32)__builtin_amdgcn_readlane((int)sk, i + 1 < 64 ? i + 1 : 63);
+                    const u32 k2 = few ? f2 : (u32)__builtin_amdgcn_readlane((int)sk, i + 2 < 64 ? i + 2 : 63);
+                    const u32 k3 = few ? f3 : (u32)__builtin_amdgcn_readlane((int)sk, i + 3 < 64 ? i + 3 : 63);
                     const u32 sj = (l >> 4) == 1 ? k1 : ((l >> 4) == 2 ? k2 : ((l >> 4) == 3 ? k3 : k0));
                     u64 key = ~0ull;
                     if (j < nopen && open(lb_of(sj))) {

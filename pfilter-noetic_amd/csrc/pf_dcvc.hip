@@ -432,6 +432,12 @@ int dcvc_reset(DcvcGPU& g, hipStream_t s) {
     return PF_OK;
 }
 
+int dcvc_mark_called(DcvcGPU& g, hipStream_t s) {
+    PF_HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g.dim + D_CALLS), 1, 1, s));
+    PF_HIP_TRY(hipMemsetAsync(g.dim + D_ERR, 0, sizeof(int), s));
+    return PF_OK;
+}
+
 // cells of the voxel index space: (polarNum + 1) (width + 1) (height + 3), polarNum bounded by the
 // rings up to max(5 m, max_range) and the pitch layers (height + 1 of them, plus the top layer quirk)
 // by 180 degrees

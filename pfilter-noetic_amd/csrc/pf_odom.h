@@ -187,6 +187,21 @@ struct OdomGPU {
     hipGraphExec_t graph_b[2 * kSlots] = {};                // [slot + kSlots * mpar]
     ClsGPU* front = nullptr;                                // BPF raw-scan mode: the PCA front end
     hipGraphExec_t graph_as[kSlots] = {};                   // stage A replay in raw-scan mode
+    // BPF raw-scan mode with two front-end lanes (pf_bpf_set_front_lanes; the default): the front end of
+    // frame k runs on stream_f[k & 1] with that lane's own instance (front / front2) and scan staging
+    // (stage / stage2), so the front ends of consecutive frames overlap; VoxelGrid then runs on
+    // stream_a in frame order once the frame's front end is done (ev_f). Allocated by the first
+    // raw-scan frame. Lane 1's DCVC starts as "called before" (pf_dcvc.h dcvc_mark_called): the
+    // reference's first-call defaults belong to frame 0 only, which lane 0 runs.
+#ifndef PF_FRONT_LANES_DEFAULT
+#define PF_FRONT_LANES_DEFAULT 2
+#endif
+    int front_lanes = PF_FRONT_LANES_DEFAULT;
+    ClsGPU* front2 = nullptr;
+    float4* stage2 = nullptr;                               // [kMaxC * in_cap]
+    hipStream_t stream_f[2] = {};
+    hipEvent_t ev_f[kSlots] = {};                           // frame in slot p: front end done
+    hipGraphExec_t graph_f[2 * kSlots] = {};                // [slot + kSlots * lane] front-end replay
     // local maps, double-buffered: an update reads mapset[mpar] and writes the new maps into
     // mapset[mpar ^ 1] (rgbds cannot overwrite the map it is still reading), then the host flips mpar
     // (odom_update_done); graph B is captured per (slot, mpar)
@@ -254,6 +269,10 @@ struct OdomGPU {
 constexpr int kStageAReserveES = 128;
 constexpr int kStageAReserveBPF = 32;
 int odom_stage_a_stream(OdomGPU& o, int reserve);
+// a stream restricted to all but the last `reserve` CUs (0: unrestricted, non-blocking)
+int odom_masked_stream(int device, int reserve, hipStream_t* out);
+// waits for everything enqueued on stage A's streams (the front-end lanes and stream_a)
+hipError_t odom_sync_a(OdomGPU& o);
 
 // nc = 2: the ES estimator; nc = 3: the BPF estimator (the last class is the plane class)
 int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& prm, int device, size_t in_cap,

@@ -2786,11 +2786,10 @@ __global__ void k_init_counts(int* __restrict__ cnt, DevState* __restrict__ st, 
 // before the old one is destroyed, so a failure leaves the handle's stage A stream valid. The masked
 // stream is a blocking stream (hipExtStreamCreateWithCUMask takes no flags), so the C ABI keeps every
 // copy stream-ordered on the handle's streams and never uses the null stream.
-int odom_stage_a_stream(OdomGPU& o, int reserve) {
+int odom_masked_stream(int device, int reserve, hipStream_t* out) {
     int ncu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, o.device) != hipSuccess) return PF_EHIP;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return PF_EHIP;
     if (reserve < 0 || (reserve > 0 && reserve > ncu - 32)) return PF_EINVAL;
-    if (o.stream_a && hipStreamSynchronize(o.stream_a) != hipSuccess) return PF_EHIP;
     hipStream_t s = nullptr;
     if (reserve > 0) {
         std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
@@ -2799,8 +2798,37 @@ int odom_stage_a_stream(OdomGPU& o, int reserve) {
     } else if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
         return PF_EHIP;
     }
+    *out = s;
+    return PF_OK;
+}
+
+hipError_t odom_sync_a(OdomGPU& o) {
+    for (hipStream_t f : o.stream_f)
+        if (f) {
+            const hipError_t e = hipStreamSynchronize(f);
+            if (e != hipSuccess) return e;
+        }
+    return o.stream_a ? hipStreamSynchronize(o.stream_a) : hipSuccess;
+}
+
+int odom_stage_a_stream(OdomGPU& o, int reserve) {
+    if (odom_sync_a(o) != hipSuccess) return PF_EHIP;
+    hipStream_t s = nullptr, f[2] = {};
+    if (int rc = odom_masked_stream(o.device, reserve, &s)) return rc;
+    for (int l = 0; l < 2; ++l)                        // the front-end lanes share stage A's CUs
+        if (o.stream_f[l])
+            if (int rc = odom_masked_stream(o.device, reserve, &f[l])) {
+                (void)hipStreamDestroy(s);
+                if (f[0]) (void)hipStreamDestroy(f[0]);
+                return rc;
+            }
     if (o.stream_a) (void)hipStreamDestroy(o.stream_a);
     o.stream_a = s;
+    for (int l = 0; l < 2; ++l)
+        if (o.stream_f[l]) {
+            (void)hipStreamDestroy(o.stream_f[l]);
+            o.stream_f[l] = f[l];
+        }
     o.cu_reserve = reserve;
     // graphs were captured on the old stream's work; they are stream-independent, keep them
     return PF_OK;
@@ -2961,7 +2989,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
 // back to the state after init (identity pose, empty maps, optimization_count 2), keeping every
 // allocation and captured graph: the next frame seeds the maps again
 int odom_reset(OdomGPU& o) {
-    if (hipStreamSynchronize(o.stream_a) != hipSuccess || hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
+    if (odom_sync_a(o) != hipSuccess || hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
     DevState h{};
     h.params[3] = 1.0;
     for (int i = 0; i < 3; ++i) h.odomR[4 * i] = h.lastR[4 * i] = 1.0;
@@ -2980,6 +3008,7 @@ int odom_reset(OdomGPU& o) {
         if (hipMemsetAsync(o.sb[p].cnt, 0, sizeof(int) * C_COUNT, o.stream) != hipSuccess) return PF_EHIP;
     hipLaunchKernelGGL(k_init_buckets, dim3(1024), dim3(256), 0, o.stream, o.pbkt, (size_t)o.cls.nc * o.map_cap);
     if (o.front && o.front->dcvc && dcvc_reset(*o.front->dcvc, o.stream) != PF_OK) return PF_EHIP;   // a first frame again
+    if (o.front2 && o.front2->dcvc && dcvc_mark_called(*o.front2->dcvc, o.stream) != PF_OK) return PF_EHIP;
     if (hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
     o.opt_count_host = 2;
     o.inited = false;
@@ -2996,6 +3025,9 @@ void odom_destroy(OdomGPU& o) {
         for (int q = 0; q < 2; ++q)
             if (o.graph_b[p + kSlots * q]) (void)hipGraphExecDestroy(o.graph_b[p + kSlots * q]);
         if (o.graph_as[p]) (void)hipGraphExecDestroy(o.graph_as[p]);
+        for (int l = 0; l < 2; ++l)
+            if (o.graph_f[p + kSlots * l]) (void)hipGraphExecDestroy(o.graph_f[p + kSlots * l]);
+        if (o.ev_f[p]) (void)hipEventDestroy(o.ev_f[p]);
         if (o.ev_a[p]) (void)hipEventDestroy(o.ev_a[p]);
         if (o.ev_b[p]) (void)hipEventDestroy(o.ev_b[p]);
         for (int c = 0; c < kMaxC; ++c) {
@@ -3011,12 +3043,17 @@ void odom_destroy(OdomGPU& o) {
         o.prim.err = nullptr;
         o.vprim.err = nullptr;
         if (o.front) o.front->grid.err = nullptr;
+        if (o.front2) o.front2->grid.err = nullptr;
     }
     fe_free(o.fe);
-    if (o.front) {
-        cls_free(*o.front);
-        delete o.front;
-    }
+    for (ClsGPU* f : {o.front, o.front2})
+        if (f) {
+            cls_free(*f);
+            delete f;
+        }
+    (void)hipFree(o.stage2);
+    for (hipStream_t f : o.stream_f)
+        if (f) (void)hipStreamDestroy(f);
     grid_free(o.grid);
     prim_free(o.prim);
     prim_free(o.vprim);
@@ -3192,7 +3229,7 @@ int odom_probe_assoc(OdomGPU& o, int iters, double* avg_ms, double* alg_bytes, i
     const int nc = o.cls.nc;
     const int p = (o.frames - 1) % kSlots;
     int nq = 0;
-    PF_HIP_TRY(hipStreamSynchronize(o.stream_a));
+    PF_HIP_TRY(odom_sync_a(o));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     PF_HIP_TRY(hipMemcpy(&nq, o.cnt + C_NQ, sizeof(int), hipMemcpyDeviceToHost));
     *nq_out = nq;

@@ -139,7 +139,7 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_odom_stage_times", "pf_odom_set_state", "pf_cls_normals", "pf_dcvc_default_params",
            "pf_dcvc_create", "pf_dcvc_destroy", "pf_dcvc_run", "pf_dcvc_reset", "pf_cls_set_dcvc", "pf_bpf_set_dcvc",
            "pf_host_alloc", "pf_host_free", "pf_odom_set_tie_order", "pf_odom_probe_assoc",
-           "pf_odom_merge_stats"]
+           "pf_odom_merge_stats", "pf_bpf_set_front_lanes"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -181,6 +181,7 @@ def lib():
     L.pf_dcvc_reset.argtypes = [_vp]
     L.pf_cls_set_dcvc.argtypes = [_vp, ctypes.POINTER(DcvcParams)]
     L.pf_bpf_set_dcvc.argtypes = [_vp, ctypes.POINTER(DcvcParams)]
+    L.pf_bpf_set_front_lanes.argtypes = [_vp, ctypes.c_int]
     L.pf_odom_stage_times.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(_sz)]
     if hasattr(L, "pf_odom_set_stage_a_reserve"):
@@ -655,6 +656,10 @@ class Odom_BPF_EstimationClass(Odom_ES_EstimationClass):
         """curvedfilter (pf_bpf_set_dcvc): DCVC between ground_seg and featureExtract in raw-scan mode"""
         p = ctypes.byref(dcvc_params(**params)) if enable else None
         _check("pf_bpf_set_dcvc", lib().pf_bpf_set_dcvc(self._h, p), allow_warn=False)
+
+    def set_front_lanes(self, lanes):
+        """pf_bpf_set_front_lanes: 2 (default) overlaps consecutive frames' front ends, 1 runs it in line"""
+        _check("pf_bpf_set_front_lanes", lib().pf_bpf_set_front_lanes(self._h, int(lanes)), allow_warn=False)
 
     def frame_scan_device(self, dptr, n, want_pose=False):
         """one raw scan already in HBM (packed float4) -> pose"""

@@ -155,6 +155,43 @@ def test_bpf_scan_pipeline(pa, pfref, pfsynth):
     np.testing.assert_array_equal(last, poses_h[3])
 
 
+@pytest.mark.parametrize("dcvc", [False, True])
+def test_bpf_front_lanes_identical(pa, pfsynth, dcvc):
+    """Two front-end lanes (pf_bpf_set_front_lanes(2), the default: consecutive frames' front ends on
+    two streams with an instance each) give the bits of one lane, with and without the curvedfilter
+    (whose first-call defaults belong to frame 0 on lane 0), through graph replay, and again after
+    pf_odom_reset on the same handle."""
+    nf = 24
+    seq = pfsynth.Sequence("S64", n_frames=nf, az_steps=1500)
+    scans = [seq.frame(k) for k in range(nf)]
+    n = max(x.shape[0] for x in scans)
+    buf = pa.DeviceBuffer(16 * n * nf)
+    for k, x in enumerate(scans):
+        buf.upload(x, 16 * n * k)
+
+    def run(lanes, od=None):
+        if od is None:
+            od = pa.Odom_BPF_EstimationClass(device=0)
+            od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+            od.set_front_lanes(lanes)
+            if dcvc:
+                od.set_dcvc(True)
+        for k, x in enumerate(scans):
+            od.frame_scan_device(buf.ptr + 16 * n * k, x.shape[0])
+        od.sync()
+        return od, od.poses(), [od._map(c) for c in range(3)]
+
+    _, p1, m1 = run(1)
+    od2, p2, m2 = run(2)
+    np.testing.assert_array_equal(p1, p2)
+    for a, b in zip(m1, m2):
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+    od2.reset()
+    _, p3, _ = run(2, od2)
+    np.testing.assert_array_equal(p1, p3)
+
+
 def test_bpf_scan_edge_cases(pa, pfsynth):
     """Raw-scan mode with an empty scan and a scan of a few points (the front end yields empty class
     clouds; the estimator warns that the map is too small, as the reference prints and continues), a
