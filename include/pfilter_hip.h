@@ -243,10 +243,12 @@ int pf_bpf_set_front_end(pf_odom* h, const pf_cls_params* p);
 /* curvedfilter in the raw-scan BPF pipeline (the KITTI launch's default); p NULL turns it off */
 int pf_bpf_set_dcvc(pf_odom* h, const pf_dcvc_params* p);
 int pf_bpf_frame_scan_device(pf_odom* h, const float* d_xyzi, size_t n, double pose_out[7]);
-/* EXTENSION (not in the reference): front-end lanes of the raw-scan mode. 2 (the default): the front
- * ends of consecutive frames run on two streams with one front-end instance each (about 2x the front
- * end's device memory), overlapping frame k + 1's front end with frame k's; VoxelGrid and the
- * odometry still run in frame order. 1: one front end, in line with VoxelGrid. Results are identical. */
+/* EXTENSION (not in the reference): front-end lanes of the raw-scan mode. 2: the front ends of
+ * consecutive frames run on two streams with one front-end instance each (about 2x the front end's
+ * device memory), overlapping frame k + 1's front end with frame k's; VoxelGrid and the odometry still
+ * run in frame order. 1: one front end, in line with VoxelGrid. 0 (the default): 2 while the handle is
+ * the only one on the host, else 1 (several handles' lanes oversubscribe the GPU's hardware queues).
+ * Results are identical in every mode. */
 int pf_bpf_set_front_lanes(pf_odom* h, int lanes);
 
 /* ---------------- global map (LaserMappingClass, src/laserMappingClass.cpp) ----------------

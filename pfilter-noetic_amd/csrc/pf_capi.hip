@@ -775,8 +775,14 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
     const bool steady_b = steady && (gm & PF_GRAPH_STAGE_B) && (o.dims_fresh || !odom_merge_mode(o));
     if (scan && n > o.in_cap) return PF_ECAPACITY;
     int rc = 0;
-    const bool lanes = scan && o.front_lanes == 2;
+    const bool lanes = scan && (o.front_lanes == 2 ||
+                                (o.front_lanes == 0 && g_live_handles.load(std::memory_order_relaxed) <= 1));
     if (lanes && (rc = front_lanes_ready(o))) return rc;
+    if (scan && o.lanes_used != (lanes ? 2 : 1)) {
+        // a change of lane mode: the instances the other mode used may still be busy (host wait, once)
+        if (o.lanes_used) PF_HIP_TRY(odom_sync_a(o));
+        o.lanes_used = lanes ? 2 : 1;
+    }
     PF_HT(0, rc = stage_a_begin(h, p));
     if (rc) return rc;
     if (lanes) {
@@ -960,7 +966,7 @@ int pf_bpf_set_dcvc(pf_odom* h, const pf_dcvc_params* p) {
 }
 
 int pf_bpf_set_front_lanes(pf_odom* h, int lanes) {
-    if (!h || h->o.cls.nc != 3 || lanes < 1 || lanes > 2) return PF_EINVAL;
+    if (!h || h->o.cls.nc != 3 || lanes < 0 || lanes > 2) return PF_EINVAL;
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
     PF_HIP_TRY(odom_sync_a(o));

@@ -443,14 +443,19 @@ __device__ __forceinline__ u64 shfl_xor_u64(u64 v, int m) {
 #define PF_CLS_BATCH 16
 #endif
 #ifndef PF_CLS_NOSORT
-#define PF_CLS_NOSORT 4
+#define PF_CLS_NOSORT 0
 #endif
-constexpr int kClsNoSort = PF_CLS_NOSORT;   // open chunks in a round up to which the round is not sorted
+constexpr int kClsNoSort = PF_CLS_NOSORT;   // open chunks in a round up to which the round is not sorted (0: a round
+                                            // without open chunks skips its sort; 4 measured 249 vs 244 us)
 #ifdef PF_CLS_ROWS_PLAIN
 __constant__ constexpr int kClsRowOrder[9] = {0, 1, 2, 3, 4, 5, 6, 7, 8};
 #else
 __constant__ constexpr int kClsRowOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // row r = (oz + 1) * 3 + oy + 1
 #endif
+#ifndef PF_CLS_PHASES
+#define PF_CLS_PHASES 2
+#endif
+constexpr int kClsPhases = PF_CLS_PHASES;   // 1: the nine rows in one pass of rounds (r03 before)
 constexpr int kBatch = PF_CLS_BATCH;   // winners in one pass above which the pass is merged as a whole
 __device__ __forceinline__ u64 readlane_u64(u64 v, int lane) {
     const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, lane);
@@ -568,8 +573,13 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                     w3 = xi + 1 < dx ? cs[PF_IDX(d, c0 + 2, d.cell_cap + 1)] : w2;
                 }
             }
-            // each row's point range [ra, rb) (end cells dropped when their bound is >= r^2) and the
-            // prefix of the rows' chunk counts
+            // Two phases: the query's own row, then the other eight with their ranges cut by the k-th
+            // distance found in the first (with a full list most of them close at once). Per phase:
+            // each row's point range [ra, rb) (end cells dropped when their bound cannot hold a
+            // winner: >= r^2, or above the k-th distance) and the prefix of the rows' chunk counts
+            bool first = true;
+            CLS_STAT(0, 1);
+            for (int ph = 0; ph < kClsPhases; ++ph) {
             u32 ra[9], rb[9], pre[9];
             u32 total = 0;
 #pragma unroll
@@ -585,8 +595,9 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                 const float brow = (0.0f + by * by) + bz * bz;
                 const float bl = (lx * lx + by * by) + bz * bz;
                 const float bh = (hx * hx + by * by) + bz * bz;
-                u32 a0 = bl < r2 ? s0 : s1, b0 = bh < r2 ? s3 : s2;
-                if (!(brow < r2) || a0 >= b0) a0 = b0 = 0;
+                u32 a0 = open(bl) ? s0 : s1, b0 = open(bh) ? s3 : s2;
+                const bool in_phase = kClsPhases == 1 || (ph == 0 ? k == 0 : k > 0);
+                if (!in_phase || !open(brow) || a0 >= b0) a0 = b0 = 0;
                 ra[k] = a0;
                 rb[k] = b0;
                 pre[k] = total;
@@ -611,8 +622,6 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
             // sort keys: the bound's float bits with the low 6 bits replaced by the chunk's lane in the
             // round (truncation only lowers a bound, so stopping at the first truncated bound above
             // the k-th distance stays exact; a chunk is still read only if its bound may hold a winner)
-            bool first = true;
-            CLS_STAT(0, 1);
             CLS_STAT(2, total);
             for (u32 g = 0; g < total; g += 64) {
                 CLS_STAT(1, 1);
@@ -691,6 +700,7 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                         thr = readlane_u64(ent, K - 1);
                     }
                 }
+            }
             }
         }
         const int found = __popcll(__ballot(l < K && ent != ~0ull));

@@ -187,16 +187,18 @@ struct OdomGPU {
     hipGraphExec_t graph_b[2 * kSlots] = {};                // [slot + kSlots * mpar]
     ClsGPU* front = nullptr;                                // BPF raw-scan mode: the PCA front end
     hipGraphExec_t graph_as[kSlots] = {};                   // stage A replay in raw-scan mode
-    // BPF raw-scan mode with two front-end lanes (pf_bpf_set_front_lanes; the default): the front end of
+    // BPF raw-scan mode with two front-end lanes (pf_bpf_set_front_lanes; the default for a handle alone
+    // on the host, as PF_GRAPH_AUTO: several handles' lanes oversubscribe the hardware queues): the front end of
     // frame k runs on stream_f[k & 1] with that lane's own instance (front / front2) and scan staging
     // (stage / stage2), so the front ends of consecutive frames overlap; VoxelGrid then runs on
     // stream_a in frame order once the frame's front end is done (ev_f). Allocated by the first
     // raw-scan frame. Lane 1's DCVC starts as "called before" (pf_dcvc.h dcvc_mark_called): the
     // reference's first-call defaults belong to frame 0 only, which lane 0 runs.
 #ifndef PF_FRONT_LANES_DEFAULT
-#define PF_FRONT_LANES_DEFAULT 2
+#define PF_FRONT_LANES_DEFAULT 0
 #endif
-    int front_lanes = PF_FRONT_LANES_DEFAULT;
+    int front_lanes = PF_FRONT_LANES_DEFAULT;   // 1, 2, or 0 = auto: 2 while the handle is alone on the host
+    int lanes_used = 0;                         // the lane count of the last raw-scan frame (0: none yet)
     ClsGPU* front2 = nullptr;
     float4* stage2 = nullptr;                               // [kMaxC * in_cap]
     hipStream_t stream_f[2] = {};

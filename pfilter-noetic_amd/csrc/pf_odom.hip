@@ -933,6 +933,42 @@ __device__ __forceinline__ u64 rgm_old_key(const RgView<NC>& V, const VgLeaf& le
     return rgm_key(p, c, leaf.at(c), box);
 }
 
+// First map element (classes concatenated) of bucket b; bucket b merges map elements
+// [rgm_bucket_lo(b), rgm_bucket_lo(b + 1)). Every class with map points gets at least
+// ceil(2 a_c / kRgmBucketCap) buckets, so its appended points average at most half a list even when
+// its map is small next to another class's (configs[4]: a 7k-point edge map beside a 2M-point surf
+// map); the remaining buckets go by map size, and a class's map range is split evenly.
+template <int NC>
+__device__ __forceinline__ int rgm_bucket_lo(const RgView<NC>& V, int b) {
+    int M = 0, need = 0, want[kMaxC] = {0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int a = V.end[c] - (c ? V.end[c - 1] : 0) - V.m[c];
+        want[c] = V.m[c] > 0 ? max(1, (2 * a + kRgmBucketCap - 1) / kRgmBucketCap) : 0;
+        need += want[c];
+        M += V.m[c];
+    }
+    if (M == 0) return 0;
+    if (need > kRgmBuckets) return (int)(((long long)b * M) / kRgmBuckets);   // the plain split
+    const int rem = kRgmBuckets - need;
+    int nb[kMaxC] = {0, 0, 0}, given = 0, last = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        nb[c] = want[c] + (int)(((long long)rem * V.m[c]) / M);
+        given += nb[c];
+        if (V.m[c] > 0) last = c;
+    }
+    nb[last] += kRgmBuckets - given;
+    int b0 = 0, m0 = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        if (nb[c] > 0 && b < b0 + nb[c]) return m0 + (int)(((long long)(b - b0) * V.m[c]) / nb[c]);
+        b0 += nb[c];
+        m0 += V.m[c];
+    }
+    return M;
+}
+
 // lower / upper bound of k in sorted keys[0 .. n) (LDS or global)
 __device__ __forceinline__ int rgm_lower(const u64* keys, int n, u64 k) {
     int lo = 0, hi = n;
@@ -984,7 +1020,7 @@ __device__ void rgm_prep_apps(const RgmPrep& r, const int* cnt, const double* x)
     for (int k = 0; k < 7; ++k) prm[k] = x[k];
     const RgmBox box = rgm_box(prm);
     for (int i = threadIdx.x; i < kRgmBuckets; i += blockDim.x) {
-        const int l0 = (int)(((long long)i * M) / kRgmBuckets);
+        const int l0 = rgm_bucket_lo<NC>(V, i);
         s_sp[i] = i == 0 ? 0ull : (l0 >= M ? ~0ull : rgm_old_key<NC>(V, r.leaf, box, l0));
     }
     __syncthreads();
@@ -2242,7 +2278,7 @@ __global__ void __launch_bounds__(kRgmThreads) k_rgm_bucket(RgmArgs a) {
         return;
     }
     const RgmBox box = rgm_box(a.st->params);
-    const int lo = (int)(((long long)b * M) / kRgmBuckets), hi = (int)(((long long)(b + 1) * M) / kRgmBuckets);
+    const int lo = rgm_bucket_lo<NC>(V, b), hi = rgm_bucket_lo<NC>(V, b + 1);
     RGM_MARK(0);
     const int nold = hi - lo;
     const bool cache = nold <= kRgmOldLds;

@@ -157,7 +157,7 @@ def test_bpf_scan_pipeline(pa, pfref, pfsynth):
 
 @pytest.mark.parametrize("dcvc", [False, True])
 def test_bpf_front_lanes_identical(pa, pfsynth, dcvc):
-    """Two front-end lanes (pf_bpf_set_front_lanes(2), the default: consecutive frames' front ends on
+    """Two front-end lanes (pf_bpf_set_front_lanes(2), what the auto default picks for a lone handle: consecutive frames' front ends on
     two streams with an instance each) give the bits of one lane, with and without the curvedfilter
     (whose first-call defaults belong to frame 0 on lane 0), through graph replay, and again after
     pf_odom_reset on the same handle."""
@@ -190,6 +190,17 @@ def test_bpf_front_lanes_identical(pa, pfsynth, dcvc):
     od2.reset()
     _, p3, _ = run(2, od2)
     np.testing.assert_array_equal(p1, p3)
+    # the lane mode changed mid-sequence (as the auto mode does when a second handle appears)
+    od3 = pa.Odom_BPF_EstimationClass(device=0)
+    od3.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    if dcvc:
+        od3.set_dcvc(True)
+    for k, x in enumerate(scans):
+        if k in (7, 13, 18):
+            od3.set_front_lanes({7: 1, 13: 2, 18: 0}[k])
+        od3.frame_scan_device(buf.ptr + 16 * n * k, x.shape[0])
+    od3.sync()
+    np.testing.assert_array_equal(p1, od3.poses())
 
 
 def test_bpf_scan_edge_cases(pa, pfsynth):
