@@ -247,7 +247,8 @@ int pf_bpf_frame_scan_device(pf_odom* h, const float* d_xyzi, size_t n, double p
  * consecutive frames run on two streams with one front-end instance each (about 2x the front end's
  * device memory), overlapping frame k + 1's front end with frame k's; VoxelGrid and the odometry still
  * run in frame order. 1: one front end, in line with VoxelGrid. 0 (the default): 2 while the handle is
- * the only one on the host, else 1 (several handles' lanes oversubscribe the GPU's hardware queues).
+ * the process's only handle with a raw-scan front end, else 1 (several such handles' lanes
+ * oversubscribe the GPU's hardware queues).
  * Results are identical in every mode. */
 int pf_bpf_set_front_lanes(pf_odom* h, int lanes);
 

@@ -126,6 +126,7 @@ struct pf_odom {
     OdomGPU o;
     StageTiming* timing = nullptr;
     bool counted = false;      // in g_live_handles
+    bool front_counted = false;  // in g_front_handles (has run the BPF raw-scan front end)
 };
 
 static int timing_harvest(StageTiming& t, int j) {
@@ -260,6 +261,9 @@ int pf_fe_set_ring_model(pf_fe* h, double top_deg, double bottom_deg) {
 // live handles of the process (PF_GRAPH_AUTO: stage B replays its graph when several handles share
 // the host's launch path)
 static std::atomic<int> g_live_handles{0};
+// handles of this process with a BPF raw-scan front end: the auto lane mode gives two front-end lanes
+// only while one such handle exists (idle ES handles in the same process do not count)
+static std::atomic<int> g_front_handles{0};
 
 static int create(const pf_lidar_params* lidar, const pf_odom_params* params, int device, size_t max_points,
                   size_t map_capacity, int nc, pf_odom** out) {
@@ -306,6 +310,7 @@ int pf_odom_destroy(pf_odom* h) {
     host_prof_report();
     odom_destroy(h->o);
     if (h->counted) g_live_handles.fetch_sub(1);
+    if (h->front_counted) g_front_handles.fetch_sub(1);
     delete h;
     return PF_OK;
 }
@@ -776,7 +781,7 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
     if (scan && n > o.in_cap) return PF_ECAPACITY;
     int rc = 0;
     const bool lanes = scan && (o.front_lanes == 2 ||
-                                (o.front_lanes == 0 && g_live_handles.load(std::memory_order_relaxed) <= 1));
+                                (o.front_lanes == 0 && g_front_handles.load(std::memory_order_relaxed) <= 1));
     if (lanes && (rc = front_lanes_ready(o))) return rc;
     if (scan && o.lanes_used != (lanes ? 2 : 1)) {
         // a change of lane mode: the instances the other mode used may still be busy (host wait, once)
@@ -925,6 +930,10 @@ int pf_bpf_set_front_end(pf_odom* h, const pf_cls_params* p) {
         }
         o.front->sticky = o.errw + E_FRONT;                     // CC_ERR latches into the handle
         alias_err(o.front->grid.err, o.errw + E_FRONT_GRID);
+        if (!h->front_counted) {
+            h->front_counted = true;
+            g_front_handles.fetch_add(1);
+        }
     }
     o.front->prm = *p;
     if (o.front2) o.front2->prm = *p;

@@ -453,9 +453,11 @@ __constant__ constexpr int kClsRowOrder[9] = {0, 1, 2, 3, 4, 5, 6, 7, 8};
 __constant__ constexpr int kClsRowOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // row r = (oz + 1) * 3 + oy + 1
 #endif
 #ifndef PF_CLS_PHASES
-#define PF_CLS_PHASES 2
+#define PF_CLS_PHASES 1
 #endif
-constexpr int kClsPhases = PF_CLS_PHASES;   // 1: the nine rows in one pass of rounds (r03 before)
+// 2: the query's own row first, then the other eight re-cut by the k-th distance (fewer rounds and
+// chunks, but 281 vs 238 us in one A/B run: the phase loop costs more than the rounds it saves)
+constexpr int kClsPhases = PF_CLS_PHASES;
 constexpr int kBatch = PF_CLS_BATCH;   // winners in one pass above which the pass is merged as a whole
 __device__ __forceinline__ u64 readlane_u64(u64 v, int lane) {
     const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, lane);
@@ -541,6 +543,11 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
         };
         auto merge_batch = [&](u64 key) {                    // all keys of a pass below thr, at once
             u64 v = wave_sort_u64(key < thr ? key : ~0ull);
+            if (readlane_u64(ent, 0) == ~0ull) {             // empty list: the sorted batch's 32 smallest
+                ent = l < 32 ? v : ~0ull;
+                thr = readlane_u64(ent, K - 1);
+                return;
+            }
             const u64 rev = shfl_u64(v, 63 - l);             // lanes 32.. : the 32 smallest, descending
             v = l < 32 ? ent : rev;                          // bitonic: list ascending, keys descending
 #pragma unroll

@@ -197,7 +197,7 @@ struct OdomGPU {
 #ifndef PF_FRONT_LANES_DEFAULT
 #define PF_FRONT_LANES_DEFAULT 0
 #endif
-    int front_lanes = PF_FRONT_LANES_DEFAULT;   // 1, 2, or 0 = auto: 2 while the handle is alone on the host
+    int front_lanes = PF_FRONT_LANES_DEFAULT;   // 1, 2, or 0 = auto: 2 while it is the process's only raw-scan handle
     int lanes_used = 0;                         // the lane count of the last raw-scan frame (0: none yet)
     ClsGPU* front2 = nullptr;
     float4* stage2 = nullptr;                               // [kMaxC * in_cap]

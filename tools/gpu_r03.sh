@@ -5,7 +5,7 @@
 #   tools/gpu_r03.sh [bench] [prof] [cls] [stats] [conc] [pmc]   (default: all)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/r03
+OUT=$R/gpurun_out/${R03_OUT:-r03}
 mkdir -p $OUT
 cd $R
 export TMPDIR=/tmp
