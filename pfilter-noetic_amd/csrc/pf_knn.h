@@ -209,6 +209,10 @@ __device__ __forceinline__ int cell_of_checked(const int* dm, float4 p) {
 // way (the queries order candidates by (d^2, index)). Every point is also counted in its scan tile
 // (ttot, one atomic per distinct tile in a wave: consecutive points share a tile).
 // A Tail with kActive runs on one extra workgroup (the last), as in k_grid_bounds.
+#ifndef PF_GRID_AGG_RUNS
+#define PF_GRID_AGG_RUNS 4
+#endif
+constexpr int kGridAggRuns = PF_GRID_AGG_RUNS;   // runs of equal cells per wave taken by one atomic each
 template <bool Agg, class Tail>
 __global__ void __launch_bounds__(256) k_grid_count(GridPtrs gp, const int* __restrict__ dims, u32* __restrict__ cnt,
                                                      u32* __restrict__ slot, u32* __restrict__ ttot,
@@ -246,7 +250,7 @@ __global__ void __launch_bounds__(256) k_grid_count(GridPtrs gp, const int* __re
             continue;
         }
         u64 todo = __ballot(cid >= 0);
-        for (int it = 0; it < 4 && todo; ++it) {          // wave-uniform
+        for (int it = 0; it < kGridAggRuns && todo; ++it) {   // wave-uniform
             const int leader = __ffsll((unsigned long long)todo) - 1;
             const int c = __shfl(cid, leader, 64);
             const u64 m = __ballot(cid == c) & todo;

@@ -13,6 +13,6 @@ for v in tree "$@"; do
     PFILTER_HIP_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/$v -o run --output-format csv -- \
         python3 tools/cls_probe.py --iters 50 > $OUT/$v.log 2>&1 || { echo "$v failed"; tail -5 $OUT/$v.log; exit 1; }
     echo "== $v: $(grep ms/frame $OUT/$v.log)"
-    python3 tools/kstats.py $(find $OUT/$v -name "*kernel_stats.csv" | head -1) 3
+    python3 tools/kstats.py $(find $OUT/$v -name "*kernel_stats.csv" | head -1) 5
     find $OUT/$v -name "*_kernel_trace.csv" -delete
 done
