@@ -452,6 +452,9 @@ __constant__ constexpr int kClsRowOrder[9] = {0, 1, 2, 3, 4, 5, 6, 7, 8};
 #else
 __constant__ constexpr int kClsRowOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // row r = (oz + 1) * 3 + oy + 1
 #endif
+#ifndef PF_CLS_MINX
+#define PF_CLS_MINX 0
+#endif
 #ifndef PF_CLS_PHASES
 #define PF_CLS_PHASES 1
 #endif
@@ -643,6 +646,26 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                 u64 om = __ballot(sk != ~0u);
                 const int nopen = __popcll(om);
                 CLS_STAT(3, nopen);
+#if PF_CLS_MINX
+                // nearest first without the sort: each pass takes the four smallest open bounds by
+                // wave minima (a key's low 6 bits are its lane, so the minimum names its lane)
+                u32 rem = sk;
+                auto take_min = [&]() {
+                    u32 m = rem;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const u32 v = (u32)__shfl_xor((int)m, o, 64);
+                        m = v < m ? v : m;
+                    }
+                    m = (u32)__builtin_amdgcn_readfirstlane((int)m);
+                    if (m != ~0u && l == (int)(m & 0x3Fu)) rem = ~0u;
+                    return m;
+                };
+                if (!om) continue;
+                const bool few = false;
+                u32 f0 = ~0u, f1 = ~0u, f2 = ~0u, f3 = ~0u;
+                (void)f0; (void)f1; (void)f2; (void)f3;
+#else
                 // up to one pass of open chunks: read them as they lie (no sort); else nearest first
                 const bool few = nopen <= kClsNoSort;
                 u32 f0 = ~0u, f1 = ~0u, f2 = ~0u, f3 = ~0u;
@@ -658,8 +681,18 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                 } else {
                     sk = wave_sort_u32(sk);
                 }
+#endif
                 auto lb_of = [](u32 k) { return __uint_as_float(k & ~0x3Fu); };
                 for (int i = 0; i < nopen; i += 4) {
+#if PF_CLS_MINX
+                    const u32 k0 = take_min();
+                    if (!open(lb_of(k0))) break;                   // ascending: the rest are closed too
+                    const u32 k1 = i + 1 < nopen ? take_min() : ~0u;
+                    const u32 k2 = i + 2 < nopen ? take_min() : ~0u;
+                    const u32 k3 = i + 3 < nopen ? take_min() : ~0u;
+                    const int j = i + (l >> 4);
+                    CLS_STAT(4, 1);
+#else
                     // sorted: a closed chunk closes the rest too
                     if (!few && !open(lb_of((u32)__builtin_amdgcn_readlane((int)sk, i)))) break;
                     const int j = i + (l >> 4);
@@ -668,6 +701,7 @@ __global__ void __launch_bounds__(256) k_cls_search(ClsDev d, GridView gv, u32* 
                     const u32 k1 = few ? f1 : (u32)__builtin_amdgcn_readlane((int)sk, i + 1 < 64 ? i + 1 : 63);
                     const u32 k2 = few ? f2 : (u32)__builtin_amdgcn_readlane((int)sk, i + 2 < 64 ? i + 2 : 63);
                     const u32 k3 = few ? f3 : (u32)__builtin_amdgcn_readlane((int)sk, i + 3 < 64 ? i + 3 : 63);
+#endif
                     const u32 sj = (l >> 4) == 1 ? k1 : ((l >> 4) == 2 ? k2 : ((l >> 4) == 3 ? k3 : k0));
                     u64 key = ~0ull;
                     if (j < nopen && open(lb_of(sj))) {
@@ -823,9 +857,7 @@ int cls_set_dcvc(ClsGPU& c, const pf_dcvc_params* p) {
         }
         return PF_OK;
     }
-    if (!(p->delta_p > 0) || !(p->delta_a > 0) || !(p->start_r > 0) || p->delta_r < 0 || !(p->max_range > 0) ||
-        p->max_range >= 1e5 || p->min_seg < 0)
-        return PF_EINVAL;
+    if (!dcvc_params_valid(p)) return PF_EINVAL;
     if (!c.dcvc) {
         c.dcvc = new DcvcGPU();
         int rc = dcvc_alloc(*c.dcvc, c.cap);

@@ -73,6 +73,9 @@ int dcvc_reset(DcvcGPU& d, hipStream_t s);
 // as after one call: the next run is not the first (its range bounds start from 0, not the member
 // defaults); the second front-end lane of a BPF handle (pf_odom.h OdomGPU::front2)
 int dcvc_mark_called(DcvcGPU& d, hipStream_t s);
+// the parameter check of pf_dcvc_create: positive steps and a ring width start_r - k delta_r that
+// stays positive up to max_range within the bound table (else a frame would overflow it)
+bool dcvc_params_valid(const pf_dcvc_params* p);
 
 // DCVC of pts[0 .. *d_n) (float4 x, y, z, any). Result: kept point indices in the published order at
 // *out_idx (device, dim[D_NKEPT] of them), per point label in plab. Enqueued on s, no host round trip.

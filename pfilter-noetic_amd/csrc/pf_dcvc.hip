@@ -530,6 +530,10 @@ bool dcvc_params_ok(const pf_dcvc_params* p) {
 }
 }  // namespace
 
+namespace pf {
+bool dcvc_params_valid(const pf_dcvc_params* p) { return dcvc_params_ok(p); }
+}  // namespace pf
+
 extern "C" {
 
 void pf_dcvc_default_params(pf_dcvc_params* p) {

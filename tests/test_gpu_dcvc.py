@@ -181,3 +181,19 @@ def test_dcvc_rejects_rings_that_never_reach_max_range(pa):
         pa.Dcvc(max_points=1000, max_range=200.0)
     assert ei.value.code == pa.PF_EINVAL
     pa.Dcvc(max_points=1000, max_range=150.0)
+
+
+def test_front_end_dcvc_rejects_rings_that_never_reach_max_range(pa):
+    """The same parameter check for the curvedfilter inside the front end and the BPF pipeline
+    (pf_cls_set_dcvc / pf_bpf_set_dcvc), so an accepted configuration cannot overflow the ring bounds
+    on every frame."""
+    fe = pa.BPFFrontEnd(max_points=1000, device=0)
+    with pytest.raises(pa.PFError) as ei:
+        fe.set_dcvc(True, max_range=200.0)
+    assert ei.value.code == pa.PF_EINVAL
+    fe.set_dcvc(True, max_range=150.0)
+    od = pa.Odom_BPF_EstimationClass(device=0)
+    od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    with pytest.raises(pa.PFError) as ei:
+        od.set_dcvc(True, max_range=200.0)
+    assert ei.value.code == pa.PF_EINVAL
