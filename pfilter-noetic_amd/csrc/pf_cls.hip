@@ -453,7 +453,7 @@ __constant__ constexpr int kClsRowOrder[9] = {0, 1, 2, 3, 4, 5, 6, 7, 8};
 __constant__ constexpr int kClsRowOrder[9] = {4, 1, 3, 5, 7, 0, 2, 6, 8};   // row r = (oz + 1) * 3 + oy + 1
 #endif
 #ifndef PF_CLS_MINX
-#define PF_CLS_MINX 0
+#define PF_CLS_MINX 0   // 1: passes take their chunks by wave minima, no round sort (266.6 vs 238.3 us, off)
 #endif
 #ifndef PF_CLS_PHASES
 #define PF_CLS_PHASES 1
