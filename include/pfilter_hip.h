@@ -228,6 +228,9 @@ int pf_dcvc_run(pf_dcvc* h, const float* xyz, size_t n, size_t stride_bytes, int
                 int32_t* label, size_t cap);
 /* the next call is a first call again (a new sequence) */
 int pf_dcvc_reset(pf_dcvc* h);
+/* grows the point capacity to max_points (no-op when already that large), keeping the call state: a
+ * run after it is still a later call (curvedVoxel's members persist across scans) */
+int pf_dcvc_reserve(pf_dcvc* h, size_t max_points);
 /* curvedfilter in the front end: DCVC runs on the non-ground cloud and featureExtract on its output
  * (src/additionNode.cpp:29-39); p NULL turns it off (the default) */
 int pf_cls_set_dcvc(pf_cls* h, const pf_dcvc_params* p);
@@ -315,20 +318,24 @@ int pf_odom_map_export(pf_odom* h, int which, const float** xyzw, size_t* n);
  * end / VoxelGrid stage) and PF_GRAPH_STAGE_B (the odometry stage), 0 = eager launches, or
  * PF_GRAPH_AUTO (the default): stage A replays its graph; stage B launches eagerly while this is the
  * process's only handle and replays its graph when several handles share the host's launch path.
+ * The mode was a boolean before the per-stage bits existed; 1 (a caller's "true") is PF_GRAPH_AUTO and
+ * the stage bits do not overlap it.
  * Measured on MI355X (configs[1], 4521 frames): a graph replay costs about 0.4 us more per kernel
  * boundary than eager launches (tools/mb/graph_gap.hip) and stage B is the critical path, so one
  * sequence runs 4525-4557 frames/s with stage B eager against 4404-4452 with both graphs; four
  * concurrent handles (configs[3]) run 6558 frames/s with both graphs against 5459 with stage B
  * eager (their host threads contend on the launch path). */
-#define PF_GRAPH_STAGE_A 1
-#define PF_GRAPH_STAGE_B 2
-#define PF_GRAPH_AUTO 4
+#define PF_GRAPH_AUTO 1
+#define PF_GRAPH_STAGE_A 2
+#define PF_GRAPH_STAGE_B 4
 int pf_odom_set_graph(pf_odom* h, int mode);
 /* Reference tie order (default off): VoxelGrid (stage A) and rgbds (stage B) order the points of a
  * voxel as libstdc++'s std::sort leaves them -- the reference's own sorts (PCL 1.10 VoxelGrid, SURVEY
  * B.1; src/odomEstimationClass.cpp:74), which are not stable -- instead of in input order, so that every
- * f32 centroid is summed in the reference's order. A parity mode: it runs introsort's recursion levels
- * on the device (a few ms per frame); off, the sorts are stable radix sorts. */
+ * f32 centroid is summed in the reference's order. It runs introsort's recursion on the device
+ * (pf_tie.h: tile-parallel partitions for segments above 14336 keys, the rest of every subtree in LDS)
+ * in place of the radix sorts; off, the sorts are stable radix sorts (VoxelGrid) and a merge of the
+ * voxel-ordered map with the sorted appended points (rgbds). */
 int pf_odom_set_tie_order(pf_odom* h, int enable);
 /* Measurement: the association's kNN alone (the exact 5-NN of k_assoc, src/odomEstimationClass.cpp:299,
  * 447) on the last frame's queries -- its down-sampled points through the solved pose -- against the
@@ -341,8 +348,8 @@ int pf_odom_probe_assoc(pf_odom* h, int iters, double* avg_ms, double* alg_bytes
 /* rgbds bookkeeping (the default order merges this frame's sorted appended points into the map, which
  * stays in voxel order): how many updates since create / reset had to sort every element instead (the
  * first update after initMapWithPoints or pf_odom_set_map, a centroid that rounded into a neighbouring
- * voxel, or more than 65536 appended points), and the largest appended-point count seen. Waits for
- * the handle's work. */
+ * voxel, or more than 2048 appended points falling into one of the 512 map-key buckets), and the
+ * largest appended-point count seen. Waits for the handle's work. */
 int pf_odom_merge_stats(pf_odom* h, int* full_sorts, int* max_appended);
 /* Per-stage device time (the reference's per-stage timers, src/laserProcessingNode.cpp:71-79 and
  * src/odomEstimationNode copy.cpp:92-100, as HIP events on the handle's two streams): with enable,

@@ -790,6 +790,20 @@ static int enqueue_frame(pf_odom* h, const float4* d_in, size_t n, const float4*
     }
     PF_HT(0, rc = stage_a_begin(h, p));
     if (rc) return rc;
+    if (scan && o.dcvc_first && o.front->dcvc) {
+        // the first curvedfilter frame since DCVC was enabled / reset: the instance of the lane that runs
+        // it starts as never called (the reference's 5 m ring start, .hpp:105-106), every other instance
+        // as called before, whichever lane the frame count gives: the reference has one curvedVoxel.
+        // Each word is written on the stream of the lane that reads it, ahead of that lane's next frame.
+        const int lane = lanes ? (o.frames & 1) : 0;
+        ClsGPU* inst[2] = {o.front, o.front2};
+        for (int q = 0; q < 2; ++q) {
+            if (!inst[q] || !inst[q]->dcvc) continue;
+            hipStream_t qs = lanes ? o.stream_f[q] : o.stream_a;
+            if ((rc = q == lane ? dcvc_reset(*inst[q]->dcvc, qs) : dcvc_mark_called(*inst[q]->dcvc, qs))) return rc;
+        }
+        o.dcvc_first = false;
+    }
     if (lanes) {
         // the front end on lane (frame & 1) once slot p is free, then VoxelGrid on stream_a in frame
         // order after it: two consecutive frames' front ends run at once
@@ -893,8 +907,10 @@ int pf_odom_frame_host(pf_odom* h, const float* xyzi, size_t n, size_t stride_by
     int rc = host_upload(o, p, 1, &xyzi, &n, &stride_bytes, &direct);
     if (rc) return rc;
     rc = enqueue_frame(h, o.hs->d[p], n, nullptr, nullptr);
+    // direct: a DMA from the caller's own pinned buffer is queued; the header lets the caller reuse the
+    // buffer once this returns, so wait for that copy on the error path too
+    if (direct && hipEventSynchronize(o.hs->ev[p]) != hipSuccess && !rc) rc = PF_EHIP;
     if (rc) return rc;
-    if (direct) PF_HIP_TRY(hipEventSynchronize(o.hs->ev[p]));
     if (pose_out) return read_pose(h, pose_out);
     return PF_OK;
 }
@@ -957,7 +973,9 @@ int pf_bpf_set_dcvc(pf_odom* h, const pf_dcvc_params* p) {
         if (rc) return rc;
     }
     PF_HIP_TRY(odom_sync_a(o));
+    const bool was_on = o.front->dcvc != nullptr;
     int rc = cls_set_dcvc(*o.front, p);
+    if (!rc) o.dcvc_first = p && (!was_on || o.dcvc_first);    // a fresh instance: its first call is next
     if (!rc && o.front2) {
         const bool fresh = p && !o.front2->dcvc;
         rc = cls_set_dcvc(*o.front2, p);
@@ -1353,51 +1371,69 @@ extern "C" int pf_dev_set_rg_radix(pf_odom* h, int enable) {
 }
 
 // development / test probe (not part of include/pfilter_hip.h): the reference-tie-order sort alone on
-// n host keys (bits 30-31 the class, 0xFFFFFFFF dropped); perm receives the vals (input indices) of the
-// kept pairs in std::sort's order, *n_out their count
-extern "C" int pf_dev_tie_sort(int device, const uint32_t* keys, size_t n, uint32_t* perm, size_t* n_out) {
-    if ((!keys && n) || !perm || !n_out || n > (size_t)INT_MAX / 2) return PF_EINVAL;
+// n host keys (bits 30-31 the class, classes back to back as the pipeline's batches hold them,
+// 0xFFFFFFFF dropped anywhere); perm receives the vals (input indices) of the kept pairs in std::sort's
+// order, *n_out their count. PF_EINVAL when the valid keys are not class-major.
+// depth >= 0 replaces the depth limit 2 lg n of every class (the heap-sort branch, against the oracle's
+// settable-depth restatement), levels = the big levels before the single-workgroup fallback.
+extern "C" int pf_dev_tie_sort2(int device, const uint32_t* keys, size_t n, int depth, int levels, uint32_t* perm,
+                                size_t* n_out) {
+    if ((!keys && n) || !perm || !n_out || n > (size_t)INT_MAX / 2 || levels < 0 || levels > 6) return PF_EINVAL;
+    int sizes[4] = {0, 0, 0, 0};
+    {
+        int end[4] = {0, 0, 0, 0};                 // one past the last valid key of class <= c
+        int prev = 0;
+        for (size_t i = 0; i < n; ++i) {
+            if (keys[i] == 0xFFFFFFFFu) continue;
+            const int c = (int)(keys[i] >> 30);
+            if (c < prev) return PF_EINVAL;
+            prev = c;
+            for (int q = c; q < 4; ++q) end[q] = (int)i + 1;
+        }
+        end[3] = (int)n;
+        for (int c = 0; c < 4; ++c) sizes[c] = end[c] - (c ? end[c - 1] : 0);
+    }
     PF_HIP_TRY(hipSetDevice(device));
     const size_t cap = n ? n : 1;
     TieSort t;
-    PrimWork w;
     u32 *dk = nullptr, *dv = nullptr;
-    int* dn = nullptr;
+    int* dsz = nullptr;
     hipStream_t s = nullptr;
-    int rc = tie_alloc(t, cap);
-    if (!rc) rc = prim_alloc(w, cap);
+    int rc = tie_alloc(t, cap, levels);
+    t.depth0 = depth;
     if (!rc && (hipMalloc(&dk, sizeof(u32) * cap) != hipSuccess || hipMalloc(&dv, sizeof(u32) * cap) != hipSuccess ||
-                hipMalloc(&dn, sizeof(int)) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess))
+                hipMalloc(&dsz, sizeof(int) * 8) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess))
         rc = PF_ENOMEM;
     std::vector<u32> iota(cap);
     for (size_t i = 0; i < cap; ++i) iota[i] = (u32)i;
-    const int ni = (int)n;
+    int hsz[8] = {sizes[0], sizes[1], sizes[2], sizes[3], 0, 0, 0, 0};
     if (!rc && (hipMemcpyAsync(dk, keys, sizeof(u32) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
                 hipMemcpyAsync(dv, iota.data(), sizeof(u32) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-                hipMemcpyAsync(dn, &ni, sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess))
+                hipMemcpyAsync(dsz, hsz, sizeof(hsz), hipMemcpyHostToDevice, s) != hipSuccess))
         rc = PF_EHIP;
     if (!rc) {
-        tie_sort_enqueue(t, dk, dv, dn, w, s);
-        tie_sort_finish(t, dk, dv, s);
-        int cnt[8];
-        if (hipMemcpyAsync(cnt, t.cnt, sizeof(cnt), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        tie_sort(t, dk, dv, TieClasses{dsz, 0, -1, 4}, dsz + 4, s);
+        int nv = 0, err = 0;
+        if (hipMemcpyAsync(&nv, tie_valid_count(t), sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(&err, dsz + 4, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             rc = PF_EHIP;
         else {
-            *n_out = (size_t)(u32)cnt[5];
-            if (*n_out && (hipMemcpy(perm, dv, sizeof(u32) * *n_out, hipMemcpyDeviceToHost) != hipSuccess)) rc = PF_EHIP;
+            *n_out = (size_t)nv;
+            if (err) rc = PF_EHIP;
+            else if (nv && (hipMemcpy(perm, dv, sizeof(u32) * (size_t)nv, hipMemcpyDeviceToHost) != hipSuccess)) rc = PF_EHIP;
         }
-        int err = 0;
-        if (!rc && hipMemcpy(&err, w.err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess && err) rc = PF_EHIP;
     }
     if (s) (void)hipStreamSynchronize(s);
     (void)hipFree(dk);
     (void)hipFree(dv);
-    (void)hipFree(dn);
+    (void)hipFree(dsz);
     if (s) (void)hipStreamDestroy(s);
     tie_free(t);
-    prim_free(w);
     return rc;
+}
+extern "C" int pf_dev_tie_sort(int device, const uint32_t* keys, size_t n, uint32_t* perm, size_t* n_out) {
+    return pf_dev_tie_sort2(device, keys, n, -1, 2, perm, n_out);
 }
 
 int pf_odom_probe_assoc(pf_odom* h, int iters, double* avg_ms, double* alg_bytes, size_t* nq, float* queries,
@@ -1424,7 +1460,7 @@ int pf_odom_merge_stats(pf_odom* h, int* full_sorts, int* max_appended) {
 }
 
 int pf_odom_set_graph(pf_odom* h, int mode) {
-    if (!h || mode < 0 || mode > PF_GRAPH_AUTO) return PF_EINVAL;
+    if (!h || !(mode == PF_GRAPH_AUTO || (mode & ~(PF_GRAPH_STAGE_A | PF_GRAPH_STAGE_B)) == 0)) return PF_EINVAL;
     h->o.graph_mode = mode;
     return PF_OK;
 }

@@ -607,6 +607,25 @@ int pf_dcvc_reset(pf_dcvc* h) {
     return PF_OK;
 }
 
+int pf_dcvc_reserve(pf_dcvc* h, size_t max_points) {
+    if (!h || max_points == 0 || max_points > (size_t)INT_MAX / 2) return PF_EINVAL;
+    if (max_points <= h->g.cap) return PF_OK;
+    PF_HIP_TRY(hipSetDevice(h->device));
+    PF_HIP_TRY(hipStreamSynchronize(h->stream));
+    int calls = 0;                                   // the call state survives the re-allocation
+    PF_HIP_TRY(hipMemcpy(&calls, h->g.dim + D_CALLS, sizeof(int), hipMemcpyDeviceToHost));
+    const pf_dcvc_params prm = h->g.prm;
+    dcvc_free(h->g);
+    (void)hipFree(h->d_pts);
+    h->d_pts = nullptr;
+    h->g.prm = prm;
+    int rc = dcvc_alloc(h->g, max_points);
+    if (rc == PF_OK) rc = dcvc_set_params(h->g, prm);
+    if (rc == PF_OK && hipMalloc(&h->d_pts, sizeof(float4) * max_points) != hipSuccess) rc = PF_ENOMEM;
+    if (rc == PF_OK && hipMemcpy(h->g.dim + D_CALLS, &calls, sizeof(int), hipMemcpyHostToDevice) != hipSuccess) rc = PF_EHIP;
+    return rc;
+}
+
 int pf_dcvc_run(pf_dcvc* h, const float* xyz, size_t n, size_t stride_bytes, int32_t* out_idx, size_t* n_out,
                 int32_t* label, size_t cap) {
     if (!h || (!xyz && n) || stride_bytes < 12) return PF_EINVAL;

@@ -199,6 +199,8 @@ struct OdomGPU {
 #endif
     int front_lanes = PF_FRONT_LANES_DEFAULT;   // 1, 2, or 0 = auto: 2 while it is the process's only raw-scan handle
     int lanes_used = 0;                         // the lane count of the last raw-scan frame (0: none yet)
+    bool dcvc_first = false;                    // no curvedfilter frame since DCVC was enabled / reset: the
+                                                // next one starts the reference's single instance (first call)
     ClsGPU* front2 = nullptr;
     float4* stage2 = nullptr;                               // [kMaxC * in_cap]
     hipStream_t stream_f[2] = {};

@@ -3046,6 +3046,7 @@ int odom_reset(OdomGPU& o) {
     if (o.front && o.front->dcvc && dcvc_reset(*o.front->dcvc, o.stream) != PF_OK) return PF_EHIP;   // a first frame again
     if (o.front2 && o.front2->dcvc && dcvc_mark_called(*o.front2->dcvc, o.stream) != PF_OK) return PF_EHIP;
     if (hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
+    o.dcvc_first = o.front && o.front->dcvc;
     o.opt_count_host = 2;
     o.inited = false;
     o.dims_fresh = false;
@@ -3153,9 +3154,10 @@ void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s) {
     PF_LAUNCH_NC(nc, k_vg_minmax, dim3(128), dim3(256), 0, s, clouds(sb.in), cnt, o.acc_a);
     PF_LAUNCH_NC(nc, k_vg_keys, dim3(kGrid), dim3(256), 0, s, clouds(sb.in), cnt, o.acc_a, leaf, o.vkeys, o.vvals,
                  sort_hist(o.vprim, 32, true));
-    if (o.tie_order) tie_sort_enqueue(*o.tie_a, o.vkeys, o.vvals, cnt + C_VGN, o.vprim, s);
-    radix_sort_pairs(o.vkeys, o.vvals, cnt + C_VGN, 32, o.vprim, s, nullptr, nullptr, true);
-    if (o.tie_order) tie_sort_finish(*o.tie_a, o.vkeys, o.vvals, s);      // std::sort's order of equal keys
+    if (o.tie_order)                       // std::sort's order of equal keys (PCL VoxelGrid, B.1)
+        tie_sort(*o.tie_a, o.vkeys, o.vvals, TieClasses{cnt, C_IN, -1, nc}, o.vprim.err, s);
+    else
+        radix_sort_pairs(o.vkeys, o.vvals, cnt + C_VGN, 32, o.vprim, s, nullptr, nullptr, true);
     segment_starts(o.vkeys, cnt + C_VGN, o.vsegstart, cnt + C_NSEG, cnt + C_NLT, cnt + C_NRG_VALID, o.vprim, s);
     PF_LAUNCH_NC(nc, k_vg_reduce, dim3(kGrid * 4), dim3(256), 0, s, clouds(sb.in), o.vkeys, o.vvals, o.vsegstart, cnt,
                  clouds_w(sb.ds));
@@ -3248,9 +3250,10 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
         PF_LAUNCH_NC(nc, k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, clouds(map_cur(o)), clouds(o.app),
                      leaf, o.keys, o.vals, sort_hist(o.prim, 32, true));
     }
-    if (o.tie_order) tie_sort_enqueue(*o.tie_b, o.keys, o.vals, cnt + C_NRG, o.prim, s);
-    radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
-    if (o.tie_order) tie_sort_finish(*o.tie_b, o.keys, o.vals, s);        // std::sort's order (:74)
+    if (o.tie_order)                       // std::sort's order of equal keys (:74)
+        tie_sort(*o.tie_b, o.keys, o.vals, TieClasses{cnt, C_M, C_DS, nc}, o.prim.err, s);
+    else
+        radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
     RgTailArgs ta{cnt, clouds(map_cur(o)), clouds(o.app), o.keys, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,
                   o.prm.theta_max, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err};
     const unsigned tail_grid = (unsigned)(o.tail_tiles < (size_t)kSortMaxBlocks ? o.tail_tiles : kSortMaxBlocks);

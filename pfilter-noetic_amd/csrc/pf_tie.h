@@ -4,45 +4,67 @@
 // 1.10's VoxelGrid and in rgbds (src/odomEstimationClass.cpp:74), then sums every voxel's
 // points in f32 in the sorted order, so a centroid's last bits depend on how introsort happened to
 // permute the points of its voxel. The pipeline's radix sorts are stable (points of a voxel in input
-// order); this mode reproduces introsort's permutation instead, so that VoxelGrid and rgbds centroids
+// order); this mode runs libstdc++'s introsort itself instead, so that VoxelGrid and rgbds centroids
 // are the reference's bit for bit (the faithful oracle's, which calls std::sort itself).
 //
-// Introsort's segments never interact, so every partition of one recursion level runs at once (one
-// wavefront per segment): a Hoare partition of [first + 1, last) around the median-of-three pivot at
-// first is computed from the ascending positions L_1 < L_2 < ... of its left stops (key >= pivot) and
-// R_1 < R_2 < ... of its right stops (key <= pivot, first included): with m the largest k for which
-// L_k < R_(nR + 1 - k), the partition swaps L_k <-> R_(nR + 1 - k) for k <= m and returns
-// min(L_(m + 1), R_(nR + 1 - m)) (L_1 for m = 0). Segments that reach the depth limit 2 lg(n) are
-// heap-sorted by libstdc++'s make_heap / sort_heap (one thread each), and the final insertion sort is
-// a stable insertion sort inside every leaf of at most 16 elements. oracle/pfref_sort.cpp holds the
-// same algorithm on the CPU, checked against std::sort itself (tests/test_oracle_units.py).
+// A Hoare partition of [first + 1, last) around the median-of-three pivot at first is computed from
+// the ascending positions L_1 < L_2 < ... of its left stops (key >= pivot) and R_1 < R_2 < ... of its
+// right stops (key <= pivot, first included): with m the largest k for which L_k < R_(nR + 1 - k), the
+// partition swaps L_k <-> R_(nR + 1 - k) for k <= m and returns min(L_(m + 1), R_(nR + 1 - m)) (L_1 for
+// m = 0). Introsort's segments never interact, so the recursion runs breadth-first:
+//   k_tie_compact   drops the 0xFFFFFFFF keys (cropped points) per class, one pass with a look-back;
+//   big levels      segments above kTieLocal keys: every tile of 4096 keys of every segment finds its
+//                   stops in parallel (a look-back per segment ranks them), then one workgroup per
+//                   segment searches m, swaps the pairs and files the children;
+//   k_tie_local     one workgroup per segment of at most kTieLocal keys finishes its whole subtree in
+//                   LDS, one wavefront per segment per recursion level; leaves of at most 16 keys are
+//                   sorted stably (libstdc++'s final insertion sort moves no key across a leaf), the
+//                   depth limit 2 lg n hands a segment to libstdc++'s heap sort. Segments still above
+//                   kTieLocal after the big levels (very large classes) are partitioned by their
+//                   workgroup in global memory until they fit.
+// oracle/pfref_sort.cpp holds the same algorithm on the CPU next to a line-by-line restatement of
+// libstdc++'s introsort, both checked against std::sort itself (tests/test_oracle_units.py).
 #pragma once
 #include "pf_prims.h"
 
 namespace pf {
 
-struct TieSort {
-    u32 *k = nullptr, *v = nullptr;       // [cap] the pairs being sorted (compacted, class-major)
-    u32 *flag = nullptr, *pos = nullptr;  // [cap + 1] compaction: valid flags and their exclusive scan
-    int4* seg[3] = {};                    // [scap] segment lists {first, last, depth}, rotating per level
-    int4* heap = nullptr;                 // [scap] segments at the depth limit
-    int2* leaf = nullptr;                 // [cap / 2 + 8] leaves {first, last} of 2 .. 16 elements
-    int *lp = nullptr, *rq = nullptr;     // [cap] left / right stop positions per segment
-    int* cnt = nullptr;                   // [8]: segment counts 0-2, leaves 3, heaps 4, valid pairs 5
-    size_t cap = 0, scap = 0;
-    int levels = 0;                       // level launches: 2 floor(lg(cap)) + 2
+constexpr int kTieLocal = 14336;      // largest segment sorted in LDS (10 B per key)
+constexpr int kTieTile = 4096;        // keys per tile of the compaction and the big levels
+
+// class c of the input is its next cnt[ia + c] (+ cnt[ib + c] when ib >= 0) pairs, c < nc: the
+// reference sorts every cloud with its own std::sort call
+struct TieClasses {
+    const int* cnt;
+    int ia, ib, nc;
 };
 
-int tie_alloc(TieSort& t, size_t cap);
+struct TieSort {
+    u32 *k = nullptr, *v = nullptr;       // [cap] compacted pairs, class-major (the working copy)
+    u32 *lp = nullptr, *rq = nullptr;     // [cap] left / right stop positions of the big partitions
+    u64* status = nullptr;                // [tiles] look-back words, zero between launches
+    u32* arrive = nullptr;                // [2] look-back arrival counters
+    int4* big = nullptr;                  // [2][bcap] big segments of a level {first, last, depth, tile base}
+    u64* tot = nullptr;                   // [bcap] stop totals of a big segment (nL << 32 | nR)
+    int4* jobs = nullptr;                 // [jcap] local jobs {first, last, depth, 0}
+    int* ctl = nullptr;                   // counters (pf_tie.hip)
+    size_t cap = 0, tiles = 0;
+    int bcap = 0, jcap = 0;
+    int levels = 0;                       // big levels launched per sort
+    int depth0 = -1;                      // test probe: >= 0 replaces every class's depth limit
+};
+
+// cap: most pairs of one sort; levels: big levels per sort (classes up to about 2^levels x kTieLocal
+// keys are sorted without the single-workgroup fallback)
+int tie_alloc(TieSort& t, size_t cap, int levels = 2);
 void tie_free(TieSort& t);
 
-// tie_sort_enqueue sorts the pairs (keys, vals)[0 .. *d_n) as std::sort would, each class (key bits
-// 30-31) on its own (the reference's separate calls per cloud), 0xFFFFFFFF keys (cropped points)
-// dropped: enqueue it before the pipeline's stable radix sort of the same pairs (it reads them
-// unsorted). tie_sort_finish, enqueued after that sort, writes the result over its output's first
-// (valid count) pairs: the same keys, the vals of equal keys in std::sort's order. `w`: the stream's
-// sort / scan scratch (its scan words only).
-void tie_sort_enqueue(TieSort& t, const u32* keys, const u32* vals, const int* d_n, PrimWork& w, hipStream_t s);
-void tie_sort_finish(TieSort& t, u32* keys_out, u32* vals_out, hipStream_t s);
+// Sorts (keys, vals)[0 .. n) in place, n = the classes' total, each class as std::sort would (keys
+// compared as whole 32-bit words), the 0xFFFFFFFF pairs dropped from the classes and the key array
+// ended by them: keys[0 .. valid) sorted class after class, keys[valid .. n) = 0xFFFFFFFF (their
+// vals too). Replaces a stable radix sort of the same pairs. A look-back wait that gives up sets bit 2
+// of *err (the caller's sticky error word).
+void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s);
+const int* tie_valid_count(const TieSort& t);   // device word: the valid pairs of the last sort
 
 }  // namespace pf

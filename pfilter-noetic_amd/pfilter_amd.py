@@ -139,7 +139,7 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_odom_stage_times", "pf_odom_set_state", "pf_cls_normals", "pf_dcvc_default_params",
            "pf_dcvc_create", "pf_dcvc_destroy", "pf_dcvc_run", "pf_dcvc_reset", "pf_cls_set_dcvc", "pf_bpf_set_dcvc",
            "pf_host_alloc", "pf_host_free", "pf_odom_set_tie_order", "pf_odom_probe_assoc",
-           "pf_odom_merge_stats", "pf_bpf_set_front_lanes"]
+           "pf_odom_merge_stats", "pf_bpf_set_front_lanes", "pf_dcvc_reserve"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -203,6 +203,7 @@ def lib():
                                       ctypes.POINTER(_sz), _vp, _sz]
     L.pf_odom_merge_stats.argtypes = [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]
     L.pf_dev_tie_sort.argtypes = [_i, _vp, _sz, _vp, ctypes.POINTER(_sz)]
+    L.pf_dev_tie_sort2.argtypes = [_i, _vp, _sz, _i, _i, _vp, ctypes.POINTER(_sz)]
     L.pf_host_alloc.argtypes = [_sz, ctypes.POINTER(_vp)]
     L.pf_host_free.argtypes = [_vp]
     L.pf_knn_create.argtypes = [_i, _sz, _sz, ctypes.POINTER(_vp)]
@@ -267,14 +268,16 @@ def make_lidar(num_lines=64, min_dist=3.0, max_dist=90.0, scan_period=0.1, ring_
     return lp
 
 
-def tie_sort(keys, device=0):
-    """development probe pf_dev_tie_sort: the input indices of the kept keys (not 0xFFFFFFFF) in the
-    order the device's reference-tie-order sort (libstdc++ std::sort per class, bits 30-31) puts them"""
+def tie_sort(keys, device=0, depth=-1, levels=2):
+    """development probe pf_dev_tie_sort2: the input indices of the kept keys (not 0xFFFFFFFF) in the
+    order the device's reference-tie-order sort (libstdc++ std::sort per class, bits 30-31, classes back
+    to back) puts them. depth >= 0 replaces the depth limit 2 lg n (the heap-sort branch); levels = big
+    levels before the single-workgroup fallback."""
     k = np.ascontiguousarray(keys, np.uint32)
     out = np.empty(max(k.size, 1), np.uint32)
     n = _sz()
-    _check("pf_dev_tie_sort", lib().pf_dev_tie_sort(device, k.ctypes.data, k.size, out.ctypes.data, ctypes.byref(n)),
-           allow_warn=False)
+    _check("pf_dev_tie_sort2", lib().pf_dev_tie_sort2(device, k.ctypes.data, k.size, int(depth), int(levels),
+                                                      out.ctypes.data, ctypes.byref(n)), allow_warn=False)
     return out[:n.value].copy()
 
 
@@ -485,7 +488,12 @@ class Odom_ES_EstimationClass:
         """hipGraph replay per stage (pf_odom_set_graph): 1 = stage A, 2 = stage B, 3 = both, 0 / False
         = eager launches, 4 / True = PF_GRAPH_AUTO (the default: stage A, and stage B when the process
         holds several handles)"""
-        _check("pf_odom_set_graph", lib().pf_odom_set_graph(self._h, 4 if mode is True else int(mode)))
+        # this wrapper's numbering -> the C constants (PF_GRAPH_AUTO 1, PF_GRAPH_STAGE_A 2, _STAGE_B 4)
+        m = 4 if mode is True else int(mode)
+        if m not in (0, 1, 2, 3, 4):
+            raise ValueError("graph mode %r" % (mode,))
+        c = 1 if m == 4 else ((2 if m & 1 else 0) | (4 if m & 2 else 0))
+        _check("pf_odom_set_graph", lib().pf_odom_set_graph(self._h, c))
 
     def set_stage_timing(self, enable):
         _check("pf_odom_set_stage_timing", lib().pf_odom_set_stage_timing(self._h, int(bool(enable))))

@@ -745,7 +745,8 @@ private:
         p.max_range = sensorMaxRange;
         return p;
     }
-    // the device handle, re-created (a first run again) when the parameters or the capacity change
+    // the device handle: re-created (a first run again) when the parameters change; a scan above the
+    // capacity grows it in place, keeping the call state (pf_dcvc_reserve)
     struct State {
         State(int device, size_t max_points) : device(device), max_points(max_points) {}
         ~State() {
@@ -755,12 +756,15 @@ private:
             const bool same = p.start_r == prm.start_r && p.delta_r == prm.delta_r && p.delta_p == prm.delta_p &&
                               p.delta_a == prm.delta_a && p.min_seg == prm.min_seg && p.min_range == prm.min_range &&
                               p.max_range == prm.max_range;
-            if (!h || !same || n > cap) {
+            if (!h || !same) {
                 if (h) pf_dcvc_destroy(h);
                 h = nullptr;
                 cap = n > max_points ? n : max_points;
                 check("pf_dcvc_create", pf_dcvc_create(&p, device, cap, &h));
                 prm = p;
+            } else if (n > cap) {
+                check("pf_dcvc_reserve", pf_dcvc_reserve(h, n));
+                cap = n;
             }
             return h;
         }

@@ -201,6 +201,21 @@ def test_bpf_front_lanes_identical(pa, pfsynth, dcvc):
         od3.frame_scan_device(buf.ptr + 16 * n * k, x.shape[0])
     od3.sync()
     np.testing.assert_array_equal(p1, od3.poses())
+    if dcvc:
+        # the curvedfilter switched on after an odd number of frames: its first call (the 5 m ring
+        # start) is that frame's, on whichever lane runs it, as with one lane
+        def late(lanes, when):
+            od = pa.Odom_BPF_EstimationClass(device=0)
+            od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+            od.set_front_lanes(lanes)
+            for k, x in enumerate(scans):
+                if k == when:
+                    od.set_dcvc(True)
+                od.frame_scan_device(buf.ptr + 16 * n * k, x.shape[0])
+            od.sync()
+            return od.poses()
+        for when in (5, 6):
+            np.testing.assert_array_equal(late(1, when), late(2, when), err_msg="DCVC from frame %d" % when)
 
 
 def test_bpf_scan_edge_cases(pa, pfsynth):

@@ -47,3 +47,35 @@ def test_tie_sort_classes_and_dropped_keys(pa, pfref):
             parts.append(k)
         keys = np.concatenate(parts)
         np.testing.assert_array_equal(pa.tie_sort(keys), _expected(pfref, keys))
+
+
+def test_tie_sort_big_levels_and_fallback(pa, pfref):
+    """Classes above the LDS size (kTieLocal, 14336 keys) go through the big levels (tile-parallel
+    partitions) and, past them, the single-workgroup partitions in global memory: every level count
+    gives std::sort's permutation."""
+    rng = np.random.default_rng(23)
+    cases = [rng.integers(0, 3000, 200000).astype(np.uint32),                   # tie-heavy
+             rng.integers(0, 1 << 30, 150000).astype(np.uint32),
+             np.sort(rng.integers(0, 50000, 120000)).astype(np.uint32),
+             np.full(90000, 5, np.uint32)]
+    m = np.sort(rng.integers(0, 60000, 80000)).astype(np.uint32)               # rgbds: map + new points
+    cases.append(np.concatenate([m, rng.integers(0, 60000, 12000).astype(np.uint32)]))
+    for keys in cases:
+        want = _expected(pfref, keys)
+        for levels in (0, 1, 2, 4):
+            np.testing.assert_array_equal(pa.tie_sort(keys, levels=levels), want,
+                                          err_msg="n=%d levels=%d" % (keys.size, levels))
+
+
+def test_tie_sort_depth_limit_heap_branch(pa, pfref):
+    """The depth-limit branch (libstdc++'s make_heap + sort_heap) on the device against the oracle's
+    restatement with the same settable depth limit (itself checked against std::sort's own branch in
+    tests/test_oracle_units.py): LDS segments, and big segments at the limit (global heap sort)."""
+    rng = np.random.default_rng(24)
+    for n in (17, 40, 300, 5000, 20000):
+        keys = rng.integers(0, max(2, n // 5), n).astype(np.uint32)
+        for depth in (0, 1, 2, 3, 5):
+            if n == 20000 and depth < 2:
+                continue                                 # one-thread global heap sort: slow, covered at 5000
+            want = pfref.sort_perm(keys, "literal", depth)
+            np.testing.assert_array_equal(pa.tie_sort(keys, depth=depth), want, err_msg="n=%d depth=%d" % (n, depth))
