@@ -60,6 +60,9 @@ def parse(argv=None):
                          "configs[3], KITTI 00-10 LPT-assigned to the ranks (strong scaling)")
     ap.add_argument("--knn-shard", action="store_true",
                     help="configs[4] kNN leg over the ranks: map broadcast once (RCCL), queries sharded")
+    ap.add_argument("--poses-out", default=None,
+                    help="kitti11: directory for the gathered trajectories, one KITTI pose file per sequence "
+                         "(NN.txt, 3x4 row-major per frame, runkitti.py's layout)")
     ap.add_argument("--concurrent", type=int, default=4,
                     help="kitti11: host threads per GPU, each driving its share of the sequences on its own "
                          "handle and streams")
@@ -266,22 +269,26 @@ def run_kitti11(rank, local_rank, world, warmup, threads, use_graph, barrier, co
         handles.append(od)
     shares = [[] for _ in range(nthreads)]         # LPT again over the threads
     loads = [0] * nthreads
-    for ptrs, _ in seqs:
+    for sq, (ptrs, _) in zip(mine, seqs):
         j = loads.index(min(loads))
-        shares[j].append(ptrs)
+        shares[j].append((sq, ptrs))
         loads[j] += len(ptrs)
 
     errors = []
+    poses = {}                     # sequence -> its trajectory (n, 7), read before the handle's reset
 
     def drive(od, items):          # ctypes releases the GIL inside every C call
         try:
-            for k, ptrs in enumerate(items):
+            for k, (sq, ptrs) in enumerate(items):
                 if k:
                     od.sync()          # raises on a sticky device error of the finished sequence
+                    poses[items[k - 1][0]] = od.poses()
                     od.reset()
                 for ptr, n in ptrs:
                     od.frame_device(ptr, n)
             od.sync()
+            if items:
+                poses[items[-1][0]] = od.poses()
         except Exception as e:     # re-raised in the main thread: a failed frame is never counted
             errors.append(repr(e))
 
@@ -298,7 +305,51 @@ def run_kitti11(rank, local_rank, world, warmup, threads, use_graph, barrier, co
         raise RuntimeError("kitti11: device errors on rank %d: %s" % (rank, errors))
     for od in handles:
         assert od.stats()["errors"] == 0
-    return dict(elapsed=el, frames=sum(len(p) for p, _ in seqs), sequences=["%02d" % sq for sq in mine])
+    return dict(elapsed=el, frames=sum(len(p) for p, _ in seqs), sequences=["%02d" % sq for sq in mine],
+                poses=poses)
+
+
+def stub_poses(sq, n):
+    """the stubbed pipeline's trajectory of sequence sq (pose7 = qx qy qz qw tx ty tz): identity
+    rotations, x = frame, y = sequence"""
+    p = np.zeros((n, 7))
+    p[:, 3] = 1.0
+    p[:, 4] = np.arange(n)
+    p[:, 5] = sq
+    return p
+
+
+def gather_poses(poses, world, rank, dist, dev):
+    """configs[3]'s one collective (after the timed region): every rank's per-sequence trajectories to
+    every rank, as one padded float64 all_gather (each rank's sequences and their frame counts follow
+    from the LPT assignment, so no sizes travel). Returns {sequence: (n, 7)} of every sequence."""
+    assign = lpt_assign(KITTI_SEQ_FRAMES, world)
+    sizes = [sum(KITTI_SEQ_FRAMES[sq] for sq in assign[r]) for r in range(world)]
+    mine = np.zeros((max(sizes), 7))
+    o = 0
+    for sq in assign[rank]:
+        n = KITTI_SEQ_FRAMES[sq]
+        p = poses[sq]
+        if p.shape != (n, 7):
+            raise RuntimeError("sequence %02d: %s poses, expected %d" % (sq, p.shape, n))
+        mine[o:o + n] = p
+        o += n
+    if dist is None:
+        parts = [mine]
+    else:
+        import torch
+        t = torch.from_numpy(mine).to(dev)
+        got = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(got, t)
+        parts = [g.cpu().numpy() for g in got]
+    out = {}
+    for r in range(world):
+        o = 0
+        for sq in assign[r]:
+            n = KITTI_SEQ_FRAMES[sq]
+            out[sq] = parts[r][o:o + n].copy()
+            o += n
+    return out
 
 
 def shard_bounds(n, world, rank):
@@ -1015,7 +1066,8 @@ def main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev="cud
     if stub:                       # CPU test of the rank plumbing: rank r 'takes' 1 + r seconds
         mine = lpt_assign(KITTI_SEQ_FRAMES, world)[rank]
         r = dict(elapsed=1.0 + rank, frames=sum(KITTI_SEQ_FRAMES[sq] for sq in mine),
-                 sequences=["%02d" % sq for sq in mine])
+                 sequences=["%02d" % sq for sq in mine],
+                 poses={sq: stub_poses(sq, KITTI_SEQ_FRAMES[sq]) for sq in mine})
     else:
         r = run_kitti11(rank, local_rank, world, args.warmup, threads, graph_mode(args), barrier, args.concurrent)
     elapsed, frames = r["elapsed"], r["frames"]
@@ -1028,7 +1080,20 @@ def main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev="cud
         elapsed, total = float(t.item()), int(f.item())
     else:
         total = frames
+    # the trajectories of all eleven sequences to every rank (runkitti.py:111-157 evaluates them together)
+    allp = gather_poses(r["poses"], world, rank, dist, dev)
+    pose_info = {"sequences": sorted(allp), "frames": [int(allp[sq].shape[0]) for sq in sorted(allp)],
+                 "dir": None}
     if rank == 0:
+        if args.poses_out:
+            import kitti
+            os.makedirs(args.poses_out, exist_ok=True)
+            for sq in sorted(allp):
+                kitti.write_poses(os.path.join(args.poses_out, "%02d.txt" % sq), allp[sq])
+            pose_info["dir"] = args.poses_out
+        if stub:
+            pose_info["stub_match"] = all(np.array_equal(allp[sq], stub_poses(sq, KITTI_SEQ_FRAMES[sq]))
+                                          for sq in allp)
         out = {"metric": METRIC, "value": round(total / elapsed, 2), "unit": "frames/s", "n_gpus": world,
                "steps": total, "warmup": args.warmup, "ms_per_step": round(elapsed / max(1, total) * 1e3, 4),
                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32/f64",
@@ -1037,7 +1102,8 @@ def main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev="cud
                                       "by sequence) as independent streams, LPT-assigned to the GPUs",
                           "assignment": lpt_assign(KITTI_SEQ_FRAMES, world), "rank0_sequences": r["sequences"],
                           "parallelism": "sequences over GPUs", "concurrent_per_gpu": args.concurrent,
-                          "graph": GRAPH_NAMES[graph_mode(args)]}}
+                          "graph": GRAPH_NAMES[graph_mode(args)]},
+               "poses": pose_info}
         if stub:
             out["stub"] = True
         print(json.dumps(out), flush=True)

@@ -137,14 +137,25 @@ def _launch(extra):
     return json.loads(lines[0])
 
 
-def test_kitti11_mode_gloo_world2():
+def test_kitti11_mode_gloo_world2(tmp_path):
     """configs[3] (`--sequences kitti11`) at 2 ranks over gloo with the stubbed pipeline: one JSON line,
-    n_gpus 2, all 23,201 frames of the 11 sequences counted once, time = the slowest rank's."""
-    out = _launch(["--sequences", "kitti11", "--warmup", "0"])
+    n_gpus 2, all 23,201 frames of the 11 sequences counted once, time = the slowest rank's; every
+    sequence's trajectory all-gathered and written as KITTI pose files (runkitti.py:111-157)."""
+    out = _launch(["--sequences", "kitti11", "--warmup", "0", "--poses-out", str(tmp_path)])
     assert out["n_gpus"] == 2 and out["stub"] and out["scaling"] == "strong"
     assert out["steps"] == sum(bench_frames()) == 23201
     assert abs(out["value"] - 23201 / 2.0) < 1e-6
     assert sorted(s for r in out["config"]["assignment"] for s in r) == list(range(11))
+    # the pose all-gather: every sequence's stub trajectory reaches rank 0 complete and in order
+    assert out["poses"]["sequences"] == list(range(11))
+    assert out["poses"]["frames"] == bench_frames()
+    assert out["poses"]["stub_match"] is True
+    sys.path.insert(0, os.path.join(ROOT, "pfilter-noetic_amd"))
+    import kitti
+    for sq, n in enumerate(bench_frames()):
+        m = kitti.read_poses(str(tmp_path / ("%02d.txt" % sq)))
+        assert m.shape[0] == n
+        assert np.allclose(m[:, 0, 3], np.arange(n)) and np.allclose(m[:, 1, 3], sq)
 
 
 def bench_frames():
