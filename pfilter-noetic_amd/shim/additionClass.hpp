@@ -4,13 +4,14 @@
 // publishers) and the same yaml keys (src/additionClass.cpp:17-52); the clustering runs on the MI355X
 // through libpfilter_hip.so (pfilter_hip::CurvedVoxelT in pfilter_hip_shim.hpp), so additionNode.cpp
 // builds without src/additionClass.cpp (whose OpenMP loops race: SURVEY §2 row 9). The per-cluster
-// colours and bounding boxes of colorSegmentation (:364-416) are computed here from the clusters the
-// device returns. The reference's distanceWeight / segmentation helper classes are not on the path
+// colours and bounding boxes of colorSegmentation (:364-416) come from the device's clustered cloud
+// (CurvedVoxelT::clusterBoxes: one pass over its contiguous cluster runs). The reference's distanceWeight / segmentation helper classes are not on the path
 // and are not provided.
 #ifndef PFILTER_HIP_ADDITIONCLASS_HPP
 #define PFILTER_HIP_ADDITIONCLASS_HPP
 
 #include <algorithm>
+#include <cmath>
 #include <limits>
 #include <sstream>
 
@@ -62,49 +63,54 @@ public:
         publishData();
     }
 
-    bool colorSegmentation() {                                                       // :364-416
+    // :364-416: the clusters' boxes from the device's clustered cloud (CurvedVoxelT::clusterBoxes, one
+    // pass over its contiguous runs) and the cloud coloured run by run from the yaml colour list
+    bool colorSegmentation() {
+        const auto boxes = clusterBoxes();
         pointCloudSegRGBLPtr.reset(new pointTypeRGBLCloud());
-        boxInfo.clear();
-        for (auto& label : labelRecords) {
-            jsk_recognition_msgs::BoundingBox box;
-            float min_x = std::numeric_limits<float>::max(), max_x = -std::numeric_limits<float>::max();
-            float min_y = min_x, max_y = max_x, min_z = min_x, max_z = max_x;
-            for (int id : label.second.index) {
-                const auto& p = pointCloudPtr->points[id];
-                min_x = std::min(min_x, p.x); max_x = std::max(max_x, p.x);
-                min_y = std::min(min_y, p.y); max_y = std::max(max_y, p.y);
-                min_z = std::min(min_z, p.z); max_z = std::max(max_z, p.z);
-                pointTypeRGBL pp;
-                pp.x = p.x; pp.y = p.y; pp.z = p.z;
-                if (!colorList.empty()) {
-                    const std::vector<int>& c = colorList[label.first % colorList.size()];
-                    pp.r = c[0]; pp.g = c[1]; pp.b = c[2];
+        pointCloudSegRGBLPtr->points.resize(pointCloudSegPtr->points.size());
+        boxInfo.assign(boxes.size(), jsk_recognition_msgs::BoundingBox());
+        for (size_t c = 0; c < boxes.size(); ++c) {
+            const auto& cb = boxes[c];
+            const std::vector<int>* rgb = colorList.empty() ? nullptr : &colorList[cb.label % colorList.size()];
+            for (size_t j = cb.first; j < cb.first + cb.count; ++j) {
+                auto& out = pointCloudSegRGBLPtr->points[j];
+                const auto& in = pointCloudSegPtr->points[j];
+                out.x = in.x;
+                out.y = in.y;
+                out.z = in.z;
+                if (rgb) {
+                    out.r = (*rgb)[0];
+                    out.g = (*rgb)[1];
+                    out.b = (*rgb)[2];
                 }
-                pointCloudSegRGBLPtr->points.push_back(pp);
             }
-            const double lx = max_x - min_x, ly = max_y - min_y, lz = max_z - min_z;
+            jsk_recognition_msgs::BoundingBox& box = boxInfo[c];
             box.header = cloudHeader;
-            box.label = label.first;
-            box.pose.position.x = min_x + lx / 2.0;
-            box.pose.position.y = min_y + ly / 2.0;
-            box.pose.position.z = min_z + lz / 2.0;
-            box.dimensions.x = lx < 0 ? -lx : lx;
-            box.dimensions.y = ly < 0 ? -ly : ly;
-            box.dimensions.z = lz < 0 ? -lz : lz;
-            boxInfo.emplace_back(box);
+            box.label = cb.label;
+            // extent = hi - lo in float, widened; centre = lo + extent / 2 in double (the reference's types)
+            const double ext[3] = {(double)(cb.hi[0] - cb.lo[0]), (double)(cb.hi[1] - cb.lo[1]),
+                                   (double)(cb.hi[2] - cb.lo[2])};
+            box.pose.position.x = cb.lo[0] + ext[0] / 2.0;
+            box.pose.position.y = cb.lo[1] + ext[1] / 2.0;
+            box.pose.position.z = cb.lo[2] + ext[2] / 2.0;
+            box.dimensions.x = std::abs(ext[0]);
+            box.dimensions.y = std::abs(ext[1]);
+            box.dimensions.z = std::abs(ext[2]);
         }
         return true;
     }
 
-    void publishData() {                                                             // :422-440
+    // :422-440: the boxes, then the coloured cloud, both stamped with the scan's header
+    void publishData() {
         jsk_recognition_msgs::BoundingBoxArray boxArray;
-        for (auto& box : boxInfo) boxArray.boxes.emplace_back(box);
         boxArray.header = cloudHeader;
+        boxArray.boxes = boxInfo;
         pubBoundingBox.publish(boxArray);
-        sensor_msgs::PointCloud2 msg;
-        pcl::toROSMsg(*pointCloudSegRGBLPtr, msg);
-        msg.header = cloudHeader;
-        pubCurvedPointCloudRGBA.publish(msg);
+        sensor_msgs::PointCloud2 coloured;
+        pcl::toROSMsg(*pointCloudSegRGBLPtr, coloured);
+        coloured.header = cloudHeader;
+        pubCurvedPointCloudRGBA.publish(coloured);
     }
     void resetParams() {}                            // :442-455: the device handle carries the ring start
 

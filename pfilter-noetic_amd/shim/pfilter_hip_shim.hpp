@@ -725,6 +725,34 @@ public:
     // per input point of the last run: its cluster's rank (1 = largest) or 0 when dropped
     const std::vector<int32_t>& labels() const { return lab_; }
 
+    // the axis-aligned bounds of every cluster of the last run, in labelRecords order: the clustered
+    // cloud holds each cluster as one contiguous run (the device publishes them rank by rank), so one
+    // pass over pointCloudSegPtr, run by run, gives them all
+    struct ClusterBox {
+        int label;
+        float lo[3], hi[3];
+        size_t first, count;        // the cluster's run in pointCloudSegPtr
+    };
+    std::vector<ClusterBox> clusterBoxes() const {
+        std::vector<ClusterBox> out;
+        out.reserve(labelRecords.size());
+        size_t at = 0;
+        for (const auto& rec : labelRecords) {
+            ClusterBox b{rec.first, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, at, rec.second.index.size()};
+            for (size_t j = at; j < at + b.count; ++j) {
+                const auto& q = pointCloudSegPtr->points[j];
+                const float xyz[3] = {q.x, q.y, q.z};
+                for (int a = 0; a < 3; ++a) {
+                    b.lo[a] = j == at ? xyz[a] : std::min(b.lo[a], xyz[a]);
+                    b.hi[a] = j == at ? xyz[a] : std::max(b.hi[a], xyz[a]);
+                }
+            }
+            at += b.count;
+            out.push_back(b);
+        }
+        return out;
+    }
+
     // members (include/additionClass.hpp:73-115), defaults of config/config.yaml:7-8, 49-54
     Ptr pointCloudPtr, pointCloudSegPtr;
     std::vector<std::pair<int, segInfo>> labelRecords;

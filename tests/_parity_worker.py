@@ -56,3 +56,62 @@ def compare(k, dev, ref, report, tol_t, tol_r, pose_err, tol_xyz=None):
             report["xyz_bitexact_frames"] += int(np.array_equal(gx.view(np.uint32), rx.view(np.uint32)))
             if d >= tol_xyz:
                 report["map_bad"].append((k, c, "xyz", d))
+
+
+# ---- Odom_BPF_EstimationClass (src/odomEstimationClass.cpp:649-1306) ----
+BPF_COUNTS = ("n_ds", "n_map", "n_res", "n_valid", "outer_iterations", "map_too_small")
+
+
+def bpf_clouds(k):
+    """frame k's beam / pillar / facade clouds by the oracle front end (ground_seg + featureExtract,
+    include/preProcess.hpp), xyz + 0 as the node publishes them; the device's front end is bit-exact
+    with it (tests/test_gpu_cls.py)"""
+    import pfref
+    x = _ctx["seq"].frame(k)
+    r = pfref.bpf_preprocess(x, pfref.cls_params())
+    return [np.c_[x[r[c], :3], np.zeros(len(r[c]))].astype(np.float32) for c in ("beam", "pillar", "facade")]
+
+
+def bpf_counts(st):
+    return {c: (list(st[c]) if isinstance(st[c], (list, tuple)) else int(st[c])) for c in BPF_COUNTS}
+
+
+def run_bpf(task):
+    """task = (k, [(xyz, rg) x 3] before frame k, odom, last_odom, optimization_count) -> (k, pose, counts,
+    maps after frame k) of the faithful OdomBPF on frame k's classified clouds"""
+    import pfref
+    k, maps, odom_pose, last_pose, opt = task
+    lid, ring_model, prm, opts = _ctx["args"]
+    orc = pfref.OdomBPF(pfref.make_lidar(*lid, ring_model=ring_model), *prm, opts=opts)
+    for c, (xyz, rg) in enumerate(maps):
+        orc.set_map(c, xyz, rg)
+    orc.set_state(odom_pose, last_pose)
+    orc.set_opt_count(opt)
+    orc.inited = True
+    pose = orc.update(*bpf_clouds(k))
+    return k, pose, bpf_counts(orc.stats()), [orc.get_map(c) for c in range(3)]
+
+
+def compare_bpf(k, dev, ref, report, tol_t, tol_r, pose_err):
+    """as compare(), over the three map classes"""
+    dt, dr = pose_err(dev[0], ref[0])
+    report["worst_t"] = max(report["worst_t"], dt)
+    report["worst_r"] = max(report["worst_r"], dr)
+    report["frames"] += 1
+    if not (dt < tol_t and dr < tol_r):
+        report["pose_bad"].append((k, dt, dr))
+    bad = {c: (dev[1][c], ref[1][c]) for c in BPF_COUNTS if dev[1][c] != ref[1][c]}
+    if bad:
+        report["count_bad"].append((k, bad))
+    for c, ((gx, grg), (rx, rrg)) in enumerate(zip(dev[2], ref[2])):
+        if gx.shape != rx.shape:
+            report["map_bad"].append((k, c, "size", gx.shape[0], rx.shape[0]))
+            continue
+        if not np.array_equal(grg, rrg):
+            report["map_bad"].append((k, c, "rg", int(np.sum(np.any(grg != rrg, axis=1)))))
+        if gx.size:
+            d = float(np.max(np.abs(gx.astype(np.float64) - rx)))
+            report["worst_xyz"] = max(report["worst_xyz"], d)
+            report["xyz_bitexact_frames"] += int(np.array_equal(gx.view(np.uint32), rx.view(np.uint32)))
+            if d >= tol_t:
+                report["map_bad"].append((k, c, "xyz", d))

@@ -1,7 +1,8 @@
 // Drives the curvedVoxel shim (pfilter_hip::CurvedVoxelT) the way src/additionNode.cpp:29-39 does:
 // one object, run() per frame, then reads pointCloudSegPtr and labelRecords. Input: frames (int64 n,
 // then n x 4 float32). Output per frame: the kept count and the cluster count, then per kept point its
-// x, y, z (float32) and per cluster its rank, size and first input index (int32).
+// x, y, z (float32), per cluster its rank, size and first input index (int32), then per cluster the
+// bounds clusterBoxes() gives colorSegmentation (lo xyz, hi xyz, float32).
 //   shim_dcvc_driver scans.bin out.bin
 #include <cstdio>
 #include <vector>
@@ -39,6 +40,10 @@ int main(int argc, char** argv) {
         for (const auto& r : bound.labelRecords) {
             const int32_t v[3] = {r.first, r.second.clusterNum, r.second.index.empty() ? -1 : r.second.index[0]};
             std::fwrite(v, sizeof(int32_t), 3, o);
+        }
+        for (const auto& b : bound.clusterBoxes()) {
+            std::fwrite(b.lo, sizeof(float), 3, o);
+            std::fwrite(b.hi, sizeof(float), 3, o);
         }
     }
     std::fclose(o);

@@ -146,12 +146,17 @@ def test_synced_parity_every_frame(pa, pfsynth, name, preset, n, theta, lines):
 
 
 @pytest.mark.parametrize("name,preset,n,theta,lines", CONFIGS)
-def test_synced_parity_stable_order(pa, pfsynth, name, preset, n, theta, lines):
-    """The default (fast) mode: VoxelGrid / rgbds sorted stably, so centroids differ from the
-    reference's in the last bits; the statistics of the per-frame comparison (every 4th frame) are
-    recorded."""
+def test_synced_statistics_stable_order(pa, pfsynth, name, preset, n, theta, lines):
+    """A statistics run, not a parity check: the stable-order mode (VoxelGrid / rgbds sorted stably,
+    pf_odom_set_tie_order off) does NOT meet the per-frame bar -- its centroids differ from the
+    reference's in the last bits, which tips a residual or map count on a few per cent of frames and a
+    few poses past 1e-4 m (profiles/r03_parity_synced/). Every 4th frame is compared and the summary
+    recorded; what is asserted is the envelope that deviation stayed in (r03: worst 1.44e-4 m /
+    1.4e-5 rad, count differences on 1.9 % of compared frames): 10x the pose tolerance and 5 % of frames."""
     rep = synced_run(pa, pfsynth, name, preset, n, theta, lines=lines, every=4)
     assert rep["frames"] == len(range(4, n, 4))
+    assert rep["worst_t"] < 10 * TOL_T and rep["worst_r"] < 10 * TOL_R, (rep["worst_t"], rep["worst_r"])
+    assert len(rep["count_bad"]) <= 0.05 * rep["frames"], len(rep["count_bad"])
 
 
 def test_synced_parity_s128_2m_point_map(pa, pfref, pfsynth):

@@ -151,7 +151,8 @@ def test_curved_voxel_shim_matches_c_abi(pa, pfsynth, tmp_path):
     """curvedVoxel drop-in (pfilter_hip::CurvedVoxelT, the class shim/additionClass.hpp gives
     additionNode.cpp) driven per frame like src/additionNode.cpp:29-39: pointCloudSegPtr and labelRecords
     equal pf_dcvc_run's kept points and cluster ranks bit for bit, the first frame included (rings from
-    5 m, then from 0, through the device handle the object's copies share)."""
+    5 m, then from 0, through the device handle the object's copies share); clusterBoxes() (the bounds
+    colorSegmentation publishes, src/additionClass.cpp:364-416) equal each cluster run's min / max."""
     exe = str(tmp_path / "shim_dcvc_driver")
     lib = os.path.join(ROOT, "pfilter-noetic_amd")
     subprocess.check_call(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
@@ -182,4 +183,10 @@ def test_curved_voxel_shim_matches_c_abi(pa, pfsynth, tmp_path):
         np.testing.assert_array_equal(rec[:, 1], sizes)
         starts = np.cumsum(np.r_[0, sizes[:-1]])
         np.testing.assert_array_equal(rec[:, 2], idx[starts])
+        box = np.frombuffer(raw, np.float32, 6 * nc, off).reshape(-1, 6)       # colorSegmentation's bounds
+        off += 24 * nc
+        for c in range(nc):
+            run = xyz[starts[c]:starts[c] + sizes[c]]
+            np.testing.assert_array_equal(box[c, :3], run.min(0))
+            np.testing.assert_array_equal(box[c, 3:], run.max(0))
     assert off == len(raw)
