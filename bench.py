@@ -60,6 +60,11 @@ def parse(argv=None):
                          "configs[3], KITTI 00-10 LPT-assigned to the ranks (strong scaling)")
     ap.add_argument("--knn-shard", action="store_true",
                     help="configs[4] kNN leg over the ranks: map broadcast once (RCCL), queries sharded")
+    ap.add_argument("--order", default="tie", choices=["tie", "stable"],
+                    help="sort order of every leg: tie = libstdc++ std::sort's order of equal keys (the "
+                         "reference's results frame by frame, pf_odom_set_tie_order), stable = stable sorts")
+    ap.add_argument("--other-order-frames", type=int, default=1000,
+                    help="frames of the headline workload run again in the other sort order (0: skip)")
     ap.add_argument("--poses-out", default=None,
                     help="kitti11: directory for the gathered trajectories, one KITTI pose file per sequence "
                          "(NN.txt, 3x4 row-major per frame, runkitti.py's layout)")
@@ -130,6 +135,16 @@ def lidar_cfg():
 
 
 ODOM_CFG = dict(map_resolution=0.4, k_new=0, theta_p=0.4, theta_max=75, weightType=0)
+# the sort order of VoxelGrid / rgbds / the featureExtraction sectors in every leg of the run (--order):
+# "tie" = libstdc++ std::sort's order of equal keys (pf_odom_set_tie_order, the reference's own results
+# frame by frame), "stable" = stable radix sorts and rgbds by merge (faster, last bits of the centroids
+# differ). ORDER[0] is read by every handle the bench creates.
+ORDER = ["tie"]
+
+
+def set_order(h):
+    """apply the run's sort order to a freshly initialised odometry handle"""
+    h.set_tie_order(ORDER[0] == "tie")
 
 
 # KITTI odometry sequences 00-10 (frame counts, SURVEY §8(d) config 4)
@@ -191,6 +206,7 @@ def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier,
     lid = lidar_cfg()
     od = pa.Odom_ES_EstimationClass(device=local_rank, max_points=300000, map_capacity=1 << 22)
     od.init(lid, **ODOM_CFG)
+    set_order(od)
     od.set_graph(use_graph)
     # stage every scan in HBM (untimed)
     bufs, ptrs, hbufs, hptrs = [], [], [], []
@@ -259,6 +275,7 @@ def run_kitti11(rank, local_rank, world, warmup, threads, use_graph, barrier, co
     for _ in range(nthreads):
         od = pa.Odom_ES_EstimationClass(device=local_rank, max_points=300000, map_capacity=1 << 22)
         od.init(lidar_cfg(), **ODOM_CFG)
+        set_order(od)
         od.set_graph(use_graph)
         if concurrent > 1:
             od.set_stage_a_reserve(0)      # several sequences share the GPU: stage A may use every CU
@@ -494,6 +511,7 @@ def pcie_leg(device, hptrs, warmup, use_graph=True):
     import pfilter_amd as pa
     od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lidar_cfg(), **ODOM_CFG)
+    set_order(od)
     od.set_graph(use_graph)
     for ptr, n in hptrs[:warmup]:
         od.frame_host_ptr(ptr, n)
@@ -523,6 +541,7 @@ def pageable_leg(device, nframes, threads, warmup=20, use_graph=True):
     del buf
     od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lidar_cfg(), **ODOM_CFG)
+    set_order(od)
     od.set_graph(use_graph)
     for k in range(warmup):
         od.frame_host(scans[k], want_pose=False)
@@ -548,8 +567,10 @@ def node_pattern_leg(device, hptrs, warmup, nframes):
     lid = lidar_cfg()
     fe = ctypes.c_void_p()
     pa._check("pf_fe_create", L.pf_fe_create(ctypes.byref(lid), device, 300000, ctypes.byref(fe)))
+    pa._check("pf_fe_set_tie_order", L.pf_fe_set_tie_order(fe, int(ORDER[0] == "tie")))
     od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lid, **ODOM_CFG)
+    set_order(od)
     eb, sb = pa.HostBuffer(300000 * 16), pa.HostBuffer(300000 * 16)
     ne, ns = ctypes.c_size_t(), ctypes.c_size_t()
     pose = np.empty(7)
@@ -605,6 +626,7 @@ def configs4_leg(device, nframes, threads, warmup=3, timing_frames=20, use_graph
     lid = pa.make_lidar(128, 3.0, 90.0, 0.1, ring_model=(15.0, -25.0))
     od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lid, 0.4, 0, 0.0, 0, 0)
+    set_order(od)
     od.set_graph(use_graph)
     od.frame_device(*ptrs[0])
     od.sync()
@@ -683,6 +705,7 @@ def bpf_leg(device, nframes, threads, warmup=20, cpu_seconds=10.0, with_cpu=True
             counts.append(int(cnt[i]))
     od = pa.Odom_BPF_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lidar_cfg(), **ODOM_CFG)
+    set_order(od)
     od.set_graph(use_graph)
     if dcvc:
         od.set_dcvc(True)                        # curvedfilter on, as launch/pfilter_kitti.launch:8
@@ -830,6 +853,7 @@ def es_leg(name, device, nframes, threads, cpu_seconds, warmup=20, use_graph=Tru
     def run(timing):
         od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
         od.init(pa.make_lidar(lines, 3.0, 90.0, 0.1), **cfg)
+        set_order(od)
         od.set_graph(use_graph)
         for k in range(warmup):
             od.frame_device(*ptrs[k])
@@ -868,6 +892,7 @@ def stage_pass(device, ptrs, warmup, nframes, use_graph=True):
     import pfilter_amd as pa
     od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lidar_cfg(), **ODOM_CFG)
+    set_order(od)
     od.set_graph(use_graph)
     for k in range(warmup):
         od.frame_device(*ptrs[k])
@@ -879,12 +904,122 @@ def stage_pass(device, ptrs, warmup, nframes, use_graph=True):
     return {"A_features_voxelgrid": round(st["a_us"], 1), "B_odometry": round(st["b_us"], 1), "frames": st["frames"]}
 
 
+def node_threads_leg(device, hptrs, warmup, nframes):
+    """The nodes as ROS runs them: laserProcessingNode and odomEstimationNode are separate processes
+    joined by a topic, so frame k + 1's featureExtraction runs while frame k's updatePointsToMap does.
+    Two host threads, each with its own handle, joined by a two-deep queue of edge / surf clouds in
+    pinned host RAM (the subscriber queue): pf_fe_extract on one, pf_odom_update on the other, both
+    synchronous calls as in the nodes."""
+    import ctypes
+    import queue
+    import threading
+    import pfilter_amd as pa
+    L = pa.lib()
+    lid = lidar_cfg()
+    fe = ctypes.c_void_p()
+    pa._check("pf_fe_create", L.pf_fe_create(ctypes.byref(lid), device, 300000, ctypes.byref(fe)))
+    pa._check("pf_fe_set_tie_order", L.pf_fe_set_tie_order(fe, int(ORDER[0] == "tie")))
+    od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
+    od.init(lid, **ODOM_CFG)
+    set_order(od)
+    total = min(len(hptrs), warmup + nframes)
+    slots = [(pa.HostBuffer(300000 * 16), pa.HostBuffer(300000 * 16)) for _ in range(3)]
+    full, free = queue.Queue(), queue.Queue()
+    for i in range(3):
+        free.put(i)
+    errors, marks = [], {}
+
+    def extract():
+        try:
+            ne, ns = ctypes.c_size_t(), ctypes.c_size_t()
+            for k in range(total):
+                i = free.get()
+                eb, sb = slots[i]
+                ptr, n = hptrs[k]
+                pa._check("pf_fe_extract", L.pf_fe_extract(fe, ptr, n, 16, eb.ptr, ctypes.byref(ne), sb.ptr,
+                                                           ctypes.byref(ns), 300000))
+                full.put((k, i, ne.value, ns.value))
+        except Exception as e:
+            errors.append(repr(e))
+            full.put(None)
+
+    def odometry():
+        try:
+            pose = np.empty(7)
+            for _ in range(total):
+                item = full.get()
+                if item is None:
+                    return
+                k, i, ne, ns = item
+                eb, sb = slots[i]
+                if k == 0:
+                    pa._check("pf_odom_init_map", L.pf_odom_init_map(od._h, eb.ptr, ne, 16, sb.ptr, ns, 16))
+                else:
+                    pa._check("pf_odom_update", L.pf_odom_update(od._h, eb.ptr, ne, 16, sb.ptr, ns, 16,
+                                                                 pose.ctypes.data))
+                free.put(i)
+                if k == warmup - 1 or (warmup == 0 and k == 0):
+                    marks["t0"] = time.perf_counter()
+                if k == total - 1:
+                    marks["t1"] = time.perf_counter()
+        except Exception as e:
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=extract), threading.Thread(target=odometry)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    L.pf_fe_destroy(fe)
+    if errors:
+        raise RuntimeError("node threads: %s" % errors)
+    nf = total - max(warmup, 1)
+    el = marks["t1"] - marks["t0"]
+    return {"value": round(nf / el, 2), "unit": "frames/s", "frames": nf, "poses": od.poses(),
+            "note": "two host threads as the two ROS nodes: pf_fe_extract -> 2-deep queue of pinned clouds -> "
+                    "pf_odom_update, every call synchronous; frames %d..%d" % (warmup, total - 1)}
+
+
+def order_leg(device, ptrs, warmup, nframes, order, use_graph=True):
+    """The headline workload's first `nframes` timed frames in the given sort order on a fresh handle,
+    timed like the headline (HBM-resident scans, one sync at the end), then once more with per-stage
+    device timing."""
+    import pfilter_amd as pa
+    total = min(len(ptrs), warmup + nframes)
+
+    def run(timing):
+        od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
+        od.init(lidar_cfg(), **ODOM_CFG)
+        od.set_tie_order(order == "tie")
+        od.set_graph(use_graph)
+        for k in range(warmup):
+            od.frame_device(*ptrs[k])
+        od.sync()
+        if timing:
+            od.set_stage_timing(True)
+        t0 = time.perf_counter()
+        for k in range(warmup, total):
+            od.frame_device(*ptrs[k])
+        od.sync()
+        el = time.perf_counter() - t0
+        assert od.stats()["errors"] == 0
+        return el, (od.stage_times() if timing else None)
+
+    el, _ = run(False)
+    _, st = run(True)
+    nf = total - warmup
+    return {"order": order, "value": round(nf / el, 2), "unit": "frames/s", "frames": nf,
+            "stage_us": {"A_features_voxelgrid": round(st["a_us"], 1), "B_odometry": round(st["b_us"], 1),
+                         "frames": st["frames"]}}
+
+
 def gpu_window(device, f0, f1, threads, use_graph=True):
     """The GPU pipeline timed over exactly frames [f0, f1) of S64 seed 0 (frames 0..f0-1 run untimed
     first, as the CPU baseline's warm-up): the CPU baseline's own window, for a like-for-like ratio."""
     import pfilter_amd as pa
     od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lidar_cfg(), **ODOM_CFG)
+    set_order(od)
     od.set_graph(use_graph)
     bufs, ptrs = [], []
     for _, buf, counts, _ in load_frames(0, f1, threads):
@@ -933,6 +1068,7 @@ def reduce_results(dist, elapsed, frames, poses, device):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
+    ORDER[0] = args.order
     world, launch = resolve_world(args, os.environ)
     if launch:                     # nothing has touched the GPU yet
         sys.exit(launch_ranks(world, argv))
@@ -994,7 +1130,12 @@ def main(argv=None):
                    "sequence": r["data"], "frames_per_rank": frames,
                    "mean_points_per_frame": round(r["mean_points"], 1),
                    "parallelism": "one independent sequence per GPU" if world > 1 else "single sequence",
-                   "graph": GRAPH_NAMES[graph_mode(args)]},
+                   "graph": GRAPH_NAMES[graph_mode(args)],
+                   "sort_order": args.order + (" (libstdc++ std::sort's order of equal keys in featureExtraction's "
+                                               "sectors, VoxelGrid and rgbds: the reference's results frame by "
+                                               "frame)" if args.order == "tie" else
+                                               " (stable sorts: centroids differ from the reference's in the "
+                                               "last bits)")},
     }
     log("pipeline: %d frames in %.3f s (host enqueue %.3f s), last-frame stats %s"
         % (frames, elapsed, r.get("enqueue", 0.0), r["stats"]))
@@ -1002,6 +1143,16 @@ def main(argv=None):
         out["config"]["host_enqueue_us_per_frame"] = round(r["enqueue"] / max(1, frames) * 1e6, 1)
     if world == 1 and not stub:
         out["stage_us"] = stage_pass(local_rank, r["ptrs"], args.warmup, min(1000, frames), graph_mode(args))
+    if world == 1 and not stub and args.other_order_frames > 0:
+        other = "stable" if args.order == "tie" else "tie"
+        try:
+            oo = order_leg(local_rank, r["ptrs"], args.warmup, args.other_order_frames, other, graph_mode(args))
+            oo["ratio_to_value"] = round(oo["value"] / value, 4)
+            out["other_order"] = oo
+            log("other_order: %s" % oo)
+        except Exception as e:  # report, never hide
+            log("other-order leg failed: %r" % (e,))
+            out["other_order"] = None
     if stub:
         out["stub"] = True
     elif world == 1 and not args.no_roofline:
@@ -1039,6 +1190,16 @@ def main(argv=None):
         nd["poses_equal_headline"] = bool(np.array_equal(npo, r["poses"][:npo.shape[0]]))
         out["node_pattern"] = nd
         log("node_pattern: %s" % nd)
+        try:
+            nt = node_threads_leg(local_rank, r["hptrs"], args.warmup, args.node_frames)
+            ntp = nt.pop("poses")
+            nt["poses_equal_headline"] = bool(np.array_equal(ntp, r["poses"][:ntp.shape[0]]))
+            nt["ratio_to_value"] = round(nt["value"] / value, 4)
+            out["node_threads"] = nt
+            log("node_threads: %s" % nt)
+        except Exception as e:  # report, never hide
+            log("node-threads leg failed: %r" % (e,))
+            out["node_threads"] = None
     if world == 1 and not stub and args.configs4_frames > 0:
         try:
             out["configs4"] = configs4_leg(local_rank, args.configs4_frames, threads, use_graph=graph_mode(args))

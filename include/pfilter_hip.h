@@ -98,6 +98,11 @@ int pf_fe_extract(pf_fe* h, const float* xyzi, size_t n, size_t stride_bytes, fl
  * [0, num_lines) dropped. SURVEY 8(d) config 5 (synthetic 128-line scans, -25..+15 deg) runs with it.
  * top_deg == bottom_deg == 0 restores the reference's formulas (the default). */
 int pf_fe_set_ring_model(pf_fe* h, double top_deg, double bottom_deg);
+/* Reference tie order (default off): a sector whose curvature list holds equal values is ordered as
+ * libstdc++'s std::sort leaves it (src/laserProcessingClass.cpp:101-104 sorts by value alone, and the
+ * surf cloud is written in that order) instead of by (value, ring position); sectors without an
+ * exact tie are identical either way. pf_odom_set_tie_order switches the handle's featureExtraction too. */
+int pf_fe_set_tie_order(pf_fe* h, int enable);
 
 /* ---------------- odometry (Odom_ES_EstimationClass) ---------------- */
 typedef struct pf_odom pf_odom;

@@ -63,6 +63,9 @@ enum {
     PFREF_VG_STABLE      = 4,   /* VoxelGrid/rgbds ties kept in input order (stable sort)        */
     PFREF_KNN_BRUTE      = 8,   /* brute-force kNN instead of the FLANN-style kd-tree            */
     PFREF_LM_NORMAL_EQ   = 16,  /* LM step by 6x6 normal equations instead of dense Householder QR */
+    PFREF_LD_TRIG        = 32,  /* (experiment) the LM's sin / cos / cubes in long double, rounded once:
+                                   another libm's last bit (tools/drift_probe.py)                   */
+    PFREF_QR_REVSUM      = 64,  /* (experiment) the LM's Householder QR sums its rows in reverse order  */
     PFREF_GPU_EQUIV      = 1 | 4 | 16
 };
 

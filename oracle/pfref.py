@@ -17,6 +17,8 @@ FE_SQRT_DOUBLE = 2
 VG_STABLE = 4
 KNN_BRUTE = 8
 LM_NORMAL_EQ = 16
+QR_REVSUM = 64         # experiment: the LM's Householder QR sums its rows in reverse order
+LD_TRIG = 32           # experiment: the LM's sin / cos / cubes in long double (another libm's last bit)
 GPU_EQUIV = FE_STABLE_TIES | VG_STABLE | LM_NORMAL_EQ
 
 

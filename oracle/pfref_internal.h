@@ -6,6 +6,8 @@
 #include <cstdint>
 #include <vector>
 
+extern "C" void pfref_introsort_stats(const uint32_t* keys, size_t n, long* st);   // pfref_sort.cpp
+
 namespace pfref {
 
 struct PtI { float x, y, z, intensity; };                 // pcl::PointXYZI (fields used)

@@ -236,20 +236,29 @@ inline M3 skew(V3 v) {
 }
 
 // getTransformFromSe3 (src/lidarOptimization.cpp:106-143)
+void trig_dump(double v);   // development: PFREF_TRIG_DUMP (pfref_odom.cpp)
+extern thread_local bool g_ld_trig;   // PFREF_LD_TRIG for the solve in progress
+extern thread_local bool g_qr_rev;    // PFREF_QR_REVSUM for the solve in progress
+inline double lsin(double x) { return g_ld_trig ? (double)sinl((long double)x) : std::sin(x); }
+inline double lcos(double x) { return g_ld_trig ? (double)cosl((long double)x) : std::cos(x); }
+inline double lcube(double x) {
+    return g_ld_trig ? (double)((long double)x * (long double)x * (long double)x) : std::pow(x, 3);
+}
 inline void se3_exp(const double se3[6], Quat& q, V3& t) {
     V3 omega{se3[0], se3[1], se3[2]};
     V3 upsilon{se3[3], se3[4], se3[5]};
     M3 Omega = skew(omega);
     double theta = norm(omega);
+    trig_dump(theta);
     double half_theta = 0.5 * theta;
     double imag_factor;
-    double real_factor = std::cos(half_theta);
+    double real_factor = lcos(half_theta);
     if (theta < 1e-10) {
         double theta_sq = theta * theta;
         double theta_po4 = theta_sq * theta_sq;
         imag_factor = 0.5 - 0.0208333 * theta_sq + 0.000260417 * theta_po4;
     } else {
-        double sin_half_theta = std::sin(half_theta);
+        double sin_half_theta = lsin(half_theta);
         imag_factor = sin_half_theta / theta;
     }
     q = {imag_factor * omega.x, imag_factor * omega.y, imag_factor * omega.z, real_factor};
@@ -258,8 +267,8 @@ inline void se3_exp(const double se3[6], Quat& q, V3& t) {
         J = q2m(q);
     } else {
         M3 Omega2 = mmul(Omega, Omega);
-        double a = (1.0 - std::cos(theta)) / (theta * theta);
-        double b = (theta - std::sin(theta)) / std::pow(theta, 3);
+        double a = (1.0 - lcos(theta)) / (theta * theta);
+        double b = (theta - lsin(theta)) / lcube(theta);
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j)
                 J.m[i][j] = (i == j ? 1.0 : 0.0) + a * Omega.m[i][j] + b * Omega2.m[i][j];
@@ -448,7 +457,10 @@ inline void eigen_sym3(const double in[3][3], double ev[3], double V[3][3]) {
 // Eigen makeHouseholder on x[0..n): returns tau, beta; essential part in ess[1..n)
 inline void make_householder(const double* x, int n, double* ess, double& tau, double& beta) {
     double tail = 0.0;
-    for (int i = 1; i < n; ++i) tail += x[i] * x[i];
+    if (g_qr_rev)
+        for (int i = n - 1; i >= 1; --i) tail += x[i] * x[i];
+    else
+        for (int i = 1; i < n; ++i) tail += x[i] * x[i];
     double c0 = x[0];
     const double tol = std::numeric_limits<double>::min();
     if (tail <= tol) {

@@ -8,6 +8,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <array>
 #include <map>
 #include <memory>
@@ -17,6 +18,15 @@ namespace pfref {
 // ------------------------------------------------------------------------------------------
 // PCL 1.10 VoxelGrid<PointXYZRGB>::applyFilter, downsample_all_data_ = true
 // ------------------------------------------------------------------------------------------
+thread_local bool g_ld_trig = false;
+thread_local bool g_qr_rev = false;
+
+// development: PFREF_TRIG_DUMP=<file> appends every libm argument of the faithful LM (doubles)
+void trig_dump(double v) {
+    static FILE* f = std::getenv("PFREF_TRIG_DUMP") ? std::fopen(std::getenv("PFREF_TRIG_DUMP"), "ab") : nullptr;
+    if (f) std::fwrite(&v, sizeof(v), 1, f);
+}
+
 namespace {
 struct IdxPair { unsigned idx, cloud_point_index; };
 
@@ -30,6 +40,15 @@ void minmax3(const std::vector<PtC>& in, float mn[3], float mx[3]) {  // pcl::ge
 
 void sort_pairs(std::vector<IdxPair>& iv, bool stable) {
     auto lt = [](const IdxPair& a, const IdxPair& b) { return a.idx < b.idx; };
+    static const bool trace = std::getenv("PFREF_SORT_STATS") != nullptr;   // development statistics
+    if (trace && !stable) {
+        std::vector<uint32_t> k(iv.size());
+        for (size_t i = 0; i < iv.size(); ++i) k[i] = iv[i].idx;
+        long st[6];
+        pfref_introsort_stats(k.data(), k.size(), st);
+        std::fprintf(stderr, "sort n %zu levels %ld heaps %ld max %ld keys %ld g3segs %ld g3max %ld\n", k.size(), st[0], st[1],
+                     st[2], st[3], st[4], st[5]);
+    }
     if (stable) std::stable_sort(iv.begin(), iv.end(), lt);
     else std::sort(iv.begin(), iv.end(), lt);
 }
@@ -344,7 +363,10 @@ void householder_solve(std::vector<double>& A, int rows, int cols, std::vector<d
         if (tau != 0.0 && n > 1) {
             for (int j = k + 1; j < cols; ++j) {
                 double tmp = 0.0;
-                for (int i = 1; i < n; ++i) tmp += ess[i] * at(k + i, j);
+                if (g_qr_rev)
+                    for (int i = n - 1; i >= 1; --i) tmp += ess[i] * at(k + i, j);
+                else
+                    for (int i = 1; i < n; ++i) tmp += ess[i] * at(k + i, j);
                 tmp += at(k, j);
                 at(k, j) -= tau * tmp;
                 for (int i = 1; i < n; ++i) at(k + i, j) -= tau * ess[i] * tmp;
@@ -355,7 +377,10 @@ void householder_solve(std::vector<double>& A, int rows, int cols, std::vector<d
         int n = rows - k;
         if (hc[k] == 0.0 || n < 2) continue;
         double tmp = 0.0;
-        for (int i = 1; i < n; ++i) tmp += at(k + i, k) * rhs[k + i];
+        if (g_qr_rev)
+            for (int i = n - 1; i >= 1; --i) tmp += at(k + i, k) * rhs[k + i];
+        else
+            for (int i = 1; i < n; ++i) tmp += at(k + i, k) * rhs[k + i];
         tmp += rhs[k];
         rhs[k] -= hc[k] * tmp;
         for (int i = 1; i < n; ++i) rhs[k + i] -= hc[k] * at(k + i, k) * tmp;
@@ -726,7 +751,9 @@ int solve_lm(double* params, const std::vector<Residual>& res, bool normal_eq) {
                 for (int i = 0; i < m; ++i)
                     for (int j = 0; j < 6; ++j) J[6 * (size_t)i + j] *= scale[j];
                 gmax = grad_max_norm(x, g);
-                radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3));
+                trig_dump(-1e300);                                  // marks the next value: a cube base
+                trig_dump(2.0 * rel - 1.0);
+                radius = radius / std::max(1.0 / 3.0, 1.0 - lcube(2.0 * rel - 1.0));
                 radius = std::min(1e16, radius);
                 decrease_factor = 2.0;
                 reuse_diag = false;
@@ -1057,7 +1084,10 @@ int odom_update(Odom& o, const std::vector<PtC>* in) {
                 qbase += (int)ds[c].size();
             }
             double tb = now_s();
+            g_ld_trig = (o.opts & PFREF_LD_TRIG) != 0;
+            g_qr_rev = (o.opts & PFREF_QR_REVSUM) != 0;
             st.lm_iterations += solve_lm(o.params, res, (o.opts & PFREF_LM_NORMAL_EQ) != 0);
+            g_ld_trig = g_qr_rev = false;
             double tc = now_s();
             st.t_assoc += tb - ta;
             st.t_solve += tc - tb;

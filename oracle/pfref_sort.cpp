@@ -254,6 +254,49 @@ void pfref_introsort_literal(const uint32_t* keys, size_t n, int depth, uint32_t
     perm(a, out);
 }
 
+// development statistics of one std::sort call's introsort (the literal form): st = {partition
+// levels reached, depth-limit segments, largest of them, their total keys, of those the segments holding
+// three or more equal keys, the largest of those}
+void pfref_introsort_stats(const uint32_t* keys, size_t n, long* st) {
+    std::vector<E> a = pairs(keys, n);
+    for (int i = 0; i < 6; ++i) st[i] = 0;
+    struct F { long f, l, d, lev; };
+    std::vector<F> stack;
+    const long d0 = n > 1 ? 2L * lg(n) : 0;
+    if (n > 16) stack.push_back(F{0, (long)n, d0, 0});
+    while (!stack.empty()) {
+        F s = stack.back();
+        stack.pop_back();
+        E* first = a.data() + s.f;
+        E* last = a.data() + s.l;
+        long lev = s.lev, depth = s.d;
+        while (last - first > 16) {
+            st[0] = std::max(st[0], lev + 1);
+            if (depth == 0) {
+                const long len = last - first;
+                ++st[1];
+                st[2] = std::max(st[2], len);
+                st[3] += len;
+                std::vector<uint32_t> k(len);
+                for (long i = 0; i < len; ++i) k[i] = first[i].key;
+                std::sort(k.begin(), k.end());
+                bool g3 = false;
+                for (long i = 2; i < len; ++i) g3 |= k[i] == k[i - 2];
+                st[4] += g3;
+                if (g3) st[5] = std::max(st[5], len);
+                break;
+            }
+            --depth;
+            E* mid = first + (last - first) / 2;
+            move_median_to_first(first, first + 1, mid, last - 1);
+            E* cut = unguarded_partition(first + 1, last, first);
+            stack.push_back(F{cut - a.data(), last - a.data(), depth, lev + 1});
+            last = cut;
+            ++lev;
+        }
+    }
+}
+
 void pfref_introsort_levels(const uint32_t* keys, size_t n, int depth, uint32_t* out) {
     std::vector<E> a = pairs(keys, n);
     sort_levels(a.data(), (long)n, depth < 0 ? 2 * lg(n) : depth);

@@ -22,6 +22,10 @@ namespace {
 __global__ void k_set_int(int* p, int v) {
     if (threadIdx.x == 0) *p = v;
 }
+__global__ void k_set_counts(int* p, int a, int b, int c, int nc) {
+    const int t = threadIdx.x;
+    if (t < nc) p[t] = t == 0 ? a : (t == 1 ? b : c);
+}
 
 // repack points with x,y,z at offsets 0,4,8 (+ intensity at 16 for a 32-byte PCL stride, at 12 for
 // 16-byte packing) into packed float4
@@ -257,6 +261,14 @@ int pf_fe_set_ring_model(pf_fe* h, double top_deg, double bottom_deg) {
     return fe_set_ring_model(h->fe, top_deg, bottom_deg);
 }
 
+int pf_fe_set_tie_order(pf_fe* h, int enable) {
+    if (!h) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(h->device));
+    PF_HIP_TRY(hipStreamSynchronize(h->stream));
+    h->fe.tie_order = enable != 0;
+    return PF_OK;
+}
+
 // ------------------------------------------------------------------------------------------------
 // live handles of the process (PF_GRAPH_AUTO: stage B replays its graph when several handles share
 // the host's launch path)
@@ -367,7 +379,7 @@ static int host_stage(OdomGPU& o) {
 // nor the streams wait for each other in steady state. *direct: some cloud was read from the caller's
 // memory (the caller must wait for hs->ev[p] before its buffers may change).
 static int host_upload(OdomGPU& o, int p, int nc, const float* const* cl, const size_t* n, const size_t* stride,
-                       bool* direct) {
+                       bool* direct, float4* const* dst_dev = nullptr) {
     if (int rc = host_stage(o)) return rc;
     HostStage& hs = *o.hs;
     *direct = false;
@@ -389,27 +401,27 @@ static int host_upload(OdomGPU& o, int p, int nc, const float* const* cl, const 
             repack(cl[c], n[c], stride[c], dst);
             src = dst;
         }
-        PF_HIP_TRY(hipMemcpyAsync(hs.d[p] + (size_t)c * o.in_cap, src, sizeof(float4) * n[c], hipMemcpyHostToDevice,
-                                  hs.stream));
+        PF_HIP_TRY(hipMemcpyAsync(dst_dev ? dst_dev[c] : hs.d[p] + (size_t)c * o.in_cap, src, sizeof(float4) * n[c],
+                                  hipMemcpyHostToDevice, hs.stream));
     }
     PF_HIP_TRY(hipEventRecord(hs.ev[p], hs.stream));
     PF_HIP_TRY(hipStreamWaitEvent(o.stream_a, hs.ev[p], 0));
     return PF_OK;
 }
 
-// the caller's class clouds (host memory) into slot p's inputs, on stage A's stream
+// the caller's class clouds (host memory) straight into slot p's inputs (the copy stream waits for the
+// slot's previous stage A, stage A's stream for the copies). The callers (init_map_n / update_n) return
+// after a readback of stage B, which waits for stage A and so for these copies: the caller's buffers are
+// free on return without a wait here.
 static int stage_inputs(pf_odom* h, int p, const float* const* cl, const size_t* n, const size_t* stride) {
     OdomGPU& o = h->o;
     const int nc = o.cls.nc;
     bool direct = false;
-    if (int rc = host_upload(o, p, nc, cl, n, stride, &direct)) return rc;
     StageBuf& sb = o.sb[p];
-    for (int c = 0; c < nc; ++c) {
-        if (n[c]) PF_HIP_TRY(hipMemcpyAsync(sb.in[c], o.hs->d[p] + (size_t)c * o.in_cap, sizeof(float4) * n[c],
-                                            hipMemcpyDeviceToDevice, o.stream_a));
-        hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream_a, sb.cnt + C_IN + c, (int)n[c]);
-    }
-    if (direct) PF_HIP_TRY(hipEventSynchronize(o.hs->ev[p]));   // the caller's buffers are free on return
+    if (int rc = host_upload(o, p, nc, cl, n, stride, &direct, sb.in)) return rc;
+    int cnt[kMaxC] = {0, 0, 0};
+    for (int c = 0; c < nc; ++c) cnt[c] = (int)n[c];
+    hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(64), 0, o.stream_a, sb.cnt + C_IN, cnt[0], cnt[1], cnt[2], nc);
     return PF_OK;
 }
 
@@ -585,6 +597,7 @@ int pf_odom_set_map(pf_odom* h, int which, const float* xyz, const uint8_t* rg, 
     if (n) PF_HIP_TRY(hipMemcpyAsync(map_cur(o)[which], tmp.data(), sizeof(float4) * n, hipMemcpyHostToDevice, o.stream));
     hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_M + which, (int)n);
     o.dims_fresh = false;                               // the next update's grid takes its bounds pass
+    if (n + 65536 > o.tie_hint) o.tie_hint = n + 65536;  // the tie-order rgbds sort starts in big levels above kTieMed
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     return PF_OK;
 }
@@ -1342,6 +1355,7 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
         drop_graphs_b(o);
     }
     o.tie_order = enable != 0;
+    o.fe.tie_order = o.tie_order;                   // featureExtraction's sector sort (:101-104)
     return PF_OK;
 }
 
@@ -1375,7 +1389,7 @@ extern "C" int pf_dev_set_rg_radix(pf_odom* h, int enable) {
 // 0xFFFFFFFF dropped anywhere); perm receives the vals (input indices) of the kept pairs in std::sort's
 // order, *n_out their count. PF_EINVAL when the valid keys are not class-major.
 // depth >= 0 replaces the depth limit 2 lg n of every class (the heap-sort branch, against the oracle's
-// settable-depth restatement), levels = the big levels before the single-workgroup fallback.
+// settable-depth restatement), levels = the big levels run before the medium workgroups (0: none).
 extern "C" int pf_dev_tie_sort2(int device, const uint32_t* keys, size_t n, int depth, int levels, uint32_t* perm,
                                 size_t* n_out) {
     if ((!keys && n) || !perm || !n_out || n > (size_t)INT_MAX / 2 || levels < 0 || levels > 6) return PF_EINVAL;
@@ -1412,7 +1426,7 @@ extern "C" int pf_dev_tie_sort2(int device, const uint32_t* keys, size_t n, int 
                 hipMemcpyAsync(dsz, hsz, sizeof(hsz), hipMemcpyHostToDevice, s) != hipSuccess))
         rc = PF_EHIP;
     if (!rc) {
-        tie_sort(t, dk, dv, TieClasses{dsz, 0, -1, 4}, dsz + 4, s);
+        tie_sort(t, dk, dv, TieClasses{dsz, 0, -1, 4}, dsz + 4, s, levels);
         int nv = 0, err = 0;
         if (hipMemcpyAsync(&nv, tie_valid_count(t), sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipMemcpyAsync(&err, dsz + 4, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||

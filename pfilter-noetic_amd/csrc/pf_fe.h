@@ -16,6 +16,7 @@ struct FeGPU {
     // ring model extension (pf_fe_set_ring_model): scale > 0 selects a linear beam model, ring =
     // int((ring_top - elevation_deg) * ring_scale), for line counts the reference has no formula for
     double ring_top = 0.0, ring_scale = 0.0;
+    int tie_order = 0;           // sectors with equal curvatures in libstdc++ std::sort's order (:101-104)
     size_t cap = 0;              // max input points
     int nblk_cap = 0;            // ceil(cap / 256)
     int rings = 0;               // number of ring lists (num_lines)

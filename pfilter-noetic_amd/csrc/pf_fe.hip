@@ -4,7 +4,7 @@
 //  k_fe_ring_scan exclusive scan of the (ring, block) histogram -> stable ring partition offsets
 //  k_fe_scatter   stable scatter into ring order (input order kept inside a ring, :62)
 //  k_fe_sector    one workgroup per (ring, sector): 11-tap curvature (:73-77), LDS bitonic sort by
-//                 (curvature, id), greedy edge pick with neighbour suppression (:110-148) and the
+//                 (curvature, id) (tie order: std::sort's own order for a sector with equal curvatures), greedy edge pick with neighbour suppression (:110-148) and the
 //                 ascending surf sweep (:198-205)
 //  k_fe_out_scan  output offsets in ring -> sector order
 //  k_fe_gather    bit-exact copies of the picked points
@@ -177,6 +177,112 @@ __device__ __forceinline__ double curvature_at(const float4* __restrict__ rr, in
     return X * X + Y * Y + Z * Z;
 }
 
+// libstdc++'s std::sort (GCC 9-11 bits/stl_algo.h: __introsort_loop with _S_threshold 16 and depth
+// 2 __lg(n), __move_median_to_first(first, first + 1, mid, last - 1), __unguarded_partition, heap sort
+// at the depth limit, final insertion sort) on the pairs (val, id) compared by val alone -- the
+// reference's sector sort (:101-104). One thread; stk: 3 * 64 ints of LDS for the pending right parts.
+template <class VP, class IP>
+__device__ void pair_swap(VP* val, IP* id, int a, int b) {
+    const double va = val[a];
+    const int ia = id[a];
+    val[a] = val[b];
+    id[a] = id[b];
+    val[b] = va;
+    id[b] = ia;
+}
+template <class VP, class IP>
+__device__ void pair_adjust_heap(VP* val, IP* id, int base, int hole, int len, double vv, int vi) {
+    const int top = hole;
+    int child = hole;
+    while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        if (val[base + child] < val[base + child - 1]) child--;
+        val[base + hole] = val[base + child];
+        id[base + hole] = id[base + child];
+        hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        val[base + hole] = val[base + child - 1];
+        id[base + hole] = id[base + child - 1];
+        hole = child - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && val[base + parent] < vv) {
+        val[base + hole] = val[base + parent];
+        id[base + hole] = id[base + parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    val[base + hole] = vv;
+    id[base + hole] = vi;
+}
+template <class VP, class IP>
+__device__ void std_sort_pairs(VP* val, IP* id, int n, int* stk) {
+    if (n < 2) return;
+    int sp = 0;
+    stk[0] = 0;
+    stk[1] = n;
+    stk[2] = 2 * (31 - __clz(n));
+    sp = 1;
+    while (sp > 0) {
+        --sp;
+        int first = stk[3 * sp], last = stk[3 * sp + 1], depth = stk[3 * sp + 2];
+        while (last - first > 16) {
+            if (depth == 0) {                                   // __partial_sort: make_heap + sort_heap
+                const int len = last - first;
+                for (int parent = (len - 2) / 2;; --parent) {
+                    pair_adjust_heap(val, id, first, parent, len, (double)val[first + parent], (int)id[first + parent]);
+                    if (parent == 0) break;
+                }
+                for (int e = len; e > 1;) {
+                    --e;
+                    const double vv = val[first + e];
+                    const int vi = id[first + e];
+                    val[first + e] = val[first];
+                    id[first + e] = id[first];
+                    pair_adjust_heap(val, id, first, 0, e, vv, vi);
+                }
+                break;
+            }
+            --depth;
+            const int a = first + 1, b = first + (last - first) / 2, c = last - 1;
+            const double va = val[a], vb = val[b], vc = val[c];
+            int sel;
+            if (va < vb) sel = vb < vc ? b : (va < vc ? c : a);
+            else sel = va < vc ? a : (vb < vc ? c : b);
+            pair_swap(val, id, first, sel);
+            const double pv = val[first];
+            int lo = first + 1, hi = last;
+            for (;;) {                                          // __unguarded_partition
+                while (val[lo] < pv) ++lo;
+                --hi;
+                while (pv < val[hi]) --hi;
+                if (!(lo < hi)) break;
+                pair_swap(val, id, lo, hi);
+                ++lo;
+            }
+            stk[3 * sp] = lo;                                   // __introsort_loop(cut, last, depth)
+            stk[3 * sp + 1] = last;
+            stk[3 * sp + 2] = depth;
+            ++sp;
+            last = lo;
+        }
+    }
+    for (int i = 1; i < n; ++i) {                               // final insertion sort (stable)
+        const double vv = val[i];
+        const int vi = id[i];
+        int j = i;
+        while (j > 0 && vv < val[j - 1]) {
+            val[j] = val[j - 1];
+            id[j] = id[j - 1];
+            --j;
+        }
+        val[j] = vv;
+        id[j] = vi;
+    }
+}
+
 __device__ __forceinline__ bool kv_greater(double va, int ia, double vb, int ib) {
     return va > vb || (va == vb && ia > ib);
 }
@@ -189,7 +295,7 @@ __device__ __forceinline__ void sector_select(const float4* __restrict__ rr, int
                                               double* sval, int* sid, unsigned char* picked,
                                               unsigned char* gapbig, int* sedge, int* lw_int, int* ivl_lo, int* ivl_hi,
                                               int* __restrict__ sec_edge_ids, int* __restrict__ surf_ids,
-                                              int* __restrict__ sec_cnt) {
+                                              int* __restrict__ sec_cnt, int tie, int* stk) {
     const int t = threadIdx.x;
     int P = 64;
     while (P < size) P <<= 1;
@@ -230,6 +336,22 @@ __device__ __forceinline__ void sector_select(const float4* __restrict__ rr, int
                     }
                 }
             }
+            __syncthreads();
+        }
+    }
+    if (tie) {
+        // reference tie order: libstdc++'s std::sort orders equal curvatures its own way (:101-104), so
+        // a sector holding an exact tie is sorted again, from the unsorted list, by introsort itself
+        // (one thread); without a tie both orders are the same
+        bool has = false;
+        for (int i = t; i + 1 < size; i += 256) has = has || sval[i] == sval[i + 1];
+        if (__syncthreads_or(has)) {
+            for (int k = t; k < size; k += 256) {
+                sval[k] = curvature_at(rr, cs + k + 5);
+                sid[k] = cs + k + 5;
+            }
+            __syncthreads();
+            if (t == 0) std_sort_pairs(sval, sid, size, stk);
             __syncthreads();
         }
     }
@@ -320,8 +442,9 @@ __global__ void __launch_bounds__(256) k_fe_sector(const float4* __restrict__ rp
                                                     int* __restrict__ sec_edge_ids, int* __restrict__ surf_ids,
                                                     int* __restrict__ sec_cnt, double* __restrict__ g_val,
                                                     int* __restrict__ g_id, unsigned char* __restrict__ g_picked,
-                                                    unsigned char* __restrict__ g_gap) {
+                                                    unsigned char* __restrict__ g_gap, int tie) {
     __shared__ double sval[kSecLds];
+    __shared__ int stk[3 * 64];
     __shared__ int sid[kSecLds];
     __shared__ unsigned char picked[kSecLds + 16];
     __shared__ unsigned char gapbig[kSecLds + 16];
@@ -346,14 +469,14 @@ __global__ void __launch_bounds__(256) k_fe_sector(const float4* __restrict__ rp
     const float4* rr = rp + base;
     if (size <= kSecLds) {
         sector_select<false>(rr, cs, size, base, sec, sval, sid, picked, gapbig, sedge, lw_int, ivl_lo, ivl_hi,
-                             sec_edge_ids, surf_ids, sec_cnt);
+                             sec_edge_ids, surf_ids, sec_cnt, tie, stk);
     } else {
         // a sector larger than LDS (e.g. every point in ring 0 for a line count without a ring
         // formula, :58-61): the same selection on global scratch; slots 2 (base + cs) .. of the
         // scratch arrays are this sector's own (P <= 2 size, windows of size + 10 <= 2 size bytes)
         const size_t o = 2 * (size_t)(base + cs);
         sector_select<true>(rr, cs, size, base, sec, g_val + o, g_id + o, g_picked + o, g_gap + o, sedge, lw_int, ivl_lo,
-                            ivl_hi, sec_edge_ids, surf_ids, sec_cnt);
+                            ivl_hi, sec_edge_ids, surf_ids, sec_cnt, tie, stk);
     }
 }
 
@@ -462,7 +585,7 @@ void fe_enqueue(FeGPU& f, const float4* d_in, const int* d_n, float4* edge, int*
     hipLaunchKernelGGL(k_fe_ring_scan, dim3(1), dim3(1024), 0, s, f.blkhist, L, d_n, f.ring_start);
     hipLaunchKernelGGL(k_fe_scatter, dim3(f.nblk_cap), dim3(256), 0, s, d_in, d_n, f.ring, f.blkhist, f.rp);
     hipLaunchKernelGGL(k_fe_sector, dim3(L * 6), dim3(256), 0, s, f.rp, f.ring_start, f.sec_edge_ids,
-                       f.sec_surf_ids, f.sec_cnt, f.big_val, f.big_id, f.big_picked, f.big_gap);
+                       f.sec_surf_ids, f.sec_cnt, f.big_val, f.big_id, f.big_picked, f.big_gap, f.tie_order);
     hipLaunchKernelGGL(k_fe_out_scan, dim3(1), dim3(1024), 0, s, f.sec_cnt, L * 6, f.sec_off, d_ne, d_ns);
     hipLaunchKernelGGL(k_fe_gather, dim3(L * 6), dim3(256), 0, s, f.rp, f.ring_start, f.sec_edge_ids,
                        f.sec_surf_ids, f.sec_cnt, f.sec_off, edge, surf);

@@ -263,6 +263,7 @@ struct OdomGPU {
     bool rg_radix = false;         // development: rgbds by the full radix sort instead of the merge
     TieSort* tie_a = nullptr;
     TieSort* tie_b = nullptr;
+    size_t tie_hint = 0;                        // largest class an rgbds tie sort may see (pf_odom_set_map)
 };
 
 // Stage A keeps off the last CUs of the device by default: with one sequence per GPU, stage B's LM

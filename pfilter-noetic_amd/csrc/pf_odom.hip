@@ -1379,7 +1379,8 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     unsigned long long* dbg = a.dbg;
     const bool rec = dbg && blockIdx.x == 0 && threadIdx.x == 0;
     if (rec) dbg[0] = __builtin_amdgcn_s_memrealtime();
-    __shared__ double rows[256][8];                             // per residual: J[6], r, 0.5 rho
+    __shared__ double rows[256][9];                             // per residual: J[6], r, 0.5 rho (+1 pad:
+                                                                // a stride of 18 words spreads a wave's rows over the 32 banks)
     __shared__ double red9[28][9];
     __shared__ int nbad[3];                                     // bad residuals, bad Jacobians, kept rows
     __shared__ unsigned char hi_[21], hj_[21];
@@ -3047,6 +3048,7 @@ int odom_reset(OdomGPU& o) {
     if (o.front2 && o.front2->dcvc && dcvc_mark_called(*o.front2->dcvc, o.stream) != PF_OK) return PF_EHIP;
     if (hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
     o.dcvc_first = o.front && o.front->dcvc;
+    o.tie_hint = 0;
     o.opt_count_host = 2;
     o.inited = false;
     o.dims_fresh = false;
@@ -3251,7 +3253,8 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
                      leaf, o.keys, o.vals, sort_hist(o.prim, 32, true));
     }
     if (o.tie_order)                       // std::sort's order of equal keys (:74)
-        tie_sort(*o.tie_b, o.keys, o.vals, TieClasses{cnt, C_M, C_DS, nc}, o.prim.err, s);
+        tie_sort(*o.tie_b, o.keys, o.vals, TieClasses{cnt, C_M, C_DS, nc}, o.prim.err, s,
+                 tie_levels_for(*o.tie_b, o.tie_hint));
     else
         radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
     RgTailArgs ta{cnt, clouds(map_cur(o)), clouds(o.app), o.keys, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,

@@ -11,25 +11,41 @@
 // the ascending positions L_1 < L_2 < ... of its left stops (key >= pivot) and R_1 < R_2 < ... of its
 // right stops (key <= pivot, first included): with m the largest k for which L_k < R_(nR + 1 - k), the
 // partition swaps L_k <-> R_(nR + 1 - k) for k <= m and returns min(L_(m + 1), R_(nR + 1 - m)) (L_1 for
-// m = 0). Introsort's segments never interact, so the recursion runs breadth-first:
-//   k_tie_compact   drops the 0xFFFFFFFF keys (cropped points) per class, one pass with a look-back;
-//   big levels      segments above kTieLocal keys: every tile of 4096 keys of every segment finds its
-//                   stops in parallel (a look-back per segment ranks them), then one workgroup per
-//                   segment searches m, swaps the pairs and files the children;
-//   k_tie_local     one workgroup per segment of at most kTieLocal keys finishes its whole subtree in
-//                   LDS, one wavefront per segment per recursion level; leaves of at most 16 keys are
-//                   sorted stably (libstdc++'s final insertion sort moves no key across a leaf), the
-//                   depth limit 2 lg n hands a segment to libstdc++'s heap sort. Segments still above
-//                   kTieLocal after the big levels (very large classes) are partitioned by their
-//                   workgroup in global memory until they fit.
-// oracle/pfref_sort.cpp holds the same algorithm on the CPU next to a line-by-line restatement of
-// libstdc++'s introsort, both checked against std::sort itself (tests/test_oracle_units.py).
+// m = 0). The test k <= m is local to the k-th left stop: L_k < R_(nR + 1 - k) holds exactly when at
+// least k right stops lie after L_k, and the cut is the smallest of {R_(nR + 1 - k) : k <= m} and
+// {L_k : k > m}, a minimum every left stop can contribute to. Introsort's segments never interact, so
+// the recursion runs breadth-first, every segment of a level at once:
+//   k_tie_medium  one 1024-thread workgroup per class (or per medium segment): drops the 0xFFFFFFFF
+//                 keys (cropped points), then partitions in global memory, one sweep per level (tiles
+//                 of 14336 keys ranked by ballots and a carried workgroup scan; the hit count m, the
+//                 cut and the swaps in rank space), until every segment fits 14336 keys;
+//   k_tie_mid     one workgroup per segment of 2049 .. 14336 keys: the same levels on the segment staged
+//                 in LDS, until every piece fits 2048 keys (many CUs in parallel from here on);
+//   k_tie_local   one workgroup per job of at most 2048 keys finishes the whole subtree in LDS: per
+//                 level one pass ranks every segment's stops at once, one thread per segment searches
+//                 m and the cut, a pass does the swaps, and one thread per segment files the children
+//                 (median of three applied as it files them). Leaves of at most 16 keys are sorted
+//                 stably at the end (libstdc++'s final insertion sort moves no key across a leaf);
+//   k_tie_heap    the segments that reached the depth limit 2 lg n (in any tier) are written to the
+//                 output as they stand and heap-sorted there as libstdc++'s __partial_sort does, one
+//                 workgroup per segment: __make_heap a tree level at a time, __sort_heap's pops
+//                 pipelined two tree levels apart in one wave (a pop every two LDS steps instead of one
+//                 every 2 lg n).
+// The levels are bound by VALU issue (about 50 instructions per 64 keys per level), so the tiers exist to
+// spread a class over many CUs as early as the cost of a launch boundary allows: work handed from one
+// workgroup to another inside a launch would pay an agent-scope release and acquire per hand-off.
+//   big levels    (classes above kTieMed keys, e.g. a 2M-point rgbds map) first: k_tie_compact, then per
+//                 level every tile of 4096 keys of every segment finds its stops in parallel (a
+//                 look-back per segment ranks them) and one workgroup per segment swaps and files.
+// oracle/pfref_sort.cpp holds the level-synchronous algorithm on the CPU next to a line-by-line
+// restatement of libstdc++'s introsort, both checked against std::sort itself
+// (tests/test_oracle_units.py).
 #pragma once
 #include "pf_prims.h"
 
 namespace pf {
 
-constexpr int kTieLocal = 14336;      // largest segment sorted in LDS (10 B per key)
+constexpr int kTieMed = 65536;        // classes above this run the multi-workgroup big levels first
 constexpr int kTieTile = 4096;        // keys per tile of the compaction and the big levels
 
 // class c of the input is its next cnt[ia + c] (+ cnt[ib + c] when ib >= 0) pairs, c < nc: the
@@ -40,31 +56,37 @@ struct TieClasses {
 };
 
 struct TieSort {
-    u32 *k = nullptr, *v = nullptr;       // [cap] compacted pairs, class-major (the working copy)
-    u32 *lp = nullptr, *rq = nullptr;     // [cap] left / right stop positions of the big partitions
+    u32 *k = nullptr, *v = nullptr;       // [cap] compacted pairs (the working copy)
+    u32 *lp = nullptr, *rq = nullptr;     // [cap] left / right stop positions by rank
     u64* status = nullptr;                // [tiles] look-back words, zero between launches
-    u32* arrive = nullptr;                // [2] look-back arrival counters
+    u32* arrive = nullptr;                // [4] arrival counters (look-backs, local-kernel exit)
     int4* big = nullptr;                  // [2][bcap] big segments of a level {first, last, depth, tile base}
     u64* tot = nullptr;                   // [bcap] stop totals of a big segment (nL << 32 | nR)
-    int4* jobs = nullptr;                 // [jcap] local jobs {first, last, depth, 0}
+    int4* med = nullptr;                  // [mcap] medium segments {first, last, depth, class}
+    int4* mid = nullptr;                  // [midcap] mid-tier segments {first, last, depth, class}
+    int4* jobs = nullptr;                 // [jcap] local jobs {first, last, depth (-1: at the limit), class}
+    int2* heaps = nullptr;                // [hcap] depth-limit segments {output offset, length}
     int* ctl = nullptr;                   // counters (pf_tie.hip)
     size_t cap = 0, tiles = 0;
-    int bcap = 0, jcap = 0;
-    int levels = 0;                       // big levels launched per sort
+    int bcap = 0, mcap = 0, midcap = 0, jcap = 0, hcap = 0;
+    int max_levels = 0;                   // big levels the buffers are sized for
     int depth0 = -1;                      // test probe: >= 0 replaces every class's depth limit
 };
 
-// cap: most pairs of one sort; levels: big levels per sort (classes up to about 2^levels x kTieLocal
-// keys are sorted without the single-workgroup fallback)
-int tie_alloc(TieSort& t, size_t cap, int levels = 2);
+// cap: most pairs of one sort; max_levels < 0: as many big levels as cap can need
+int tie_alloc(TieSort& t, size_t cap, int max_levels = -1);
 void tie_free(TieSort& t);
+// big levels for classes of up to `size_hint` keys (0 below kTieMed; clamped to max_levels)
+int tie_levels_for(const TieSort& t, size_t size_hint);
 
 // Sorts (keys, vals)[0 .. n) in place, n = the classes' total, each class as std::sort would (keys
 // compared as whole 32-bit words), the 0xFFFFFFFF pairs dropped from the classes and the key array
 // ended by them: keys[0 .. valid) sorted class after class, keys[valid .. n) = 0xFFFFFFFF (their
-// vals too). Replaces a stable radix sort of the same pairs. A look-back wait that gives up sets bit 2
-// of *err (the caller's sticky error word).
-void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s);
+// vals too). Replaces a stable radix sort of the same pairs. levels: big levels to run first (0: every
+// class goes straight to its medium workgroup, which handles any size, slowly above kTieMed). A
+// look-back wait that gives up sets bit 2 of *err (the caller's sticky error word), a list overflow
+// bit 4.
+void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s, int levels = 0);
 const int* tie_valid_count(const TieSort& t);   // device word: the valid pairs of the last sort
 
 }  // namespace pf

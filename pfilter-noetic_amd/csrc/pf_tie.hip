@@ -10,17 +10,23 @@ constexpr u32 kTieDrop = 0xFFFFFFFFu;
 constexpr int kThreshold = 16;           // libstdc++ _S_threshold
 constexpr int kMaxTieC = 4;              // classes of one sort (key bits 30-31)
 constexpr int kTieGrid = 256;            // workgroups of the tile launches (co-resident, look-back)
-constexpr int kTieSegLds = kTieLocal / (kThreshold + 1) + 4;   // segments of one LDS recursion level
-constexpr int kTieStack = 128;           // pending big segments of the fallback
+constexpr int kLocalGrid = 256;          // workgroups of k_tie_local (two per CU)
+constexpr int kMidGrid = 128;            // workgroups of k_tie_mid (LDS-limited: one per CU)
+constexpr int kMedGrid = 64;             // workgroups of k_tie_medium over a segment list
 typedef unsigned short u16;
 
 // control words (TieSort::ctl)
 enum {
-    T_VALID = 0,        // valid pairs (compacted)
+    T_VALID = 0,        // valid pairs (all classes)
     T_NJOBS = 1,        // local jobs
-    T_CS = 2,           // [kMaxTieC] compacted start of every class
+    T_CS = 2,           // [kMaxTieC] big path: compacted start of every class
     T_BIG = 8,          // u64 [2]: big segments << 32 | their tiles, per level parity
-    T_WORDS = 16
+    T_NMED = 12,        // medium segments (big path)
+    T_NMID = 13,        // mid-tier segments
+    T_NHEAP = 14,       // depth-limit segments for k_tie_heap
+    T_VC = 16,          // [kMaxTieC] valid pairs of every class
+    T_BASE = 20,        // [kMaxTieC] where class c starts in the working copy
+    T_WORDS = 32
 };
 __device__ __forceinline__ u64* big_ctr(int* ctl, int p) { return reinterpret_cast<u64*>(ctl + T_BIG) + p; }
 
@@ -46,10 +52,114 @@ __device__ __forceinline__ int median3(u32 ka, u32 kb, u32 kc, int a, int b, int
 
 __device__ __forceinline__ int tiles_of(int len) { return (len + kTieTile - 1) / kTieTile; }
 
+__device__ __forceinline__ u32 wave_min_u32(u32 v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const u32 w = (u32)__shfl_xor((int)v, o, 64);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+
+// atomicMin of each active lane's value into slot[seg]: one atomic per wave when every active lane
+// names the same segment (the common case above the deepest levels)
+template <class A>
+__device__ __forceinline__ void seg_min(A* slot, bool act, u32 seg, u32 val) {
+    const u64 am = __ballot(act);
+    if (!am) return;
+    const u32 s0 = (u32)__shfl((int)seg, __ffsll((long long)am) - 1, 64);
+    if (__ballot(act && seg != s0) == 0) {
+        const u32 m = wave_min_u32(act ? val : 0xFFFFFFFFu);
+        if (lane_id() == 0) atomicMin(&slot[s0], m);
+    } else if (act) {
+        atomicMin(&slot[seg], val);
+    }
+}
+
+// libstdc++ __adjust_heap + __push_heap on [base, base + len)
+template <class KA, class VA>
+__device__ void adjust_heap(KA* k, VA* v, int base, int hole, int len, u32 vk, VA vv) {
+    const int top = hole;
+    int child = hole;
+    while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        if (k[base + child] < k[base + child - 1]) child--;
+        k[base + hole] = k[base + child];
+        v[base + hole] = v[base + child];
+        hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        k[base + hole] = k[base + child - 1];
+        v[base + hole] = v[base + child - 1];
+        hole = child - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && k[base + parent] < vk) {
+        k[base + hole] = k[base + parent];
+        v[base + hole] = v[base + parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    k[base + hole] = vk;
+    v[base + hole] = vv;
+}
+// libstdc++'s __partial_sort(first, last, last) = __make_heap + __sort_heap (one thread)
+template <class KA, class VA>
+__device__ void heap_sort(KA* k, VA* v, int base, int len) {
+    if (len >= 2)
+        for (int parent = (len - 2) / 2;; --parent) {
+            adjust_heap(k, v, base, parent, len, (u32)k[base + parent], v[base + parent]);
+            if (parent == 0) break;
+        }
+    for (int last = len; last > 1;) {
+        --last;
+        const u32 vk = k[base + last];
+        const VA vv = v[base + last];
+        k[base + last] = k[base];
+        v[base + last] = v[base];
+        adjust_heap(k, v, base, 0, last, vk, vv);
+    }
+}
+
+// the median of three moved to first (one thread); returns the pivot
+template <class KA, class VA>
+__device__ __forceinline__ u32 median_to_first(KA* k, VA* v, int first, int last) {
+    const int a = first + 1, b = first + (last - first) / 2, c = last - 1;
+    const u32 ka = k[a], kb = k[b], kc = k[c];
+    const int sel = median3(ka, kb, kc, a, b, c);
+    const u32 pv = sel == a ? ka : (sel == b ? kb : kc);
+    const u32 kf = k[first];
+    const VA vf = v[first], vs = v[sel];
+    k[first] = pv;
+    k[sel] = kf;
+    v[first] = vs;
+    v[sel] = vf;
+    return pv;
+}
+
+__device__ __forceinline__ void file_job(int* ctl, int4* jobs, int jcap, int* err, int f, int e, int d, int c) {
+    if (e - f < 1) return;
+    const int j = atomicAdd(&ctl[T_NJOBS], 1);
+    if (j < jcap) jobs[j] = make_int4(f, e, d, c);
+    else atomicOr(err, 4);
+}
+
+// a segment at the depth limit, already at its place in the output [off, off + len): k_tie_heap sorts it
+struct HeapList {
+    int2* seg;
+    int cap;
+    int* err;
+    __device__ __forceinline__ void file(int* ctl, long long off, int len) const {
+        const int j = atomicAdd(&ctl[T_NHEAP], 1);
+        if (j < cap) seg[j] = make_int2((int)off, len);
+        else atomicOr(err, 4);
+    }
+};
+
 // ------------------------------------------------------------------------------------------------
-// compaction: the valid pairs of the input, class-major (the classes are contiguous in the input), one
-// pass of 4096-pair tiles (16 rows of 256) with a decoupled look-back; the tile holding a class's first
-// input element records where the class starts among the valid pairs
+// big path: compaction, one pass of 4096-pair tiles (16 rows of 256) with a decoupled look-back; the
+// tile holding a class's first input element records where the class starts among the valid pairs
 __global__ void __launch_bounds__(256) k_tie_compact(const u32* __restrict__ keys, const u32* __restrict__ vals,
                                                      TieClasses cls, u32* __restrict__ k, u32* __restrict__ v,
                                                      int* __restrict__ ctl, u64* __restrict__ status,
@@ -116,8 +226,9 @@ __global__ void __launch_bounds__(256) k_tie_compact(const u32* __restrict__ key
     lookback_finish(status, ntiles, arrive, G);
 }
 
-// level 0: every class is one std::sort call; above kTieLocal keys it starts in the big levels
-__global__ void k_tie_setup(TieClasses cls, int* __restrict__ ctl, int4* __restrict__ big, int4* __restrict__ jobs,
+// level 0 of the big path: every class is one std::sort call; above kTieMed keys it starts in the
+// big levels, otherwise in a medium workgroup
+__global__ void k_tie_setup(TieClasses cls, int* __restrict__ ctl, int4* __restrict__ big, int4* __restrict__ med,
                             int levels, int depth0) {
     if (threadIdx.x != 0) return;
     const int nv = ctl[T_VALID];
@@ -125,24 +236,35 @@ __global__ void k_tie_setup(TieClasses cls, int* __restrict__ ctl, int4* __restr
     for (int c = 0; c < kMaxTieC; ++c) cs[c] = c < cls.nc ? ctl[T_CS + c] : nv;
     cs[kMaxTieC] = nv;
     u64 ctr = 0;
-    int nj = 0;
+    int nm = 0;
     for (int c = 0; c < kMaxTieC; ++c) {
         const int f = cs[c], e = cs[c + 1], len = e - f;
+        ctl[T_VC + c] = len > 0 ? len : 0;
+        ctl[T_BASE + c] = f;
         if (len < 1) continue;
         const int depth = depth0 >= 0 ? depth0 : 2 * lg_floor(len);   // std::__lg(last - first) * 2
-        if (levels > 0 && len > kTieLocal && depth > 0) {
+        if (levels > 0 && len > kTieMed && depth > 0) {
             big[(int)(ctr >> 32)] = make_int4(f, e, depth, (int)(u32)ctr);
             ctr += (1ull << 32) | (u64)tiles_of(len);
         } else {
-            jobs[nj++] = make_int4(f, e, depth, 0);
+            med[nm++] = make_int4(f, e, depth, c);
         }
     }
     *big_ctr(ctl, 0) = ctr;
     *big_ctr(ctl, 1) = 0;
-    ctl[T_NJOBS] = nj;
+    ctl[T_NMED] = nm;
+    ctl[T_NJOBS] = 0;
 }
 
-// ------------------------------------------------------------------------------------------------
+// the class of a position of the compacted big-path layout
+__device__ __forceinline__ int class_of(const int* ctl, int pos) {
+    int c = 0;
+#pragma unroll
+    for (int q = 1; q < kMaxTieC; ++q)
+        if (pos >= ctl[T_BASE + q] && ctl[T_VC + q] > 0) c = q;
+    return c;
+}
+
 // big levels. Status word of a tile: tag << 62 | (left stops << 31 | right stops); the look-back of a
 // tile stops at the first tile of its segment.
 constexpr u64 kValMask = (1ull << 62) - 1;
@@ -285,52 +407,44 @@ __device__ __forceinline__ int wg_msearch(const u32* lp, const u32* rq, int firs
 }
 
 // the cut of a partition with m swaps: min(L_(m+1), R_(nR+1-m)), L_1 for m = 0
-template <class PA>
-__device__ __forceinline__ int cut_of(const PA* lp, const PA* rq, int first, int nL, int nR, int m) {
-    if (m == 0) return (int)lp[first];
+__device__ __forceinline__ int cut_of(const u32* lp, const u32* rq, int first, int last, int nL, int nR, int m) {
+    if (m == 0) return nL ? (int)lp[first] : last;
     const int r = (int)rq[first + nR - m];
     const int lf = m < nL ? (int)lp[first + m] : INT_MAX;
     return lf < r ? lf : r;
 }
 
-__device__ __forceinline__ void file_child(int* ctl, int pn, int4* next, int4* jobs, int f, int e, int d,
-                                           bool may_big) {
+__device__ __forceinline__ void file_big_child(int* ctl, int pn, int4* next, int4* med, int mcap, int* err, int f,
+                                               int e, int d, bool may_big) {
     const int len = e - f;
     if (len < 1) return;
-    if (may_big && len > kTieLocal && d > 0) {
+    if (may_big && len > kTieMed && d > 0) {
         const u64 r = atomicAdd((unsigned long long*)big_ctr(ctl, pn), (1ull << 32) | (u64)tiles_of(len));
         next[(int)(r >> 32)] = make_int4(f, e, d, (int)(u32)r);
     } else {
-        jobs[atomicAdd(&ctl[T_NJOBS], 1)] = make_int4(f, e, d, 0);
+        const int i = atomicAdd(&ctl[T_NMED], 1);
+        if (i < mcap) med[i] = make_int4(f, e, d, class_of(ctl, f));
+        else atomicOr(err, 4);
     }
 }
 
 // one workgroup per big segment of level parity p: the median swap, m, the cut, the m swaps, and the
-// two children filed as big segments of the next level or as local jobs
-__global__ void __launch_bounds__(1024) k_tie_split(u32* __restrict__ k, u32* __restrict__ v,
-                                                    const u32* __restrict__ lp, const u32* __restrict__ rq,
-                                                    const int4* __restrict__ big, const u64* __restrict__ tot,
-                                                    int* __restrict__ ctl, int p, int last_level,
-                                                    int4* __restrict__ next, int4* __restrict__ jobs) {
+// two children filed as big segments of the next level or as medium segments
+__global__ void __launch_bounds__(1024) k_tie_split(u32* k, u32* v, const u32* __restrict__ lp,
+                                                    const u32* __restrict__ rq, const int4* __restrict__ big,
+                                                    const u64* __restrict__ tot, int* ctl, int p, int last_level,
+                                                    int4* next, int4* med, int mcap, int* err) {
     __shared__ int s_cut;
     const int nb = (int)(*big_ctr(ctl, p) >> 32);
     const int t = threadIdx.x;
     for (int s = blockIdx.x; s < nb; s += gridDim.x) {
         const int4 sg = big[s];
         const int first = sg.x, last = sg.y, depth = sg.z;
-        if (t == 0) {
-            const int a = first + 1, b = first + (last - first) / 2, c = last - 1;
-            const int sel = median3(k[a], k[b], k[c], a, b, c);
-            const u32 kf = k[first], ks = k[sel], vf = v[first], vs = v[sel];
-            k[first] = ks;
-            k[sel] = kf;
-            v[first] = vs;
-            v[sel] = vf;
-        }
+        if (t == 0) median_to_first(k, v, first, last);
         const u64 tt = tot[s];
         const int nL = (int)(tt >> 32), nR = (int)(u32)tt;
         const int m = wg_msearch<1024>(lp, rq, first, nL, nR);
-        if (t == 0) s_cut = cut_of(lp, rq, first, nL, nR, m);
+        if (t == 0) s_cut = cut_of(lp, rq, first, last, nL, nR, m);
         __threadfence_block();
         __syncthreads();
         for (int q = t; q < m; q += 1024) {
@@ -343,359 +457,1185 @@ __global__ void __launch_bounds__(1024) k_tie_split(u32* __restrict__ k, u32* __
         }
         if (t == 0) {
             const int cut = s_cut;
-            file_child(ctl, p ^ 1, next, jobs, first, cut, depth - 1, !last_level);
-            file_child(ctl, p ^ 1, next, jobs, cut, last, depth - 1, !last_level);
+            file_big_child(ctl, p ^ 1, next, med, mcap, err, first, cut, depth - 1, !last_level);
+            file_big_child(ctl, p ^ 1, next, med, mcap, err, cut, last, depth - 1, !last_level);
         }
         __syncthreads();
     }
 }
+
+#ifdef PF_TIE_PROF
+// development build (-DPF_TIE_PROF): workgroup 0's first job records the real-time counter at every
+// phase boundary of every level (pf_dev_tie_prof reads it back)
+__device__ unsigned long long g_tie_prof[1024];
+#define TIE_PROF(slot, val) \
+    do { if (blockIdx.x == 0 && threadIdx.x == 0 && jb == 0 && (slot) < 1024) g_tie_prof[(slot)] = (val); } while (0)
+#else
+#define TIE_PROF(slot, val) do { } while (0)
+#endif
+#ifdef PF_TIE_PROF
+#define PART_PROF(slot, val) \
+    do { if (prof >= 0 && threadIdx.x == 0 && prof + (slot) < 1024) g_tie_prof[prof + (slot)] = (val); } while (0)
+#else
+#define PART_PROF(slot, val) do { } while (0)
+#endif
 
 // ------------------------------------------------------------------------------------------------
-// local sort: one workgroup of 1024 threads per job
+// Partition levels over an item whose active segments are all longer than a stop size (so a wave's 896
+// positions meet at most two of them): per level one sweep ranks every active position's stops (tiles of
+// 14336 positions, wave w owning rows 14 w .. 14 w + 13 of 64, ranks from ballots, a carried workgroup
+// scan across tiles) and lists them by rank (LP / RP); in rank space every left stop then tests
+// L_k < R_(nR + 1 - k) and the hits are counted per segment (m: the predicate is monotone), one thread
+// per segment finds the cut, a second rank-space pass swaps L_k <-> R_(nR + 1 - k) for k <= m, and the
+// children are filed in position order: longer than the stop into the next level (median of three moved
+// to first), the others handed on. Two stores: the working copy in global memory (k_tie_medium, one
+// workgroup per class) and an item staged in LDS (k_tie_mid).
+constexpr int kMT = 1024;
+constexpr int kMRows = 7;
+constexpr int kMTile = kMT * kMRows;     // 7168
+constexpr int kTieMid = 2 * kMTile;      // largest segment the LDS mid tier takes (14336)
+constexpr int kTieSmall = 2048;          // largest local job
+constexpr int kMBatch = 8;               // left stops per thread in flight in the rank-space passes
 
-// libstdc++ __adjust_heap + __push_heap on [base, base + len)
-template <class KA, class VA>
-__device__ void adjust_heap(KA* k, VA* v, int base, int hole, int len, u32 vk, VA vv) {
-    const int top = hole;
-    int child = hole;
-    while (child < (len - 1) / 2) {
-        child = 2 * (child + 1);
-        if (k[base + child] < k[base + child - 1]) child--;
-        k[base + hole] = k[base + child];
-        v[base + hole] = v[base + child];
-        hole = child;
-    }
-    if ((len & 1) == 0 && child == (len - 2) / 2) {
-        child = 2 * (child + 1);
-        k[base + hole] = k[base + child - 1];
-        v[base + hole] = v[base + child - 1];
-        hole = child - 1;
-    }
-    int parent = (hole - 1) / 2;
-    while (hole > top && k[base + parent] < vk) {
-        k[base + hole] = k[base + parent];
-        v[base + hole] = v[base + parent];
-        hole = parent;
-        parent = (hole - 1) / 2;
-    }
-    k[base + hole] = vk;
-    v[base + hole] = vv;
-}
-// libstdc++'s __partial_sort(first, last, last) = __make_heap + __sort_heap (one thread)
-template <class KA, class VA>
-__device__ void heap_sort(KA* k, VA* v, int base, int len) {
-    if (len >= 2)
-        for (int parent = (len - 2) / 2;; --parent) {
-            adjust_heap(k, v, base, parent, len, (u32)k[base + parent], v[base + parent]);
-            if (parent == 0) break;
-        }
-    for (int last = len; last > 1;) {
-        --last;
-        const u32 vk = k[base + last];
-        const VA vv = v[base + last];
-        k[base + last] = k[base];
-        v[base + last] = v[base];
-        adjust_heap(k, v, base, 0, last, vk, vv);
-    }
-}
-
-// stable sort of up to two leaves of <= 16 keys by one wavefront: lanes 16 g .. 16 g + 15 rank leaf g
-// (final insertion sort: no key leaves its leaf, and insertion sort is stable)
-template <class VA>
-__device__ __forceinline__ void leaf_sort2(u32* K, VA* V, int f0, int e0, int f1, int e1) {
-    const int l = lane_id(), g = l >> 4, j = l & 15;
-    const int f = g == 0 ? f0 : f1, len = g == 0 ? e0 - f0 : (g == 1 ? e1 - f1 : 0);
-    const bool leaf = g < 2 && len >= 2 && len <= kThreshold;
-    const bool mine = leaf && j < len;
-    const u32 key = mine ? K[f + j] : kTieDrop;
-    const VA val = mine ? V[f + j] : (VA)0;
-    int r = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const u32 ki = (u32)__shfl((int)key, (l & ~15) + i, 64);
-        r += (i < len) && (ki < key || (ki == key && i < j));
-    }
-    if (mine) {
-        K[f + r] = key;
-        V[f + r] = val;
-    }
-}
-
-// one Hoare partition of [first, last) by one wavefront (median of three first); LP / RQ receive the
-// stop positions at first + rank. Returns the cut.
-template <class VA, class PA>
-__device__ int wave_partition(u32* K, VA* V, PA* LP, PA* RQ, int first, int last) {
-    const int l = lane_id();
-    const u64 lt = lanemask_lt();
-    const int a = first + 1, b = first + (last - first) / 2, c = last - 1;
-    const u32 ka = K[a], kb = K[b], kc = K[c];
-    const int sel = median3(ka, kb, kc, a, b, c);
-    const u32 pv = sel == a ? ka : (sel == b ? kb : kc);
-    if (l == 0) {
-        const u32 kf = K[first];
-        const VA vf = V[first], vs = V[sel];
-        K[first] = pv;
-        K[sel] = kf;
-        V[first] = vs;
-        V[sel] = vf;
-    }
-    __builtin_amdgcn_wave_barrier();
-    int nL = 0, nR = 0;
-    for (int base = first; base < last; base += 256) {
-        u32 kk[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = base + 64 * u + l;
-            kk[u] = i < last ? K[i] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = base + 64 * u + l;
-            const bool in = i < last;
-            const bool fl = in && i > first && !(kk[u] < pv);
-            const bool fr = in && !(pv < kk[u]);
-            const u64 bl = __ballot(fl), br = __ballot(fr);
-            if (fl) LP[first + nL + __popcll(bl & lt)] = (PA)i;
-            if (fr) RQ[first + nR + __popcll(br & lt)] = (PA)i;
-            nL += __popcll(bl);
-            nR += __popcll(br);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    int lo = 0, hi = nL < nR ? nL : nR;                  // m: 64 candidates per round
-    while (lo < hi) {
-        const int step = (hi - lo + 63) / 64;
-        int kq = lo + (l + 1) * step;
-        kq = kq < hi ? kq : hi;
-        const bool ok = (int)LP[first + kq - 1] < (int)RQ[first + nR - kq];
-        const int cnt = __popcll(__ballot(ok));
-        if (cnt == 0) {
-            hi = lo + step - 1;
-        } else {
-            const int nlo = lo + cnt * step < hi ? lo + cnt * step : hi;
-            const int nhi = cnt < 64 ? (lo + (cnt + 1) * step < hi ? lo + (cnt + 1) * step : hi) - 1 : hi;
-            lo = nlo;
-            hi = nhi > lo ? nhi : lo;
-        }
-    }
-    const int m = lo;
-    const int cut = cut_of(LP, RQ, first, nL, nR, m);
-    for (int q = l; q < m; q += 64) {
-        const int pl = (int)LP[first + q], pr = (int)RQ[first + nR - 1 - q];
-        const u32 kl = K[pl], kr = K[pr];
-        const VA vl = V[pl], vr = V[pr];
-        K[pl] = kr;
-        K[pr] = kl;
-        V[pl] = vr;
-        V[pr] = vl;
-    }
-    __builtin_amdgcn_wave_barrier();
-    return cut;
-}
-
-struct LocalLds {
-    u32 K[kTieLocal];
-    u16 I[kTieLocal], LP[kTieLocal], RQ[kTieLocal];
-    u64 seg[2][kTieSegLds];        // first | last << 16 | depth << 32
-    int nseg[2];
-    int4 stk[kTieStack];           // fallback: pending big segments
-    int nstk;
-    int4 top;
-    u32 cnt[64];                   // fallback: per-row-wave stop counts, then their prefixes
-    u32 tot;
-    int cut;
+template <int NSEG>
+struct MedTab {                          // one level's active segments, in position order
+    int f[NSEG], e[NSEG], d[NSEG], cut[NSEG];
+    u32 pv[NSEG], m[NSEG];
+    u32 bl[NSEG], br[NSEG], el[NSEG], er[NSEG];   // stop ranks before first / up to last - 1
+};
+template <int NSEG>
+struct MedWork {
+    MedTab<NSEG> tab[2];
+    u32 wt[2][16];
+    u32 carry[2][2];
+    int n[2];
 };
 
-__device__ __forceinline__ u64 seg_pack(int f, int e, int d) {
-    return (u64)(u32)f | ((u64)(u32)e << 16) | ((u64)(u32)d << 32);
+// working copy in global memory; ranks listed at the item's own offset of t.lp / t.rq
+struct GStore {
+    u32 *k, *v, *lp, *rq;
+    int base;
+    __device__ __forceinline__ u32 key(int p) const { return k[p]; }
+    __device__ __forceinline__ void setL(u32 g, int p) { lp[base + g] = (u32)p; }
+    __device__ __forceinline__ void setR(u32 g, int p) { rq[base + g] = (u32)p; }
+    __device__ __forceinline__ int getL(u32 g) const { return (int)lp[base + g]; }
+    __device__ __forceinline__ int getR(u32 g) const { return (int)rq[base + g]; }
+    __device__ __forceinline__ void load2(int p, int q, u32 (&x)[4]) const {
+        x[0] = k[p];
+        x[1] = k[q];
+        x[2] = v[p];
+        x[3] = v[q];
+    }
+    __device__ __forceinline__ void store2(int p, int q, const u32 (&x)[4]) {
+        k[p] = x[1];
+        k[q] = x[0];
+        v[p] = x[3];
+        v[q] = x[2];
+    }
+    __device__ __forceinline__ u32 median(int f, int e) { return median_to_first(k, v, f, e); }
+};
+// an item staged in LDS, positions relative to the item
+struct LStore {
+    u32* K;
+    u16 *I, *LP, *RP;
+    __device__ __forceinline__ u32 key(int p) const { return K[p]; }
+    __device__ __forceinline__ void setL(u32 g, int p) { LP[g] = (u16)p; }
+    __device__ __forceinline__ void setR(u32 g, int p) { RP[g] = (u16)p; }
+    __device__ __forceinline__ int getL(u32 g) const { return LP[g]; }
+    __device__ __forceinline__ int getR(u32 g) const { return RP[g]; }
+    __device__ __forceinline__ void load2(int p, int q, u32 (&x)[4]) const {
+        x[0] = K[p];
+        x[1] = K[q];
+        x[2] = I[p];
+        x[3] = I[q];
+    }
+    __device__ __forceinline__ void store2(int p, int q, const u32 (&x)[4]) {
+        K[p] = x[1];
+        K[q] = x[0];
+        I[p] = (u16)x[3];
+        I[q] = (u16)x[2];
+    }
+    __device__ __forceinline__ u32 median(int f, int e) { return median_to_first(K, I, f, e); }
+};
+
+// the last segment of T starting at or before p, -1 when none
+template <int NSEG>
+__device__ __forceinline__ int med_lo(const MedTab<NSEG>& T, int n, int p) {
+    if (n == 0 || p < T.f[0]) return -1;
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (T.f[mid] <= p) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+// the segment owning left-stop rank g (the last one whose first rank is <= g)
+template <int NSEG>
+__device__ __forceinline__ int med_rank_seg(const MedTab<NSEG>& T, int n, u32 g) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (T.bl[mid] <= g) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+// atomicAdd of each active lane's 1 into slot[seg]: one atomic per wave when every active lane names
+// the same segment
+__device__ __forceinline__ void seg_count(u32* slot, bool act, int seg) {
+    const u64 am = __ballot(act);
+    if (!am) return;
+    const int s0 = __shfl(seg, __ffsll((long long)am) - 1, 64);
+    if (__ballot(act && seg != s0) == 0) {
+        if (lane_id() == 0) atomicAdd(&slot[s0], (u32)__popcll(am));
+    } else if (act) {
+        atomicAdd(&slot[seg], 1u);
+    }
 }
 
-// [f, f + len) of the compacted pairs, len <= kTieLocal: the whole subtree in LDS, then the sorted
-// keys and the vals they carry to the output
-__device__ void lds_sort(LocalLds& S, const u32* __restrict__ k, const u32* __restrict__ v, u32* __restrict__ keys,
-                         u32* __restrict__ vals, int f, int len, int depth) {
-    const int t = threadIdx.x, wv = t >> 6, l = lane_id();
-    for (int i = t; i < len; i += 1024) {
-        S.K[i] = k[f + i];
-        S.I[i] = (u16)i;
+// emit(f, e, d): a segment of at most `stop` keys (d >= 0) or one at the depth limit (d = -1: copied to
+// the output as it stands by the locals, then heap-sorted there by k_tie_heap)
+template <int NSEG, class St, class Emit>
+__device__ void part_levels(St& st, MedWork<NSEG>& S, int f0, int e0, int d0, int stop, Emit emit, int* err,
+                            int prof = -1) {
+    const int t = threadIdx.x, w = t >> 6, l = lane_id();
+    const u64 lt = lanemask_lt();
+    if (e0 - f0 <= stop || d0 <= 0) {
+        if (t == 0) {
+            if (e0 - f0 > stop) {                                   // the depth limit above the stop size
+                emit(f0, e0, -1);
+            } else {
+                emit(f0, e0, d0);
+            }
+        }
+        __syncthreads();
+        return;
     }
     if (t == 0) {
-        S.nseg[0] = len > kThreshold ? 1 : 0;
-        S.nseg[1] = 0;
-        S.seg[0][0] = seg_pack(0, len, depth);
+        MedTab<NSEG>& T = S.tab[0];
+        T.f[0] = f0;
+        T.e[0] = e0;
+        T.d[0] = d0;
+        T.m[0] = 0;
+        T.pv[0] = st.median(f0, e0);
+        S.n[0] = 1;
     }
+    __threadfence_block();
     __syncthreads();
-    if (len <= kThreshold) {
-        if (wv == 0) leaf_sort2(S.K, S.I, 0, len, 0, 0);
-    } else {
-        int cur = 0;
-        for (;;) {
-            const int ns = S.nseg[cur];
-            if (ns == 0) break;
-            for (int s = wv; s < ns; s += 16) {
-                const u64 e = S.seg[cur][s];
-                const int first = (int)(e & 0xffff), last = (int)((e >> 16) & 0xffff), d = (int)(e >> 32);
-                if (d == 0) {                                    // depth limit: __partial_sort
-                    if (l == 0) heap_sort(S.K, S.I, first, last - first);
-                    __builtin_amdgcn_wave_barrier();
-                    continue;
+    int cur = 0;
+    [[maybe_unused]] int lev = 0;
+    for (;;) {
+        const int ns = S.n[cur];
+        PART_PROF(8 * lev, rt_now());
+        PART_PROF(8 * lev + 7, (unsigned long long)ns);
+        if (ns == 0) break;
+        MedTab<NSEG>& T = S.tab[cur];
+        // 1. every active position's stops ranked (item-relative ranks), tile by tile
+        if (t == 0) {
+            S.carry[0][0] = 0;
+            S.carry[0][1] = 0;
+        }
+        __syncthreads();
+        int nt = 0;
+        for (int tb = f0; tb < e0; tb += kMTile, ++nt) {
+            const int par = nt & 1;
+            const int wb = tb + w * kMRows * 64;
+            const int sa = med_lo(T, ns, wb), sb = sa + 1 < ns ? sa + 1 : -1;
+            const int fa = sa >= 0 ? T.f[sa] : 0, ea = sa >= 0 ? T.e[sa] : 0;
+            const u32 pa = sa >= 0 ? T.pv[sa] : 0u;
+            const int fb = sb >= 0 ? T.f[sb] : INT_MAX, eb = sb >= 0 ? T.e[sb] : 0;
+            const u32 pb = sb >= 0 ? T.pv[sb] : 0u;
+            // a wave whose positions lie in no active segment (handed on, or past the item) skips its rows
+            const bool live = (sa >= 0 && wb < ea) || (sb >= 0 && fb < wb + kMRows * 64 && fb < e0);
+            u32 kv[kMRows];
+            u32 rk[kMRows];
+            u32 bstop = 0, bend = 0, bsel = 0;   // bit j: left / right stop (j + 16); first / last - 1; segment b
+            u32 cL = 0, cR = 0;
+#pragma unroll
+            for (int j = 0; j < kMRows; ++j) {
+                kv[j] = 0u;
+                rk[j] = 0u;
+                if (live && wb + j * 64 + l < e0) kv[j] = st.key(wb + j * 64 + l);
+            }
+            // the common case: every position of the wave strictly inside segment a (neither its first nor
+            // its last): no per-row segment selection
+            const bool inner = sa >= 0 && wb > fa && wb + kMRows * 64 < ea && wb + kMRows * 64 <= e0;
+            if (inner) {
+#pragma unroll
+                for (int j = 0; j < kMRows; ++j) {
+                    const bool bl = !(kv[j] < pa), br = !(pa < kv[j]);
+                    const u64 mL = __ballot(bl), mR = __ballot(br);
+                    rk[j] = (cL + (u32)__popcll(mL & lt)) | ((cR + (u32)__popcll(mR & lt)) << 16);
+                    bstop |= ((u32)bl << j) | ((u32)br << (j + 16));
+                    cL += (u32)__popcll(mL);
+                    cR += (u32)__popcll(mR);
                 }
-                const int cut = wave_partition(S.K, S.I, S.LP, S.RQ, first, last);
-                if (l == 0) {
-                    if (cut - first > kThreshold) S.seg[cur ^ 1][atomicAdd(&S.nseg[cur ^ 1], 1)] = seg_pack(first, cut, d - 1);
-                    if (last - cut > kThreshold) S.seg[cur ^ 1][atomicAdd(&S.nseg[cur ^ 1], 1)] = seg_pack(cut, last, d - 1);
+            }
+#pragma unroll
+            for (int j = 0; j < kMRows; ++j) {
+                if (!live || inner) break;
+                const int p = wb + j * 64 + l;
+                const bool ina = p < e0 && sa >= 0 && p >= fa && p < ea;
+                const bool inb = p < e0 && !ina && p >= fb && p < eb;
+                const bool in = ina || inb;
+                const int first = ina ? fa : fb, last = ina ? ea : eb;
+                const u32 pv = ina ? pa : pb;
+                const bool bl = in && p > first && !(kv[j] < pv);
+                const bool br = in && !(pv < kv[j]);
+                bend |= ((u32)(in && p == first) << j) | ((u32)(in && p == last - 1) << (j + 16));
+                bsel |= (u32)inb << j;
+                const u64 mL = __ballot(bl), mR = __ballot(br);
+                rk[j] = (cL + (u32)__popcll(mL & lt)) | ((cR + (u32)__popcll(mR & lt)) << 16);
+                bstop |= ((u32)bl << j) | ((u32)br << (j + 16));
+                cL += (u32)__popcll(mL);
+                cR += (u32)__popcll(mR);
+            }
+            if (l == 0) S.wt[par][w] = (cL << 16) | cR;
+            __syncthreads();
+            u32 oL = 0, oR = 0, tL = 0, tR = 0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const u32 c = S.wt[par][q];
+                oL += q < w ? (c >> 16) : 0u;
+                oR += q < w ? (c & 0xffffu) : 0u;
+                tL += c >> 16;
+                tR += c & 0xffffu;
+            }
+            const u32 c0L = S.carry[par][0], c0R = S.carry[par][1];
+            oL += c0L;
+            oR += c0R;
+            if (t == 0) {
+                S.carry[par ^ 1][0] = c0L + tL;
+                S.carry[par ^ 1][1] = c0R + tR;
+            }
+#pragma unroll
+            for (int j = 0; j < kMRows; ++j) {
+                if (!live) break;
+                const int p = wb + j * 64 + l;
+                const bool bl = (bstop >> j) & 1u, br = (bstop >> (j + 16)) & 1u;
+                const u32 gL = oL + (rk[j] & 0xFFFFu), gR = oR + (rk[j] >> 16);
+                const int sx = ((bsel >> j) & 1u) ? sb : sa;
+                if (bl) st.setL(gL, p);
+                if (br) st.setR(gR, p);
+                if ((bend >> j) & 1u) {
+                    T.bl[sx] = gL;
+                    T.br[sx] = gR;
                 }
-                leaf_sort2(S.K, S.I, first, cut, cut, last);
-                __builtin_amdgcn_wave_barrier();
+                if ((bend >> (j + 16)) & 1u) {
+                    T.el[sx] = gL + (bl ? 1u : 0u);
+                    T.er[sx] = gR + (br ? 1u : 0u);
+                }
             }
             __syncthreads();
-            if (t == 0) S.nseg[cur] = 0;
-            cur ^= 1;
-            __syncthreads();
         }
-    }
-    __syncthreads();
-    for (int i = t; i < len; i += 1024) {
-        keys[f + i] = S.K[i];
-        vals[f + i] = v[f + S.I[i]];
+        const u32 TL = S.carry[nt & 1][0];
+        __threadfence_block();
+        __syncthreads();
+        PART_PROF(8 * lev + 1, rt_now());
+        // 2. in rank space: left stop k of its segment hits when L_k < R_(nR + 1 - k); m = the hits
+        for (u32 gb = 0; gb < TL; gb += kMT * kMBatch) {
+            int s[kMBatch];
+            int pp[kMBatch], qq[kMBatch];
+#pragma unroll
+            for (int i = 0; i < kMBatch; ++i) {
+                const u32 g = gb + (u32)(i * kMT + t);
+                s[i] = -1;
+                pp[i] = 0;
+                qq[i] = -1;
+                if (g < TL) {
+                    const int sx = med_rank_seg(T, ns, g);
+                    const u32 kk = g - T.bl[sx] + 1, nR = T.er[sx] - T.br[sx];
+                    s[i] = sx;
+                    pp[i] = st.getL(g);
+                    if (kk <= nR) qq[i] = st.getR(T.br[sx] + nR - kk);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kMBatch; ++i) seg_count(T.m, s[i] >= 0 && pp[i] < qq[i], s[i]);
+        }
+        __threadfence_block();
+        __syncthreads();
+        PART_PROF(8 * lev + 2, rt_now());
+        // 3. one thread per segment: the cut min(L_(m + 1), R_(nR + 1 - m)) (L_1 for m = 0)
+        for (int i = t; i < ns; i += kMT) {
+            const int m = (int)T.m[i];
+            const int nL = (int)(T.el[i] - T.bl[i]), nR = (int)(T.er[i] - T.br[i]);
+            int cut;
+            if (m == 0) {
+                cut = nL ? st.getL(T.bl[i]) : T.e[i];
+            } else {
+                const int r = st.getR(T.br[i] + (u32)(nR - m));
+                const int lf = m < nL ? st.getL(T.bl[i] + (u32)m) : INT_MAX;
+                cut = lf < r ? lf : r;
+            }
+            T.cut[i] = cut;
+        }
+        __syncthreads();
+        PART_PROF(8 * lev + 3, rt_now());
+        // 4. the swaps L_k <-> R_(nR + 1 - k), k <= m
+        for (u32 gb = 0; gb < TL; gb += kMT * kMBatch) {
+            int pp[kMBatch], qq[kMBatch];
+            u32 pr = 0;
+#pragma unroll
+            for (int i = 0; i < kMBatch; ++i) {
+                const u32 g = gb + (u32)(i * kMT + t);
+                pp[i] = 0;
+                qq[i] = 0;
+                if (g < TL) {
+                    const int sx = med_rank_seg(T, ns, g);
+                    const u32 kk = g - T.bl[sx] + 1;
+                    if (kk <= T.m[sx]) {
+                        pr |= 1u << i;
+                        pp[i] = st.getL(g);
+                        qq[i] = st.getR(T.er[sx] - kk);
+                    }
+                }
+            }
+            u32 x[kMBatch][4];
+#pragma unroll
+            for (int i = 0; i < kMBatch; ++i)
+                if ((pr >> i) & 1u) st.load2(pp[i], qq[i], x[i]);
+#pragma unroll
+            for (int i = 0; i < kMBatch; ++i)
+                if ((pr >> i) & 1u) st.store2(pp[i], qq[i], x[i]);
+        }
+        __threadfence_block();
+        __syncthreads();
+        PART_PROF(8 * lev + 4, rt_now());
+        // 5. children in position order: above the stop into the next table, the others handed on
+        const int nx = cur ^ 1;
+        if (w == 0) {
+            MedTab<NSEG>& N = S.tab[nx];
+            int nn = 0;
+            for (int c0 = 0; c0 < ns; c0 += 64) {
+                const int si = c0 + l;
+                const bool ok = si < ns;
+                int ff = 0, ee = 0, cut = 0, dd = 0;
+                if (ok) {
+                    ff = T.f[si];
+                    ee = T.e[si];
+                    cut = T.cut[si];
+                    dd = T.d[si] - 1;
+                }
+                const bool bigL = ok && cut - ff > stop && dd > 0;
+                const bool bigR = ok && ee - cut > stop && dd > 0;
+                const u64 b1 = __ballot(bigL), b2 = __ballot(bigR);
+                const int iL = nn + __popcll(b1 & lt) + __popcll(b2 & lt);
+                const int iR = iL + (bigL ? 1 : 0);
+                nn += __popcll(b1) + __popcll(b2);
+                if (ok) {
+                    const int cf[2] = {ff, cut}, ce[2] = {cut, ee};
+                    const bool bg[2] = {bigL, bigR};
+                    const int ix[2] = {iL, iR};
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int a = cf[h], b = ce[h];
+                        if (b - a < 1) continue;
+                        if (bg[h]) {
+                            if (ix[h] < NSEG) {
+                                N.f[ix[h]] = a;
+                                N.e[ix[h]] = b;
+                                N.d[ix[h]] = dd;
+                                N.m[ix[h]] = 0;
+                                N.pv[ix[h]] = st.median(a, b);
+                            } else {
+                                atomicOr(err, 4);
+                            }
+                        } else if (b - a > stop) {             // the depth limit above the stop size
+                            emit(a, b, -1);
+                        } else {
+                            emit(a, b, dd);
+                        }
+                    }
+                }
+            }
+            if (l == 0) S.n[nx] = nn < NSEG ? nn : NSEG;
+        }
+        __threadfence_block();
+        __syncthreads();
+        PART_PROF(8 * lev + 5, rt_now());
+        cur = nx;
+        ++lev;
     }
     __syncthreads();
 }
 
-// fallback for a segment above kTieLocal left by the big levels: one Hoare partition of [first, last)
-// by the whole workgroup in global memory (4 rows of 1024 keys per round); returns the cut
-__device__ int wg_partition(LocalLds& S, u32* k, u32* v, u32* lp, u32* rq, int first, int last) {
-    const int t = threadIdx.x, wv = t >> 6, l = lane_id();
+// hands a segment on: to the LDS mid tier above kTieSmall keys, else (and final segments) to the locals
+struct EmitGlobal {
+    int* ctl;
+    int4 *mid, *jobs;
+    int midcap, jcap, cls;
+    int* err;
+    __device__ void operator()(int f, int e, int d) const {
+        if (e - f < 1) return;
+        if (d >= 0 && e - f > kTieSmall) {
+            const int j = atomicAdd(&ctl[T_NMID], 1);
+            if (j < midcap) mid[j] = make_int4(f, e, d, cls);
+            else atomicOr(err, 4);
+        } else {
+            file_job(ctl, jobs, jcap, err, f, e, d, cls);
+        }
+    }
+};
+
+// L1: one 1024-thread workgroup per class (from_classes: after moving the class's valid pairs into the
+// working copy at its input offset) or per medium segment of the big path
+__global__ void __launch_bounds__(1024) k_tie_medium(const u32* __restrict__ keys, const u32* __restrict__ vals,
+                                                     TieClasses cls, int from_classes, int depth0, u32* k, u32* v,
+                                                     u32* lp, u32* rq, int* ctl, const int4* __restrict__ med,
+                                                     int4* mid, int midcap, int4* jobs, int jcap, int* err) {
+    __shared__ MedWork<512> S;
+    const int t = threadIdx.x, w = t >> 6, l = lane_id();
     const u64 lt = lanemask_lt();
-    if (t == 0) {
-        const int a = first + 1, b = first + (last - first) / 2, c = last - 1;
-        const int sel = median3(k[a], k[b], k[c], a, b, c);
-        const u32 kf = k[first], ks = k[sel], vf = v[first], vs = v[sel];
-        k[first] = ks;
-        k[sel] = kf;
-        v[first] = vs;
-        v[sel] = vf;
-        S.tot = ks;
-    }
-    __threadfence_block();
-    __syncthreads();
-    const u32 pv = S.tot;
-    int nL = 0, nR = 0;
-    for (int base = first; base < last; base += 4096) {
-        __syncthreads();                                         // S.tot / S.cnt reuse
-        u64 mL[4], mR[4];
+    const int nitems = from_classes ? cls.nc : ctl[T_NMED];
+    for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+        int f0, e0, d0, cl;
+        if (from_classes) {
+            int start[kMaxTieC + 1];
+            class_starts(cls, start);
+            cl = it;
+            const int a = start[cl], b = start[cl + 1];
+            if (t == 0) S.carry[0][0] = 0;
+            __syncthreads();
+            int nt = 0;
+            for (int tb = a; tb < b; tb += kMTile, ++nt) {
+                const int par = nt & 1;
+                u32 kk[kMRows], vv[kMRows], pos[kMRows];
+                u32 cnt = 0;
+                const int ib = tb + w * kMRows * 64 + l;           // one base, immediate row offsets
+                const u32* kb = keys + ib;
+                const u32* vb = vals + ib;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = base + j * 1024 + t;
-            const bool in = i < last;
-            const u32 key = in ? k[i] : 0u;
-            mL[j] = __ballot(in && i > first && !(key < pv));
-            mR[j] = __ballot(in && !(pv < key));
-            if (l == 0) S.cnt[j * 16 + wv] = ((u32)__popcll(mL[j]) << 16) | (u32)__popcll(mR[j]);
-        }
-        __syncthreads();
-        if (wv == 0) {
-            const u32 cc = S.cnt[l];
-            const u32 inc = wave_incl_scan_u32(cc);
-            S.cnt[l] = inc - cc;
-            if (l == 63) S.tot = inc;
-        }
-        __syncthreads();
+                for (int j = 0; j < kMRows; ++j) {
+                    kk[j] = kTieDrop;
+                    vv[j] = 0u;
+                    if (ib + j * 64 < b) {
+                        kk[j] = kb[j * 64];
+                        vv[j] = vb[j * 64];
+                    }
+                }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = base + j * 1024 + t;
-            const u32 o = S.cnt[j * 16 + wv];
-            if ((mL[j] >> l) & 1ull) lp[first + nL + (int)(o >> 16) + __popcll(mL[j] & lt)] = (u32)i;
-            if ((mR[j] >> l) & 1ull) rq[first + nR + (int)(o & 0xffffu) + __popcll(mR[j] & lt)] = (u32)i;
+                for (int j = 0; j < kMRows; ++j) {
+                    const u64 m = __ballot(kk[j] != kTieDrop);
+                    pos[j] = cnt + (u32)__popcll(m & lt);
+                    cnt += (u32)__popcll(m);
+                }
+                if (l == 0) S.wt[par][w] = cnt;
+                __syncthreads();
+                u32 off = 0, tot = 0;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const u32 c = S.wt[par][q];
+                    off += q < w ? c : 0u;
+                    tot += c;
+                }
+                const u32 c0 = S.carry[par][0];
+                off += c0;
+                if (t == 0) S.carry[par ^ 1][0] = c0 + tot;
+#pragma unroll
+                for (int j = 0; j < kMRows; ++j)
+                    if (kk[j] != kTieDrop) {
+                        k[a + off + pos[j]] = kk[j];
+                        v[a + off + pos[j]] = vv[j];
+                    }
+                __syncthreads();
+            }
+            const int vc = (int)S.carry[nt & 1][0];
+            f0 = a;
+            e0 = a + vc;
+            d0 = vc > 0 ? (depth0 >= 0 ? depth0 : 2 * lg_floor(vc)) : 0;
+            if (t == 0) {
+                ctl[T_VC + cl] = vc;
+                ctl[T_BASE + cl] = a;
+            }
+            __threadfence_block();
+            __syncthreads();
+        } else {
+            const int4 mi = med[it];
+            f0 = mi.x;
+            e0 = mi.y;
+            d0 = mi.z;
+            cl = mi.w;
         }
-        nL += (int)(S.tot >> 16);
-        nR += (int)(S.tot & 0xffffu);
+        GStore st{k, v, lp, rq, f0};
+        part_levels<512>(st, S, f0, e0, d0, kTieMid, EmitGlobal{ctl, mid, jobs, midcap, jcap, cl, err}, err,
+                         blockIdx.x == 0 && it == 0 ? 256 : -1);
     }
-    __threadfence_block();
-    __syncthreads();
-    const int m = wg_msearch<1024>(lp, rq, first, nL, nR);
-    if (t == 0) S.cut = cut_of(lp, rq, first, nL, nR, m);
-    for (int q = t; q < m; q += 1024) {
-        const int pl = (int)lp[first + q], pr = (int)rq[first + nR - 1 - q];
-        const u32 kl = k[pl], kr = k[pr], vl = v[pl], vr = v[pr];
-        k[pl] = kr;
-        k[pr] = kl;
-        v[pl] = vr;
-        v[pr] = vl;
-    }
-    __threadfence_block();
-    __syncthreads();
-    return S.cut;
 }
 
-// the local jobs; workgroup 0 also ends the key array with the dropped pairs
-__global__ void __launch_bounds__(1024) k_tie_local(u32* __restrict__ k, u32* __restrict__ v, u32* __restrict__ lp,
-                                                    u32* __restrict__ rq, const int4* __restrict__ jobs,
-                                                    const int* __restrict__ ctl, u32* __restrict__ keys,
-                                                    u32* __restrict__ vals, TieClasses cls) {
-    __shared__ LocalLds S;
+// L2: one workgroup per segment of kTieSmall .. kTieMid keys, staged in LDS, partitioned until every
+// segment fits kTieSmall, then written back
+struct MidLds {
+    u32 K[kTieMid];
+    u16 I[kTieMid], LP[kTieMid], RP[kTieMid];   // LP and RP adjacent: u32[kTieMid] for the write-back
+    MedWork<16> W;
+};
+struct EmitJob {
+    int* ctl;
+    int4* jobs;
+    int jcap, cls, off;
+    int* err;
+    __device__ void operator()(int f, int e, int d) const { file_job(ctl, jobs, jcap, err, off + f, off + e, d, cls); }
+};
+__global__ void __launch_bounds__(1024) k_tie_mid(u32* k, u32* v, int* ctl, const int4* __restrict__ mid,
+                                                  int4* jobs, int jcap, int* err) {
+    __shared__ MidLds S;
     const int t = threadIdx.x;
+    const int nm = ctl[T_NMID];
+    for (int it = blockIdx.x; it < nm; it += gridDim.x) {
+        const int4 mi = mid[it];
+        const int f = mi.x, len = mi.y - mi.x;
+        for (int i = t; i < len; i += kMT) {
+            S.K[i] = k[f + i];
+            S.I[i] = (u16)i;
+        }
+        __syncthreads();
+        LStore st{S.K, S.I, S.LP, S.RP};
+        part_levels<16>(st, S.W, 0, len, mi.z, kTieSmall, EmitJob{ctl, jobs, jcap, mi.w, f, err}, err,
+                        blockIdx.x == 0 && it == 0 ? 512 : -1);
+        // back to the working copy: the values the keys carry gathered into the (now free) rank lists
+        // first, since the gather reads the same range of v that is then written
+        u32* VV = reinterpret_cast<u32*>(S.LP);
+        for (int i = t; i < len; i += kMT) VV[i] = v[f + S.I[i]];
+        __syncthreads();
+        for (int i = t; i < len; i += kMT) {
+            k[f + i] = S.K[i];
+            v[f + i] = VV[i];
+        }
+        __syncthreads();
+    }
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// L3 local: one 1024-thread workgroup per job of at most kTieSmall keys, the whole subtree in LDS, every
+// segment of a level at once. Wave w owns rows 2 w, 2 w + 1 of 64 (ranks within a row from ballots).
+constexpr int kLWaves = 16;
+constexpr int kLRows = kTieSmall / (64 * kLWaves);
+constexpr int kLSeg = kTieSmall / (kThreshold + 1) + 2;    // segments of one level (> 16 keys each)
+constexpr int kWaveSeg = 64;                                // segments this short: finished by one wave
+constexpr int kLSmall = kTieSmall / (kThreshold + 1) + 2;  // such segments of one job
+// segment ids: a level's table index, or a terminal state (leaf, heap-sorted, finished by a wave)
+constexpr u32 kSegLeaf = 0xFFFFu, kSegHeap = 0xFFFEu, kSegWave = 0xFFFDu, kSegLive = 0xFFFDu;
+static_assert(kLRows * 64 * kLWaves == kTieSmall, "rows");
+
+struct LocTab {
+    u64 A[kLSeg];       // first | last << 16 | pivot << 32
+    u32 cd[kLSeg];      // depth while the level runs, then the children: left | right << 16
+    u32 cut[kLSeg];     // min of the cut candidates (starts at last)
+    u32 base[kLSeg];    // L | R << 16: stop ranks before first
+    u32 ends[kLSeg];    // R rank up to last - 1
+};
+struct LocalLds {
+    u32 K[kTieSmall];
+    u16 I[kTieSmall], RP[kTieSmall];
+    LocTab tab[2];
+    u32 lb[kTieSmall / 32];      // first positions of the leaves / heap segments
+    u32 small[kLSmall];          // segments for the waves: first | length << 16 | depth << 24
+    unsigned char SL[kLWaves][64], SR[kLWaves][64];   // a wave's rank lists while it finishes a segment
+    u32 wl[kLWaves], wr[kLWaves];
+    int n[2], nsmall;
+};
+
+__device__ __forceinline__ void lb_set(u32* lb, int p) { atomicOr(&lb[p >> 5], 1u << (p & 31)); }
+
+// a row's position: wave w owns rows kLRows w .. kLRows w + kLRows - 1
+__device__ __forceinline__ int lpos(int w, int j, int l) { return (w * kLRows + j) * 64 + l; }
+
+// the segment id one level down: the child of the parent segment on p's side of its cut
+__device__ __forceinline__ u32 child_of(const LocTab& P, u32 s, int p) {
+    if (s >= kSegLive) return s;
+    const u32 ch = P.cd[s];
+    return p < (int)P.cut[s] ? (ch & 0xFFFFu) : (ch >> 16);
+}
+
+// one wave finishes a segment of 17 .. 64 keys [f, f + n) at depth d, one key per lane: every
+// recursion level of its subtree at once in registers (a lane's segment [sf, se) in lane space), the
+// rank lists in the wave's LDS bytes, the exchange of a partition by lane shuffles; then the leaves sorted
+// stably and written back; a segment at the depth limit goes back as it stands and is filed for k_tie_heap
+// (ofs: the output index of the job's position 0)
+__device__ void wave_finish(LocalLds& S, int f, int n, int d, long long ofs, int* ctl, const HeapList& hl) {
+    const int w = threadIdx.x >> 6, l = lane_id();
+    const u64 lt = lanemask_lt(), le = lt | (1ull << l);
+    const bool in = l < n;
+    u32 key = in ? S.K[f + l] : 0xFFFFFFFFu;
+    u32 idx = in ? S.I[f + l] : 0u;
+    int sf = 0, se = n, dd = d;
+    unsigned char* SL = S.SL[w];
+    unsigned char* SR = S.SR[w];
+    for (;;) {
+        const bool act = in && se - sf > kThreshold && dd > 0;
+        if (!__ballot(act)) break;
+        const int a = sf + 1, b = sf + (se - sf) / 2, c = se - 1;
+        const u32 ka = (u32)__shfl((int)key, a, 64), kb = (u32)__shfl((int)key, b, 64), kc = (u32)__shfl((int)key, c, 64);
+        const int sel = median3(ka, kb, kc, a, b, c);
+        const u32 ksel = (u32)__shfl((int)key, sel, 64), isel = (u32)__shfl((int)idx, sel, 64);
+        const u32 kfst = (u32)__shfl((int)key, sf, 64), ifst = (u32)__shfl((int)idx, sf, 64);
+        if (act && l == sf) {
+            key = ksel;
+            idx = isel;
+        } else if (act && l == sel) {
+            key = kfst;
+            idx = ifst;
+        }
+        const u32 pv = ksel;
+        const bool bl = act && l > sf && !(key < pv);
+        const bool br = act && !(pv < key);
+        const u64 ML = __ballot(bl), MR = __ballot(br);
+        const u64 smask = (se >= 64 ? ~0ull : ((1ull << se) - 1)) & ~((1ull << sf) - 1);
+        const int kL = __popcll(ML & smask & le);                 // 1-based rank of a left stop
+        const int nL = __popcll(ML & smask), nR = __popcll(MR & smask);
+        const int rlt = __popcll(MR & smask & lt);                // right stops before l
+        const bool pred = bl && nR - (rlt + (br ? 1 : 0)) >= kL;  // L_k < R_(nR + 1 - k)
+        if (bl) SL[sf + kL - 1] = (unsigned char)l;
+        if (br) SR[sf + rlt] = (unsigned char)l;
+        const int m = __popcll(__ballot(pred) & smask);
+        __builtin_amdgcn_s_waitcnt(0xc07f);                       // lgkmcnt(0): the lists are written
+        __builtin_amdgcn_wave_barrier();
+        int src = l;
+        const int kr = nR - rlt;                                  // a right stop's rank from the right
+        if (pred) src = SR[sf + nR - kL];
+        else if (br && kr <= m) src = SL[sf + kr - 1];
+        int cut = se;
+        if (act) {
+            if (m == 0) cut = nL ? SL[sf] : se;
+            else {
+                const int r = SR[sf + nR - m];
+                const int lf = m < nL ? SL[sf + m] : 64;
+                cut = lf < r ? lf : r;
+            }
+        }
+        key = (u32)__shfl((int)key, src, 64);
+        idx = (u32)__shfl((int)idx, src, 64);
+        if (act) {
+            if (l < cut) se = cut;
+            else sf = cut;
+            --dd;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    // leaves: a stable rank inside [sf, se); heap segments (depth limit) go back as they are
+    const bool heap = in && se - sf > kThreshold;
+    int dest = l;
+    if (!heap) {
+        int r = 0;
+#pragma unroll
+        for (int i = 0; i < kThreshold; ++i) {
+            const int q = sf + i;
+            const u32 kq = (u32)__shfl((int)key, q < 64 ? q : 63, 64);
+            r += (q < se && (kq < key || (kq == key && q < l))) ? 1 : 0;
+        }
+        dest = sf + r;
+    }
+    if (in) {
+        S.K[f + dest] = key;
+        S.I[f + dest] = (u16)idx;
+    }
+    if (heap && l == sf) hl.file(ctl, ofs + f + sf, se - sf);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+}
+
+// the pass after the level loop: every key to its final place in the output. A leaf [st, en) (at most 16
+// keys, bounded by the nearest set bits of lb) is sorted stably (libstdc++'s final insertion sort moves
+// no key across a leaf); wave-finished segments are final, depth-limit ones stay as they are (k_tie_heap). The destinations go to RP
+// (free after the levels), then every row's value is gathered at once.
+__device__ __forceinline__ void local_output(LocalLds& S, int len, const u32 (&sg)[kLRows], const u32* v, int f,
+                                             long long obase, u32* keys_out, u32* vals_out) {
+    const int w = threadIdx.x >> 6, l = lane_id();
+    constexpr int kW = kTieSmall / 32;
+#pragma unroll 1
+    for (int j = 0; j < kLRows; ++j) {
+        const int p = lpos(w, j, l);
+        if (w * kLRows * 64 + j * 64 >= len) break;          // rows past the job (uniform)
+        if (sg[j] != kSegLeaf) {                              // final in place
+            if (p < len) S.RP[p] = (u16)p;
+            continue;
+        }
+        const int pc = p < len ? p : 0;
+        const u32 key = S.K[pc];
+        const int w0 = pc >> 5, b = pc & 31;
+        const u32 m0 = S.lb[w0], mm = S.lb[w0 > 0 ? w0 - 1 : 0], mp = S.lb[w0 + 1 < kW ? w0 + 1 : w0];
+        const u32 le = (b == 31) ? 0xFFFFFFFFu : ((2u << b) - 1u);
+        const u32 lo = m0 & le, hi = m0 & ~le;
+        const int st = lo ? (w0 << 5) + 31 - __clz(lo) : (mm ? ((w0 - 1) << 5) + 31 - __clz(mm) : 0);
+        int en = hi ? (w0 << 5) + __ffs(hi) - 1 : ((w0 + 1 < kW && mp) ? ((w0 + 1) << 5) + __ffs(mp) - 1 : len);
+        en = en < len ? en : len;
+        u32 kq[kThreshold];
+#pragma unroll
+        for (int i = 0; i < kThreshold; ++i) {
+            const int q = st + i;
+            kq[i] = S.K[q < en ? q : st];
+        }
+        int r = 0;
+#pragma unroll
+        for (int i = 0; i < kThreshold; ++i) {
+            const int q = st + i;
+            r += (q < en && (kq[i] < key || (kq[i] == key && q < p))) ? 1 : 0;
+        }
+        if (p < len) S.RP[p] = (u16)(st + r);
+    }
+    u32 dst[kLRows], ky[kLRows], ip[kLRows];
+#pragma unroll
+    for (int j = 0; j < kLRows; ++j) {
+        const int p = lpos(w, j, l), pc = p < len ? p : 0;
+        dst[j] = S.RP[pc];
+        ky[j] = S.K[pc];
+        ip[j] = S.I[pc];
+    }
+#pragma unroll
+    for (int j = 0; j < kLRows; ++j) ip[j] = v[f + (int)ip[j]];
+#pragma unroll
+    for (int j = 0; j < kLRows; ++j)
+        if (lpos(w, j, l) < len) {
+            const long long o = obase + f + (int)dst[j];
+            keys_out[o] = ky[j];
+            vals_out[o] = ip[j];
+        }
+}
+
+__global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, const u32* __restrict__ v,
+                                                    const int4* __restrict__ jobs, int* ctl, u32* __restrict__ arrive,
+                                                    u32* __restrict__ keys, u32* __restrict__ vals, TieClasses cls,
+                                                    HeapList hl) {
+    __shared__ LocalLds S;
+    const int t = threadIdx.x, w = t >> 6, l = lane_id();
+    const u64 lt = lanemask_lt();
     const int nj = ctl[T_NJOBS];
-    if (blockIdx.x == 0) {
+#ifdef PF_TIE_PROF
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        g_tie_prof[6] = (unsigned long long)nj;
+        g_tie_prof[7] = (unsigned long long)ctl[T_NMID];
+    }
+#endif
+    int vcs[kMaxTieC], obase[kMaxTieC];
+    int tot = 0;
+#pragma unroll
+    for (int c = 0; c < kMaxTieC; ++c) {
+        vcs[c] = c < cls.nc ? ctl[T_VC + c] : 0;
+        obase[c] = tot - ctl[T_BASE + c];           // output index = working-copy index + obase[class]
+        tot += vcs[c];
+    }
+    if (blockIdx.x == 0) {                          // the dropped pairs end the arrays
         int start[kMaxTieC + 1];
         const int n = class_starts(cls, start);
-        for (int i = ctl[T_VALID] + t; i < n; i += 1024) {
+        for (int i = tot + t; i < n; i += 1024) {
             keys[i] = kTieDrop;
             vals[i] = kTieDrop;
         }
+        if (t == 0) ctl[T_VALID] = tot;
     }
-    for (int j = blockIdx.x; j < nj; j += gridDim.x) {
-        const int4 jb = jobs[j];
-        if (jb.y - jb.x <= kTieLocal) {
-            lds_sort(S, k, v, keys, vals, jb.x, jb.y - jb.x, jb.z);
+    for (int jb = blockIdx.x; jb < nj; jb += gridDim.x) {
+        const int4 job = jobs[jb];
+        const int f = job.x, len = job.y - job.x, d = job.z;
+        long long ob = 0;
+#pragma unroll
+        for (int c = 0; c < kMaxTieC; ++c)
+            if (c == job.w) ob = obase[c];
+        if (d < 0) {                                // at the depth limit in a partition tier: as it stands
+            for (int i = t; i < len; i += 1024) {
+                keys[ob + f + i] = k[f + i];
+                vals[ob + f + i] = v[f + i];
+            }
+            if (t == 0) hl.file(ctl, ob + f, len);
             continue;
         }
+        // the segment id of every position this lane owns stays in its registers for the whole job;
+        // ract: this wave's rows holding a position still in an active segment (wave-uniform)
+        const u32 root = len <= kThreshold ? kSegLeaf : (d == 0 ? kSegHeap : (len <= kWaveSeg ? kSegWave : 0u));
+        u32 sg[kLRows];
+        u32 ract = 0;
+#pragma unroll
+        for (int j = 0; j < kLRows; ++j) {
+            const int p = lpos(w, j, l);
+            sg[j] = p < len ? root : kSegLeaf;
+            if (p < len) {
+                S.K[p] = k[f + p];
+                S.I[p] = (u16)p;
+            }
+            ract |= (root == 0u && w * kLRows * 64 + j * 64 < len) ? (1u << j) : 0u;
+        }
+        for (int i = t; i < kTieSmall / 32; i += 1024) S.lb[i] = i == 0 ? 1u : 0u;
+        __syncthreads();
         if (t == 0) {
-            S.stk[0] = make_int4(jb.x, jb.y, jb.z, 0);
-            S.nstk = 1;
+            S.n[0] = root == 0u ? 1 : 0;
+            S.n[1] = 0;
+            S.nsmall = root == kSegWave ? 1 : 0;
+            S.small[0] = (u32)len << 16 | (u32)d << 24;
+            if (root == 0u) {
+                LocTab& T = S.tab[0];
+                const u32 pv = median_to_first(S.K, S.I, 0, len);
+                T.A[0] = ((u64)pv << 32) | ((u32)len << 16);
+                T.cd[0] = (u32)d;
+                T.cut[0] = (u32)len;
+            } else if (root == kSegHeap) {
+                hl.file(ctl, ob + f, len);
+            }
         }
         __syncthreads();
-        while (S.nstk > 0) {
-            __syncthreads();
-            if (t == 0) S.top = S.stk[--S.nstk];
-            __syncthreads();
-            const int4 sg = S.top;
-            const int first = sg.x, last = sg.y, len = sg.y - sg.x, d = sg.z;
-            if (len <= kTieLocal) {
-                lds_sort(S, k, v, keys, vals, first, len, d);
-                continue;
-            }
-            if (d == 0) {                                        // depth limit on a big segment
-                if (t == 0) heap_sort(k, v, first, len);
-                __threadfence_block();
-                __syncthreads();
-                for (int i = t; i < len; i += 1024) {
-                    keys[first + i] = k[first + i];
-                    vals[first + i] = v[first + i];
+        int cur = 0;
+        bool remap = false;
+        [[maybe_unused]] int lev = 0;
+        TIE_PROF(0, rt_now());
+        TIE_PROF(4, __builtin_amdgcn_s_memtime());
+        for (;;) {
+            const int ns = S.n[cur];
+            TIE_PROF(8 + 8 * lev, rt_now());
+            TIE_PROF(8 + 8 * lev + 5, (unsigned long long)ns);
+            if (ns == 0) break;
+            LocTab& T = S.tab[cur];
+            LocTab& P = S.tab[cur ^ 1];
+            // 1. every active position: its segment (the parent's child on its side of the cut), its
+            // stops, its wave-local ranks
+            u32 rk[kLRows];
+            u32 bstop = 0, bend = 0;           // bit j: left stop / right stop (j + 16); first / last - 1
+            u32 rstop = 0;                     // rows with any stop (wave-uniform)
+            {
+                u32 cL = 0, cR = 0;
+                u32 still = 0;
+#pragma unroll
+                for (int j = 0; j < kLRows; ++j) {
+                    rk[j] = 0;
+                    if (!((ract >> j) & 1u)) continue;
+                    const int p = lpos(w, j, l);
+                    const u32 key = S.K[p < len ? p : 0];
+                    if (remap) sg[j] = child_of(P, sg[j], p);
+                    const bool act = sg[j] < kSegLive;
+                    const u64 a = T.A[act ? sg[j] : 0u];
+                    const int first = (int)(a & 0xFFFFu), last = (int)((a >> 16) & 0xFFFFu);
+                    const u32 pv = (u32)(a >> 32);
+                    const bool bl = act && p > first && !(key < pv);
+                    const bool br = act && !(pv < key);
+                    bend |= ((u32)(act && p == first) << j) | ((u32)(act && p == last - 1) << (j + 16));
+                    const u64 mL = __ballot(bl), mR = __ballot(br);
+                    still |= __ballot(act) ? (1u << j) : 0u;
+                    rstop |= (mL | mR) ? (1u << j) : 0u;
+                    rk[j] = (cL + (u32)__popcll(mL & lt)) | ((cR + (u32)__popcll(mR & lt)) << 16);
+                    bstop |= ((u32)bl << j) | ((u32)br << (j + 16));
+                    cL += (u32)__popcll(mL);
+                    cR += (u32)__popcll(mR);
                 }
-                __syncthreads();
-                continue;
+                ract = still;
+                if (l == 0) {
+                    S.wl[w] = cL;
+                    S.wr[w] = cR;
+                }
             }
-            const int cut = wg_partition(S, k, v, lp, rq, first, last);
-            if (t == 0) {
-                S.stk[S.nstk++] = make_int4(cut, last, d - 1, 0);
-                S.stk[S.nstk++] = make_int4(first, cut, d - 1, 0);
+            __syncthreads();
+            TIE_PROF(8 + 8 * lev + 1, rt_now());
+            // 2. ranks: the right stops listed by rank, every segment's ranks at its ends
+            {
+                u32 oL = 0, oR = 0;
+#pragma unroll
+                for (int q = 0; q < kLWaves; ++q) {
+                    const u32 a = S.wl[q], b = S.wr[q];
+                    oL += q < w ? a : 0u;
+                    oR += q < w ? b : 0u;
+                }
+                const u32 off = oL | (oR << 16);
+#pragma unroll
+                for (int j = 0; j < kLRows; ++j) {
+                    if (!((rstop >> j) & 1u) && !((bend >> j) & 1u) && !((bend >> (j + 16)) & 1u)) continue;
+                    const int p = lpos(w, j, l);
+                    rk[j] += off;
+                    const u32 gR = rk[j] >> 16;
+                    const bool br = (bstop >> (j + 16)) & 1u;
+                    if (br) S.RP[gR] = (u16)p;
+                    if ((bend >> j) & 1u) T.base[sg[j]] = rk[j];
+                    if ((bend >> (j + 16)) & 1u) T.ends[sg[j]] = gR + (br ? 1u : 0u);
+                }
+            }
+            __syncthreads();
+            TIE_PROF(8 + 8 * lev + 2, rt_now());
+            // 3. the swaps: left stop k of its segment with R_(nR + 1 - k) while that lies after it
+            // (at least k right stops after L_k); every left stop offers the cut a candidate
+#pragma unroll
+            for (int j = 0; j < kLRows; ++j) {
+                if (!((rstop >> j) & 1u)) continue;
+                const bool bl = (bstop >> j) & 1u, br = (bstop >> (j + 16)) & 1u;
+                const int p = lpos(w, j, l);
+                u32 cand = (u32)p, s = 0;
+                if (bl) {
+                    s = sg[j];
+                    const u32 bs = T.base[s];
+                    const int bR = (int)(bs >> 16), eR = (int)T.ends[s];
+                    const int kk = (int)(rk[j] & 0xFFFFu) - (int)(bs & 0xFFFFu) + 1;
+                    const int rin = (int)(rk[j] >> 16) + (br ? 1 : 0) - bR;
+                    if (eR - bR - rin >= kk) {
+                        const int q = S.RP[eR - kk];
+                        const u32 kq = S.K[q], kp = S.K[p];
+                        const u16 iq = S.I[q], ip = S.I[p];
+                        S.K[p] = kq;
+                        S.I[p] = iq;
+                        S.K[q] = kp;
+                        S.I[q] = ip;
+                        cand = (u32)q;
+                    }
+                }
+                seg_min(T.cut, bl, s, cand);
+            }
+            __syncthreads();
+            TIE_PROF(8 + 8 * lev + 3, rt_now());
+            // 4. one thread per segment files its children: above 64 keys with depth left into the next
+            // table (median of three moved to first), 17 .. 64 keys to the waves, a child at the depth
+            // limit to k_tie_heap
+            const int nx = cur ^ 1;
+            LocTab& N = S.tab[nx];
+            {
+                const bool ok = t < ns;
+                int ff = 0, ee = 0, cut = 0, dd = 0;
+                if (ok) {
+                    const u64 a = T.A[t];
+                    ff = (int)(a & 0xFFFFu);
+                    ee = (int)((a >> 16) & 0xFFFFu);
+                    cut = (int)T.cut[t];
+                    dd = (int)T.cd[t] - 1;
+                }
+                const bool aL = ok && cut - ff > kWaveSeg && dd > 0;
+                const bool aR = ok && ee - cut > kWaveSeg && dd > 0;
+                const u64 b1 = __ballot(aL), b2 = __ballot(aR);
+                int wb = 0;
+                if (l == 0 && (b1 | b2)) wb = atomicAdd(&S.n[nx], __popcll(b1) + __popcll(b2));
+                wb = __shfl(wb, 0, 64);
+                const int iL = wb + __popcll(b1 & lt) + __popcll(b2 & lt);
+                const int iR = iL + (aL ? 1 : 0);
+                if (ok) {
+                    u32 ids[2];
+                    const int cf[2] = {ff, cut}, ce[2] = {cut, ee};
+                    const bool ac[2] = {aL, aR};
+                    const int ix[2] = {iL, iR};
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int a = cf[h], b = ce[h];
+                        if (ac[h]) {
+                            const u32 pv = median_to_first(S.K, S.I, a, b);
+                            N.A[ix[h]] = ((u64)pv << 32) | (u32)a | ((u32)b << 16);
+                            N.cd[ix[h]] = (u32)dd;
+                            N.cut[ix[h]] = (u32)b;
+                            ids[h] = (u32)ix[h];
+                        } else if (b - a > kThreshold && dd == 0) {
+                            hl.file(ctl, ob + f + a, b - a);      // depth limit (__partial_sort)
+                            ids[h] = kSegHeap;
+                        } else if (b - a > kThreshold) {
+                            S.small[atomicAdd(&S.nsmall, 1)] = (u32)a | ((u32)(b - a) << 16) | ((u32)dd << 24);
+                            ids[h] = kSegWave;
+                        } else {
+                            ids[h] = kSegLeaf;
+                        }
+                    }
+                    if (cut < ee && cut > ff) lb_set(S.lb, cut);
+                    T.cd[t] = ids[0] | (ids[1] << 16);
+                }
+                if (t == 0) S.n[cur] = 0;
+            }
+            __syncthreads();
+            TIE_PROF(8 + 8 * lev + 4, rt_now());
+            TIE_PROF(8 + 8 * lev + 6, rt_now());
+            cur = nx;
+            remap = true;
+            ++lev;
+        }
+        TIE_PROF(1, rt_now());
+        TIE_PROF(5, __builtin_amdgcn_s_memtime());
+        TIE_PROF(3, (unsigned long long)lev);
+        if (remap) {
+#pragma unroll
+            for (int j = 0; j < kLRows; ++j)
+                if ((ract >> j) & 1u) sg[j] = child_of(S.tab[cur ^ 1], sg[j], lpos(w, j, l));
+        }
+        // the short segments, one wave each
+        for (int i = w; i < S.nsmall; i += kLWaves) {
+            const u32 e = S.small[i];
+            wave_finish(S, (int)(e & 0xFFFFu), (int)((e >> 16) & 0xFFu), (int)(e >> 24), ob + f, ctl, hl);
+        }
+        __syncthreads();
+        local_output(S, len, sg, v, f, ob, keys, vals);
+        __syncthreads();
+        TIE_PROF(2, rt_now());
+    }
+    // the last workgroup out resets the job counter for the next sort
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+        const u32 a = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a == gridDim.x - 1) {
+            __hip_atomic_store(&ctl[T_NJOBS], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl[T_NMID], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// The depth-limit segments: libstdc++'s __partial_sort(first, last, last) = __make_heap + __sort_heap, on
+// the output in place, one workgroup per segment staged in LDS as key << 32 | value.
+//
+// __adjust_heap walks the hole from its start to a leaf, always to the larger child (the right one unless
+// right < left), moving each child up, then __push_heap lifts the value back while its parent is less than
+// it. Along a max-heap path the values never increase, so the same result comes top-down: at each hole
+// take the larger child as above; if it is less than the value, the value lands in the hole, else the
+// child moves up. A sift then only reads the two children of its hole and writes the hole, one level per
+// step, which is what lets __sort_heap's pops run as a pipeline: pop i + 1 reads the root's children
+// once pop i has left level 1, so with pops started two steps apart every later pop stays two levels
+// behind the one before it on any shared path and never reads a node that is still to change. A pop
+// starts by taking the last element q (its value) and writing the root there; it waits while an earlier
+// pop's hole is q or an ancestor of q, since that pop may still write q. __make_heap's sifts of one tree
+// level touch disjoint subtrees and run in parallel, deepest level first.
+constexpr int kHeapCap = 16384;     // longest segment staged in LDS (128 KB); longer: one thread, global
+constexpr int kHeapT = 256;
+constexpr int kHeapGrid = 256;
+
+__device__ __forceinline__ u32 hkey(u64 x) { return (u32)(x >> 32); }
+__device__ __forceinline__ int hlev(int x) { return 31 - __clz(x + 1); }
+
+// one step of __sort_heap's pipelined pops (wave 0; H as {value, key}): every step reads the children of
+// every hole in flight (and, on a step that may start a pop, the last element and the root) and writes
+// every hole, with no branch on the lane (a lane with nothing to write writes its own spare slot)
+struct HeapPops {
+    int nxt;              // the next pop to start (wave-uniform)
+    bool act;             // this lane's pop is in flight
+    int h, m;             // its hole, its heap size
+    uint2 vk;             // its value
+};
+template <bool MAY>
+__device__ __forceinline__ void heap_step(uint2* H2, HeapPops& P, int npops, int l) {
+    const int spare = kHeapCap + l;
+    bool start = false, mine = false;
+    int q = 0;
+    if (MAY) {
+        q = npops - P.nxt;                                    // the last element of the heap before pop nxt
+        const int sh = hlev(q) - hlev(P.h);
+        const bool blk = P.act && sh >= 0 && ((q + 1) >> sh) == P.h + 1;   // hole h is q or an ancestor
+        start = P.nxt < npops && __ballot(blk) == 0;
+        mine = start && l == (P.nxt & 63);
+        P.h = mine ? 0 : P.h;
+        P.m = mine ? q : P.m;
+        P.act = P.act || mine;
+    }
+    const int c1 = 2 * P.h + 1;
+    const bool has = P.act && c1 < P.m;                       // then c1 + 1 <= m < n
+    const int cr = has ? c1 : 0;
+    const uint2 a = H2[cr], b = H2[cr + 1];
+    if (MAY) {
+        const uint2 vq = H2[q], r0 = H2[0];
+        P.vk = mine ? vq : P.vk;
+        H2[mine ? q : spare] = r0;
+    }
+    const bool right = c1 + 1 < P.m && !(b.y < a.y);
+    const uint2 ch = right ? b : a;
+    const bool stop = !has || ch.y < P.vk.y;
+    H2[P.act ? P.h : spare] = stop ? P.vk : ch;
+    P.h = P.act ? (right ? c1 + 1 : c1) : P.h;
+    P.act = P.act && !stop;
+    P.nxt += start ? 1 : 0;
+    asm volatile("" ::: "memory");                            // LDS runs a wave's accesses in order
+}
+
+__global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32* __restrict__ vals, int* ctl,
+                                                     const int2* __restrict__ segs, u32* __restrict__ arrive) {
+    __shared__ u64 H[kHeapCap + 64];               // + a spare slot per lane of wave 0
+    const int t = threadIdx.x, l = lane_id();
+    const int nh = ctl[T_NHEAP];
+    for (int jb = blockIdx.x; jb < nh; jb += gridDim.x) {
+        const int2 sg = segs[jb];
+        const int off = sg.x, n = sg.y;
+        if (n > kHeapCap) {                                   // rare: one thread in global memory
+            if (t == 0) heap_sort(keys, vals, off, n);
+            __syncthreads();
+            continue;
+        }
+        for (int i = t; i < n; i += kHeapT) H[i] = ((u64)keys[off + i] << 32) | vals[off + i];
+        __syncthreads();
+        TIE_PROF(960, rt_now());
+        TIE_PROF(965, __builtin_amdgcn_s_memtime());
+        TIE_PROF(963, (unsigned long long)n);
+        // __make_heap: parents (n - 2) / 2 .. 0, a tree level at a time
+        for (int L = hlev((n - 2) / 2); L >= 0; --L) {
+            const int lo = (1 << L) - 1, hi = min((2 << L) - 2, (n - 2) / 2);
+            for (int x = lo + t; x <= hi; x += kHeapT) {
+                const u64 vk = H[x];
+                int h = x;
+                for (;;) {
+                    const int c1 = 2 * h + 1;
+                    if (c1 >= n) break;
+                    int c = c1;
+                    u64 a = H[c1];
+                    if (c1 + 1 < n) {
+                        const u64 b = H[c1 + 1];
+                        if (!(hkey(b) < hkey(a))) {
+                            a = b;
+                            c = c1 + 1;
+                        }
+                    }
+                    if (hkey(a) < hkey(vk)) break;
+                    H[h] = a;
+                    h = c;
+                }
+                H[h] = vk;
             }
             __syncthreads();
         }
+        // __sort_heap: pop i (i = 0 .. n - 2) in lane i % 64 of wave 0, a step at a time: every step reads
+        // the children of every hole in flight (and the last element and the root for a pop that starts)
+        // and writes every hole, with no branch on the lane (a lane with nothing to write writes its own
+        // spare slot). Steps go in pairs, a pop starting only on the first of a pair.
+        TIE_PROF(961, rt_now());
+        [[maybe_unused]] unsigned long long steps = 0;
+        if (t < 64) {
+            HeapPops P{0, false, 0, 0, make_uint2(0u, 0u)};
+            const int npops = n - 1;
+            for (;;) {
+                heap_step<true>(reinterpret_cast<uint2*>(H), P, npops, l);
+                heap_step<false>(reinterpret_cast<uint2*>(H), P, npops, l);
+#ifdef PF_TIE_PROF
+                steps += 2;
+#endif
+                if (P.nxt >= npops && __ballot(P.act) == 0) break;
+            }
+        }
+        TIE_PROF(962, rt_now());
+        TIE_PROF(966, __builtin_amdgcn_s_memtime());
+        TIE_PROF(964, steps);
         __syncthreads();
+        for (int i = t; i < n; i += kHeapT) {
+            const u64 x = H[i];
+            keys[off + i] = hkey(x);
+            vals[off + i] = (u32)x;
+        }
+        __syncthreads();
+    }
+    // the last workgroup out resets the list for the next sort
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+        const u32 a = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a == gridDim.x - 1) {
+            __hip_atomic_store(&ctl[T_NHEAP], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
 }  // namespace
 
-int tie_alloc(TieSort& t, size_t cap, int levels) {
-    if (levels < 0) levels = 0;
-    if (levels > 6) levels = 6;
+int tie_alloc(TieSort& t, size_t cap, int max_levels) {
+    if (cap < 1) cap = 1;
+    if (max_levels < 0) {
+        max_levels = 0;
+        while (max_levels < 8 && ((size_t)kTieMed << max_levels) < cap) ++max_levels;
+    }
+    if (max_levels > 8) max_levels = 8;
     t.cap = cap;
-    t.levels = levels;
-    t.bcap = kMaxTieC << levels;
-    t.jcap = kMaxTieC + 2 * (kMaxTieC << (levels + 1));
+    t.max_levels = max_levels;
+    t.bcap = kMaxTieC << max_levels;
+    t.mcap = 2 * t.bcap + kMaxTieC + 8;
+    // a partitioned segment files at most two pieces per level; the partitioned segments of a level
+    // are disjoint and longer than the tier's stop size
+    t.jcap = (int)(2 * 64 * (cap / kTieSmall + 1) + 64);
+    t.midcap = (int)(2 * 64 * (cap / kTieMid + 1) + 64);
+    t.hcap = (int)(cap / (kThreshold + 1) + 64);     // depth-limit segments are disjoint, > 16 keys each
     t.tiles = cap / kTieTile + (size_t)t.bcap + 8;
 #define PF_TALLOC(p, bytes) \
     if (hipMalloc(&(p), (bytes)) != hipSuccess) return PF_ENOMEM;
@@ -707,7 +1647,10 @@ int tie_alloc(TieSort& t, size_t cap, int levels) {
     PF_TALLOC(t.arrive, sizeof(u32) * 4);
     PF_TALLOC(t.big, sizeof(int4) * 2 * t.bcap);
     PF_TALLOC(t.tot, sizeof(u64) * t.bcap);
+    PF_TALLOC(t.med, sizeof(int4) * t.mcap);
+    PF_TALLOC(t.mid, sizeof(int4) * t.midcap);
     PF_TALLOC(t.jobs, sizeof(int4) * t.jcap);
+    PF_TALLOC(t.heaps, sizeof(int2) * t.hcap);
     PF_TALLOC(t.ctl, sizeof(int) * T_WORDS);
 #undef PF_TALLOC
     if (hipMemset(t.status, 0, sizeof(u64) * t.tiles) != hipSuccess || hipMemset(t.arrive, 0, sizeof(u32) * 4) != hipSuccess ||
@@ -717,25 +1660,51 @@ int tie_alloc(TieSort& t, size_t cap, int levels) {
 }
 
 void tie_free(TieSort& t) {
-    void* ptrs[] = {t.k, t.v, t.lp, t.rq, t.status, t.arrive, t.big, t.tot, t.jobs, t.ctl};
+    void* ptrs[] = {t.k, t.v, t.lp, t.rq, t.status, t.arrive, t.big, t.tot, t.med, t.mid, t.jobs, t.heaps, t.ctl};
     for (void* p : ptrs) (void)hipFree(p);
     t = TieSort{};
 }
 
-void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s) {
-    const int tg = (int)(t.tiles < (size_t)kTieGrid ? t.tiles : (size_t)kTieGrid);
-    hipLaunchKernelGGL(k_tie_compact, dim3(tg), dim3(256), 0, s, keys, vals, cls, t.k, t.v, t.ctl, t.status, t.arrive, err);
-    hipLaunchKernelGGL(k_tie_setup, dim3(1), dim3(64), 0, s, cls, t.ctl, t.big, t.jobs, t.levels, t.depth0);
-    for (int lev = 0; lev < t.levels; ++lev) {
-        const int p = lev & 1;
-        hipLaunchKernelGGL(k_tie_scan, dim3(tg), dim3(256), 0, s, t.k, t.big + p * t.bcap, t.ctl, p, t.lp, t.rq, t.tot,
-                           t.status, t.arrive + 1, err);
-        hipLaunchKernelGGL(k_tie_split, dim3(t.bcap), dim3(1024), 0, s, t.k, t.v, t.lp, t.rq, t.big + p * t.bcap, t.tot,
-                           t.ctl, p, lev == t.levels - 1 ? 1 : 0, t.big + (p ^ 1) * t.bcap, t.jobs);
+int tie_levels_for(const TieSort& t, size_t size_hint) {
+    int lv = 0;
+    while (lv < t.max_levels && ((size_t)kTieMed << lv) < size_hint) ++lv;
+    return lv;
+}
+
+void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s, int levels) {
+    if (levels > t.max_levels) levels = t.max_levels;
+    if (levels <= 0) {
+        hipLaunchKernelGGL(k_tie_medium, dim3(kMaxTieC), dim3(kMT), 0, s, keys, vals, cls, 1, t.depth0, t.k, t.v,
+                           t.lp, t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err);
+    } else {
+        const int tg = (int)(t.tiles < (size_t)kTieGrid ? t.tiles : (size_t)kTieGrid);
+        hipLaunchKernelGGL(k_tie_compact, dim3(tg), dim3(256), 0, s, keys, vals, cls, t.k, t.v, t.ctl, t.status,
+                           t.arrive, err);
+        hipLaunchKernelGGL(k_tie_setup, dim3(1), dim3(64), 0, s, cls, t.ctl, t.big, t.med, levels, t.depth0);
+        for (int lev = 0; lev < levels; ++lev) {
+            const int p = lev & 1;
+            hipLaunchKernelGGL(k_tie_scan, dim3(tg), dim3(256), 0, s, t.k, t.big + p * t.bcap, t.ctl, p, t.lp, t.rq,
+                               t.tot, t.status, t.arrive + 1, err);
+            hipLaunchKernelGGL(k_tie_split, dim3(t.bcap), dim3(1024), 0, s, t.k, t.v, t.lp, t.rq, t.big + p * t.bcap,
+                               t.tot, t.ctl, p, lev == levels - 1 ? 1 : 0, t.big + (p ^ 1) * t.bcap, t.med, t.mcap,
+                               err);
+        }
+        hipLaunchKernelGGL(k_tie_medium, dim3(kMedGrid), dim3(kMT), 0, s, keys, vals, cls, 0, t.depth0, t.k, t.v, t.lp,
+                           t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err);
     }
-    hipLaunchKernelGGL(k_tie_local, dim3(t.jcap), dim3(1024), 0, s, t.k, t.v, t.lp, t.rq, t.jobs, t.ctl, keys, vals, cls);
+    hipLaunchKernelGGL(k_tie_mid, dim3(kMidGrid), dim3(kMT), 0, s, t.k, t.v, t.ctl, t.mid, t.jobs, t.jcap, err);
+    hipLaunchKernelGGL(k_tie_local, dim3(kLocalGrid), dim3(1024), 0, s, t.k, t.v, t.jobs, t.ctl, t.arrive + 2, keys,
+                       vals, cls, HeapList{t.heaps, t.hcap, err});
+    hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heaps, t.arrive + 3);
 }
 
 const int* tie_valid_count(const TieSort& t) { return t.ctl + T_VALID; }
+
+#ifdef PF_TIE_PROF
+extern "C" int pf_dev_tie_prof(unsigned long long* out, int n) {
+    if (n > 1024) n = 1024;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tie_prof), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace pf

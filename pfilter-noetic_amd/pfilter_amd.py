@@ -139,7 +139,7 @@ EXPORTS = ["pf_fe_create", "pf_fe_destroy", "pf_fe_extract", "pf_odom_create", "
            "pf_odom_stage_times", "pf_odom_set_state", "pf_cls_normals", "pf_dcvc_default_params",
            "pf_dcvc_create", "pf_dcvc_destroy", "pf_dcvc_run", "pf_dcvc_reset", "pf_cls_set_dcvc", "pf_bpf_set_dcvc",
            "pf_host_alloc", "pf_host_free", "pf_odom_set_tie_order", "pf_odom_probe_assoc",
-           "pf_odom_merge_stats", "pf_bpf_set_front_lanes", "pf_dcvc_reserve"]
+           "pf_odom_merge_stats", "pf_bpf_set_front_lanes", "pf_dcvc_reserve", "pf_fe_set_tie_order"]
 
 _lib = None
 _vp = ctypes.c_void_p
@@ -187,6 +187,7 @@ def lib():
     if hasattr(L, "pf_odom_set_stage_a_reserve"):
         L.pf_odom_set_stage_a_reserve.argtypes = [_vp, _i]
     L.pf_fe_set_ring_model.argtypes = [_vp, ctypes.c_double, ctypes.c_double]
+    L.pf_fe_set_tie_order.argtypes = [_vp, _i]
     L.pf_odom_set_ring_model.argtypes = [_vp, ctypes.c_double, ctypes.c_double]
     L.pf_odom_get_state.argtypes = [_vp, _vp, _vp, ctypes.POINTER(_i)]
     L.pf_odom_snapshot.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_sz)]
@@ -373,6 +374,11 @@ class LaserProcessingClass:
         _check("pf_fe_extract", lib().pf_fe_extract(self._h, x.ctypes.data, n, 16, edge.ctypes.data,
                                                     ctypes.byref(ne), surf.ctypes.data, ctypes.byref(ns), cap))
         return edge[:ne.value].copy(), surf[:ns.value].copy()
+
+    def set_tie_order(self, enable):
+        """reference tie order of the sector sort (pf_fe_set_tie_order): equal curvatures as
+        libstdc++'s std::sort leaves them (src/laserProcessingClass.cpp:101-104)"""
+        _check("pf_fe_set_tie_order", lib().pf_fe_set_tie_order(self._h, int(bool(enable))))
 
     def __del__(self):
         if getattr(self, "_h", None):

@@ -152,3 +152,40 @@ def test_fe_sector_sizes_around_the_lds_limit(pa, pfref, pfsynth):
         re_, rs_ = _ref(pfref, x, 16)
         _same(ge, re_)
         _same(gs, rs_)
+
+
+def _tie_scan(pfsynth):
+    """an S64 frame plus five rings that repeat two points in runs of 16 (A x16, B x16, ...): exact
+    curvature ties, at 0 inside the runs (surf points) and at equal non-zero values on every A->B / B->A
+    boundary (edge candidates above 0.1)"""
+    x = pfsynth.Sequence("S64", n_frames=2, az_steps=800).frame(1)
+    parts = [x]
+    rng = np.random.default_rng(7)
+    for r in (3, 8, 14, 20, 27):
+        el = np.deg2rad(2.0 - r / 3.0)                       # ring r's centre (64-line formula, :38-39)
+        th = rng.uniform(0, 2 * np.pi, 2)
+        a = np.array([10 * np.cos(th[0]), 10 * np.sin(th[0]), 10 * np.tan(el), 0.5], np.float32)
+        b = np.array([13 * np.cos(th[1]), 13 * np.sin(th[1]), 13 * np.tan(el), 0.7], np.float32)
+        run = np.concatenate([np.repeat(a[None], 16, 0), np.repeat(b[None], 16, 0)])
+        parts.append(np.tile(run, (20, 1)))
+    return np.concatenate(parts).astype(np.float32)
+
+
+def test_fe_tie_order_equal_curvatures(pa, pfref, pfsynth):
+    """Reference tie order (pf_fe_set_tie_order): on a scan with exact curvature ties the device
+    equals the faithful oracle (libstdc++ std::sort itself, opts=0) bit for bit, and the stable
+    order still equals FE_STABLE_TIES; the two orders differ on this scan, so the check has teeth."""
+    x = _tie_scan(pfsynth)
+    lid = pfref.make_lidar(64, 3.0, 90.0)
+    fe = _fe(pa, 64)
+    se, ss = fe.featureExtraction(x)
+    _same(se, _ref(pfref, x, 64)[0])
+    _same(ss, _ref(pfref, x, 64)[1])
+    fe.set_tie_order(True)
+    te, ts = fe.featureExtraction(x)
+    re_, rs_ = pfref.feature_extraction(x, lid, opts=0)
+    _same(te, re_)
+    _same(ts, rs_)
+    assert not np.array_equal(ts.view(np.uint32), ss.view(np.uint32)), "no tie changed the surf order"
+    fe.set_tie_order(False)
+    _same(fe.featureExtraction(x)[1], ss)

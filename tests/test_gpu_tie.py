@@ -70,12 +70,26 @@ def test_tie_sort_big_levels_and_fallback(pa, pfref):
 def test_tie_sort_depth_limit_heap_branch(pa, pfref):
     """The depth-limit branch (libstdc++'s make_heap + sort_heap) on the device against the oracle's
     restatement with the same settable depth limit (itself checked against std::sort's own branch in
-    tests/test_oracle_units.py): LDS segments, and big segments at the limit (global heap sort)."""
+    tests/test_oracle_units.py): segments at the limit from every tier, in LDS and (20000 keys at depth 0)
+    in global memory."""
     rng = np.random.default_rng(24)
     for n in (17, 40, 300, 5000, 20000):
         keys = rng.integers(0, max(2, n // 5), n).astype(np.uint32)
         for depth in (0, 1, 2, 3, 5):
-            if n == 20000 and depth < 2:
-                continue                                 # one-thread global heap sort: slow, covered at 5000
             want = pfref.sort_perm(keys, "literal", depth)
             np.testing.assert_array_equal(pa.tie_sort(keys, depth=depth), want, err_msg="n=%d depth=%d" % (n, depth))
+
+
+def test_tie_sort_natural_depth_limit(pa, pfref):
+    """rgbds inputs reach libstdc++'s own depth limit: a voxel-ordered map with a few new points
+    appended sends median-of-three to one end, level after level, and leaves segments of thousands of
+    keys (up to nearly the whole map) to the heap sort (k_tie_heap: LDS up to 16384 keys, one thread in
+    global memory above)."""
+    rng = np.random.default_rng(25)
+    for nmap, napp in ((22000, 100), (12000, 60), (22000, 3700), (40000, 900)):
+        m = np.sort(rng.choice(1 << 24, nmap, replace=False))
+        keys = np.concatenate([m, rng.choice(m, napp)]).astype(np.uint32)
+        want = _expected(pfref, keys)
+        for levels in (0, 2):
+            np.testing.assert_array_equal(pa.tie_sort(keys, levels=levels), want,
+                                          err_msg="map %d + %d levels=%d" % (nmap, napp, levels))
