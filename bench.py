@@ -89,6 +89,11 @@ def parse(argv=None):
                     help="frames of pf_odom_frame_host from pageable memory (pcie_pageable); 0 = skip")
     ap.add_argument("--configs4-frames", type=int, default=100,
                     help="frames of the configs[4] pipeline leg (S128 scans, 2M-point map); 0 = skip")
+    ap.add_argument("--configs4-order", default="stable", choices=["tie", "stable"],
+                    help="sort order of the configs[4] leg: in the tie order a 2M-point voxel-ordered map "
+                         "with a few thousand appended points drives introsort to its depth limit on "
+                         "segments of up to the whole map, whose heap sort is serial (measured apart: "
+                         "DESIGN.md section 5)")
     ap.add_argument("--node-frames", type=int, default=1000,
                     help="frames of the node call pattern (pf_fe_extract -> pf_odom_update); 0 = skip")
     a = ap.parse_args(argv)
@@ -599,7 +604,7 @@ def node_pattern_leg(device, hptrs, warmup, nframes):
                     "pinned host RAM; frames %d..%d of the headline sequence" % (warmup, total - 1)}
 
 
-def configs4_leg(device, nframes, threads, warmup=3, timing_frames=20, use_graph=True):
+def configs4_leg(device, nframes, threads, warmup=3, timing_frames=20, use_graph=True, order=None):
     """BASELINE.json configs[4] as a pipeline: synthetic 128-line scans (~200k points; the reference has
     no 128-line ring formula, so the linear beam-model extension pf_odom_set_ring_model(15, -25) bins
     them) against a 2,000,000-point surf map (pfsynth.voxel_map: voxel centroids
@@ -607,7 +612,8 @@ def configs4_leg(device, nframes, threads, warmup=3, timing_frames=20, use_graph
     parameters (theta 0: no stability filter, the map keeps its size), scans HBM-resident, graph replay.
     Then the association's kNN alone on the last frame (pf_odom_probe_assoc: the exact 5-NN of k_assoc
     against the 2M-point grid, HIP events, algorithmic bytes per SURVEY 8(d)) and, for comparison, the
-    standalone thick-row kNN (k_knn_thick) on the same surf map and the same surf queries."""
+    standalone thick-row kNN (k_knn_thick) on the same surf map and the same surf queries.
+    order: "tie" / "stable" for this leg alone (default: the run's --order)"""
     import pfilter_amd as pa
     import pfsynth
     total = 1 + warmup + nframes + timing_frames
@@ -626,7 +632,7 @@ def configs4_leg(device, nframes, threads, warmup=3, timing_frames=20, use_graph
     lid = pa.make_lidar(128, 3.0, 90.0, 0.1, ring_model=(15.0, -25.0))
     od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
     od.init(lid, 0.4, 0, 0.0, 0, 0)
-    set_order(od)
+    od.set_tie_order((order or ORDER[0]) == "tie")
     od.set_graph(use_graph)
     od.frame_device(*ptrs[0])
     od.sync()
@@ -1146,6 +1152,7 @@ def main(argv=None):
     if world == 1 and not stub and args.other_order_frames > 0:
         other = "stable" if args.order == "tie" else "tie"
         try:
+            log("other-order leg (%s) ..." % other)
             oo = order_leg(local_rank, r["ptrs"], args.warmup, args.other_order_frames, other, graph_mode(args))
             oo["ratio_to_value"] = round(oo["value"] / value, 4)
             out["other_order"] = oo
@@ -1157,6 +1164,7 @@ def main(argv=None):
         out["stub"] = True
     elif world == 1 and not args.no_roofline:
         try:
+            log("roofline leg ...")
             out["roofline"] = knn_roofline(local_rank, pmc=not args.no_pmc)
         except Exception as e:  # report, never hide
             log("roofline leg failed: %r" % (e,))
@@ -1164,6 +1172,7 @@ def main(argv=None):
     if world == 1 and args.bpf_frames > 0 and not stub:
         for name, dc in (("bpf", False), ("bpf_dcvc", True)):
             try:
+                log("%s leg ..." % name)
                 out[name] = bpf_leg(local_rank, args.bpf_frames, threads, with_cpu=not args.no_cpu,
                                     use_graph=graph_mode(args), dcvc=dc)
             except Exception as e:  # report, never hide
@@ -1172,6 +1181,7 @@ def main(argv=None):
     if world == 1 and args.leg_frames > 0 and not stub:
         for name in ES_LEGS:
             try:
+                log("%s leg ..." % name)
                 out[name] = es_leg(name, local_rank, args.leg_frames, threads, args.leg_cpu_seconds,
                                    use_graph=graph_mode(args), with_cpu=not args.no_cpu)
             except Exception as e:  # report, never hide
@@ -1202,14 +1212,19 @@ def main(argv=None):
             out["node_threads"] = None
     if world == 1 and not stub and args.configs4_frames > 0:
         try:
-            out["configs4"] = configs4_leg(local_rank, args.configs4_frames, threads, use_graph=graph_mode(args))
+            log("configs4 leg (%s order) ..." % args.configs4_order)
+            out["configs4"] = configs4_leg(local_rank, args.configs4_frames, threads, use_graph=graph_mode(args),
+                                           order=args.configs4_order)
+            out["configs4"]["order"] = args.configs4_order
             log("configs4: %s" % out["configs4"])
         except Exception as e:  # report, never hide
             log("configs4 leg failed: %r" % (e,))
             out["configs4"] = None
     if world == 1 and not stub and args.pageable_frames > 0:
+        log("pageable leg ...")
         out["pcie_pageable"] = pageable_leg(local_rank, args.pageable_frames, threads, use_graph=graph_mode(args))
     if world == 1 and not args.no_cpu and not stub:
+        log("cpu baseline ...")
         cb = cpu_baseline(args.cpu_seconds, args.warmup)
         f0, f1 = cb.pop("frames")
         # the GPU on exactly the CPU sample's frames, for a like-for-like ratio

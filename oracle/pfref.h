@@ -66,6 +66,11 @@ enum {
     PFREF_LD_TRIG        = 32,  /* (experiment) the LM's sin / cos / cubes in long double, rounded once:
                                    another libm's last bit (tools/drift_probe.py)                   */
     PFREF_QR_REVSUM      = 64,  /* (experiment) the LM's Householder QR sums its rows in reverse order  */
+    PFREF_LM_QUAD        = 128, /* (experiment) LM_NORMAL_EQ's products and step in binary128         */
+    PFREF_COST_REVSUM    = 256, /* (experiment) the faithful LM sums its cost in reverse order           */
+    PFREF_DEV_LIBM       = 512, /* (experiment) LM_NORMAL_EQ's SE(3) updates by libm sin/cos (se3_plus) */
+    PFREF_DEV_HALFANGLE  = 1024,/* (experiment) LM_NORMAL_EQ's SE(3) update by round 3's half-angle
+                                   identities instead of the reference's form                      */
     PFREF_GPU_EQUIV      = 1 | 4 | 16
 };
 

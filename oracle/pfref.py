@@ -17,6 +17,10 @@ FE_SQRT_DOUBLE = 2
 VG_STABLE = 4
 KNN_BRUTE = 8
 LM_NORMAL_EQ = 16
+DEV_HALFANGLE = 1024   # experiment: LM_NORMAL_EQ's SE(3) update by round 3's half-angle identities
+DEV_LIBM = 512         # experiment: LM_NORMAL_EQ's SE(3) updates by libm sin / cos
+COST_REVSUM = 256      # experiment: the faithful LM sums its cost in reverse order
+LM_QUAD = 128          # experiment: LM_NORMAL_EQ's products and step in binary128
 QR_REVSUM = 64         # experiment: the LM's Householder QR sums its rows in reverse order
 LD_TRIG = 32           # experiment: the LM's sin / cos / cubes in long double (another libm's last bit)
 GPU_EQUIV = FE_STABLE_TIES | VG_STABLE | LM_NORMAL_EQ
@@ -293,7 +297,7 @@ def se3_plus(x, delta):
 
 
 def se3_plus_half(x, delta):
-    """the GPU_EQUIV SE(3) update (one deterministic sincos of theta/2, half-angle identities)"""
+    """the GPU_EQUIV SE(3) update (pf_geom.h se3_exp: the source's form on the deterministic sincos)"""
     x = np.ascontiguousarray(x, np.float64)
     d = np.ascontiguousarray(delta, np.float64)
     out = np.empty(7)

@@ -239,6 +239,7 @@ inline M3 skew(V3 v) {
 void trig_dump(double v);   // development: PFREF_TRIG_DUMP (pfref_odom.cpp)
 extern thread_local bool g_ld_trig;   // PFREF_LD_TRIG for the solve in progress
 extern thread_local bool g_qr_rev;    // PFREF_QR_REVSUM for the solve in progress
+extern thread_local bool g_dev_half;  // PFREF_DEV_HALFANGLE for the solve in progress
 inline double lsin(double x) { return g_ld_trig ? (double)sinl((long double)x) : std::sin(x); }
 inline double lcos(double x) { return g_ld_trig ? (double)cosl((long double)x) : std::cos(x); }
 inline double lcube(double x) {
@@ -344,8 +345,16 @@ inline void se3_exp_half(const double se3[6], Quat& q, V3& t) {
         J = q2m(q);
     } else {
         M3 Omega2 = mmul(Omega, Omega);
-        const double a = (2.0 * (s_h * s_h)) / (theta * theta);
-        const double b = (theta - 2.0 * (s_h * c_h)) / (theta * theta * theta);
+        double a, b;
+        if (!g_dev_half) {                               // the reference's own form, full-angle sincos
+            double s_t, c_t;
+            det_sincos(theta, &s_t, &c_t);
+            a = (1.0 - c_t) / (theta * theta);
+            b = (theta - s_t) / (theta * theta * theta);
+        } else {                                         // round 3's half-angle identities (experiment)
+            a = (2.0 * (s_h * s_h)) / (theta * theta);
+            b = (theta - 2.0 * (s_h * c_h)) / (theta * theta * theta);
+        }
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) J.m[i][j] = (i == j ? 1.0 : 0.0) + a * Omega.m[i][j] + b * Omega2.m[i][j];
     }

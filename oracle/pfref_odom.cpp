@@ -20,6 +20,10 @@ namespace pfref {
 // ------------------------------------------------------------------------------------------
 thread_local bool g_ld_trig = false;
 thread_local bool g_qr_rev = false;
+thread_local bool g_quad = false;      // PFREF_LM_QUAD (experiment)
+thread_local bool g_cost_rev = false;  // PFREF_COST_REVSUM (experiment)
+thread_local bool g_dev_libm = false;  // PFREF_DEV_LIBM (experiment)
+thread_local bool g_dev_half = false;  // PFREF_DEV_HALFANGLE (experiment)
 
 // development: PFREF_TRIG_DUMP=<file> appends every libm argument of the faithful LM (doubles)
 void trig_dump(double v) {
@@ -323,6 +327,8 @@ const double kHuberB = 0.1 * 0.1;
 bool evaluate(const std::vector<Residual>& res, const double* x, double& cost, std::vector<double>* r,
               std::vector<double>* J) {
     cost = 0.0;
+    static thread_local std::vector<double> hc;
+    if (g_cost_rev) hc.assign(res.size(), 0.0);
     for (size_t i = 0; i < res.size(); ++i) {
         const Residual& q = res[i];
         double Jl[7];
@@ -339,11 +345,14 @@ bool evaluate(const std::vector<Residual>& res, const double* x, double& cost, s
         } else {
             rho0 = s; rho1 = 1.0;
         }
-        cost += 0.5 * rho0;
+        if (g_cost_rev) hc[i] = 0.5 * rho0;
+        else cost += 0.5 * rho0;
         double srho1 = std::sqrt(rho1);
         if (J) for (int j = 0; j < 6; ++j) (*J)[6 * i + j] = Jl[j] * srho1;
         if (r) (*r)[i] = ri * srho1;
     }
+    if (g_cost_rev)
+        for (size_t i = res.size(); i-- > 0;) cost += hc[i];
     return true;
 }
 
@@ -425,9 +434,12 @@ inline int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 // order and the total adds the 32 block sums in block order. Queries without a kept residual (and
 // residuals that are not finite) are zero rows there, which leave every partial unchanged, so only
 // the kept residuals are visited, in increasing q as the device takes them.
+thread_local __float128 g_totq[28];   // PFREF_LM_QUAD: the evaluation's products summed in binary128
+thread_local __float128 g_Hq[21], g_gq[6];
 void dev_evaluate(const std::vector<Residual>& res, const double* x, double tot[30]) {
     static thread_local std::vector<double> part;
     part.assign((size_t)kDevBlocks * kDevProducts * 9, 0.0);
+    for (int k = 0; k < 28; ++k) g_totq[k] = 0;
     int bad_r = 0, bad_j = 0;
     for (const Residual& rs : res) {
         double J[7];
@@ -460,6 +472,13 @@ void dev_evaluate(const std::vector<Residual>& res, const double* x, double tot[
         int h = 7;
         for (int i = 0; i < 6; ++i)
             for (int j = i; j < 6; ++j, ++h) P[9 * h] += J[i] * J[j];
+        if (g_quad) {
+            g_totq[0] += (__float128)hc;
+            for (int k = 0; k < 6; ++k) g_totq[1 + k] += (__float128)J[k] * (__float128)r;
+            int hq = 7;
+            for (int i = 0; i < 6; ++i)
+                for (int j = i; j < 6; ++j, ++hq) g_totq[hq] += (__float128)J[i] * (__float128)J[j];
+        }
     }
     for (int k = 0; k < kDevProducts; ++k) {
         double v = 0.0;
@@ -479,6 +498,49 @@ DevStep dev_try_step(const DevLm& lm) {                       // lm_try_step
     DevStep r;
     for (int j = 0; j < 6; ++j)
         r.D[j] = lm.reuse ? lm.D[j] : std::fmin(std::fmax(lm.scale[j] * lm.H[hup(j, j)] * lm.scale[j], 1e-6), 1e32);
+    if (g_quad) {                                            // the same step in binary128 (experiment)
+        typedef __float128 Q;
+        Q A[21], L[21], d[6], y[6];
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j <= i; ++j) A[tri(i, j)] = (Q)lm.scale[i] * g_Hq[hup(i, j)] * (Q)lm.scale[j];
+        for (int j = 0; j < 6; ++j) A[tri(j, j)] += (Q)r.D[j] / (Q)lm.radius;
+        bool ok = true;
+        for (int i = 0; i < 6; ++i) {
+            for (int j = 0; j < i; ++j) {
+                Q s2 = A[tri(i, j)];
+                for (int k = 0; k < j; ++k) s2 -= L[tri(i, k)] * d[k] * L[tri(j, k)];
+                L[tri(i, j)] = s2 / d[j];
+            }
+            Q dd = A[tri(i, i)];
+            for (int k = 0; k < i; ++k) dd -= L[tri(i, k)] * L[tri(i, k)] * d[k];
+            ok = ok && dd > 0;
+            d[i] = dd;
+        }
+        for (int i = 0; i < 6; ++i) {
+            Q s2 = (Q)lm.scale[i] * g_gq[i];
+            for (int k = 0; k < i; ++k) s2 -= L[tri(i, k)] * y[k];
+            y[i] = s2;
+        }
+        for (int i = 5; i >= 0; --i) {
+            Q s2 = y[i] / d[i];
+            for (int k = i + 1; k < 6; ++k) s2 -= L[tri(k, i)] * y[k];
+            y[i] = s2;
+        }
+        for (int j = 0; j < 6; ++j) { r.y[j] = (double)y[j]; ok = ok && std::isfinite(r.y[j]); }
+        r.mcc = 0.0;
+        if (ok) {
+            Q sg = 0, sHs = 0;
+            for (int i = 0; i < 6; ++i) {
+                sg -= y[i] * (Q)lm.scale[i] * g_gq[i];
+                Q hi = 0;
+                for (int j = 0; j < 6; ++j) hi -= (Q)lm.scale[i] * g_Hq[hup(i, j)] * (Q)lm.scale[j] * y[j];
+                sHs -= y[i] * hi;
+            }
+            r.mcc = (double)(-(sg + sHs / 2));
+        }
+        r.ok = ok && r.mcc > 0.0;
+        return r;
+    }
     // Hs + D / radius (D times the reciprocal radius), LDL^T with reciprocal pivots: the device's
     // operation order (W_ij = L_ij d_j accumulated first, L_ij = W_ij / d_j as a product) and its
     // fused multiply-adds (std::fma: one rounding, as v_fma_f64)
@@ -548,7 +610,8 @@ void dev_next_step(DevLm& lm, DevStep st, const double* cand_first) {   // lm_ne
         } else {
             double delta[6];
             for (int j = 0; j < 6; ++j) delta[j] = -st.y[j] * lm.scale[j];
-            se3_plus_half(lm.x, delta, lm.cand);
+            if (g_dev_libm) se3_plus(lm.x, delta, lm.cand);
+            else se3_plus_half(lm.x, delta, lm.cand);
         }
         lm.mcc = st.mcc;
         lm.phase = 1;
@@ -566,6 +629,8 @@ void dev_accept(DevLm& lm, const double* tot) {                     // lm_accept
         lm.cost = cost_c;
         for (int k = 0; k < 6; ++k) lm.g[k] = tot[1 + k];
         for (int k = 0; k < 21; ++k) lm.H[k] = tot[7 + k];
+        for (int k = 0; k < 6; ++k) g_gq[k] = g_totq[1 + k];
+        for (int k = 0; k < 21; ++k) g_Hq[k] = g_totq[7 + k];
         for (int i = 0; i < 6; ++i) lm.scale[i] = 1.0 / (1.0 + std::sqrt(lm.H[hup(i, i)]));
         lm.min_cost = lm.cost;
         for (int k = 0; k < 7; ++k) lm.best[k] = lm.x[k];
@@ -586,6 +651,8 @@ void dev_accept(DevLm& lm, const double* tot) {                     // lm_accept
             lm.cost = cand_cost;
             for (int k = 0; k < 6; ++k) lm.g[k] = tot[1 + k];
             for (int k = 0; k < 21; ++k) lm.H[k] = tot[7 + k];
+            for (int k = 0; k < 6; ++k) g_gq[k] = g_totq[1 + k];
+            for (int k = 0; k < 21; ++k) g_Hq[k] = g_totq[7 + k];
             const double r3 = 2.0 * rel - 1.0;
             const double f = 1.0 - r3 * r3 * r3;
             lm.radius = lm.radius / std::fmax(1.0 / 3.0, f);
@@ -607,8 +674,13 @@ void dev_accept(DevLm& lm, const double* tot) {                     // lm_accept
     const DevStep st = dev_try_step(lm);
     double ng[6], gx[7], delta[6], cand[7];
     for (int j = 0; j < 6; ++j) { ng[j] = -lm.g[j]; delta[j] = -st.y[j] * lm.scale[j]; }
-    se3_plus_half(lm.x, ng, gx);                                 // gradient max-norm check
-    se3_plus_half(lm.x, delta, cand);                            // the first attempt's candidate
+    if (g_dev_libm) {
+        se3_plus(lm.x, ng, gx);
+        se3_plus(lm.x, delta, cand);
+    } else {
+        se3_plus_half(lm.x, ng, gx);                             // gradient max-norm check
+        se3_plus_half(lm.x, delta, cand);                        // the first attempt's candidate
+    }
     double gm = 0.0;
     for (int j = 0; j < 7; ++j) gm = std::fmax(gm, std::fabs(lm.x[j] - gx[j]));
     if (step_ok && gm <= 1e-10) lm.done = 1;
@@ -1086,8 +1158,12 @@ int odom_update(Odom& o, const std::vector<PtC>* in) {
             double tb = now_s();
             g_ld_trig = (o.opts & PFREF_LD_TRIG) != 0;
             g_qr_rev = (o.opts & PFREF_QR_REVSUM) != 0;
+            g_quad = (o.opts & PFREF_LM_QUAD) != 0;
+            g_cost_rev = (o.opts & PFREF_COST_REVSUM) != 0;
+            g_dev_libm = (o.opts & PFREF_DEV_LIBM) != 0;
+            g_dev_half = (o.opts & PFREF_DEV_HALFANGLE) != 0;
             st.lm_iterations += solve_lm(o.params, res, (o.opts & PFREF_LM_NORMAL_EQ) != 0);
-            g_ld_trig = g_qr_rev = false;
+            g_ld_trig = g_qr_rev = g_quad = g_cost_rev = g_dev_libm = g_dev_half = false;
             double tc = now_s();
             st.t_assoc += tb - ta;
             st.t_solve += tc - tb;

@@ -286,11 +286,16 @@ PF_HD void det_sincos(double x, double* sn, double* cs) {
     }
 }
 
-// getTransformFromSe3 (src/lidarOptimization.cpp:106-143). One sincos of theta/2 serves all four
-// trigonometric terms: sin(theta) = 2 s c and 1 - cos(theta) = 2 s^2 (half-angle identities), and
-// theta^3 is a product where the source calls pow; each differs from the source's libm calls by at
-// most an ulp or two, far inside the pose tolerance, and saves three transcendental evaluations on
-// the LM's serial path.
+// getTransformFromSe3 (src/lidarOptimization.cpp:106-143) in the source's own form: the quaternion
+// from sin / cos of theta / 2, the translation Jacobian from (1 - cos(theta)) / theta^2 and
+// (theta - sin(theta)) / theta^3 of the full angle, both sincos from det_sincos and theta^3 as a product
+// where the source calls pow (an ulp now and then). Round 3 took the half-angle identities
+// 1 - cos(theta) = 2 sin^2(theta / 2) and sin(theta) = 2 s c instead: more accurate for small theta,
+// where 1 - cos(theta) cancels, but not the source's arithmetic, and that systematic difference (up to
+// ~1e-8 relative in the two coefficients) is what an ill-conditioned stretch of the S64T town
+// sequence amplified into a count flip at frame 338 (tools/drift_probe.py: the oracle's device-LM
+// restatement separates from the faithful oracle there with the half-angle form and tracks it with
+// this one; neither the LM's normal equations nor libm's last bit do it).
 PF_HD void se3_exp(const double* se3, qd& q, d3& t) {
     d3 omega{se3[0], se3[1], se3[2]};
     d3 upsilon{se3[3], se3[4], se3[5]};
@@ -314,8 +319,10 @@ PF_HD void se3_exp(const double* se3, qd& q, d3& t) {
         J = q2m(q);
     } else {
         m3 Om2 = m3_mul(Om, Om);
-        const double a = (2.0 * (s_h * s_h)) / (theta * theta);                // (1 - cos) / theta^2
-        const double b = (theta - 2.0 * (s_h * c_h)) / (theta * theta * theta); // (theta - sin) / theta^3
+        double s_t, c_t;
+        det_sincos(theta, &s_t, &c_t);
+        const double a = (1.0 - c_t) / (theta * theta);
+        const double b = (theta - s_t) / (theta * theta * theta);
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) J.m[i][j] = (i == j ? 1.0 : 0.0) + a * Om.m[i][j] + b * Om2.m[i][j];
     }

@@ -1483,7 +1483,8 @@ __global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, c
 // starts by taking the last element q (its value) and writing the root there; it waits while an earlier
 // pop's hole is q or an ancestor of q, since that pop may still write q. __make_heap's sifts of one tree
 // level touch disjoint subtrees and run in parallel, deepest level first.
-constexpr int kHeapCap = 16384;     // longest segment staged in LDS (128 KB); longer: one thread, global
+constexpr int kHeapCap = 20480 - 64;  // longest segment staged in LDS (with the spare slots: all 160 KB);
+                                      // longer ones: one thread in global memory
 constexpr int kHeapT = 256;
 constexpr int kHeapGrid = 256;
 

@@ -83,7 +83,7 @@ def test_tie_sort_depth_limit_heap_branch(pa, pfref):
 def test_tie_sort_natural_depth_limit(pa, pfref):
     """rgbds inputs reach libstdc++'s own depth limit: a voxel-ordered map with a few new points
     appended sends median-of-three to one end, level after level, and leaves segments of thousands of
-    keys (up to nearly the whole map) to the heap sort (k_tie_heap: LDS up to 16384 keys, one thread in
+    keys (up to nearly the whole map) to the heap sort (k_tie_heap: LDS up to 20416 keys, one thread in
     global memory above)."""
     rng = np.random.default_rng(25)
     for nmap, napp in ((22000, 100), (12000, 60), (22000, 3700), (40000, 900)):

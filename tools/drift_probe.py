@@ -6,8 +6,14 @@ device takes (LM_NORMAL_EQ) side by side over the same frames, and prints the pe
 difference and the first frame whose counts differ. Variant "ldtrig" instead perturbs only the libm:
 the LM's sin / cos / cubes taken in long double and rounded once (PFREF_LD_TRIG), which differs from
 glibc's double sin in the last bit now and then, as another C library would; "qrrev" keeps the QR
-but sums its rows in reverse order (another QR implementation's rounding).
-    python3 tools/drift_probe.py [preset] [frames] [out.json] [normaleq|ldtrig|qrrev]"""
+but sums its rows in reverse order (another QR implementation's rounding); "quad" is the device's
+LM (LM_NORMAL_EQ) with its normal equations formed and solved in binary128; "costrev" is the faithful
+LM with only its cost sums taken in reverse order; "devlibm" the device's LM with libm's sin / cos in its
+SE(3) updates ("devlibmquad": and binary128 normal equations); "devhalf" the device's LM with round 3's
+half-angle SE(3) update (2 sin^2(theta/2), 2 s c) instead of the reference's 1 - cos(theta),
+theta - sin(theta): the variant that separates at frame 338 ("normaleq" is now the device's LM as it is,
+in the reference's form).
+    python3 tools/drift_probe.py [preset] [frames] [out.json] [variant]"""
 import json
 import os
 import sys
@@ -29,7 +35,12 @@ seq = pfsynth.Sequence(preset, n_frames=n)
 lid = pfref.make_lidar(64, 3.0, 90.0)
 a = pfref.Odom(lid, 0.4, 0, 0.4, 75, 0, opts=0)
 b = pfref.Odom(lid, 0.4, 0, 0.4, 75, 0, opts={"normaleq": pfref.LM_NORMAL_EQ, "ldtrig": pfref.LD_TRIG,
-                                               "qrrev": pfref.QR_REVSUM}[variant])
+                                               "qrrev": pfref.QR_REVSUM,
+                                               "quad": pfref.LM_NORMAL_EQ | pfref.LM_QUAD,
+                                               "costrev": pfref.COST_REVSUM,
+                                               "devlibm": pfref.LM_NORMAL_EQ | pfref.DEV_LIBM,
+                                               "devlibmquad": pfref.LM_NORMAL_EQ | pfref.DEV_LIBM | pfref.LM_QUAD,
+                                               "devhalf": pfref.LM_NORMAL_EQ | pfref.DEV_HALFANGLE}[variant])
 keys = ("n_edge_ds", "n_surf_ds", "n_edge_map", "n_surf_map", "n_edge_res", "n_surf_res", "outer_iterations",
         "lm_iterations")
 rows, first_count = [], None
