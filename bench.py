@@ -681,10 +681,14 @@ def configs4_leg(device, nframes, threads, warmup=3, timing_frames=20, use_graph
         kn.set_map(np.c_[mxyz, np.zeros(mxyz.shape[0], np.float32)])
         kn.query(np.c_[surf[:, :3], np.zeros(surf.shape[0], np.float32)])
         tms, talg = kn.bench(20)
-        out["thick_knn_same_queries"] = {"avg_kernel_ms": round(tms, 5), "alg_bytes_per_launch": talg,
+        # the frame's surf queries only, against the surf map (k_assoc's launch above also holds the
+        # edge queries against the edge map, so its query count and bytes are not this one's)
+        out["thick_knn_surf_queries"] = {"avg_kernel_ms": round(tms, 5), "alg_bytes_per_launch": talg,
                                          "frac": round(talg / (tms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                          "queries": int(surf.shape[0]), "map_points": int(mxyz.shape[0]),
-                                         "kernel": "k_knn_thick (standalone pf_knn, thick-row layout)"}
+                                         "assoc_queries_edge_and_surf": int(nq),
+                                         "kernel": "k_knn_thick (standalone pf_knn, thick-row layout) on the "
+                                                   "last frame's surf queries and the surf map"}
     for db in bufs:
         db.free()
     return out

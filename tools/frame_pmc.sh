@@ -18,7 +18,7 @@ i=0
 for grp in "${GROUPS_[@]}"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp -d $OUT/p$i -o run --output-format csv -- \
-      python3 bench.py --steps 100 --warmup 10 --no-graph --only-headline \
+      python3 bench.py --steps 100 --warmup 10 --no-graph --only-headline --order ${ORDER:-stable} \
       > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
 python3 tools/frame_pmc.py $OUT
