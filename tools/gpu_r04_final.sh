@@ -6,10 +6,13 @@ cd ${GRAFT_REPO_ROOT:-$(pwd)}
 export TMPDIR=/tmp
 OUT=gpurun_out/r04f
 mkdir -p $OUT
-ORDER=stable tools/frame_pmc.sh > $OUT/pmc.log 2>&1 || { tail -5 $OUT/pmc.log; exit 1; }
+[ -n "$SKIP_PMC" ] || ORDER=stable tools/frame_pmc.sh > $OUT/pmc.log 2>&1 || { tail -5 $OUT/pmc.log; exit 1; }
 echo "pmc done"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-    python3 tools/tie_probe.py 4521 S64 tie > $OUT/probe_full.txt 2>&1 || { tail -5 $OUT/probe_full.txt; exit 1; }
+# eager launches: rocprofv3's kernel trace of this image faults on the host side in hipGraphLaunch
+# after a few hundred replays of these graphs (a segfault inside the tool's interception)
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
+    python3 bench.py --only-headline --no-graph --steps ${TRACE_N:-2000} --warmup 20 > $OUT/trace_bench.json 2> $OUT/trace_bench.err \
+    || { tail -5 $OUT/trace_bench.err; exit 1; }
 rm -f $OUT/trace/run_kernel_trace.csv
 python3 tools/kstats.py $OUT/trace/run_kernel_stats.csv 40 > $OUT/kstats.txt
 head -12 $OUT/kstats.txt
