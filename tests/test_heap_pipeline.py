@@ -1,0 +1,122 @@
+"""CPU: the schedule k_tie_heap runs __sort_heap's pops on (csrc/pf_tie.hip heap_step), restated in
+Python and checked against libstdc++'s heap sort (the oracle's line-by-line __make_heap + __sort_heap,
+pfref.sort_perm(keys, "literal", depth=0): introsort whose depth limit is 0 heap-sorts the whole input).
+
+The device pipelines the pops: each pop is a top-down sift (take the larger child, the right one unless
+right < left; stop when it is less than the value), which equals __adjust_heap + __push_heap on a valid
+heap; every pop in flight moves one tree level per step, reads happen before the step's writes, a pop
+may start only on the first step of a pair and only while no hole in flight is its last element q or an
+ancestor of q. The keys are compared as the device does: the low 30 bits << 1, the right child's + 1
+under one max (ties to the right). This test runs the same schedule lane by lane."""
+import numpy as np
+
+NL = 64
+
+
+def hlev(x):
+    return (x + 1).bit_length() - 1
+
+
+def make_heap(H, n):
+    """__make_heap as the device runs it: a tree level at a time, top-down sifts"""
+    for L in range(hlev((n - 2) // 2), -1, -1):
+        for x in range((1 << L) - 1, min((2 << L) - 2, (n - 2) // 2) + 1):
+            vk, h = H[x], x
+            while 2 * h + 1 < n:
+                c = 2 * h + 1
+                if c + 1 < n and not (H[c + 1][0] < H[c][0]):
+                    c += 1
+                if H[c][0] < vk[0]:
+                    break
+                H[h] = H[c]
+                h = c
+            H[h] = vk
+
+
+def pipelined_sort_heap(H, n):
+    npops = n - 1
+    act = [0] * NL
+    h = [0] * NL
+    m = [0] * NL
+    vk = [None] * NL
+    nxt = 0
+    steps = 0
+
+    def step(may):
+        nonlocal nxt
+        reads = {}
+        for i in range(NL):                            # children of every hole (before this step's writes)
+            if act[i]:
+                c1 = 2 * h[i] + 1
+                reads[i] = (c1, H[c1] if c1 < m[i] else None, H[c1 + 1] if c1 + 1 < m[i] else None)
+        start = None
+        if may and nxt < npops:
+            q = npops - nxt
+            blk = False
+            for i in range(NL):
+                if act[i]:
+                    sh = hlev(q) - hlev(h[i])
+                    blk |= sh >= 0 and ((q + 1) >> sh) == h[i] + 1
+            if not blk:
+                s = nxt & (NL - 1)
+                assert not act[s]
+                vq, r0 = H[q], H[0]
+                act[s], h[s], m[s], vk[s] = 1, 0, q, vq
+                reads[s] = (1, H[1] if 1 < q else None, H[2] if 2 < q else None)
+                start = (q, r0)
+                nxt += 1
+        writes = []
+        for i, (c1, a, b) in reads.items():
+            has = a is not None
+            ak = (a[0] & 0x3FFFFFFF) << 1 if has else 0
+            bk = (((b[0] & 0x3FFFFFFF) << 1) | 1) if b is not None else 0
+            mx = max(ak, bk)
+            right = mx & 1
+            ch = (b if right else a) if has else None
+            stop = (not has) or (mx ^ right) < ((vk[i][0] & 0x3FFFFFFF) << 1)
+            writes.append((h[i], vk[i] if stop else ch))
+            if stop:
+                act[i] = 0
+            else:
+                h[i] = c1 + right
+        if start:
+            H[start[0]] = start[1]
+        for pos, v in writes:
+            H[pos] = v
+
+    while True:
+        step(True)
+        step(False)
+        steps += 2
+        if nxt >= npops and not any(act):
+            return steps
+
+
+def device_heap_perm(keys):
+    n = keys.size
+    H = [(int(k), i) for i, k in enumerate(keys)]
+    if n >= 2:
+        make_heap(H, n)
+        pipelined_sort_heap(H, n)
+    return np.array([v for _, v in H], np.uint32)
+
+
+def test_pipelined_heap_equals_libstdcxx(pfref):
+    rng = np.random.default_rng(31)
+    for trial in range(60):
+        n = int(rng.choice([17, 18, 31, 64, 65, 100, 257, 500, 1200]))
+        span = int(rng.choice([2, 5, 40, 1000, 1 << 30]))
+        keys = rng.integers(0, span, n).astype(np.uint32)
+        if trial % 5 == 0:
+            keys = np.sort(keys)
+        elif trial % 5 == 1:
+            keys = np.sort(keys)[::-1].copy()
+        want = pfref.sort_perm(keys, "literal", 0)
+        np.testing.assert_array_equal(device_heap_perm(keys), want, err_msg="trial %d n=%d span=%d" % (trial, n, span))
+
+
+def test_pipelined_heap_keeps_class_bits_out_of_the_compare(pfref):
+    """a segment lies in one class (key bits 30-31): comparing the low 30 bits orders it the same"""
+    rng = np.random.default_rng(32)
+    keys = (rng.integers(0, 300, 700).astype(np.uint32) | np.uint32(2 << 30))
+    np.testing.assert_array_equal(device_heap_perm(keys), pfref.sort_perm(keys, "literal", 0))

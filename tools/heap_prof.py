@@ -27,3 +27,5 @@ for n in [int(a) for a in sys.argv[1:]] or [500, 3000, 7000]:
     steps = b[964]
     print("n %d make %.1f us sort %.1f us steps %d (%.2f per pop) %.0f cycles/step %.0f cycles/pop clock %.0f MHz"
           % (b[963], mk, so, steps, steps / max(1, n - 1), so * clk / max(1, steps), so * clk / max(1, n - 1), clk))
+    if b[967] or b[968]:                  # per-step cycles of the two steps of a pair (s_memtime)
+        print("   step A %.0f cycles, step B %.0f cycles" % (2 * b[967] / max(1, steps), 2 * b[968] / max(1, steps)))
