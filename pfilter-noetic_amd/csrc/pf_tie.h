@@ -30,7 +30,7 @@
 //                 output as they stand and heap-sorted there as libstdc++'s __partial_sort does, one
 //                 workgroup per segment: __make_heap a tree level at a time, __sort_heap's pops
 //                 pipelined two tree levels apart in one wave (a pop every two LDS steps instead of one
-//                 every 2 lg n).
+//                 every 2 lg n); a segment above the LDS size runs the same on a global scratch copy.
 // The levels are bound by VALU issue (about 50 instructions per 64 keys per level), so the tiers exist to
 // spread a class over many CUs as early as the cost of a launch boundary allows: work handed from one
 // workgroup to another inside a launch would pay an agent-scope release and acquire per hand-off.
@@ -66,6 +66,7 @@ struct TieSort {
     int4* mid = nullptr;                  // [midcap] mid-tier segments {first, last, depth, class}
     int4* jobs = nullptr;                 // [jcap] local jobs {first, last, depth (-1: at the limit), class}
     int2* heaps = nullptr;                // [hcap] depth-limit segments {output offset, length}
+    u64* hbig = nullptr;                  // [cap + 64] heap entries of segments above the LDS size
     int* ctl = nullptr;                   // counters (pf_tie.hip)
     size_t cap = 0, tiles = 0;
     int bcap = 0, mcap = 0, midcap = 0, jcap = 0, hcap = 0;

@@ -1484,25 +1484,44 @@ __global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, c
 // pop's hole is q or an ancestor of q, since that pop may still write q. __make_heap's sifts of one tree
 // level touch disjoint subtrees and run in parallel, deepest level first.
 constexpr int kHeapCap = 20480 - 64;  // longest segment staged in LDS (with the spare slots: all 160 KB);
-                                      // longer ones: one thread in global memory
+                                      // longer ones run the same schedule on a global scratch copy
 constexpr int kHeapT = 256;
 constexpr int kHeapGrid = 256;
 
-__device__ __forceinline__ u32 hkey(u64 x) { return (u32)(x >> 32); }
 __device__ __forceinline__ int hlev(int x) { return 31 - __clz(x + 1); }
 
-// one step of __sort_heap's pipelined pops (wave 0; H as {value, key}): every step reads the children of
-// every hole in flight (and, on a step that may start a pop, the last element and the root) and writes
-// every hole, with no branch on the lane (a lane with nothing to write writes its own spare slot)
+// where a segment's heap lives: LDS, or (above kHeapCap) a global scratch copy whose loads and stores go
+// to L2 at agent scope (one wave's lanes hand values to each other through it, and to the other waves of
+// the workgroup during __make_heap), with the step's stores complete before the next step's loads
+struct LdsHeap {
+    uint2* H;
+    __device__ __forceinline__ uint2 ld(int i) const { return H[i]; }
+    __device__ __forceinline__ void st(int i, uint2 v) const { H[i] = v; }
+    __device__ __forceinline__ void step_done() const { asm volatile("" ::: "memory"); }   // LDS: in order
+};
+struct GlbHeap {
+    u64* H;
+    __device__ __forceinline__ uint2 ld(int i) const {
+        const u64 x = __hip_atomic_load(H + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return make_uint2((u32)x, (u32)(x >> 32));
+    }
+    __device__ __forceinline__ void st(int i, uint2 v) const {
+        __hip_atomic_store(H + i, ((u64)v.y << 32) | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ __forceinline__ void step_done() const { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+};
+
+// one step of __sort_heap's pipelined pops (wave 0; entries {value, key}): every step reads the children
+// of every hole in flight (and, on a step that may start a pop, the last element and the root) and
+// writes every hole, with no branch on the lane (a lane with nothing to write writes its own spare slot)
 struct HeapPops {
     int nxt;              // the next pop to start (wave-uniform)
     bool act;             // this lane's pop is in flight
     int h, m;             // its hole, its heap size
     uint2 vk;             // its value
 };
-template <bool MAY>
-__device__ __forceinline__ void heap_step(uint2* H2, HeapPops& P, int npops, int l) {
-    const int spare = kHeapCap + l;
+template <bool MAY, class M>
+__device__ __forceinline__ void heap_step(const M& H2, HeapPops& P, int npops, int l, int spare) {
     bool start = false, mine = false;
     int q = 0;
     if (MAY) {
@@ -1518,92 +1537,107 @@ __device__ __forceinline__ void heap_step(uint2* H2, HeapPops& P, int npops, int
     const int c1 = 2 * P.h + 1;
     const bool has = P.act && c1 < P.m;                       // then c1 + 1 <= m < n
     const int cr = has ? c1 : 0;
-    const uint2 a = H2[cr], b = H2[cr + 1];
+    const uint2 a = H2.ld(cr), b = H2.ld(cr + 1);
     if (MAY) {
-        const uint2 vq = H2[q], r0 = H2[0];
+        const uint2 vq = H2.ld(q), r0 = H2.ld(0);
         P.vk = mine ? vq : P.vk;
-        H2[mine ? q : spare] = r0;
+        H2.st(mine ? q : spare, r0);
     }
     const bool right = c1 + 1 < P.m && !(b.y < a.y);
     const uint2 ch = right ? b : a;
     const bool stop = !has || ch.y < P.vk.y;
-    H2[P.act ? P.h : spare] = stop ? P.vk : ch;
+    H2.st(P.act ? P.h : spare, stop ? P.vk : ch);
     P.h = P.act ? (right ? c1 + 1 : c1) : P.h;
     P.act = P.act && !stop;
     P.nxt += start ? 1 : 0;
-    asm volatile("" ::: "memory");                            // LDS runs a wave's accesses in order
+    H2.step_done();
+}
+
+// __make_heap (every thread) then __sort_heap (wave 0) on the n entries of H; spare: the index of lane
+// 0's spare slot (lane l writes spare + l); jb: the job's index (the prof build records job 0)
+template <class M>
+__device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int jb) {
+    const int t = threadIdx.x, l = lane_id();
+    TIE_PROF(960, rt_now());
+    TIE_PROF(965, __builtin_amdgcn_s_memtime());
+    TIE_PROF(963, (unsigned long long)n);
+    // __make_heap: parents (n - 2) / 2 .. 0, a tree level at a time (the sifts of a level touch disjoint
+    // subtrees), each the top-down form of __adjust_heap + __push_heap
+    for (int L = hlev((n - 2) / 2); L >= 0; --L) {
+        const int lo = (1 << L) - 1, hi = min((2 << L) - 2, (n - 2) / 2);
+        for (int x = lo + t; x <= hi; x += kHeapT) {
+            const uint2 vk = H.ld(x);
+            int h = x;
+            for (;;) {
+                const int c1 = 2 * h + 1;
+                if (c1 >= n) break;
+                int c = c1;
+                uint2 a = H.ld(c1);
+                if (c1 + 1 < n) {
+                    const uint2 b = H.ld(c1 + 1);
+                    if (!(b.y < a.y)) {
+                        a = b;
+                        c = c1 + 1;
+                    }
+                }
+                if (a.y < vk.y) break;
+                H.st(h, a);
+                h = c;
+            }
+            H.st(h, vk);
+        }
+        __syncthreads();
+    }
+    // __sort_heap: pop i (i = 0 .. n - 2) in lane i % 64 of wave 0, steps in pairs, a pop starting only
+    // on the first of a pair
+    TIE_PROF(961, rt_now());
+    [[maybe_unused]] unsigned long long steps = 0;
+    if (t < 64) {
+        HeapPops P{0, false, 0, 0, make_uint2(0u, 0u)};
+        const int npops = n - 1;
+        for (;;) {
+            heap_step<true>(H, P, npops, l, spare + l);
+            heap_step<false>(H, P, npops, l, spare + l);
+#ifdef PF_TIE_PROF
+            steps += 2;
+#endif
+            if (P.nxt >= npops && __ballot(P.act) == 0) break;
+        }
+    }
+    TIE_PROF(962, rt_now());
+    TIE_PROF(966, __builtin_amdgcn_s_memtime());
+    TIE_PROF(964, steps);
+    __syncthreads();
 }
 
 __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32* __restrict__ vals, int* ctl,
-                                                     const int2* __restrict__ segs, u32* __restrict__ arrive) {
-    __shared__ u64 H[kHeapCap + 64];               // + a spare slot per lane of wave 0
-    const int t = threadIdx.x, l = lane_id();
+                                                     const int2* __restrict__ segs, u64* __restrict__ big,
+                                                     int bigcap, u32* __restrict__ arrive) {
+    __shared__ uint2 H[kHeapCap + 64];             // + a spare slot per lane of wave 0
+    const int t = threadIdx.x;
     const int nh = ctl[T_NHEAP];
     for (int jb = blockIdx.x; jb < nh; jb += gridDim.x) {
         const int2 sg = segs[jb];
         const int off = sg.x, n = sg.y;
-        if (n > kHeapCap) {                                   // rare: one thread in global memory
-            if (t == 0) heap_sort(keys, vals, off, n);
+        if (n <= kHeapCap) {
+            for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);
             __syncthreads();
-            continue;
-        }
-        for (int i = t; i < n; i += kHeapT) H[i] = ((u64)keys[off + i] << 32) | vals[off + i];
-        __syncthreads();
-        TIE_PROF(960, rt_now());
-        TIE_PROF(965, __builtin_amdgcn_s_memtime());
-        TIE_PROF(963, (unsigned long long)n);
-        // __make_heap: parents (n - 2) / 2 .. 0, a tree level at a time
-        for (int L = hlev((n - 2) / 2); L >= 0; --L) {
-            const int lo = (1 << L) - 1, hi = min((2 << L) - 2, (n - 2) / 2);
-            for (int x = lo + t; x <= hi; x += kHeapT) {
-                const u64 vk = H[x];
-                int h = x;
-                for (;;) {
-                    const int c1 = 2 * h + 1;
-                    if (c1 >= n) break;
-                    int c = c1;
-                    u64 a = H[c1];
-                    if (c1 + 1 < n) {
-                        const u64 b = H[c1 + 1];
-                        if (!(hkey(b) < hkey(a))) {
-                            a = b;
-                            c = c1 + 1;
-                        }
-                    }
-                    if (hkey(a) < hkey(vk)) break;
-                    H[h] = a;
-                    h = c;
-                }
-                H[h] = vk;
+            heap_sort_seg(LdsHeap{H}, n, kHeapCap, jb);
+            for (int i = t; i < n; i += kHeapT) {
+                const uint2 x = H[i];
+                keys[off + i] = x.y;
+                vals[off + i] = x.x;
             }
+        } else {                                              // the copy at the segment's own offset
+            GlbHeap G{big + off};
+            for (int i = t; i < n; i += kHeapT) G.st(i, make_uint2(vals[off + i], keys[off + i]));
             __syncthreads();
-        }
-        // __sort_heap: pop i (i = 0 .. n - 2) in lane i % 64 of wave 0, a step at a time: every step reads
-        // the children of every hole in flight (and the last element and the root for a pop that starts)
-        // and writes every hole, with no branch on the lane (a lane with nothing to write writes its own
-        // spare slot). Steps go in pairs, a pop starting only on the first of a pair.
-        TIE_PROF(961, rt_now());
-        [[maybe_unused]] unsigned long long steps = 0;
-        if (t < 64) {
-            HeapPops P{0, false, 0, 0, make_uint2(0u, 0u)};
-            const int npops = n - 1;
-            for (;;) {
-                heap_step<true>(reinterpret_cast<uint2*>(H), P, npops, l);
-                heap_step<false>(reinterpret_cast<uint2*>(H), P, npops, l);
-#ifdef PF_TIE_PROF
-                steps += 2;
-#endif
-                if (P.nxt >= npops && __ballot(P.act) == 0) break;
+            heap_sort_seg(G, n, bigcap - off, jb);            // spares: big[bigcap .. bigcap + 64)
+            for (int i = t; i < n; i += kHeapT) {
+                const uint2 x = G.ld(i);
+                keys[off + i] = x.y;
+                vals[off + i] = x.x;
             }
-        }
-        TIE_PROF(962, rt_now());
-        TIE_PROF(966, __builtin_amdgcn_s_memtime());
-        TIE_PROF(964, steps);
-        __syncthreads();
-        for (int i = t; i < n; i += kHeapT) {
-            const u64 x = H[i];
-            keys[off + i] = hkey(x);
-            vals[off + i] = (u32)x;
         }
         __syncthreads();
     }
@@ -1652,6 +1686,7 @@ int tie_alloc(TieSort& t, size_t cap, int max_levels) {
     PF_TALLOC(t.mid, sizeof(int4) * t.midcap);
     PF_TALLOC(t.jobs, sizeof(int4) * t.jcap);
     PF_TALLOC(t.heaps, sizeof(int2) * t.hcap);
+    PF_TALLOC(t.hbig, sizeof(u64) * (cap + 64));     // segments above the LDS size, at their own offsets
     PF_TALLOC(t.ctl, sizeof(int) * T_WORDS);
 #undef PF_TALLOC
     if (hipMemset(t.status, 0, sizeof(u64) * t.tiles) != hipSuccess || hipMemset(t.arrive, 0, sizeof(u32) * 4) != hipSuccess ||
@@ -1661,7 +1696,8 @@ int tie_alloc(TieSort& t, size_t cap, int max_levels) {
 }
 
 void tie_free(TieSort& t) {
-    void* ptrs[] = {t.k, t.v, t.lp, t.rq, t.status, t.arrive, t.big, t.tot, t.med, t.mid, t.jobs, t.heaps, t.ctl};
+    void* ptrs[] = {t.k, t.v, t.lp, t.rq, t.status, t.arrive, t.big, t.tot, t.med, t.mid, t.jobs, t.heaps, t.hbig,
+                    t.ctl};
     for (void* p : ptrs) (void)hipFree(p);
     t = TieSort{};
 }
@@ -1696,7 +1732,8 @@ void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStr
     hipLaunchKernelGGL(k_tie_mid, dim3(kMidGrid), dim3(kMT), 0, s, t.k, t.v, t.ctl, t.mid, t.jobs, t.jcap, err);
     hipLaunchKernelGGL(k_tie_local, dim3(kLocalGrid), dim3(1024), 0, s, t.k, t.v, t.jobs, t.ctl, t.arrive + 2, keys,
                        vals, cls, HeapList{t.heaps, t.hcap, err});
-    hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heaps, t.arrive + 3);
+    hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heaps, t.hbig,
+                       (int)t.cap, t.arrive + 3);
 }
 
 const int* tie_valid_count(const TieSort& t) { return t.ctl + T_VALID; }

@@ -70,10 +70,10 @@ def test_tie_sort_big_levels_and_fallback(pa, pfref):
 def test_tie_sort_depth_limit_heap_branch(pa, pfref):
     """The depth-limit branch (libstdc++'s make_heap + sort_heap) on the device against the oracle's
     restatement with the same settable depth limit (itself checked against std::sort's own branch in
-    tests/test_oracle_units.py): segments at the limit from every tier, in LDS and (20000 keys at depth 0)
-    in global memory."""
+    tests/test_oracle_units.py): segments at the limit from every tier, in LDS and (30000 keys at depth 0,
+    above the 20416 the LDS holds) on the global scratch copy."""
     rng = np.random.default_rng(24)
-    for n in (17, 40, 300, 5000, 20000):
+    for n in (17, 40, 300, 5000, 20000, 30000):
         keys = rng.integers(0, max(2, n // 5), n).astype(np.uint32)
         for depth in (0, 1, 2, 3, 5):
             want = pfref.sort_perm(keys, "literal", depth)
@@ -83,8 +83,8 @@ def test_tie_sort_depth_limit_heap_branch(pa, pfref):
 def test_tie_sort_natural_depth_limit(pa, pfref):
     """rgbds inputs reach libstdc++'s own depth limit: a voxel-ordered map with a few new points
     appended sends median-of-three to one end, level after level, and leaves segments of thousands of
-    keys (up to nearly the whole map) to the heap sort (k_tie_heap: LDS up to 20416 keys, one thread in
-    global memory above)."""
+    keys (up to nearly the whole map) to the heap sort (k_tie_heap: LDS up to 20416 keys, a global
+    scratch copy above)."""
     rng = np.random.default_rng(25)
     for nmap, napp in ((22000, 100), (12000, 60), (22000, 3700), (40000, 900)):
         m = np.sort(rng.choice(1 << 24, nmap, replace=False))
