@@ -172,3 +172,15 @@ def test_knn_shard_mode_gloo_world2():
     assert abs(out["ms_per_step"] - 2.0) < 1e-9                  # rank 1's 2 ms
     assert abs(out["value"] - 2000 / 2e-3) < 1e-3
     assert abs(out["aggregate_alg_GBps"] - 2000 * 1000.0 / 2e-3 / 1e9) < 0.1
+
+
+def test_sort_order_flags():
+    """The headline runs in the reference tie order by default (the mode whose results are the
+    reference's frame by frame); the other order is reported beside it; configs[4]'s leg defaults to the
+    stable order (its tie order heap-sorts ~1.4M keys per frame)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    a = bench.parse([])
+    assert a.order == "tie" and a.configs4_order == "stable" and a.other_order_frames > 0
+    b = bench.parse(["--order", "stable", "--configs4-order", "tie", "--other-order-frames", "0"])
+    assert b.order == "stable" and b.configs4_order == "tie" and b.other_order_frames == 0
