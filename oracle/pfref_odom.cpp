@@ -48,10 +48,18 @@ void sort_pairs(std::vector<IdxPair>& iv, bool stable) {
     if (trace && !stable) {
         std::vector<uint32_t> k(iv.size());
         for (size_t i = 0; i < iv.size(); ++i) k[i] = iv[i].idx;
-        long st[6];
+        long st[7];
         pfref_introsort_stats(k.data(), k.size(), st);
-        std::fprintf(stderr, "sort n %zu levels %ld heaps %ld max %ld keys %ld g3segs %ld g3max %ld\n", k.size(), st[0], st[1],
-                     st[2], st[3], st[4], st[5]);
+        std::fprintf(stderr, "sort n %zu levels %ld heaps %ld max %ld keys %ld g3segs %ld g3max %ld dupkeys %ld\n", k.size(),
+                     st[0], st[1], st[2], st[3], st[4], st[5], st[6]);
+        if (const char* dump = std::getenv("PFREF_SORT_DUMP")) {         // keys of sorts above 1M, appended
+            if (k.size() > (1u << 20)) {
+                if (FILE* f = std::fopen(dump, "ab")) {
+                    std::fwrite(k.data(), sizeof(uint32_t), k.size(), f);
+                    std::fclose(f);
+                }
+            }
+        }
     }
     if (stable) std::stable_sort(iv.begin(), iv.end(), lt);
     else std::sort(iv.begin(), iv.end(), lt);

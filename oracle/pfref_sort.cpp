@@ -256,10 +256,10 @@ void pfref_introsort_literal(const uint32_t* keys, size_t n, int depth, uint32_t
 
 // development statistics of one std::sort call's introsort (the literal form): st = {partition
 // levels reached, depth-limit segments, largest of them, their total keys, of those the segments holding
-// three or more equal keys, the largest of those}
+// three or more equal keys, the largest of those, the keys of the segments holding any equal pair}
 void pfref_introsort_stats(const uint32_t* keys, size_t n, long* st) {
     std::vector<E> a = pairs(keys, n);
-    for (int i = 0; i < 6; ++i) st[i] = 0;
+    for (int i = 0; i < 7; ++i) st[i] = 0;
     struct F { long f, l, d, lev; };
     std::vector<F> stack;
     const long d0 = n > 1 ? 2L * lg(n) : 0;
@@ -280,8 +280,10 @@ void pfref_introsort_stats(const uint32_t* keys, size_t n, long* st) {
                 std::vector<uint32_t> k(len);
                 for (long i = 0; i < len; ++i) k[i] = first[i].key;
                 std::sort(k.begin(), k.end());
-                bool g3 = false;
+                bool g3 = false, g2 = false;
                 for (long i = 2; i < len; ++i) g3 |= k[i] == k[i - 2];
+                for (long i = 1; i < len; ++i) g2 |= k[i] == k[i - 1];
+                if (g2) st[6] += len;
                 st[4] += g3;
                 if (g3) st[5] = std::max(st[5], len);
                 break;

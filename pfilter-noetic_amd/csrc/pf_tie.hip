@@ -1483,16 +1483,18 @@ __global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, c
 // starts by taking the last element q (its value) and writing the root there; it waits while an earlier
 // pop's hole is q or an ancestor of q, since that pop may still write q. __make_heap's sifts of one tree
 // level touch disjoint subtrees and run in parallel, deepest level first.
-constexpr int kHeapCap = 20480 - 64;  // longest segment staged in LDS (with the spare slots: all 160 KB);
+constexpr int kHeapCap = 20480 - 128; // longest segment staged in LDS (with the spare slots: 160 KB less 512 B);
                                       // longer ones run the same schedule on a global scratch copy
 constexpr int kHeapT = 256;
 constexpr int kHeapGrid = 256;
 
 __device__ __forceinline__ int hlev(int x) { return 31 - __clz(x + 1); }
 
-// where a segment's heap lives: LDS, or (above kHeapCap) a global scratch copy whose loads and stores go
-// to L2 at agent scope (one wave's lanes hand values to each other through it, and to the other waves of
-// the workgroup during __make_heap), with the step's stores complete before the next step's loads
+// where a segment's heap lives: LDS, or (above kHeapCap) a global scratch copy read and written at
+// workgroup scope (one wave's lanes hand values to each other through it, and to the other waves of the
+// workgroup during __make_heap; one workgroup owns the copy, so its CU's L1 and the XCD's L2 serve it:
+// agent scope made every load go past the L1, 1.6 us per pop against 0.66), with the step's stores
+// complete before the next step's loads (dropping that wait measured the same, 0.657 vs 0.658 us)
 struct LdsHeap {
     uint2* H;
     __device__ __forceinline__ uint2 ld(int i) const { return H[i]; }
@@ -1502,11 +1504,11 @@ struct LdsHeap {
 struct GlbHeap {
     u64* H;
     __device__ __forceinline__ uint2 ld(int i) const {
-        const u64 x = __hip_atomic_load(H + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 x = __hip_atomic_load(H + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return make_uint2((u32)x, (u32)(x >> 32));
     }
     __device__ __forceinline__ void st(int i, uint2 v) const {
-        __hip_atomic_store(H + i, ((u64)v.y << 32) | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(H + i, ((u64)v.y << 32) | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __device__ __forceinline__ void step_done() const { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 };
@@ -1610,6 +1612,108 @@ __device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int
     __syncthreads();
 }
 
+// A segment whose keys are all distinct has one sorted order, so whatever sorts it gives __sort_heap's
+// exact result: the heap tier first sorts a copy with a bitonic network and keeps it when no two
+// neighbours are equal; a segment with an equal pair is restored and heap-sorted. (The depth limit is
+// reached mostly inside the voxel-ordered map part of an rgbds input: configs[4]'s ~820k-key segment,
+// whose pipelined heap sort takes 0.54 s, holds distinct keys; at configs[1] 30 % of the heap-sorted
+// keys do, oracle PFREF_SORT_STATS dupkeys.)
+// The network is the flip form (every compare-exchange puts the smaller key first; phase k opens with
+// partner i ^ (k - 1), then the half-cleaners i + j): positions at or past the segment's end act as +inf
+// and are never touched, so no padding.
+constexpr int kBitChunk = 16384;      // chunk of a global segment staged in LDS (128 KB)
+
+__device__ __forceinline__ int ce_lo(int c, int j) { return ((c & ~(j - 1)) << 1) | (c & (j - 1)); }
+__device__ __forceinline__ int pow2_ceil(int n) { return n <= 1 ? 1 : 1 << (32 - __clz(n - 1)); }
+
+// the flip step of phase k (flip) or the half-cleaner of distance j, on S[0, nv), over a network of size P
+__device__ __forceinline__ void lds_ce_step(uint2* S, int nv, int P, int j, int flipmask) {
+    for (int c = threadIdx.x; c < (P >> 1); c += kHeapT) {
+        const int i = ce_lo(c, j);
+        const int q = flipmask ? (i ^ flipmask) : i + j;
+        if (q < nv) {
+            const uint2 a = S[i], b = S[q];
+            if (b.y < a.y) {
+                S[i] = b;
+                S[q] = a;
+            }
+        }
+    }
+    __syncthreads();
+}
+// phases k0 .. k1 in full (flip + half-cleaners), or (k0 = 0) only the half-cleaners from jtop down
+__device__ void lds_bitonic(uint2* S, int nv, int P, int k0, int k1, int jtop) {
+    if (k0 == 0) {
+        for (int j = jtop; j >= 1; j >>= 1) lds_ce_step(S, nv, P, j, 0);
+        return;
+    }
+    for (int k = k0; k <= k1; k <<= 1) {
+        lds_ce_step(S, nv, P, k >> 1, k - 1);
+        for (int j = k >> 2; j >= 1; j >>= 1) lds_ce_step(S, nv, P, j, 0);
+    }
+}
+// one step of the network on the global copy (four compare-exchanges in flight per thread)
+__device__ void glb_ce_step(const GlbHeap& G, int n, int P, int j, int flipmask) {
+    constexpr int U = 4;
+    for (int c0 = threadIdx.x; c0 < (P >> 1); c0 += U * kHeapT) {
+        int i[U], q[U];
+        uint2 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = c0 + u * kHeapT;
+            i[u] = ce_lo(c, j);
+            q[u] = flipmask ? (i[u] ^ flipmask) : i[u] + j;
+            if (c >= (P >> 1) || q[u] >= n) q[u] = -1;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (q[u] >= 0) {
+                a[u] = G.ld(i[u]);
+                b[u] = G.ld(q[u]);
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (q[u] >= 0 && b[u].y < a[u].y) {
+                G.st(i[u], b[u]);
+                G.st(q[u], a[u]);
+            }
+    }
+    __syncthreads();
+}
+// true when two neighbours of the sorted S[0, n) / G[0, n) hold the same key
+__device__ bool lds_has_equal(const uint2* S, int n) {
+    int eq = 0;
+    for (int i = threadIdx.x + 1; i < n; i += kHeapT) eq |= S[i].y == S[i - 1].y;
+    return __syncthreads_or(eq) != 0;
+}
+__device__ bool glb_has_equal(const GlbHeap& G, int n) {
+    int eq = 0;
+    for (int i = threadIdx.x + 1; i < n; i += kHeapT) eq |= G.ld(i).y == G.ld(i - 1).y;
+    return __syncthreads_or(eq) != 0;
+}
+// the network on the global copy G[0, n): chunks of kBitChunk sorted in LDS, then per phase the steps whose
+// partners lie in other chunks on G and the rest chunk by chunk in LDS
+__device__ void glb_bitonic(const GlbHeap& G, uint2* S, int n) {
+    const int P = pow2_ceil(n), t = threadIdx.x;
+    const int Pc = P < kBitChunk ? P : kBitChunk;
+    for (int kk = 0; kk == 0 || (2 * kBitChunk << (kk - 1)) <= P; ++kk) {
+        const int k = kk == 0 ? 0 : kBitChunk << kk;
+        if (k) {
+            glb_ce_step(G, n, P, k >> 1, k - 1);
+            for (int j = k >> 2; j >= kBitChunk; j >>= 1) glb_ce_step(G, n, P, j, 0);
+        }
+        for (int c0 = 0; c0 < n; c0 += kBitChunk) {
+            const int nv = min(kBitChunk, n - c0);
+            for (int i = t; i < nv; i += kHeapT) S[i] = G.ld(c0 + i);
+            __syncthreads();
+            if (k) lds_bitonic(S, nv, Pc, 0, 0, kBitChunk >> 1);
+            else lds_bitonic(S, nv, Pc, 2, Pc, 0);
+            for (int i = t; i < nv; i += kHeapT) G.st(c0 + i, S[i]);
+            __syncthreads();
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32* __restrict__ vals, int* ctl,
                                                      const int2* __restrict__ segs, u64* __restrict__ big,
                                                      int bigcap, u32* __restrict__ arrive) {
@@ -1622,7 +1726,13 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
         if (n <= kHeapCap) {
             for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);
             __syncthreads();
-            heap_sort_seg(LdsHeap{H}, n, kHeapCap, jb);
+            const int P = pow2_ceil(n);
+            lds_bitonic(H, n, P, 2, P, 0);
+            if (lds_has_equal(H, n)) {                        // restore, then the heap sort
+                for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);
+                __syncthreads();
+                heap_sort_seg(LdsHeap{H}, n, kHeapCap, jb);
+            }
             for (int i = t; i < n; i += kHeapT) {
                 const uint2 x = H[i];
                 keys[off + i] = x.y;
@@ -1632,7 +1742,12 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
             GlbHeap G{big + off};
             for (int i = t; i < n; i += kHeapT) G.st(i, make_uint2(vals[off + i], keys[off + i]));
             __syncthreads();
-            heap_sort_seg(G, n, bigcap - off, jb);            // spares: big[bigcap .. bigcap + 64)
+            glb_bitonic(G, H, n);
+            if (glb_has_equal(G, n)) {
+                for (int i = t; i < n; i += kHeapT) G.st(i, make_uint2(vals[off + i], keys[off + i]));
+                __syncthreads();
+                heap_sort_seg(G, n, bigcap - off, jb);        // spares: big[bigcap .. bigcap + 64)
+            }
             for (int i = t; i < n; i += kHeapT) {
                 const uint2 x = G.ld(i);
                 keys[off + i] = x.y;

@@ -71,11 +71,19 @@ def test_tie_sort_depth_limit_heap_branch(pa, pfref):
     """The depth-limit branch (libstdc++'s make_heap + sort_heap) on the device against the oracle's
     restatement with the same settable depth limit (itself checked against std::sort's own branch in
     tests/test_oracle_units.py): segments at the limit from every tier, in LDS and (30000 keys at depth 0,
-    above the 20416 the LDS holds) on the global scratch copy."""
+    above the 20352 the LDS holds) on the global scratch copy. Keys drawn with repeats (the heap sort
+    itself: a segment with an equal pair) and without (the bitonic network, kept when no two keys are
+    equal: random, sorted and reversed permutations, in LDS and across the global copy's 16384-key
+    chunks)."""
     rng = np.random.default_rng(24)
-    for n in (17, 40, 300, 5000, 20000, 30000):
-        keys = rng.integers(0, max(2, n // 5), n).astype(np.uint32)
-        for depth in (0, 1, 2, 3, 5):
+    cases = [rng.integers(0, max(2, n // 5), n).astype(np.uint32) for n in (17, 40, 300, 5000, 20000, 30000)]
+    for n in (17, 33, 1000, 16384, 20352, 20353, 40000, 70001):
+        perm = rng.permutation(n).astype(np.uint32) * 3
+        cases += [perm, np.sort(perm), np.sort(perm)[::-1].copy()]
+    cases.append(np.r_[rng.permutation(50000), 7, 7].astype(np.uint32))   # one equal pair in 50002
+    for keys in cases:
+        n = keys.size
+        for depth in ((0, 1, 2, 3, 5) if n <= 30000 else (0, 2)):
             want = pfref.sort_perm(keys, "literal", depth)
             np.testing.assert_array_equal(pa.tie_sort(keys, depth=depth), want, err_msg="n=%d depth=%d" % (n, depth))
 
@@ -83,7 +91,7 @@ def test_tie_sort_depth_limit_heap_branch(pa, pfref):
 def test_tie_sort_natural_depth_limit(pa, pfref):
     """rgbds inputs reach libstdc++'s own depth limit: a voxel-ordered map with a few new points
     appended sends median-of-three to one end, level after level, and leaves segments of thousands of
-    keys (up to nearly the whole map) to the heap sort (k_tie_heap: LDS up to 20416 keys, a global
+    keys (up to nearly the whole map) to the heap sort (k_tie_heap: LDS up to 20352 keys, a global
     scratch copy above)."""
     rng = np.random.default_rng(25)
     for nmap, napp in ((22000, 100), (12000, 60), (22000, 3700), (40000, 900)):

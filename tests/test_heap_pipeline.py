@@ -120,3 +120,72 @@ def test_pipelined_heap_keeps_class_bits_out_of_the_compare(pfref):
     rng = np.random.default_rng(32)
     keys = (rng.integers(0, 300, 700).astype(np.uint32) | np.uint32(2 << 30))
     np.testing.assert_array_equal(device_heap_perm(keys), pfref.sort_perm(keys, "literal", 0))
+
+
+# k_tie_heap's distinct-key path (pf_tie.hip lds_bitonic / glb_bitonic): the flip-form bitonic network
+# with positions past the segment's end left out (+inf), run whole (LDS) or as chunks of C positions
+# with the cross-chunk steps on the global copy; restated to check the index arithmetic at small C
+def _p2(n):
+    return 1 if n <= 1 else 1 << (n - 1).bit_length()
+
+
+def _ce_step(S, nv, P, j, flip):
+    for c in range(P >> 1):
+        i = ((c & ~(j - 1)) << 1) | (c & (j - 1))
+        q = (i ^ flip) if flip else i + j
+        if q < nv and S[q][0] < S[i][0]:
+            S[i], S[q] = S[q], S[i]
+
+
+def _lds_bitonic(S, nv, P, k0, k1, jtop):
+    if k0 == 0:
+        j = jtop
+        while j >= 1:
+            _ce_step(S, nv, P, j, 0)
+            j >>= 1
+        return
+    k = k0
+    while k <= k1:
+        _ce_step(S, nv, P, k >> 1, k - 1)
+        j = k >> 2
+        while j >= 1:
+            _ce_step(S, nv, P, j, 0)
+            j >>= 1
+        k <<= 1
+
+
+def _glb_bitonic(G, n, C):
+    P = _p2(n)
+    Pc = min(P, C)
+    kk = 0
+    while kk == 0 or (2 * C << (kk - 1)) <= P:
+        k = 0 if kk == 0 else C << kk
+        if k:
+            _ce_step(G, n, P, k >> 1, k - 1)
+            j = k >> 2
+            while j >= C:
+                _ce_step(G, n, P, j, 0)
+                j >>= 1
+        for c0 in range(0, n, C):
+            nv = min(C, n - c0)
+            S = G[c0:c0 + nv]
+            if k:
+                _lds_bitonic(S, nv, Pc, 0, 0, C >> 1)
+            else:
+                _lds_bitonic(S, nv, Pc, 2, Pc, 0)
+            G[c0:c0 + nv] = S
+        kk += 1
+
+
+def test_bitonic_network_equals_heap_sort_on_distinct_keys(pfref):
+    rng = np.random.default_rng(33)
+    for n in (17, 33, 100, 129, 257, 600, 1025):
+        for C in (16, 64, 4096):
+            keys = (rng.permutation(n) * 5).astype(np.uint32)
+            G = [(int(k), i) for i, k in enumerate(keys)]
+            if C == 4096:
+                _lds_bitonic(G, n, _p2(n), 2, _p2(n), 0)
+            else:
+                _glb_bitonic(G, n, C)
+            got = np.array([v for _, v in G], np.uint32)
+            np.testing.assert_array_equal(got, pfref.sort_perm(keys, "literal", 0), err_msg="n=%d C=%d" % (n, C))

@@ -1,6 +1,6 @@
 """Development probe: configs[4] (S128 scans against a seeded 2M-point surf map) frame by frame: the
 synchronous time of each frame and the map merge's counters (updates that fell back to the full sort,
-largest appended-point count of a bucket).  python3 tools/c4_probe.py [frames]"""
+largest appended-point count of a bucket).  python3 tools/c4_probe.py [frames] [tie|stable] [graph|eager]"""
 import os
 import sys
 import time
@@ -13,6 +13,8 @@ import pfilter_amd as pa  # noqa: E402
 import pfsynth  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+ORDER = sys.argv[2] if len(sys.argv) > 2 else "stable"
+GRAPH = (sys.argv[3] if len(sys.argv) > 3 else "graph") == "graph"
 seq = pfsynth.Sequence("S128", n_frames=N, speed=1.0)
 buf, counts = seq.frames(0, N, threads=16)
 db = pa.DeviceBuffer(buf.nbytes)
@@ -20,6 +22,8 @@ db.upload(buf)
 ptrs = [(db.ptr + i * buf.shape[1] * 16, int(counts[i])) for i in range(N)]
 od = pa.Odom_ES_EstimationClass(max_points=300000, map_capacity=1 << 22)
 od.init(pa.make_lidar(128, 3.0, 90.0, 0.1, ring_model=(15.0, -25.0)), 0.4, 0, 0.0, 0, 0)
+od.set_tie_order(ORDER == "tie")
+od.set_graph(GRAPH)
 od.frame_device(*ptrs[0])
 od.sync()
 m = pfsynth.voxel_map(2_000_000, 0.8, seed=5)
