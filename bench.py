@@ -89,11 +89,11 @@ def parse(argv=None):
                     help="frames of pf_odom_frame_host from pageable memory (pcie_pageable); 0 = skip")
     ap.add_argument("--configs4-frames", type=int, default=100,
                     help="frames of the configs[4] pipeline leg (S128 scans, 2M-point map); 0 = skip")
-    ap.add_argument("--configs4-order", default="stable", choices=["tie", "stable"],
-                    help="sort order of the configs[4] leg: in the tie order a 2M-point voxel-ordered map "
-                         "with a few thousand appended points drives introsort to its depth limit on "
-                         "segments of up to the whole map, whose heap sort is serial (measured apart: "
-                         "DESIGN.md section 5)")
+    ap.add_argument("--configs4-order", default="tie", choices=["tie", "stable"],
+                    help="sort order of the configs[4] leg (default the reference's tie order: the 2M-point "
+                         "voxel-ordered map with a few thousand appended points drives introsort to its "
+                         "depth limit on a ~820k-key segment of distinct keys, which k_tie_heap sorts by a "
+                         "bitonic network; DESIGN.md section 5)")
     ap.add_argument("--node-frames", type=int, default=1000,
                     help="frames of the node call pattern (pf_fe_extract -> pf_odom_update); 0 = skip")
     a = ap.parse_args(argv)

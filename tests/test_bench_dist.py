@@ -181,6 +181,6 @@ def test_sort_order_flags():
     sys.path.insert(0, ROOT)
     import bench
     a = bench.parse([])
-    assert a.order == "tie" and a.configs4_order == "stable" and a.other_order_frames > 0
-    b = bench.parse(["--order", "stable", "--configs4-order", "tie", "--other-order-frames", "0"])
-    assert b.order == "stable" and b.configs4_order == "tie" and b.other_order_frames == 0
+    assert a.order == "tie" and a.configs4_order == "tie" and a.other_order_frames > 0
+    b = bench.parse(["--order", "stable", "--configs4-order", "stable", "--other-order-frames", "0"])
+    assert b.order == "stable" and b.configs4_order == "stable" and b.other_order_frames == 0
