@@ -1485,7 +1485,7 @@ __global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, c
 // level touch disjoint subtrees and run in parallel, deepest level first.
 constexpr int kHeapCap = 20480 - 128; // longest segment staged in LDS (with the spare slots: 160 KB less 512 B);
                                       // longer ones run the same schedule on a global scratch copy
-constexpr int kHeapT = 256;
+constexpr int kHeapT = 1024;
 constexpr int kHeapGrid = 256;
 
 __device__ __forceinline__ int hlev(int x) { return 31 - __clz(x + 1); }
@@ -1680,6 +1680,20 @@ __device__ void glb_ce_step(const GlbHeap& G, int n, int P, int j, int flipmask)
     }
     __syncthreads();
 }
+// i = 0 .. n - 1 over the workgroup, U loads in flight per thread before their stores (the global-side
+// passes over a long segment are latency-bound otherwise)
+template <int U, class Ld, class St>
+__device__ __forceinline__ void copy_batched(int n, const Ld& load, const St& store) {
+    for (int i0 = threadIdx.x; i0 < n; i0 += U * kHeapT) {
+        uint2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * kHeapT < n) v[u] = load(i0 + u * kHeapT);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * kHeapT < n) store(i0 + u * kHeapT, v[u]);
+    }
+}
 // true when two neighbours of the sorted S[0, n) / G[0, n) hold the same key
 __device__ bool lds_has_equal(const uint2* S, int n) {
     int eq = 0;
@@ -1688,7 +1702,8 @@ __device__ bool lds_has_equal(const uint2* S, int n) {
 }
 __device__ bool glb_has_equal(const GlbHeap& G, int n) {
     int eq = 0;
-    for (int i = threadIdx.x + 1; i < n; i += kHeapT) eq |= G.ld(i).y == G.ld(i - 1).y;
+    copy_batched<4>(n - 1, [&](int i) { return make_uint2(G.ld(i).y, G.ld(i + 1).y); },
+                    [&](int, uint2 v) { eq |= v.x == v.y; });
     return __syncthreads_or(eq) != 0;
 }
 // the network on the global copy G[0, n): chunks of kBitChunk sorted in LDS, then per phase the steps whose
@@ -1704,11 +1719,11 @@ __device__ void glb_bitonic(const GlbHeap& G, uint2* S, int n) {
         }
         for (int c0 = 0; c0 < n; c0 += kBitChunk) {
             const int nv = min(kBitChunk, n - c0);
-            for (int i = t; i < nv; i += kHeapT) S[i] = G.ld(c0 + i);
+            copy_batched<4>(nv, [&](int i) { return G.ld(c0 + i); }, [&](int i, uint2 v) { S[i] = v; });
             __syncthreads();
             if (k) lds_bitonic(S, nv, Pc, 0, 0, kBitChunk >> 1);
             else lds_bitonic(S, nv, Pc, 2, Pc, 0);
-            for (int i = t; i < nv; i += kHeapT) G.st(c0 + i, S[i]);
+            copy_batched<4>(nv, [&](int i) { return S[i]; }, [&](int i, uint2 v) { G.st(c0 + i, v); });
             __syncthreads();
         }
     }
@@ -1740,7 +1755,8 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
             }
         } else {                                              // the copy at the segment's own offset
             GlbHeap G{big + off};
-            for (int i = t; i < n; i += kHeapT) G.st(i, make_uint2(vals[off + i], keys[off + i]));
+            copy_batched<4>(n, [&](int i) { return make_uint2(vals[off + i], keys[off + i]); },
+                            [&](int i, uint2 v) { G.st(i, v); });
             __syncthreads();
             glb_bitonic(G, H, n);
             if (glb_has_equal(G, n)) {
@@ -1748,11 +1764,10 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
                 __syncthreads();
                 heap_sort_seg(G, n, bigcap - off, jb);        // spares: big[bigcap .. bigcap + 64)
             }
-            for (int i = t; i < n; i += kHeapT) {
-                const uint2 x = G.ld(i);
+            copy_batched<4>(n, [&](int i) { return G.ld(i); }, [&](int i, uint2 x) {
                 keys[off + i] = x.y;
                 vals[off + i] = x.x;
-            }
+            });
         }
         __syncthreads();
     }
