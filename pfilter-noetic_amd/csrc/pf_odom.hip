@@ -27,6 +27,13 @@
 #include <vector>
 #include <cstring>
 
+#ifndef PF_TIE_LEVELS_A
+#define PF_TIE_LEVELS_A 0   // big levels of the tie-order VoxelGrid sort (0: classes straight to k_tie_medium)
+#endif
+#ifndef PF_TIE_LEVELS_B
+#define PF_TIE_LEVELS_B 0   // least big levels of the tie-order rgbds sort
+#endif
+
 namespace pf {
 namespace {
 
@@ -3157,7 +3164,7 @@ void stage_enqueue_vg(OdomGPU& o, int p, hipStream_t s) {
     PF_LAUNCH_NC(nc, k_vg_keys, dim3(kGrid), dim3(256), 0, s, clouds(sb.in), cnt, o.acc_a, leaf, o.vkeys, o.vvals,
                  sort_hist(o.vprim, 32, true));
     if (o.tie_order)                       // std::sort's order of equal keys (PCL VoxelGrid, B.1)
-        tie_sort(*o.tie_a, o.vkeys, o.vvals, TieClasses{cnt, C_IN, -1, nc}, o.vprim.err, s);
+        tie_sort(*o.tie_a, o.vkeys, o.vvals, TieClasses{cnt, C_IN, -1, nc}, o.vprim.err, s, PF_TIE_LEVELS_A);
     else
         radix_sort_pairs(o.vkeys, o.vvals, cnt + C_VGN, 32, o.vprim, s, nullptr, nullptr, true);
     segment_starts(o.vkeys, cnt + C_VGN, o.vsegstart, cnt + C_NSEG, cnt + C_NLT, cnt + C_NRG_VALID, o.vprim, s);
@@ -3254,7 +3261,7 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     }
     if (o.tie_order)                       // std::sort's order of equal keys (:74)
         tie_sort(*o.tie_b, o.keys, o.vals, TieClasses{cnt, C_M, C_DS, nc}, o.prim.err, s,
-                 tie_levels_for(*o.tie_b, o.tie_hint));
+                 std::max(tie_levels_for(*o.tie_b, o.tie_hint), PF_TIE_LEVELS_B));
     else
         radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
     RgTailArgs ta{cnt, clouds(map_cur(o)), clouds(o.app), o.keys, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,

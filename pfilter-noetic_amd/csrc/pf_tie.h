@@ -45,7 +45,10 @@
 
 namespace pf {
 
-constexpr int kTieMed = 65536;        // classes above this run the multi-workgroup big levels first
+#ifndef PF_TIE_MED
+#define PF_TIE_MED 65536
+#endif
+constexpr int kTieMed = PF_TIE_MED;   // classes above this run the multi-workgroup big levels first
 constexpr int kTieTile = 4096;        // keys per tile of the compaction and the big levels
 
 // class c of the input is its next cnt[ia + c] (+ cnt[ib + c] when ib >= 0) pairs, c < nc: the
