@@ -1621,6 +1621,9 @@ __device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int
 // The network is the flip form (every compare-exchange puts the smaller key first; phase k opens with
 // partner i ^ (k - 1), then the half-cleaners i + j): positions at or past the segment's end act as +inf
 // and are never touched, so no padding.
+#ifndef PF_HEAP_U
+#define PF_HEAP_U 4                   // loads in flight per thread in the long segments' global passes
+#endif
 constexpr int kBitChunk = 16384;      // chunk of a global segment staged in LDS (128 KB)
 
 __device__ __forceinline__ int ce_lo(int c, int j) { return ((c & ~(j - 1)) << 1) | (c & (j - 1)); }
@@ -1654,7 +1657,7 @@ __device__ void lds_bitonic(uint2* S, int nv, int P, int k0, int k1, int jtop) {
 }
 // one step of the network on the global copy (four compare-exchanges in flight per thread)
 __device__ void glb_ce_step(const GlbHeap& G, int n, int P, int j, int flipmask) {
-    constexpr int U = 4;
+    constexpr int U = PF_HEAP_U;
     for (int c0 = threadIdx.x; c0 < (P >> 1); c0 += U * kHeapT) {
         int i[U], q[U];
         uint2 a[U], b[U];
@@ -1702,7 +1705,7 @@ __device__ bool lds_has_equal(const uint2* S, int n) {
 }
 __device__ bool glb_has_equal(const GlbHeap& G, int n) {
     int eq = 0;
-    copy_batched<4>(n - 1, [&](int i) { return make_uint2(G.ld(i).y, G.ld(i + 1).y); },
+    copy_batched<PF_HEAP_U>(n - 1, [&](int i) { return make_uint2(G.ld(i).y, G.ld(i + 1).y); },
                     [&](int, uint2 v) { eq |= v.x == v.y; });
     return __syncthreads_or(eq) != 0;
 }
@@ -1719,11 +1722,11 @@ __device__ void glb_bitonic(const GlbHeap& G, uint2* S, int n) {
         }
         for (int c0 = 0; c0 < n; c0 += kBitChunk) {
             const int nv = min(kBitChunk, n - c0);
-            copy_batched<4>(nv, [&](int i) { return G.ld(c0 + i); }, [&](int i, uint2 v) { S[i] = v; });
+            copy_batched<PF_HEAP_U>(nv, [&](int i) { return G.ld(c0 + i); }, [&](int i, uint2 v) { S[i] = v; });
             __syncthreads();
             if (k) lds_bitonic(S, nv, Pc, 0, 0, kBitChunk >> 1);
             else lds_bitonic(S, nv, Pc, 2, Pc, 0);
-            copy_batched<4>(nv, [&](int i) { return S[i]; }, [&](int i, uint2 v) { G.st(c0 + i, v); });
+            copy_batched<PF_HEAP_U>(nv, [&](int i) { return S[i]; }, [&](int i, uint2 v) { G.st(c0 + i, v); });
             __syncthreads();
         }
     }
@@ -1755,7 +1758,7 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
             }
         } else {                                              // the copy at the segment's own offset
             GlbHeap G{big + off};
-            copy_batched<4>(n, [&](int i) { return make_uint2(vals[off + i], keys[off + i]); },
+            copy_batched<PF_HEAP_U>(n, [&](int i) { return make_uint2(vals[off + i], keys[off + i]); },
                             [&](int i, uint2 v) { G.st(i, v); });
             __syncthreads();
             glb_bitonic(G, H, n);
@@ -1764,7 +1767,7 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
                 __syncthreads();
                 heap_sort_seg(G, n, bigcap - off, jb);        // spares: big[bigcap .. bigcap + 64)
             }
-            copy_batched<4>(n, [&](int i) { return G.ld(i); }, [&](int i, uint2 x) {
+            copy_batched<PF_HEAP_U>(n, [&](int i) { return G.ld(i); }, [&](int i, uint2 x) {
                 keys[off + i] = x.y;
                 vals[off + i] = x.x;
             });
