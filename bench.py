@@ -804,14 +804,6 @@ class pinned_core:
                 "cores_available": len(self.saved) if self.saved else os.cpu_count()}
 
 
-def cpu_baseline(budget_s, warmup):
-    """pfref oracle, single thread, reference-faithful options (kd-tree, dense-QR LM, std::sort)."""
-    with pinned_core() as pc:
-        out = _cpu_baseline(budget_s, warmup)
-        out["host"] = pc.host()
-    return out
-
-
 def _cpu_baseline(budget_s, warmup, preset="S64", theta=(0.4, 75), max_frames=2000, lines=64):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pfref
@@ -831,6 +823,109 @@ def _cpu_baseline(budget_s, warmup, preset="S64", theta=(0.4, 75), max_frames=20
     return {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port", "frames": [warmup, k],
             "sample": "pfref (oracle/, reference-faithful opts=0) frames %d..%d of the same %s seed-0 sequence "
                       "after %d warm-up frames, single thread, %.1f s of CPU time" % (warmup, k - 1, preset, warmup, el)}
+
+
+def vdc_order(n):
+    """0 .. n-1 in van der Corput (bit-reversed) order: every prefix is spread over the whole range"""
+    bits = max(1, (n - 1).bit_length())
+    out = []
+    for i in range(1 << bits):
+        r = int(format(i, "0%db" % bits)[::-1], 2)
+        if r < n:
+            out.append(r)
+    return out
+
+
+def cpu_baseline_synced(device, ptrs, warmup, budget_s, use_graph=True, strata=512, preset="S64", seed=0):
+    """pfref (oracle/, reference-faithful opts=0) timed per frame on a stratified sample of the headline's
+    own frames [warmup, len(ptrs)): one frame per stratum (its middle), strata visited in van der Corput
+    order so that the frames timed before the budget ran out are spread over the whole sequence.
+
+    The oracle is not run through the sequence: before each sampled frame k it is given the device's
+    estimator state after frame k - 1 -- both local maps with their age / p-index bytes, odom, last_odom,
+    optimization_count, the transfer of the synced parity test (tests/test_gpu_parity_synced.py) -- from
+    a capture pass of the device pipeline over the same frames (outside every timed region). Only the
+    oracle's frame call (featureExtraction + updatePointsToMap, the reference's timed boundary:
+    src/laserProcessingNode.cpp:71-78 + src/odomEstimationNode copy.cpp:92-100) is timed, single thread,
+    pinned to one core. Each timed frame's oracle pose is also compared with the device's pose of that
+    frame from the same state (`parity`)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pfilter_amd as pa
+    import pfref
+    import pfsynth
+    from_ = warmup
+    total = len(ptrs)
+    span = total - from_
+    strata = max(1, min(strata, span))
+    frames = sorted({from_ + (2 * s + 1) * span // (2 * strata) for s in range(strata)})
+    want = set(frames)
+    # capture pass: the device pipeline in frame order, the state taken before every sampled frame
+    od = pa.Odom_ES_EstimationClass(device=device, max_points=300000, map_capacity=1 << 22)
+    od.init(lidar_cfg(), **ODOM_CFG)
+    set_order(od)
+    od.set_graph(use_graph)
+    states, dev_pose = {}, {}
+    poses_so_far = None
+    for k in range(total):
+        if k in want and k > 0:
+            poses_so_far = od.poses()
+            p1, p2 = poses_so_far[k - 1], poses_so_far[max(k - 2, 0)]
+            opt = od.state()["optimization_count"]
+            states[k] = ([od._map(0), od._map(1)], p1, p2, opt)
+        od.frame_device(*ptrs[k])
+        if k in want:
+            od.sync()
+    allp = od.poses()
+    assert od.stats()["errors"] == 0
+    del od
+    for k in states:
+        dev_pose[k] = allp[k]
+    # the CPU pass
+    seq = pfsynth.Sequence(preset, n_frames=total, seed=seed)
+    orc = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), ODOM_CFG["map_resolution"], ODOM_CFG["k_new"],
+                     ODOM_CFG["theta_p"], ODOM_CFG["theta_max"], ODOM_CFG["weightType"], opts=0)
+    order = [frames[i] for i in vdc_order(len(frames))]
+    n, el = 0, 0.0
+    worst_t = worst_r = 0.0
+    timed = []
+    with pinned_core() as pc:
+        for k in order:
+            if el >= budget_s:
+                break
+            if k not in states:
+                continue
+            maps, p1, p2, opt = states[k]
+            for c, (xyz, rg) in enumerate(maps):
+                orc.set_map(c, xyz, rg)
+            orc.set_state(p1, p2)
+            orc.set_opt_count(opt)
+            x = seq.frame(k)
+            t = time.perf_counter()
+            pose = orc.frame(x)
+            el += time.perf_counter() - t
+            n += 1
+            timed.append(k)
+            dt, dr = pose_diff(pose, dev_pose[k])
+            worst_t, worst_r = max(worst_t, dt), max(worst_r, dr)
+        host = pc.host()
+    timed.sort()
+    return {"value": round(n / el, 3), "unit": "frames/s", "cores": 1, "kind": "port", "host": host,
+            "frames_timed": n, "strata": len(frames), "frame_range": [from_, total - 1],
+            "first_last_timed": [timed[0], timed[-1]] if timed else None,
+            "sample": "pfref (oracle/, reference-faithful opts=0), single thread pinned to one core: %d frames "
+                      "of the headline's own frames %d..%d (one per stratum of %d, strata in van der Corput "
+                      "order until %.1f s of CPU time), each from the device's estimator state before it "
+                      "(maps with age / p-index bytes, odom, last_odom, optimization_count)"
+                      % (n, from_, total - 1, len(frames), el),
+            "parity": {"frames": n, "worst_t_m": worst_t, "worst_r_rad": worst_r,
+                       "note": "oracle pose vs the device's pose of the same frame from the same state"}}
+
+
+def pose_diff(a, b):
+    """(translation m, rotation rad) between two {qx, qy, qz, qw, tx, ty, tz} poses"""
+    dt = float(np.linalg.norm(np.asarray(a[4:7]) - np.asarray(b[4:7])))
+    q = np.asarray(a[:4]) * (1.0 if float(np.dot(a[:4], b[:4])) >= 0 else -1.0)
+    return dt, float(2.0 * np.linalg.norm(q - np.asarray(b[:4])))     # tests/_util.py pose_err
 
 
 ES_LEGS = {
@@ -1152,7 +1247,8 @@ def main(argv=None):
     if "enqueue" in r:
         out["config"]["host_enqueue_us_per_frame"] = round(r["enqueue"] / max(1, frames) * 1e6, 1)
     if world == 1 and not stub:
-        out["stage_us"] = stage_pass(local_rank, r["ptrs"], args.warmup, min(1000, frames), graph_mode(args))
+        # over the same frames as `value` (every timed frame)
+        out["stage_us"] = stage_pass(local_rank, r["ptrs"], args.warmup, frames, graph_mode(args))
     if world == 1 and not stub and args.other_order_frames > 0:
         other = "stable" if args.order == "tie" else "tie"
         try:
@@ -1199,7 +1295,12 @@ def main(argv=None):
         out["pcie_inclusive"] = pc
         log("pcie_inclusive: %s" % pc)
     if host_legs and args.node_frames > 0:
+        # the device pipeline (value's path) over exactly the node legs' frames, for like-for-like ratios
+        gw = gpu_window(local_rank, args.warmup, min(frames + args.warmup, args.warmup + args.node_frames), threads,
+                        graph_mode(args))
         nd = node_pattern_leg(local_rank, r["hptrs"], args.warmup, args.node_frames)
+        nd["pipeline_same_frames"] = gw
+        nd["ratio_to_pipeline_same_frames"] = round(nd["value"] / gw["value"], 4)
         npo = nd.pop("poses")
         nd["poses_equal_headline"] = bool(np.array_equal(npo, r["poses"][:npo.shape[0]]))
         out["node_pattern"] = nd
@@ -1208,7 +1309,7 @@ def main(argv=None):
             nt = node_threads_leg(local_rank, r["hptrs"], args.warmup, args.node_frames)
             ntp = nt.pop("poses")
             nt["poses_equal_headline"] = bool(np.array_equal(ntp, r["poses"][:ntp.shape[0]]))
-            nt["ratio_to_value"] = round(nt["value"] / value, 4)
+            nt["ratio_to_pipeline_same_frames"] = round(nt["value"] / gw["value"], 4)
             out["node_threads"] = nt
             log("node_threads: %s" % nt)
         except Exception as e:  # report, never hide
@@ -1228,15 +1329,13 @@ def main(argv=None):
         log("pageable leg ...")
         out["pcie_pageable"] = pageable_leg(local_rank, args.pageable_frames, threads, use_graph=graph_mode(args))
     if world == 1 and not args.no_cpu and not stub:
-        log("cpu baseline ...")
-        cb = cpu_baseline(args.cpu_seconds, args.warmup)
-        f0, f1 = cb.pop("frames")
-        # the GPU on exactly the CPU sample's frames, for a like-for-like ratio
-        gw = gpu_window(local_rank, f0, f1, threads, graph_mode(args))
-        cb["gpu_same_frames"] = gw
-        cb["speedup_same_frames"] = round(gw["value"] / cb["value"], 2)
+        log("cpu baseline (stratified over the headline's frames, device state synced) ...")
+        cb = cpu_baseline_synced(local_rank, r["ptrs"], args.warmup, args.cpu_seconds, graph_mode(args))
         out["cpu_baseline"] = cb
+        # like for like: both rates are over the same population of frames (every timed frame for the GPU,
+        # a stratified sample of those frames for the CPU)
         out["speedup_vs_cpu"] = round(value / cb["value"], 2)
+        log("cpu_baseline: %s" % cb)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

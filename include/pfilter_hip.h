@@ -98,10 +98,11 @@ int pf_fe_extract(pf_fe* h, const float* xyzi, size_t n, size_t stride_bytes, fl
  * [0, num_lines) dropped. SURVEY 8(d) config 5 (synthetic 128-line scans, -25..+15 deg) runs with it.
  * top_deg == bottom_deg == 0 restores the reference's formulas (the default). */
 int pf_fe_set_ring_model(pf_fe* h, double top_deg, double bottom_deg);
-/* Reference tie order (default off): a sector whose curvature list holds equal values is ordered as
- * libstdc++'s std::sort leaves it (src/laserProcessingClass.cpp:101-104 sorts by value alone, and the
- * surf cloud is written in that order) instead of by (value, ring position); sectors without an
- * exact tie are identical either way. pf_odom_set_tie_order switches the handle's featureExtraction too. */
+/* Reference tie order (default ON since round 5): a sector whose curvature list holds equal values is
+ * ordered as libstdc++'s std::sort leaves it (src/laserProcessingClass.cpp:101-104 sorts by value alone,
+ * and the surf cloud is written in that order); 0 orders it by (value, ring position) instead. Sectors
+ * without an exact tie are identical either way. pf_odom_set_tie_order switches the handle's
+ * featureExtraction too. */
 int pf_fe_set_tie_order(pf_fe* h, int enable);
 
 /* ---------------- odometry (Odom_ES_EstimationClass) ---------------- */
@@ -334,13 +335,14 @@ int pf_odom_map_export(pf_odom* h, int which, const float** xyzw, size_t* n);
 #define PF_GRAPH_STAGE_A 2
 #define PF_GRAPH_STAGE_B 4
 int pf_odom_set_graph(pf_odom* h, int mode);
-/* Reference tie order (default off): VoxelGrid (stage A) and rgbds (stage B) order the points of a
- * voxel as libstdc++'s std::sort leaves them -- the reference's own sorts (PCL 1.10 VoxelGrid, SURVEY
- * B.1; src/odomEstimationClass.cpp:74), which are not stable -- instead of in input order, so that every
- * f32 centroid is summed in the reference's order. It runs introsort's recursion on the device
- * (pf_tie.h: tile-parallel partitions for segments above 14336 keys, the rest of every subtree in LDS)
- * in place of the radix sorts; off, the sorts are stable radix sorts (VoxelGrid) and a merge of the
- * voxel-ordered map with the sorted appended points (rgbds). */
+/* Reference tie order (default ON since round 5: pf_odom_create / pf_bpf_create enable it, so a handle
+ * gives the reference's results frame by frame unless the caller opts out): VoxelGrid (stage A) and
+ * rgbds (stage B) order the points of a voxel as libstdc++'s std::sort leaves them -- the reference's own
+ * sorts (PCL 1.10 VoxelGrid; src/odomEstimationClass.cpp:74), which are not stable -- so that
+ * every f32 centroid is summed in the reference's order. It runs introsort's recursion on the device
+ * (pf_tie.h) in place of the radix sorts. enable = 0 is the faster stable mode: stable radix sorts
+ * (VoxelGrid) and a merge of the voxel-ordered map with the sorted appended points (rgbds); its
+ * centroids' last bits differ from the reference's in 0.5-1 % of frames. */
 int pf_odom_set_tie_order(pf_odom* h, int enable);
 /* Measurement: the association's kNN alone (the exact 5-NN of k_assoc, src/odomEstimationClass.cpp:299,
  * 447) on the last frame's queries -- its down-sampled points through the solved pose -- against the

@@ -7,6 +7,7 @@
 #include <vector>
 
 extern "C" void pfref_introsort_stats(const uint32_t* keys, size_t n, long* st);   // pfref_sort.cpp
+extern "C" void pfref_introsort_heapdep(const uint32_t* keys, const uint8_t* dep, size_t n, const char* tag);
 
 namespace pfref {
 

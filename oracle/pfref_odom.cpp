@@ -64,6 +64,48 @@ void sort_pairs(std::vector<IdxPair>& iv, bool stable) {
     if (stable) std::stable_sort(iv.begin(), iv.end(), lt);
     else std::sort(iv.begin(), iv.end(), lt);
 }
+
+// development statistics (PFREF_GROUP_STATS): of one sorted call, the voxel groups whose f32 centroid
+// sum depends on the order of their points. A group of <= 2 is order-free (0 + a is exact, + commutes);
+// a group of 3 has three left folds, compared per coordinate; 4 and more count as order-dependent.
+void group_stats(const char* what, const std::vector<PtC>& in, const std::vector<IdxPair>& iv) {
+    static const bool on = std::getenv("PFREF_GROUP_STATS") != nullptr;
+    if (!on) return;
+    long g[4] = {0, 0, 0, 0}, dep3 = 0, gmax = 0, dep_keys = 0;
+    std::vector<uint32_t> keys(iv.size());
+    std::vector<uint8_t> depf(iv.size(), 0);
+    for (const IdxPair& q : iv) keys[q.cloud_point_index] = q.idx;
+    size_t index = 0;
+    while (index < iv.size()) {
+        size_t i = index + 1;
+        while (i < iv.size() && iv[i].idx == iv[index].idx) ++i;
+        const long n = (long)(i - index);
+        gmax = std::max(gmax, n);
+        ++g[std::min(n, 4L) - 1];
+        if (n == 3) {
+            const PtC& a = in[iv[index].cloud_point_index];
+            const PtC& b = in[iv[index + 1].cloud_point_index];
+            const PtC& c = in[iv[index + 2].cloud_point_index];
+            bool dep = false;
+            const float va[3] = {a.x, a.y, a.z}, vb[3] = {b.x, b.y, b.z}, vc[3] = {c.x, c.y, c.z};
+            for (int d = 0; d < 3; ++d) {
+                volatile float f1 = (va[d] + vb[d]) + vc[d], f2 = (va[d] + vc[d]) + vb[d], f3 = (vb[d] + vc[d]) + va[d];
+                dep |= !(f1 == f2 && f1 == f3);
+            }
+            dep3 += dep;
+            if (dep) dep_keys += 3;
+            if (dep)
+                for (size_t li = index; li < i; ++li) depf[iv[li].cloud_point_index] = 1;
+        } else if (n >= 4) {
+            dep_keys += n;
+            for (size_t li = index; li < i; ++li) depf[iv[li].cloud_point_index] = 1;
+        }
+        index = i;
+    }
+    pfref_introsort_heapdep(keys.data(), depf.data(), keys.size(), what);
+    std::fprintf(stderr, "groups %s n %zu g1 %ld g2 %ld g3 %ld dep3 %ld g4+ %ld max %ld depkeys %ld\n", what, iv.size(),
+                 g[0], g[1], g[2], dep3, g[3], gmax, dep_keys);
+}
 }  // namespace
 
 void voxel_grid(const std::vector<PtC>& in, float leaf, bool stable, std::vector<PtC>& out) {
@@ -97,6 +139,7 @@ void voxel_grid(const std::vector<PtC>& in, float leaf, bool stable, std::vector
         iv.push_back({static_cast<unsigned>(idx), static_cast<unsigned>(i)});
     }
     sort_pairs(iv, stable);
+    group_stats("vg", in, iv);
     size_t index = 0;
     while (index < iv.size()) {
         size_t i = index + 1;
@@ -143,6 +186,7 @@ void rgbds(const std::vector<PtC>& in, float dsleaf, bool stable, std::vector<Pt
         iv.push_back({static_cast<unsigned>(idx), static_cast<unsigned>(i)});
     }
     sort_pairs(iv, stable);                                        // :74
+    group_stats("rg", in, iv);
     size_t index = 0;
     while (index < iv.size()) {                                    // :86-131
         size_t i = index + 1;

@@ -21,6 +21,7 @@
 #include <climits>
 #include <cstddef>
 #include <cstdint>
+#include <cstdio>
 #include <utility>
 #include <vector>
 
@@ -295,6 +296,51 @@ void pfref_introsort_stats(const uint32_t* keys, size_t n, long* st) {
             stack.push_back(F{cut - a.data(), last - a.data(), depth, lev + 1});
             last = cut;
             ++lev;
+        }
+    }
+}
+
+// development statistics: every depth-limit segment of one std::sort call with, per element, whether
+// its voxel group's f32 sum depends on the order (dep[i] != 0, indexed by input position): prints the
+// segment length, its distinct keys, the keys of order-dependent groups in it, those groups, and the
+// heap pops needed before the smallest order-dependent key (pops run from the largest key down)
+void pfref_introsort_heapdep(const uint32_t* keys, const uint8_t* dep, size_t n, const char* tag) {
+    std::vector<E> a = pairs(keys, n);
+    struct F { long f, l, d; };
+    std::vector<F> stack;
+    const long d0 = n > 1 ? 2L * lg(n) : 0;
+    if (n > 16) stack.push_back(F{0, (long)n, d0});
+    while (!stack.empty()) {
+        F s = stack.back();
+        stack.pop_back();
+        E* first = a.data() + s.f;
+        E* last = a.data() + s.l;
+        long depth = s.d;
+        while (last - first > 16) {
+            if (depth == 0) {
+                const long len = last - first;
+                std::vector<E> seg(first, last);
+                std::stable_sort(seg.begin(), seg.end(), lt);
+                long ndk = 0, ndg = 0, distinct = 0, pops = 0;
+                for (long i = 0; i < len; ++i) {
+                    const bool head = i == 0 || seg[i].key != seg[i - 1].key;
+                    distinct += head;
+                    if (dep[seg[i].val]) {
+                        ++ndk;
+                        if (head || !dep[seg[i - 1].val]) ++ndg;
+                        if (!pops) pops = len - i;
+                    }
+                }
+                std::fprintf(stderr, "heapdep %s len %ld distinct %ld depkeys %ld depgroups %ld pops %ld\n", tag, len,
+                             distinct, ndk, ndg, pops);
+                break;
+            }
+            --depth;
+            E* mid = first + (last - first) / 2;
+            move_median_to_first(first, first + 1, mid, last - 1);
+            E* cut = unguarded_partition(first + 1, last, first);
+            stack.push_back(F{cut - a.data(), last - a.data(), depth});
+            last = cut;
         }
     }
 }

@@ -180,6 +180,7 @@ int pf_fe_create(const pf_lidar_params* lidar, int device, size_t max_points, pf
     if (!h) return PF_ENOMEM;
     h->device = device;
     int rc = fe_alloc(h->fe, *lidar, max_points);
+    h->fe.tie_order = true;               // the reference's std::sort order by default (pf_fe_set_tie_order)
     const size_t ecap = (size_t)h->fe.rings * 6 * kEdgePerSector;
     if (rc == PF_OK && hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) rc = PF_EHIP;
     if (rc == PF_OK && hipMalloc(&h->d_edge, sizeof(float4) * ecap) != hipSuccess) rc = PF_ENOMEM;
@@ -289,6 +290,9 @@ static int create(const pf_lidar_params* lidar, const pf_odom_params* params, in
     pf_odom* h = new (std::nothrow) pf_odom();
     if (!h) return PF_ENOMEM;
     int rc = odom_create(h->o, *lidar, *params, device, max_points, map_capacity, nc);
+    // the reference's results by default: VoxelGrid / rgbds / the sector sort in std::sort's order of
+    // equal keys (pf_odom_set_tie_order(h, 0) selects the stable sorts)
+    if (rc == PF_OK) rc = pf_odom_set_tie_order(h, 1);
     if (rc != PF_OK) {
         pf_odom_destroy(h);
         return rc;

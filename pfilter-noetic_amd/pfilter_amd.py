@@ -350,8 +350,10 @@ class HostBuffer:
 class LaserProcessingClass:
     """Drop-in for LaserProcessingClass (featureExtraction on the GPU)."""
 
-    def __init__(self, device=0, max_points=300000):
-        self.device, self.max_points = device, max_points
+    def __init__(self, device=0, max_points=300000, tie_order=None):
+        """tie_order: None = the library default (the reference's std::sort order, on), False = the
+        stable (value, ring position) order"""
+        self.device, self.max_points, self.tie_order = device, max_points, tie_order
         self._h = None
 
     def init(self, lidar_param):
@@ -359,6 +361,8 @@ class LaserProcessingClass:
         _check("pf_fe_create", lib().pf_fe_create(ctypes.byref(lidar_param), self.device, self.max_points,
                                                   ctypes.byref(h)))
         self._h = h.value
+        if self.tie_order is not None:
+            self.set_tie_order(self.tie_order)
         self._rings = lidar_param.num_lines
         rm = getattr(lidar_param, "ring_model", None)
         if rm:
@@ -389,10 +393,17 @@ class LaserProcessingClass:
 class Odom_ES_EstimationClass:
     """Drop-in for Odom_ES_EstimationClass (the whole update on the GPU)."""
 
-    def __init__(self, device=0, max_points=300000, map_capacity=1 << 22):
+    def __init__(self, device=0, max_points=300000, map_capacity=1 << 22, tie_order=None):
+        """tie_order: None = the library default (the reference's std::sort order of equal keys, on:
+        pf_odom_set_tie_order), False = the stable sorts (faster, centroids' last bits not the reference's)"""
         self.device, self.max_points, self.map_capacity = device, max_points, map_capacity
+        self.tie_order = tie_order
         self._h = None
         self.last_status = PF_OK
+
+    def _apply_order(self):
+        if self.tie_order is not None:
+            self.set_tie_order(self.tie_order)
 
     def init(self, lidar_param, map_resolution, k_new, theta_p, theta_max, weightType):
         self.lidar = lidar_param
@@ -401,6 +412,7 @@ class Odom_ES_EstimationClass:
         _check("pf_odom_create", lib().pf_odom_create(ctypes.byref(lidar_param), ctypes.byref(prm), self.device,
                                                       self.max_points, self.map_capacity, ctypes.byref(h)))
         self._h = h.value
+        self._apply_order()
         rm = getattr(lidar_param, "ring_model", None)
         if rm:
             _check("pf_odom_set_ring_model", lib().pf_odom_set_ring_model(self._h, float(rm[0]), float(rm[1])))
@@ -614,6 +626,7 @@ class Odom_BPF_EstimationClass(Odom_ES_EstimationClass):
         _check("pf_bpf_create", lib().pf_bpf_create(ctypes.byref(lidar_param), ctypes.byref(prm), self.device,
                                                     self.max_points, self.map_capacity, ctypes.byref(h)))
         self._h = h.value
+        self._apply_order()
 
     def initMapWithPoints(self, beam_in, pillar_in, facade_in):
         b, p, f = _f32x4(beam_in), _f32x4(pillar_in), _f32x4(facade_in)

@@ -95,6 +95,16 @@ public:
         if (h_) { pf_fe_destroy(h_); h_ = nullptr; }
         const pf_lidar_params p = lidar_params(lidar_param_in);
         check("pf_fe_create", pf_fe_create(&p, device_, max_points_, &h_));
+        check("pf_fe_set_tie_order", pf_fe_set_tie_order(h_, reference_tie_order ? 1 : 0));
+    }
+
+    // true (the default): equal curvatures in a sector come out as libstdc++'s std::sort leaves them
+    // (src/laserProcessingClass.cpp:101-104), i.e. the reference's clouds; false: (value, ring position)
+    // order. Read by init(); setReferenceTieOrder() switches a live handle.
+    bool reference_tie_order = true;
+    void setReferenceTieOrder(bool on) {
+        reference_tie_order = on;
+        if (h_) check("pf_fe_set_tie_order", pf_fe_set_tie_order(h_, on ? 1 : 0));
     }
 
     // appends to pc_out_edge / pc_out_surf, never modifies pc_in (laserProcessingClass.cpp:10-96)
@@ -145,7 +155,18 @@ public:
 #endif
     int optimization_count = 2;
 
+    // true (the default): VoxelGrid, rgbds and featureExtraction's sector sort order equal keys as
+    // libstdc++'s std::sort does (pf_odom_set_tie_order), so the poses and maps are the reference's frame
+    // by frame; false: the faster stable-sort mode, whose centroids differ from the reference's in the
+    // last bits. Read by init(); setReferenceTieOrder() switches a live handle.
+    bool reference_tie_order = true;
+
 protected:
+    void apply_tie_order(pf_odom* h, bool on) {
+        reference_tie_order = on;
+        if (h) check("pf_odom_set_tie_order", pf_odom_set_tie_order(h, on ? 1 : 0));
+    }
+
     void pull_state(pf_odom* h) {
         double lo[12];
         check("pf_odom_get_state", pf_odom_get_state(h, parameters, lo, &optimization_count));
@@ -236,6 +257,7 @@ public:
         op.theta_max = theta_max_para;
         op.weight_type = (int)weightType_para;
         check("pf_odom_create", pf_odom_create(&lp, &op, device_, max_points_, map_capacity_, &h_));
+        check("pf_odom_set_tie_order", pf_odom_set_tie_order(h_, reference_tie_order ? 1 : 0));
         export_on_ = false;
         set_identity();
         laserCloudCornerMap->clear();
@@ -272,6 +294,7 @@ public:
     // subscriber reads them, as in src/odomEstimationNode copy.cpp:129-141)
     bool refresh_maps_every_frame = true;
     void syncMaps() { fill_map(h_, 0, *laserCloudCornerMap); fill_map(h_, 1, *laserCloudSurfMap); }
+    void setReferenceTieOrder(bool on) { apply_tie_order(h_, on); }
 
 #ifndef PFILTER_HIP_NO_EIGEN
     Eigen::Isometry3d odom = Eigen::Isometry3d::Identity();
@@ -337,6 +360,7 @@ public:
         op.theta_max = theta_max_para;
         op.weight_type = (int)weightType_para;
         check("pf_bpf_create", pf_bpf_create(&lp, &op, device_, max_points_, map_capacity_, &h_));
+        check("pf_odom_set_tie_order", pf_odom_set_tie_order(h_, reference_tie_order ? 1 : 0));
         export_on_ = false;
         set_pose(kIdentity);
         for (Ptr* m : maps()) (*m)->clear();
@@ -389,6 +413,7 @@ public:
     }
 
     bool refresh_maps_every_frame = true;
+    void setReferenceTieOrder(bool on) { apply_tie_order(h_, on); }
     void syncMaps() {
         int c = 0;
         for (Ptr* m : maps()) fill_map(h_, c++, **m);

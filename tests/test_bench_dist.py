@@ -184,3 +184,27 @@ def test_sort_order_flags():
     assert a.order == "tie" and a.configs4_order == "tie" and a.other_order_frames > 0
     b = bench.parse(["--order", "stable", "--configs4-order", "stable", "--other-order-frames", "0"])
     assert b.order == "stable" and b.configs4_order == "stable" and b.other_order_frames == 0
+
+
+def test_cpu_baseline_sample_order():
+    """bench.py's CPU baseline times one frame per stratum of the headline's frames, strata in van der
+    Corput order: a permutation of the strata whose every prefix is spread over the whole sequence, so a
+    budget that ends the sample early still covers early and late frames alike."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for n in (1, 2, 7, 64, 512, 1000):
+        o = bench.vdc_order(n)
+        assert sorted(o) == list(range(n))
+    o = bench.vdc_order(512)
+    for m in (8, 32, 128):
+        pre = sorted(o[:m])
+        assert pre[0] < 512 // m and pre[-1] >= 512 - 512 // m      # both ends covered
+        assert max(np.diff(pre)) <= 2 * 512 // m                    # no gap above twice the stride
+    a = np.array([0.0, 0.0, 0.0, 1.0, 1.0, 2.0, 3.0])
+    b = a.copy()
+    b[4] += 1e-5
+    dt, dr = bench.pose_diff(a, b)
+    assert abs(dt - 1e-5) < 1e-12 and dr == 0.0
+    c = a.copy()
+    c[:4] = -c[:4]                                                  # q and -q are the same rotation
+    assert bench.pose_diff(a, c) == (0.0, 0.0)

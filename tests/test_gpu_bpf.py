@@ -1,5 +1,6 @@
 """GPU: Odom_BPF_EstimationClass (src/odomEstimationClass.cpp:649-1306) through the C ABI against the
-oracle in GPU_EQUIV mode. Beam / pillar / facade inputs come from pfsynth.bpf_split (a deterministic
+oracle with the device's default sort order (libstdc++ std::sort's order of equal keys, the reference
+tie order) and its normal-equation LM step (opts = LM_NORMAL_EQ). Beam / pillar / facade inputs come from pfsynth.bpf_split (a deterministic
 stand-in for the reference's PCA classifier, which is outside this path: SURVEY §8(f) rank 3).
 
 Tolerances as for the ES estimator (BASELINE.json north_star): pose within 1e-4 m / 1e-5 rad per
@@ -21,7 +22,7 @@ def _pair(pa, pfref, map_res=0.4, k_new=0, theta_p=0.4, theta_max=75, wt=0):
     od = pa.Odom_BPF_EstimationClass(device=0)
     od.init(pa.make_lidar(64, 3.0, 90.0), map_res, k_new, theta_p, theta_max, wt)
     orc = pfref.OdomBPF(pfref.make_lidar(64, 3.0, 90.0), map_res, k_new, theta_p, theta_max, wt,
-                        opts=pfref.GPU_EQUIV)
+                        opts=pfref.LM_NORMAL_EQ)
     return od, orc
 
 
@@ -125,7 +126,7 @@ def test_bpf_scan_pipeline(pa, pfref, pfsynth):
     clouds = [_front_clouds(pfref, x) for x in scans]
     host = pa.Odom_BPF_EstimationClass(device=0)
     host.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
-    orc = pfref.OdomBPF(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=pfref.GPU_EQUIV)
+    orc = pfref.OdomBPF(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=pfref.LM_NORMAL_EQ)
     poses_h = []
     for k, cl in enumerate(clouds):
         if k == 0:

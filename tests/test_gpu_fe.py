@@ -1,8 +1,9 @@
 """GPU: LaserProcessingClass::featureExtraction (src/laserProcessingClass.cpp:10-209) through
 pf_fe_extract, bit-exact against the oracle.
 
-Order and bits of every edge / surf point must equal the oracle with FE_STABLE_TIES (equal
-curvatures ordered by index; std::sort leaves that order unspecified)."""
+Order and bits of every edge / surf point must equal the oracle: in the library's default order (the
+reference's: equal curvatures in a sector as libstdc++'s std::sort leaves them) against opts=0, in the
+stable order (pf_fe_set_tie_order off: equal curvatures by index) against FE_STABLE_TIES."""
 import ctypes
 
 import numpy as np
@@ -11,14 +12,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _fe(pa, lines, mn=3.0, mx=90.0):
-    fe = pa.LaserProcessingClass(device=0)
+def _fe(pa, lines, mn=3.0, mx=90.0, order="tie"):
+    fe = pa.LaserProcessingClass(device=0, tie_order=None if order == "tie" else False)
     fe.init(pa.make_lidar(lines, mn, mx))
     return fe
 
 
-def _ref(pfref, x, lines, mn=3.0, mx=90.0):
-    return pfref.feature_extraction(x, pfref.make_lidar(lines, mn, mx), opts=pfref.FE_STABLE_TIES)
+def _ref(pfref, x, lines, mn=3.0, mx=90.0, order="tie"):
+    return pfref.feature_extraction(x, pfref.make_lidar(lines, mn, mx),
+                                    opts=0 if order == "tie" else pfref.FE_STABLE_TIES)
 
 
 def _same(a, b):
@@ -84,8 +86,9 @@ def test_fe_empty_and_tiny(pa, pfref):
     _same(gs, rs_)
 
 
-def test_fe_random_cloud_with_ties(pa, pfref):
-    """Quantised coordinates: many equal curvatures, exercising the stable tie order."""
+@pytest.mark.parametrize("order", ["tie", "stable"])
+def test_fe_random_cloud_with_ties(pa, pfref, order):
+    """Quantised coordinates: many equal curvatures, exercising both tie orders."""
     rng = np.random.default_rng(4)
     n = 60000
     az = rng.uniform(-np.pi, np.pi, n)
@@ -96,9 +99,9 @@ def test_fe_random_cloud_with_ties(pa, pfref):
     x[:, 1] = r * np.cos(el) * np.sin(az)
     x[:, 2] = r * np.sin(el)
     x[:, 3] = rng.uniform(0, 1, n)
-    fe = _fe(pa, 64)
+    fe = _fe(pa, 64, order=order)
     ge, gs = fe.featureExtraction(x)
-    re_, rs_ = _ref(pfref, x, 64)
+    re_, rs_ = _ref(pfref, x, 64, order=order)
     _same(ge, re_)
     _same(gs, rs_)
 
@@ -112,11 +115,11 @@ def test_fe_capacity_error(pa):
 
 
 def test_fe_golden(pa, pfsynth):
-    """Against the committed oracle vectors (tests/golden/fe_s32_f3.npz)."""
+    """Against the committed oracle vectors (tests/golden/fe_s32_f3.npz, FE_STABLE_TIES)."""
     import os
     g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fe_s32_f3.npz"))
     x = pfsynth.Sequence("S32", n_frames=6, az_steps=600).frame(3)
-    fe = _fe(pa, 32)
+    fe = _fe(pa, 32, order="stable")
     e, s = fe.featureExtraction(x)
     _same(e, g["edge"])
     _same(s, g["surf"])
@@ -135,7 +138,7 @@ def test_fe_s128_linear_ring_model(pa, pfref, pfsynth):
         fe.init(pa.make_lidar(128, 3.0, 90.0, ring_model=model))
         ge, gs = fe.featureExtraction(x)
         re_, rs_ = pfref.feature_extraction(x, pfref.make_lidar(128, 3.0, 90.0, ring_model=model),
-                                            opts=pfref.FE_STABLE_TIES)
+                                            opts=0)
         _same(ge, re_)
         _same(gs, rs_)
         assert ge.shape[0] > (128 * 6 * 5 if model else 6 * 5)
@@ -177,10 +180,10 @@ def test_fe_tie_order_equal_curvatures(pa, pfref, pfsynth):
     order still equals FE_STABLE_TIES; the two orders differ on this scan, so the check has teeth."""
     x = _tie_scan(pfsynth)
     lid = pfref.make_lidar(64, 3.0, 90.0)
-    fe = _fe(pa, 64)
+    fe = _fe(pa, 64, order="stable")
     se, ss = fe.featureExtraction(x)
-    _same(se, _ref(pfref, x, 64)[0])
-    _same(ss, _ref(pfref, x, 64)[1])
+    _same(se, _ref(pfref, x, 64, order="stable")[0])
+    _same(ss, _ref(pfref, x, 64, order="stable")[1])
     fe.set_tie_order(True)
     te, ts = fe.featureExtraction(x)
     re_, rs_ = pfref.feature_extraction(x, lid, opts=0)

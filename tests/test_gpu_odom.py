@@ -1,5 +1,8 @@
 """GPU: Odom_ES_EstimationClass (src/odomEstimationClass.cpp:182-647) through the C ABI against the
-oracle in GPU_EQUIV mode (stable tie orders + normal-equation LM step).
+oracle. The handles run the library default, the reference tie order (std::sort's order of equal keys
+in VoxelGrid / rgbds / the sector sort), against the oracle with the same sort order and the device's
+normal-equation LM step (opts = LM_NORMAL_EQ); tests marked "stable" run the stable-sort mode
+(pf_odom_set_tie_order off) against GPU_EQUIV (stable tie orders + normal-equation LM).
 
 Tolerances (BASELINE.json north_star): pose within 1e-4 m / 1e-5 rad per frame. Integer work —
 down-sampled counts, residual counts, map sizes, ages / p-index bytes — must be identical. Map
@@ -20,10 +23,12 @@ COUNTS = ("n_edge_ds", "n_surf_ds", "n_edge_map", "n_surf_map", "n_edge_res", "n
           "n_surf_valid", "outer_iterations", "map_too_small")
 
 
-def _pair(pa, pfref, lines=64, map_res=0.4, k_new=0, theta_p=0.4, theta_max=75, wt=0, mn=3.0, mx=90.0):
-    od = pa.Odom_ES_EstimationClass(device=0)
+def _pair(pa, pfref, lines=64, map_res=0.4, k_new=0, theta_p=0.4, theta_max=75, wt=0, mn=3.0, mx=90.0, order="tie"):
+    tie = order == "tie"
+    od = pa.Odom_ES_EstimationClass(device=0, tie_order=None if tie else False)
     od.init(pa.make_lidar(lines, mn, mx), map_res, k_new, theta_p, theta_max, wt)
-    orc = pfref.Odom(pfref.make_lidar(lines, mn, mx), map_res, k_new, theta_p, theta_max, wt, opts=pfref.GPU_EQUIV)
+    orc = pfref.Odom(pfref.make_lidar(lines, mn, mx), map_res, k_new, theta_p, theta_max, wt,
+                     opts=pfref.LM_NORMAL_EQ if tie else pfref.GPU_EQUIV)
     return od, orc
 
 
@@ -53,10 +58,11 @@ def _run(od, orc, seq, frames, check_maps_every=0):
     return worst
 
 
-def test_pose_and_map_parity_kitti_config(pa, pfref, pfsynth):
+@pytest.mark.parametrize("order", ["tie", "stable"])
+def test_pose_and_map_parity_kitti_config(pa, pfref, pfsynth, order):
     """configs[1]: 64 lines, k_new 0, theta_p 0.4, theta_max 75, weightType 0, map_res 0.4."""
     seq = pfsynth.Sequence("S64", n_frames=60)
-    od, orc = _pair(pa, pfref)
+    od, orc = _pair(pa, pfref, order=order)
     worst = _run(od, orc, seq, range(40), check_maps_every=13)
     _compare_maps(od, orc)
     assert worst[0] < 1e-6 and worst[1] < 1e-7
@@ -268,9 +274,9 @@ def test_long_sequence_matches_oracle(pa, pfref, pfsynth):
     passing 90 degrees, every pose within the north-star tolerance of the oracle, |q| = 1."""
     n = 400
     seq = pfsynth.Sequence("S64", n_frames=n)
-    od = pa.Odom_ES_EstimationClass(device=0)
+    od = pa.Odom_ES_EstimationClass(device=0)           # the library default: reference tie order
     od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
-    orc = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=pfref.GPU_EQUIV)
+    orc = pfref.Odom(pfref.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0, opts=pfref.LM_NORMAL_EQ)
     ref = []
     for f0 in range(0, n, 100):
         buf, counts = seq.frames(f0, 100)
@@ -298,7 +304,7 @@ def _sha(a):
 
 
 def test_full_sequence_bench_path(pa, pfsynth):
-    """configs[1] end to end through bench.py's own path: all 4541 S64 seed-0 scans HBM-resident,
+    """Stable order. configs[1] end to end through bench.py's own path: all 4541 S64 seed-0 scans HBM-resident,
     pf_odom_frame_device per frame with hipGraph replay, no host round trip. Against the committed
     oracle trajectory (tests/golden/odom_s64_full.npz, GPU_EQUIV): every frame's pose within the
     north-star 1e-4 m / 1e-5 rad (the design target is bit-identity: the device's LM reduction tree
@@ -310,9 +316,9 @@ def test_full_sequence_bench_path(pa, pfsynth):
     names = [str(c) for c in g["count_names"]]
     seq = pfsynth.Sequence("S64", n_frames=n, seed=0)
     lid = pa.make_lidar(64, 3.0, 90.0)
-    bench_h = pa.Odom_ES_EstimationClass(device=0, max_points=300000, map_capacity=1 << 22)
+    bench_h = pa.Odom_ES_EstimationClass(device=0, max_points=300000, map_capacity=1 << 22, tie_order=False)
     bench_h.init(lid, 0.4, 0, 0.4, 75, 0)
-    count_h = pa.Odom_ES_EstimationClass(device=0, max_points=300000, map_capacity=1 << 22)
+    count_h = pa.Odom_ES_EstimationClass(device=0, max_points=300000, map_capacity=1 << 22, tie_order=False)
     count_h.init(lid, 0.4, 0, 0.4, 75, 0)
     checks = dict(zip((int(k) for k in g["input_frames"]), (str(h) for h in g["input_sha"])))
     bufs, bad_counts = [], []
@@ -355,12 +361,13 @@ def test_full_sequence_bench_path(pa, pfsynth):
 
 
 def test_golden_trajectory(pa):
-    """The device pipeline against the committed oracle trajectory (tests/golden/odom_s64_24f.npz)."""
+    """Stable order: the device pipeline against the committed GPU_EQUIV oracle trajectory
+    (tests/golden/odom_s64_24f.npz)."""
     import os
     import pfsynth
     g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "odom_s64_24f.npz"))
     seq = pfsynth.Sequence("S64", n_frames=30, az_steps=1000)
-    od = pa.Odom_ES_EstimationClass(device=0)
+    od = pa.Odom_ES_EstimationClass(device=0, tie_order=False)
     od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
     for k in range(24):
         p = od.frame_host(seq.frame(k))
@@ -486,9 +493,10 @@ def test_s128_odometry_with_2m_point_map(pa, pfref, pfsynth):
     128-line ring formula) and updatePointsToMap against a 2,000,000-point surf
     map seeded by pf_odom_set_map (voxel centroids of the dense synthetic block at the 0.8 m surf leaf,
     a fixed point of rgbds). FLOAM parameters (theta_p 0) keep the map at its size. Poses within the
-    tolerance and every count identical per frame; both maps compared at the end."""
+    tolerance and every count identical per frame; both maps compared at the end. Stable order (the
+    reference tie order at this size: tests/test_gpu_parity_synced.py::test_synced_parity_s128_2m_point_map_tie)."""
     seq = pfsynth.Sequence("S128", n_frames=16)
-    od = pa.Odom_ES_EstimationClass(device=0)
+    od = pa.Odom_ES_EstimationClass(device=0, tie_order=False)
     od.init(pa.make_lidar(128, 3.0, 90.0, ring_model=(15.0, -25.0)), 0.4, 0, 0.0, 0, 0)
     orc = pfref.Odom(pfref.make_lidar(128, 3.0, 90.0, ring_model=(15.0, -25.0)), 0.4, 0, 0.0, 0, 0,
                      opts=pfref.GPU_EQUIV)

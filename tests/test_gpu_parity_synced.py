@@ -46,8 +46,7 @@ def synced_run(pa, pfsynth, name, preset, n, theta, lines=64, seed=0, ring_model
     pool = ctx.Pool(_workers(), initializer=pw.init, initargs=(preset, n, seed, lid, ring_model, prm, 0))
     od = pa.Odom_ES_EstimationClass(device=0, max_points=300000, map_capacity=1 << 22)
     od.init(pa.make_lidar(*lid, ring_model=ring_model), *prm)
-    if tie_order:
-        od.set_tie_order(True)
+    od.set_tie_order(tie_order)
     seq = pfsynth.Sequence(preset, n_frames=n, seed=seed)
     report = dict(name=name, preset=preset, theta=list(theta), frames=0, worst_t=0.0, worst_r=0.0, worst_xyz=0.0,
                   xyz_bitexact_frames=0, pose_bad=[], count_bad=[], map_bad=[], tie_order=tie_order)
@@ -159,12 +158,28 @@ def test_synced_statistics_stable_order(pa, pfsynth, name, preset, n, theta, lin
     assert len(rep["count_bad"]) <= 0.05 * rep["frames"], len(rep["count_bad"])
 
 
-def test_synced_parity_s128_2m_point_map(pa, pfref, pfsynth):
-    """configs[4] as a pipeline: synthetic 128-line scans (~200k points, the linear beam-model
-    extension) against a 2,000,000-point surf map (voxel centroids of the dense block at the 0.8 m
-    leaf, seeded after frame 0), theta 0 so the map keeps its size; every frame synced."""
+def _seed_map_2m(pfref, pfsynth):
     m = pfref.rgbds(pfsynth.dense_map(7_000_000, seed=5), 0.8)[:2_000_000, :3]
-    seed_map = (np.ascontiguousarray(m), np.zeros((m.shape[0], 2), np.uint8))
+    return (np.ascontiguousarray(m), np.zeros((m.shape[0], 2), np.uint8))
+
+
+def test_synced_parity_s128_2m_point_map_tie(pa, pfref, pfsynth):
+    """configs[4] in the reference tie order, the mode bench.py runs it in: synthetic 128-line scans
+    (~200k points, the linear beam-model extension) against a 2,000,000-point surf map (voxel centroids of
+    the dense block at the 0.8 m leaf, seeded after frame 0), theta 0 so the map keeps its size; every
+    frame synced against the faithful oracle (opts=0), the strict bar: every count identical, both maps'
+    r / g bytes identical, pose and map coordinates within the tolerance. Each rgbds sort of the ~2M-point
+    voxel-ordered map plus the appended points reaches libstdc++'s depth limit on a ~820k-key segment and
+    runs the big partition levels and the heap tier's global path at their full size
+    (src/odomEstimationClass.cpp:74, 606-626)."""
+    rep = synced_run(pa, pfsynth, "configs4_S128_2M_tie", "S128", 13, (0.0, 0), lines=128,
+                     ring_model=(15.0, -25.0), seed_map=_seed_map_2m(pfref, pfsynth), tie_order=True)
+    _check(rep, 12)
+
+
+def test_synced_parity_s128_2m_point_map_stable(pa, pfref, pfsynth):
+    """configs[4] in the stable-sort mode, every frame synced: within the strict bar on these 12 frames
+    (round 3), although the stable mode does not meet it in general (test_synced_statistics_stable_order)."""
     rep = synced_run(pa, pfsynth, "configs4_S128_2M", "S128", 13, (0.0, 0), lines=128, ring_model=(15.0, -25.0),
-                     seed_map=seed_map)
+                     seed_map=_seed_map_2m(pfref, pfsynth), tie_order=False)
     _check(rep, 12)

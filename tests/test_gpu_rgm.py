@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 def _es_run(pa, pfsynth, preset, frames, radix, theta=(0.4, 75), lines=64, shuffle_at=None):
     seq = pfsynth.Sequence(preset, n_frames=frames, seed=0)
-    od = pa.Odom_ES_EstimationClass(device=0, max_points=300000, map_capacity=1 << 21)
+    od = pa.Odom_ES_EstimationClass(device=0, max_points=300000, map_capacity=1 << 21, tie_order=False)
     od.init(pa.make_lidar(lines, 3.0, 90.0), 0.4, 0, theta[0], theta[1], 0)
     od.set_rg_radix(radix)
     buf, cnt = seq.frames(0, frames, threads=16)
@@ -82,7 +82,7 @@ def test_merge_bpf_three_classes(pa, pfsynth):
     buf, cnt = seq.frames(0, 150, threads=16)
     out = []
     for radix in (False, True):
-        od = pa.Odom_BPF_EstimationClass(device=0)
+        od = pa.Odom_BPF_EstimationClass(device=0, tie_order=False)
         od.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
         od.set_rg_radix(radix)
         db = pa.DeviceBuffer(buf.nbytes)

@@ -50,6 +50,47 @@ def test_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
         assert int(lines[k].split()[20]) == cs
 
 
+def test_shim_default_is_reference_order_against_faithful_trajectory(pa, pfsynth, tmp_path):
+    """The drop-in as the unchanged ROS nodes build it -- shim classes with their default settings, driven
+    like src/laserProcessingNode.cpp:71-78 + src/odomEstimationNode copy.cpp:86-107 -- against the
+    reference-faithful oracle's own free run of the headline sequence (tests/golden/odom_s64_faithful.npz:
+    pfref opts=0, libstdc++ std::sort tie orders, Householder-QR LM, FLANN-style kd-tree): every frame's
+    pose within 1e-4 m / 1e-5 rad and both map sizes equal. The shims default to the reference tie order
+    (reference_tie_order = true, pf_odom_set_tie_order / pf_fe_set_tie_order), so no node change is needed
+    for the reference's results."""
+    import hashlib
+    from _util import pose_err
+    g = np.load(os.path.join(ROOT, "tests", "golden", "odom_s64_faithful.npz"))
+    n = 400
+    exe = str(tmp_path / "shim_driver")
+    lib = os.path.join(ROOT, "pfilter-noetic_amd")
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "shim", "shim_driver.cpp"), "-o", exe, "-L", lib,
+                           "-lpfilter_hip", "-Wl,-rpath," + lib, "-Wl,-rpath-link,/opt/rocm/lib"])
+    seq = pfsynth.Sequence("S64", n_frames=n, seed=0)
+    checks = dict(zip((int(k) for k in g["input_frames"]), (str(h) for h in g["input_sha"])))
+    with open(tmp_path / "frames.bin", "wb") as f:
+        for k in range(n):
+            x = np.ascontiguousarray(seq.frame(k), np.float32)
+            if k in checks:
+                assert hashlib.sha256(x.tobytes()).hexdigest() == checks[k], "generator changed at frame %d" % k
+            np.array([x.shape[0]], np.int64).tofile(f)
+            x.tofile(f)
+    subprocess.check_call([exe, str(tmp_path / "frames.bin"), str(tmp_path / "poses.txt")], timeout=600)
+    got = np.loadtxt(tmp_path / "poses.txt")
+    assert got.shape[0] == n
+    names = [str(c) for c in g["count_names"]]
+    ie, is_ = names.index("n_edge_map"), names.index("n_surf_map")
+    worst = 0.0
+    for k in range(n):
+        dt, dr = pose_err(got[k, :7], g["poses"][k])
+        worst = max(worst, dt)
+        assert dt < 1e-4 and dr < 1e-5, (k, dt, dr)
+        if k > 0:
+            assert (got[k, 7], got[k, 8]) == (g["counts"][k][ie], g["counts"][k][is_]), k
+    print("shim (default settings) vs faithful oracle: %d frames, worst %.3e m" % (n, worst))
+
+
 def test_bpf_shim_matches_python_binding(pa, pfref, pfsynth, tmp_path):
     """Odom_BPF_EstimationClass drop-in (shim) driven like src/odomEstimationNode.cpp:254-264."""
     exe = str(tmp_path / "shim_bpf_driver")
