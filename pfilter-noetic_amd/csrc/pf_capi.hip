@@ -1348,6 +1348,8 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
         if (int rc = tie_alloc(*o.tie_a, (size_t)o.cls.nc * o.in_cap)) return rc;
         if (int rc = tie_alloc(*o.tie_b, o.sort_cap)) return rc;
     }
+    if (enable)
+        if (int rc = odom_dep_alloc(o)) return rc;
     if ((enable != 0) != o.tie_order) {             // both stages' captured kernel sequences change
         for (int s = 0; s < kSlots; ++s)
             for (hipGraphExec_t* g : {&o.graph_a[s], &o.graph_as[s]})

@@ -264,7 +264,17 @@ struct OdomGPU {
     TieSort* tie_a = nullptr;
     TieSort* tie_b = nullptr;
     size_t tie_hint = 0;                        // largest class an rgbds tie sort may see (pf_odom_set_map)
+    // rgbds voxel groups whose f32 centroid does not depend on the order of their points (pf_odom.hip
+    // k_rg_dep): an open-addressing table key -> {count, first three elements}, empty between updates
+    u32* dep_key = nullptr;        // [dep_h] voxel key, 0xFFFFFFFF = empty
+    u32* dep_cnt = nullptr;        // [dep_h] elements with that key
+    u32* dep_mem = nullptr;        // [3 * dep_h] the first three elements
+    u32* dep_slot = nullptr;       // [sort_cap] each element's slot (0xFFFFFFFF: cropped)
+    u8* dep_free = nullptr;        // [sort_cap] 1 = the element's group is order-free
+    u32 dep_hbits = 0;             // dep_h = 1 << dep_hbits
 };
+// the dependence table of the tie-order rgbds (allocated with the tie sorts, pf_odom_set_tie_order)
+int odom_dep_alloc(OdomGPU& o);
 
 // Stage A keeps off the last CUs of the device by default: with one sequence per GPU, stage B's LM
 // (kLmBlocks co-resident workgroups) otherwise waits for stage A's waves to drain. Measured on one

@@ -1800,11 +1800,84 @@ __global__ void __launch_bounds__(256) k_rg_append_minmax(DevState* __restrict__
     minmax_commit(v, acc + A_RG, nc);
 }
 
+// ---- order-free voxel groups of the tie-order rgbds (the heap tier's dependence flags, pf_tie.h) ----
+// The reference sums a voxel's points in the order std::sort leaves them (:108-125), so the tie order is
+// observable only through groups whose f32 sum depends on that order: a group of one or two points is
+// order-free (0 + a is exact and + commutes), a group of three is order-free when its three left folds
+// ((0 + a) + b) + c, ((0 + a) + c) + b and ((0 + b) + c) + a agree bit for bit in x, y and z (the first two
+// terms commute), and a larger group counts as order-dependent. The key kernels insert every element into
+// an open-addressing table (key -> count and the first three elements); k_rg_dep lets the first element of
+// every group decide it, marks its members and empties the slot for the next update.
+struct DepTab {
+    u32* key;
+    u32* cnt;
+    u32* mem;
+    u32* slot;
+    u8* freef;
+    u32 hbits;
+};
+constexpr u32 kDepEmpty = 0xFFFFFFFFu;
+
+__device__ __forceinline__ void dep_insert(const DepTab& T, u32 key, u32 e) {
+    if (!T.key) return;
+    if (key == kSentinel) {                        // cropped: in no voxel
+        T.slot[e] = kDepEmpty;
+        T.freef[e] = 1;
+        return;
+    }
+    const u32 mask = (1u << T.hbits) - 1u;
+    u32 sl = (key * 0x9E3779B1u) >> (32u - T.hbits);
+    for (;;) {
+        const u32 old = atomicCAS(&T.key[sl], kDepEmpty, key);
+        if (old == kDepEmpty || old == key) break;
+        sl = (sl + 1u) & mask;
+    }
+    const u32 c = atomicAdd(&T.cnt[sl], 1u);
+    if (c < 3u) T.mem[3u * sl + c] = e;
+    T.slot[e] = sl;
+    T.freef[e] = 0;
+}
+
+__device__ __forceinline__ bool folds_agree(float4 a, float4 b, float4 c) {
+    const float A[3] = {a.x, a.y, a.z}, B[3] = {b.x, b.y, b.z}, C[3] = {c.x, c.y, c.z};
+    bool same = true;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const float f1 = ((0.f + A[d]) + B[d]) + C[d];
+        const float f2 = ((0.f + A[d]) + C[d]) + B[d];
+        const float f3 = ((0.f + B[d]) + C[d]) + A[d];
+        same = same && __float_as_uint(f1) == __float_as_uint(f2) && __float_as_uint(f1) == __float_as_uint(f3);
+    }
+    return same;
+}
+
+template <int NC>
+__global__ void __launch_bounds__(256) k_rg_dep(const int* __restrict__ cnt, Clouds map, Clouds app, DepTab T) {
+    const RgView<NC> V = rg_view<NC>(cnt, map, app);
+    const int n = V.total();
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        const u32 sl = T.slot[e];
+        if (sl == kDepEmpty || T.mem[3u * sl] != (u32)e) continue;   // only the group's first element
+        const u32 c = T.cnt[sl];
+        bool fre = c <= 2u;
+        if (c == 3u) {
+            int cc;
+            const float4 a = V.at((int)T.mem[3u * sl], cc), b = V.at((int)T.mem[3u * sl + 1u], cc),
+                         d = V.at((int)T.mem[3u * sl + 2u], cc);
+            fre = folds_agree(a, b, d);
+        }
+        if (fre)
+            for (u32 j = 0; j < c; ++j) T.freef[T.mem[3u * sl + j]] = 1;
+        T.key[sl] = kDepEmpty;
+        T.cnt[sl] = 0u;
+    }
+}
+
 template <int NC>
 __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st, const int* __restrict__ cnt,
                                                   const u32* __restrict__ acc, Clouds map, Clouds app,
                                                   VgLeaf leaf, u32* __restrict__ keys, u32* __restrict__ vals,
-                                                  SortHist sh) {
+                                                  SortHist sh, DepTab dt) {
     __shared__ u32 lh[4][256];
     sort_hist_begin(lh);
     const RgView<NC> V = rg_view<NC>(cnt, map, app);
@@ -1816,6 +1889,7 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
         if (!in_crop(st, p)) {
             keys[i] = kSentinel;
             sort_hist_add(lh, kSentinel, sh.passes);
+            dep_insert(dt, kSentinel, (u32)i);
             continue;
         }
         const float lf = leaf.at(c);
@@ -1831,6 +1905,7 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
         const int idx = i0 * 1 + i1 * div[0] + i2 * (div[0] * div[1]);
         keys[i] = ((u32)idx & 0x3fffffffu) | ((u32)c << 30);
         sort_hist_add(lh, keys[i], sh.passes);
+        dep_insert(dt, keys[i], (u32)i);
     }
     sort_hist_end(lh, sh, n, n);
 }
@@ -1848,7 +1923,7 @@ __global__ void __launch_bounds__(256) k_rg_append_keys(DevState* __restrict__ s
                                                          u32* __restrict__ acc, Clouds map, Clouds ds, CloudsW app,
                                                          double* __restrict__ poses, int pose_cap, VgLeaf leaf,
                                                          u32* __restrict__ keys, u32* __restrict__ vals,
-                                                         SortHist sh) {
+                                                         SortHist sh, DepTab dt) {
     double prm[7];
     for (int k = 0; k < 7; ++k) prm[k] = st->params[k];
     if (blockIdx.x == gridDim.x - 1) {
@@ -1892,6 +1967,7 @@ __global__ void __launch_bounds__(256) k_rg_append_keys(DevState* __restrict__ s
         }
         keys[i] = key;
         sort_hist_add(lh, key, sh.passes);
+        dep_insert(dt, key, (u32)i);
     }
     const int items = n < nblk * 256 ? n : nblk * 256;  // blocks holding keys: the first ceil(items / 256)
     sort_hist_end(lh, sh, n, items);
@@ -3032,6 +3108,23 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
 
 // back to the state after init (identity pose, empty maps, optimization_count 2), keeping every
 // allocation and captured graph: the next frame seeds the maps again
+// the table holds every element of one rgbds call (at most sort_cap) at a load of at most 0.8
+int odom_dep_alloc(OdomGPU& o) {
+    if (o.dep_key) return PF_OK;
+    u32 hb = 10;
+    while (((size_t)1 << hb) < o.sort_cap + o.sort_cap / 4) ++hb;
+    const size_t h = (size_t)1 << hb;
+    if (hipMalloc(&o.dep_key, sizeof(u32) * h) != hipSuccess || hipMalloc(&o.dep_cnt, sizeof(u32) * h) != hipSuccess ||
+        hipMalloc(&o.dep_mem, sizeof(u32) * 3 * h) != hipSuccess ||
+        hipMalloc(&o.dep_slot, sizeof(u32) * o.sort_cap) != hipSuccess ||
+        hipMalloc(&o.dep_free, o.sort_cap) != hipSuccess)
+        return PF_ENOMEM;
+    if (hipMemset(o.dep_key, 0xFF, sizeof(u32) * h) != hipSuccess || hipMemset(o.dep_cnt, 0, sizeof(u32) * h) != hipSuccess)
+        return PF_EHIP;
+    o.dep_hbits = hb;
+    return PF_OK;
+}
+
 int odom_reset(OdomGPU& o) {
     if (odom_sync_a(o) != hipSuccess || hipStreamSynchronize(o.stream) != hipSuccess) return PF_EHIP;
     DevState h{};
@@ -3135,6 +3228,8 @@ void odom_destroy(OdomGPU& o) {
             tie_free(*t);
             delete t;
         }
+    for (void* q : {(void*)o.dep_key, (void*)o.dep_cnt, (void*)o.dep_mem, (void*)o.dep_slot, (void*)o.dep_free})
+        (void)hipFree(q);
     o = OdomGPU{};
 }
 
@@ -3249,19 +3344,23 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
         return;
     }
     o.dims_fresh = false;
+    // the order-free voxel groups (the heap tier's dependence flags) in the tie order
+    const DepTab dt{o.tie_order ? o.dep_key : nullptr, o.dep_cnt, o.dep_mem, o.dep_slot, o.dep_free, o.dep_hbits};
     if (rg_fused_keys(o.leaf_rg, nc)) {
         PF_LAUNCH_NC(nc, k_rg_append_keys, dim3(kGrid + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(map_cur(o)),
                      clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap, leaf, o.keys, o.vals,
-                     sort_hist(o.prim, 32, true));
+                     sort_hist(o.prim, 32, true), dt);
     } else {
         PF_LAUNCH_NC(nc, k_rg_append_minmax, dim3(256 + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(map_cur(o)),
                      clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap);
         PF_LAUNCH_NC(nc, k_rg_keys, dim3(kGrid), dim3(256), 0, s, o.st, cnt, o.acc, clouds(map_cur(o)), clouds(o.app),
-                     leaf, o.keys, o.vals, sort_hist(o.prim, 32, true));
+                     leaf, o.keys, o.vals, sort_hist(o.prim, 32, true), dt);
     }
-    if (o.tie_order)                       // std::sort's order of equal keys (:74)
+    if (o.tie_order) {                     // std::sort's order of equal keys (:74)
+        if (dt.key) PF_LAUNCH_NC(nc, k_rg_dep, dim3(kGrid), dim3(256), 0, s, cnt, clouds(map_cur(o)), clouds(o.app), dt);
         tie_sort(*o.tie_b, o.keys, o.vals, TieClasses{cnt, C_M, C_DS, nc}, o.prim.err, s,
-                 std::max(tie_levels_for(*o.tie_b, o.tie_hint), PF_TIE_LEVELS_B));
+                 std::max(tie_levels_for(*o.tie_b, o.tie_hint), PF_TIE_LEVELS_B), dt.key ? o.dep_free : nullptr);
+    }
     else
         radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
     RgTailArgs ta{cnt, clouds(map_cur(o)), clouds(o.app), o.keys, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,

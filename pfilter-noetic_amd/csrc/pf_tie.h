@@ -45,6 +45,8 @@
 
 namespace pf {
 
+typedef unsigned char u8;
+
 #ifndef PF_TIE_MED
 #define PF_TIE_MED 65536
 #endif
@@ -89,8 +91,11 @@ int tie_levels_for(const TieSort& t, size_t size_hint);
 // vals too). Replaces a stable radix sort of the same pairs. levels: big levels to run first (0: every
 // class goes straight to its medium workgroup, which handles any size, slowly above kTieMed). A
 // look-back wait that gives up sets bit 2 of *err (the caller's sticky error word), a list overflow
-// bit 4.
-void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s, int levels = 0);
+// bit 4. freef (optional, indexed by val): nonzero when the element's voxel group is order-free (its f32
+// centroid sum does not depend on the order of its points; pf_odom.hip k_rg_dep): the heap tier then
+// runs only the pops the order-dependent groups need. NULL: every group counts as order-dependent.
+void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s, int levels = 0,
+              const u8* freef = nullptr);
 const int* tie_valid_count(const TieSort& t);   // device word: the valid pairs of the last sort
 
 }  // namespace pf

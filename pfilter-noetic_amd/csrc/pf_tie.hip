@@ -1523,11 +1523,11 @@ struct HeapPops {
     uint2 vk;             // its value
 };
 template <bool MAY, class M>
-__device__ __forceinline__ void heap_step(const M& H2, HeapPops& P, int npops, int l, int spare) {
+__device__ __forceinline__ void heap_step(const M& H2, HeapPops& P, int npops, int l, int spare, int last) {
     bool start = false, mine = false;
     int q = 0;
     if (MAY) {
-        q = npops - P.nxt;                                    // the last element of the heap before pop nxt
+        q = last - P.nxt;                                     // the last element of the heap before pop nxt
         const int sh = hlev(q) - hlev(P.h);
         const bool blk = P.act && sh >= 0 && ((q + 1) >> sh) == P.h + 1;   // hole h is q or an ancestor
         start = P.nxt < npops && __ballot(blk) == 0;
@@ -1558,7 +1558,7 @@ __device__ __forceinline__ void heap_step(const M& H2, HeapPops& P, int npops, i
 // __make_heap (every thread) then __sort_heap (wave 0) on the n entries of H; spare: the index of lane
 // 0's spare slot (lane l writes spare + l); jb: the job's index (the prof build records job 0)
 template <class M>
-__device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int jb) {
+__device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int jb, int npops_in = -1) {
     const int t = threadIdx.x, l = lane_id();
     TIE_PROF(960, rt_now());
     TIE_PROF(965, __builtin_amdgcn_s_memtime());
@@ -1596,10 +1596,10 @@ __device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int
     [[maybe_unused]] unsigned long long steps = 0;
     if (t < 64) {
         HeapPops P{0, false, 0, 0, make_uint2(0u, 0u)};
-        const int npops = n - 1;
+        const int npops = npops_in < 0 ? n - 1 : npops_in;
         for (;;) {
-            heap_step<true>(H, P, npops, l, spare + l);
-            heap_step<false>(H, P, npops, l, spare + l);
+            heap_step<true>(H, P, npops, l, spare + l, n - 1);
+            heap_step<false>(H, P, npops, l, spare + l, n - 1);
 #ifdef PF_TIE_PROF
             steps += 2;
 #endif
@@ -1697,12 +1697,7 @@ __device__ __forceinline__ void copy_batched(int n, const Ld& load, const St& st
             if (i0 + u * kHeapT < n) store(i0 + u * kHeapT, v[u]);
     }
 }
-// true when two neighbours of the sorted S[0, n) / G[0, n) hold the same key
-__device__ bool lds_has_equal(const uint2* S, int n) {
-    int eq = 0;
-    for (int i = threadIdx.x + 1; i < n; i += kHeapT) eq |= S[i].y == S[i - 1].y;
-    return __syncthreads_or(eq) != 0;
-}
+// true when two neighbours of the sorted G[0, n) hold the same key
 __device__ bool glb_has_equal(const GlbHeap& G, int n) {
     int eq = 0;
     copy_batched<PF_HEAP_U>(n - 1, [&](int i) { return make_uint2(G.ld(i).y, G.ld(i + 1).y); },
@@ -1732,9 +1727,66 @@ __device__ void glb_bitonic(const GlbHeap& G, uint2* S, int n) {
     }
 }
 
+// ---- which pops are needed: the dependence flags (TieSort::free) ----------------------------------------
+// Only the order of a voxel group whose f32 centroid sum depends on the order of its points is observable
+// (a group of <= 2 points is order-free: 0 + a is exact and + commutes; of 3, when its three left folds
+// agree; pf_odom.hip k_rg_dep). Pops run from the largest key down, so once the smallest key of an
+// order-dependent group in the segment has been popped (P = the elements with a key >= it), the rest of
+// the heap holds only order-free groups and any sort finishes it; a segment with no order-dependent
+// group is the sorted copy itself. Without flags (the VoxelGrid sort, the tests of the permutation) an
+// element counts as order-dependent when its key has an equal neighbour: the exact std::sort permutation.
+// (A leaner pop engine on 32-bit rank words -- one 8-byte read per step, the ancestor test only on
+// steps that may start a pop -- measured 0.48 us per pop against the pair engine's 0.39: a step is
+// bound by the wave's VALU issue, about 350-460 cycles, not by the LDS round trip)
+// One depth-limit segment [off, off + n), n <= kHeapCap, in LDS as {val, key} entries: the sorted copy
+// decides the pops, then the segment is restored and heap-sorted that far (heap_sort_seg)
+__device__ void heap_segment_pairs(u32* __restrict__ keys, u32* __restrict__ vals, const u8* __restrict__ freef,
+                                   int off, int n, uint2* H, int jb) {
+    __shared__ u32 s_kmin2, s_pops2;
+    const int t = threadIdx.x;
+    for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);
+    if (t == 0) {
+        s_kmin2 = 0xFFFFFFFFu;
+        s_pops2 = 0u;
+    }
+    __syncthreads();
+    const int P2 = pow2_ceil(n);
+    lds_bitonic(H, n, P2, 2, P2, 0);
+    u32 kmin = 0xFFFFFFFFu;
+    for (int i = t; i < n; i += kHeapT) {
+        const u32 k = H[i].y;
+        const bool dep = freef ? !freef[H[i].x] : ((i > 0 && H[i - 1].y == k) || (i + 1 < n && H[i + 1].y == k));
+        if (dep) kmin = min(kmin, k);
+    }
+    kmin = wave_min_u32(kmin);
+    if (lane_id() == 0) atomicMin(&s_kmin2, kmin);
+    __syncthreads();
+    kmin = s_kmin2;
+    if (kmin != 0xFFFFFFFFu) {
+        for (int i = t; i < n; i += kHeapT)
+            if (H[i].y == kmin && (i == 0 || H[i - 1].y != kmin)) s_pops2 = (u32)(n - i);
+        __syncthreads();
+        const int popsneed = (int)s_pops2;
+        for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);   // restore
+        __syncthreads();
+        const int npops = popsneed >= n ? n - 1 : popsneed;
+        heap_sort_seg(LdsHeap{H}, n, kHeapCap, jb, npops);
+        if (npops < n - 1) {
+            const int r = n - npops, Pr = pow2_ceil(r);
+            lds_bitonic(H, r, Pr, 2, Pr, 0);                // the rest: order-free groups only
+        }
+    }
+    for (int i = t; i < n; i += kHeapT) {
+        const uint2 x = H[i];
+        keys[off + i] = x.y;
+        vals[off + i] = x.x;
+    }
+}
+
 __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32* __restrict__ vals, int* ctl,
                                                      const int2* __restrict__ segs, u64* __restrict__ big,
-                                                     int bigcap, u32* __restrict__ arrive) {
+                                                     int bigcap, u32* __restrict__ arrive,
+                                                     const u8* __restrict__ freef) {
     __shared__ uint2 H[kHeapCap + 64];             // + a spare slot per lane of wave 0
     const int t = threadIdx.x;
     const int nh = ctl[T_NHEAP];
@@ -1742,27 +1794,25 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
         const int2 sg = segs[jb];
         const int off = sg.x, n = sg.y;
         if (n <= kHeapCap) {
-            for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);
-            __syncthreads();
-            const int P = pow2_ceil(n);
-            lds_bitonic(H, n, P, 2, P, 0);
-            if (lds_has_equal(H, n)) {                        // restore, then the heap sort
-                for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);
-                __syncthreads();
-                heap_sort_seg(LdsHeap{H}, n, kHeapCap, jb);
-            }
-            for (int i = t; i < n; i += kHeapT) {
-                const uint2 x = H[i];
-                keys[off + i] = x.y;
-                vals[off + i] = x.x;
-            }
+            heap_segment_pairs(keys, vals, freef, off, n, H, jb);
         } else {                                              // the copy at the segment's own offset
             GlbHeap G{big + off};
             copy_batched<PF_HEAP_U>(n, [&](int i) { return make_uint2(vals[off + i], keys[off + i]); },
                             [&](int i, uint2 v) { G.st(i, v); });
             __syncthreads();
             glb_bitonic(G, H, n);
-            if (glb_has_equal(G, n)) {
+            // the sorted copy is the result when no two neighbours are equal or, with the dependence
+            // flags, when no element belongs to an order-dependent group
+            bool need;
+            if (freef) {
+                int dep = 0;
+                copy_batched<PF_HEAP_U>(n, [&](int i) { return G.ld(i); },
+                                        [&](int, uint2 v) { dep |= freef[v.x] ? 0 : 1; });
+                need = __syncthreads_or(dep) != 0;
+            } else {
+                need = glb_has_equal(G, n);
+            }
+            if (need) {
                 for (int i = t; i < n; i += kHeapT) G.st(i, make_uint2(vals[off + i], keys[off + i]));
                 __syncthreads();
                 heap_sort_seg(G, n, bigcap - off, jb);        // spares: big[bigcap .. bigcap + 64)
@@ -1841,7 +1891,8 @@ int tie_levels_for(const TieSort& t, size_t size_hint) {
     return lv;
 }
 
-void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s, int levels) {
+void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s, int levels,
+              const u8* freef) {
     if (levels > t.max_levels) levels = t.max_levels;
     if (levels <= 0) {
         hipLaunchKernelGGL(k_tie_medium, dim3(kMaxTieC), dim3(kMT), 0, s, keys, vals, cls, 1, t.depth0, t.k, t.v,
@@ -1866,7 +1917,7 @@ void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStr
     hipLaunchKernelGGL(k_tie_local, dim3(kLocalGrid), dim3(1024), 0, s, t.k, t.v, t.jobs, t.ctl, t.arrive + 2, keys,
                        vals, cls, HeapList{t.heaps, t.hcap, err});
     hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heaps, t.hbig,
-                       (int)t.cap, t.arrive + 3);
+                       (int)t.cap, t.arrive + 3, freef);
 }
 
 const int* tie_valid_count(const TieSort& t) { return t.ctl + T_VALID; }

@@ -33,8 +33,10 @@ def make_heap(H, n):
             H[h] = vk
 
 
-def pipelined_sort_heap(H, n):
-    npops = n - 1
+def pipelined_sort_heap(H, n, npops=None):
+    """the first npops pops (default all, n - 1) of __sort_heap as heap_step schedules them"""
+    last = n - 1
+    npops = last if npops is None else npops
     act = [0] * NL
     h = [0] * NL
     m = [0] * NL
@@ -51,7 +53,7 @@ def pipelined_sort_heap(H, n):
                 reads[i] = (c1, H[c1] if c1 < m[i] else None, H[c1 + 1] if c1 + 1 < m[i] else None)
         start = None
         if may and nxt < npops:
-            q = npops - nxt
+            q = last - nxt
             blk = False
             for i in range(NL):
                 if act[i]:
@@ -189,3 +191,69 @@ def test_bitonic_network_equals_heap_sort_on_distinct_keys(pfref):
                 _glb_bitonic(G, n, C)
             got = np.array([v for _, v in G], np.uint32)
             np.testing.assert_array_equal(got, pfref.sort_perm(keys, "literal", 0), err_msg="n=%d C=%d" % (n, C))
+
+
+
+
+# ---- k_tie_heap's pops with the dependence flags (pf_tie.hip heap_segment_pairs) ----------------------
+# Only the pops down to the smallest key with an order-dependent element run; the rest of the heap is
+# sorted by any order. Without flags every key with an equal neighbour counts (the exact permutation).
+def segment_perm(keys, dep=None):
+    n = keys.size
+    sk = np.sort(keys)
+    if dep is None:
+        depk = [k for i, k in enumerate(sk) if (i > 0 and sk[i - 1] == k) or (i + 1 < n and sk[i + 1] == k)]
+    else:
+        depk = [int(keys[i]) for i in range(n) if dep[i]]
+    if not depk:
+        return np.argsort(keys, kind="stable").astype(np.uint32), 0
+    kmin = min(depk)
+    popsneed = int(np.sum(keys >= kmin))
+    H = [(int(k), i) for i, k in enumerate(keys)]
+    make_heap(H, n)
+    npops = n - 1 if popsneed >= n else popsneed
+    pipelined_sort_heap(H, n, npops)
+    if npops < n - 1:
+        H[:n - npops] = sorted(H[:n - npops])
+    return np.array([v for _, v in H], np.uint32), npops
+
+
+def test_early_termination_without_flags_is_libstdcxx(pfref):
+    """without dependence flags every tie counts: the exact std::sort permutation of a depth-0 introsort,
+    with the pops stopped below the smallest key that has an equal neighbour"""
+    rng = np.random.default_rng(41)
+    for trial in range(50):
+        n = int(rng.choice([17, 18, 31, 64, 65, 100, 257, 500, 1200]))
+        span = int(rng.choice([2, 5, 40, 1000, 1 << 30]))
+        keys = rng.integers(0, span, n).astype(np.uint32)
+        if trial % 5 == 0:
+            keys = np.sort(keys)
+        elif trial % 5 == 1:
+            keys = np.sort(keys)[::-1].copy()
+        got, _ = segment_perm(keys)
+        np.testing.assert_array_equal(got, pfref.sort_perm(keys, "literal", 0),
+                                      err_msg="trial %d n=%d span=%d" % (trial, n, span))
+
+
+def test_early_termination_with_dependence_flags(pfref):
+    """with flags: the order of every flagged group's elements is libstdc++'s, every key in order;
+    unflagged groups may come in any order. Pops stop after the smallest flagged key (rgbds-like
+    inputs: a sorted run with unsorted keys appended)."""
+    rng = np.random.default_rng(42)
+    saved = 0
+    for trial in range(40):
+        n = int(rng.choice([40, 300, 1500]))
+        keys = np.sort(rng.integers(0, n, n).astype(np.uint32))
+        keys = np.concatenate([keys[: n * 3 // 4], rng.permutation(keys[n * 3 // 4:])]).astype(np.uint32)
+        groups = {}
+        for i, k in enumerate(keys):
+            groups.setdefault(int(k), []).append(i)
+        flagged = {k for k, g in groups.items() if len(g) >= 3 and rng.random() < 0.3}
+        dep = np.array([int(k) in flagged for k in keys])
+        got, npops = segment_perm(keys, dep)
+        saved += n - 1 - npops
+        want = pfref.sort_perm(keys, "literal", 0)
+        np.testing.assert_array_equal(keys[got], keys[want])                  # keys in order
+        for k in flagged:                                                    # flagged groups: exact
+            np.testing.assert_array_equal([i for i in got if keys[i] == k], [i for i in want if keys[i] == k])
+    assert saved > 0
