@@ -16,7 +16,10 @@ from collections import defaultdict
 
 # every kernel of the frame path: stage A (featureExtraction + VoxelGrid) and stage B (odometry)
 STAGE_B = ["k_grid_bounds", "k_grid_count", "k_grid_scan", "k_grid_scatter", "k_assoc", "k_observe", "k_lm_solve",
-           "k_rgm_bucket", "k_rgm_finish", "k_rg_append_keys", "k_rg_tail", "k_rg_write"]
+           "k_rgm_bucket", "k_rgm_finish", "k_rg_append_keys", "k_rg_tail", "k_rg_write", "k_rg_dep"]
+# the tie-order sort's kernels run in both stages (VoxelGrid in A, rgbds in B): their means mix the two
+BOTH = ["k_tie_medium", "k_tie_mid", "k_tie_local", "k_tie_heap", "k_tie_compact", "k_tie_setup", "k_tie_scan",
+        "k_tie_split"]
 
 
 def short(name):
@@ -29,6 +32,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--source", default="rocprofv3 --pmc passes (tools/frame_pmc.sh) over bench.py --steps 100 "
+                                        "--no-graph (configs[1], S64)")
     a = ap.parse_args()
     acc = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(a.root + "/**/*counter_collection.csv", recursive=True):
@@ -37,16 +42,19 @@ def main():
             if k:
                 # one row per (dispatch, counter): sum over the per-XCD / per-SE dimension rows of a dispatch
                 acc[k][(row["Counter_Name"], row.get("Dispatch_Id", ""))].append(float(row["Counter_Value"]))
-    out = {"source": "rocprofv3 --pmc passes (tools/frame_pmc.sh) over bench.py --steps 100 --no-graph (configs[1], S64)",
-           "kernels": {}}
+    out = {"source": a.source, "kernels": {}}
     for k in sorted(acc, key=lambda x: (x not in STAGE_B, x)):
         per = defaultdict(list)
         for (ctr, _), vals in acc[k].items():
             per[ctr].append(sum(vals))
         m = {c: sum(v) / len(v) for c, v in per.items()}
-        d = {"stage": "B" if k in STAGE_B else "A", "dispatches": max(len(v) for v in per.values()),
+        d = {"stage": "B" if k in STAGE_B else ("A+B" if k in BOTH else "A"), "dispatches": max(len(v) for v in per.values()),
              "mean_per_dispatch": m}
         wc = m.get("SQ_WAVE_CYCLES")
+        if wc and m.get("SQ_WAVES"):
+            d["wave_cycles_per_wave"] = 4 * wc / m["SQ_WAVES"]          # quad-cycles -> cycles
+        if m.get("SQ_BUSY_CYCLES") and m.get("GRBM_GUI_ACTIVE"):
+            d["sq_busy_frac_of_gpu_active"] = m["SQ_BUSY_CYCLES"] / m["GRBM_GUI_ACTIVE"]
         if wc:
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"):
                 if c in m:

@@ -17,10 +17,10 @@ GROUPS_=(
 i=0
 for grp in "${GROUPS_[@]}"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $grp -d $OUT/p$i -o run --output-format csv -- \
-      python3 bench.py --steps 100 --warmup 10 --no-graph --only-headline --order ${ORDER:-stable} \
+  timeout -s KILL ${PASS_LIMIT:-120} rocprofv3 --pmc $grp -d $OUT/p$i -o run --output-format csv -- \
+      python3 bench.py --steps ${STEPS:-100} --warmup 10 --no-graph --only-headline --order ${ORDER:-stable} \
       > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 tools/frame_pmc.py $OUT
+python3 tools/frame_pmc.py $OUT --source "rocprofv3 --pmc passes (tools/frame_pmc.sh) over bench.py --steps ${STEPS:-100} --warmup 10 --no-graph --order ${ORDER:-stable} (configs[1], S64)"
 # gpurun copies back at most 64 MiB: keep the summary, drop the per-dispatch counter rows
 find $OUT -name "*.csv" -delete
