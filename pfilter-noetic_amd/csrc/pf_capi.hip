@@ -393,6 +393,9 @@ static int host_upload(OdomGPU& o, int p, int nc, const float* const* cl, const 
         if (n[c] > o.in_cap) return PF_ECAPACITY;
     }
     PF_HIP_TRY(hipStreamWaitEvent(hs.stream, o.ev_a[p], 0));
+    // straight into the slot's stage inputs: stage B of the slot's previous frame may still read them
+    // (k_init_map after an asynchronous first frame)
+    if (dst_dev) PF_HIP_TRY(hipStreamWaitEvent(hs.stream, o.ev_b[p], 0));
     for (int c = 0; c < nc; ++c) {
         if (!n[c]) continue;
         const void* src = stride[c] == 16 && pinned_dev(cl[c], sizeof(float4) * n[c]) ? (const void*)cl[c] : nullptr;
@@ -414,15 +417,17 @@ static int host_upload(OdomGPU& o, int p, int nc, const float* const* cl, const 
 }
 
 // the caller's class clouds (host memory) straight into slot p's inputs (the copy stream waits for the
-// slot's previous stage A, stage A's stream for the copies). The callers (init_map_n / update_n) return
-// after a readback of stage B, which waits for stage A and so for these copies: the caller's buffers are
-// free on return without a wait here.
-static int stage_inputs(pf_odom* h, int p, const float* const* cl, const size_t* n, const size_t* stride) {
+// slot's previous stage A and stage B, stage A's stream for the copies). The callers (init_map_n /
+// update_n) return after a readback of stage B, which waits for stage A and so for these copies: the
+// caller's buffers are free on return without a wait here. On their early-return paths the copies may
+// still be reading the caller's memory (*direct): they wait for them first (inputs_done).
+static int stage_inputs(pf_odom* h, int p, const float* const* cl, const size_t* n, const size_t* stride,
+                        bool* direct) {
     OdomGPU& o = h->o;
     const int nc = o.cls.nc;
-    bool direct = false;
     StageBuf& sb = o.sb[p];
-    if (int rc = host_upload(o, p, nc, cl, n, stride, &direct, sb.in)) return rc;
+    *direct = false;
+    if (int rc = host_upload(o, p, nc, cl, n, stride, direct, sb.in)) return rc;
     int cnt[kMaxC] = {0, 0, 0};
     for (int c = 0; c < nc; ++c) cnt[c] = (int)n[c];
     hipLaunchKernelGGL(k_set_counts, dim3(1), dim3(64), 0, o.stream_a, sb.cnt + C_IN, cnt[0], cnt[1], cnt[2], nc);
@@ -483,19 +488,26 @@ static int frame_status(pf_odom* h) {
     return PF_OK;
 }
 
+// an early return after stage_inputs: the copies from the caller's memory complete first
+static int inputs_done(pf_odom* h, int p, bool direct, int rc) {
+    if (direct && h->o.hs) (void)hipEventSynchronize(h->o.hs->ev[p]);
+    return rc;
+}
+
 static int init_map_n(pf_odom* h, const float* const* cl, const size_t* n, const size_t* stride) {
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
     const int p = o.frames % kSlots;
+    bool direct = false;
     int rc = stage_a_begin(h, p);
-    if (!rc) rc = stage_inputs(h, p, cl, n, stride);
+    if (!rc) rc = stage_inputs(h, p, cl, n, stride, &direct);
     if (!rc) rc = stage_a_end_b_begin(h, p);
-    if (rc) return rc;
+    if (rc) return inputs_done(h, p, direct, rc);
     odom_enqueue_init(o, p, o.stream);
     odom_enqueue_export(o, o.stream, false);
     rc = stage_b_end(h, p);
-    if (rc) return rc;
-    return readback(h);
+    if (rc) return inputs_done(h, p, direct, rc);
+    return inputs_done(h, p, direct, readback(h));
 }
 
 // updatePointsToMap is synchronous in the reference (the node reads `odom` right after it): one
@@ -504,18 +516,19 @@ static int update_n(pf_odom* h, const float* const* cl, const size_t* n, const s
     OdomGPU& o = h->o;
     PF_HIP_TRY(hipSetDevice(o.device));
     const int p = o.frames % kSlots;
+    bool direct = false;
     int rc = stage_a_begin(h, p);
-    if (!rc) rc = stage_inputs(h, p, cl, n, stride);
-    if (rc) return rc;
+    if (!rc) rc = stage_inputs(h, p, cl, n, stride, &direct);
+    if (rc) return inputs_done(h, p, direct, rc);
     stage_enqueue_vg(o, p, o.stream_a);
     rc = stage_a_end_b_begin(h, p);
-    if (rc) return rc;
+    if (rc) return inputs_done(h, p, direct, rc);
     odom_enqueue_update(o, p, o.stream);
     odom_enqueue_export(o, o.stream, true);
     odom_update_done(o);
     rc = stage_b_end(h, p);
-    if (rc) return rc;
-    rc = readback(h);
+    if (rc) return inputs_done(h, p, direct, rc);
+    rc = inputs_done(h, p, direct, readback(h));
     if (pose_out) std::memcpy(pose_out, o.h_rd->pose, sizeof(double) * 7);
     if (rc) return rc;
     return frame_status(h);
@@ -1398,7 +1411,7 @@ extern "C" int pf_dev_set_rg_radix(pf_odom* h, int enable) {
 // settable-depth restatement), levels = the big levels run before the medium workgroups (0: none).
 extern "C" int pf_dev_tie_sort2(int device, const uint32_t* keys, size_t n, int depth, int levels, uint32_t* perm,
                                 size_t* n_out) {
-    if ((!keys && n) || !perm || !n_out || n > (size_t)INT_MAX / 2 || levels < 0 || levels > 6) return PF_EINVAL;
+    if ((!keys && n) || !perm || !n_out || n > (size_t)INT_MAX / 2 || levels < 0 || levels > kMaxBigLevels) return PF_EINVAL;
     int sizes[4] = {0, 0, 0, 0};
     {
         int end[4] = {0, 0, 0, 0};                 // one past the last valid key of class <= c

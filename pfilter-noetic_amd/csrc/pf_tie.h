@@ -73,16 +73,30 @@ struct TieSort {
     int2* heaps = nullptr;                // [hcap] depth-limit segments {output offset, length}
     u64* hbig = nullptr;                  // [cap + 64] heap entries of segments above the LDS size
     int* ctl = nullptr;                   // counters (pf_tie.hip)
+    // sorts with big levels: depth-limit segments above the LDS size, and (with dependence flags) every
+    // one without an order-dependent group, are sorted by one device-wide radix sort of all of them
+    // (exact for a segment without an order-dependent group); the others go to the heap tier after it
+    int2* huge = nullptr;                 // [hugecap] such segments {output offset, length}
+    int2* heapf = nullptr;                // [hugecap] of those, the ones the heap tier still sorts
+    u32* need = nullptr;                  // [hugecap] a segment's sorted copy holds an order-dependent group
+    int2* hseg = nullptr;                 // [hugecap] the list in position order (k_huge_setup)
+    int* hbase = nullptr;                 // [hugecap + 1] pairs of the segments before each
+    u32 *hk = nullptr, *hv = nullptr;     // [cap] their pairs, gathered
+    PrimWork hprim;                       // the radix sort's scratch (cap)
     size_t cap = 0, tiles = 0;
-    int bcap = 0, mcap = 0, midcap = 0, jcap = 0, hcap = 0;
+    int bcap = 0, mcap = 0, midcap = 0, jcap = 0, hcap = 0, hugecap = 0;
     int max_levels = 0;                   // big levels the buffers are sized for
     int depth0 = -1;                      // test probe: >= 0 replaces every class's depth limit
 };
 
+constexpr int kMaxBigLevels = 48;     // big levels at most (the depth limit 2 lg n of a 16M-key class)
+
 // cap: most pairs of one sort; max_levels < 0: as many big levels as cap can need
 int tie_alloc(TieSort& t, size_t cap, int max_levels = -1);
 void tie_free(TieSort& t);
-// big levels for classes of up to `size_hint` keys (0 below kTieMed; clamped to max_levels)
+// big levels for classes of up to `size_hint` keys: 0 up to kTieMed, else the class's depth limit
+// 2 lg n (a segment that peels a few keys per level stays above kTieMed for tens of levels, and a big
+// level spreads it over the device where a medium workgroup walks it on one CU); clamped to max_levels
 int tie_levels_for(const TieSort& t, size_t size_hint);
 
 // Sorts (keys, vals)[0 .. n) in place, n = the classes' total, each class as std::sort would (keys

@@ -13,6 +13,8 @@ constexpr int kTieGrid = 256;            // workgroups of the tile launches (co-
 constexpr int kLocalGrid = 256;          // workgroups of k_tie_local (two per CU)
 constexpr int kMidGrid = 128;            // workgroups of k_tie_mid (LDS-limited: one per CU)
 constexpr int kMedGrid = 64;             // workgroups of k_tie_medium over a segment list
+constexpr int kHeapCap = 20480 - 128;    // longest depth-limit segment k_tie_heap stages in LDS (with the
+                                         // spare slots: 160 KB less 512 B)
 typedef unsigned short u16;
 
 // control words (TieSort::ctl)
@@ -24,8 +26,11 @@ enum {
     T_NMED = 12,        // medium segments (big path)
     T_NMID = 13,        // mid-tier segments
     T_NHEAP = 14,       // depth-limit segments for k_tie_heap
+    T_NHUGE = 15,       // of them, above the LDS size in a sort with big levels (TieSort::huge)
     T_VC = 16,          // [kMaxTieC] valid pairs of every class
     T_BASE = 20,        // [kMaxTieC] where class c starts in the working copy
+    T_NHEAPF = 24,      // huge segments the heap tier still sorts (TieSort::heapf)
+    T_HUGEN = 25,       // pairs of the huge segments
     T_WORDS = 32
 };
 __device__ __forceinline__ u64* big_ctr(int* ctl, int p) { return reinterpret_cast<u64*>(ctl + T_BIG) + p; }
@@ -146,11 +151,20 @@ __device__ __forceinline__ void file_job(int* ctl, int4* jobs, int jcap, int* er
 }
 
 // a segment at the depth limit, already at its place in the output [off, off + len): k_tie_heap sorts it
+// (with huge set, one above the LDS size goes to the device-wide radix sort first)
 struct HeapList {
     int2* seg;
     int cap;
     int* err;
+    int2* huge;
+    int hugecap;
     __device__ __forceinline__ void file(int* ctl, long long off, int len) const {
+        if (huge && len > kHeapCap) {
+            const int j = atomicAdd(&ctl[T_NHUGE], 1);
+            if (j < hugecap) huge[j] = make_int2((int)off, len);
+            else atomicOr(err, 4);
+            return;
+        }
         const int j = atomicAdd(&ctl[T_NHEAP], 1);
         if (j < cap) seg[j] = make_int2((int)off, len);
         else atomicOr(err, 4);
@@ -414,13 +428,14 @@ __device__ __forceinline__ int cut_of(const u32* lp, const u32* rq, int first, i
     return lf < r ? lf : r;
 }
 
-__device__ __forceinline__ void file_big_child(int* ctl, int pn, int4* next, int4* med, int mcap, int* err, int f,
-                                               int e, int d, bool may_big) {
+__device__ __forceinline__ void file_big_child(int* ctl, int pn, int4* next, int bcap, int4* med, int mcap, int* err,
+                                               int f, int e, int d, bool may_big) {
     const int len = e - f;
     if (len < 1) return;
     if (may_big && len > kTieMed && d > 0) {
         const u64 r = atomicAdd((unsigned long long*)big_ctr(ctl, pn), (1ull << 32) | (u64)tiles_of(len));
-        next[(int)(r >> 32)] = make_int4(f, e, d, (int)(u32)r);
+        if ((int)(r >> 32) < bcap) next[(int)(r >> 32)] = make_int4(f, e, d, (int)(u32)r);
+        else atomicOr(err, 4);
     } else {
         const int i = atomicAdd(&ctl[T_NMED], 1);
         if (i < mcap) med[i] = make_int4(f, e, d, class_of(ctl, f));
@@ -433,7 +448,7 @@ __device__ __forceinline__ void file_big_child(int* ctl, int pn, int4* next, int
 __global__ void __launch_bounds__(1024) k_tie_split(u32* k, u32* v, const u32* __restrict__ lp,
                                                     const u32* __restrict__ rq, const int4* __restrict__ big,
                                                     const u64* __restrict__ tot, int* ctl, int p, int last_level,
-                                                    int4* next, int4* med, int mcap, int* err) {
+                                                    int4* next, int bcap, int4* med, int mcap, int* err) {
     __shared__ int s_cut;
     const int nb = (int)(*big_ctr(ctl, p) >> 32);
     const int t = threadIdx.x;
@@ -457,8 +472,8 @@ __global__ void __launch_bounds__(1024) k_tie_split(u32* k, u32* v, const u32* _
         }
         if (t == 0) {
             const int cut = s_cut;
-            file_big_child(ctl, p ^ 1, next, med, mcap, err, first, cut, depth - 1, !last_level);
-            file_big_child(ctl, p ^ 1, next, med, mcap, err, cut, last, depth - 1, !last_level);
+            file_big_child(ctl, p ^ 1, next, bcap, med, mcap, err, first, cut, depth - 1, !last_level);
+            file_big_child(ctl, p ^ 1, next, bcap, med, mcap, err, cut, last, depth - 1, !last_level);
         }
         __syncthreads();
     }
@@ -502,6 +517,7 @@ struct MedTab {                          // one level's active segments, in posi
     int f[NSEG], e[NSEG], d[NSEG], cut[NSEG];
     u32 pv[NSEG], m[NSEG];
     u32 bl[NSEG], br[NSEG], el[NSEG], er[NSEG];   // stop ranks before first / up to last - 1
+    u32 mp[NSEG];                                  // swap ranks before the segment's (prefix of m)
 };
 template <int NSEG>
 struct MedWork {
@@ -509,6 +525,7 @@ struct MedWork {
     u32 wt[2][16];
     u32 carry[2][2];
     int n[2];
+    u32 msum;
 };
 
 // working copy in global memory; ranks listed at the item's own offset of t.lp / t.rq
@@ -733,31 +750,35 @@ __device__ void part_levels(St& st, MedWork<NSEG>& S, int f0, int e0, int d0, in
         __threadfence_block();
         __syncthreads();
         PART_PROF(8 * lev + 1, rt_now());
-        // 2. in rank space: left stop k of its segment hits when L_k < R_(nR + 1 - k); m = the hits
-        for (u32 gb = 0; gb < TL; gb += kMT * kMBatch) {
-            int s[kMBatch];
-            int pp[kMBatch], qq[kMBatch];
-#pragma unroll
-            for (int i = 0; i < kMBatch; ++i) {
-                const u32 g = gb + (u32)(i * kMT + t);
-                s[i] = -1;
-                pp[i] = 0;
-                qq[i] = -1;
-                if (g < TL) {
-                    const int sx = med_rank_seg(T, ns, g);
-                    const u32 kk = g - T.bl[sx] + 1, nR = T.er[sx] - T.br[sx];
-                    s[i] = sx;
-                    pp[i] = st.getL(g);
-                    if (kk <= nR) qq[i] = st.getR(T.br[sx] + nR - kk);
+        // 2. m per segment: the largest k <= min(nL, nR) with L_k < R_(nR + 1 - k) (the predicate holds for
+        // a prefix of k), one wave per segment searching 64 candidates per round (round 5: the hit count
+        // over every left stop cost a pass over all of them, though a level that peels a few keys has
+        // nL ~ n and m ~ 0)
+        for (int i = w; i < ns; i += kMT / 64) {
+            const int nL = (int)(T.el[i] - T.bl[i]), nR = (int)(T.er[i] - T.br[i]);
+            int lo = 0, hi = nL < nR ? nL : nR;
+            while (lo < hi) {
+                const int step = (hi - lo + 63) >> 6;
+                int kk = lo + (l + 1) * step;
+                kk = kk < hi ? kk : hi;
+                const bool ok = st.getL(T.bl[i] + (u32)(kk - 1)) < st.getR(T.br[i] + (u32)(nR - kk));
+                const int c = __popcll(__ballot(ok));
+                if (c == 0) {
+                    hi = lo + step - 1;
+                } else {
+                    const int nlo = lo + c * step < hi ? lo + c * step : hi;
+                    const int nhi = c < 64 ? (lo + (c + 1) * step < hi ? lo + (c + 1) * step : hi) - 1 : hi;
+                    lo = nlo;
+                    hi = nhi > lo ? nhi : lo;
                 }
             }
-#pragma unroll
-            for (int i = 0; i < kMBatch; ++i) seg_count(T.m, s[i] >= 0 && pp[i] < qq[i], s[i]);
+            if (l == 0) T.m[i] = (u32)lo;
         }
         __threadfence_block();
         __syncthreads();
         PART_PROF(8 * lev + 2, rt_now());
-        // 3. one thread per segment: the cut min(L_(m + 1), R_(nR + 1 - m)) (L_1 for m = 0)
+        // 3. one thread per segment: the cut min(L_(m + 1), R_(nR + 1 - m)) (L_1 for m = 0); wave 0: the
+        // segments' swap ranks (exclusive prefix of m)
         for (int i = t; i < ns; i += kMT) {
             const int m = (int)T.m[i];
             const int nL = (int)(T.el[i] - T.bl[i]), nR = (int)(T.er[i] - T.br[i]);
@@ -771,10 +792,21 @@ __device__ void part_levels(St& st, MedWork<NSEG>& S, int f0, int e0, int d0, in
             }
             T.cut[i] = cut;
         }
+        if (w == 0) {
+            u32 carry = 0;
+            for (int c0 = 0; c0 < ns; c0 += 64) {
+                const u32 mv = c0 + l < ns ? T.m[c0 + l] : 0u;
+                const u32 inc = wave_incl_scan_u32(mv);
+                if (c0 + l < ns) T.mp[c0 + l] = carry + inc - mv;
+                carry += (u32)__shfl((int)inc, 63, 64);
+            }
+            if (l == 0) S.msum = carry;
+        }
         __syncthreads();
         PART_PROF(8 * lev + 3, rt_now());
-        // 4. the swaps L_k <-> R_(nR + 1 - k), k <= m
-        for (u32 gb = 0; gb < TL; gb += kMT * kMBatch) {
+        // 4. the swaps L_k <-> R_(nR + 1 - k), k <= m, over the m's of all segments
+        const u32 SM = S.msum;
+        for (u32 gb = 0; gb < SM; gb += kMT * kMBatch) {
             int pp[kMBatch], qq[kMBatch];
             u32 pr = 0;
 #pragma unroll
@@ -782,14 +814,17 @@ __device__ void part_levels(St& st, MedWork<NSEG>& S, int f0, int e0, int d0, in
                 const u32 g = gb + (u32)(i * kMT + t);
                 pp[i] = 0;
                 qq[i] = 0;
-                if (g < TL) {
-                    const int sx = med_rank_seg(T, ns, g);
-                    const u32 kk = g - T.bl[sx] + 1;
-                    if (kk <= T.m[sx]) {
-                        pr |= 1u << i;
-                        pp[i] = st.getL(g);
-                        qq[i] = st.getR(T.er[sx] - kk);
+                if (g < SM) {
+                    int lo = 0, hi = ns - 1;                 // the last segment whose first swap rank is <= g
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (T.mp[mid] <= g) lo = mid;
+                        else hi = mid - 1;
                     }
+                    const u32 k = g - T.mp[lo];
+                    pr |= 1u << i;
+                    pp[i] = st.getL(T.bl[lo] + k);
+                    qq[i] = st.getR(T.er[lo] - 1u - k);
                 }
             }
             u32 x[kMBatch][4];
@@ -1483,8 +1518,8 @@ __global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, c
 // starts by taking the last element q (its value) and writing the root there; it waits while an earlier
 // pop's hole is q or an ancestor of q, since that pop may still write q. __make_heap's sifts of one tree
 // level touch disjoint subtrees and run in parallel, deepest level first.
-constexpr int kHeapCap = 20480 - 128; // longest segment staged in LDS (with the spare slots: 160 KB less 512 B);
-                                      // longer ones run the same schedule on a global scratch copy
+// kHeapCap (top of the file): the longest segment staged in LDS; longer ones run the same schedule on a
+// global scratch copy
 constexpr int kHeapT = 1024;
 constexpr int kHeapGrid = 256;
 
@@ -1595,8 +1630,8 @@ __device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int
     TIE_PROF(961, rt_now());
     [[maybe_unused]] unsigned long long steps = 0;
     if (t < 64) {
-        HeapPops P{0, false, 0, 0, make_uint2(0u, 0u)};
         const int npops = npops_in < 0 ? n - 1 : npops_in;
+        HeapPops P{0, false, 0, 0, make_uint2(0u, 0u)};
         for (;;) {
             heap_step<true>(H, P, npops, l, spare + l, n - 1);
             heap_step<false>(H, P, npops, l, spare + l, n - 1);
@@ -1707,7 +1742,7 @@ __device__ bool glb_has_equal(const GlbHeap& G, int n) {
 // the network on the global copy G[0, n): chunks of kBitChunk sorted in LDS, then per phase the steps whose
 // partners lie in other chunks on G and the rest chunk by chunk in LDS
 __device__ void glb_bitonic(const GlbHeap& G, uint2* S, int n) {
-    const int P = pow2_ceil(n), t = threadIdx.x;
+    const int P = pow2_ceil(n);
     const int Pc = P < kBitChunk ? P : kBitChunk;
     for (int kk = 0; kk == 0 || (2 * kBitChunk << (kk - 1)) <= P; ++kk) {
         const int k = kk == 0 ? 0 : kBitChunk << kk;
@@ -1783,16 +1818,31 @@ __device__ void heap_segment_pairs(u32* __restrict__ keys, u32* __restrict__ val
     }
 }
 
+// which: the list's counter (T_NHEAP, or T_NHEAPF for the huge segments the radix sort could not finish);
+// the last workgroup out zeroes it and, with also >= 0, that counter too
 __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32* __restrict__ vals, int* ctl,
                                                      const int2* __restrict__ segs, u64* __restrict__ big,
                                                      int bigcap, u32* __restrict__ arrive,
-                                                     const u8* __restrict__ freef) {
+                                                     const u8* __restrict__ freef, int which, int also,
+                                                     int2* __restrict__ route, int routecap, int* err) {
     __shared__ uint2 H[kHeapCap + 64];             // + a spare slot per lane of wave 0
     const int t = threadIdx.x;
-    const int nh = ctl[T_NHEAP];
+    const int nh = ctl[which];
     for (int jb = blockIdx.x; jb < nh; jb += gridDim.x) {
         const int2 sg = segs[jb];
         const int off = sg.x, n = sg.y;
+        if (route && freef) {               // no order-dependent element: the radix sort after this launch
+            int dep = 0;
+            for (int i = t; i < n; i += kHeapT) dep |= freef[vals[off + i]] ? 0 : 1;
+            if (__syncthreads_or(dep) == 0) {
+                if (t == 0) {
+                    const int j = atomicAdd(&ctl[T_NHUGE], 1);
+                    if (j < routecap) route[j] = sg;
+                    else atomicOr(err, 4);
+                }
+                continue;
+            }
+        }
         if (n <= kHeapCap) {
             heap_segment_pairs(keys, vals, freef, off, n, H, jb);
         } else {                                              // the copy at the segment's own offset
@@ -1830,9 +1880,146 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
     if (t == 0) {
         const u32 a = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a == gridDim.x - 1) {
-            __hip_atomic_store(&ctl[T_NHEAP], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl[which], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (also >= 0) __hip_atomic_store(&ctl[also], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+    }
+}
+
+// ---- huge depth-limit segments (sorts with big levels): one device-wide radix sort --------------------
+// A depth-limit segment above the LDS size would be sorted by one workgroup (the network, then maybe the
+// heap on a global copy: configs[4]'s ~820k-key segment took 25 ms), and with the dependence flags a
+// segment of any size that holds no order-dependent group needs no heap at all (configs[4]'s rgbds sort
+// leaves ~1200 such segments per frame, 1.6M keys, and ~15 that need pops). Segments of one sort are
+// disjoint and in key order (every key of a segment is >= every key of the segments before it, and the
+// classes come in class order), so one stable radix sort of all of them gathered back to back in position
+// order leaves every segment's keys sorted in its own range. Where that sorted copy is the result (no
+// order-dependent group, as in k_tie_heap) it is written back; the other segments keep their input and go
+// to the heap tier. The list is filed in any order: k_huge_setup ranks it by offset.
+constexpr int kHugeGrid = 256;
+constexpr int kHugeLds = 4096;           // segment bases the gather / check / finish kernels stage in LDS
+__global__ void __launch_bounds__(1024) k_huge_setup(int* ctl, const int2* __restrict__ huge, int hugecap,
+                                                     int2* __restrict__ hseg, int* __restrict__ hbase,
+                                                     u32* __restrict__ need) {
+    __shared__ u32 ws[16];
+    __shared__ u32 carry;
+    __shared__ int s_off[kHugeLds];
+    const int t = threadIdx.x, w = t >> 6, l = lane_id();
+    int nh = ctl[T_NHUGE];
+    nh = nh < hugecap ? nh : hugecap;
+    const bool lds = nh <= kHugeLds;
+    if (lds)
+        for (int i = t; i < nh; i += 1024) s_off[i] = huge[i].x;
+    __syncthreads();
+    for (int i = t; i < nh; i += 1024) {                  // rank by offset (offsets are distinct)
+        const int2 x = huge[i];
+        int r = 0;
+        if (lds)
+            for (int j = 0; j < nh; ++j) r += s_off[j] < x.x ? 1 : 0;
+        else
+            for (int j = 0; j < nh; ++j) r += huge[j].x < x.x ? 1 : 0;
+        hseg[r] = x;
+        need[r] = 0u;
+    }
+    if (t == 0) carry = 0u;
+    __threadfence_block();
+    __syncthreads();
+    for (int c0 = 0; c0 < nh; c0 += 1024) {              // exclusive prefix of the lengths in position order
+        const int i = c0 + t;
+        const u32 len = i < nh ? (u32)hseg[i].y : 0u;
+        const u32 inc = wave_incl_scan_u32(len);
+        if (l == 63) ws[w] = inc;
+        __syncthreads();
+        u32 off = carry;
+        for (int q = 0; q < w; ++q) off += ws[q];
+        if (i < nh) hbase[i] = (int)(off + inc - len);
+        __syncthreads();
+        if (t == 1023) carry = off + inc;
+        __syncthreads();
+    }
+    if (t == 0) {
+        hbase[nh] = (int)carry;
+        ctl[T_HUGEN] = (int)carry;
+    }
+}
+// the segment bases (position order) staged in LDS when they fit; returns nh
+__device__ __forceinline__ int huge_stage(const int* ctl, int hugecap, const int* hbase, int* s_base) {
+    int nh = ctl[T_NHUGE];
+    nh = nh < hugecap ? nh : hugecap;
+    if (nh < kHugeLds)
+        for (int i = threadIdx.x; i <= nh; i += blockDim.x) s_base[i] = hbase[i];
+    __syncthreads();
+    return nh;
+}
+__device__ __forceinline__ int huge_seg_of(const int* s_base, const int* hbase, int nh, int i) {
+    const int* b = nh < kHugeLds ? s_base : hbase;
+    int lo = 0, hi = nh - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (b[mid] <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+__global__ void __launch_bounds__(256) k_huge_gather(const u32* __restrict__ keys, const u32* __restrict__ vals,
+                                                     const int* ctl, int hugecap, const int2* __restrict__ hseg,
+                                                     const int* __restrict__ hbase, u32* __restrict__ hk,
+                                                     u32* __restrict__ hv, SortHist sh) {
+    __shared__ int s_base[kHugeLds + 1];
+    __shared__ u32 lh[4][256];
+    sort_hist_begin(lh);
+    const int nh = huge_stage(ctl, hugecap, hbase, s_base);
+    const int n = ctl[T_HUGEN];
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int s = huge_seg_of(s_base, hbase, nh, i);
+        const int p = hseg[s].x + (i - (nh < kHugeLds ? s_base[s] : hbase[s]));
+        const u32 key = keys[p];
+        hk[i] = key;
+        hv[i] = vals[p];
+        sort_hist_add(lh, key, sh.passes);
+    }
+    sort_hist_end(lh, sh, n, n);
+}
+// a huge segment needs the heap tier when its sorted copy holds an order-dependent element (flags) or,
+// without flags, two equal neighbours
+__global__ void __launch_bounds__(256) k_huge_check(const int* ctl, int hugecap, const int* __restrict__ hbase,
+                                                    const u32* __restrict__ hk, const u32* __restrict__ hv,
+                                                    const u8* __restrict__ freef, u32* __restrict__ need) {
+    __shared__ int s_base[kHugeLds + 1];
+    const int nh = huge_stage(ctl, hugecap, hbase, s_base);
+    const int n = ctl[T_HUGEN];
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int s = huge_seg_of(s_base, hbase, nh, i);
+        const int end = s + 1 < nh ? (nh < kHugeLds ? s_base[s + 1] : hbase[s + 1]) : n;
+        const bool dep = freef ? freef[hv[i]] == 0 : (i + 1 < end && hk[i + 1] == hk[i]);
+        if (dep && need[s] == 0u) atomicOr(&need[s], 1u);
+    }
+}
+// the sorted copies written back; the segments that need the heap filed for it (block 0)
+__global__ void __launch_bounds__(256) k_huge_finish(u32* __restrict__ keys, u32* __restrict__ vals, int* ctl,
+                                                     int hugecap, const int2* __restrict__ hseg,
+                                                     const int* __restrict__ hbase, const u32* __restrict__ hk,
+                                                     const u32* __restrict__ hv, const u32* __restrict__ need,
+                                                     int2* __restrict__ heapf) {
+    __shared__ int s_base[kHugeLds + 1];
+    __shared__ int s_nf;
+    const int nh = huge_stage(ctl, hugecap, hbase, s_base);
+    const int n = ctl[T_HUGEN];
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) s_nf = 0;
+        __syncthreads();
+        for (int s = threadIdx.x; s < nh; s += 256)
+            if (need[s]) heapf[atomicAdd(&s_nf, 1)] = hseg[s];
+        __syncthreads();
+        if (threadIdx.x == 0) ctl[T_NHEAPF] = s_nf;
+    }
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int s = huge_seg_of(s_base, hbase, nh, i);
+        if (need[s]) continue;
+        const int p = hseg[s].x + (i - (nh < kHugeLds ? s_base[s] : hbase[s]));
+        keys[p] = hk[i];
+        vals[p] = hv[i];
     }
 }
 
@@ -1840,15 +2027,16 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
 
 int tie_alloc(TieSort& t, size_t cap, int max_levels) {
     if (cap < 1) cap = 1;
-    if (max_levels < 0) {
-        max_levels = 0;
-        while (max_levels < 8 && ((size_t)kTieMed << max_levels) < cap) ++max_levels;
-    }
-    if (max_levels > 8) max_levels = 8;
+    if (max_levels < 0) max_levels = cap > (size_t)kTieMed ? 2 * (63 - __builtin_clzll((unsigned long long)cap)) : 0;
+    if (max_levels > kMaxBigLevels) max_levels = kMaxBigLevels;
     t.cap = cap;
     t.max_levels = max_levels;
-    t.bcap = kMaxTieC << max_levels;
-    t.mcap = 2 * t.bcap + kMaxTieC + 8;
+    // the big segments of one level are disjoint and longer than kTieMed (plus a short class of each
+    // kind at level 0); every big segment files at most two medium segments
+    t.bcap = (int)(cap / kTieMed) + 2 * kMaxTieC + 8;
+    if (t.bcap > kTieBigLds) return PF_EINVAL;
+    t.mcap = 2 * t.bcap * (max_levels > 0 ? max_levels : 1) + kMaxTieC + 8;
+    t.hugecap = (int)(cap / (kThreshold + 1)) + 64;   // any depth-limit segment may be routed there
     // a partitioned segment files at most two pieces per level; the partitioned segments of a level
     // are disjoint and longer than the tier's stop size
     t.jcap = (int)(2 * 64 * (cap / kTieSmall + 1) + 64);
@@ -1871,6 +2059,16 @@ int tie_alloc(TieSort& t, size_t cap, int max_levels) {
     PF_TALLOC(t.heaps, sizeof(int2) * t.hcap);
     PF_TALLOC(t.hbig, sizeof(u64) * (cap + 64));     // segments above the LDS size, at their own offsets
     PF_TALLOC(t.ctl, sizeof(int) * T_WORDS);
+    if (max_levels > 0) {
+        PF_TALLOC(t.huge, sizeof(int2) * t.hugecap);
+        PF_TALLOC(t.heapf, sizeof(int2) * t.hugecap);
+        PF_TALLOC(t.need, sizeof(u32) * t.hugecap);
+        PF_TALLOC(t.hseg, sizeof(int2) * t.hugecap);
+        PF_TALLOC(t.hbase, sizeof(int) * (t.hugecap + 1));
+        PF_TALLOC(t.hk, sizeof(u32) * cap);
+        PF_TALLOC(t.hv, sizeof(u32) * cap);
+        if (int rc = prim_alloc(t.hprim, cap)) return rc;
+    }
 #undef PF_TALLOC
     if (hipMemset(t.status, 0, sizeof(u64) * t.tiles) != hipSuccess || hipMemset(t.arrive, 0, sizeof(u32) * 4) != hipSuccess ||
         hipMemset(t.ctl, 0, sizeof(int) * T_WORDS) != hipSuccess)
@@ -1880,15 +2078,16 @@ int tie_alloc(TieSort& t, size_t cap, int max_levels) {
 
 void tie_free(TieSort& t) {
     void* ptrs[] = {t.k, t.v, t.lp, t.rq, t.status, t.arrive, t.big, t.tot, t.med, t.mid, t.jobs, t.heaps, t.hbig,
-                    t.ctl};
+                    t.ctl, t.huge, t.heapf, t.need, t.hk, t.hv, t.hseg, t.hbase};
     for (void* p : ptrs) (void)hipFree(p);
+    if (t.hprim.cap) prim_free(t.hprim);
     t = TieSort{};
 }
 
 int tie_levels_for(const TieSort& t, size_t size_hint) {
-    int lv = 0;
-    while (lv < t.max_levels && ((size_t)kTieMed << lv) < size_hint) ++lv;
-    return lv;
+    if (size_hint <= (size_t)kTieMed) return 0;
+    const int lv = 2 * (63 - __builtin_clzll((unsigned long long)size_hint));
+    return lv < t.max_levels ? lv : t.max_levels;
 }
 
 void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s, int levels,
@@ -1907,17 +2106,32 @@ void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStr
             hipLaunchKernelGGL(k_tie_scan, dim3(tg), dim3(256), 0, s, t.k, t.big + p * t.bcap, t.ctl, p, t.lp, t.rq,
                                t.tot, t.status, t.arrive + 1, err);
             hipLaunchKernelGGL(k_tie_split, dim3(t.bcap), dim3(1024), 0, s, t.k, t.v, t.lp, t.rq, t.big + p * t.bcap,
-                               t.tot, t.ctl, p, lev == levels - 1 ? 1 : 0, t.big + (p ^ 1) * t.bcap, t.med, t.mcap,
-                               err);
+                               t.tot, t.ctl, p, lev == levels - 1 ? 1 : 0, t.big + (p ^ 1) * t.bcap, t.bcap, t.med,
+                               t.mcap, err);
         }
         hipLaunchKernelGGL(k_tie_medium, dim3(kMedGrid), dim3(kMT), 0, s, keys, vals, cls, 0, t.depth0, t.k, t.v, t.lp,
                            t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err);
     }
     hipLaunchKernelGGL(k_tie_mid, dim3(kMidGrid), dim3(kMT), 0, s, t.k, t.v, t.ctl, t.mid, t.jobs, t.jcap, err);
+    const bool huge = levels > 0 && t.huge;
     hipLaunchKernelGGL(k_tie_local, dim3(kLocalGrid), dim3(1024), 0, s, t.k, t.v, t.jobs, t.ctl, t.arrive + 2, keys,
-                       vals, cls, HeapList{t.heaps, t.hcap, err});
+                       vals, cls, HeapList{t.heaps, t.hcap, err, huge ? t.huge : nullptr, t.hugecap});
     hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heaps, t.hbig,
-                       (int)t.cap, t.arrive + 3, freef);
+                       (int)t.cap, t.arrive + 3, freef, (int)T_NHEAP, -1, huge ? t.huge : nullptr, t.hugecap, err);
+    if (huge) {
+        PrimWork pw = t.hprim;
+        pw.err = err;
+        hipLaunchKernelGGL(k_huge_setup, dim3(1), dim3(1024), 0, s, t.ctl, t.huge, t.hugecap, t.hseg, t.hbase, t.need);
+        hipLaunchKernelGGL(k_huge_gather, dim3(kHugeGrid), dim3(256), 0, s, keys, vals, t.ctl, t.hugecap, t.hseg,
+                           t.hbase, t.hk, t.hv, sort_hist(pw, 32, true));
+        radix_sort_pairs(t.hk, t.hv, t.ctl + T_HUGEN, 32, pw, s, nullptr, nullptr, true);
+        hipLaunchKernelGGL(k_huge_check, dim3(kHugeGrid), dim3(256), 0, s, t.ctl, t.hugecap, t.hbase, t.hk, t.hv,
+                           freef, t.need);
+        hipLaunchKernelGGL(k_huge_finish, dim3(kHugeGrid), dim3(256), 0, s, keys, vals, t.ctl, t.hugecap, t.hseg,
+                           t.hbase, t.hk, t.hv, t.need, t.heapf);
+        hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heapf, t.hbig,
+                           (int)t.cap, t.arrive + 3, freef, (int)T_NHEAPF, (int)T_NHUGE, (int2*)nullptr, 0, err);
+    }
 }
 
 const int* tie_valid_count(const TieSort& t) { return t.ctl + T_VALID; }

@@ -176,8 +176,9 @@ def test_knn_shard_mode_gloo_world2():
 
 def test_sort_order_flags():
     """The headline runs in the reference tie order by default (the mode whose results are the
-    reference's frame by frame); the other order is reported beside it; configs[4]'s leg defaults to the
-    stable order (its tie order heap-sorts ~1.4M keys per frame)."""
+    reference's frame by frame); the other order is reported beside it; configs[4]'s leg runs in the tie
+    order too (its depth-limit segment of ~820k distinct keys is sorted by one device-wide radix sort,
+    DESIGN.md section 4)."""
     sys.path.insert(0, ROOT)
     import bench
     a = bench.parse([])

@@ -101,3 +101,36 @@ def test_tie_sort_natural_depth_limit(pa, pfref):
         for levels in (0, 2):
             np.testing.assert_array_equal(pa.tie_sort(keys, levels=levels), want,
                                           err_msg="map %d + %d levels=%d" % (nmap, napp, levels))
+
+
+def test_tie_sort_huge_segments_radix_then_heap(pa, pfref):
+    """Sorts with big levels send depth-limit segments above the LDS size (20352 keys) to one device-wide
+    radix sort of all of them (pf_tie.hip k_huge_*): kept where a segment holds no equal pair (its only
+    sorted order), else the segment keeps its input and the heap tier sorts it. Several huge segments in
+    one sort (depth limit 2: four pieces), one of them with an equal pair, in two classes."""
+    rng = np.random.default_rng(26)
+    perm = (rng.permutation(200000) * 3).astype(np.uint32)
+    dup = perm.copy()
+    dup[10] = dup[11]                                           # one equal pair: that segment heap-sorts
+    two = np.concatenate([perm[:90000], (perm[90000:] & 0x3FFFFFFF) | np.uint32(1 << 30)])
+    for keys in (perm, dup, two):
+        for depth in (0, 2):
+            want = np.concatenate([np.nonzero((keys >> 30) == c)[0][pfref.sort_perm(keys[(keys >> 30) == c],
+                                                                                     "literal", depth)]
+                                   for c in range(4) if np.any((keys >> 30) == c)]).astype(np.uint32)
+            np.testing.assert_array_equal(pa.tie_sort(keys, depth=depth, levels=4), want,
+                                          err_msg="n=%d depth=%d" % (keys.size, depth))
+
+
+def test_tie_sort_deep_big_levels(pa, pfref):
+    """tie_levels_for gives a class above kTieMed its whole depth limit in big levels (a segment that
+    peels a few keys per level stays above kTieMed for tens of levels): rgbds-like inputs, a voxel-ordered
+    map of 400k keys with new points appended, at 40 big levels and at 2."""
+    rng = np.random.default_rng(27)
+    m = np.sort(rng.choice(1 << 26, 400000, replace=False))
+    for napp in (200, 8000):
+        keys = np.concatenate([m, rng.choice(m, napp)]).astype(np.uint32)
+        want = _expected(pfref, keys)
+        for levels in (2, 40):
+            np.testing.assert_array_equal(pa.tie_sort(keys, levels=levels), want,
+                                          err_msg="map 400000 + %d levels=%d" % (napp, levels))
