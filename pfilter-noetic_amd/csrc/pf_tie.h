@@ -81,6 +81,7 @@ struct TieSort {
     u32* need = nullptr;                  // [hugecap] a segment's sorted copy holds an order-dependent group
     int2* hseg = nullptr;                 // [hugecap] the list in position order (k_huge_setup)
     int* hbase = nullptr;                 // [hugecap + 1] pairs of the segments before each
+    u32* depn = nullptr;                  // [2][512] order-dependent elements of a level's big segments
     u32 *hk = nullptr, *hv = nullptr;     // [cap] their pairs, gathered
     PrimWork hprim;                       // the radix sort's scratch (cap)
     size_t cap = 0, tiles = 0;

@@ -13,6 +13,8 @@ constexpr int kTieGrid = 256;            // workgroups of the tile launches (co-
 constexpr int kLocalGrid = 256;          // workgroups of k_tie_local (two per CU)
 constexpr int kMidGrid = 128;            // workgroups of k_tie_mid (LDS-limited: one per CU)
 constexpr int kMedGrid = 64;             // workgroups of k_tie_medium over a segment list
+constexpr int kTieBigLds = 512;          // big segments of one level at most (cached in LDS by k_tie_scan)
+constexpr int kDepFree = -2;             // a segment's depth word: no order-dependent group in it (routed)
 constexpr int kHeapCap = 20480 - 128;    // longest depth-limit segment k_tie_heap stages in LDS (with the
                                          // spare slots: 160 KB less 512 B)
 typedef unsigned short u16;
@@ -158,6 +160,12 @@ struct HeapList {
     int* err;
     int2* huge;
     int hugecap;
+    // a segment without an order-dependent group (any size): straight to the radix sort
+    __device__ __forceinline__ void file_free(int* ctl, long long off, int len) const {
+        const int j = atomicAdd(&ctl[T_NHUGE], 1);
+        if (j < hugecap) huge[j] = make_int2((int)off, len);
+        else atomicOr(err, 4);
+    }
     __device__ __forceinline__ void file(int* ctl, long long off, int len) const {
         if (huge && len > kHeapCap) {
             const int j = atomicAdd(&ctl[T_NHUGE], 1);
@@ -243,7 +251,9 @@ __global__ void __launch_bounds__(256) k_tie_compact(const u32* __restrict__ key
 // level 0 of the big path: every class is one std::sort call; above kTieMed keys it starts in the
 // big levels, otherwise in a medium workgroup
 __global__ void k_tie_setup(TieClasses cls, int* __restrict__ ctl, int4* __restrict__ big, int4* __restrict__ med,
-                            int levels, int depth0) {
+                            int levels, int depth0, u32* __restrict__ depn) {
+    if (depn)
+        for (int i = threadIdx.x; i < kTieBigLds; i += blockDim.x) depn[i] = 0u;
     if (threadIdx.x != 0) return;
     const int nv = ctl[T_VALID];
     int cs[kMaxTieC + 1];
@@ -319,7 +329,6 @@ __device__ __forceinline__ u64 pack2(u32 packed16) {              // (L << 16 | 
     return ((u64)(packed16 >> 16) << 31) | (u64)(packed16 & 0xffffu);
 }
 
-constexpr int kTieBigLds = 512;          // big segments of one level cached in LDS (bcap <= this)
 
 // every tile of every big segment of level parity p: the stops of its 4096 keys ranked in position
 // order. The median of three is applied virtually here (first holds the pivot, sel the old first key)
@@ -328,7 +337,8 @@ __global__ void __launch_bounds__(256) k_tie_scan(const u32* __restrict__ k, con
                                                   int* __restrict__ ctl, int p, u32* __restrict__ lp,
                                                   u32* __restrict__ rq, u64* __restrict__ tot,
                                                   u64* __restrict__ status, u32* __restrict__ arrive,
-                                                  int* __restrict__ err) {
+                                                  int* __restrict__ err, const u32* __restrict__ v,
+                                                  const u8* __restrict__ freef, u32* __restrict__ depn) {
     __shared__ int4 s_big[kTieBigLds];
     __shared__ u32 s_cnt[64];
     __shared__ u64 s_off[64];
@@ -337,6 +347,8 @@ __global__ void __launch_bounds__(256) k_tie_scan(const u32* __restrict__ k, con
     const int t = threadIdx.x, w = t >> 6, l = lane_id();
     const u64 lt = lanemask_lt();
     if (blockIdx.x == 0 && t == 0) *big_ctr(ctl, p ^ 1) = 0;   // the next level's list (unread here)
+    if (freef && blockIdx.x == 0)                               // and its dependent counts
+        for (int i = t; i < kTieBigLds; i += 256) depn[((p ^ 1) * kTieBigLds) + i] = 0u;
     if (ntiles == 0) return;
     const int G = ntiles < (int)gridDim.x ? ntiles : (int)gridDim.x;
     if ((int)blockIdx.x >= G) return;
@@ -358,6 +370,16 @@ __global__ void __launch_bounds__(256) k_tie_scan(const u32* __restrict__ k, con
         const u32 pv = sel == a ? ka : (sel == b ? kb : kc);
         u32 fl = 0, fr = 0;                                      // this thread's stop flags, bit j = row j
         u64 mL[16], mR[16];
+        if (freef) {                                             // order-dependent elements of the segment
+            int dep = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int i = base + j * 256 + t;
+                if (i < last) dep += freef[v[i]] ? 0 : 1;
+            }
+            dep = __syncthreads_count(dep);
+            if (t == 0 && dep) atomicAdd(&depn[p * kTieBigLds + s], (u32)dep);
+        }
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const int i = base + j * 256 + t;
@@ -448,13 +470,22 @@ __device__ __forceinline__ void file_big_child(int* ctl, int pn, int4* next, int
 __global__ void __launch_bounds__(1024) k_tie_split(u32* k, u32* v, const u32* __restrict__ lp,
                                                     const u32* __restrict__ rq, const int4* __restrict__ big,
                                                     const u64* __restrict__ tot, int* ctl, int p, int last_level,
-                                                    int4* next, int bcap, int4* med, int mcap, int* err) {
+                                                    int4* next, int bcap, int4* med, int mcap, int* err,
+                                                    u32* __restrict__ depn) {
     __shared__ int s_cut;
     const int nb = (int)(*big_ctr(ctl, p) >> 32);
     const int t = threadIdx.x;
     for (int s = blockIdx.x; s < nb; s += gridDim.x) {
         const int4 sg = big[s];
         const int first = sg.x, last = sg.y, depth = sg.z;
+        if (depn && depn[p * kTieBigLds + s] == 0u) {  // no order-dependent group: any order, no more levels
+            if (t == 0) {
+                const int i = atomicAdd(&ctl[T_NMED], 1);
+                if (i < mcap) med[i] = make_int4(first, last, kDepFree, class_of(ctl, first));
+                else atomicOr(err, 4);
+            }
+            continue;
+        }
         if (t == 0) median_to_first(k, v, first, last);
         const u64 tt = tot[s];
         const int nL = (int)(tt >> 32), nR = (int)(u32)tt;
@@ -612,7 +643,8 @@ __device__ __forceinline__ void seg_count(u32* slot, bool act, int seg) {
 }
 
 // emit(f, e, d): a segment of at most `stop` keys (d >= 0) or one at the depth limit (d = -1: copied to
-// the output as it stands by the locals, then heap-sorted there by k_tie_heap)
+// the output as it stands by the locals, then heap-sorted there by k_tie_heap), or (d = kDepFree) one
+// without an order-dependent group (copied as it stands, then sorted by the radix sort of k_huge_*)
 template <int NSEG, class St, class Emit>
 __device__ void part_levels(St& st, MedWork<NSEG>& S, int f0, int e0, int d0, int stop, Emit emit, int* err,
                             int prof = -1) {
@@ -620,7 +652,9 @@ __device__ void part_levels(St& st, MedWork<NSEG>& S, int f0, int e0, int d0, in
     const u64 lt = lanemask_lt();
     if (e0 - f0 <= stop || d0 <= 0) {
         if (t == 0) {
-            if (e0 - f0 > stop) {                                   // the depth limit above the stop size
+            if (d0 == kDepFree) {
+                emit(f0, e0, kDepFree);
+            } else if (e0 - f0 > stop) {                            // the depth limit above the stop size
                 emit(f0, e0, -1);
             } else {
                 emit(f0, e0, d0);
@@ -896,6 +930,13 @@ __device__ void part_levels(St& st, MedWork<NSEG>& S, int f0, int e0, int d0, in
     __syncthreads();
 }
 
+// true when [f, e) of the working copy (values v) holds an element of an order-dependent group
+__device__ __forceinline__ bool range_dep(const u32* v, const u8* freef, int f, int e) {
+    int dep = 0;
+    for (int i = f + (int)threadIdx.x; i < e && !dep; i += (int)blockDim.x) dep = freef[v[i]] ? 0 : 1;
+    return __syncthreads_or(dep) != 0;
+}
+
 // hands a segment on: to the LDS mid tier above kTieSmall keys, else (and final segments) to the locals
 struct EmitGlobal {
     int* ctl;
@@ -919,7 +960,8 @@ struct EmitGlobal {
 __global__ void __launch_bounds__(1024) k_tie_medium(const u32* __restrict__ keys, const u32* __restrict__ vals,
                                                      TieClasses cls, int from_classes, int depth0, u32* k, u32* v,
                                                      u32* lp, u32* rq, int* ctl, const int4* __restrict__ med,
-                                                     int4* mid, int midcap, int4* jobs, int jcap, int* err) {
+                                                     int4* mid, int midcap, int4* jobs, int jcap, int* err,
+                                                     const u8* __restrict__ freef) {
     __shared__ MedWork<512> S;
     const int t = threadIdx.x, w = t >> 6, l = lane_id();
     const u64 lt = lanemask_lt();
@@ -993,6 +1035,7 @@ __global__ void __launch_bounds__(1024) k_tie_medium(const u32* __restrict__ key
             d0 = mi.z;
             cl = mi.w;
         }
+        if (freef && d0 > 0 && e0 - f0 > kTieSmall && !range_dep(v, freef, f0, e0)) d0 = kDepFree;
         GStore st{k, v, lp, rq, f0};
         part_levels<512>(st, S, f0, e0, d0, kTieMid, EmitGlobal{ctl, mid, jobs, midcap, jcap, cl, err}, err,
                          blockIdx.x == 0 && it == 0 ? 256 : -1);
@@ -1014,13 +1057,17 @@ struct EmitJob {
     __device__ void operator()(int f, int e, int d) const { file_job(ctl, jobs, jcap, err, off + f, off + e, d, cls); }
 };
 __global__ void __launch_bounds__(1024) k_tie_mid(u32* k, u32* v, int* ctl, const int4* __restrict__ mid,
-                                                  int4* jobs, int jcap, int* err) {
+                                                  int4* jobs, int jcap, int* err, const u8* __restrict__ freef) {
     __shared__ MidLds S;
     const int t = threadIdx.x;
     const int nm = ctl[T_NMID];
     for (int it = blockIdx.x; it < nm; it += gridDim.x) {
         const int4 mi = mid[it];
         const int f = mi.x, len = mi.y - mi.x;
+        if (freef && !range_dep(v, freef, f, f + len)) {         // no order-dependent group: as it stands
+            if (t == 0) file_job(ctl, jobs, jcap, err, f, f + len, kDepFree, mi.w);
+            continue;
+        }
         for (int i = t; i < len; i += kMT) {
             S.K[i] = k[f + i];
             S.I[i] = (u16)i;
@@ -1233,7 +1280,7 @@ __device__ __forceinline__ void local_output(LocalLds& S, int len, const u32 (&s
 __global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, const u32* __restrict__ v,
                                                     const int4* __restrict__ jobs, int* ctl, u32* __restrict__ arrive,
                                                     u32* __restrict__ keys, u32* __restrict__ vals, TieClasses cls,
-                                                    HeapList hl) {
+                                                    HeapList hl, const u8* __restrict__ freef) {
     __shared__ LocalLds S;
     const int t = threadIdx.x, w = t >> 6, l = lane_id();
     const u64 lt = lanemask_lt();
@@ -1268,12 +1315,19 @@ __global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, c
 #pragma unroll
         for (int c = 0; c < kMaxTieC; ++c)
             if (c == job.w) ob = obase[c];
-        if (d < 0) {                                // at the depth limit in a partition tier: as it stands
+        // at the depth limit in a partition tier, or (with the radix route) without an order-dependent
+        // group: as it stands, for k_tie_heap or the radix sort
+        const bool freej = d == kDepFree || (hl.huge && freef && d >= 0 && len > kThreshold &&
+                                             !range_dep(v, freef, f, f + len));
+        if (d < 0 || freej) {
             for (int i = t; i < len; i += 1024) {
                 keys[ob + f + i] = k[f + i];
                 vals[ob + f + i] = v[f + i];
             }
-            if (t == 0) hl.file(ctl, ob + f, len);
+            if (t == 0) {
+                if (freej) hl.file_free(ctl, ob + f, len);
+                else hl.file(ctl, ob + f, len);
+            }
             continue;
         }
         // the segment id of every position this lane owns stays in its registers for the whole job;
@@ -2065,6 +2119,7 @@ int tie_alloc(TieSort& t, size_t cap, int max_levels) {
         PF_TALLOC(t.need, sizeof(u32) * t.hugecap);
         PF_TALLOC(t.hseg, sizeof(int2) * t.hugecap);
         PF_TALLOC(t.hbase, sizeof(int) * (t.hugecap + 1));
+        PF_TALLOC(t.depn, sizeof(u32) * 2 * kTieBigLds);
         PF_TALLOC(t.hk, sizeof(u32) * cap);
         PF_TALLOC(t.hv, sizeof(u32) * cap);
         if (int rc = prim_alloc(t.hprim, cap)) return rc;
@@ -2078,7 +2133,7 @@ int tie_alloc(TieSort& t, size_t cap, int max_levels) {
 
 void tie_free(TieSort& t) {
     void* ptrs[] = {t.k, t.v, t.lp, t.rq, t.status, t.arrive, t.big, t.tot, t.med, t.mid, t.jobs, t.heaps, t.hbig,
-                    t.ctl, t.huge, t.heapf, t.need, t.hk, t.hv, t.hseg, t.hbase};
+                    t.ctl, t.huge, t.heapf, t.need, t.hk, t.hv, t.hseg, t.hbase, t.depn};
     for (void* p : ptrs) (void)hipFree(p);
     if (t.hprim.cap) prim_free(t.hprim);
     t = TieSort{};
@@ -2093,29 +2148,33 @@ int tie_levels_for(const TieSort& t, size_t size_hint) {
 void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s, int levels,
               const u8* freef) {
     if (levels > t.max_levels) levels = t.max_levels;
+    // the radix route (sorts with big levels): huge depth-limit segments and, with dependence flags,
+    // every segment without an order-dependent group, from any tier
+    const bool huge = levels > 0 && t.huge;
+    const u8* rf = huge ? freef : nullptr;
+    u32* depn = rf ? t.depn : nullptr;
     if (levels <= 0) {
         hipLaunchKernelGGL(k_tie_medium, dim3(kMaxTieC), dim3(kMT), 0, s, keys, vals, cls, 1, t.depth0, t.k, t.v,
-                           t.lp, t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err);
+                           t.lp, t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err, rf);
     } else {
         const int tg = (int)(t.tiles < (size_t)kTieGrid ? t.tiles : (size_t)kTieGrid);
         hipLaunchKernelGGL(k_tie_compact, dim3(tg), dim3(256), 0, s, keys, vals, cls, t.k, t.v, t.ctl, t.status,
                            t.arrive, err);
-        hipLaunchKernelGGL(k_tie_setup, dim3(1), dim3(64), 0, s, cls, t.ctl, t.big, t.med, levels, t.depth0);
+        hipLaunchKernelGGL(k_tie_setup, dim3(1), dim3(64), 0, s, cls, t.ctl, t.big, t.med, levels, t.depth0, depn);
         for (int lev = 0; lev < levels; ++lev) {
             const int p = lev & 1;
             hipLaunchKernelGGL(k_tie_scan, dim3(tg), dim3(256), 0, s, t.k, t.big + p * t.bcap, t.ctl, p, t.lp, t.rq,
-                               t.tot, t.status, t.arrive + 1, err);
+                               t.tot, t.status, t.arrive + 1, err, t.v, rf, depn);
             hipLaunchKernelGGL(k_tie_split, dim3(t.bcap), dim3(1024), 0, s, t.k, t.v, t.lp, t.rq, t.big + p * t.bcap,
                                t.tot, t.ctl, p, lev == levels - 1 ? 1 : 0, t.big + (p ^ 1) * t.bcap, t.bcap, t.med,
-                               t.mcap, err);
+                               t.mcap, err, depn);
         }
         hipLaunchKernelGGL(k_tie_medium, dim3(kMedGrid), dim3(kMT), 0, s, keys, vals, cls, 0, t.depth0, t.k, t.v, t.lp,
-                           t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err);
+                           t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err, rf);
     }
-    hipLaunchKernelGGL(k_tie_mid, dim3(kMidGrid), dim3(kMT), 0, s, t.k, t.v, t.ctl, t.mid, t.jobs, t.jcap, err);
-    const bool huge = levels > 0 && t.huge;
+    hipLaunchKernelGGL(k_tie_mid, dim3(kMidGrid), dim3(kMT), 0, s, t.k, t.v, t.ctl, t.mid, t.jobs, t.jcap, err, rf);
     hipLaunchKernelGGL(k_tie_local, dim3(kLocalGrid), dim3(1024), 0, s, t.k, t.v, t.jobs, t.ctl, t.arrive + 2, keys,
-                       vals, cls, HeapList{t.heaps, t.hcap, err, huge ? t.huge : nullptr, t.hugecap});
+                       vals, cls, HeapList{t.heaps, t.hcap, err, huge ? t.huge : nullptr, t.hugecap}, rf);
     hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heaps, t.hbig,
                        (int)t.cap, t.arrive + 3, freef, (int)T_NHEAP, -1, huge ? t.huge : nullptr, t.hugecap, err);
     if (huge) {
