@@ -333,6 +333,15 @@ void pfref_introsort_heapdep(const uint32_t* keys, const uint8_t* dep, size_t n,
                 }
                 std::fprintf(stderr, "heapdep %s len %ld distinct %ld depkeys %ld depgroups %ld pops %ld\n", tag, len,
                              distinct, ndk, ndg, pops);
+                // PFREF_HEAP_DUMP: the depth-limit segments needing more than 1000 pops, as they reach the heap
+                // (int32 len, int32 pops, then len keys), for the pop-schedule studies in tools/
+                static FILE* hd = std::getenv("PFREF_HEAP_DUMP") ? std::fopen(std::getenv("PFREF_HEAP_DUMP"), "ab") : nullptr;
+                if (hd && pops > 1000) {
+                    const int32_t hdr[2] = {(int32_t)len, (int32_t)pops};
+                    std::fwrite(hdr, sizeof(hdr), 1, hd);
+                    for (long i = 0; i < len; ++i) std::fwrite(&first[i].key, sizeof(uint32_t), 1, hd);
+                    std::fflush(hd);
+                }
                 break;
             }
             --depth;

@@ -613,6 +613,7 @@ int pf_odom_set_map(pf_odom* h, int which, const float* xyz, const uint8_t* rg, 
     }
     if (n) PF_HIP_TRY(hipMemcpyAsync(map_cur(o)[which], tmp.data(), sizeof(float4) * n, hipMemcpyHostToDevice, o.stream));
     hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, o.stream, o.cnt + C_M + which, (int)n);
+    odom_dep_dirty(o, o.stream);                        // any points, several per voxel maybe
     o.dims_fresh = false;                               // the next update's grid takes its bounds pass
     if (n + 65536 > o.tie_hint) o.tie_hint = n + 65536;  // the tie-order rgbds sort starts in big levels above kTieMed
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
@@ -1302,6 +1303,7 @@ int pf_odom_restore(pf_odom* h, const void* buf, size_t size) {
             PF_HIP_TRY(hipMemcpyAsync(map_cur(o)[c], b, sizeof(float4) * hd.map_n[c], hipMemcpyHostToDevice, o.stream));
         b += sizeof(float4) * hd.map_n[c];
     }
+    odom_dep_dirty(o, o.stream);               // the snapshot's maps: checked as host-written ones
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     o.inited = hd.inited != 0;
     o.opt_count_host = hd.opt_count_host;
@@ -1361,8 +1363,13 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
         if (int rc = tie_alloc(*o.tie_a, (size_t)o.cls.nc * o.in_cap)) return rc;
         if (int rc = tie_alloc(*o.tie_b, o.sort_cap)) return rc;
     }
-    if (enable)
+    if (enable) {
         if (int rc = odom_dep_alloc(o)) return rc;
+        if (!o.tie_order) {                             // maps written by the other order's rgbds
+            odom_dep_dirty(o, o.stream);
+            PF_HIP_TRY(hipStreamSynchronize(o.stream));
+        }
+    }
     if ((enable != 0) != o.tie_order) {             // both stages' captured kernel sequences change
         for (int s = 0; s < kSlots; ++s)
             for (hipGraphExec_t* g : {&o.graph_a[s], &o.graph_as[s]})
@@ -1380,6 +1387,34 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
 
 // development / test switch (not part of include/pfilter_hip.h): rgbds in the default order by the
 // full radix sort of every element (the path before the merge) instead of the merge, for A/B checks
+// development / test switch: every tie-order rgbds takes the full dependence table (DepTab in pf_odom.hip:
+// each update starts as if the host had written the map), for the A/B check of the small table
+extern "C" int pf_dev_set_dep_full(pf_odom* h, int enable) {
+    if (!h) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(odom_sync_a(o));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    if ((enable != 0) != o.dep_force_full) drop_graphs_b(o);   // the captured stage B gains / loses a launch
+    o.dep_force_full = enable != 0;
+    return PF_OK;
+}
+
+// development: the dependence flags of the last tie-order rgbds (one byte per element, cnt[C_NRG] of them)
+extern "C" int pf_dev_dep_flags(pf_odom* h, uint8_t* out, size_t cap, int* n) {
+    if (!h || !out || !n) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    if (!o.dep_free) return PF_EINVAL;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    int c[C_COUNT];
+    PF_HIP_TRY(hipMemcpy(c, o.cnt, sizeof(c), hipMemcpyDeviceToHost));
+    *n = c[C_NRG];
+    if ((size_t)c[C_NRG] > cap) return PF_ECAPACITY;
+    PF_HIP_TRY(hipMemcpy(out, o.dep_free, (size_t)c[C_NRG], hipMemcpyDeviceToHost));
+    return PF_OK;
+}
+
 // development: the separate k_observe launch at weightType 0 too (the path before the fused observe)
 extern "C" int pf_dev_set_fuse_observe(pf_odom* h, int enable) {
     if (!h) return PF_EINVAL;

@@ -272,9 +272,12 @@ struct OdomGPU {
     u32* dep_slot = nullptr;       // [sort_cap] each element's slot (0xFFFFFFFF: cropped)
     u8* dep_free = nullptr;        // [sort_cap] 1 = the element's group is order-free
     u32 dep_hbits = 0;             // dep_h = 1 << dep_hbits
+    bool dep_force_full = false;   // pf_dev_set_dep_full
+    u32* dep_dirty = nullptr;      // [2] the map may hold two points of a voxel / k_rg_tail's verdict (DepTab)
 };
 // the dependence table of the tie-order rgbds (allocated with the tie sorts, pf_odom_set_tie_order)
 int odom_dep_alloc(OdomGPU& o);
+void odom_dep_dirty(OdomGPU& o, hipStream_t s);   // the maps were written by the host or initMapWithPoints
 
 // Stage A keeps off the last CUs of the device by default: with one sequence per GPU, stage B's LM
 // (kLmBlocks co-resident workgroups) otherwise waits for stage A's waves to drain. Measured on one

@@ -1805,9 +1805,16 @@ __global__ void __launch_bounds__(256) k_rg_append_minmax(DevState* __restrict__
 // observable only through groups whose f32 sum depends on that order: a group of one or two points is
 // order-free (0 + a is exact and + commutes), a group of three is order-free when its three left folds
 // ((0 + a) + b) + c, ((0 + a) + c) + b and ((0 + b) + c) + a agree bit for bit in x, y and z (the first two
-// terms commute), and a larger group counts as order-dependent. The key kernels insert every element into
-// an open-addressing table (key -> count and the first three elements); k_rg_dep lets the first element of
-// every group decide it, marks its members and empties the slot for the next update.
+// terms commute), and a larger group counts as order-dependent. The key kernels insert elements into an
+// open-addressing table (key -> count and the first three elements), k_rg_dep decides every group from
+// its slot, marks its members and empties the slot for the next update.
+// The map an rgbds writes holds one centroid per voxel, so two map points share a voxel only when a
+// centroid rounds across a voxel face (k_rg_tail checks every kept centroid against its voxel) or the
+// host wrote the map (initMapWithPoints, set_map, restore, the switch into this order). While neither
+// happened (dirty[0] == 0, k_rg_write moves k_rg_tail's verdict there) a group of three or more holds at
+// least two appended points, so only the appended points (a few thousand) go into a small table (the
+// first 2^kDepSmallBits slots) and the map points only probe it (k_rg_dep_probe, read-only unless their
+// voxel is there): configs[4]'s 2M-point map no longer inserts two million elements per frame.
 struct DepTab {
     u32* key;
     u32* cnt;
@@ -1815,18 +1822,34 @@ struct DepTab {
     u32* slot;
     u8* freef;
     u32 hbits;
+    u32* dirty;          // [0]: the map may hold two points of one voxel; [1]: k_rg_tail's verdict
 };
 constexpr u32 kDepEmpty = 0xFFFFFFFFu;
+constexpr u32 kDepSmallBits = 16;
+constexpr int kDepSmallApp = 1 << (kDepSmallBits - 2);   // appended points the small table takes
 
-__device__ __forceinline__ void dep_insert(const DepTab& T, u32 key, u32 e) {
+// this update's table: the small one (clean map, few appended points) or the full one
+template <int NC>
+__device__ __forceinline__ bool dep_small(const DepTab& T, const int* cnt) {
+    if (!T.key || !T.dirty || T.dirty[0] != 0u) return false;
+    int na = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) na += cnt[C_DS + c];
+    return na <= kDepSmallApp;
+}
+
+__device__ __forceinline__ u32 dep_hash(u32 key, u32 bits) { return (key * 0x9E3779B1u) >> (32u - bits); }
+
+__device__ __forceinline__ void dep_insert(const DepTab& T, u32 key, u32 e, bool small = false) {
     if (!T.key) return;
     if (key == kSentinel) {                        // cropped: in no voxel
         T.slot[e] = kDepEmpty;
         T.freef[e] = 1;
         return;
     }
-    const u32 mask = (1u << T.hbits) - 1u;
-    u32 sl = (key * 0x9E3779B1u) >> (32u - T.hbits);
+    const u32 bits = small ? kDepSmallBits : T.hbits;
+    const u32 mask = (1u << bits) - 1u;
+    u32 sl = dep_hash(key, bits);
     for (;;) {
         const u32 old = atomicCAS(&T.key[sl], kDepEmpty, key);
         if (old == kDepEmpty || old == key) break;
@@ -1836,6 +1859,18 @@ __device__ __forceinline__ void dep_insert(const DepTab& T, u32 key, u32 e) {
     if (c < 3u) T.mem[3u * sl + c] = e;
     T.slot[e] = sl;
     T.freef[e] = 0;
+}
+
+// an element of the key kernels: appended points always go into the table, map points only when the
+// map may hold two points of a voxel (otherwise k_rg_dep_probe looks them up)
+__device__ __forceinline__ void dep_element(const DepTab& T, u32 key, u32 e, bool appended, bool small) {
+    if (!T.key) return;
+    if (small && !appended) {
+        T.slot[e] = kDepEmpty;
+        T.freef[e] = 1;
+        return;
+    }
+    dep_insert(T, key, e, small);
 }
 
 __device__ __forceinline__ bool folds_agree(float4 a, float4 b, float4 c) {
@@ -1851,25 +1886,66 @@ __device__ __forceinline__ bool folds_agree(float4 a, float4 b, float4 c) {
     return same;
 }
 
+// the small table's map members: a map point joins the group of its voxel when appended points are there
+template <int NC>
+__global__ void __launch_bounds__(256) k_rg_dep_probe(const int* __restrict__ cnt, const u32* __restrict__ keys,
+                                                      DepTab T) {
+    if (!dep_small<NC>(T, cnt)) return;
+    const RgView<NC> V = rg_view<NC>(cnt, Clouds{}, Clouds{});
+    const int n = V.total();
+    const u32 mask = (1u << kDepSmallBits) - 1u;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        int c, li;
+        bool ap;
+        V.locate(e, c, li, ap);
+        const u32 key = keys[e];
+        if (ap || key == kSentinel) continue;
+        u32 sl = dep_hash(key, kDepSmallBits);
+        for (;;) {
+            const u32 k = T.key[sl];
+            if (k == kDepEmpty) break;
+            if (k == key) {
+                const u32 m = atomicAdd(&T.cnt[sl], 1u);
+                if (m < 3u) T.mem[3u * sl + m] = (u32)e;
+                T.slot[e] = sl;
+                T.freef[e] = 0;
+                break;
+            }
+            sl = (sl + 1u) & mask;
+        }
+    }
+}
+
+// decides every group of the table: one thread per group
+template <int NC>
+__device__ __forceinline__ void dep_decide(const DepTab& T, const RgView<NC>& V, u32 sl) {
+    const u32 c = T.cnt[sl];
+    bool fre = c <= 2u;
+    if (c == 3u) {
+        int cc;
+        const float4 a = V.at((int)T.mem[3u * sl], cc), b = V.at((int)T.mem[3u * sl + 1u], cc),
+                     d = V.at((int)T.mem[3u * sl + 2u], cc);
+        fre = folds_agree(a, b, d);
+    }
+    if (fre)
+        for (u32 j = 0; j < c; ++j) T.freef[T.mem[3u * sl + j]] = 1;
+    T.key[sl] = kDepEmpty;
+    T.cnt[sl] = 0u;
+}
+
 template <int NC>
 __global__ void __launch_bounds__(256) k_rg_dep(const int* __restrict__ cnt, Clouds map, Clouds app, DepTab T) {
     const RgView<NC> V = rg_view<NC>(cnt, map, app);
+    if (dep_small<NC>(T, cnt)) {                   // the small table's slots
+        for (u32 sl = blockIdx.x * blockDim.x + threadIdx.x; sl < (1u << kDepSmallBits); sl += gridDim.x * blockDim.x)
+            if (T.key[sl] != kDepEmpty) dep_decide(T, V, sl);
+        return;
+    }
     const int n = V.total();
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
         const u32 sl = T.slot[e];
         if (sl == kDepEmpty || T.mem[3u * sl] != (u32)e) continue;   // only the group's first element
-        const u32 c = T.cnt[sl];
-        bool fre = c <= 2u;
-        if (c == 3u) {
-            int cc;
-            const float4 a = V.at((int)T.mem[3u * sl], cc), b = V.at((int)T.mem[3u * sl + 1u], cc),
-                         d = V.at((int)T.mem[3u * sl + 2u], cc);
-            fre = folds_agree(a, b, d);
-        }
-        if (fre)
-            for (u32 j = 0; j < c; ++j) T.freef[T.mem[3u * sl + j]] = 1;
-        T.key[sl] = kDepEmpty;
-        T.cnt[sl] = 0u;
+        dep_decide(T, V, sl);
     }
 }
 
@@ -1882,6 +1958,7 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
     sort_hist_begin(lh);
     const RgView<NC> V = rg_view<NC>(cnt, map, app);
     const int n = V.total();
+    const bool small = dep_small<NC>(dt, cnt);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         int c;
         const float4 p = V.at(i, c);
@@ -1889,7 +1966,7 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
         if (!in_crop(st, p)) {
             keys[i] = kSentinel;
             sort_hist_add(lh, kSentinel, sh.passes);
-            dep_insert(dt, kSentinel, (u32)i);
+            dep_element(dt, kSentinel, (u32)i, false, false);
             continue;
         }
         const float lf = leaf.at(c);
@@ -1905,7 +1982,10 @@ __global__ void __launch_bounds__(256) k_rg_keys(const DevState* __restrict__ st
         const int idx = i0 * 1 + i1 * div[0] + i2 * (div[0] * div[1]);
         keys[i] = ((u32)idx & 0x3fffffffu) | ((u32)c << 30);
         sort_hist_add(lh, keys[i], sh.passes);
-        dep_insert(dt, keys[i], (u32)i);
+        int cc, li;
+        bool ap;
+        V.locate(i, cc, li, ap);
+        dep_element(dt, keys[i], (u32)i, ap, small);
     }
     sort_hist_end(lh, sh, n, n);
 }
@@ -1937,6 +2017,7 @@ __global__ void __launch_bounds__(256) k_rg_append_keys(DevState* __restrict__ s
     const float hi[3] = {(float)(prm[4] + 100), (float)(prm[5] + 100), (float)(prm[6] + 100)};
     const RgView<NC> V = rg_view<NC>(cnt, map, Clouds{{app.p[0], app.p[1], app.p[2]}});
     const int n = V.total();
+    const bool small = dep_small<NC>(dt, cnt);
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt[C_NRG] = n;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
         int c, li;
@@ -1967,7 +2048,7 @@ __global__ void __launch_bounds__(256) k_rg_append_keys(DevState* __restrict__ s
         }
         keys[i] = key;
         sort_hist_add(lh, key, sh.passes);
-        dep_insert(dt, key, (u32)i);
+        dep_element(dt, key, (u32)i, ap, small);
     }
     const int items = n < nblk * 256 ? n : nblk * 256;  // blocks holding keys: the first ceil(items / 256)
     sort_hist_end(lh, sh, n, items);
@@ -1995,6 +2076,8 @@ struct RgTailArgs {
     u64* status;           // look-back words (zero between calls)
     u32* arrive;
     int* err;
+    VgLeaf leaf;           // the classes' voxel sizes (the centroid check)
+    u32* dirty;            // DepTab::dirty (tie order) or null: [1] |= a kept centroid left its voxel
 };
 
 // The rest of addPointsToMap in one pass over the sorted keys (one tile of 256 x kTailPer keys per
@@ -2057,6 +2140,7 @@ __global__ void __launch_bounds__(256) k_rg_tail(RgTailArgs a) {
             int r_max = -1;
             float g_max = -1;
             int e = i;
+            float4 p0 = make_float4(0.f, 0.f, 0.f, 0.f);        // the voxel's first point
             for (;;) {
                 float4 p;
                 if (e - base < kPer) {
@@ -2067,6 +2151,7 @@ __global__ void __launch_bounds__(256) k_rg_tail(RgTailArgs a) {
                     int c;
                     p = V.at((int)a.vals[e], c);
                 }
+                if (e == i) p0 = p;
                 cx += p.x; cy += p.y; cz += p.z;
                 const int r = (int)w_r(p);
                 const float g = (float)w_g(p);
@@ -2083,6 +2168,12 @@ __global__ void __launch_bounds__(256) k_rg_tail(RgTailArgs a) {
             const u32 aged = r > 250 ? 255u : r + 2u;                   // :634-646
             out[j] = make_float4(cx / nn, cy / nn, cz / nn, __uint_as_float(pack_rg(aged, g)));
             if (!drop) keepm |= 1u << j;
+            if (!drop && a.dirty) {                             // the centroid's voxel, keyed as the next update will
+                const float lf = a.leaf.at((int)(k[j + 1] >> 30));
+                if (floorf(out[j].x / lf) != floorf(p0.x / lf) || floorf(out[j].y / lf) != floorf(p0.y / lf) ||
+                    floorf(out[j].z / lf) != floorf(p0.z / lf))
+                    atomicOr(a.dirty + 1, 1u);
+            }
         }
         u32 agg;
         const u32 tex = block_excl_scan256((u32)__popc(keepm), lw, agg);
@@ -2116,9 +2207,13 @@ __global__ void __launch_bounds__(256) k_rg_tail(RgTailArgs a) {
 // the kept voxels into the class maps (class c's are seg_out[kb(c) .. kb(c + 1)), in order)
 template <int NC>
 __global__ void __launch_bounds__(256) k_rg_write(int* __restrict__ cnt, const float4* __restrict__ seg_out,
-                                                   CloudsW map) {
+                                                   CloudsW map, u32* __restrict__ dirty) {
     constexpr int nc = NC;
     const int total = cnt[C_KEEP_TOTAL];
+    if (dirty && blockIdx.x == 0 && threadIdx.x == 0) {   // k_rg_tail's verdict on the map written here
+        dirty[0] = dirty[1];
+        dirty[1] = 0u;
+    }
     int kb[kMaxC + 1];                             // kept-voxel start of every class
     kb[0] = 0;
 #pragma unroll
@@ -3108,6 +3203,18 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
 
 // back to the state after init (identity pose, empty maps, optimization_count 2), keeping every
 // allocation and captured graph: the next frame seeds the maps again
+__global__ void k_dep_dirty(u32* dirty) {
+    if (threadIdx.x == 0) {
+        dirty[0] = 1u;
+        dirty[1] = 0u;
+    }
+}
+
+// the maps were written other than by the tie-order rgbds: the next one takes the full table (DepTab)
+void odom_dep_dirty(OdomGPU& o, hipStream_t s) {
+    if (o.dep_dirty) hipLaunchKernelGGL(k_dep_dirty, dim3(1), dim3(64), 0, s, o.dep_dirty);
+}
+
 // the table holds every element of one rgbds call (at most sort_cap) at a load of at most 0.8
 int odom_dep_alloc(OdomGPU& o) {
     if (o.dep_key) return PF_OK;
@@ -3117,9 +3224,11 @@ int odom_dep_alloc(OdomGPU& o) {
     if (hipMalloc(&o.dep_key, sizeof(u32) * h) != hipSuccess || hipMalloc(&o.dep_cnt, sizeof(u32) * h) != hipSuccess ||
         hipMalloc(&o.dep_mem, sizeof(u32) * 3 * h) != hipSuccess ||
         hipMalloc(&o.dep_slot, sizeof(u32) * o.sort_cap) != hipSuccess ||
-        hipMalloc(&o.dep_free, o.sort_cap) != hipSuccess)
+        hipMalloc(&o.dep_free, o.sort_cap) != hipSuccess || hipMalloc(&o.dep_dirty, sizeof(u32) * 2) != hipSuccess)
         return PF_ENOMEM;
-    if (hipMemset(o.dep_key, 0xFF, sizeof(u32) * h) != hipSuccess || hipMemset(o.dep_cnt, 0, sizeof(u32) * h) != hipSuccess)
+    const u32 dirty0[2] = {1u, 0u};
+    if (hipMemset(o.dep_key, 0xFF, sizeof(u32) * h) != hipSuccess || hipMemset(o.dep_cnt, 0, sizeof(u32) * h) != hipSuccess ||
+        hipMemcpy(o.dep_dirty, dirty0, sizeof(dirty0), hipMemcpyHostToDevice) != hipSuccess)
         return PF_EHIP;
     o.dep_hbits = hb;
     return PF_OK;
@@ -3228,7 +3337,8 @@ void odom_destroy(OdomGPU& o) {
             tie_free(*t);
             delete t;
         }
-    for (void* q : {(void*)o.dep_key, (void*)o.dep_cnt, (void*)o.dep_mem, (void*)o.dep_slot, (void*)o.dep_free})
+    for (void* q : {(void*)o.dep_key, (void*)o.dep_cnt, (void*)o.dep_mem, (void*)o.dep_slot, (void*)o.dep_free,
+                    (void*)o.dep_dirty})
         (void)hipFree(q);
     o = OdomGPU{};
 }
@@ -3279,6 +3389,7 @@ void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s) {
     const int nc = o.cls.nc;
     hipLaunchKernelGGL(k_pull_counts, dim3(1), dim3(64), 0, s, o.cnt, sb.cnt);
     PF_LAUNCH_NC(nc, k_init_map, dim3(kGrid), dim3(256), 0, s, o.cnt, clouds(sb.in), clouds_w(map_cur(o)));
+    odom_dep_dirty(o, s);                                // initMapWithPoints: several points per voxel
     hipLaunchKernelGGL(k_init_counts, dim3(1), dim3(64), 0, s, o.cnt, o.st, nc);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, o.st, o.poses, (int)o.pose_cap, 0, o.acc);
     o.opt_count_host = 12;
@@ -3345,7 +3456,9 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     }
     o.dims_fresh = false;
     // the order-free voxel groups (the heap tier's dependence flags) in the tie order
-    const DepTab dt{o.tie_order ? o.dep_key : nullptr, o.dep_cnt, o.dep_mem, o.dep_slot, o.dep_free, o.dep_hbits};
+    const DepTab dt{o.tie_order ? o.dep_key : nullptr, o.dep_cnt, o.dep_mem, o.dep_slot, o.dep_free, o.dep_hbits,
+                    o.dep_dirty};
+    if (dt.key && o.dep_force_full) odom_dep_dirty(o, s);   // test switch: the full table every update
     if (rg_fused_keys(o.leaf_rg, nc)) {
         PF_LAUNCH_NC(nc, k_rg_append_keys, dim3(kGrid + 1), dim3(256), 0, s, o.st, cnt, o.acc, clouds(map_cur(o)),
                      clouds(sb.ds), clouds_w(o.app), o.poses, (int)o.pose_cap, leaf, o.keys, o.vals,
@@ -3357,17 +3470,21 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
                      leaf, o.keys, o.vals, sort_hist(o.prim, 32, true), dt);
     }
     if (o.tie_order) {                     // std::sort's order of equal keys (:74)
-        if (dt.key) PF_LAUNCH_NC(nc, k_rg_dep, dim3(kGrid), dim3(256), 0, s, cnt, clouds(map_cur(o)), clouds(o.app), dt);
+        if (dt.key) {
+            PF_LAUNCH_NC(nc, k_rg_dep_probe, dim3(kGrid), dim3(256), 0, s, cnt, o.keys, dt);
+            PF_LAUNCH_NC(nc, k_rg_dep, dim3(kGrid), dim3(256), 0, s, cnt, clouds(map_cur(o)), clouds(o.app), dt);
+        }
         tie_sort(*o.tie_b, o.keys, o.vals, TieClasses{cnt, C_M, C_DS, nc}, o.prim.err, s,
                  std::max(tie_levels_for(*o.tie_b, o.tie_hint), PF_TIE_LEVELS_B), dt.key ? o.dep_free : nullptr);
     }
     else
         radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);
+    u32* dirty = o.tie_order ? o.dep_dirty : nullptr;
     RgTailArgs ta{cnt, clouds(map_cur(o)), clouds(o.app), o.keys, o.vals, o.seg_out, o.prm.k_new, o.prm.theta_p,
-                  o.prm.theta_max, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err};
+                  o.prm.theta_max, o.tail_status, (u32*)(o.tail_status + o.tail_tiles), o.prim.err, leaf, dirty};
     const unsigned tail_grid = (unsigned)(o.tail_tiles < (size_t)kSortMaxBlocks ? o.tail_tiles : kSortMaxBlocks);
     PF_LAUNCH_NC(nc, k_rg_tail, dim3(tail_grid > 0 ? tail_grid : 1), dim3(256), 0, s, ta);
-    PF_LAUNCH_NC(nc, k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, clouds_w(map_next(o)));
+    PF_LAUNCH_NC(nc, k_rg_write, dim3(kGrid), dim3(256), 0, s, cnt, o.seg_out, clouds_w(map_next(o)), dirty);
 }
 
 // the association kNN probe (pf_odom.h)

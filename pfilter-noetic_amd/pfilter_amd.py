@@ -569,6 +569,13 @@ class Odom_ES_EstimationClass:
         L.pf_dev_set_rg_radix.argtypes = [_vp, _i]
         _check("pf_dev_set_rg_radix", L.pf_dev_set_rg_radix(self._h, int(bool(enable))))
 
+    def set_dep_full(self, enable):
+        """development switch pf_dev_set_dep_full: every tie-order rgbds takes the full dependence table
+        (each update as if the host had written the map) instead of the appended points' small table"""
+        L = lib()
+        L.pf_dev_set_dep_full.argtypes = [_vp, _i]
+        _check("pf_dev_set_dep_full", L.pf_dev_set_dep_full(self._h, int(bool(enable))))
+
     def set_fuse_observe(self, enable):
         """development switch pf_dev_set_fuse_observe: False = the separate k_observe launch at weightType 0"""
         L = lib()

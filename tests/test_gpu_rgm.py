@@ -96,3 +96,56 @@ def test_merge_bpf_three_classes(pa, pfsynth):
     for w in range(3):
         assert np.array_equal(out[0][1][w][0].view(np.uint32), out[1][1][w][0].view(np.uint32)), w
         assert np.array_equal(out[0][1][w][1], out[1][1][w][1]), w
+
+
+# ---- the tie order's dependence table (pf_odom.hip DepTab) --------------------------------------------
+# While the map holds one centroid per voxel (no host write since the last rgbds, no centroid rounded
+# across a voxel face), a group of three or more holds two appended points, so only the appended points
+# go into a small table and the map points probe it; the full table takes every element. The flags are
+# the heap tier's pop bound, so any difference shows in the map bytes: both runs must be bit-identical.
+def _tie_run(pa, pfsynth, preset, frames, full, theta=(0.4, 75), lines=64, set_map_at=None, big_map=False):
+    seq = pfsynth.Sequence(preset, n_frames=frames, seed=0)
+    od = pa.Odom_ES_EstimationClass(device=0, max_points=300000, map_capacity=1 << 22, tie_order=True)
+    if lines == 128:
+        od.init(pa.make_lidar(128, 3.0, 90.0, 0.1, ring_model=(15.0, -25.0)), 0.4, 0, theta[0], theta[1], 0)
+    else:
+        od.init(pa.make_lidar(lines, 3.0, 90.0), 0.4, 0, theta[0], theta[1], 0)
+    od.set_dep_full(full)
+    buf, cnt = seq.frames(0, frames, threads=16)
+    db = pa.DeviceBuffer(buf.nbytes)
+    db.upload(buf)
+    try:
+        for i in range(frames):
+            if set_map_at is not None and i == set_map_at:
+                od.sync()
+                if big_map:                          # configs[4]: the 2M-point surf map
+                    m = pfsynth.voxel_map(2_000_000, 0.8, seed=5)
+                    od.set_map(1, m, np.zeros((m.shape[0], 2), np.uint8))
+                else:                                # a host write: shuffled, several frames later
+                    for which in (0, 1):
+                        xyz, rg = od._map(which)
+                        perm = np.random.default_rng(which).permutation(xyz.shape[0])
+                        od.set_map(which, xyz[perm], rg[perm])
+            od.frame_device(db.ptr + i * buf.shape[1] * 16, int(cnt[i]))
+        od.sync()
+        return od.poses(), [od._map(w) for w in (0, 1)], None
+    finally:
+        db.free()
+
+
+@pytest.mark.parametrize("preset,frames,theta,lines,set_map_at", [
+    ("S64", 600, (0.4, 75), 64, None),    # configs[1]
+    ("S64", 200, (0.0, 0), 64, 120),      # configs[0], a host map write half way
+    ("S64V", 200, (0.4, 75), 64, None),   # the dense scene
+])
+def test_dep_small_table_equals_full(pa, pfsynth, preset, frames, theta, lines, set_map_at):
+    a = _tie_run(pa, pfsynth, preset, frames, False, theta, lines, set_map_at)
+    b = _tie_run(pa, pfsynth, preset, frames, True, theta, lines, set_map_at)
+    _same(a, b)
+
+
+def test_dep_small_table_configs4(pa, pfsynth):
+    """configs[4]: S128 scans against the 2M-point surf map (set after frame 1), 12 frames"""
+    a = _tie_run(pa, pfsynth, "S128", 12, False, (0.0, 0), 128, set_map_at=1, big_map=True)
+    b = _tie_run(pa, pfsynth, "S128", 12, True, (0.0, 0), 128, set_map_at=1, big_map=True)
+    _same(a, b)

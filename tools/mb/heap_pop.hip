@@ -1,0 +1,561 @@
+// Microbenchmark + check: __sort_heap's pipelined pops in one wave (gfx950), the shipped engine (pf_tie.hip
+// heap_step: a pop may start only on the first step of a pair) against a candidate (a pop may start on any
+// step two or more steps after the previous one; the lane that would start loads the root's children in
+// the same instruction as every other lane's children, and the ancestor test + ballot run while the loads
+// are in flight). Both are checked against std::make_heap + std::sort_heap (libstdc++'s __make_heap /
+// __sort_heap, what introsort's depth-limit branch runs) on tie-heavy and ordered inputs.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb/heap_pop.hip -o /tmp/heap_pop && /tmp/heap_pop
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+typedef unsigned int u32;
+typedef unsigned long long u64;
+constexpr int kT = 1024;
+constexpr int kCap = 20480 - 128;     // entries in LDS (+ 64 spare slots)
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); std::exit(1); } } while (0)
+
+__device__ __forceinline__ int hlev(int x) { return 31 - __clz(x + 1); }
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// ---- shipped engine (pf_tie.hip heap_step, LDS form) ----
+struct HeapPops {
+    int nxt;
+    bool act;
+    int h, m;
+    uint2 vk;
+};
+template <bool MAY>
+__device__ __forceinline__ void heap_step(uint2* H2, HeapPops& P, int npops, int l, int spare, int last) {
+    bool start = false, mine = false;
+    int q = 0;
+    if (MAY) {
+        q = last - P.nxt;
+        const int sh = hlev(q) - hlev(P.h);
+        const bool blk = P.act && sh >= 0 && ((q + 1) >> sh) == P.h + 1;
+        start = P.nxt < npops && __ballot(blk) == 0;
+        mine = start && l == (P.nxt & 63);
+        P.h = mine ? 0 : P.h;
+        P.m = mine ? q : P.m;
+        P.act = P.act || mine;
+    }
+    const int c1 = 2 * P.h + 1;
+    const bool has = P.act && c1 < P.m;
+    const int cr = has ? c1 : 0;
+    const uint2 a = H2[cr], b = H2[cr + 1];
+    if (MAY) {
+        const uint2 vq = H2[q], r0 = H2[0];
+        P.vk = mine ? vq : P.vk;
+        H2[mine ? q : spare] = r0;
+    }
+    const bool right = c1 + 1 < P.m && !(b.y < a.y);
+    const uint2 ch = right ? b : a;
+    const bool stop = !has || ch.y < P.vk.y;
+    H2[P.act ? P.h : spare] = stop ? P.vk : ch;
+    P.h = P.act ? (right ? c1 + 1 : c1) : P.h;
+    P.act = P.act && !stop;
+    P.nxt += start ? 1 : 0;
+    asm volatile("" ::: "memory");
+}
+__device__ u64 pops_v1(uint2* H, int n, int npops, int spare) {
+    const int l = lane_id();
+    u64 steps = 0;
+    HeapPops P{0, false, 0, 0, make_uint2(0u, 0u)};
+    for (;;) {
+        heap_step<true>(H, P, npops, l, spare + l, n - 1);
+        heap_step<false>(H, P, npops, l, spare + l, n - 1);
+        steps += 2;
+        if (P.nxt >= npops && __ballot(P.act) == 0) break;
+        if (steps > 64ull * (u64)n + 1000ull) break;            // benchmark guard
+    }
+    return steps;
+}
+
+// ---- candidate engine ----
+// Lane j % 64 runs pop j. A pop may start on any step at least two steps after the previous start (so the
+// previous pop has written its level-1 hole and never touches levels 0 and 1 again), and not while an
+// in-flight hole is q (the heap's last element, the new pop's value) or an ancestor of q. The lane that
+// would start is idle (its previous pop, 64 pops earlier, is long finished), so it loads the root's
+// children with the same instruction as the other lanes; the ancestor test and the ballot overlap the loads.
+__device__ u64 pops_v2(uint2* H, int n, int npops, int spare) {
+    const int l = lane_id();
+    const int last = n - 1;
+    int nxt = 0, since = 2;
+    bool act = false;
+    int h = 0, m = 0;
+    uint2 vk = make_uint2(0u, 0u);
+    u64 steps = 0;
+    for (;;) {
+        const int q = last - nxt;                               // wave-uniform
+        const bool can = nxt < npops && since >= 2;             // wave-uniform
+        const bool cand = can && l == (nxt & 63);
+        const int hh = cand ? 0 : h;
+        const int mm = cand ? q : m;
+        const int c1 = 2 * hh + 1;
+        const bool has = (act || cand) && c1 < mm;
+        const int cr = has ? c1 : 0;
+        const uint2 a = H[cr], b = H[cr + 1];
+        const uint2 vq = H[q], r0 = H[0];
+        bool start = false;
+        if (can) {
+            const int sh = hlev(q) - hlev(h);
+            const bool blk = act && sh >= 0 && ((q + 1) >> sh) == h + 1;
+            start = __ballot(blk) == 0;
+        }
+        const bool mine = cand && start;
+        const bool ae = act || mine;
+        const uint2 v = mine ? vq : vk;
+        const bool right = c1 + 1 < mm && !(b.y < a.y);
+        const uint2 ch = right ? b : a;
+        const bool stop = !(has && ae) || ch.y < v.y;
+        H[ae ? hh : spare] = stop ? v : ch;
+        H[mine ? q : spare] = r0;
+        asm volatile("" ::: "memory");
+        h = right ? c1 + 1 : c1;
+        m = mm;
+        vk = v;
+        act = ae && !stop;
+        nxt += start ? 1 : 0;
+        since = start ? 1 : since + 1;
+        ++steps;
+        if (nxt >= npops && __ballot(act) == 0) break;
+        if (steps > 64ull * (u64)n + 1000ull) break;            // benchmark guard
+    }
+    return steps;
+}
+
+
+// ---- candidate v3: sentinels instead of bounds, a spare hole instead of an activity flag ----
+// Keys are stored + 1, so {0, 0} is below every key: H[n], H[n + 1] hold it, a pop writes it at q (the
+// position it vacates) and sends the root to the output, so a child past the pop's heap reads as absent
+// without a per-lane heap size; the children of any hole at or past n are read at n (clamped). A lane
+// with no pop in flight parks its hole at its own spare slot n + 2 + l, whose children are sentinels, so it
+// stops every step and writes only its spare: no activity mask. The start is decided before the step's
+// loads (ancestor test, ballot); the new pop's lane then takes hole 0.
+__device__ u64 pops_v3(uint2* H, int n, int npops, u64* out) {
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    int nxt = 0, since = 2;
+    int h = spare;
+    uint2 v = make_uint2(0u, 1u);                               // above the sentinels: an idle lane stops
+    u64 steps = 0;
+    const u32 nb = (u32)n * 8u;
+    char* Hb = reinterpret_cast<char*>(H);
+    for (;;) {
+        if (since >= 2 && nxt < npops) {                       // wave-uniform
+            const int q = last - nxt;
+            const int sh = (31 - __clz(q + 1)) - (31 - __clz(h + 1));
+            const bool blk = sh >= 0 && ((q + 1) >> sh) == h + 1;
+            if (__ballot(blk) == 0) {
+                if (l == (nxt & 63)) {
+                    v = H[q];
+                    const uint2 r = H[0];
+                    H[q] = make_uint2(0u, 0u);
+                    out[q] = ((u64)(r.y - 1u) << 32) | r.x;
+                    h = 0;
+                }
+                ++nxt;
+                since = 0;
+            }
+        }
+        ++since;
+        const u32 ca = min((u32)h * 16u + 8u, nb);             // byte offset of child 2h + 1, clamped to n
+        const uint2 a = *reinterpret_cast<const uint2*>(Hb + ca);
+        const uint2 b = *reinterpret_cast<const uint2*>(Hb + ca + 8u);
+        const bool right = !(b.y < a.y);
+        const uint2 ch = right ? b : a;
+        const bool stop = ch.y < v.y;
+        H[h] = stop ? v : ch;
+        asm volatile("" ::: "memory");
+        h = stop ? spare : 2 * h + 1 + (right ? 1 : 0);
+        ++steps;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64ull * (u64)n + 1000ull) break;            // benchmark guard
+    }
+    return steps;
+}
+
+
+// ---- candidate v4: v3's sentinels and spare holes, with the start off the step's dependent chain ----
+// The lane that would start (nxt % 64, idle) addresses the root's children before the start is decided,
+// the new pop's value H[q] and the root H[0] are read with the step's children (broadcast), and the
+// ancestor test for the next step is taken on both children of the current hole while the loads are in
+// flight (if a pop starts this step, the next step cannot start one, so q is the same when it is used).
+__device__ __forceinline__ bool anc_or_self(int x, int q) {      // x is q or an ancestor of q (0-based heap)
+    const int sh = __clz(x + 1) - __clz(q + 1);
+    return sh >= 0 && ((q + 1) >> sh) == x + 1;
+}
+__device__ u64 pops_v4(uint2* H, int n, int npops, u64* out) {
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    int nxt = 0, since = 2;
+    int h = spare;
+    uint2 v = make_uint2(0u, 1u);
+    bool blk = false;                                            // my hole is q or an ancestor of q
+    u64 steps = 0;
+    const u32 nb = (u32)n * 8u;
+    char* Hb = reinterpret_cast<char*>(H);
+    for (;;) {
+        const bool elig = since >= 2 && nxt < npops;             // wave-uniform
+        const int q = last - nxt;
+        const bool cand = elig && l == (nxt & 63);
+        const int hh = cand ? 0 : h;
+        const u32 ca = min((u32)hh * 16u + 8u, nb);
+        const uint2 a = *reinterpret_cast<const uint2*>(Hb + ca);
+        const uint2 b = *reinterpret_cast<const uint2*>(Hb + ca + 8u);
+        const uint2 vq = H[q], r0 = H[0];
+        const bool start = elig && __ballot(blk) == 0;           // wave-uniform
+        const bool mine = cand && start;
+        const bool dead = cand && !start;                        // the candidate lane stays idle
+        const int c1 = 2 * hh + 1;
+        const bool aL = anc_or_self(c1, q), aR = anc_or_self(c1 + 1, q);
+        const uint2 vv = mine ? vq : v;
+        const bool right = !(b.y < a.y);
+        const uint2 ch = right ? b : a;
+        const bool stop = dead || ch.y < vv.y;
+        H[dead ? spare : hh] = stop ? vv : ch;
+        if (mine) {
+            H[q] = make_uint2(0u, 0u);
+            out[q] = ((u64)(r0.y - 1u) << 32) | r0.x;
+        }
+        asm volatile("" ::: "memory");
+        v = vv;
+        h = stop ? spare : c1 + (right ? 1 : 0);
+        blk = !stop && (right ? aR : aL);
+        nxt += start ? 1 : 0;
+        since = start ? 1 : since + 1;
+        ++steps;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64ull * (u64)n + 1000ull) break;            // benchmark guard
+    }
+    return steps;
+}
+
+
+// ---- candidate v5: branch-free steps. Entries {position in the segment, key + 1}; a pop marks the position it
+// vacates {root's position, 0} (a sentinel that still names the popped element), so the output is read back
+// through the positions at the end. The root's position rides in a wave-uniform register (read from the lane
+// that wrote the root), the new pop's value H[q] is prefetched after the previous step's writes, and the
+// ancestor test for the next step is taken on both children during the loads.
+template <int U>
+__device__ u64 pops_v5(uint2* H, int n, int npops) {
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    int nxt = 0, since = 2;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    bool blk = false;
+    u32 rpos = H[0].x;
+    uint2 vq = H[last];
+    u64 steps = 0;
+    const u32 nb = (u32)n * 8u;
+    char* Hb = reinterpret_cast<char*>(H);
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool elig = since >= 2 && nxt < npops;         // wave-uniform
+            const int q = last - nxt;
+            const bool start = elig && __ballot(blk) == 0;      // wave-uniform
+            const bool mine = start && l == (nxt & 63);
+            const int hh = mine ? 0 : h;
+            const u32 ca = min((u32)hh * 16u + 8u, nb);
+            const uint2 a = *reinterpret_cast<const uint2*>(Hb + ca);
+            const uint2 b = *reinterpret_cast<const uint2*>(Hb + ca + 8u);
+            vx = mine ? vq.x : vx;
+            vy = mine ? vq.y : vy;
+            const int qn = q - (start ? 1 : 0);
+            const int c1 = 2 * hh + 1;
+            const bool aL = anc_or_self(c1, qn), aR = anc_or_self(c1 + 1, qn);
+            const bool right = !(b.y < a.y);
+            const u32 chx = right ? b.x : a.x, chy = right ? b.y : a.y;
+            const bool stop = chy < vy;
+            const u32 wx = stop ? vx : chx, wy = stop ? vy : chy;
+            H[hh] = make_uint2(wx, wy);
+            H[mine ? q : spare] = make_uint2(rpos, 0u);
+            asm volatile("" ::: "memory");
+            if (start) rpos = __builtin_amdgcn_readlane(wx, nxt & 63);
+            h = stop ? spare : c1 + (right ? 1 : 0);
+            blk = !stop && (right ? aR : aL);
+            nxt += start ? 1 : 0;
+            since = start ? 1 : since + 1;
+            vq = H[last - nxt];
+        }
+        steps += U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64ull * (u64)n + 1000ull) break;            // benchmark guard
+    }
+    return steps;
+}
+
+
+// ---- candidate v7: v5 with the schedule pinned (ancestor test between the loads' issue and their use, no
+// branches in the step, SALU-only loop bookkeeping) and the last pops' children inside q handled
+template <int U>
+__device__ int pops_v7(uint2* H, int n, int npops) {
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    int nxt = 0, since = 2;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    bool blk = false;
+    u32 rpos = H[0].x;
+    uint2 vq = H[last];
+    int steps = 0;
+    const u32 nb = (u32)n * 8u;
+    char* Hb = reinterpret_cast<char*>(H);
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool elig = since >= 2 && nxt < npops;         // wave-uniform
+            const int q = last - nxt;
+            const bool start = elig && __ballot(blk) == 0;      // wave-uniform
+            const bool mine = start && l == (nxt & 63);
+            const int hh = mine ? 0 : h;
+            const u32 ca = min((u32)hh * 16u + 8u, nb);
+            uint2 a = *reinterpret_cast<const uint2*>(Hb + ca);
+            uint2 b = *reinterpret_cast<const uint2*>(Hb + ca + 8u);
+            __builtin_amdgcn_sched_barrier(0);
+            const int qn = q - (start ? 1 : 0);
+            const int c1 = 2 * hh + 1;
+            const bool aL = anc_or_self(c1, qn), aR = anc_or_self(c1 + 1, qn);
+            const u32 nvx = mine ? vq.x : vx, nvy = mine ? vq.y : vy;
+            const bool lowq = mine && q <= 2;                    // the last pops: q is a child of the root
+            __builtin_amdgcn_sched_barrier(0);
+            a.y = (lowq && q <= 1) ? 0u : a.y;
+            b.y = lowq ? 0u : b.y;
+            const bool right = !(b.y < a.y);
+            const u32 chx = right ? b.x : a.x, chy = right ? b.y : a.y;
+            const bool stop = chy < nvy;
+            const u32 wx = stop ? nvx : chx, wy = stop ? nvy : chy;
+            H[hh] = make_uint2(wx, wy);
+            H[mine ? q : spare] = make_uint2(rpos, 0u);
+            asm volatile("" ::: "memory");
+            const u32 rl = __builtin_amdgcn_readlane(wx, nxt & 63);
+            rpos = start ? rl : rpos;
+            vx = nvx;
+            vy = nvy;
+            h = stop ? spare : c1 + (right ? 1 : 0);
+            blk = !stop && (right ? aR : aL);
+            nxt += start ? 1 : 0;
+            since = start ? 1 : since + 1;
+            vq = H[last - nxt];
+        }
+        steps += U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
+template <int U>
+__device__ int pops_v9(uint2* H, int n, int npops) {
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    int nxt = 0, since = 2;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    bool blk = false;
+    u32 rpos = H[0].x;
+    uint2 vq = H[last];
+    int steps = 0;
+    const u32 nb = (u32)n * 8u;
+    char* Hb = reinterpret_cast<char*>(H);
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool elig = since >= 2 && nxt < npops;         // wave-uniform
+            const int q = last - nxt;
+            const bool start = elig && __ballot(blk) == 0;      // wave-uniform
+            const bool cand = elig && l == (nxt & 63);          // idle: its last pop is 64 pops old
+            const bool mine = start && cand;
+            const bool dead = cand && !start;
+            const int hh = cand ? 0 : h;
+            const u32 ca = min((u32)hh * 16u + 8u, nb);
+            uint2 a = *reinterpret_cast<const uint2*>(Hb + ca);
+            uint2 b = *reinterpret_cast<const uint2*>(Hb + ca + 8u);
+            __builtin_amdgcn_sched_barrier(0);
+            const int qn = q - (start ? 1 : 0);
+            const int c1 = 2 * hh + 1;
+            const bool aL = anc_or_self(c1, qn), aR = anc_or_self(c1 + 1, qn);
+            const u32 nvx = mine ? vq.x : vx, nvy = mine ? vq.y : vy;
+            const bool lowq = mine && q <= 2;                    // the last pops: q is a child of the root
+            __builtin_amdgcn_sched_barrier(0);
+            a.y = (lowq && q <= 1) ? 0u : a.y;
+            b.y = lowq ? 0u : b.y;
+            const bool right = !(b.y < a.y);
+            const u32 chx = right ? b.x : a.x, chy = right ? b.y : a.y;
+            const bool stop = dead || chy < nvy;
+            const u32 wx = stop ? nvx : chx, wy = stop ? nvy : chy;
+            H[dead ? spare : hh] = make_uint2(wx, wy);
+            H[mine ? q : spare] = make_uint2(rpos, 0u);
+            asm volatile("" ::: "memory");
+            const u32 rl = __builtin_amdgcn_readlane(wx, nxt & 63);
+            rpos = start ? rl : rpos;
+            vx = nvx;
+            vy = nvy;
+            h = stop ? spare : c1 + (right ? 1 : 0);
+            blk = !stop && (right ? aR : aL);
+            nxt += start ? 1 : 0;
+            since = start ? 1 : since + 1;
+            vq = H[last - nxt];
+        }
+        steps += U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
+template <int V>
+__global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, const int* npops_in, u64* out_t, const u64* input) {
+    __shared__ uint2 H[kCap + 72];
+    const int n = segn[blockIdx.x];
+    const int npops = npops_in[blockIdx.x] < 0 ? n - 1 : npops_in[blockIdx.x];
+    u64* g = keys_vals + (size_t)blockIdx.x * kCap;
+    const int t = threadIdx.x;
+    for (int i = t; i < n; i += kT) {
+        const u64 x = g[i];
+        H[i] = make_uint2(V >= 5 ? (u32)i : (u32)x, (u32)(x >> 32) + (V >= 3 ? 1u : 0u));
+    }
+    if (V >= 3 && t < 2) H[n + t] = make_uint2(0u, 0u);
+    __syncthreads();
+    for (int L = hlev((n - 2) / 2); n >= 2 && L >= 0; --L) {       // __make_heap, a level at a time
+        const int lo = (1 << L) - 1, hi = min((2 << L) - 2, (n - 2) / 2);
+        for (int x = lo + t; x <= hi; x += kT) {
+            const uint2 vk = H[x];
+            int h = x;
+            for (;;) {
+                const int c1 = 2 * h + 1;
+                if (c1 >= n) break;
+                int c = c1;
+                uint2 a = H[c1];
+                if (c1 + 1 < n) {
+                    const uint2 b = H[c1 + 1];
+                    if (!(b.y < a.y)) { a = b; c = c1 + 1; }
+                }
+                if (a.y < vk.y) break;
+                H[h] = a;
+                h = c;
+            }
+            H[h] = vk;
+        }
+        __syncthreads();
+    }
+    if (t < 64 && n >= 2 && npops > 0) {
+        const u64 r0 = __builtin_amdgcn_s_memrealtime();
+        const u64 t0 = __builtin_amdgcn_s_memtime();
+        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : (u64)pops_v9<2>(H, n, npops);
+        const u64 t1 = __builtin_amdgcn_s_memtime();
+        const u64 r1 = __builtin_amdgcn_s_memrealtime();
+        if (t == 0) {
+            out_t[3 * blockIdx.x] = t1 - t0;
+            out_t[3 * blockIdx.x + 1] = steps;
+            out_t[3 * blockIdx.x + 2] = r1 - r0;
+        }
+    }
+    __syncthreads();
+    if (V >= 5) {                                  // entries name their input position
+        const u64* src = input + (size_t)blockIdx.x * kCap;
+        for (int i = t; i < n; i += kT) g[i] = src[H[i].x];
+    } else {
+        const int keep = V >= 3 ? (npops > 0 ? n - npops : n) : n;     // v3/v4: the popped tail is in g already
+        for (int i = t; i < keep; i += kT) g[i] = ((u64)(H[i].y - (V >= 3 ? 1u : 0u)) << 32) | H[i].x;
+    }
+}
+
+struct Case { const char* name; int n; int kind; int npops; };
+
+static std::vector<u64> make_input(int n, int kind, std::mt19937& rng) {
+    std::vector<u64> a(n);
+    for (int i = 0; i < n; ++i) {
+        u32 k;
+        if (kind == 0) k = rng() % std::max(1, n / 3);            // ties
+        else if (kind == 1) k = rng();                            // distinct-ish
+        else if (kind == 2) k = (u32)(i / 2);                     // ascending with pairs
+        else if (kind == 3) k = (u32)((n - i) / 2);               // descending with pairs
+        else k = (i < n * 7 / 8) ? (u32)(i / 2) : (rng() % (u32)(n / 2));   // sorted map + appended points
+        a[i] = ((u64)k << 32) | (u32)i;
+    }
+    return a;
+}
+
+int main(int argc, char** argv) {
+    const int reps = argc > 1 ? std::atoi(argv[1]) : 3;
+    std::mt19937 rng(11);
+    std::vector<Case> cases = {{"ties", 3000, 0, -1},  {"ties", 7000, 0, -1},  {"ties", 15000, 0, -1},
+                               {"ties", 20000, 0, -1}, {"dist", 7000, 1, -1},  {"asc", 7000, 2, -1},
+                               {"desc", 7000, 3, -1},  {"map", 12000, 4, -1},  {"ties-part", 9000, 0, 3000},
+                               {"small", 2, 0, -1},    {"small", 3, 0, -1},    {"small", 17, 0, -1},
+                               {"small", 100, 0, -1},  {"map", 18000, 4, 11000}};
+    const int nb = (int)cases.size();
+    std::vector<u64> in((size_t)nb * kCap), ref((size_t)nb * kCap);
+    std::vector<int> segn(nb), np(nb);
+    for (int b = 0; b < nb; ++b) {
+        const Case& c = cases[b];
+        std::vector<u64> a = make_input(c.n, c.kind, rng);
+        std::copy(a.begin(), a.end(), in.begin() + (size_t)b * kCap);
+        auto cmp = [](u64 x, u64 y) { return (x >> 32) < (y >> 32); };
+        std::make_heap(a.begin(), a.end(), cmp);
+        if (c.npops < 0) std::sort_heap(a.begin(), a.end(), cmp);
+        else for (int i = 0; i < c.npops; ++i) std::pop_heap(a.begin(), a.end() - i, cmp);
+        std::copy(a.begin(), a.end(), ref.begin() + (size_t)b * kCap);
+        segn[b] = c.n;
+        np[b] = c.npops;
+    }
+    u64 *d_kv, *d_t;
+    int *d_n, *d_np;
+    CK(hipMalloc(&d_kv, in.size() * 8));
+    u64* d_in;
+    CK(hipMalloc(&d_in, in.size() * 8));
+    CK(hipMemcpy(d_in, in.data(), in.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMalloc(&d_t, nb * 24));
+    CK(hipMalloc(&d_n, nb * 4));
+    CK(hipMalloc(&d_np, nb * 4));
+    CK(hipMemcpy(d_n, segn.data(), nb * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_np, np.data(), nb * 4, hipMemcpyHostToDevice));
+    std::vector<u64> out(in.size()), tt(3 * nb);
+    for (int v = 1; v <= 10; ++v) {
+        if (v >= 2 && v <= 6) continue;
+        for (int r = 0; r < reps; ++r) {
+            CK(hipMemcpy(d_kv, in.data(), in.size() * 8, hipMemcpyHostToDevice));
+            if (v == 1) hipLaunchKernelGGL(k_heap<1>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 2) hipLaunchKernelGGL(k_heap<2>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 3) hipLaunchKernelGGL(k_heap<3>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 4) hipLaunchKernelGGL(k_heap<4>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 5) hipLaunchKernelGGL(k_heap<5>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 6) hipLaunchKernelGGL(k_heap<6>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 7) hipLaunchKernelGGL(k_heap<7>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 8) hipLaunchKernelGGL(k_heap<8>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 9) hipLaunchKernelGGL(k_heap<9>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else hipLaunchKernelGGL(k_heap<10>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            CK(hipDeviceSynchronize());
+        }
+        CK(hipMemcpy(out.data(), d_kv, out.size() * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(tt.data(), d_t, nb * 24, hipMemcpyDeviceToHost));
+        for (int b = 0; b < nb; ++b) {
+            const Case& c = cases[b];
+            const size_t o = (size_t)b * kCap;
+            int bad = -1;
+            const int from = c.npops < 0 ? 0 : c.n - c.npops;   // partial: the popped tail is final
+            for (int i = from; i < c.n; ++i)
+                if (out[o + i] != ref[o + i]) { bad = i; break; }
+            const int pops = c.npops < 0 ? c.n - 1 : c.npops;
+            std::printf("v%d %-9s n %6d pops %6d  %s  %7.1f cycles/pop  %.2f steps/pop  %6.1f cycles/step  %.3f us/pop\n", v,
+                        c.name, c.n, pops, bad < 0 ? "ok  " : "DIFF", (double)tt[3 * b] / std::max(1, pops),
+                        (double)tt[3 * b + 1] / std::max(1, pops), (double)tt[3 * b] / std::max<u64>(1, tt[3 * b + 1]),
+                        tt[3 * b + 2] / 100.0 / std::max(1, pops));
+            if (bad >= 0) std::printf("   first difference at %d\n", bad);
+            std::fflush(stdout);
+        }
+    }
+    return 0;
+}
