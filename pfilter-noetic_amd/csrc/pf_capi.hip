@@ -462,6 +462,7 @@ static int sticky_status(OdomGPU& o, bool peek = false) {
 // After the work enqueued so far: counters, error words, the latest pose and the estimator state in
 // one gather (k_readback) and one synchronisation; reports the sticky words. The state read stays
 // cached for pf_odom_get_state until the next frame / update / set_state.
+static void drop_graphs_b(OdomGPU& o);
 static int readback(pf_odom* h) {
     OdomGPU& o = h->o;
     const double* pose = o.frames > 0 ? o.poses + 7 * ((size_t)(o.frames - 1) % o.pose_cap) : nullptr;
@@ -469,6 +470,16 @@ static int readback(pf_odom* h) {
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     PF_HIP_TRY(hipGetLastError());
     o.rd_frames = o.frames;
+    // a map grown past the tie sort's big-level threshold since the last hint (pf_odom_set_map raises it
+    // at once): the next rgbds sorts start in big levels, so the captured stage B is re-captured
+    if (o.tie_b) {
+        size_t mx = 0;
+        for (int c = 0; c < o.cls.nc; ++c) mx = std::max(mx, (size_t)o.h_rd->cnt[C_M + c] + (size_t)o.h_rd->cnt[C_DS + c]);
+        if (mx > o.tie_hint && tie_levels_for(*o.tie_b, mx + 65536) != tie_levels_for(*o.tie_b, o.tie_hint)) {
+            o.tie_hint = mx + 65536;
+            drop_graphs_b(o);
+        }
+    }
     return sticky_report(o, o.h_rd->err, false);
 }
 

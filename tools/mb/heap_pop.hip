@@ -75,6 +75,64 @@ __device__ u64 pops_v1(uint2* H, int n, int npops, int spare) {
     return steps;
 }
 
+// ---- v11: the shipped engine with the key compares kept 32-bit (opaque register copies) ----
+struct HeapPops11 {
+    int nxt;
+    bool act;
+    int h, m;
+    uint2 vk;
+};
+template <bool MAY>
+__device__ __forceinline__ void heap_step11(uint2* H2, HeapPops11& P, int npops, int l, int spare, int last) {
+    bool start = false, mine = false;
+    int q = 0;
+    if (MAY) {
+        q = last - P.nxt;
+        const int sh = hlev(q) - hlev(P.h);
+        const bool blk = P.act && sh >= 0 && ((q + 1) >> sh) == P.h + 1;
+        start = P.nxt < npops && __ballot(blk) == 0;
+        mine = start && l == (P.nxt & 63);
+        P.h = mine ? 0 : P.h;
+        P.m = mine ? q : P.m;
+        P.act = P.act || mine;
+    }
+    const int c1 = 2 * P.h + 1;
+    const bool has = P.act && c1 < P.m;
+    const int cr = has ? c1 : 0;
+    uint2 a = H2[cr], b = H2[cr + 1];
+    asm volatile("" : "+v"(a.y), "+v"(b.y));
+    if (MAY) {
+        uint2 vq = H2[q];
+        const uint2 r0 = H2[0];
+        asm volatile("" : "+v"(vq.y));
+        P.vk = mine ? vq : P.vk;
+        H2[mine ? q : spare] = r0;
+    }
+    const bool right = c1 + 1 < P.m && !(b.y < a.y);
+    const uint2 ch = right ? b : a;
+    u32 chy = ch.y, vky = P.vk.y;
+    asm volatile("" : "+v"(chy), "+v"(vky));
+    const bool stop = !has || chy < vky;
+    H2[P.act ? P.h : spare] = stop ? P.vk : ch;
+    P.h = P.act ? (right ? c1 + 1 : c1) : P.h;
+    P.act = P.act && !stop;
+    P.nxt += start ? 1 : 0;
+    asm volatile("" ::: "memory");
+}
+__device__ u64 pops_v11(uint2* H, int n, int npops, int spare) {
+    const int l = lane_id();
+    u64 steps = 0;
+    HeapPops11 P{0, false, 0, 0, make_uint2(0u, 0u)};
+    for (;;) {
+        heap_step11<true>(H, P, npops, l, spare + l, n - 1);
+        heap_step11<false>(H, P, npops, l, spare + l, n - 1);
+        steps += 2;
+        if (P.nxt >= npops && __ballot(P.act) == 0) break;
+        if (steps > 64ull * (u64)n + 1000ull) break;            // benchmark guard
+    }
+    return steps;
+}
+
 // ---- candidate engine ----
 // Lane j % 64 runs pop j. A pop may start on any step at least two steps after the previous start (so the
 // previous pop has written its level-1 hole and never touches levels 0 and 1 again), and not while an
@@ -424,9 +482,9 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
     const int t = threadIdx.x;
     for (int i = t; i < n; i += kT) {
         const u64 x = g[i];
-        H[i] = make_uint2(V >= 5 ? (u32)i : (u32)x, (u32)(x >> 32) + (V >= 3 ? 1u : 0u));
+        H[i] = make_uint2(V >= 5 && V <= 10 ? (u32)i : (u32)x, (u32)(x >> 32) + (V >= 3 && V <= 10 ? 1u : 0u));
     }
-    if (V >= 3 && t < 2) H[n + t] = make_uint2(0u, 0u);
+    if (V >= 3 && V <= 10 && t < 2) H[n + t] = make_uint2(0u, 0u);
     __syncthreads();
     for (int L = hlev((n - 2) / 2); n >= 2 && L >= 0; --L) {       // __make_heap, a level at a time
         const int lo = (1 << L) - 1, hi = min((2 << L) - 2, (n - 2) / 2);
@@ -453,7 +511,7 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
     if (t < 64 && n >= 2 && npops > 0) {
         const u64 r0 = __builtin_amdgcn_s_memrealtime();
         const u64 t0 = __builtin_amdgcn_s_memtime();
-        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : (u64)pops_v9<2>(H, n, npops);
+        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : pops_v11(H, n, npops, kCap);
         const u64 t1 = __builtin_amdgcn_s_memtime();
         const u64 r1 = __builtin_amdgcn_s_memrealtime();
         if (t == 0) {
@@ -463,12 +521,12 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
         }
     }
     __syncthreads();
-    if (V >= 5) {                                  // entries name their input position
+    if (V >= 5 && V <= 10) {                       // entries name their input position
         const u64* src = input + (size_t)blockIdx.x * kCap;
         for (int i = t; i < n; i += kT) g[i] = src[H[i].x];
     } else {
-        const int keep = V >= 3 ? (npops > 0 ? n - npops : n) : n;     // v3/v4: the popped tail is in g already
-        for (int i = t; i < keep; i += kT) g[i] = ((u64)(H[i].y - (V >= 3 ? 1u : 0u)) << 32) | H[i].x;
+        const int keep = V >= 3 && V <= 10 ? (npops > 0 ? n - npops : n) : n;     // v3/v4: the popped tail is in g already
+        for (int i = t; i < keep; i += kT) g[i] = ((u64)(H[i].y - (V >= 3 && V <= 10 ? 1u : 0u)) << 32) | H[i].x;
     }
 }
 
@@ -523,8 +581,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d_n, segn.data(), nb * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_np, np.data(), nb * 4, hipMemcpyHostToDevice));
     std::vector<u64> out(in.size()), tt(3 * nb);
-    for (int v = 1; v <= 10; ++v) {
-        if (v >= 2 && v <= 6) continue;
+    for (int v = 1; v <= 11; ++v) {
+        if (v >= 2 && v <= 10) continue;
         for (int r = 0; r < reps; ++r) {
             CK(hipMemcpy(d_kv, in.data(), in.size() * 8, hipMemcpyHostToDevice));
             if (v == 1) hipLaunchKernelGGL(k_heap<1>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
@@ -536,7 +594,8 @@ int main(int argc, char** argv) {
             else if (v == 7) hipLaunchKernelGGL(k_heap<7>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 8) hipLaunchKernelGGL(k_heap<8>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 9) hipLaunchKernelGGL(k_heap<9>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
-            else hipLaunchKernelGGL(k_heap<10>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 10) hipLaunchKernelGGL(k_heap<10>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else hipLaunchKernelGGL(k_heap<11>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             CK(hipDeviceSynchronize());
         }
         CK(hipMemcpy(out.data(), d_kv, out.size() * 8, hipMemcpyDeviceToHost));
