@@ -1646,15 +1646,12 @@ __device__ __forceinline__ void heap_step(const M& H2, HeapPops& P, int npops, i
 
 // __make_heap (every thread) then __sort_heap (wave 0) on the n entries of H; spare: the index of lane
 // 0's spare slot (lane l writes spare + l); jb: the job's index (the prof build records job 0)
+// __make_heap: parents (n - 2) / 2 .. 0, a tree level at a time (the sifts of a level touch disjoint
+// subtrees), each the top-down form of __adjust_heap + __push_heap; every thread
 template <class M>
-__device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int jb, int npops_in = -1) {
-    const int t = threadIdx.x, l = lane_id();
-    TIE_PROF(960, rt_now());
-    TIE_PROF(965, __builtin_amdgcn_s_memtime());
-    TIE_PROF(963, (unsigned long long)n);
-    // __make_heap: parents (n - 2) / 2 .. 0, a tree level at a time (the sifts of a level touch disjoint
-    // subtrees), each the top-down form of __adjust_heap + __push_heap
-    for (int L = hlev((n - 2) / 2); L >= 0; --L) {
+__device__ void heap_make(const M& H, int n) {
+    const int t = threadIdx.x;
+    for (int L = hlev((n - 2) / 2); n >= 2 && L >= 0; --L) {
         const int lo = (1 << L) - 1, hi = min((2 << L) - 2, (n - 2) / 2);
         for (int x = lo + t; x <= hi; x += kHeapT) {
             const uint2 vk = H.ld(x);
@@ -1679,6 +1676,15 @@ __device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int
         }
         __syncthreads();
     }
+}
+
+template <class M>
+__device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int jb, int npops_in = -1) {
+    const int t = threadIdx.x, l = lane_id();
+    TIE_PROF(960, rt_now());
+    TIE_PROF(965, __builtin_amdgcn_s_memtime());
+    TIE_PROF(963, (unsigned long long)n);
+    heap_make(H, n);
     // __sort_heap: pop i (i = 0 .. n - 2) in lane i % 64 of wave 0, steps in pairs, a pop starting only
     // on the first of a pair
     TIE_PROF(961, rt_now());
@@ -1699,6 +1705,121 @@ __device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int
     TIE_PROF(966, __builtin_amdgcn_s_memtime());
     TIE_PROF(964, steps);
     __syncthreads();
+}
+
+// __sort_heap's pops on a segment staged in LDS (round 5): the same pipeline with fewer instructions per
+// step. Entries are {position in the segment, key + 1}; the pop that vacates position q writes {the
+// root's position, 0} there, so the popped element keeps its name (the output is gathered through the
+// positions at the end) and reads as absent to every later pop: no per-lane heap size, and H[n], H[n + 1]
+// hold the same sentinel for the children of the last holes. A lane with no pop in flight parks its hole
+// at its own spare slot n + 2 + lane, whose children are sentinels, so it stops every step and writes only
+// there: no activity flag. A pop starts on the first step of a pair (as heap_step), by its own lane under
+// its exec bit, with the value and the root prefetched after the previous pair's writes; the block test
+// for the next start (an in-flight hole at q or an ancestor of q) is taken on both children of every hole
+// while the second step's loads are in flight and selected by the step's own right / stop decisions. The
+// step's post-load chain is written out in gfx950 assembly (tools/mb/heap_pop.hip: 0.34 us per pop against
+// 0.48 for heap_step, both checked there against std::make_heap + std::sort_heap).
+// kHeapCapP: the longest segment this path takes (two sentinels and 64 spare slots after it)
+constexpr int kHeapCapP = kHeapCap - 2;
+
+template <bool BLK>
+__device__ __forceinline__ unsigned long long lds_pop_step(const char* Hb, u32 nbb, u32 base, int& h, u32 vx, u32 vy,
+                                                           int spare, u32 aLv, u32 aRv) {
+    const u32 ca = min((u32)h * 16u + 8u + base, nbb);         // children 2h + 1, 2h + 2 (clamped: sentinels)
+    const uint2 a = *reinterpret_cast<const uint2*>(Hb + (ca - base));
+    const uint2 b = *reinterpret_cast<const uint2*>(Hb + (ca - base) + 8u);
+    int hn;
+    u32 t0, t1, t2, t3, t4, t5;
+    unsigned long long sm, blk = 0, tt, rm;
+    if (BLK) {
+        asm volatile(
+            "v_cmp_ge_u32_e64 %[rm], %[by], %[ay]\n\t"          // right: !(b < a)
+            "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+            "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %[t0], %[ax], %[bx], %[rm]\n\t"
+            "v_cndmask_b32_e64 %[t1], %[ay], %[by], %[rm]\n\t"
+            "v_cndmask_b32_e64 %[t5], %[aL], %[aR], %[rm]\n\t"
+            "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+            "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"          // stop: the child is below the value
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[t5], %[t5], 0, %[sm]\n\t"
+            "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+            "v_cmp_ne_u32_e64 %[blk], 0, %[t5]\n\t"
+            : [hn] "=&v"(hn), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
+              [t5] "=&v"(t5), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm)
+            : [ax] "v"(a.x), [ay] "v"(a.y), [bx] "v"(b.x), [by] "v"(b.y), [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy),
+              [sp] "v"(spare), [base] "s"(base), [aL] "v"(aLv), [aR] "v"(aRv)
+            : "memory");
+    } else {
+        asm volatile(
+            "v_cmp_ge_u32_e64 %[rm], %[by], %[ay]\n\t"
+            "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+            "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %[t0], %[ax], %[bx], %[rm]\n\t"
+            "v_cndmask_b32_e64 %[t1], %[ay], %[by], %[rm]\n\t"
+            "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+            "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+            "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+            : [hn] "=&v"(hn), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
+              [sm] "=&s"(sm), [tt] "=&s"(tt), [rm] "=&s"(rm)
+            : [ax] "v"(a.x), [ay] "v"(a.y), [bx] "v"(b.x), [by] "v"(b.y), [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy),
+              [sp] "v"(spare), [base] "s"(base)
+            : "memory");
+    }
+    h = hn;
+    return blk;
+}
+
+__device__ __forceinline__ bool anc_or_self(int x, int q) {     // x is q or an ancestor of q (0-based)
+    const int sh = __clz(x + 1) - __clz(q + 1);
+    return sh >= 0 && ((q + 1) >> sh) == x + 1;
+}
+
+// the pops of a heap built in H[0, n) (sentinel layout above), wave 0
+__device__ void lds_pops(uint2* H, int n, int npops) {
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    const char* Hb = reinterpret_cast<const char*>(H);
+    int nxt = 0;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;                                        // an idle lane's value: above the sentinels
+    unsigned long long blk = 0;
+    uint2 vq = H[last];
+    u32 rp = H[0].x;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (nxt < npops && blk == 0) {                       // wave-uniform: pop nxt starts
+                if (l == (nxt & 63)) {
+                    H[last - nxt] = make_uint2(rp, 0u);
+                    vx = vq.x;
+                    vy = vq.y;
+                    h = 0;
+                }
+                ++nxt;
+            }
+            lds_pop_step<false>(Hb, nbb, base, h, vx, vy, spare, 0u, 0u);
+            const int q = last - nxt;                            // the next start's position
+            const u32 aL = anc_or_self(2 * h + 1, q) ? 1u : 0u;
+            const u32 aR = anc_or_self(2 * h + 2, q) ? 1u : 0u;
+            blk = lds_pop_step<true>(Hb, nbb, base, h, vx, vy, spare, aL, aR);
+            vq = H[last - nxt];
+            rp = H[0].x;
+        }
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+    }
 }
 
 // A segment whose keys are all distinct has one sorted order, so whatever sorts it gives __sort_heap's
@@ -1856,9 +1977,45 @@ __device__ void heap_segment_pairs(u32* __restrict__ keys, u32* __restrict__ val
             if (H[i].y == kmin && (i == 0 || H[i - 1].y != kmin)) s_pops2 = (u32)(n - i);
         __syncthreads();
         const int popsneed = (int)s_pops2;
+        const int npops = popsneed >= n ? n - 1 : popsneed;
+        if (n <= kHeapCapP) {
+            // the restored segment as {position, key + 1} (keys are below 0xFFFFFFFF: dropped keys never
+            // reach a segment), two sentinels after it
+            for (int i = t; i < n; i += kHeapT) H[i] = make_uint2((u32)i, keys[off + i] + 1u);
+            if (t < 2) H[n + t] = make_uint2(0u, 0u);
+            __syncthreads();
+            heap_make(LdsHeap{H}, n);
+            if (t < 64) lds_pops(H, n, npops);
+            __syncthreads();
+            if (npops < n - 1) {
+                const int r = n - npops, Pr = pow2_ceil(r);
+                lds_bitonic(H, r, Pr, 2, Pr, 0);            // the rest: order-free groups only
+            }
+            // gather through the positions, then write back
+            constexpr int kPer = (kHeapCapP + kHeapT - 1) / kHeapT;
+            u32 gk[kPer], gv[kPer];
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+                const int i = t + j * kHeapT;
+                if (i < n) {
+                    const u32 p = H[i].x;
+                    gk[j] = keys[off + p];
+                    gv[j] = vals[off + p];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+                const int i = t + j * kHeapT;
+                if (i < n) {
+                    keys[off + i] = gk[j];
+                    vals[off + i] = gv[j];
+                }
+            }
+            return;
+        }
         for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);   // restore
         __syncthreads();
-        const int npops = popsneed >= n ? n - 1 : popsneed;
         heap_sort_seg(LdsHeap{H}, n, kHeapCap, jb, npops);
         if (npops < n - 1) {
             const int r = n - npops, Pr = pow2_ceil(r);

@@ -473,6 +473,284 @@ __device__ int pops_v9(uint2* H, int n, int npops) {
     return steps;
 }
 
+
+// ---- v12: v9 with the schedule pinned by empty asm statements: the loads issue first, the ancestor
+// test runs on a copy of the hole defined after them (so it fills the load latency), its results are
+// consumed before the loaded data; no branch inside the steps (unconditional readlane, selected)
+template <int U>
+__device__ int pops_v12(uint2* H, int n, int npops) {
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    int nxt = 0, since = 2;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    bool blk = false;
+    u32 rpos = H[0].x;
+    uint2 vq = H[last];
+    int steps = 0;
+    const u32 nb = (u32)n * 8u;
+    char* Hb = reinterpret_cast<char*>(H);
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool elig = since >= 2 && nxt < npops;         // wave-uniform
+            const int q = last - nxt;
+            const bool start = elig && __ballot(blk) == 0;      // wave-uniform
+            const bool cand = elig && l == (nxt & 63);          // idle: its last pop is 64 pops old
+            const bool mine = start && cand;
+            const bool dead = cand && !start;
+            const int hh = cand ? 0 : h;
+            const u32 ca = min((u32)hh * 16u + 8u, nb);
+            uint2 a = *reinterpret_cast<const uint2*>(Hb + ca);
+            uint2 b = *reinterpret_cast<const uint2*>(Hb + ca + 8u);
+            int h2 = hh;
+            asm volatile("" : "+v"(h2) : : "memory");
+            const int qn = q - (start ? 1 : 0);
+            const int c1 = 2 * h2 + 1;
+            const bool aL = anc_or_self(c1, qn), aR = anc_or_self(c1 + 1, qn);
+            const u32 nvx = mine ? vq.x : vx, nvy = mine ? vq.y : vy;
+            const bool lowq = mine && q <= 2;
+            const u32 rl = __builtin_amdgcn_readlane(rpos, 0);   // keep rpos in a VGPR-free form
+            int aLi = aL ? 1 : 0, aRi = aR ? 1 : 0;
+            asm volatile("" : "+v"(aLi), "+v"(aRi) : "v"(nvx), "v"(nvy) : "memory");
+            a.y = (lowq && q <= 1) ? 0u : a.y;
+            b.y = lowq ? 0u : b.y;
+            const bool right = !(b.y < a.y);
+            const u32 chx = right ? b.x : a.x, chy = right ? b.y : a.y;
+            const bool stop = dead || chy < nvy;
+            const u32 wx = stop ? nvx : chx, wy = stop ? nvy : chy;
+            H[dead ? spare : hh] = make_uint2(wx, wy);
+            H[mine ? q : spare] = make_uint2(rl, 0u);
+            asm volatile("" ::: "memory");
+            const u32 nr = __builtin_amdgcn_readlane(wx, nxt & 63);
+            rpos = start ? nr : rpos;
+            vx = nvx;
+            vy = nvy;
+            h = stop ? spare : c1 + (right ? 1 : 0);
+            blk = !stop && ((right ? aRi : aLi) != 0);
+            nxt += start ? 1 : 0;
+            since = start ? 1 : since + 1;
+            vq = H[last - nxt];
+        }
+        steps += U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
+
+// ---- v20: sentinel layout ({position, key + 1}; a popped position holds {root's position, 0}), starts only
+// on the first step of a pair as the shipped engine, the start done by the new pop's lane alone under its
+// own exec mask (reads q and the root, writes the sentinel), and the step's post-load chain in hand-written
+// gfx950 assembly (compare, selects, the hole's write, the next hole) so the compiler adds nothing to it
+__device__ __forceinline__ void step_asm(const char* Hb, u32 nbb, u32 base, int& h, u32 vx, u32 vy, int spare) {
+    const u32 ca = min((u32)h * 16u + 8u + base, nbb);
+    const uint2 a = *reinterpret_cast<const uint2*>(Hb + (ca - base));
+    const uint2 b = *reinterpret_cast<const uint2*>(Hb + (ca - base) + 8u);
+    int hn;
+    u32 t0, t1, t2, t3, t4;
+    unsigned long long sm;
+    asm volatile(
+        "v_cmp_ge_u32_e32 vcc, %[by], %[ay]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_cndmask_b32_e32 %[t0], %[ax], %[bx], vcc\n\t"
+        "v_cndmask_b32_e32 %[t1], %[ay], %[by], vcc\n\t"
+        "v_addc_co_u32_e32 %[t3], vcc, 0, %[t3], vcc\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        : [hn] "=&v"(hn), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
+          [sm] "=&s"(sm)
+        : [ax] "v"(a.x), [ay] "v"(a.y), [bx] "v"(b.x), [by] "v"(b.y), [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy),
+          [sp] "v"(spare), [base] "s"(base)
+        : "vcc", "memory");
+    h = hn;
+}
+__device__ int pops_v20(uint2* H, int n, int npops) {
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;                             // LDS byte address of H[0]
+    const u32 nbb = base + (u32)n * 8u;                          // the sentinel pair
+    const char* Hb = reinterpret_cast<const char*>(H);
+    int nxt = 0;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    int steps = 0;
+    for (;;) {
+        if (nxt < npops) {                                       // a pop may start on the first step
+            const int q = last - nxt;
+            const bool blk = anc_or_self(h, q);                  // idle lanes' spare holes lie past q
+            if (__ballot(blk) == 0) {
+                if (l == (nxt & 63)) {
+                    const uint2 v = H[q], r = H[0];
+                    H[q] = make_uint2(r.x, 0u);
+                    vx = v.x;
+                    vy = v.y;
+                    h = 0;
+                }
+                ++nxt;
+            }
+        }
+        step_asm(Hb, nbb, base, h, vx, vy, spare);
+        step_asm(Hb, nbb, base, h, vx, vy, spare);
+        steps += 2;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
+
+// ---- v21: v20 plus: the block test for the next start folded into the B step (the ancestor test of both
+// children of every hole taken before the step's loads return, combined with the step's right / stop
+// masks in scalar ops), the new pop's value and the root prefetched after the B step's write, one
+// termination check per two pairs
+template <bool BLK>
+__device__ __forceinline__ unsigned long long step_asm2(const char* Hb, u32 nbb, u32 base, int& h, u32 vx, u32 vy,
+                                                        int spare, u32 aLv, u32 aRv) {
+    const u32 ca = min((u32)h * 16u + 8u + base, nbb);
+    const uint2 a = *reinterpret_cast<const uint2*>(Hb + (ca - base));
+    const uint2 b = *reinterpret_cast<const uint2*>(Hb + (ca - base) + 8u);
+    int hn;
+    u32 t0, t1, t2, t3, t4, t5;
+    unsigned long long sm, blk = 0, tt, rm;
+    if (BLK) {
+        asm volatile(
+            "v_cmp_ge_u32_e64 %[rm], %[by], %[ay]\n\t"
+            "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+            "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %[t0], %[ax], %[bx], %[rm]\n\t"
+            "v_cndmask_b32_e64 %[t1], %[ay], %[by], %[rm]\n\t"
+            "v_cndmask_b32_e64 %[t5], %[aL], %[aR], %[rm]\n\t"
+            "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+            "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[t5], %[t5], 0, %[sm]\n\t"
+            "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+            "v_cmp_ne_u32_e64 %[blk], 0, %[t5]\n\t"
+            : [hn] "=&v"(hn), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
+              [t5] "=&v"(t5), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm)
+            : [ax] "v"(a.x), [ay] "v"(a.y), [bx] "v"(b.x), [by] "v"(b.y), [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy),
+              [sp] "v"(spare), [base] "s"(base), [aL] "v"(aLv), [aR] "v"(aRv)
+            : "memory");
+    } else {
+        asm volatile(
+            "v_cmp_ge_u32_e32 vcc, %[by], %[ay]\n\t"
+            "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+            "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+            "v_cndmask_b32_e32 %[t0], %[ax], %[bx], vcc\n\t"
+            "v_cndmask_b32_e32 %[t1], %[ay], %[by], vcc\n\t"
+            "v_addc_co_u32_e32 %[t3], vcc, 0, %[t3], vcc\n\t"
+            "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+            "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+            : [hn] "=&v"(hn), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
+              [sm] "=&s"(sm)
+            : [ax] "v"(a.x), [ay] "v"(a.y), [bx] "v"(b.x), [by] "v"(b.y), [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy),
+              [sp] "v"(spare), [base] "s"(base)
+            : "vcc", "memory");
+    }
+    h = hn;
+    return blk;
+}
+__device__ int pops_v21(uint2* H, int n, int npops) {
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    const char* Hb = reinterpret_cast<const char*>(H);
+    int nxt = 0;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0;
+    uint2 vq = H[last];
+    u32 rp = H[0].x;
+    int steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (nxt < npops && blk == 0) {                       // wave-uniform: a pop starts
+                if (l == (nxt & 63)) {
+                    H[last - nxt] = make_uint2(rp, 0u);
+                    vx = vq.x;
+                    vy = vq.y;
+                    h = 0;
+                }
+                ++nxt;
+            }
+            step_asm2<false>(Hb, nbb, base, h, vx, vy, spare, 0u, 0u);
+            const int q = last - nxt;                            // the next start's q
+            const u32 aL = anc_or_self(2 * h + 1, q) ? 1u : 0u;
+            const u32 aR = anc_or_self(2 * h + 2, q) ? 1u : 0u;
+            blk = step_asm2<true>(Hb, nbb, base, h, vx, vy, spare, aL, aR);
+            vq = H[last - nxt];
+            rp = H[0].x;
+        }
+        steps += 4;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
+__device__ int pops_v22(uint2* H, int n, int npops) {
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    const char* Hb = reinterpret_cast<const char*>(H);
+    int nxt = 0;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0;
+    uint2 vq = H[last];
+    u32 rp = H[0].x;
+    int steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (nxt < npops && blk == 0) {                       // wave-uniform: a pop starts
+                if (l == (nxt & 63)) {
+                    H[last - nxt] = make_uint2(rp, 0u);
+                    vx = vq.x;
+                    vy = vq.y;
+                    h = 0;
+                }
+                ++nxt;
+            }
+            step_asm2<false>(Hb, nbb, base, h, vx, vy, spare, 0u, 0u);
+            const int q = last - nxt;                            // the next start's q
+            const u32 aL = anc_or_self(2 * h + 1, q) ? 1u : 0u;
+            const u32 aR = anc_or_self(2 * h + 2, q) ? 1u : 0u;
+            const unsigned long long blk_asm = step_asm2<true>(Hb, nbb, base, h, vx, vy, spare, aL, aR);
+            blk = __ballot(anc_or_self(h, q));
+            if (blk != blk_asm && l == 0) atomicAdd(reinterpret_cast<unsigned*>(&H[n + 2 + 64]), 1u);
+            vq = H[last - nxt];
+            rp = H[0].x;
+        }
+        steps += 4;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
 template <int V>
 __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, const int* npops_in, u64* out_t, const u64* input) {
     __shared__ uint2 H[kCap + 72];
@@ -482,9 +760,9 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
     const int t = threadIdx.x;
     for (int i = t; i < n; i += kT) {
         const u64 x = g[i];
-        H[i] = make_uint2(V >= 5 && V <= 10 ? (u32)i : (u32)x, (u32)(x >> 32) + (V >= 3 && V <= 10 ? 1u : 0u));
+        H[i] = make_uint2((V >= 5 && V <= 10) || V >= 12 ? (u32)i : (u32)x, (u32)(x >> 32) + ((V >= 3 && V <= 10) || V >= 12 ? 1u : 0u));
     }
-    if (V >= 3 && V <= 10 && t < 2) H[n + t] = make_uint2(0u, 0u);
+    if (((V >= 3 && V <= 10) || V >= 12) && t < 2) H[n + t] = make_uint2(0u, 0u);
     __syncthreads();
     for (int L = hlev((n - 2) / 2); n >= 2 && L >= 0; --L) {       // __make_heap, a level at a time
         const int lo = (1 << L) - 1, hi = min((2 << L) - 2, (n - 2) / 2);
@@ -511,7 +789,7 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
     if (t < 64 && n >= 2 && npops > 0) {
         const u64 r0 = __builtin_amdgcn_s_memrealtime();
         const u64 t0 = __builtin_amdgcn_s_memtime();
-        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : pops_v11(H, n, npops, kCap);
+        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : (u64)pops_v22(H, n, npops);
         const u64 t1 = __builtin_amdgcn_s_memtime();
         const u64 r1 = __builtin_amdgcn_s_memrealtime();
         if (t == 0) {
@@ -521,7 +799,7 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
         }
     }
     __syncthreads();
-    if (V >= 5 && V <= 10) {                       // entries name their input position
+    if ((V >= 5 && V <= 10) || V >= 12) {          // entries name their input position
         const u64* src = input + (size_t)blockIdx.x * kCap;
         for (int i = t; i < n; i += kT) g[i] = src[H[i].x];
     } else {
@@ -581,8 +859,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d_n, segn.data(), nb * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_np, np.data(), nb * 4, hipMemcpyHostToDevice));
     std::vector<u64> out(in.size()), tt(3 * nb);
-    for (int v = 1; v <= 11; ++v) {
-        if (v >= 2 && v <= 10) continue;
+    for (int v = 1; v <= 16; ++v) {
+        if (v >= 2 && v <= 14) continue;
         for (int r = 0; r < reps; ++r) {
             CK(hipMemcpy(d_kv, in.data(), in.size() * 8, hipMemcpyHostToDevice));
             if (v == 1) hipLaunchKernelGGL(k_heap<1>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
@@ -595,7 +873,12 @@ int main(int argc, char** argv) {
             else if (v == 8) hipLaunchKernelGGL(k_heap<8>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 9) hipLaunchKernelGGL(k_heap<9>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 10) hipLaunchKernelGGL(k_heap<10>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
-            else hipLaunchKernelGGL(k_heap<11>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 11) hipLaunchKernelGGL(k_heap<11>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 12) hipLaunchKernelGGL(k_heap<12>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 13) hipLaunchKernelGGL(k_heap<13>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 14) hipLaunchKernelGGL(k_heap<14>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 15) hipLaunchKernelGGL(k_heap<15>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else hipLaunchKernelGGL(k_heap<16>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             CK(hipDeviceSynchronize());
         }
         CK(hipMemcpy(out.data(), d_kv, out.size() * 8, hipMemcpyDeviceToHost));
