@@ -1717,81 +1717,118 @@ __device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int
 // its exec bit, with the value and the root prefetched after the previous pair's writes; the block test
 // for the next start (an in-flight hole at q or an ancestor of q) is taken on both children of every hole
 // while the second step's loads are in flight and selected by the step's own right / stop decisions. The
-// step's post-load chain is written out in gfx950 assembly (tools/mb/heap_pop.hip: 0.34 us per pop against
-// 0.48 for heap_step, both checked there against std::make_heap + std::sort_heap).
+// steps are written out in gfx950 assembly, loads and waits included (tools/mb/heap_pop.hip v24: 0.29 us per
+// pop against 0.48 for heap_step, both checked there against std::make_heap + std::sort_heap).
 // kHeapCapP: the longest segment this path takes (two sentinels and 64 spare slots after it)
 constexpr int kHeapCapP = kHeapCap - 2;
 
-template <bool BLK>
-__device__ __forceinline__ unsigned long long lds_pop_step(const char* Hb, u32 nbb, u32 base, int& h, u32 vx, u32 vy,
-                                                           int spare, u32 aLv, u32 aRv) {
-    const u32 ca = min((u32)h * 16u + 8u + base, nbb);         // children 2h + 1, 2h + 2 (clamped: sentinels)
-    const uint2 a = *reinterpret_cast<const uint2*>(Hb + (ca - base));
-    const uint2 b = *reinterpret_cast<const uint2*>(Hb + (ca - base) + 8u);
+// the first step of a pair: a pop may start (mine: its lane, by mask), then one level for every lane
+__device__ __forceinline__ void lds_pop_step_a(u32 nbb, u32 base8, u32 base, int& h, u32& vx, u32& vy, int spare,
+                                          unsigned long long mine, u32 q, u32 rp, u32 vqx, u32 vqy) {
     int hn;
-    u32 t0, t1, t2, t3, t4, t5;
-    unsigned long long sm, blk = 0, tt, rm;
-    if (BLK) {
-        asm volatile(
-            "v_cmp_ge_u32_e64 %[rm], %[by], %[ay]\n\t"          // right: !(b < a)
-            "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
-            "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
-            "s_nop 1\n\t"
-            "v_cndmask_b32_e64 %[t0], %[ax], %[bx], %[rm]\n\t"
-            "v_cndmask_b32_e64 %[t1], %[ay], %[by], %[rm]\n\t"
-            "v_cndmask_b32_e64 %[t5], %[aL], %[aR], %[rm]\n\t"
-            "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
-            "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"          // stop: the child is below the value
-            "s_nop 1\n\t"
-            "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
-            "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
-            "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
-            "v_cndmask_b32_e64 %[t5], %[t5], 0, %[sm]\n\t"
-            "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
-            "v_cmp_ne_u32_e64 %[blk], 0, %[t5]\n\t"
-            : [hn] "=&v"(hn), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
-              [t5] "=&v"(t5), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm)
-            : [ax] "v"(a.x), [ay] "v"(a.y), [bx] "v"(b.x), [by] "v"(b.y), [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy),
-              [sp] "v"(spare), [base] "s"(base), [aL] "v"(aLv), [aR] "v"(aRv)
-            : "memory");
-    } else {
-        asm volatile(
-            "v_cmp_ge_u32_e64 %[rm], %[by], %[ay]\n\t"
-            "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
-            "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
-            "s_nop 1\n\t"
-            "v_cndmask_b32_e64 %[t0], %[ax], %[bx], %[rm]\n\t"
-            "v_cndmask_b32_e64 %[t1], %[ay], %[by], %[rm]\n\t"
-            "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
-            "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
-            "s_nop 1\n\t"
-            "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
-            "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
-            "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
-            "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
-            : [hn] "=&v"(hn), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
-              [sm] "=&s"(sm), [tt] "=&s"(tt), [rm] "=&s"(rm)
-            : [ax] "v"(a.x), [ay] "v"(a.y), [bx] "v"(b.x), [by] "v"(b.y), [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy),
-              [sp] "v"(spare), [base] "s"(base)
-            : "memory");
-    }
+    u32 ad, ax, ay, bx, by, tq, sa, rv, zz, t0, t1, t2, t3, t4;
+    unsigned long long sm, tt, rm;
+    asm volatile(
+        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
+        "v_mov_b32_e32 %[tq], %[q]\n\t"
+        "v_mov_b32_e32 %[rv], %[rp]\n\t"
+        "v_mov_b32_e32 %[zz], 0\n\t"
+        "v_cndmask_b32_e64 %[sa], %[sp], %[tq], %[mine]\n\t"
+        "v_lshl_add_u32 %[ad], %[h], 4, %[b8]\n\t"
+        "v_lshl_add_u32 %[sa], %[sa], 3, %[base]\n\t"
+        "v_min_u32_e32 %[ad], %[nbb], %[ad]\n\t"
+        "ds_write2_b32 %[sa], %[rv], %[zz] offset1:1\n\t"
+        "ds_read_b32 %[ax], %[ad]\n\t"
+        "ds_read_b32 %[ay], %[ad] offset:4\n\t"
+        "ds_read_b32 %[bx], %[ad] offset:8\n\t"
+        "ds_read_b32 %[by], %[ad] offset:12\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], %[vqx], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], %[vqy], %[mine]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], %[by], %[ay]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[ax], %[bx], %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t1], %[ay], %[by], %[rm]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        : [hn] "=&v"(hn), [h] "+v"(h), [vx] "+v"(vx), [vy] "+v"(vy), [ad] "=&v"(ad), [ax] "=&v"(ax),
+          [ay] "=&v"(ay), [bx] "=&v"(bx), [by] "=&v"(by), [tq] "=&v"(tq), [sa] "=&v"(sa), [rv] "=&v"(rv),
+          [zz] "=&v"(zz), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
+          [sm] "=&s"(sm), [tt] "=&s"(tt), [rm] "=&s"(rm)
+        : [sp] "v"(spare), [base] "s"(base), [b8] "s"(base8), [nbb] "s"(nbb), [mine] "s"(mine), [q] "s"(q),
+          [rp] "s"(rp), [vqx] "v"(vqx), [vqy] "v"(vqy)
+        : "memory");
+    h = hn;
+}
+// the second step: one level for every lane, the ancestor test of both children of every hole (q1 = q + 1,
+// cq = clz(q1)) between the loads' issue and their wait; returns the lanes whose new hole is q or an
+// ancestor of q (the next start waits for none)
+__device__ __forceinline__ unsigned long long lds_pop_step_b(u32 nbb, u32 base8, u32 base, int& h, u32 vx, u32 vy,
+                                                        int spare, u32 q1, u32 cq) {
+    int hn;
+    u32 ad, ax, ay, bx, by, l1, r1, cl, cr, tl, tr, aLv, aRv, t0, t1, t2, t3, t4, t5;
+    unsigned long long sm, blk, tt, rm, am, bm;
+    asm volatile(
+        "v_lshl_add_u32 %[ad], %[h], 4, %[b8]\n\t"
+        "v_min_u32_e32 %[ad], %[nbb], %[ad]\n\t"
+        "ds_read_b32 %[ax], %[ad]\n\t"
+        "ds_read_b32 %[ay], %[ad] offset:4\n\t"
+        "ds_read_b32 %[bx], %[ad] offset:8\n\t"
+        "ds_read_b32 %[by], %[ad] offset:12\n\t"
+        "v_lshl_add_u32 %[l1], %[h], 1, 2\n\t"
+        "v_add_u32_e32 %[r1], 1, %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cl], %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cr], %[r1]\n\t"
+        "v_sub_u32_e64 %[cl], %[cl], %[cq]\n\t"
+        "v_sub_u32_e64 %[cr], %[cr], %[cq]\n\t"
+        "v_lshrrev_b32_e64 %[tl], %[cl], %[q1]\n\t"
+        "v_lshrrev_b32_e64 %[tr], %[cr], %[q1]\n\t"
+        "v_cmp_eq_u32_e64 %[am], %[tl], %[l1]\n\t"
+        "v_cmp_eq_u32_e64 %[bm], %[tr], %[r1]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_cndmask_b32_e64 %[aLv], 0, 1, %[am]\n\t"
+        "v_cndmask_b32_e64 %[aRv], 0, 1, %[bm]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], %[by], %[ay]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[ax], %[bx], %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t1], %[ay], %[by], %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[aLv], %[aRv], %[rm]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[t5], 0, %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "v_cmp_ne_u32_e64 %[blk], 0, %[t5]\n\t"
+        : [hn] "=&v"(hn), [ad] "=&v"(ad), [ax] "=&v"(ax), [ay] "=&v"(ay), [bx] "=&v"(bx), [by] "=&v"(by),
+          [l1] "=&v"(l1), [r1] "=&v"(r1), [cl] "=&v"(cl), [cr] "=&v"(cr), [tl] "=&v"(tl), [tr] "=&v"(tr),
+          [aLv] "=&v"(aLv), [aRv] "=&v"(aRv), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+          [t4] "=&v"(t4), [t5] "=&v"(t5), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm),
+          [am] "=&s"(am), [bm] "=&s"(bm)
+        : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b8] "s"(base8),
+          [nbb] "s"(nbb), [q1] "s"(q1), [cq] "s"(cq)
+        : "memory");
     h = hn;
     return blk;
 }
-
-__device__ __forceinline__ bool anc_or_self(int x, int q) {     // x is q or an ancestor of q (0-based)
-    const int sh = __clz(x + 1) - __clz(q + 1);
-    return sh >= 0 && ((q + 1) >> sh) == x + 1;
-}
-
-// the pops of a heap built in H[0, n) (sentinel layout above), wave 0
+// the pops of a heap built in H[0, n) (sentinel layout above), wave 0; four pairs per exit test
 __device__ void lds_pops(uint2* H, int n, int npops) {
     const int l = lane_id();
     const int last = n - 1;
     const int spare = n + 2 + l;
     const u32 base = (u32)(size_t)H;
     const u32 nbb = base + (u32)n * 8u;
-    const char* Hb = reinterpret_cast<const char*>(H);
     int nxt = 0;
     int h = spare;
     u32 vx = 0u, vy = 1u;                                        // an idle lane's value: above the sentinels
@@ -1800,22 +1837,15 @@ __device__ void lds_pops(uint2* H, int n, int npops) {
     u32 rp = H[0].x;
     for (;;) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (nxt < npops && blk == 0) {                       // wave-uniform: pop nxt starts
-                if (l == (nxt & 63)) {
-                    H[last - nxt] = make_uint2(rp, 0u);
-                    vx = vq.x;
-                    vy = vq.y;
-                    h = 0;
-                }
-                ++nxt;
-            }
-            lds_pop_step<false>(Hb, nbb, base, h, vx, vy, spare, 0u, 0u);
-            const int q = last - nxt;                            // the next start's position
-            const u32 aL = anc_or_self(2 * h + 1, q) ? 1u : 0u;
-            const u32 aR = anc_or_self(2 * h + 2, q) ? 1u : 0u;
-            blk = lds_pop_step<true>(Hb, nbb, base, h, vx, vy, spare, aL, aR);
-            vq = H[last - nxt];
+        for (int u = 0; u < 4; ++u) {
+            const bool start = nxt < npops && blk == 0;          // wave-uniform
+            const unsigned long long mine = start ? (1ull << (nxt & 63)) : 0ull;
+            lds_pop_step_a(nbb, base + 8u, base, h, vx, vy, spare, mine, (u32)(last - nxt),
+                           __builtin_amdgcn_readfirstlane(rp), vq.x, vq.y);
+            nxt += start ? 1 : 0;
+            const u32 q1 = (u32)(last - nxt + 1);
+            blk = lds_pop_step_b(nbb, base + 8u, base, h, vx, vy, spare, q1, (u32)__clz(q1));
+            vq = H[last - nxt];                                  // the next start's value and root
             rp = H[0].x;
         }
         if (nxt >= npops && __ballot(h != spare) == 0) break;
