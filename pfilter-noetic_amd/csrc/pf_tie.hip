@@ -1824,6 +1824,8 @@ __device__ __forceinline__ unsigned long long lds_pop_step_b(u32 nbb, u32 base8,
 }
 // the pops of a heap built in H[0, n) (sentinel layout above), wave 0; four pairs per exit test
 __device__ void lds_pops(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);                      // wave-uniform (the step's masks are scalar)
+    npops = __builtin_amdgcn_readfirstlane(npops);
     const int l = lane_id();
     const int last = n - 1;
     const int spare = n + 2 + l;
@@ -1978,17 +1980,78 @@ __device__ void glb_bitonic(const GlbHeap& G, uint2* S, int n) {
 // (A leaner pop engine on 32-bit rank words -- one 8-byte read per step, the ancestor test only on
 // steps that may start a pop -- measured 0.48 us per pop against the pair engine's 0.39: a step is
 // bound by the wave's VALU issue, about 350-460 cycles, not by the LDS round trip)
+// the segment restored in LDS as {position, key + 1} (keys are below 0xFFFFFFFF: dropped keys never reach a
+// segment), two sentinels after it, __make_heap, npops pops (lds_pops), the order-free rest sorted, and the
+// output gathered through the positions
+__device__ void heap_pops_lds(u32* __restrict__ keys, u32* __restrict__ vals, int off, int n, int npops, uint2* H) {
+    const int t = threadIdx.x;
+    for (int i = t; i < n; i += kHeapT) H[i] = make_uint2((u32)i, keys[off + i] + 1u);
+    if (t < 2) H[n + t] = make_uint2(0u, 0u);
+    __syncthreads();
+    heap_make(LdsHeap{H}, n);
+    if (t < 64) lds_pops(H, n, npops);
+    __syncthreads();
+    if (npops < n - 1) {
+        const int r = n - npops, Pr = pow2_ceil(r);
+        lds_bitonic(H, r, Pr, 2, Pr, 0);                    // the rest: order-free groups only
+    }
+    constexpr int kPer = (kHeapCapP + kHeapT - 1) / kHeapT;
+    u32 gk[kPer], gv[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int i = t + j * kHeapT;
+        if (i < n) {
+            const u32 p = H[i].x;
+            gk[j] = keys[off + p];
+            gv[j] = vals[off + p];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int i = t + j * kHeapT;
+        if (i < n) {
+            keys[off + i] = gk[j];
+            vals[off + i] = gv[j];
+        }
+    }
+}
+
 // One depth-limit segment [off, off + n), n <= kHeapCap, in LDS as {val, key} entries: the sorted copy
 // decides the pops, then the segment is restored and heap-sorted that far (heap_sort_seg)
 __device__ void heap_segment_pairs(u32* __restrict__ keys, u32* __restrict__ vals, const u8* __restrict__ freef,
                                    int off, int n, uint2* H, int jb) {
     __shared__ u32 s_kmin2, s_pops2;
     const int t = threadIdx.x;
-    for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);
     if (t == 0) {
         s_kmin2 = 0xFFFFFFFFu;
         s_pops2 = 0u;
     }
+    __syncthreads();
+    if (freef && n <= kHeapCapP) {
+        // with the dependence flags the pops needed come from two reductions, no sorted copy: the smallest
+        // key of an order-dependent element, then the count of keys at or above it
+        u32 km = 0xFFFFFFFFu;
+        for (int i = t; i < n; i += kHeapT)
+            if (!freef[vals[off + i]]) km = min(km, keys[off + i]);
+        km = wave_min_u32(km);
+        if (lane_id() == 0 && km != 0xFFFFFFFFu) atomicMin(&s_kmin2, km);
+        __syncthreads();
+        km = s_kmin2;
+        if (km != 0xFFFFFFFFu) {
+            u32 c = 0;
+            for (int i = t; i < n; i += kHeapT) c += keys[off + i] >= km ? 1u : 0u;
+            for (int o = 32; o > 0; o >>= 1) c += (u32)__shfl_xor((int)c, o, 64);
+            if (lane_id() == 0) atomicAdd(&s_pops2, c);
+            __syncthreads();
+            const int popsneed = (int)s_pops2;
+            heap_pops_lds(keys, vals, off, n, popsneed >= n ? n - 1 : popsneed, H);
+            return;
+        }
+        s_kmin2 = 0xFFFFFFFFu;                          // no order-dependent element: sorted below
+        __syncthreads();
+    }
+    for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);
     __syncthreads();
     const int P2 = pow2_ceil(n);
     lds_bitonic(H, n, P2, 2, P2, 0);
@@ -2009,39 +2072,8 @@ __device__ void heap_segment_pairs(u32* __restrict__ keys, u32* __restrict__ val
         const int popsneed = (int)s_pops2;
         const int npops = popsneed >= n ? n - 1 : popsneed;
         if (n <= kHeapCapP) {
-            // the restored segment as {position, key + 1} (keys are below 0xFFFFFFFF: dropped keys never
-            // reach a segment), two sentinels after it
-            for (int i = t; i < n; i += kHeapT) H[i] = make_uint2((u32)i, keys[off + i] + 1u);
-            if (t < 2) H[n + t] = make_uint2(0u, 0u);
             __syncthreads();
-            heap_make(LdsHeap{H}, n);
-            if (t < 64) lds_pops(H, n, npops);
-            __syncthreads();
-            if (npops < n - 1) {
-                const int r = n - npops, Pr = pow2_ceil(r);
-                lds_bitonic(H, r, Pr, 2, Pr, 0);            // the rest: order-free groups only
-            }
-            // gather through the positions, then write back
-            constexpr int kPer = (kHeapCapP + kHeapT - 1) / kHeapT;
-            u32 gk[kPer], gv[kPer];
-#pragma unroll
-            for (int j = 0; j < kPer; ++j) {
-                const int i = t + j * kHeapT;
-                if (i < n) {
-                    const u32 p = H[i].x;
-                    gk[j] = keys[off + p];
-                    gv[j] = vals[off + p];
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < kPer; ++j) {
-                const int i = t + j * kHeapT;
-                if (i < n) {
-                    keys[off + i] = gk[j];
-                    vals[off + i] = gv[j];
-                }
-            }
+            heap_pops_lds(keys, vals, off, n, npops, H);
             return;
         }
         for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);   // restore
