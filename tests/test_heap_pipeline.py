@@ -124,6 +124,114 @@ def test_pipelined_heap_keeps_class_bits_out_of_the_compare(pfref):
     np.testing.assert_array_equal(device_heap_perm(keys), pfref.sort_perm(keys, "literal", 0))
 
 
+# the round-5 LDS engine (pf_tie.hip lds_pops / lds_pop_step_a / lds_pop_step_b), restated lane by lane:
+# entries {position, key + 1}; H[n], H[n + 1] sentinels {_, 0}; a pop that starts writes {root's position,
+# 0} at q (so the popped element keeps its name and reads as absent); the children of any hole h are read
+# at min(2h + 1, n); idle lanes park on spare holes n + 2 + lane (children: the sentinels) with a value of
+# key 1, so they stop every step; a pop may start only in the first step of a pair, by its own lane, with
+# the value H[q] and the root's position prefetched after the previous pair's second step; the block mask
+# for the next start is the second step's: not stopped, and the chosen child (right on !(b < a)) is q or
+# an ancestor of q, q being the next pop's position
+def _anc_or_self(x, q):
+    x += 1
+    q += 1
+    while q > x:
+        q >>= 1
+    return q == x
+
+
+def lds_pops_restated(keys, npops=None):
+    n = keys.size
+    last = n - 1
+    npops = last if npops is None else npops
+    H = [(i, int(k) + 1) for i, k in enumerate(keys)] + [(0, 0), (0, 0)] + [(0, 0)] * NL
+    # __make_heap on key + 1 (the same order)
+    for L in range(hlev((n - 2) // 2), -1, -1) if n >= 2 else []:
+        for x in range((1 << L) - 1, min((2 << L) - 2, (n - 2) // 2) + 1):
+            vk, h = H[x], x
+            while 2 * h + 1 < n:
+                c = 2 * h + 1
+                if c + 1 < n and not (H[c + 1][1] < H[c][1]):
+                    c += 1
+                if H[c][1] < vk[1]:
+                    break
+                H[h] = H[c]
+                h = c
+            H[h] = vk
+    spare = [n + 2 + l for l in range(NL)]
+    h = list(spare)
+    v = [(0, 1)] * NL
+    nxt, blk = 0, 0
+    vq, rp = H[last], H[0][0]
+
+    def step(mine):
+        """every lane one level; mine: the lane starting a pop this step (or None); returns the lanes whose
+        new hole is q' or an ancestor of q' (q' = the next pop's position)"""
+        if mine is not None:                          # the start, before the step's loads
+            H[last - nxt] = (rp, 0)
+            h[mine], v[mine] = 0, vq
+        q2 = last - (nxt + (1 if mine is not None else 0))
+        reads = []
+        for l in range(NL):
+            c1 = min(2 * h[l] + 1, n)
+            reads.append((c1, H[c1], H[c1 + 1]))
+        out = []
+        for l in range(NL):
+            c1, a, b = reads[l]
+            right = not (b[1] < a[1])
+            ch = b if right else a
+            stop = ch[1] < v[l][1]
+            H[h[l]] = v[l] if stop else ch
+            child = 2 * h[l] + 1 + (1 if right else 0)
+            out.append((not stop) and _anc_or_self(child, q2))
+            h[l] = spare[l] if stop else child
+        return any(out)
+
+    steps = 0
+    while True:
+        for _ in range(4):
+            start = nxt < npops and not blk
+            step((nxt & (NL - 1)) if start else None)
+            nxt += 1 if start else 0
+            blk = step(None)
+            vq, rp = H[last - nxt] if nxt <= last else (0, 0), H[0][0]
+            steps += 2
+        if nxt >= npops and all(h[l] == spare[l] for l in range(NL)):
+            return H[:n], steps
+
+
+def test_lds_engine_equals_libstdcxx(pfref):
+    rng = np.random.default_rng(41)
+    for trial in range(40):
+        n = int(rng.choice([2, 3, 17, 18, 64, 65, 100, 257, 700]))
+        span = int(rng.choice([2, 5, 40, 1000, 1 << 30]))
+        keys = rng.integers(0, span, n).astype(np.uint32)
+        if trial % 5 == 0:
+            keys = np.sort(keys)
+        elif trial % 5 == 1:
+            keys = np.sort(keys)[::-1].copy()
+        H, steps = lds_pops_restated(keys)
+        got = np.array([p for p, _ in H], np.uint32)              # output positions (values = indices)
+        want = pfref.sort_perm(keys, "literal", 0)
+        np.testing.assert_array_equal(got, want, err_msg="trial %d n=%d span=%d" % (trial, n, span))
+        assert steps <= 8 * n + 16
+
+
+def test_lds_engine_partial_pops(pfref):
+    """npops < n - 1: the popped tail is __sort_heap's after that many pops (pop_heap repeated)"""
+    rng = np.random.default_rng(42)
+    for trial in range(20):
+        n = int(rng.choice([40, 200, 600]))
+        keys = rng.integers(0, int(rng.choice([7, 300])), n).astype(np.uint32)
+        npops = int(rng.integers(1, n - 1))
+        H, _ = lds_pops_restated(keys, npops)
+        want = pfref.sort_perm(keys, "literal", 0)                 # the full heap sort's order
+        got_tail = [p for p, _ in H[n - npops:]]
+        # the popped tail of a full heap sort is the same after npops pops (the later pops leave it alone)
+        np.testing.assert_array_equal(np.array(got_tail, np.uint32), want[n - npops:], err_msg="trial %d" % trial)
+        assert all(k == 0 for _, k in H[n - npops:])             # popped positions hold the sentinel key
+
+
 # k_tie_heap's distinct-key path (pf_tie.hip lds_bitonic / glb_bitonic): the flip-form bitonic network
 # with positions past the segment's end left out (+inf), run whole (LDS) or as chunks of C positions
 # with the cross-chunk steps on the global copy; restated to check the index arithmetic at small C
