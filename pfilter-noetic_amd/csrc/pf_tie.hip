@@ -1717,8 +1717,9 @@ __device__ void heap_sort_seg(const M& H, int n, int spare, [[maybe_unused]] int
 // its exec bit, with the value and the root prefetched after the previous pair's writes; the block test
 // for the next start (an in-flight hole at q or an ancestor of q) is taken on both children of every hole
 // while the second step's loads are in flight and selected by the step's own right / stop decisions. The
-// steps are written out in gfx950 assembly, loads and waits included (tools/mb/heap_pop.hip v24: 0.29 us per
-// pop against 0.48 for heap_step, both checked there against std::make_heap + std::sort_heap).
+// steps are written out in gfx950 assembly, loads and waits included, the children read by one ds_read2_b64
+// into four pinned registers (tools/mb/heap_pop.hip v27: 0.286 us per pop against 0.48 for heap_step, both
+// checked there against std::make_heap + std::sort_heap).
 // kHeapCapP: the longest segment this path takes (two sentinels and 64 spare slots after it)
 constexpr int kHeapCapP = kHeapCap - 2;
 
@@ -1738,19 +1739,16 @@ __device__ __forceinline__ void lds_pop_step_a(u32 nbb, u32 base8, u32 base, int
         "v_lshl_add_u32 %[sa], %[sa], 3, %[base]\n\t"
         "v_min_u32_e32 %[ad], %[nbb], %[ad]\n\t"
         "ds_write2_b32 %[sa], %[rv], %[zz] offset1:1\n\t"
-        "ds_read_b32 %[ax], %[ad]\n\t"
-        "ds_read_b32 %[ay], %[ad] offset:4\n\t"
-        "ds_read_b32 %[bx], %[ad] offset:8\n\t"
-        "ds_read_b32 %[by], %[ad] offset:12\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
         "v_cndmask_b32_e64 %[vx], %[vx], %[vqx], %[mine]\n\t"
         "v_cndmask_b32_e64 %[vy], %[vy], %[vqy], %[mine]\n\t"
         "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
         "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
-        "v_cmp_ge_u32_e64 %[rm], %[by], %[ay]\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
         "s_nop 1\n\t"
-        "v_cndmask_b32_e64 %[t0], %[ax], %[bx], %[rm]\n\t"
-        "v_cndmask_b32_e64 %[t1], %[ay], %[by], %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
         "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
         "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
         "s_nop 1\n\t"
@@ -1759,12 +1757,12 @@ __device__ __forceinline__ void lds_pop_step_a(u32 nbb, u32 base8, u32 base, int
         "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
         "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
         : [hn] "=&v"(hn), [h] "+v"(h), [vx] "+v"(vx), [vy] "+v"(vy), [ad] "=&v"(ad), [ax] "=&v"(ax),
-          [ay] "=&v"(ay), [bx] "=&v"(bx), [by] "=&v"(by), [tq] "=&v"(tq), [sa] "=&v"(sa), [rv] "=&v"(rv),
+          [tq] "=&v"(tq), [sa] "=&v"(sa), [rv] "=&v"(rv),
           [zz] "=&v"(zz), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
           [sm] "=&s"(sm), [tt] "=&s"(tt), [rm] "=&s"(rm)
         : [sp] "v"(spare), [base] "s"(base), [b8] "s"(base8), [nbb] "s"(nbb), [mine] "s"(mine), [q] "s"(q),
           [rp] "s"(rp), [vqx] "v"(vqx), [vqy] "v"(vqy)
-        : "memory");
+        : "memory", "v40", "v41", "v42", "v43");
     h = hn;
 }
 // the second step: one level for every lane, the ancestor test of both children of every hole (q1 = q + 1,
@@ -1778,10 +1776,7 @@ __device__ __forceinline__ unsigned long long lds_pop_step_b(u32 nbb, u32 base8,
     asm volatile(
         "v_lshl_add_u32 %[ad], %[h], 4, %[b8]\n\t"
         "v_min_u32_e32 %[ad], %[nbb], %[ad]\n\t"
-        "ds_read_b32 %[ax], %[ad]\n\t"
-        "ds_read_b32 %[ay], %[ad] offset:4\n\t"
-        "ds_read_b32 %[bx], %[ad] offset:8\n\t"
-        "ds_read_b32 %[by], %[ad] offset:12\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
         "v_lshl_add_u32 %[l1], %[h], 1, 2\n\t"
         "v_add_u32_e32 %[r1], 1, %[l1]\n\t"
         "v_ffbh_u32_e32 %[cl], %[l1]\n\t"
@@ -1797,10 +1792,10 @@ __device__ __forceinline__ unsigned long long lds_pop_step_b(u32 nbb, u32 base8,
         "v_cndmask_b32_e64 %[aLv], 0, 1, %[am]\n\t"
         "v_cndmask_b32_e64 %[aRv], 0, 1, %[bm]\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
-        "v_cmp_ge_u32_e64 %[rm], %[by], %[ay]\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
         "s_nop 1\n\t"
-        "v_cndmask_b32_e64 %[t0], %[ax], %[bx], %[rm]\n\t"
-        "v_cndmask_b32_e64 %[t1], %[ay], %[by], %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
         "v_cndmask_b32_e64 %[t5], %[aLv], %[aRv], %[rm]\n\t"
         "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
         "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
@@ -1811,17 +1806,18 @@ __device__ __forceinline__ unsigned long long lds_pop_step_b(u32 nbb, u32 base8,
         "v_cndmask_b32_e64 %[t5], %[t5], 0, %[sm]\n\t"
         "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
         "v_cmp_ne_u32_e64 %[blk], 0, %[t5]\n\t"
-        : [hn] "=&v"(hn), [ad] "=&v"(ad), [ax] "=&v"(ax), [ay] "=&v"(ay), [bx] "=&v"(bx), [by] "=&v"(by),
+        : [hn] "=&v"(hn), [ad] "=&v"(ad), [by] "=&v"(by),
           [l1] "=&v"(l1), [r1] "=&v"(r1), [cl] "=&v"(cl), [cr] "=&v"(cr), [tl] "=&v"(tl), [tr] "=&v"(tr),
           [aLv] "=&v"(aLv), [aRv] "=&v"(aRv), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
           [t4] "=&v"(t4), [t5] "=&v"(t5), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm),
           [am] "=&s"(am), [bm] "=&s"(bm)
         : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b8] "s"(base8),
           [nbb] "s"(nbb), [q1] "s"(q1), [cq] "s"(cq)
-        : "memory");
+        : "memory", "v40", "v41", "v42", "v43");
     h = hn;
     return blk;
 }
+
 // the pops of a heap built in H[0, n) (sentinel layout above), wave 0; four pairs per exit test
 __device__ void lds_pops(uint2* H, int n, int npops) {
     n = __builtin_amdgcn_readfirstlane(n);                      // wave-uniform (the step's masks are scalar)

@@ -927,6 +927,407 @@ __device__ int pops_v24(uint2* H, int n, int npops) {
     return steps;
 }
 
+
+// ---- v25: any-step starts (a pop may start on every step two or more after the previous start): every
+// step folds the start in by lane mask and takes the block test for the next step
+__device__ __forceinline__ unsigned long long step_asm5(u32 nbb, u32 base8, u32 base, int& h, u32& vx, u32& vy,
+                                                        int spare, unsigned long long mine, u32 q, u32 rp, u32 vqx,
+                                                        u32 vqy, u32 q1, u32 cq) {
+    int hn;
+    u32 ad, ax, ay, bx, by, tq, sa, rv, zz, l1, r1, cl, cr, tl, tr, aLv, aRv, t0, t1, t2, t3, t4, t5;
+    unsigned long long sm, blk, tt, rm, am, bm;
+    asm volatile(
+        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
+        "v_mov_b32_e32 %[tq], %[q]\n\t"
+        "v_mov_b32_e32 %[rv], %[rp]\n\t"
+        "v_mov_b32_e32 %[zz], 0\n\t"
+        "v_cndmask_b32_e64 %[sa], %[sp], %[tq], %[mine]\n\t"
+        "v_lshl_add_u32 %[ad], %[h], 4, %[b8]\n\t"
+        "v_lshl_add_u32 %[sa], %[sa], 3, %[base]\n\t"
+        "v_min_u32_e32 %[ad], %[nbb], %[ad]\n\t"
+        "ds_write2_b32 %[sa], %[rv], %[zz] offset1:1\n\t"
+        "ds_read_b32 %[ax], %[ad]\n\t"
+        "ds_read_b32 %[ay], %[ad] offset:4\n\t"
+        "ds_read_b32 %[bx], %[ad] offset:8\n\t"
+        "ds_read_b32 %[by], %[ad] offset:12\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], %[vqx], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], %[vqy], %[mine]\n\t"
+        "v_lshl_add_u32 %[l1], %[h], 1, 2\n\t"
+        "v_add_u32_e32 %[r1], 1, %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cl], %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cr], %[r1]\n\t"
+        "v_sub_u32_e64 %[cl], %[cl], %[cq]\n\t"
+        "v_sub_u32_e64 %[cr], %[cr], %[cq]\n\t"
+        "v_lshrrev_b32_e64 %[tl], %[cl], %[q1]\n\t"
+        "v_lshrrev_b32_e64 %[tr], %[cr], %[q1]\n\t"
+        "v_cmp_eq_u32_e64 %[am], %[tl], %[l1]\n\t"
+        "v_cmp_eq_u32_e64 %[bm], %[tr], %[r1]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_cndmask_b32_e64 %[aLv], 0, 1, %[am]\n\t"
+        "v_cndmask_b32_e64 %[aRv], 0, 1, %[bm]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], %[by], %[ay]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[ax], %[bx], %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t1], %[ay], %[by], %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[aLv], %[aRv], %[rm]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[t5], 0, %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "v_cmp_ne_u32_e64 %[blk], 0, %[t5]\n\t"
+        : [hn] "=&v"(hn), [h] "+v"(h), [vx] "+v"(vx), [vy] "+v"(vy), [ad] "=&v"(ad), [ax] "=&v"(ax),
+          [ay] "=&v"(ay), [bx] "=&v"(bx), [by] "=&v"(by), [tq] "=&v"(tq), [sa] "=&v"(sa), [rv] "=&v"(rv),
+          [zz] "=&v"(zz), [l1] "=&v"(l1), [r1] "=&v"(r1), [cl] "=&v"(cl), [cr] "=&v"(cr), [tl] "=&v"(tl),
+          [tr] "=&v"(tr), [aLv] "=&v"(aLv), [aRv] "=&v"(aRv), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t4] "=&v"(t4), [t5] "=&v"(t5), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt),
+          [rm] "=&s"(rm), [am] "=&s"(am), [bm] "=&s"(bm)
+        : [sp] "v"(spare), [base] "s"(base), [b8] "s"(base8), [nbb] "s"(nbb), [mine] "s"(mine), [q] "s"(q),
+          [rp] "s"(rp), [vqx] "v"(vqx), [vqy] "v"(vqy), [q1] "s"(q1), [cq] "s"(cq)
+        : "memory");
+    h = hn;
+    return blk;
+}
+template <int U>
+__device__ int pops_v25(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    int nxt = 0, since = 2;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0;
+    uint2 vq = H[last];
+    u32 rp = H[0].x;
+    int steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool start = nxt < npops && blk == 0 && since >= 2;   // wave-uniform
+            const unsigned long long mine = start ? (1ull << (nxt & 63)) : 0ull;
+            const int nn = nxt + (start ? 1 : 0);
+            const u32 q1 = (u32)(last - nn + 1);
+            blk = step_asm5(nbb, base + 8u, base, h, vx, vy, spare, mine, (u32)(last - nxt),
+                            __builtin_amdgcn_readfirstlane(rp), vq.x, vq.y, q1, (u32)__clz(q1));
+            nxt = nn;
+            since = start ? 1 : since + 1;
+            vq = H[last - nxt];
+            rp = H[0].x;
+        }
+        steps += U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
+__device__ __forceinline__ unsigned long long step_asm6(u32 nbb, u32 base8, u32 base, int& h, u32 vx, u32 vy,
+                                                        int spare, u32 q1, u32 cq, u32 qa, u32& vqx, u32& vqy, u32& rp) {
+    int hn;
+    u32 ad, ax, ay, bx, by, l1, r1, cl, cr, tl, tr, aLv, aRv, t0, t1, t2, t3, t4, t5, qv, rb;
+    unsigned long long sm, blk, tt, rm, am, bm;
+    asm volatile(
+        "v_lshl_add_u32 %[ad], %[h], 4, %[b8]\n\t"
+        "v_min_u32_e32 %[ad], %[nbb], %[ad]\n\t"
+        "ds_read_b32 %[ax], %[ad]\n\t"
+        "ds_read_b32 %[ay], %[ad] offset:4\n\t"
+        "ds_read_b32 %[bx], %[ad] offset:8\n\t"
+        "ds_read_b32 %[by], %[ad] offset:12\n\t"
+        "v_mov_b32_e32 %[qv], %[qa]\n\t"
+        "v_mov_b32_e32 %[rb], %[base]\n\t"
+        "ds_read_b32 %[vqx], %[qv]\n\t"
+        "ds_read_b32 %[vqy], %[qv] offset:4\n\t"
+        "ds_read_b32 %[rp], %[rb]\n\t"
+        "v_lshl_add_u32 %[l1], %[h], 1, 2\n\t"
+        "v_add_u32_e32 %[r1], 1, %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cl], %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cr], %[r1]\n\t"
+        "v_sub_u32_e64 %[cl], %[cl], %[cq]\n\t"
+        "v_sub_u32_e64 %[cr], %[cr], %[cq]\n\t"
+        "v_lshrrev_b32_e64 %[tl], %[cl], %[q1]\n\t"
+        "v_lshrrev_b32_e64 %[tr], %[cr], %[q1]\n\t"
+        "v_cmp_eq_u32_e64 %[am], %[tl], %[l1]\n\t"
+        "v_cmp_eq_u32_e64 %[bm], %[tr], %[r1]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_cndmask_b32_e64 %[aLv], 0, 1, %[am]\n\t"
+        "v_cndmask_b32_e64 %[aRv], 0, 1, %[bm]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], %[by], %[ay]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[ax], %[bx], %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t1], %[ay], %[by], %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[aLv], %[aRv], %[rm]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[t5], 0, %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "v_cmp_ne_u32_e64 %[blk], 0, %[t5]\n\t"
+        : [hn] "=&v"(hn), [ad] "=&v"(ad), [ax] "=&v"(ax), [ay] "=&v"(ay), [bx] "=&v"(bx), [by] "=&v"(by),
+          [l1] "=&v"(l1), [r1] "=&v"(r1), [cl] "=&v"(cl), [cr] "=&v"(cr), [tl] "=&v"(tl), [tr] "=&v"(tr),
+          [aLv] "=&v"(aLv), [aRv] "=&v"(aRv), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+          [t4] "=&v"(t4), [t5] "=&v"(t5), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm),
+          [am] "=&s"(am), [bm] "=&s"(bm), [vqx] "=&v"(vqx), [vqy] "=&v"(vqy), [rp] "=&v"(rp), [qv] "=&v"(qv),
+          [rb] "=&v"(rb)
+        : [qa] "s"(qa), [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b8] "s"(base8),
+          [nbb] "s"(nbb), [q1] "s"(q1), [cq] "s"(cq)
+        : "memory");
+    h = hn;
+    return blk;
+}
+template <int U>
+__device__ int pops_v26(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    int nxt = 0;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0;
+    u32 vqx = H[last].x, vqy = H[last].y, rp = H[0].x;
+    int steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool start = nxt < npops && blk == 0;          // wave-uniform
+            const unsigned long long mine = start ? (1ull << (nxt & 63)) : 0ull;
+            step_asm4(nbb, base + 8u, base, h, vx, vy, spare, mine, (u32)(last - nxt),
+                      __builtin_amdgcn_readfirstlane(rp), vqx, vqy);
+            nxt += start ? 1 : 0;
+            const u32 q1 = (u32)(last - nxt + 1);
+            blk = step_asm6(nbb, base + 8u, base, h, vx, vy, spare, q1, (u32)__clz(q1),
+                            base + 8u * (u32)(last - nxt), vqx, vqy, rp);
+        }
+        steps += 2 * U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
+__device__ __forceinline__ void step_asm7(u32 nbb, u32 base8, u32 base, int& h, u32& vx, u32& vy, int spare,
+                                          unsigned long long mine, u32 q, u32 rp, u32 vqx, u32 vqy) {
+    int hn;
+    u32 ad, ax, ay, bx, by, tq, sa, rv, zz, t0, t1, t2, t3, t4;
+    unsigned long long sm, tt, rm;
+    asm volatile(
+        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
+        "v_mov_b32_e32 %[tq], %[q]\n\t"
+        "v_mov_b32_e32 %[rv], %[rp]\n\t"
+        "v_mov_b32_e32 %[zz], 0\n\t"
+        "v_cndmask_b32_e64 %[sa], %[sp], %[tq], %[mine]\n\t"
+        "v_lshl_add_u32 %[ad], %[h], 4, %[b8]\n\t"
+        "v_lshl_add_u32 %[sa], %[sa], 3, %[base]\n\t"
+        "v_min_u32_e32 %[ad], %[nbb], %[ad]\n\t"
+        "ds_write2_b32 %[sa], %[rv], %[zz] offset1:1\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], %[vqx], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], %[vqy], %[mine]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        : [hn] "=&v"(hn), [h] "+v"(h), [vx] "+v"(vx), [vy] "+v"(vy), [ad] "=&v"(ad), [ax] "=&v"(ax),
+          [tq] "=&v"(tq), [sa] "=&v"(sa), [rv] "=&v"(rv),
+          [zz] "=&v"(zz), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
+          [sm] "=&s"(sm), [tt] "=&s"(tt), [rm] "=&s"(rm)
+        : [sp] "v"(spare), [base] "s"(base), [b8] "s"(base8), [nbb] "s"(nbb), [mine] "s"(mine), [q] "s"(q),
+          [rp] "s"(rp), [vqx] "v"(vqx), [vqy] "v"(vqy)
+        : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+}
+__device__ __forceinline__ unsigned long long step_asm8(u32 nbb, u32 base8, u32 base, int& h, u32 vx, u32 vy,
+                                                        int spare, u32 q1, u32 cq) {
+    int hn;
+    u32 ad, ax, ay, bx, by, l1, r1, cl, cr, tl, tr, aLv, aRv, t0, t1, t2, t3, t4, t5;
+    unsigned long long sm, blk, tt, rm, am, bm;
+    asm volatile(
+        "v_lshl_add_u32 %[ad], %[h], 4, %[b8]\n\t"
+        "v_min_u32_e32 %[ad], %[nbb], %[ad]\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_lshl_add_u32 %[l1], %[h], 1, 2\n\t"
+        "v_add_u32_e32 %[r1], 1, %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cl], %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cr], %[r1]\n\t"
+        "v_sub_u32_e64 %[cl], %[cl], %[cq]\n\t"
+        "v_sub_u32_e64 %[cr], %[cr], %[cq]\n\t"
+        "v_lshrrev_b32_e64 %[tl], %[cl], %[q1]\n\t"
+        "v_lshrrev_b32_e64 %[tr], %[cr], %[q1]\n\t"
+        "v_cmp_eq_u32_e64 %[am], %[tl], %[l1]\n\t"
+        "v_cmp_eq_u32_e64 %[bm], %[tr], %[r1]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_cndmask_b32_e64 %[aLv], 0, 1, %[am]\n\t"
+        "v_cndmask_b32_e64 %[aRv], 0, 1, %[bm]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[aLv], %[aRv], %[rm]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[t5], 0, %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "v_cmp_ne_u32_e64 %[blk], 0, %[t5]\n\t"
+        : [hn] "=&v"(hn), [ad] "=&v"(ad), [by] "=&v"(by),
+          [l1] "=&v"(l1), [r1] "=&v"(r1), [cl] "=&v"(cl), [cr] "=&v"(cr), [tl] "=&v"(tl), [tr] "=&v"(tr),
+          [aLv] "=&v"(aLv), [aRv] "=&v"(aRv), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+          [t4] "=&v"(t4), [t5] "=&v"(t5), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm),
+          [am] "=&s"(am), [bm] "=&s"(bm)
+        : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b8] "s"(base8),
+          [nbb] "s"(nbb), [q1] "s"(q1), [cq] "s"(cq)
+        : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+    return blk;
+}
+template <int U>
+__device__ int pops_v27(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    int nxt = 0;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0;
+    uint2 vq = H[last];
+    u32 rp = H[0].x;
+    int steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool start = nxt < npops && blk == 0;
+            const unsigned long long mine = start ? (1ull << (nxt & 63)) : 0ull;
+            step_asm7(nbb, base + 8u, base, h, vx, vy, spare, mine, (u32)(last - nxt), __builtin_amdgcn_readfirstlane(rp),
+                      vq.x, vq.y);
+            nxt += start ? 1 : 0;
+            const u32 q1 = (u32)(last - nxt + 1);
+            blk = step_asm8(nbb, base + 8u, base, h, vx, vy, spare, q1, (u32)__clz(q1));
+            vq = H[last - nxt];
+            rp = H[0].x;
+        }
+        steps += 2 * U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
+__device__ __forceinline__ unsigned long long step_asm9(u32 nbb, u32 base8, u32 base, int& h, u32 vx, u32 vy,
+                                                        int spare, u32 q1, u32 cq) {
+    int hn;
+    u32 ad, ax, ay, bx, by, l1, r1, cl, cr, tl, tr, aLv, aRv, t0, t1, t2, t3, t4, t5;
+    unsigned long long sm, blk, tt, rm, am, bm;
+    asm volatile(
+        "v_lshl_add_u32 %[ad], %[h], 4, %[b8]\n\t"
+        "v_min_u32_e32 %[ad], %[nbb], %[ad]\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_add_u32_e32 %[l1], 1, %[h]\n\t"
+        "v_ffbh_u32_e32 %[cl], %[l1]\n\t"
+        "v_sub_u32_e64 %[cl], %[cl], %[cq]\n\t"
+        "v_lshrrev_b32_e64 %[tl], %[cl], %[q1]\n\t"
+        "v_subrev_u32_e32 %[tl], 1, %[tl]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "v_cmp_eq_u32_e64 %[am], %[tl], %[t3]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t5], 0, 1, %[am]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[t5], 0, %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "v_cmp_ne_u32_e64 %[blk], 0, %[t5]\n\t"
+        : [hn] "=&v"(hn), [ad] "=&v"(ad), [by] "=&v"(by),
+          [l1] "=&v"(l1), [r1] "=&v"(r1), [cl] "=&v"(cl), [cr] "=&v"(cr), [tl] "=&v"(tl), [tr] "=&v"(tr),
+          [aLv] "=&v"(aLv), [aRv] "=&v"(aRv), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+          [t4] "=&v"(t4), [t5] "=&v"(t5), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm),
+          [am] "=&s"(am), [bm] "=&s"(bm)
+        : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b8] "s"(base8),
+          [nbb] "s"(nbb), [q1] "s"(q1), [cq] "s"(cq)
+        : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+    return blk;
+}
+template <int U>
+__device__ int pops_v28(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    int nxt = 0;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0;
+    uint2 vq = H[last];
+    u32 rp = H[0].x;
+    int steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool start = nxt < npops && blk == 0;
+            const unsigned long long mine = start ? (1ull << (nxt & 63)) : 0ull;
+            step_asm7(nbb, base + 8u, base, h, vx, vy, spare, mine, (u32)(last - nxt), __builtin_amdgcn_readfirstlane(rp),
+                      vq.x, vq.y);
+            nxt += start ? 1 : 0;
+            const u32 q1 = (u32)(last - nxt + 1);
+            blk = step_asm9(nbb, base + 8u, base, h, vx, vy, spare, q1, (u32)__clz(q1) + 1u);
+            vq = H[last - nxt];
+            rp = H[0].x;
+        }
+        steps += 2 * U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
 template <int V>
 __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, const int* npops_in, u64* out_t, const u64* input) {
     __shared__ uint2 H[kCap + 72];
@@ -965,7 +1366,7 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
     if (t < 64 && n >= 2 && npops > 0) {
         const u64 r0 = __builtin_amdgcn_s_memrealtime();
         const u64 t0 = __builtin_amdgcn_s_memtime();
-        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : (u64)pops_v24<4>(H, n, npops);
+        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : (u64)pops_v28<4>(H, n, npops);
         const u64 t1 = __builtin_amdgcn_s_memtime();
         const u64 r1 = __builtin_amdgcn_s_memrealtime();
         if (t == 0) {
@@ -1035,8 +1436,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d_n, segn.data(), nb * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_np, np.data(), nb * 4, hipMemcpyHostToDevice));
     std::vector<u64> out(in.size()), tt(3 * nb);
-    for (int v = 1; v <= 19; ++v) {
-        if (v >= 2 && v <= 16) continue;
+    for (int v = 1; v <= 23; ++v) {
+        if (v >= 2 && v <= 21) continue;
         for (int r = 0; r < reps; ++r) {
             CK(hipMemcpy(d_kv, in.data(), in.size() * 8, hipMemcpyHostToDevice));
             if (v == 1) hipLaunchKernelGGL(k_heap<1>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
@@ -1057,7 +1458,11 @@ int main(int argc, char** argv) {
             else if (v == 16) hipLaunchKernelGGL(k_heap<16>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 17) hipLaunchKernelGGL(k_heap<17>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 18) hipLaunchKernelGGL(k_heap<18>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
-            else hipLaunchKernelGGL(k_heap<19>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 19) hipLaunchKernelGGL(k_heap<19>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 20) hipLaunchKernelGGL(k_heap<20>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 21) hipLaunchKernelGGL(k_heap<21>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 22) hipLaunchKernelGGL(k_heap<22>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else hipLaunchKernelGGL(k_heap<23>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             CK(hipDeviceSynchronize());
         }
         CK(hipMemcpy(out.data(), d_kv, out.size() * 8, hipMemcpyDeviceToHost));
