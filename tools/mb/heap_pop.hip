@@ -1328,6 +1328,141 @@ __device__ int pops_v28(uint2* H, int n, int npops) {
     return steps;
 }
 
+__device__ __forceinline__ void step_asm10(u32 nbb, u32 base8, u32 base, int& h, u32& vx, u32& vy, int spare,
+                                          unsigned long long mine, u32 q, u32 rp, u32 vqx, u32 vqy) {
+    int hn;
+    u32 ad, ax, ay, bx, by, tq, sa, rv, zz, t0, t1, t2, t3, t4;
+    unsigned long long em, es, sm, tt, rm;
+    asm volatile(
+        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
+        "v_mov_b32_e32 %[tq], %[q]\n\t"
+        "v_mov_b32_e32 %[rv], %[rp]\n\t"
+        "v_mov_b32_e32 %[zz], 0\n\t"
+        "v_cndmask_b32_e64 %[sa], %[sp], %[tq], %[mine]\n\t"
+        "v_lshl_add_u32 %[ad], %[h], 4, %[b8]\n\t"
+        "v_lshl_add_u32 %[sa], %[sa], 3, %[base]\n\t"
+        "v_min_u32_e32 %[ad], %[nbb], %[ad]\n\t"
+        "ds_write2_b32 %[sa], %[rv], %[zz] offset1:1\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], %[vqx], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], %[vqy], %[mine]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "v_cmp_ne_u32_e64 %[em], %[h], %[sp]\n\t"
+        "s_nop 1\n\t"
+        "s_and_saveexec_b64 %[es], %[em]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "s_or_b64 exec, exec, %[es]\n\t"
+        : [hn] "=&v"(hn), [h] "+v"(h), [vx] "+v"(vx), [vy] "+v"(vy), [ad] "=&v"(ad), [ax] "=&v"(ax),
+          [tq] "=&v"(tq), [sa] "=&v"(sa), [rv] "=&v"(rv),
+          [zz] "=&v"(zz), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
+          [sm] "=&s"(sm), [em] "=&s"(em), [es] "=&s"(es), [tt] "=&s"(tt), [rm] "=&s"(rm)
+        : [sp] "v"(spare), [base] "s"(base), [b8] "s"(base8), [nbb] "s"(nbb), [mine] "s"(mine), [q] "s"(q),
+          [rp] "s"(rp), [vqx] "v"(vqx), [vqy] "v"(vqy)
+        : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+}
+__device__ __forceinline__ unsigned long long step_asm11(u32 nbb, u32 base8, u32 base, int& h, u32 vx, u32 vy,
+                                                        int spare, u32 q1, u32 cq) {
+    int hn;
+    u32 ad, ax, ay, bx, by, l1, r1, cl, cr, tl, tr, aLv, aRv, t0, t1, t2, t3, t4, t5;
+    unsigned long long em, es, sm, blk, tt, rm, am, bm;
+    asm volatile(
+        "v_lshl_add_u32 %[ad], %[h], 4, %[b8]\n\t"
+        "v_min_u32_e32 %[ad], %[nbb], %[ad]\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_lshl_add_u32 %[l1], %[h], 1, 2\n\t"
+        "v_add_u32_e32 %[r1], 1, %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cl], %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cr], %[r1]\n\t"
+        "v_sub_u32_e64 %[cl], %[cl], %[cq]\n\t"
+        "v_sub_u32_e64 %[cr], %[cr], %[cq]\n\t"
+        "v_lshrrev_b32_e64 %[tl], %[cl], %[q1]\n\t"
+        "v_lshrrev_b32_e64 %[tr], %[cr], %[q1]\n\t"
+        "v_cmp_eq_u32_e64 %[am], %[tl], %[l1]\n\t"
+        "v_cmp_eq_u32_e64 %[bm], %[tr], %[r1]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_cndmask_b32_e64 %[aLv], 0, 1, %[am]\n\t"
+        "v_cndmask_b32_e64 %[aRv], 0, 1, %[bm]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[aLv], %[aRv], %[rm]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[t5], 0, %[sm]\n\t"
+        "v_cmp_ne_u32_e64 %[em], %[h], %[sp]\n\t"
+        "s_nop 1\n\t"
+        "s_and_saveexec_b64 %[es], %[em]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "s_or_b64 exec, exec, %[es]\n\t"
+        "v_cmp_ne_u32_e64 %[blk], 0, %[t5]\n\t"
+        : [hn] "=&v"(hn), [ad] "=&v"(ad), [by] "=&v"(by),
+          [l1] "=&v"(l1), [r1] "=&v"(r1), [cl] "=&v"(cl), [cr] "=&v"(cr), [tl] "=&v"(tl), [tr] "=&v"(tr),
+          [aLv] "=&v"(aLv), [aRv] "=&v"(aRv), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+          [t4] "=&v"(t4), [t5] "=&v"(t5), [sm] "=&s"(sm), [em] "=&s"(em), [es] "=&s"(es), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm),
+          [am] "=&s"(am), [bm] "=&s"(bm)
+        : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b8] "s"(base8),
+          [nbb] "s"(nbb), [q1] "s"(q1), [cq] "s"(cq)
+        : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+    return blk;
+}
+template <int U>
+__device__ int pops_v29(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    int nxt = 0;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0;
+    uint2 vq = H[last];
+    u32 rp = H[0].x;
+    int steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool start = nxt < npops && blk == 0;
+            const unsigned long long mine = start ? (1ull << (nxt & 63)) : 0ull;
+            step_asm10(nbb, base + 8u, base, h, vx, vy, spare, mine, (u32)(last - nxt), __builtin_amdgcn_readfirstlane(rp),
+                      vq.x, vq.y);
+            nxt += start ? 1 : 0;
+            const u32 q1 = (u32)(last - nxt + 1);
+            blk = step_asm11(nbb, base + 8u, base, h, vx, vy, spare, q1, (u32)__clz(q1));
+            vq = H[last - nxt];
+            rp = H[0].x;
+        }
+        steps += 2 * U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
+
 template <int V>
 __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, const int* npops_in, u64* out_t, const u64* input) {
     __shared__ uint2 H[kCap + 72];
@@ -1366,7 +1501,7 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
     if (t < 64 && n >= 2 && npops > 0) {
         const u64 r0 = __builtin_amdgcn_s_memrealtime();
         const u64 t0 = __builtin_amdgcn_s_memtime();
-        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : (u64)pops_v28<4>(H, n, npops);
+        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : V == 23 ? (u64)pops_v28<4>(H, n, npops) : (u64)pops_v29<4>(H, n, npops);
         const u64 t1 = __builtin_amdgcn_s_memtime();
         const u64 r1 = __builtin_amdgcn_s_memrealtime();
         if (t == 0) {
@@ -1383,6 +1518,97 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
         const int keep = V >= 3 && V <= 10 ? (npops > 0 ? n - npops : n) : n;     // v3/v4: the popped tail is in g already
         for (int i = t; i < keep; i += kT) g[i] = ((u64)(H[i].y - (V >= 3 && V <= 10 ? 1u : 0u)) << 32) | H[i].x;
     }
+}
+
+
+// ---- the whole LDS segment path as pf_tie.hip heap_pops_lds runs it, phase by phase (s_memtime) ----------
+__device__ __forceinline__ int ce_lo(int c, int j) { return ((c & ~(j - 1)) << 1) | (c & (j - 1)); }
+__device__ __forceinline__ int pow2_ceil(int n) { return n <= 1 ? 1 : 1 << (32 - __clz(n - 1)); }
+__device__ __forceinline__ void lds_ce_step(uint2* S, int nv, int P, int j, int flipmask) {
+    for (int c = threadIdx.x; c < (P >> 1); c += kT) {
+        const int i = ce_lo(c, j);
+        const int q = flipmask ? (i ^ flipmask) : i + j;
+        if (q < nv) {
+            const uint2 a = S[i], b = S[q];
+            if (b.y < a.y) {
+                S[i] = b;
+                S[q] = a;
+            }
+        }
+    }
+    __syncthreads();
+}
+__device__ void lds_bitonic(uint2* S, int nv, int P) {
+    for (int k = 2; k <= P; k <<= 1) {
+        lds_ce_step(S, nv, P, k >> 1, k - 1);
+        for (int j = k >> 2; j >= 1; j >>= 1) lds_ce_step(S, nv, P, j, 0);
+    }
+}
+__global__ void __launch_bounds__(kT) k_full(u32* keys, u32* vals, int n, int npops, u64* out_t) {
+    __shared__ uint2 H[kCap + 72];
+    const int t = threadIdx.x;
+    u64 tm[6];
+    __syncthreads();
+    tm[0] = __builtin_amdgcn_s_memtime();
+    for (int i = t; i < n; i += kT) H[i] = make_uint2((u32)i, keys[i] + 1u);
+    if (t < 2) H[n + t] = make_uint2(0u, 0u);
+    __syncthreads();
+    tm[1] = __builtin_amdgcn_s_memtime();
+    for (int L = hlev((n - 2) / 2); n >= 2 && L >= 0; --L) {
+        const int lo = (1 << L) - 1, hi = min((2 << L) - 2, (n - 2) / 2);
+        for (int x = lo + t; x <= hi; x += kT) {
+            const uint2 vk = H[x];
+            int h = x;
+            for (;;) {
+                const int c1 = 2 * h + 1;
+                if (c1 >= n) break;
+                int c = c1;
+                uint2 a = H[c1];
+                if (c1 + 1 < n) {
+                    const uint2 b = H[c1 + 1];
+                    if (!(b.y < a.y)) { a = b; c = c1 + 1; }
+                }
+                if (a.y < vk.y) break;
+                H[h] = a;
+                h = c;
+            }
+            H[h] = vk;
+        }
+        __syncthreads();
+    }
+    tm[2] = __builtin_amdgcn_s_memtime();
+    if (t < 64) pops_v27<4>(H, n, npops);
+    __syncthreads();
+    tm[3] = __builtin_amdgcn_s_memtime();
+    if (npops < n - 1) {
+        const int r = n - npops;
+        lds_bitonic(H, r, pow2_ceil(r));
+    }
+    tm[4] = __builtin_amdgcn_s_memtime();
+    constexpr int kPer = (kCap + kT - 1) / kT;
+    u32 gk[kPer], gv[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int i = t + j * kT;
+        if (i < n) {
+            const u32 p = H[i].x;
+            gk[j] = keys[p];
+            gv[j] = vals[p];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int i = t + j * kT;
+        if (i < n) {
+            keys[i] = gk[j];
+            vals[i] = gv[j];
+        }
+    }
+    __syncthreads();
+    tm[5] = __builtin_amdgcn_s_memtime();
+    if (t == 0)
+        for (int k = 0; k < 6; ++k) out_t[k] = tm[k];
 }
 
 struct Case { const char* name; int n; int kind; int npops; };
@@ -1436,8 +1662,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d_n, segn.data(), nb * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_np, np.data(), nb * 4, hipMemcpyHostToDevice));
     std::vector<u64> out(in.size()), tt(3 * nb);
-    for (int v = 1; v <= 23; ++v) {
-        if (v >= 2 && v <= 21) continue;
+    for (int v = 1; v <= 24; ++v) {
+        if (v >= 2 && v <= 21 || v == 23) continue;
         for (int r = 0; r < reps; ++r) {
             CK(hipMemcpy(d_kv, in.data(), in.size() * 8, hipMemcpyHostToDevice));
             if (v == 1) hipLaunchKernelGGL(k_heap<1>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
@@ -1462,7 +1688,8 @@ int main(int argc, char** argv) {
             else if (v == 20) hipLaunchKernelGGL(k_heap<20>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 21) hipLaunchKernelGGL(k_heap<21>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 22) hipLaunchKernelGGL(k_heap<22>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
-            else hipLaunchKernelGGL(k_heap<23>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 23) hipLaunchKernelGGL(k_heap<23>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else hipLaunchKernelGGL(k_heap<24>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             CK(hipDeviceSynchronize());
         }
         CK(hipMemcpy(out.data(), d_kv, out.size() * 8, hipMemcpyDeviceToHost));
@@ -1481,6 +1708,30 @@ int main(int argc, char** argv) {
                         tt[3 * b + 2] / 100.0 / std::max(1, pops));
             if (bad >= 0) std::printf("   first difference at %d\n", bad);
             std::fflush(stdout);
+        }
+    }
+    {   // the whole segment path, phase by phase, on map-like segments with partial pops
+        const int shapes[][2] = {{1500, 400}, {6500, 3900}, {12000, 8000}, {18000, 11000}};
+        for (auto& sh : shapes) {
+            const int n = sh[0], np_ = sh[1];
+            std::vector<u64> a = make_input(n, 4, rng);
+            std::vector<u32> kk(n), vv(n);
+            for (int i = 0; i < n; ++i) { kk[i] = (u32)(a[i] >> 32); vv[i] = (u32)a[i]; }
+            u32 *dk, *dv;
+            u64* dt;
+            CK(hipMalloc(&dk, n * 4)); CK(hipMalloc(&dv, n * 4)); CK(hipMalloc(&dt, 64));
+            u64 tmv[6];
+            for (int r = 0; r < 3; ++r) {
+                CK(hipMemcpy(dk, kk.data(), n * 4, hipMemcpyHostToDevice));
+                CK(hipMemcpy(dv, vv.data(), n * 4, hipMemcpyHostToDevice));
+                hipLaunchKernelGGL(k_full, dim3(1), dim3(kT), 0, 0, dk, dv, n, np_, dt);
+                CK(hipDeviceSynchronize());
+            }
+            CK(hipMemcpy(tmv, dt, 48, hipMemcpyDeviceToHost));
+            std::printf("full n %6d pops %6d: restore %.1f  make_heap %.1f  pops %.1f  rest-sort %.1f  gather %.1f us (at 2.4 GHz)\n",
+                        n, np_, (tmv[1] - tmv[0]) / 2400.0, (tmv[2] - tmv[1]) / 2400.0, (tmv[3] - tmv[2]) / 2400.0,
+                        (tmv[4] - tmv[3]) / 2400.0, (tmv[5] - tmv[4]) / 2400.0);
+            CK(hipFree(dk)); CK(hipFree(dv)); CK(hipFree(dt));
         }
     }
     return 0;
