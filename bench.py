@@ -213,6 +213,8 @@ def run_gpu(rank, local_rank, world, steps, warmup, threads, use_graph, barrier,
     od.init(lid, **ODOM_CFG)
     set_order(od)
     od.set_graph(use_graph)
+    if os.environ.get("PF_BENCH_STAGE_A_RESERVE"):           # development sweep of the stage-A CU mask
+        od.set_stage_a_reserve(int(os.environ["PF_BENCH_STAGE_A_RESERVE"]))
     # stage every scan in HBM (untimed)
     bufs, ptrs, hbufs, hptrs = [], [], [], []
     data_desc = None
