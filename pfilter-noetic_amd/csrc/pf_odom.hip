@@ -3086,6 +3086,17 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
     if (const char* e = std::getenv("PF_STAGE_A_CU_RESERVE")) reserve = std::atoi(e);   // development override
     if (odom_stage_a_stream(o, reserve) != PF_OK && odom_stage_a_stream(o, 0) != PF_OK) return PF_EHIP;
     trace_create("stage A stream");
+    if (std::getenv("PF_STAGE_B_CU_EXCL") && reserve > 0) {   // development: stage B on the reserved CUs only
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, o.device) != hipSuccess) return PF_EHIP;
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int c = ncu - reserve; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
+        hipStream_t sb = nullptr;
+        if (hipExtStreamCreateWithCUMask(&sb, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+            (void)hipStreamDestroy(o.stream);
+            o.stream = sb;
+        }
+    }
     int rc = fe_alloc(o.fe, lidar, in_cap);
     if (rc) return rc;
     trace_create("fe_alloc");
