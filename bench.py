@@ -96,10 +96,16 @@ def parse(argv=None):
                          "bitonic network; DESIGN.md section 5)")
     ap.add_argument("--node-frames", type=int, default=1000,
                     help="frames of the node call pattern (pf_fe_extract -> pf_odom_update); 0 = skip")
+    ap.add_argument("--full-frames", type=int, default=KITTI00_FRAMES - 20,
+                    help="full_sequence object: the headline workload over this many timed frames after 20 "
+                         "warm-up frames whatever --steps is (the KITTI-00 length by default), with its own "
+                         "stage times, stratified CPU baseline and node call patterns; 0 = skip")
+    ap.add_argument("--full-cpu-seconds", type=float, default=40.0,
+                    help="CPU budget of the full sequence's stratified baseline (512 strata take ~12 s)")
     a = ap.parse_args(argv)
     if a.only_headline:
         a.no_roofline = a.no_cpu = a.no_pcie = True
-        a.bpf_frames = a.leg_frames = a.pageable_frames = a.node_frames = a.configs4_frames = 0
+        a.bpf_frames = a.leg_frames = a.pageable_frames = a.node_frames = a.configs4_frames = a.full_frames = 0
     return a
 
 
@@ -806,12 +812,12 @@ class pinned_core:
                 "cores_available": len(self.saved) if self.saved else os.cpu_count()}
 
 
-def _cpu_baseline(budget_s, warmup, preset="S64", theta=(0.4, 75), max_frames=2000, lines=64):
+def _cpu_baseline(budget_s, warmup, preset="S64", theta=(0.4, 75), max_frames=2000, lines=64, wt=0):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pfref
     import pfsynth
     seq = pfsynth.Sequence(preset, n_frames=warmup + max_frames, seed=0)
-    orc = pfref.Odom(pfref.make_lidar(lines, 3.0, 90.0), 0.4, 0, theta[0], theta[1], 0, opts=0)
+    orc = pfref.Odom(pfref.make_lidar(lines, 3.0, 90.0), 0.4, 0, theta[0], theta[1], wt, opts=0)
     for k in range(warmup):
         orc.frame(seq.frame(k))
     n, el, k = 0, 0.0, warmup
@@ -931,8 +937,10 @@ def pose_diff(a, b):
 
 
 ES_LEGS = {
-    # name: (preset, theta_p, theta_max, what it is)
+    # name: (preset, theta_p, theta_max, what it is[, weightType])
     "theta0": ("S64", 0.0, 0, "configs[0] parameters (k_new=0 theta_p=0 theta_max=0, FLOAM-equivalent) on S64"),
+    "weight2": ("S64", 0.4, 75, "configs[1] parameters with weightType 2 (launch/pfilter_kitti.launch:7's default; "
+                                "SURVEY 8(d) config 2's secondary run) on S64", 2),
     "campus32": ("S32", 1.0, 200, "configs[2]: 32-line campus scans (S32, 2 m/s), k_new=0 theta_p=1 theta_max=200"),
     "dense": ("S64V", 0.4, 75, "configs[1] parameters on S64V: residential scene with vegetation and rough "
                                "ground, denser features and maps than S64 (KITTI-00-like sizes)"),
@@ -946,8 +954,9 @@ def es_leg(name, device, nframes, threads, cpu_seconds, warmup=20, use_graph=Tru
     with per-stage device timing (pf_odom_set_stage_timing: stage A = featureExtraction + VoxelGrid,
     stage B = odometry), and the CPU port on the leg's first frames after the same warm-up."""
     import pfilter_amd as pa
-    preset, tp, tm, what = ES_LEGS[name]
-    cfg = dict(ODOM_CFG, theta_p=tp, theta_max=tm)
+    preset, tp, tm, what = ES_LEGS[name][:4]
+    wt = ES_LEGS[name][4] if len(ES_LEGS[name]) > 4 else 0
+    cfg = dict(ODOM_CFG, theta_p=tp, theta_max=tm, weightType=wt)
     lines = 32 if preset == "S32" else 64
     total = warmup + nframes
     bufs, ptrs = [], []
@@ -985,7 +994,8 @@ def es_leg(name, device, nframes, threads, cpu_seconds, warmup=20, use_graph=Tru
            "last_frame": {k: st[k] for k in ("n_in", "n_ds", "n_map", "n_res")}}
     if with_cpu:
         with pinned_core() as pc:
-            cb = _cpu_baseline(cpu_seconds, warmup, preset=preset, theta=(tp, tm), max_frames=nframes, lines=lines)
+            cb = _cpu_baseline(cpu_seconds, warmup, preset=preset, theta=(tp, tm), max_frames=nframes, lines=lines,
+                               wt=wt)
             cb["host"] = pc.host()
         f0, f1 = cb.pop("frames")
         out["cpu_baseline"] = cb
@@ -1143,6 +1153,51 @@ def gpu_window(device, f0, f1, threads, use_graph=True):
     od.sync()
     el = time.perf_counter() - t0
     return {"value": round((f1 - f0) / el, 2), "frames": [f0, f1]}
+
+
+def full_sequence_leg(local_rank, threads, use_graph, nframes, cpu_seconds, with_cpu, head=None, head_cpu=None,
+                      node=True):
+    """The north star's number over the whole sequence, whatever the headline's --steps: the headline
+    workload (configs[1], S64 seed 0) over `nframes` timed frames after 20 warm-up frames (the KITTI-00
+    length by default), timed like the headline; the per-stage device times over the same frames; the
+    stratified synced CPU baseline over them (512 strata, cpu_baseline_synced); the ratio; and the
+    nodes' synchronous call pattern (node_pattern, node_threads) over all of them. head: the headline's
+    own run when it already covers these frames (then it is reused, not re-run)."""
+    warm = 20
+    if head is not None and head["frames"] == nframes:
+        r = head
+        reused = True
+    else:
+        r = run_gpu(0, local_rank, 1, nframes, warm, threads, use_graph, lambda: None, keep_host=node)
+        reused = False
+    value = r["frames"] / r["elapsed"]
+    out = {"value": round(value, 2), "unit": "frames/s", "frames": r["frames"], "warmup": warm,
+           "frame_range": [warm, warm + r["frames"] - 1], "ms_per_step": round(r["elapsed"] / r["frames"] * 1e3, 4),
+           "sequence": r["data"], "same_run_as_value": reused,
+           "host_enqueue_us_per_frame": round(r.get("enqueue", 0.0) / max(1, r["frames"]) * 1e6, 1)}
+    out["stage_us"] = stage_pass(local_rank, r["ptrs"], warm, r["frames"], use_graph)
+    log("full_sequence: %s" % out)
+    if node and r.get("hptrs"):
+        try:
+            nd = node_pattern_leg(local_rank, r["hptrs"], warm, r["frames"])
+            npo = nd.pop("poses")
+            nd["poses_equal_pipeline"] = bool(np.array_equal(npo, r["poses"][:npo.shape[0]]))
+            nd["ratio_to_pipeline"] = round(nd["value"] / value, 4)
+            out["node_pattern"] = nd
+            nt = node_threads_leg(local_rank, r["hptrs"], warm, r["frames"])
+            ntp = nt.pop("poses")
+            nt["poses_equal_pipeline"] = bool(np.array_equal(ntp, r["poses"][:ntp.shape[0]]))
+            nt["ratio_to_pipeline"] = round(nt["value"] / value, 4)
+            out["node_threads"] = nt
+            log("full_sequence node legs: %s / %s" % (nd["value"], nt["value"]))
+        except Exception as e:  # report, never hide
+            log("full-sequence node legs failed: %r" % (e,))
+    if with_cpu:
+        cb = head_cpu if (reused and head_cpu is not None) else \
+            cpu_baseline_synced(local_rank, r["ptrs"], warm, cpu_seconds, use_graph)
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu"] = round(value / cb["value"], 2)
+    return out
 
 
 def stub_run(rank, steps):
@@ -1338,6 +1393,19 @@ def main(argv=None):
         # a stratified sample of those frames for the CPU)
         out["speedup_vs_cpu"] = round(value / cb["value"], 2)
         log("cpu_baseline: %s" % cb)
+    if world == 1 and not stub and args.full_frames > 0:
+        log("full sequence (%d frames) ..." % args.full_frames)
+        same = args.warmup == 20 and frames == args.full_frames
+        head = dict(r) if same else None
+        del r                                    # the headline's scans leave HBM / pinned RAM first
+        try:
+            out["full_sequence"] = full_sequence_leg(local_rank, threads, graph_mode(args), args.full_frames,
+                                                     args.full_cpu_seconds, not args.no_cpu, head=head,
+                                                     head_cpu=out.get("cpu_baseline"))
+            log("full_sequence: %s" % out["full_sequence"])
+        except Exception as e:  # report, never hide
+            log("full-sequence leg failed: %r" % (e,))
+            out["full_sequence"] = None
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

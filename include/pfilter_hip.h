@@ -342,7 +342,12 @@ int pf_odom_set_graph(pf_odom* h, int mode);
  * every f32 centroid is summed in the reference's order. It runs introsort's recursion on the device
  * (pf_tie.h) in place of the radix sorts. enable = 0 is the faster stable mode: stable radix sorts
  * (VoxelGrid) and a merge of the voxel-ordered map with the sorted appended points (rgbds); its
- * centroids' last bits differ from the reference's in 0.5-1 % of frames. */
+ * centroids' last bits differ from the reference's in 0.5-1 % of frames.
+ * Capacity limit: the tie sort keeps one level's big segments (> 65536 keys each) in a 512-entry list,
+ * so a handle whose rgbds sort capacity (the maps plus appended points, about 2 x map_capacity for ES,
+ * 3 x for BPF) exceeds about 32M elements cannot run it: pf_odom_set_tie_order(h, 1) returns PF_EINVAL
+ * and leaves the handle unchanged, and pf_odom_create / pf_bpf_create create such a handle in the stable
+ * order instead of failing. A failed allocation (PF_ENOMEM) leaves the handle in its previous order. */
 int pf_odom_set_tie_order(pf_odom* h, int enable);
 /* Measurement: the association's kNN alone (the exact 5-NN of k_assoc, src/odomEstimationClass.cpp:299,
  * 447) on the last frame's queries -- its down-sampled points through the solved pose -- against the

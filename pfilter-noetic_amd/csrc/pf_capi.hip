@@ -291,8 +291,14 @@ static int create(const pf_lidar_params* lidar, const pf_odom_params* params, in
     if (!h) return PF_ENOMEM;
     int rc = odom_create(h->o, *lidar, *params, device, max_points, map_capacity, nc);
     // the reference's results by default: VoxelGrid / rgbds / the sector sort in std::sort's order of
-    // equal keys (pf_odom_set_tie_order(h, 0) selects the stable sorts)
-    if (rc == PF_OK) rc = pf_odom_set_tie_order(h, 1);
+    // equal keys (pf_odom_set_tie_order(h, 0) selects the stable sorts). A sort capacity past the tie
+    // sort's per-level big-segment list (tie_alloc: PF_EINVAL from about 32M elements, i.e. map_capacity
+    // of about 16M for ES / 10.5M for BPF) keeps the handle in the stable order rather than failing the
+    // create, as before round 5; pf_odom_set_tie_order(h, 1) then returns PF_EINVAL for it
+    if (rc == PF_OK) {
+        rc = pf_odom_set_tie_order(h, 1);
+        if (rc == PF_EINVAL) rc = PF_OK;
+    }
     if (rc != PF_OK) {
         pf_odom_destroy(h);
         return rc;
@@ -1368,11 +1374,24 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
     PF_HIP_TRY(odom_sync_a(o));
     PF_HIP_TRY(hipStreamSynchronize(o.stream));
     if (enable && !o.tie_a) {
+        // all or nothing: a failed allocation leaves neither sort behind, so the handle stays in the
+        // stable order and a later call starts from scratch
+        auto drop = [&o]() {
+            for (TieSort** t : {&o.tie_a, &o.tie_b})
+                if (*t) {
+                    tie_free(**t);
+                    delete *t;
+                    *t = nullptr;
+                }
+        };
         o.tie_a = new (std::nothrow) TieSort();
         o.tie_b = new (std::nothrow) TieSort();
-        if (!o.tie_a || !o.tie_b) return PF_ENOMEM;
-        if (int rc = tie_alloc(*o.tie_a, (size_t)o.cls.nc * o.in_cap)) return rc;
-        if (int rc = tie_alloc(*o.tie_b, o.sort_cap)) return rc;
+        int rc = (!o.tie_a || !o.tie_b) ? PF_ENOMEM : tie_alloc(*o.tie_a, (size_t)o.cls.nc * o.in_cap);
+        if (rc == PF_OK) rc = tie_alloc(*o.tie_b, o.sort_cap);
+        if (rc != PF_OK) {
+            drop();
+            return rc;
+        }
     }
     if (enable) {
         if (int rc = odom_dep_alloc(o)) return rc;

@@ -277,6 +277,7 @@ struct OdomGPU {
 };
 // the dependence table of the tie-order rgbds (allocated with the tie sorts, pf_odom_set_tie_order)
 int odom_dep_alloc(OdomGPU& o);
+void odom_dep_release(OdomGPU& o);                 // frees the table (also after a failed alloc)
 void odom_dep_dirty(OdomGPU& o, hipStream_t s);   // the maps were written by the host or initMapWithPoints
 
 // Stage A keeps off the last CUs of the device by default: with one sequence per GPU, stage B's LM

@@ -1831,7 +1831,7 @@ constexpr int kDepSmallApp = 1 << (kDepSmallBits - 2);   // appended points the 
 // this update's table: the small one (clean map, few appended points) or the full one
 template <int NC>
 __device__ __forceinline__ bool dep_small(const DepTab& T, const int* cnt) {
-    if (!T.key || !T.dirty || T.dirty[0] != 0u) return false;
+    if (!T.key || !T.dirty || T.dirty[0] != 0u || T.hbits < kDepSmallBits) return false;
     int na = 0;
 #pragma unroll
     for (int c = 0; c < NC; ++c) na += cnt[C_DS + c];
@@ -3226,23 +3226,42 @@ void odom_dep_dirty(OdomGPU& o, hipStream_t s) {
     if (o.dep_dirty) hipLaunchKernelGGL(k_dep_dirty, dim3(1), dim3(64), 0, s, o.dep_dirty);
 }
 
-// the table holds every element of one rgbds call (at most sort_cap) at a load of at most 0.8
+// the table holds every element of one rgbds call (at most sort_cap) at a load of at most 0.8, and never
+// fewer than the 2^kDepSmallBits slots the small-table path (dep_small, k_rg_dep_probe, k_rg_dep) hashes
+// into and scans whatever the handle's capacity
 int odom_dep_alloc(OdomGPU& o) {
     if (o.dep_key) return PF_OK;
-    u32 hb = 10;
+    u32 hb = kDepSmallBits;
     while (((size_t)1 << hb) < o.sort_cap + o.sort_cap / 4) ++hb;
     const size_t h = (size_t)1 << hb;
+    int rc = PF_OK;
     if (hipMalloc(&o.dep_key, sizeof(u32) * h) != hipSuccess || hipMalloc(&o.dep_cnt, sizeof(u32) * h) != hipSuccess ||
         hipMalloc(&o.dep_mem, sizeof(u32) * 3 * h) != hipSuccess ||
         hipMalloc(&o.dep_slot, sizeof(u32) * o.sort_cap) != hipSuccess ||
-        hipMalloc(&o.dep_free, o.sort_cap) != hipSuccess || hipMalloc(&o.dep_dirty, sizeof(u32) * 2) != hipSuccess)
-        return PF_ENOMEM;
-    const u32 dirty0[2] = {1u, 0u};
-    if (hipMemset(o.dep_key, 0xFF, sizeof(u32) * h) != hipSuccess || hipMemset(o.dep_cnt, 0, sizeof(u32) * h) != hipSuccess ||
-        hipMemcpy(o.dep_dirty, dirty0, sizeof(dirty0), hipMemcpyHostToDevice) != hipSuccess)
-        return PF_EHIP;
+        hipMalloc(&o.dep_free, o.sort_cap) != hipSuccess || hipMalloc(&o.dep_dirty, sizeof(u32) * 2) != hipSuccess) {
+        rc = PF_ENOMEM;
+    } else {
+        const u32 dirty0[2] = {1u, 0u};
+        if (hipMemset(o.dep_key, 0xFF, sizeof(u32) * h) != hipSuccess ||
+            hipMemset(o.dep_cnt, 0, sizeof(u32) * h) != hipSuccess ||
+            hipMemcpy(o.dep_dirty, dirty0, sizeof(dirty0), hipMemcpyHostToDevice) != hipSuccess)
+            rc = PF_EHIP;
+    }
+    if (rc != PF_OK) {                 // nothing half-allocated stays behind (a later call retries cleanly)
+        odom_dep_release(o);
+        return rc;
+    }
     o.dep_hbits = hb;
     return PF_OK;
+}
+
+void odom_dep_release(OdomGPU& o) {
+    for (void* q : {(void*)o.dep_key, (void*)o.dep_cnt, (void*)o.dep_mem, (void*)o.dep_slot, (void*)o.dep_free,
+                    (void*)o.dep_dirty})
+        if (q) (void)hipFree(q);
+    o.dep_key = o.dep_cnt = o.dep_mem = o.dep_slot = o.dep_dirty = nullptr;
+    o.dep_free = nullptr;
+    o.dep_hbits = 0;
 }
 
 int odom_reset(OdomGPU& o) {
@@ -3348,9 +3367,7 @@ void odom_destroy(OdomGPU& o) {
             tie_free(*t);
             delete t;
         }
-    for (void* q : {(void*)o.dep_key, (void*)o.dep_cnt, (void*)o.dep_mem, (void*)o.dep_slot, (void*)o.dep_free,
-                    (void*)o.dep_dirty})
-        (void)hipFree(q);
+    odom_dep_release(o);
     o = OdomGPU{};
 }
 

@@ -16,6 +16,24 @@ def init(preset, n_frames, seed, lidar, ring_model, params, opts):
     _ctx["args"] = (lidar, ring_model, params, opts)
 
 
+def init_multi(preset, n_by_seed, lidar, ring_model, params, opts):
+    """several sequences in one pool (configs[3]: KITTI 00-10 as seeds 0..10): built on first use"""
+    _ctx["multi"] = (preset, dict(n_by_seed))
+    _ctx["seqs"] = {}
+    _ctx["args"] = (lidar, ring_model, params, opts)
+
+
+def run_multi(task):
+    """task = (seed, k, maps, odom pose, last_odom pose, optimization_count) -> (seed, k, pose, counts, maps)"""
+    import pfsynth
+    seed, k = task[0], task[1]
+    if seed not in _ctx["seqs"]:
+        preset, nbs = _ctx["multi"]
+        _ctx["seqs"][seed] = pfsynth.Sequence(preset, n_frames=nbs[seed], seed=seed)
+    _ctx["seq"] = _ctx["seqs"][seed]
+    return (seed,) + run(task[1:])
+
+
 def run(task):
     """task = (k, [(xyz, rg) per map class] before frame k, odom pose, last_odom pose, optimization_count)
     -> (k, pose after frame k, counts, [(xyz, rg) per map class] after frame k)"""

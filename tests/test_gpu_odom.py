@@ -70,9 +70,13 @@ def test_pose_and_map_parity_kitti_config(pa, pfref, pfsynth, order):
 
 @pytest.mark.parametrize("wt", [1, 2, 12])
 def test_weight_types(pa, pfref, pfsynth, wt):
-    seq = pfsynth.Sequence("S64", n_frames=20, az_steps=1200)
+    """weightType 1 / 2 / 12 (include/odomEstimationClass.h:111-126; 2 is pfilter_kitti.launch:7's
+    default) free-running against the oracle over 120 frames, maps every 17th; weightType 2 also has a
+    whole-sequence synced case (tests/test_gpu_parity_synced.py configs1_S64_wt2)."""
+    seq = pfsynth.Sequence("S64", n_frames=130, az_steps=1200)
     od, orc = _pair(pa, pfref, wt=wt)
-    _run(od, orc, seq, range(12), check_maps_every=11)
+    _run(od, orc, seq, range(120), check_maps_every=17)
+    _compare_maps(od, orc)
 
 
 @pytest.mark.parametrize("k_new,theta_p,theta_max", [(0, 0.0, 0), (2, 0.4, 75), (1, 0.8, 30)])
@@ -199,6 +203,44 @@ def test_update_api_matches_oracle(pa, pfref, pfsynth):
         assert dt < TOL_T and dr < TOL_R
         np.testing.assert_array_equal(pg, od.odom)
     _compare_maps(od, orc)
+
+
+def test_small_capacity_handle_tie_order(pa, pfref, pfsynth):
+    """A handle with small caps (max_points 2000, map_capacity 10000: rgbds sort capacity 24000, so the
+    dependence table's own size would be 2^15 slots, below the 2^16 the small-table path hashes into)
+    in the default tie order, fed sub-sampled features through the update API for 12 frames: poses,
+    every count and both maps (xyz within the tolerance, age / p-index bytes identical) against the
+    oracle, and the same bits as a default-capacity handle (the table is now never smaller
+    than the small path's 2^16 slots)."""
+    seq = pfsynth.Sequence("S64", n_frames=12, az_steps=1000)
+    lid = pfref.make_lidar(64, 3.0, 90.0)
+    small = pa.Odom_ES_EstimationClass(device=0, max_points=2000, map_capacity=10000)
+    small.init(pa.make_lidar(64, 3.0, 90.0), 0.4, 0, 0.4, 75, 0)
+    big, orc = _pair(pa, pfref)
+    for k in range(12):
+        e, s = pfref.feature_extraction(seq.frame(k), lid, opts=0)
+        e = e[:: max(1, -(-len(e) // 1500))][:2000]
+        s = s[:: max(1, -(-len(s) // 1500))][:2000]
+        if k == 0:
+            for od in (small, big):
+                od.initMapWithPoints(e, s)
+            orc.init_map(e, s)
+            continue
+        ps = small.updatePointsToMap(e, s)
+        pb = big.updatePointsToMap(e, s)
+        pr = orc.update(e, s)
+        np.testing.assert_array_equal(ps, pb)
+        dt, dr = pose_err(ps, pr)
+        assert dt < TOL_T and dr < TOL_R, (k, dt, dr)
+        ss, sr = small.stats(), orc.stats()
+        for c in COUNTS:
+            assert ss[c] == sr[c], (k, c, ss[c], sr[c])
+        assert ss["errors"] == 0
+    _compare_maps(small, orc)
+    for a, b in ((small.laserCloudCornerMap, big.laserCloudCornerMap),
+                 (small.laserCloudSurfMap, big.laserCloudSurfMap)):
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
 
 
 def test_device_pipeline_graph_equals_eager(pa, pfsynth):
