@@ -52,9 +52,13 @@ void sort_pairs(std::vector<IdxPair>& iv, bool stable) {
         pfref_introsort_stats(k.data(), k.size(), st);
         std::fprintf(stderr, "sort n %zu levels %ld heaps %ld max %ld keys %ld g3segs %ld g3max %ld dupkeys %ld\n", k.size(),
                      st[0], st[1], st[2], st[3], st[4], st[5], st[6]);
-        if (const char* dump = std::getenv("PFREF_SORT_DUMP")) {         // keys of sorts above 1M, appended
-            if (k.size() > (1u << 20)) {
+        if (const char* dump = std::getenv("PFREF_SORT_DUMP")) {   // keys of sorts above PFREF_SORT_DUMP_MIN
+            static const size_t dmin = std::getenv("PFREF_SORT_DUMP_MIN") ?     // (default 1M), appended,
+                std::strtoull(std::getenv("PFREF_SORT_DUMP_MIN"), nullptr, 10) : (1u << 20);   // each after its count
+            if (k.size() > dmin) {
                 if (FILE* f = std::fopen(dump, "ab")) {
+                    const uint32_t cnt = (uint32_t)k.size();
+                    if (dmin != (1u << 20)) std::fwrite(&cnt, sizeof(cnt), 1, f);
                     std::fwrite(k.data(), sizeof(uint32_t), k.size(), f);
                     std::fclose(f);
                 }

@@ -1417,6 +1417,20 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
 
 // development / test switch (not part of include/pfilter_hip.h): rgbds in the default order by the
 // full radix sort of every element (the path before the merge) instead of the merge, for A/B checks
+// development / test switch (not part of include/pfilter_hip.h): the rgbds tie sort's partition-tier
+// depth-limit segments heap-sorted on stage B's side stream beside k_tie_local (1, the default) or after
+// it on stage B's own stream (0), for A/B checks (TieAux, pf_tie.h)
+extern "C" int pf_dev_set_tie_aux(pf_odom* h, int enable) {
+    if (!h) return PF_EINVAL;
+    OdomGPU& o = h->o;
+    PF_HIP_TRY(hipSetDevice(o.device));
+    PF_HIP_TRY(odom_sync_a(o));
+    PF_HIP_TRY(hipStreamSynchronize(o.stream));
+    if ((enable != 0) != o.tie_aux) drop_graphs_b(o);   // the captured stage B gains / loses the fork
+    o.tie_aux = enable != 0;
+    return PF_OK;
+}
+
 // development / test switch: every tie-order rgbds takes the full dependence table (DepTab in pf_odom.hip:
 // each update starts as if the host had written the map), for the A/B check of the small table
 extern "C" int pf_dev_set_dep_full(pf_odom* h, int enable) {

@@ -3079,6 +3079,11 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
         o.leaf_rg[c] = plane ? (float)prm.map_res * 2 : (float)prm.map_res;     // float map_resolution (.h:62)
     }
     if (hipStreamCreateWithFlags(&o.stream, hipStreamNonBlocking) != hipSuccess) return PF_EHIP;
+    if (hipStreamCreateWithFlags(&o.stream_bx, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&o.ev_bx_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&o.ev_bx_join, hipEventDisableTiming) != hipSuccess)
+        return PF_EHIP;
+    if (const char* e = std::getenv("PF_TIE_AUX")) o.tie_aux = std::atoi(e) != 0;   // development A/B
     trace_create("stream");
     // stage A is kept off the last compute units by default (odom_stage_a_stream), so that stage B's
     // kernels — the LM needs kLmBlocks co-resident workgroups — find free CUs while stage A runs
@@ -3362,6 +3367,9 @@ void odom_destroy(OdomGPU& o) {
     if (o.h_map_n) (void)hipHostFree(o.h_map_n);
     if (o.stream) (void)hipStreamDestroy(o.stream);
     if (o.stream_a) (void)hipStreamDestroy(o.stream_a);
+    if (o.stream_bx) (void)hipStreamDestroy(o.stream_bx);
+    if (o.ev_bx_fork) (void)hipEventDestroy(o.ev_bx_fork);
+    if (o.ev_bx_join) (void)hipEventDestroy(o.ev_bx_join);
     for (TieSort* t : {o.tie_a, o.tie_b})
         if (t) {
             tie_free(*t);
@@ -3502,8 +3510,13 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
             PF_LAUNCH_NC(nc, k_rg_dep_probe, dim3(kGrid), dim3(256), 0, s, cnt, o.keys, dt);
             PF_LAUNCH_NC(nc, k_rg_dep, dim3(kGrid), dim3(256), 0, s, cnt, clouds(map_cur(o)), clouds(o.app), dt);
         }
+        TieAux aux;
+        aux.s = o.tie_aux ? o.stream_bx : nullptr;
+        aux.fork = o.ev_bx_fork;
+        aux.join = o.ev_bx_join;
         tie_sort(*o.tie_b, o.keys, o.vals, TieClasses{cnt, C_M, C_DS, nc}, o.prim.err, s,
-                 std::max(tie_levels_for(*o.tie_b, o.tie_hint), PF_TIE_LEVELS_B), dt.key ? o.dep_free : nullptr);
+                 std::max(tie_levels_for(*o.tie_b, o.tie_hint), PF_TIE_LEVELS_B), dt.key ? o.dep_free : nullptr,
+                 &aux);
     }
     else
         radix_sort_pairs(o.keys, o.vals, cnt + C_NRG, 32, o.prim, s, nullptr, nullptr, true);

@@ -64,13 +64,15 @@ struct TieSort {
     u32 *k = nullptr, *v = nullptr;       // [cap] compacted pairs (the working copy)
     u32 *lp = nullptr, *rq = nullptr;     // [cap] left / right stop positions by rank
     u64* status = nullptr;                // [tiles] look-back words, zero between launches
-    u32* arrive = nullptr;                // [4] arrival counters (look-backs, local-kernel exit)
+    u32* arrive = nullptr;                // [8] arrival counters (look-backs, local-kernel / heap exits)
     int4* big = nullptr;                  // [2][bcap] big segments of a level {first, last, depth, tile base}
     u64* tot = nullptr;                   // [bcap] stop totals of a big segment (nL << 32 | nR)
     int4* med = nullptr;                  // [mcap] medium segments {first, last, depth, class}
     int4* mid = nullptr;                  // [midcap] mid-tier segments {first, last, depth, class}
     int4* jobs = nullptr;                 // [jcap] local jobs {first, last, depth (-1: at the limit), class}
     int2* heaps = nullptr;                // [hcap] depth-limit segments {output offset, length}
+    int4* heapw = nullptr;                // [hcap] those the partition tiers filed (TieAux): {working offset,
+                                          // length, class, 0}, heap-sorted beside k_tie_local
     u64* hbig = nullptr;                  // [cap + 64] heap entries of segments above the LDS size
     int* ctl = nullptr;                   // counters (pf_tie.hip)
     // sorts with big levels: depth-limit segments above the LDS size, and (with dependence flags) every
@@ -109,8 +111,17 @@ int tie_levels_for(const TieSort& t, size_t size_hint);
 // bit 4. freef (optional, indexed by val): nonzero when the element's voxel group is order-free (its f32
 // centroid sum does not depend on the order of its points; pf_odom.hip k_rg_dep): the heap tier then
 // runs only the pops the order-dependent groups need. NULL: every group counts as order-dependent.
+// aux (optional, sorts without big levels): a second stream and two events. The depth-limit segments the
+// partition tiers k_tie_medium / k_tie_mid produce are then heap-sorted by a k_tie_heap launch on aux that
+// starts when k_tie_mid ends and runs beside k_tie_local (and the heap launch of the local tier's own
+// depth-limit segments); s waits for it before the sort returns. Without aux every depth-limit segment
+// goes through k_tie_local to the one heap launch after it.
+struct TieAux {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
 void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s, int levels = 0,
-              const u8* freef = nullptr);
+              const u8* freef = nullptr, const TieAux* aux = nullptr);
 const int* tie_valid_count(const TieSort& t);   // device word: the valid pairs of the last sort
 
 }  // namespace pf

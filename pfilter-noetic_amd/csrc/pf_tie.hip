@@ -33,6 +33,7 @@ enum {
     T_BASE = 20,        // [kMaxTieC] where class c starts in the working copy
     T_NHEAPF = 24,      // huge segments the heap tier still sorts (TieSort::heapf)
     T_HUGEN = 25,       // pairs of the huge segments
+    T_NHEAPW = 26,      // depth-limit segments the partition tiers filed for the aux heap launch (TieAux)
     T_WORDS = 32
 };
 __device__ __forceinline__ u64* big_ctr(int* ctl, int p) { return reinterpret_cast<u64*>(ctl + T_BIG) + p; }
@@ -938,14 +939,24 @@ __device__ __forceinline__ bool range_dep(const u32* v, const u8* freef, int f, 
 }
 
 // hands a segment on: to the LDS mid tier above kTieSmall keys, else (and final segments) to the locals
+// with a heap list (TieAux) a segment at the depth limit goes there, to be heap-sorted beside k_tie_local
+__device__ __forceinline__ void file_heapw(int* ctl, int4* hw, int hwcap, int* err, int f, int e, int c) {
+    const int j = atomicAdd(&ctl[T_NHEAPW], 1);
+    if (j < hwcap) hw[j] = make_int4(f, e - f, c, 0);
+    else atomicOr(err, 4);
+}
 struct EmitGlobal {
     int* ctl;
     int4 *mid, *jobs;
     int midcap, jcap, cls;
     int* err;
+    int4* hw;
+    int hwcap;
     __device__ void operator()(int f, int e, int d) const {
         if (e - f < 1) return;
-        if (d >= 0 && e - f > kTieSmall) {
+        if (d == -1 && hw) {
+            file_heapw(ctl, hw, hwcap, err, f, e, cls);
+        } else if (d >= 0 && e - f > kTieSmall) {
             const int j = atomicAdd(&ctl[T_NMID], 1);
             if (j < midcap) mid[j] = make_int4(f, e, d, cls);
             else atomicOr(err, 4);
@@ -961,7 +972,7 @@ __global__ void __launch_bounds__(1024) k_tie_medium(const u32* __restrict__ key
                                                      TieClasses cls, int from_classes, int depth0, u32* k, u32* v,
                                                      u32* lp, u32* rq, int* ctl, const int4* __restrict__ med,
                                                      int4* mid, int midcap, int4* jobs, int jcap, int* err,
-                                                     const u8* __restrict__ freef) {
+                                                     const u8* __restrict__ freef, int4* hw, int hwcap) {
     __shared__ MedWork<512> S;
     const int t = threadIdx.x, w = t >> 6, l = lane_id();
     const u64 lt = lanemask_lt();
@@ -1037,7 +1048,7 @@ __global__ void __launch_bounds__(1024) k_tie_medium(const u32* __restrict__ key
         }
         if (freef && d0 > 0 && e0 - f0 > kTieSmall && !range_dep(v, freef, f0, e0)) d0 = kDepFree;
         GStore st{k, v, lp, rq, f0};
-        part_levels<512>(st, S, f0, e0, d0, kTieMid, EmitGlobal{ctl, mid, jobs, midcap, jcap, cl, err}, err,
+        part_levels<512>(st, S, f0, e0, d0, kTieMid, EmitGlobal{ctl, mid, jobs, midcap, jcap, cl, err, hw, hwcap}, err,
                          blockIdx.x == 0 && it == 0 ? 256 : -1);
     }
 }
@@ -1054,10 +1065,16 @@ struct EmitJob {
     int4* jobs;
     int jcap, cls, off;
     int* err;
-    __device__ void operator()(int f, int e, int d) const { file_job(ctl, jobs, jcap, err, off + f, off + e, d, cls); }
+    int4* hw;
+    int hwcap;
+    __device__ void operator()(int f, int e, int d) const {
+        if (d == -1 && hw && e - f > 0) file_heapw(ctl, hw, hwcap, err, off + f, off + e, cls);
+        else file_job(ctl, jobs, jcap, err, off + f, off + e, d, cls);
+    }
 };
 __global__ void __launch_bounds__(1024) k_tie_mid(u32* k, u32* v, int* ctl, const int4* __restrict__ mid,
-                                                  int4* jobs, int jcap, int* err, const u8* __restrict__ freef) {
+                                                  int4* jobs, int jcap, int* err, const u8* __restrict__ freef,
+                                                  int4* hw, int hwcap) {
     __shared__ MidLds S;
     const int t = threadIdx.x;
     const int nm = ctl[T_NMID];
@@ -1074,7 +1091,7 @@ __global__ void __launch_bounds__(1024) k_tie_mid(u32* k, u32* v, int* ctl, cons
         }
         __syncthreads();
         LStore st{S.K, S.I, S.LP, S.RP};
-        part_levels<16>(st, S.W, 0, len, mi.z, kTieSmall, EmitJob{ctl, jobs, jcap, mi.w, f, err}, err,
+        part_levels<16>(st, S.W, 0, len, mi.z, kTieSmall, EmitJob{ctl, jobs, jcap, mi.w, f, err, hw, hwcap}, err,
                         blockIdx.x == 0 && it == 0 ? 512 : -1);
         // back to the working copy: the values the keys carry gathered into the (now free) rank lists
         // first, since the gather reads the same range of v that is then written
@@ -1576,6 +1593,7 @@ __global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, c
 // global scratch copy
 constexpr int kHeapT = 1024;
 constexpr int kHeapGrid = 256;
+constexpr int kHeapGridW = 64;          // the aux launch (TieAux): a few depth-limit segments per sort
 
 __device__ __forceinline__ int hlev(int x) { return 31 - __clz(x + 1); }
 
@@ -2089,16 +2107,34 @@ __device__ void heap_segment_pairs(u32* __restrict__ keys, u32* __restrict__ val
 
 // which: the list's counter (T_NHEAP, or T_NHEAPF for the huge segments the radix sort could not finish);
 // the last workgroup out zeroes it and, with also >= 0, that counter too
+// wsegs (TieAux): the list holds working-copy segments {offset, length, class} of a partition tier,
+// copied to their place in the output (working index + the class's output base, as k_tie_local places
+// them) before they are sorted there
 __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32* __restrict__ vals, int* ctl,
                                                      const int2* __restrict__ segs, u64* __restrict__ big,
                                                      int bigcap, u32* __restrict__ arrive,
                                                      const u8* __restrict__ freef, int which, int also,
-                                                     int2* __restrict__ route, int routecap, int* err) {
+                                                     int2* __restrict__ route, int routecap, int* err,
+                                                     const int4* __restrict__ wsegs, const u32* __restrict__ wk,
+                                                     const u32* __restrict__ wv, int nc) {
     __shared__ uint2 H[kHeapCap + 64];             // + a spare slot per lane of wave 0
     const int t = threadIdx.x;
     const int nh = ctl[which];
     for (int jb = blockIdx.x; jb < nh; jb += gridDim.x) {
-        const int2 sg = segs[jb];
+        int2 sg;
+        if (wsegs) {
+            const int4 w4 = wsegs[jb];
+            int ob = -ctl[T_BASE + w4.z];
+            for (int c = 0; c < nc && c < w4.z; ++c) ob += ctl[T_VC + c];
+            sg = make_int2(w4.x + ob, w4.y);
+            for (int i = t; i < w4.y; i += kHeapT) {
+                keys[sg.x + i] = wk[w4.x + i];
+                vals[sg.x + i] = wv[w4.x + i];
+            }
+            __syncthreads();
+        } else {
+            sg = segs[jb];
+        }
         const int off = sg.x, n = sg.y;
         if (route && freef) {               // no order-dependent element: the radix sort after this launch
             int dep = 0;
@@ -2319,13 +2355,14 @@ int tie_alloc(TieSort& t, size_t cap, int max_levels) {
     PF_TALLOC(t.lp, sizeof(u32) * cap);
     PF_TALLOC(t.rq, sizeof(u32) * cap);
     PF_TALLOC(t.status, sizeof(u64) * t.tiles);
-    PF_TALLOC(t.arrive, sizeof(u32) * 4);
+    PF_TALLOC(t.arrive, sizeof(u32) * 8);
     PF_TALLOC(t.big, sizeof(int4) * 2 * t.bcap);
     PF_TALLOC(t.tot, sizeof(u64) * t.bcap);
     PF_TALLOC(t.med, sizeof(int4) * t.mcap);
     PF_TALLOC(t.mid, sizeof(int4) * t.midcap);
     PF_TALLOC(t.jobs, sizeof(int4) * t.jcap);
     PF_TALLOC(t.heaps, sizeof(int2) * t.hcap);
+    PF_TALLOC(t.heapw, sizeof(int4) * t.hcap);
     PF_TALLOC(t.hbig, sizeof(u64) * (cap + 64));     // segments above the LDS size, at their own offsets
     PF_TALLOC(t.ctl, sizeof(int) * T_WORDS);
     if (max_levels > 0) {
@@ -2340,14 +2377,14 @@ int tie_alloc(TieSort& t, size_t cap, int max_levels) {
         if (int rc = prim_alloc(t.hprim, cap)) return rc;
     }
 #undef PF_TALLOC
-    if (hipMemset(t.status, 0, sizeof(u64) * t.tiles) != hipSuccess || hipMemset(t.arrive, 0, sizeof(u32) * 4) != hipSuccess ||
+    if (hipMemset(t.status, 0, sizeof(u64) * t.tiles) != hipSuccess || hipMemset(t.arrive, 0, sizeof(u32) * 8) != hipSuccess ||
         hipMemset(t.ctl, 0, sizeof(int) * T_WORDS) != hipSuccess)
         return PF_EHIP;
     return PF_OK;
 }
 
 void tie_free(TieSort& t) {
-    void* ptrs[] = {t.k, t.v, t.lp, t.rq, t.status, t.arrive, t.big, t.tot, t.med, t.mid, t.jobs, t.heaps, t.hbig,
+    void* ptrs[] = {t.k, t.v, t.lp, t.rq, t.status, t.arrive, t.big, t.tot, t.med, t.mid, t.jobs, t.heaps, t.heapw, t.hbig,
                     t.ctl, t.huge, t.heapf, t.need, t.hk, t.hv, t.hseg, t.hbase, t.depn};
     for (void* p : ptrs) (void)hipFree(p);
     if (t.hprim.cap) prim_free(t.hprim);
@@ -2361,16 +2398,19 @@ int tie_levels_for(const TieSort& t, size_t size_hint) {
 }
 
 void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s, int levels,
-              const u8* freef) {
+              const u8* freef, const TieAux* aux) {
     if (levels > t.max_levels) levels = t.max_levels;
     // the radix route (sorts with big levels): huge depth-limit segments and, with dependence flags,
     // every segment without an order-dependent group, from any tier
     const bool huge = levels > 0 && t.huge;
     const u8* rf = huge ? freef : nullptr;
     u32* depn = rf ? t.depn : nullptr;
+    // the partition tiers' depth-limit segments heap-sorted on aux beside k_tie_local (no big levels)
+    const bool side = aux && aux->s && levels <= 0;
+    int4* hw = side ? t.heapw : nullptr;
     if (levels <= 0) {
         hipLaunchKernelGGL(k_tie_medium, dim3(kMaxTieC), dim3(kMT), 0, s, keys, vals, cls, 1, t.depth0, t.k, t.v,
-                           t.lp, t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err, rf);
+                           t.lp, t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err, rf, hw, t.hcap);
     } else {
         const int tg = (int)(t.tiles < (size_t)kTieGrid ? t.tiles : (size_t)kTieGrid);
         hipLaunchKernelGGL(k_tie_compact, dim3(tg), dim3(256), 0, s, keys, vals, cls, t.k, t.v, t.ctl, t.status,
@@ -2385,13 +2425,24 @@ void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStr
                                t.mcap, err, depn);
         }
         hipLaunchKernelGGL(k_tie_medium, dim3(kMedGrid), dim3(kMT), 0, s, keys, vals, cls, 0, t.depth0, t.k, t.v, t.lp,
-                           t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err, rf);
+                           t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err, rf, (int4*)nullptr, 0);
     }
-    hipLaunchKernelGGL(k_tie_mid, dim3(kMidGrid), dim3(kMT), 0, s, t.k, t.v, t.ctl, t.mid, t.jobs, t.jcap, err, rf);
+    hipLaunchKernelGGL(k_tie_mid, dim3(kMidGrid), dim3(kMT), 0, s, t.k, t.v, t.ctl, t.mid, t.jobs, t.jcap, err, rf, hw,
+                       t.hcap);
+    if (side) {     // fork: the tiers' depth-limit segments are all filed, in the working copy
+        (void)hipEventRecord(aux->fork, s);
+        (void)hipStreamWaitEvent(aux->s, aux->fork, 0);
+        hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGridW), dim3(kHeapT), 0, aux->s, keys, vals, t.ctl, (const int2*)nullptr,
+                           t.hbig, (int)t.cap, t.arrive + 4, freef, (int)T_NHEAPW, -1, (int2*)nullptr, 0, err,
+                           (const int4*)t.heapw, (const u32*)t.k, (const u32*)t.v, cls.nc);
+        (void)hipEventRecord(aux->join, aux->s);
+    }
     hipLaunchKernelGGL(k_tie_local, dim3(kLocalGrid), dim3(1024), 0, s, t.k, t.v, t.jobs, t.ctl, t.arrive + 2, keys,
                        vals, cls, HeapList{t.heaps, t.hcap, err, huge ? t.huge : nullptr, t.hugecap}, rf);
     hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heaps, t.hbig,
-                       (int)t.cap, t.arrive + 3, freef, (int)T_NHEAP, -1, huge ? t.huge : nullptr, t.hugecap, err);
+                       (int)t.cap, t.arrive + 3, freef, (int)T_NHEAP, -1, huge ? t.huge : nullptr, t.hugecap, err,
+                       (const int4*)nullptr, (const u32*)nullptr, (const u32*)nullptr, cls.nc);
+    if (side) (void)hipStreamWaitEvent(s, aux->join, 0);   // join
     if (huge) {
         PrimWork pw = t.hprim;
         pw.err = err;
@@ -2404,7 +2455,8 @@ void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStr
         hipLaunchKernelGGL(k_huge_finish, dim3(kHugeGrid), dim3(256), 0, s, keys, vals, t.ctl, t.hugecap, t.hseg,
                            t.hbase, t.hk, t.hv, t.need, t.heapf);
         hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heapf, t.hbig,
-                           (int)t.cap, t.arrive + 3, freef, (int)T_NHEAPF, (int)T_NHUGE, (int2*)nullptr, 0, err);
+                           (int)t.cap, t.arrive + 3, freef, (int)T_NHEAPF, (int)T_NHUGE, (int2*)nullptr, 0, err,
+                           (const int4*)nullptr, (const u32*)nullptr, (const u32*)nullptr, cls.nc);
     }
 }
 

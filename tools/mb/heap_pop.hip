@@ -1292,6 +1292,328 @@ __device__ __forceinline__ unsigned long long step_asm9(u32 nbb, u32 base8, u32 
     h = hn;
     return blk;
 }
+
+// v30..v32 (round 6): v27 with the idle lanes' spare holes shared (one slot n + 2 for every idle lane:
+// their ds_write2_b32 then hit one address, where 64 distinct 8-byte slots put two lanes of a 32-lane
+// group on every even bank) and / or consecutive pops dealt to different 16-lane groups of ds_read2_b64
+// (pop i on lane ((i & 3) << 4) | ((i >> 2) & 15): <= 2 pops in flight share a group up to 8 in flight)
+template <int U, bool SHARED, bool PERM>
+__device__ int pops_v30(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = SHARED ? n + 2 : n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    int nxt = 0;
+    int h = spare;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0;
+    uint2 vq = H[last];
+    u32 rp = H[0].x;
+    int steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool start = nxt < npops && blk == 0;
+            const int ln = PERM ? (((nxt & 3) << 4) | ((nxt >> 2) & 15)) : (nxt & 63);
+            const unsigned long long mine = start ? (1ull << ln) : 0ull;
+            step_asm7(nbb, base + 8u, base, h, vx, vy, spare, mine, (u32)(last - nxt), __builtin_amdgcn_readfirstlane(rp),
+                      vq.x, vq.y);
+            nxt += start ? 1 : 0;
+            const u32 q1 = (u32)(last - nxt + 1);
+            blk = step_asm8(nbb, base + 8u, base, h, vx, vy, spare, q1, (u32)__clz(q1));
+            vq = H[last - nxt];
+            rp = H[0].x;
+        }
+        steps += 2 * U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
+// v33..v35 (round 6): the children address of every hole carried from step to step instead of recomputed
+// from the hole at the next step's start: a step computes both candidates (left child's children, right
+// child's children, each clamped to the sentinels) while its loads are in flight and selects the next one
+// with the same right / stop masks as the hole, so the chain between the loads' return and the next loads'
+// issue loses the shift-add and the clamp (two dependent VALU). Idle lanes carry the sentinel address.
+__device__ __forceinline__ void step_asm12(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32 vb8, u32 vnbb, u32& vx,
+                                           u32& vy, int spare, unsigned long long mine, u32 q, u32 rp, u32 vqx,
+                                           u32 vqy) {
+    int hn;
+    u32 tq, sa, rv, zz, t0, t1, t2, t3, t4, aL, aR, aN;
+    unsigned long long sm, tt, rm;
+    asm volatile(
+        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
+        "v_cndmask_b32_e64 %[ad], %[ad], %[vb8], %[mine]\n\t"
+        "v_mov_b32_e32 %[tq], %[q]\n\t"
+        "v_mov_b32_e32 %[rv], %[rp]\n\t"
+        "v_mov_b32_e32 %[zz], 0\n\t"
+        "v_cndmask_b32_e64 %[sa], %[sp], %[tq], %[mine]\n\t"
+        "v_lshl_add_u32 %[sa], %[sa], 3, %[base]\n\t"
+        "ds_write2_b32 %[sa], %[rv], %[zz] offset1:1\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], %[vqx], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], %[vqy], %[mine]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+        "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+        "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+        "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        : [hn] "=&v"(hn), [h] "+v"(h), [ad] "+v"(ad), [vx] "+v"(vx), [vy] "+v"(vy), [tq] "=&v"(tq), [sa] "=&v"(sa),
+          [rv] "=&v"(rv), [zz] "=&v"(zz), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+          [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR), [aN] "=&v"(aN), [sm] "=&s"(sm), [tt] "=&s"(tt),
+          [rm] "=&s"(rm)
+        : [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24), [nbb] "s"(nbb), [vb8] "v"(vb8), [vnbb] "v"(vnbb),
+          [mine] "s"(mine), [q] "s"(q), [rp] "s"(rp), [vqx] "v"(vqx), [vqy] "v"(vqy)
+        : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+}
+__device__ __forceinline__ unsigned long long step_asm13(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32 vnbb, u32 vx,
+                                                         u32 vy, int spare, u32 q1, u32 cq) {
+    int hn;
+    u32 l1, r1, cl, cr, tl, tr, aLv, aRv, t0, t1, t2, t3, t4, t5, aL, aR, aN;
+    unsigned long long sm, blk, tt, rm, am, bm;
+    asm volatile(
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_lshl_add_u32 %[l1], %[h], 1, 2\n\t"
+        "v_add_u32_e32 %[r1], 1, %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cl], %[l1]\n\t"
+        "v_ffbh_u32_e32 %[cr], %[r1]\n\t"
+        "v_sub_u32_e64 %[cl], %[cl], %[cq]\n\t"
+        "v_sub_u32_e64 %[cr], %[cr], %[cq]\n\t"
+        "v_lshrrev_b32_e64 %[tl], %[cl], %[q1]\n\t"
+        "v_lshrrev_b32_e64 %[tr], %[cr], %[q1]\n\t"
+        "v_cmp_eq_u32_e64 %[am], %[tl], %[l1]\n\t"
+        "v_cmp_eq_u32_e64 %[bm], %[tr], %[r1]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+        "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+        "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+        "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+        "v_cndmask_b32_e64 %[aLv], 0, 1, %[am]\n\t"
+        "v_cndmask_b32_e64 %[aRv], 0, 1, %[bm]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[aLv], %[aRv], %[rm]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t5], %[t5], 0, %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "v_cmp_ne_u32_e64 %[blk], 0, %[t5]\n\t"
+        : [hn] "=&v"(hn), [ad] "+v"(ad), [l1] "=&v"(l1), [r1] "=&v"(r1), [cl] "=&v"(cl), [cr] "=&v"(cr),
+          [tl] "=&v"(tl), [tr] "=&v"(tr), [aLv] "=&v"(aLv), [aRv] "=&v"(aRv), [t0] "=&v"(t0), [t1] "=&v"(t1),
+          [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [t5] "=&v"(t5), [aL] "=&v"(aL), [aR] "=&v"(aR),
+          [aN] "=&v"(aN), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm), [am] "=&s"(am),
+          [bm] "=&s"(bm)
+        : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24),
+          [nbb] "s"(nbb), [vnbb] "v"(vnbb), [q1] "s"(q1), [cq] "s"(cq)
+        : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+    return blk;
+}
+template <int U, bool SHARED, bool PERM>
+__device__ int pops_v33(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = SHARED ? n + 2 : n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    const u32 b24 = base + 24u;                 // children of child c = 2h + 1 + r: base + 8 + 16 c
+    u32 vb8 = base + 8u, vnbb = nbb;            // VGPR copies (a VOP3 select reads one SGPR: the mask)
+    asm volatile("" : "+v"(vb8), "+v"(vnbb));
+    int nxt = 0;
+    int h = spare;
+    u32 ad = nbb;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0;
+    uint2 vq = H[last];
+    u32 rp = H[0].x;
+    int steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool start = nxt < npops && blk == 0;
+            const int ln = PERM ? (((nxt & 3) << 4) | ((nxt >> 2) & 15)) : (nxt & 63);
+            const unsigned long long mine = start ? (1ull << ln) : 0ull;
+            step_asm12(nbb, base, b24, h, ad, vb8, vnbb, vx, vy, spare, mine, (u32)(last - nxt),
+                       __builtin_amdgcn_readfirstlane(rp), vq.x, vq.y);
+            nxt += start ? 1 : 0;
+            const u32 q1 = (u32)(last - nxt + 1);
+            blk = step_asm13(nbb, base, b24, h, ad, vnbb, vx, vy, spare, q1, (u32)__clz(q1));
+            vq = H[last - nxt];
+            rp = H[0].x;
+        }
+        steps += 2 * U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+
+// v36/v37 (round 6): v33's carried address plus a block test on the level of each hole: q's ancestor at the
+// level of a lane's new hole is (q + 1) >> (lev(q) - lev) (one shift, taken while the loads are in flight;
+// the level is a per-lane counter), so the test after the loads is one compare of that ancestor with the new
+// hole (a stopped lane's new hole is its spare, which is never an ancestor of q): 13 VALU -> 5 per step B
+__device__ __forceinline__ void step_asm14(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32& lh, u32 vb8, u32 vnbb,
+                                           u32& vx, u32& vy, int spare, unsigned long long mine, u32 q, u32 rp,
+                                           u32 vqx, u32 vqy) {
+    int hn;
+    u32 tq, sa, rv, zz, t0, t1, t2, t3, t4, aL, aR, aN;
+    unsigned long long sm, tt, rm;
+    asm volatile(
+        "v_cndmask_b32_e64 %[ad], %[ad], %[vb8], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
+        "v_mov_b32_e32 %[tq], %[q]\n\t"
+        "v_mov_b32_e32 %[rv], %[rp]\n\t"
+        "v_mov_b32_e32 %[zz], 0\n\t"
+        "v_cndmask_b32_e64 %[sa], %[sp], %[tq], %[mine]\n\t"
+        "v_lshl_add_u32 %[sa], %[sa], 3, %[base]\n\t"
+        "ds_write2_b32 %[sa], %[rv], %[zz] offset1:1\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], %[vqx], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], %[vqy], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[lh], %[lh], 0, %[mine]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+        "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+        "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+        "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+        "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        : [hn] "=&v"(hn), [h] "+v"(h), [ad] "+v"(ad), [lh] "+v"(lh), [vx] "+v"(vx), [vy] "+v"(vy), [tq] "=&v"(tq),
+          [sa] "=&v"(sa), [rv] "=&v"(rv), [zz] "=&v"(zz), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR), [aN] "=&v"(aN), [sm] "=&s"(sm),
+          [tt] "=&s"(tt), [rm] "=&s"(rm)
+        : [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24), [nbb] "s"(nbb), [vb8] "v"(vb8), [vnbb] "v"(vnbb),
+          [mine] "s"(mine), [q] "s"(q), [rp] "s"(rp), [vqx] "v"(vqx), [vqy] "v"(vqy)
+        : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+}
+// lq1 = lev(q) - 1 (scalar); the lane's new hole is at level lh + 1
+__device__ __forceinline__ unsigned long long step_asm15(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32& lh,
+                                                         u32 vnbb, u32 vx, u32 vy, int spare, u32 q1, u32 lq1) {
+    int hn;
+    u32 sh, an, t0, t1, t2, t3, t4, aL, aR, aN;
+    unsigned long long sm, blk, tt, rm;
+    asm volatile(
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_sub_u32_e32 %[sh], %[lq1], %[lh]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshrrev_b32_e64 %[an], %[sh], %[q1]\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+        "v_add_u32_e32 %[an], -1, %[an]\n\t"
+        "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+        "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+        "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+        "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cmp_eq_u32_e64 %[blk], %[an], %[hn]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        : [hn] "=&v"(hn), [ad] "+v"(ad), [lh] "+v"(lh), [sh] "=&v"(sh), [an] "=&v"(an), [t0] "=&v"(t0),
+          [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR),
+          [aN] "=&v"(aN), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm)
+        : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24),
+          [nbb] "s"(nbb), [vnbb] "v"(vnbb), [q1] "s"(q1), [lq1] "s"(lq1)
+        : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+    return blk;
+}
+template <int U, bool SHARED, bool PERM>
+__device__ int pops_v36(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = SHARED ? n + 2 : n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    const u32 b24 = base + 24u;
+    u32 vb8 = base + 8u, vnbb = nbb;
+    asm volatile("" : "+v"(vb8), "+v"(vnbb));
+    int nxt = 0;
+    int h = spare;
+    u32 ad = nbb, lh = 0u;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0;
+    uint2 vq = H[last];
+    u32 rp = H[0].x;
+    int steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool start = nxt < npops && blk == 0;
+            const int ln = PERM ? (((nxt & 3) << 4) | ((nxt >> 2) & 15)) : (nxt & 63);
+            const unsigned long long mine = start ? (1ull << ln) : 0ull;
+            step_asm14(nbb, base, b24, h, ad, lh, vb8, vnbb, vx, vy, spare, mine, (u32)(last - nxt),
+                       __builtin_amdgcn_readfirstlane(rp), vq.x, vq.y);
+            nxt += start ? 1 : 0;
+            const u32 q1 = (u32)(last - nxt + 1);
+            blk = step_asm15(nbb, base, b24, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)));
+            vq = H[last - nxt];
+            rp = H[0].x;
+        }
+        steps += 2 * U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
 template <int U>
 __device__ int pops_v28(uint2* H, int n, int npops) {
     n = __builtin_amdgcn_readfirstlane(n);
@@ -1501,7 +1823,7 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
     if (t < 64 && n >= 2 && npops > 0) {
         const u64 r0 = __builtin_amdgcn_s_memrealtime();
         const u64 t0 = __builtin_amdgcn_s_memtime();
-        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : V == 23 ? (u64)pops_v28<4>(H, n, npops) : (u64)pops_v29<4>(H, n, npops);
+        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : V == 23 ? (u64)pops_v28<4>(H, n, npops) : V == 24 ? (u64)pops_v29<4>(H, n, npops) : V == 25 ? (u64)pops_v30<4, true, false>(H, n, npops) : V == 26 ? (u64)pops_v30<4, false, true>(H, n, npops) : V == 27 ? (u64)pops_v30<4, true, true>(H, n, npops) : V == 28 ? (u64)pops_v33<4, false, false>(H, n, npops) : V == 29 ? (u64)pops_v33<4, true, true>(H, n, npops) : V == 30 ? (u64)pops_v36<4, false, false>(H, n, npops) : (u64)pops_v36<4, true, true>(H, n, npops);
         const u64 t1 = __builtin_amdgcn_s_memtime();
         const u64 r1 = __builtin_amdgcn_s_memrealtime();
         if (t == 0) {
@@ -1662,8 +1984,9 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d_n, segn.data(), nb * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_np, np.data(), nb * 4, hipMemcpyHostToDevice));
     std::vector<u64> out(in.size()), tt(3 * nb);
-    for (int v = 1; v <= 24; ++v) {
-        if (v >= 2 && v <= 21 || v == 23) continue;
+    const int vlo = argc > 2 ? std::atoi(argv[2]) : 22;
+    for (int v = vlo; v <= 31; ++v) {
+        if (v >= 2 && v <= 21 || v == 23 || v == 24) continue;
         for (int r = 0; r < reps; ++r) {
             CK(hipMemcpy(d_kv, in.data(), in.size() * 8, hipMemcpyHostToDevice));
             if (v == 1) hipLaunchKernelGGL(k_heap<1>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
@@ -1689,7 +2012,14 @@ int main(int argc, char** argv) {
             else if (v == 21) hipLaunchKernelGGL(k_heap<21>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 22) hipLaunchKernelGGL(k_heap<22>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 23) hipLaunchKernelGGL(k_heap<23>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
-            else hipLaunchKernelGGL(k_heap<24>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 24) hipLaunchKernelGGL(k_heap<24>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 25) hipLaunchKernelGGL(k_heap<25>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 26) hipLaunchKernelGGL(k_heap<26>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 27) hipLaunchKernelGGL(k_heap<27>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 28) hipLaunchKernelGGL(k_heap<28>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 29) hipLaunchKernelGGL(k_heap<29>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 30) hipLaunchKernelGGL(k_heap<30>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else hipLaunchKernelGGL(k_heap<31>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             CK(hipDeviceSynchronize());
         }
         CK(hipMemcpy(out.data(), d_kv, out.size() * 8, hipMemcpyDeviceToHost));
