@@ -1418,8 +1418,8 @@ int pf_odom_set_tie_order(pf_odom* h, int enable) {
 // development / test switch (not part of include/pfilter_hip.h): rgbds in the default order by the
 // full radix sort of every element (the path before the merge) instead of the merge, for A/B checks
 // development / test switch (not part of include/pfilter_hip.h): the rgbds tie sort's partition-tier
-// depth-limit segments heap-sorted on stage B's side stream beside k_tie_local (1, the default) or after
-// it on stage B's own stream (0), for A/B checks (TieAux, pf_tie.h)
+// depth-limit segments heap-sorted on stage B's side stream beside k_tie_local (1) or after
+// it on stage B's own stream (0, the default), for A/B checks (TieAux, pf_tie.h)
 extern "C" int pf_dev_set_tie_aux(pf_odom* h, int enable) {
     if (!h) return PF_EINVAL;
     OdomGPU& o = h->o;

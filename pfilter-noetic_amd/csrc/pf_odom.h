@@ -144,11 +144,14 @@ struct OdomGPU {
     int device = 0;
     hipStream_t stream = nullptr;      // stage B: odometry
     hipStream_t stream_a = nullptr;    // stage A: featureExtraction + VoxelGrid
-    // stage B's side stream: the rgbds tie sort heap-sorts its partition tiers' depth-limit segments there
-    // beside k_tie_local (TieAux, pf_tie.h); tie_aux = 0 keeps them on stage B's stream (pf_dev_set_tie_aux)
+    // stage B's side stream (development switch pf_dev_set_tie_aux / PF_TIE_AUX=1, off by default): the
+    // rgbds tie sort heap-sorts its partition tiers' depth-limit segments there beside k_tie_local
+    // (TieAux, pf_tie.h). Measured on the headline: 844.9 frames/s on against 844.7 off -- the heap
+    // workgroups need a whole CU's LDS and wait for k_tie_local's to drain -- and the stage-B timing
+    // events then miss the side stream's work, so it stays off
     hipStream_t stream_bx = nullptr;
     hipEvent_t ev_bx_fork = nullptr, ev_bx_join = nullptr;
-    bool tie_aux = true;
+    bool tie_aux = false;
     size_t in_cap = 0, map_cap = 0, sort_cap = 0, pose_cap = 0;
     int opt_count_host = 2;
     bool inited = false;

@@ -560,7 +560,8 @@ struct MedWork {
     u32 msum;
 };
 
-// working copy in global memory; ranks listed at the item's own offset of t.lp / t.rq
+// working copy in global memory; ranks listed at the item's own offset of t.lp / t.rq (round 6 measured
+// an LDS cache of the ranks the rank-space passes read: no change, 845.2 vs 844.9 frames/s, not kept)
 struct GStore {
     u32 *k, *v, *lp, *rq;
     int base;
@@ -781,7 +782,6 @@ __device__ void part_levels(St& st, MedWork<NSEG>& S, int f0, int e0, int d0, in
             }
             __syncthreads();
         }
-        const u32 TL = S.carry[nt & 1][0];
         __threadfence_block();
         __syncthreads();
         PART_PROF(8 * lev + 1, rt_now());
@@ -1868,6 +1868,155 @@ __device__ void lds_pops(uint2* H, int n, int npops) {
     }
 }
 
+
+// Round 6 engine (tools/mb/heap_pop.hip v36/v37): the same pipelined pops with (1) every hole's children
+// address carried from step to step (both candidates computed while the loads are in flight, selected by
+// the step's own right / stop masks: the shift-add and the clamp leave the chain between a step's loads and
+// the next step's), (2) the block test on the level of each hole: q's ancestor at the level of a lane's new
+// hole is (q + 1) >> (lev(q) - lev) - 1, one shift taken while the loads are in flight, so the test after
+// them is one compare with the new hole (a stopped lane's new hole is its spare, never an ancestor of q);
+// 13 VALU of step B's block test become 5, (3) PF_POP_SHARED: every idle lane parks on one spare slot
+// (their hole writes then hit one address; 64 distinct 8-byte slots put two lanes of a 32-lane store group
+// on every even bank), (4) PF_POP_PERM: consecutive pops dealt to different 16-lane groups of ds_read2_b64
+// (pop i on lane ((i & 3) << 4) | ((i >> 2) & 15))
+__device__ __forceinline__ void lds_pop_step_c(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32& lh, u32 vb8, u32 vnbb,
+                                           u32& vx, u32& vy, int spare, unsigned long long mine, u32 q, u32 rp,
+                                           u32 vqx, u32 vqy) {
+    int hn;
+    u32 tq, sa, rv, zz, t0, t1, t2, t3, t4, aL, aR, aN;
+    unsigned long long sm, tt, rm;
+    asm volatile(
+        "v_cndmask_b32_e64 %[ad], %[ad], %[vb8], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
+        "v_mov_b32_e32 %[tq], %[q]\n\t"
+        "v_mov_b32_e32 %[rv], %[rp]\n\t"
+        "v_mov_b32_e32 %[zz], 0\n\t"
+        "v_cndmask_b32_e64 %[sa], %[sp], %[tq], %[mine]\n\t"
+        "v_lshl_add_u32 %[sa], %[sa], 3, %[base]\n\t"
+        "ds_write2_b32 %[sa], %[rv], %[zz] offset1:1\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], %[vqx], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], %[vqy], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[lh], %[lh], 0, %[mine]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+        "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+        "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+        "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+        "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        : [hn] "=&v"(hn), [h] "+v"(h), [ad] "+v"(ad), [lh] "+v"(lh), [vx] "+v"(vx), [vy] "+v"(vy), [tq] "=&v"(tq),
+          [sa] "=&v"(sa), [rv] "=&v"(rv), [zz] "=&v"(zz), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR), [aN] "=&v"(aN), [sm] "=&s"(sm),
+          [tt] "=&s"(tt), [rm] "=&s"(rm)
+        : [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24), [nbb] "s"(nbb), [vb8] "v"(vb8), [vnbb] "v"(vnbb),
+          [mine] "s"(mine), [q] "s"(q), [rp] "s"(rp), [vqx] "v"(vqx), [vqy] "v"(vqy)
+        : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+}
+// lq1 = lev(q) - 1 (scalar); the lane's new hole is at level lh + 1
+__device__ __forceinline__ unsigned long long lds_pop_step_d(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32& lh,
+                                                         u32 vnbb, u32 vx, u32 vy, int spare, u32 q1, u32 lq1) {
+    int hn;
+    u32 sh, an, t0, t1, t2, t3, t4, aL, aR, aN;
+    unsigned long long sm, blk, tt, rm;
+    asm volatile(
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_sub_u32_e32 %[sh], %[lq1], %[lh]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshrrev_b32_e64 %[an], %[sh], %[q1]\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+        "v_add_u32_e32 %[an], -1, %[an]\n\t"
+        "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+        "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+        "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+        "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cmp_eq_u32_e64 %[blk], %[an], %[hn]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        : [hn] "=&v"(hn), [ad] "+v"(ad), [lh] "+v"(lh), [sh] "=&v"(sh), [an] "=&v"(an), [t0] "=&v"(t0),
+          [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR),
+          [aN] "=&v"(aN), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm)
+        : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24),
+          [nbb] "s"(nbb), [vnbb] "v"(vnbb), [q1] "s"(q1), [lq1] "s"(lq1)
+        : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+    return blk;
+}
+
+template <bool SHARED, bool PERM>
+__device__ void lds_pops2(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = SHARED ? n + 2 : n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    const u32 b24 = base + 24u;                 // children of child c = 2h + 1 + r: base + 8 + 16 c
+    u32 vb8 = base + 8u, vnbb = nbb;            // VGPR copies (a VOP3 select reads one SGPR: the mask)
+    asm volatile("" : "+v"(vb8), "+v"(vnbb));
+    int nxt = 0;
+    int h = spare;
+    u32 ad = nbb, lh = 0u;
+    u32 vx = 0u, vy = 1u;                       // an idle lane's value: above the sentinels
+    unsigned long long blk = 0;
+    uint2 vq = H[last];
+    u32 rp = H[0].x;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool start = nxt < npops && blk == 0;          // wave-uniform
+            const int ln = PERM ? (((nxt & 3) << 4) | ((nxt >> 2) & 15)) : (nxt & 63);
+            const unsigned long long mine = start ? (1ull << ln) : 0ull;
+            lds_pop_step_c(nbb, base, b24, h, ad, lh, vb8, vnbb, vx, vy, spare, mine, (u32)(last - nxt),
+                           __builtin_amdgcn_readfirstlane(rp), vq.x, vq.y);
+            nxt += start ? 1 : 0;
+            const u32 q1 = (u32)(last - nxt + 1);
+            blk = lds_pop_step_d(nbb, base, b24, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)));
+            vq = H[last - nxt];                                  // the next start's value and root
+            rp = H[0].x;
+        }
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+    }
+}
+#ifndef PF_POP_ENGINE
+#define PF_POP_ENGINE 2       // 1: round 5's lds_pops; 2: lds_pops2 (round 6)
+#endif
+#ifndef PF_POP_SHARED
+#define PF_POP_SHARED 0
+#endif
+#ifndef PF_POP_PERM
+#define PF_POP_PERM 0
+#endif
+
 // A segment whose keys are all distinct has one sorted order, so whatever sorts it gives __sort_heap's
 // exact result: the heap tier first sorts a copy with a bitonic network and keeps it when no two
 // neighbours are equal; a segment with an equal pair is restored and heap-sorted. (The depth limit is
@@ -2003,7 +2152,10 @@ __device__ void heap_pops_lds(u32* __restrict__ keys, u32* __restrict__ vals, in
     if (t < 2) H[n + t] = make_uint2(0u, 0u);
     __syncthreads();
     heap_make(LdsHeap{H}, n);
-    if (t < 64) lds_pops(H, n, npops);
+    if (t < 64) {
+        if (PF_POP_ENGINE == 2) lds_pops2<PF_POP_SHARED != 0, PF_POP_PERM != 0>(H, n, npops);
+        else lds_pops(H, n, npops);
+    }
     __syncthreads();
     if (npops < n - 1) {
         const int r = n - npops, Pr = pow2_ceil(r);

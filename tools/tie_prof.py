@@ -1,5 +1,6 @@
 """Development probe (variant build with -DPF_TIE_PROF, loaded through PFILTER_HIP_LIB): per-level
-phase times of k_tie_local's first job on a synthetic key set.  python3 tools/tie_prof.py [n] [per]"""
+phase times of the partition tiers and k_tie_local's first job on a synthetic key set, or on the keys of a
+real sort call the oracle dumped.  python3 tools/tie_prof.py [n] [per] | [dump file] [call]"""
 import ctypes
 import os
 import sys
@@ -10,10 +11,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "pfilter-noetic_amd"))
 import pfilter_amd as pa  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 11000
-per = int(sys.argv[2]) if len(sys.argv) > 2 else 13
 rng = np.random.default_rng(5)
-if per > 0:
+if len(sys.argv) > 1 and os.path.exists(sys.argv[1]):
+    # keys of a real sort call dumped by the oracle (PFREF_SORT_DUMP / PFREF_SORT_DUMP_MIN: count, keys ...)
+    raw = np.fromfile(sys.argv[1], np.uint32)
+    want = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    i = c = 0
+    while True:
+        cnt = int(raw[i])
+        if c == want:
+            keys = raw[i + 1:i + 1 + cnt].copy()
+            break
+        i += 1 + cnt
+        c += 1
+    n, per = keys.size, 0
+else:
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 11000
+    per = int(sys.argv[2]) if len(sys.argv) > 2 else 13
+if per == 0:
+    pass
+elif per > 0:
     keys = rng.integers(0, max(1, n // per), n).astype(np.uint32)
 else:                             # rgbds-like: a sorted distinct map plus -per appended points on it
     napp = -per
@@ -30,8 +47,8 @@ lev = int(buf[3])
 print("shader clock %.0f MHz" % ((int(buf[5]) - int(buf[4])) / ((int(buf[1]) - t0) / 100.0)))
 print("jobs", int(buf[6]), "mid items", int(buf[7]))
 print("n", n, "levels", lev, "loop %.1f us" % ((int(buf[1]) - t0) / 100.0), "output %.1f us" % ((int(buf[2]) - int(buf[1])) / 100.0))
-def tier(base, name):
-    for k in range(16):
+def tier(base, name, nlev=16):
+    for k in range(nlev):
         b = buf[base + 8 * k: base + 8 * k + 8].astype(np.int64)
         if b[0] == 0:
             break
@@ -43,7 +60,7 @@ def tier(base, name):
               % (name, k, b[7], *ph))
 
 
-tier(256, "medium")
+tier(256, "medium", 32)
 tier(512, "mid")
 for k in range(lev + 1):
     b = buf[8 + 8 * k: 8 + 8 * k + 6].astype(np.int64)
