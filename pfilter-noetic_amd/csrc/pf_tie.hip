@@ -1869,7 +1869,7 @@ __device__ void lds_pops(uint2* H, int n, int npops) {
 }
 
 
-// Round 6 engine (tools/mb/heap_pop.hip v36/v37): the same pipelined pops with (1) every hole's children
+// Round 6 engine (tools/mb/heap_pop.hip v38): the same pipelined pops with (1) every hole's children
 // address carried from step to step (both candidates computed while the loads are in flight, selected by
 // the step's own right / stop masks: the shift-add and the clamp leave the chain between a step's loads and
 // the next step's), (2) the block test on the level of each hole: q's ancestor at the level of a lane's new
@@ -1878,25 +1878,27 @@ __device__ void lds_pops(uint2* H, int n, int npops) {
 // 13 VALU of step B's block test become 5, (3) PF_POP_SHARED: every idle lane parks on one spare slot
 // (their hole writes then hit one address; 64 distinct 8-byte slots put two lanes of a 32-lane store group
 // on every even bank), (4) PF_POP_PERM: consecutive pops dealt to different 16-lane groups of ds_read2_b64
-// (pop i on lane ((i & 3) << 4) | ((i >> 2) & 15))
-__device__ __forceinline__ void lds_pop_step_c(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32& lh, u32 vb8, u32 vnbb,
-                                           u32& vx, u32& vy, int spare, unsigned long long mine, u32 q, u32 rp,
-                                           u32 vqx, u32 vqy) {
+// (pop i on lane ((i & 3) << 4) | ((i >> 2) & 15)); (5) no LDS round trip between a pair's second step and
+// the next pair's first: the root's position (broadcast to every lane) is read by step B beside its own
+// loads, and the last element's entry by step A itself, first, consumed after step A's wait. Measured in
+// the microbenchmark (one wave, s_memtime): 253 (round 5's engine) -> 239 ((1) + (2)) -> 226 cycles per
+// step ((5)); (3) and (4) measured no gain and are off (PF_POP_SHARED / PF_POP_PERM)
+__device__ __forceinline__ void lds_pop_step_e(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32& lh, u32 vb8, u32 vnbb,
+                                           u32& vx, u32& vy, int spare, unsigned long long mine, u32 q, u32 vrp) {
     int hn;
-    u32 tq, sa, rv, zz, t0, t1, t2, t3, t4, aL, aR, aN;
+    u32 tq, sa, zz, t0, t1, t2, t3, t4, aL, aR, aN, aq;
     unsigned long long sm, tt, rm;
     asm volatile(
-        "v_cndmask_b32_e64 %[ad], %[ad], %[vb8], %[mine]\n\t"
-        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
         "v_mov_b32_e32 %[tq], %[q]\n\t"
-        "v_mov_b32_e32 %[rv], %[rp]\n\t"
-        "v_mov_b32_e32 %[zz], 0\n\t"
+        "v_lshl_add_u32 %[aq], %[tq], 3, %[base]\n\t"
+        "ds_read_b64 v[44:45], %[aq]\n\t"
+        "v_cndmask_b32_e64 %[ad], %[ad], %[vb8], %[mine]\n\t"
         "v_cndmask_b32_e64 %[sa], %[sp], %[tq], %[mine]\n\t"
+        "v_mov_b32_e32 %[zz], 0\n\t"
         "v_lshl_add_u32 %[sa], %[sa], 3, %[base]\n\t"
-        "ds_write2_b32 %[sa], %[rv], %[zz] offset1:1\n\t"
+        "ds_write2_b32 %[sa], %[rp], %[zz] offset1:1\n\t"
         "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
-        "v_cndmask_b32_e64 %[vx], %[vx], %[vqx], %[mine]\n\t"
-        "v_cndmask_b32_e64 %[vy], %[vy], %[vqy], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
         "v_cndmask_b32_e64 %[lh], %[lh], 0, %[mine]\n\t"
         "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
         "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
@@ -1907,7 +1909,8 @@ __device__ __forceinline__ void lds_pop_step_c(u32 nbb, u32 base, u32 b24, int& 
         "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
         "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
-        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], v44, %[mine]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], v45, %[mine]\n\t"
         "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
         "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
         "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
@@ -1920,22 +1923,24 @@ __device__ __forceinline__ void lds_pop_step_c(u32 nbb, u32 base, u32 b24, int& 
         "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
         "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
         : [hn] "=&v"(hn), [h] "+v"(h), [ad] "+v"(ad), [lh] "+v"(lh), [vx] "+v"(vx), [vy] "+v"(vy), [tq] "=&v"(tq),
-          [sa] "=&v"(sa), [rv] "=&v"(rv), [zz] "=&v"(zz), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
-          [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR), [aN] "=&v"(aN), [sm] "=&s"(sm),
-          [tt] "=&s"(tt), [rm] "=&s"(rm)
+          [sa] "=&v"(sa), [zz] "=&v"(zz), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR), [aN] "=&v"(aN), [aq] "=&v"(aq),
+          [sm] "=&s"(sm), [tt] "=&s"(tt), [rm] "=&s"(rm)
         : [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24), [nbb] "s"(nbb), [vb8] "v"(vb8), [vnbb] "v"(vnbb),
-          [mine] "s"(mine), [q] "s"(q), [rp] "s"(rp), [vqx] "v"(vqx), [vqy] "v"(vqy)
-        : "memory", "v40", "v41", "v42", "v43");
+          [mine] "s"(mine), [q] "s"(q), [rp] "v"(vrp)
+        : "memory", "v40", "v41", "v42", "v43", "v44", "v45");
     h = hn;
 }
-// lq1 = lev(q) - 1 (scalar); the lane's new hole is at level lh + 1
-__device__ __forceinline__ unsigned long long lds_pop_step_d(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32& lh,
-                                                         u32 vnbb, u32 vx, u32 vy, int spare, u32 q1, u32 lq1) {
+// as step_asm15, and the root's position read (every lane) beside its loads: vrp
+__device__ __forceinline__ unsigned long long lds_pop_step_f(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32& lh,
+                                                         u32 vnbb, u32 vx, u32 vy, int spare, u32 q1, u32 lq1,
+                                                         u32 vbase, u32& vrp) {
     int hn;
     u32 sh, an, t0, t1, t2, t3, t4, aL, aR, aN;
     unsigned long long sm, blk, tt, rm;
     asm volatile(
         "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "ds_read_b32 %[rp], %[vb]\n\t"
         "v_sub_u32_e32 %[sh], %[lq1], %[lh]\n\t"
         "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
         "v_lshrrev_b32_e64 %[an], %[sh], %[q1]\n\t"
@@ -1963,14 +1968,13 @@ __device__ __forceinline__ unsigned long long lds_pop_step_d(u32 nbb, u32 base, 
         "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
         : [hn] "=&v"(hn), [ad] "+v"(ad), [lh] "+v"(lh), [sh] "=&v"(sh), [an] "=&v"(an), [t0] "=&v"(t0),
           [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR),
-          [aN] "=&v"(aN), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm)
+          [aN] "=&v"(aN), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm), [rp] "=&v"(vrp)
         : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24),
-          [nbb] "s"(nbb), [vnbb] "v"(vnbb), [q1] "s"(q1), [lq1] "s"(lq1)
+          [nbb] "s"(nbb), [vnbb] "v"(vnbb), [q1] "s"(q1), [lq1] "s"(lq1), [vb] "v"(vbase)
         : "memory", "v40", "v41", "v42", "v43");
     h = hn;
     return blk;
 }
-
 template <bool SHARED, bool PERM>
 __device__ void lds_pops2(uint2* H, int n, int npops) {
     n = __builtin_amdgcn_readfirstlane(n);
@@ -1981,32 +1985,32 @@ __device__ void lds_pops2(uint2* H, int n, int npops) {
     const u32 base = (u32)(size_t)H;
     const u32 nbb = base + (u32)n * 8u;
     const u32 b24 = base + 24u;                 // children of child c = 2h + 1 + r: base + 8 + 16 c
-    u32 vb8 = base + 8u, vnbb = nbb;            // VGPR copies (a VOP3 select reads one SGPR: the mask)
-    asm volatile("" : "+v"(vb8), "+v"(vnbb));
+    u32 vb8 = base + 8u, vnbb = nbb, vbase = base;   // VGPR copies (a VOP3 select reads one SGPR: the mask)
+    asm volatile("" : "+v"(vb8), "+v"(vnbb), "+v"(vbase));
     int nxt = 0;
     int h = spare;
     u32 ad = nbb, lh = 0u;
     u32 vx = 0u, vy = 1u;                       // an idle lane's value: above the sentinels
     unsigned long long blk = 0;
-    uint2 vq = H[last];
-    u32 rp = H[0].x;
+    u32 vrp = H[0].x;                           // the root's position (every lane)
     for (;;) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const bool start = nxt < npops && blk == 0;          // wave-uniform
             const int ln = PERM ? (((nxt & 3) << 4) | ((nxt >> 2) & 15)) : (nxt & 63);
             const unsigned long long mine = start ? (1ull << ln) : 0ull;
-            lds_pop_step_c(nbb, base, b24, h, ad, lh, vb8, vnbb, vx, vy, spare, mine, (u32)(last - nxt),
-                           __builtin_amdgcn_readfirstlane(rp), vq.x, vq.y);
+            lds_pop_step_e(nbb, base, b24, h, ad, lh, vb8, vnbb, vx, vy, spare, mine, (u32)(last - nxt), vrp);
             nxt += start ? 1 : 0;
             const u32 q1 = (u32)(last - nxt + 1);
-            blk = lds_pop_step_d(nbb, base, b24, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)));
-            vq = H[last - nxt];                                  // the next start's value and root
-            rp = H[0].x;
+            blk = lds_pop_step_f(nbb, base, b24, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)), vbase,
+                                 vrp);
         }
         if (nxt >= npops && __ballot(h != spare) == 0) break;
     }
 }
+#ifndef PF_HEAP_SIDE
+#define PF_HEAP_SIDE 1        // development A/B: 0 = the rest sorted after the pops by the whole workgroup
+#endif
 #ifndef PF_POP_ENGINE
 #define PF_POP_ENGINE 2       // 1: round 5's lds_pops; 2: lds_pops2 (round 6)
 #endif
@@ -2143,31 +2147,88 @@ __device__ void glb_bitonic(const GlbHeap& G, uint2* S, int n) {
 // (A leaner pop engine on 32-bit rank words -- one 8-byte read per step, the ancestor test only on
 // steps that may start a pop -- measured 0.48 us per pop against the pair engine's 0.39: a step is
 // bound by the wave's VALU issue, about 350-460 cycles, not by the LDS round trip)
+// The order-free rest beside the pops (round 6): after npops pops the heap's first r = n - npops entries are
+// exactly the elements with a key below kmin (npops counts the keys >= kmin), in heap order, and any sort
+// of them is exact (they belong to order-free groups). So the set is taken before __make_heap into its own
+// LDS region, and waves 1-15 sort it (the flip-form bitonic network, 960 threads, a barrier of their own
+// on an LDS counter) while wave 0 pops, instead of the whole workgroup sorting the heap's rest after the
+// pops (34.9 us for r = 2600, 85.6 us for r = 7000 on the critical path, tools/mb/heap_pop.hip k_full).
+// Used when the region fits beside the heap and the network's ~1.2 us per stage stays well below the pops.
+constexpr int kSideT = kHeapT - 64;
+// waves 1-15: arrive on the counter and wait for all 15 (the counter only grows: barrier b waits for 15 b)
+__device__ __forceinline__ void side_barrier(u32* ctr, u32& gen) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    ++gen;
+    if (lane_id() == 0) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen * (kSideT / 64))
+            __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ void side_ce_step(uint2* S, int nv, int P, int j, int flipmask, u32* ctr, u32& gen) {
+    for (int c = (int)threadIdx.x - 64; c < (P >> 1); c += kSideT) {
+        const int i = ce_lo(c, j);
+        const int q = flipmask ? (i ^ flipmask) : i + j;
+        if (q < nv) {
+            const uint2 a = S[i], b = S[q];
+            if (b.y < a.y) {
+                S[i] = b;
+                S[q] = a;
+            }
+        }
+    }
+    side_barrier(ctr, gen);
+}
+__device__ __forceinline__ int bitonic_stages(int P) {
+    const int lg = 31 - __clz(P);
+    return lg * (lg + 1) / 2;
+}
+
 // the segment restored in LDS as {position, key + 1} (keys are below 0xFFFFFFFF: dropped keys never reach a
-// segment), two sentinels after it, __make_heap, npops pops (lds_pops), the order-free rest sorted, and the
-// output gathered through the positions
-__device__ void heap_pops_lds(u32* __restrict__ keys, u32* __restrict__ vals, int off, int n, int npops, uint2* H) {
+// segment), two sentinels after it, __make_heap, npops pops (lds_pops), the order-free rest (the keys below
+// kmin) sorted, and the output gathered through the positions
+__device__ void heap_pops_lds(u32* __restrict__ keys, u32* __restrict__ vals, int off, int n, int npops, uint2* H,
+                              u32 kmin) {
+    __shared__ u32 s_rc, s_bar;
     const int t = threadIdx.x;
-    for (int i = t; i < n; i += kHeapT) H[i] = make_uint2((u32)i, keys[off + i] + 1u);
+    const int r = n - npops;
+    const int Pr = pow2_ceil(r > 1 ? r : 1);
+    const bool side = PF_HEAP_SIDE && r >= 2 && n + r + 2 <= kHeapCap && npops >= 6 * bitonic_stages(Pr);
+    uint2* R = H + n + 66;                                       // past the sentinels and the spare slots
+    if (t == 0) {
+        s_rc = 0u;
+        s_bar = 0u;
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += kHeapT) {
+        const u32 k = keys[off + i];
+        H[i] = make_uint2((u32)i, k + 1u);
+        if (side && k < kmin) R[atomicAdd(&s_rc, 1u)] = make_uint2((u32)i, k + 1u);
+    }
     if (t < 2) H[n + t] = make_uint2(0u, 0u);
     __syncthreads();
     heap_make(LdsHeap{H}, n);
     if (t < 64) {
         if (PF_POP_ENGINE == 2) lds_pops2<PF_POP_SHARED != 0, PF_POP_PERM != 0>(H, n, npops);
         else lds_pops(H, n, npops);
+    } else if (side) {
+        u32 gen = 0;
+        for (int k = 2; k <= Pr; k <<= 1) {
+            side_ce_step(R, r, Pr, k >> 1, k - 1, &s_bar, gen);
+            for (int j = k >> 2; j >= 1; j >>= 1) side_ce_step(R, r, Pr, j, 0, &s_bar, gen);
+        }
     }
     __syncthreads();
-    if (npops < n - 1) {
-        const int r = n - npops, Pr = pow2_ceil(r);
-        lds_bitonic(H, r, Pr, 2, Pr, 0);                    // the rest: order-free groups only
-    }
+    if (!side && npops < n - 1) lds_bitonic(H, r, Pr, 2, Pr, 0);   // the rest: order-free groups only
     constexpr int kPer = (kHeapCapP + kHeapT - 1) / kHeapT;
     u32 gk[kPer], gv[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
         const int i = t + j * kHeapT;
         if (i < n) {
-            const u32 p = H[i].x;
+            const u32 p = side && i < r ? R[i].x : H[i].x;
             gk[j] = keys[off + p];
             gv[j] = vals[off + p];
         }
@@ -2211,7 +2272,7 @@ __device__ void heap_segment_pairs(u32* __restrict__ keys, u32* __restrict__ val
             if (lane_id() == 0) atomicAdd(&s_pops2, c);
             __syncthreads();
             const int popsneed = (int)s_pops2;
-            heap_pops_lds(keys, vals, off, n, popsneed >= n ? n - 1 : popsneed, H);
+            heap_pops_lds(keys, vals, off, n, popsneed >= n ? n - 1 : popsneed, H, km);
             return;
         }
         s_kmin2 = 0xFFFFFFFFu;                          // no order-dependent element: sorted below
@@ -2239,7 +2300,7 @@ __device__ void heap_segment_pairs(u32* __restrict__ keys, u32* __restrict__ val
         const int npops = popsneed >= n ? n - 1 : popsneed;
         if (n <= kHeapCapP) {
             __syncthreads();
-            heap_pops_lds(keys, vals, off, n, npops, H);
+            heap_pops_lds(keys, vals, off, n, npops, H, kmin);
             return;
         }
         for (int i = t; i < n; i += kHeapT) H[i] = make_uint2(vals[off + i], keys[off + i]);   // restore
