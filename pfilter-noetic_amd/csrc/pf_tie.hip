@@ -1882,20 +1882,19 @@ __device__ void lds_pops(uint2* H, int n, int npops) {
 // the next pair's first: the root's position (broadcast to every lane) is read by step B beside its own
 // loads, and the last element's entry by step A itself, first, consumed after step A's wait. Measured in
 // the microbenchmark (one wave, s_memtime): 253 (round 5's engine) -> 239 ((1) + (2)) -> 226 cycles per
-// step ((5)); (3) and (4) measured no gain and are off (PF_POP_SHARED / PF_POP_PERM)
-__device__ __forceinline__ void lds_pop_step_e(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32& lh, u32 vb8, u32 vnbb,
-                                           u32& vx, u32& vy, int spare, unsigned long long mine, u32 q, u32 vrp) {
+// step ((5)) -> 219.5 ((6): the block mask taken from the unselected hole, (ancestor == 2h + 1 + right),
+// and the stop mask by one SALU and-not, so the next start's decision no longer waits for the hole's
+// select; tools/mb/heap_pop.hip v40); (3) and (4) measured no gain and are off (PF_POP_SHARED / _PERM)
+__device__ __forceinline__ void lds_pop_step_e(u32 base, u32 b24, u32 nbb, int& h, u32& ad, u32& lh, u32 vb8, u32 vnbb,
+                                           u32& vx, u32& vy, int spare, u32 vsp8, u32 vzero,
+                                           unsigned long long mine, u32 aq, u32 vrp) {
     int hn;
-    u32 tq, sa, zz, t0, t1, t2, t3, t4, aL, aR, aN, aq;
+    u32 sa, t0, t1, t2, t3, t4, aL, aR, aN;
     unsigned long long sm, tt, rm;
     asm volatile(
-        "v_mov_b32_e32 %[tq], %[q]\n\t"
-        "v_lshl_add_u32 %[aq], %[tq], 3, %[base]\n\t"
         "ds_read_b64 v[44:45], %[aq]\n\t"
+        "v_cndmask_b32_e64 %[sa], %[sp8], %[aq], %[mine]\n\t"
         "v_cndmask_b32_e64 %[ad], %[ad], %[vb8], %[mine]\n\t"
-        "v_cndmask_b32_e64 %[sa], %[sp], %[tq], %[mine]\n\t"
-        "v_mov_b32_e32 %[zz], 0\n\t"
-        "v_lshl_add_u32 %[sa], %[sa], 3, %[base]\n\t"
         "ds_write2_b32 %[sa], %[rp], %[zz] offset1:1\n\t"
         "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
         "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
@@ -1917,27 +1916,26 @@ __device__ __forceinline__ void lds_pop_step_e(u32 nbb, u32 base, u32 b24, int& 
         "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
         "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
         "s_nop 0\n\t"
-        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
         "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
         "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
-        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
         "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
-        : [hn] "=&v"(hn), [h] "+v"(h), [ad] "+v"(ad), [lh] "+v"(lh), [vx] "+v"(vx), [vy] "+v"(vy), [tq] "=&v"(tq),
-          [sa] "=&v"(sa), [zz] "=&v"(zz), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
-          [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR), [aN] "=&v"(aN), [aq] "=&v"(aq),
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        : [hn] "=&v"(hn), [h] "+v"(h), [ad] "+v"(ad), [lh] "+v"(lh), [vx] "+v"(vx), [vy] "+v"(vy),
+          [sa] "=&v"(sa), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR), [aN] "=&v"(aN),
           [sm] "=&s"(sm), [tt] "=&s"(tt), [rm] "=&s"(rm)
-        : [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24), [nbb] "s"(nbb), [vb8] "v"(vb8), [vnbb] "v"(vnbb),
-          [mine] "s"(mine), [q] "s"(q), [rp] "v"(vrp)
+        : [sp] "v"(spare), [sp8] "v"(vsp8), [zz] "v"(vzero), [base] "s"(base), [b24] "s"(b24), [nbb] "s"(nbb),
+          [vb8] "v"(vb8), [vnbb] "v"(vnbb), [mine] "s"(mine), [aq] "v"(aq), [rp] "v"(vrp)
         : "memory", "v40", "v41", "v42", "v43", "v44", "v45");
     h = hn;
 }
-// as step_asm15, and the root's position read (every lane) beside its loads: vrp
-__device__ __forceinline__ unsigned long long lds_pop_step_f(u32 nbb, u32 base, u32 b24, int& h, u32& ad, u32& lh,
+__device__ __forceinline__ unsigned long long lds_pop_step_f(u32 base, u32 b24, u32 nbb, int& h, u32& ad, u32& lh,
                                                          u32 vnbb, u32 vx, u32 vy, int spare, u32 q1, u32 lq1,
-                                                         u32 vbase, u32& vrp) {
+                                                         u32 vbase, u32& vrp, u32 aqs, u32& aq) {
     int hn;
     u32 sh, an, t0, t1, t2, t3, t4, aL, aR, aN;
-    unsigned long long sm, blk, tt, rm;
+    unsigned long long sm, blk, tt, rm, bm;
     asm volatile(
         "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
         "ds_read_b32 %[rp], %[vb]\n\t"
@@ -1951,6 +1949,7 @@ __device__ __forceinline__ unsigned long long lds_pop_step_f(u32 nbb, u32 base, 
         "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
         "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
         "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+        "v_mov_b32_e32 %[aq], %[aqs]\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
         "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
         "s_nop 1\n\t"
@@ -1960,17 +1959,19 @@ __device__ __forceinline__ unsigned long long lds_pop_step_f(u32 nbb, u32 base, 
         "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
         "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
         "s_nop 0\n\t"
-        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
-        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
         "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
         "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
-        "v_cmp_eq_u32_e64 %[blk], %[an], %[hn]\n\t"
+        "v_cmp_eq_u32_e64 %[bm], %[an], %[t3]\n\t"
         "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "s_andn2_b64 %[blk], %[bm], %[sm]\n\t"
         : [hn] "=&v"(hn), [ad] "+v"(ad), [lh] "+v"(lh), [sh] "=&v"(sh), [an] "=&v"(an), [t0] "=&v"(t0),
           [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR),
-          [aN] "=&v"(aN), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm), [rp] "=&v"(vrp)
+          [aN] "=&v"(aN), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm), [bm] "=&s"(bm),
+          [rp] "=&v"(vrp), [aq] "=&v"(aq)
         : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24),
-          [nbb] "s"(nbb), [vnbb] "v"(vnbb), [q1] "s"(q1), [lq1] "s"(lq1), [vb] "v"(vbase)
+          [nbb] "s"(nbb), [vnbb] "v"(vnbb), [q1] "s"(q1), [lq1] "s"(lq1), [vb] "v"(vbase), [aqs] "s"(aqs)
         : "memory", "v40", "v41", "v42", "v43");
     h = hn;
     return blk;
@@ -1985,25 +1986,27 @@ __device__ void lds_pops2(uint2* H, int n, int npops) {
     const u32 base = (u32)(size_t)H;
     const u32 nbb = base + (u32)n * 8u;
     const u32 b24 = base + 24u;                 // children of child c = 2h + 1 + r: base + 8 + 16 c
-    u32 vb8 = base + 8u, vnbb = nbb, vbase = base;   // VGPR copies (a VOP3 select reads one SGPR: the mask)
-    asm volatile("" : "+v"(vb8), "+v"(vnbb), "+v"(vbase));
+    // VGPR copies of loop constants (a VOP3 select reads one SGPR: the mask)
+    u32 vb8 = base + 8u, vnbb = nbb, vbase = base, vsp8 = base + 8u * (u32)spare, vzero = 0u;
+    asm volatile("" : "+v"(vb8), "+v"(vnbb), "+v"(vbase), "+v"(vsp8), "+v"(vzero));
     int nxt = 0;
     int h = spare;
     u32 ad = nbb, lh = 0u;
     u32 vx = 0u, vy = 1u;                       // an idle lane's value: above the sentinels
     unsigned long long blk = 0;
     u32 vrp = H[0].x;                           // the root's position (every lane)
+    u32 aq = base + 8u * (u32)last;             // the address of the next start's q
     for (;;) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const bool start = nxt < npops && blk == 0;          // wave-uniform
             const int ln = PERM ? (((nxt & 3) << 4) | ((nxt >> 2) & 15)) : (nxt & 63);
             const unsigned long long mine = start ? (1ull << ln) : 0ull;
-            lds_pop_step_e(nbb, base, b24, h, ad, lh, vb8, vnbb, vx, vy, spare, mine, (u32)(last - nxt), vrp);
+            lds_pop_step_e(base, b24, nbb, h, ad, lh, vb8, vnbb, vx, vy, spare, vsp8, vzero, mine, aq, vrp);
             nxt += start ? 1 : 0;
             const u32 q1 = (u32)(last - nxt + 1);
-            blk = lds_pop_step_f(nbb, base, b24, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)), vbase,
-                                 vrp);
+            blk = lds_pop_step_f(base, b24, nbb, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)), vbase,
+                                 vrp, base + 8u * (u32)(last - nxt), aq);
         }
         if (nxt >= npops && __ballot(h != spare) == 0) break;
     }

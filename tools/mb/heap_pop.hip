@@ -1746,6 +1746,180 @@ __device__ int pops_v38(uint2* H, int n, int npops) {
     }
     return steps;
 }
+
+// v39 (round 6): v38 with the pair boundary shortened: step B computes the next start's write / read address
+// of q (aq, from the scalar q) while its loads are in flight, and issues its hole write before the selects
+// of its next address and hole; step A then needs only the start's two selects (the write address and the
+// children address) before its write of the root's name and its children read. v40: v39 with the block
+// mask formed before the hole select: (ancestor == 2h + 1 + right) and not stopped (SALU and-not)
+__device__ __forceinline__ void step_asm18(u32 base, u32 b24, u32 nbb, int& h, u32& ad, u32& lh, u32 vb8, u32 vnbb,
+                                           u32& vx, u32& vy, int spare, u32 vsp8, u32 vzero,
+                                           unsigned long long mine, u32 aq, u32 vrp) {
+    int hn;
+    u32 sa, t0, t1, t2, t3, t4, aL, aR, aN;
+    unsigned long long sm, tt, rm;
+    asm volatile(
+        "ds_read_b64 v[44:45], %[aq]\n\t"
+        "v_cndmask_b32_e64 %[sa], %[sp8], %[aq], %[mine]\n\t"
+        "v_cndmask_b32_e64 %[ad], %[ad], %[vb8], %[mine]\n\t"
+        "ds_write2_b32 %[sa], %[rp], %[zz] offset1:1\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
+        "v_cndmask_b32_e64 %[lh], %[lh], 0, %[mine]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+        "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+        "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+        "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+        "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], v44, %[mine]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], v45, %[mine]\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        : [hn] "=&v"(hn), [h] "+v"(h), [ad] "+v"(ad), [lh] "+v"(lh), [vx] "+v"(vx), [vy] "+v"(vy),
+          [sa] "=&v"(sa), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR), [aN] "=&v"(aN),
+          [sm] "=&s"(sm), [tt] "=&s"(tt), [rm] "=&s"(rm)
+        : [sp] "v"(spare), [sp8] "v"(vsp8), [zz] "v"(vzero), [base] "s"(base), [b24] "s"(b24), [nbb] "s"(nbb),
+          [vb8] "v"(vb8), [vnbb] "v"(vnbb), [mine] "s"(mine), [aq] "v"(aq), [rp] "v"(vrp)
+        : "memory", "v40", "v41", "v42", "v43", "v44", "v45");
+    h = hn;
+}
+template <bool SALU_BLK>
+__device__ __forceinline__ unsigned long long step_asm19(u32 base, u32 b24, u32 nbb, int& h, u32& ad, u32& lh,
+                                                         u32 vnbb, u32 vx, u32 vy, int spare, u32 q1, u32 lq1,
+                                                         u32 vbase, u32& vrp, u32 aqs, u32& aq) {
+    int hn;
+    u32 sh, an, t0, t1, t2, t3, t4, aL, aR, aN;
+    unsigned long long sm, blk, tt, rm, bm;
+    if (SALU_BLK)
+        asm volatile(
+            "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+            "ds_read_b32 %[rp], %[vb]\n\t"
+            "v_sub_u32_e32 %[sh], %[lq1], %[lh]\n\t"
+            "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+            "v_lshrrev_b32_e64 %[an], %[sh], %[q1]\n\t"
+            "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+            "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+            "v_add_u32_e32 %[an], -1, %[an]\n\t"
+            "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+            "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+            "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+            "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+            "v_mov_b32_e32 %[aq], %[aqs]\n\t"
+            "s_waitcnt lgkmcnt(0)\n\t"
+            "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+            "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+            "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+            "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+            "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+            "s_nop 0\n\t"
+            "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+            "v_cmp_eq_u32_e64 %[bm], %[an], %[t3]\n\t"
+            "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+            "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+            "s_andn2_b64 %[blk], %[bm], %[sm]\n\t"
+            : [hn] "=&v"(hn), [ad] "+v"(ad), [lh] "+v"(lh), [sh] "=&v"(sh), [an] "=&v"(an), [t0] "=&v"(t0),
+              [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR),
+              [aN] "=&v"(aN), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm), [bm] "=&s"(bm),
+              [rp] "=&v"(vrp), [aq] "=&v"(aq)
+            : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24),
+              [nbb] "s"(nbb), [vnbb] "v"(vnbb), [q1] "s"(q1), [lq1] "s"(lq1), [vb] "v"(vbase), [aqs] "s"(aqs)
+            : "memory", "v40", "v41", "v42", "v43");
+    else
+        asm volatile(
+            "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+            "ds_read_b32 %[rp], %[vb]\n\t"
+            "v_sub_u32_e32 %[sh], %[lq1], %[lh]\n\t"
+            "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+            "v_lshrrev_b32_e64 %[an], %[sh], %[q1]\n\t"
+            "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+            "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+            "v_add_u32_e32 %[an], -1, %[an]\n\t"
+            "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+            "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+            "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+            "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+            "v_mov_b32_e32 %[aq], %[aqs]\n\t"
+            "s_waitcnt lgkmcnt(0)\n\t"
+            "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+            "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+            "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+            "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+            "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+            "s_nop 0\n\t"
+            "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+            "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+            "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+            "v_cmp_eq_u32_e64 %[blk], %[an], %[hn]\n\t"
+            : [hn] "=&v"(hn), [ad] "+v"(ad), [lh] "+v"(lh), [sh] "=&v"(sh), [an] "=&v"(an), [t0] "=&v"(t0),
+              [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR),
+              [aN] "=&v"(aN), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm),
+              [rp] "=&v"(vrp), [aq] "=&v"(aq)
+            : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24),
+              [nbb] "s"(nbb), [vnbb] "v"(vnbb), [q1] "s"(q1), [lq1] "s"(lq1), [vb] "v"(vbase), [aqs] "s"(aqs)
+            : "memory", "v40", "v41", "v42", "v43");
+    (void)bm;
+    h = hn;
+    return blk;
+}
+template <int U, bool SALU_BLK>
+__device__ int pops_v39(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    const u32 b24 = base + 24u;
+    u32 vb8 = base + 8u, vnbb = nbb, vbase = base, vsp8 = base + 8u * (u32)spare, vzero = 0u;
+    asm volatile("" : "+v"(vb8), "+v"(vnbb), "+v"(vbase), "+v"(vsp8), "+v"(vzero));
+    int nxt = 0;
+    int h = spare;
+    u32 ad = nbb, lh = 0u;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0;
+    u32 vrp = H[0].x;
+    u32 aq = base + 8u * (u32)last;
+    int steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool start = nxt < npops && blk == 0;
+            const unsigned long long mine = start ? (1ull << (nxt & 63)) : 0ull;
+            step_asm18(base, b24, nbb, h, ad, lh, vb8, vnbb, vx, vy, spare, vsp8, vzero, mine, aq, vrp);
+            nxt += start ? 1 : 0;
+            const u32 q1 = (u32)(last - nxt + 1);
+            blk = step_asm19<SALU_BLK>(base, b24, nbb, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)), vbase,
+                                       vrp, base + 8u * (u32)(last - nxt), aq);
+        }
+        steps += 2 * U;
+        if (nxt >= npops && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
 template <int U>
 __device__ int pops_v28(uint2* H, int n, int npops) {
     n = __builtin_amdgcn_readfirstlane(n);
@@ -1955,7 +2129,7 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
     if (t < 64 && n >= 2 && npops > 0) {
         const u64 r0 = __builtin_amdgcn_s_memrealtime();
         const u64 t0 = __builtin_amdgcn_s_memtime();
-        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : V == 23 ? (u64)pops_v28<4>(H, n, npops) : V == 24 ? (u64)pops_v29<4>(H, n, npops) : V == 25 ? (u64)pops_v30<4, true, false>(H, n, npops) : V == 26 ? (u64)pops_v30<4, false, true>(H, n, npops) : V == 27 ? (u64)pops_v30<4, true, true>(H, n, npops) : V == 28 ? (u64)pops_v33<4, false, false>(H, n, npops) : V == 29 ? (u64)pops_v33<4, true, true>(H, n, npops) : V == 30 ? (u64)pops_v36<4, false, false>(H, n, npops) : V == 31 ? (u64)pops_v36<4, true, true>(H, n, npops) : (u64)pops_v38<4>(H, n, npops);
+        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : V == 23 ? (u64)pops_v28<4>(H, n, npops) : V == 24 ? (u64)pops_v29<4>(H, n, npops) : V == 25 ? (u64)pops_v30<4, true, false>(H, n, npops) : V == 26 ? (u64)pops_v30<4, false, true>(H, n, npops) : V == 27 ? (u64)pops_v30<4, true, true>(H, n, npops) : V == 28 ? (u64)pops_v33<4, false, false>(H, n, npops) : V == 29 ? (u64)pops_v33<4, true, true>(H, n, npops) : V == 30 ? (u64)pops_v36<4, false, false>(H, n, npops) : V == 31 ? (u64)pops_v36<4, true, true>(H, n, npops) : V == 32 ? (u64)pops_v38<4>(H, n, npops) : V == 33 ? (u64)pops_v39<4, false>(H, n, npops) : (u64)pops_v39<4, true>(H, n, npops);
         const u64 t1 = __builtin_amdgcn_s_memtime();
         const u64 r1 = __builtin_amdgcn_s_memrealtime();
         if (t == 0) {
@@ -2117,8 +2291,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d_np, np.data(), nb * 4, hipMemcpyHostToDevice));
     std::vector<u64> out(in.size()), tt(3 * nb);
     const int vlo = argc > 2 ? std::atoi(argv[2]) : 22;
-    for (int v = vlo; v <= 32; ++v) {
-        if (v >= 2 && v <= 21 || (v >= 23 && v <= 29) || v == 31) continue;
+    for (int v = vlo; v <= 34; ++v) {
+        if (v >= 2 && v <= 21 || (v >= 23 && v <= 31)) continue;
         for (int r = 0; r < reps; ++r) {
             CK(hipMemcpy(d_kv, in.data(), in.size() * 8, hipMemcpyHostToDevice));
             if (v == 1) hipLaunchKernelGGL(k_heap<1>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
@@ -2152,7 +2326,9 @@ int main(int argc, char** argv) {
             else if (v == 29) hipLaunchKernelGGL(k_heap<29>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 30) hipLaunchKernelGGL(k_heap<30>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 31) hipLaunchKernelGGL(k_heap<31>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
-            else hipLaunchKernelGGL(k_heap<32>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 32) hipLaunchKernelGGL(k_heap<32>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 33) hipLaunchKernelGGL(k_heap<33>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else hipLaunchKernelGGL(k_heap<34>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             CK(hipDeviceSynchronize());
         }
         CK(hipMemcpy(out.data(), d_kv, out.size() * 8, hipMemcpyDeviceToHost));
