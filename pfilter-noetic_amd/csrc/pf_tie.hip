@@ -34,11 +34,29 @@ enum {
     T_NHEAPF = 24,      // huge segments the heap tier still sorts (TieSort::heapf)
     T_HUGEN = 25,       // pairs of the huge segments
     T_NHEAPW = 26,      // depth-limit segments the partition tiers filed for the aux heap launch (TieAux)
+    T_CLM_MED = 27,     // items claimed past the first gridDim.x (next_item) by k_tie_medium's segment list,
+    T_CLM_MID = 28,     // k_tie_mid, k_tie_local (these three reset by k_tie_local's last workgroup),
+    T_CLM_LOCAL = 29,
+    T_CLM_HEAP = 30,    // the stream's k_tie_heap launches and the aux one (reset by their last workgroup)
+    T_CLM_HEAPW = 31,
     T_WORDS = 32
 };
 __device__ __forceinline__ u64* big_ctr(int* ctl, int p) { return reinterpret_cast<u64*>(ctl + T_BIG) + p; }
 
 __device__ __forceinline__ int lg_floor(int n) { return 31 - __clz(n); }
+
+// The item after `cur` of a launch over n list items: workgroup b takes item b first, then claims the next
+// unclaimed one (a counter from gridDim.x) when it is done, so a long item never holds back items dealt
+// behind it (configs[4]'s lists hold thousands of segments, a few of them hundreds of times longer than
+// the rest). No claim when the first round covers the list. Every thread of the workgroup calls it.
+__device__ __forceinline__ int next_item(int n, int* ctr) {
+    if (n <= (int)gridDim.x) return n;
+    __shared__ int s_next;
+    __syncthreads();
+    if (threadIdx.x == 0) s_next = (int)gridDim.x + atomicAdd(ctr, 1);
+    __syncthreads();
+    return s_next;
+}
 
 // the class boundaries of the input: start[c], start[nc] = n
 __device__ __forceinline__ int class_starts(const TieClasses& cls, int (&start)[kMaxTieC + 1]) {
@@ -161,8 +179,16 @@ struct HeapList {
     int* err;
     int2* huge;
     int hugecap;
-    // a segment without an order-dependent group (any size): straight to the radix sort
+    // a segment without an order-dependent group: above the LDS size to the radix sort, else to k_tie_heap,
+    // whose idle workgroups sort it in LDS beside the few segments that need pops (configs[4]: ~1200 such
+    // segments per sort, half of the radix sort's keys, sorted off its critical path)
     __device__ __forceinline__ void file_free(int* ctl, long long off, int len) const {
+        if (len <= kHeapCap) {
+            const int j = atomicAdd(&ctl[T_NHEAP], 1);
+            if (j < cap) seg[j] = make_int2((int)off, len);
+            else atomicOr(err, 4);
+            return;
+        }
         const int j = atomicAdd(&ctl[T_NHUGE], 1);
         if (j < hugecap) huge[j] = make_int2((int)off, len);
         else atomicOr(err, 4);
@@ -977,7 +1003,7 @@ __global__ void __launch_bounds__(1024) k_tie_medium(const u32* __restrict__ key
     const int t = threadIdx.x, w = t >> 6, l = lane_id();
     const u64 lt = lanemask_lt();
     const int nitems = from_classes ? cls.nc : ctl[T_NMED];
-    for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    for (int it = blockIdx.x; it < nitems; it = next_item(nitems, &ctl[T_CLM_MED])) {
         int f0, e0, d0, cl;
         if (from_classes) {
             int start[kMaxTieC + 1];
@@ -1078,7 +1104,7 @@ __global__ void __launch_bounds__(1024) k_tie_mid(u32* k, u32* v, int* ctl, cons
     __shared__ MidLds S;
     const int t = threadIdx.x;
     const int nm = ctl[T_NMID];
-    for (int it = blockIdx.x; it < nm; it += gridDim.x) {
+    for (int it = blockIdx.x; it < nm; it = next_item(nm, &ctl[T_CLM_MID])) {
         const int4 mi = mid[it];
         const int f = mi.x, len = mi.y - mi.x;
         if (freef && !range_dep(v, freef, f, f + len)) {         // no order-dependent group: as it stands
@@ -1325,7 +1351,7 @@ __global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, c
         }
         if (t == 0) ctl[T_VALID] = tot;
     }
-    for (int jb = blockIdx.x; jb < nj; jb += gridDim.x) {
+    for (int jb = blockIdx.x; jb < nj; jb = next_item(nj, &ctl[T_CLM_LOCAL])) {
         const int4 job = jobs[jb];
         const int f = job.x, len = job.y - job.x, d = job.z;
         long long ob = 0;
@@ -1568,6 +1594,7 @@ __global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, c
         if (a == gridDim.x - 1) {
             __hip_atomic_store(&ctl[T_NJOBS], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&ctl[T_NMID], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int c = T_CLM_MED; c <= T_CLM_LOCAL; ++c) __hip_atomic_store(&ctl[c], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -2336,7 +2363,8 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
     __shared__ uint2 H[kHeapCap + 64];             // + a spare slot per lane of wave 0
     const int t = threadIdx.x;
     const int nh = ctl[which];
-    for (int jb = blockIdx.x; jb < nh; jb += gridDim.x) {
+    const int clm = which == T_NHEAPW ? T_CLM_HEAPW : T_CLM_HEAP;
+    for (int jb = blockIdx.x; jb < nh; jb = next_item(nh, &ctl[clm])) {
         int2 sg;
         if (wsegs) {
             const int4 w4 = wsegs[jb];
@@ -2352,7 +2380,7 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
             sg = segs[jb];
         }
         const int off = sg.x, n = sg.y;
-        if (route && freef) {               // no order-dependent element: the radix sort after this launch
+        if (route && freef && n > kHeapCap) {   // no order-dependent element: the radix sort after this launch
             int dep = 0;
             for (int i = t; i < n; i += kHeapT) dep |= freef[vals[off + i]] ? 0 : 1;
             if (__syncthreads_or(dep) == 0) {
@@ -2403,6 +2431,7 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
         if (a == gridDim.x - 1) {
             __hip_atomic_store(&ctl[which], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (also >= 0) __hip_atomic_store(&ctl[also], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl[clm], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }

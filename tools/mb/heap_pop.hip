@@ -2263,12 +2263,34 @@ int main(int argc, char** argv) {
                                {"desc", 7000, 3, -1},  {"map", 12000, 4, -1},  {"ties-part", 9000, 0, 3000},
                                {"small", 2, 0, -1},    {"small", 3, 0, -1},    {"small", 17, 0, -1},
                                {"small", 100, 0, -1},  {"map", 18000, 4, 11000}};
+    // HEAP_DUMP=<file> (oracle PFREF_HEAP_DUMP: int32 len, int32 pops, len keys per segment): real depth-limit
+    // segments as extra cases, partial pops as the library runs them (HEAP_DUMP_MAX of them, default 24)
+    std::vector<std::vector<u64>> dumped;
+    if (const char* dp = std::getenv("HEAP_DUMP")) {
+        FILE* f = std::fopen(dp, "rb");
+        const int dmax = std::getenv("HEAP_DUMP_MAX") ? std::atoi(std::getenv("HEAP_DUMP_MAX")) : 24;
+        int hdr[2], skip = std::getenv("HEAP_DUMP_SKIP") ? std::atoi(std::getenv("HEAP_DUMP_SKIP")) : 0;
+        while (f && (int)dumped.size() < dmax && std::fread(hdr, sizeof(hdr), 1, f) == 1) {
+            std::vector<u32> k(hdr[0]);
+            if (std::fread(k.data(), 4, hdr[0], f) != (size_t)hdr[0]) break;
+            if (hdr[0] > kCap - 2 || skip-- > 0) continue;
+            std::vector<u64> a(hdr[0]);
+            for (int i = 0; i < hdr[0]; ++i) a[i] = ((u64)k[i] << 32) | (u32)i;
+            int asc = 0;
+            for (int i = 1; i < hdr[0]; ++i) asc += k[i] >= k[i - 1];
+            std::printf("dump %d: n %d pops %d, ascending neighbours %.3f\n", (int)dumped.size(), hdr[0], hdr[1],
+                        (double)asc / std::max(1, hdr[0] - 1));
+            dumped.push_back(a);
+            cases.push_back({"dump", hdr[0], 100 + (int)dumped.size() - 1, std::min(hdr[1], hdr[0] - 1)});
+        }
+        if (f) std::fclose(f);
+    }
     const int nb = (int)cases.size();
     std::vector<u64> in((size_t)nb * kCap), ref((size_t)nb * kCap);
     std::vector<int> segn(nb), np(nb);
     for (int b = 0; b < nb; ++b) {
         const Case& c = cases[b];
-        std::vector<u64> a = make_input(c.n, c.kind, rng);
+        std::vector<u64> a = c.kind >= 100 ? dumped[c.kind - 100] : make_input(c.n, c.kind, rng);
         std::copy(a.begin(), a.end(), in.begin() + (size_t)b * kCap);
         auto cmp = [](u64 x, u64 y) { return (x >> 32) < (y >> 32); };
         std::make_heap(a.begin(), a.end(), cmp);
