@@ -1523,8 +1523,21 @@ extern "C" int pf_dev_tie_sort2(int device, const uint32_t* keys, size_t n, int 
                 hipMemcpyAsync(dv, iota.data(), sizeof(u32) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
                 hipMemcpyAsync(dsz, hsz, sizeof(hsz), hipMemcpyHostToDevice, s) != hipSuccess))
         rc = PF_EHIP;
+    // the radix route beside the tiers (TieAux::hs) as stage B runs it; PF_TIE_HS=0: on s (both tested)
+    hipStream_t hs = nullptr;
+    hipEvent_t evf = nullptr, evj = nullptr;
+    const char* hse = std::getenv("PF_TIE_HS");
+    if (!rc && levels > 0 && !(hse && std::atoi(hse) == 0) &&
+        (hipStreamCreateWithFlags(&hs, hipStreamNonBlocking) != hipSuccess ||
+         hipEventCreateWithFlags(&evf, hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&evj, hipEventDisableTiming) != hipSuccess))
+        rc = PF_EHIP;
     if (!rc) {
-        tie_sort(t, dk, dv, TieClasses{dsz, 0, -1, 4}, dsz + 4, s, levels);
+        TieAux aux;
+        aux.fork = evf;
+        aux.join = evj;
+        aux.hs = hs;
+        tie_sort(t, dk, dv, TieClasses{dsz, 0, -1, 4}, dsz + 4, s, levels, nullptr, hs ? &aux : nullptr);
         int nv = 0, err = 0;
         if (hipMemcpyAsync(&nv, tie_valid_count(t), sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipMemcpyAsync(&err, dsz + 4, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1541,6 +1554,10 @@ extern "C" int pf_dev_tie_sort2(int device, const uint32_t* keys, size_t n, int 
     (void)hipFree(dv);
     (void)hipFree(dsz);
     if (s) (void)hipStreamDestroy(s);
+    if (hs) (void)hipStreamSynchronize(hs);
+    if (hs) (void)hipStreamDestroy(hs);
+    if (evf) (void)hipEventDestroy(evf);
+    if (evj) (void)hipEventDestroy(evj);
     tie_free(t);
     return rc;
 }

@@ -152,6 +152,9 @@ struct OdomGPU {
     hipStream_t stream_bx = nullptr;
     hipEvent_t ev_bx_fork = nullptr, ev_bx_join = nullptr;
     bool tie_aux = false;
+    // the radix route of a sort with big levels (configs[4]'s ~820k-key depth-limit segment) on stream_bx
+    // beside the partition tiers (TieAux::hs); PF_TIE_HS=0 keeps it on stage B's stream (A/B checks)
+    bool tie_hs = true;
     size_t in_cap = 0, map_cap = 0, sort_cap = 0, pose_cap = 0;
     int opt_count_host = 2;
     bool inited = false;

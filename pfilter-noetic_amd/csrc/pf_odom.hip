@@ -3084,6 +3084,7 @@ int odom_create(OdomGPU& o, const pf_lidar_params& lidar, const pf_odom_params& 
         hipEventCreateWithFlags(&o.ev_bx_join, hipEventDisableTiming) != hipSuccess)
         return PF_EHIP;
     if (const char* e = std::getenv("PF_TIE_AUX")) o.tie_aux = std::atoi(e) != 0;   // development A/B
+    if (const char* e = std::getenv("PF_TIE_HS")) o.tie_hs = std::atoi(e) != 0;
     trace_create("stream");
     // stage A is kept off the last compute units by default (odom_stage_a_stream), so that stage B's
     // kernels — the LM needs kLmBlocks co-resident workgroups — find free CUs while stage A runs
@@ -3514,6 +3515,7 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
         aux.s = o.tie_aux ? o.stream_bx : nullptr;
         aux.fork = o.ev_bx_fork;
         aux.join = o.ev_bx_join;
+        aux.hs = o.tie_hs ? o.stream_bx : nullptr;
         tie_sort(*o.tie_b, o.keys, o.vals, TieClasses{cnt, C_M, C_DS, nc}, o.prim.err, s,
                  std::max(tie_levels_for(*o.tie_b, o.tie_hint), PF_TIE_LEVELS_B), dt.key ? o.dep_free : nullptr,
                  &aux);

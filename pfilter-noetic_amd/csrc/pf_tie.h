@@ -116,9 +116,14 @@ int tie_levels_for(const TieSort& t, size_t size_hint);
 // starts when k_tie_mid ends and runs beside k_tie_local (and the heap launch of the local tier's own
 // depth-limit segments); s waits for it before the sort returns. Without aux every depth-limit segment
 // goes through k_tie_local to the one heap launch after it.
+// hs (optional, sorts with big levels and the radix route): the depth-limit and dependence-free segments
+// above the LDS size that the big levels and k_tie_medium leave are filed by k_tie_medium straight from the
+// working copy, and their radix sort (and the heap launch for those of them that need pops) runs on hs
+// beside k_tie_mid / k_tie_local / k_tie_heap, joined before the sort returns (fork / join as above).
 struct TieAux {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t hs = nullptr;
 };
 void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStream_t s, int levels = 0,
               const u8* freef = nullptr, const TieAux* aux = nullptr);

@@ -39,7 +39,8 @@ enum {
     T_CLM_LOCAL = 29,
     T_CLM_HEAP = 30,    // the stream's k_tie_heap launches and the aux one (reset by their last workgroup)
     T_CLM_HEAPW = 31,
-    T_WORDS = 32
+    T_CLM_HEAPF = 32,   // the heap launch of the radix route's segments that need pops (TieAux::hs: beside T_NHEAP's)
+    T_WORDS = 40
 };
 __device__ __forceinline__ u64* big_ctr(int* ctl, int p) { return reinterpret_cast<u64*>(ctl + T_BIG) + p; }
 
@@ -177,13 +178,14 @@ struct HeapList {
     int2* seg;
     int cap;
     int* err;
-    int2* huge;
+    int2* huge;            // the radix route's list (null: segments above the LDS size go to the heap list)
     int hugecap;
+    bool route;            // dependence-free jobs leave k_tie_local unpartitioned (a sort with the radix route)
     // a segment without an order-dependent group: above the LDS size to the radix sort, else to k_tie_heap,
     // whose idle workgroups sort it in LDS beside the few segments that need pops (configs[4]: ~1200 such
     // segments per sort, half of the radix sort's keys, sorted off its critical path)
     __device__ __forceinline__ void file_free(int* ctl, long long off, int len) const {
-        if (len <= kHeapCap) {
+        if (len <= kHeapCap || !huge) {
             const int j = atomicAdd(&ctl[T_NHEAP], 1);
             if (j < cap) seg[j] = make_int2((int)off, len);
             else atomicOr(err, 4);
@@ -978,9 +980,15 @@ struct EmitGlobal {
     int* err;
     int4* hw;
     int hwcap;
+    int2* hg;              // TieAux::hs: segments above the LDS size with no levels left -> the radix route,
+    int hgcap;             // in working-copy offsets (k_huge_gather reads the working copy)
     __device__ void operator()(int f, int e, int d) const {
         if (e - f < 1) return;
-        if (d == -1 && hw) {
+        if (hg && (d == -1 || d == kDepFree) && e - f > kHeapCap) {
+            const int j = atomicAdd(&ctl[T_NHUGE], 1);
+            if (j < hgcap) hg[j] = make_int2(f, e - f);
+            else atomicOr(err, 4);
+        } else if (d == -1 && hw) {
             file_heapw(ctl, hw, hwcap, err, f, e, cls);
         } else if (d >= 0 && e - f > kTieSmall) {
             const int j = atomicAdd(&ctl[T_NMID], 1);
@@ -998,7 +1006,8 @@ __global__ void __launch_bounds__(1024) k_tie_medium(const u32* __restrict__ key
                                                      TieClasses cls, int from_classes, int depth0, u32* k, u32* v,
                                                      u32* lp, u32* rq, int* ctl, const int4* __restrict__ med,
                                                      int4* mid, int midcap, int4* jobs, int jcap, int* err,
-                                                     const u8* __restrict__ freef, int4* hw, int hwcap) {
+                                                     const u8* __restrict__ freef, int4* hw, int hwcap,
+                                                     int2* hg, int hgcap) {
     __shared__ MedWork<512> S;
     const int t = threadIdx.x, w = t >> 6, l = lane_id();
     const u64 lt = lanemask_lt();
@@ -1074,7 +1083,7 @@ __global__ void __launch_bounds__(1024) k_tie_medium(const u32* __restrict__ key
         }
         if (freef && d0 > 0 && e0 - f0 > kTieSmall && !range_dep(v, freef, f0, e0)) d0 = kDepFree;
         GStore st{k, v, lp, rq, f0};
-        part_levels<512>(st, S, f0, e0, d0, kTieMid, EmitGlobal{ctl, mid, jobs, midcap, jcap, cl, err, hw, hwcap}, err,
+        part_levels<512>(st, S, f0, e0, d0, kTieMid, EmitGlobal{ctl, mid, jobs, midcap, jcap, cl, err, hw, hwcap, hg, hgcap}, err,
                          blockIdx.x == 0 && it == 0 ? 256 : -1);
     }
 }
@@ -1360,7 +1369,7 @@ __global__ void __launch_bounds__(1024) k_tie_local(const u32* __restrict__ k, c
             if (c == job.w) ob = obase[c];
         // at the depth limit in a partition tier, or (with the radix route) without an order-dependent
         // group: as it stands, for k_tie_heap or the radix sort
-        const bool freej = d == kDepFree || (hl.huge && freef && d >= 0 && len > kThreshold &&
+        const bool freej = d == kDepFree || (hl.route && freef && d >= 0 && len > kThreshold &&
                                              !range_dep(v, freef, f, f + len));
         if (d < 0 || freej) {
             for (int i = t; i < len; i += 1024) {
@@ -2363,7 +2372,7 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
     __shared__ uint2 H[kHeapCap + 64];             // + a spare slot per lane of wave 0
     const int t = threadIdx.x;
     const int nh = ctl[which];
-    const int clm = which == T_NHEAPW ? T_CLM_HEAPW : T_CLM_HEAP;
+    const int clm = which == T_NHEAPW ? T_CLM_HEAPW : (which == T_NHEAPF ? T_CLM_HEAPF : T_CLM_HEAP);
     for (int jb = blockIdx.x; jb < nh; jb = next_item(nh, &ctl[clm])) {
         int2 sg;
         if (wsegs) {
@@ -2546,12 +2555,25 @@ __global__ void __launch_bounds__(256) k_huge_check(const int* ctl, int hugecap,
         if (dep && need[s] == 0u) atomicOr(&need[s], 1u);
     }
 }
-// the sorted copies written back; the segments that need the heap filed for it (block 0)
+// the sorted copies written back; the segments that need the heap filed for it (block 0). wk / wv (TieAux::hs):
+// the list is in working-copy offsets, so every segment goes to its output place (working offset + its class's
+// output base, as k_tie_local places jobs), those that need the heap in their working-copy order
+__device__ __forceinline__ int out_base(const int* ctl, int pos) {
+    int ob = 0, tot = 0;
+#pragma unroll
+    for (int c = 0; c < kMaxTieC; ++c) {
+        const int vc = ctl[T_VC + c];
+        if (pos >= ctl[T_BASE + c] && vc > 0) ob = tot - ctl[T_BASE + c];
+        tot += vc;
+    }
+    return ob;
+}
 __global__ void __launch_bounds__(256) k_huge_finish(u32* __restrict__ keys, u32* __restrict__ vals, int* ctl,
                                                      int hugecap, const int2* __restrict__ hseg,
                                                      const int* __restrict__ hbase, const u32* __restrict__ hk,
                                                      const u32* __restrict__ hv, const u32* __restrict__ need,
-                                                     int2* __restrict__ heapf) {
+                                                     int2* __restrict__ heapf, const u32* __restrict__ wk,
+                                                     const u32* __restrict__ wv) {
     __shared__ int s_base[kHugeLds + 1];
     __shared__ int s_nf;
     const int nh = huge_stage(ctl, hugecap, hbase, s_base);
@@ -2560,17 +2582,47 @@ __global__ void __launch_bounds__(256) k_huge_finish(u32* __restrict__ keys, u32
         if (threadIdx.x == 0) s_nf = 0;
         __syncthreads();
         for (int s = threadIdx.x; s < nh; s += 256)
-            if (need[s]) heapf[atomicAdd(&s_nf, 1)] = hseg[s];
+            if (need[s]) {
+                int2 sg = hseg[s];
+                if (wk) sg.x += out_base(ctl, sg.x);
+                heapf[atomicAdd(&s_nf, 1)] = sg;
+            }
         __syncthreads();
         if (threadIdx.x == 0) ctl[T_NHEAPF] = s_nf;
     }
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int s = huge_seg_of(s_base, hbase, nh, i);
-        if (need[s]) continue;
         const int p = hseg[s].x + (i - (nh < kHugeLds ? s_base[s] : hbase[s]));
+        if (wk) {
+            const int o = p + out_base(ctl, hseg[s].x);
+            const bool nd = need[s] != 0u;
+            keys[o] = nd ? wk[p] : hk[i];
+            vals[o] = nd ? wv[p] : hv[i];
+            continue;
+        }
+        if (need[s]) continue;
         keys[p] = hk[i];
         vals[p] = hv[i];
     }
+}
+
+// the radix route on stream s: every segment of the huge list sorted by one device-wide radix sort, written
+// back, and those that need pops heap-sorted (k_tie_heap's global path). work: the list holds working-copy
+// offsets (TieAux::hs; read from t.k / t.v, written to keys / vals at their output places), else output ones
+void huge_route(TieSort& t, u32* keys, u32* vals, int* err, const u8* freef, hipStream_t s, bool work, int nc) {
+    PrimWork pw = t.hprim;
+    pw.err = err;
+    hipLaunchKernelGGL(k_huge_setup, dim3(1), dim3(1024), 0, s, t.ctl, t.huge, t.hugecap, t.hseg, t.hbase, t.need);
+    hipLaunchKernelGGL(k_huge_gather, dim3(kHugeGrid), dim3(256), 0, s, work ? t.k : keys, work ? t.v : vals, t.ctl,
+                       t.hugecap, t.hseg, t.hbase, t.hk, t.hv, sort_hist(pw, 32, true));
+    radix_sort_pairs(t.hk, t.hv, t.ctl + T_HUGEN, 32, pw, s, nullptr, nullptr, true);
+    hipLaunchKernelGGL(k_huge_check, dim3(kHugeGrid), dim3(256), 0, s, t.ctl, t.hugecap, t.hbase, t.hk, t.hv, freef,
+                       t.need);
+    hipLaunchKernelGGL(k_huge_finish, dim3(kHugeGrid), dim3(256), 0, s, keys, vals, t.ctl, t.hugecap, t.hseg, t.hbase,
+                       t.hk, t.hv, t.need, t.heapf, work ? (const u32*)t.k : nullptr, work ? (const u32*)t.v : nullptr);
+    hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heapf, t.hbig, (int)t.cap,
+                       t.arrive + (work ? 5 : 3), freef, (int)T_NHEAPF, (int)T_NHUGE, (int2*)nullptr, 0, err,
+                       (const int4*)nullptr, (const u32*)nullptr, (const u32*)nullptr, nc);
 }
 
 }  // namespace
@@ -2652,10 +2704,13 @@ void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStr
     u32* depn = rf ? t.depn : nullptr;
     // the partition tiers' depth-limit segments heap-sorted on aux beside k_tie_local (no big levels)
     const bool side = aux && aux->s && levels <= 0;
+    // the radix route on aux->hs beside the tiers after k_tie_medium (big levels)
+    const bool early = huge && aux && aux->hs;
     int4* hw = side ? t.heapw : nullptr;
     if (levels <= 0) {
         hipLaunchKernelGGL(k_tie_medium, dim3(kMaxTieC), dim3(kMT), 0, s, keys, vals, cls, 1, t.depth0, t.k, t.v,
-                           t.lp, t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err, rf, hw, t.hcap);
+                           t.lp, t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err, rf, hw, t.hcap,
+                           (int2*)nullptr, 0);
     } else {
         const int tg = (int)(t.tiles < (size_t)kTieGrid ? t.tiles : (size_t)kTieGrid);
         hipLaunchKernelGGL(k_tie_compact, dim3(tg), dim3(256), 0, s, keys, vals, cls, t.k, t.v, t.ctl, t.status,
@@ -2670,7 +2725,14 @@ void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStr
                                t.mcap, err, depn);
         }
         hipLaunchKernelGGL(k_tie_medium, dim3(kMedGrid), dim3(kMT), 0, s, keys, vals, cls, 0, t.depth0, t.k, t.v, t.lp,
-                           t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err, rf, (int4*)nullptr, 0);
+                           t.rq, t.ctl, t.med, t.mid, t.midcap, t.jobs, t.jcap, err, rf, (int4*)nullptr, 0,
+                           early ? t.huge : (int2*)nullptr, t.hugecap);
+        if (early) {    // fork: the segments for the radix route are all filed
+            (void)hipEventRecord(aux->fork, s);
+            (void)hipStreamWaitEvent(aux->hs, aux->fork, 0);
+            huge_route(t, keys, vals, err, freef, aux->hs, true, cls.nc);
+            (void)hipEventRecord(aux->join, aux->hs);
+        }
     }
     hipLaunchKernelGGL(k_tie_mid, dim3(kMidGrid), dim3(kMT), 0, s, t.k, t.v, t.ctl, t.mid, t.jobs, t.jcap, err, rf, hw,
                        t.hcap);
@@ -2683,26 +2745,12 @@ void tie_sort(TieSort& t, u32* keys, u32* vals, TieClasses cls, int* err, hipStr
         (void)hipEventRecord(aux->join, aux->s);
     }
     hipLaunchKernelGGL(k_tie_local, dim3(kLocalGrid), dim3(1024), 0, s, t.k, t.v, t.jobs, t.ctl, t.arrive + 2, keys,
-                       vals, cls, HeapList{t.heaps, t.hcap, err, huge ? t.huge : nullptr, t.hugecap}, rf);
+                       vals, cls, HeapList{t.heaps, t.hcap, err, huge && !early ? t.huge : nullptr, t.hugecap, huge}, rf);
     hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heaps, t.hbig,
-                       (int)t.cap, t.arrive + 3, freef, (int)T_NHEAP, -1, huge ? t.huge : nullptr, t.hugecap, err,
-                       (const int4*)nullptr, (const u32*)nullptr, (const u32*)nullptr, cls.nc);
-    if (side) (void)hipStreamWaitEvent(s, aux->join, 0);   // join
-    if (huge) {
-        PrimWork pw = t.hprim;
-        pw.err = err;
-        hipLaunchKernelGGL(k_huge_setup, dim3(1), dim3(1024), 0, s, t.ctl, t.huge, t.hugecap, t.hseg, t.hbase, t.need);
-        hipLaunchKernelGGL(k_huge_gather, dim3(kHugeGrid), dim3(256), 0, s, keys, vals, t.ctl, t.hugecap, t.hseg,
-                           t.hbase, t.hk, t.hv, sort_hist(pw, 32, true));
-        radix_sort_pairs(t.hk, t.hv, t.ctl + T_HUGEN, 32, pw, s, nullptr, nullptr, true);
-        hipLaunchKernelGGL(k_huge_check, dim3(kHugeGrid), dim3(256), 0, s, t.ctl, t.hugecap, t.hbase, t.hk, t.hv,
-                           freef, t.need);
-        hipLaunchKernelGGL(k_huge_finish, dim3(kHugeGrid), dim3(256), 0, s, keys, vals, t.ctl, t.hugecap, t.hseg,
-                           t.hbase, t.hk, t.hv, t.need, t.heapf);
-        hipLaunchKernelGGL(k_tie_heap, dim3(kHeapGrid), dim3(kHeapT), 0, s, keys, vals, t.ctl, t.heapf, t.hbig,
-                           (int)t.cap, t.arrive + 3, freef, (int)T_NHEAPF, (int)T_NHUGE, (int2*)nullptr, 0, err,
-                           (const int4*)nullptr, (const u32*)nullptr, (const u32*)nullptr, cls.nc);
-    }
+                       (int)t.cap, t.arrive + 3, freef, (int)T_NHEAP, -1, huge && !early ? t.huge : nullptr, t.hugecap,
+                       err, (const int4*)nullptr, (const u32*)nullptr, (const u32*)nullptr, cls.nc);
+    if (side || early) (void)hipStreamWaitEvent(s, aux->join, 0);   // join
+    else if (huge) huge_route(t, keys, vals, err, freef, s, false, cls.nc);
 }
 
 const int* tie_valid_count(const TieSort& t) { return t.ctl + T_VALID; }
