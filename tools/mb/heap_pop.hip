@@ -7,6 +7,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb/heap_pop.hip -o /tmp/heap_pop && /tmp/heap_pop
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -1883,6 +1884,242 @@ __device__ __forceinline__ unsigned long long step_asm19(u32 base, u32 b24, u32 
     h = hn;
     return blk;
 }
+__device__ __forceinline__ unsigned long long step_e41(u32 base, u32 b24, u32 nbb, int& h, u32& ad, u32& lh, u32 vb8, u32 vnbb,
+                                           u32& vx, u32& vy, int spare, u32 vsp8, u32 vzero,
+                                           unsigned long long mine, unsigned long long minew, u32 aq, u32 vrp) {
+    int hn;
+    u32 sa, t0, t1, t2, t3, t4, aL, aR, aN;
+    unsigned long long sm, tt, rm;
+    asm volatile(
+        "ds_read_b64 v[44:45], %[aq]\n\t"
+        "v_cndmask_b32_e64 %[sa], %[sp8], %[aq], %[minew]\n\t"
+        "v_cndmask_b32_e64 %[ad], %[ad], %[vb8], %[mine]\n\t"
+        "ds_write2_b32 %[sa], %[rp], %[zz] offset1:1\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
+        "v_cndmask_b32_e64 %[lh], %[lh], 0, %[mine]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+        "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+        "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+        "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+        "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], v44, %[mine]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], v45, %[mine]\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        : [hn] "=&v"(hn), [h] "+v"(h), [ad] "+v"(ad), [lh] "+v"(lh), [vx] "+v"(vx), [vy] "+v"(vy),
+          [sa] "=&v"(sa), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR), [aN] "=&v"(aN),
+          [sm] "=&s"(sm), [tt] "=&s"(tt), [rm] "=&s"(rm)
+        : [sp] "v"(spare), [sp8] "v"(vsp8), [zz] "v"(vzero), [base] "s"(base), [b24] "s"(b24), [nbb] "s"(nbb),
+          [vb8] "v"(vb8), [vnbb] "v"(vnbb), [mine] "s"(mine), [minew] "s"(minew), [aq] "v"(aq), [rp] "v"(vrp)
+        : "memory", "v40", "v41", "v42", "v43", "v44", "v45");
+    h = hn;
+    return sm;
+}
+__device__ __forceinline__ unsigned long long step_f41(u32 base, u32 b24, u32 nbb, int& h, u32& ad, u32& lh,
+                                                     u32 vnbb, u32 vx, u32 vy, int spare, u32 q1, u32 lq1,
+                                                     u32 vbase, unsigned long long& vrp64, u32 aqs, u32& aq,
+                                                     unsigned long long& smo) {
+    int hn;
+    u32 sh, an, t0, t1, t2, t3, t4, aL, aR, aN;
+    unsigned long long sm, blk, tt, rm, bm;
+    asm volatile(
+            "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+            "ds_read_b64 %[rp], %[vb]\n\t"
+            "v_sub_u32_e32 %[sh], %[lq1], %[lh]\n\t"
+            "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+            "v_lshrrev_b32_e64 %[an], %[sh], %[q1]\n\t"
+            "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+            "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+            "v_add_u32_e32 %[an], -1, %[an]\n\t"
+            "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+            "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+            "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+            "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+            "v_mov_b32_e32 %[aq], %[aqs]\n\t"
+            "s_waitcnt lgkmcnt(0)\n\t"
+            "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+            "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+            "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+            "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+            "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+            "s_nop 0\n\t"
+            "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+            "v_cmp_eq_u32_e64 %[bm], %[an], %[t3]\n\t"
+            "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+            "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+            "s_andn2_b64 %[blk], %[bm], %[sm]\n\t"
+            : [hn] "=&v"(hn), [ad] "+v"(ad), [lh] "+v"(lh), [sh] "=&v"(sh), [an] "=&v"(an), [t0] "=&v"(t0),
+              [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR),
+              [aN] "=&v"(aN), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm), [bm] "=&s"(bm),
+              [rp] "=&v"(vrp64), [aq] "=&v"(aq)
+            : [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24),
+              [nbb] "s"(nbb), [vnbb] "v"(vnbb), [q1] "s"(q1), [lq1] "s"(lq1), [vb] "v"(vbase), [aqs] "s"(aqs)
+            : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+    smo = sm;
+    return blk;
+}
+
+// v41 (round 6): v40's steps plus speculative starts (one pending pop at a time; the protocol of
+// pops_spec, checked step by step by /tmp-side simulation): a start blocked by an older hole at or above
+// its last element q (q >= 64, so q is a leaf of every older pop's heap) takes H[q] now, writes its output
+// (the root's name) only once no older hole covers q, and takes the value of an older pop that ends at q;
+// a pending pop that would stop first undoes that step's write and freezes with every younger pop (parked
+// as idle lanes) until then, the younger ones one step longer; a start needs the youngest pop two levels
+// deep and a block mask taken with no lane parked.
+__device__ __forceinline__ bool anc41(int h, int q) {
+    const int sh = hlev(q) - hlev(h);
+    return sh >= 0 && ((q + 1) >> sh) == h + 1;
+}
+__device__ int pops_v41(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    const u32 b24 = base + 24u;
+    u32 vb8 = base + 8u, vnbb = nbb, vbase = base, vsp8 = base + 8u * (u32)spare, vzero = 0u;
+    asm volatile("" : "+v"(vb8), "+v"(vnbb), "+v"(vbase), "+v"(vsp8), "+v"(vzero));
+    int nxt = 0;
+    int h = spare;
+    u32 ad = nbb, lh = 0u;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0, sm = 0;
+    unsigned long long vrp64 = ((unsigned long long)H[0].y << 32) | H[0].x;
+    u32 aq = base + 8u * (u32)last;
+    int steps = 0;
+    bool pact = false, pstall = false, hold = false, rel = false, fzprev = false;
+    int pq = 0, plane = 0, ydep = 2;
+    u32 prp = 0u, prk = 0u, pq1 = 0u, lpq = 0u;
+    unsigned long long pold = 0;
+    for (;;) {
+        if (!pact && !fzprev) {
+            // fast path: v40's pairs; leaves when a start is blocked and may go speculative
+            bool spec = false;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (blk != 0 && nxt < npops && last - nxt >= 64) { spec = true; break; }
+                const bool start = nxt < npops && blk == 0;
+                const unsigned long long mine = start ? (1ull << (nxt & 63)) : 0ull;
+                step_e41(base, b24, nbb, h, ad, lh, vb8, vnbb, vx, vy, spare, vsp8, vzero, mine, mine, aq, (u32)vrp64);
+                nxt += start ? 1 : 0;
+                const u32 q1 = (u32)(last - nxt + 1);
+                blk = step_f41(base, b24, nbb, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)), vbase, vrp64,
+                               base + 8u * (u32)(last - nxt), aq, sm);
+                steps += 2;
+            }
+            if (!spec) {
+                if (nxt >= npops && __ballot(h != spare) == 0) break;
+                continue;
+            }
+            ydep = 2;
+        }
+        // slow path: one pair with a pending (or frozen) pop
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            if (pact && rel) {                                   // the held output, now that no older hole covers q
+                if (l == plane) H[pq] = make_uint2(prp, 0u);
+                pact = false;
+                rel = false;
+                if (pstall) { pstall = false; hold = true; }
+            }
+            unsigned long long fz = 0;
+            if (pstall || hold) {
+                fz = __ballot(h != spare) & ~pold;
+                if (hold) fz &= ~(1ull << plane);
+            }
+            unsigned long long mine = 0, minew = 0;
+            if (sub == 0 && nxt < npops && !pstall && !hold && !fzprev && ydep >= 2) {
+                const int q = last - nxt;
+                const int L = nxt & 63;
+                if (blk == 0) {
+                    mine = minew = 1ull << L;
+                } else if (!pact && q >= 64) {
+                    mine = 1ull << L;
+                    pact = true;
+                    rel = false;
+                    pq = q;
+                    pq1 = (u32)q + 1u;
+                    lpq = (u32)hlev(q);
+                    plane = L;
+                    prp = (u32)__builtin_amdgcn_readfirstlane((int)(u32)vrp64);
+                    prk = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(vrp64 >> 32));
+                    pold = __ballot(h != spare);
+                }
+                pold &= ~mine;
+            }
+            int sh_ = h;
+            u32 sad = ad, slh = lh;
+            if (fz) {
+                if ((fz >> l) & 1ull) { h = spare; ad = nbb; }
+            }
+            const int hold_h = h;
+            if (sub == 0) {
+                sm = step_e41(base, b24, nbb, h, ad, lh, vb8, vnbb, vx, vy, spare, vsp8, vzero, mine, minew, aq, (u32)vrp64);
+                nxt += mine ? 1 : 0;
+            } else {
+                const u32 q1 = (u32)(last - nxt + 1);
+                blk = step_f41(base, b24, nbb, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)), vbase, vrp64,
+                               base + 8u * (u32)(last - nxt), aq, sm);
+            }
+            if (fz) {
+                if ((fz >> l) & 1ull) { h = sh_; ad = sad; lh = slh; }
+            }
+            fzprev = fz != 0;
+            if (pact) {
+                if (!pstall && ((sm >> plane) & 1ull) && !((fz >> plane) & 1ull)) {
+                    // the pending pop would stop: undo its write, keep it at its hole, freeze
+                    const int hs = __builtin_amdgcn_readlane(hold_h, plane);
+                    if (l == plane) {
+                        H[hs] = hs > 0 ? H[(hs - 1) >> 1] : make_uint2(prp, prk);
+                        h = hs;
+                        const u32 a0 = base + 8u + 16u * (u32)hs;
+                        ad = a0 < nbb ? a0 : nbb;
+                        lh = (u32)hlev(hs);
+                    }
+                    pstall = true;
+                }
+                const unsigned long long ho = __ballot(hold_h == pq) & sm & pold & ~fz;
+                if (ho) {                                        // an older pop ended at q: its value is the pending pop's
+                    const int src = __ffsll((long long)ho) - 1;
+                    const u32 nx = (u32)__builtin_amdgcn_readlane((int)vx, src), ny = (u32)__builtin_amdgcn_readlane((int)vy, src);
+                    if (l == plane) { vx = nx; vy = ny; }
+                }
+                // an older hole still at q or above it: q's ancestor at the hole's level (lh) is the hole
+                const u32 anp = (pq1 >> (lpq - lh)) - 1u;
+                rel = (__ballot(lh <= lpq && anp == (u32)h) & pold) == 0;
+            }
+            hold = false;
+            if (mine) ydep = 1;
+            else if (!((fz >> ((nxt - 1) & 63)) & 1ull)) ++ydep;
+            ++steps;
+        }
+        if (nxt >= npops && !pact && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
 template <int U, bool SALU_BLK>
 __device__ int pops_v39(uint2* H, int n, int npops) {
     n = __builtin_amdgcn_readfirstlane(n);
@@ -2091,6 +2328,111 @@ __device__ int pops_v29(uint2* H, int n, int npops) {
 }
 
 
+// ---- speculative starts (round 6): a pop whose last element q still lies under an older pop's hole starts
+// anyway, with the value it reads there, and holds its output (the root's name) back; the older pop that
+// ends at q hands it its value instead (that value is <= the one read, so a pop that has not stopped
+// stays consistent), and the held output is written once no older hole is q or an ancestor of q. A
+// pending pop that would stop first waits (it and every younger pop freeze, no pop starts) until then.
+// Entries {position, key + 1} as the LDS engines; explicit heap size per lane. PMAX pending pops at most.
+__device__ __forceinline__ bool anc_of(int h, int q) {        // hole h is q or an ancestor of q
+    const int sh = hlev(q) - hlev(h);
+    return sh >= 0 && ((q + 1) >> sh) == h + 1;
+}
+template <int PMAX>
+__device__ u64 pops_spec(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    int h = spare, m = 0, idx = -1;
+    u32 vx = 0u, vy = 1u;
+    int nxt = 0;
+    int pl[PMAX], pq[PMAX];
+    u32 po[PMAX];
+    unsigned long long pold[PMAX];
+    bool pst[PMAX];
+#pragma unroll
+    for (int s = 0; s < PMAX; ++s) { pl[s] = -1; pq[s] = 0; po[s] = 0u; pold[s] = 0ull; pst[s] = false; }
+    u64 steps = 0;
+    for (;;) {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            ++steps;
+            // held outputs whose q no older hole covers any more
+#pragma unroll
+            for (int s = 0; s < PMAX; ++s)
+                if (pl[s] >= 0 && (__ballot(anc_of(h, pq[s])) & pold[s]) == 0) {
+                    if (l == 0) H[pq[s]] = make_uint2(po[s], 0u);
+                    pl[s] = -1;
+                    pst[s] = false;
+                }
+            int ff = INT_MAX;                                      // frozen from this pop index on
+#pragma unroll
+            for (int s = 0; s < PMAX; ++s) if (pl[s] >= 0 && pst[s]) ff = min(ff, pl[s]);
+            if (sub == 0 && nxt < npops && ff == INT_MAX) {
+                const int q = last - nxt;
+                const unsigned long long blk = __ballot(idx >= 0 && anc_of(h, q));
+                int fs = -1;
+#pragma unroll
+                for (int s = PMAX - 1; s >= 0; --s) if (pl[s] < 0) fs = s;
+                if (blk == 0 || (q >= 64 && fs >= 0)) {
+                    const int L = nxt & 63;
+                    const uint2 vq = H[q], r0 = H[0];
+                    const unsigned long long act = __ballot(idx >= 0);
+#pragma unroll
+                    for (int s = 0; s < PMAX; ++s) pold[s] &= ~(1ull << L);
+                    if (blk == 0) {
+                        if (l == 0) H[q] = make_uint2(r0.x, 0u);
+                    } else {
+#pragma unroll
+                        for (int s = 0; s < PMAX; ++s)
+                            if (s == fs) { pl[s] = nxt; pq[s] = q; po[s] = r0.x; pold[s] = act & ~(1ull << L); pst[s] = false; }
+                    }
+                    if (l == L) { h = 0; m = q; vx = vq.x; vy = vq.y; idx = nxt; }
+                    ++nxt;
+                }
+            }
+            // one level for every live lane
+            const bool live = idx >= 0 && idx < ff;
+            const int c1 = 2 * h + 1;
+            const bool has = live && c1 < m;
+            const int cr = has ? c1 : n;
+            const uint2 a = H[cr], b = H[cr + 1];
+            const bool right = has && c1 + 1 < m && !(b.y < a.y);
+            const uint2 ch = right ? b : a;
+            const bool stop = !has || ch.y < vy;
+            bool isp = false;
+#pragma unroll
+            for (int s = 0; s < PMAX; ++s) isp = isp || (pl[s] >= 0 && idx == pl[s]);
+            const bool stall = live && isp && stop;
+            const bool wr = live && !stall;
+            H[wr ? h : spare] = stop ? make_uint2(vx, vy) : ch;
+            // a stopping older pop at a held q hands its value to that pending pop
+#pragma unroll
+            for (int s = 0; s < PMAX; ++s) {
+                if (pl[s] < 0) continue;
+                const unsigned long long hb = __ballot(wr && stop && h == pq[s] && idx < pl[s]);
+                if (hb) {
+                    const int src = __ffsll((long long)hb) - 1;
+                    const u32 nx = (u32)__shfl((int)vx, src, 64), ny = (u32)__shfl((int)vy, src, 64);
+                    if (idx == pl[s]) { vx = nx; vy = ny; }
+                }
+                if (__ballot(stall && idx == pl[s])) pst[s] = true;
+            }
+            if (wr) {
+                if (stop) { idx = -1; h = spare; m = 0; }
+                else h = c1 + (right ? 1 : 0);
+            }
+        }
+        bool pend = false;
+#pragma unroll
+        for (int s = 0; s < PMAX; ++s) pend = pend || pl[s] >= 0;
+        if (nxt >= npops && __ballot(idx >= 0) == 0 && !pend) break;
+    }
+    return steps;
+}
+
 template <int V>
 __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, const int* npops_in, u64* out_t, const u64* input) {
     __shared__ uint2 H[kCap + 72];
@@ -2129,7 +2471,7 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
     if (t < 64 && n >= 2 && npops > 0) {
         const u64 r0 = __builtin_amdgcn_s_memrealtime();
         const u64 t0 = __builtin_amdgcn_s_memtime();
-        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : V == 23 ? (u64)pops_v28<4>(H, n, npops) : V == 24 ? (u64)pops_v29<4>(H, n, npops) : V == 25 ? (u64)pops_v30<4, true, false>(H, n, npops) : V == 26 ? (u64)pops_v30<4, false, true>(H, n, npops) : V == 27 ? (u64)pops_v30<4, true, true>(H, n, npops) : V == 28 ? (u64)pops_v33<4, false, false>(H, n, npops) : V == 29 ? (u64)pops_v33<4, true, true>(H, n, npops) : V == 30 ? (u64)pops_v36<4, false, false>(H, n, npops) : V == 31 ? (u64)pops_v36<4, true, true>(H, n, npops) : V == 32 ? (u64)pops_v38<4>(H, n, npops) : V == 33 ? (u64)pops_v39<4, false>(H, n, npops) : (u64)pops_v39<4, true>(H, n, npops);
+        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : V == 23 ? (u64)pops_v28<4>(H, n, npops) : V == 24 ? (u64)pops_v29<4>(H, n, npops) : V == 25 ? (u64)pops_v30<4, true, false>(H, n, npops) : V == 26 ? (u64)pops_v30<4, false, true>(H, n, npops) : V == 27 ? (u64)pops_v30<4, true, true>(H, n, npops) : V == 28 ? (u64)pops_v33<4, false, false>(H, n, npops) : V == 29 ? (u64)pops_v33<4, true, true>(H, n, npops) : V == 30 ? (u64)pops_v36<4, false, false>(H, n, npops) : V == 31 ? (u64)pops_v36<4, true, true>(H, n, npops) : V == 32 ? (u64)pops_v38<4>(H, n, npops) : V == 33 ? (u64)pops_v39<4, false>(H, n, npops) : V == 34 ? (u64)pops_v39<4, true>(H, n, npops) : V == 35 ? pops_spec<1>(H, n, npops) : V == 36 ? pops_spec<2>(H, n, npops) : V == 37 ? pops_spec<4>(H, n, npops) : (u64)pops_v41(H, n, npops);
         const u64 t1 = __builtin_amdgcn_s_memtime();
         const u64 r1 = __builtin_amdgcn_s_memrealtime();
         if (t == 0) {
@@ -2239,6 +2581,135 @@ __global__ void __launch_bounds__(kT) k_full(u32* keys, u32* vals, int n, int np
         for (int k = 0; k < 6; ++k) out_t[k] = tm[k];
 }
 
+// ---- register-resident serial pops (segments of at most 2048 keys): the heap in 32 VGPRs of wave 0 ----------
+// Entries are packed rank << 11 | name (rank: the key's rank among the segment's sorted keys, lower bound,
+// so equal keys share it; name: the input position). One pop at a time, top-down (libstdc++'s __adjust_heap +
+// __push_heap in the form the LDS engines use); every index is wave-uniform, so a heap read is an indexed
+// VGPR move plus v_readlane and a write an indexed move, a lane select and a move back.
+constexpr int kRegRows = 32;
+__device__ __forceinline__ u32 re_rd(const u32 (&E)[kRegRows], int p) {
+    return (u32)__builtin_amdgcn_readlane((int)E[p >> 6], p & 63);
+}
+__device__ __forceinline__ void re_wr(u32 (&E)[kRegRows], int p, u32 v) {
+    const int r = p >> 6;
+    const u32 x = E[r];
+    E[r] = (int)(threadIdx.x & 63) == (p & 63) ? v : x;
+}
+__device__ u64 pops_reg(u32 (&E)[kRegRows], int n, int npops) {
+    const int last = n - 1;
+    u64 lv = 0;
+    for (int i = 0; i < npops; ++i) {
+        const int q = last - i;
+        const u32 x = re_rd(E, q), xr = x >> 11;
+        re_wr(E, q, re_rd(E, 0));
+        int h = 0;
+        for (;;) {
+            const int c1 = 2 * h + 1;
+            if (c1 >= q) break;
+            u32 a = re_rd(E, c1);
+            int c = c1;
+            if (c1 + 1 < q) {
+                const u32 b = re_rd(E, c1 + 1);
+                if (!((b >> 11) < (a >> 11))) { a = b; c = c1 + 1; }
+            }
+            if ((a >> 11) < xr) break;
+            re_wr(E, h, a);
+            h = c;
+            ++lv;
+        }
+        re_wr(E, h, x);
+    }
+    return lv;
+}
+__global__ void __launch_bounds__(kT) k_heap_reg(u64* keys_vals, const int* segn, const int* npops_in, u64* out_t,
+                                                 const u64* input) {
+    __shared__ uint2 H[2048 + 2];
+    __shared__ u32 S[2048];
+    const int n = segn[blockIdx.x];
+    if (n > 2048) return;
+    const int npops = npops_in[blockIdx.x] < 0 ? n - 1 : npops_in[blockIdx.x];
+    u64* g = keys_vals + (size_t)blockIdx.x * kCap;
+    const int t = threadIdx.x;
+    for (int i = t; i < n; i += kT) {
+        const u64 x = g[i];
+        H[i] = make_uint2((u32)i, (u32)(x >> 32));
+        S[i] = (u32)(x >> 32);
+    }
+    __syncthreads();
+    for (int L = hlev((n - 2) / 2); n >= 2 && L >= 0; --L) {       // __make_heap, a level at a time
+        const int lo = (1 << L) - 1, hi = min((2 << L) - 2, (n - 2) / 2);
+        for (int x = lo + t; x <= hi; x += kT) {
+            const uint2 vk = H[x];
+            int h = x;
+            for (;;) {
+                const int c1 = 2 * h + 1;
+                if (c1 >= n) break;
+                int c = c1;
+                uint2 a = H[c1];
+                if (c1 + 1 < n) {
+                    const uint2 b = H[c1 + 1];
+                    if (!(b.y < a.y)) { a = b; c = c1 + 1; }
+                }
+                if (a.y < vk.y) break;
+                H[h] = a;
+                h = c;
+            }
+            H[h] = vk;
+        }
+        __syncthreads();
+    }
+    const int P = n <= 1 ? 1 : 1 << (32 - __clz(n - 1));
+    for (int k = 2; k <= P; k <<= 1)                                // the keys sorted (ranks)
+        for (int j = k >> 1; j >= 1; j >>= 1) {
+            for (int c = t; c < (P >> 1); c += kT) {
+                const int i = ((c & ~(j - 1)) << 1) | (c & (j - 1));
+                const int q = j == (k >> 1) ? (i ^ (k - 1)) : i + j;
+                if (q < n) {
+                    const u32 a = S[i], b = S[q];
+                    if (b < a) { S[i] = b; S[q] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    if (t < 64) {
+        u32 E[kRegRows];
+#pragma unroll
+        for (int r = 0; r < kRegRows; ++r) {
+            const int i = r * 64 + t;
+            u32 e = 0;
+            if (i < n) {
+                const uint2 x = H[i];
+                int lo = 0, hi = n;                                 // lower bound of the key in S
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (S[mid] < x.y) lo = mid + 1;
+                    else hi = mid;
+                }
+                e = ((u32)lo << 11) | x.x;
+            }
+            E[r] = e;
+        }
+        const u64 r0 = __builtin_amdgcn_s_memrealtime();
+        const u64 t0 = __builtin_amdgcn_s_memtime();
+        const u64 lv = n >= 2 && npops > 0 ? pops_reg(E, n, npops) : 0;
+        const u64 t1 = __builtin_amdgcn_s_memtime();
+        const u64 r1 = __builtin_amdgcn_s_memrealtime();
+        if (t == 0) {
+            out_t[3 * blockIdx.x] = t1 - t0;
+            out_t[3 * blockIdx.x + 1] = lv;
+            out_t[3 * blockIdx.x + 2] = r1 - r0;
+        }
+#pragma unroll
+        for (int r = 0; r < kRegRows; ++r) {
+            const int i = r * 64 + t;
+            if (i < n) H[i].x = E[r] & 2047u;
+        }
+    }
+    __syncthreads();
+    const u64* src = input + (size_t)blockIdx.x * kCap;
+    for (int i = t; i < n; i += kT) g[i] = src[H[i].x];
+}
+
 struct Case { const char* name; int n; int kind; int npops; };
 
 static std::vector<u64> make_input(int n, int kind, std::mt19937& rng) {
@@ -2262,7 +2733,9 @@ int main(int argc, char** argv) {
                                {"ties", 20000, 0, -1}, {"dist", 7000, 1, -1},  {"asc", 7000, 2, -1},
                                {"desc", 7000, 3, -1},  {"map", 12000, 4, -1},  {"ties-part", 9000, 0, 3000},
                                {"small", 2, 0, -1},    {"small", 3, 0, -1},    {"small", 17, 0, -1},
-                               {"small", 100, 0, -1},  {"map", 18000, 4, 11000}};
+                               {"small", 100, 0, -1},  {"map", 18000, 4, 11000},
+                               {"ties", 1300, 0, 1000}, {"asc", 1300, 2, 1000},  {"asc", 2048, 2, -1},
+                               {"map", 1500, 4, 1200},  {"dist", 2000, 1, -1}};
     // HEAP_DUMP=<file> (oracle PFREF_HEAP_DUMP: int32 len, int32 pops, len keys per segment): real depth-limit
     // segments as extra cases, partial pops as the library runs them (HEAP_DUMP_MAX of them, default 24)
     std::vector<std::vector<u64>> dumped;
@@ -2313,8 +2786,9 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d_np, np.data(), nb * 4, hipMemcpyHostToDevice));
     std::vector<u64> out(in.size()), tt(3 * nb);
     const int vlo = argc > 2 ? std::atoi(argv[2]) : 22;
-    for (int v = vlo; v <= 34; ++v) {
-        if (v >= 2 && v <= 21 || (v >= 23 && v <= 31)) continue;
+    const int vhi = argc > 3 ? std::atoi(argv[3]) : 34;
+    for (int v = vlo; v <= vhi; ++v) {
+        if (v >= 2 && v <= 21 || (v >= 23 && v <= 31) || (v >= 35 && v <= 37)) continue;
         for (int r = 0; r < reps; ++r) {
             CK(hipMemcpy(d_kv, in.data(), in.size() * 8, hipMemcpyHostToDevice));
             if (v == 1) hipLaunchKernelGGL(k_heap<1>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
@@ -2350,7 +2824,11 @@ int main(int argc, char** argv) {
             else if (v == 31) hipLaunchKernelGGL(k_heap<31>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 32) hipLaunchKernelGGL(k_heap<32>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 33) hipLaunchKernelGGL(k_heap<33>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
-            else hipLaunchKernelGGL(k_heap<34>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 34) hipLaunchKernelGGL(k_heap<34>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 35) hipLaunchKernelGGL(k_heap<35>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 36) hipLaunchKernelGGL(k_heap<36>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 37) hipLaunchKernelGGL(k_heap<37>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else hipLaunchKernelGGL(k_heap<38>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             CK(hipDeviceSynchronize());
         }
         CK(hipMemcpy(out.data(), d_kv, out.size() * 8, hipMemcpyDeviceToHost));
@@ -2369,6 +2847,31 @@ int main(int argc, char** argv) {
                         tt[3 * b + 2] / 100.0 / std::max(1, pops));
             if (bad >= 0) std::printf("   first difference at %d\n", bad);
             std::fflush(stdout);
+        }
+    }
+    {   // the register engine (k_heap_reg, segments of at most 2048 keys)
+        for (int r = 0; r < reps; ++r) {
+            CK(hipMemcpy(d_kv, in.data(), in.size() * 8, hipMemcpyHostToDevice));
+            CK(hipMemset(d_t, 0, nb * 24));
+            hipLaunchKernelGGL(k_heap_reg, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            CK(hipDeviceSynchronize());
+        }
+        CK(hipMemcpy(out.data(), d_kv, out.size() * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(tt.data(), d_t, nb * 24, hipMemcpyDeviceToHost));
+        for (int b = 0; b < nb; ++b) {
+            const Case& c = cases[b];
+            if (c.n > 2048) continue;
+            const size_t o = (size_t)b * kCap;
+            int bad = -1;
+            const int from = c.npops < 0 ? 0 : c.n - c.npops;
+            for (int i = from; i < c.n; ++i)
+                if (out[o + i] != ref[o + i]) { bad = i; break; }
+            const int pops = c.npops < 0 ? c.n - 1 : c.npops;
+            std::printf("reg %-9s n %6d pops %6d  %s  %7.1f cycles/pop  %.2f levels/pop  %6.1f cycles/level  %.3f us/pop\n",
+                        c.name, c.n, pops, bad < 0 ? "ok  " : "DIFF", (double)tt[3 * b] / std::max(1, pops),
+                        (double)tt[3 * b + 1] / std::max(1, pops), (double)tt[3 * b] / std::max<u64>(1, tt[3 * b + 1]),
+                        tt[3 * b + 2] / 100.0 / std::max(1, pops));
+            if (bad >= 0) std::printf("   first difference at %d\n", bad);
         }
     }
     {   // the whole segment path, phase by phase, on map-like segments with partial pops
