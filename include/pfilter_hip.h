@@ -111,13 +111,16 @@ typedef struct pf_odom pf_odom;
  * Any number of handles may share a device (bounded by device memory): no kernel of the pipeline
  * depends on its workgroups being co-resident with each other or with other handles' kernels.
  *
- * Device memory per handle grows with map_capacity, about 180 B per map point per class (nc = 2 map
+ * Device memory per handle grows with map_capacity, about 280 B per map point per class (nc = 2 map
  * classes for ES, 3 for BPF): the p-index buckets take 64 B (pf_odom.h kBktQuads), the two map sets
- * 32 B, and the map update's keys, sort buffers and voxel staging about 84 B (pf_odom.hip odom_create).
- * The default map_capacity 1 << 22 therefore needs about 1.5 GiB (ES) / 2.3 GiB (BPF) per handle,
- * and the per-scan buffers scale with max_points on top. configs[3] runs 11 handles per GPU, about
- * 17 GiB of the 288 GiB. Size map_capacity to the largest expected local map when many handles share
- * a device.
+ * 32 B, the map update's keys, sort buffers and voxel staging about 84 B, and the reference tie order's
+ * sort structures (working copy, rank lists, heap scratch, radix route) and its dependence table the
+ * rest (pf_odom.hip odom_create, pf_tie.hip tie_alloc, odom_dep_alloc). Measured (tools/mem_probe.py,
+ * round 6): 3.2 GiB (ES) / 4.6 GiB (BPF) per handle at the defaults (max_points 300000, map_capacity
+ * 1 << 22), 1.2 GiB for ES at map_capacity 1 << 18 (the per-scan buffers, which scale with max_points,
+ * dominate there). bench.py's configs[3] runs 4 handles per GPU (about 13 GiB of the 288 GiB), the
+ * 12-handle concurrency test about 39 GiB. Size map_capacity to the largest expected local map when
+ * many handles share a device.
  *
  * Device-side failures (a bounded wait that gave up, a featureExtraction sector above 4096 points,
  * a map grid or front-end grid above capacity) latch sticky error words on the device. They are

@@ -2455,7 +2455,9 @@ __global__ void __launch_bounds__(kHeapT) k_tie_heap(u32* __restrict__ keys, u32
 // classes come in class order), so one stable radix sort of all of them gathered back to back in position
 // order leaves every segment's keys sorted in its own range. Where that sorted copy is the result (no
 // order-dependent group, as in k_tie_heap) it is written back; the other segments keep their input and go
-// to the heap tier. The list is filed in any order: k_huge_setup ranks it by offset.
+// to the heap tier. The list is filed in any order: k_huge_setup ranks it by offset (O(nh^2)
+// on one workgroup: since round 6 the list only holds segments above the LDS size, the shorter dependence-free
+// ones being sorted by k_tie_heap's idle workgroups, so nh <= cap / 20352, about 200 at the default capacity).
 constexpr int kHugeGrid = 256;
 constexpr int kHugeLds = 4096;           // segment bases the gather / check / finish kernels stage in LDS
 __global__ void __launch_bounds__(1024) k_huge_setup(int* ctl, const int2* __restrict__ huge, int hugecap,
