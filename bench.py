@@ -475,9 +475,10 @@ def knn_roofline(device=0, nmap=2_000_000, nq=200_000, iters=50, pmc=True):
     return out
 
 
-def knn_pmc_traffic(timeout_s=90):
-    """HBM (fabric) bytes per launch of k_knn_thick (the standalone query's kernel), measured now: two rocprofv3 --pmc passes
-    (FETCH_SIZE, then WRITE_SIZE: they do not fit one pass) over tools/knn_probe.py as child processes.
+def knn_pmc_traffic(timeout_s=90, probe=("knn_probe.py", "--iters", "5"), kernel="k_knn_thick"):
+    """HBM (fabric) bytes per launch of k_knn_thick (the standalone query's kernel; or `kernel` of the
+    `probe` script), measured now: two rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE: they do not fit
+    one pass) over tools/<probe> as child processes.
     MI355X_MICROARCH.md: FETCH_SIZE is doubled on gfx950 (128-B requests tallied at 64 B); WRITE_SIZE
     is exact. None when rocprofv3 is unavailable or a pass fails (never a stale number)."""
     import csv
@@ -493,8 +494,7 @@ def knn_pmc_traffic(timeout_s=90):
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(tmp, ctr)
             cmd = ["timeout", "-s", "KILL", str(timeout_s), "rocprofv3", "--pmc", ctr, "-d", d, "-o", "run",
-                   "--output-format", "csv", "--", sys.executable, os.path.join(ROOT, "tools", "knn_probe.py"),
-                   "--iters", "5"]
+                   "--output-format", "csv", "--", sys.executable, os.path.join(ROOT, "tools", probe[0])] + list(probe[1:])
             env = dict(os.environ, TMPDIR="/tmp")
             r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, cwd="/tmp")
             if r.returncode != 0:
@@ -503,7 +503,7 @@ def knn_pmc_traffic(timeout_s=90):
             xs = []
             for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
                 for row in csv.DictReader(open(f)):
-                    if "k_knn_thick" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                    if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
                         xs.append(float(row["Counter_Value"]))
             if not xs:
                 return None
@@ -513,7 +513,7 @@ def knn_pmc_traffic(timeout_s=90):
     rd, wr = 2.0 * vals["FETCH_SIZE"], vals["WRITE_SIZE"]
     return {"bytes_per_launch": round(rd + wr), "read": round(rd), "write": round(wr),
             "source": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, measured in this run "
-                      "(tools/knn_probe.py, median over launches)"}
+                      "(tools/%s, median over launches)" % probe[0]}
 
 
 def pcie_leg(device, hptrs, warmup, use_graph=True):
@@ -612,7 +612,7 @@ def node_pattern_leg(device, hptrs, warmup, nframes):
                     "pinned host RAM; frames %d..%d of the headline sequence" % (warmup, total - 1)}
 
 
-def configs4_leg(device, nframes, threads, warmup=3, timing_frames=20, use_graph=True, order=None):
+def configs4_leg(device, nframes, threads, warmup=3, timing_frames=20, use_graph=True, order=None, pmc=False):
     """BASELINE.json configs[4] as a pipeline: synthetic 128-line scans (~200k points; the reference has
     no 128-line ring formula, so the linear beam-model extension pf_odom_set_ring_model(15, -25) bins
     them) against a 2,000,000-point surf map (pfsynth.voxel_map: voxel centroids
@@ -682,6 +682,14 @@ def configs4_leg(device, nframes, threads, warmup=3, timing_frames=20, use_graph
                        "kernel": "k_assoc's exact 5-NN (knn5_team on the 1 m grid of the frame's maps), "
                                  "pf_odom_probe_assoc on the last frame",
                        "queries": nq, "alg_bytes_per_launch": alg, "avg_kernel_ms": round(ms, 5)}
+    if pmc:
+        # the same kernel's fabric bytes per launch, from tools/assoc_probe.py (configs[4]'s state rebuilt in
+        # a child process: a few frames against the same seeded map, so the query set is similar, not equal)
+        t = knn_pmc_traffic(timeout_s=240, probe=("assoc_probe.py", "--frames", "4", "--iters", "5"),
+                            kernel="k_assoc_probe")
+        if t is not None:
+            out["roofline"]["traffic"] = t["bytes_per_launch"]
+            out["roofline"]["traffic_source"] = t["source"]
     surf = q[q[:, 3].view(np.int32) == 1]
     mxyz = od._map(1)[0]
     if surf.shape[0] and mxyz.shape[0]:
@@ -1376,7 +1384,7 @@ def main(argv=None):
         try:
             log("configs4 leg (%s order) ..." % args.configs4_order)
             out["configs4"] = configs4_leg(local_rank, args.configs4_frames, threads, use_graph=graph_mode(args),
-                                           order=args.configs4_order)
+                                           order=args.configs4_order, pmc=not args.no_pmc)
             out["configs4"]["order"] = args.configs4_order
             log("configs4: %s" % out["configs4"])
         except Exception as e:  # report, never hide
