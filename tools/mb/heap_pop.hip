@@ -1979,6 +1979,126 @@ __device__ __forceinline__ unsigned long long step_f41(u32 base, u32 b24, u32 nb
     return blk;
 }
 
+__device__ __forceinline__ unsigned long long step_ep(u32 base, u32 b24, u32 nbb, int& h, u32& ad, u32& lh, u32 vb8, u32 vnbb,
+                                           u32& vx, u32& vy, int spare, u32 vsp8, u32 vzero,
+                                           unsigned long long mine, unsigned long long minew, u32 aq, u32 vrp,
+                                           u32 pq, u32 pq1, u32 lpq1, unsigned long long& bpo,
+                                           unsigned long long& hoo) {
+    int hn;
+    u32 sa, t0, t1, t2, t3, t4, aL, aR, aN;
+    u32 shp, anp;
+    unsigned long long sm, tt, rm, eqm, bpm, hom;
+    asm volatile(
+        "ds_read_b64 v[44:45], %[aq]\n\t"
+        "v_cndmask_b32_e64 %[sa], %[sp8], %[aq], %[minew]\n\t"
+        "v_cndmask_b32_e64 %[ad], %[ad], %[vb8], %[mine]\n\t"
+        "ds_write2_b32 %[sa], %[rp], %[zz] offset1:1\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_cmp_eq_u32_e64 %[eqm], %[pq], %[h]\n\t"
+        "v_cndmask_b32_e64 %[h], %[h], 0, %[mine]\n\t"
+        "v_cndmask_b32_e64 %[lh], %[lh], 0, %[mine]\n\t"
+        "v_sub_u32_e32 %[shp], %[lpq1], %[lh]\n\t"
+        "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+        "v_lshrrev_b32_e64 %[anp], %[shp], %[pq1]\n\t"
+        "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+        "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+        "v_add_u32_e32 %[anp], -1, %[anp]\n\t"
+        "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+        "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+        "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+        "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], v44, %[mine]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], v45, %[mine]\n\t"
+        "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+        "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+        "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+        "v_cmp_eq_u32_e64 %[bpm], %[anp], %[t3]\n\t"
+        "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+        "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+        "s_and_b64 %[hom], %[eqm], %[sm]\n\t"
+        "s_andn2_b64 %[bpm], %[bpm], %[sm]\n\t"
+        : [hn] "=&v"(hn), [h] "+v"(h), [ad] "+v"(ad), [lh] "+v"(lh), [vx] "+v"(vx), [vy] "+v"(vy),
+          [sa] "=&v"(sa), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
+          [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR), [aN] "=&v"(aN),
+          [sm] "=&s"(sm), [tt] "=&s"(tt), [rm] "=&s"(rm), [shp] "=&v"(shp), [anp] "=&v"(anp),
+          [eqm] "=&s"(eqm), [bpm] "=&s"(bpm), [hom] "=&s"(hom)
+        : [pq] "s"(pq), [pq1] "s"(pq1), [lpq1] "s"(lpq1), [sp] "v"(spare), [sp8] "v"(vsp8), [zz] "v"(vzero), [base] "s"(base), [b24] "s"(b24), [nbb] "s"(nbb),
+          [vb8] "v"(vb8), [vnbb] "v"(vnbb), [mine] "s"(mine), [minew] "s"(minew), [aq] "v"(aq), [rp] "v"(vrp)
+        : "memory", "v40", "v41", "v42", "v43", "v44", "v45");
+    h = hn;
+    bpo = bpm;
+    hoo = hom;
+    return sm;
+}
+__device__ __forceinline__ unsigned long long step_fp(u32 base, u32 b24, u32 nbb, int& h, u32& ad, u32& lh,
+                                                     u32 vnbb, u32 vx, u32 vy, int spare, u32 q1, u32 lq1,
+                                                     u32 vbase, unsigned long long& vrp64, u32 aqs, u32& aq,
+                                                     unsigned long long& smo, u32 pq, u32 pq1, u32 lpq1,
+                                                     unsigned long long& bpo, unsigned long long& hoo) {
+    int hn;
+    u32 sh, an, t0, t1, t2, t3, t4, aL, aR, aN;
+    u32 shp, anp;
+    unsigned long long sm, blk, tt, rm, bm, eqm, bpm, hom;
+    asm volatile(
+            "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+            "ds_read_b64 %[rp], %[vb]\n\t"
+            "v_sub_u32_e32 %[sh], %[lq1], %[lh]\n\t"
+            "v_sub_u32_e32 %[shp], %[lpq1], %[lh]\n\t"
+            "v_cmp_eq_u32_e64 %[eqm], %[pq], %[h]\n\t"
+            "v_lshl_add_u32 %[t3], %[h], 1, 1\n\t"
+            "v_lshrrev_b32_e64 %[an], %[sh], %[q1]\n\t"
+            "v_lshrrev_b32_e64 %[anp], %[shp], %[pq1]\n\t"
+            "v_lshl_add_u32 %[t4], %[h], 3, %[base]\n\t"
+            "v_lshl_add_u32 %[aL], %[h], 5, %[b24]\n\t"
+            "v_add_u32_e32 %[an], -1, %[an]\n\t"
+            "v_add_u32_e32 %[anp], -1, %[anp]\n\t"
+            "v_min_u32_e32 %[aL], %[nbb], %[aL]\n\t"
+            "v_add_u32_e32 %[aR], 16, %[aL]\n\t"
+            "v_min_u32_e32 %[aR], %[nbb], %[aR]\n\t"
+            "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+            "v_mov_b32_e32 %[aq], %[aqs]\n\t"
+            "s_waitcnt lgkmcnt(0)\n\t"
+            "v_cmp_ge_u32_e64 %[rm], v43, v41\n\t"
+            "s_nop 1\n\t"
+            "v_cndmask_b32_e64 %[t1], v41, v43, %[rm]\n\t"
+            "v_cndmask_b32_e64 %[t0], v40, v42, %[rm]\n\t"
+            "v_cndmask_b32_e64 %[aN], %[aL], %[aR], %[rm]\n\t"
+            "v_cmp_lt_u32_e64 %[sm], %[t1], %[vy]\n\t"
+            "v_addc_co_u32_e64 %[t3], %[tt], 0, %[t3], %[rm]\n\t"
+            "s_nop 0\n\t"
+            "v_cndmask_b32_e64 %[t0], %[t0], %[vx], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[t2], %[t1], %[vy], %[sm]\n\t"
+            "v_cmp_eq_u32_e64 %[bm], %[an], %[t3]\n\t"
+            "v_cmp_eq_u32_e64 %[bpm], %[anp], %[t3]\n\t"
+            "ds_write2_b32 %[t4], %[t0], %[t2] offset1:1\n\t"
+            "v_cndmask_b32_e64 %[ad], %[aN], %[vnbb], %[sm]\n\t"
+            "v_cndmask_b32_e64 %[hn], %[t3], %[sp], %[sm]\n\t"
+            "s_andn2_b64 %[blk], %[bm], %[sm]\n\t"
+            "s_andn2_b64 %[bpm], %[bpm], %[sm]\n\t"
+            "s_and_b64 %[hom], %[eqm], %[sm]\n\t"
+            : [hn] "=&v"(hn), [ad] "+v"(ad), [lh] "+v"(lh), [sh] "=&v"(sh), [an] "=&v"(an), [t0] "=&v"(t0),
+              [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4), [aL] "=&v"(aL), [aR] "=&v"(aR),
+              [aN] "=&v"(aN), [sm] "=&s"(sm), [blk] "=&s"(blk), [tt] "=&s"(tt), [rm] "=&s"(rm), [bm] "=&s"(bm),
+              [rp] "=&v"(vrp64), [aq] "=&v"(aq), [shp] "=&v"(shp), [anp] "=&v"(anp), [eqm] "=&s"(eqm),
+              [bpm] "=&s"(bpm), [hom] "=&s"(hom)
+            : [pq] "s"(pq), [pq1] "s"(pq1), [lpq1] "s"(lpq1), [h] "v"(h), [vx] "v"(vx), [vy] "v"(vy), [sp] "v"(spare), [base] "s"(base), [b24] "s"(b24),
+              [nbb] "s"(nbb), [vnbb] "v"(vnbb), [q1] "s"(q1), [lq1] "s"(lq1), [vb] "v"(vbase), [aqs] "s"(aqs)
+            : "memory", "v40", "v41", "v42", "v43");
+    h = hn;
+    smo = sm;
+    bpo = bpm;
+    hoo = hom;
+    return blk;
+}
+
 // v41 (round 6): v40's steps plus speculative starts (one pending pop at a time; the protocol of
 // pops_spec, checked step by step by /tmp-side simulation): a start blocked by an older hole at or above
 // its last element q (q >= 64, so q is a leaf of every older pop's heap) takes H[q] now, writes its output
@@ -2113,6 +2233,219 @@ __device__ int pops_v41(uint2* H, int n, int npops) {
             hold = false;
             if (mine) ydep = 1;
             else if (!((fz >> ((nxt - 1) & 63)) & 1ull)) ++ydep;
+            ++steps;
+        }
+        if (nxt >= npops && !pact && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+// v42: v41 with the pending phase's checks inside the assembly steps (step_ep / step_fp: the release test
+// against the pending q's ancestor at the new hole's level and the hand-off mask, in the loads' shadow), so
+// a step with a pending pop costs one compare and two SALU more than v40's; frozen phases and transitions
+// run v41's general step.
+__device__ __forceinline__ unsigned long long uni64(unsigned long long x) {   // a wave-uniform value in SGPRs
+    return ((unsigned long long)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(x >> 32)) << 32) |
+           (u32)__builtin_amdgcn_readfirstlane((int)(u32)x);
+}
+__device__ int pops_v42(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    const u32 b24 = base + 24u;
+    u32 vb8 = base + 8u, vnbb = nbb, vbase = base, vsp8 = base + 8u * (u32)spare, vzero = 0u;
+    asm volatile("" : "+v"(vb8), "+v"(vnbb), "+v"(vbase), "+v"(vsp8), "+v"(vzero));
+    int nxt = 0;
+    int h = spare;
+    u32 ad = nbb, lh = 0u;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0, sm = 0, bpm = 0, hom = 0;
+    unsigned long long vrp64 = ((unsigned long long)H[0].y << 32) | H[0].x;
+    u32 aq = base + 8u * (u32)last;
+    int steps = 0, sub = 0;
+    bool pact = false, pstall = false, hold = false, rel = false, fzprev = false;
+    int pq = 0, plane = 0, ydep = 2;
+    u32 prp = 0u, prk = 0u, pq1 = 0u, lpq1 = 0u;
+    unsigned long long pold = 0;
+    unsigned long long zmask = 0;
+    asm volatile("" : "+s"(zmask));                // an opaque zero write mask (never an inline constant)
+    for (;;) {
+        if (!pact && !pstall && !hold && !fzprev && ydep >= 2 && sub == 0) {
+            // no pending pop: v40's pairs
+            bool spec = false;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (blk != 0 && nxt < npops && last - nxt >= 64) { spec = true; break; }
+                const bool start = nxt < npops && blk == 0;
+                const unsigned long long mine = start ? (1ull << (nxt & 63)) : 0ull;
+                step_e41(base, b24, nbb, h, ad, lh, vb8, vnbb, vx, vy, spare, vsp8, vzero, uni64(mine), uni64(mine), aq, (u32)vrp64);
+                nxt += start ? 1 : 0;
+                const u32 q1 = (u32)(last - nxt + 1);
+                blk = step_f41(base, b24, nbb, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)), vbase, vrp64,
+                               base + 8u * (u32)(last - nxt), aq, sm);
+                steps += 2;
+            }
+            if (!spec) {
+                if (nxt >= npops && __ballot(h != spare) == 0) break;
+                continue;
+            }
+            // the blocked start goes ahead, pending
+            const int q = last - nxt;
+            const int L = nxt & 63;
+            const unsigned long long mine = 1ull << L;
+            pact = true;
+            rel = false;
+            pq = q;
+            pq1 = (u32)q + 1u;
+            lpq1 = (u32)hlev(q) - 1u;
+            plane = L;
+            prp = (u32)__builtin_amdgcn_readfirstlane((int)(u32)vrp64);
+            prk = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(vrp64 >> 32));
+            pold = __ballot(h != spare) & ~mine;
+            const int hprev = h;
+            sm = step_ep(base, b24, nbb, h, ad, lh, vb8, vnbb, vx, vy, spare, vsp8, vzero, uni64(mine), uni64(zmask), aq, (u32)vrp64,
+                         (u32)pq, pq1, lpq1, bpm, hom);
+            ++nxt;
+            ydep = 1;
+            sub = 1;
+            ++steps;
+            if ((sm >> plane) & 1ull) {                          // stopped at the root at once: undo, freeze
+                if (l == plane) {
+                    H[0] = make_uint2(prp, prk);
+                    h = 0;
+                    ad = base + 8u < nbb ? base + 8u : nbb;
+                    lh = 0u;
+                }
+                pstall = true;
+            }
+            if (hom & pold) {
+                const int src = __ffsll((long long)(hom & pold)) - 1;
+                const u32 nx = (u32)__builtin_amdgcn_readlane((int)vx, src), ny = (u32)__builtin_amdgcn_readlane((int)vy, src);
+                if (l == plane) { vx = nx; vy = ny; }
+            }
+            rel = (bpm & pold) == 0;
+            (void)hprev;
+            continue;
+        }
+        if (pact && !pstall && !hold && !fzprev) {
+            // a pending pop, nothing frozen: the pending-aware steps
+            if (rel) {
+                if (l == plane) H[pq] = make_uint2(prp, 0u);
+                pact = false;
+                rel = false;
+                continue;
+            }
+            unsigned long long mine = 0;
+            if (sub == 0 && nxt < npops && blk == 0 && ydep >= 2) mine = 1ull << (nxt & 63);
+            pold &= ~mine;
+            const int hprev = h;
+            if (sub == 0) {
+                sm = step_ep(base, b24, nbb, h, ad, lh, vb8, vnbb, vx, vy, spare, vsp8, vzero, uni64(mine), uni64(mine), aq, (u32)vrp64,
+                             (u32)pq, pq1, lpq1, bpm, hom);
+                nxt += mine ? 1 : 0;
+            } else {
+                const u32 q1 = (u32)(last - nxt + 1);
+                blk = step_fp(base, b24, nbb, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)), vbase, vrp64,
+                              base + 8u * (u32)(last - nxt), aq, sm, (u32)pq, pq1, lpq1, bpm, hom);
+            }
+            ydep = mine ? 1 : ydep + 1;
+            sub ^= 1;
+            ++steps;
+            if ((sm >> plane) & 1ull) {                          // the pending pop would stop: undo, freeze
+                const int hs = __builtin_amdgcn_readlane(hprev, plane);
+                if (l == plane) {
+                    H[hs] = hs > 0 ? H[(hs - 1) >> 1] : make_uint2(prp, prk);
+                    h = hs;
+                    const u32 a0 = base + 8u + 16u * (u32)hs;
+                    ad = a0 < nbb ? a0 : nbb;
+                    lh = (u32)hlev(hs);
+                }
+                pstall = true;
+            }
+            if (hom & pold) {                                    // an older pop ended at q
+                const int src = __ffsll((long long)(hom & pold)) - 1;
+                const u32 nx = (u32)__builtin_amdgcn_readlane((int)vx, src), ny = (u32)__builtin_amdgcn_readlane((int)vy, src);
+                if (l == plane) { vx = nx; vy = ny; }
+            }
+            rel = (bpm & pold) == 0;
+            continue;
+        }
+        // general step (frozen lanes, hold, transitions): v41's
+        {
+            if (pact && rel) {
+                if (l == plane) H[pq] = make_uint2(prp, 0u);
+                pact = false;
+                rel = false;
+                if (pstall) { pstall = false; hold = true; }
+            }
+            unsigned long long fz = 0;
+            if (pstall || hold) {
+                fz = __ballot(h != spare) & ~pold;
+                if (hold) fz &= ~(1ull << plane);
+            }
+            unsigned long long mine = 0, minew = 0;
+            if (sub == 0 && nxt < npops && !pstall && !hold && !fzprev && ydep >= 2) {
+                const int q = last - nxt;
+                const int L = nxt & 63;
+                if (blk == 0) {
+                    mine = minew = 1ull << L;
+                } else if (!pact && q >= 64) {
+                    mine = 1ull << L;
+                    pact = true;
+                    rel = false;
+                    pq = q;
+                    pq1 = (u32)q + 1u;
+                    lpq1 = (u32)hlev(q) - 1u;
+                    plane = L;
+                    prp = (u32)__builtin_amdgcn_readfirstlane((int)(u32)vrp64);
+                    prk = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(vrp64 >> 32));
+                    pold = __ballot(h != spare);
+                }
+                pold &= ~mine;
+            }
+            int sh_ = h;
+            u32 sad = ad, slh = lh;
+            if (fz && ((fz >> l) & 1ull)) { h = spare; ad = nbb; }
+            const int hold_h = h;
+            if (sub == 0) {
+                sm = step_e41(base, b24, nbb, h, ad, lh, vb8, vnbb, vx, vy, spare, vsp8, vzero, uni64(mine), uni64(minew), aq, (u32)vrp64);
+                nxt += mine ? 1 : 0;
+            } else {
+                const u32 q1 = (u32)(last - nxt + 1);
+                blk = step_f41(base, b24, nbb, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)), vbase, vrp64,
+                               base + 8u * (u32)(last - nxt), aq, sm);
+            }
+            if (fz && ((fz >> l) & 1ull)) { h = sh_; ad = sad; lh = slh; }
+            fzprev = fz != 0;
+            if (pact) {
+                if (!pstall && ((sm >> plane) & 1ull) && !((fz >> plane) & 1ull)) {
+                    const int hs = __builtin_amdgcn_readlane(hold_h, plane);
+                    if (l == plane) {
+                        H[hs] = hs > 0 ? H[(hs - 1) >> 1] : make_uint2(prp, prk);
+                        h = hs;
+                        const u32 a0 = base + 8u + 16u * (u32)hs;
+                        ad = a0 < nbb ? a0 : nbb;
+                        lh = (u32)hlev(hs);
+                    }
+                    pstall = true;
+                }
+                const unsigned long long ho = __ballot(hold_h == pq) & sm & pold & ~fz;
+                if (ho) {
+                    const int src = __ffsll((long long)ho) - 1;
+                    const u32 nx = (u32)__builtin_amdgcn_readlane((int)vx, src), ny = (u32)__builtin_amdgcn_readlane((int)vy, src);
+                    if (l == plane) { vx = nx; vy = ny; }
+                }
+                const u32 anp = (pq1 >> (lpq1 + 1u - lh)) - 1u;
+                rel = (__ballot(lh <= lpq1 + 1u && anp == (u32)h) & pold) == 0;
+            }
+            hold = false;
+            if (mine) ydep = 1;
+            else if (!((fz >> ((nxt - 1) & 63)) & 1ull)) ++ydep;
+            sub ^= 1;
             ++steps;
         }
         if (nxt >= npops && !pact && __ballot(h != spare) == 0) break;
@@ -2471,7 +2804,7 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
     if (t < 64 && n >= 2 && npops > 0) {
         const u64 r0 = __builtin_amdgcn_s_memrealtime();
         const u64 t0 = __builtin_amdgcn_s_memtime();
-        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : V == 23 ? (u64)pops_v28<4>(H, n, npops) : V == 24 ? (u64)pops_v29<4>(H, n, npops) : V == 25 ? (u64)pops_v30<4, true, false>(H, n, npops) : V == 26 ? (u64)pops_v30<4, false, true>(H, n, npops) : V == 27 ? (u64)pops_v30<4, true, true>(H, n, npops) : V == 28 ? (u64)pops_v33<4, false, false>(H, n, npops) : V == 29 ? (u64)pops_v33<4, true, true>(H, n, npops) : V == 30 ? (u64)pops_v36<4, false, false>(H, n, npops) : V == 31 ? (u64)pops_v36<4, true, true>(H, n, npops) : V == 32 ? (u64)pops_v38<4>(H, n, npops) : V == 33 ? (u64)pops_v39<4, false>(H, n, npops) : V == 34 ? (u64)pops_v39<4, true>(H, n, npops) : V == 35 ? pops_spec<1>(H, n, npops) : V == 36 ? pops_spec<2>(H, n, npops) : V == 37 ? pops_spec<4>(H, n, npops) : (u64)pops_v41(H, n, npops);
+        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : V == 23 ? (u64)pops_v28<4>(H, n, npops) : V == 24 ? (u64)pops_v29<4>(H, n, npops) : V == 25 ? (u64)pops_v30<4, true, false>(H, n, npops) : V == 26 ? (u64)pops_v30<4, false, true>(H, n, npops) : V == 27 ? (u64)pops_v30<4, true, true>(H, n, npops) : V == 28 ? (u64)pops_v33<4, false, false>(H, n, npops) : V == 29 ? (u64)pops_v33<4, true, true>(H, n, npops) : V == 30 ? (u64)pops_v36<4, false, false>(H, n, npops) : V == 31 ? (u64)pops_v36<4, true, true>(H, n, npops) : V == 32 ? (u64)pops_v38<4>(H, n, npops) : V == 33 ? (u64)pops_v39<4, false>(H, n, npops) : V == 34 ? (u64)pops_v39<4, true>(H, n, npops) : V == 35 ? pops_spec<1>(H, n, npops) : V == 36 ? pops_spec<2>(H, n, npops) : V == 37 ? pops_spec<4>(H, n, npops) : V == 38 ? (u64)pops_v41(H, n, npops) : (u64)pops_v42(H, n, npops);
         const u64 t1 = __builtin_amdgcn_s_memtime();
         const u64 r1 = __builtin_amdgcn_s_memrealtime();
         if (t == 0) {
@@ -2828,7 +3161,8 @@ int main(int argc, char** argv) {
             else if (v == 35) hipLaunchKernelGGL(k_heap<35>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 36) hipLaunchKernelGGL(k_heap<36>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 37) hipLaunchKernelGGL(k_heap<37>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
-            else hipLaunchKernelGGL(k_heap<38>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 38) hipLaunchKernelGGL(k_heap<38>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else hipLaunchKernelGGL(k_heap<39>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             CK(hipDeviceSynchronize());
         }
         CK(hipMemcpy(out.data(), d_kv, out.size() * 8, hipMemcpyDeviceToHost));
