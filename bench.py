@@ -283,6 +283,7 @@ def run_kitti11(rank, local_rank, world, warmup, threads, use_graph, barrier, co
             ptrs += [(db.ptr + i * stride, int(counts[i])) for i in range(buf.shape[0])]
             bufs.append(db)
         seqs.append((ptrs, bufs))
+        log("kitti11: sequence %02d staged in HBM (%d frames)" % (sq, len(ptrs)))   # progress on a long staging
     nthreads = max(1, min(concurrent, len(seqs)))
     handles = []
     for _ in range(nthreads):

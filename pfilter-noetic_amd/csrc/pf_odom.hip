@@ -3515,7 +3515,12 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
         aux.s = o.tie_aux ? o.stream_bx : nullptr;
         aux.fork = o.ev_bx_fork;
         aux.join = o.ev_bx_join;
-        aux.hs = o.tie_hs ? o.stream_bx : nullptr;
+        // the side-stream radix route only for eager launches: captured into stage B's graph (several
+        // handles, PF_GRAPH_AUTO) the fork / join measured slower than the route on the stage's own stream
+        // (configs[4] 173 against 281 frames/s in the full bench), so a captured stage B keeps it in line
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        (void)hipStreamIsCapturing(s, &cap);
+        aux.hs = o.tie_hs && cap == hipStreamCaptureStatusNone ? o.stream_bx : nullptr;
         tie_sort(*o.tie_b, o.keys, o.vals, TieClasses{cnt, C_M, C_DS, nc}, o.prim.err, s,
                  std::max(tie_levels_for(*o.tie_b, o.tie_hint), PF_TIE_LEVELS_B), dt.key ? o.dep_free : nullptr,
                  &aux);
