@@ -1384,9 +1384,16 @@ def main(argv=None):
     if world == 1 and not stub and args.configs4_frames > 0:
         try:
             log("configs4 leg (%s order) ..." % args.configs4_order)
-            out["configs4"] = configs4_leg(local_rank, args.configs4_frames, threads, use_graph=graph_mode(args),
+            # PF_GRAPH_AUTO replays stage B's graph only while a process holds several handles; here the
+            # headline's handle is still alive (the CPU baseline syncs from it later), which a configs[4]
+            # user's single handle would not have: run the leg as AUTO runs one handle (stage A's graph,
+            # stage B eager, its radix route on the side stream)
+            g4 = graph_mode(args)
+            g4 = 1 if g4 == 4 else g4
+            out["configs4"] = configs4_leg(local_rank, args.configs4_frames, threads, use_graph=g4,
                                            order=args.configs4_order, pmc=not args.no_pmc)
             out["configs4"]["order"] = args.configs4_order
+            out["configs4"]["graph_mode"] = g4
             log("configs4: %s" % out["configs4"])
         except Exception as e:  # report, never hide
             log("configs4 leg failed: %r" % (e,))
