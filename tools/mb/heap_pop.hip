@@ -2453,9 +2453,8 @@ __device__ int pops_v42(uint2* H, int n, int npops) {
     }
     return steps;
 }
-// v43 (unfinished, round 6: NOT exact yet -- DIFF on tie-heavy and ascending inputs -- and no faster, 600-900
-// cycles per step; kept as the starting point of the hand-written pending phase):
-// v42 with the pending phase as one hand-written loop (pend_loop): pairs of v42's pending-aware steps
+// v43 (round 6): exact once the release is taken before re-entering the loop, but 450-820 cycles per step (it
+// returns to C++ at every speculative start and release). v42 with the pending phase as one hand-written loop (pend_loop): pairs of v42's pending-aware steps
 // with the start decision, the next q's scalars and the three checks (the pending pop stopped, an older
 // pop ended at q, no older hole covers q any more) in SALU between them; any of the three leaves the loop
 // (why = 1 / 2 / 3, after step A (sub 0) or B (sub 1)) for the C++ handlers. Fixed temporaries v46..v59,
@@ -2713,6 +2712,12 @@ __device__ int pops_v43(uint2* H, int n, int npops) {
             continue;
         }
         if (pact && !pstall && !hold && !fzprev) {
+            if (rel) {                                           // the held output, now that no older hole covers q
+                if (l == plane) H[pq] = make_uint2(prp, 0u);
+                pact = false;
+                rel = false;
+                continue;
+            }
             // a pending pop, nothing frozen: the hand-written loop until a check fires
             int why = 0, sub2 = sub, phole = 0;
             nxt = __builtin_amdgcn_readfirstlane(nxt);
@@ -2778,6 +2783,379 @@ __device__ int pops_v43(uint2* H, int n, int npops) {
                     pq = q;
                     pq1 = (u32)q + 1u;
                     lpq1 = (u32)hlev(q) - 1u;
+                    plane = L;
+                    prp = (u32)__builtin_amdgcn_readfirstlane((int)(u32)vrp64);
+                    prk = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(vrp64 >> 32));
+                    pold = __ballot(h != spare);
+                }
+                pold &= ~mine;
+            }
+            int sh_ = h;
+            u32 sad = ad, slh = lh;
+            if (fz && ((fz >> l) & 1ull)) { h = spare; ad = nbb; }
+            const int hold_h = h;
+            if (sub == 0) {
+                sm = step_e41(base, b24, nbb, h, ad, lh, vb8, vnbb, vx, vy, spare, vsp8, vzero, uni64(mine), uni64(minew), aq, (u32)vrp64);
+                nxt += mine ? 1 : 0;
+            } else {
+                const u32 q1 = (u32)(last - nxt + 1);
+                blk = step_f41(base, b24, nbb, h, ad, lh, vnbb, vx, vy, spare, q1, (u32)(30 - __clz(q1)), vbase, vrp64,
+                               base + 8u * (u32)(last - nxt), aq, sm);
+            }
+            if (fz && ((fz >> l) & 1ull)) { h = sh_; ad = sad; lh = slh; }
+            fzprev = fz != 0;
+            if (pact) {
+                if (!pstall && ((sm >> plane) & 1ull) && !((fz >> plane) & 1ull)) {
+                    const int hs = __builtin_amdgcn_readlane(hold_h, plane);
+                    if (l == plane) {
+                        H[hs] = hs > 0 ? H[(hs - 1) >> 1] : make_uint2(prp, prk);
+                        h = hs;
+                        const u32 a0 = base + 8u + 16u * (u32)hs;
+                        ad = a0 < nbb ? a0 : nbb;
+                        lh = (u32)hlev(hs);
+                    }
+                    pstall = true;
+                }
+                const unsigned long long ho = __ballot(hold_h == pq) & sm & pold & ~fz;
+                if (ho) {
+                    const int src = __ffsll((long long)ho) - 1;
+                    const u32 nx = (u32)__builtin_amdgcn_readlane((int)vx, src), ny = (u32)__builtin_amdgcn_readlane((int)vy, src);
+                    if (l == plane) { vx = nx; vy = ny; }
+                }
+                const u32 anp = (pq1 >> (lpq1 + 1u - lh)) - 1u;
+                rel = (__ballot(lh <= lpq1 + 1u && anp == (u32)h) & pold) == 0;
+            }
+            hold = false;
+            if (mine) ydep = 1;
+            else if (!((fz >> ((nxt - 1) & 63)) & 1ull)) ++ydep;
+            sub ^= 1;
+            ++steps;
+        }
+        if (nxt >= npops && !pact && __ballot(h != spare) == 0) break;
+        if (steps > 64 * n + 1000) break;                        // benchmark guard
+    }
+    return steps;
+}
+// v44 (round 6): exact on every case, 320-380 cycles per step (profiles/r06/heap_pop_mb_v44_*.txt): the whole engine in one hand-written loop (eng_loop): v40's starts, speculative starts, the held
+// output's release, and the pending checks, all between the assembly steps; it leaves to C++ only when the
+// pending pop would stop (why 1: undo + frozen steps, v41's general step), when an older pop ended at the
+// pending q (why 2: the value hand-off), and when every pop is done (why 0).
+__device__ __forceinline__ void eng_loop(u32 base, u32 b24, u32 nbb, u32 n, u32 npops, int& h, u32& ad, u32& lh,
+                                         u32 vb8, u32 vnbb, u32& vx, u32& vy, int spare, u32 vsp8, u32 vzero,
+                                         u32& aq, u32& rplo, u32& rphi, u32& prp, u32& prk, u32 vbase, int& nxt,
+                                         unsigned long long& blk, u32& pact, u32& rel, u32& pq, u32& pq1, u32& lpq1,
+                                         u32& pqa, unsigned long long& pbit, unsigned long long& pold, int sub_in,
+                                         int& why, int& sub_out, unsigned long long& sm, unsigned long long& bpm,
+                                         unsigned long long& hom, int& steps, int& hold) {
+    u32 hn = 0;
+    int sub = sub_in;
+    asm volatile(
+        "v_mov_b32_e32 v60, %[rplo]\n\t"
+        "v_mov_b32_e32 v61, %[rphi]\n\t"
+        "s_mov_b32 %[why], 0\n\t"
+        "s_cmp_eq_u32 %[sub], 1\n\t"
+        "s_cbranch_scc0 .Le_A%=\n\t"
+        "s_sub_u32 s94, %[n], %[nxt]\n\t"
+        "s_flbit_i32_b32 s95, s94\n\t"
+        "s_sub_u32 s95, 30, s95\n\t"
+        "s_sub_u32 s96, s94, 1\n\t"
+        "s_lshl_b32 s96, s96, 3\n\t"
+        "s_add_u32 s96, s96, %[base]\n\t"
+        "s_branch .Le_B%=\n"
+        ".Le_A%=:\n\t"
+        // the held output, once released
+        "s_cmp_eq_u32 %[rel], 0\n\t"
+        "s_cbranch_scc1 .Le_A0%=\n\t"
+        "v_mov_b32_e32 v59, %[pqa]\n\t"
+        "v_cndmask_b32_e64 v59, %[sp8], v59, %[pbit]\n\t"
+        "ds_write2_b32 v59, %[prp], %[zz] offset1:1\n\t"
+        "s_mov_b32 %[pact], 0\n\t"
+        "s_mov_b32 %[rel], 0\n"
+        ".Le_A0%=:\n\t"
+        // start decision: s[90:91] = mine (value taken), s[86:87] = minew (output written)
+        "s_and_b32 s97, %[nxt], 63\n\t"
+        "s_lshl_b64 s[88:89], 1, s97\n\t"
+        "s_cmp_lt_u32 %[nxt], %[npops]\n\t"
+        "s_cselect_b64 s[88:89], s[88:89], 0\n\t"
+        "s_cmp_eq_u64 %[blk], 0\n\t"
+        "s_cselect_b64 s[90:91], s[88:89], 0\n\t"
+        "s_mov_b64 s[86:87], s[90:91]\n\t"
+        "s_cbranch_scc1 .Le_A3%=\n\t"               // unblocked: a plain start (or none left)
+        "s_cmp_lg_u32 %[pact], 0\n\t"                // blocked: speculative if none pending, q >= 64
+        "s_cbranch_scc1 .Le_A2%=\n\t"
+        "s_sub_u32 s94, %[n], %[nxt]\n\t"
+        "s_cmp_lt_u32 s94, 65\n\t"
+        "s_cbranch_scc1 .Le_A2%=\n\t"
+        "s_cmp_eq_u64 s[88:89], 0\n\t"
+        "s_cbranch_scc1 .Le_A2%=\n\t"
+        "s_mov_b64 s[90:91], s[88:89]\n\t"
+        "s_mov_b32 %[pact], 1\n\t"
+        "s_mov_b32 %[rel], 0\n\t"
+        "s_sub_u32 %[pq], s94, 1\n\t"
+        "s_mov_b32 %[pq1], s94\n\t"
+        "s_flbit_i32_b32 s95, s94\n\t"
+        "s_sub_u32 %[lpq1], 30, s95\n\t"
+        "s_lshl_b32 %[pqa], %[pq], 3\n\t"
+        "s_add_u32 %[pqa], %[pqa], %[base]\n\t"
+        "s_mov_b64 %[pbit], s[88:89]\n\t"
+        "v_cmp_ne_u32_e64 %[pold], %[sp], %[h]\n\t"
+        "v_mov_b32_e32 %[prp], v60\n\t"
+        "v_mov_b32_e32 %[prk], v61\n\t"
+        "s_nop 1\n"
+        ".Le_A3%=:\n\t"
+        "s_andn2_b64 %[pold], %[pold], s[90:91]\n\t"
+        "s_cmp_lg_u64 s[90:91], 0\n\t"
+        "s_addc_u32 %[nxt], %[nxt], 0\n"
+        ".Le_A2%=:\n\t"
+        // step A (step_ep; mine s[90:91], minew s[86:87])
+        "ds_read_b64 v[44:45], %[aq]\n\t"
+        "v_cndmask_b32_e64 v46, %[sp8], %[aq], s[86:87]\n\t"
+        "v_cndmask_b32_e64 %[ad], %[ad], %[vb8], s[90:91]\n\t"
+        "ds_write2_b32 v46, v60, %[zz] offset1:1\n\t"
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "v_cmp_eq_u32_e64 s[92:93], %[pq], %[h]\n\t"
+        "v_cndmask_b32_e64 %[h], %[h], 0, s[90:91]\n\t"
+        "v_cndmask_b32_e64 %[lh], %[lh], 0, s[90:91]\n\t"
+        "v_sub_u32_e32 v47, %[lpq1], %[lh]\n\t"
+        "v_lshl_add_u32 v48, %[h], 1, 1\n\t"
+        "v_lshrrev_b32_e64 v49, v47, %[pq1]\n\t"
+        "v_lshl_add_u32 v50, %[h], 3, %[base]\n\t"
+        "v_lshl_add_u32 v51, %[h], 5, %[b24]\n\t"
+        "v_add_u32_e32 v49, -1, v49\n\t"
+        "v_min_u32_e32 v51, %[nbb], v51\n\t"
+        "v_add_u32_e32 v52, 16, v51\n\t"
+        "v_min_u32_e32 v52, %[nbb], v52\n\t"
+        "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+        "s_sub_u32 s94, %[n], %[nxt]\n\t"            // the next step's q1, lq1, aqs
+        "s_flbit_i32_b32 s95, s94\n\t"
+        "s_sub_u32 s95, 30, s95\n\t"
+        "s_sub_u32 s96, s94, 1\n\t"
+        "s_lshl_b32 s96, s96, 3\n\t"
+        "s_add_u32 s96, s96, %[base]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 s[98:99], v43, v41\n\t"
+        "v_cndmask_b32_e64 %[vx], %[vx], v44, s[90:91]\n\t"
+        "v_cndmask_b32_e64 %[vy], %[vy], v45, s[90:91]\n\t"
+        "v_cndmask_b32_e64 v53, v41, v43, s[98:99]\n\t"
+        "v_cndmask_b32_e64 v54, v40, v42, s[98:99]\n\t"
+        "v_cndmask_b32_e64 v55, v51, v52, s[98:99]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], v53, %[vy]\n\t"
+        "v_addc_co_u32_e64 v48, s[100:101], 0, v48, s[98:99]\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_e64 v54, v54, %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 v56, v53, %[vy], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[ad], v55, %[vnbb], %[sm]\n\t"
+        "v_cmp_eq_u32_e64 %[bpm], v49, v48\n\t"
+        "ds_write2_b32 v50, v54, v56 offset1:1\n\t"
+        "v_cndmask_b32_e64 %[hn], v48, %[sp], %[sm]\n\t"
+        "s_and_b64 %[hom], s[92:93], %[sm]\n\t"
+        "s_andn2_b64 %[bpm], %[bpm], %[sm]\n\t"
+        "s_add_u32 %[steps], %[steps], 1\n\t"
+        "s_cmp_eq_u32 %[pact], 0\n\t"
+        "s_cbranch_scc1 .Le_An%=\n\t"
+        "s_and_b64 s[88:89], %[sm], %[pbit]\n\t"
+        "s_and_b64 s[92:93], %[hom], %[pold]\n\t"
+        "s_or_b64 s[88:89], s[88:89], s[92:93]\n\t"
+        "s_cmp_lg_u64 s[88:89], 0\n\t"
+        "s_cbranch_scc1 .Le_xA%=\n\t"
+        "s_and_b64 s[88:89], %[bpm], %[pold]\n\t"
+        "s_cmp_eq_u64 s[88:89], 0\n\t"
+        "s_cselect_b32 %[rel], 1, 0\n"
+        ".Le_An%=:\n\t"
+        "v_mov_b32_e32 %[h], %[hn]\n"
+        ".Le_B%=:\n\t"
+        "s_cmp_eq_u32 %[rel], 0\n\t"
+        "s_cbranch_scc1 .Le_B0%=\n\t"
+        "v_mov_b32_e32 v59, %[pqa]\n\t"
+        "v_cndmask_b32_e64 v59, %[sp8], v59, %[pbit]\n\t"
+        "ds_write2_b32 v59, %[prp], %[zz] offset1:1\n\t"
+        "s_mov_b32 %[pact], 0\n\t"
+        "s_mov_b32 %[rel], 0\n"
+        ".Le_B0%=:\n\t"
+        // step B (step_fp)
+        "ds_read2_b64 v[40:43], %[ad] offset1:1\n\t"
+        "ds_read_b64 v[60:61], %[vb]\n\t"
+        "v_sub_u32_e32 v57, s95, %[lh]\n\t"
+        "v_sub_u32_e32 v47, %[lpq1], %[lh]\n\t"
+        "v_cmp_eq_u32_e64 s[92:93], %[pq], %[h]\n\t"
+        "v_lshl_add_u32 v48, %[h], 1, 1\n\t"
+        "v_lshrrev_b32_e64 v58, v57, s94\n\t"
+        "v_lshrrev_b32_e64 v49, v47, %[pq1]\n\t"
+        "v_lshl_add_u32 v50, %[h], 3, %[base]\n\t"
+        "v_lshl_add_u32 v51, %[h], 5, %[b24]\n\t"
+        "v_add_u32_e32 v58, -1, v58\n\t"
+        "v_add_u32_e32 v49, -1, v49\n\t"
+        "v_min_u32_e32 v51, %[nbb], v51\n\t"
+        "v_add_u32_e32 v52, 16, v51\n\t"
+        "v_min_u32_e32 v52, %[nbb], v52\n\t"
+        "v_add_u32_e32 %[lh], 1, %[lh]\n\t"
+        "v_mov_b32_e32 %[aq], s96\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 s[98:99], v43, v41\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 v53, v41, v43, s[98:99]\n\t"
+        "v_cndmask_b32_e64 v54, v40, v42, s[98:99]\n\t"
+        "v_cndmask_b32_e64 v55, v51, v52, s[98:99]\n\t"
+        "v_cmp_lt_u32_e64 %[sm], v53, %[vy]\n\t"
+        "v_addc_co_u32_e64 v48, s[100:101], 0, v48, s[98:99]\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_e64 v54, v54, %[vx], %[sm]\n\t"
+        "v_cndmask_b32_e64 v56, v53, %[vy], %[sm]\n\t"
+        "v_cmp_eq_u32_e64 s[90:91], v58, v48\n\t"
+        "v_cmp_eq_u32_e64 %[bpm], v49, v48\n\t"
+        "ds_write2_b32 v50, v54, v56 offset1:1\n\t"
+        "v_cndmask_b32_e64 %[ad], v55, %[vnbb], %[sm]\n\t"
+        "v_cndmask_b32_e64 %[hn], v48, %[sp], %[sm]\n\t"
+        "s_andn2_b64 %[blk], s[90:91], %[sm]\n\t"
+        "s_andn2_b64 %[bpm], %[bpm], %[sm]\n\t"
+        "s_and_b64 %[hom], s[92:93], %[sm]\n\t"
+        "s_add_u32 %[steps], %[steps], 1\n\t"
+        "s_cmp_eq_u32 %[pact], 0\n\t"
+        "s_cbranch_scc1 .Le_Bn%=\n\t"
+        "s_and_b64 s[88:89], %[sm], %[pbit]\n\t"
+        "s_and_b64 s[92:93], %[hom], %[pold]\n\t"
+        "s_or_b64 s[88:89], s[88:89], s[92:93]\n\t"
+        "s_cmp_lg_u64 s[88:89], 0\n\t"
+        "s_cbranch_scc1 .Le_xB%=\n\t"
+        "s_and_b64 s[88:89], %[bpm], %[pold]\n\t"
+        "s_cmp_eq_u64 s[88:89], 0\n\t"
+        "s_cselect_b32 %[rel], 1, 0\n"
+        ".Le_Bn%=:\n\t"
+        "v_mov_b32_e32 %[h], %[hn]\n\t"
+        // done: no start left, none pending, no lane in flight
+        "s_cmp_lt_u32 %[nxt], %[npops]\n\t"
+        "s_cbranch_scc1 .Le_A%=\n\t"
+        "s_cmp_eq_u32 %[pact], 0\n\t"
+        "s_cbranch_scc0 .Le_A%=\n\t"
+        "v_cmp_ne_u32_e64 s[88:89], %[sp], %[h]\n\t"
+        "s_nop 1\n\t"
+        "s_cmp_eq_u64 s[88:89], 0\n\t"
+        "s_cbranch_scc0 .Le_A%=\n\t"
+        "s_branch .Le_end%=\n"
+        ".Le_xA%=:\n\t"
+        "s_mov_b32 %[sub], 0\n\t"
+        "s_mov_b32 %[why], 2\n\t"
+        "s_branch .Le_end%=\n"
+        ".Le_xB%=:\n\t"
+        "s_mov_b32 %[sub], 1\n\t"
+        "s_mov_b32 %[why], 2\n"
+        ".Le_end%=:\n\t"
+        "v_mov_b32_e32 %[rplo], v60\n\t"
+        "v_mov_b32_e32 %[rphi], v61\n\t"
+        : [h] "+v"(h), [hn] "+v"(hn), [ad] "+v"(ad), [lh] "+v"(lh), [vx] "+v"(vx), [vy] "+v"(vy), [aq] "+v"(aq),
+          [rplo] "+v"(rplo), [rphi] "+v"(rphi), [prp] "+v"(prp), [prk] "+v"(prk), [nxt] "+s"(nxt), [blk] "+s"(blk),
+          [pact] "+s"(pact), [rel] "+s"(rel), [pq] "+s"(pq), [pq1] "+s"(pq1), [lpq1] "+s"(lpq1), [pqa] "+s"(pqa),
+          [pbit] "+s"(pbit), [pold] "+s"(pold), [sub] "+s"(sub), [why] "=&s"(why), [sm] "=&s"(sm), [bpm] "=&s"(bpm),
+          [hom] "=&s"(hom), [steps] "+s"(steps)
+        : [base] "s"(base), [b24] "s"(b24), [nbb] "s"(nbb), [n] "s"(n), [npops] "s"(npops), [vb8] "v"(vb8),
+          [vnbb] "v"(vnbb), [sp] "v"(spare), [sp8] "v"(vsp8), [zz] "v"(vzero), [vb] "v"(vbase)
+        : "memory", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52",
+          "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "s88", "s89", "s90", "s91", "s92", "s93",
+          "s94", "s95", "s96", "s97", "s98", "s99", "s100", "s101", "s86", "s87");
+    hold = h;                   // the step that fired (why 2: the pending pop stopped or an older pop ended at q)
+    if (why != 0) h = (int)hn;
+    sub_out = sub;
+}
+__device__ int pops_v44(uint2* H, int n, int npops) {
+    n = __builtin_amdgcn_readfirstlane(n);
+    npops = __builtin_amdgcn_readfirstlane(npops);
+    const int l = lane_id();
+    const int last = n - 1;
+    const int spare = n + 2 + l;
+    const u32 base = (u32)(size_t)H;
+    const u32 nbb = base + (u32)n * 8u;
+    const u32 b24 = base + 24u;
+    u32 vb8 = base + 8u, vnbb = nbb, vbase = base, vsp8 = base + 8u * (u32)spare, vzero = 0u;
+    asm volatile("" : "+v"(vb8), "+v"(vnbb), "+v"(vbase), "+v"(vsp8), "+v"(vzero));
+    int nxt = 0;
+    int h = spare;
+    u32 ad = nbb, lh = 0u;
+    u32 vx = 0u, vy = 1u;
+    unsigned long long blk = 0, sm = 0, bpm = 0, hom = 0;
+    unsigned long long vrp64 = ((unsigned long long)H[0].y << 32) | H[0].x;
+    u32 aq = base + 8u * (u32)last;
+    int steps = 0, sub = 0;
+    bool pact = false, pstall = false, hold = false, rel = false, fzprev = false;
+    int pq = 0, plane = 0, ydep = 2;
+    u32 prp = 0u, prk = 0u, pq1 = 0u, lpq1 = 0u, pqa = 0u;
+    unsigned long long pold = 0;
+    unsigned long long zmask = 0;
+    asm volatile("" : "+s"(zmask));                // an opaque zero write mask (never an inline constant)
+    for (;;) {
+        if (!pstall && !hold && !fzprev && (sub == 1 || ydep >= 2)) {
+            int why = 0, sub2 = sub, phole = 0;
+            u32 upact = pact ? 1u : 0u, urel = rel ? 1u : 0u, upq = (u32)pq;
+            u32 rplo = (u32)vrp64, rphi = (u32)(vrp64 >> 32);
+            unsigned long long pbit = 1ull << plane;
+            nxt = __builtin_amdgcn_readfirstlane(nxt);
+            sub = __builtin_amdgcn_readfirstlane(sub);
+            steps = __builtin_amdgcn_readfirstlane(steps);
+            upact = (u32)__builtin_amdgcn_readfirstlane((int)upact);
+            urel = (u32)__builtin_amdgcn_readfirstlane((int)urel);
+            upq = (u32)__builtin_amdgcn_readfirstlane((int)upq);
+            pq1 = (u32)__builtin_amdgcn_readfirstlane((int)pq1);
+            lpq1 = (u32)__builtin_amdgcn_readfirstlane((int)lpq1);
+            pqa = (u32)__builtin_amdgcn_readfirstlane((int)pqa);
+            blk = uni64(blk);
+            pold = uni64(pold);
+            pbit = uni64(pbit);
+            eng_loop(base, b24, nbb, (u32)n, (u32)npops, h, ad, lh, vb8, vnbb, vx, vy, spare, vsp8, vzero, aq, rplo, rphi,
+                     prp, prk, vbase, nxt, blk, upact, urel, upq, pq1, lpq1, pqa, pbit, pold, sub, why, sub2, sm, bpm,
+                     hom, steps, phole);
+            vrp64 = ((unsigned long long)rphi << 32) | rplo;
+            pact = upact != 0;
+            rel = urel != 0;
+            pq = (int)upq;
+            plane = pbit ? __ffsll((long long)pbit) - 1 : 0;
+            if (why == 0) break;                                 // every pop done
+            sub = sub2 ^ 1;
+            ydep = 2;
+            if (hom & pold) {                                    // an older pop ended at q: its value
+                const int src = __ffsll((long long)(hom & pold)) - 1;
+                const u32 nx = (u32)__builtin_amdgcn_readlane((int)vx, src), ny = (u32)__builtin_amdgcn_readlane((int)vy, src);
+                if (l == plane) { vx = nx; vy = ny; }
+            }
+            rel = (bpm & pold) == 0;
+            if ((sm >> plane) & 1ull) {                          // the pending pop would stop: undo, freeze
+                const int hs = __builtin_amdgcn_readlane(phole, plane);
+                if (l == plane) {
+                    H[hs] = hs > 0 ? H[(hs - 1) >> 1] : make_uint2(prp, prk);
+                    h = hs;
+                    const u32 a0 = base + 8u + 16u * (u32)hs;
+                    ad = a0 < nbb ? a0 : nbb;
+                    lh = (u32)hlev(hs);
+                }
+                pstall = true;
+            }
+            continue;
+        }
+        // general step (frozen lanes, hold, transitions): v41's
+        {
+            if (pact && rel) {
+                if (l == plane) H[pq] = make_uint2(prp, 0u);
+                pact = false;
+                rel = false;
+                if (pstall) { pstall = false; hold = true; }
+            }
+            unsigned long long fz = 0;
+            if (pstall || hold) {
+                fz = __ballot(h != spare) & ~pold;
+                if (hold) fz &= ~(1ull << plane);
+            }
+            unsigned long long mine = 0, minew = 0;
+            if (sub == 0 && nxt < npops && !pstall && !hold && !fzprev && ydep >= 2) {
+                const int q = last - nxt;
+                const int L = nxt & 63;
+                if (blk == 0) {
+                    mine = minew = 1ull << L;
+                } else if (!pact && q >= 64) {
+                    mine = 1ull << L;
+                    pact = true;
+                    rel = false;
+                    pq = q;
+                    pq1 = (u32)q + 1u;
+                    lpq1 = (u32)hlev(q) - 1u;
+                    pqa = base + 8u * (u32)q;
                     plane = L;
                     prp = (u32)__builtin_amdgcn_readfirstlane((int)(u32)vrp64);
                     prk = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(vrp64 >> 32));
@@ -3182,7 +3560,7 @@ __global__ void __launch_bounds__(kT) k_heap(u64* keys_vals, const int* segn, co
     if (t < 64 && n >= 2 && npops > 0) {
         const u64 r0 = __builtin_amdgcn_s_memrealtime();
         const u64 t0 = __builtin_amdgcn_s_memtime();
-        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : V == 23 ? (u64)pops_v28<4>(H, n, npops) : V == 24 ? (u64)pops_v29<4>(H, n, npops) : V == 25 ? (u64)pops_v30<4, true, false>(H, n, npops) : V == 26 ? (u64)pops_v30<4, false, true>(H, n, npops) : V == 27 ? (u64)pops_v30<4, true, true>(H, n, npops) : V == 28 ? (u64)pops_v33<4, false, false>(H, n, npops) : V == 29 ? (u64)pops_v33<4, true, true>(H, n, npops) : V == 30 ? (u64)pops_v36<4, false, false>(H, n, npops) : V == 31 ? (u64)pops_v36<4, true, true>(H, n, npops) : V == 32 ? (u64)pops_v38<4>(H, n, npops) : V == 33 ? (u64)pops_v39<4, false>(H, n, npops) : V == 34 ? (u64)pops_v39<4, true>(H, n, npops) : V == 35 ? pops_spec<1>(H, n, npops) : V == 36 ? pops_spec<2>(H, n, npops) : V == 37 ? pops_spec<4>(H, n, npops) : V == 38 ? (u64)pops_v41(H, n, npops) : V == 39 ? (u64)pops_v42(H, n, npops) : (u64)pops_v43(H, n, npops);
+        const u64 steps = V == 1 ? pops_v1(H, n, npops, kCap) : V == 2 ? pops_v2(H, n, npops, kCap) : V == 3 ? pops_v3(H, n, npops, g) : V == 4 ? pops_v4(H, n, npops, g) : V == 5 ? pops_v5<1>(H, n, npops) : V == 6 ? pops_v5<2>(H, n, npops) : V == 7 ? (u64)pops_v7<1>(H, n, npops) : V == 8 ? (u64)pops_v7<2>(H, n, npops) : V == 9 ? (u64)pops_v9<1>(H, n, npops) : V == 10 ? (u64)pops_v9<2>(H, n, npops) : V == 11 ? pops_v11(H, n, npops, kCap) : V == 12 ? (u64)pops_v12<1>(H, n, npops) : V == 13 ? (u64)pops_v12<2>(H, n, npops) : V == 14 ? (u64)pops_v20(H, n, npops) : V == 15 ? (u64)pops_v21(H, n, npops) : V == 16 ? (u64)pops_v22(H, n, npops) : V == 17 ? (u64)pops_v23(H, n, npops) : V == 18 ? (u64)pops_v24<2>(H, n, npops) : V == 19 ? (u64)pops_v24<4>(H, n, npops) : V == 20 ? (u64)pops_v25<8>(H, n, npops) : V == 21 ? (u64)pops_v26<4>(H, n, npops) : V == 22 ? (u64)pops_v27<4>(H, n, npops) : V == 23 ? (u64)pops_v28<4>(H, n, npops) : V == 24 ? (u64)pops_v29<4>(H, n, npops) : V == 25 ? (u64)pops_v30<4, true, false>(H, n, npops) : V == 26 ? (u64)pops_v30<4, false, true>(H, n, npops) : V == 27 ? (u64)pops_v30<4, true, true>(H, n, npops) : V == 28 ? (u64)pops_v33<4, false, false>(H, n, npops) : V == 29 ? (u64)pops_v33<4, true, true>(H, n, npops) : V == 30 ? (u64)pops_v36<4, false, false>(H, n, npops) : V == 31 ? (u64)pops_v36<4, true, true>(H, n, npops) : V == 32 ? (u64)pops_v38<4>(H, n, npops) : V == 33 ? (u64)pops_v39<4, false>(H, n, npops) : V == 34 ? (u64)pops_v39<4, true>(H, n, npops) : V == 35 ? pops_spec<1>(H, n, npops) : V == 36 ? pops_spec<2>(H, n, npops) : V == 37 ? pops_spec<4>(H, n, npops) : V == 38 ? (u64)pops_v41(H, n, npops) : V == 39 ? (u64)pops_v42(H, n, npops) : V == 40 ? (u64)pops_v43(H, n, npops) : (u64)pops_v44(H, n, npops);
         const u64 t1 = __builtin_amdgcn_s_memtime();
         const u64 r1 = __builtin_amdgcn_s_memrealtime();
         if (t == 0) {
@@ -3499,7 +3877,7 @@ int main(int argc, char** argv) {
     const int vlo = argc > 2 ? std::atoi(argv[2]) : 22;
     const int vhi = argc > 3 ? std::atoi(argv[3]) : 34;
     for (int v = vlo; v <= vhi; ++v) {
-        if (v >= 2 && v <= 21 || (v >= 23 && v <= 31) || (v >= 35 && v <= 39)) continue;
+        if (v >= 2 && v <= 21 || (v >= 23 && v <= 31) || (v >= 35 && v <= 40)) continue;
         for (int r = 0; r < reps; ++r) {
             CK(hipMemcpy(d_kv, in.data(), in.size() * 8, hipMemcpyHostToDevice));
             if (v == 1) hipLaunchKernelGGL(k_heap<1>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
@@ -3541,7 +3919,8 @@ int main(int argc, char** argv) {
             else if (v == 37) hipLaunchKernelGGL(k_heap<37>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 38) hipLaunchKernelGGL(k_heap<38>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             else if (v == 39) hipLaunchKernelGGL(k_heap<39>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
-            else hipLaunchKernelGGL(k_heap<40>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else if (v == 40) hipLaunchKernelGGL(k_heap<40>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
+            else hipLaunchKernelGGL(k_heap<41>, dim3(nb), dim3(kT), 0, 0, d_kv, d_n, d_np, d_t, d_in);
             CK(hipDeviceSynchronize());
         }
         CK(hipMemcpy(out.data(), d_kv, out.size() * 8, hipMemcpyDeviceToHost));
