@@ -3434,6 +3434,9 @@ void odom_enqueue_init(OdomGPU& o, int p, hipStream_t s) {
     o.dims_fresh = false;
 }
 
+#ifndef PF_ODOM_GRID_AGG
+#define PF_ODOM_GRID_AGG 0      // development A/B: 1 = one counter atomic per run of equal cells in a wave
+#endif
 void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     if (o.opt_count_host > 2) o.opt_count_host--;
     StageBuf& sb = o.sb[p];
@@ -3447,15 +3450,18 @@ void odom_enqueue_update(OdomGPU& o, int p, hipStream_t s) {
     GridPtrs gp{{map_cur(o)[0], map_cur(o)[1], map_cur(o)[2]}, {cnt + C_M, cnt + C_M + 1, cnt + C_M + 2}, nc};
     const PredictTail pred{o.st, cnt, sb.cnt, o.acc, o.cls};
     if (o.dims_fresh) {                       // dims from the previous update's k_rgm_finish: the count first
-        hipLaunchKernelGGL((k_grid_count<false, FreshTail>), dim3(kGridCountBlocks + 1), dim3(256), 0, s, gp,
+        hipLaunchKernelGGL((k_grid_count<PF_ODOM_GRID_AGG != 0, FreshTail>), dim3(kGridCountBlocks + 1), dim3(256), 0, s, gp,
                            o.dims_next, o.grid.cell_count, o.grid.slot, o.grid.ttot, o.grid.err,
                            FreshTail{pred, o.dims_next, o.grid.dims, o.grid.d_ncells});
         grid_scan_scatter(o.grid, gp, s);
     } else {
         hipLaunchKernelGGL(k_grid_bounds<PredictTail>, dim3(kGridBoundsBlocks + 1), dim3(256), 0, s,
                            grid_bounds_args(o.grid, gp), pred);
-        grid_build(o.grid, gp, o.prim, s, true);
+        grid_build(o.grid, gp, o.prim, s, true, PF_ODOM_GRID_AGG != 0);
     }
+    // (PF_ODOM_GRID_AGG, round 6: the count's atomics taken per run of equal cells in a wave, as the front
+    // end's: measured slightly slower here, configs[4] 315 vs 317 and the headline 912 vs 915 frames/s --
+    // voxel order at the 0.4 / 0.8 m leaves gives short runs of 1 m cells -- so one atomic per point stays)
     const GridView gv{o.grid.dims, o.grid.cell_start, o.grid.cpts};
     for (int it = 0; it < o.opt_count_host; ++it) {
         AssocArgs aa{o.st, cnt, o.acc, gv, o.cls, clouds(sb.ds), clouds(map_cur(o)), o.nbr, o.qflag, o.geo, o.spars,
