@@ -101,6 +101,7 @@ constexpr int kLmParts = 31;   // cost, g[6], H[21], bad_r, bad_J, kept rows
 constexpr int kLmEvalSlots = 8; // LM claim masks per solve (>= evaluations per solve)
 constexpr int kLmEvals = 5;      // evaluations per solve: 1 + max_num_iterations (4)
 constexpr int kLmBlocks = 32;    // LM workgroups = residual chunks per evaluation
+constexpr int kLmBlkProbe = kDbgWords - 512;   // PF_PROBE: per-workgroup LM timestamps from here
 // an LM partial not yet published (a NaN payload no arithmetic produces); k_assoc writes it over
 // every partial slot before each solve
 constexpr unsigned long long kPartSentinel = 0x7FF4C0DE5E47F00Dull;

@@ -636,7 +636,12 @@ struct ObsRes {
 };
 template <int NC>
 __device__ __forceinline__ void observe_eval(const ObsArgs& a, const CatIdx<NC>& qi, int nq, int q, ObsRes& r) {
+    // the flag and the five neighbours are read together (one memory round trip: the neighbours of an
+    // invalid query are in bounds and unused), then the buckets and the neighbours' g bytes together
     r.f = a.qflag[q];
+    int nb[5], cur[5], rank[5], len[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) nb[j] = a.nbr[5 * q + j];
     r.c = 0;
     r.skip = true;
     r.observe = r.round = 0.f;
@@ -649,14 +654,14 @@ __device__ __forceinline__ void observe_eval(const ObsArgs& a, const CatIdx<NC>&
     // c_i(n) = valid queries before q sharing neighbour n: count the smaller pair ids in n's bucket
     // (filled in any order by k_assoc: two pairs inline, the rest on an overflow list); the pair
     // with the largest id carries n's increment
-    int nb[5], cur[5], rank[5], len[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) nb[j] = a.nbr[5 * q + j];
     int4 bk[5][kBktQuads];                               // every bucket read at once
 #pragma unroll
     for (int j = 0; j < 5; ++j)
 #pragma unroll
         for (int k = 0; k < kBktQuads; ++k) bk[j][k] = a.pbkt[(size_t)kBktQuads * ((u32)c * a.map_cap + (u32)nb[j]) + k];
+    u32 g0[5];                                           // the g bytes (nothing writes them in this pass)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) g0[j] = w_g(mp[nb[j]]);
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
         const int p = 5 * q + j;
@@ -685,8 +690,7 @@ __device__ __forceinline__ void observe_eval(const ObsArgs& a, const CatIdx<NC>&
     int gs = 0;
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-        const u32 g0 = w_g(mp[nb[j]]);
-        gs += min(255u, g0 + (u32)rank[j]);
+        gs += min(255u, g0[j] + (u32)rank[j]);
         r.tinc[j] = rank[j] == len[j] - 1 ? (u32)len[j] : 0u;
     }
     float observe = gs / 5.0 + 1;                        // :332-338 / :480-486
@@ -1381,30 +1385,61 @@ __device__ __forceinline__ void pidx_apply_pair(const int* nbr, u32 inc, int p, 
     reinterpret_cast<int*>(b)[kBktHead] = -1;
 }
 
+// the p-index increments of the chunks in mask m (k_lm_solve's fused observe pass), by threads i0,
+// i0 + ni, ... of the workgroup; out of line, so the solve's register allocation does not carry it
+template <int NC>
+__device__ __noinline__ void lm_apply_commits(const int* nbr, const u32* tailinc, CloudsW map, int4* pbkt, u32 map_cap,
+                                              CatIdx<NC> qi, int nq, u32 m, int i0, int ni) {
+    for (int ch = 0; ch < kLmBlocks; ++ch) {
+        if (!((m >> ch) & 1u)) continue;
+        for (int base = ch * 256; base < nq; base += kLmBlocks * 256)
+            for (int i = i0; i < 256; i += ni) {
+                const int q = base + i;
+                if (q >= nq) continue;
+                const int c = qi.cls(q);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const u32 inc = tailinc[5 * q + j];
+                    if (inc) pidx_apply_pair(nbr, inc, 5 * q + j, c, map, pbkt, map_cap);
+                }
+            }
+    }
+}
+
 template <int NC>
 __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     unsigned long long* dbg = a.dbg;
     const bool rec = dbg && blockIdx.x == 0 && threadIdx.x == 0;
     if (rec) dbg[0] = __builtin_amdgcn_s_memrealtime();
+    // per-workgroup probe (every block's thread 0): start, and per evaluation the home chunk's
+    // publish and the end of the arrival wait
+    unsigned long long* recb = dbg && threadIdx.x == 0 ? dbg + kLmBlkProbe : nullptr;
+    if (recb) recb[2 * kLmEvals * kLmBlocks + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     __shared__ double rows[256][9];                             // per residual: J[6], r, 0.5 rho (+1 pad:
                                                                 // a stride of 18 words spreads a wave's rows over the 32 banks)
     __shared__ double red9[28][9];
     __shared__ int nbad[3];                                     // bad residuals, bad Jacobians, kept rows
-    __shared__ unsigned char hi_[21], hj_[21];
     __shared__ double tot[kLmParts];
     __shared__ LMState lm;
     __shared__ int aborted;
     const int t = threadIdx.x;
     // the map's p-index bytes are not read by the solve: this iteration's increments are applied
     // while the blocks wait for the first evaluation's arrivals (or here, when there is no solve)
+    // every value the set-up reads from memory is loaded here, in one round trip: the counts, the gate
+    // and (thread 0) the pose
     const CatIdx<NC> qi = cat_idx<NC>(a.cnt + C_DS);
+    const int nq = a.cnt[C_NQ];
+    const int gate = a.st->gate;
+    double prm0[7];
+    if (t == 0)
+        for (int k = 0; k < 7; ++k) prm0[k] = a.st->params[k];
     // fused observe pass (weightType 0): the residual count is known after the first evaluation
     // (its partials carry each chunk's kept rows); without a gate there is nothing to observe
     const bool fuse = a.fuse != 0;
     int nres = 0;
     if (!fuse)
         for (int c = 0; c < NC; ++c) nres += a.cnt[C_KEPT + c];
-    if (!a.st->gate || (!fuse && nres == 0)) {                   // no residual blocks: untouched
+    if (!gate || (!fuse && nres == 0)) {                         // no residual blocks: untouched
         if (!fuse) pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
         if (a.prep.on) rgm_prep_apps<NC>(a.prep, a.cnt, a.st->params);
         return;
@@ -1421,8 +1456,8 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     if (t == 0) {                                                // problem set-up (:252-266)
         double xn = 0;
         for (int k = 0; k < 7; ++k) {
-            lm.x[k] = lm.cand[k] = lm.best[k] = a.st->params[k];
-            xn += lm.x[k] * lm.x[k];
+            lm.x[k] = lm.cand[k] = lm.best[k] = prm0[k];
+            xn += prm0[k] * prm0[k];
         }
         lm.x_norm = sqrt(xn);
         lm.radius = 1e4;
@@ -1432,17 +1467,18 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         lm.done = 0;
         aborted = 0;
         nbad[0] = nbad[1] = nbad[2] = 0;                         // before the barrier: every wave may count
-        int h = 0;
-        for (int i = 0; i < 6; ++i)
-            for (int j = i; j < 6; ++j) { hi_[h] = (unsigned char)i; hj_[h] = (unsigned char)j; ++h; }
     }
     __syncthreads();
-    const int nq = a.cnt[C_NQ];
     const int wt = a.weight_type;
-    // reduction roles: thread (k, p) sums product k (0: cost, 1-6: g, 7-27: upper J^T J) over the
-    // chunk rows p, p + 9, ...; 28 x 9 = 252 threads
+    // reduction roles: thread (k, p) sums product k (0: cost, 1-6: g, 7-27: upper J^T J, row by row)
+    // over the chunk rows p, p + 9, ...; 28 x 9 = 252 threads
     const int rk = t / 9, rp = t % 9;
-    const int ri = rk >= 7 && rk < 28 ? hi_[rk - 7] : 0, rj_ = rk >= 7 && rk < 28 ? hj_[rk - 7] : 0;
+    int ri = 0, rj_ = 0;
+    if (rk >= 7 && rk < 28) {
+        int h = rk - 7;
+        while (h >= 6 - ri) { h -= 6 - ri; ++ri; }
+        rj_ = ri + h;
+    }
     // chunk c of an evaluation = the queries c * 256 + k * kLmBlocks * 256; block b first reduces its
     // home chunk b and claims it with one atomicOr on the evaluation's claim mask, whose result is
     // only needed when the partials are published (the atomic's latency hides behind the reduction).
@@ -1486,6 +1522,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     __shared__ u32 s_commit, s_claim0;
     __shared__ int s_ocnt[2 * kMaxC];
     auto observe_chunk = [&](int ch, bool home_claim) -> bool {
+        if (rec && home_claim) dbg[55] = __builtin_amdgcn_s_memrealtime();
         if (t < 2 * kMaxC) s_ocnt[t] = 0;
         bool kept0 = false, won = true;
         for (int base = ch * 256, k = 0; base < nq; base += kLmBlocks * 256, ++k) {
@@ -1493,8 +1530,10 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             ObsRes r;
             r.f = 0;
             if (q < nq) observe_eval<NC>(a.obs, qi, nq, q, r);
+            if (rec && home_claim && k == 0) dbg[50] = __builtin_amdgcn_s_memrealtime();
             if (k == 0) {
                 __syncthreads();                                 // s_claim0 (thread 0's claim) and s_ocnt
+                if (rec && home_claim) dbg[51] = __builtin_amdgcn_s_memrealtime();
                 won = !home_claim || ((s_claim0 >> ch) & 1u) == 0u;
                 kept0 = (r.f & 1) && !r.skip;
             }
@@ -1508,29 +1547,19 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         }
         // the commits complete before this chunk's partials are published (consumers that see the
         // partials read the kept bits)
+        if (rec && home_claim) dbg[52] = __builtin_amdgcn_s_memrealtime();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (rec && home_claim) dbg[53] = __builtin_amdgcn_s_memrealtime();
         if (won && t < 2 * NC && s_ocnt[t]) atomicAdd(&a.cnt[(t & 1) ? C_KEPT + t / 2 : C_VALID + t / 2], s_ocnt[t]);
         if (won && t == 0) s_commit |= 1u << ch;
         return kept0;
     };
-    // the p-index increments of the chunks this workgroup observed, by the threads that computed them
-    // (after the first evaluation: every observe pass of the launch has read the map's g bytes)
-    auto apply_commits = [&]() {
-        const u32 m = s_commit;
-        for (int ch = 0; ch < kLmBlocks; ++ch) {
-            if (!((m >> ch) & 1u)) continue;
-            for (int base = ch * 256; base < nq; base += kLmBlocks * 256) {
-                const int q = base + t;
-                if (q >= nq) continue;
-                const int c = qi.cls(q);
-#pragma unroll
-                for (int j = 0; j < 5; ++j) {
-                    const u32 inc = a.tailinc[5 * q + j];
-                    if (inc) pidx_apply_pair(a.nbr, inc, 5 * q + j, c, a.map, a.pbkt, a.map_cap);
-                }
-            }
-        }
+    // the p-index increments of the chunks this workgroup observed, by threads i0, i0 + ni, ... of the
+    // workgroup (after the first evaluation's arrivals: every observe pass of the launch has read the
+    // map's g bytes)
+    auto apply_commits = [&](int i0, int ni) {
+        lm_apply_commits<NC>(a.nbr, a.tailinc, a.map, a.pbkt, a.map_cap, qi, nq, s_commit, i0, ni);
     };
     u32 old0 = 0;
     bool applied = !fuse;
@@ -1542,6 +1571,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         const bool kept0 = observe_chunk((int)blockIdx.x, true);
         old0 = s_claim0;
         s_mine[t] = load_res_k((int)blockIdx.x * 256 + t, kept0);
+        if (rec) dbg[54] = __builtin_amdgcn_s_memrealtime();
     } else {
         s_mine[t] = load_res((int)blockIdx.x * 256 + t);
     }
@@ -1591,15 +1621,19 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             __syncthreads();
             if (rk < 28) {                                       // rows rp*29 .. rp*29+28
                 const int ca = rk == 0 ? 7 : (rk < 7 ? rk - 1 : ri), cb = rk == 0 ? -1 : (rk < 7 ? 6 : rj_);
-                double pa[29], pb[29];
+                // in groups of 8 rows: every group's LDS reads issued at once, the sum in row order
 #pragma unroll
-                for (int i = 0; i < 29; ++i) {
-                    const int j = rp * 29 + i;
-                    pa[i] = j < 256 ? rows[j][ca] : 0.0;
-                    pb[i] = (j < 256 && cb >= 0) ? rows[j][cb] : 1.0;
+                for (int i0 = 0; i0 < 29; i0 += 8) {
+                    double pa[8], pb[8];
+#pragma unroll
+                    for (int i = 0; i < 8 && i0 + i < 29; ++i) {
+                        const int j = rp * 29 + i0 + i;
+                        pa[i] = j < 256 ? rows[j][ca] : 0.0;
+                        pb[i] = (j < 256 && cb >= 0) ? rows[j][cb] : 1.0;
+                    }
+#pragma unroll
+                    for (int i = 0; i < 8 && i0 + i < 29; ++i) part += pa[i] * pb[i];
                 }
-#pragma unroll
-                for (int i = 0; i < 29; ++i) part += pa[i] * pb[i];
             }
             __syncthreads();
         }
@@ -1630,11 +1664,8 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         else if (t == 0) old = __hip_atomic_fetch_or(&claim[ev], 1u << home, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         reduce_chunk(home, ev, old, true);
         if (rec) dbg[1 + 4 * ev] = dbg[2 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
+        if (recb) recb[2 * (ev * kLmBlocks + home)] = __builtin_amdgcn_s_memrealtime();
         if (!fuse && ev == 0) pidx_apply(a.nbr, a.tailinc, a.cnt[C_NPAIR], qi, a.map, a.pbkt, a.map_cap);
-        if (fuse && ev == 1 && !applied) {                      // overlaps this evaluation's wait
-            apply_commits();
-            applied = true;
-        }
         // wait until no partial of this evaluation is the sentinel any more (threads t < 30 poll
         // their product over the 32 chunks); after kLmStealPolls rounds, claim and reduce chunks
         // nobody has claimed (their home workgroups have not started)
@@ -1682,6 +1713,7 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         }
         if (aborted) break;
         if (rec) dbg[3 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
+        if (recb) recb[2 * (ev * kLmBlocks + blockIdx.x) + 1] = __builtin_amdgcn_s_memrealtime();
         if (t < kLmParts) {
             double v = 0.0;
 #pragma unroll
@@ -1692,11 +1724,15 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
         if (fuse && ev == 0) {                                   // the residual count (kept rows)
             const int nr = (int)tot[kLmParts - 1];
             if (nr == 0) {                                       // no residual blocks: untouched
-                apply_commits();
+                apply_commits(t, 256);
                 if (a.prep.on) rgm_prep_apps<NC>(a.prep, a.cnt, a.st->params);
                 return;
             }
             if (t == 0) lm.n_res = nr;
+            // a home chunk another workgroup claimed first (this one started late): its observe pass
+            // here may have read g bytes that were already incremented, so the kept bits are re-read
+            // from the claimant's commits, complete since its partials arrived
+            if ((old0 >> blockIdx.x) & 1u) s_mine[t] = load_res((int)blockIdx.x * 256 + t);
         }
         if (rec) dbg[40 + ev] = __builtin_amdgcn_s_memrealtime();
         if (t < 2) {                                             // lanes 0 and 1, identical state
@@ -1708,11 +1744,14 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
             if (pr) pr[3] = __builtin_amdgcn_s_memrealtime();
             if (ev == kLmEvals - 1) c.done = 1;
             if (t == 0) core_store(c, lm);
+        } else if (fuse && ev == 0 && t >= 64) {
+            apply_commits(t - 64, 192);                          // waves 1-3, beside the serial step
         }
+        if (fuse && ev == 0) applied = true;
         __syncthreads();
         if (rec) dbg[4 + 4 * ev] = __builtin_amdgcn_s_memrealtime();
     }
-    if (!applied) apply_commits();
+    if (!applied) apply_commits(t, 256);
     if (blockIdx.x == 0 && t == 0) {
         for (int k = 0; k < 7; ++k) a.st->params[k] = lm.best[k];
         atomicAdd(&a.cnt[C_LM_ITERS], lm.iteration);
@@ -2286,7 +2325,7 @@ struct RgmArgs {
     const u32* btag;
     unsigned long long* dbg;   // development probe (PF_PROBE): [64 + 10 b + i] phase timestamps of bucket b
 };
-static_assert(64 + 10 * (kRgmBuckets + 1) <= kDbgWords, "probe words");
+static_assert(64 + 10 * (kRgmBuckets + 1) <= kLmBlkProbe, "probe words");
 constexpr int kRgmMeta = 32;                           // ints per bucket in bmeta
 constexpr int kRgmBnd = 8;                             // bmeta offset of the bounds
 
