@@ -136,6 +136,8 @@ CONFIGS = [
     ("dense_S64V", "S64V", 1000, (0.4, 75), 64, 0, 10),       # dense vegetation scene, KITTI-like map sizes
     ("town_S64T", "S64T", 4541, (0.4, 75), 64, 0, 10),        # the well-conditioned town (free-running scene)
     ("configs1_S64_wt2", "S64", 4541, (0.4, 75), 64, 2, 10),  # weightType 2: pfilter_kitti.launch:7's default
+    ("configs1_S64_wt1", "S64", 4541, (0.4, 75), 64, 1, 10),  # weightType 1: the observe weight alone
+    ("configs1_S64_wt12", "S64", 4541, (0.4, 75), 64, 12, 10),  # weightType 12: observe and sparsity averaged
 ]
 
 
