@@ -38,10 +38,10 @@ def _workers():
 
 
 def synced_run(pa, pfsynth, name, preset, n, theta, lines=64, seed=0, ring_model=None, seed_map=None, every=1,
-               tie_order=False, wt=0):
+               tie_order=False, wt=0, k_new=0):
     from multiprocessing import get_context
     lid = (lines, 3.0, 90.0)
-    prm = (0.4, 0, theta[0], theta[1], wt)
+    prm = (0.4, k_new, theta[0], theta[1], wt)
     ctx = get_context("spawn")
     pool = ctx.Pool(_workers(), initializer=pw.init, initargs=(preset, n, seed, lid, ring_model, prm, 0))
     od = pa.Odom_ES_EstimationClass(device=0, max_points=300000, map_capacity=1 << 22)
@@ -157,6 +157,16 @@ def test_synced_parity_every_frame(pa, pfsynth, name, preset, n, theta, lines, w
     _check(rep, n - 1)
     if xyz_off is not None:
         assert rep["xyz_bitexact_frames"] >= 2 * rep["frames"] - xyz_off, (rep["xyz_bitexact_frames"], rep["frames"])
+
+
+@pytest.mark.parametrize("k_new,theta", [(2, (0.4, 75)), (1, (0.8, 30))])
+def test_synced_parity_pindex_variants(pa, pfsynth, k_new, theta):
+    """The p-index filter's other parameters (k_new > 0 keeps map points younger than k_new rounds,
+    src/odomEstimationClass.cpp:350-353) over the whole S64 sequence in the tie order, every frame synced:
+    the strict bar of test_synced_parity_every_frame."""
+    rep = synced_run(pa, pfsynth, "pindex_k%d_S64_tie" % k_new, "S64", 4541, theta, tie_order=True, k_new=k_new)
+    _check(rep, 4540)
+    assert rep["xyz_bitexact_frames"] >= 2 * rep["frames"] - 10, (rep["xyz_bitexact_frames"], rep["frames"])
 
 
 @pytest.mark.parametrize("name,preset,n,theta,lines", [c[:5] for c in CONFIGS if c[5] == 0])
