@@ -118,10 +118,10 @@ def _check(rep, n_expected):
 
 
 def test_bpf_synced_parity_raw_scan_chain(pa, pfsynth):
-    """configs[1] parameters, the BPF raw-scan chain, every frame of 1000 (S64)"""
-    _check(synced_bpf(pa, pfsynth, "S64_raw", "S64", 1000, raw_scan=True), 999)
+    """configs[1] parameters, the BPF raw-scan chain, every frame of the whole sequence (S64, 4541)"""
+    _check(synced_bpf(pa, pfsynth, "S64_raw", "S64", 4541, raw_scan=True), 4540)
 
 
 def test_bpf_synced_parity_update_api(pa, pfsynth):
-    """the update API (pf_bpf_update) fed the oracle front end's clouds, every frame of 300 (S64T)"""
-    _check(synced_bpf(pa, pfsynth, "S64T_update", "S64T", 300, raw_scan=False), 299)
+    """the update API (pf_bpf_update) fed the oracle front end's clouds, every frame of 1000 (S64T)"""
+    _check(synced_bpf(pa, pfsynth, "S64T_update", "S64T", 1000, raw_scan=False), 999)
