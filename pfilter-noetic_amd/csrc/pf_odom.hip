@@ -652,7 +652,7 @@ __device__ __forceinline__ void observe_eval(const ObsArgs& a, const CatIdx<NC>&
     r.c = c;
     const float4* mp = a.map.at(c);
     // c_i(n) = valid queries before q sharing neighbour n: count the smaller pair ids in n's bucket
-    // (filled in any order by k_assoc: two pairs inline, the rest on an overflow list); the pair
+    // (filled in any order by k_assoc: kBktInline pairs inline, the rest on an overflow list); the pair
     // with the largest id carries n's increment
     int4 bk[5][kBktQuads];                               // every bucket read at once
 #pragma unroll
@@ -1423,9 +1423,10 @@ __global__ void __launch_bounds__(256) k_lm_solve(LmArgs a) {
     __shared__ LMState lm;
     __shared__ int aborted;
     const int t = threadIdx.x;
-    // the map's p-index bytes are not read by the solve: this iteration's increments are applied
-    // while the blocks wait for the first evaluation's arrivals (or here, when there is no solve)
-    // every value the set-up reads from memory is loaded here, in one round trip: the counts, the gate
+    // the map's p-index bytes are not read by the solve: this iteration's increments are applied while
+    // the blocks wait for the first evaluation's arrivals (k_observe launched), beside the first LM step
+    // (observe pass fused), or here when there is no solve.
+    // Every value the set-up reads from memory is loaded here, in one round trip: the counts, the gate
     // and (thread 0) the pose
     const CatIdx<NC> qi = cat_idx<NC>(a.cnt + C_DS);
     const int nq = a.cnt[C_NQ];
