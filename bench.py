@@ -317,12 +317,14 @@ def run_kitti11(rank, local_rank, world, warmup, threads, use_graph, barrier, co
                     od.reset()
                 for ptr, n in ptrs:
                     od.frame_device(ptr, n)
+                log("kitti11: sequence %02d enqueued (%.1f s)" % (sq, time.perf_counter() - t0))
             od.sync()
             if items:
                 poses[items[-1][0]] = od.poses()
         except Exception as e:     # re-raised in the main thread: a failed frame is never counted
             errors.append(repr(e))
 
+    log("kitti11: %d handles ready" % nthreads)
     barrier()
     t0 = time.perf_counter()
     ths = [threading.Thread(target=drive, args=(handles[j], shares[j])) for j in range(nthreads)]
@@ -1236,10 +1238,31 @@ def reduce_results(dist, elapsed, frames, poses, device):
     return float(t.item()), int(f.item()), poses_all
 
 
+KITTI11_HW_QUEUES = 16
+
+
+def kitti11_hw_queues(args, env):
+    """configs[3] with several concurrent sequences per GPU: the HIP runtime's hardware queues per process
+    raised to KITTI11_HW_QUEUES (before the runtime starts; never lowered). At the image's default of 4, the
+    2-3 streams of every handle share the queues: in the tie order K = 4 ran 1286-1764 frames/s and K = 6
+    stalled (cross-stream waits queued behind each other's kernels); at 16 queues K = 4 ran 2198 and K = 6
+    2183-2208 (profiles/r06/k11conc/). Returns the value set, or None."""
+    if args.sequences != "kitti11" or args.concurrent <= 1:
+        return None
+    try:
+        cur = int(env.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        cur = 4
+    if cur < KITTI11_HW_QUEUES:
+        env["GPU_MAX_HW_QUEUES"] = str(KITTI11_HW_QUEUES)
+    return int(env["GPU_MAX_HW_QUEUES"])
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
     ORDER[0] = args.order
+    hw_queues = kitti11_hw_queues(args, os.environ)   # before anything starts the HIP runtime
     world, launch = resolve_world(args, os.environ)
     if launch:                     # nothing has touched the GPU yet
         sys.exit(launch_ranks(world, argv))
@@ -1266,7 +1289,7 @@ def main(argv=None):
     if args.knn_shard:
         return main_knn_shard(args, rank, local_rank, world, dist, barrier, dev, stub)
     if args.sequences == "kitti11":
-        return main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev, stub)
+        return main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev, stub, hw_queues)
     host_legs = world == 1 and not stub and (not args.no_pcie or args.node_frames > 0)
     if stub:
         r = stub_run(rank, args.steps)
@@ -1427,7 +1450,7 @@ def main(argv=None):
         dist.destroy_process_group()
 
 
-def main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev="cuda", stub=False):
+def main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev="cuda", stub=False, hw_queues=None):
     if stub:                       # CPU test of the rank plumbing: rank r 'takes' 1 + r seconds
         mine = lpt_assign(KITTI_SEQ_FRAMES, world)[rank]
         r = dict(elapsed=1.0 + rank, frames=sum(KITTI_SEQ_FRAMES[sq] for sq in mine),
@@ -1467,6 +1490,7 @@ def main_kitti11(args, rank, local_rank, world, dist, barrier, threads, dev="cud
                                       "by sequence) as independent streams, LPT-assigned to the GPUs",
                           "assignment": lpt_assign(KITTI_SEQ_FRAMES, world), "rank0_sequences": r["sequences"],
                           "parallelism": "sequences over GPUs", "concurrent_per_gpu": args.concurrent,
+                          "hw_queues_per_process": hw_queues,
                           "graph": GRAPH_NAMES[graph_mode(args)]},
                "poses": pose_info}
         if stub:

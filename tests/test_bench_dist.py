@@ -209,3 +209,17 @@ def test_cpu_baseline_sample_order():
     c = a.copy()
     c[:4] = -c[:4]                                                  # q and -q are the same rotation
     assert bench.pose_diff(a, c) == (0.0, 0.0)
+
+
+def test_kitti11_hw_queues_raised_only_for_concurrent_sequences():
+    """configs[3] with several sequences per GPU raises the process's hardware queues to 16 before the HIP
+    runtime starts (bench.kitti11_hw_queues); never lowers a larger value, leaves other runs alone."""
+    import bench
+    env = {"GPU_MAX_HW_QUEUES": "4"}
+    assert bench.kitti11_hw_queues(bench.parse(["--sequences", "kitti11", "--concurrent", "4"]), env) == 16
+    assert env["GPU_MAX_HW_QUEUES"] == "16"
+    env = {"GPU_MAX_HW_QUEUES": "24"}
+    assert bench.kitti11_hw_queues(bench.parse(["--sequences", "kitti11", "--concurrent", "4"]), env) == 24
+    env = {}
+    assert bench.kitti11_hw_queues(bench.parse(["--sequences", "kitti11", "--concurrent", "1"]), env) is None
+    assert bench.kitti11_hw_queues(bench.parse([]), env) is None and env == {}
